@@ -1,0 +1,244 @@
+/*
+ * siddhi_hip.h — C ABI of libsiddhi_hip.so, the MI355X (gfx950) execution path for Siddhi's
+ * filtered, windowed group-by aggregation and incremental `define aggregation` roll-ups.
+ *
+ * The reference (Arshardh/siddhi, Java) has no native code; this ABI is what the Java window /
+ * aggregator extension shim binds through JNI or Panama FFM. Every entry
+ * point names the reference interface whose behaviour it replaces. Citations use
+ *   core/  = modules/siddhi-core/src/main/java/io/siddhi/core/
+ *   qapi/  = modules/siddhi-query-api/src/main/java/io/siddhi/query/api/
+ *
+ * Rules of the ABI:
+ *  - plain C types only; no C++ or torch types cross it;
+ *  - every call returns an int: SH_OK (0) or a negative SH_ERR_* code; sh_last_error() gives a
+ *    thread-local message (the Java shim turns it into SiddhiAppRuntimeException, which the
+ *    StreamJunction publisher routes by @OnError, core/stream/StreamJunction.java:486-535);
+ *  - a query handle is single-threaded, matching the per-query LockWrapper the reference takes in
+ *    ProcessStreamReceiver.process (core/query/input/ProcessStreamReceiver.java:74-96) and in
+ *    Scheduler.sendTimerEvents (core/util/Scheduler.java:171-209);
+ *  - output buffers are owned by the library and stay valid until the next call on that handle.
+ */
+#ifndef SIDDHI_HIP_H
+#define SIDDHI_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SH_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------------------------- */
+#define SH_OK 0
+#define SH_ERR_INVALID (-1)     /* malformed descriptor or batch (SiddhiAppValidationException) */
+#define SH_ERR_UNSUPPORTED (-2) /* a feature this build does not run on the GPU (fails loudly)   */
+#define SH_ERR_DEVICE (-3)      /* HIP / RCCL failure                                           */
+#define SH_ERR_OOM (-4)         /* device allocation failed                                     */
+#define SH_ERR_STATE (-5)       /* call out of order (e.g. clock moved backwards in a batch)    */
+
+/* ---- attribute types: qapi/definition/Attribute.java:105-113 ---------------------------- */
+#define SH_T_INT 1    /* int32                                                              */
+#define SH_T_LONG 2   /* int64                                                              */
+#define SH_T_FLOAT 3  /* float                                                              */
+#define SH_T_DOUBLE 4 /* double                                                             */
+#define SH_T_STRID 5  /* string, dictionary-encoded by the host to int32 ids (equality only) */
+#define SH_T_BOOL 6   /* uint8 0/1                                                          */
+
+/* ---- filter program: postfix form of the `S[cond]` expression --------------------------
+ * Replaces FilterProcessor.process (core/query/processor/filter/FilterProcessor.java:47-60)
+ * and the Compare/And/Or/Not condition executors (core/executor/condition/ and compare/). Comparisons
+ * follow the reference's per-type-pair executors: relational ops use Java binary numeric
+ * promotion; ==/!= do too except Float<->Long which compare as double
+ * (compare/equal/EqualCompareConditionExpressionExecutorFloatLong.java).                    */
+#define SH_OP_COL 1   /* push column `col`                                                 */
+#define SH_OP_CONST 2 /* push constant of `type` (ival for INT/LONG/STRID/BOOL, dval FLOAT/DOUBLE) */
+#define SH_OP_GT 3
+#define SH_OP_GE 4
+#define SH_OP_LT 5
+#define SH_OP_LE 6
+#define SH_OP_EQ 7
+#define SH_OP_NE 8
+#define SH_OP_AND 9
+#define SH_OP_OR 10
+#define SH_OP_NOT 11
+
+typedef struct {
+    int32_t op;
+    int32_t type; /* SH_T_* of the constant (SH_OP_CONST)                                  */
+    int32_t col;  /* column index (SH_OP_COL)                                              */
+    int32_t pad;
+    int64_t ival;
+    double dval;
+} sh_filter_op;
+
+/* ---- windows ---------------------------------------------------------------------------- */
+#define SH_WIN_NONE 0         /* no window: filter -> selector (oracle/KAT use; not a GPU path) */
+#define SH_WIN_LENGTH_BATCH 1 /* core/query/processor/stream/window/LengthBatchWindowProcessor.java */
+#define SH_WIN_TIME_BATCH 2   /* core/query/processor/stream/window/TimeBatchWindowProcessor.java   */
+#define SH_WIN_TIME 3         /* core/query/processor/stream/window/TimeWindowProcessor.java        */
+
+/* ---- aggregators: core/query/selector/attribute/aggregator/ [Sum,Avg,Count,Min,Max]AttributeAggregatorExecutor ---- */
+#define SH_AGG_SUM 1
+#define SH_AGG_AVG 2
+#define SH_AGG_COUNT 3
+#define SH_AGG_MIN 4
+#define SH_AGG_MAX 5
+
+typedef struct {
+    int32_t fn;  /* SH_AGG_*                                     */
+    int32_t col; /* input column (ignored for SH_AGG_COUNT)      */
+} sh_agg_spec;
+
+#define SH_MAX_COLS 8
+#define SH_MAX_AGGS 8
+#define SH_MAX_GROUP 2
+
+/* Compiled form of
+ *   [partition with (pcol of S) begin]
+ *   from S[filter]#window.<kind>(param[, start][, streamCurrent])
+ *   select g..., agg(col)... group by g... insert [current|all|expired] events into O;
+ * built by the Java shim from the parsed Query (the reference parser stays in charge). */
+typedef struct {
+    int32_t n_cols;
+    int32_t col_types[SH_MAX_COLS];
+    int32_t n_filter_ops; /* 0 = no filter                                              */
+    const sh_filter_op* filter;
+    int32_t window;         /* SH_WIN_*                                                 */
+    int32_t stream_current; /* lengthBatch/timeBatch `stream.current.event` flag        */
+    int64_t window_param;   /* lengthBatch: length; timeBatch/time: milliseconds        */
+    int32_t has_start_time; /* timeBatch(T, start)                                       */
+    int32_t n_group_by;     /* 0..SH_MAX_GROUP                                           */
+    int64_t start_time;
+    int32_t group_by[SH_MAX_GROUP];
+    int32_t n_aggs;
+    int32_t current_on;     /* insert [current|all] events  (QueryParser.java:221-223)   */
+    sh_agg_spec aggs[SH_MAX_AGGS];
+    int32_t expired_on;     /* insert [expired|all] events                               */
+    int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`     */
+    int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing)  */
+} sh_query_desc;
+
+/* ---- incremental aggregation: core/aggregation/ + util/parser/AggregationParser.java ---- */
+#define SH_DUR_SECONDS 0
+#define SH_DUR_MINUTES 1
+#define SH_DUR_HOURS 2
+#define SH_DUR_DAYS 3
+#define SH_DUR_MONTHS 4
+#define SH_DUR_YEARS 5
+
+/* `define aggregation A from S[filter] select g..., agg(col)... group by g...
+ *   aggregate [by ts_col] every min_dur ... max_dur;` with the default GMT aggTimeZone.
+ * Per duration the library keeps the base values AggregationParser derives
+ * (avg -> sum + count, count -> sum of 1L; AggregationParser.java:693-728). */
+typedef struct {
+    int32_t n_cols;
+    int32_t col_types[SH_MAX_COLS];
+    int32_t n_filter_ops;
+    const sh_filter_op* filter;
+    int32_t n_group_by;
+    int32_t group_by[SH_MAX_GROUP];
+    int32_t n_aggs;
+    sh_agg_spec aggs[SH_MAX_AGGS];
+    int32_t ts_col;       /* `aggregate by` attribute (LONG); -1 = processing time only */
+    int32_t min_duration; /* SH_DUR_*                                                    */
+    int32_t max_duration;
+    int64_t key_capacity;
+} sh_aggregation_desc;
+
+/* ---- input batch: a run of InputHandler.send(Event[]) calls -----------------------------
+ * One sh_batch stands for `n_sends` consecutive sends (core/stream/input/InputHandler.java:85-96),
+ * processed with the per-send semantics of the reference (clock set from the send's last event
+ * in playback mode, timers fired before the send is processed: Scheduler.java:71-104).
+ *   send_size > 0 : consecutive sends of send_size events (the last may be shorter);
+ *   send_size == 0: one send of all n events.
+ * Columns are SoA, column c holds n values of col_types[c] (int32 for INT/STRID, uint8 BOOL).
+ * For sh_push the pointers are host memory; for sh_push_device they are device memory.    */
+typedef struct {
+    int64_t n;
+    int64_t send_size;
+    const int64_t* ts; /* Event.getTimestamp() per event                                 */
+    const void* cols[SH_MAX_COLS];
+} sh_batch;
+
+/* ---- output -------------------------------------------------------------------------------
+ * One flush = one selector output chunk = one StreamCallback.receive(Event[]) call
+ * (core/query/output/ratelimit/OutputRateLimiter.java:64-104). Rows are in the reference's
+ * order (first-occurrence order of the group key inside the flush, QuerySelector.java:315-374);
+ * a row carries the timestamp and aggregate values of the key's last qualifying event.
+ * vals are raw 8-byte slots: int64 for LONG/INT outputs, IEEE double bits for DOUBLE/FLOAT. */
+typedef struct {
+    int64_t n_flushes;
+    int64_t n_rows;
+    int32_t n_keys;
+    int32_t n_vals;
+    int32_t val_types[SH_MAX_AGGS];
+    const int64_t* flush_offsets; /* [n_flushes + 1]                                       */
+    const int64_t* flush_clock;   /* [n_flushes] clock of the send / timer that emitted it */
+    const int64_t* ts;            /* [n_rows]                                              */
+    const uint8_t* expired;       /* [n_rows] 1 = EXPIRED before OutputRateLimiter's flip  */
+    const int64_t* keys;          /* [n_keys][n_rows] group-by values widened to int64     */
+    const uint64_t* vals;         /* [n_vals][n_rows]                                      */
+    const uint8_t* nulls;         /* [n_vals][n_rows] 1 = Java null                         */
+} sh_out;
+
+/* Rows written to one duration's aggregation table (core/aggregation/IncrementalExecutor.java:
+ * 201-258). keys[0] is AGG_TIMESTAMP of the bucket (event-time bucket when `aggregate by` is
+ * used), keys[1..] the group-by values; vals are the base values in the order
+ * (per agg: SUM -> sum, AVG -> sum,count, COUNT -> count, MIN -> min, MAX -> max),
+ * de-duplicated as AggregationParser.populateFinalBaseAggregators does.                  */
+
+/* ---- lifecycle ---------------------------------------------------------------------------*/
+typedef struct sh_ctx sh_ctx;
+typedef struct sh_query sh_query;
+typedef struct sh_aggregation sh_aggregation;
+
+/* Device context on `device` (HIP ordinal). Multi-GPU: one process per GPU, each with its own
+ * context; sharding is done by the caller.                       */
+int sh_init(int32_t device, sh_ctx** out);
+int sh_ctx_destroy(sh_ctx* ctx);
+
+/* Replaces WindowProcessor.init + AttributeAggregatorExecutor.initAggregator + SelectorParser
+ * (core/query/processor/stream/window/BatchingWindowProcessor.java:63-67,
+ *  core/query/selector/attribute/aggregator/AttributeAggregatorExecutor.java:43-57).        */
+int sh_query_create(sh_ctx* ctx, const sh_query_desc* desc, sh_query** out);
+int sh_query_destroy(sh_query* q);
+
+/* Replaces InputHandler.send(Event[]) -> filter -> window.process -> QuerySelector.process ->
+ * OutputRateLimiter for every send in the batch. Host-memory batch (H2D included).          */
+int sh_push(sh_query* q, const sh_batch* batch, const sh_out** out);
+/* Same with device-resident columns (the HBM-resident hot path). *out is host memory.       */
+int sh_push_device(sh_query* q, const sh_batch* batch, const sh_out** out);
+/* TIMER path: advance the playback clock to `now` without events (Scheduler.onTimeChange). */
+int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
+
+int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* desc, sh_aggregation** out);
+int sh_aggregation_destroy(sh_aggregation* a);
+/* AggregationRuntime.processEvents via IncrementalAggregationProcessor.process
+ * (core/aggregation/IncrementalAggregationProcessor.java:66-101). */
+int sh_aggregation_push(sh_aggregation* a, const sh_batch* batch);
+int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* batch);
+int sh_aggregation_advance_time(sh_aggregation* a, int64_t now);
+/* Rows added to the table of `duration` since the previous call for that duration. */
+int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out);
+
+/* Pinned host buffers for zero-copy packing of Event[] chunks (hipHostMalloc). */
+int sh_alloc_pinned(int64_t bytes, void** out);
+int sh_free_pinned(void* p);
+
+/* Device timing of the last push: kernel time of the dominant kernel and of the whole push. */
+typedef struct {
+    double push_ms;        /* HIP-event time of the whole device pipeline of the last push */
+    double main_kernel_ms; /* HIP-event time of the aggregation kernel(s)                   */
+    int64_t main_kernel_bytes; /* algorithmic bytes the aggregation kernel(s) moved          */
+    int64_t events;        /* events consumed by the last push                              */
+} sh_stats;
+int sh_query_stats(sh_query* q, sh_stats* out);
+
+const char* sh_last_error(void);
+int32_t sh_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIDDHI_HIP_H */

@@ -1,0 +1,23 @@
+/* oracle.h — C API of the CPU restatement (TEST INFRASTRUCTURE ONLY; see siddhi_oracle.cpp).
+ * Same descriptor / batch / output structs as include/siddhi_hip.h so the parity tests drive both
+ * libraries with identical inputs. */
+#ifndef SIDDHI_ORACLE_H
+#define SIDDHI_ORACLE_H
+#include "../include/siddhi_hip.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+const char* or_last_error(void);
+void* or_query_create(const sh_query_desc* desc);
+void or_query_destroy(void* q);
+int or_push(void* q, const sh_batch* b, const sh_out** out);
+int or_advance_time(void* q, int64_t now, const sh_out** out);
+void* or_aggregation_create(const sh_aggregation_desc* desc);
+void or_aggregation_destroy(void* a);
+int or_aggregation_push(void* a, const sh_batch* b);
+int or_aggregation_advance_time(void* a, int64_t now);
+int or_aggregation_table(void* a, int32_t duration, const sh_out** out);
+#ifdef __cplusplus
+}
+#endif
+#endif

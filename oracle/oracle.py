@@ -1,0 +1,125 @@
+"""Python loader for the CPU restatement (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker. The product path (siddhi_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+from siddhi_amd import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.or_last_error.restype = C.c_char_p
+        L.or_query_create.argtypes = [P(abi.QueryDesc)]
+        L.or_query_create.restype = C.c_void_p
+        L.or_query_destroy.argtypes = [C.c_void_p]
+        L.or_push.argtypes = [C.c_void_p, P(abi.Batch), P(P(abi.Out))]
+        L.or_advance_time.argtypes = [C.c_void_p, C.c_int64, P(P(abi.Out))]
+        L.or_aggregation_create.argtypes = [P(abi.AggregationDesc)]
+        L.or_aggregation_create.restype = C.c_void_p
+        L.or_aggregation_destroy.argtypes = [C.c_void_p]
+        L.or_aggregation_push.argtypes = [C.c_void_p, P(abi.Batch)]
+        L.or_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
+        L.or_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(abi.Out))]
+        _lib = L
+    return _lib
+
+
+class OracleQuery:
+    """Window query run by the restatement. push()/advance_time() return decoded flushes."""
+
+    def __init__(self, spec: abi.QuerySpec):
+        self.spec = spec
+        self._desc = spec.desc()
+        self.h = lib().or_query_create(C.byref(self._desc))
+        if not self.h:
+            raise ValueError(lib().or_last_error().decode())
+
+    def push_raw(self, batch: abi.HostBatch):
+        out = C.POINTER(abi.Out)()
+        rc = lib().or_push(self.h, C.byref(batch.b), C.byref(out))
+        if rc != 0:
+            raise RuntimeError(lib().or_last_error().decode())
+        return out
+
+    def push(self, batch: abi.HostBatch):
+        return abi.decode_out(self.push_raw(batch))
+
+    def advance_time_raw(self, now: int):
+        out = C.POINTER(abi.Out)()
+        rc = lib().or_advance_time(self.h, now, C.byref(out))
+        if rc != 0:
+            raise RuntimeError(lib().or_last_error().decode())
+        return out
+
+    def advance_time(self, now: int):
+        return abi.decode_out(self.advance_time_raw(now))
+
+    def close(self):
+        if self.h:
+            lib().or_query_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class OracleAggregation:
+    def __init__(self, spec: abi.AggregationSpec):
+        self.spec = spec
+        self._desc = spec.desc()
+        self.h = lib().or_aggregation_create(C.byref(self._desc))
+        if not self.h:
+            raise ValueError(lib().or_last_error().decode())
+
+    def push(self, batch: abi.HostBatch):
+        rc = lib().or_aggregation_push(self.h, C.byref(batch.b))
+        if rc != 0:
+            raise RuntimeError(lib().or_last_error().decode())
+
+    def advance_time(self, now: int):
+        lib().or_aggregation_advance_time(self.h, now)
+
+    def table_raw(self, duration: int):
+        out = C.POINTER(abi.Out)()
+        rc = lib().or_aggregation_table(self.h, duration, C.byref(out))
+        if rc != 0:
+            raise RuntimeError(lib().or_last_error().decode())
+        return out
+
+    def table(self, duration: int):
+        fl = abi.decode_out(self.table_raw(duration))
+        return [r for f in fl for r in f.rows]
+
+    def close(self):
+        if self.h:
+            lib().or_aggregation_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

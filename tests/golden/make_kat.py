@@ -1,0 +1,190 @@
+"""Transcribe the reference's own TestNG known-answer cases into tests/golden/kat_reference.json.
+
+Each case records the query, the exact sends of the Java test (timestamps added: the wall-clock
+tests are transcribed to playback timestamps that reproduce the timer firing the test relies on),
+and ONLY the expectations the Java test asserts (counts, values). Nothing here is computed by
+the oracle: this file pins the oracle, it is not produced by it.
+
+ctest/ = /root/reference/modules/siddhi-core/src/test/java/io/siddhi/core/
+Run: python tests/golden/make_kat.py
+"""
+import json
+import os
+
+CASES = []
+
+
+def case(**kw):
+    CASES.append(kw)
+
+
+CSE_FLOAT_INT = "symbol string, price float, volume int"
+B = 1_000_000  # base timestamp for transcribed wall-clock sends
+
+# ---------------------------------------------------------------- lengthBatch (LengthBatchWindowTestCase)
+_six = [["IBM", 700.0, 1], ["WSO2", 60.5, 2], ["IBM", 700.0, 3], ["WSO2", 60.5, 4], ["IBM", 700.0, 5],
+        ["WSO2", 60.5, 6]]
+case(name="lengthBatch2_passthrough", source="ctest/query/window/LengthBatchWindowTestCase.java:89-132",
+     schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=4, output="current"),
+     sends=[[[B + i] + r] for i, r in enumerate(_six)],
+     expect=dict(in_count=4, in_order_col="volume", in_order=[1, 2, 3, 4]))
+case(name="lengthBatch3_all_events", source="ctest/query/window/LengthBatchWindowTestCase.java:134-190",
+     schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=2, output="all"),
+     sends=[[[B + i] + r] for i, r in enumerate(_six)],
+     expect=dict(in_count=6, remove_count=4, in_order_col="volume", in_order=[1, 2, 3, 4, 5, 6],
+                 remove_order=[1, 2, 3, 4]))
+_lb4 = [["IBM", 10.0, 0], ["WSO2", 20.0, 1], ["IBM", 30.0, 0], ["WSO2", 40.0, 1], ["IBM", 50.0, 0],
+        ["WSO2", 60.0, 1]]
+case(name="lengthBatch4_sum", source="ctest/query/window/LengthBatchWindowTestCase.java:192-234",
+     schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=4, aggs=[["sum", "price"]], output="current"),
+     sends=[[[B + i] + r] for i, r in enumerate(_lb4)],
+     expect=dict(in_count=1, remove_count=0, values=[[100.0]]))
+case(name="lengthBatch5_expired", source="ctest/query/window/LengthBatchWindowTestCase.java:236-277",
+     schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=2, output="expired"),
+     sends=[[[B + i] + r] for i, r in enumerate(_six)],
+     expect=dict(remove_count=4, in_count=0, remove_order=[1, 2, 3, 4]))
+_lb6 = _lb4 + [["WSO2", 60.0, 1], ["IBM", 70.0, 0], ["WSO2", 80.0, 1]]
+case(name="lengthBatch6_sum_all_events", source="ctest/query/window/LengthBatchWindowTestCase.java:279-327",
+     schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=4, aggs=[["sum", "price"]], output="all"),
+     sends=[[[B + i] + r] for i, r in enumerate(_lb6)],
+     expect=dict(in_count=2, values=[[100.0], [240.0]]))
+_nine = _six + [["WSO2", 60.5, 4], ["IBM", 700.0, 5], ["WSO2", 60.5, 6]]
+case(name="lengthBatch11_stream_current_count", source="ctest/query/window/LengthBatchWindowTestCase.java:534-590",
+     schema=CSE_FLOAT_INT,
+     query=dict(window="lengthBatch", param=4, stream_current=True, aggs=[["count", None]], output="current"),
+     sends=[[[B + i] + r] for i, r in enumerate(_nine)],
+     expect=dict(in_count=9, flush_sizes=[1] * 9, value_range=[0, 1, 4]))
+case(name="lengthBatch12_stream_current_expired", source="ctest/query/window/LengthBatchWindowTestCase.java:592-646",
+     schema=CSE_FLOAT_INT,
+     query=dict(window="lengthBatch", param=4, stream_current=True, aggs=[["count", None]], output="expired"),
+     sends=[[[B + i] + r] for i, r in enumerate(_nine)],
+     expect=dict(total_count=2, flush_sizes=[1, 1], values=[[0], [0]]))
+
+# ---------------------------------------------------------------- playback (PlaybackTestCase)
+case(name="playback1_timeBatch", source="ctest/managment/PlaybackTestCase.java:48-107",
+     schema=CSE_FLOAT_INT, query=dict(window="timeBatch", param=1000, output="all"),
+     sends=[[[B, "IBM", 700.0, 0]], [[B + 500, "WSO2", 60.5, 1]], [[B + 1000, "GOOGLE", 85.0, 1]],
+            [[B + 2000, "ORACLE", 90.5, 1]]],
+     expect=dict(in_count=3, remove_count=2))
+case(name="playback2_timeBatch_start", source="ctest/managment/PlaybackTestCase.java:109-169",
+     schema=CSE_FLOAT_INT,
+     query=dict(window="timeBatch", param=2000, start_time=0, aggs=[["sum", "price"]], output="current"),
+     sends=[[[0, "IBM", 700.0, 0]], [[0, "WSO2", 60.5, 1]], [[8500, "WSO2", 60.5, 1]], [[8500, "II", 60.5, 1]],
+            [[21500, "TT", 60.5, 1]], [[21500, "YY", 60.5, 1]], [[26500, "ZZ", 0.0, 0]]],
+     expect=dict(in_count=3, remove_count=0))
+case(name="playback7_time", source="ctest/managment/PlaybackTestCase.java:383-432",
+     schema=CSE_FLOAT_INT, query=dict(window="time", param=2000, output="all"),
+     sends=[[[B, "IBM", 700.0, 0]], [[B, "WSO2", 60.5, 1]], [[B + 2000, "GOOGLE", 0.0, 1]]],
+     expect=dict(in_count=3, remove_count=2))
+
+# ---------------------------------------------------------------- sliding max (MaxAggregatorExtensionTestCase)
+# wall-clock sends at t and t+100, then the two expiry timers fire at t+1000 and t+1100
+case(name="max_sliding_time", source="ctest/query/aggregator/MaxAggregatorExtensionTestCase.java:47-101",
+     schema="price1 double, price2 double, price3 double",
+     query=dict(window="time", param=1000, aggs=[["max", "price1"]], output="all"),
+     sends=[[[B, 36.0, 36.75, 35.75]], [[B + 100, 37.88, 38.12, 37.62]], {"advance": B + 1000},
+            {"advance": B + 1100}],
+     expect=dict(total_count=4, values=[[36.0], [37.88], [37.88], [None]]))
+
+# ---------------------------------------------------------------- partitioned timeBatch (WindowPartitionTestCase)
+case(name="partition5_timeBatch", source="ctest/query/partition/WindowPartitionTestCase.java:291-348",
+     schema="symbol string, price double, volume int",
+     query=dict(window="timeBatch", param=5000, partition="symbol", aggs=[["sum", "price"]], output="current"),
+     sends=[[[B + i] + r] for i, r in enumerate([["IBM", 70.0, 100], ["WSO2", 700.0, 100], ["IBM", 100.0, 100],
+                                                ["IBM", 200.0, 100], ["ORACLE", 75.6, 100],
+                                                ["WSO2", 1000.0, 100], ["WSO2", 500.0, 100]])]
+     + [{"advance": B + 7000}],
+     expect=dict(in_count_max=7, remove_count=0, min_in_count=1, partition_values={"IBM": 370.0, "WSO2": 2200.0,
+                                                                                    "ORACLE": 75.6}))
+
+# ---------------------------------------------------------------- incremental aggregation (Aggregation1TestCase)
+AGG_SCHEMA = "symbol string, price float, lastClosingPrice float, volume long, quantity int, timestamp long"
+_t5 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+       ["WSO2", 60.0, 44.0, 200, 56, 1496289952000], ["WSO2", 100.0, 0.0, 200, 16, 1496289952500],
+       ["IBM", 100.0, 0.0, 200, 26, 1496289954000], ["IBM", 100.0, 0.0, 200, 96, 1496289954500]]
+case(name="aggregation5_seconds", source="ctest/aggregation/Aggregation1TestCase.java:138-189",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "hour"]),
+     sends=[[[r[-1]] + r] for r in _t5] + [{"advance": 1496289954500 + 3_600_000 * 2}],
+     expect=dict(table="sec", rows=[[1496289952000, "WSO2", 80.0, 160.0], [1496289950000, "WSO2", 60.0, 120.0],
+                                    [1496289954000, "IBM", 100.0, 200.0]]))
+_t6 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+       ["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+       ["IBM", 100.0, 0.0, 200, 26, 1496289951000], ["IBM", 100.0, 0.0, 200, 96, 1496289951000],
+       ["IBM", 900.0, 0.0, 200, 60, 1496289952000], ["IBM", 500.0, 0.0, 200, 7, 1496289952000],
+       ["WSO2", 60.0, 44.0, 200, 56, 1496289953000], ["WSO2", 100.0, 0.0, 200, 16, 1496289953000],
+       ["IBM", 400.0, 0.0, 200, 9, 1496289953000], ["WSO2", 140.0, 0.0, 200, 11, 1496289953000],
+       ["IBM", 600.0, 0.0, 200, 6, 1496289954000], ["IBM", 1000.0, 0.0, 200, 9, 1496290016000]]
+case(name="aggregation6_seconds_to_year", source="ctest/aggregation/Aggregation1TestCase.java:191-299",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[r[-1]] + r] for r in _t6] + [{"advance": 1496290016000 + 400 * 86_400_000}],
+     expect=dict(table="sec", rows=[[1496289950000, "WSO2", 60.0, 240.0], [1496289951000, "IBM", 100.0, 200.0],
+                                    [1496289952000, "IBM", 700.0, 1400.0], [1496289953000, "WSO2", 100.0, 300.0],
+                                    [1496289953000, "IBM", 400.0, 400.0], [1496289954000, "IBM", 600.0, 600.0],
+                                    [1496290016000, "IBM", 1000.0, 1000.0]]))
+
+# ---------------------------------------------------------------- filters (FilterTestCase1): expected counts
+F = "ctest/query/FilterTestCase1.java"
+FL = "symbol string, price float, volume long"
+case(name="filter1", source=F + ":60-118", schema=FL, query=dict(window=None, filter=[">", 70, "price"]),
+     sends=[[[B, "IBM", 700.0, 100]], [[B + 1, "WSO2", 60.5, 200]]], expect=dict(in_count=1))
+case(name="filter2", source=F + ":120-152", schema=FL, query=dict(window=None, filter=[">", 150, "volume"]),
+     sends=[[[B, "IBM", 700.0, 100]], [[B + 1, "WSO2", 60.5, 200]]], expect=dict(in_count=1))
+case(name="filter3", source=F + ":154-186", schema=CSE_FLOAT_INT, query=dict(window=None, filter=[">", 70, "price"]),
+     sends=[[[B, "WSO2", 55.6, 100]], [[B + 1, "IBM", 75.6, 100]], [[B + 2, "WSO2", 57.6, 200]]],
+     expect=dict(in_count=2))
+_v3 = lambda schema_t: [[[B, "WSO2", 50.0, 60]], [[B + 1, "WSO2", 70.0, 40]], [[B + 2, "WSO2", 44.0, 200]]]
+for nm, rng, vt, const in [("filter4", ":188-217", "long", ["float", 50.0]), ("filter5", ":219-249", "long", ["long", 50]),
+                           ("filter6", ":251-281", "int", ["long", 50]), ("filter7", ":283-313", "double", ["long", 50]),
+                           ("filter8", ":315-346", "float", ["long", 50]), ("filter9", ":348-379", "float", ["float", 50.0]),
+                           ("filter10", ":381-411", "double", ["double", 50.0]),
+                           ("filter11", ":413-443", "double", ["float", 50.0]),
+                           ("filter12", ":445-475", "double", ["int", 45]),
+                           ("filter13", ":477-507", "float", ["double", 50.0]),
+                           ("filter14", ":509-539", "float", ["int", 45]),
+                           ("filter16", ":574-603", "long", ["double", 50.0])]:
+    case(name=nm, source=F + rng, schema=f"symbol string, price float, volume {vt}",
+         query=dict(window=None, filter=[">", "volume", const]), sends=_v3(vt), expect=dict(in_count=2))
+case(name="filter15", source=F + ":541-572", schema="symbol string, price float, volume float, quantity int",
+     query=dict(window=None, filter=[">", "quantity", ["double", 4.0]]),
+     sends=[[[B, "WSO2", 50.0, 60.0, 5]], [[B + 1, "WSO2", 70.0, 60.0, 2]], [[B + 2, "WSO2", 60.0, 200.0, 4]]],
+     expect=dict(in_count=1))
+case(name="filter21", source=F + ":746-776", schema=FL, query=dict(window=None, filter=["!=", "volume", 100]),
+     sends=[[[B, "WSO2", 55.6, 100]], [[B + 1, "WSO2", 57.6, 10]]], expect=dict(in_count=1))
+case(name="filter22", source=F + ":778-810", schema="symbol string, price float, volume double",
+     query=dict(window=None, filter=["and", [">", "volume", ["long", 12]], ["<", "price", 56]]),
+     sends=[[[B, "WSO2", 55.6, 100.0]], [[B + 1, "WSO2", 57.6, 10.0]]], expect=dict(in_count=1))
+case(name="filter23", source=F + ":812-841", schema=FL,
+     query=dict(window=None, filter=["and", ["and", ["!=", "symbol", ["string", "WSO2"]], ["!=", "volume", ["long", 55]]],
+                                     ["!=", "price", ["float", 45.0]]]),
+     sends=[[[B, "WSO2", 45.0, 100]], [[B + 1, "IBM", 35.0, 50]]], expect=dict(in_count=1))
+case(name="filter24", source=F + ":843-873", schema=FL, query=dict(window=None, filter=["!=", "volume", ["float", 50.0]]),
+     sends=[[[B, "WSO2", 45.0, 100]], [[B + 1, "IBM", 35.0, 50]]], expect=dict(in_count=1))
+case(name="filter25", source=F + ":875-906", schema=FL, query=dict(window=None, filter=["!=", "price", ["long", 35]]),
+     sends=[[[B, "WSO2", 45.0, 100]], [[B + 1, "IBM", 35.0, 50]]], expect=dict(in_count=1))
+case(name="filter26", source=F + ":908-938", schema=FL,
+     query=dict(window=None, filter=["and", ["!=", "volume", 100], ["!=", "volume", ["double", 70.0]]]),
+     sends=[[[B, "WSO2", 55.6, 100]], [[B + 1, "IBM", 57.6, 10]]], expect=dict(in_count=1))
+case(name="filter27", source=F + ":940-969", schema=FL,
+     query=dict(window=None, filter=["or", ["!=", "price", ["double", 53.6]], ["!=", "price", 87]]),
+     sends=[[[B, "WSO2", 55.6, 100]], [[B + 1, "IBM", 57.6, 10]]], expect=dict(in_count=2))
+case(name="filter28", source=F + ":971-1002", schema=CSE_FLOAT_INT,
+     query=dict(window=None, filter=["and", ["!=", "volume", ["float", 40.0]], ["!=", "volume", 400]]),
+     sends=[[[B, "WSO2", 55.5, 40]], [[B + 1, "WSO2", 53.5, 50]], [[B + 2, "WSO2", 50.5, 400]]],
+     expect=dict(in_count=1))
+case(name="filter29", source=F + ":1004-1034", schema=CSE_FLOAT_INT,
+     query=dict(window=None, filter=["and", ["!=", "volume", ["double", 40.0]], ["!=", "volume", ["double", 400.0]]]),
+     sends=[[[B, "WSO2", 55.5, 40]], [[B + 1, "WSO2", 53.5, 50]], [[B + 2, "WSO2", 50.5, 400]]],
+     expect=dict(in_count=1))
+case(name="filter30_bool", source=F + ":1036-1064", schema="symbol string, price float, available bool",
+     query=dict(window=None, filter=["!=", "available", ["bool", 1]]),
+     sends=[[[B, "IBM", 55.6, True]], [[B + 1, "WSO2", 57.6, False]]], expect=dict(in_count=1))
+
+if __name__ == "__main__":
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat_reference.json")
+    with open(out, "w") as f:
+        json.dump({"generated_by": "tests/golden/make_kat.py", "cases": CASES}, f, indent=1)
+    print(f"wrote {len(CASES)} cases to {out}")
