@@ -1,0 +1,195 @@
+// sh_device.h — device helpers for the gfx950 kernels: Java value semantics, filter evaluation,
+// group-key hashing, wave64 / workgroup scans.
+#pragma once
+
+#include "sh_internal.h"
+
+namespace shd {
+
+// ---- column access ---------------------------------------------------------------------------
+// Raw 8-byte form: integral types sign-extended to int64, FLOAT widened exactly to double bits,
+// DOUBLE bits. Same convention as the oracle (oracle/siddhi_oracle.cpp load_event).
+__device__ __forceinline__ i64 load_raw(const ColSet& cs, int c, i64 e) {
+    switch (cs.type[c]) {
+        case SH_T_INT:
+        case SH_T_STRID: return (i64)((const int*)cs.ptr[c])[e];
+        case SH_T_LONG: return ((const i64*)cs.ptr[c])[e];
+        case SH_T_BOOL: return ((const unsigned char*)cs.ptr[c])[e] ? 1 : 0;
+        case SH_T_FLOAT: return __double_as_longlong((double)((const float*)cs.ptr[c])[e]);
+        default: return __double_as_longlong(((const double*)cs.ptr[c])[e]);
+    }
+}
+
+__device__ __forceinline__ bool is_fp(int t) { return t == SH_T_FLOAT || t == SH_T_DOUBLE; }
+__device__ __forceinline__ int prank(int t) { return t == SH_T_LONG ? 2 : t == SH_T_FLOAT ? 3 : t == SH_T_DOUBLE ? 4 : 1; }
+
+// Compare executors (core/executor/condition/compare/**): binary numeric promotion, except ==/!=
+// between FLOAT and LONG which compare doubleValue() of both sides (EqualCompare...FloatLong.java).
+__device__ __forceinline__ bool java_cmp(int op, int ta, i64 a, int tb, i64 b) {
+    int r = max(prank(ta), prank(tb));
+    bool eq = (op == SH_OP_EQ || op == SH_OP_NE);
+    if (eq && ((ta == SH_T_FLOAT && tb == SH_T_LONG) || (ta == SH_T_LONG && tb == SH_T_FLOAT))) r = 4;
+    if (r >= 3) {
+        double x = is_fp(ta) ? __longlong_as_double(a) : (double)a;
+        double y = is_fp(tb) ? __longlong_as_double(b) : (double)b;
+        if (r == 3) {
+            float fx = is_fp(ta) ? (float)x : (float)a;
+            float fy = is_fp(tb) ? (float)y : (float)b;
+            switch (op) {
+                case SH_OP_GT: return fx > fy; case SH_OP_GE: return fx >= fy;
+                case SH_OP_LT: return fx < fy; case SH_OP_LE: return fx <= fy;
+                case SH_OP_EQ: return fx == fy; default: return fx != fy;
+            }
+        }
+        switch (op) {
+            case SH_OP_GT: return x > y; case SH_OP_GE: return x >= y;
+            case SH_OP_LT: return x < y; case SH_OP_LE: return x <= y;
+            case SH_OP_EQ: return x == y; default: return x != y;
+        }
+    }
+    switch (op) {
+        case SH_OP_GT: return a > b; case SH_OP_GE: return a >= b;
+        case SH_OP_LT: return a < b; case SH_OP_LE: return a <= b;
+        case SH_OP_EQ: return a == b; default: return a != b;
+    }
+}
+
+// FilterProcessor.process (core/query/processor/filter/FilterProcessor.java:47-60): a postfix
+// program over column refs and constants; the result must be TRUE to keep the event.
+__device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& cs, i64 e) {
+    if (f.n == 0) return true;
+    i64 sv[16];
+    int st[16];
+    int sp = 0;
+    for (int i = 0; i < f.n; i++) {
+        const FilterOpD& o = f.ops[i];
+        switch (o.op) {
+            case SH_OP_COL: sv[sp] = load_raw(cs, o.col, e); st[sp] = cs.type[o.col]; sp++; break;
+            case SH_OP_CONST:
+                st[sp] = o.type;
+                if (o.type == SH_T_FLOAT) sv[sp] = __double_as_longlong((double)(float)o.dval);
+                else if (o.type == SH_T_DOUBLE) sv[sp] = __double_as_longlong(o.dval);
+                else if (o.type == SH_T_INT) sv[sp] = (i64)(int)o.ival;
+                else sv[sp] = o.ival;
+                sp++;
+                break;
+            case SH_OP_AND: sp--; sv[sp - 1] = (sv[sp - 1] && sv[sp]) ? 1 : 0; st[sp - 1] = SH_T_BOOL; break;
+            case SH_OP_OR: sp--; sv[sp - 1] = (sv[sp - 1] || sv[sp]) ? 1 : 0; st[sp - 1] = SH_T_BOOL; break;
+            case SH_OP_NOT: sv[sp - 1] = sv[sp - 1] ? 0 : 1; st[sp - 1] = SH_T_BOOL; break;
+            default: {
+                sp--;
+                bool r = java_cmp(o.op, st[sp - 1], sv[sp - 1], st[sp], sv[sp]);
+                sv[sp - 1] = r ? 1 : 0;
+                st[sp - 1] = SH_T_BOOL;
+            }
+        }
+    }
+    return sp > 0 && sv[sp - 1] != 0;
+}
+
+// ---- group keys ---------------------------------------------------------------------------------
+// GroupByKeyGenerator.constructEventKey (core/query/selector/GroupByKeyGenerator.java:63-73) keys
+// by the values' string form; for the integral key columns string equality is value equality.
+__device__ __forceinline__ u64 make_key(const KeyPlan& kp, const ColSet& cs, i64 e) {
+    if (kp.n == 0) return 0;
+    if (kp.n == 1) return (u64)load_raw(cs, kp.col[0], e);
+    u64 a = (u64)(u32)load_raw(cs, kp.col[0], e);
+    u64 b = (u64)(u32)load_raw(cs, kp.col[1], e);
+    return (a << 32) | b;
+}
+
+__device__ __forceinline__ void unpack_key(const KeyPlan& kp, u64 key, i64* out, i64 stride) {
+    if (kp.n == 1) out[0] = (i64)key;
+    else if (kp.n == 2) {
+        out[0] = (i64)(int)(u32)(key >> 32);
+        out[stride] = (i64)(int)(u32)key;
+    }
+}
+
+__device__ __forceinline__ u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// Open-addressing lookup-or-insert. The position is the group slot. A plain load that sees a
+// stale EMPTY (another CU inserted meanwhile) is corrected by the CAS, which reads the line at the
+// memory side; a non-EMPTY key never changes, so it can't be stale.
+__device__ __forceinline__ u32 key_slot(const KeyTable& kt, u64 key) {
+    if (key == kEmptyKey) return kt.mask + 1;
+    u32 h = (u32)mix64(key) & kt.mask;
+    for (u32 probe = 0; probe <= kt.mask; probe++) {
+        u64 k = kt.keys[h];
+        if (k == key) return h;
+        if (k == kEmptyKey) {
+            u64 old = atomicCAS(&kt.keys[h], kEmptyKey, key);
+            if (old == kEmptyKey) { atomicAdd(kt.n_keys, 1u); return h; }
+            if (old == key) return h;
+        }
+        h = (h + 1) & kt.mask;
+    }
+    atomicExch(kt.overflow, 1);
+    return 0;
+}
+
+__device__ __forceinline__ u64 slot_key(const KeyTable& kt, u32 pos) {
+    return pos > kt.mask ? kEmptyKey : kt.keys[pos];
+}
+
+// ---- scans --------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_incl_scan(T v, Op op) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane_id() >= d) v = op(v, o);
+    }
+    return v;
+}
+
+struct SumOp { __device__ i64 operator()(i64 a, i64 b) const { return a + b; } };
+struct MaxOp { __device__ i64 operator()(i64 a, i64 b) const { return a > b ? a : b; } };
+struct MinOp { __device__ i64 operator()(i64 a, i64 b) const { return a < b ? a : b; } };
+
+// Workgroup exclusive scan (kBlock threads); returns exclusive prefix, *total gets the reduction.
+template <typename Op>
+__device__ __forceinline__ i64 block_excl_scan(i64 v, Op op, i64 identity, i64* total) {
+    __shared__ i64 wsum[kBlock / 64];
+    i64 incl = wave_incl_scan(v, op);
+    int w = threadIdx.x >> 6;
+    if (lane_id() == 63) wsum[w] = incl;
+    __syncthreads();
+    i64 pre = identity;
+    for (int i = 0; i < w; i++) pre = op(pre, wsum[i]);
+    i64 tot = identity;
+    for (int i = 0; i < kBlock / 64; i++) tot = op(tot, wsum[i]);
+    __syncthreads();
+    if (total) *total = tot;
+    i64 excl = __shfl_up(incl, 1, 64);
+    if (lane_id() == 0) excl = identity;
+    return op(pre, excl);
+}
+
+template <typename Op>
+__device__ __forceinline__ i64 block_reduce(i64 v, Op op, i64 identity) {
+    i64 t;
+    block_excl_scan(v, op, identity, &t);
+    return t;
+}
+
+// Send bookkeeping: InputHandler.send(Event[]) sets the playback clock from the last event of
+// each send (core/stream/input/InputHandler.java:85-96).
+__device__ __forceinline__ i64 send_len(const WinParams& wp) { return wp.send_size > 0 ? wp.send_size : wp.N; }
+__device__ __forceinline__ bool is_send_last(const WinParams& wp, i64 e) {
+    i64 s = send_len(wp);
+    return ((e + 1) % s == 0) || (e == wp.N - 1);
+}
+__device__ __forceinline__ i64 send_last_of(const WinParams& wp, i64 e) {
+    i64 s = send_len(wp);
+    i64 l = (e / s) * s + s - 1;
+    return l < wp.N - 1 ? l : wp.N - 1;
+}
+
+}  // namespace shd

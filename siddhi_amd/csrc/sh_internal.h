@@ -1,0 +1,163 @@
+// sh_internal.h — structures shared by the host runtime (sh_runtime.cpp) and the gfx950 kernels
+// (sh_kernels.hip). Nothing here crosses the public C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/siddhi_hip.h"
+
+namespace shd {
+
+typedef unsigned long long u64;
+typedef int64_t i64;
+typedef unsigned int u32;
+
+constexpr int kMaxFilterOps = 32;
+constexpr int kBlock = 256;           // threads per workgroup (4 wave64)
+constexpr int kItems = 8;             // events per thread in the scan-type passes
+constexpr int kTile = kBlock * kItems;  // events per workgroup in the scan-type passes
+constexpr u64 kEmptyKey = 0x8000000000000001ull;  // open-addressing EMPTY sentinel
+
+// Filter program (postfix), evaluated per event on device. Mirrors sh_filter_op.
+struct FilterOpD {
+    int op, type, col, pad;
+    i64 ival;
+    double dval;
+};
+struct FilterProg {
+    int n;
+    int pad;
+    FilterOpD ops[kMaxFilterOps];
+};
+
+// Stream columns of one batch (device pointers) with their SH_T_* types.
+struct ColSet {
+    const void* ptr[SH_MAX_COLS];
+    int type[SH_MAX_COLS];
+    int n;
+    int pad;
+};
+
+// Aggregator execution plan. kinds restate the Java State classes for BATCH (add-only) use:
+//   Sum{Long,Int} -> SUM_L, Sum{Double,Float} -> SUM_D, Avg* -> AVG (double value, long count),
+//   Count -> COUNT, Min/Max typed compare on the input type.
+enum AggKind {
+    AK_COUNT = 0, AK_SUM_L, AK_SUM_D, AK_AVG, AK_MIN_L, AK_MIN_F, AK_MIN_D, AK_MAX_L, AK_MAX_F, AK_MAX_D
+};
+struct AggPlan {
+    int n;         // aggregators
+    int n_fields;  // 8-byte LDS fields per key
+    int n_vcols;   // distinct value columns carried by records / pending
+    int pad;
+    int kind[SH_MAX_AGGS];
+    int field[SH_MAX_AGGS];  // LDS field index (-1 for COUNT)
+    int vcol[SH_MAX_AGGS];   // value-column slot (-1 for COUNT)
+    int vcol_src[SH_MAX_AGGS];   // stream column index of value slot v
+    int vcol_type[SH_MAX_AGGS];  // SH_T_* of value slot v
+};
+
+// Group key plan: 0, 1 or 2 integral columns packed into a u64.
+struct KeyPlan {
+    int n;
+    int col[SH_MAX_GROUP];
+    int type[SH_MAX_GROUP];
+    int pad;
+};
+
+// Hash table (key -> position = group slot). positions [0, mask] plus the reserved mask+1
+// for a key equal to the EMPTY sentinel.
+struct KeyTable {
+    u64* keys;
+    u32 mask;
+    u32 pad;
+    u32* n_keys;      // distinct keys inserted
+    int* overflow;    // set when probing exhausts the table
+};
+
+// Window assignment for one push (see DESIGN.md "Window assignment").
+struct WinParams {
+    int kind;          // SH_WIN_LENGTH_BATCH / SH_WIN_TIME_BATCH
+    int e0_valid;      // timeBatch: nextEmitTime initialised
+    int clock_valid;   // playback clock initialised before the push
+    int has_start;
+    i64 L;             // lengthBatch length
+    i64 T;             // timeBatch period
+    i64 E0;            // timeBatch: first nextEmitTime
+    i64 start_time;
+    i64 clock0;        // clock before the push
+    i64 W_open;        // window number of the pending events
+    i64 n_pend;        // pending (open-window) events carried in
+    i64 send_size;     // events per send (0 = one send)
+    i64 N;             // new events in this push
+};
+
+// Result of the block-aggregate scan (written by k_scan_blocks, read back by the host).
+struct PushInfo {
+    i64 total_pass;
+    i64 max_tl;        // max ts over send-last events (INT64_MIN if none)
+    i64 first_pass;    // first passing new event (INT64_MAX if none)
+    i64 E0;            // nextEmitTime after initialisation
+    int e0_valid;
+    int n_bounds;      // boundaries appended by k_boundaries
+    i64 pad[2];
+};
+
+// A window boundary inside the push: first combined index of a new window.
+struct Bound {
+    i64 idx;         // combined index (pending first, then new events)
+    i64 W;           // window number starting at idx
+    i64 clock;       // clock of event idx
+    i64 clock_prev;  // clock of event idx-1
+    i64 pcb;         // passing new events before idx (new-event space)
+    i64 pad;
+};
+
+// A closed segment handed to the aggregation kernel: combined index range of one window.
+struct Segment {
+    i64 lo, hi;
+};
+
+// Temp row written by the aggregation kernel; ordered afterwards by `first`.
+struct RowTmp {
+    u32 pos;
+    u32 first;
+    u32 last;
+    u32 pad;
+};
+
+// Launchers (sh_kernels.hip).
+void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
+                     i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk);
+void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
+                        WinParams wp, PushInfo* info);
+void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
+                       const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
+                       int max_bounds, int nblk);
+void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
+                      const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const i64* ts, ColSet cols,
+                      FilterProg f, KeyPlan kp, KeyTable kt, AggPlan ap, RowTmp* rows, u64* row_vals,
+                      u32* row_counter, unsigned char* flags, u32* rowref, i64* seg_rows,
+                      // partitioned source (P > 1)
+                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
+                      const i64* part_off);
+void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
+void launch_scan_sum(hipStream_t s, i64* a, int n);
+void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
+                 const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
+                 const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                 unsigned char* out_nulls);
+void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt,
+                            AggPlan ap, i64 e_lo, i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre,
+                            u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap);
+// multisplit (partitioned aggregation, P > 1)
+void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const i64* ts, ColSet cols,
+                     FilterProg f, KeyPlan kp, KeyTable kt, int P, i64* counts, int nblk);
+void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
+                       i64 pend_cap, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt,
+                       AggPlan ap, int P, const i64* offsets, int nblk, u32* rec_pos, u32* rec_idx,
+                       u64* rec_vals, i64 rec_cap);
+void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
+void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
+
+}  // namespace shd

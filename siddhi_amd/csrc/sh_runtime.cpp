@@ -1,0 +1,229 @@
+// sh_runtime.cpp — host runtime behind include/siddhi_hip.h: query objects, device buffers,
+// launch sequencing and output assembly. Runs only the HIP path; any feature without a GPU
+// implementation is refused with SH_ERR_UNSUPPORTED (there is no CPU fallback).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sh_internal.h"
+#include "sh_runtime.h"
+
+using namespace shd;
+
+thread_local std::string g_last_error;
+
+int sh_fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// device buffer helpers
+// ---------------------------------------------------------------------------------------------
+int DevBuf::reserve(size_t n, bool keep) {
+    if (n <= cap) return SH_OK;
+    size_t ncap = std::max(n, cap + cap / 2);
+    void* np = nullptr;
+    hipError_t e = hipMalloc(&np, ncap);
+    if (e != hipSuccess) return sh_fail(SH_ERR_OOM, "hipMalloc failed: " + std::string(hipGetErrorString(e)));
+    if (p) {
+        if (keep && used) {
+            e = hipMemcpy(np, p, used, hipMemcpyDeviceToDevice);
+            if (e != hipSuccess) return sh_fail(SH_ERR_DEVICE, "hipMemcpy (grow) failed");
+        }
+        (void)hipDeviceSynchronize();
+        (void)hipFree(p);
+    }
+    p = np;
+    cap = ncap;
+    return SH_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = used = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------------
+extern "C" int sh_init(int32_t device, sh_ctx** out) {
+    if (!out) return sh_fail(SH_ERR_INVALID, "sh_init: out is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return sh_fail(SH_ERR_DEVICE, "no HIP device visible (this library has no CPU path)");
+    if (device < 0 || device >= n) return sh_fail(SH_ERR_INVALID, "sh_init: bad device ordinal");
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return sh_fail(SH_ERR_DEVICE, std::string("built for gfx950, found ") + prop.gcnArchName);
+    sh_ctx* c = new sh_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    c->max_lds = (int)prop.sharedMemPerBlock;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return sh_fail(SH_ERR_DEVICE, "hipStreamCreate failed");
+    }
+    *out = c;
+    return SH_OK;
+}
+
+extern "C" int sh_ctx_destroy(sh_ctx* c) {
+    if (!c) return SH_OK;
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SH_OK;
+}
+
+extern "C" int sh_alloc_pinned(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return sh_fail(SH_ERR_INVALID, "sh_alloc_pinned: bad arguments");
+    HIPCHK(hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return SH_OK;
+}
+
+extern "C" int sh_free_pinned(void* p) {
+    if (p) HIPCHK(hipHostFree(p));
+    return SH_OK;
+}
+
+extern "C" const char* sh_last_error(void) { return g_last_error.c_str(); }
+extern "C" int32_t sh_abi_version(void) { return SH_ABI_VERSION; }
+
+// ---------------------------------------------------------------------------------------------
+// descriptor compilation
+// ---------------------------------------------------------------------------------------------
+static bool integral(int t) { return t == SH_T_INT || t == SH_T_LONG || t == SH_T_STRID || t == SH_T_BOOL; }
+static bool numeric(int t) { return t == SH_T_INT || t == SH_T_LONG || t == SH_T_FLOAT || t == SH_T_DOUBLE; }
+
+int compile_filter(int n_ops, const sh_filter_op* ops, int n_cols, const int32_t* types, FilterProg& fp) {
+    if (n_ops < 0 || n_ops > kMaxFilterOps) return sh_fail(SH_ERR_UNSUPPORTED, "filter program longer than 32 ops");
+    fp = FilterProg{};
+    fp.n = n_ops;
+    int depth = 0;
+    for (int i = 0; i < n_ops; i++) {
+        const sh_filter_op& o = ops[i];
+        FilterOpD d{o.op, o.type, o.col, 0, o.ival, o.dval};
+        switch (o.op) {
+            case SH_OP_COL:
+                if (o.col < 0 || o.col >= n_cols) return sh_fail(SH_ERR_INVALID, "filter column out of range");
+                if (types[o.col] == SH_T_STRID && false) {}
+                depth++;
+                break;
+            case SH_OP_CONST: depth++; break;
+            case SH_OP_NOT: if (depth < 1) return sh_fail(SH_ERR_INVALID, "filter stack underflow"); break;
+            case SH_OP_GT: case SH_OP_GE: case SH_OP_LT: case SH_OP_LE: case SH_OP_EQ: case SH_OP_NE:
+            case SH_OP_AND: case SH_OP_OR:
+                if (depth < 2) return sh_fail(SH_ERR_INVALID, "filter stack underflow");
+                depth--;
+                break;
+            default: return sh_fail(SH_ERR_INVALID, "unknown filter opcode");
+        }
+        if (depth > 16) return sh_fail(SH_ERR_UNSUPPORTED, "filter stack deeper than 16");
+        fp.ops[i] = d;
+    }
+    if (n_ops > 0 && depth != 1) return sh_fail(SH_ERR_INVALID, "filter program leaves stack depth != 1");
+    return SH_OK;
+}
+
+int compile_aggs(int n_aggs, const sh_agg_spec* aggs, int n_cols, const int32_t* types, AggPlan& ap,
+                 int32_t* out_types) {
+    ap = AggPlan{};
+    ap.n = n_aggs;
+    for (int a = 0; a < n_aggs; a++) {
+        int fn = aggs[a].fn, col = aggs[a].col;
+        if (fn == SH_AGG_COUNT) {
+            ap.kind[a] = AK_COUNT; ap.field[a] = -1; ap.vcol[a] = -1;
+            out_types[a] = SH_T_LONG;
+            continue;
+        }
+        if (col < 0 || col >= n_cols) return sh_fail(SH_ERR_INVALID, "aggregator column out of range");
+        int t = types[col];
+        if (!numeric(t)) return sh_fail(SH_ERR_INVALID, "aggregator over a non-numeric attribute");
+        int v = -1;
+        for (int j = 0; j < ap.n_vcols; j++) if (ap.vcol_src[j] == col) v = j;
+        if (v < 0) { v = ap.n_vcols++; ap.vcol_src[v] = col; ap.vcol_type[v] = t; }
+        ap.vcol[a] = v;
+        ap.field[a] = ap.n_fields++;
+        bool fp = t == SH_T_FLOAT || t == SH_T_DOUBLE;
+        switch (fn) {
+            case SH_AGG_SUM: ap.kind[a] = fp ? AK_SUM_D : AK_SUM_L; out_types[a] = fp ? SH_T_DOUBLE : SH_T_LONG; break;
+            case SH_AGG_AVG: ap.kind[a] = AK_AVG; out_types[a] = SH_T_DOUBLE; break;
+            case SH_AGG_MIN:
+                ap.kind[a] = t == SH_T_DOUBLE ? AK_MIN_D : t == SH_T_FLOAT ? AK_MIN_F : AK_MIN_L;
+                out_types[a] = t;
+                break;
+            case SH_AGG_MAX:
+                ap.kind[a] = t == SH_T_DOUBLE ? AK_MAX_D : t == SH_T_FLOAT ? AK_MAX_F : AK_MAX_L;
+                out_types[a] = t;
+                break;
+            default: return sh_fail(SH_ERR_INVALID, "unknown aggregator");
+        }
+    }
+    return SH_OK;
+}
+
+int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* types, KeyPlan& kp) {
+    kp = KeyPlan{};
+    kp.n = n_group;
+    if (n_group < 0 || n_group > SH_MAX_GROUP) return sh_fail(SH_ERR_INVALID, "bad group-by count");
+    for (int g = 0; g < n_group; g++) {
+        int c = group[g];
+        if (c < 0 || c >= n_cols) return sh_fail(SH_ERR_INVALID, "group-by column out of range");
+        if (!integral(types[c]))
+            return sh_fail(SH_ERR_UNSUPPORTED, "GPU group-by supports int/long/string(dictionary id)/bool keys");
+        kp.col[g] = c;
+        kp.type[g] = types[c];
+    }
+    if (n_group == 2 && (kp.type[0] == SH_T_LONG || kp.type[1] == SH_T_LONG))
+        return sh_fail(SH_ERR_UNSUPPORTED, "two group-by columns must both be 32-bit");
+    return SH_OK;
+}
+
+int KeyTableHost::init(int64_t capacity) {
+    int64_t want = std::max<int64_t>(16, 2 * std::max<int64_t>(1, capacity));
+    size_t ts = 16;
+    while ((int64_t)ts < want) ts <<= 1;
+    size_ = ts;
+    int rc = keys.reserve(ts * 8, false);
+    if (rc) return rc;
+    rc = ctrl.reserve(64, false);
+    if (rc) return rc;
+    std::vector<u64> init(ts, kEmptyKey);
+    if (hipMemcpy(keys.p, init.data(), ts * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return sh_fail(SH_ERR_DEVICE, "key table init failed");
+    if (hipMemset(ctrl.p, 0, 64) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table init failed");
+    return SH_OK;
+}
+
+KeyTable KeyTableHost::dev() const {
+    KeyTable kt;
+    kt.keys = (u64*)keys.p;
+    kt.mask = (u32)(size_ - 1);
+    kt.pad = 0;
+    kt.n_keys = (u32*)ctrl.p;
+    kt.overflow = (int*)((char*)ctrl.p + 8);
+    return kt;
+}
+
+int KeyTableHost::check(hipStream_t s) {
+    int ov = 0;
+    if (hipMemcpyAsync(&ov, (char*)ctrl.p + 8, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return sh_fail(SH_ERR_DEVICE, "key table check failed");
+    if (ov) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
+    return SH_OK;
+}

@@ -1,0 +1,134 @@
+// sh_runtime.h — host-side objects behind the C ABI (not part of the public interface).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "sh_internal.h"
+
+struct sh_ctx {
+    int device = 0;
+    int num_cus = 0;
+    int max_lds = 0;
+    hipStream_t stream = nullptr;
+};
+
+int sh_fail(int code, const std::string& msg);
+
+// Growable device allocation. `used` is the byte count that must survive a grow (keep=true).
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    size_t used = 0;
+    int reserve(size_t n, bool keep);
+    void release();
+    template <typename T> T* as() const { return (T*)p; }
+};
+
+// Open-addressing group-key table on the device (key -> position).
+struct KeyTableHost {
+    DevBuf keys, ctrl;
+    size_t size_ = 0;
+    int init(int64_t capacity);
+    shd::KeyTable dev() const;
+    int check(hipStream_t s);
+    void release() { keys.release(); ctrl.release(); }
+};
+
+// Host copy of a push's output (sh_out points into these vectors).
+struct OutHost {
+    std::vector<int64_t> flush_offsets{0}, flush_clock, ts, keys;
+    std::vector<uint8_t> expired, nulls;
+    std::vector<uint64_t> vals;
+    sh_out out{};
+    void reset() {
+        flush_offsets.assign(1, 0);
+        flush_clock.clear();
+        ts.clear(); keys.clear(); expired.clear(); nulls.clear(); vals.clear();
+    }
+    const sh_out* view(int n_keys, int n_vals, const int32_t* vtypes) {
+        out = sh_out{};
+        out.n_flushes = (int64_t)flush_clock.size();
+        out.n_rows = (int64_t)ts.size();
+        out.n_keys = n_keys;
+        out.n_vals = n_vals;
+        for (int i = 0; i < n_vals; i++) out.val_types[i] = vtypes[i];
+        out.flush_offsets = flush_offsets.data();
+        out.flush_clock = flush_clock.data();
+        out.ts = ts.data();
+        out.expired = expired.data();
+        out.keys = keys.data();
+        out.vals = vals.data();
+        out.nulls = nulls.data();
+        return &out;
+    }
+};
+
+int compile_filter(int n_ops, const sh_filter_op* ops, int n_cols, const int32_t* types, shd::FilterProg& fp);
+int compile_aggs(int n_aggs, const sh_agg_spec* aggs, int n_cols, const int32_t* types, shd::AggPlan& ap,
+                 int32_t* out_types);
+int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* types, shd::KeyPlan& kp);
+
+// Host batch staged to the device (sh_push): one DevBuf per column + timestamps.
+struct StagedBatch {
+    DevBuf ts, cols[SH_MAX_COLS];
+    int stage(hipStream_t s, const sh_batch* b, int n_cols, const int32_t* types, sh_batch* dev);
+};
+
+size_t type_size(int t);
+
+using shd::AggPlan;
+using shd::FilterProg;
+using shd::KeyPlan;
+using shd::PushInfo;
+
+struct SlidingImpl;
+
+struct sh_query {
+    int kind = 0;            // 0 = batch window (lengthBatch/timeBatch), 1 = sliding time window
+    SlidingImpl* sl = nullptr;
+    // partitioned timeBatch (R12): only the first partition key ever flushes
+    bool partitioned = false, p0_known = false;
+    int64_t p0 = 0;
+    FilterProg fp_orig{};
+    sh_ctx* ctx = nullptr;
+    sh_query_desc d{};
+    FilterProg fp{};
+    AggPlan ap{};
+    KeyPlan kp{};
+    int32_t vtypes[SH_MAX_AGGS]{};
+    KeyTableHost kt;
+    int P = 1, logP = 0, NL = 0;
+    // playback clock + window state
+    bool clock_valid = false;
+    int64_t clock = 0;
+    bool e0_valid = false;
+    int64_t E0 = 0;
+    int64_t W_open = 0;
+    int64_t n_pend = 0, pend_cap = 0;
+    DevBuf pend_pos, pend_ts, pend_vals;
+    // scratch
+    DevBuf blk_pass, blk_tl, blk_first, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
+        out_ts, out_keys, out_vals, out_nulls, out_expired, blk_cnt;
+    DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
+    PushInfo* h_info = nullptr;
+    StagedBatch staged;
+    OutHost out;
+    sh_out dev_out{};
+    std::vector<int64_t> dev_flush_offsets{0}, dev_flush_clock;
+    hipEvent_t ev_push0 = nullptr, ev_push1 = nullptr, ev_agg0 = nullptr, ev_agg1 = nullptr;
+    sh_stats stats{};
+    int64_t agg_bytes = 0;
+};
+
+
+// sliding time window (sh_sliding.cpp)
+int sliding_create(sh_query* q);
+int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
+int sliding_advance(sh_query* q, int64_t now, const sh_out** out);
+void sliding_destroy(sh_query* q);
+int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const shd::u32** rec_pos,
+                   const shd::u32** rec_idx, const shd::u64** rec_vals, int64_t* rec_cap);
+

@@ -1,0 +1,528 @@
+// sh_window.cpp — batch-window group-by queries (lengthBatch / timeBatch) behind sh_query_*.
+//
+// Replaces, for the query shape `from S[cond]#window.lengthBatch|timeBatch(...) select k, aggs group by k
+// insert into O`, the chain FilterProcessor -> {LengthBatch,TimeBatch}WindowProcessor -> QuerySelector
+// (processInBatchGroupBy) -> OutputRateLimiter of the reference. The window's queued events are kept on
+// the device (pending buffer); a push runs whole windows in parallel and emits every window that
+// closed during the push as one flush, exactly as the reference emits one chunk per flush.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sh_internal.h"
+#include "sh_runtime.h"
+
+using namespace shd;
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+size_t type_size(int t) {
+    switch (t) {
+        case SH_T_LONG: case SH_T_DOUBLE: return 8;
+        case SH_T_BOOL: return 1;
+        default: return 4;
+    }
+}
+
+int StagedBatch::stage(hipStream_t s, const sh_batch* b, int n_cols, const int32_t* types, sh_batch* dev) {
+    *dev = *b;
+    size_t n = (size_t)b->n;
+    if (n == 0) return SH_OK;
+    RCHK(ts.reserve(n * 8, false));
+    HIPCHK(hipMemcpyAsync(ts.p, b->ts, n * 8, hipMemcpyHostToDevice, s));
+    dev->ts = ts.as<int64_t>();
+    for (int c = 0; c < n_cols; c++) {
+        if (!b->cols[c]) { dev->cols[c] = nullptr; continue; }
+        size_t bytes = n * type_size(types[c]);
+        RCHK(cols[c].reserve(bytes, false));
+        HIPCHK(hipMemcpyAsync(cols[c].p, b->cols[c], bytes, hipMemcpyHostToDevice, s));
+        dev->cols[c] = cols[c].p;
+    }
+    return SH_OK;
+}
+
+static int64_t wfun_host(const sh_query* q, int64_t clock) {
+    if (!q->e0_valid) return q->W_open;
+    return clock < q->E0 ? 0 : (clock - q->E0) / q->d.window_param + 1;
+}
+
+static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
+    if (need <= q->pend_cap) return SH_OK;
+    int64_t ncap = std::max<int64_t>(need, q->pend_cap + q->pend_cap / 2);
+    ncap = std::max<int64_t>(ncap, 4096);
+    DevBuf np, nt, nv;
+    RCHK(np.reserve(ncap * 4, false));
+    RCHK(nt.reserve(ncap * 8, false));
+    RCHK(nv.reserve(std::max(1, q->ap.n_vcols) * ncap * 8, false));
+    hipStream_t s = q->ctx->stream;
+    if (keep > 0) {
+        HIPCHK(hipMemcpyAsync(np.p, q->pend_pos.p, keep * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(nt.p, q->pend_ts.p, keep * 8, hipMemcpyDeviceToDevice, s));
+        for (int j = 0; j < q->ap.n_vcols; j++)
+            HIPCHK(hipMemcpyAsync((char*)nv.p + j * ncap * 8, (char*)q->pend_vals.p + j * q->pend_cap * 8, keep * 8,
+                                  hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    q->pend_pos.release(); q->pend_ts.release(); q->pend_vals.release();
+    q->pend_pos = np; q->pend_ts = nt; q->pend_vals = nv;
+    np.p = nt.p = nv.p = nullptr;
+    q->pend_cap = ncap;
+    return SH_OK;
+}
+
+extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
+    if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_query_create: NULL argument");
+    if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
+    for (int c = 0; c < d->n_cols; c++)
+        if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
+    if (d->n_aggs < 1 || d->n_aggs > SH_MAX_AGGS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path runs aggregation queries (1..8 aggregators)");
+    if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME)
+        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path needs a lengthBatch, timeBatch or time window");
+    if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
+    if (!d->current_on || d->expired_on)
+        return sh_fail(SH_ERR_UNSUPPORTED, "GPU windows emit current events only (`insert into`)");
+    if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "stream.current.event batch windows not on the GPU yet");
+    if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
+        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
+    if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
+                                  d->col_types[d->partition_col] == SH_T_LONG || d->col_types[d->partition_col] == SH_T_STRID)))
+        return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/string column");
+
+    sh_query* q = new sh_query();
+    q->ctx = ctx;
+    q->d = *d;
+    q->d.filter = nullptr;
+    int rc;
+    if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, q->fp)) ||
+        (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, q->ap, q->vtypes)) ||
+        (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->kp))) {
+        delete q;
+        return rc;
+    }
+    int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
+    if ((rc = q->kt.init(cap))) { delete q; return rc; }
+    q->fp_orig = q->fp;
+    q->partitioned = d->partition_col >= 0;
+    if (d->window == SH_WIN_TIME) {
+        q->kind = 1;
+        if ((rc = sliding_create(q))) { delete q; return rc; }
+        *out = q;
+        return SH_OK;
+    }
+    // key partitions: smallest power of two whose per-partition LDS state fits the budget
+    const size_t budget = 80 * 1024;
+    size_t bpk = 16 + 8 * (size_t)q->ap.n_fields;
+    size_t ts = q->kt.size_;
+    int P = 1;
+    while (((ts / P) + 1) * bpk + 16 > budget && P < (1 << 14)) P <<= 1;
+    q->P = P;
+    q->logP = 0;
+    while ((1 << q->logP) < P) q->logP++;
+    q->NL = (int)(ts / P) + 1;
+    if (((ts / P) + 1) * bpk + 16 > budget) { delete q; return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large"); }
+    if (hipHostMalloc((void**)&q->h_info, sizeof(PushInfo), hipHostMallocDefault) != hipSuccess) {
+        delete q;
+        return sh_fail(SH_ERR_OOM, "pinned alloc failed");
+    }
+    if ((rc = q->info.reserve(sizeof(PushInfo), false)) || (rc = q->counters.reserve(64, false))) { delete q; return rc; }
+    (void)hipEventCreate(&q->ev_push0); (void)hipEventCreate(&q->ev_push1);
+    (void)hipEventCreate(&q->ev_agg0); (void)hipEventCreate(&q->ev_agg1);
+    *out = q;
+    return SH_OK;
+}
+
+// Aggregate the closed segments [segs[i].lo, segs[i].hi) of the combined (pending + new) sequence
+// and append one flush per non-empty segment.
+static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::vector<int64_t>& clocks,
+                      const sh_batch* b, bool host_out) {
+    hipStream_t s = q->ctx->stream;
+    int nseg = (int)segs.size();
+    int64_t closed_hi = segs.back().hi;
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
+    const int64_t* ts = b ? b->ts : nullptr;
+    // row capacity: per segment at most min(len, distinct keys)
+    int64_t row_cap = 0;
+    for (auto& sg : segs) row_cap += std::min<int64_t>(sg.hi - sg.lo, (int64_t)q->kt.size_ + 1);
+    row_cap = std::max<int64_t>(row_cap, 1);
+    RCHK(q->flags.reserve(closed_hi + 16, false));
+    RCHK(q->rowref.reserve((closed_hi + 16) * 4, false));
+    RCHK(q->rows.reserve(row_cap * sizeof(RowTmp), false));
+    RCHK(q->row_vals.reserve(row_cap * q->ap.n * 8, false));
+    RCHK(q->segs.reserve(nseg * sizeof(Segment), false));
+    RCHK(q->seg_rows.reserve(nseg * 8, false));
+    HIPCHK(hipMemsetAsync(q->flags.p, 0, closed_hi, s));
+    HIPCHK(hipMemsetAsync(q->seg_rows.p, 0, nseg * 8, s));
+    HIPCHK(hipMemsetAsync(q->counters.p, 0, 64, s));
+    HIPCHK(hipMemcpyAsync(q->segs.p, segs.data(), nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
+    const u32* rec_pos = nullptr; const u32* rec_idx = nullptr; const u64* rec_vals = nullptr;
+    int64_t rec_cap = 0;
+    if (q->P > 1) {
+        RCHK(run_multisplit(q, closed_hi, b, &rec_pos, &rec_idx, &rec_vals, &rec_cap));
+    }
+    HIPCHK(hipEventRecord(q->ev_agg0, s));
+    launch_aggregate(s, q->segs.as<Segment>(), nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(),
+                     q->pend_vals.as<u64>(), q->pend_cap, ts, cs, q->fp, q->kp, q->kt.dev(), q->ap,
+                     q->rows.as<RowTmp>(), q->row_vals.as<u64>(), q->counters.as<u32>(), q->flags.as<unsigned char>(),
+                     q->rowref.as<u32>(), q->seg_rows.as<int64_t>(), rec_pos, rec_idx, rec_vals, rec_cap,
+                     q->part_off.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(q->ev_agg1, s));
+    std::vector<int64_t> seg_rows(nseg);
+    HIPCHK(hipMemcpyAsync(seg_rows.data(), q->seg_rows.p, nseg * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float agg_ms = 0;
+    (void)hipEventElapsedTime(&agg_ms, q->ev_agg0, q->ev_agg1);
+    q->stats.main_kernel_ms += agg_ms;
+    int64_t n_rows = 0;
+    for (auto r : seg_rows) n_rows += r;
+    // algorithmic bytes of the aggregation kernel: every closed event's referenced columns + rows out
+    {
+        int64_t ev = closed_hi;
+        int64_t per = 4 + 8 * q->ap.n_vcols;  // key + values
+        q->agg_bytes += ev * per + n_rows * (int64_t)(sizeof(RowTmp) + 8 * q->ap.n);
+    }
+    int nk = q->kp.n, na = q->ap.n;
+    if (n_rows > 0) {
+        int64_t cap = n_rows;
+        RCHK(q->out_ts.reserve(cap * 8, false));
+        RCHK(q->out_keys.reserve(std::max(1, nk) * cap * 8, false));
+        RCHK(q->out_vals.reserve(na * cap * 8, false));
+        RCHK(q->out_nulls.reserve(na * cap, false));
+        RCHK(q->out_expired.reserve(cap, false));
+        int nblk2 = (int)((closed_hi + kTile - 1) / kTile);
+        RCHK(q->blk_cnt.reserve(nblk2 * 8, false));
+        launch_count_flags(s, q->flags.as<unsigned char>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2);
+        launch_scan_sum(s, q->blk_cnt.as<int64_t>(), nblk2);
+        launch_emit(s, q->flags.as<unsigned char>(), q->rowref.as<u32>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2,
+                    q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp, q->n_pend,
+                    q->pend_ts.as<int64_t>(), ts, cap, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(),
+                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>());
+        HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
+        HIPCHK(hipGetLastError());
+        if (host_out) {
+            size_t base = q->out.ts.size();
+            size_t nb = base + n_rows;
+            q->out.ts.resize(nb);
+            q->out.expired.resize(nb, 0);
+            HIPCHK(hipMemcpyAsync(q->out.ts.data() + base, q->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+            // keys / vals / nulls are [k][n] blocks; append per push into temporaries and interleave later
+            std::vector<int64_t> k(nk * n_rows);
+            std::vector<uint64_t> v(na * n_rows);
+            std::vector<uint8_t> nl(na * n_rows);
+            if (nk) HIPCHK(hipMemcpyAsync(k.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(v.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(nl.data(), q->out_nulls.p, na * n_rows, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            // q->out keeps rows grouped: store column blocks per push in pending vectors, merged in finish_out
+            q->out.keys.insert(q->out.keys.end(), k.begin(), k.end());
+            q->out.vals.insert(q->out.vals.end(), v.begin(), v.end());
+            q->out.nulls.insert(q->out.nulls.end(), nl.begin(), nl.end());
+        }
+    }
+    // flush bookkeeping (one flush per non-empty closed segment)
+    std::vector<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
+    std::vector<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
+    int64_t acc = fo.back();
+    for (int i = 0; i < nseg; i++) {
+        if (seg_rows[i] == 0) continue;
+        acc += seg_rows[i];
+        fo.push_back(acc);
+        fc.push_back(clocks[i]);
+    }
+    if (!host_out) {
+        q->dev_out.n_rows = n_rows;
+    }
+    return SH_OK;
+}
+
+static void finish_out(sh_query* q, bool host_out, const sh_out** out) {
+    if (host_out) {
+        *out = q->out.view(q->kp.n, q->ap.n, q->vtypes);
+    } else {
+        sh_out& o = q->dev_out;
+        o.n_flushes = (int64_t)q->dev_flush_clock.size();
+        o.n_keys = q->kp.n;
+        o.n_vals = q->ap.n;
+        for (int i = 0; i < q->ap.n; i++) o.val_types[i] = q->vtypes[i];
+        o.flush_offsets = q->dev_flush_offsets.data();
+        o.flush_clock = q->dev_flush_clock.data();
+        o.ts = q->out_ts.as<int64_t>();
+        o.expired = q->out_expired.as<uint8_t>();
+        o.keys = q->out_keys.as<int64_t>();
+        o.vals = q->out_vals.as<uint64_t>();
+        o.nulls = q->out_nulls.as<uint8_t>();
+        *out = &o;
+    }
+}
+
+// Partitioned timeBatch (`partition with (pcol of S)`): TimeBatchWindowProcessor.nextEmitTime is a
+// processor field shared by every partition (:128) and only the partition that first initialised it
+// registered a scheduler timer (:266-276, Scheduler.notifyAt under that partition flow); timers re-arm
+// under the same flow, so only that partition (p0) is ever flushed (the reference test
+// WindowPartitionTestCase:291-348 tolerates exactly this). The GPU runs the query restricted to p0.
+static int resolve_first_partition(sh_query* q, const sh_batch* b) {
+    hipStream_t s = q->ctx->stream;
+    int64_t N = b->n;
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    int nblk = (int)((N + kTile - 1) / kTile);
+    RCHK(q->blk_pass.reserve(nblk * 8, false));
+    RCHK(q->blk_tl.reserve(nblk * 8, false));
+    RCHK(q->blk_first.reserve(nblk * 8, false));
+    WinParams wp{};
+    wp.kind = SH_WIN_LENGTH_BATCH;  // no nextEmitTime initialisation in this probe
+    wp.N = N;
+    wp.send_size = b->send_size;
+    launch_blockagg(s, b->ts, cs, q->fp_orig, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                    q->blk_first.as<int64_t>(), nblk);
+    launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk, b->ts,
+                       wp, q->info.as<PushInfo>());
+    HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int64_t first = q->h_info->first_pass;
+    if (first == INT64_MAX) {
+        // nothing reached the window; the playback clock still advances (InputHandler.send)
+        q->clock = q->clock_valid ? std::max(q->clock, q->h_info->max_tl) : q->h_info->max_tl;
+        q->clock_valid = true;
+        return SH_OK;
+    }
+    int pc = q->d.partition_col;
+    int t = q->d.col_types[pc];
+    int64_t key = 0;
+    if (t == SH_T_LONG) {
+        HIPCHK(hipMemcpy(&key, (const char*)b->cols[pc] + first * 8, 8, hipMemcpyDeviceToHost));
+    } else {
+        int32_t k32 = 0;
+        HIPCHK(hipMemcpy(&k32, (const char*)b->cols[pc] + first * 4, 4, hipMemcpyDeviceToHost));
+        key = k32;
+    }
+    q->p0 = key;
+    q->p0_known = true;
+    FilterProg fp = q->fp_orig;
+    if (fp.n + 4 > kMaxFilterOps) return sh_fail(SH_ERR_UNSUPPORTED, "filter too long for a partitioned query");
+    fp.ops[fp.n++] = FilterOpD{SH_OP_COL, 0, pc, 0, 0, 0.0};
+    fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, t, 0, 0, key, 0.0};
+    fp.ops[fp.n++] = FilterOpD{SH_OP_EQ, 0, 0, 0, 0, 0.0};
+    if (q->fp_orig.n > 0) fp.ops[fp.n++] = FilterOpD{SH_OP_AND, 0, 0, 0, 0, 0.0};
+    q->fp = fp;
+    return SH_OK;
+}
+
+static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    hipStream_t s = q->ctx->stream;
+    q->out.reset();
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    q->dev_out = sh_out{};
+    q->stats = sh_stats{};
+    q->agg_bytes = 0;
+    int64_t N = b->n;
+    if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
+    if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
+    if (q->n_pend + N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
+    HIPCHK(hipEventRecord(q->ev_push0, s));
+    if (N > 0 && q->partitioned && !q->p0_known) RCHK(resolve_first_partition(q, b));
+    if (N > 0 && !(q->partitioned && !q->p0_known)) {
+        ColSet cs{};
+        cs.n = q->d.n_cols;
+        for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+        int nblk = (int)((N + kTile - 1) / kTile);
+        RCHK(q->blk_pass.reserve(nblk * 8, false));
+        RCHK(q->blk_tl.reserve(nblk * 8, false));
+        RCHK(q->blk_first.reserve(nblk * 8, false));
+        WinParams wp{};
+        wp.kind = q->d.window;
+        wp.e0_valid = q->e0_valid;
+        wp.clock_valid = q->clock_valid;
+        wp.has_start = q->d.has_start_time;
+        wp.L = q->d.window_param;
+        wp.T = q->d.window_param;
+        wp.E0 = q->E0;
+        wp.start_time = q->d.start_time;
+        wp.clock0 = q->clock;
+        wp.W_open = q->W_open;
+        wp.n_pend = q->n_pend;
+        wp.send_size = b->send_size;
+        wp.N = N;
+        launch_blockagg(s, b->ts, cs, q->fp, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                        q->blk_first.as<int64_t>(), nblk);
+        launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk,
+                           b->ts, wp, q->info.as<PushInfo>());
+        int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
+        RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
+        launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                          q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        PushInfo info = *q->h_info;
+        if (info.n_bounds > max_bounds) return sh_fail(SH_ERR_INVALID, "more than 4M windows closed in one push");
+        std::vector<Bound> bounds(info.n_bounds);
+        if (info.n_bounds) {
+            HIPCHK(hipMemcpyAsync(bounds.data(), q->bounds.p, info.n_bounds * sizeof(Bound), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
+        }
+        q->e0_valid = info.e0_valid;
+        q->E0 = info.E0;
+        q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+        q->clock_valid = true;
+        int64_t e_lo, pcb_lo, dst_base, new_pend;
+        if (!bounds.empty()) {
+            std::vector<Segment> segs;
+            std::vector<int64_t> clocks;
+            int64_t lo = 0;
+            for (auto& bd : bounds) {
+                segs.push_back(Segment{lo, bd.idx});
+                clocks.push_back(q->d.window == SH_WIN_LENGTH_BATCH ? bd.clock_prev : bd.clock);
+                lo = bd.idx;
+            }
+            RCHK(run_closed(q, segs, clocks, b, host_out));
+            e_lo = bounds.back().idx - q->n_pend;
+            pcb_lo = bounds.back().pcb;
+            dst_base = 0;
+            new_pend = info.total_pass - pcb_lo;
+            q->W_open = bounds.back().W;
+        } else {
+            e_lo = 0;
+            pcb_lo = 0;
+            dst_base = q->n_pend;
+            new_pend = q->n_pend + info.total_pass;
+        }
+        RCHK(grow_pending(q, new_pend, dst_base));
+        launch_compact_pending(s, b->ts, cs, q->fp, q->kp, q->kt.dev(), q->ap, e_lo, N, pcb_lo, dst_base,
+                               q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
+                               q->pend_vals.as<u64>(), q->pend_cap);
+        HIPCHK(hipGetLastError());
+        q->n_pend = new_pend;
+    }
+    HIPCHK(hipEventRecord(q->ev_push1, s));
+    RCHK(q->kt.check(s));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.events = N;
+    q->stats.main_kernel_bytes = q->agg_bytes;
+    finish_out(q, host_out, out);
+    return SH_OK;
+}
+
+// The host-output path stores keys/vals/nulls as [col][n] blocks per segment batch; when several
+// run_closed calls append (only one per push today) the layout stays [col][n_rows] because a push
+// calls run_closed at most once.
+extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
+    if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
+    sh_batch dev;
+    RCHK(q->staged.stage(q->ctx->stream, b, q->d.n_cols, q->d.col_types, &dev));
+    if (q->kind == 1) return sliding_push(q, &dev, true, out);
+    return push_core(q, &dev, true, out);
+}
+
+extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out) {
+    if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
+    if (q->kind == 1) return sliding_push(q, b, false, out);
+    return push_core(q, b, false, out);
+}
+
+extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
+    if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
+    if (q->kind == 1) return sliding_advance(q, now, out);
+    q->out.reset();
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    // TimestampGeneratorImpl.setCurrentTimestamp only moves the clock forward (:104-122)
+    if (q->clock_valid && now < q->clock) { finish_out(q, true, out); return SH_OK; }
+    q->clock = now;
+    q->clock_valid = true;
+    if (q->d.window == SH_WIN_TIME_BATCH && q->e0_valid) {
+        int64_t W = wfun_host(q, now);
+        if (W > q->W_open && q->n_pend > 0) {
+            std::vector<Segment> segs{Segment{0, q->n_pend}};
+            std::vector<int64_t> clocks{now};
+            RCHK(run_closed(q, segs, clocks, nullptr, true));
+            q->n_pend = 0;
+        }
+        q->W_open = std::max(q->W_open, W);
+    }
+    finish_out(q, true, out);
+    return SH_OK;
+}
+
+extern "C" int sh_query_destroy(sh_query* q) {
+    if (!q) return SH_OK;
+    (void)hipStreamSynchronize(q->ctx->stream);
+    if (q->kind == 1) sliding_destroy(q);
+    DevBuf* bufs[] = {&q->pend_pos, &q->pend_ts, &q->pend_vals, &q->blk_pass, &q->blk_tl, &q->blk_first, &q->info,
+                      &q->bounds, &q->segs, &q->seg_rows, &q->flags, &q->rowref, &q->rows, &q->row_vals,
+                      &q->counters, &q->out_ts, &q->out_keys, &q->out_vals, &q->out_nulls, &q->out_expired,
+                      &q->blk_cnt, &q->ms_counts, &q->ms_tmp, &q->rec_pos, &q->rec_idx, &q->rec_vals,
+                      &q->part_off};
+    for (DevBuf* bf : bufs) bf->release();
+    for (auto& c : q->staged.cols) c.release();
+    q->staged.ts.release();
+    q->kt.release();
+    if (q->h_info) (void)hipHostFree(q->h_info);
+    hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1};
+    for (auto e : evs) if (e) (void)hipEventDestroy(e);
+    delete q;
+    return SH_OK;
+}
+
+extern "C" int sh_query_stats(sh_query* q, sh_stats* out) {
+    if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_query_stats: NULL argument");
+    *out = q->stats;
+    return SH_OK;
+}
+
+// ---- multisplit: closed events of the push into P key partitions (stable) -----------------------
+int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32** rec_pos, const u32** rec_idx,
+                   const u64** rec_vals, int64_t* rec_cap) {
+    hipStream_t s = q->ctx->stream;
+    int P = q->P;
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
+    const int64_t* ts = b ? b->ts : nullptr;
+    int nblk = (int)((closed_hi + kTile - 1) / kTile);
+    int64_t ncnt = (int64_t)P * nblk;
+    RCHK(q->ms_counts.reserve((ncnt + 1) * 8, false));
+    RCHK(q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false));
+    RCHK(q->part_off.reserve((P + 1) * 8, false));
+    int64_t cap = std::max<int64_t>(closed_hi, 1);
+    RCHK(q->rec_pos.reserve(cap * 4, false));
+    RCHK(q->rec_idx.reserve(cap * 4, false));
+    RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
+    launch_ms_count(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), ts, cs, q->fp, q->kp, q->kt.dev(), P,
+                    q->ms_counts.as<int64_t>(), nblk);
+    // counts are laid out [p][blk]; one exclusive scan gives every (partition, block) its offset,
+    // and partition p starts at offset[p * nblk]
+    HIPCHK(hipMemsetAsync(q->ms_counts.as<int64_t>() + ncnt, 0, 8, s));
+    launch_scan_sum_large(s, q->ms_counts.as<int64_t>(), ncnt + 1, q->ms_tmp.as<int64_t>());
+    launch_ms_scatter(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, ts, cs,
+                      q->fp, q->kp, q->kt.dev(), q->ap, P, q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(),
+                      q->rec_idx.as<u32>(), q->rec_vals.as<u64>(), cap);
+    // part_off[p] = counts[p * nblk] (exclusive); part_off[P] = total
+    launch_part_off(s, q->ms_counts.as<int64_t>(), nblk, P, q->part_off.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    *rec_pos = q->rec_pos.as<u32>();
+    *rec_idx = q->rec_idx.as<u32>();
+    *rec_vals = q->rec_vals.as<u64>();
+    *rec_cap = cap;
+    return SH_OK;
+}

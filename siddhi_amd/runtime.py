@@ -1,0 +1,184 @@
+"""Host-side Python mirror of the reference's interface for the GPU path.
+
+`GpuQuery` plays the role of a Siddhi query whose window / aggregator extensions run on the MI355X:
+`send()` is `InputHandler.send(Event[])` (core/stream/input/InputHandler.java:85-96) and the
+registered callbacks receive one list of rows per flush, as `StreamCallback.receive(Event[])` does
+(core/stream/output/StreamCallback.java:93-129). Everything runs through libsiddhi_hip.so; there is
+no CPU fallback — importing this module on a box without the built library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Callable, List, Optional
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsiddhi_hip.so")
+
+_lib = None
+
+
+def lib():
+    """Load libsiddhi_hip.so (built in-tree by `make -C siddhi_amd/csrc`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C siddhi_amd/csrc` "
+                              "(the GPU path has no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        abi.setup_lib_prototypes(L, "sh")
+        if L.sh_abi_version() != 1:
+            raise ImportError("libsiddhi_hip ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+class SiddhiError(RuntimeError):
+    """SiddhiAppRuntimeException analogue: carries the library's error code and message."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SiddhiError(rc, lib().sh_last_error().decode())
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self.h = C.c_void_p()
+        _check(lib().sh_init(device, C.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib().sh_ctx_destroy(self.h)
+            self.h = None
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("SH_DEVICE", "0")))
+    return _default_ctx
+
+
+class GpuQuery:
+    """A window query on the GPU: `from S[cond]#window.<kind>(...) select k, aggs group by k insert into O`."""
+
+    def __init__(self, spec: abi.QuerySpec, ctx: Optional[Context] = None):
+        self.spec = spec
+        self.ctx = ctx or default_context()
+        self._desc = spec.desc()
+        self.h = C.c_void_p()
+        _check(lib().sh_query_create(self.ctx.h, C.byref(self._desc), C.byref(self.h)))
+        self.callbacks: List[Callable] = []
+
+    # -- reference-shaped API --------------------------------------------------------------
+    def add_callback(self, fn: Callable[[List[tuple]], None]):
+        """StreamCallback.receive(Event[]): fn(rows) once per flush."""
+        self.callbacks.append(fn)
+
+    def send(self, batch: abi.HostBatch):
+        flushes = self.push(batch)
+        for f in flushes:
+            for cb in self.callbacks:
+                cb(f.rows)
+        return flushes
+
+    # -- ABI-level API ---------------------------------------------------------------------
+    def push_raw(self, batch: abi.HostBatch):
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_push(self.h, C.byref(batch.b), C.byref(out)))
+        return out
+
+    def push(self, batch: abi.HostBatch):
+        return abi.decode_out(self.push_raw(batch))
+
+    def push_device(self, n: int, ts_ptr: int, col_ptrs: List[int], send_size: int = 0):
+        """Device-resident batch (HBM pointers, e.g. torch tensors' data_ptr()). Returns the sh_out
+        pointer: flush metadata on the host, row arrays in device memory."""
+        b = abi.Batch()
+        b.n = n
+        b.send_size = send_size
+        b.ts = ts_ptr
+        for i, p in enumerate(col_ptrs):
+            b.cols[i] = p
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_push_device(self.h, C.byref(b), C.byref(out)))
+        return out
+
+    def advance_time_raw(self, now: int):
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_advance_time(self.h, now, C.byref(out)))
+        return out
+
+    def advance_time(self, now: int):
+        return abi.decode_out(self.advance_time_raw(now))
+
+    def stats(self) -> abi.Stats:
+        s = abi.Stats()
+        _check(lib().sh_query_stats(self.h, C.byref(s)))
+        return s
+
+    def close(self):
+        if self.h:
+            lib().sh_query_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GpuAggregation:
+    """`define aggregation ... every sec...year` on the GPU."""
+
+    def __init__(self, spec: abi.AggregationSpec, ctx: Optional[Context] = None):
+        self.spec = spec
+        self.ctx = ctx or default_context()
+        self._desc = spec.desc()
+        self.h = C.c_void_p()
+        _check(lib().sh_aggregation_create(self.ctx.h, C.byref(self._desc), C.byref(self.h)))
+
+    def push(self, batch: abi.HostBatch):
+        _check(lib().sh_aggregation_push(self.h, C.byref(batch.b)))
+
+    def push_device(self, n: int, ts_ptr: int, col_ptrs: List[int], send_size: int = 0):
+        b = abi.Batch()
+        b.n = n
+        b.send_size = send_size
+        b.ts = ts_ptr
+        for i, p in enumerate(col_ptrs):
+            b.cols[i] = p
+        _check(lib().sh_aggregation_push_device(self.h, C.byref(b)))
+
+    def advance_time(self, now: int):
+        _check(lib().sh_aggregation_advance_time(self.h, now))
+
+    def table_raw(self, duration: int):
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_aggregation_table(self.h, duration, C.byref(out)))
+        return out
+
+    def table(self, duration: int):
+        return [r for f in abi.decode_out(self.table_raw(duration)) for r in f.rows]
+
+    def close(self):
+        if self.h:
+            lib().sh_aggregation_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,141 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU restatement on identical pushes.
+Marked `gpu`: needs an MI355X; the library refuses to run without one (no CPU fallback)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleQuery
+from siddhi_amd import abi, synth
+from tests import kat_runner
+from tests.parity import assert_same, run_pushes, split_batches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def both(rt, spec, pushes, rtol=None, label=""):
+    g = rt.GpuQuery(spec)
+    o = OracleQuery(spec)
+    gout = run_pushes(g, pushes)
+    oout = run_pushes(o, pushes)
+    assert_same(gout, oout, rtol=rtol, label=label)
+    g.close()
+    o.close()
+    return gout
+
+
+# ---- reference KATs that the GPU path runs (aggregating lengthBatch / timeBatch, current events) ----
+GPU_KATS = [c for c in kat_runner.load_cases()
+            if c.get("kind") != "aggregation" and c["query"].get("window") in ("lengthBatch", "timeBatch", "time")
+            and c["query"].get("aggs") and c["query"].get("output", "current") == "current"
+            and not c["query"].get("stream_current")]
+
+
+@pytest.mark.parametrize("case", GPU_KATS, ids=[c["name"] for c in GPU_KATS])
+def test_reference_kat_on_gpu(rt, case):
+    schema, spec, dic, flushes = kat_runner.run_query(case, rt.GpuQuery)
+    kat_runner.check_query(case, flushes, schema, dic)
+    # and identical to the oracle
+    _, _, _, oflushes = kat_runner.run_query(case, OracleQuery)
+    assert [(f.clock, f.rows) for f in flushes] == [(f.clock, f.rows) for f in oflushes]
+
+
+# ---- C1: filtered lengthBatch group-by, 1k symbols --------------------------------------------------
+C1_SCHEMA = abi.Schema.parse("symbol string, price double, volume long, ts long")
+
+
+def c1_spec(L=10000):
+    return abi.QuerySpec(C1_SCHEMA, "lengthBatch", L, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
+                         filter=(">", "price", 100), key_capacity=1000)
+
+
+@pytest.mark.parametrize("send_size,cuts", [(1000, [250_000]), (1, [7, 123_457]), (0, [99_999, 100_000, 100_001])])
+def test_c1_lengthbatch_matches_oracle(rt, send_size, cuts):
+    ts, cols = synth.c1_stock(0, 300_000)
+    pushes = split_batches(C1_SCHEMA, ts, cols, cuts, send_size)
+    out = both(rt, c1_spec(), pushes, label="C1")
+    assert out["flush_offsets"].size > 20
+
+
+def test_c1_quantized_prices(rt):
+    ts, cols = synth.c1_stock(0, 120_000, quantized=True)
+    both(rt, c1_spec(L=777), split_batches(C1_SCHEMA, ts, cols, [50_000], 1000), label="C1q")
+
+
+# ---- C2: timeBatch(1 sec) count/min/max/avg by 100k keys (partitioned LDS path) ----------------------
+C2_SCHEMA = abi.Schema.parse("k int, v double, ts long")
+
+
+def c2_spec(keys=100_000, start=None):
+    return abi.QuerySpec(C2_SCHEMA, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], start_time=start,
+                         key_capacity=keys)
+
+
+@pytest.mark.parametrize("send_size", [1, 1000])
+def test_c2_timebatch_matches_oracle(rt, send_size):
+    ts, cols = synth.keyed_stream(0, 600_000, 0xC2, 100_000, 100)  # 100 events/ms -> 100k per window
+    pushes = split_batches(C2_SCHEMA, ts, cols, [123_456, 400_000], send_size)
+    pushes.append(("advance", int(ts[-1]) + 5000))
+    out = both(rt, c2_spec(), pushes, label="C2")
+    assert out["flush_offsets"].size >= 6
+
+
+def test_timebatch_small_keys_start_time_and_gaps(rt):
+    # clock jumps (empty windows), start.time alignment, filter that drops whole sends
+    rng = np.random.default_rng(7)
+    n = 40_000
+    ts = np.cumsum(rng.integers(0, 40, n)).astype(np.int64) + 5_000
+    ts[20_000:] += 100_000  # a long idle gap
+    k = rng.integers(0, 50, n).astype(np.int32)
+    v = rng.integers(-1000, 1000, n).astype(np.float64) / 8.0
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 2500, group_by=["k"], start_time=1000,
+                         aggs=[("sum", "v"), ("min", "v"), ("max", "v"), ("count", None), ("avg", "v")],
+                         filter=(">", "v", -50.0), key_capacity=64)
+    pushes = split_batches(schema, ts, [k, v, ts.copy()], [1, 17_000, 20_000, 20_001, 33_333], 10)
+    pushes.append(("advance", int(ts[-1]) + 10_000))
+    both(rt, spec, pushes, label="gaps")
+
+
+def test_lengthbatch_types_and_two_keys(rt):
+    rng = np.random.default_rng(11)
+    n = 50_000
+    schema = abi.Schema.parse("a int, b string, x int, y long, f float, d double")
+    cols = [rng.integers(-3, 3, n).astype(np.int32), rng.integers(0, 7, n).astype(np.int32),
+            rng.integers(-10**6, 10**6, n).astype(np.int32), rng.integers(-10**12, 10**12, n).astype(np.int64),
+            (rng.standard_normal(n) * 100).astype(np.float32), rng.standard_normal(n) * 1e6]
+    ts = np.arange(n, dtype=np.int64)
+    spec = abi.QuerySpec(schema, "lengthBatch", 333, group_by=["a", "b"],
+                         aggs=[("sum", "x"), ("sum", "y"), ("sum", "f"), ("avg", "x"), ("avg", "f"), ("min", "f"),
+                               ("max", "y"), ("min", "d")], key_capacity=64)
+    both(rt, spec, split_batches(schema, ts, cols, [1000, 1001, 30_000], 7), label="types")
+
+
+def test_no_group_by_single_key(rt):
+    ts, cols = synth.c1_stock(0, 20_000)
+    spec = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 1500, aggs=[("sum", "price"), ("count", None), ("max", "volume")])
+    both(rt, spec, split_batches(C1_SCHEMA, ts, cols, [5000], 100), label="nogroup")
+
+
+def test_empty_and_all_filtered_pushes(rt):
+    ts, cols = synth.c1_stock(0, 30_000)
+    spec = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 1000, group_by=["symbol"], aggs=[("sum", "volume")],
+                         filter=(">", "price", 150.0), key_capacity=1000)
+    pushes = split_batches(C1_SCHEMA, ts, cols, [10, 10, 2000], 50)
+    empty = abi.HostBatch(C1_SCHEMA, ts[:0], [c[:0] for c in cols], 0)
+    none_pass = abi.HostBatch(C1_SCHEMA, ts[:100], [cols[0][:100], np.zeros(100), cols[2][:100], cols[3][:100]], 0)
+    both(rt, spec, [empty] + pushes[:2] + [none_pass] + pushes[2:] + [empty], label="empty")
+
+
+def test_key_capacity_overflow_fails_loudly(rt):
+    from siddhi_amd.runtime import SiddhiError
+    ts, cols = synth.keyed_stream(0, 10_000, 0xC2, 5000, 10)
+    spec = abi.QuerySpec(C2_SCHEMA, "timeBatch", 100, group_by=["k"], aggs=[("count", None)], key_capacity=8)
+    g = rt.GpuQuery(spec)
+    with pytest.raises(SiddhiError):
+        g.push(abi.HostBatch(C2_SCHEMA, ts, cols, 1))
