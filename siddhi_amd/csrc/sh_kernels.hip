@@ -648,11 +648,6 @@ void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pen
                        int P, const i64* offsets, int nblk, u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     (void)ts;
     size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 12 + (size_t)P * 4 * 7 + 16;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_ms_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
     hipLaunchKernelGGL(k_ms_scatter, dim3(nblk), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
                        cols, f, kp, kt, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);
 }

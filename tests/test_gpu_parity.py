@@ -58,7 +58,7 @@ def test_c1_lengthbatch_matches_oracle(rt, send_size, cuts):
     ts, cols = synth.c1_stock(0, 300_000)
     pushes = split_batches(C1_SCHEMA, ts, cols, cuts, send_size)
     out = both(rt, c1_spec(), pushes, label="C1")
-    assert out["flush_offsets"].size > 20
+    assert out["flush_offsets"].size >= 15
 
 
 def test_c1_quantized_prices(rt):
