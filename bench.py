@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""bench.py — events/sec of the MI355X windowed group-by path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], the configuration the metric is quoted on for one GPU):
+  C2: `@app:playback from S#window.timeBatch(1 sec) select k, count(), min(v), max(v), avg(v)
+       group by k insert into O` over (k int, v double, ts long), 100k uniform keys,
+       1,000,000 events per event-time second, one InputHandler.send per event (PER_EVENT clock).
+A step = one sh_push_device of `--batch` events (inputs already resident in HBM; the window state,
+key table and outputs stay on the device). Each rank owns a disjoint key range and its own stream
+(weak scaling, no data-path collective).
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]
+   or:  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "events/sec (node) windowed group-by agg at 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+C2_BYTES_PER_EVENT = 24.4  # 20 B/event in + 100k rows x 44 B per 1M-event window
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 25, help="events per step (per GPU)")
+    ap.add_argument("--keys", type=int, default=100_000)
+    ap.add_argument("--events-per-ms", type=int, default=1000)
+    ap.add_argument("--send-size", type=int, default=1, help="events per InputHandler.send (1 = PER_EVENT)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Time the C++ restatement (oracle/, single thread) on a bounded sample of the same workload."""
+    import numpy as np
+    from oracle.oracle import OracleQuery
+    from siddhi_amd import abi, synth
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=args.keys)
+    q = OracleQuery(spec)
+    n_done, t_used, chunk = 0, 0.0, 500_000
+    while t_used < args.cpu_seconds and n_done < 60_000_000:
+        ts, cols = synth.keyed_stream(n_done, chunk, 0xC2, args.keys, args.events_per_ms)
+        b = abi.HostBatch(schema, ts, cols, args.send_size)
+        t0 = time.perf_counter()
+        q.push_raw(b)
+        t_used += time.perf_counter() - t0
+        n_done += chunk
+    q.close()
+    return {"value": n_done / t_used, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": f"{n_done} events of the same C2 stream (seed 0xC2, {args.keys} keys, per-event sends), "
+                      f"{t_used:.1f} s single-thread in the C++ restatement (oracle/), not stock Siddhi (no JVM)"}
+
+
+def main():
+    args = parse()
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from siddhi_amd import abi, runtime, synth
+    ctx = runtime.Context(local)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=args.keys)
+    q = runtime.GpuQuery(spec, ctx)
+
+    # synthetic stream of this rank, generated on the device; keys offset so ranks own disjoint keys
+    B = args.batch
+    nb = args.warmup + args.steps
+    batches = []
+    for i in range(nb):
+        ts, cols = synth.torch_keyed_stream(i * B, B, 0xC2 ^ (rank * 0x9E37), args.keys, args.events_per_ms, dev)
+        if rank:
+            cols[0] += rank * args.keys
+        batches.append((ts, cols))
+    torch.cuda.synchronize()
+
+    def push(i):
+        ts, cols = batches[i]
+        return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
+
+    for i in range(args.warmup):
+        push(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms, kern_bytes, flushes, rows = 0.0, 0, 0, 0
+    t0 = time.perf_counter()
+    for i in range(args.warmup, nb):
+        o = push(i).contents
+        st = q.stats()
+        kern_ms += st.main_kernel_ms
+        flushes += o.n_flushes
+        rows += o.n_rows
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_events = B * args.steps * world
+    # roofline of the dominant kernel (k_aggregate): algorithmic bytes per launch / its HIP-event time
+    n_launch = args.steps
+    ach = (C2_BYTES_PER_EVENT * B * n_launch) / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    result = {
+        "metric": METRIC,
+        "value": total_events / elapsed,
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: SplitMix64 stream seed 0xC2 (per rank seed ^ rank*0x9E37), generated in HBM",
+        "config": {"workload": "C2 timeBatch(1 sec) count/min/max/avg group by k, per-event sends",
+                   "keys_per_gpu": args.keys, "events_per_step_per_gpu": B,
+                   "event_rate": f"{args.events_per_ms * 1000} events per event-time second",
+                   "send_size": args.send_size, "parallelism": f"key-sharded x{world}",
+                   "flushes": flushes, "rows": rows},
+        "roofline": {"bound": "hbm", "kernel": "k_aggregate", "achieved": ach, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "kernel_ms_per_step": kern_ms / args.steps,
+                     "bytes_per_event": C2_BYTES_PER_EVENT},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    q.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -36,12 +36,17 @@ def uniform_price(u: np.ndarray, quantized: bool = False) -> np.ndarray:
     return p
 
 
+def hi53(u: np.ndarray) -> np.ndarray:
+    """Top 53 bits of a draw (non-negative as int64, so the device generator can use signed ops)."""
+    return u >> np.uint64(11)
+
+
 def c1_stock(start: int, n: int, seed: int = 0xC1, symbols: int = 1000, quantized: bool = False):
     """C1: StockStream(symbol string, price double, volume long, ts long); symbol 'S%04d' -> dict id."""
     d = draws(seed, start, n, 3)
-    symbol = (d[:, 0] % np.uint64(symbols)).astype(np.int32)
+    symbol = (hi53(d[:, 0]) % np.uint64(symbols)).astype(np.int32)
     price = uniform_price(d[:, 1], quantized)
-    volume = (np.uint64(1) + d[:, 2] % np.uint64(10000)).astype(np.int64)
+    volume = (np.uint64(1) + hi53(d[:, 2]) % np.uint64(10000)).astype(np.int64)
     ts = T0 + np.arange(start, start + n, dtype=np.int64)
     return ts, [symbol, price, volume, ts.copy()]
 
@@ -49,7 +54,7 @@ def c1_stock(start: int, n: int, seed: int = 0xC1, symbols: int = 1000, quantize
 def keyed_stream(start: int, n: int, seed: int, keys: int, events_per_ms: int, quantized: bool = False):
     """C2/C3/C4: (k int, v double, ts long) with `events_per_ms` events per event-time millisecond."""
     d = draws(seed, start, n, 2)
-    k = (d[:, 0] % np.uint64(keys)).astype(np.int32)
+    k = (hi53(d[:, 0]) % np.uint64(keys)).astype(np.int32)
     v = uniform_price(d[:, 1], quantized)
     ts = T0 + np.arange(start, start + n, dtype=np.int64) // events_per_ms
     return ts, [k, v, ts.copy()]
@@ -64,3 +69,36 @@ def zipf_keys(start: int, n: int, seed: int, keys: int, s: float = 1.1) -> np.nd
     hi = (keys + 1.0) ** a
     x = (1.0 + u * (hi - 1.0)) ** (1.0 / a)
     return np.minimum(np.floor(x) - 1, keys - 1).astype(np.int32)
+
+
+# ---- the same streams generated on the GPU with torch (bench inputs resident in HBM) --------------
+def _t_lsr(x, s):
+    import torch
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _t_mix64(z):
+    c1 = 0xBF58476D1CE4E5B9 - (1 << 64)
+    c2 = 0x94D049BB133111EB - (1 << 64)
+    z = (z ^ _t_lsr(z, 30)) * c1
+    z = (z ^ _t_lsr(z, 27)) * c2
+    return z ^ _t_lsr(z, 31)
+
+
+def torch_draws(seed: int, start: int, n: int, width: int, device):
+    """Same values as draws() (as int64 bit patterns), computed on `device`."""
+    import torch
+    g = 0x9E3779B97F4A7C15 - (1 << 64)
+    j = torch.arange(start * width, (start + n) * width, dtype=torch.int64, device=device) + 1
+    z = (seed - (1 << 64) if seed >= (1 << 63) else seed) + j * g
+    return _t_mix64(z).reshape(n, width)
+
+
+def torch_keyed_stream(start: int, n: int, seed: int, keys: int, events_per_ms: int, device):
+    """keyed_stream() on the GPU: returns (ts, [k int32, v float64, ts int64]) torch tensors."""
+    import torch
+    d = torch_draws(seed, start, n, 2, device)
+    k = (_t_lsr(d[:, 0], 11) % keys).to(torch.int32)
+    v = _t_lsr(d[:, 1], 11).to(torch.float64) * (2.0 ** -53) * 200.0
+    ts = T0 + torch.arange(start, start + n, dtype=torch.int64, device=device) // events_per_ms
+    return ts, [k.contiguous(), v.contiguous(), ts.clone()]
