@@ -20,6 +20,14 @@ __device__ __forceinline__ i64 load_raw(const ColSet& cs, int c, i64 e) {
     }
 }
 
+// Java (long) cast of a double (JLS 5.1.3): NaN -> 0, saturating, truncation toward zero
+__device__ __forceinline__ i64 java_d2l(double x) {
+    if (x != x) return 0;
+    if (x >= 9.2233720368547758e18) return INT64_MAX;
+    if (x <= -9.2233720368547758e18) return INT64_MIN;
+    return (i64)x;
+}
+
 __device__ __forceinline__ bool is_fp(int t) { return t == SH_T_FLOAT || t == SH_T_DOUBLE; }
 __device__ __forceinline__ int prank(int t) { return t == SH_T_LONG ? 2 : t == SH_T_FLOAT ? 3 : t == SH_T_DOUBLE ? 4 : 1; }
 

@@ -1,18 +1,339 @@
-// sh_sliding.cpp — sliding `#window.time(T)` group-by queries (TimeWindowProcessor semantics).
-#include "sh_runtime.h"
+// sh_sliding.cpp — sliding `from S[cond]#window.time(T) select k, aggs group by k insert into O`
+// (TimeWindowProcessor + QuerySelector in SLIDE mode) behind sh_query_* (kind 1).
+//
+// The window contents of every key live on the device in per-key rings; aggregator state per key
+// (counts, running sums with Java's residue, min/max deques) persists across pushes. A push emits,
+// per send, one row per key that had a current event in that send (first-occurrence order), with
+// the aggregate values after that key's last event in the send (QuerySelector.java:315-374).
+#include <hip/hip_runtime.h>
 
-struct SlidingImpl {};
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sh_runtime.h"
+#include "sh_sliding.h"
+
+using namespace shd;
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+struct SlidingImpl {
+    int64_t nslots = 0, rc = 0;
+    int P = 1;
+    int64_t pm = INT64_MIN;   // PM carried across pushes
+    int64_t send_base = 0;    // global send number of the push's first send
+    DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
+    // per push scratch
+    DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
+        tmp, ranks, part_off, flags, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
+        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, flush_off, flush_clock;
+    SlInfo* h_info = nullptr;
+    sh_out dev_out{};
+};
+
+static SlState state_of(SlidingImpl* s) {
+    SlState S;
+    S.nslots = s->nslots;
+    S.rc = s->rc;
+    S.cnt = s->cnt.as<int64_t>();
+    S.f = s->f.as<u64>();
+    S.mm = s->mm.as<u64>();
+    S.mm_has = s->mm_has.as<unsigned char>();
+    S.dq_head = s->dq_head.as<int64_t>();
+    S.dq_len = s->dq_len.as<int64_t>();
+    S.dq = s->dq.as<u64>();
+    S.rhead = s->rhead.as<int64_t>();
+    S.rlen = s->rlen.as<int64_t>();
+    S.rpm = s->rpm.as<int64_t>();
+    S.rval = s->rval.as<u64>();
+    S.cur_send = s->cur_send.as<int64_t>();
+    S.cur_first = s->cur_first.as<int64_t>();
+    return S;
+}
+
+static int alloc_zero(DevBuf& b, size_t bytes, int fill = 0) {
+    RCHK(b.reserve(std::max<size_t>(bytes, 8), false));
+    if (hipMemset(b.p, fill, std::max<size_t>(bytes, 8)) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "memset failed");
+    return SH_OK;
+}
+
+// (re)size the per-key rings and deques to capacity rc (power of two), keeping their contents
+static int size_rings(sh_query* q, int64_t new_rc) {
+    SlidingImpl* s = q->sl;
+    int F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols);
+    int64_t n = s->nslots;
+    DevBuf rpm2, rval2, dq2;
+    RCHK(rpm2.reserve((size_t)n * new_rc * 8, false));
+    RCHK(rval2.reserve((size_t)V * n * new_rc * 8, false));
+    RCHK(dq2.reserve((size_t)F * n * new_rc * 8, false));
+    hipStream_t st = q->ctx->stream;
+    if (s->rc > 0) {
+        launch_sl_regrow(st, (const u64*)s->rpm.p, (u64*)rpm2.p, s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, 1,
+                         s->rc, new_rc, false);
+        launch_sl_regrow(st, s->rval.as<u64>(), rval2.as<u64>(), s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, V,
+                         s->rc, new_rc, false);
+        launch_sl_regrow(st, s->dq.as<u64>(), dq2.as<u64>(), s->dq_head.as<int64_t>(), s->dq_len.as<int64_t>(), n, F,
+                         s->rc, new_rc, true);
+        HIPCHK(hipMemsetAsync(s->rhead.p, 0, n * 8, st));
+        HIPCHK(hipMemsetAsync(s->dq_head.p, 0, (size_t)F * n * 8, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    s->rpm.release(); s->rval.release(); s->dq.release();
+    s->rpm = rpm2; s->rval = rval2; s->dq = dq2;
+    rpm2.p = rval2.p = dq2.p = nullptr;
+    s->rc = new_rc;
+    return SH_OK;
+}
 
 int sliding_create(sh_query* q) {
-    (void)q;
-    return sh_fail(SH_ERR_UNSUPPORTED, "sliding time window not yet on the GPU");
+    if (q->partitioned) return sh_fail(SH_ERR_UNSUPPORTED, "partitioned sliding windows are not on the GPU");
+    SlidingImpl* s = new SlidingImpl();
+    q->sl = s;
+    s->nslots = (int64_t)q->kt.size_ + 1;
+    int F = std::max(1, q->ap.n_fields);
+    int64_t n = s->nslots;
+    RCHK(alloc_zero(s->cnt, n * 8));
+    RCHK(alloc_zero(s->f, (size_t)F * n * 8));
+    RCHK(alloc_zero(s->mm, (size_t)F * n * 8));
+    RCHK(alloc_zero(s->mm_has, (size_t)F * n));
+    RCHK(alloc_zero(s->dq_head, (size_t)F * n * 8));
+    RCHK(alloc_zero(s->dq_len, (size_t)F * n * 8));
+    RCHK(alloc_zero(s->rhead, n * 8));
+    RCHK(alloc_zero(s->rlen, n * 8));
+    RCHK(alloc_zero(s->cur_send, n * 8, 0xff));
+    RCHK(alloc_zero(s->cur_first, n * 8));
+    RCHK(s->info.reserve(sizeof(SlInfo), false));
+    if (hipHostMalloc((void**)&s->h_info, sizeof(SlInfo), hipHostMallocDefault) != hipSuccess)
+        return sh_fail(SH_ERR_OOM, "pinned alloc failed");
+    RCHK(size_rings(q, 64));
+    int P = 1;
+    while (P < 1024 && (int64_t)P * 8 < n) P <<= 1;
+    s->P = P;
+    (void)hipEventCreate(&q->ev_push0); (void)hipEventCreate(&q->ev_push1);
+    (void)hipEventCreate(&q->ev_agg0); (void)hipEventCreate(&q->ev_agg1);
+    return SH_OK;
 }
+
+void sliding_destroy(sh_query* q) {
+    SlidingImpl* s = q->sl;
+    if (!s) return;
+    DevBuf* bufs[] = {&s->cnt, &s->f, &s->mm, &s->mm_has, &s->dq_head, &s->dq_len, &s->dq, &s->rhead, &s->rlen,
+                      &s->rpm, &s->rval, &s->cur_send, &s->cur_first, &s->blk_pass, &s->blk_tl, &s->blk_pm,
+                      &s->info, &s->rec_raw, &s->rec_slot, &s->rec_clock, &s->rec_pm, &s->rec_ts, &s->rec_vals,
+                      &s->slot_cnt, &s->counts, &s->tmp, &s->ranks, &s->part_off, &s->flags, &s->rows_ts,
+                      &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
+                      &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
+                      &s->out_expired, &s->flush_off, &s->flush_clock};
+    for (DevBuf* b : bufs) b->release();
+    if (s->h_info) (void)hipHostFree(s->h_info);
+    delete s;
+    q->sl = nullptr;
+}
+
+static int empty_out(sh_query* q, const sh_out** out) {
+    q->out.reset();
+    *out = q->out.view(q->kp.n, q->ap.n, q->vtypes);
+    return SH_OK;
+}
+
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
-    (void)q; (void)b; (void)host_out; (void)out;
-    return sh_fail(SH_ERR_UNSUPPORTED, "sliding time window not yet on the GPU");
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    int64_t N = b->n;
+    if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
+    if (N == 0) return empty_out(q, out);
+    if (N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    int nblk = (int)((N + kTile - 1) / kTile);
+    RCHK(s->blk_pass.reserve(nblk * 8, false));
+    RCHK(s->blk_tl.reserve(nblk * 8, false));
+    RCHK(s->blk_pm.reserve(nblk * 8, false));
+    WinParams wp{};
+    wp.kind = SH_WIN_TIME;
+    wp.clock_valid = q->clock_valid;
+    wp.clock0 = q->clock;
+    wp.send_size = b->send_size;
+    wp.N = N;
+    launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                     s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+    // records of all passing events (capacity N; the exact count is known after the prefix scan)
+    int V = std::max(1, q->ap.n_vcols);
+    RCHK(s->rec_raw.reserve(N * 4, false));
+    RCHK(s->rec_slot.reserve(N * 4, false));
+    RCHK(s->rec_clock.reserve(N * 8, false));
+    RCHK(s->rec_pm.reserve(N * 8, false));
+    RCHK(s->rec_ts.reserve(N * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * N * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), N};
+    launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+    HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
+    launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
+                   (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    RCHK(q->kt.check(st));
+    SlInfo info = *s->h_info;
+    int64_t M = info.total_pass;
+    if (info.need > s->rc) {
+        int64_t nrc = s->rc;
+        while (nrc < info.need) nrc <<= 1;
+        RCHK(size_rings(q, nrc));
+    }
+    int64_t n_rows = 0;
+    if (M > 0) {
+        // stable split of the records by key partition
+        int P = s->P;
+        int mblk = (int)((M + kTile - 1) / kTile);
+        int64_t ncnt = (int64_t)P * mblk;
+        RCHK(s->counts.reserve((ncnt + 1) * 8, false));
+        RCHK(s->tmp.reserve(((ncnt + kTile) / kTile + 16) * 8, false));
+        RCHK(s->ranks.reserve(M * 4, false));
+        RCHK(s->part_off.reserve((P + 1) * 8, false));
+        launch_sl_multisplit(st, s->rec_slot.as<u32>(), M, P, s->counts.as<int64_t>(), s->tmp.as<int64_t>(),
+                             s->ranks.as<u32>(), s->part_off.as<int64_t>());
+        // rows indexed by first-occurrence rank
+        int na = q->ap.n;
+        RCHK(s->flags.reserve(M + 16, false));
+        RCHK(s->rows_ts.reserve(M * 8, false));
+        RCHK(s->rows_slot.reserve(M * 4, false));
+        RCHK(s->rows_send.reserve(M * 8, false));
+        RCHK(s->rows_clock.reserve(M * 8, false));
+        RCHK(s->rows_vals.reserve((size_t)na * M * 8, false));
+        RCHK(s->rows_nulls.reserve((size_t)na * M, false));
+        HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
+        SlRows rows{s->rows_ts.as<int64_t>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
+                    s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
+        HIPCHK(hipEventRecord(q->ev_agg0, st));
+        launch_sliding(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, rec, state_of(s), q->ap,
+                       q->d.window_param, b->send_size, s->send_base, rows, s->flags.as<unsigned char>());
+        HIPCHK(hipEventRecord(q->ev_agg1, st));
+        HIPCHK(hipGetLastError());
+        // emit in rank order
+        int fblk = (int)((M + kTile - 1) / kTile);
+        RCHK(s->blk_cnt.reserve((fblk + 16) * 8, false));
+        launch_count_flags(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk);
+        std::vector<int64_t> bc(fblk);
+        HIPCHK(hipMemcpyAsync(bc.data(), s->blk_cnt.p, fblk * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, q->ev_agg0, q->ev_agg1);
+        q->stats.main_kernel_ms = ms;
+        for (auto c : bc) n_rows += c;
+        int nk = q->kp.n;
+        int64_t cap = std::max<int64_t>(n_rows, 1);
+        RCHK(s->out_ts.reserve(cap * 8, false));
+        RCHK(s->out_keys.reserve(std::max(1, nk) * cap * 8, false));
+        RCHK(s->out_vals.reserve((size_t)na * cap * 8, false));
+        RCHK(s->out_nulls.reserve((size_t)na * cap, false));
+        RCHK(s->out_send.reserve(cap * 8, false));
+        RCHK(s->out_clock.reserve(cap * 8, false));
+        RCHK(s->out_expired.reserve(cap, false));
+        HIPCHK(hipMemsetAsync(s->out_expired.p, 0, cap, st));
+        launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
+        launch_sl_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, rows, na, q->kt.dev(),
+                       q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
+                       s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>());
+        HIPCHK(hipGetLastError());
+    }
+    // flush structure: a flush per send that produced rows (one selector output chunk per send)
+    int64_t n_flushes = 0;
+    if (n_rows > 0) {
+        int rb = (int)((n_rows + kTile - 1) / kTile);
+        RCHK(s->blk_cnt.reserve((rb + 16) * 8, false));
+        launch_flush_starts(st, s->out_send.as<int64_t>(), n_rows, s->blk_cnt.as<int64_t>(), rb);
+        std::vector<int64_t> fc(rb);
+        HIPCHK(hipMemcpyAsync(fc.data(), s->blk_cnt.p, rb * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (auto c : fc) n_flushes += c;
+        RCHK(s->flush_off.reserve((n_flushes + 1) * 8, false));
+        RCHK(s->flush_clock.reserve((n_flushes + 1) * 8, false));
+        launch_scan_sum(st, s->blk_cnt.as<int64_t>(), rb);
+        launch_flush_write(st, s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), n_rows, s->blk_cnt.as<int64_t>(),
+                           rb, s->flush_off.as<int64_t>(), s->flush_clock.as<int64_t>());
+        HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, &n_rows, 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipGetLastError());
+    }
+    // window state moves on
+    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+    q->clock_valid = true;
+    s->pm = std::max(s->pm, info.max_pm);
+    s->send_base += b->send_size > 0 ? (N + b->send_size - 1) / b->send_size : 1;
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.events = N;
+    q->stats.main_kernel_bytes = M * (int64_t)(4 + 8 + 8 + 8 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 + 8 * q->ap.n);
+    int nk = q->kp.n, na = q->ap.n;
+    if (host_out) {
+        OutHost& o = q->out;
+        o.reset();
+        o.flush_offsets.resize(n_flushes + 1);
+        o.flush_clock.resize(n_flushes);
+        o.ts.resize(n_rows);
+        o.expired.assign(n_rows, 0);
+        o.keys.resize((size_t)nk * n_rows);
+        o.vals.resize((size_t)na * n_rows);
+        o.nulls.resize((size_t)na * n_rows);
+        if (n_rows > 0) {
+            HIPCHK(hipMemcpyAsync(o.flush_offsets.data(), s->flush_off.p, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.flush_clock.data(), s->flush_clock.p, n_flushes * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.ts.data(), s->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, st));
+            // device arrays have stride cap == n_rows
+            if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), s->out_keys.p, (size_t)nk * n_rows * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.vals.data(), s->out_vals.p, (size_t)na * n_rows * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.nulls.data(), s->out_nulls.p, (size_t)na * n_rows, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        } else {
+            o.flush_offsets.assign(1, 0);
+        }
+        *out = o.view(nk, na, q->vtypes);
+    } else {
+        sh_out& o = s->dev_out;
+        o = sh_out{};
+        o.n_flushes = n_flushes;
+        o.n_rows = n_rows;
+        o.n_keys = nk;
+        o.n_vals = na;
+        for (int i = 0; i < na; i++) o.val_types[i] = q->vtypes[i];
+        o.flush_offsets = s->flush_off.as<int64_t>();
+        o.flush_clock = s->flush_clock.as<int64_t>();
+        o.ts = s->out_ts.as<int64_t>();
+        o.expired = s->out_expired.as<uint8_t>();
+        o.keys = s->out_keys.as<int64_t>();
+        o.vals = s->out_vals.as<uint64_t>();
+        o.nulls = s->out_nulls.as<uint8_t>();
+        *out = &o;
+    }
+    return SH_OK;
 }
+
 int sliding_advance(sh_query* q, int64_t now, const sh_out** out) {
-    (void)q; (void)now; (void)out;
-    return sh_fail(SH_ERR_UNSUPPORTED, "sliding time window not yet on the GPU");
+    // expiry is applied lazily at each key's next event; with current-events-only output the
+    // timer path changes no visible result, only the clock (TimestampGeneratorImpl :104-122)
+    if (!q->clock_valid || now >= q->clock) {
+        q->clock = now;
+        q->clock_valid = true;
+    }
+    return empty_out(q, out);
 }
-void sliding_destroy(sh_query* q) { (void)q; }

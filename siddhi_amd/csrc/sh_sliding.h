@@ -1,0 +1,70 @@
+// sh_sliding.h — device structures of the sliding time-window path (sh_sliding_kernels.hip).
+#pragma once
+#include "sh_internal.h"
+
+namespace shd {
+
+struct SlInfo {
+    i64 total_pass, max_tl, max_pm, need;
+};
+
+// rank-indexed records of the passing events of one push
+struct SlRecords {
+    u32* raw;     // event index in the push
+    u32* slot;    // group key slot
+    i64* clock;   // playback clock of the event's send
+    i64* pm;      // max ts over passing events up to and including this one (all pushes)
+    i64* ts;
+    u64* vals;    // [n_vcols][cap]
+    i64 cap;
+};
+
+// persistent per-key state (indexed by key slot)
+struct SlState {
+    i64 nslots, rc;       // slots, ring capacity (power of two)
+    i64* cnt;             // Count / Avg / Sum counts (equal for every aggregator)
+    u64* f;               // [n_fields][nslots] sums (raw)
+    u64* mm;              // [n_fields][nslots] minValue / maxValue
+    unsigned char* mm_has;
+    i64* dq_head;         // [n_fields][nslots]
+    i64* dq_len;
+    u64* dq;              // [n_fields][nslots][rc] monotone deque rings
+    i64* rhead;           // [nslots] window ring of the key
+    i64* rlen;
+    i64* rpm;             // [nslots][rc] PM of each window event
+    u64* rval;            // [n_vcols][nslots][rc] values of each window event
+    i64* cur_send;        // last send that touched the key (global send number)
+    i64* cur_first;       // rank of the key's first event in that send
+};
+
+// rows indexed by the rank of the (send, key) first occurrence
+struct SlRows {
+    i64* ts;
+    u32* slot;
+    i64* send;
+    i64* clock;
+    u64* vals;            // [n_aggs][cap]
+    unsigned char* nulls; // [n_aggs][cap]
+    i64 cap;
+};
+
+void launch_sl_prefix(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, i64* blk_pass,
+                      i64* blk_tl, i64* blk_pm, int nblk, SlInfo* info);
+void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
+                       KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
+                       i64 pm0, SlRecords rec, u32* slot_cnt, int nblk);
+void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* out);
+void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* counts, i64* tmp, u32* out_rank,
+                          i64* part_off);
+void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, int P, SlRecords rec, SlState S,
+                    AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags);
+void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
+                    int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                    unsigned char* out_nulls, i64* out_send, i64* out_clock);
+void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb);
+void launch_flush_write(hipStream_t s, const i64* out_send, const i64* out_clock, i64 n_rows, const i64* blk_pre,
+                        int nb, i64* flush_off, i64* flush_clock);
+void launch_sl_regrow(hipStream_t s, const u64* old_buf, u64* new_buf, const i64* head, const i64* len, i64 nslots,
+                      int nsub, i64 old_rc, i64 new_rc, bool per_sub);
+
+}  // namespace shd

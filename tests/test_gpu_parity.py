@@ -139,3 +139,48 @@ def test_key_capacity_overflow_fails_loudly(rt):
     g = rt.GpuQuery(spec)
     with pytest.raises(SiddhiError):
         g.push(abi.HostBatch(C2_SCHEMA, ts, cols, 1))
+
+
+# ---- C3: sliding time window (per-key sequential state, SLIDE-mode aggregators) -----------------------
+def c3_spec(keys=10_000, T=10_000):
+    return abi.QuerySpec(C2_SCHEMA, "time", T, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys)
+
+
+@pytest.mark.parametrize("send_size", [1, 250])
+def test_c3_sliding_matches_oracle(rt, send_size):
+    ts, cols = synth.keyed_stream(0, 200_000, 0xC3, 2000, 20)   # 20 events/ms, 10 s window ~ 100 per key
+    pushes = split_batches(C2_SCHEMA, ts, cols, [77_777, 150_000], send_size)
+    both(rt, c3_spec(keys=2000, T=1000), pushes, label="C3")
+
+
+def test_sliding_quantized_deque_quirk(rt):
+    # few distinct values -> duplicates -> removeFirstOccurrence hits other equal elements (R9 quirk)
+    rng = np.random.default_rng(3)
+    n = 60_000
+    ts = np.cumsum(rng.integers(0, 3, n)).astype(np.int64)
+    k = rng.integers(0, 40, n).astype(np.int32)
+    v = rng.integers(0, 6, n).astype(np.float64)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "time", 300, group_by=["k"],
+                         aggs=[("min", "v"), ("max", "v"), ("sum", "v"), ("count", None), ("avg", "v")], key_capacity=64)
+    both(rt, spec, split_batches(schema, ts, [k, v, ts.copy()], [1, 20_000, 40_001], 1), label="quirk")
+
+
+def test_sliding_nonmonotone_ts_filter_and_longs(rt):
+    rng = np.random.default_rng(5)
+    n = 80_000
+    ts = (np.arange(n) // 4 + rng.integers(-50, 50, n)).astype(np.int64) + 10_000
+    k = rng.integers(0, 300, n).astype(np.int32)
+    x = rng.integers(-10**9, 10**9, n).astype(np.int64)
+    f = (rng.standard_normal(n) * 10).astype(np.float32)
+    schema = abi.Schema.parse("k int, x long, f float, ts long")
+    spec = abi.QuerySpec(schema, "time", 500, group_by=["k"], filter=(">", "f", ("float", -5.0)),
+                         aggs=[("sum", "x"), ("min", "f"), ("max", "x"), ("avg", "f"), ("sum", "f")], key_capacity=512)
+    both(rt, spec, split_batches(schema, ts, [k, x, f, ts.copy()], [33_333], 7), label="nonmono")
+
+
+def test_sliding_no_group_by(rt):
+    ts, cols = synth.keyed_stream(0, 30_000, 0xC3, 100, 5)
+    spec = abi.QuerySpec(C2_SCHEMA, "time", 700, aggs=[("sum", "v"), ("max", "v"), ("count", None)])
+    both(rt, spec, split_batches(C2_SCHEMA, ts, cols, [10_000], 3), label="slide-nogroup")
