@@ -1,0 +1,238 @@
+// sh_agg_kernels.hip — gfx950 kernels of the incremental-aggregation roll-up levels (minutes ... years).
+//
+// The root duration runs on the batch-window pipeline (sh_kernels.hip). Every dispatch of a level's
+// store sends one row per (bucket, key) to the next duration (IncrementalExecutor.dispatchEvent,
+// core/aggregation/IncrementalExecutor.java:201-258), whose BaseIncrementalValueStore folds them with
+// sum / min / max executors (BaseIncrementalValueStore.process :141-160). Here a level's store is a
+// device hash table keyed by (bucket, key) with one 8-byte state per base value.
+#include "sh_device.h"
+#include "sh_agg.h"
+
+namespace shd {
+
+// ---- GMT calendar (IncrementalTimeConverterUtil with ZoneId "GMT") ------------------------------
+__device__ __forceinline__ i64 floor_div_d(i64 a, i64 b) {
+    i64 q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q--;
+    return q;
+}
+__device__ __forceinline__ i64 days_from_civil_d(i64 y, unsigned m, unsigned d) {
+    y -= m <= 2;
+    const i64 era = (y >= 0 ? y : y - 399) / 400;
+    const unsigned yoe = (unsigned)(y - era * 400);
+    const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + (i64)doe - 719468;
+}
+__device__ __forceinline__ void civil_from_days_d(i64 z, i64& y, unsigned& m, unsigned& d) {
+    z += 719468;
+    const i64 era = (z >= 0 ? z : z - 146096) / 146097;
+    const unsigned doe = (unsigned)(z - era * 146097);
+    const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    y = (i64)yoe + era * 400;
+    const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const unsigned mp = (5 * doy + 2) / 153;
+    d = doy - (153 * mp + 2) / 5 + 1;
+    m = mp + (mp < 10 ? 3 : -9);
+    y += (m <= 2);
+}
+
+// getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69); sec/min use `t - t % d`
+__device__ __forceinline__ i64 start_of_dev(i64 t, int dur) {
+    switch (dur) {
+        case SH_DUR_SECONDS: return t - t % 1000;
+        case SH_DUR_MINUTES: return t - t % 60000;
+        case SH_DUR_HOURS: return floor_div_d(t, 3600000) * 3600000;
+        case SH_DUR_DAYS: return floor_div_d(t, 86400000) * 86400000;
+        default: {
+            i64 days = floor_div_d(t, 86400000);
+            i64 y; unsigned m, d;
+            civil_from_days_d(days, y, m, d);
+            if (dur == SH_DUR_MONTHS) return days_from_civil_d(y, m, 1) * 86400000;
+            return days_from_civil_d(y, 1, 1) * 86400000;
+        }
+    }
+}
+
+__device__ __forceinline__ u64 level_key(int has_bucket, i64 bucket, i64 key) {
+    if (!has_bucket) return (u64)key;
+    return ((u64)(u32)(bucket / 1000) << 32) | (u64)(u32)key;
+}
+
+// one lookup per incoming row; `first_seq` keeps the arrival index of a slot's first row since the last
+// dispatch so extraction can restore insertion order (the oracle's store order)
+__global__ __launch_bounds__(kBlock) void k_level_lookup(i64 n, const i64* __restrict__ bucket_in,
+                                                        const i64* __restrict__ key_in, int has_bucket, int dur,
+                                                        LevelDev L, u32 epoch, u32 seq0, u32* slot_out, int* dup) {
+    i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    i64 cb = has_bucket ? start_of_dev(bucket_in[i], dur) : 0;
+    u32 pos = key_slot(L.kt, level_key(has_bucket, cb, key_in ? key_in[i] : 0));
+    slot_out[i] = pos;
+    atomicMin(&L.first_seq[pos], seq0 + (u32)i);
+    u32 old = atomicExch(&L.tag[pos], epoch);
+    if (old == epoch) atomicExch(dup, 1);
+}
+
+__device__ __forceinline__ void level_fold(const LevelDev& L, const BasePlan& bp, u32 pos, const u64* vin,
+                                           i64 stride, i64 i) {
+    for (int b = 0; b < bp.n; b++) {
+        u64 x = vin[(size_t)b * stride + i];
+        size_t fi = (size_t)b * L.nslots + pos;
+        bool first = !L.has[fi];
+        u64 cur = L.vals[fi];
+        switch (bp.kind[b]) {
+            case AK_SUM_L: case AK_COUNT: L.vals[fi] = (u64)((first ? 0 : (i64)cur) + (i64)x); break;  // sum += v
+            case AK_SUM_D:
+                L.vals[fi] = (u64)__double_as_longlong((first ? 0.0 : __longlong_as_double((i64)cur)) +
+                                                       __longlong_as_double((i64)x));
+                break;
+            case AK_MIN_L: if (first || (i64)cur > (i64)x) L.vals[fi] = x; break;
+            case AK_MAX_L: if (first || (i64)cur < (i64)x) L.vals[fi] = x; break;
+            case AK_MIN_D: if (first || __longlong_as_double((i64)cur) > __longlong_as_double((i64)x)) L.vals[fi] = x; break;
+            case AK_MAX_D: if (first || __longlong_as_double((i64)cur) < __longlong_as_double((i64)x)) L.vals[fi] = x; break;
+            case AK_MIN_F: if (first || (float)__longlong_as_double((i64)cur) > (float)__longlong_as_double((i64)x)) L.vals[fi] = x; break;
+            case AK_MAX_F: if (first || (float)__longlong_as_double((i64)cur) < (float)__longlong_as_double((i64)x)) L.vals[fi] = x; break;
+        }
+        L.has[fi] = 1;
+    }
+}
+
+// rows with distinct slots: fold in parallel
+__global__ __launch_bounds__(kBlock) void k_level_fold_par(i64 n, const u32* __restrict__ slots,
+                                                          const u64* __restrict__ vin, i64 stride, LevelDev L,
+                                                          BasePlan bp) {
+    i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    level_fold(L, bp, slots[i], vin, stride, i);
+}
+
+// rows sharing a slot within one dispatch (late events): fold in row order, one lane
+__global__ void k_level_fold_seq(i64 n, const u32* __restrict__ slots, const u64* __restrict__ vin, i64 stride,
+                                 LevelDev L, BasePlan bp) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (i64 i = 0; i < n; i++) level_fold(L, bp, slots[i], vin, stride, i);
+}
+
+void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
+                        const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
+                        int* dup_dev, int* dup_host) {
+    if (n == 0) return;
+    unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+    (void)hipMemsetAsync(dup_dev, 0, 4, s);
+    hipLaunchKernelGGL(k_level_lookup, dim3(g), dim3(kBlock), 0, s, n, bucket_in, key_in, has_bucket, dur, L, epoch,
+                       seq0, slots, dup_dev);
+    (void)hipMemcpyAsync(dup_host, dup_dev, 4, hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    if (*dup_host)
+        hipLaunchKernelGGL(k_level_fold_seq, dim3(1), dim3(64), 0, s, n, slots, vin, stride, L, bp);
+    else
+        hipLaunchKernelGGL(k_level_fold_par, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp);
+}
+
+// ---- extraction of a level's store (dispatch) -----------------------------------------------------
+// order[first_seq[slot]] = slot, so walking `order` visits the slots in first-arrival order
+__global__ __launch_bounds__(kBlock) void k_level_mark(LevelDev L) {
+    i64 p = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= L.nslots) return;
+    u32 f = L.first_seq[p];
+    if (f != 0xFFFFFFFFu) {
+        L.order[f] = (u32)p;
+        L.first_seq[p] = 0xFFFFFFFFu;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_level_count(LevelDev L, i64 n_in, i64* blk_cnt) {
+    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    i64 c = 0;
+    for (int i = 0; i < kItems; i++) {
+        i64 q = base + i;
+        if (q < n_in && L.order[q] != 0xFFFFFFFFu) c++;
+    }
+    i64 t = block_reduce(c, SumOp(), 0);
+    if (threadIdx.x == 0) blk_cnt[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kBlock) void k_level_extract(LevelDev L, BasePlan bp, int has_bucket, i64 store_ts,
+                                                         i64 n_in, const i64* blk_pre, i64 cap, i64* out_bucket,
+                                                         i64* out_key, u64* out_vals) {
+    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    u32 slot[kItems];
+    i64 c = 0;
+    for (int i = 0; i < kItems; i++) {
+        i64 q = base + i;
+        slot[i] = q < n_in ? L.order[q] : 0xFFFFFFFFu;
+        c += slot[i] != 0xFFFFFFFFu;
+    }
+    i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + blk_pre[blockIdx.x];
+    for (int i = 0; i < kItems; i++) {
+        if (slot[i] == 0xFFFFFFFFu) continue;
+        u32 p = slot[i];
+        u64 k = slot_key(L.kt, p);
+        if (has_bucket) {
+            out_bucket[r] = (i64)(u32)(k >> 32) * 1000;
+            out_key[r] = (i64)(int)(u32)k;
+        } else {
+            out_bucket[r] = store_ts;
+            out_key[r] = (i64)k;
+        }
+        for (int b = 0; b < bp.n; b++) {
+            out_vals[(size_t)b * cap + r] = L.vals[(size_t)b * L.nslots + p];
+            L.has[(size_t)b * L.nslots + p] = 0;
+        }
+        if (p <= L.kt.mask) L.kt.keys[p] = kEmptyKey;  // BaseIncrementalValueStore.clearValues (:73-78)
+        r++;
+    }
+}
+
+void launch_level_mark(hipStream_t s, LevelDev L, i64 n_in) {
+    (void)hipMemsetAsync(L.order, 0xFF, (size_t)n_in * 4, s);
+    unsigned g = (unsigned)((L.nslots + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_level_mark, dim3(g), dim3(kBlock), 0, s, L);
+}
+
+void launch_level_count(hipStream_t s, LevelDev L, i64 n_in, i64* blk, int nblk) {
+    hipLaunchKernelGGL(k_level_count, dim3(nblk), dim3(kBlock), 0, s, L, n_in, blk);
+}
+
+void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket, i64 store_ts, i64 n_in, i64* blk,
+                          int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals) {
+    hipLaunchKernelGGL(k_level_extract, dim3(nblk), dim3(kBlock), 0, s, L, bp, has_bucket, store_ts, n_in, blk, cap,
+                       out_bucket, out_key, out_vals);
+}
+
+// min / max of an int64 column (event-time span of a push -> root key-table bound)
+__global__ __launch_bounds__(kBlock) void k_minmax_i64(const i64* __restrict__ x, i64 n, i64* out) {
+    i64 lo = INT64_MAX, hi = INT64_MIN;
+    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
+        i64 v = x[i];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    lo = block_reduce(lo, MinOp(), INT64_MAX);
+    hi = block_reduce(hi, MaxOp(), INT64_MIN);
+    if (threadIdx.x == 0) {
+        atomicMin((long long*)&out[0], (long long)lo);
+        atomicMax((long long*)&out[1], (long long)hi);
+    }
+}
+
+void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out) {
+    const i64 init[2] = {INT64_MAX, INT64_MIN};
+    (void)hipMemcpyAsync(out, init, 16, hipMemcpyHostToDevice, s);
+    if (n <= 0) return;
+    unsigned g = (unsigned)std::min<i64>(1024, (n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_minmax_i64, dim3(g), dim3(kBlock), 0, s, x, n, out);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill_i64(i64* p, i64 n, i64 v) {
+    i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_fill_i64, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, n, v);
+}
+
+}  // namespace shd

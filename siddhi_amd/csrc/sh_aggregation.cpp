@@ -1,26 +1,569 @@
-// sh_aggregation.cpp — incremental `define aggregation ... every sec...year` roll-ups.
+// sh_aggregation.cpp — `define aggregation A from S[cond] select k, aggs group by k aggregate [by ts]
+// every <min> ... <max>` on the GPU (core/aggregation/*, util/parser/AggregationParser.java).
+//
+// Root duration: AGG_TIMESTAMP = currentTimeMillis() = the playback clock (AggregationParser.java:977-990),
+// so the root executor's stores are processing-time buckets that close when the clock crosses the next
+// bucket boundary (IncrementalExecutor.execute :110-139). That is exactly timeBatch(T_root, 0) with group
+// key (event-time bucket of `ts` at the root duration, k) — the root runs on the batch-window pipeline.
+// Upper durations fold the dispatched rows in device hash tables; their emission cascade (rows with the
+// parent's store timestamp, then a TIMER with the parent's new bucket start, :141-150) is scalar control
+// flow driven here on the host, restated from IncrementalExecutor.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sh_agg.h"
 #include "sh_runtime.h"
 
-struct sh_aggregation {};
+using namespace shd;
 
-extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* desc, sh_aggregation** out) {
-    (void)ctx; (void)desc; (void)out;
-    return sh_fail(SH_ERR_UNSUPPORTED, "incremental aggregation not yet on the GPU");
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+// ---- host restatement of IncrementalTimeConverterUtil (GMT) ----------------------------------------
+static int64_t h_floor_div(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q--;
+    return q;
 }
-extern "C" int sh_aggregation_destroy(sh_aggregation* a) { delete a; return SH_OK; }
+static int64_t h_days_from_civil(int64_t y, unsigned m, unsigned d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const unsigned yoe = (unsigned)(y - era * 400);
+    const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + (int64_t)doe - 719468;
+}
+static void h_civil_from_days(int64_t z, int64_t& y, unsigned& m, unsigned& d) {
+    z += 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const unsigned doe = (unsigned)(z - era * 146097);
+    const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    y = (int64_t)yoe + era * 400;
+    const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const unsigned mp = (5 * doy + 2) / 153;
+    d = doy - (153 * mp + 2) / 5 + 1;
+    m = mp + (mp < 10 ? 3 : -9);
+    y += (m <= 2);
+}
+struct HCivil { int64_t y; unsigned m, d; int64_t h; };
+static HCivil h_civil(int64_t ms) {
+    int64_t days = h_floor_div(ms, 86400000);
+    HCivil c;
+    h_civil_from_days(days, c.y, c.m, c.d);
+    c.h = (ms - days * 86400000) / 3600000;
+    return c;
+}
+static int64_t h_epoch(int64_t y, int64_t m, int64_t d, int64_t h) {
+    return (h_days_from_civil(y, (unsigned)m, (unsigned)d) * 86400 + h * 3600) * 1000;
+}
+static int h_month_len(unsigned m, bool leap) {
+    static const int L[13] = {0, 31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    return (m == 2 && leap) ? 29 : L[m];
+}
+static int64_t h_start_of(int64_t t, int dur) {
+    switch (dur) {
+        case SH_DUR_SECONDS: return t - t % 1000;
+        case SH_DUR_MINUTES: return t - t % 60000;
+        case SH_DUR_HOURS: { HCivil c = h_civil(t); return h_epoch(c.y, c.m, c.d, c.h); }
+        case SH_DUR_DAYS: { HCivil c = h_civil(t); return h_epoch(c.y, c.m, c.d, 0); }
+        case SH_DUR_MONTHS: { HCivil c = h_civil(t); return h_epoch(c.y, c.m, 1, 0); }
+        default: { HCivil c = h_civil(t); return h_epoch(c.y, 1, 1, 0); }
+    }
+}
+// getNextEmitTime (IncrementalTimeConverterUtil.java:33-50, 89-160), month length via `year % 4 == 0`
+static int64_t h_next_emit(int64_t t, int dur) {
+    switch (dur) {
+        case SH_DUR_SECONDS: return t - t % 1000 + 1000;
+        case SH_DUR_MINUTES: return t - t % 60000 + 60000;
+        case SH_DUR_HOURS: {
+            HCivil c = h_civil(t);
+            if (c.h == 23) {
+                if ((int)c.d + 1 > h_month_len(c.m, c.y % 4 == 0)) {
+                    if (c.m == 12) return h_epoch(c.y + 1, 1, 1, 0);
+                    return h_epoch(c.y, c.m + 1, 1, 0);
+                }
+                return h_epoch(c.y, c.m, c.d + 1, 0);
+            }
+            return h_epoch(c.y, c.m, c.d, c.h + 1);
+        }
+        case SH_DUR_DAYS: {
+            HCivil c = h_civil(t);
+            if ((int)c.d + 1 > h_month_len(c.m, c.y % 4 == 0)) {
+                if (c.m == 12) return h_epoch(c.y + 1, 1, 1, 0);
+                return h_epoch(c.y, c.m + 1, 1, 0);
+            }
+            return h_epoch(c.y, c.m, c.d + 1, 0);
+        }
+        case SH_DUR_MONTHS: {
+            HCivil c = h_civil(t);
+            if (c.m == 12) return h_epoch(c.y + 1, 1, 1, 0);
+            return h_epoch(c.y, c.m + 1, 1, 0);
+        }
+        default: { HCivil c = h_civil(t); return h_epoch(c.y + 1, 1, 1, 0); }
+    }
+}
+
+// A batch of rows on the device: bucket / key / base values (stride = cap).
+struct RowBatch {
+    int64_t n = 0, cap = 0;
+    const int64_t* bucket = nullptr;
+    const int64_t* key = nullptr;
+    const u64* vals = nullptr;
+};
+
+// Rows accumulated in a duration's table.
+struct TableBuf {
+    DevBuf bucket, key, vals;
+    int64_t n = 0, cap = 0;
+};
+
+struct Level {
+    int dur = 0;
+    // IncrementalExecutor.ExecutorState (:283-317) + BaseIncrementalValueStore store state (:231-262)
+    int64_t next_emit = -1, start = -1, store_ts = -1;
+    bool processed = false;
+    KeyTableHost kt;
+    DevBuf vals, has, tag, first_seq, order, slots, dup, blk, out_bucket, out_key, out_vals;
+    int64_t n_in = 0;  // rows merged since the last dispatch
+    int64_t nslots = 0;
+    uint32_t epoch = 0;
+    int* dup_host = nullptr;
+};
+
+struct sh_aggregation {
+    sh_ctx* ctx = nullptr;
+    sh_aggregation_desc d{};
+    BasePlan bp{};
+    int32_t btypes[SH_MAX_AGGS]{};
+    int nb = 0;
+    bool has_bucket = false;
+    int64_t T_root = 0;
+    sh_query* root = nullptr;
+    bool root_init = false;
+    int64_t root_bucket = 0;
+    std::vector<Level> levels;            // durations above the root
+    TableBuf tables[SH_DUR_YEARS + 1];
+    OutHost tout;
+    DevBuf root_bucket_col, root_key_col, minmax;
+    int64_t* h_minmax = nullptr;
+};
+
+static LevelDev level_dev(Level& L, int nb) {
+    LevelDev D;
+    D.kt = L.kt.dev();
+    D.nslots = L.nslots;
+    D.vals = L.vals.as<u64>();
+    D.has = L.has.as<unsigned char>();
+    D.tag = L.tag.as<u32>();
+    D.first_seq = L.first_seq.as<u32>();
+    D.order = L.order.as<u32>();
+    (void)nb;
+    return D;
+}
+
+// append rows to the duration's table buffer
+static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
+    if (rb.n == 0) return SH_OK;
+    TableBuf& t = a->tables[dur];
+    hipStream_t s = a->ctx->stream;
+    int64_t need = t.n + rb.n;
+    if (need > t.cap) {
+        int64_t ncap = std::max<int64_t>(need, std::max<int64_t>(1024, t.cap * 2));
+        DevBuf b2, k2, v2;
+        RCHK(b2.reserve(ncap * 8, false));
+        RCHK(k2.reserve(ncap * 8, false));
+        RCHK(v2.reserve((size_t)a->nb * ncap * 8, false));
+        if (t.n) {
+            HIPCHK(hipMemcpyAsync(b2.p, t.bucket.p, t.n * 8, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(k2.p, t.key.p, t.n * 8, hipMemcpyDeviceToDevice, s));
+            for (int b = 0; b < a->nb; b++)
+                HIPCHK(hipMemcpyAsync((char*)v2.p + (size_t)b * ncap * 8, (char*)t.vals.p + (size_t)b * t.cap * 8,
+                                      t.n * 8, hipMemcpyDeviceToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        t.bucket.release(); t.key.release(); t.vals.release();
+        t.bucket = b2; t.key = k2; t.vals = v2;
+        b2.p = k2.p = v2.p = nullptr;
+        t.cap = ncap;
+    }
+    HIPCHK(hipMemcpyAsync(t.bucket.as<int64_t>() + t.n, rb.bucket, rb.n * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(t.key.as<int64_t>() + t.n, rb.key, rb.n * 8, hipMemcpyDeviceToDevice, s));
+    for (int b = 0; b < a->nb; b++)
+        HIPCHK(hipMemcpyAsync(t.vals.as<u64>() + (size_t)b * t.cap + t.n, rb.vals + (size_t)b * rb.cap, rb.n * 8,
+                              hipMemcpyDeviceToDevice, s));
+    t.n = need;
+    return SH_OK;
+}
+
+static int level_timer(sh_aggregation* a, size_t li, int64_t ts);
+static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t ts);
+
+// dispatchEvent (:201-258) + cleanBaseIncrementalValueStore (:260-266)
+static int level_dispatch(sh_aggregation* a, size_t li, int64_t start_of_new) {
+    Level& L = a->levels[li];
+    hipStream_t s = a->ctx->stream;
+    if (L.processed) {
+        int64_t n_in = L.n_in;
+        int nblk = (int)((n_in + kTile - 1) / kTile);
+        RCHK(L.blk.reserve((nblk + 8) * 8, false));
+        RCHK(L.order.reserve(std::max<int64_t>(n_in, 1) * 4, false));
+        LevelDev D = level_dev(L, a->nb);
+        launch_level_mark(s, D, n_in);
+        launch_level_count(s, D, n_in, L.blk.as<int64_t>(), nblk);
+        std::vector<int64_t> bc(nblk);
+        HIPCHK(hipMemcpyAsync(bc.data(), L.blk.p, nblk * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int64_t n = 0;
+        for (auto c : bc) n += c;
+        int64_t cap = std::max<int64_t>(n, 1);
+        RCHK(L.out_bucket.reserve(cap * 8, false));
+        RCHK(L.out_key.reserve(cap * 8, false));
+        RCHK(L.out_vals.reserve((size_t)a->nb * cap * 8, false));
+        launch_scan_sum(s, L.blk.as<int64_t>(), nblk);
+        launch_level_extract(s, D, a->bp, a->has_bucket, L.store_ts, n_in, L.blk.as<int64_t>(), nblk, cap,
+                             L.out_bucket.as<int64_t>(), L.out_key.as<int64_t>(), L.out_vals.as<u64>());
+        HIPCHK(hipGetLastError());
+        L.n_in = 0;
+        RowBatch rb;
+        rb.n = n; rb.cap = cap;
+        rb.bucket = L.out_bucket.as<int64_t>();
+        rb.key = L.out_key.as<int64_t>();
+        rb.vals = L.out_vals.as<u64>();
+        RCHK(table_append(a, L.dur, rb));
+        if (li + 1 < a->levels.size()) RCHK(level_rows(a, li + 1, rb, L.store_ts));
+    }
+    L.store_ts = start_of_new;
+    L.processed = false;
+    return SH_OK;
+}
+
+// IncrementalExecutor.execute for a chunk of rows that share AGG_TIMESTAMP `ts` (:110-139)
+static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t ts) {
+    Level& L = a->levels[li];
+    L.start = h_start_of(ts, L.dur);
+    if (ts >= L.next_emit) {
+        L.next_emit = h_next_emit(ts, L.dur);
+        RCHK(level_dispatch(a, li, L.start));
+        if (li + 1 < a->levels.size()) RCHK(level_timer(a, li + 1, L.start));
+    }
+    if (rb.n > 0) {
+        hipStream_t s = a->ctx->stream;
+        RCHK(L.slots.reserve(rb.n * 4, false));
+        L.epoch++;
+        if (L.n_in + rb.n >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "too many rows in one roll-up bucket");
+        launch_level_merge(s, rb.n, rb.bucket, rb.key, a->has_bucket, L.dur, rb.vals, rb.cap, level_dev(L, a->nb),
+                           a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>(), L.dup_host);
+        L.n_in += rb.n;
+        HIPCHK(hipGetLastError());
+        RCHK(L.kt.check(s));
+        L.processed = true;
+    }
+    return SH_OK;
+}
+
+// TIMER event at a child executor (getTimestamp for non-CURRENT events, :163-168)
+static int level_timer(sh_aggregation* a, size_t li, int64_t ts) {
+    RowBatch none;
+    return level_rows(a, li, none, ts);
+}
+
+// a run of `count` TIMERs at first, first+step, ... (one per root bucket the clock passed)
+static int level_timer_run(sh_aggregation* a, size_t li, int64_t first, int64_t step, int64_t count) {
+    Level& L = a->levels[li];
+    while (count > 0) {
+        if (first >= L.next_emit) {
+            RCHK(level_timer(a, li, first));
+            first += step;
+            count--;
+        } else {
+            // timers below nextEmitTime only refresh startTimeOfAggregates
+            int64_t k = (L.next_emit - first + step - 1) / step;
+            if (k >= count) {
+                L.start = h_start_of(first + (count - 1) * step, L.dur);
+                return SH_OK;
+            }
+            first += k * step;
+            count -= k;
+        }
+    }
+    return SH_OK;
+}
+
+static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
+    sh_query* q = a->root;
+    int64_t T = a->T_root;
+    int64_t E0 = q->E0;
+    int nk = o->n_keys;
+    for (int64_t f = 0; f < o->n_flushes; f++) {
+        int64_t W = q->flush_window[f];
+        int64_t s_f = E0 + (W - 1) * T;  // processing bucket of the closed root store
+        int64_t lo = o->flush_offsets[f], hi = o->flush_offsets[f + 1];
+        RowBatch rb;
+        rb.n = hi - lo;
+        rb.cap = o->n_rows;
+        const int64_t* keys = o->keys;
+        if (a->has_bucket) {
+            rb.bucket = keys + lo;
+            rb.key = nk > 1 ? keys + (size_t)o->n_rows + lo : a->root_key_col.as<int64_t>();
+        } else {
+            rb.bucket = a->root_bucket_col.as<int64_t>();
+            rb.key = nk > 0 ? keys + lo : a->root_key_col.as<int64_t>();
+        }
+        rb.vals = (const u64*)o->vals + lo;
+        // timers of the empty root buckets before s_f
+        if (s_f > a->root_bucket && !a->levels.empty())
+            RCHK(level_timer_run(a, 0, a->root_bucket + T, T, (s_f - a->root_bucket) / T));
+        a->root_bucket = std::max(a->root_bucket, s_f);
+        // the root table gets the rows; without `aggregate by` AGG_TIMESTAMP is the store timestamp
+        if (!a->has_bucket) {
+            RCHK(a->root_bucket_col.reserve(std::max<int64_t>(rb.n, 1) * 8, false));
+            launch_fill_i64(a->ctx->stream, a->root_bucket_col.as<int64_t>(), rb.n, s_f);
+            rb.bucket = a->root_bucket_col.as<int64_t>();
+        }
+        RCHK(table_append(a, a->d.min_duration, rb));
+        if (!a->levels.empty()) {
+            RCHK(level_rows(a, 0, rb, s_f));
+            RCHK(level_timer(a, 0, s_f + T));
+        }
+        a->root_bucket = s_f + T;
+    }
+    return SH_OK;
+}
+
+// after a push / advance: timers of the root buckets up to the clock
+static int catch_up(sh_aggregation* a) {
+    sh_query* q = a->root;
+    if (!q->e0_valid) return SH_OK;
+    int64_t T = a->T_root;
+    if (!a->root_init) {
+        // first event: root store opens at the bucket of the first clock and TIMERs its child (:141-150)
+        a->root_init = true;
+        a->root_bucket = q->E0 - T;
+        if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
+    }
+    int64_t cb = h_floor_div(q->clock, T) * T;
+    if (cb > a->root_bucket && !a->levels.empty())
+        RCHK(level_timer_run(a, 0, a->root_bucket + T, T, (cb - a->root_bucket) / T));
+    a->root_bucket = std::max(a->root_bucket, cb);
+    return SH_OK;
+}
+
+extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, sh_aggregation** out) {
+    if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_create: NULL argument");
+    if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS || d->n_aggs <= 0 || d->n_aggs > SH_MAX_AGGS ||
+        d->min_duration < 0 || d->max_duration > SH_DUR_YEARS || d->min_duration > d->max_duration)
+        return sh_fail(SH_ERR_INVALID, "invalid aggregation descriptor");
+    if (d->min_duration > SH_DUR_DAYS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation roots are sec/min/hour/day");
+    if (d->n_group_by > 1) return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation supports one group-by column");
+    if (d->ts_col >= 0 && (d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG))
+        return sh_fail(SH_ERR_INVALID, "`aggregate by` attribute must be a long");
+    sh_aggregation* a = new sh_aggregation();
+    a->ctx = ctx;
+    a->d = *d;
+    a->d.filter = nullptr;
+    a->has_bucket = d->ts_col >= 0;
+    static const int64_t unit[] = {1000, 60000, 3600000, 86400000};
+    a->T_root = unit[d->min_duration];
+    // base values, de-duplicated like AggregationParser.populateFinalBaseAggregators
+    struct B { int kind; int col; };
+    std::vector<B> bases;
+    auto add = [&](int kind, int col) {
+        for (auto& b : bases) if (b.kind == kind && (kind == 0 || b.col == col)) return;
+        bases.push_back(B{kind, col});
+    };
+    for (int i = 0; i < d->n_aggs; i++) {
+        int fn = d->aggs[i].fn, col = d->aggs[i].col;
+        if (fn != SH_AGG_COUNT && (col < 0 || col >= d->n_cols)) { delete a; return sh_fail(SH_ERR_INVALID, "bad aggregator column"); }
+        if (fn == SH_AGG_SUM) add(1, col);
+        else if (fn == SH_AGG_AVG) { add(1, col); add(0, -1); }
+        else if (fn == SH_AGG_COUNT) add(0, -1);
+        else if (fn == SH_AGG_MIN) add(2, col);
+        else add(3, col);
+    }
+    // the root query's aggregators restate those base executors over the raw events
+    sh_query_desc rd{};
+    rd.n_cols = d->n_cols;
+    for (int c = 0; c < d->n_cols; c++) rd.col_types[c] = d->col_types[c];
+    rd.n_filter_ops = d->n_filter_ops;
+    rd.filter = d->filter;
+    rd.window = SH_WIN_TIME_BATCH;
+    rd.window_param = a->T_root;
+    rd.has_start_time = 1;
+    rd.start_time = 0;
+    rd.current_on = 1;
+    rd.partition_col = -1;
+    rd.n_aggs = (int)bases.size();
+    for (size_t i = 0; i < bases.size(); i++) {
+        static const int fn[] = {SH_AGG_COUNT, SH_AGG_SUM, SH_AGG_MIN, SH_AGG_MAX};
+        rd.aggs[i].fn = fn[bases[i].kind];
+        rd.aggs[i].col = bases[i].col < 0 ? 0 : bases[i].col;
+    }
+    rd.key_capacity = d->key_capacity > 0 ? d->key_capacity : (1 << 16);
+    KeyPlan kp{};
+    int g = 0;
+    if (a->has_bucket) { kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->T_root; g++; }
+    if (d->n_group_by == 1) {
+        int c = d->group_by[0];
+        int t = d->col_types[c];
+        if (!(t == SH_T_INT || t == SH_T_STRID || t == SH_T_BOOL || (t == SH_T_LONG && !a->has_bucket))) {
+            delete a;
+            return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation group-by must be a 32-bit key (long only without `aggregate by`)");
+        }
+        kp.col[g] = c; kp.type[g] = t; kp.div[g] = 0; g++;
+    }
+    kp.n = g;
+    rd.n_group_by = 0;
+    int rc = sh_query_create_internal(ctx, &rd, kp, &a->root);
+    if (rc) { delete a; return rc; }
+    a->nb = a->root->ap.n;
+    a->bp.n = a->nb;
+    for (int i = 0; i < a->nb; i++) {
+        a->bp.kind[i] = a->root->ap.kind[i];
+        a->btypes[i] = a->root->vtypes[i];
+    }
+    // constant key / bucket columns for rows without them
+    RCHK(a->minmax.reserve(16, false));
+    HIPCHK(hipHostMalloc((void**)&a->h_minmax, 16, hipHostMallocDefault));
+    RCHK(a->root_key_col.reserve(8 << 20, false));
+    HIPCHK(hipMemset(a->root_key_col.p, 0, 8 << 20));
+    // upper durations
+    for (int dur = d->min_duration + 1; dur <= d->max_duration; dur++) {
+        a->levels.emplace_back();
+        Level& L = a->levels.back();
+        L.dur = dur;
+        RCHK(L.kt.init(std::max<int64_t>(2 * rd.key_capacity, 64)));
+        L.nslots = (int64_t)L.kt.size_ + 1;
+        RCHK(L.vals.reserve((size_t)a->nb * L.nslots * 8, false));
+        RCHK(L.has.reserve((size_t)a->nb * L.nslots, false));
+        RCHK(L.tag.reserve(L.nslots * 4, false));
+        RCHK(L.first_seq.reserve(L.nslots * 4, false));
+        HIPCHK(hipMemset(L.first_seq.p, 0xFF, L.nslots * 4));
+        RCHK(L.dup.reserve(64, false));
+        HIPCHK(hipMemset(L.has.p, 0, (size_t)a->nb * L.nslots));
+        HIPCHK(hipMemset(L.tag.p, 0, L.nslots * 4));
+        HIPCHK(hipHostMalloc((void**)&L.dup_host, 64, hipHostMallocDefault));
+    }
+    *out = a;
+    return SH_OK;
+}
+
+extern "C" int sh_aggregation_destroy(sh_aggregation* a) {
+    if (!a) return SH_OK;
+    (void)hipStreamSynchronize(a->ctx->stream);
+    if (a->root) sh_query_destroy(a->root);
+    for (auto& L : a->levels) {
+        DevBuf* bufs[] = {&L.vals, &L.has, &L.tag, &L.first_seq, &L.order, &L.slots, &L.dup, &L.blk, &L.out_bucket, &L.out_key, &L.out_vals};
+        for (auto* b : bufs) b->release();
+        L.kt.release();
+        if (L.dup_host) (void)hipHostFree(L.dup_host);
+    }
+    for (auto& t : a->tables) { t.bucket.release(); t.key.release(); t.vals.release(); }
+    a->root_bucket_col.release();
+    a->root_key_col.release();
+    a->minmax.release();
+    if (a->h_minmax) (void)hipHostFree(a->h_minmax);
+    delete a;
+    return SH_OK;
+}
+
+// Room in the root's key table for this push: (event-time bucket, key) pairs are bounded by
+// min(N, keys x buckets spanned); closed buckets' keys are dropped by the rebuild.
+static int reserve_root_keys(sh_aggregation* a, const sh_batch* dev) {
+    int64_t N = dev->n;
+    if (N <= 0) return SH_OK;
+    int64_t keys = a->d.n_group_by ? std::max<int64_t>(1, a->d.key_capacity > 0 ? a->d.key_capacity : (1 << 16)) : 1;
+    int64_t bound = std::min(N, keys);
+    if (a->has_bucket) {
+        hipStream_t s = a->ctx->stream;
+        launch_minmax_i64(s, (const int64_t*)dev->cols[a->d.ts_col], N, a->minmax.as<int64_t>());
+        HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int64_t nb = a->h_minmax[1] / a->T_root - a->h_minmax[0] / a->T_root + 1;
+        bound = (nb > 0 && keys <= N / nb) ? keys * nb : N;
+    }
+    return query_reserve_keys(a->root, bound);
+}
+
+static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
+    const sh_out* o = nullptr;
+    sh_batch dev;
+    if (host) {
+        RCHK(a->root->staged.stage(a->ctx->stream, b, a->root->d.n_cols, a->root->d.col_types, &dev));
+    } else {
+        dev = *b;
+    }
+    RCHK(reserve_root_keys(a, &dev));
+    RCHK(sh_push_device(a->root, &dev, &o));
+    if (o->n_rows > (8 << 20) / 8 && a->d.n_group_by == 0)
+        return sh_fail(SH_ERR_UNSUPPORTED, "too many rows in one flush for a constant key column");
+    bool was_init = a->root_init;
+    if (!was_init && a->root->e0_valid) {
+        a->root_init = true;
+        a->root_bucket = a->root->E0 - a->T_root;
+        if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
+    }
+    RCHK(pass_root_flushes(a, o));
+    return catch_up(a);
+}
+
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
-    (void)a; (void)b;
-    return sh_fail(SH_ERR_UNSUPPORTED, "incremental aggregation not yet on the GPU");
+    if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push: NULL argument");
+    return agg_push(a, b, true);
 }
+
 extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) {
-    (void)a; (void)b;
-    return sh_fail(SH_ERR_UNSUPPORTED, "incremental aggregation not yet on the GPU");
+    if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push_device: NULL argument");
+    return agg_push(a, b, false);
 }
+
+
+
 extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
-    (void)a; (void)now;
-    return sh_fail(SH_ERR_UNSUPPORTED, "incremental aggregation not yet on the GPU");
+    if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
+    const sh_out* o = nullptr;
+    RCHK(sh_advance_time_device(a->root, now, &o));
+    RCHK(pass_root_flushes(a, o));
+    return catch_up(a);
 }
-extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out) {
-    (void)a; (void)duration; (void)out;
-    return sh_fail(SH_ERR_UNSUPPORTED, "incremental aggregation not yet on the GPU");
+
+extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out** out) {
+    if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_table: NULL argument");
+    if (dur < a->d.min_duration || dur > a->d.max_duration) return sh_fail(SH_ERR_INVALID, "duration not aggregated");
+    TableBuf& t = a->tables[dur];
+    hipStream_t s = a->ctx->stream;
+    OutHost& o = a->tout;
+    o.reset();
+    int64_t n = t.n;
+    int nk = 1 + a->d.n_group_by;
+    o.ts.resize(n);
+    o.expired.assign(n, 0);
+    o.keys.resize((size_t)nk * n);
+    o.vals.resize((size_t)a->nb * n);
+    o.nulls.assign((size_t)a->nb * n, 0);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(o.ts.data(), t.bucket.p, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(o.keys.data(), t.bucket.p, n * 8, hipMemcpyDeviceToHost, s));
+        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + n, t.key.p, n * 8, hipMemcpyDeviceToHost, s));
+        for (int b = 0; b < a->nb; b++)
+            HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * n, (char*)t.vals.p + (size_t)b * t.cap * 8, n * 8,
+                                  hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        o.flush_offsets.push_back(n);
+        o.flush_clock.push_back(a->root->clock);
+    }
+    t.n = 0;
+    *out = o.view(nk, a->nb, a->btypes);
+    return SH_OK;
 }

@@ -98,19 +98,30 @@ __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& c
 // ---- group keys ---------------------------------------------------------------------------------
 // GroupByKeyGenerator.constructEventKey (core/query/selector/GroupByKeyGenerator.java:63-73) keys
 // by the values' string form; for the integral key columns string equality is value equality.
+__device__ __forceinline__ i64 key_part(const KeyPlan& kp, const ColSet& cs, int g, i64 e) {
+    i64 v = load_raw(cs, kp.col[g], e);
+    // aggregation time bucket: getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69)
+    if (kp.div[g] > 0) v = v / kp.div[g];
+    return v;
+}
+
 __device__ __forceinline__ u64 make_key(const KeyPlan& kp, const ColSet& cs, i64 e) {
     if (kp.n == 0) return 0;
-    if (kp.n == 1) return (u64)load_raw(cs, kp.col[0], e);
-    u64 a = (u64)(u32)load_raw(cs, kp.col[0], e);
-    u64 b = (u64)(u32)load_raw(cs, kp.col[1], e);
+    if (kp.n == 1) return (u64)key_part(kp, cs, 0, e);
+    u64 a = (u64)(u32)key_part(kp, cs, 0, e);
+    u64 b = (u64)(u32)key_part(kp, cs, 1, e);
     return (a << 32) | b;
 }
 
+__device__ __forceinline__ i64 unpack_part(const KeyPlan& kp, int g, u32 x) {
+    return kp.div[g] > 0 ? (i64)x * kp.div[g] : (i64)(int)x;
+}
+
 __device__ __forceinline__ void unpack_key(const KeyPlan& kp, u64 key, i64* out, i64 stride) {
-    if (kp.n == 1) out[0] = (i64)key;
+    if (kp.n == 1) out[0] = kp.div[0] > 0 ? (i64)key * kp.div[0] : (i64)key;
     else if (kp.n == 2) {
-        out[0] = (i64)(int)(u32)(key >> 32);
-        out[stride] = (i64)(int)(u32)key;
+        out[0] = unpack_part(kp, 0, (u32)(key >> 32));
+        out[stride] = unpack_part(kp, 1, (u32)key);
     }
 }
 

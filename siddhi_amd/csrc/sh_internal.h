@@ -63,6 +63,7 @@ struct KeyPlan {
     int col[SH_MAX_GROUP];
     int type[SH_MAX_GROUP];
     int pad;
+    i64 div[SH_MAX_GROUP];  // > 0: the component is (u32)(value / div) (aggregation time buckets)
 };
 
 // Hash table (key -> position = group slot). positions [0, mask] plus the reserved mask+1
@@ -159,5 +160,6 @@ void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pen
                        u64* rec_vals, i64 rec_cap);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
+void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 }  // namespace shd

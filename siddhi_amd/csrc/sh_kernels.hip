@@ -688,4 +688,16 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
     hipLaunchKernelGGL(k_part_off, dim3((P + 1 + 255) / 256), dim3(256), 0, s, counts, nblk, P, part_off);
 }
 
+// ---- key-table rebuild: the open window's keys move to a fresh table (drops dead keys / grows) ------
+__global__ __launch_bounds__(kBlock) void k_rekey(i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt) {
+    i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    pos[i] = key_slot(new_kt, slot_key(old_kt, pos[i]));
+}
+
+void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_rekey, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, pos, old_kt, new_kt);
+}
+
 }  // namespace shd

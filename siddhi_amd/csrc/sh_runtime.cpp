@@ -197,7 +197,12 @@ int KeyTableHost::init(int64_t capacity) {
     int64_t want = std::max<int64_t>(16, 2 * std::max<int64_t>(1, capacity));
     size_t ts = 16;
     while ((int64_t)ts < want) ts <<= 1;
+    return init_size(ts);
+}
+
+int KeyTableHost::init_size(size_t ts) {
     size_ = ts;
+    n_keys = 0;
     int rc = keys.reserve(ts * 8, false);
     if (rc) return rc;
     rc = ctrl.reserve(64, false);
@@ -220,10 +225,11 @@ KeyTable KeyTableHost::dev() const {
 }
 
 int KeyTableHost::check(hipStream_t s) {
-    int ov = 0;
-    if (hipMemcpyAsync(&ov, (char*)ctrl.p + 8, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    uint32_t c[4] = {0, 0, 0, 0};
+    if (hipMemcpyAsync(c, ctrl.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return sh_fail(SH_ERR_DEVICE, "key table check failed");
-    if (ov) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
+    n_keys = c[0];
+    if (c[2]) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
     return SH_OK;
 }

@@ -31,7 +31,9 @@ struct DevBuf {
 struct KeyTableHost {
     DevBuf keys, ctrl;
     size_t size_ = 0;
+    int64_t n_keys = 0;  // keys inserted so far (read back by check)
     int init(int64_t capacity);
+    int init_size(size_t ts);
     shd::KeyTable dev() const;
     int check(hipStream_t s);
     void release() { keys.release(); ctrl.release(); }
@@ -121,7 +123,19 @@ struct sh_query {
     hipEvent_t ev_push0 = nullptr, ev_push1 = nullptr, ev_agg0 = nullptr, ev_agg1 = nullptr;
     sh_stats stats{};
     int64_t agg_bytes = 0;
+    // per flush of the last push: window number (internal use by the aggregation root)
+    std::vector<int64_t> flush_window;
+    bool internal_keys = false;  // key plan set by an internal owner (aggregation root)
+    size_t kt_min_size = 0;      // table size at creation (rebuilds never shrink below it)
 };
+
+// make room for `extra` new keys in a batch query's table (rebuild / grow; batch windows only)
+int query_reserve_keys(sh_query* q, int64_t extra);
+
+// internal constructor for the aggregation root: a batch query with a prepared key plan
+int sh_query_create_internal(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, sh_query** out);
+// device-output advance (aggregation root)
+int sh_advance_time_device(sh_query* q, int64_t now, const sh_out** out);
 
 
 // sliding time window (sh_sliding.cpp)

@@ -82,7 +82,56 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
     return SH_OK;
 }
 
+static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out);
+
+// key partitions: smallest power of two whose per-partition LDS state fits the budget
+static int size_partitions(sh_query* q) {
+    const size_t budget = 80 * 1024;
+    size_t bpk = 16 + 8 * (size_t)q->ap.n_fields;
+    size_t ts = q->kt.size_;
+    int P = 1;
+    while (((ts / P) + 1) * bpk + 16 > budget && P < (1 << 14)) P <<= 1;
+    if (((ts / P) + 1) * bpk + 16 > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large");
+    q->P = P;
+    q->logP = 0;
+    while ((1 << q->logP) < P) q->logP++;
+    q->NL = (int)(ts / P) + 1;
+    return SH_OK;
+}
+
+// Move the open window's keys into a fresh table of `size` slots: keys of closed windows are dead
+// (their group states were destroyed on flush, R9), so the rebuild drops them; the pending events'
+// slot positions are remapped.
+static int rekey(sh_query* q, size_t size) {
+    KeyTableHost nk;
+    RCHK(nk.init_size(size));
+    launch_rekey(q->ctx->stream, q->n_pend, q->pend_pos.as<u32>(), q->kt.dev(), nk.dev());
+    HIPCHK(hipGetLastError());
+    RCHK(nk.check(q->ctx->stream));
+    q->kt.release();
+    q->kt = nk;
+    nk.keys.p = nk.ctrl.p = nullptr;
+    return size_partitions(q);
+}
+
+int query_reserve_keys(sh_query* q, int64_t extra) {
+    int64_t ts = (int64_t)q->kt.size_;
+    if (q->kt.n_keys + extra <= ts / 2) return SH_OK;
+    int64_t live = std::min<int64_t>(q->kt.n_keys, q->n_pend);
+    size_t want = 16;
+    while ((int64_t)want < 2 * (live + extra)) want <<= 1;
+    return rekey(q, std::max(want, q->kt_min_size));
+}
+
 extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
+    return query_create(ctx, d, nullptr, out);
+}
+
+int sh_query_create_internal(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, sh_query** out) {
+    return query_create(ctx, d, &kp, out);
+}
+
+static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out) {
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_query_create: NULL argument");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     for (int c = 0; c < d->n_cols; c++)
@@ -108,10 +157,11 @@ extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** o
     int rc;
     if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, q->fp)) ||
         (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, q->ap, q->vtypes)) ||
-        (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->kp))) {
+        (!kp_override && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->kp)))) {
         delete q;
         return rc;
     }
+    if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
     if ((rc = q->kt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
@@ -122,17 +172,8 @@ extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** o
         *out = q;
         return SH_OK;
     }
-    // key partitions: smallest power of two whose per-partition LDS state fits the budget
-    const size_t budget = 80 * 1024;
-    size_t bpk = 16 + 8 * (size_t)q->ap.n_fields;
-    size_t ts = q->kt.size_;
-    int P = 1;
-    while (((ts / P) + 1) * bpk + 16 > budget && P < (1 << 14)) P <<= 1;
-    q->P = P;
-    q->logP = 0;
-    while ((1 << q->logP) < P) q->logP++;
-    q->NL = (int)(ts / P) + 1;
-    if (((ts / P) + 1) * bpk + 16 > budget) { delete q; return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large"); }
+    q->kt_min_size = q->kt.size_;
+    if ((rc = size_partitions(q))) { delete q; return rc; }
     if (hipHostMalloc((void**)&q->h_info, sizeof(PushInfo), hipHostMallocDefault) != hipSuccess) {
         delete q;
         return sh_fail(SH_ERR_OOM, "pinned alloc failed");
@@ -147,7 +188,7 @@ extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** o
 // Aggregate the closed segments [segs[i].lo, segs[i].hi) of the combined (pending + new) sequence
 // and append one flush per non-empty segment.
 static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::vector<int64_t>& clocks,
-                      const sh_batch* b, bool host_out) {
+                      const std::vector<int64_t>& windows, const sh_batch* b, bool host_out) {
     hipStream_t s = q->ctx->stream;
     int nseg = (int)segs.size();
     int64_t closed_hi = segs.back().hi;
@@ -243,6 +284,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         acc += seg_rows[i];
         fo.push_back(acc);
         fc.push_back(clocks[i]);
+        q->flush_window.push_back(windows[i]);
     }
     if (!host_out) {
         q->dev_out.n_rows = n_rows;
@@ -329,6 +371,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     q->out.reset();
     q->dev_flush_offsets.assign(1, 0);
     q->dev_flush_clock.clear();
+    q->flush_window.clear();
     q->dev_out = sh_out{};
     q->stats = sh_stats{};
     q->agg_bytes = 0;
@@ -336,6 +379,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
     if (q->n_pend + N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
+    if (N > 0 && !q->internal_keys && q->kt.n_keys > (int64_t)q->kt.size_ / 2) RCHK(query_reserve_keys(q, 0));
     HIPCHK(hipEventRecord(q->ev_push0, s));
     if (N > 0 && q->partitioned && !q->p0_known) RCHK(resolve_first_partition(q, b));
     if (N > 0 && !(q->partitioned && !q->p0_known)) {
@@ -386,14 +430,16 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         int64_t e_lo, pcb_lo, dst_base, new_pend;
         if (!bounds.empty()) {
             std::vector<Segment> segs;
-            std::vector<int64_t> clocks;
-            int64_t lo = 0;
+            std::vector<int64_t> clocks, windows;
+            int64_t lo = 0, wprev = q->W_open;
             for (auto& bd : bounds) {
                 segs.push_back(Segment{lo, bd.idx});
                 clocks.push_back(q->d.window == SH_WIN_LENGTH_BATCH ? bd.clock_prev : bd.clock);
+                windows.push_back(wprev);
                 lo = bd.idx;
+                wprev = bd.W;
             }
-            RCHK(run_closed(q, segs, clocks, b, host_out));
+            RCHK(run_closed(q, segs, clocks, windows, b, host_out));
             e_lo = bounds.back().idx - q->n_pend;
             pcb_lo = bounds.back().pcb;
             dst_base = 0;
@@ -440,28 +486,39 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
     return push_core(q, b, false, out);
 }
 
-extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
-    if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
-    if (q->kind == 1) return sliding_advance(q, now, out);
+static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** out) {
     q->out.reset();
     q->dev_flush_offsets.assign(1, 0);
     q->dev_flush_clock.clear();
+    q->flush_window.clear();
+    q->dev_out = sh_out{};
     // TimestampGeneratorImpl.setCurrentTimestamp only moves the clock forward (:104-122)
-    if (q->clock_valid && now < q->clock) { finish_out(q, true, out); return SH_OK; }
+    if (q->clock_valid && now < q->clock) { finish_out(q, host_out, out); return SH_OK; }
     q->clock = now;
     q->clock_valid = true;
     if (q->d.window == SH_WIN_TIME_BATCH && q->e0_valid) {
         int64_t W = wfun_host(q, now);
         if (W > q->W_open && q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
-            std::vector<int64_t> clocks{now};
-            RCHK(run_closed(q, segs, clocks, nullptr, true));
+            std::vector<int64_t> clocks{now}, windows{q->W_open};
+            RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
             q->n_pend = 0;
         }
         q->W_open = std::max(q->W_open, W);
     }
-    finish_out(q, true, out);
+    finish_out(q, host_out, out);
     return SH_OK;
+}
+
+extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
+    if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
+    if (q->kind == 1) return sliding_advance(q, now, out);
+    return advance_core(q, now, true, out);
+}
+
+// device-output variant for the aggregation root (batch windows only)
+int sh_advance_time_device(sh_query* q, int64_t now, const sh_out** out) {
+    return advance_core(q, now, false, out);
 }
 
 extern "C" int sh_query_destroy(sh_query* q) {

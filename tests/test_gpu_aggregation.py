@@ -1,0 +1,137 @@
+"""GPU parity of `define aggregation ... every sec...year` (incremental roll-ups) against the CPU
+restatement: every duration's table, row for row (insertion order, bit-exact base values)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleAggregation
+from siddhi_amd import abi, synth
+from tests import kat_runner
+from tests.parity import split_batches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def tables(a, spec):
+    lo, hi = abi.DUR_NAMES[spec.durations[0]], abi.DUR_NAMES[spec.durations[1]]
+    return {d: abi.out_arrays(a.table_raw(d)) for d in range(lo, hi + 1)}
+
+
+def assert_tables_equal(gt, ot, label):
+    assert gt.keys() == ot.keys()
+    for d in gt:
+        g, o = gt[d], ot[d]
+        assert np.array_equal(g["keys"], o["keys"]), f"{label} dur {d}: rows differ ({g['keys'].shape} vs {o['keys'].shape})"
+        assert np.array_equal(g["ts"], o["ts"]), f"{label} dur {d}: timestamps differ"
+        assert np.array_equal(g["val_types"], o["val_types"]), f"{label} dur {d}: value types differ"
+        for b in range(len(o["val_types"])):
+            bad = np.nonzero(g["vals"][b] != o["vals"][b])[0]
+            assert bad.size == 0, f"{label} dur {d} base {b}: differs at rows {bad[:8]}"
+
+
+def drive(a, pushes):
+    for p in pushes:
+        if isinstance(p, tuple):
+            a.advance_time(p[1])
+        else:
+            a.push(p)
+
+
+def both(rt, spec, pushes, label, checkpoints=()):
+    """Run GPU and oracle; compare the tables after every push index in `checkpoints` and at the end."""
+    g = rt.GpuAggregation(spec)
+    o = OracleAggregation(spec)
+    n_rows = 0
+    for i, p in enumerate(pushes):
+        drive(g, [p])
+        drive(o, [p])
+        if i in checkpoints or i == len(pushes) - 1:
+            gt, ot = tables(g, spec), tables(o, spec)
+            assert_tables_equal(gt, ot, f"{label}@{i}")
+            n_rows += sum(len(t["ts"]) for t in ot.values())
+    g.close()
+    o.close()
+    return n_rows
+
+
+AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"]
+
+
+@pytest.mark.parametrize("case", AGG_KATS, ids=[c["name"] for c in AGG_KATS])
+def test_reference_aggregation_kat_on_gpu(rt, case):
+    schema, spec, dic, a = kat_runner.run_aggregation(case, rt.GpuAggregation)
+    dur = abi.DUR_NAMES[case["expect"]["table"]]
+    kat_runner.check_aggregation_table(case, spec, dic, a.table(dur))
+    # every duration identical to the oracle (tables drain on read, so run both afresh)
+    _, _, _, a = kat_runner.run_aggregation(case, rt.GpuAggregation)
+    _, _, _, o = kat_runner.run_aggregation(case, OracleAggregation)
+    assert_tables_equal(tables(a, spec), tables(o, spec), case["name"])
+
+
+C4_SCHEMA = abi.Schema.parse("k int, v double, ts long")
+
+
+def c4_spec(durations=("sec", "day"), ts="ts", keys=10_000, aggs=None):
+    aggs = aggs or [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")]
+    return abi.AggregationSpec(C4_SCHEMA, aggs, group_by=["k"], ts=ts, durations=durations, key_capacity=keys)
+
+
+@pytest.mark.parametrize("send_size", [1, 500])
+def test_c4_event_time_rollups(rt, send_size):
+    # 200k events, 2k keys, 5 events/ms -> 40 s of event time across minute boundaries
+    ts, cols = synth.keyed_stream(1_700_000_000_000 - 15_000, 200_000, 0xC4, 2_000, 5)
+    pushes = split_batches(C4_SCHEMA, ts, cols, [33_333, 100_000, 150_001], send_size)
+    pushes.append(("advance", int(ts[-1]) + 3_600_000 * 30))  # close sec ... day
+    n = both(rt, c4_spec(keys=2_000), pushes, "C4", checkpoints=(1, 2))
+    assert n > 0
+
+
+def test_processing_time_rollups_without_aggregate_by(rt):
+    ts, cols = synth.keyed_stream(1_600_000_000_000, 100_000, 7, 300, 2)
+    pushes = split_batches(C4_SCHEMA, ts, cols, [10_000, 60_000], 100)
+    pushes.append(("advance", int(ts[-1]) + 90_000_000))
+    both(rt, c4_spec(ts=None, durations=("sec", "hour"), keys=300), pushes, "proc-time")
+
+
+def test_late_events_and_long_gaps_to_month_and_year(rt):
+    # event time lags the clock by up to a minute (late rows land in older buckets), then idle gaps
+    rng = np.random.default_rng(11)
+    n = 60_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 20, n)).astype(np.int64)  # late Jan 2024
+    ext = clock - rng.integers(0, 60_000, n).astype(np.int64)
+    k = rng.integers(0, 50, n).astype(np.int32)
+    v = np.round(rng.normal(100, 30, n), 2)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("count", None), ("max", "v")], group_by=["k"], ts="ts",
+                               durations=("min", "year"), key_capacity=64)
+    b1 = abi.HostBatch(schema, clock[: n // 2], [k[: n // 2], v[: n // 2], ext[: n // 2]], 250)
+    b2 = abi.HostBatch(schema, clock[n // 2:], [k[n // 2:], v[n // 2:], ext[n // 2:]], 1)
+    pushes = [b1, ("advance", int(clock[n // 2 - 1]) + 40 * 86_400_000), b2,
+              ("advance", int(clock[-1]) + 400 * 86_400_000)]
+    both(rt, spec, pushes, "late+gaps", checkpoints=(0, 1, 2))
+
+
+def test_no_group_by_and_filter(rt):
+    ts, cols = synth.keyed_stream(1_650_000_000_000, 50_000, 3, 100, 3)
+    spec = abi.AggregationSpec(C4_SCHEMA, [("sum", "v"), ("min", "k"), ("count", None)], ts="ts",
+                               durations=("sec", "min"), filter=(">", "v", 0.5))
+    pushes = split_batches(C4_SCHEMA, ts, cols, [25_000], 7) + [("advance", int(ts[-1]) + 120_000)]
+    both(rt, spec, pushes, "nogroup")
+
+
+def test_long_sums_and_int_min_max(rt):
+    schema = abi.Schema.parse("k int, q long, p int, ts long")
+    rng = np.random.default_rng(5)
+    n = 80_000
+    ts = 1_690_000_000_000 + np.arange(n, dtype=np.int64) * 3
+    cols = [rng.integers(0, 700, n).astype(np.int32), rng.integers(-10**12, 10**12, n).astype(np.int64),
+            rng.integers(-1000, 1000, n).astype(np.int32), ts]
+    spec = abi.AggregationSpec(schema, [("sum", "q"), ("avg", "p"), ("min", "p"), ("max", "q")], group_by=["k"],
+                               ts="ts", durations=("sec", "hour"), key_capacity=700)
+    pushes = split_batches(schema, ts, cols, [40_000], 1000) + [("advance", int(ts[-1]) + 7_200_000)]
+    both(rt, spec, pushes, "longs")
