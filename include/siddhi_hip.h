@@ -207,7 +207,8 @@ int sh_query_destroy(sh_query* q);
 /* Replaces InputHandler.send(Event[]) -> filter -> window.process -> QuerySelector.process ->
  * OutputRateLimiter for every send in the batch. Host-memory batch (H2D included).          */
 int sh_push(sh_query* q, const sh_batch* batch, const sh_out** out);
-/* Same with device-resident columns (the HBM-resident hot path). *out is host memory.       */
+/* Same with device-resident columns (the HBM-resident hot path). flush_offsets/flush_clock of
+ * *out are host memory; ts/expired/keys/vals/nulls are device pointers (results stay in HBM). */
 int sh_push_device(sh_query* q, const sh_batch* batch, const sh_out** out);
 /* TIMER path: advance the playback clock to `now` without events (Scheduler.onTimeChange). */
 int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);

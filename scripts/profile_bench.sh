@@ -1,0 +1,19 @@
+#!/bin/bash
+# Bench + rocprofv3 evidence for one round, run on the GPU box from the repo root:
+#   scripts/profile_bench.sh <tag>
+# 1) the default bench line (with cpu_baseline), 2) kernel trace + stats, 3) FETCH_SIZE and
+# 4) WRITE_SIZE in separate passes (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2; never combined).
+set -o pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
+cat "$OUT/bench.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/kt.json" 2> "$OUT/kt.err" || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/fetch.json" 2> "$OUT/fetch.err" || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/write.json" 2> "$OUT/write.err" || exit $?
+echo profile done
