@@ -131,24 +131,64 @@ __device__ __forceinline__ u64 mix64(u64 z) {
     return z ^ (z >> 31);
 }
 
-// Open-addressing lookup-or-insert. The position is the group slot. A plain load that sees a
-// stale EMPTY (another CU inserted meanwhile) is corrected by the CAS, which reads the line at the
-// memory side; a non-EMPTY key never changes, so it can't be stale.
+// Home slot: Fibonacci (multiplicative) hashing, top log2(size) bits of key * 2^64/phi. Dense key
+// ranges (dictionary ids, small integers) land on distinct slots (three-gap theorem), so most
+// lookups take one probe; other keys are spread like any multiplicative hash.
+__device__ __forceinline__ u32 key_home(const KeyTable& kt, u64 key) {
+    return (u32)((key * 0x9E3779B97F4A7C15ull) >> kt.shift) & kt.mask;
+}
+
+// Open-addressing lookup-or-insert (linear probing). The position is the group slot. A plain load
+// that sees a stale EMPTY (another CU inserted meanwhile) is corrected by the CAS, which reads the
+// line at the memory side; a non-EMPTY key never changes, so it can't be stale.
+__device__ __forceinline__ bool probe_step(const KeyTable& kt, u64 key, u64 k, u32& h) {
+    if (k == key) return true;
+    if (k == kEmptyKey) {
+        u64 old = atomicCAS(&kt.keys[h], kEmptyKey, key);
+        if (old == kEmptyKey) { atomicAdd(kt.n_keys, 1u); return true; }
+        if (old == key) return true;
+    }
+    h = (h + 1) & kt.mask;
+    return false;
+}
+
 __device__ __forceinline__ u32 key_slot(const KeyTable& kt, u64 key) {
     if (key == kEmptyKey) return kt.mask + 1;
-    u32 h = (u32)mix64(key) & kt.mask;
-    for (u32 probe = 0; probe <= kt.mask; probe++) {
-        u64 k = kt.keys[h];
-        if (k == key) return h;
-        if (k == kEmptyKey) {
-            u64 old = atomicCAS(&kt.keys[h], kEmptyKey, key);
-            if (old == kEmptyKey) { atomicAdd(kt.n_keys, 1u); return h; }
-            if (old == key) return h;
-        }
-        h = (h + 1) & kt.mask;
-    }
+    u32 h = key_home(kt, key);
+    for (u32 probe = 0; probe <= kt.mask; probe++)
+        if (probe_step(kt, key, kt.keys[h], h)) return h;
     atomicExch(kt.overflow, 1);
     return 0;
+}
+
+// K independent lookups advanced together: each probe round issues the loads of every unresolved
+// lookup back to back, so their latencies overlap.
+template <int K>
+__device__ __forceinline__ void key_slots(const KeyTable& kt, const u64* key, const bool* valid, u32* out) {
+    u32 h[K];
+    bool done[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        done[i] = !valid[i] || key[i] == kEmptyKey;
+        if (valid[i] && key[i] == kEmptyKey) out[i] = kt.mask + 1;
+        h[i] = key_home(kt, key[i]);
+    }
+    for (u32 probe = 0; probe <= kt.mask; probe++) {
+        u64 k[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) k[i] = done[i] ? 0 : kt.keys[h[i]];
+        bool left = false;
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            if (done[i]) continue;
+            if (probe_step(kt, key[i], k[i], h[i])) { out[i] = h[i]; done[i] = true; }
+            left |= !done[i];
+        }
+        if (!left) return;
+    }
+    atomicExch(kt.overflow, 1);
+#pragma unroll
+    for (int i = 0; i < K; i++) if (!done[i]) out[i] = 0;
 }
 
 __device__ __forceinline__ u64 slot_key(const KeyTable& kt, u32 pos) {
@@ -189,6 +229,20 @@ __device__ __forceinline__ i64 block_excl_scan(i64 v, Op op, i64 identity, i64* 
     i64 excl = __shfl_up(incl, 1, 64);
     if (lane_id() == 0) excl = identity;
     return op(pre, excl);
+}
+
+// Sum scan for any workgroup size that is a multiple of 64 (up to 1024 threads).
+__device__ __forceinline__ i64 block_excl_scan_any(i64 v, i64* total) {
+    __shared__ i64 wsum_any[16];
+    i64 incl = wave_incl_scan(v, SumOp());
+    int w = threadIdx.x >> 6, nw = (int)(blockDim.x >> 6);
+    if (lane_id() == 63) wsum_any[w] = incl;
+    __syncthreads();
+    i64 pre = 0, tot = 0;
+    for (int i = 0; i < nw; i++) { if (i < w) pre += wsum_any[i]; tot += wsum_any[i]; }
+    __syncthreads();
+    if (total) *total = tot;
+    return pre + incl - v;
 }
 
 template <typename Op>

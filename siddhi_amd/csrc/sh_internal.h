@@ -18,6 +18,7 @@ constexpr int kBlock = 256;           // threads per workgroup (4 wave64)
 constexpr int kItems = 8;             // events per thread in the scan-type passes
 constexpr int kTile = kBlock * kItems;  // events per workgroup in the scan-type passes
 constexpr u64 kEmptyKey = 0x8000000000000001ull;  // open-addressing EMPTY sentinel
+constexpr u32 kNoPos = 0xFFFFFFFFu;              // event filtered out (no key slot)
 
 // Filter program (postfix), evaluated per event on device. Mirrors sh_filter_op.
 struct FilterOpD {
@@ -71,7 +72,7 @@ struct KeyPlan {
 struct KeyTable {
     u64* keys;
     u32 mask;
-    u32 pad;
+    u32 shift;        // 64 - log2(mask + 1): Fibonacci-hash shift
     u32* n_keys;      // distinct keys inserted
     int* overflow;    // set when probing exhausts the table
 };
@@ -134,32 +135,34 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
                         WinParams wp, PushInfo* info);
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk);
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos);
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
-                      const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const i64* ts, ColSet cols,
-                      FilterProg f, KeyPlan kp, KeyTable kt, AggPlan ap, RowTmp* rows, u64* row_vals,
+                      const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
+                      AggPlan ap, RowTmp* rows, u64* row_vals,
                       u32* row_counter, unsigned char* flags, u32* rowref, i64* seg_rows,
                       // partitioned source (P > 1)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
-                      const i64* part_off);
+                      const i64* seg_off);
+size_t aggregate_part_lds(int NL, int n_fields, int n_vcols);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
 void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
-                 const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
-                 const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                 unsigned char* out_nulls);
-void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt,
-                            AggPlan ap, i64 e_lo, i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre,
-                            u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap);
+                 u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
+                 i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
+                 u64* out_vals, unsigned char* out_nulls);
+void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
+                            i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
+                            u64* pend_vals, i64 pend_cap);
 // multisplit (partitioned aggregation, P > 1)
-void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const i64* ts, ColSet cols,
-                     FilterProg f, KeyPlan kp, KeyTable kt, int P, i64* counts, int nblk);
+void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+                     i64* counts, int nblk);
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt,
-                       AggPlan ap, int P, const i64* offsets, int nblk, u32* rec_pos, u32* rec_idx,
-                       u64* rec_vals, i64 rec_cap);
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
+                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
+void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
+                        const u32* new_pos, int P, const i64* counts, int nblk, i64* seg_off);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 }  // namespace shd

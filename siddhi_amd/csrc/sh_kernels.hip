@@ -16,17 +16,31 @@ namespace shd {
 // k_blockagg: per workgroup (kTile events, blocked kItems per thread) the number of passing events,
 // the max timestamp over send-last events and the first passing event.
 // ================================================================================================
+// Send bookkeeping of a thread's kItems consecutive events with one division: r = e % send_len.
+struct SendCursor {
+    i64 s, r;
+    __device__ __forceinline__ SendCursor(const WinParams& wp, i64 base) {
+        s = send_len(wp);
+        r = s == 1 ? 0 : base % s;
+    }
+    __device__ __forceinline__ bool last(const WinParams& wp, i64 e) const { return r == s - 1 || e == wp.N - 1; }
+    __device__ __forceinline__ i64 last_of(const WinParams& wp, i64 e) const { return min(e - r + s - 1, wp.N - 1); }
+    __device__ __forceinline__ void next() { if (++r == s) r = 0; }
+};
+
 __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                     WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     i64 cnt = 0, tl = INT64_MIN, first = INT64_MAX;
+    SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
             if (eval_filter(f, cols, e)) { cnt++; if (first == INT64_MAX) first = e; }
-            if (is_send_last(wp, e)) tl = max(tl, ts[e]);
+            if (sc.last(wp, e)) tl = max(tl, ts[e]);
         }
+        sc.next();
     }
     i64 c = block_reduce(cnt, SumOp(), 0);
     i64 t = block_reduce(tl, MaxOp(), INT64_MIN);
@@ -130,19 +144,53 @@ __device__ __forceinline__ i64 wfun(const WinParams& wp, i64 E0, int e0_valid, i
     return clock < E0 ? 0 : (clock - E0) / wp.T + 1;
 }
 
+// W of successive events with at most one division per window change: `lim` is the smallest pcb
+// (lengthBatch) or clock (timeBatch) at which W grows.
+struct WinCursor {
+    i64 W, lim;
+    __device__ __forceinline__ void set(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
+        W = wfun(wp, E0, e0v, pcb, clk);
+        if (wp.kind == SH_WIN_LENGTH_BATCH) lim = (W + 1) * wp.L - wp.n_pend;
+        else if (!e0v) lim = INT64_MAX;
+        else lim = E0 + W * wp.T;
+    }
+    __device__ __forceinline__ i64 at(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
+        i64 x = wp.kind == SH_WIN_LENGTH_BATCH ? pcb : clk;
+        if (x >= lim) set(wp, E0, e0v, pcb, clk);
+        return W;
+    }
+};
+
 __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const PushInfo* info, Bound* bounds, int max_bounds,
-                                                      int* n_bounds) {
+                                                      int* n_bounds, KeyPlan kp, KeyTable kt, u32* new_pos) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
+    i64 t[kItems];
     i64 cnt = 0, tl = INT64_MIN;
+    SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        pass[i] = e < wp.N && eval_filter(f, cols, e);
+        bool in = e < wp.N;
+        t[i] = in ? ts[e] : INT64_MIN;
+        pass[i] = in && eval_filter(f, cols, e);
         cnt += pass[i];
-        if (e < wp.N && is_send_last(wp, e)) tl = max(tl, ts[e]);
+        if (in && sc.last(wp, e)) tl = max(tl, t[i]);
+        sc.next();
+    }
+    // group-key slot of every passing event, looked up once for the whole pipeline
+    // (GroupByKeyGenerator.constructEventKey, QuerySelector.java:331-336)
+    {
+        u64 key[kItems];
+        u32 pos[kItems];
+#pragma unroll
+        for (int i = 0; i < kItems; i++) key[i] = pass[i] ? make_key(kp, cols, base + i) : 0;
+        key_slots<kItems>(kt, key, pass, pos);
+#pragma unroll
+        for (int i = 0; i < kItems; i++)
+            if (base + i < wp.N) new_pos[base + i] = pass[i] ? pos[i] : kNoPos;
     }
     i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x];
     i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
@@ -150,6 +198,8 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     const i64 E0 = info->E0;
     const int e0v = info->e0_valid;
     if (base >= wp.N) return;
+    const bool per_event = send_len(wp) == 1;
+    SendCursor sc2(wp, base);
     // previous event's window
     i64 Wprev, clock_prev;
     if (base == 0) {
@@ -159,17 +209,21 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         i64 ep = base - 1;
         bool pp = eval_filter(f, cols, ep);
         i64 pcb_prev = pcb - (pp ? 1 : 0);
-        i64 sl = send_len(wp);
-        if (ep / sl == base / sl) clock_prev = max(c0, max(pm, ts[send_last_of(wp, base)]));
+        // ep and base in one send: ep's clock is that send's clock; else it closed the previous send
+        if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
         else clock_prev = max(c0, pm);
         Wprev = wfun(wp, E0, e0v, pcb_prev, clock_prev);
     }
+    WinCursor wc;
+    wc.W = Wprev;
+    wc.lim = INT64_MIN;  // first event recomputes
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e >= wp.N) break;
-        i64 clk = max(c0, max(pm, ts[send_last_of(wp, e)]));
-        i64 W = wfun(wp, E0, e0v, pcb, clk);
+        i64 tsl = per_event ? t[i] : ts[sc2.last_of(wp, e)];
+        i64 clk = max(c0, max(pm, tsl));
+        i64 W = wc.at(wp, E0, e0v, pcb, clk);
         if (W > Wprev) {
             int k = atomicAdd(n_bounds, 1);
             if (k < max_bounds) {
@@ -181,15 +235,16 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         Wprev = W;
         clock_prev = clk;
         pcb += pass[i];
-        if (is_send_last(wp, e)) pm = max(pm, ts[e]);
+        if (sc2.last(wp, e)) pm = max(pm, t[i]);
+        sc2.next();
     }
 }
 
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk) {
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos) {
     hipLaunchKernelGGL(k_boundaries, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass_pre, blk_tl_pre,
-                       info, bounds, max_bounds, (int*)&((PushInfo*)info)->n_bounds);
+                       info, bounds, max_bounds, (int*)&((PushInfo*)info)->n_bounds, kp, kt, new_pos);
 }
 
 // ================================================================================================
@@ -209,16 +264,27 @@ struct AggLds {
     u32* owner;
 };
 
-__device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL, u32 li, u32 idx, const i64* v) {
+// value column j of an event held in registers (unrolled select: no dynamic register indexing)
+template <int V>
+__device__ __forceinline__ i64 pick(const i64 (&v)[V], int j) {
+    i64 x = v[0];
+#pragma unroll
+    for (int i = 1; i < V; i++) if (j == i) x = v[i];
+    return x;
+}
+
+template <int V>
+__device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL, u32 li, u32 idx, const i64 (&v)[V]) {
     u32 c = L.cnt[li];
     if (c == 0) L.first[li] = idx;
     L.cnt[li] = c + 1;
     L.last[li] = idx;
+#pragma unroll 1
     for (int a = 0; a < ap.n; a++) {
         int k = ap.kind[a];
         if (k == AK_COUNT) continue;
         u64* fp = L.fields + (size_t)ap.field[a] * NL + li;
-        i64 x = v[ap.vcol[a]];
+        i64 x = pick<V>(v, ap.vcol[a]);
         switch (k) {
             case AK_SUM_L: *fp = (u64)((c == 0 ? 0 : (i64)*fp) + x); break;  // SumAttributeAggregatorExecutor long: sum += data
             case AK_SUM_D:                                                // double: sum += data
@@ -240,90 +306,15 @@ __device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL
     }
 }
 
-template <bool PARTITIONED>
-__global__ __launch_bounds__(kBlock) void k_aggregate(const Segment* __restrict__ segs, int P, int logP, int NL,
-                                                     i64 n_pend, const u32* __restrict__ pend_pos,
-                                                     const u64* __restrict__ pend_vals, i64 pend_cap,
-                                                     const i64* __restrict__ ts, ColSet cols, FilterProg f,
-                                                     KeyPlan kp, KeyTable kt, AggPlan ap, RowTmp* rows,
-                                                     u64* row_vals, u32* row_counter, unsigned char* flags,
-                                                     u32* rowref, i64* seg_rows, const u32* __restrict__ rec_pos,
-                                                     const u32* __restrict__ rec_idx,
-                                                     const u64* __restrict__ rec_vals, i64 rec_cap,
-                                                     const i64* __restrict__ part_off) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    // static __shared__ of the scan helpers precede the dynamic region; realign it to 16 bytes
-    unsigned char* smem = (unsigned char*)(((uintptr_t)smem_raw + 15) & ~(uintptr_t)15);
-    AggLds L;
-    L.fields = (u64*)smem;
-    L.cnt = (u32*)(smem + (size_t)ap.n_fields * NL * 8);
-    L.first = L.cnt + NL;
-    L.last = L.first + NL;
-    L.owner = L.last + NL;
-    const int seg = blockIdx.x / P;
-    const int p = blockIdx.x % P;
-    for (int i = threadIdx.x; i < NL; i += kBlock) { L.cnt[i] = 0; L.owner[i] = 0; }
-    __syncthreads();
-
-    i64 lo = segs[seg].lo, hi = segs[seg].hi;
-    if (PARTITIONED) {
-        // binary search the partition's record list (sorted by combined index) for [lo, hi)
-        i64 a0 = part_off[p], a1 = part_off[p + 1];
-        i64 l = a0, r = a1;
-        while (l < r) { i64 m = (l + r) >> 1; if ((i64)rec_idx[m] < lo) l = m + 1; else r = m; }
-        i64 s0 = l;
-        l = s0; r = a1;
-        while (l < r) { i64 m = (l + r) >> 1; if ((i64)rec_idx[m] < hi) l = m + 1; else r = m; }
-        lo = s0; hi = l;
-    }
-    u32 round = 0;
-    for (i64 b = lo; b < hi; b += kBlock) {
-        i64 e = b + threadIdx.x;
-        bool pend = false;
-        u32 li = 0, idx = 0;
-        i64 v[SH_MAX_AGGS];
-        if (e < hi) {
-            if (PARTITIONED) {
-                u32 pos = rec_pos[e];
-                li = pos >> logP;
-                idx = rec_idx[e];
-                for (int j = 0; j < ap.n_vcols; j++) v[j] = (i64)rec_vals[(size_t)j * rec_cap + e];
-                pend = true;
-            } else if (e < n_pend) {
-                li = pend_pos[e] >> logP;
-                idx = (u32)e;
-                for (int j = 0; j < ap.n_vcols; j++) v[j] = (i64)pend_vals[(size_t)j * pend_cap + e];
-                pend = true;
-            } else {
-                i64 x = e - n_pend;
-                if (eval_filter(f, cols, x)) {
-                    u32 pos = key_slot(kt, make_key(kp, cols, x));
-                    li = pos >> logP;
-                    idx = (u32)e;
-                    for (int j = 0; j < ap.n_vcols; j++) v[j] = load_raw(cols, ap.vcol_src[j], x);
-                    pend = true;
-                }
-            }
-        }
-        // ordered conflict rounds: owner = max(round<<9 | (511 - lane)) picks the lowest lane per key
-        while (__syncthreads_or(pend)) {
-            round++;
-            u32 tag = (round << 9) | (511u - threadIdx.x);
-            if (pend) atomicMax(&L.owner[li], tag);
-            __syncthreads();
-            if (pend && L.owner[li] == tag) {
-                apply_event(ap, L, NL, li, idx, v);
-                pend = false;
-            }
-        }
-    }
-    __syncthreads();
-
-    // emit one row per touched key
+// Row emission shared by both variants: one row per touched local key (RowTmp + values), the
+// first-occurrence flag and the row reference at the key's first event.
+__device__ __forceinline__ void emit_rows(const AggPlan& ap, AggLds& L, int NL, int logP, int p, int seg,
+                                          RowTmp* rows, u64* row_vals, u32* row_counter, unsigned char* flags,
+                                          u32* rowref, i64* seg_rows) {
     int mine = 0;
-    for (int i = threadIdx.x; i < NL; i += kBlock) mine += L.cnt[i] > 0;
+    for (int i = threadIdx.x; i < NL; i += blockDim.x) mine += L.cnt[i] > 0;
     i64 tot;
-    i64 pre = block_excl_scan((i64)mine, SumOp(), 0, &tot);
+    i64 pre = block_excl_scan_any((i64)mine, &tot);
     __shared__ u32 base_row;
     if (threadIdx.x == 0) {
         base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
@@ -331,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(const Segment* __restrict_
     }
     __syncthreads();
     u32 r = base_row + (u32)pre;
-    for (int i = threadIdx.x; i < NL; i += kBlock) {
+    for (int i = threadIdx.x; i < NL; i += blockDim.x) {
         u32 c = L.cnt[i];
         if (!c) continue;
         RowTmp t;
@@ -340,6 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(const Segment* __restrict_
         t.last = L.last[i];
         t.pad = c;
         rows[r] = t;
+#pragma unroll 1
         for (int a = 0; a < ap.n; a++) {
             u64 out;
             int k = ap.kind[a];
@@ -357,21 +349,232 @@ __global__ __launch_bounds__(kBlock) void k_aggregate(const Segment* __restrict_
     }
 }
 
+__device__ __forceinline__ void lds_layout(unsigned char* smem_raw, const AggPlan& ap, int NL, AggLds& L) {
+    // realign by pointer arithmetic on the LDS base (an int->pointer cast would lose the address space)
+    unsigned char* smem = smem_raw + ((16u - ((unsigned)(size_t)smem_raw & 15u)) & 15u);
+    L.fields = (u64*)smem;
+    L.cnt = (u32*)(smem + (size_t)ap.n_fields * NL * 8);
+    L.first = L.cnt + NL;
+    L.last = L.first + NL;
+    L.owner = L.last + NL;
+}
+
+// Unpartitioned (P == 1, few keys): one workgroup per closed segment reads the events directly;
+// lanes that share a key resolve in ordered rounds (lowest lane first).
+__global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __restrict__ segs, int NL, i64 n_pend,
+                                                          const u32* __restrict__ pend_pos,
+                                                          const u64* __restrict__ pend_vals, i64 pend_cap,
+                                                          const u32* __restrict__ new_pos, ColSet cols, AggPlan ap,
+                                                          RowTmp* rows, u64* row_vals, u32* row_counter,
+                                                          unsigned char* flags, u32* rowref, i64* seg_rows) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    AggLds L;
+    lds_layout(smem_raw, ap, NL, L);
+    const int seg = blockIdx.x;
+    for (int i = threadIdx.x; i < NL; i += kBlock) { L.cnt[i] = 0; L.owner[i] = 0; }
+    __syncthreads();
+    i64 lo = segs[seg].lo, hi = segs[seg].hi;
+    u32 round = 0;
+    for (i64 b = lo; b < hi; b += kBlock) {
+        i64 e = b + threadIdx.x;
+        bool pend = false;
+        u32 li = 0, idx = (u32)e;
+        i64 v[SH_MAX_AGGS];
+        if (e < hi) {
+            if (e < n_pend) {
+                li = pend_pos[e];
+#pragma unroll
+                for (int j = 0; j < SH_MAX_AGGS; j++)
+                    if (j < ap.n_vcols) v[j] = (i64)pend_vals[(size_t)j * pend_cap + e];
+                pend = true;
+            } else {
+                i64 x = e - n_pend;
+                u32 pos = new_pos[x];
+                if (pos != kNoPos) {
+                    li = pos;
+#pragma unroll
+                    for (int j = 0; j < SH_MAX_AGGS; j++)
+                        if (j < ap.n_vcols) v[j] = load_raw(cols, ap.vcol_src[j], x);
+                    pend = true;
+                }
+            }
+        }
+        // ordered conflict rounds: owner = max(round<<9 | (511 - lane)) picks the lowest lane per key
+        while (__syncthreads_or(pend)) {
+            round++;
+            u32 tag = (round << 9) | (511u - threadIdx.x);
+            if (pend) atomicMax(&L.owner[li], tag);
+            __syncthreads();
+            if (pend && L.owner[li] == tag) {
+                apply_event(ap, L, NL, li, idx, v);
+                pend = false;
+            }
+        }
+    }
+    __syncthreads();
+    emit_rows(ap, L, NL, 0, 0, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
+}
+
+// Partitioned (P > 1): one workgroup of W waves per (closed segment, key partition). The partition's
+// record list (event order) is consumed in chunks of CH = 64*W*R records: the chunk is split stably
+// in LDS into W sub-lists by li % W, and wave w folds sub-list w into the keys it owns. Inside a
+// wave, lanes that hit the same key apply in lane (= event) order, one round per repeat; a wave's
+// LDS operations complete in program order, so per chunk only the split needs workgroup barriers.
+template <int W, int R, int V>
+__global__ __launch_bounds__(W * 64, 4) void k_aggregate_part(const Segment* __restrict__ segs, int P, int logP, int NL,
+                                                          AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter,
+                                                          unsigned char* flags, u32* rowref, i64* seg_rows,
+                                                          const u32* __restrict__ rec_pos,
+                                                          const u32* __restrict__ rec_idx,
+                                                          const u64* __restrict__ rec_vals, i64 rec_cap,
+                                                          const i64* __restrict__ seg_off, int key_bits) {
+    constexpr int CH = 64 * W * R;
+    constexpr int logW = W == 1 ? 0 : W == 2 ? 1 : W == 4 ? 2 : W == 8 ? 3 : 4;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    AggLds L;
+    lds_layout(smem_raw, ap, NL, L);
+    // staging after the key state (16-byte aligned)
+    unsigned char* stg0 = (unsigned char*)(L.owner + NL);
+    unsigned char* stg = stg0 + ((16u - ((unsigned)(size_t)stg0 & 15u)) & 15u);
+    u64* st_v = (u64*)stg;                           // [V][CH]
+    u32* st_li = (u32*)(st_v + (size_t)V * CH);      // [CH]
+    u32* st_idx = st_li + CH;                        // [CH]
+    u32* cnt = st_idx + CH;                          // [R*W][W]
+    u32* off = cnt + R * W * W;                      // [R*W][W]
+    u32* sub_start = off + R * W * W;                // [W + 1]
+
+    const int seg = blockIdx.x / P;
+    const int p = blockIdx.x % P;
+    for (int i = threadIdx.x; i < NL; i += W * 64) L.cnt[i] = 0;
+    // the (segment, partition) record range, from k_seg_offsets
+    const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    __syncthreads();
+
+    for (i64 c0 = lo; c0 < hi; c0 += CH) {
+        const int n = (int)min((i64)CH, hi - c0);
+        // (a) load R records per lane, in chunk order q = j*W + w
+        u32 li[R], idx[R], rk[R];
+        int sub[R];
+        i64 v[R][V];
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            int r = (j * W + w) * 64 + lane;
+            bool ok = r < n;
+            li[j] = ok ? (rec_pos[c0 + r] >> logP) : 0xFFFFFFFFu;
+            idx[j] = 0;
+#pragma unroll
+            for (int x = 0; x < V; x++) v[j][x] = 0;
+            if (ok) {
+                idx[j] = rec_idx[c0 + r];
+#pragma unroll
+                for (int x = 0; x < V; x++)
+                    if (x < ap.n_vcols) v[j][x] = (i64)rec_vals[(size_t)x * rec_cap + c0 + r];
+            }
+            sub[j] = ok ? (int)(li[j] & (W - 1)) : -1;
+            // (b) stable rank among this wave's lanes of the same sub-list, and per-sub counts
+            u64 peers = __ballot(ok);
+#pragma unroll
+            for (int bt = 0; bt < logW; bt++) {
+                bool bit = ok && ((li[j] >> bt) & 1);
+                u64 mb = __ballot(bit);
+                peers &= bit ? mb : ~mb;
+            }
+            rk[j] = (u32)__popcll(peers & lt_mask);
+#pragma unroll
+            for (int sb = 0; sb < W; sb++) {
+                u64 ms = __ballot(sub[j] == sb);
+                if (lane == sb) cnt[(j * W + w) * W + sb] = (u32)__popcll(ms);
+            }
+        }
+        __syncthreads();
+        // (c) offsets: sub-lists in sub order, each in chunk order
+        if (threadIdx.x < W) {
+            const int t = threadIdx.x;
+            u32 base = 0;
+            for (int sb = 0; sb < t; sb++)
+                for (int q = 0; q < R * W; q++) base += cnt[q * W + sb];
+            sub_start[t] = base;
+            u32 run = base;
+            for (int q = 0; q < R * W; q++) { off[q * W + t] = run; run += cnt[q * W + t]; }
+            if (t == W - 1) sub_start[W] = run;
+        }
+        __syncthreads();
+        // (d) scatter into the staging sub-lists
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            if (sub[j] < 0) continue;
+            u32 d = off[(j * W + w) * W + sub[j]] + rk[j];
+            st_li[d] = li[j];
+            st_idx[d] = idx[j];
+#pragma unroll
+            for (int x = 0; x < V; x++) if (x < ap.n_vcols) st_v[(size_t)x * CH + d] = (u64)v[j][x];
+        }
+        __syncthreads();
+        // (e) wave w folds its sub-list in order
+        const int s0 = (int)sub_start[w], s1 = (int)sub_start[w + 1];
+        for (int b = s0; b < s1; b += 64) {
+            int e = b + lane;
+            bool ok = e < s1;
+            u32 k = ok ? st_li[e] : 0;
+            u32 ix = ok ? st_idx[e] : 0;
+            i64 vv[V];
+#pragma unroll
+            for (int x = 0; x < V; x++) vv[x] = (ok && x < ap.n_vcols) ? (i64)st_v[(size_t)x * CH + e] : 0;
+            u64 peers = __ballot(ok);
+            for (int bt = logW; bt < key_bits; bt++) {
+                bool bit = ok && ((k >> bt) & 1);
+                u64 mb = __ballot(bit);
+                peers &= bit ? mb : ~mb;
+            }
+            u32 rank = ok ? (u32)__popcll(peers & lt_mask) : 0xFFFFFFFFu;
+            for (u32 r = 0;; r++) {
+                bool go = rank == r;
+                if (__ballot(go) == 0) break;
+                if (go) apply_event(ap, L, NL, k, ix, vv);
+            }
+        }
+    }
+    __syncthreads();
+    emit_rows(ap, L, NL, logP, p, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
+}
+
+// records per lane per chunk: keep R x V value registers <= 8
+constexpr int part_rounds(int V) { return V <= 2 ? 4 : V <= 4 ? 2 : 1; }
+
+size_t aggregate_part_lds(int NL, int n_fields, int n_vcols) {
+    n_vcols = n_vcols <= 1 ? 1 : n_vcols <= 2 ? 2 : n_vcols <= 4 ? 4 : 8;
+    const int W = 8, R = part_rounds(n_vcols), CH = 64 * W * R;
+    size_t state = (size_t)NL * (8 * n_fields + 16) + 16;
+    state = (state + 15) & ~(size_t)15;
+    return state + (size_t)CH * (8 * n_vcols + 8) + (size_t)R * W * W * 8 + (W + 1) * 4 + 32;
+}
+
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
-                      const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const i64* ts, ColSet cols,
-                      FilterProg f, KeyPlan kp, KeyTable kt, AggPlan ap, RowTmp* rows, u64* row_vals,
-                      u32* row_counter, unsigned char* flags, u32* rowref, i64* seg_rows, const u32* rec_pos,
-                      const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* part_off) {
+                      const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
+                      AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter, unsigned char* flags, u32* rowref,
+                      i64* seg_rows, const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
+                      const i64* seg_off) {
     size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
-    dim3 grid(nseg * P);
-    if (P > 1)
-        hipLaunchKernelGGL(k_aggregate<true>, grid, dim3(kBlock), lds, s, segs, P, logP, NL, n_pend, pend_pos,
-                           pend_vals, pend_cap, ts, cols, f, kp, kt, ap, rows, row_vals, row_counter, flags, rowref,
-                           seg_rows, rec_pos, rec_idx, rec_vals, rec_cap, part_off);
-    else
-        hipLaunchKernelGGL(k_aggregate<false>, grid, dim3(kBlock), lds, s, segs, P, logP, NL, n_pend, pend_pos,
-                           pend_vals, pend_cap, ts, cols, f, kp, kt, ap, rows, row_vals, row_counter, flags, rowref,
-                           seg_rows, rec_pos, rec_idx, rec_vals, rec_cap, part_off);
+    if (P > 1) {
+        int key_bits = 0;
+        while ((1 << key_bits) < NL) key_bits++;
+        lds = aggregate_part_lds(NL, ap.n_fields, ap.n_vcols);
+#define SH_AGG_PART(VV)                                                                                          \
+    hipLaunchKernelGGL((k_aggregate_part<8, part_rounds(VV), VV>), dim3(nseg * P), dim3(8 * 64), lds, s, segs, P, logP, NL, ap, \
+                       rows, row_vals, row_counter, flags, rowref, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap,  \
+                       seg_off, key_bits)
+        if (ap.n_vcols <= 1) SH_AGG_PART(1);
+        else if (ap.n_vcols <= 2) SH_AGG_PART(2);
+        else if (ap.n_vcols <= 4) SH_AGG_PART(4);
+        else SH_AGG_PART(8);
+#undef SH_AGG_PART
+    } else {
+        hipLaunchKernelGGL(k_aggregate_flat, dim3(nseg), dim3(kBlock), lds, s, segs, NL, n_pend, pend_pos, pend_vals,
+                           pend_cap, new_pos, cols, ap, rows, row_vals, row_counter, flags, rowref, seg_rows);
+    }
 }
 
 // ================================================================================================
@@ -413,12 +616,10 @@ void launch_scan_sum(hipStream_t s, i64* a, int n) {
     hipLaunchKernelGGL(k_scan_sum, dim3(1), dim3(1024), 0, s, a, n);
 }
 
-__global__ __launch_bounds__(kBlock) void k_emit(const unsigned char* __restrict__ flags, const u32* __restrict__ rowref,
-                                                i64 n, const i64* __restrict__ blk_pre, const RowTmp* __restrict__ rows,
-                                                const u64* __restrict__ row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
-                                                i64 n_pend, const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
-                                                i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                                                unsigned char* out_nulls) {
+// Rank of each flagged first occurrence -> perm[rank] = row (tile-local scan + tile prefix).
+__global__ __launch_bounds__(kBlock) void k_emit_perm(const unsigned char* __restrict__ flags,
+                                                     const u32* __restrict__ rowref, i64 n,
+                                                     const i64* __restrict__ blk_pre, u32* perm) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     unsigned char fl[kItems];
     i64 c = 0;
@@ -426,55 +627,67 @@ __global__ __launch_bounds__(kBlock) void k_emit(const unsigned char* __restrict
     for (int i = 0; i < kItems; i++) { fl[i] = base + i < n ? flags[base + i] : 0; c += fl[i]; }
     i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + blk_pre[blockIdx.x];
 #pragma unroll
-    for (int i = 0; i < kItems; i++) {
-        if (!fl[i]) continue;
-        u32 row = rowref[base + i];
-        RowTmp t = rows[row];
-        out_ts[r] = t.last < n_pend ? pend_ts[t.last] : ts[t.last - n_pend];
-        unpack_key(kp, slot_key(kt, t.pos), out_keys + r, out_cap);
-        for (int a = 0; a < n_aggs; a++) {
-            out_vals[(size_t)a * out_cap + r] = row_vals[(size_t)row * n_aggs + a];
-            out_nulls[(size_t)a * out_cap + r] = 0;
-        }
-        r++;
+    for (int i = 0; i < kItems; i++)
+        if (fl[i]) perm[r++] = rowref[base + i];
+}
+
+// One output row per thread, in output order: gather the row, its last event's timestamp and key.
+__global__ __launch_bounds__(kBlock) void k_emit_gather(const u32* __restrict__ perm, i64 n_rows,
+                                                       const RowTmp* __restrict__ rows,
+                                                       const u64* __restrict__ row_vals, int n_aggs, KeyTable kt,
+                                                       KeyPlan kp, i64 n_pend, const i64* __restrict__ pend_ts,
+                                                       const i64* __restrict__ ts, i64 out_cap, i64* out_ts,
+                                                       i64* out_keys, u64* out_vals, unsigned char* out_nulls) {
+    i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (o >= n_rows) return;
+    u32 row = perm[o];
+    RowTmp t = rows[row];
+    u64 k = slot_key(kt, t.pos);
+    out_ts[o] = t.last < n_pend ? pend_ts[t.last] : ts[t.last - n_pend];
+    unpack_key(kp, k, out_keys + o, out_cap);
+    for (int a = 0; a < n_aggs; a++) {
+        out_vals[(size_t)a * out_cap + o] = row_vals[(size_t)row * n_aggs + a];
+        out_nulls[(size_t)a * out_cap + o] = 0;
     }
 }
 
 void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
-                 const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
-                 const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                 unsigned char* out_nulls) {
-    hipLaunchKernelGGL(k_emit, dim3(nblk), dim3(kBlock), 0, s, flags, rowref, n, blk_pre, rows, row_vals, n_aggs,
-                       kt, kp, n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls);
+                 u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
+                 i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
+                 u64* out_vals, unsigned char* out_nulls) {
+    hipLaunchKernelGGL(k_emit_perm, dim3(nblk), dim3(kBlock), 0, s, flags, rowref, n, blk_pre, perm);
+    unsigned g = (unsigned)((n_rows + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_emit_gather, dim3(g), dim3(kBlock), 0, s, perm, n_rows, rows, row_vals, n_aggs, kt, kp,
+                       n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls);
 }
 
 // ================================================================================================
 // k_compact_pending: passing events of the open window [e_lo, N) appended to the pending buffer
 // (the window's queued events, LengthBatch WindowState.currentEventQueue / TimeBatch queue).
 // ================================================================================================
-__global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restrict__ ts, ColSet cols, FilterProg f,
-                                                           KeyPlan kp, KeyTable kt, AggPlan ap, i64 e_lo, i64 N,
-                                                           i64 pcb_lo, i64 dst_base, const i64* blk_pass_pre,
+__global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restrict__ ts, ColSet cols,
+                                                           const u32* __restrict__ new_pos, AggPlan ap, i64 e_lo,
+                                                           i64 N, i64 pcb_lo, i64 dst_base, const i64* blk_pass_pre,
                                                            int blk0, u32* pend_pos, i64* pend_ts, u64* pend_vals,
                                                            i64 pend_cap) {
     int blk = blk0 + blockIdx.x;
     i64 base = (i64)blk * kTile + (i64)threadIdx.x * kItems;
-    bool pass[kItems];
+    u32 pos[kItems];
     i64 cnt = 0;
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        pass[i] = e < N && eval_filter(f, cols, e);
-        cnt += pass[i];
+        pos[i] = e < N ? new_pos[e] : kNoPos;
+        cnt += pos[i] != kNoPos;
     }
     i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blk];
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        if (pass[i]) {
+        if (pos[i] != kNoPos) {
             if (e >= e_lo) {
                 i64 d = dst_base + (pcb - pcb_lo);
-                pend_pos[d] = key_slot(kt, make_key(kp, cols, e));
+                pend_pos[d] = pos[i];
                 pend_ts[d] = ts[e];
                 for (int j = 0; j < ap.n_vcols; j++) pend_vals[(size_t)j * pend_cap + d] = (u64)load_raw(cols, ap.vcol_src[j], e);
             }
@@ -483,13 +696,13 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
     }
 }
 
-void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt,
-                            AggPlan ap, i64 e_lo, i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre,
-                            u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap) {
+void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
+                            i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
+                            u64* pend_vals, i64 pend_cap) {
     if (e_lo >= N) return;
     int blk0 = (int)(e_lo / kTile);
     int blk1 = (int)((N + kTile - 1) / kTile);
-    hipLaunchKernelGGL(k_compact_pending, dim3(blk1 - blk0), dim3(kBlock), 0, s, ts, cols, f, kp, kt, ap, e_lo, N,
+    hipLaunchKernelGGL(k_compact_pending, dim3(blk1 - blk0), dim3(kBlock), 0, s, ts, cols, new_pos, ap, e_lo, N,
                        pcb_lo, base, blk_pass_pre, blk0, pend_pos, pend_ts, pend_vals, pend_cap);
 }
 
@@ -507,49 +720,56 @@ struct EvLoad {
     u32 pos;
 };
 
-__device__ __forceinline__ EvLoad load_pos(i64 e, i64 n_pend, const u32* pend_pos, const ColSet& cols,
-                                           const FilterProg& f, const KeyPlan& kp, const KeyTable& kt) {
-    EvLoad r{false, 0};
-    if (e < n_pend) { r.ok = true; r.pos = pend_pos[e]; return r; }
-    i64 x = e - n_pend;
-    if (eval_filter(f, cols, x)) { r.ok = true; r.pos = key_slot(kt, make_key(kp, cols, x)); }
-    return r;
+// combined index space: pending events [0, n_pend), then the push's events
+__device__ __forceinline__ EvLoad load_pos(i64 e, i64 n_pend, const u32* pend_pos, const u32* new_pos) {
+    u32 p = e < n_pend ? pend_pos[e] : new_pos[e - n_pend];
+    return EvLoad{p != kNoPos, p};
+}
+
+// XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin, so give each XCD a
+// contiguous run of tiles; a partition's consecutive record runs are then written through one L2.
+__device__ __forceinline__ int xcd_tile(int nblk) {
+    int per = (nblk + 7) >> 3;
+    return (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
 }
 
 __global__ __launch_bounds__(kBlock) void k_ms_count(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
-                                                    ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt, int P,
-                                                    i64* counts, int nblk) {
+                                                    const u32* __restrict__ new_pos, int P, i64* counts, int nblk) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
+    const int tile = xcd_tile(nblk);
+    if (tile >= nblk) return;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
     __syncthreads();
-    i64 t0 = lo + (i64)blockIdx.x * kTile;
+    i64 t0 = lo + (i64)tile * kTile;
     for (int r = 0; r < kItems; r++) {
         i64 e = t0 + (i64)r * kBlock + threadIdx.x;
         if (e < hi) {
-            EvLoad ev = load_pos(e, n_pend, pend_pos, cols, f, kp, kt);
+            EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
             if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)i * nblk + blockIdx.x] = hist[i];
+    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)i * nblk + tile] = hist[i];
 }
 
-void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const i64* ts, ColSet cols,
-                     FilterProg f, KeyPlan kp, KeyTable kt, int P, i64* counts, int nblk) {
-    (void)ts;
-    hipLaunchKernelGGL(k_ms_count, dim3(nblk), dim3(kBlock), P * 4, s, lo, hi, n_pend, pend_pos, cols, f, kp, kt, P,
-                       counts, nblk);
+void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+                     i64* counts, int nblk) {
+    int grid = ((nblk + 7) >> 3) * 8;
+    hipLaunchKernelGGL(k_ms_count, dim3(grid), dim3(kBlock), P * 4, s, lo, hi, n_pend, pend_pos, new_pos, P, counts,
+                       nblk);
 }
 
 // LDS: hist[P] (u32) | local_start[P] (u32) | running[P] (u32) | wave_cnt[4][P] (u32) |
 //      stage_pos[kTile] | stage_idx[kTile] | stage_p[kTile] | stage_vals[V][kTile] (u64)
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
-                                                      const u64* __restrict__ pend_vals, i64 pend_cap, ColSet cols,
-                                                      FilterProg f, KeyPlan kp, KeyTable kt, AggPlan ap, int P,
+                                                      const u64* __restrict__ pend_vals, i64 pend_cap,
+                                                      const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
                                                       const i64* __restrict__ offsets, int nblk, u32* rec_pos,
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
+    const int tile = xcd_tile(nblk);
+    if (tile >= nblk) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    unsigned char* sm = (unsigned char*)(((uintptr_t)smem_raw + 15) & ~(uintptr_t)15);
+    unsigned char* sm = smem_raw + ((16u - ((unsigned)(size_t)smem_raw & 15u)) & 15u);
     u64* stage_vals = (u64*)sm;
     u32* stage_pos = (u32*)(stage_vals + (size_t)ap.n_vcols * kTile);
     u32* stage_idx = stage_pos + kTile;
@@ -563,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         for (int w = 0; w < 4; w++) wave_cnt[w * P + i] = 0;
     }
     __syncthreads();
-    const i64 t0 = lo + (i64)blockIdx.x * kTile;
+    const i64 t0 = lo + (i64)tile * kTile;
     // pass 1: histogram of this tile
     u32 my_pos[kItems];
     bool my_ok[kItems];
@@ -572,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         i64 e = t0 + (i64)r * kBlock + threadIdx.x;
         my_ok[r] = false;
         if (e < hi) {
-            EvLoad ev = load_pos(e, n_pend, pend_pos, cols, f, kp, kt);
+            EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
             my_ok[r] = ev.ok;
             my_pos[r] = ev.pos;
             if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
@@ -635,7 +855,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     }
     for (u32 j = threadIdx.x; j < n_tile; j += kBlock) {
         u32 p = stage_p[j];
-        i64 dst = offsets[(i64)p * nblk + blockIdx.x] + (j - local_start[p]);
+        i64 dst = offsets[(i64)p * nblk + tile] + (j - local_start[p]);
         rec_pos[dst] = stage_pos[j];
         rec_idx[dst] = stage_idx[j];
         for (int v = 0; v < ap.n_vcols; v++) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
@@ -644,12 +864,12 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
 }
 
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const i64* ts, ColSet cols, FilterProg f, KeyPlan kp, KeyTable kt, AggPlan ap,
-                       int P, const i64* offsets, int nblk, u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
-    (void)ts;
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
+                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 12 + (size_t)P * 4 * 7 + 16;
-    hipLaunchKernelGGL(k_ms_scatter, dim3(nblk), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
-                       cols, f, kp, kt, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);
+    int grid = ((nblk + 7) >> 3) * 8;
+    hipLaunchKernelGGL(k_ms_scatter, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
+                       new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);
 }
 
 // three-phase exclusive scan for long arrays
@@ -686,6 +906,32 @@ __global__ void k_part_off(const i64* counts, int nblk, int P, i64* part_off) {
 
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off) {
     hipLaunchKernelGGL(k_part_off, dim3((P + 1 + 255) / 256), dim3(256), 0, s, counts, nblk, P, part_off);
+}
+
+// Record offset of every segment boundary in every partition's list: boundary b lies in tile
+// t = b / kTile; offset = (scanned count of p before tile t) + (p-records of tile t before b).
+__global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restrict__ segs, int nseg, i64 n_pend,
+                                                       const u32* __restrict__ pend_pos,
+                                                       const u32* __restrict__ new_pos, int P,
+                                                       const i64* __restrict__ counts, int nblk, i64* seg_off) {
+    extern __shared__ __attribute__((aligned(16))) u32 hist[];
+    const int k = blockIdx.x;
+    const i64 b = k < nseg ? segs[k].lo : segs[nseg - 1].hi;
+    const i64 t = b / kTile;
+    for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
+    __syncthreads();
+    for (i64 e = t * kTile + threadIdx.x; e < b; e += kBlock) {
+        EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
+        if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += kBlock) seg_off[(i64)k * P + p] = counts[(i64)p * nblk + t] + hist[p];
+}
+
+void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
+                        const u32* new_pos, int P, const i64* counts, int nblk, i64* seg_off) {
+    hipLaunchKernelGGL(k_seg_offsets, dim3(nseg + 1), dim3(kBlock), P * 4, s, segs, nseg, n_pend, pend_pos, new_pos, P,
+                       counts, nblk, seg_off);
 }
 
 // ---- key-table rebuild: the open window's keys move to a fresh table (drops dead keys / grows) ------

@@ -218,7 +218,9 @@ KeyTable KeyTableHost::dev() const {
     KeyTable kt;
     kt.keys = (u64*)keys.p;
     kt.mask = (u32)(size_ - 1);
-    kt.pad = 0;
+    int lg = 0;
+    while (((size_t)1 << lg) < size_) lg++;
+    kt.shift = (u32)(64 - lg);
     kt.n_keys = (u32*)ctrl.p;
     kt.overflow = (int*)((char*)ctrl.p + 8);
     return kt;

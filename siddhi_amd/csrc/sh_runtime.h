@@ -115,6 +115,7 @@ struct sh_query {
     DevBuf blk_pass, blk_tl, blk_first, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
         out_ts, out_keys, out_vals, out_nulls, out_expired, blk_cnt;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
+    DevBuf new_pos, perm, seg_off;  // key slot per event of the push (kNoPos = filtered out); output permutation
     PushInfo* h_info = nullptr;
     StagedBatch staged;
     OutHost out;

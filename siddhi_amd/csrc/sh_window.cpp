@@ -84,14 +84,19 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
 
 static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out);
 
-// key partitions: smallest power of two whose per-partition LDS state fits the budget
+// key partitions: smallest power of two whose per-partition LDS state (plus, when partitioned, the
+// record staging of k_aggregate_part) fits the budget that keeps two workgroups per CU
 static int size_partitions(sh_query* q) {
     const size_t budget = 80 * 1024;
-    size_t bpk = 16 + 8 * (size_t)q->ap.n_fields;
     size_t ts = q->kt.size_;
     int P = 1;
-    while (((ts / P) + 1) * bpk + 16 > budget && P < (1 << 14)) P <<= 1;
-    if (((ts / P) + 1) * bpk + 16 > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large");
+    auto need = [&](int p) {
+        int nl = (int)(ts / p) + 1;
+        return p == 1 ? (size_t)nl * (16 + 8 * (size_t)q->ap.n_fields) + 16
+                      : aggregate_part_lds(nl, q->ap.n_fields, q->ap.n_vcols);
+    };
+    while (need(P) > budget && P < (1 << 14)) P <<= 1;
+    if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large");
     q->P = P;
     q->logP = 0;
     while ((1 << q->logP) < P) q->logP++;
@@ -214,13 +219,18 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     int64_t rec_cap = 0;
     if (q->P > 1) {
         RCHK(run_multisplit(q, closed_hi, b, &rec_pos, &rec_idx, &rec_vals, &rec_cap));
+        RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
+        int nblk = (int)((closed_hi + kTile - 1) / kTile);
+        launch_seg_offsets(s, q->segs.as<Segment>(), nseg, q->n_pend, q->pend_pos.as<u32>(),
+                           b ? q->new_pos.as<u32>() : nullptr, q->P, q->ms_counts.as<int64_t>(), nblk,
+                           q->seg_off.as<int64_t>());
     }
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_aggregate(s, q->segs.as<Segment>(), nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(),
-                     q->pend_vals.as<u64>(), q->pend_cap, ts, cs, q->fp, q->kp, q->kt.dev(), q->ap,
+                     q->pend_vals.as<u64>(), q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap,
                      q->rows.as<RowTmp>(), q->row_vals.as<u64>(), q->counters.as<u32>(), q->flags.as<unsigned char>(),
                      q->rowref.as<u32>(), q->seg_rows.as<int64_t>(), rec_pos, rec_idx, rec_vals, rec_cap,
-                     q->part_off.as<int64_t>());
+                     q->seg_off.as<int64_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     std::vector<int64_t> seg_rows(nseg);
@@ -249,8 +259,10 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         RCHK(q->blk_cnt.reserve(nblk2 * 8, false));
         launch_count_flags(s, q->flags.as<unsigned char>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2);
         launch_scan_sum(s, q->blk_cnt.as<int64_t>(), nblk2);
+        RCHK(q->perm.reserve(cap * 4, false));
         launch_emit(s, q->flags.as<unsigned char>(), q->rowref.as<u32>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2,
-                    q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp, q->n_pend,
+                    q->perm.as<u32>(), n_rows, q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp,
+                    q->n_pend,
                     q->pend_ts.as<int64_t>(), ts, cap, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(),
                     q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>());
         HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
@@ -410,8 +422,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
                            b->ts, wp, q->info.as<PushInfo>());
         int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
         RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
+        RCHK(q->new_pos.reserve((size_t)N * 4, false));
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
-                          q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk);
+                          q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
+                          q->new_pos.as<u32>());
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
@@ -452,7 +466,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             new_pend = q->n_pend + info.total_pass;
         }
         RCHK(grow_pending(q, new_pend, dst_base));
-        launch_compact_pending(s, b->ts, cs, q->fp, q->kp, q->kt.dev(), q->ap, e_lo, N, pcb_lo, dst_base,
+        launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
                                q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                                q->pend_vals.as<u64>(), q->pend_cap);
         HIPCHK(hipGetLastError());
@@ -529,7 +543,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
                       &q->bounds, &q->segs, &q->seg_rows, &q->flags, &q->rowref, &q->rows, &q->row_vals,
                       &q->counters, &q->out_ts, &q->out_keys, &q->out_vals, &q->out_nulls, &q->out_expired,
                       &q->blk_cnt, &q->ms_counts, &q->ms_tmp, &q->rec_pos, &q->rec_idx, &q->rec_vals,
-                      &q->part_off};
+                      &q->part_off, &q->new_pos, &q->perm, &q->seg_off};
     for (DevBuf* bf : bufs) bf->release();
     for (auto& c : q->staged.cols) c.release();
     q->staged.ts.release();
@@ -555,7 +569,6 @@ int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32*
     ColSet cs{};
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
-    const int64_t* ts = b ? b->ts : nullptr;
     int nblk = (int)((closed_hi + kTile - 1) / kTile);
     int64_t ncnt = (int64_t)P * nblk;
     RCHK(q->ms_counts.reserve((ncnt + 1) * 8, false));
@@ -565,15 +578,15 @@ int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32*
     RCHK(q->rec_pos.reserve(cap * 4, false));
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
-    launch_ms_count(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), ts, cs, q->fp, q->kp, q->kt.dev(), P,
-                    q->ms_counts.as<int64_t>(), nblk);
+    const u32* np = b ? q->new_pos.as<u32>() : nullptr;
+    launch_ms_count(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<int64_t>(), nblk);
     // counts are laid out [p][blk]; one exclusive scan gives every (partition, block) its offset,
     // and partition p starts at offset[p * nblk]
     HIPCHK(hipMemsetAsync(q->ms_counts.as<int64_t>() + ncnt, 0, 8, s));
     launch_scan_sum_large(s, q->ms_counts.as<int64_t>(), ncnt + 1, q->ms_tmp.as<int64_t>());
-    launch_ms_scatter(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, ts, cs,
-                      q->fp, q->kp, q->kt.dev(), q->ap, P, q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(),
-                      q->rec_idx.as<u32>(), q->rec_vals.as<u64>(), cap);
+    launch_ms_scatter(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs,
+                      q->ap, P, q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
+                      q->rec_vals.as<u64>(), cap);
     // part_off[p] = counts[p * nblk] (exclusive); part_off[P] = total
     launch_part_off(s, q->ms_counts.as<int64_t>(), nblk, P, q->part_off.as<int64_t>());
     HIPCHK(hipGetLastError());
