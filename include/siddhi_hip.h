@@ -223,6 +223,60 @@ int sh_aggregation_advance_time(sh_aggregation* a, int64_t now);
 /* Rows added to the table of `duration` since the previous call for that duration. */
 int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out);
 
+/* ---- sharded ingest across G GPUs (one process per GPU) ---------------------
+ * Rank g of G holds slice g of every global micro-batch: a contiguous run of the global stream
+ * (rank order = stream order), cut at send boundaries (send_size >= 1). Group keys are re-sharded
+ * to owner = mix64(key) % G over an all-to-all that the CALLER performs (RCCL through
+ * torch.distributed, or any transport): the library only packs and consumes device buffers.
+ * The playback clock, nextEmitTime and the window of every event are global quantities
+ * (TimeBatchWindowProcessor.java:262-347, Scheduler.java:71-127); they are computed from the G
+ * slice summaries, which every rank all-gathers, so each owner reproduces the single-stream
+ * windows exactly. One global push is:
+ *   1. sh_shard_summarize(slice)                 -> sh_slice_summary      [caller: all-gather]
+ *   2. sh_shard_pack(all summaries, slice, buf)  -> per-owner byte counts + this slice's window
+ *                                                   starts                [caller: all-to-all the
+ *                                                   bytes, all-gather the sh_bound lists]
+ *   3. sh_shard_consume(received bytes, all bounds) -> this owner's flushes (its keys only) plus
+ *                                                   `order`: the global stream index of each row's
+ *                                                   first event, so merging the G outputs of a
+ *                                                   flush by `order` yields the single-stream row
+ *                                                   order of QuerySelector.processInBatchGroupBy.
+ * Supported: timeBatch group-by (not partitioned).                                          */
+typedef struct {
+    int64_t n;           /* events in the slice                                              */
+    int64_t n_pass;      /* events passing the filter                                        */
+    int64_t max_tl;      /* max timestamp over the slice's send-last events (INT64_MIN: none) */
+    int64_t first_clock; /* clock of the send of the slice's first passing event, without the
+                            clock carried in (INT64_MIN: no passing event)                    */
+} sh_slice_summary;
+
+typedef struct {
+    int64_t W;     /* window number that starts here                                         */
+    int64_t clock; /* playback clock of the send that opened it (the flush clock of W-1...)  */
+    int64_t gidx;  /* global stream index of the first event of window W                    */
+    int64_t pad;
+} sh_bound;
+
+typedef struct sh_shard sh_shard;
+int sh_shard_create(sh_ctx* ctx, const sh_query_desc* desc, int32_t rank, int32_t world, sh_shard** out);
+int sh_shard_destroy(sh_shard* s);
+/* Bytes per packed event record (depends on the query's value columns). */
+int sh_shard_record_bytes(sh_shard* s, int64_t* out);
+/* Phase 1 (device slice). */
+int sh_shard_summarize(sh_shard* s, const sh_batch* slice, sh_slice_summary* out);
+/* Phase 2: `all` = the G summaries in rank order; `send_buf` = caller-owned device buffer of at
+ * least slice.n * record_bytes; on return send_bytes[o] bytes for owner o lie contiguously in
+ * owner order; *bounds (host, valid until the next call) lists the windows starting in this slice. */
+int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_batch* slice, void* send_buf,
+                  int64_t send_cap, int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds);
+/* Phase 3: recv_buf = the G received blocks concatenated in source-rank order (device),
+ * recv_bytes[g] their sizes; all_bounds = every rank's bound list (any order). host_out selects
+ * host (1) or device (0) row arrays, as sh_push / sh_push_device. *order has n_rows entries. */
+int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, const sh_bound* all_bounds,
+                     int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order);
+/* TIMER path of the sharded query: every rank calls it with the same `now`. */
+int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out, const int64_t** order);
+
 /* Pinned host buffers for zero-copy packing of Event[] chunks (hipHostMalloc). */
 int sh_alloc_pinned(int64_t bytes, void** out);
 int sh_free_pinned(void* p);

@@ -77,6 +77,14 @@ class Out(C.Structure):
                 ("nulls", C.POINTER(C.c_uint8))]
 
 
+class SliceSummary(C.Structure):
+    _fields_ = [("n", C.c_int64), ("n_pass", C.c_int64), ("max_tl", C.c_int64), ("first_clock", C.c_int64)]
+
+
+class Bound(C.Structure):
+    _fields_ = [("W", C.c_int64), ("clock", C.c_int64), ("gidx", C.c_int64), ("pad", C.c_int64)]
+
+
 class Stats(C.Structure):
     _fields_ = [("push_ms", C.c_double), ("main_kernel_ms", C.c_double),
                 ("main_kernel_bytes", C.c_int64), ("events", C.c_int64)]
@@ -371,6 +379,17 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_query_stats.argtypes = [C.c_void_p, P(Stats)]
     lib.sh_last_error.restype = C.c_char_p
     lib.sh_abi_version.restype = C.c_int32
+    if hasattr(lib, "sh_shard_create"):
+        PI = P(C.c_int64)
+        lib.sh_shard_create.argtypes = [C.c_void_p, P(QueryDesc), C.c_int32, C.c_int32, P(C.c_void_p)]
+        lib.sh_shard_destroy.argtypes = [C.c_void_p]
+        lib.sh_shard_record_bytes.argtypes = [C.c_void_p, PI]
+        lib.sh_shard_summarize.argtypes = [C.c_void_p, P(Batch), P(SliceSummary)]
+        lib.sh_shard_pack.argtypes = [C.c_void_p, P(SliceSummary), P(Batch), C.c_void_p, C.c_int64, PI,
+                                      P(P(Bound)), PI]
+        lib.sh_shard_consume.argtypes = [C.c_void_p, C.c_void_p, PI, P(Bound), C.c_int64, C.c_int32,
+                                         P(P(Out)), P(PI)]
+        lib.sh_shard_advance_time.argtypes = [C.c_void_p, C.c_int64, C.c_int32, P(P(Out)), P(PI)]
 
 
 # every exported symbol include/siddhi_hip.h declares
@@ -379,4 +398,6 @@ ABI_SYMBOLS = [
     "sh_advance_time", "sh_aggregation_create", "sh_aggregation_destroy", "sh_aggregation_push",
     "sh_aggregation_push_device", "sh_aggregation_advance_time", "sh_aggregation_table",
     "sh_alloc_pinned", "sh_free_pinned", "sh_query_stats", "sh_last_error", "sh_abi_version",
+    "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
+    "sh_shard_consume", "sh_shard_advance_time",
 ]

@@ -265,4 +265,39 @@ __device__ __forceinline__ i64 send_last_of(const WinParams& wp, i64 e) {
     return l < wp.N - 1 ? l : wp.N - 1;
 }
 
+// Send bookkeeping of a thread's kItems consecutive events with one division: r = e % send_len.
+struct SendCursor {
+    i64 s, r;
+    __device__ __forceinline__ SendCursor(const WinParams& wp, i64 base) {
+        s = send_len(wp);
+        r = s == 1 ? 0 : base % s;
+    }
+    __device__ __forceinline__ bool last(const WinParams& wp, i64 e) const { return r == s - 1 || e == wp.N - 1; }
+    __device__ __forceinline__ i64 last_of(const WinParams& wp, i64 e) const { return min(e - r + s - 1, wp.N - 1); }
+    __device__ __forceinline__ void next() { if (++r == s) r = 0; }
+};
+
+__device__ __forceinline__ i64 wfun(const WinParams& wp, i64 E0, int e0_valid, i64 pcb, i64 clock) {
+    if (wp.kind == SH_WIN_LENGTH_BATCH) return (wp.n_pend + pcb) / wp.L;
+    if (!e0_valid) return wp.W_open;
+    return clock < E0 ? 0 : (clock - E0) / wp.T + 1;
+}
+
+// W of successive events with at most one division per window change: `lim` is the smallest pcb
+// (lengthBatch) or clock (timeBatch) at which W grows.
+struct WinCursor {
+    i64 W, lim;
+    __device__ __forceinline__ void set(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
+        W = wfun(wp, E0, e0v, pcb, clk);
+        if (wp.kind == SH_WIN_LENGTH_BATCH) lim = (W + 1) * wp.L - wp.n_pend;
+        else if (!e0v) lim = INT64_MAX;
+        else lim = E0 + W * wp.T;
+    }
+    __device__ __forceinline__ i64 at(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
+        i64 x = wp.kind == SH_WIN_LENGTH_BATCH ? pcb : clk;
+        if (x >= lim) set(wp, E0, e0v, pcb, clk);
+        return W;
+    }
+};
+
 }  // namespace shd

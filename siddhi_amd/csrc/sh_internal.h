@@ -92,6 +92,10 @@ struct WinParams {
     i64 n_pend;        // pending (open-window) events carried in
     i64 send_size;     // events per send (0 = one send)
     i64 N;             // new events in this push
+    const int* wcol;   // sharded owner: window of every event given (W_base + wcol[e]); else null
+    i64 W_base;
+    int want_first_clk;  // sharded summary: report PushInfo.first_clk
+    int pad2;
 };
 
 // Result of the block-aggregate scan (written by k_scan_blocks, read back by the host).
@@ -102,7 +106,8 @@ struct PushInfo {
     i64 E0;            // nextEmitTime after initialisation
     int e0_valid;
     int n_bounds;      // boundaries appended by k_boundaries
-    i64 pad[2];
+    i64 first_clk;     // clock of the first passing event's send, before the carried-in clock
+    i64 pad;
 };
 
 // A window boundary inside the push: first combined index of a new window.
@@ -149,10 +154,11 @@ void launch_scan_sum(hipStream_t s, i64* a, int n);
 void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
                  u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
                  i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
-                 u64* out_vals, unsigned char* out_nulls);
+                 u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
+                 i64* out_order);
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
-                            u64* pend_vals, i64 pend_cap);
+                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx);
 // multisplit (partitioned aggregation, P > 1)
 void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
                      i64* counts, int nblk);
@@ -164,5 +170,22 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
                         const u32* new_pos, int P, const i64* counts, int nblk, i64* seg_off);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
+
+// sharded ingest (sh_shard_kernels.hip)
+constexpr int kMaxShards = 16;
+void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
+                         const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code, i64* counts, Bound* bounds,
+                         int max_bounds, int* n_bounds);
+void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
+                       i64 N, int nblk, const i64* offsets, u64 gidx0, unsigned char* out, int rec_words);
+struct ColRoles {
+    int role[SH_MAX_COLS];  // -1 unused, 0..7 value slot, 16 + g group-key component g
+    int n;
+};
+struct ColPtrs {
+    u64* p[SH_MAX_COLS];
+};
+void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec_words, KeyPlan kp, ColRoles roles,
+                         i64* ts, ColPtrs cols, int* wcol, u64* gidx);
 
 }  // namespace shd

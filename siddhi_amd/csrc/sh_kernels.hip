@@ -16,18 +16,6 @@ namespace shd {
 // k_blockagg: per workgroup (kTile events, blocked kItems per thread) the number of passing events,
 // the max timestamp over send-last events and the first passing event.
 // ================================================================================================
-// Send bookkeeping of a thread's kItems consecutive events with one division: r = e % send_len.
-struct SendCursor {
-    i64 s, r;
-    __device__ __forceinline__ SendCursor(const WinParams& wp, i64 base) {
-        s = send_len(wp);
-        r = s == 1 ? 0 : base % s;
-    }
-    __device__ __forceinline__ bool last(const WinParams& wp, i64 e) const { return r == s - 1 || e == wp.N - 1; }
-    __device__ __forceinline__ i64 last_of(const WinParams& wp, i64 e) const { return min(e - r + s - 1, wp.N - 1); }
-    __device__ __forceinline__ void next() { if (++r == s) r = 0; }
-};
-
 __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                     WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
@@ -100,8 +88,10 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
         info->e0_valid = wp.e0_valid;
         info->E0 = wp.E0;
         info->n_bounds = 0;
-        if (wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && sh_min[0] != INT64_MAX) {
-            // clock of the send that carries the first passing event
+        info->first_clk = INT64_MIN;
+        const bool init_e0 = wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && !wp.wcol;
+        if (sh_min[0] != INT64_MAX && (init_e0 || wp.want_first_clk)) {
+            // clock of the send that carries the first passing event (before the carried-in clock)
             i64 e0 = sh_min[0];
             i64 sl = wp.send_size > 0 ? wp.send_size : wp.N;
             i64 start = (e0 / sl) * sl;
@@ -111,16 +101,19 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
             for (i64 e = (i64)b0 * kTile; e < start; e++)
                 if (is_send_last(wp, e)) pm = max(pm, ts[e]);
             i64 c = max(pm, ts[last]);
-            if (wp.clock_valid) c = max(c, wp.clock0);
-            i64 E0;
-            if (wp.has_start) {
-                i64 elapsed = (c - wp.start_time) % wp.T;  // Java % truncates like C++
-                E0 = c + (wp.T - elapsed);
-            } else {
-                E0 = c + wp.T;
+            info->first_clk = c;
+            if (init_e0) {
+                if (wp.clock_valid) c = max(c, wp.clock0);
+                i64 E0;
+                if (wp.has_start) {
+                    i64 elapsed = (c - wp.start_time) % wp.T;  // Java % truncates like C++
+                    E0 = c + (wp.T - elapsed);
+                } else {
+                    E0 = c + wp.T;
+                }
+                info->E0 = E0;
+                info->e0_valid = 1;
             }
-            info->E0 = E0;
-            info->e0_valid = 1;
         }
     }
 }
@@ -138,29 +131,6 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
 //                e's send. Due timers fire before the send is processed and catch up one period
 //                each (Scheduler.sendTimerEvents :171-209), so the window boundaries sit at E0 + kT.
 // ================================================================================================
-__device__ __forceinline__ i64 wfun(const WinParams& wp, i64 E0, int e0_valid, i64 pcb, i64 clock) {
-    if (wp.kind == SH_WIN_LENGTH_BATCH) return (wp.n_pend + pcb) / wp.L;
-    if (!e0_valid) return wp.W_open;
-    return clock < E0 ? 0 : (clock - E0) / wp.T + 1;
-}
-
-// W of successive events with at most one division per window change: `lim` is the smallest pcb
-// (lengthBatch) or clock (timeBatch) at which W grows.
-struct WinCursor {
-    i64 W, lim;
-    __device__ __forceinline__ void set(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
-        W = wfun(wp, E0, e0v, pcb, clk);
-        if (wp.kind == SH_WIN_LENGTH_BATCH) lim = (W + 1) * wp.L - wp.n_pend;
-        else if (!e0v) lim = INT64_MAX;
-        else lim = E0 + W * wp.T;
-    }
-    __device__ __forceinline__ i64 at(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {
-        i64 x = wp.kind == SH_WIN_LENGTH_BATCH ? pcb : clk;
-        if (x >= lim) set(wp, E0, e0v, pcb, clk);
-        return W;
-    }
-};
-
 __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const PushInfo* info, Bound* bounds, int max_bounds,
@@ -212,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         // ep and base in one send: ep's clock is that send's clock; else it closed the previous send
         if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
         else clock_prev = max(c0, pm);
-        Wprev = wfun(wp, E0, e0v, pcb_prev, clock_prev);
+        Wprev = wp.wcol ? wp.W_base + wp.wcol[ep] : wfun(wp, E0, e0v, pcb_prev, clock_prev);
     }
     WinCursor wc;
     wc.W = Wprev;
@@ -223,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         if (e >= wp.N) break;
         i64 tsl = per_event ? t[i] : ts[sc2.last_of(wp, e)];
         i64 clk = max(c0, max(pm, tsl));
-        i64 W = wc.at(wp, E0, e0v, pcb, clk);
+        i64 W = wp.wcol ? wp.W_base + wp.wcol[e] : wc.at(wp, E0, e0v, pcb, clk);
         if (W > Wprev) {
             int k = atomicAdd(n_bounds, 1);
             if (k < max_bounds) {
@@ -637,13 +607,16 @@ __global__ __launch_bounds__(kBlock) void k_emit_gather(const u32* __restrict__ 
                                                        const u64* __restrict__ row_vals, int n_aggs, KeyTable kt,
                                                        KeyPlan kp, i64 n_pend, const i64* __restrict__ pend_ts,
                                                        const i64* __restrict__ ts, i64 out_cap, i64* out_ts,
-                                                       i64* out_keys, u64* out_vals, unsigned char* out_nulls) {
+                                                       i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                                                       const u64* __restrict__ pend_gidx,
+                                                       const u64* __restrict__ new_gidx, i64* out_order) {
     i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (o >= n_rows) return;
     u32 row = perm[o];
     RowTmp t = rows[row];
     u64 k = slot_key(kt, t.pos);
     out_ts[o] = t.last < n_pend ? pend_ts[t.last] : ts[t.last - n_pend];
+    if (out_order) out_order[o] = (i64)(t.first < n_pend ? pend_gidx[t.first] : new_gidx[t.first - n_pend]);
     unpack_key(kp, k, out_keys + o, out_cap);
     for (int a = 0; a < n_aggs; a++) {
         out_vals[(size_t)a * out_cap + o] = row_vals[(size_t)row * n_aggs + a];
@@ -654,11 +627,13 @@ __global__ __launch_bounds__(kBlock) void k_emit_gather(const u32* __restrict__ 
 void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
                  u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
                  i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
-                 u64* out_vals, unsigned char* out_nulls) {
+                 u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
+                 i64* out_order) {
     hipLaunchKernelGGL(k_emit_perm, dim3(nblk), dim3(kBlock), 0, s, flags, rowref, n, blk_pre, perm);
     unsigned g = (unsigned)((n_rows + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_emit_gather, dim3(g), dim3(kBlock), 0, s, perm, n_rows, rows, row_vals, n_aggs, kt, kp,
-                       n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls);
+                       n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls, pend_gidx, new_gidx,
+                       out_order);
 }
 
 // ================================================================================================
@@ -669,7 +644,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
                                                            const u32* __restrict__ new_pos, AggPlan ap, i64 e_lo,
                                                            i64 N, i64 pcb_lo, i64 dst_base, const i64* blk_pass_pre,
                                                            int blk0, u32* pend_pos, i64* pend_ts, u64* pend_vals,
-                                                           i64 pend_cap) {
+                                                           i64 pend_cap, const u64* __restrict__ new_gidx,
+                                                           u64* pend_gidx) {
     int blk = blk0 + blockIdx.x;
     i64 base = (i64)blk * kTile + (i64)threadIdx.x * kItems;
     u32 pos[kItems];
@@ -690,6 +666,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
                 pend_pos[d] = pos[i];
                 pend_ts[d] = ts[e];
                 for (int j = 0; j < ap.n_vcols; j++) pend_vals[(size_t)j * pend_cap + d] = (u64)load_raw(cols, ap.vcol_src[j], e);
+                if (pend_gidx) pend_gidx[d] = new_gidx[e];
             }
             pcb++;
         }
@@ -698,12 +675,13 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
 
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
-                            u64* pend_vals, i64 pend_cap) {
+                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx) {
     if (e_lo >= N) return;
     int blk0 = (int)(e_lo / kTile);
     int blk1 = (int)((N + kTile - 1) / kTile);
     hipLaunchKernelGGL(k_compact_pending, dim3(blk1 - blk0), dim3(kBlock), 0, s, ts, cols, new_pos, ap, e_lo, N,
-                       pcb_lo, base, blk_pass_pre, blk0, pend_pos, pend_ts, pend_vals, pend_cap);
+                       pcb_lo, base, blk_pass_pre, blk0, pend_pos, pend_ts, pend_vals, pend_cap, new_gidx,
+                       pend_gidx);
 }
 
 }  // namespace shd

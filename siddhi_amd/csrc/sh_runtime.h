@@ -128,7 +128,24 @@ struct sh_query {
     std::vector<int64_t> flush_window;
     bool internal_keys = false;  // key plan set by an internal owner (aggregation root)
     size_t kt_min_size = 0;      // table size at creation (rebuilds never shrink below it)
+    // column widths as loaded by the kernels (the sharded owner reads 8-byte raw columns)
+    int32_t load_type[SH_MAX_COLS]{};
+    // sharded owner (sh_shard.cpp): windows given per event, flush clocks from the global
+    // window starts, global stream index carried per pending event and reported per row
+    bool given = false;
+    const int* given_wcol = nullptr;
+    const shd::u64* given_gidx = nullptr;
+    int64_t given_W_base = 0, given_W_end = 0;
+    std::vector<sh_bound> gbounds;  // this push's global window starts, sorted by gidx
+    DevBuf pend_gidx, out_order;
+    std::vector<int64_t> order_host;
 };
+
+// sharded owner helpers (sh_window.cpp)
+int64_t given_flush_clock(const sh_query* q, int64_t W);
+int query_push_given(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
+int query_close_given(sh_query* q, bool host_out, const sh_out** out);
+int query_advance(sh_query* q, int64_t now, bool host_out, const sh_out** out);
 
 // make room for `extra` new keys in a batch query's table (rebuild / grow; batch windows only)
 int query_reserve_keys(sh_query* q, int64_t extra);

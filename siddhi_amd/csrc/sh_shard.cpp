@@ -1,0 +1,366 @@
+// sh_shard.cpp — sharded ingest of a timeBatch group-by query across G GPUs (one process per GPU),
+// behind sh_shard_* (include/siddhi_hip.h). SURVEY.md §8e: the per-key aggregates are independent,
+// so keys are owned by GPU mix64(key) % G; three quantities are global and are reproduced here from
+// the all-gathered slice summaries:
+//   - the playback clock (InputHandler.send sets it per send, TimestampGeneratorImpl :77-122): the
+//     clock carried into slice g is the max over the clock before the push and slices < g;
+//   - nextEmitTime, initialised by the first send that reaches the window anywhere in the stream
+//     (TimeBatchWindowProcessor.process :266-276) — it is a processor field shared by all keys;
+//   - the window of every event and therefore every flush boundary and flush clock
+//     (TimeBatchWindowProcessor :278-340 with Scheduler.sendTimerEvents :171-209).
+// Output order inside a flush (first occurrence, QuerySelector.processInBatchGroupBy :315-374) is
+// global too: each owner reports the global stream index of every row's first event.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sh_internal.h"
+#include "sh_runtime.h"
+
+using namespace shd;
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+struct sh_shard {
+    sh_ctx* ctx = nullptr;
+    sh_query_desc d{};
+    int rank = 0, world = 1;
+    FilterProg fp{};
+    KeyPlan kp{};
+    AggPlan ap{};
+    int rec_words = 3;
+    sh_query* owner = nullptr;
+    // global stream state (identical on every rank)
+    bool clock_valid = false;
+    int64_t clock = 0;
+    bool e0_valid = false;
+    int64_t E0 = 0;
+    int64_t W = 0;        // window of the last event of the stream so far
+    uint64_t seq = 0;     // events of the stream so far (global index of the next event)
+    // the push in flight (pack -> consume)
+    bool packed = false;
+    int64_t cur_W_base = 0, cur_W_end = 0;
+    // ingest scratch
+    int64_t slice_n = -1;
+    DevBuf blk_pass, blk_tl, blk_first, info, code, counts, tmp, part_off, bounds;
+    PushInfo* h_info = nullptr;
+    std::vector<sh_bound> my_bounds;
+    // owner scratch
+    DevBuf u_ts, u_wcol, u_gidx, u_cols[SH_MAX_COLS];
+    ColRoles roles{};
+};
+
+static int64_t wfun_g(const sh_shard* s, int64_t clock) {
+    if (!s->e0_valid) return 0;
+    return clock < s->E0 ? 0 : (clock - s->E0) / s->d.window_param + 1;
+}
+
+extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank, int32_t world, sh_shard** out) {
+    if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_create: NULL argument");
+    if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
+        return sh_fail(SH_ERR_INVALID, "sh_shard_create: need 0 <= rank < world <= 16");
+    if (d->window != SH_WIN_TIME_BATCH)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch group-by queries");
+    if (d->partition_col >= 0) return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest of partitioned queries");
+    if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
+    sh_shard* s = new sh_shard();
+    s->ctx = ctx;
+    s->d = *d;
+    s->d.filter = nullptr;
+    s->rank = rank;
+    s->world = world;
+    int32_t vt[SH_MAX_AGGS];
+    int rc;
+    if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, s->fp)) ||
+        (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, s->ap, vt)) ||
+        (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, s->kp))) {
+        delete s;
+        return rc;
+    }
+    s->rec_words = 3 + s->ap.n_vcols;
+    // the owner runs the same query over the records it receives: no filter (applied at ingest),
+    // 8-byte raw columns, windows given per event
+    sh_query_desc od = *d;
+    od.n_filter_ops = 0;
+    od.filter = nullptr;
+    if ((rc = sh_query_create(ctx, &od, &s->owner))) { delete s; return rc; }
+    sh_query* q = s->owner;
+    q->given = true;
+    s->roles.n = d->n_cols;
+    for (int c = 0; c < d->n_cols; c++) {
+        int t = d->col_types[c];
+        q->load_type[c] = (t == SH_T_FLOAT || t == SH_T_DOUBLE) ? SH_T_DOUBLE : SH_T_LONG;
+        s->roles.role[c] = -1;
+        for (int g = 0; g < s->kp.n; g++) if (s->kp.col[g] == c) s->roles.role[c] = 16 + g;
+        for (int j = 0; j < s->ap.n_vcols; j++) if (s->ap.vcol_src[j] == c) s->roles.role[c] = j;
+    }
+    if (hipHostMalloc((void**)&s->h_info, sizeof(PushInfo), hipHostMallocDefault) != hipSuccess) {
+        sh_query_destroy(s->owner);
+        delete s;
+        return sh_fail(SH_ERR_OOM, "pinned alloc failed");
+    }
+    if ((rc = s->info.reserve(sizeof(PushInfo), false))) { sh_shard_destroy(s); return rc; }
+    *out = s;
+    return SH_OK;
+}
+
+extern "C" int sh_shard_destroy(sh_shard* s) {
+    if (!s) return SH_OK;
+    (void)hipStreamSynchronize(s->ctx->stream);
+    if (s->owner) sh_query_destroy(s->owner);
+    DevBuf* bufs[] = {&s->blk_pass, &s->blk_tl, &s->blk_first, &s->info, &s->code, &s->counts, &s->tmp,
+                      &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& c : s->u_cols) c.release();
+    if (s->h_info) (void)hipHostFree(s->h_info);
+    delete s;
+    return SH_OK;
+}
+
+extern "C" int sh_shard_record_bytes(sh_shard* s, int64_t* out) {
+    if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_record_bytes: NULL argument");
+    *out = 8 * (int64_t)s->rec_words;
+    return SH_OK;
+}
+
+static ColSet colset(const sh_shard* s, const sh_batch* b) {
+    ColSet cs{};
+    cs.n = s->d.n_cols;
+    for (int c = 0; c < s->d.n_cols; c++) { cs.type[c] = s->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    return cs;
+}
+
+// Phase 1: pass count, send clocks and the first passing send of the slice (k_blockagg + k_scan_blocks).
+extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summary* out) {
+    if (!s || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_summarize: NULL argument");
+    if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative slice size");
+    if (b->n > 0 && (b->send_size < 1 || !b->ts))
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded slices need send_size >= 1 (slices cut at send boundaries)");
+    *out = sh_slice_summary{b->n, 0, INT64_MIN, INT64_MIN};
+    s->slice_n = b->n;
+    if (b->n == 0) return SH_OK;
+    hipStream_t st = s->ctx->stream;
+    int nblk = (int)((b->n + kTile - 1) / kTile);
+    RCHK(s->blk_pass.reserve(nblk * 8, false));
+    RCHK(s->blk_tl.reserve(nblk * 8, false));
+    RCHK(s->blk_first.reserve(nblk * 8, false));
+    launch_blockagg(st, b->ts, colset(s, b), s->fp, b->n, b->send_size, s->blk_pass.as<int64_t>(),
+                    s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(), nblk);
+    WinParams wp{};
+    wp.kind = SH_WIN_LENGTH_BATCH;  // no nextEmitTime initialisation: that is a global decision
+    wp.N = b->n;
+    wp.send_size = b->send_size;
+    wp.want_first_clk = 1;
+    launch_scan_blocks(st, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(), nblk, b->ts,
+                       wp, s->info.as<PushInfo>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    out->n_pass = s->h_info->total_pass;
+    out->max_tl = s->h_info->max_tl;
+    out->first_clock = s->h_info->first_pass == INT64_MAX ? INT64_MIN : s->h_info->first_clk;
+    return SH_OK;
+}
+
+// Phase 2: global clock / nextEmitTime / windows from the G summaries, then the per-owner records.
+extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_batch* b, void* send_buf,
+                             int64_t send_cap, int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds) {
+    if (!s || !all || !b || !send_bytes || !bounds || !n_bounds)
+        return sh_fail(SH_ERR_INVALID, "sh_shard_pack: NULL argument");
+    if (s->slice_n != b->n || all[s->rank].n != b->n)
+        return sh_fail(SH_ERR_STATE, "sh_shard_pack: call sh_shard_summarize on the same slice first");
+    const int G = s->world;
+    const int64_t RB = 8 * (int64_t)s->rec_words;
+    if (b->n > 0 && (!send_buf || send_cap < b->n * RB))
+        return sh_fail(SH_ERR_INVALID, "sh_shard_pack: send buffer smaller than slice.n * record_bytes");
+    // clock carried into every slice; stream offset of every slice
+    std::vector<int64_t> cin(G), off(G);
+    int64_t c = s->clock_valid ? s->clock : INT64_MIN, o = 0;
+    for (int r = 0; r < G; r++) {
+        cin[r] = c;
+        off[r] = o;
+        c = std::max(c, all[r].max_tl);
+        o += all[r].n;
+    }
+    const int64_t clock_end = c, n_total = o;
+    if (s->seq + (uint64_t)n_total >= (1ull << 40)) return sh_fail(SH_ERR_UNSUPPORTED, "stream longer than 2^40 events");
+    // nextEmitTime: initialised by the first send that reaches the window (TimeBatch :266-276, 342-347)
+    if (!s->e0_valid) {
+        for (int r = 0; r < G; r++) {
+            if (all[r].n_pass == 0) continue;
+            int64_t ck = std::max(cin[r], all[r].first_clock);
+            const int64_t T = s->d.window_param;
+            s->E0 = s->d.has_start_time ? ck + (T - (ck - s->d.start_time) % T) : ck + T;
+            s->e0_valid = true;
+            break;
+        }
+    }
+    const int64_t W_start = s->W;
+    const int64_t W_end = std::max(W_start, wfun_g(s, clock_end));
+    if (W_end - W_start >= (1 << 23)) return sh_fail(SH_ERR_UNSUPPORTED, "more than 8M windows in one push");
+    s->cur_W_base = W_start;
+    s->cur_W_end = W_end;
+    s->my_bounds.clear();
+    for (int r = 0; r < G; r++) send_bytes[r] = 0;
+    const int64_t N = b->n;
+    if (N > 0) {
+        hipStream_t st = s->ctx->stream;
+        int nblk = (int)((N + kTile - 1) / kTile);
+        int64_t ncnt = (int64_t)G * nblk;
+        RCHK(s->code.reserve(N * 4, false));
+        RCHK(s->counts.reserve((ncnt + 1) * 8, false));
+        RCHK(s->tmp.reserve(((ncnt + kTile) / kTile + 16) * 8, false));
+        RCHK(s->part_off.reserve((G + 1) * 8, false));
+        int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
+        RCHK(s->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
+        HIPCHK(hipMemsetAsync(s->info.p, 0, sizeof(PushInfo), st));
+        WinParams wp{};
+        wp.kind = SH_WIN_TIME_BATCH;
+        wp.e0_valid = s->e0_valid;
+        wp.E0 = s->E0;
+        wp.T = s->d.window_param;
+        wp.clock_valid = cin[s->rank] != INT64_MIN;
+        wp.clock0 = cin[s->rank];
+        // window of the event before this slice: the last event of the slices before it
+        wp.W_open = (off[s->rank] > 0 && wp.clock_valid) ? std::max(W_start, wfun_g(s, cin[s->rank])) : W_start;
+        wp.W_base = W_start;
+        wp.N = N;
+        wp.send_size = b->send_size;
+        PushInfo* info = s->info.as<PushInfo>();
+        launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), info, s->kp, G, nblk,
+                            s->code.as<u32>(), s->counts.as<int64_t>(), s->bounds.as<Bound>(), max_bounds,
+                            &info->n_bounds);
+        HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
+        launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
+        launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->kp, s->ap, G, N, nblk,
+                          s->counts.as<int64_t>(), (u64)(s->seq + off[s->rank]), (unsigned char*)send_buf,
+                          s->rec_words);
+        launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        std::vector<int64_t> po(G + 1);
+        HIPCHK(hipMemcpyAsync(po.data(), s->part_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        int nb = s->h_info->n_bounds;
+        if (nb > max_bounds) return sh_fail(SH_ERR_UNSUPPORTED, "more than 4M windows started in one slice");
+        std::vector<Bound> bd(nb);
+        if (nb) {
+            HIPCHK(hipMemcpyAsync(bd.data(), s->bounds.p, nb * sizeof(Bound), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        for (const Bound& x : bd)
+            s->my_bounds.push_back(sh_bound{x.W, x.clock, (int64_t)s->seq + off[s->rank] + x.idx, 0});
+        std::sort(s->my_bounds.begin(), s->my_bounds.end(),
+                  [](const sh_bound& a, const sh_bound& c2) { return a.gidx < c2.gidx; });
+        for (int r = 0; r < G; r++) send_bytes[r] = (po[r + 1] - po[r]) * RB;
+    }
+    // commit the global stream state (every rank computes the same values)
+    if (clock_end != INT64_MIN) {
+        s->clock = clock_end;
+        s->clock_valid = true;
+    }
+    s->W = W_end;
+    s->seq += (uint64_t)n_total;
+    s->packed = true;
+    s->slice_n = -1;
+    *bounds = s->my_bounds.data();
+    *n_bounds = (int64_t)s->my_bounds.size();
+    return SH_OK;
+}
+
+static void sync_owner(sh_shard* s) {
+    sh_query* q = s->owner;
+    q->clock = s->clock;
+    q->clock_valid = s->clock_valid;
+    q->E0 = s->E0;
+    q->e0_valid = s->e0_valid;
+}
+
+static void set_order(sh_shard* s, bool host_out, const int64_t** order) {
+    if (!order) return;
+    sh_query* q = s->owner;
+    *order = host_out ? q->order_host.data() : q->out_order.as<int64_t>();
+}
+
+// Phase 3: the owner aggregates the records of its keys (event order preserved: sources are
+// concatenated in rank order and every source run is in stream order).
+extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, const sh_bound* all_bounds,
+                                int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order) {
+    if (!s || !recv_bytes || !out || (n_all_bounds > 0 && !all_bounds))
+        return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
+    if (!s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
+    s->packed = false;
+    const int64_t RB = 8 * (int64_t)s->rec_words;
+    int64_t bytes = 0;
+    for (int r = 0; r < s->world; r++) {
+        if (recv_bytes[r] < 0 || recv_bytes[r] % RB) return sh_fail(SH_ERR_INVALID, "received block not a whole number of records");
+        bytes += recv_bytes[r];
+    }
+    const int64_t M = bytes / RB;
+    if (M > 0 && !recv_buf) return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL receive buffer");
+    sh_query* q = s->owner;
+    q->gbounds.assign(all_bounds, all_bounds + n_all_bounds);
+    std::sort(q->gbounds.begin(), q->gbounds.end(), [](const sh_bound& a, const sh_bound& c) { return a.gidx < c.gidx; });
+    q->given_W_base = s->cur_W_base;
+    q->given_W_end = s->cur_W_end;
+    sync_owner(s);
+    if (M == 0) {
+        RCHK(query_close_given(q, host_out != 0, out));
+        set_order(s, host_out != 0, order);
+        return SH_OK;
+    }
+    hipStream_t st = s->ctx->stream;
+    RCHK(s->u_ts.reserve(M * 8, false));
+    RCHK(s->u_wcol.reserve(M * 4, false));
+    RCHK(s->u_gidx.reserve(M * 8, false));
+    ColPtrs cp{};
+    sh_batch b{};
+    b.n = M;
+    b.send_size = 1;
+    for (int c = 0; c < s->d.n_cols; c++) {
+        if (s->roles.role[c] < 0) continue;
+        RCHK(s->u_cols[c].reserve(M * 8, false));
+        cp.p[c] = s->u_cols[c].as<u64>();
+        b.cols[c] = cp.p[c];
+    }
+    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->kp, s->roles, s->u_ts.as<int64_t>(), cp,
+                        s->u_wcol.as<int>(), s->u_gidx.as<u64>());
+    HIPCHK(hipGetLastError());
+    b.ts = s->u_ts.as<int64_t>();
+    q->given_wcol = s->u_wcol.as<int>();
+    q->given_gidx = s->u_gidx.as<u64>();
+    int rc = query_push_given(q, &b, host_out != 0, out);
+    q->given_wcol = nullptr;
+    q->given_gidx = nullptr;
+    if (rc) return rc;
+    sync_owner(s);
+    set_order(s, host_out != 0, order);
+    return SH_OK;
+}
+
+extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out,
+                                     const int64_t** order) {
+    if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_advance_time: NULL argument");
+    if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");
+    sh_query* q = s->owner;
+    sync_owner(s);
+    RCHK(query_advance(q, now, host_out != 0, out));
+    if (!(s->clock_valid && now < s->clock)) {
+        s->clock = now;
+        s->clock_valid = true;
+        s->W = std::max(s->W, wfun_g(s, now));
+    }
+    set_order(s, host_out != 0, order);
+    return SH_OK;
+}

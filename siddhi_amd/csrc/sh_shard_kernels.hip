@@ -1,0 +1,186 @@
+// sh_shard_kernels.hip — gfx950 kernels of the sharded ingest: every rank holds a
+// contiguous slice of the global stream, assigns each event its GLOBAL window (the playback clock
+// and nextEmitTime are global, TimeBatchWindowProcessor.java:262-347) and re-keys it to the GPU that
+// owns its group key. The all-to-all itself is done by the caller over RCCL/xGMI.
+//
+//   k_shard_assign  window of every event (clock carried in from the slices before), owner =
+//                   mix64(key) % G, per-(owner, tile) histogram, window starts of the slice
+//   k_shard_pack    stable multisplit of the passing events into per-owner runs of AoS records
+//                   {key, ts, gidx | W << 40, values...} (event order kept inside every run)
+//   k_shard_unpack  received records -> SoA columns of the owner's pipeline (given-window mode)
+#include "sh_device.h"
+
+namespace shd {
+
+__device__ __forceinline__ u32 owner_of(u64 key, int G) { return (u32)(mix64(key ^ 0x5851F42D4C957F2Dull) % (u64)G); }
+
+// code of a passing event: (W - W_base) << 4 | owner; kNoPos when it is filtered out
+constexpr int kOwnerBits = 4;
+
+__global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__ ts, ColSet cols, FilterProg f,
+                                                        WinParams wp, const i64* __restrict__ blk_tl_pre, KeyPlan kp,
+                                                        int G, int nblk, u32* code, i64* counts, Bound* bounds,
+                                                        int max_bounds, int* n_bounds) {
+    __shared__ u32 hist[kMaxShards];
+    if (threadIdx.x < kMaxShards) hist[threadIdx.x] = 0;
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    bool pass[kItems];
+    i64 t[kItems];
+    i64 tl = INT64_MIN;
+    SendCursor sc(wp, base);
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        i64 e = base + i;
+        bool in = e < wp.N;
+        t[i] = in ? ts[e] : INT64_MIN;
+        pass[i] = in && eval_filter(f, cols, e);
+        if (in && sc.last(wp, e)) tl = max(tl, t[i]);
+        sc.next();
+    }
+    i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
+    const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
+    const i64 E0 = wp.E0;
+    const int e0v = wp.e0_valid;
+    if (base < wp.N) {
+        SendCursor sc2(wp, base);
+        i64 Wprev, clock_prev;
+        if (base == 0) {
+            Wprev = wp.W_open;
+            clock_prev = c0;
+        } else {
+            if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
+            else clock_prev = max(c0, pm);
+            Wprev = max(wp.W_open, wfun(wp, E0, e0v, 0, clock_prev));
+        }
+        WinCursor wc;
+        wc.W = Wprev;
+        wc.lim = INT64_MIN;
+#pragma unroll
+        for (int i = 0; i < kItems; i++) {
+            i64 e = base + i;
+            if (e >= wp.N) break;
+            i64 tsl = sc2.s == 1 ? t[i] : ts[sc2.last_of(wp, e)];
+            i64 clk = max(c0, max(pm, tsl));
+            i64 W = max(wp.W_open, wc.at(wp, E0, e0v, 0, clk));
+            if (W > Wprev) {
+                int k = atomicAdd(n_bounds, 1);
+                if (k < max_bounds) {
+                    Bound b;
+                    b.idx = e; b.W = W; b.clock = clk; b.clock_prev = clock_prev; b.pcb = 0; b.pad = 0;
+                    bounds[k] = b;
+                }
+            }
+            u32 c = kNoPos;
+            if (pass[i]) {
+                u32 o = owner_of(make_key(kp, cols, e), G);
+                c = ((u32)(W - wp.W_base) << kOwnerBits) | o;
+                atomicAdd(&hist[o], 1u);
+            }
+            code[e] = c;
+            Wprev = W;
+            clock_prev = clk;
+            if (sc2.last(wp, e)) pm = max(pm, t[i]);
+            sc2.next();
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < G) counts[(i64)threadIdx.x * nblk + blockIdx.x] = hist[threadIdx.x];
+}
+
+void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
+                         const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code, i64* counts, Bound* bounds,
+                         int max_bounds, int* n_bounds) {
+    (void)info;
+    hipLaunchKernelGGL(k_shard_assign, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_tl_pre, kp, G, nblk, code,
+                       counts, bounds, max_bounds, n_bounds);
+}
+
+// Stable multisplit by owner. Tile events are taken in kItems rounds of kBlock consecutive events;
+// inside a round, the rank of an event among the same owner's events is (waves before) + (lanes
+// before), so every owner's run keeps event order. offsets = exclusive scan of counts[o][tile].
+__global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* __restrict__ ts,
+                                                      const u32* __restrict__ code, KeyPlan kp, AggPlan ap, int G,
+                                                      i64 N, int nblk, const i64* __restrict__ offsets, u64 gidx0,
+                                                      u64* out, int rec_words) {
+    __shared__ u32 running[kMaxShards];
+    __shared__ u32 wave_cnt[kBlock / 64][kMaxShards];
+    const int tile = blockIdx.x;
+    if (threadIdx.x < kMaxShards) running[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    __syncthreads();
+    for (int r = 0; r < kItems; r++) {
+        const i64 e = (i64)tile * kTile + (i64)r * kBlock + threadIdx.x;
+        u32 c = e < N ? code[e] : kNoPos;
+        bool ok = c != kNoPos;
+        u32 o = ok ? (c & ((1u << kOwnerBits) - 1)) : 0;
+        u64 peers = __ballot(ok);
+#pragma unroll
+        for (int bt = 0; bt < kOwnerBits; bt++) {
+            bool bit = (o >> bt) & 1;
+            u64 m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        u32 lrank = (u32)__popcll(peers & lt_mask);
+        if (lane < G) wave_cnt[wave][lane] = 0;
+        __syncthreads();
+        if (ok && lrank == 0) wave_cnt[wave][o] = (u32)__popcll(peers);
+        __syncthreads();
+        if (ok) {
+            u32 before = running[o];
+            for (int w = 0; w < wave; w++) before += wave_cnt[w][o];
+            i64 dst = offsets[(i64)o * nblk + tile] + before + lrank;
+            u64* rec = out + dst * rec_words;
+            rec[0] = make_key(kp, cols, e);
+            rec[1] = (u64)ts[e];
+            rec[2] = (gidx0 + (u64)e) | ((u64)(c >> kOwnerBits) << 40);
+            for (int j = 0; j < ap.n_vcols; j++) rec[3 + j] = (u64)load_raw(cols, ap.vcol_src[j], e);
+        }
+        __syncthreads();
+        if (threadIdx.x < G) {
+            u32 add = 0;
+            for (int w = 0; w < kBlock / 64; w++) add += wave_cnt[w][threadIdx.x];
+            running[threadIdx.x] += add;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
+                       i64 N, int nblk, const i64* offsets, u64 gidx0, unsigned char* out, int rec_words) {
+    hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, kp, ap, G, N, nblk, offsets, gidx0,
+                       (u64*)out, rec_words);
+}
+
+// Received records -> the owner's SoA columns (8-byte raw form for every referenced column).
+// role[c]: -1 unused, 0..7 value slot, 16 + g group-key component g.
+__global__ __launch_bounds__(kBlock) void k_shard_unpack(const u64* __restrict__ rec, i64 M, int rec_words, KeyPlan kp,
+                                                        ColRoles roles, i64* ts, ColPtrs cols, int* wcol, u64* gidx) {
+    i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M) return;
+    const u64* r = rec + m * rec_words;
+    u64 key = r[0];
+    ts[m] = (i64)r[1];
+    u64 g = r[2];
+    gidx[m] = g & ((1ull << 40) - 1);
+    wcol[m] = (int)(g >> 40);
+    for (int c = 0; c < roles.n; c++) {
+        int role = roles.role[c];
+        if (role < 0) continue;
+        u64 v;
+        if (role < 16) v = r[3 + role];
+        else if (kp.n == 1) v = key;
+        else if (role == 16) v = (u64)(i64)(int)(u32)(key >> 32);
+        else v = (u64)(i64)(int)(u32)key;
+        cols.p[c][m] = v;
+    }
+}
+
+void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec_words, KeyPlan kp, ColRoles roles,
+                         i64* ts, ColPtrs cols, int* wcol, u64* gidx) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_shard_unpack, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (const u64*)rec,
+                       M, rec_words, kp, roles, ts, cols, wcol, gidx);
+}
+
+}  // namespace shd

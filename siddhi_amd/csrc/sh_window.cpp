@@ -62,12 +62,14 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
     if (need <= q->pend_cap) return SH_OK;
     int64_t ncap = std::max<int64_t>(need, q->pend_cap + q->pend_cap / 2);
     ncap = std::max<int64_t>(ncap, 4096);
-    DevBuf np, nt, nv;
+    DevBuf np, nt, nv, ng;
     RCHK(np.reserve(ncap * 4, false));
     RCHK(nt.reserve(ncap * 8, false));
     RCHK(nv.reserve(std::max(1, q->ap.n_vcols) * ncap * 8, false));
+    if (q->given) RCHK(ng.reserve(ncap * 8, false));
     hipStream_t s = q->ctx->stream;
     if (keep > 0) {
+        if (q->given) HIPCHK(hipMemcpyAsync(ng.p, q->pend_gidx.p, keep * 8, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(np.p, q->pend_pos.p, keep * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(nt.p, q->pend_ts.p, keep * 8, hipMemcpyDeviceToDevice, s));
         for (int j = 0; j < q->ap.n_vcols; j++)
@@ -75,9 +77,9 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
                                   hipMemcpyDeviceToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    q->pend_pos.release(); q->pend_ts.release(); q->pend_vals.release();
-    q->pend_pos = np; q->pend_ts = nt; q->pend_vals = nv;
-    np.p = nt.p = nv.p = nullptr;
+    q->pend_pos.release(); q->pend_ts.release(); q->pend_vals.release(); q->pend_gidx.release();
+    q->pend_pos = np; q->pend_ts = nt; q->pend_vals = nv; q->pend_gidx = ng;
+    np.p = nt.p = nv.p = ng.p = nullptr;
     q->pend_cap = ncap;
     return SH_OK;
 }
@@ -170,6 +172,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
     if ((rc = q->kt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
+    for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0;
     if (d->window == SH_WIN_TIME) {
         q->kind = 1;
@@ -199,7 +202,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     int64_t closed_hi = segs.back().hi;
     ColSet cs{};
     cs.n = q->d.n_cols;
-    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     const int64_t* ts = b ? b->ts : nullptr;
     // row capacity: per segment at most min(len, distinct keys)
     int64_t row_cap = 0;
@@ -255,6 +258,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         RCHK(q->out_vals.reserve(na * cap * 8, false));
         RCHK(q->out_nulls.reserve(na * cap, false));
         RCHK(q->out_expired.reserve(cap, false));
+        if (q->given) RCHK(q->out_order.reserve(cap * 8, false));
         int nblk2 = (int)((closed_hi + kTile - 1) / kTile);
         RCHK(q->blk_cnt.reserve(nblk2 * 8, false));
         launch_count_flags(s, q->flags.as<unsigned char>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2);
@@ -264,7 +268,9 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
                     q->perm.as<u32>(), n_rows, q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp,
                     q->n_pend,
                     q->pend_ts.as<int64_t>(), ts, cap, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(),
-                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>());
+                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>(),
+                    q->given ? q->pend_gidx.as<u64>() : nullptr, q->given && b ? q->given_gidx : nullptr,
+                    q->given ? q->out_order.as<int64_t>() : nullptr);
         HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
         HIPCHK(hipGetLastError());
         if (host_out) {
@@ -278,6 +284,11 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
             std::vector<uint64_t> v(na * n_rows);
             std::vector<uint8_t> nl(na * n_rows);
             if (nk) HIPCHK(hipMemcpyAsync(k.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+            if (q->given) {
+                size_t ob = q->order_host.size();
+                q->order_host.resize(ob + n_rows);
+                HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+            }
             HIPCHK(hipMemcpyAsync(v.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(nl.data(), q->out_nulls.p, na * n_rows, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
@@ -387,6 +398,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     q->dev_out = sh_out{};
     q->stats = sh_stats{};
     q->agg_bytes = 0;
+    q->order_host.clear();
     int64_t N = b->n;
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
@@ -397,7 +409,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     if (N > 0 && !(q->partitioned && !q->p0_known)) {
         ColSet cs{};
         cs.n = q->d.n_cols;
-        for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+        for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b->cols[c]; }
         int nblk = (int)((N + kTile - 1) / kTile);
         RCHK(q->blk_pass.reserve(nblk * 8, false));
         RCHK(q->blk_tl.reserve(nblk * 8, false));
@@ -416,6 +428,13 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         wp.n_pend = q->n_pend;
         wp.send_size = b->send_size;
         wp.N = N;
+        if (q->given) {
+            // sharded owner: windows were assigned from the global clock by the ingest ranks
+            wp.kind = SH_WIN_TIME_BATCH;
+            wp.e0_valid = 1;
+            wp.wcol = q->given_wcol;
+            wp.W_base = q->given_W_base;
+        }
         launch_blockagg(s, b->ts, cs, q->fp, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                         q->blk_first.as<int64_t>(), nblk);
         launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk,
@@ -437,28 +456,48 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             HIPCHK(hipStreamSynchronize(s));
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
-        q->e0_valid = info.e0_valid;
-        q->E0 = info.E0;
-        q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
-        q->clock_valid = true;
+        if (!q->given) {
+            q->e0_valid = info.e0_valid;
+            q->E0 = info.E0;
+            q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+            q->clock_valid = true;
+        }
         int64_t e_lo, pcb_lo, dst_base, new_pend;
-        if (!bounds.empty()) {
+        // sharded owner: the global clock closed every window below given_W_end during this push,
+        // including the one this owner's last events belong to (a timer flush, Scheduler.java:171-209)
+        const int64_t W_last = bounds.empty() ? q->W_open : bounds.back().W;
+        const bool close_all = q->given && q->given_W_end > W_last;
+        if (!bounds.empty() || close_all) {
             std::vector<Segment> segs;
             std::vector<int64_t> clocks, windows;
             int64_t lo = 0, wprev = q->W_open;
             for (auto& bd : bounds) {
                 segs.push_back(Segment{lo, bd.idx});
-                clocks.push_back(q->d.window == SH_WIN_LENGTH_BATCH ? bd.clock_prev : bd.clock);
+                clocks.push_back(q->given ? given_flush_clock(q, wprev)
+                                          : q->d.window == SH_WIN_LENGTH_BATCH ? bd.clock_prev : bd.clock);
                 windows.push_back(wprev);
                 lo = bd.idx;
                 wprev = bd.W;
             }
+            if (close_all) {
+                segs.push_back(Segment{lo, q->n_pend + N});
+                clocks.push_back(given_flush_clock(q, wprev));
+                windows.push_back(wprev);
+            }
             RCHK(run_closed(q, segs, clocks, windows, b, host_out));
-            e_lo = bounds.back().idx - q->n_pend;
-            pcb_lo = bounds.back().pcb;
-            dst_base = 0;
-            new_pend = info.total_pass - pcb_lo;
-            q->W_open = bounds.back().W;
+            if (close_all) {
+                e_lo = N;
+                pcb_lo = info.total_pass;
+                dst_base = 0;
+                new_pend = 0;
+                q->W_open = q->given_W_end;
+            } else {
+                e_lo = bounds.back().idx - q->n_pend;
+                pcb_lo = bounds.back().pcb;
+                dst_base = 0;
+                new_pend = info.total_pass - pcb_lo;
+                q->W_open = bounds.back().W;
+            }
         } else {
             e_lo = 0;
             pcb_lo = 0;
@@ -468,7 +507,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         RCHK(grow_pending(q, new_pend, dst_base));
         launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
                                q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
-                               q->pend_vals.as<u64>(), q->pend_cap);
+                               q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
+                               q->given ? q->pend_gidx.as<u64>() : nullptr);
         HIPCHK(hipGetLastError());
         q->n_pend = new_pend;
     }
@@ -502,6 +542,7 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
 
 static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** out) {
     q->out.reset();
+    q->order_host.clear();
     q->dev_flush_offsets.assign(1, 0);
     q->dev_flush_clock.clear();
     q->flush_window.clear();
@@ -543,7 +584,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
                       &q->bounds, &q->segs, &q->seg_rows, &q->flags, &q->rowref, &q->rows, &q->row_vals,
                       &q->counters, &q->out_ts, &q->out_keys, &q->out_vals, &q->out_nulls, &q->out_expired,
                       &q->blk_cnt, &q->ms_counts, &q->ms_tmp, &q->rec_pos, &q->rec_idx, &q->rec_vals,
-                      &q->part_off, &q->new_pos, &q->perm, &q->seg_off};
+                      &q->part_off, &q->new_pos, &q->perm, &q->seg_off, &q->pend_gidx, &q->out_order};
     for (DevBuf* bf : bufs) bf->release();
     for (auto& c : q->staged.cols) c.release();
     q->staged.ts.release();
@@ -568,7 +609,7 @@ int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32*
     int P = q->P;
     ColSet cs{};
     cs.n = q->d.n_cols;
-    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     int nblk = (int)((closed_hi + kTile - 1) / kTile);
     int64_t ncnt = (int64_t)P * nblk;
     RCHK(q->ms_counts.reserve((ncnt + 1) * 8, false));
@@ -595,4 +636,43 @@ int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32*
     *rec_vals = q->rec_vals.as<u64>();
     *rec_cap = cap;
     return SH_OK;
+}
+
+// ---- sharded owner (given windows) ------------------------------------------------------------
+// Flush clock of window W: the clock of the first global window start above W in this push (the
+// send whose clock fired the timer, Scheduler.sendTimerEvents :171-209).
+int64_t given_flush_clock(const sh_query* q, int64_t W) {
+    for (const sh_bound& b : q->gbounds)
+        if (b.W > W) return b.clock;
+    return q->clock;
+}
+
+int query_push_given(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    return push_core(q, b, host_out, out);
+}
+
+// No events reached this owner in the push: close its open window if the global clock moved past it.
+int query_close_given(sh_query* q, bool host_out, const sh_out** out) {
+    q->out.reset();
+    q->order_host.clear();
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    q->flush_window.clear();
+    q->dev_out = sh_out{};
+    q->stats = sh_stats{};
+    if (q->given_W_end > q->W_open) {
+        if (q->n_pend > 0) {
+            std::vector<Segment> segs{Segment{0, q->n_pend}};
+            std::vector<int64_t> clocks{given_flush_clock(q, q->W_open)}, windows{q->W_open};
+            RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
+            q->n_pend = 0;
+        }
+        q->W_open = q->given_W_end;
+    }
+    finish_out(q, host_out, out);
+    return SH_OK;
+}
+
+int query_advance(sh_query* q, int64_t now, bool host_out, const sh_out** out) {
+    return advance_core(q, now, host_out, out);
 }

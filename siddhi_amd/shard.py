@@ -1,0 +1,259 @@
+"""Sharded ingest of a timeBatch group-by query across G GPUs (one process per GPU).
+
+Rank g holds slice g of every global micro-batch (a contiguous, send-aligned run of the stream).
+The library (`sh_shard_*`, include/siddhi_hip.h) computes the global clock, nextEmitTime and the
+window of every event from the all-gathered slice summaries, packs every passing event into the
+run of the GPU that owns its key (owner = mix64(key) % G), and aggregates what an owner receives.
+The exchange itself is done here, over `torch.distributed` — RCCL over xGMI with the `nccl`
+backend on MI355X, or gloo on CPU tensors in the CPU tests:
+
+    summaries  all_gather_into_tensor   4 x int64 per rank
+    records    all_to_all_single        variable bytes per (source, owner), counts exchanged first
+    bounds     all_gather               the window starts of every slice (few per push)
+
+`LocalShards` runs G shards inside one process on one device, exchanging through device copies:
+the same protocol without a transport (used by the single-GPU parity tests).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .runtime import Context, _check, default_context, lib
+
+SUMMARY_WORDS = 4
+BOUND_WORDS = 4
+
+
+def _batch(n: int, ts_ptr: int, col_ptrs: Sequence[int], send_size: int) -> abi.Batch:
+    b = abi.Batch()
+    b.n = n
+    b.send_size = send_size
+    b.ts = ts_ptr
+    for i, p in enumerate(col_ptrs):
+        b.cols[i] = p
+    return b
+
+
+class ShardedQuery:
+    """Rank `rank` of `world` of a sharded `from S[cond]#window.timeBatch(T) select k, aggs group by k`."""
+
+    def __init__(self, spec: abi.QuerySpec, rank: int, world: int, ctx: Optional[Context] = None):
+        self.spec, self.rank, self.world = spec, rank, world
+        self.ctx = ctx or default_context()
+        self._desc = spec.desc()
+        self.h = C.c_void_p()
+        _check(lib().sh_shard_create(self.ctx.h, C.byref(self._desc), rank, world, C.byref(self.h)))
+        rb = C.c_int64()
+        _check(lib().sh_shard_record_bytes(self.h, C.byref(rb)))
+        self.record_bytes = rb.value
+
+    def summarize(self, n: int, ts_ptr: int, col_ptrs: Sequence[int], send_size: int) -> np.ndarray:
+        self._b = _batch(n, ts_ptr, col_ptrs, send_size)
+        s = abi.SliceSummary()
+        _check(lib().sh_shard_summarize(self.h, C.byref(self._b), C.byref(s)))
+        return np.array([s.n, s.n_pass, s.max_tl, s.first_clock], dtype=np.int64)
+
+    def pack(self, summaries: np.ndarray, send_ptr: int, send_cap: int) -> Tuple[np.ndarray, np.ndarray]:
+        """summaries: [world, 4] int64. Returns (send_bytes[world], bounds[k, 4] int64)."""
+        summ = np.ascontiguousarray(summaries, dtype=np.int64).reshape(self.world, SUMMARY_WORDS)
+        arr = (abi.SliceSummary * self.world)()
+        for r in range(self.world):
+            arr[r].n, arr[r].n_pass, arr[r].max_tl, arr[r].first_clock = (int(x) for x in summ[r])
+        sb = (C.c_int64 * self.world)()
+        bp = C.POINTER(abi.Bound)()
+        nb = C.c_int64()
+        _check(lib().sh_shard_pack(self.h, arr, C.byref(self._b), send_ptr, send_cap, sb, C.byref(bp), C.byref(nb)))
+        bounds = np.zeros((nb.value, BOUND_WORDS), dtype=np.int64)
+        for i in range(nb.value):
+            bounds[i] = (bp[i].W, bp[i].clock, bp[i].gidx, 0)
+        return np.frombuffer(sb, dtype=np.int64).copy(), bounds
+
+    def consume(self, recv_ptr: int, recv_bytes: Sequence[int], bounds: np.ndarray, host_out: bool = True):
+        """Returns (sh_out pointer, order pointer): rows of this owner's keys."""
+        rb = (C.c_int64 * self.world)(*[int(x) for x in recv_bytes])
+        bd = np.ascontiguousarray(bounds, dtype=np.int64).reshape(-1, BOUND_WORDS)
+        barr = (abi.Bound * max(1, len(bd)))()
+        for i, row in enumerate(bd):
+            barr[i].W, barr[i].clock, barr[i].gidx = int(row[0]), int(row[1]), int(row[2])
+        out = C.POINTER(abi.Out)()
+        order = C.POINTER(C.c_int64)()
+        _check(lib().sh_shard_consume(self.h, recv_ptr, rb, barr, len(bd), int(host_out), C.byref(out),
+                                      C.byref(order)))
+        return out, order
+
+    def advance_time(self, now: int, host_out: bool = True):
+        out = C.POINTER(abi.Out)()
+        order = C.POINTER(C.c_int64)()
+        _check(lib().sh_shard_advance_time(self.h, now, int(host_out), C.byref(out), C.byref(order)))
+        return out, order
+
+    def close(self):
+        if self.h:
+            lib().sh_shard_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_rows(out, order) -> dict:
+    """Host sh_out + order -> out_arrays dict with an 'order' column."""
+    d = abi.out_arrays(out)
+    n = int(out.contents.n_rows)
+    d["order"] = np.ctypeslib.as_array(order, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+    return d
+
+
+def merge_owner_outputs(parts: List[dict]) -> dict:
+    """Merge the G owners' outputs of one global push into the single-stream output: flushes are
+    matched by flush clock (every owner flushes window w at the same global clock) and rows inside a
+    flush are ordered by the global first-occurrence index."""
+    clocks = sorted(set(int(c) for p in parts for c in p["flush_clock"]))
+    fo, fc, rows = [0], [], []
+    for ck in clocks:
+        sel = []
+        for p in parts:
+            idx = np.nonzero(p["flush_clock"] == ck)[0]
+            for f in idx:
+                a, b = int(p["flush_offsets"][f]), int(p["flush_offsets"][f + 1])
+                sel.append((p, a, b))
+        order = np.concatenate([p["order"][a:b] for p, a, b in sel])
+        perm = np.argsort(order, kind="stable")
+        rows.append((sel, perm))
+        fo.append(fo[-1] + len(perm))
+        fc.append(ck)
+
+    def gather(key, axis_rows=True):
+        out = []
+        for sel, perm in rows:
+            if key in ("keys", "vals", "nulls"):
+                cat = np.concatenate([p[key][:, a:b] for p, a, b in sel], axis=1)
+                out.append(cat[:, perm])
+            else:
+                cat = np.concatenate([p[key][a:b] for p, a, b in sel])
+                out.append(cat[perm])
+        return out
+
+    ref = parts[0]
+    res = {"flush_offsets": np.array(fo, np.int64), "flush_clock": np.array(fc, np.int64),
+           "val_types": ref["val_types"]}
+    for key in ("ts", "expired", "order"):
+        g = gather(key)
+        res[key] = np.concatenate(g) if g else np.zeros(0, ref[key].dtype)
+    for key in ("keys", "vals", "nulls"):
+        g = gather(key)
+        res[key] = np.concatenate(g, axis=1) if g else np.zeros((ref[key].shape[0], 0), ref[key].dtype)
+    return res
+
+
+class LocalShards:
+    """G shards of one query in one process on one device; the exchange is a device copy.
+    Drives exactly the protocol a multi-process run drives over torch.distributed."""
+
+    def __init__(self, spec: abi.QuerySpec, world: int, ctx: Optional[Context] = None):
+        self.shards = [ShardedQuery(spec, r, world, ctx) for r in range(world)]
+        self.world = world
+
+    def push(self, slices, send_size: int, device) -> List[dict]:
+        """slices: per rank (ts tensor, [col tensors]) on `device`. Returns per-owner host outputs."""
+        import torch
+        G = self.world
+        summ = np.stack([s.summarize(int(ts.numel()), ts.data_ptr(), [c.data_ptr() for c in cols], send_size)
+                         for s, (ts, cols) in zip(self.shards, slices)])
+        sends, counts, bounds = [], [], []
+        for s, (ts, cols) in zip(self.shards, slices):
+            cap = max(1, int(ts.numel()) * s.record_bytes)
+            buf = torch.empty(cap, dtype=torch.uint8, device=device)
+            sb, bd = s.pack(summ, buf.data_ptr(), cap)
+            sends.append(buf)
+            counts.append(sb)
+            bounds.append(bd)
+        all_bounds = np.concatenate(bounds) if bounds else np.zeros((0, BOUND_WORDS), np.int64)
+        outs = []
+        for o, s in enumerate(self.shards):
+            blocks, rbytes = [], []
+            for g in range(G):
+                start = int(counts[g][:o].sum())
+                n = int(counts[g][o])
+                blocks.append(sends[g][start:start + n])
+                rbytes.append(n)
+            recv = torch.cat(blocks) if sum(rbytes) else torch.empty(1, dtype=torch.uint8, device=device)
+            out, order = s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=True)
+            outs.append(host_rows(out, order))
+        return outs
+
+    def advance_time(self, now: int) -> List[dict]:
+        return [host_rows(*s.advance_time(now, True)) for s in self.shards]
+
+    def close(self):
+        for s in self.shards:
+            s.close()
+
+
+class TorchExchange:
+    """The three collectives of a sharded push over torch.distributed (nccl = RCCL on ROCm, or gloo).
+    Tensors live on `device` (a CUDA device for nccl, CPU for gloo)."""
+
+    def __init__(self, device, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.device = device
+        self.world = dist.get_world_size(group)
+
+    def all_gather_summaries(self, summary: np.ndarray) -> np.ndarray:
+        import torch
+        t = torch.as_tensor(summary, dtype=torch.int64).to(self.device)
+        out = torch.empty(self.world * SUMMARY_WORDS, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return out.cpu().numpy().reshape(self.world, SUMMARY_WORDS)
+
+    def all_to_all(self, send, send_bytes: np.ndarray):
+        """send: uint8 tensor holding the per-owner runs back to back. Returns (recv tensor, recv_bytes)."""
+        import torch
+        sc = torch.as_tensor(np.asarray(send_bytes, dtype=np.int64)).to(self.device)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc, group=self.group)
+        recv_bytes = rc.cpu().numpy()
+        total = int(recv_bytes.sum())
+        recv = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
+        used = int(np.asarray(send_bytes).sum())
+        self.dist.all_to_all_single(recv[:total], send[:used], [int(x) for x in recv_bytes],
+                                    [int(x) for x in send_bytes], group=self.group)
+        return recv, recv_bytes
+
+    def all_gather_bounds(self, bounds: np.ndarray) -> np.ndarray:
+        import torch
+        n = torch.tensor([len(bounds)], dtype=torch.int64, device=self.device)
+        ns = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(ns, n, group=self.group)
+        counts = ns.cpu().numpy()
+        mx = int(counts.max())
+        if mx == 0:
+            return np.zeros((0, BOUND_WORDS), np.int64)
+        pad = np.zeros((mx, BOUND_WORDS), np.int64)
+        pad[:len(bounds)] = bounds
+        t = torch.as_tensor(pad).to(self.device)
+        out = torch.empty(self.world * mx * BOUND_WORDS, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t.reshape(-1), group=self.group)
+        allb = out.cpu().numpy().reshape(self.world, mx, BOUND_WORDS)
+        return np.concatenate([allb[r, :counts[r]] for r in range(self.world)])
+
+
+def distributed_push(q: ShardedQuery, ex: TorchExchange, n: int, ts_ptr: int, col_ptrs: Sequence[int],
+                     send_size: int, send_buf, host_out: bool = False):
+    """One global push on this rank: summarize -> all-gather -> pack -> all-to-all + all-gather ->
+    consume. send_buf: uint8 device tensor of >= n * record_bytes bytes."""
+    summ = q.summarize(n, ts_ptr, col_ptrs, send_size)
+    all_summ = ex.all_gather_summaries(summ)
+    send_bytes, bounds = q.pack(all_summ, send_buf.data_ptr(), int(send_buf.numel()))
+    recv, recv_bytes = ex.all_to_all(send_buf, send_bytes)
+    all_bounds = ex.all_gather_bounds(bounds)
+    return q.consume(recv.data_ptr(), recv_bytes, all_bounds, host_out)

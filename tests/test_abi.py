@@ -39,12 +39,14 @@ def test_struct_layout_matches_c(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "siddhi_hip.h"\n'
                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(sh_filter_op), sizeof(sh_query_desc),'
                    ' sizeof(sh_aggregation_desc), sizeof(sh_batch), sizeof(sh_out), sizeof(sh_stats),'
-                   ' offsetof(sh_query_desc, key_capacity), offsetof(sh_out, nulls));return 0;}\n')
+                   ' offsetof(sh_query_desc, key_capacity), offsetof(sh_out, nulls));'
+                   'printf("%zu %zu\\n", sizeof(sh_slice_summary), sizeof(sh_bound));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     want = [C.sizeof(abi.FilterOp), C.sizeof(abi.QueryDesc), C.sizeof(abi.AggregationDesc), C.sizeof(abi.Batch),
-            C.sizeof(abi.Out), C.sizeof(abi.Stats), abi.QueryDesc.key_capacity.offset, abi.Out.nulls.offset]
+            C.sizeof(abi.Out), C.sizeof(abi.Stats), abi.QueryDesc.key_capacity.offset, abi.Out.nulls.offset,
+            C.sizeof(abi.SliceSummary), C.sizeof(abi.Bound)]
     assert got == want
 
 

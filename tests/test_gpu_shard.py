@@ -1,0 +1,103 @@
+"""GPU parity of the sharded ingest: G shards of a timeBatch group-by query — each
+holding a slice of every global push, re-keying its events to the owner GPU — must together emit
+exactly what the single-stream oracle emits for the whole stream: same flushes, flush clocks, rows,
+row order (merged by the global first-occurrence index), timestamps and bit-identical values.
+
+The G shards run in one process on one device and exchange through device copies (LocalShards);
+the multi-process transport (torch.distributed all-to-all) carries the same bytes."""
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleQuery
+from siddhi_amd import abi, synth
+from tests.parity import assert_same, run_pushes
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = abi.Schema.parse("k int, v double, ts long")
+
+
+def spec(keys, filt=None, start=None, aggs=None, group_by=("k",), schema=SCHEMA):
+    return abi.QuerySpec(schema, "timeBatch", 1000, group_by=list(group_by),
+                         aggs=aggs or [("count", None), ("min", "v"), ("max", "v"), ("avg", "v")],
+                         filter=filt, start_time=start, key_capacity=keys)
+
+
+def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
+    """pushes: list of (ts, cols) numpy global pushes; each is cut into `world` send-aligned slices."""
+    import torch
+    from siddhi_amd.shard import LocalShards, merge_owner_outputs
+    dev = torch.device("cuda", 0)
+    ls = LocalShards(sp, world)
+    parts = []
+    for pi, (ts, cols) in enumerate(pushes):
+        n = len(ts)
+        units = (n + send_size - 1) // send_size
+        cuts = sorted(min(n, int(units * f) * send_size) for f in cut_fracs[pi % len(cut_fracs)])
+        edges = [0] + cuts + [n]
+        slices = []
+        for g in range(world):
+            a, b = edges[g], edges[g + 1]
+            slices.append((torch.from_numpy(np.ascontiguousarray(ts[a:b])).to(dev),
+                           [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in cols]))
+        parts.append(merge_owner_outputs(ls.push(slices, send_size, dev)))
+    if advance is not None:
+        parts.append(merge_owner_outputs(ls.advance_time(advance)))
+    ls.close()
+    return abi.concat_arrays(parts)
+
+
+def run_oracle(sp, pushes, send_size, advance=None):
+    o = OracleQuery(sp)
+    bl = [abi.HostBatch(sp.schema, ts, cols, send_size) for ts, cols in pushes]
+    if advance is not None:
+        bl.append(("advance", advance))
+    out = run_pushes(o, bl)
+    o.close()
+    return out
+
+
+def stream_pushes(n, sizes, seed, keys, per_ms, quantized=False):
+    ts, cols = synth.keyed_stream(0, n, seed, keys, per_ms, quantized)
+    out, a = [], 0
+    for s in sizes:
+        out.append((ts[a:a + s], [c[a:a + s] for c in cols]))
+        a += s
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_c2_matches_single_stream(world):
+    sp = spec(20_000)
+    pushes = stream_pushes(600_000, [150_000, 1, 249_999, 200_000], 0xC2, 20_000, 100)
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.1 * (g + 1) for g in range(world - 1)]]
+    adv = int(pushes[-1][0][-1]) + 5000
+    got = run_sharded(sp, world, pushes, 1, fr, advance=adv)
+    ref = run_oracle(sp, pushes, 1, advance=adv)
+    assert ref["flush_offsets"].size > 5
+    assert_same(got, ref, label=f"sharded x{world}")
+
+
+def test_sharded_filter_send_chunks_start_time():
+    sp = spec(5_000, filt=(">", "v", 150.0), start=137)
+    pushes = stream_pushes(300_000, [100_000, 200_000], 0xC5, 5_000, 50)
+    fr = [[0.25, 0.5, 0.75], [0.05, 0.06, 0.9]]
+    got = run_sharded(sp, 4, pushes, 100, fr, advance=int(pushes[-1][0][-1]) + 10_000)
+    ref = run_oracle(sp, pushes, 100, advance=int(pushes[-1][0][-1]) + 10_000)
+    assert_same(got, ref, label="sharded filter/start")
+
+
+def test_sharded_two_keys_long_sums_and_quiet_owner():
+    sch = abi.Schema.parse("a int, b int, x long, v double, ts long")
+    ts, cols = synth.keyed_stream(0, 120_000, 0xA7, 3, 20)
+    rng = np.random.default_rng(7)
+    a = cols[0]
+    b = rng.integers(0, 2, size=len(ts)).astype(np.int32)
+    x = rng.integers(-1000, 1000, size=len(ts)).astype(np.int64)
+    full = [a, b, x, cols[1], cols[2]]
+    sp = spec(64, aggs=[("sum", "x"), ("max", "x"), ("sum", "v"), ("count", None)], group_by=("a", "b"), schema=sch)
+    pushes = [(ts[:60_000], [c[:60_000] for c in full]), (ts[60_000:], [c[60_000:] for c in full])]
+    # 6 keys over 5 owners: some owners receive nothing and only close windows on the global clock
+    got = run_sharded(sp, 5, pushes, 1, [[0.2, 0.4, 0.6, 0.8]], advance=int(ts[-1]) + 3000)
+    ref = run_oracle(sp, pushes, 1, advance=int(ts[-1]) + 3000)
+    assert_same(got, ref, label="sharded two keys")
