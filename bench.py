@@ -6,8 +6,14 @@ Workload (BASELINE.json configs[1], the configuration the metric is quoted on fo
        group by k insert into O` over (k int, v double, ts long), 100k uniform keys,
        1,000,000 events per event-time second, one InputHandler.send per event (PER_EVENT clock).
 A step = one sh_push_device of `--batch` events (inputs already resident in HBM; the window state,
-key table and outputs stay on the device). Each rank owns a disjoint key range and its own stream
-(weak scaling, no data-path collective).
+key table and outputs stay on the device).
+
+N > 1 (`--ingest slice`, the default; north_star / SURVEY.md §8e): ONE global stream with N x the
+keys and N x the event rate; every step each rank ingests a contiguous slice of `--batch` events,
+the global clock / windows are agreed from all-gathered slice summaries, and every event is
+re-keyed to the GPU owning its key over an RCCL all-to-all (xGMI), then aggregated by its owner
+(sh_shard_*). Per-GPU work equals the N = 1 configuration (weak scaling). `--ingest keyed` instead
+gives each rank its own pre-partitioned stream (no data-path collective).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
    or:  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -38,6 +44,10 @@ def parse():
     ap.add_argument("--send-size", type=int, default=1, help="events per InputHandler.send (1 = PER_EVENT)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ingest", choices=["slice", "keyed"], default="slice",
+                    help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
     return ap.parse_args()
 
 
@@ -72,33 +82,55 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = max(1, torch.cuda.device_count())
+    if args.backend == "nccl" and world > 1 and local >= ndev:
+        raise SystemExit(f"rank {local} has no GPU of its own ({ndev} visible)")
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from siddhi_amd import abi, runtime, synth
-    ctx = runtime.Context(local)
+    ctx = runtime.Context(local % ndev)
     schema = abi.Schema.parse("k int, v double, ts long")
+    sliced = world > 1 and args.ingest == "slice"
+    keys_total = args.keys * world if sliced else args.keys
+    # owner tables: keys per owner ~ keys/N (+ hashing spread)
+    cap = int(args.keys * 1.1) if sliced else args.keys
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
-                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=args.keys)
-    q = runtime.GpuQuery(spec, ctx)
-
-    # synthetic stream of this rank, generated on the device; keys offset so ranks own disjoint keys
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=cap)
     B = args.batch
     nb = args.warmup + args.steps
     batches = []
-    for i in range(nb):
-        ts, cols = synth.torch_keyed_stream(i * B, B, 0xC2 ^ (rank * 0x9E37), args.keys, args.events_per_ms, dev)
-        if rank:
-            cols[0] += rank * args.keys
-        batches.append((ts, cols))
+    if sliced:
+        # rank r's slice of global push i: events [(i*N + r)*B, (i*N + r + 1)*B) of one stream
+        from siddhi_amd.shard import ShardedQuery, TorchExchange, distributed_push
+        q = ShardedQuery(spec, rank, world, ctx)
+        ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
+        send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
+        for i in range(nb):
+            batches.append(synth.torch_keyed_stream((i * world + rank) * B, B, 0xC2, keys_total,
+                                                    args.events_per_ms * world, dev))
+    else:
+        # keyed: this rank's own stream; keys offset so ranks own disjoint keys
+        q = runtime.GpuQuery(spec, ctx)
+        for i in range(nb):
+            ts, cols = synth.torch_keyed_stream(i * B, B, 0xC2 ^ (rank * 0x9E37), args.keys, args.events_per_ms, dev)
+            if rank:
+                cols[0] += rank * args.keys
+            batches.append((ts, cols))
     torch.cuda.synchronize()
 
     def push(i):
         ts, cols = batches[i]
+        if sliced:
+            return distributed_push(q, ex, B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size,
+                                    send_buf, host_out=False)[0]
         return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
 
     for i in range(args.warmup):
@@ -121,7 +153,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_events = B * args.steps * world
@@ -140,18 +172,21 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: SplitMix64 stream seed 0xC2 (per rank seed ^ rank*0x9E37), generated in HBM",
+        "data": ("synthetic: SplitMix64 stream seed 0xC2, one global stream sliced across ranks, generated in HBM"
+                 if sliced else "synthetic: SplitMix64 stream seed 0xC2 (per rank seed ^ rank*0x9E37), generated in HBM"),
         "config": {"workload": "C2 timeBatch(1 sec) count/min/max/avg group by k, per-event sends",
-                   "keys_per_gpu": args.keys, "events_per_step_per_gpu": B,
-                   "event_rate": f"{args.events_per_ms * 1000} events per event-time second",
-                   "send_size": args.send_size, "parallelism": f"key-sharded x{world}",
+                   "keys_per_gpu": args.keys, "keys_total": keys_total, "events_per_step_per_gpu": B,
+                   "event_rate": f"{args.events_per_ms * 1000 * (world if sliced else 1)} events per event-time second",
+                   "send_size": args.send_size,
+                   "parallelism": (f"slice ingest x{world}, key re-shard over RCCL all-to-all" if sliced
+                                   else f"key-sharded x{world}"),
                    "flushes": flushes, "rows": rows},
         "roofline": {"bound": "hbm", "kernel": "k_aggregate", "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
                      "kernel_ms_per_step": kern_ms / args.steps,
                      "bytes_per_event": C2_BYTES_PER_EVENT},
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -289,6 +289,8 @@ typedef struct {
     int64_t events;        /* events consumed by the last push                              */
 } sh_stats;
 int sh_query_stats(sh_query* q, sh_stats* out);
+/* The same for the owner pipeline of a sharded query (its last sh_shard_consume). */
+int sh_shard_stats(sh_shard* s, sh_stats* out);
 
 const char* sh_last_error(void);
 int32_t sh_abi_version(void);

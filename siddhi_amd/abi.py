@@ -389,6 +389,7 @@ def setup_lib_prototypes(lib, prefix: str):
                                       P(P(Bound)), PI]
         lib.sh_shard_consume.argtypes = [C.c_void_p, C.c_void_p, PI, P(Bound), C.c_int64, C.c_int32,
                                          P(P(Out)), P(PI)]
+        lib.sh_shard_stats.argtypes = [C.c_void_p, P(Stats)]
         lib.sh_shard_advance_time.argtypes = [C.c_void_p, C.c_int64, C.c_int32, P(P(Out)), P(PI)]
 
 
@@ -399,5 +400,5 @@ ABI_SYMBOLS = [
     "sh_aggregation_push_device", "sh_aggregation_advance_time", "sh_aggregation_table",
     "sh_alloc_pinned", "sh_free_pinned", "sh_query_stats", "sh_last_error", "sh_abi_version",
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
-    "sh_shard_consume", "sh_shard_advance_time",
+    "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats",
 ]

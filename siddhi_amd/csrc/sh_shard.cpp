@@ -364,3 +364,8 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
     set_order(s, host_out != 0, order);
     return SH_OK;
 }
+
+extern "C" int sh_shard_stats(sh_shard* s, sh_stats* out) {
+    if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_stats: NULL argument");
+    return sh_query_stats(s->owner, out);
+}

@@ -91,6 +91,11 @@ class ShardedQuery:
         _check(lib().sh_shard_advance_time(self.h, now, int(host_out), C.byref(out), C.byref(order)))
         return out, order
 
+    def stats(self) -> abi.Stats:
+        st = abi.Stats()
+        _check(lib().sh_shard_stats(self.h, C.byref(st)))
+        return st
+
     def close(self):
         if self.h:
             lib().sh_shard_destroy(self.h)
@@ -185,6 +190,7 @@ class LocalShards:
                 blocks.append(sends[g][start:start + n])
                 rbytes.append(n)
             recv = torch.cat(blocks) if sum(rbytes) else torch.empty(1, dtype=torch.uint8, device=device)
+            torch.cuda.current_stream(device).synchronize()  # the library runs on its own HIP stream
             out, order = s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=True)
             outs.append(host_rows(out, order))
         return outs
@@ -225,7 +231,8 @@ class TorchExchange:
         total = int(recv_bytes.sum())
         recv = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
         used = int(np.asarray(send_bytes).sum())
-        self.dist.all_to_all_single(recv[:total], send[:used], [int(x) for x in recv_bytes],
+        send = send[:used].to(self.device)
+        self.dist.all_to_all_single(recv[:total], send, [int(x) for x in recv_bytes],
                                     [int(x) for x in send_bytes], group=self.group)
         return recv, recv_bytes
 
@@ -255,5 +262,9 @@ def distributed_push(q: ShardedQuery, ex: TorchExchange, n: int, ts_ptr: int, co
     all_summ = ex.all_gather_summaries(summ)
     send_bytes, bounds = q.pack(all_summ, send_buf.data_ptr(), int(send_buf.numel()))
     recv, recv_bytes = ex.all_to_all(send_buf, send_bytes)
+    if recv.device != send_buf.device:  # host transport (gloo): the owner consumes device memory
+        recv = recv.to(send_buf.device)
     all_bounds = ex.all_gather_bounds(bounds)
+    import torch
+    torch.cuda.current_stream(send_buf.device).synchronize()  # recv was written on torch's stream
     return q.consume(recv.data_ptr(), recv_bytes, all_bounds, host_out)
