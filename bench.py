@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ingest", choices=["slice", "keyed"], default="slice",
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
+    ap.add_argument("--key-type", choices=["string", "int"], default="string",
+                    help="k as a dictionary-encoded string (ids are dense key slots) or as an int (hashed)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
     return ap.parse_args()
@@ -56,7 +58,7 @@ def cpu_baseline(args):
     import numpy as np
     from oracle.oracle import OracleQuery
     from siddhi_amd import abi, synth
-    schema = abi.Schema.parse("k int, v double, ts long")
+    schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=args.keys)
     q = OracleQuery(spec)
@@ -97,11 +99,10 @@ def main():
 
     from siddhi_amd import abi, runtime, synth
     ctx = runtime.Context(local % ndev)
-    schema = abi.Schema.parse("k int, v double, ts long")
+    schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")
     sliced = world > 1 and args.ingest == "slice"
     keys_total = args.keys * world if sliced else args.keys
-    # owner tables: keys per owner ~ keys/N (+ hashing spread)
-    cap = int(args.keys * 1.1) if sliced else args.keys
+    cap = keys_total  # whole-stream key capacity (each owner sizes its table for its share)
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=cap)
     B = args.batch
@@ -175,6 +176,7 @@ def main():
         "data": ("synthetic: SplitMix64 stream seed 0xC2, one global stream sliced across ranks, generated in HBM"
                  if sliced else "synthetic: SplitMix64 stream seed 0xC2 (per rank seed ^ rank*0x9E37), generated in HBM"),
         "config": {"workload": "C2 timeBatch(1 sec) count/min/max/avg group by k, per-event sends",
+                   "key_type": f"{args.key_type} ({'dictionary ids = dense slots' if args.key_type == 'string' else 'hashed'})",
                    "keys_per_gpu": args.keys, "keys_total": keys_total, "events_per_step_per_gpu": B,
                    "event_rate": f"{args.events_per_ms * 1000 * (world if sliced else 1)} events per event-time second",
                    "send_size": args.send_size,

@@ -152,7 +152,17 @@ __device__ __forceinline__ bool probe_step(const KeyTable& kt, u64 key, u64 k, u
     return false;
 }
 
+// Dense mode: a dictionary id maps to its slot directly (the sharded owner of ids = dadd mod dmul
+// keeps them compact as (id - dadd) / dmul); an id outside the table fails the push loudly.
+__device__ __forceinline__ u32 dense_slot(const KeyTable& kt, u64 key) {
+    u32 id = (u32)key;
+    u32 s = kt.dmul == 1 ? id - kt.dadd : (id - kt.dadd) / kt.dmul;
+    if ((i64)key < 0 || s > kt.mask) { atomicExch(kt.overflow, 2); return 0; }
+    return s;
+}
+
 __device__ __forceinline__ u32 key_slot(const KeyTable& kt, u64 key) {
+    if (kt.dense) return dense_slot(kt, key);
     if (key == kEmptyKey) return kt.mask + 1;
     u32 h = key_home(kt, key);
     for (u32 probe = 0; probe <= kt.mask; probe++)
@@ -167,6 +177,11 @@ template <int K>
 __device__ __forceinline__ void key_slots(const KeyTable& kt, const u64* key, const bool* valid, u32* out) {
     u32 h[K];
     bool done[K];
+    if (kt.dense) {
+#pragma unroll
+        for (int i = 0; i < K; i++) if (valid[i]) out[i] = dense_slot(kt, key[i]);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < K; i++) {
         done[i] = !valid[i] || key[i] == kEmptyKey;
@@ -192,6 +207,7 @@ __device__ __forceinline__ void key_slots(const KeyTable& kt, const u64* key, co
 }
 
 __device__ __forceinline__ u64 slot_key(const KeyTable& kt, u32 pos) {
+    if (kt.dense) return (u64)(pos * kt.dmul + kt.dadd);
     return pos > kt.mask ? kEmptyKey : kt.keys[pos];
 }
 

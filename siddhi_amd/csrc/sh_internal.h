@@ -56,14 +56,19 @@ struct AggPlan {
     int vcol[SH_MAX_AGGS];   // value-column slot (-1 for COUNT)
     int vcol_src[SH_MAX_AGGS];   // stream column index of value slot v
     int vcol_type[SH_MAX_AGGS];  // SH_T_* of value slot v
+    // per LDS field f (batch folds): update op and the value slot it reads
+    int fop[SH_MAX_AGGS];
+    int fvcol[SH_MAX_AGGS];
 };
+// field update ops: sums (long, double, int->double for avg) and typed min/max
+enum FieldOp { FOP_ADD_I = 0, FOP_ADD_D, FOP_ADD_DI, FOP_MIN_I, FOP_MAX_I, FOP_MIN_D, FOP_MAX_D, FOP_MIN_F, FOP_MAX_F };
 
 // Group key plan: 0, 1 or 2 integral columns packed into a u64.
 struct KeyPlan {
     int n;
     int col[SH_MAX_GROUP];
     int type[SH_MAX_GROUP];
-    int pad;
+    int dense;  // one STRID column: dictionary ids are dense in [0, key_capacity) -> slot = id
     i64 div[SH_MAX_GROUP];  // > 0: the component is (u32)(value / div) (aggregation time buckets)
 };
 
@@ -75,6 +80,10 @@ struct KeyTable {
     u32 shift;        // 64 - log2(mask + 1): Fibonacci-hash shift
     u32* n_keys;      // distinct keys inserted
     int* overflow;    // set when probing exhausts the table
+    // dense mode (dictionary ids): slot = (id - dadd) / dmul, no probing, no table
+    int dense;
+    u32 dmul, dadd;
+    int pad;
 };
 
 // Window assignment for one push (see DESIGN.md "Window assignment").
@@ -148,7 +157,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       // partitioned source (P > 1)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
                       const i64* seg_off);
-size_t aggregate_part_lds(int NL, int n_fields, int n_vcols);
+size_t aggregate_own_lds(int NL, int n_fields, int n_vcols);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
 void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,

@@ -276,6 +276,44 @@ __device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL
     }
 }
 
+// A key's aggregate fields held in registers while one of its events is folded (k_aggregate_own),
+// field j in register slot j: the per-event updates of apply_event, driven by the per-field op
+// table (sums: sum += x / value += (double) x; min/max: replace when the state is new or x is
+// smaller / larger in the column's type — MinAttributeAggregatorExecutor `minValue > value`).
+template <int V>
+__device__ __forceinline__ void fold_fields(const AggPlan& ap, u64 (&f)[SH_MAX_AGGS], bool first, const i64 (&v)[V]) {
+#pragma unroll
+    for (int j = 0; j < SH_MAX_AGGS; j++) {
+        if (j >= ap.n_fields) break;
+        const int op = ap.fop[j];
+        const i64 x = pick<V>(v, ap.fvcol[j]);
+        const u64 cur = f[j];
+        u64 r;
+        if (op <= FOP_ADD_DI) {
+            if (op == FOP_ADD_I) {
+                r = (u64)((first ? 0 : (i64)cur) + x);
+            } else {
+                double xd = op == FOP_ADD_DI ? (double)x : __longlong_as_double(x);
+                r = (u64)__double_as_longlong((first ? 0.0 : __longlong_as_double((i64)cur)) + xd);
+            }
+        } else {
+            bool lt, gt;  // x < cur, x > cur in the column's type (false on NaN, as in Java)
+            if (op <= FOP_MAX_I) {
+                lt = x < (i64)cur; gt = x > (i64)cur;
+            } else if (op <= FOP_MAX_D) {
+                double a = __longlong_as_double(x), b = __longlong_as_double((i64)cur);
+                lt = a < b; gt = a > b;
+            } else {
+                float a = (float)__longlong_as_double(x), b = (float)__longlong_as_double((i64)cur);
+                lt = a < b; gt = a > b;
+            }
+            const bool is_min = op == FOP_MIN_I || op == FOP_MIN_D || op == FOP_MIN_F;
+            r = (first || (is_min ? lt : gt)) ? (u64)x : cur;
+        }
+        f[j] = r;
+    }
+}
+
 // Row emission shared by both variants: one row per touched local key (RowTmp + values), the
 // first-occurrence flag and the row reference at the key's first event.
 __device__ __forceinline__ void emit_rows(const AggPlan& ap, AggLds& L, int NL, int logP, int p, int seg,
@@ -385,141 +423,144 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
     emit_rows(ap, L, NL, 0, 0, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
 }
 
-// Partitioned (P > 1): one workgroup of W waves per (closed segment, key partition). The partition's
-// record list (event order) is consumed in chunks of CH = 64*W*R records: the chunk is split stably
-// in LDS into W sub-lists by li % W, and wave w folds sub-list w into the keys it owns. Inside a
-// wave, lanes that hit the same key apply in lane (= event) order, one round per repeat; a wave's
-// LDS operations complete in program order, so per chunk only the split needs workgroup barriers.
-template <int W, int R, int V>
-__global__ __launch_bounds__(W * 64, 4) void k_aggregate_part(const Segment* __restrict__ segs, int P, int logP, int NL,
-                                                          AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter,
-                                                          unsigned char* flags, u32* rowref, i64* seg_rows,
-                                                          const u32* __restrict__ rec_pos,
-                                                          const u32* __restrict__ rec_idx,
-                                                          const u64* __restrict__ rec_vals, i64 rec_cap,
-                                                          const i64* __restrict__ seg_off, int key_bits) {
-    constexpr int CH = 64 * W * R;
-    constexpr int logW = W == 1 ? 0 : W == 2 ? 1 : W == 4 ? 2 : W == 8 ? 3 : 4;
+// Partitioned (P > 1), lane ownership: thread t of the workgroup owns the local keys li with
+// li mod 512 == t. Every chunk of CH records (event order) is split stably in LDS into 512 per-thread
+// lists: piece q (64 consecutive records, loaded by one wave) gets per-bucket counts pc[q][b] and
+// in-piece ranks from ballots over the 9 bucket bits; a per-bucket scan over the pieces and a
+// workgroup scan over the buckets give every record its slot. Thread t then folds its list in order
+// straight into the LDS state — keys owned by different lanes of a wave fall in different LDS banks,
+// and no two lanes ever touch one key, so there are no conflict rounds at all.
+constexpr int kOwnT = 512;
+template <int R, int V>
+__global__ __launch_bounds__(kOwnT, 2) void k_aggregate_own(const Segment* __restrict__ segs, int P, int logP, int NL,
+                                                           AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter,
+                                                           unsigned char* flags, u32* rowref, i64* seg_rows,
+                                                           const u32* __restrict__ rec_pos,
+                                                           const u32* __restrict__ rec_idx,
+                                                           const u64* __restrict__ rec_vals, i64 rec_cap,
+                                                           const i64* __restrict__ seg_off) {
+    constexpr int W = kOwnT / 64;
+    constexpr int NQ = W * R;        // pieces per chunk
+    constexpr int CH = 64 * NQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     AggLds L;
     lds_layout(smem_raw, ap, NL, L);
-    // staging after the key state (16-byte aligned)
     unsigned char* stg0 = (unsigned char*)(L.owner + NL);
     unsigned char* stg = stg0 + ((16u - ((unsigned)(size_t)stg0 & 15u)) & 15u);
-    u64* st_v = (u64*)stg;                           // [V][CH]
-    u32* st_li = (u32*)(st_v + (size_t)V * CH);      // [CH]
-    u32* st_idx = st_li + CH;                        // [CH]
-    u32* cnt = st_idx + CH;                          // [R*W][W]
-    u32* off = cnt + R * W * W;                      // [R*W][W]
-    u32* sub_start = off + R * W * W;                // [W + 1]
+    u64* st_v = (u64*)stg;                               // [V][CH]
+    u32* st_li = (u32*)(st_v + (size_t)V * CH);          // [CH]
+    u32* st_idx = st_li + CH;                            // [CH]
+    unsigned short* pc = (unsigned short*)(st_idx + CH); // [NQ][512]: count, then in-bucket offset
+    u32* bstart = (u32*)(pc + NQ * kOwnT);               // [512]
 
     const int seg = blockIdx.x / P;
     const int p = blockIdx.x % P;
-    for (int i = threadIdx.x; i < NL; i += W * 64) L.cnt[i] = 0;
-    // the (segment, partition) record range, from k_seg_offsets
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int i = t; i < NL; i += kOwnT) L.cnt[i] = 0;
     const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    __syncthreads();
 
-    for (i64 c0 = lo; c0 < hi; c0 += CH) {
-        const int n = (int)min((i64)CH, hi - c0);
-        // (a) load R records per lane, in chunk order q = j*W + w
-        u32 li[R], idx[R], rk[R];
-        int sub[R];
-        i64 v[R][V];
+    // records of chunk c0 for this lane: piece q = j * W + w holds records q*64 .. q*64+63
+    u32 li[R], idx[R], rk[R];
+    i64 v[R][V];
+    u32 nli[R], nidx[R];
+    i64 nv[R][V];
+    auto load = [&](i64 c, u32 (&a)[R], u32 (&b)[R], i64 (&vals)[R][V]) {
+        const int n = (int)min((i64)CH, hi - c);
 #pragma unroll
         for (int j = 0; j < R; j++) {
-            int r = (j * W + w) * 64 + lane;
-            bool ok = r < n;
-            li[j] = ok ? (rec_pos[c0 + r] >> logP) : 0xFFFFFFFFu;
-            idx[j] = 0;
+            const int r = (j * W + w) * 64 + lane;
+            const bool ok = r < n;
+            a[j] = ok ? (rec_pos[c + r] >> logP) : 0xFFFFFFFFu;
+            b[j] = ok ? rec_idx[c + r] : 0;
 #pragma unroll
-            for (int x = 0; x < V; x++) v[j][x] = 0;
-            if (ok) {
-                idx[j] = rec_idx[c0 + r];
+            for (int x = 0; x < V; x++)
+                vals[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c + r] : 0;
+        }
+    };
+    if (lo < hi) load(lo, li, idx, v);
+    for (i64 c0 = lo; c0 < hi; c0 += CH) {
+        // (a) the next chunk's loads are issued now and land while this chunk is split and folded
+        if (c0 + CH < hi) load(c0 + CH, nli, nidx, nv);
+        for (int i = t; i < NQ * kOwnT / 8; i += kOwnT) ((uint4*)pc)[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        // (b) in-piece rank among lanes of the same bucket (li mod 512), per-piece bucket counts
 #pragma unroll
-                for (int x = 0; x < V; x++)
-                    if (x < ap.n_vcols) v[j][x] = (i64)rec_vals[(size_t)x * rec_cap + c0 + r];
-            }
-            sub[j] = ok ? (int)(li[j] & (W - 1)) : -1;
-            // (b) stable rank among this wave's lanes of the same sub-list, and per-sub counts
+        for (int j = 0; j < R; j++) {
+            const bool ok = li[j] != 0xFFFFFFFFu;
             u64 peers = __ballot(ok);
 #pragma unroll
-            for (int bt = 0; bt < logW; bt++) {
-                bool bit = ok && ((li[j] >> bt) & 1);
-                u64 mb = __ballot(bit);
+            for (int bt = 0; bt < 9; bt++) {
+                const bool bit = ok && ((li[j] >> bt) & 1);
+                const u64 mb = __ballot(bit);
                 peers &= bit ? mb : ~mb;
             }
             rk[j] = (u32)__popcll(peers & lt_mask);
+            if (ok && rk[j] == 0) pc[(j * W + w) * kOwnT + (li[j] & (kOwnT - 1))] = (unsigned short)__popcll(peers);
+        }
+        __syncthreads();
+        // (c) bucket t: offsets over the pieces, then bucket starts over the buckets
+        u32 tot = 0;
 #pragma unroll
-            for (int sb = 0; sb < W; sb++) {
-                u64 ms = __ballot(sub[j] == sb);
-                if (lane == sb) cnt[(j * W + w) * W + sb] = (u32)__popcll(ms);
-            }
+        for (int q = 0; q < NQ; q++) {
+            u32 c = pc[q * kOwnT + t];
+            pc[q * kOwnT + t] = (unsigned short)tot;
+            tot += c;
         }
+        i64 all;
+        const u32 my_start = (u32)block_excl_scan_any((i64)tot, &all);
+        bstart[t] = my_start;
         __syncthreads();
-        // (c) offsets: sub-lists in sub order, each in chunk order
-        if (threadIdx.x < W) {
-            const int t = threadIdx.x;
-            u32 base = 0;
-            for (int sb = 0; sb < t; sb++)
-                for (int q = 0; q < R * W; q++) base += cnt[q * W + sb];
-            sub_start[t] = base;
-            u32 run = base;
-            for (int q = 0; q < R * W; q++) { off[q * W + t] = run; run += cnt[q * W + t]; }
-            if (t == W - 1) sub_start[W] = run;
-        }
-        __syncthreads();
-        // (d) scatter into the staging sub-lists
+        // (d) place every record in its owner's list
 #pragma unroll
         for (int j = 0; j < R; j++) {
-            if (sub[j] < 0) continue;
-            u32 d = off[(j * W + w) * W + sub[j]] + rk[j];
+            if (li[j] == 0xFFFFFFFFu) continue;
+            const int b = li[j] & (kOwnT - 1);
+            const u32 d = bstart[b] + pc[(j * W + w) * kOwnT + b] + rk[j];
             st_li[d] = li[j];
             st_idx[d] = idx[j];
 #pragma unroll
             for (int x = 0; x < V; x++) if (x < ap.n_vcols) st_v[(size_t)x * CH + d] = (u64)v[j][x];
         }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            li[j] = nli[j];
+            idx[j] = nidx[j];
+#pragma unroll
+            for (int x = 0; x < V; x++) v[j][x] = nv[j][x];
+        }
         __syncthreads();
-        // (e) wave w folds its sub-list in order
-        const int s0 = (int)sub_start[w], s1 = (int)sub_start[w + 1];
-        for (int b = s0; b < s1; b += 64) {
-            int e = b + lane;
-            bool ok = e < s1;
-            u32 k = ok ? st_li[e] : 0;
-            u32 ix = ok ? st_idx[e] : 0;
+        // (e) thread t folds its list in event order into the LDS state of its keys
+        for (u32 i = my_start; i < my_start + tot; i++) {
+            const u32 k = st_li[i];
+            const u32 ix = st_idx[i];
             i64 vv[V];
 #pragma unroll
-            for (int x = 0; x < V; x++) vv[x] = (ok && x < ap.n_vcols) ? (i64)st_v[(size_t)x * CH + e] : 0;
-            u64 peers = __ballot(ok);
-            for (int bt = logW; bt < key_bits; bt++) {
-                bool bit = ok && ((k >> bt) & 1);
-                u64 mb = __ballot(bit);
-                peers &= bit ? mb : ~mb;
-            }
-            u32 rank = ok ? (u32)__popcll(peers & lt_mask) : 0xFFFFFFFFu;
-            for (u32 r = 0;; r++) {
-                bool go = rank == r;
-                if (__ballot(go) == 0) break;
-                if (go) apply_event(ap, L, NL, k, ix, vv);
-            }
+            for (int x = 0; x < V; x++) vv[x] = x < ap.n_vcols ? (i64)st_v[(size_t)x * CH + i] : 0;
+            const u32 c = L.cnt[k];
+            u64 f[SH_MAX_AGGS];
+#pragma unroll
+            for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = (j < ap.n_fields && c) ? L.fields[(size_t)j * NL + k] : 0;
+            fold_fields<V>(ap, f, c == 0, vv);
+#pragma unroll
+            for (int j = 0; j < SH_MAX_AGGS; j++) if (j < ap.n_fields) L.fields[(size_t)j * NL + k] = f[j];
+            if (c == 0) L.first[k] = ix;
+            L.last[k] = ix;
+            L.cnt[k] = c + 1;
         }
     }
     __syncthreads();
     emit_rows(ap, L, NL, logP, p, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
 }
 
-// records per lane per chunk: keep R x V value registers <= 8
-constexpr int part_rounds(int V) { return V <= 2 ? 4 : V <= 4 ? 2 : 1; }
+constexpr int own_rounds(int V) { return V <= 2 ? 2 : 1; }
 
-size_t aggregate_part_lds(int NL, int n_fields, int n_vcols) {
+size_t aggregate_own_lds(int NL, int n_fields, int n_vcols) {
     n_vcols = n_vcols <= 1 ? 1 : n_vcols <= 2 ? 2 : n_vcols <= 4 ? 4 : 8;
-    const int W = 8, R = part_rounds(n_vcols), CH = 64 * W * R;
+    const int R = own_rounds(n_vcols), NQ = (kOwnT / 64) * R, CH = 64 * NQ;
     size_t state = (size_t)NL * (8 * n_fields + 16) + 16;
     state = (state + 15) & ~(size_t)15;
-    return state + (size_t)CH * (8 * n_vcols + 8) + (size_t)R * W * W * 8 + (W + 1) * 4 + 32;
+    return state + 16 + (size_t)CH * (8 * n_vcols + 8) + (size_t)NQ * kOwnT * 2 + kOwnT * 4 + 64;
 }
 
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
@@ -529,18 +570,15 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const i64* seg_off) {
     size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
     if (P > 1) {
-        int key_bits = 0;
-        while ((1 << key_bits) < NL) key_bits++;
-        lds = aggregate_part_lds(NL, ap.n_fields, ap.n_vcols);
-#define SH_AGG_PART(VV)                                                                                          \
-    hipLaunchKernelGGL((k_aggregate_part<8, part_rounds(VV), VV>), dim3(nseg * P), dim3(8 * 64), lds, s, segs, P, logP, NL, ap, \
-                       rows, row_vals, row_counter, flags, rowref, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap,  \
-                       seg_off, key_bits)
-        if (ap.n_vcols <= 1) SH_AGG_PART(1);
-        else if (ap.n_vcols <= 2) SH_AGG_PART(2);
-        else if (ap.n_vcols <= 4) SH_AGG_PART(4);
-        else SH_AGG_PART(8);
-#undef SH_AGG_PART
+        lds = aggregate_own_lds(NL, ap.n_fields, ap.n_vcols);
+#define SH_AGG_OWN(VV)                                                                                           \
+    hipLaunchKernelGGL((k_aggregate_own<own_rounds(VV), VV>), dim3(nseg * P), dim3(kOwnT), lds, s, segs, P, logP, NL, ap, \
+                       rows, row_vals, row_counter, flags, rowref, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap, seg_off)
+        if (ap.n_vcols <= 1) SH_AGG_OWN(1);
+        else if (ap.n_vcols <= 2) SH_AGG_OWN(2);
+        else if (ap.n_vcols <= 4) SH_AGG_OWN(4);
+        else SH_AGG_OWN(8);
+#undef SH_AGG_OWN
     } else {
         hipLaunchKernelGGL(k_aggregate_flat, dim3(nseg), dim3(kBlock), lds, s, segs, NL, n_pend, pend_pos, pend_vals,
                            pend_cap, new_pos, cols, ap, rows, row_vals, row_counter, flags, rowref, seg_rows);

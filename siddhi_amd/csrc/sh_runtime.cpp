@@ -173,6 +173,23 @@ int compile_aggs(int n_aggs, const sh_agg_spec* aggs, int n_cols, const int32_t*
             default: return sh_fail(SH_ERR_INVALID, "unknown aggregator");
         }
     }
+    for (int a = 0; a < n_aggs; a++) {
+        if (ap.kind[a] == AK_COUNT) continue;
+        int f = ap.field[a], v = ap.vcol[a];
+        bool fpcol = ap.vcol_type[v] == SH_T_FLOAT || ap.vcol_type[v] == SH_T_DOUBLE;
+        ap.fvcol[f] = v;
+        switch (ap.kind[a]) {
+            case AK_SUM_L: ap.fop[f] = FOP_ADD_I; break;
+            case AK_SUM_D: ap.fop[f] = FOP_ADD_D; break;
+            case AK_AVG: ap.fop[f] = fpcol ? FOP_ADD_D : FOP_ADD_DI; break;
+            case AK_MIN_L: ap.fop[f] = FOP_MIN_I; break;
+            case AK_MAX_L: ap.fop[f] = FOP_MAX_I; break;
+            case AK_MIN_D: ap.fop[f] = FOP_MIN_D; break;
+            case AK_MAX_D: ap.fop[f] = FOP_MAX_D; break;
+            case AK_MIN_F: ap.fop[f] = FOP_MIN_F; break;
+            case AK_MAX_F: ap.fop[f] = FOP_MAX_F; break;
+        }
+    }
     return SH_OK;
 }
 
@@ -190,6 +207,8 @@ int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* t
     }
     if (n_group == 2 && (kp.type[0] == SH_T_LONG || kp.type[1] == SH_T_LONG))
         return sh_fail(SH_ERR_UNSUPPORTED, "two group-by columns must both be 32-bit");
+    // string keys arrive as dictionary ids the host assigns densely from 0: the id is the slot
+    kp.dense = n_group == 1 && kp.type[0] == SH_T_STRID;
     return SH_OK;
 }
 
@@ -200,7 +219,24 @@ int KeyTableHost::init(int64_t capacity) {
     return init_size(ts);
 }
 
+int KeyTableHost::init_dense(int64_t capacity, uint32_t mul, uint32_t add) {
+    size_t ts = 16;
+    while ((int64_t)ts < capacity) ts <<= 1;
+    dense = true;
+    dmul = mul;
+    dadd = add;
+    size_ = ts;
+    n_keys = 0;
+    int rc = keys.reserve(64, false);
+    if (rc) return rc;
+    rc = ctrl.reserve(64, false);
+    if (rc) return rc;
+    if (hipMemset(ctrl.p, 0, 64) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table init failed");
+    return SH_OK;
+}
+
 int KeyTableHost::init_size(size_t ts) {
+    dense = false;
     size_ = ts;
     n_keys = 0;
     int rc = keys.reserve(ts * 8, false);
@@ -223,6 +259,10 @@ KeyTable KeyTableHost::dev() const {
     kt.shift = (u32)(64 - lg);
     kt.n_keys = (u32*)ctrl.p;
     kt.overflow = (int*)((char*)ctrl.p + 8);
+    kt.dense = dense ? 1 : 0;
+    kt.dmul = dmul;
+    kt.dadd = dadd;
+    kt.pad = 0;
     return kt;
 }
 
@@ -232,6 +272,7 @@ int KeyTableHost::check(hipStream_t s) {
         hipStreamSynchronize(s) != hipSuccess)
         return sh_fail(SH_ERR_DEVICE, "key table check failed");
     n_keys = c[0];
+    if (c[2] == 2) return sh_fail(SH_ERR_INVALID, "dictionary id outside [0, key_capacity): raise key_capacity");
     if (c[2]) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
     return SH_OK;
 }

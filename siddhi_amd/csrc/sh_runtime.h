@@ -32,7 +32,10 @@ struct KeyTableHost {
     DevBuf keys, ctrl;
     size_t size_ = 0;
     int64_t n_keys = 0;  // keys inserted so far (read back by check)
+    bool dense = false;  // dictionary ids: slot = (id - dadd) / dmul, no hashing
+    uint32_t dmul = 1, dadd = 0;
     int init(int64_t capacity);
+    int init_dense(int64_t capacity, uint32_t mul, uint32_t add);
     int init_size(size_t ts);
     shd::KeyTable dev() const;
     int check(hipStream_t s);

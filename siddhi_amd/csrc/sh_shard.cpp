@@ -91,12 +91,20 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
     s->rec_words = 3 + s->ap.n_vcols;
     // the owner runs the same query over the records it receives: no filter (applied at ingest),
     // 8-byte raw columns, windows given per event
+    // key_capacity is the whole stream's; an owner holds about 1/G of the keys (dictionary ids
+    // exactly the ids = rank mod G, compacted to id / G)
     sh_query_desc od = *d;
     od.n_filter_ops = 0;
     od.filter = nullptr;
+    int64_t cap = d->key_capacity > 0 ? d->key_capacity : (1 << 16);
+    od.key_capacity = s->kp.dense ? (cap + world - 1) / world : cap / world + cap / (4 * world) + 64;
     if ((rc = sh_query_create(ctx, &od, &s->owner))) { delete s; return rc; }
     sh_query* q = s->owner;
     q->given = true;
+    if (s->kp.dense) {
+        q->kt.dmul = (uint32_t)world;
+        q->kt.dadd = (uint32_t)rank;
+    }
     s->roles.n = d->n_cols;
     for (int c = 0; c < d->n_cols; c++) {
         int t = d->col_types[c];

@@ -12,7 +12,12 @@
 
 namespace shd {
 
-__device__ __forceinline__ u32 owner_of(u64 key, int G) { return (u32)(mix64(key ^ 0x5851F42D4C957F2Dull) % (u64)G); }
+// owner GPU of a group key: dictionary ids (dense keys) round-robin, so every owner's ids stay dense
+// as id / G; other keys by a 64-bit mix (independent of the owner's Fibonacci slot hash)
+__device__ __forceinline__ u32 owner_of(const KeyPlan& kp, u64 key, int G) {
+    if (kp.dense) return (u32)key % (u32)G;
+    return (u32)(mix64(key ^ 0x5851F42D4C957F2Dull) % (u64)G);
+}
 
 // code of a passing event: (W - W_base) << 4 | owner; kNoPos when it is filtered out
 constexpr int kOwnerBits = 4;
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
             }
             u32 c = kNoPos;
             if (pass[i]) {
-                u32 o = owner_of(make_key(kp, cols, e), G);
+                u32 o = owner_of(kp, make_key(kp, cols, e), G);
                 c = ((u32)(W - wp.W_base) << kOwnerBits) | o;
                 atomicAdd(&hist[o], 1u);
             }

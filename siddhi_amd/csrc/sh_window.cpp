@@ -87,7 +87,7 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
 static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out);
 
 // key partitions: smallest power of two whose per-partition LDS state (plus, when partitioned, the
-// record staging of k_aggregate_part) fits the budget that keeps two workgroups per CU
+// record staging of k_aggregate_own) fits the budget that keeps two workgroups per CU
 static int size_partitions(sh_query* q) {
     const size_t budget = 80 * 1024;
     size_t ts = q->kt.size_;
@@ -95,7 +95,7 @@ static int size_partitions(sh_query* q) {
     auto need = [&](int p) {
         int nl = (int)(ts / p) + 1;
         return p == 1 ? (size_t)nl * (16 + 8 * (size_t)q->ap.n_fields) + 16
-                      : aggregate_part_lds(nl, q->ap.n_fields, q->ap.n_vcols);
+                      : aggregate_own_lds(nl, q->ap.n_fields, q->ap.n_vcols);
     };
     while (need(P) > budget && P < (1 << 14)) P <<= 1;
     if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large");
@@ -122,6 +122,7 @@ static int rekey(sh_query* q, size_t size) {
 }
 
 int query_reserve_keys(sh_query* q, int64_t extra) {
+    if (q->kt.dense) return SH_OK;  // slots are the dictionary ids themselves
     int64_t ts = (int64_t)q->kt.size_;
     if (q->kt.n_keys + extra <= ts / 2) return SH_OK;
     int64_t live = std::min<int64_t>(q->kt.n_keys, q->n_pend);
@@ -170,7 +171,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
-    if ((rc = q->kt.init(cap))) { delete q; return rc; }
+    if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0;

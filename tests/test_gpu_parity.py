@@ -85,6 +85,37 @@ def test_c2_timebatch_matches_oracle(rt, send_size):
     assert out["flush_offsets"].size >= 6
 
 
+C2S_SCHEMA = abi.Schema.parse("k string, v double, ts long")
+
+
+@pytest.mark.parametrize("send_size", [1, 1000])
+def test_c2_dictionary_keys_dense_slots(rt, send_size):
+    """k as a dictionary-encoded string: ids are the key slots (no hashing); same output as the oracle."""
+    ts, cols = synth.keyed_stream(0, 600_000, 0xC2, 100_000, 100)
+    spec = abi.QuerySpec(C2S_SCHEMA, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=100_000)
+    pushes = split_batches(C2S_SCHEMA, ts, cols, [123_456, 400_000], send_size)
+    pushes.append(("advance", int(ts[-1]) + 5000))
+    out = both(rt, spec, pushes, label="C2 dict")
+    assert out["flush_offsets"].size >= 6
+
+
+def test_c3_sliding_dictionary_keys(rt):
+    ts, cols = synth.keyed_stream(0, 200_000, 0xC3, 3_000, 50)
+    spec = abi.QuerySpec(C2S_SCHEMA, "time", 2_000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=3_000)
+    both(rt, spec, split_batches(C2S_SCHEMA, ts, cols, [77_777], 1), label="C3 dict")
+
+
+def test_dictionary_id_beyond_capacity_fails_loudly(rt):
+    from siddhi_amd.runtime import SiddhiError
+    ts, cols = synth.keyed_stream(0, 10_000, 0xC2, 5000, 10)
+    spec = abi.QuerySpec(C2S_SCHEMA, "timeBatch", 100, group_by=["k"], aggs=[("count", None)], key_capacity=1000)
+    g = rt.GpuQuery(spec)
+    with pytest.raises(SiddhiError, match="dictionary id"):
+        g.push(abi.HostBatch(C2S_SCHEMA, ts, cols, 1))
+
+
 def test_timebatch_small_keys_start_time_and_gaps(rt):
     # clock jumps (empty windows), start.time alignment, filter that drops whole sends
     rng = np.random.default_rng(7)

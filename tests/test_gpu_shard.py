@@ -101,3 +101,14 @@ def test_sharded_two_keys_long_sums_and_quiet_owner():
     got = run_sharded(sp, 5, pushes, 1, [[0.2, 0.4, 0.6, 0.8]], advance=int(ts[-1]) + 3000)
     ref = run_oracle(sp, pushes, 1, advance=int(ts[-1]) + 3000)
     assert_same(got, ref, label="sharded two keys")
+
+
+def test_sharded_dictionary_keys_round_robin_owners():
+    """string (dictionary id) keys: owner = id % G and each owner keeps its ids dense as id / G."""
+    sch = abi.Schema.parse("k string, v double, ts long")
+    sp = spec(30_000, schema=sch)
+    pushes = stream_pushes(400_000, [180_000, 220_000], 0xD1, 30_000, 80)
+    adv = int(pushes[-1][0][-1]) + 4000
+    got = run_sharded(sp, 4, pushes, 1, [[0.3, 0.5, 0.9]], advance=adv)
+    ref = run_oracle(sp, pushes, 1, advance=adv)
+    assert_same(got, ref, label="sharded dict x4")
