@@ -213,6 +213,16 @@ int sh_push_device(sh_query* q, const sh_batch* batch, const sh_out** out);
 /* TIMER path: advance the playback clock to `now` without events (Scheduler.onTimeChange). */
 int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
 
+/* Checkpoint of the query's state: State.snapshot()/restore() (core/util/snapshot/state/State.java:
+ * 26-36) driven by SnapshotService.persist/restore (core/util/snapshot/SnapshotService.java:90-296)
+ * — the open window's queued events (and lengthBatch count), the sliding window's queue with every
+ * key's aggregator state and min/max deques, the partition key, the playback clock and
+ * nextEmitTime. Two calls: buf = NULL returns the size in *len. A blob restores only into a query
+ * created from the same descriptor (SH_ERR_INVALID otherwise); the restored query then continues
+ * exactly as the snapshotted one would have. */
+int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len);
+int sh_query_restore(sh_query* q, const void* buf, int64_t len);
+
 int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* desc, sh_aggregation** out);
 int sh_aggregation_destroy(sh_aggregation* a);
 /* AggregationRuntime.processEvents via IncrementalAggregationProcessor.process

@@ -337,3 +337,27 @@ int sliding_advance(sh_query* q, int64_t now, const sh_out** out) {
     }
     return empty_out(q, out);
 }
+
+// Persistent buffers of the sliding state and their byte sizes, for sh_query_snapshot/restore
+// (sh_snapshot.cpp). scalars = {nslots, rc, pm, send_base}; with set = true the ring capacity is
+// first made `new_rc` and the scalars are taken from the snapshot.
+int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* sc, int n_sc, bool set,
+                          int64_t new_rc) {
+    SlidingImpl* s = q->sl;
+    if (n_sc != 4) return sh_fail(SH_ERR_INVALID, "sliding snapshot layout");
+    if (set) {
+        if (sc[0] != s->nslots) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+        if (new_rc != s->rc) RCHK(size_rings(q, new_rc));
+        s->pm = sc[2];
+        s->send_base = sc[3];
+    } else {
+        sc[0] = s->nslots; sc[1] = s->rc; sc[2] = s->pm; sc[3] = s->send_base;
+    }
+    const size_t n = (size_t)s->nslots, rc = (size_t)s->rc;
+    const size_t F = (size_t)std::max(1, q->ap.n_fields), V = (size_t)std::max(1, q->ap.n_vcols);
+    bufs = {{&s->cnt, n * 8},          {&s->f, F * n * 8},         {&s->mm, F * n * 8},      {&s->mm_has, F * n},
+            {&s->dq_head, F * n * 8},  {&s->dq_len, F * n * 8},    {&s->dq, F * n * rc * 8}, {&s->rhead, n * 8},
+            {&s->rlen, n * 8},         {&s->rpm, n * rc * 8},      {&s->rval, V * n * rc * 8},
+            {&s->cur_send, n * 8},     {&s->cur_first, n * 8}};
+    return SH_OK;
+}

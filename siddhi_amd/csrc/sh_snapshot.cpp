@@ -1,0 +1,260 @@
+// sh_snapshot.cpp — checkpoint of a query's device state behind sh_query_snapshot / sh_query_restore.
+//
+// Replaces State.snapshot()/restore() (core/util/snapshot/state/State.java:26-36) as driven by
+// SnapshotService.persist/restore (core/util/snapshot/SnapshotService.java:90-296) for the states
+// this path owns: the batch windows' queued events and count (LengthBatchWindowProcessor
+// WindowState :302-350, TimeBatchWindowProcessor WindowState :376-418), the sliding window's
+// queue and every key's aggregator state (TimeWindowProcessor :196-222, the Sum/Avg/Count/Min/Max
+// State classes incl. the min/max deques), and the partition the window belongs to. The playback
+// clock and nextEmitTime travel with them, so a restored query continues exactly where the
+// snapshot was taken.
+//
+// Blob: "SHQ1" | u32 version | u64 descriptor fingerprint | u32 kind | sections (host scalars and
+// device buffers copied through the host, in a fixed order).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sh_internal.h"
+#include "sh_runtime.h"
+
+using namespace shd;
+
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+namespace {
+
+constexpr uint32_t kVersion = 1;
+
+struct Writer {
+    std::vector<uint8_t> b;
+    void put(const void* p, size_t n) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + n); }
+    template <typename T> void val(const T& x) { put(&x, sizeof(T)); }
+    int dev(const void* d, size_t n, hipStream_t s) {
+        val<uint64_t>(n);
+        size_t o = b.size();
+        b.resize(o + n);
+        if (n && (hipMemcpyAsync(b.data() + o, d, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess))
+            return sh_fail(SH_ERR_DEVICE, "snapshot: device read failed");
+        return SH_OK;
+    }
+};
+
+struct Reader {
+    const uint8_t* p;
+    size_t n, o = 0;
+    bool ok = true;
+    template <typename T> T val() {
+        T x{};
+        if (o + sizeof(T) > n) { ok = false; return x; }
+        std::memcpy(&x, p + o, sizeof(T));
+        o += sizeof(T);
+        return x;
+    }
+    // device section into `buf` (grown to at least `min_cap` bytes)
+    int dev(DevBuf& buf, size_t min_cap, hipStream_t s) {
+        uint64_t len = val<uint64_t>();
+        if (!ok || o + len > n) { ok = false; return sh_fail(SH_ERR_INVALID, "snapshot blob truncated"); }
+        RCHK(buf.reserve(std::max<size_t>({len, min_cap, 8}), false));
+        if (len && (hipMemcpyAsync(buf.p, p + o, len, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess))
+            return sh_fail(SH_ERR_DEVICE, "restore: device write failed");
+        o += len;
+        return SH_OK;
+    }
+};
+
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const uint8_t* c = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+    return h;
+}
+
+// the query's semantics: a blob only restores into a query built from the same descriptor
+uint64_t fingerprint(const sh_query* q) {
+    const sh_query_desc& d = q->d;
+    uint64_t h = 1469598103934665603ull;
+    int32_t ints[] = {d.n_cols, d.window, d.stream_current, d.has_start_time, d.n_group_by, d.n_aggs, d.current_on,
+                      d.expired_on, d.partition_col};
+    h = fnv(h, ints, sizeof(ints));
+    h = fnv(h, d.col_types, sizeof(int32_t) * d.n_cols);
+    h = fnv(h, &d.window_param, 8);
+    h = fnv(h, &d.start_time, 8);
+    h = fnv(h, d.group_by, sizeof(int32_t) * d.n_group_by);
+    h = fnv(h, d.aggs, sizeof(sh_agg_spec) * d.n_aggs);
+    h = fnv(h, &q->fp_orig.n, sizeof(int));
+    for (int i = 0; i < q->fp_orig.n; i++) {
+        const FilterOpD& o = q->fp_orig.ops[i];
+        int32_t oi[] = {o.op, o.type, o.col};
+        h = fnv(h, oi, sizeof(oi));
+        h = fnv(h, &o.ival, 8);
+        h = fnv(h, &o.dval, 8);
+    }
+    return h;
+}
+
+}  // namespace
+
+// ---- per-kind sections (batch windows: sh_window.cpp; sliding: sh_sliding.cpp) -----------------
+int batch_snapshot(sh_query* q, Writer& w);
+int batch_restore(sh_query* q, Reader& r);
+int sliding_snapshot(sh_query* q, Writer& w);
+int sliding_restore(sh_query* q, Reader& r);
+
+int batch_snapshot(sh_query* q, Writer& w) {
+    hipStream_t s = q->ctx->stream;
+    w.val<uint8_t>(q->clock_valid);
+    w.val<int64_t>(q->clock);
+    w.val<uint8_t>(q->e0_valid);
+    w.val<int64_t>(q->E0);
+    w.val<int64_t>(q->W_open);
+    w.val<uint8_t>(q->p0_known);
+    w.val<int64_t>(q->p0);
+    // group-key table: the queued events refer to its slots
+    w.val<uint8_t>(q->kt.dense);
+    w.val<uint64_t>(q->kt.size_);
+    RCHK(q->kt.check(s));
+    w.val<int64_t>(q->kt.n_keys);
+    RCHK(w.dev(q->kt.keys.p, q->kt.dense ? 0 : q->kt.size_ * 8, s));
+    // the open window's queued events (currentEventQueue / count)
+    const int64_t n = q->n_pend;
+    w.val<int64_t>(n);
+    RCHK(w.dev(q->pend_pos.p, n * 4, s));
+    RCHK(w.dev(q->pend_ts.p, n * 8, s));
+    w.val<int32_t>(q->ap.n_vcols);
+    for (int j = 0; j < q->ap.n_vcols; j++) RCHK(w.dev(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, n * 8, s));
+    return SH_OK;
+}
+
+int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend);
+int query_set_partition(sh_query* q, int64_t p0);
+
+int batch_restore(sh_query* q, Reader& r) {
+    hipStream_t s = q->ctx->stream;
+    q->clock_valid = r.val<uint8_t>();
+    q->clock = r.val<int64_t>();
+    q->e0_valid = r.val<uint8_t>();
+    q->E0 = r.val<int64_t>();
+    q->W_open = r.val<int64_t>();
+    bool p0k = r.val<uint8_t>();
+    int64_t p0 = r.val<int64_t>();
+    bool dense = r.val<uint8_t>();
+    uint64_t size = r.val<uint64_t>();
+    int64_t nk = r.val<int64_t>();
+    if (!r.ok || dense != q->kt.dense) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    // table of the snapshot's size, then its keys
+    int64_t n_pend_peek;
+    {
+        Reader t = r;
+        uint64_t klen = t.val<uint64_t>();
+        t.o += klen;
+        n_pend_peek = t.val<int64_t>();
+        if (!t.ok || n_pend_peek < 0) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    }
+    RCHK(query_resize_for_restore(q, size, n_pend_peek));
+    RCHK(r.dev(q->kt.keys, dense ? 8 : size * 8, s));
+    uint32_t ctrl[4] = {(uint32_t)nk, 0, 0, 0};
+    if (hipMemcpy(q->kt.ctrl.p, ctrl, 16, hipMemcpyHostToDevice) != hipSuccess)
+        return sh_fail(SH_ERR_DEVICE, "restore: key table counter");
+    q->kt.n_keys = nk;
+    const int64_t n = r.val<int64_t>();
+    q->n_pend = n;
+    // pending buffers were sized by query_resize_for_restore; copy the sections into them
+    DevBuf tmp;
+    RCHK(r.dev(tmp, 8, s));
+    if (n && hipMemcpy(q->pend_pos.p, tmp.p, n * 4, hipMemcpyDeviceToDevice) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
+    RCHK(r.dev(tmp, 8, s));
+    if (n && hipMemcpy(q->pend_ts.p, tmp.p, n * 8, hipMemcpyDeviceToDevice) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
+    int32_t nv = r.val<int32_t>();
+    if (nv != q->ap.n_vcols) { tmp.release(); return sh_fail(SH_ERR_INVALID, "snapshot does not match this query"); }
+    for (int j = 0; j < nv; j++) {
+        RCHK(r.dev(tmp, 8, s));
+        if (n && hipMemcpy(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, tmp.p, n * 8, hipMemcpyDeviceToDevice) !=
+                     hipSuccess)
+            return sh_fail(SH_ERR_DEVICE, "restore");
+    }
+    tmp.release();
+    if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    q->p0_known = false;
+    if (p0k) RCHK(query_set_partition(q, p0));
+    return SH_OK;
+}
+
+extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len) {
+    if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
+    if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
+    Writer w;
+    w.put("SHQ1", 4);
+    w.val<uint32_t>(kVersion);
+    w.val<uint64_t>(fingerprint(q));
+    w.val<uint32_t>((uint32_t)q->kind);
+    RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    *len = (int64_t)w.b.size();
+    if (buf) {
+        if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: buffer too small (call with buf=NULL for the size)");
+        std::memcpy(buf, w.b.data(), w.b.size());
+    }
+    return SH_OK;
+}
+
+extern "C" int sh_query_restore(sh_query* q, const void* buf, int64_t len) {
+    if (!q || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_query_restore: bad arguments");
+    Reader r{(const uint8_t*)buf, (size_t)len};
+    if (std::memcmp(buf, "SHQ1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip query snapshot");
+    r.o = 4;
+    if (r.val<uint32_t>() != kVersion) return sh_fail(SH_ERR_INVALID, "snapshot version mismatch");
+    if (r.val<uint64_t>() != fingerprint(q)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different query");
+    if (r.val<uint32_t>() != (uint32_t)q->kind) return sh_fail(SH_ERR_INVALID, "snapshot kind mismatch");
+    (void)hipStreamSynchronize(q->ctx->stream);
+    return q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
+}
+
+// ---- sliding window (state in SlidingImpl, sh_sliding.cpp) ---------------------------------------
+struct SlidingImpl;
+int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* scalars, int n_scalars,
+                          bool set, int64_t new_rc);
+
+int sliding_snapshot(sh_query* q, Writer& w) {
+    hipStream_t s = q->ctx->stream;
+    w.val<uint8_t>(q->clock_valid);
+    w.val<int64_t>(q->clock);
+    w.val<uint64_t>(q->kt.size_);
+    RCHK(q->kt.check(s));
+    w.val<int64_t>(q->kt.n_keys);
+    RCHK(w.dev(q->kt.keys.p, q->kt.dense ? 0 : q->kt.size_ * 8, s));
+    int64_t sc[4];
+    std::vector<std::pair<DevBuf*, size_t>> bufs;
+    RCHK(sliding_state_buffers(q, bufs, sc, 4, false, 0));
+    for (int i = 0; i < 4; i++) w.val<int64_t>(sc[i]);
+    for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+    return SH_OK;
+}
+
+int sliding_restore(sh_query* q, Reader& r) {
+    hipStream_t s = q->ctx->stream;
+    q->clock_valid = r.val<uint8_t>();
+    q->clock = r.val<int64_t>();
+    uint64_t size = r.val<uint64_t>();
+    int64_t nk = r.val<int64_t>();
+    if (!r.ok || size != q->kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    RCHK(r.dev(q->kt.keys, q->kt.dense ? 8 : size * 8, s));
+    uint32_t ctrl[4] = {(uint32_t)nk, 0, 0, 0};
+    if (hipMemcpy(q->kt.ctrl.p, ctrl, 16, hipMemcpyHostToDevice) != hipSuccess)
+        return sh_fail(SH_ERR_DEVICE, "restore: key table counter");
+    q->kt.n_keys = nk;
+    int64_t sc[4];
+    for (int i = 0; i < 4; i++) sc[i] = r.val<int64_t>();
+    if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    std::vector<std::pair<DevBuf*, size_t>> bufs;
+    RCHK(sliding_state_buffers(q, bufs, sc, 4, true, sc[1]));
+    for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+    if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    return SH_OK;
+}

@@ -85,6 +85,7 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
 }
 
 static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out);
+int query_set_partition(sh_query* q, int64_t key);
 
 // key partitions: smallest power of two whose per-partition LDS state (plus, when partitioned, the
 // record staging of k_aggregate_own) fits the budget that keeps two workgroups per CU
@@ -378,6 +379,13 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
         HIPCHK(hipMemcpy(&k32, (const char*)b->cols[pc] + first * 4, 4, hipMemcpyDeviceToHost));
         key = k32;
     }
+    return query_set_partition(q, key);
+}
+
+// Restrict the query to partition key p0 (the partition that armed the shared timer, R12).
+int query_set_partition(sh_query* q, int64_t key) {
+    int pc = q->d.partition_col;
+    int t = q->d.col_types[pc];
     q->p0 = key;
     q->p0_known = true;
     FilterProg fp = q->fp_orig;
@@ -388,6 +396,19 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
     if (q->fp_orig.n > 0) fp.ops[fp.n++] = FilterOpD{SH_OP_AND, 0, 0, 0, 0, 0.0};
     q->fp = fp;
     return SH_OK;
+}
+
+// sh_query_restore: a key table of the snapshot's size and room for its queued events.
+int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend) {
+    if (q->kt.dense) {
+        if (table_size != q->kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    } else if (table_size != q->kt.size_) {
+        q->kt.release();
+        RCHK(q->kt.init_size(table_size));
+    }
+    RCHK(size_partitions(q));
+    q->n_pend = 0;
+    return grow_pending(q, n_pend, 0);
 }
 
 static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {

@@ -127,6 +127,18 @@ class GpuQuery:
         _check(lib().sh_query_stats(self.h, C.byref(s)))
         return s
 
+    def snapshot(self) -> bytes:
+        """State.snapshot(): the query's device state as bytes (sh_query_snapshot)."""
+        n = C.c_int64()
+        _check(lib().sh_query_snapshot(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().sh_query_snapshot(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, blob: bytes):
+        """State.restore(): continue from a snapshot of a query built from the same descriptor."""
+        _check(lib().sh_query_restore(self.h, blob, len(blob)))
+
     def close(self):
         if self.h:
             lib().sh_query_destroy(self.h)
