@@ -76,6 +76,25 @@ def cpu_baseline(args):
                       f"{t_used:.1f} s single-thread in the C++ restatement (oracle/), not stock Siddhi (no JVM)"}
 
 
+def measured_traffic(args, sliced):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/r*_c2_*_pmc.json: FETCH_SIZE x 2 + WRITE_SIZE per launch, gfx950-corrected by
+    scripts/pmc_summary.py), valid for the default single-GPU configuration it was collected on."""
+    import glob
+    if sliced or args.batch != 1 << 25 or args.keys != 100_000 or args.key_type != "string" or args.send_size != 1:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c2_*_pmc.json")))
+    for f in reversed(files):
+        try:
+            ks = json.load(open(f))["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, v in ks.items():
+            if name.startswith("shd::k_aggregate_own"):
+                return v["hbm_bytes"]
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -161,6 +180,7 @@ def main():
     # roofline of the dominant kernel (k_aggregate): algorithmic bytes per launch / its HIP-event time
     n_launch = args.steps
     ach = (C2_BYTES_PER_EVENT * B * n_launch) / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
+    traffic = measured_traffic(args, sliced)
     result = {
         "metric": METRIC,
         "value": total_events / elapsed,
@@ -183,8 +203,8 @@ def main():
                    "parallelism": (f"slice ingest x{world}, key re-shard over RCCL all-to-all" if sliced
                                    else f"key-sharded x{world}"),
                    "flushes": flushes, "rows": rows},
-        "roofline": {"bound": "hbm", "kernel": "k_aggregate", "achieved": ach, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+        "roofline": {"bound": "hbm", "kernel": "k_aggregate_own", "achieved": ach, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms_per_step": kern_ms / args.steps,
                      "bytes_per_event": C2_BYTES_PER_EVENT},
     }
