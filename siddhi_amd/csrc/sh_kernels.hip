@@ -775,8 +775,14 @@ void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_
                        nblk);
 }
 
-// LDS: hist[P] (u32) | local_start[P] (u32) | running[P] (u32) | wave_cnt[4][P] (u32) |
-//      stage_pos[kTile] | stage_idx[kTile] | stage_p[kTile] | stage_vals[V][kTile] (u64)
+// Stable multisplit of one tile of kTile closed events into the P key partitions. Wave w takes
+// the tile's events [w*512, w*512+512) in 8 rounds of 64 (coalesced loads); an event's rank inside
+// its partition is the wave's running count for that partition plus its rank among the round's
+// lanes of the same partition (ballots over the partition bits). Waves never wait for each other
+// until the tile is ranked: one barrier, a scan over (partition, wave) gives every event its
+// staging slot (partition-major, event order inside a partition), and the staged tile is written
+// out as one contiguous run per partition.
+// LDS: run[4][P] (u16) | start[P] (u32) | stage_pos[kTile] | stage_idx[kTile] | stage_vals[V][kTile]
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
                                                       const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
@@ -784,105 +790,101 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     const int tile = xcd_tile(nblk);
     if (tile >= nblk) return;
+    constexpr int NW = kBlock / 64;
+    constexpr int PER_WAVE = kTile / NW;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     unsigned char* sm = smem_raw + ((16u - ((unsigned)(size_t)smem_raw & 15u)) & 15u);
     u64* stage_vals = (u64*)sm;
     u32* stage_pos = (u32*)(stage_vals + (size_t)ap.n_vcols * kTile);
     u32* stage_idx = stage_pos + kTile;
-    u32* stage_p = stage_idx + kTile;
-    u32* hist = stage_p + kTile;
-    u32* local_start = hist + P;
-    u32* running = local_start + P;
-    u32* wave_cnt = running + P;  // [4][P]
-    for (int i = threadIdx.x; i < P; i += kBlock) {
-        hist[i] = 0; running[i] = 0;
-        for (int w = 0; w < 4; w++) wave_cnt[w * P + i] = 0;
-    }
+    u32* start = stage_idx + kTile;
+    unsigned short* run = (unsigned short*)(start + P);  // [NW][P]
+    for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
     __syncthreads();
-    const i64 t0 = lo + (i64)tile * kTile;
-    // pass 1: histogram of this tile
-    u32 my_pos[kItems];
-    bool my_ok[kItems];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int bits = 0;
+    while ((1 << bits) < P) bits++;
+    const i64 t0 = lo + (i64)tile * kTile + (i64)w * PER_WAVE;
+    unsigned short* wrun = run + w * P;
+    u32 my_pos[kItems], my_rank[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
-        i64 e = t0 + (i64)r * kBlock + threadIdx.x;
-        my_ok[r] = false;
+        const i64 e = t0 + (i64)r * 64 + lane;
+        bool ok = false;
+        u32 pos = 0;
         if (e < hi) {
             EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
-            my_ok[r] = ev.ok;
-            my_pos[r] = ev.pos;
-            if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
+            ok = ev.ok;
+            pos = ev.pos;
         }
+        const u32 p = ok ? (pos & (P - 1)) : 0;
+        u64 peers = __ballot(ok);
+        for (int bt = 0; bt < bits; bt++) {
+            const bool bit = (p >> bt) & 1;
+            const u64 m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const u32 lr = (u32)__popcll(peers & lt_mask);
+        u32 base = ok ? wrun[p] : 0;  // the wave's LDS operations complete in program order
+        if (ok && lr == 0) wrun[p] = (unsigned short)(base + __popcll(peers));
+        my_pos[r] = ok ? pos : kNoPos;
+        my_rank[r] = base + lr;
     }
     __syncthreads();
-    // exclusive scan of hist -> local_start (each thread scans a contiguous chunk of P)
+    // partition starts in the tile (p-major), then each wave's offset inside its partition
+    __shared__ u32 s_total;
     {
         int per = (P + kBlock - 1) / kBlock;
         int a = threadIdx.x * per, b = min(P, a + per);
         i64 sum = 0;
-        for (int i = a; i < b; i++) sum += hist[i];
-        i64 pre = block_excl_scan(sum, SumOp(), 0, nullptr);
-        for (int i = a; i < b; i++) { local_start[i] = (u32)pre; pre += hist[i]; }
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const u64 lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int bits = 0;
-    while ((1 << bits) < P) bits++;
-    // pass 2: ordered ranks per sub-round of kBlock events
-    for (int r = 0; r < kItems; r++) {
-        bool ok = my_ok[r];
-        u32 p = ok ? (my_pos[r] & (P - 1)) : 0;
-        u64 peers = __ballot(ok);
-        for (int bt = 0; bt < bits; bt++) {
-            u64 m = __ballot((p >> bt) & 1);
-            peers &= ((p >> bt) & 1) ? m : ~m;
-        }
-        u32 lrank = __popcll(peers & lt_mask);
-        bool leader = ok && lrank == 0;
-        if (leader) wave_cnt[wave * P + p] = __popcll(peers);
-        __syncthreads();
-        if (ok) {
-            u32 before = running[p];
-            for (int w = 0; w < wave; w++) before += wave_cnt[w * P + p];
-            u32 slot = local_start[p] + before + lrank;
-            i64 e = t0 + (i64)r * kBlock + threadIdx.x;
-            stage_pos[slot] = my_pos[r];
-            stage_idx[slot] = (u32)e;
-            stage_p[slot] = p;
-            if (e < n_pend) {
-                for (int j = 0; j < ap.n_vcols; j++) stage_vals[(size_t)j * kTile + slot] = pend_vals[(size_t)j * pend_cap + e];
-            } else {
-                for (int j = 0; j < ap.n_vcols; j++)
-                    stage_vals[(size_t)j * kTile + slot] = (u64)load_raw(cols, ap.vcol_src[j], e - n_pend);
+        for (int i = a; i < b; i++)
+            for (int x = 0; x < NW; x++) sum += run[x * P + i];
+        i64 tot;
+        i64 pre = block_excl_scan(sum, SumOp(), 0, &tot);
+        if (threadIdx.x == 0) s_total = (u32)tot;
+        for (int i = a; i < b; i++) {
+            const i64 st = pre;
+            start[i] = (u32)st;
+            for (int x = 0; x < NW; x++) {
+                u32 c = run[x * P + i];
+                run[x * P + i] = (unsigned short)(pre - st);  // wave x's offset inside partition i
+                pre += c;
             }
         }
-        __syncthreads();
-        if (leader) { atomicAdd(&running[p], wave_cnt[wave * P + p]); wave_cnt[wave * P + p] = 0; }
-        __syncthreads();
     }
-    // pass 3: write each partition's run of this tile contiguously
-    i64 total = 0;
-    for (int i = 0; i < P; i++) {}
-    u32 n_tile = 0;
-    {
-        // total valid = local_start[P-1] + hist[P-1]
-        n_tile = local_start[P - 1] + hist[P - 1];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kItems; r++) {
+        if (my_pos[r] == kNoPos) continue;
+        const u32 p = my_pos[r] & (P - 1);
+        const u32 slot = start[p] + wrun[p] + my_rank[r];
+        const i64 e = t0 + (i64)r * 64 + lane;
+        stage_pos[slot] = my_pos[r];
+        stage_idx[slot] = (u32)e;
+        if (e < n_pend) {
+            for (int j = 0; j < ap.n_vcols; j++) stage_vals[(size_t)j * kTile + slot] = pend_vals[(size_t)j * pend_cap + e];
+        } else {
+            for (int j = 0; j < ap.n_vcols; j++)
+                stage_vals[(size_t)j * kTile + slot] = (u64)load_raw(cols, ap.vcol_src[j], e - n_pend);
+        }
     }
+    __syncthreads();
+    // write every partition's run of this tile contiguously
+    const u32 n_tile = s_total;
     for (u32 j = threadIdx.x; j < n_tile; j += kBlock) {
-        u32 p = stage_p[j];
-        i64 dst = offsets[(i64)p * nblk + tile] + (j - local_start[p]);
+        const u32 pp = stage_pos[j] & (P - 1);
+        const i64 dst = offsets[(i64)pp * nblk + tile] + (j - start[pp]);
         rec_pos[dst] = stage_pos[j];
         rec_idx[dst] = stage_idx[j];
         for (int v = 0; v < ap.n_vcols; v++) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
     }
-    (void)total;
 }
 
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
                        i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
-    size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 12 + (size_t)P * 4 * 7 + 16;
+    size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + (size_t)P * 2 * (kBlock / 64) + 32;
     int grid = ((nblk + 7) >> 3) * 8;
     hipLaunchKernelGGL(k_ms_scatter, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
                        new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);

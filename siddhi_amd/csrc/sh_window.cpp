@@ -98,8 +98,8 @@ static int size_partitions(sh_query* q) {
         return p == 1 ? (size_t)nl * (16 + 8 * (size_t)q->ap.n_fields) + 16
                       : aggregate_own_lds(nl, q->ap.n_fields, q->ap.n_vcols);
     };
-    while (need(P) > budget && P < (1 << 14)) P <<= 1;
-    if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large");
+    while (need(P) > budget && P < 4096) P <<= 1;
+    if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
     q->P = P;
     q->logP = 0;
     while ((1 << q->logP) < P) q->logP++;
