@@ -20,6 +20,44 @@ __device__ __forceinline__ i64 load_raw(const ColSet& cs, int c, i64 e) {
     }
 }
 
+// kItems consecutive 8-byte values p[base..base+kItems) of one thread's blocked run: four 16-byte
+// loads when the run is aligned and inside [0, N), else element loads (`fill` past N).
+__device__ __forceinline__ void load_items_i64(const i64* __restrict__ p, i64 base, i64 N, i64 (&out)[kItems],
+                                               i64 fill) {
+    if (base + kItems <= N && (((size_t)(p + base)) & 15) == 0) {
+        const longlong2* q = (const longlong2*)(p + base);
+#pragma unroll
+        for (int j = 0; j < kItems / 2; j++) {
+            longlong2 v = q[j];
+            out[2 * j] = v.x;
+            out[2 * j + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) out[j] = base + j < N ? p[base + j] : fill;
+    }
+}
+
+// Raw values of column c for one thread's kItems consecutive events (vector loads for 4- and
+// 8-byte integral columns when aligned; load_raw otherwise).
+__device__ __forceinline__ void load_items_raw(const ColSet& cs, int c, i64 base, i64 N, i64 (&out)[kItems]) {
+    const int t = cs.type[c];
+    if ((t == SH_T_INT || t == SH_T_STRID) && base + kItems <= N &&
+        (((size_t)((const int*)cs.ptr[c] + base)) & 15) == 0) {
+        const int4* q = (const int4*)((const int*)cs.ptr[c] + base);
+#pragma unroll
+        for (int j = 0; j < kItems / 4; j++) {
+            int4 v = q[j];
+            out[4 * j] = v.x; out[4 * j + 1] = v.y; out[4 * j + 2] = v.z; out[4 * j + 3] = v.w;
+        }
+    } else if (t == SH_T_LONG) {
+        load_items_i64((const i64*)cs.ptr[c], base, N, out, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) out[j] = base + j < N ? load_raw(cs, c, base + j) : 0;
+    }
+}
+
 // Java (long) cast of a double (JLS 5.1.3): NaN -> 0, saturating, truncation toward zero
 __device__ __forceinline__ i64 java_d2l(double x) {
     if (x != x) return 0;

@@ -20,13 +20,15 @@ __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts,
                                                     WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     i64 cnt = 0, tl = INT64_MIN, first = INT64_MAX;
+    i64 tsv[kItems];
+    load_items_i64(ts, base, wp.N, tsv, INT64_MIN);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
             if (eval_filter(f, cols, e)) { cnt++; if (first == INT64_MAX) first = e; }
-            if (sc.last(wp, e)) tl = max(tl, ts[e]);
+            if (sc.last(wp, e)) tl = max(tl, tsv[i]);
         }
         sc.next();
     }
@@ -57,7 +59,19 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
     int per = (nblk + 1023) / 1024;
     int lo = t * per, hi = min(nblk, lo + per);
     i64 s = 0, m = INT64_MIN, mn = INT64_MAX;
-    for (int i = lo; i < hi; i++) { s += blk_pass[i]; m = max(m, blk_tl[i]); mn = min(mn, blk_first[i]); }
+    // 8 tiles at a time so the loads of a thread's run are in flight together
+    for (int i0 = lo; i0 < hi; i0 += 8) {
+        i64 a[8], b[8], c[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int i = i0 + j;
+            a[j] = i < hi ? blk_pass[i] : 0;
+            b[j] = i < hi ? blk_tl[i] : INT64_MIN;
+            c[j] = i < hi ? blk_first[i] : INT64_MAX;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) { s += a[j]; m = max(m, b[j]); mn = min(mn, c[j]); }
+    }
     sh_sum[t] = s; sh_max[t] = m; sh_min[t] = mn;
     __syncthreads();
     // Hillis-Steele inclusive scans over 1024 partials
@@ -75,10 +89,18 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
     }
     i64 run_s = t > 0 ? sh_sum[t - 1] : 0;
     i64 run_m = t > 0 ? sh_max[t - 1] : INT64_MIN;
-    for (int i = lo; i < hi; i++) {
-        i64 c = blk_pass[i], x = blk_tl[i];
-        blk_pass[i] = run_s; blk_tl[i] = run_m;
-        run_s += c; run_m = max(run_m, x);
+    for (int i0 = lo; i0 < hi; i0 += 8) {
+        i64 a[8], b[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[j] = i0 + j < hi ? blk_pass[i0 + j] : 0;
+            b[j] = i0 + j < hi ? blk_tl[i0 + j] : INT64_MIN;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (i0 + j < hi) { blk_pass[i0 + j] = run_s; blk_tl[i0 + j] = run_m; }
+            run_s += a[j]; run_m = max(run_m, b[j]);
+        }
     }
     __syncthreads();
     if (t == 0) {
@@ -139,12 +161,12 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     bool pass[kItems];
     i64 t[kItems];
     i64 cnt = 0, tl = INT64_MIN;
+    load_items_i64(ts, base, wp.N, t, INT64_MIN);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         bool in = e < wp.N;
-        t[i] = in ? ts[e] : INT64_MIN;
         pass[i] = in && eval_filter(f, cols, e);
         cnt += pass[i];
         if (in && sc.last(wp, e)) tl = max(tl, t[i]);
@@ -155,8 +177,15 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     {
         u64 key[kItems];
         u32 pos[kItems];
+        if (kp.n == 1 && kp.div[0] == 0) {
+            i64 raw[kItems];
+            load_items_raw(cols, kp.col[0], base, wp.N, raw);
 #pragma unroll
-        for (int i = 0; i < kItems; i++) key[i] = pass[i] ? make_key(kp, cols, base + i) : 0;
+            for (int i = 0; i < kItems; i++) key[i] = pass[i] ? (u64)raw[i] : 0;
+        } else {
+#pragma unroll
+            for (int i = 0; i < kItems; i++) key[i] = pass[i] ? make_key(kp, cols, base + i) : 0;
+        }
         key_slots<kItems>(kt, key, pass, pos);
 #pragma unroll
         for (int i = 0; i < kItems; i++)
