@@ -52,69 +52,68 @@ void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i6
 // call: nextEmitTime = now + T, or getNextEmitTime(now) when start.time is given
 // (TimeBatchWindowProcessor.java:266-276, 342-347).
 // ================================================================================================
+// 1024-thread exclusive scans of the tile partials, in coalesced passes of 1024 elements
+// (thread t takes element c*1024 + t) carrying the running totals between passes.
+struct Scan3 {
+    i64 s, m, mn;  // sum, max, min
+};
+__device__ __forceinline__ Scan3 block1024_excl(Scan3 v, Scan3* tot) {
+    __shared__ i64 w_sum[16], w_max[16], w_min[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const i64 si = wave_incl_scan(v.s, SumOp());
+    const i64 mi = wave_incl_scan(v.m, MaxOp());
+    const i64 ni = wave_incl_scan(v.mn, MinOp());
+    if (lane == 63) { w_sum[wv] = si; w_max[wv] = mi; w_min[wv] = ni; }
+    __syncthreads();
+    Scan3 pre{0, INT64_MIN, INT64_MAX}, all{0, INT64_MIN, INT64_MAX};
+    for (int x = 0; x < 16; x++) {
+        if (x < wv) { pre.s += w_sum[x]; pre.m = max(pre.m, w_max[x]); }
+        all.s += w_sum[x]; all.m = max(all.m, w_max[x]); all.mn = min(all.mn, w_min[x]);
+    }
+    __syncthreads();
+    i64 mex = __shfl_up(mi, 1, 64);
+    if (lane == 0) mex = INT64_MIN;
+    *tot = all;
+    return Scan3{pre.s + si - v.s, max(pre.m, mex), 0};
+}
+
 __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk,
                                                      const i64* __restrict__ ts, WinParams wp, PushInfo* info) {
-    __shared__ i64 sh_sum[1024], sh_max[1024], sh_min[1024];
-    int t = threadIdx.x;
-    int per = (nblk + 1023) / 1024;
-    int lo = t * per, hi = min(nblk, lo + per);
-    i64 s = 0, m = INT64_MIN, mn = INT64_MAX;
-    // 8 tiles at a time so the loads of a thread's run are in flight together
-    for (int i0 = lo; i0 < hi; i0 += 8) {
-        i64 a[8], b[8], c[8];
+    const int t = threadIdx.x;
+    constexpr int G = 4;  // passes whose loads are issued together (the scans then run back to back)
+    i64 tot_s = 0, tot_m = INT64_MIN, tot_mn = INT64_MAX;
+    for (int g0 = 0; g0 < nblk; g0 += G * 1024) {
+        i64 vs[G], vm[G], vn[G];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int i = i0 + j;
-            a[j] = i < hi ? blk_pass[i] : 0;
-            b[j] = i < hi ? blk_tl[i] : INT64_MIN;
-            c[j] = i < hi ? blk_first[i] : INT64_MAX;
+        for (int g = 0; g < G; g++) {
+            const int i = min(g0 + g * 1024 + t, nblk - 1);
+            vs[g] = blk_pass[i]; vm[g] = blk_tl[i]; vn[g] = blk_first[i];
         }
 #pragma unroll
-        for (int j = 0; j < 8; j++) { s += a[j]; m = max(m, b[j]); mn = min(mn, c[j]); }
-    }
-    sh_sum[t] = s; sh_max[t] = m; sh_min[t] = mn;
-    __syncthreads();
-    // Hillis-Steele inclusive scans over 1024 partials
-    for (int d = 1; d < 1024; d <<= 1) {
-        i64 a = t >= d ? sh_sum[t - d] : 0;
-        i64 b = t >= d ? sh_max[t - d] : INT64_MIN;
-        __syncthreads();
-        sh_sum[t] += a;
-        sh_max[t] = max(sh_max[t], b);
-        __syncthreads();
-    }
-    for (int d = 512; d > 0; d >>= 1) {
-        if (t < d) sh_min[t] = min(sh_min[t], sh_min[t + d]);
-        __syncthreads();
-    }
-    i64 run_s = t > 0 ? sh_sum[t - 1] : 0;
-    i64 run_m = t > 0 ? sh_max[t - 1] : INT64_MIN;
-    for (int i0 = lo; i0 < hi; i0 += 8) {
-        i64 a[8], b[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            a[j] = i0 + j < hi ? blk_pass[i0 + j] : 0;
-            b[j] = i0 + j < hi ? blk_tl[i0 + j] : INT64_MIN;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            if (i0 + j < hi) { blk_pass[i0 + j] = run_s; blk_tl[i0 + j] = run_m; }
-            run_s += a[j]; run_m = max(run_m, b[j]);
+        for (int g = 0; g < G; g++) {
+            const int i = g0 + g * 1024 + t;
+            if (g0 + g * 1024 >= nblk) break;
+            const bool in = i < nblk;
+            Scan3 v{in ? vs[g] : 0, in ? vm[g] : INT64_MIN, in ? vn[g] : INT64_MAX};
+            Scan3 all;
+            Scan3 ex = block1024_excl(v, &all);
+            if (in) { blk_pass[i] = tot_s + ex.s; blk_tl[i] = max(tot_m, ex.m); }
+            tot_s += all.s; tot_m = max(tot_m, all.m); tot_mn = min(tot_mn, all.mn);
         }
     }
     __syncthreads();
     if (t == 0) {
-        info->total_pass = sh_sum[1023];
-        info->max_tl = sh_max[1023];
-        info->first_pass = sh_min[0];
+        info->total_pass = tot_s;
+        info->max_tl = tot_m;
+        info->first_pass = tot_mn;
         info->e0_valid = wp.e0_valid;
         info->E0 = wp.E0;
         info->n_bounds = 0;
         info->first_clk = INT64_MIN;
         const bool init_e0 = wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && !wp.wcol;
-        if (sh_min[0] != INT64_MAX && (init_e0 || wp.want_first_clk)) {
+        if (tot_mn != INT64_MAX && (init_e0 || wp.want_first_clk)) {
             // clock of the send that carries the first passing event (before the carried-in clock)
-            i64 e0 = sh_min[0];
+            i64 e0 = tot_mn;
             i64 sl = wp.send_size > 0 ? wp.send_size : wp.N;
             i64 start = (e0 / sl) * sl;
             i64 last = min(wp.N - 1, start + sl - 1);
@@ -631,22 +630,25 @@ void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* b
 }
 
 __global__ __launch_bounds__(1024) void k_scan_sum(i64* a, int n) {
-    __shared__ i64 sh[1024];
-    int t = threadIdx.x;
-    int per = (n + 1023) / 1024;
-    int lo = t * per, hi = min(n, lo + per);
-    i64 s = 0;
-    for (int i = lo; i < hi; i++) s += a[i];
-    sh[t] = s;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        i64 x = t >= d ? sh[t - d] : 0;
-        __syncthreads();
-        sh[t] += x;
-        __syncthreads();
+    if (n <= 0) return;
+    constexpr int G = 8;
+    i64 run = 0;
+    for (int g0 = 0; g0 < n; g0 += G * 1024) {
+        i64 va[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) va[g] = a[min(g0 + g * 1024 + (int)threadIdx.x, n - 1)];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            if (g0 + g * 1024 >= n) break;
+            const int i = g0 + g * 1024 + threadIdx.x;
+            const bool in = i < n;
+            Scan3 v{in ? va[g] : 0, INT64_MIN, INT64_MAX};
+            Scan3 all;
+            Scan3 ex = block1024_excl(v, &all);
+            if (in) a[i] = run + ex.s;
+            run += all.s;
+        }
     }
-    i64 run = t > 0 ? sh[t - 1] : 0;
-    for (int i = lo; i < hi; i++) { i64 c = a[i]; a[i] = run; run += c; }
 }
 
 void launch_scan_sum(hipStream_t s, i64* a, int n) {
