@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 1
+#define SH_ABI_VERSION 2
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -77,6 +77,8 @@ typedef struct {
 #define SH_WIN_LENGTH_BATCH 1 /* core/query/processor/stream/window/LengthBatchWindowProcessor.java */
 #define SH_WIN_TIME_BATCH 2   /* core/query/processor/stream/window/TimeBatchWindowProcessor.java   */
 #define SH_WIN_TIME 3         /* core/query/processor/stream/window/TimeWindowProcessor.java        */
+#define SH_WIN_EXT_TIME_BATCH 4 /* core/query/processor/stream/window/ExternalTimeBatchWindowProcessor.java:
+                                   externalTimeBatch(ts_col, T[, start]) — event-time batches, no timeout */
 
 /* ---- aggregators: core/query/selector/attribute/aggregator/ [Sum,Avg,Count,Min,Max]AttributeAggregatorExecutor ---- */
 #define SH_AGG_SUM 1
@@ -107,7 +109,8 @@ typedef struct {
     int32_t window;         /* SH_WIN_*                                                 */
     int32_t stream_current; /* lengthBatch/timeBatch `stream.current.event` flag        */
     int64_t window_param;   /* lengthBatch: length; timeBatch/time: milliseconds        */
-    int32_t has_start_time; /* timeBatch(T, start)                                       */
+    int32_t has_start_time; /* timeBatch(T, start) / externalTimeBatch(.., T, start): 1 = constant
+                               start_time; 2 = externalTimeBatch start from attribute start_col */
     int32_t n_group_by;     /* 0..SH_MAX_GROUP                                           */
     int64_t start_time;
     int32_t group_by[SH_MAX_GROUP];
@@ -117,6 +120,8 @@ typedef struct {
     int32_t expired_on;     /* insert [expired|all] events                               */
     int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`     */
     int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing)  */
+    int32_t ts_col;         /* externalTimeBatch: the LONG timestamp attribute               */
+    int32_t start_col;      /* externalTimeBatch: LONG start-time attribute (has_start_time 2) */
 } sh_query_desc;
 
 /* ---- incremental aggregation: core/aggregation/ + util/parser/AggregationParser.java ---- */

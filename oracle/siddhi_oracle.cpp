@@ -388,6 +388,11 @@ struct PartitionState {
     std::vector<std::unordered_map<GKey, std::unique_ptr<AggState>, GKeyHash>> agg_states;
     // Scheduler.SchedulerState (core/util/Scheduler.java:330-367): toNotifyQueue
     std::deque<int64_t> notify_queue;
+    // ExternalTimeBatchWindowProcessor.WindowState (:495-517): endTime = -1, startTime = the constant
+    // start (commonStartTime, 0 when absent), lastCurrentEventTime = 0 (Java default)
+    int64_t ext_end = -1, ext_start = 0, ext_last = 0;
+    Chunk ext_current, ext_expired;
+    bool ext_has_reset = false; OEvent ext_reset;
 };
 
 struct Query {
@@ -412,6 +417,7 @@ struct Query {
         if (it != parts.end()) return *it->second;
         auto ps = std::unique_ptr<PartitionState>(new PartitionState());
         ps->agg_states.resize(aggs.size());
+        if (d.window == SH_WIN_EXT_TIME_BATCH && d.has_start_time == 1) ps->ext_start = d.start_time;
         PartitionState& r = *ps;
         parts.emplace(key, std::move(ps));
         part_order.push_back(key);
@@ -596,8 +602,70 @@ struct Query {
         selector(ps, outc);
     }
 
+    // ExternalTimeBatchWindowProcessor.process (:238-311) without a timeout (no TIMER events reach it):
+    // initTiming (:313-334), flushToOutputChunk (:336-383), findEndTime (:440-444), cloneAppend
+    // (:446-456). Every batch an event closes is its own downstream chunk, emitted after the whole
+    // incoming chunk is consumed (:308-310).
+    int64_t ext_attr(const OEvent& e, int col) const { return e.raw[col]; }
+    static int64_t find_end_time(int64_t current, int64_t start, int64_t T) {
+        int64_t elapsed = (current - start) % T;  // Java % truncates like C++
+        return current + (T - elapsed);
+    }
+    void ext_flush(PartitionState& ps, std::vector<Chunk>& outs, int64_t current_time) {
+        Chunk c;
+        if (output_expects_expired && !ps.ext_expired.empty()) {
+            for (auto& x : ps.ext_expired) { x.ts = current_time; c.push_back(x); }
+        }
+        ps.ext_expired.clear();
+        if (!ps.ext_current.empty()) {
+            ps.ext_reset.ts = current_time;
+            c.push_back(ps.ext_reset);
+            ps.ext_has_reset = false;
+            if (output_expects_expired)
+                for (auto& e : ps.ext_current) { OEvent x = e; x.type = EXPIRED; ps.ext_expired.push_back(x); }
+            for (auto& e : ps.ext_current) c.push_back(e);
+        }
+        ps.ext_current.clear();
+        if (!c.empty()) outs.push_back(std::move(c));
+    }
+    void ext_append(PartitionState& ps, const OEvent& ev) {
+        ps.ext_current.push_back(ev);
+        if (!ps.ext_has_reset) { ps.ext_reset = ev; ps.ext_reset.type = RESET; ps.ext_has_reset = true; }
+    }
+    void ext_time_batch(PartitionState& ps, Chunk& in) {
+        if (in.empty()) return;
+        const int64_t T = d.window_param;
+        if (ps.ext_end < 0) {
+            const OEvent& f = in.front();
+            if (d.has_start_time == 1) {
+                ps.ext_end = find_end_time(ext_attr(f, d.ts_col), ps.ext_start, T);
+            } else if (d.has_start_time == 2) {
+                ps.ext_start = ext_attr(f, d.start_col);
+                ps.ext_end = ps.ext_start + T;
+            } else {
+                ps.ext_start = ext_attr(f, d.ts_col);
+                ps.ext_end = ps.ext_start + T;
+            }
+        }
+        std::vector<Chunk> outs;
+        for (OEvent& ev : in) {
+            if (ev.type != CURRENT) continue;
+            int64_t t = ext_attr(ev, d.ts_col);
+            if (ps.ext_last < t) ps.ext_last = t;
+            if (t < ps.ext_end) {
+                ext_append(ps, ev);
+            } else {
+                ext_flush(ps, outs, ps.ext_last);
+                ps.ext_end = find_end_time(ps.ext_last, ps.ext_start, T);
+                ext_append(ps, ev);
+            }
+        }
+        for (auto& c : outs) selector(ps, c);
+    }
+
     void window(PartitionState& ps, Chunk& c) {
         switch (d.window) {
+            case SH_WIN_EXT_TIME_BATCH: ext_time_batch(ps, c); break;
             case SH_WIN_NONE: { Chunk k; for (auto& e : c) if (e.type != TIMER) k.push_back(e); if (!k.empty()) selector(ps, k); break; }
             case SH_WIN_LENGTH_BATCH: length_batch(ps, c); break;
             case SH_WIN_TIME_BATCH: time_batch(ps, c); break;
@@ -969,7 +1037,7 @@ void* or_query_create(const sh_query_desc* desc) {
         desc->n_aggs > SH_MAX_AGGS || desc->n_group_by < 0 || desc->n_group_by > SH_MAX_GROUP) {
         g_err = "invalid descriptor"; return nullptr;
     }
-    if (desc->window < SH_WIN_NONE || desc->window > SH_WIN_TIME) { g_err = "bad window"; return nullptr; }
+    if (desc->window < SH_WIN_NONE || desc->window > SH_WIN_EXT_TIME_BATCH) { g_err = "bad window"; return nullptr; }
     Query* q = new Query();
     q->d = *desc;
     q->schema.n = desc->n_cols;

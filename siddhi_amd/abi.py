@@ -27,7 +27,7 @@ NP_DTYPE = {INT: np.int32, LONG: np.int64, FLOAT: np.float32, DOUBLE: np.float64
 OP_COL, OP_CONST, OP_GT, OP_GE, OP_LT, OP_LE, OP_EQ, OP_NE, OP_AND, OP_OR, OP_NOT = range(1, 12)
 CMP_OPS = {">": OP_GT, ">=": OP_GE, "<": OP_LT, "<=": OP_LE, "==": OP_EQ, "!=": OP_NE}
 
-WIN_NONE, WIN_LENGTH_BATCH, WIN_TIME_BATCH, WIN_TIME = 0, 1, 2, 3
+WIN_NONE, WIN_LENGTH_BATCH, WIN_TIME_BATCH, WIN_TIME, WIN_EXT_TIME_BATCH = 0, 1, 2, 3, 4
 AGG_SUM, AGG_AVG, AGG_COUNT, AGG_MIN, AGG_MAX = 1, 2, 3, 4, 5
 AGG_NAMES = {"sum": AGG_SUM, "avg": AGG_AVG, "count": AGG_COUNT, "min": AGG_MIN, "max": AGG_MAX}
 DUR_SECONDS, DUR_MINUTES, DUR_HOURS, DUR_DAYS, DUR_MONTHS, DUR_YEARS = range(6)
@@ -52,7 +52,7 @@ class QueryDesc(C.Structure):
                 ("has_start_time", C.c_int32), ("n_group_by", C.c_int32), ("start_time", C.c_int64),
                 ("group_by", C.c_int32 * MAX_GROUP), ("n_aggs", C.c_int32), ("current_on", C.c_int32),
                 ("aggs", AggSpec * MAX_AGGS), ("expired_on", C.c_int32), ("partition_col", C.c_int32),
-                ("key_capacity", C.c_int64)]
+                ("key_capacity", C.c_int64), ("ts_col", C.c_int32), ("start_col", C.c_int32)]
 
 
 class AggregationDesc(C.Structure):
@@ -169,6 +169,8 @@ class QuerySpec:
     output: str = "current"          # 'current' | 'all' | 'expired'
     partition: Optional[str] = None
     key_capacity: int = 0
+    ts_attr: Optional[str] = None      # externalTimeBatch timestamp attribute
+    start_attr: Optional[str] = None   # externalTimeBatch start time from this attribute
     _keep: list = field(default_factory=list, repr=False)
 
     def desc(self) -> QueryDesc:
@@ -182,7 +184,7 @@ class QuerySpec:
         d.n_filter_ops = len(fops)
         d.filter = C.cast(arr, C.POINTER(FilterOp))
         d.window = {None: WIN_NONE, "lengthBatch": WIN_LENGTH_BATCH, "timeBatch": WIN_TIME_BATCH,
-                    "time": WIN_TIME}[self.window]
+                    "time": WIN_TIME, "externalTimeBatch": WIN_EXT_TIME_BATCH}[self.window]
         d.window_param = self.param
         d.stream_current = int(self.stream_current)
         d.has_start_time = int(self.start_time is not None)
@@ -198,6 +200,10 @@ class QuerySpec:
         d.expired_on = int(self.output in ("expired", "all"))
         d.partition_col = self.schema.col(self.partition) if self.partition else -1
         d.key_capacity = self.key_capacity
+        d.ts_col = self.schema.col(self.ts_attr) if self.ts_attr else 0
+        d.start_col = self.schema.col(self.start_attr) if self.start_attr else 0
+        if self.start_attr:
+            d.has_start_time = 2
         return d
 
 

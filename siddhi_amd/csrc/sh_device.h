@@ -331,9 +331,14 @@ struct SendCursor {
     __device__ __forceinline__ void next() { if (++r == s) r = 0; }
 };
 
+// Window number of an event. lengthBatch: from the passing-event count; timeBatch: from the
+// playback clock; externalTimeBatch: `clock` is the running max M of the timestamp attribute and
+// E0 the start time — the batch end is findEndTime(M) = E0 + T * ((M - E0) / T + 1)
+// (ExternalTimeBatchWindowProcessor :440-444), so the window is (M - E0) / T.
 __device__ __forceinline__ i64 wfun(const WinParams& wp, i64 E0, int e0_valid, i64 pcb, i64 clock) {
     if (wp.kind == SH_WIN_LENGTH_BATCH) return (wp.n_pend + pcb) / wp.L;
     if (!e0_valid) return wp.W_open;
+    if (wp.kind == SH_WIN_EXT_TIME_BATCH) return clock < E0 ? 0 : (clock - E0) / wp.T;
     return clock < E0 ? 0 : (clock - E0) / wp.T + 1;
 }
 
@@ -345,6 +350,7 @@ struct WinCursor {
         W = wfun(wp, E0, e0v, pcb, clk);
         if (wp.kind == SH_WIN_LENGTH_BATCH) lim = (W + 1) * wp.L - wp.n_pend;
         else if (!e0v) lim = INT64_MAX;
+        else if (wp.kind == SH_WIN_EXT_TIME_BATCH) lim = E0 + (W + 1) * wp.T;
         else lim = E0 + W * wp.T;
     }
     __device__ __forceinline__ i64 at(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {

@@ -105,6 +105,10 @@ struct WinParams {
     i64 W_base;
     int want_first_clk;  // sharded summary: report PushInfo.first_clk
     int pad2;
+    // externalTimeBatch: window of an event = bucket (from the start time E0) of the running max of
+    // the ts_col attribute over the events reaching the window; xm0 = that max before the push
+    int ts_col, start_col;
+    i64 xm0;
 };
 
 // Result of the block-aggregate scan (written by k_scan_blocks, read back by the host).
@@ -116,7 +120,9 @@ struct PushInfo {
     int e0_valid;
     int n_bounds;      // boundaries appended by k_boundaries
     i64 first_clk;     // clock of the first passing event's send, before the carried-in clock
-    i64 pad;
+    i64 max_xm;        // externalTimeBatch: max of the timestamp attribute over passing events
+    int err;           // externalTimeBatch: first event before its start time
+    int pad;
 };
 
 // A window boundary inside the push: first combined index of a new window.
@@ -144,12 +150,12 @@ struct RowTmp {
 
 // Launchers (sh_kernels.hip).
 void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
-                     i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk);
+                     i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, i64* blk_xm = nullptr, int ts_col = -1);
 void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
-                        WinParams wp, PushInfo* info);
+                        WinParams wp, PushInfo* info, i64* blk_xm = nullptr, ColSet cols = ColSet{});
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos);
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr);
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, RowTmp* rows, u64* row_vals,

@@ -17,9 +17,10 @@ namespace shd {
 // the max timestamp over send-last events and the first passing event.
 // ================================================================================================
 __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts, ColSet cols, FilterProg f,
-                                                    WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first) {
+                                                    WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first,
+                                                    i64* blk_xm) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
-    i64 cnt = 0, tl = INT64_MIN, first = INT64_MAX;
+    i64 cnt = 0, tl = INT64_MIN, first = INT64_MAX, xm = INT64_MIN;
     i64 tsv[kItems];
     load_items_i64(ts, base, wp.N, tsv, INT64_MIN);
     SendCursor sc(wp, base);
@@ -27,7 +28,11 @@ __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts,
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
-            if (eval_filter(f, cols, e)) { cnt++; if (first == INT64_MAX) first = e; }
+            if (eval_filter(f, cols, e)) {
+                cnt++;
+                if (first == INT64_MAX) first = e;
+                if (blk_xm) xm = max(xm, load_raw(cols, wp.ts_col, e));
+            }
             if (sc.last(wp, e)) tl = max(tl, tsv[i]);
         }
         sc.next();
@@ -35,15 +40,21 @@ __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts,
     i64 c = block_reduce(cnt, SumOp(), 0);
     i64 t = block_reduce(tl, MaxOp(), INT64_MIN);
     i64 fp = block_reduce(first, MinOp(), INT64_MAX);
-    if (threadIdx.x == 0) { blk_pass[blockIdx.x] = c; blk_tl[blockIdx.x] = t; blk_first[blockIdx.x] = fp; }
+    i64 x = blk_xm ? block_reduce(xm, MaxOp(), INT64_MIN) : INT64_MIN;
+    if (threadIdx.x == 0) {
+        blk_pass[blockIdx.x] = c; blk_tl[blockIdx.x] = t; blk_first[blockIdx.x] = fp;
+        if (blk_xm) blk_xm[blockIdx.x] = x;
+    }
 }
 
 void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
-                     i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk) {
+                     i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, i64* blk_xm, int ts_col) {
     WinParams wp{};
     wp.N = N;
     wp.send_size = send_size;
-    hipLaunchKernelGGL(k_blockagg, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first);
+    wp.ts_col = ts_col;
+    hipLaunchKernelGGL(k_blockagg, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first,
+                       ts_col >= 0 ? blk_xm : nullptr);
 }
 
 // ================================================================================================
@@ -55,50 +66,59 @@ void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i6
 // 1024-thread exclusive scans of the tile partials, in coalesced passes of 1024 elements
 // (thread t takes element c*1024 + t) carrying the running totals between passes.
 struct Scan3 {
-    i64 s, m, mn;  // sum, max, min
+    i64 s, m, mn, x;  // sum, max, min, second max
 };
 __device__ __forceinline__ Scan3 block1024_excl(Scan3 v, Scan3* tot) {
-    __shared__ i64 w_sum[16], w_max[16], w_min[16];
+    __shared__ i64 w_sum[16], w_max[16], w_min[16], w_x[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const i64 si = wave_incl_scan(v.s, SumOp());
     const i64 mi = wave_incl_scan(v.m, MaxOp());
     const i64 ni = wave_incl_scan(v.mn, MinOp());
-    if (lane == 63) { w_sum[wv] = si; w_max[wv] = mi; w_min[wv] = ni; }
+    const i64 xi = wave_incl_scan(v.x, MaxOp());
+    if (lane == 63) { w_sum[wv] = si; w_max[wv] = mi; w_min[wv] = ni; w_x[wv] = xi; }
     __syncthreads();
-    Scan3 pre{0, INT64_MIN, INT64_MAX}, all{0, INT64_MIN, INT64_MAX};
+    Scan3 pre{0, INT64_MIN, INT64_MAX, INT64_MIN}, all{0, INT64_MIN, INT64_MAX, INT64_MIN};
     for (int x = 0; x < 16; x++) {
-        if (x < wv) { pre.s += w_sum[x]; pre.m = max(pre.m, w_max[x]); }
-        all.s += w_sum[x]; all.m = max(all.m, w_max[x]); all.mn = min(all.mn, w_min[x]);
+        if (x < wv) { pre.s += w_sum[x]; pre.m = max(pre.m, w_max[x]); pre.x = max(pre.x, w_x[x]); }
+        all.s += w_sum[x]; all.m = max(all.m, w_max[x]); all.mn = min(all.mn, w_min[x]); all.x = max(all.x, w_x[x]);
     }
     __syncthreads();
     i64 mex = __shfl_up(mi, 1, 64);
-    if (lane == 0) mex = INT64_MIN;
+    i64 xex = __shfl_up(xi, 1, 64);
+    if (lane == 0) { mex = INT64_MIN; xex = INT64_MIN; }
     *tot = all;
-    return Scan3{pre.s + si - v.s, max(pre.m, mex), 0};
+    return Scan3{pre.s + si - v.s, max(pre.m, mex), 0, max(pre.x, xex)};
 }
 
 __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk,
-                                                     const i64* __restrict__ ts, WinParams wp, PushInfo* info) {
+                                                     const i64* __restrict__ ts, WinParams wp, PushInfo* info,
+                                                     i64* blk_xm, ColSet cols) {
     const int t = threadIdx.x;
+    i64 tot_x = INT64_MIN;
     constexpr int G = 4;  // passes whose loads are issued together (the scans then run back to back)
     i64 tot_s = 0, tot_m = INT64_MIN, tot_mn = INT64_MAX;
     for (int g0 = 0; g0 < nblk; g0 += G * 1024) {
-        i64 vs[G], vm[G], vn[G];
+        i64 vs[G], vm[G], vn[G], vx[G];
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const int i = min(g0 + g * 1024 + t, nblk - 1);
             vs[g] = blk_pass[i]; vm[g] = blk_tl[i]; vn[g] = blk_first[i];
+            vx[g] = blk_xm ? blk_xm[i] : INT64_MIN;
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const int i = g0 + g * 1024 + t;
             if (g0 + g * 1024 >= nblk) break;
             const bool in = i < nblk;
-            Scan3 v{in ? vs[g] : 0, in ? vm[g] : INT64_MIN, in ? vn[g] : INT64_MAX};
+            Scan3 v{in ? vs[g] : 0, in ? vm[g] : INT64_MIN, in ? vn[g] : INT64_MAX, in ? vx[g] : INT64_MIN};
             Scan3 all;
             Scan3 ex = block1024_excl(v, &all);
-            if (in) { blk_pass[i] = tot_s + ex.s; blk_tl[i] = max(tot_m, ex.m); }
-            tot_s += all.s; tot_m = max(tot_m, all.m); tot_mn = min(tot_mn, all.mn);
+            if (in) {
+                blk_pass[i] = tot_s + ex.s;
+                blk_tl[i] = max(tot_m, ex.m);
+                if (blk_xm) blk_xm[i] = max(tot_x, ex.x);
+            }
+            tot_s += all.s; tot_m = max(tot_m, all.m); tot_mn = min(tot_mn, all.mn); tot_x = max(tot_x, all.x);
         }
     }
     __syncthreads();
@@ -110,6 +130,17 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
         info->E0 = wp.E0;
         info->n_bounds = 0;
         info->first_clk = INT64_MIN;
+        info->max_xm = tot_x;
+        info->err = 0;
+        // externalTimeBatch initTiming (:313-334): the start is the constant, the start attribute or
+        // the timestamp attribute of the first event reaching the window
+        if (wp.kind == SH_WIN_EXT_TIME_BATCH && !wp.e0_valid && tot_mn != INT64_MAX) {
+            const i64 a = load_raw(cols, wp.ts_col, tot_mn);
+            const i64 st = wp.has_start == 1 ? wp.start_time : wp.has_start == 2 ? load_raw(cols, wp.start_col, tot_mn) : a;
+            info->E0 = st;
+            info->e0_valid = 1;
+            if (a < st || st < 0) info->err = 1;
+        }
         const bool init_e0 = wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && !wp.wcol;
         if (tot_mn != INT64_MAX && (init_e0 || wp.want_first_clk)) {
             // clock of the send that carries the first passing event (before the carried-in clock)
@@ -140,8 +171,9 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
 }
 
 void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
-                        WinParams wp, PushInfo* info) {
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, ts, wp, info);
+                        WinParams wp, PushInfo* info, i64* blk_xm, ColSet cols) {
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, ts, wp, info,
+                       wp.kind == SH_WIN_EXT_TIME_BATCH ? blk_xm : nullptr, cols);
 }
 
 // ================================================================================================
@@ -155,7 +187,8 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
 __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const PushInfo* info, Bound* bounds, int max_bounds,
-                                                      int* n_bounds, KeyPlan kp, KeyTable kt, u32* new_pos) {
+                                                      int* n_bounds, KeyPlan kp, KeyTable kt, u32* new_pos,
+                                                      const i64* blk_xm_pre) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     i64 t[kItems];
@@ -192,6 +225,17 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     }
     i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x];
     i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
+    // externalTimeBatch: running max of the timestamp attribute over the events reaching the window
+    const bool ext = wp.kind == SH_WIN_EXT_TIME_BATCH;
+    i64 av[kItems];
+    i64 M = INT64_MIN;
+    if (ext) {
+        load_items_raw(cols, wp.ts_col, base, wp.N, av);
+        i64 xm = INT64_MIN;
+#pragma unroll
+        for (int i = 0; i < kItems; i++) if (pass[i]) xm = max(xm, av[i]);
+        M = max(wp.xm0, max(block_excl_scan(xm, MaxOp(), INT64_MIN, nullptr), blk_xm_pre[blockIdx.x]));
+    }
     const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
     const i64 E0 = info->E0;
     const int e0v = info->e0_valid;
@@ -210,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         // ep and base in one send: ep's clock is that send's clock; else it closed the previous send
         if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
         else clock_prev = max(c0, pm);
-        Wprev = wp.wcol ? wp.W_base + wp.wcol[ep] : wfun(wp, E0, e0v, pcb_prev, clock_prev);
+        Wprev = wp.wcol ? wp.W_base + wp.wcol[ep] : wfun(wp, E0, e0v, pcb_prev, ext ? M : clock_prev);
     }
     WinCursor wc;
     wc.W = Wprev;
@@ -221,7 +265,8 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         if (e >= wp.N) break;
         i64 tsl = per_event ? t[i] : ts[sc2.last_of(wp, e)];
         i64 clk = max(c0, max(pm, tsl));
-        i64 W = wp.wcol ? wp.W_base + wp.wcol[e] : wc.at(wp, E0, e0v, pcb, clk);
+        if (ext && pass[i]) M = max(M, av[i]);
+        i64 W = wp.wcol ? wp.W_base + wp.wcol[e] : wc.at(wp, E0, e0v, pcb, ext ? M : clk);
         if (W > Wprev) {
             int k = atomicAdd(n_bounds, 1);
             if (k < max_bounds) {
@@ -240,9 +285,9 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
 
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos) {
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre) {
     hipLaunchKernelGGL(k_boundaries, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass_pre, blk_tl_pre,
-                       info, bounds, max_bounds, (int*)&((PushInfo*)info)->n_bounds, kp, kt, new_pos);
+                       info, bounds, max_bounds, (int*)&((PushInfo*)info)->n_bounds, kp, kt, new_pos, blk_xm_pre);
 }
 
 // ================================================================================================

@@ -112,10 +112,11 @@ struct sh_query {
     bool e0_valid = false;
     int64_t E0 = 0;
     int64_t W_open = 0;
+    int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
     int64_t n_pend = 0, pend_cap = 0;
     DevBuf pend_pos, pend_ts, pend_vals;
     // scratch
-    DevBuf blk_pass, blk_tl, blk_first, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
+    DevBuf blk_pass, blk_tl, blk_first, blk_xm, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
         out_ts, out_keys, out_vals, out_nulls, out_expired, blk_cnt;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
     DevBuf new_pos, perm, seg_off;  // key slot per event of the push (kNoPos = filtered out); output permutation

@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -82,7 +82,7 @@ uint64_t fingerprint(const sh_query* q) {
     const sh_query_desc& d = q->d;
     uint64_t h = 1469598103934665603ull;
     int32_t ints[] = {d.n_cols, d.window, d.stream_current, d.has_start_time, d.n_group_by, d.n_aggs, d.current_on,
-                      d.expired_on, d.partition_col};
+                      d.expired_on, d.partition_col, d.ts_col, d.start_col};
     h = fnv(h, ints, sizeof(ints));
     h = fnv(h, d.col_types, sizeof(int32_t) * d.n_cols);
     h = fnv(h, &d.window_param, 8);
@@ -115,6 +115,7 @@ int batch_snapshot(sh_query* q, Writer& w) {
     w.val<uint8_t>(q->e0_valid);
     w.val<int64_t>(q->E0);
     w.val<int64_t>(q->W_open);
+    w.val<int64_t>(q->xm);
     w.val<uint8_t>(q->p0_known);
     w.val<int64_t>(q->p0);
     // group-key table: the queued events refer to its slots
@@ -143,6 +144,7 @@ int batch_restore(sh_query* q, Reader& r) {
     q->e0_valid = r.val<uint8_t>();
     q->E0 = r.val<int64_t>();
     q->W_open = r.val<int64_t>();
+    q->xm = r.val<int64_t>();
     bool p0k = r.val<uint8_t>();
     int64_t p0 = r.val<int64_t>();
     bool dense = r.val<uint8_t>();

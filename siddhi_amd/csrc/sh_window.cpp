@@ -147,8 +147,18 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
     if (d->n_aggs < 1 || d->n_aggs > SH_MAX_AGGS)
         return sh_fail(SH_ERR_UNSUPPORTED, "GPU path runs aggregation queries (1..8 aggregators)");
-    if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME)
-        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path needs a lengthBatch, timeBatch or time window");
+    if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME &&
+        d->window != SH_WIN_EXT_TIME_BATCH)
+        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path needs a lengthBatch, timeBatch, time or externalTimeBatch window");
+    if (d->window == SH_WIN_EXT_TIME_BATCH) {
+        if (d->ts_col < 0 || d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG)
+            return sh_fail(SH_ERR_INVALID, "externalTimeBatch timestamp must be a long attribute");
+        if (d->has_start_time == 2 &&
+            (d->start_col < 0 || d->start_col >= d->n_cols || d->col_types[d->start_col] != SH_T_LONG))
+            return sh_fail(SH_ERR_INVALID, "externalTimeBatch start time attribute must be long");
+        if (d->partition_col >= 0)
+            return sh_fail(SH_ERR_UNSUPPORTED, "partitioned externalTimeBatch is not on the GPU");
+    }
     if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
     if (!d->current_on || d->expired_on)
         return sh_fail(SH_ERR_UNSUPPORTED, "GPU windows emit current events only (`insert into`)");
@@ -450,6 +460,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         wp.n_pend = q->n_pend;
         wp.send_size = b->send_size;
         wp.N = N;
+        wp.ts_col = q->d.ts_col;
+        wp.start_col = q->d.start_col;
+        wp.xm0 = q->xm;
+        const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
+        if (ext) RCHK(q->blk_xm.reserve(nblk * 8, false));
         if (q->given) {
             // sharded owner: windows were assigned from the global clock by the ingest ranks
             wp.kind = SH_WIN_TIME_BATCH;
@@ -458,20 +473,25 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             wp.W_base = q->given_W_base;
         }
         launch_blockagg(s, b->ts, cs, q->fp, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
-                        q->blk_first.as<int64_t>(), nblk);
+                        q->blk_first.as<int64_t>(), nblk, ext ? q->blk_xm.as<int64_t>() : nullptr,
+                        ext ? q->d.ts_col : -1);
         launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk,
-                           b->ts, wp, q->info.as<PushInfo>());
+                           b->ts, wp, q->info.as<PushInfo>(), ext ? q->blk_xm.as<int64_t>() : nullptr, cs);
         int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
         RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
         RCHK(q->new_pos.reserve((size_t)N * 4, false));
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                           q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                          q->new_pos.as<u32>());
+                          q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         PushInfo info = *q->h_info;
         if (info.n_bounds > max_bounds) return sh_fail(SH_ERR_INVALID, "more than 4M windows closed in one push");
+        if (ext && info.err)
+            return sh_fail(SH_ERR_UNSUPPORTED,
+                           "externalTimeBatch: the first event's timestamp is before its start time (not on the GPU)");
+        if (ext) q->xm = std::max(q->xm, info.max_xm);
         std::vector<Bound> bounds(info.n_bounds);
         if (info.n_bounds) {
             HIPCHK(hipMemcpyAsync(bounds.data(), q->bounds.p, info.n_bounds * sizeof(Bound), hipMemcpyDeviceToHost, s));
@@ -602,7 +622,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     if (!q) return SH_OK;
     (void)hipStreamSynchronize(q->ctx->stream);
     if (q->kind == 1) sliding_destroy(q);
-    DevBuf* bufs[] = {&q->pend_pos, &q->pend_ts, &q->pend_vals, &q->blk_pass, &q->blk_tl, &q->blk_first, &q->info,
+    DevBuf* bufs[] = {&q->pend_pos, &q->pend_ts, &q->pend_vals, &q->blk_pass, &q->blk_tl, &q->blk_first, &q->blk_xm, &q->info,
                       &q->bounds, &q->segs, &q->seg_rows, &q->flags, &q->rowref, &q->rows, &q->row_vals,
                       &q->counters, &q->out_ts, &q->out_keys, &q->out_vals, &q->out_nulls, &q->out_expired,
                       &q->blk_cnt, &q->ms_counts, &q->ms_tmp, &q->rec_pos, &q->rec_idx, &q->rec_vals,

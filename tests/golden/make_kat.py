@@ -86,6 +86,26 @@ case(name="max_sliding_time", source="ctest/query/aggregator/MaxAggregatorExtens
             {"advance": B + 1100}],
      expect=dict(total_count=4, values=[[36.0], [37.88], [37.88], [None]]))
 
+# ---------------------------------------------------------------- externalTimeBatch (ExternalTimeBatchWindowTestCase)
+# The window keys on an attribute; the (wall-clock) event timestamps of these tests never matter, so
+# each send carries a distinct timestamp B + value that lets the checks map a row back to `value`.
+E = "ctest/query/window/ExternalTimeBatchWindowTestCase.java"
+_e1 = [10000, 11000, 12000, 13000, 14000, 15000, 16500, 17000, 18000, 19000, 20000, 20500, 22000, 25000]
+case(name="externalTimeBatch_test1", source=E + ":225-285", schema="currentTime long, value int",
+     query=dict(window="externalTimeBatch", param=5000, ts_attr="currentTime", output="current"),
+     sends=[[[B + i + 1, t, i + 1]] for i, t in enumerate(_e1)],
+     expect=dict(flush_count=3, flush_first_col=["value", [1, 6, 11]]))
+case(name="externalTimeBatch_test2_start", source=E + ":287-323", schema="currentTime long, value int",
+     query=dict(window="externalTimeBatch", param=5000, ts_attr="currentTime", start_time=1200, output="current"),
+     sends=[[[B + i // 100, i + 10000, i // 100]] for i in range(0, 10000, 100)],
+     expect=dict(flush_first_col=["value", [0, 12]], flush_last_col=["value", [11]]))
+case(name="externalTimeBatch_test05_edge", source=E + ":99-141", schema="cpu int, timestamp long",
+     query=dict(window="externalTimeBatch", param=10000, ts_attr="timestamp", aggs=[["avg", "cpu"], ["count", None]],
+                output="current"),
+     sends=[[[B + i, c, t]] for i, (c, t) in enumerate([(15, 0), (15, 10), (15, 20), (85, 10000), (85, 10010),
+                                                        (85, 10020), (10000, 100000)])],
+     expect=dict(in_count=2, flush_sizes=[1, 1], values=[[15.0, 3], [85.0, 3]]))
+
 # ---------------------------------------------------------------- partitioned timeBatch (WindowPartitionTestCase)
 case(name="partition5_timeBatch", source="ctest/query/partition/WindowPartitionTestCase.java:291-348",
      schema="symbol string, price double, volume int",

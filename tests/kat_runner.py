@@ -56,7 +56,8 @@ def build(case, dic):
     spec = abi.QuerySpec(schema, q["window"], q.get("param", 0), group_by=q.get("group_by", ()),
                          aggs=[tuple(x) for x in q.get("aggs", [])], filter=_conv_filter(q.get("filter"), dic),
                          start_time=q.get("start_time"), stream_current=q.get("stream_current", False),
-                         output=q.get("output", "current"), partition=q.get("partition"))
+                         output=q.get("output", "current"), partition=q.get("partition"),
+                         ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"))
     return schema, spec
 
 
@@ -104,6 +105,18 @@ def check_query(case, flushes, schema, dic):
     if "values" in e:
         got = [list(r[3]) for r in rows]
         assert got == e["values"], (got, e["values"])
+    if "flush_count" in e:
+        assert len(flushes) == e["flush_count"], (len(flushes), e)
+    if "flush_first_col" in e or "flush_last_col" in e:
+        # rows carry their event timestamp, unique per send here: map it back to the sent column
+        for key, pick in (("flush_first_col", 0), ("flush_last_col", -1)):
+            if key not in e:
+                continue
+            col, want = e[key]
+            c = schema.col(col)
+            ts2v = {r[0]: r[1 + c] for s in case["sends"] if isinstance(s, list) for r in s}
+            got = [ts2v[f.rows[pick][0]] for f in flushes[:len(want)]]
+            assert got == want, (key, got, want)
     if "value_range" in e:
         idx, lo, hi = e["value_range"]
         for r in rows:
