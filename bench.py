@@ -48,6 +48,8 @@ def parse():
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
     ap.add_argument("--key-type", choices=["string", "int"], default="string",
                     help="k as a dictionary-encoded string (ids are dense key slots) or as an int (hashed)")
+    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "ext"], default="c2",
+                    help="c2 = the headline (BASELINE configs[1]); c1/c3/c4/ext = secondary single-GPU lines")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
     return ap.parse_args()
@@ -95,6 +97,87 @@ def measured_traffic(args, sliced):
     return None
 
 
+# ---- secondary single-GPU workloads (BASELINE.json configs[0], [2], [3]; externalTimeBatch) ---------
+SECONDARY = {
+    # name: (description, algorithmic bytes per event from SURVEY.md §8d)
+    "c1": ("C1 lengthBatch(10000) [price>100] sum(volume), avg(price) group by symbol, 1k symbols, send(Event[1000])",
+           29.4),
+    "c3": ("C3 sliding time(10 sec) count/min/max/avg group by k, 10k keys, per-event sends", 84.0),
+    "c4": ("C4 define aggregation sum/avg/count/min/max group by k aggregate by ts every sec...day; one GPU's share "
+           "of C4 on 8 GPUs: 125k of the 1M keys, 1.25M of the 10M events per event-time second", 25.2),
+    "ext": ("externalTimeBatch(et, 1 sec) count/min/max/avg group by k, 100k keys, per-event sends", 32.4),
+}
+
+
+def run_secondary(args, dev):
+    """One GPU, inputs resident in HBM, `--steps` pushes of `--batch` events of the workload."""
+    import numpy as np
+    import torch
+    from siddhi_amd import abi, runtime, synth
+    ctx = runtime.Context(dev.index)
+    B, nb = args.batch, args.warmup + args.steps
+    agg = None
+    if args.workload == "c1":
+        schema = abi.Schema.parse("symbol string, price double, volume long, ts long")
+        spec = abi.QuerySpec(schema, "lengthBatch", 10000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
+                             filter=(">", "price", 100), key_capacity=1000)
+        send = 1000
+        gen = lambda i: [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in synth.c1_stock(i * B, B)[1]]
+        mk = lambda cols: (cols[3], cols)
+    elif args.workload == "c4":
+        schema = abi.Schema.parse("k string, v double, ts long")
+        agg = abi.AggregationSpec(schema, [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                                  group_by=["k"], ts="ts", durations=("sec", "day"), key_capacity=125_000)
+        send = 1
+        gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC4, 125_000, 1_250, dev)[1]
+        mk = lambda cols: (cols[2], cols)
+    else:
+        if args.workload == "c3":
+            schema = abi.Schema.parse("k string, v double, ts long")
+            spec = abi.QuerySpec(schema, "time", 10_000, group_by=["k"],
+                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=10_000)
+            gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC3, 10_000, 1000, dev)[1]
+        else:
+            schema = abi.Schema.parse("k string, v double, ts long")
+            spec = abi.QuerySpec(schema, "externalTimeBatch", 1000, group_by=["k"], ts_attr="ts",
+                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=100_000)
+            gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xE7, 100_000, 1000, dev)[1]
+        send = 1
+        mk = lambda cols: (cols[2], cols)
+    q = runtime.GpuAggregation(agg, ctx) if agg else runtime.GpuQuery(spec, ctx)
+    batches = [mk(gen(i)) for i in range(nb)]
+    torch.cuda.synchronize()
+
+    def push(i):
+        ts, cols = batches[i]
+        return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], send)
+
+    for i in range(args.warmup):
+        push(i)
+    torch.cuda.synchronize()
+    kern_ms, t0 = 0.0, time.perf_counter()
+    for i in range(args.warmup, nb):
+        push(i)
+        if not agg:
+            kern_ms += q.stats().main_kernel_ms
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    desc, bpe = SECONDARY[args.workload]
+    roof = None
+    if kern_ms > 0:
+        ach = bpe * B * args.steps / (kern_ms / 1e3) / 1e9
+        roof = {"bound": "hbm", "kernel": "main (aggregate / sliding)", "achieved": ach, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms_per_step": kern_ms / args.steps,
+                "bytes_per_event": bpe}
+    print(json.dumps({"metric": METRIC, "value": B * args.steps / elapsed, "unit": "events/s", "n_gpus": 1,
+                      "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+                      "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                      "data": "synthetic SplitMix64 stream (SURVEY.md §8d seeds), resident in HBM",
+                      "config": {"workload": desc, "events_per_step": B, "send_size": send},
+                      "roofline": roof}), flush=True)
+    q.close()
+
+
 def main():
     args = parse()
     import torch
@@ -116,6 +199,10 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if args.workload != "c2":
+        if world > 1:
+            raise SystemExit("secondary workloads run on one GPU")
+        return run_secondary(args, dev)
     from siddhi_amd import abi, runtime, synth
     ctx = runtime.Context(local % ndev)
     schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")

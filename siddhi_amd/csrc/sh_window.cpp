@@ -98,7 +98,12 @@ static int size_partitions(sh_query* q) {
         return p == 1 ? (size_t)nl * (16 + 8 * (size_t)q->ap.n_fields) + 16
                       : aggregate_own_lds(nl, q->ap.n_fields, q->ap.n_vcols);
     };
-    while (need(P) > budget && P < 4096) P <<= 1;
+    // the multisplit's per-tile LDS (staging + per-wave partition counters) must fit one CU too
+    auto scatter_fits = [&](int p) {
+        size_t v = (size_t)std::max(1, q->ap.n_vcols);
+        return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 12 + 64 <= 160 * 1024;
+    };
+    while (need(P) > budget && P < 16384 && scatter_fits(P << 1)) P <<= 1;
     if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
     q->P = P;
     q->logP = 0;
