@@ -237,12 +237,14 @@ def main():
         ts, cols = batches[i]
         if sliced:
             return distributed_push(q, ex, B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size,
-                                    send_buf, host_out=False)[0]
+                                    send_buf, host_out=False, timings=phases if timing else None)[0]
         return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
 
+    phases, timing = {}, False
     for i in range(args.warmup):
         push(i)
     torch.cuda.synchronize()
+    timing = True
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -287,7 +289,7 @@ def main():
                    "keys_per_gpu": args.keys, "keys_total": keys_total, "events_per_step_per_gpu": B,
                    "event_rate": f"{args.events_per_ms * 1000 * (world if sliced else 1)} events per event-time second",
                    "send_size": args.send_size,
-                   "parallelism": (f"slice ingest x{world}, key re-shard over RCCL all-to-all" if sliced
+                   "parallelism": (f"slice ingest x{world}, key re-shard over {'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all" if sliced
                                    else f"key-sharded x{world}"),
                    "flushes": flushes, "rows": rows},
         "roofline": {"bound": "hbm", "kernel": "k_aggregate_own", "achieved": ach, "peak": HBM_PEAK_GBS,
@@ -295,6 +297,10 @@ def main():
                      "kernel_ms_per_step": kern_ms / args.steps,
                      "bytes_per_event": C2_BYTES_PER_EVENT},
     }
+    if sliced:
+        # rank 0's wall time per step in each phase of the sharded push (summaries all-gather,
+        # pack, record all-to-all over RCCL, owner pipeline) and its bytes sent per step
+        result["config"]["phases_ms_per_step_rank0"] = {k: v / args.steps for k, v in phases.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

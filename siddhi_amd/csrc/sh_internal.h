@@ -191,8 +191,17 @@ constexpr int kMaxShards = 16;
 void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
                          const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code, i64* counts, Bound* bounds,
                          int max_bounds, int* n_bounds);
+// Record of one re-keyed event (4-byte words): [key u32 | key u64][slice position u32 (+pad)][ts i64]
+// [values u64...]; the owner derives the global index from the source and position, and the
+// window from the global window starts.
+struct ShardSrc {
+    i64 start[kMaxShards + 1];  // first record of each source's block in the received buffer
+    i64 gbase[kMaxShards];      // global stream index of each source slice's first event
+    int G;
+    int key32;
+};
 void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
-                       i64 N, int nblk, const i64* offsets, u64 gidx0, unsigned char* out, int rec_words);
+                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32);
 struct ColRoles {
     int role[SH_MAX_COLS];  // -1 unused, 0..7 value slot, 16 + g group-key component g
     int n;
@@ -201,6 +210,7 @@ struct ColPtrs {
     u64* p[SH_MAX_COLS];
 };
 void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec_words, KeyPlan kp, ColRoles roles,
-                         i64* ts, ColPtrs cols, int* wcol, u64* gidx);
+                         ShardSrc src, const i64* bound_gidx, const i64* bound_W, int n_bounds, i64 W_base, i64* ts,
+                         ColPtrs cols, int* wcol, u64* gidx);
 
 }  // namespace shd

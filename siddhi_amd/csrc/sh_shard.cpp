@@ -39,7 +39,8 @@ struct sh_shard {
     FilterProg fp{};
     KeyPlan kp{};
     AggPlan ap{};
-    int rec_words = 3;
+    int rec_words = 6;   // 4-byte words per record
+    int key32 = 0;       // the packed group key fits 32 bits
     sh_query* owner = nullptr;
     // global stream state (identical on every rank)
     bool clock_valid = false;
@@ -51,13 +52,16 @@ struct sh_shard {
     // the push in flight (pack -> consume)
     bool packed = false;
     int64_t cur_W_base = 0, cur_W_end = 0;
+    int64_t cur_seq = 0;                  // global index of the push's first event
+    std::vector<int64_t> cur_off;         // stream offset of every slice in the push
+    std::vector<int64_t> h_bg, h_bw;      // host copies of the window starts being uploaded
     // ingest scratch
     int64_t slice_n = -1;
     DevBuf blk_pass, blk_tl, blk_first, info, code, counts, tmp, part_off, bounds;
     PushInfo* h_info = nullptr;
     std::vector<sh_bound> my_bounds;
     // owner scratch
-    DevBuf u_ts, u_wcol, u_gidx, u_cols[SH_MAX_COLS];
+    DevBuf u_ts, u_wcol, u_gidx, u_cols[SH_MAX_COLS], u_bg, u_bw;
     ColRoles roles{};
 };
 
@@ -88,7 +92,8 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
         delete s;
         return rc;
     }
-    s->rec_words = 3 + s->ap.n_vcols;
+    s->key32 = (s->kp.n == 0 || (s->kp.n == 1 && s->kp.type[0] != SH_T_LONG && s->kp.div[0] == 0)) ? 1 : 0;
+    s->rec_words = (s->key32 ? 4 : 6) + 2 * s->ap.n_vcols;
     // the owner runs the same query over the records it receives: no filter (applied at ingest),
     // 8-byte raw columns, windows given per event
     // key_capacity is the whole stream's; an owner holds about 1/G of the keys (dictionary ids
@@ -128,7 +133,7 @@ extern "C" int sh_shard_destroy(sh_shard* s) {
     (void)hipStreamSynchronize(s->ctx->stream);
     if (s->owner) sh_query_destroy(s->owner);
     DevBuf* bufs[] = {&s->blk_pass, &s->blk_tl, &s->blk_first, &s->info, &s->code, &s->counts, &s->tmp,
-                      &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx};
+                      &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx, &s->u_bg, &s->u_bw};
     for (DevBuf* b : bufs) b->release();
     for (auto& c : s->u_cols) c.release();
     if (s->h_info) (void)hipHostFree(s->h_info);
@@ -138,7 +143,7 @@ extern "C" int sh_shard_destroy(sh_shard* s) {
 
 extern "C" int sh_shard_record_bytes(sh_shard* s, int64_t* out) {
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_record_bytes: NULL argument");
-    *out = 8 * (int64_t)s->rec_words;
+    *out = 4 * (int64_t)s->rec_words;
     return SH_OK;
 }
 
@@ -189,7 +194,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     if (s->slice_n != b->n || all[s->rank].n != b->n)
         return sh_fail(SH_ERR_STATE, "sh_shard_pack: call sh_shard_summarize on the same slice first");
     const int G = s->world;
-    const int64_t RB = 8 * (int64_t)s->rec_words;
+    const int64_t RB = 4 * (int64_t)s->rec_words;
     if (b->n > 0 && (!send_buf || send_cap < b->n * RB))
         return sh_fail(SH_ERR_INVALID, "sh_shard_pack: send buffer smaller than slice.n * record_bytes");
     // clock carried into every slice; stream offset of every slice
@@ -219,6 +224,8 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     if (W_end - W_start >= (1 << 23)) return sh_fail(SH_ERR_UNSUPPORTED, "more than 8M windows in one push");
     s->cur_W_base = W_start;
     s->cur_W_end = W_end;
+    s->cur_seq = (int64_t)s->seq;
+    s->cur_off = off;
     s->my_bounds.clear();
     for (int r = 0; r < G; r++) send_bytes[r] = 0;
     const int64_t N = b->n;
@@ -252,8 +259,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
         launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
         launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->kp, s->ap, G, N, nblk,
-                          s->counts.as<int64_t>(), (u64)(s->seq + off[s->rank]), (unsigned char*)send_buf,
-                          s->rec_words);
+                          s->counts.as<int64_t>(), (unsigned char*)send_buf, s->rec_words, s->key32);
         launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
         HIPCHK(hipGetLastError());
         std::vector<int64_t> po(G + 1);
@@ -309,7 +315,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
     if (!s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
     s->packed = false;
-    const int64_t RB = 8 * (int64_t)s->rec_words;
+    const int64_t RB = 4 * (int64_t)s->rec_words;
     int64_t bytes = 0;
     for (int r = 0; r < s->world; r++) {
         if (recv_bytes[r] < 0 || recv_bytes[r] % RB) return sh_fail(SH_ERR_INVALID, "received block not a whole number of records");
@@ -342,7 +348,31 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         cp.p[c] = s->u_cols[c].as<u64>();
         b.cols[c] = cp.p[c];
     }
-    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->kp, s->roles, s->u_ts.as<int64_t>(), cp,
+    // the global window starts, sorted by stream index, for the per-record window lookup
+    const int nb = (int)q->gbounds.size();
+    std::vector<int64_t>& bg = s->h_bg;
+    std::vector<int64_t>& bw = s->h_bw;
+    bg.resize(nb);
+    bw.resize(nb);
+    for (int i = 0; i < nb; i++) { bg[i] = q->gbounds[i].gidx; bw[i] = q->gbounds[i].W; }
+    RCHK(s->u_bg.reserve(std::max(1, nb) * 8, false));
+    RCHK(s->u_bw.reserve(std::max(1, nb) * 8, false));
+    if (nb) {
+        HIPCHK(hipMemcpyAsync(s->u_bg.p, bg.data(), nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->u_bw.p, bw.data(), nb * 8, hipMemcpyHostToDevice, st));
+    }
+    ShardSrc src{};
+    src.G = s->world;
+    src.key32 = s->key32;
+    int64_t acc = 0;
+    for (int g = 0; g < s->world; g++) {
+        src.start[g] = acc;
+        acc += recv_bytes[g] / RB;
+        src.gbase[g] = s->cur_seq + s->cur_off[g];
+    }
+    src.start[s->world] = acc;
+    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->kp, s->roles, src,
+                        s->u_bg.as<int64_t>(), s->u_bw.as<int64_t>(), nb, s->cur_W_base, s->u_ts.as<int64_t>(), cp,
                         s->u_wcol.as<int>(), s->u_gidx.as<u64>());
     HIPCHK(hipGetLastError());
     b.ts = s->u_ts.as<int64_t>();

@@ -6,7 +6,7 @@
 //   k_shard_assign  window of every event (clock carried in from the slices before), owner =
 //                   mix64(key) % G, per-(owner, tile) histogram, window starts of the slice
 //   k_shard_pack    stable multisplit of the passing events into per-owner runs of AoS records
-//                   {key, ts, gidx | W << 40, values...} (event order kept inside every run)
+//                   {key, slice position, ts, values...} (event order kept inside every run)
 //   k_shard_unpack  received records -> SoA columns of the owner's pipeline (given-window mode)
 #include "sh_device.h"
 
@@ -105,8 +105,8 @@ void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f
 // before), so every owner's run keeps event order. offsets = exclusive scan of counts[o][tile].
 __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* __restrict__ ts,
                                                       const u32* __restrict__ code, KeyPlan kp, AggPlan ap, int G,
-                                                      i64 N, int nblk, const i64* __restrict__ offsets, u64 gidx0,
-                                                      u64* out, int rec_words) {
+                                                      i64 N, int nblk, const i64* __restrict__ offsets, u32* out,
+                                                      int rec_words, int key32) {
     __shared__ u32 running[kMaxShards];
     __shared__ u32 wave_cnt[kBlock / 64][kMaxShards];
     const int tile = blockIdx.x;
@@ -135,11 +135,22 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
             u32 before = running[o];
             for (int w = 0; w < wave; w++) before += wave_cnt[w][o];
             i64 dst = offsets[(i64)o * nblk + tile] + before + lrank;
-            u64* rec = out + dst * rec_words;
-            rec[0] = make_key(kp, cols, e);
-            rec[1] = (u64)ts[e];
-            rec[2] = (gidx0 + (u64)e) | ((u64)(c >> kOwnerBits) << 40);
-            for (int j = 0; j < ap.n_vcols; j++) rec[3 + j] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            u32* rec = out + dst * rec_words;
+            const u64 key = make_key(kp, cols, e);
+            int w8;  // first 8-byte word
+            if (key32) {
+                rec[0] = (u32)key;
+                rec[1] = (u32)e;
+                w8 = 2;
+            } else {
+                *(u64*)rec = key;
+                rec[2] = (u32)e;
+                rec[3] = 0;
+                w8 = 4;
+            }
+            u64* r8 = (u64*)(rec + w8);
+            r8[0] = (u64)ts[e];
+            for (int j = 0; j < ap.n_vcols; j++) r8[1 + j] = (u64)load_raw(cols, ap.vcol_src[j], e);
         }
         __syncthreads();
         if (threadIdx.x < G) {
@@ -152,28 +163,45 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
 }
 
 void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
-                       i64 N, int nblk, const i64* offsets, u64 gidx0, unsigned char* out, int rec_words) {
-    hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, kp, ap, G, N, nblk, offsets, gidx0,
-                       (u64*)out, rec_words);
+                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32) {
+    hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, kp, ap, G, N, nblk, offsets,
+                       (u32*)out, rec_words, key32);
 }
 
 // Received records -> the owner's SoA columns (8-byte raw form for every referenced column).
-// role[c]: -1 unused, 0..7 value slot, 16 + g group-key component g.
-__global__ __launch_bounds__(kBlock) void k_shard_unpack(const u64* __restrict__ rec, i64 M, int rec_words, KeyPlan kp,
-                                                        ColRoles roles, i64* ts, ColPtrs cols, int* wcol, u64* gidx) {
+// role[c]: -1 unused, 0..7 value slot, 16 + g group-key component g. The global index of a record is
+// its source slice's base + its slice position; its window is that of the last global window start
+// at or before it (binary search over the all-gathered starts), W_base before the first.
+__global__ __launch_bounds__(kBlock) void k_shard_unpack(const u32* __restrict__ rec, i64 M, int rec_words, KeyPlan kp,
+                                                        ColRoles roles, ShardSrc src,
+                                                        const i64* __restrict__ bound_gidx,
+                                                        const i64* __restrict__ bound_W, int n_bounds, i64 W_base,
+                                                        i64* ts, ColPtrs cols, int* wcol, u64* gidx) {
     i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (m >= M) return;
-    const u64* r = rec + m * rec_words;
-    u64 key = r[0];
-    ts[m] = (i64)r[1];
-    u64 g = r[2];
-    gidx[m] = g & ((1ull << 40) - 1);
-    wcol[m] = (int)(g >> 40);
+    const u32* r = rec + m * rec_words;
+    u64 key;
+    u32 pos;
+    int w8;
+    if (src.key32) { key = (u64)(i64)(int)r[0]; pos = r[1]; w8 = 2; }
+    else { key = *(const u64*)r; pos = r[2]; w8 = 4; }
+    const u64* r8 = (const u64*)(r + w8);
+    ts[m] = (i64)r8[0];
+    int g = 0;
+    while (g + 1 < src.G && m >= src.start[g + 1]) g++;
+    const i64 gi = src.gbase[g] + (i64)pos;
+    gidx[m] = (u64)gi;
+    int lo = 0, hi = n_bounds;  // first bound with gidx > gi
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (bound_gidx[mid] <= gi) lo = mid + 1; else hi = mid;
+    }
+    wcol[m] = (int)((lo > 0 ? bound_W[lo - 1] : W_base) - W_base);
     for (int c = 0; c < roles.n; c++) {
         int role = roles.role[c];
         if (role < 0) continue;
         u64 v;
-        if (role < 16) v = r[3 + role];
+        if (role < 16) v = r8[1 + role];
         else if (kp.n == 1) v = key;
         else if (role == 16) v = (u64)(i64)(int)(u32)(key >> 32);
         else v = (u64)(i64)(int)(u32)key;
@@ -182,10 +210,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(const u64* __restrict__
 }
 
 void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec_words, KeyPlan kp, ColRoles roles,
-                         i64* ts, ColPtrs cols, int* wcol, u64* gidx) {
+                         ShardSrc src, const i64* bound_gidx, const i64* bound_W, int n_bounds, i64 W_base, i64* ts,
+                         ColPtrs cols, int* wcol, u64* gidx) {
     if (M <= 0) return;
-    hipLaunchKernelGGL(k_shard_unpack, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (const u64*)rec,
-                       M, rec_words, kp, roles, ts, cols, wcol, gidx);
+    hipLaunchKernelGGL(k_shard_unpack, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, (const u32*)rec,
+                       M, rec_words, kp, roles, src, bound_gidx, bound_W, n_bounds, W_base, ts, cols, wcol, gidx);
 }
 
 }  // namespace shd

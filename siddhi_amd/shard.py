@@ -255,16 +255,28 @@ class TorchExchange:
 
 
 def distributed_push(q: ShardedQuery, ex: TorchExchange, n: int, ts_ptr: int, col_ptrs: Sequence[int],
-                     send_size: int, send_buf, host_out: bool = False):
+                     send_size: int, send_buf, host_out: bool = False, timings: Optional[dict] = None):
     """One global push on this rank: summarize -> all-gather -> pack -> all-to-all + all-gather ->
-    consume. send_buf: uint8 device tensor of >= n * record_bytes bytes."""
+    consume. send_buf: uint8 device tensor of >= n * record_bytes bytes. `timings` (optional)
+    accumulates wall milliseconds per phase (each phase ends in a host synchronisation anyway)."""
+    import time
+    import torch
+    t0 = time.perf_counter()
     summ = q.summarize(n, ts_ptr, col_ptrs, send_size)
     all_summ = ex.all_gather_summaries(summ)
+    t1 = time.perf_counter()
     send_bytes, bounds = q.pack(all_summ, send_buf.data_ptr(), int(send_buf.numel()))
+    t2 = time.perf_counter()
     recv, recv_bytes = ex.all_to_all(send_buf, send_bytes)
     if recv.device != send_buf.device:  # host transport (gloo): the owner consumes device memory
         recv = recv.to(send_buf.device)
     all_bounds = ex.all_gather_bounds(bounds)
-    import torch
     torch.cuda.current_stream(send_buf.device).synchronize()  # recv was written on torch's stream
-    return q.consume(recv.data_ptr(), recv_bytes, all_bounds, host_out)
+    t3 = time.perf_counter()
+    res = q.consume(recv.data_ptr(), recv_bytes, all_bounds, host_out)
+    if timings is not None:
+        t4 = time.perf_counter()
+        for k, v in (("summarize", t1 - t0), ("pack", t2 - t1), ("exchange", t3 - t2), ("consume", t4 - t3)):
+            timings[k] = timings.get(k, 0.0) + v * 1e3
+        timings["bytes_sent"] = timings.get("bytes_sent", 0) + int(np.asarray(send_bytes).sum())
+    return res
