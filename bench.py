@@ -109,14 +109,19 @@ SECONDARY = {
 }
 
 
-def run_secondary(args, dev):
-    """One GPU, inputs resident in HBM, `--steps` pushes of `--batch` events of the workload."""
+def run_secondary(args, dev, rank=0, world=1, dist=None):
+    """Inputs resident in HBM, `--steps` pushes of `--batch` events (per GPU) of the workload. One
+    GPU, except C4: at N > 1 one global stream (N x the per-GPU key count and event rate) is sliced
+    across the ranks and key-sharded (ShardedAggregation over RCCL all-to-all)."""
     import numpy as np
     import torch
     from siddhi_amd import abi, runtime, synth
     ctx = runtime.Context(dev.index)
+    if args.workload == "c4" and args.batch == 1 << 25:
+        args.batch = 1 << 22  # 3.4 s of event time per push: ~4 open second-buckets x 125k keys per GPU
     B, nb = args.batch, args.warmup + args.steps
     agg = None
+    sliced = world > 1
     if args.workload == "c1":
         schema = abi.Schema.parse("symbol string, price double, volume long, ts long")
         spec = abi.QuerySpec(schema, "lengthBatch", 10000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
@@ -126,10 +131,12 @@ def run_secondary(args, dev):
         mk = lambda cols: (cols[3], cols)
     elif args.workload == "c4":
         schema = abi.Schema.parse("k string, v double, ts long")
+        # C4 = 1M keys at 10M events per event-time second on 8 GPUs: 125k keys and 1.25M ev/s per GPU
         agg = abi.AggregationSpec(schema, [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")],
-                                  group_by=["k"], ts="ts", durations=("sec", "day"), key_capacity=125_000)
+                                  group_by=["k"], ts="ts", durations=("sec", "day"), key_capacity=125_000 * world)
         send = 1
-        gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC4, 125_000, 1_250, dev)[1]
+        gen = lambda i: synth.torch_keyed_stream((i * world + rank) * B, B, 0xC4, 125_000 * world, 1_250 * world,
+                                                 dev)[1]
         mk = lambda cols: (cols[2], cols)
     else:
         if args.workload == "c3":
@@ -144,16 +151,32 @@ def run_secondary(args, dev):
             gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xE7, 100_000, 1000, dev)[1]
         send = 1
         mk = lambda cols: (cols[2], cols)
-    q = runtime.GpuAggregation(agg, ctx) if agg else runtime.GpuQuery(spec, ctx)
+    if sliced:
+        if not agg:
+            raise SystemExit("of the secondary workloads only c4 runs on N > 1 GPUs")
+        from siddhi_amd.shard import ShardedAggregation, TorchExchange, distributed_push
+        q = ShardedAggregation(agg, rank, world, ctx)
+        ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
+        send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
+    else:
+        q = runtime.GpuAggregation(agg, ctx) if agg else runtime.GpuQuery(spec, ctx)
     batches = [mk(gen(i)) for i in range(nb)]
     torch.cuda.synchronize()
+    phases, timing = {}, False
 
     def push(i):
         ts, cols = batches[i]
+        if sliced:
+            return distributed_push(q, ex, B, ts.data_ptr(), [c.data_ptr() for c in cols], send, send_buf,
+                                    host_out=False, timings=phases if timing else None)
         return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], send)
 
     for i in range(args.warmup):
         push(i)
+    torch.cuda.synchronize()
+    timing = True
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     kern_ms, t0 = 0.0, time.perf_counter()
     for i in range(args.warmup, nb):
@@ -161,7 +184,17 @@ def run_secondary(args, dev):
         if not agg:
             kern_ms += q.stats().main_kernel_ms
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        q.close()
+        return
     desc, bpe = SECONDARY[args.workload]
     roof = None
     if kern_ms > 0:
@@ -169,12 +202,18 @@ def run_secondary(args, dev):
         roof = {"bound": "hbm", "kernel": "main (aggregate / sliding)", "achieved": ach, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms_per_step": kern_ms / args.steps,
                 "bytes_per_event": bpe}
-    print(json.dumps({"metric": METRIC, "value": B * args.steps / elapsed, "unit": "events/s", "n_gpus": 1,
-                      "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
-                      "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+    config = {"workload": desc, "events_per_step_per_gpu": B, "send_size": send}
+    if sliced:
+        config.update(parallelism=f"slice ingest x{world}, key re-shard over "
+                                  f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all",
+                      keys_total=125_000 * world,
+                      phases_ms_per_step_rank0={k: v / args.steps for k, v in phases.items()})
+    print(json.dumps({"metric": METRIC, "value": B * args.steps * world / elapsed, "unit": "events/s",
+                      "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                      "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+                      "vs_baseline": None, "dtype": "f64",
                       "data": "synthetic SplitMix64 stream (SURVEY.md §8d seeds), resident in HBM",
-                      "config": {"workload": desc, "events_per_step": B, "send_size": send},
-                      "roofline": roof}), flush=True)
+                      "config": config, "roofline": roof}), flush=True)
     q.close()
 
 
@@ -200,9 +239,7 @@ def main():
             dist.init_process_group("gloo")
 
     if args.workload != "c2":
-        if world > 1:
-            raise SystemExit("secondary workloads run on one GPU")
-        return run_secondary(args, dev)
+        return run_secondary(args, dev, rank, world, dist)
     from siddhi_amd import abi, runtime, synth
     ctx = runtime.Context(local % ndev)
     schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")

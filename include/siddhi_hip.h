@@ -256,7 +256,8 @@ int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out
  *                                                   first event, so merging the G outputs of a
  *                                                   flush by `order` yields the single-stream row
  *                                                   order of QuerySelector.processInBatchGroupBy.
- * Supported: timeBatch group-by (not partitioned).                                          */
+ * Supported: timeBatch group-by (not partitioned), and incremental aggregations through
+ * sh_aggregation_shard_create (below).                                                       */
 typedef struct {
     int64_t n;           /* events in the slice                                              */
     int64_t n_pass;      /* events passing the filter                                        */
@@ -291,6 +292,15 @@ int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_byte
                      int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order);
 /* TIMER path of the sharded query: every rank calls it with the same `now`. */
 int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out, const int64_t** order);
+/* Key-sharded incremental aggregation (C4 across G GPUs): *shard ingests through the three phases
+ * above (owner = the group key's owner; an event's time bucket travels as its raw `aggregate by`
+ * column), and every owner runs the root and all roll-up levels of its keys, so the union of the G
+ * owners' sh_aggregation_table rows is the single-stream table. Replaces the single-stream
+ * AggregationRuntime.processEvents -> IncrementalExecutor.execute chain (IncrementalExecutor.java:
+ * 110-258). consume/advance_time output the root's flushes (device); tables are read with
+ * sh_aggregation_table(*agg, ...); sh_shard_destroy(*shard) releases both handles. */
+int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_desc* desc, int32_t rank, int32_t world,
+                                sh_shard** shard, sh_aggregation** agg);
 
 /* Pinned host buffers for zero-copy packing of Event[] chunks (hipHostMalloc). */
 int sh_alloc_pinned(int64_t bytes, void** out);

@@ -400,6 +400,9 @@ def setup_lib_prototypes(lib, prefix: str):
                                          P(P(Out)), P(PI)]
         lib.sh_shard_stats.argtypes = [C.c_void_p, P(Stats)]
         lib.sh_shard_advance_time.argtypes = [C.c_void_p, C.c_int64, C.c_int32, P(P(Out)), P(PI)]
+    if hasattr(lib, "sh_aggregation_shard_create"):
+        lib.sh_aggregation_shard_create.argtypes = [C.c_void_p, P(AggregationDesc), C.c_int32, C.c_int32,
+                                                    P(C.c_void_p), P(C.c_void_p)]
 
 
 # every exported symbol include/siddhi_hip.h declares
@@ -410,4 +413,5 @@ ABI_SYMBOLS = [
     "sh_alloc_pinned", "sh_free_pinned", "sh_query_stats", "sh_last_error", "sh_abi_version",
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
+    "sh_aggregation_shard_create",
 ]

@@ -150,6 +150,7 @@ struct sh_aggregation {
     bool has_bucket = false;
     int64_t T_root = 0;
     sh_query* root = nullptr;
+    sh_shard* shard = nullptr;  // sharded: the root is this shard's owner query (owned by the shard)
     bool root_init = false;
     int64_t root_bucket = 0;
     std::vector<Level> levels;            // durations above the root
@@ -359,7 +360,8 @@ static int catch_up(sh_aggregation* a) {
     return SH_OK;
 }
 
-extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, sh_aggregation** out) {
+static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, int32_t world, sh_shard** shard,
+                      sh_aggregation** out) {
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_create: NULL argument");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS || d->n_aggs <= 0 || d->n_aggs > SH_MAX_AGGS ||
         d->min_duration < 0 || d->max_duration > SH_DUR_YEARS || d->min_duration > d->max_duration)
@@ -425,8 +427,13 @@ extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, 
     }
     kp.n = g;
     rd.n_group_by = 0;
-    int rc = sh_query_create_internal(ctx, &rd, kp, &a->root);
+    int rc = shard ? shard_create_root(ctx, &rd, kp, rank, world, &a->shard, &a->root)
+                   : sh_query_create_internal(ctx, &rd, kp, &a->root);
     if (rc) { delete a; return rc; }
+    if (shard) {
+        shard_attach_aggregation(a->shard, a);
+        *shard = a->shard;
+    }
     a->nb = a->root->ap.n;
     a->bp.n = a->nb;
     for (int i = 0; i < a->nb; i++) {
@@ -459,10 +466,22 @@ extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, 
     return SH_OK;
 }
 
-extern "C" int sh_aggregation_destroy(sh_aggregation* a) {
-    if (!a) return SH_OK;
-    (void)hipStreamSynchronize(a->ctx->stream);
-    if (a->root) sh_query_destroy(a->root);
+extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, sh_aggregation** out) {
+    return agg_create(ctx, d, 0, 1, nullptr, out);
+}
+
+// Rank `rank` of `world` of a key-sharded aggregation: events reach the GPU that
+// owns their group key through the sh_shard_* protocol; each owner runs the root and every roll-up
+// level for its keys. The clock, the root buckets and every TIMER are global, so the owners' tables
+// together hold exactly the single-stream tables' rows.
+extern "C" int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, int32_t world,
+                                           sh_shard** shard, sh_aggregation** out) {
+    if (!shard) return sh_fail(SH_ERR_INVALID, "sh_aggregation_shard_create: NULL argument");
+    if (d && d->n_group_by != 1) return sh_fail(SH_ERR_UNSUPPORTED, "sharded aggregations need one group-by key");
+    return agg_create(ctx, d, rank, world, shard, out);
+}
+
+static void agg_free(sh_aggregation* a) {
     for (auto& L : a->levels) {
         DevBuf* bufs[] = {&L.vals, &L.has, &L.tag, &L.first_seq, &L.order, &L.slots, &L.dup, &L.blk, &L.out_bucket, &L.out_key, &L.out_vals};
         for (auto* b : bufs) b->release();
@@ -475,12 +494,23 @@ extern "C" int sh_aggregation_destroy(sh_aggregation* a) {
     a->minmax.release();
     if (a->h_minmax) (void)hipHostFree(a->h_minmax);
     delete a;
+}
+
+extern "C" int sh_aggregation_destroy(sh_aggregation* a) {
+    if (!a) return SH_OK;
+    if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation is released by sh_shard_destroy");
+    (void)hipStreamSynchronize(a->ctx->stream);
+    sh_query_destroy(a->root);
+    a->root = nullptr;
+    agg_free(a);
     return SH_OK;
 }
 
+void agg_release_sharded(sh_aggregation* a) { agg_free(a); }
+
 // Room in the root's key table for this push: (event-time bucket, key) pairs are bounded by
 // min(N, keys x buckets spanned); closed buckets' keys are dropped by the rebuild.
-static int reserve_root_keys(sh_aggregation* a, const sh_batch* dev) {
+int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
     int64_t N = dev->n;
     if (N <= 0) return SH_OK;
     int64_t keys = a->d.n_group_by ? std::max<int64_t>(1, a->d.key_capacity > 0 ? a->d.key_capacity : (1 << 16)) : 1;
@@ -504,12 +534,15 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     } else {
         dev = *b;
     }
-    RCHK(reserve_root_keys(a, &dev));
+    RCHK(agg_reserve_root(a, &dev));
     RCHK(sh_push_device(a->root, &dev, &o));
+    return agg_after_root(a, o);
+}
+
+int agg_after_root(sh_aggregation* a, const sh_out* o) {
     if (o->n_rows > (8 << 20) / 8 && a->d.n_group_by == 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "too many rows in one flush for a constant key column");
-    bool was_init = a->root_init;
-    if (!was_init && a->root->e0_valid) {
+    if (!a->root_init && a->root->e0_valid) {
         a->root_init = true;
         a->root_bucket = a->root->E0 - a->T_root;
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
@@ -520,11 +553,13 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
 
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push: NULL argument");
+    if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
     return agg_push(a, b, true);
 }
 
 extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) {
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push_device: NULL argument");
+    if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
     return agg_push(a, b, false);
 }
 
@@ -532,6 +567,7 @@ extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) 
 
 extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
+    if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation advances through sh_shard_advance_time");
     const sh_out* o = nullptr;
     RCHK(sh_advance_time_device(a->root, now, &o));
     RCHK(pass_root_flushes(a, o));

@@ -200,10 +200,17 @@ struct ShardSrc {
     int G;
     int key32;
 };
-void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
+// 8-byte raw columns a shard record carries: the value columns, then the columns of time-bucket key
+// components (their raw value is needed to re-derive the bucket; only the other components travel
+// in the record's key word)
+struct RawPlan {
+    int n;
+    int src[SH_MAX_COLS];
+};
+void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan wkp, RawPlan rp, int G,
                        i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32);
 struct ColRoles {
-    int role[SH_MAX_COLS];  // -1 unused, 0..7 value slot, 16 + g group-key component g
+    int role[SH_MAX_COLS];  // -1 unused, 0..15 raw slot, 16 + g wire-key component g
     int n;
 };
 struct ColPtrs {

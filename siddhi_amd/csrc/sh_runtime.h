@@ -159,6 +159,16 @@ int sh_query_create_internal(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan&
 // device-output advance (aggregation root)
 int sh_advance_time_device(sh_query* q, int64_t now, const sh_out** out);
 
+// sharded incremental aggregation: the shard's owner query is the aggregation's root
+// (sh_shard.cpp)
+int shard_create_root(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, int32_t rank, int32_t world,
+                      sh_shard** out, sh_query** owner);
+void shard_attach_aggregation(sh_shard* s, sh_aggregation* a);
+// (sh_aggregation.cpp)
+int agg_reserve_root(sh_aggregation* a, const sh_batch* dev);    // key room before the root's push
+int agg_after_root(sh_aggregation* a, const sh_out* root_out);  // root flushes -> roll-up levels
+void agg_release_sharded(sh_aggregation* a);                     // called by sh_shard_destroy
+
 
 // sliding time window (sh_sliding.cpp)
 int sliding_create(sh_query* q);

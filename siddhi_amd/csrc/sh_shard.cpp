@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "sh_agg.h"
 #include "sh_internal.h"
 #include "sh_runtime.h"
 
@@ -37,11 +38,14 @@ struct sh_shard {
     sh_query_desc d{};
     int rank = 0, world = 1;
     FilterProg fp{};
-    KeyPlan kp{};
+    KeyPlan kp{};        // the owner query's group key
+    KeyPlan wkp{};       // the key word a record carries (kp without time-bucket components)
+    RawPlan rp{};        // the 8-byte raw columns a record carries
     AggPlan ap{};
     int rec_words = 6;   // 4-byte words per record
-    int key32 = 0;       // the packed group key fits 32 bits
+    int key32 = 0;       // the wire key fits 32 bits
     sh_query* owner = nullptr;
+    sh_aggregation* agg = nullptr;  // incremental aggregation fed by the owner (its root), or null
     // global stream state (identical on every rank)
     bool clock_valid = false;
     int64_t clock = 0;
@@ -70,7 +74,8 @@ static int64_t wfun_g(const sh_shard* s, int64_t clock) {
     return clock < s->E0 ? 0 : (clock - s->E0) / s->d.window_param + 1;
 }
 
-extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank, int32_t world, sh_shard** out) {
+static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, int32_t rank, int32_t world,
+                        sh_shard** out) {
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_create: NULL argument");
     if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
         return sh_fail(SH_ERR_INVALID, "sh_shard_create: need 0 <= rank < world <= 16");
@@ -88,12 +93,33 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
     int rc;
     if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, s->fp)) ||
         (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, s->ap, vt)) ||
-        (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, s->kp))) {
+        (!kp_override && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, s->kp)))) {
         delete s;
         return rc;
     }
-    s->key32 = (s->kp.n == 0 || (s->kp.n == 1 && s->kp.type[0] != SH_T_LONG && s->kp.div[0] == 0)) ? 1 : 0;
-    s->rec_words = (s->key32 ? 4 : 6) + 2 * s->ap.n_vcols;
+    if (kp_override) s->kp = *kp_override;
+    // wire plan: the key word holds the components that are column values; a time-bucket component
+    // (aggregation roots) travels as its raw column and the owner re-derives the bucket. Owners are
+    // chosen from the key word alone, so a group key keeps its owner across buckets.
+    s->wkp = KeyPlan{};
+    s->rp.n = 0;
+    for (int j = 0; j < s->ap.n_vcols; j++) s->rp.src[s->rp.n++] = s->ap.vcol_src[j];
+    for (int g = 0; g < s->kp.n; g++) {
+        if (s->kp.div[g] > 0) {
+            bool have = false;
+            for (int j = 0; j < s->rp.n; j++) have |= s->rp.src[j] == s->kp.col[g];
+            if (!have) s->rp.src[s->rp.n++] = s->kp.col[g];
+        } else {
+            s->wkp.col[s->wkp.n] = s->kp.col[g];
+            s->wkp.type[s->wkp.n] = s->kp.type[g];
+            s->wkp.div[s->wkp.n] = 0;
+            s->wkp.n++;
+        }
+    }
+    // round-robin owners for one dictionary-id component (dense ids stay dense per owner)
+    s->wkp.dense = (s->wkp.n == 1 && s->wkp.type[0] == SH_T_STRID) ? 1 : 0;
+    s->key32 = (s->wkp.n == 0 || (s->wkp.n == 1 && s->wkp.type[0] != SH_T_LONG)) ? 1 : 0;
+    s->rec_words = (s->key32 ? 4 : 6) + 2 * s->rp.n;
     // the owner runs the same query over the records it receives: no filter (applied at ingest),
     // 8-byte raw columns, windows given per event
     // key_capacity is the whole stream's; an owner holds about 1/G of the keys (dictionary ids
@@ -103,7 +129,11 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
     od.filter = nullptr;
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (1 << 16);
     od.key_capacity = s->kp.dense ? (cap + world - 1) / world : cap / world + cap / (4 * world) + 64;
-    if ((rc = sh_query_create(ctx, &od, &s->owner))) { delete s; return rc; }
+    if ((rc = kp_override ? sh_query_create_internal(ctx, &od, *kp_override, &s->owner)
+                          : sh_query_create(ctx, &od, &s->owner))) {
+        delete s;
+        return rc;
+    }
     sh_query* q = s->owner;
     q->given = true;
     if (s->kp.dense) {
@@ -115,8 +145,8 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
         int t = d->col_types[c];
         q->load_type[c] = (t == SH_T_FLOAT || t == SH_T_DOUBLE) ? SH_T_DOUBLE : SH_T_LONG;
         s->roles.role[c] = -1;
-        for (int g = 0; g < s->kp.n; g++) if (s->kp.col[g] == c) s->roles.role[c] = 16 + g;
-        for (int j = 0; j < s->ap.n_vcols; j++) if (s->ap.vcol_src[j] == c) s->roles.role[c] = j;
+        for (int g = 0; g < s->wkp.n; g++) if (s->wkp.col[g] == c) s->roles.role[c] = 16 + g;
+        for (int j = 0; j < s->rp.n; j++) if (s->rp.src[j] == c) s->roles.role[c] = j;
     }
     if (hipHostMalloc((void**)&s->h_info, sizeof(PushInfo), hipHostMallocDefault) != hipSuccess) {
         sh_query_destroy(s->owner);
@@ -128,9 +158,25 @@ extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank
     return SH_OK;
 }
 
+extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank, int32_t world, sh_shard** out) {
+    return shard_create(ctx, d, nullptr, rank, world, out);
+}
+
+// the root query of a sharded incremental aggregation (sh_aggregation.cpp)
+int shard_create_root(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, int32_t rank, int32_t world,
+                      sh_shard** out, sh_query** owner) {
+    int rc = shard_create(ctx, d, &kp, rank, world, out);
+    if (rc) return rc;
+    *owner = (*out)->owner;
+    return SH_OK;
+}
+
+void shard_attach_aggregation(sh_shard* s, sh_aggregation* a) { s->agg = a; }
+
 extern "C" int sh_shard_destroy(sh_shard* s) {
     if (!s) return SH_OK;
     (void)hipStreamSynchronize(s->ctx->stream);
+    if (s->agg) agg_release_sharded(s->agg);
     if (s->owner) sh_query_destroy(s->owner);
     DevBuf* bufs[] = {&s->blk_pass, &s->blk_tl, &s->blk_first, &s->info, &s->code, &s->counts, &s->tmp,
                       &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx, &s->u_bg, &s->u_bw};
@@ -253,12 +299,12 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         wp.N = N;
         wp.send_size = b->send_size;
         PushInfo* info = s->info.as<PushInfo>();
-        launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), info, s->kp, G, nblk,
+        launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), info, s->wkp, G, nblk,
                             s->code.as<u32>(), s->counts.as<int64_t>(), s->bounds.as<Bound>(), max_bounds,
                             &info->n_bounds);
         HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
         launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
-        launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->kp, s->ap, G, N, nblk,
+        launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk,
                           s->counts.as<int64_t>(), (unsigned char*)send_buf, s->rec_words, s->key32);
         launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
         HIPCHK(hipGetLastError());
@@ -315,6 +361,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
     if (!s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
     s->packed = false;
+    if (s->agg) host_out = 0;  // the root's flushes feed the roll-up levels on the device
     const int64_t RB = 4 * (int64_t)s->rec_words;
     int64_t bytes = 0;
     for (int r = 0; r < s->world; r++) {
@@ -331,6 +378,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     sync_owner(s);
     if (M == 0) {
         RCHK(query_close_given(q, host_out != 0, out));
+        if (s->agg) RCHK(agg_after_root(s->agg, *out));
         set_order(s, host_out != 0, order);
         return SH_OK;
     }
@@ -371,18 +419,20 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         src.gbase[g] = s->cur_seq + s->cur_off[g];
     }
     src.start[s->world] = acc;
-    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->kp, s->roles, src,
+    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->wkp, s->roles, src,
                         s->u_bg.as<int64_t>(), s->u_bw.as<int64_t>(), nb, s->cur_W_base, s->u_ts.as<int64_t>(), cp,
                         s->u_wcol.as<int>(), s->u_gidx.as<u64>());
     HIPCHK(hipGetLastError());
     b.ts = s->u_ts.as<int64_t>();
     q->given_wcol = s->u_wcol.as<int>();
     q->given_gidx = s->u_gidx.as<u64>();
-    int rc = query_push_given(q, &b, host_out != 0, out);
+    int rc = s->agg ? agg_reserve_root(s->agg, &b) : SH_OK;
+    if (!rc) rc = query_push_given(q, &b, host_out != 0, out);
     q->given_wcol = nullptr;
     q->given_gidx = nullptr;
     if (rc) return rc;
     sync_owner(s);
+    if (s->agg) RCHK(agg_after_root(s->agg, *out));
     set_order(s, host_out != 0, order);
     return SH_OK;
 }
@@ -393,7 +443,9 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
     if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");
     sh_query* q = s->owner;
     sync_owner(s);
+    if (s->agg) host_out = 0;
     RCHK(query_advance(q, now, host_out != 0, out));
+    if (s->agg) RCHK(agg_after_root(s->agg, *out));
     if (!(s->clock_valid && now < s->clock)) {
         s->clock = now;
         s->clock_valid = true;

@@ -104,7 +104,7 @@ void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f
 // inside a round, the rank of an event among the same owner's events is (waves before) + (lanes
 // before), so every owner's run keeps event order. offsets = exclusive scan of counts[o][tile].
 __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* __restrict__ ts,
-                                                      const u32* __restrict__ code, KeyPlan kp, AggPlan ap, int G,
+                                                      const u32* __restrict__ code, KeyPlan kp, RawPlan rp, int G,
                                                       i64 N, int nblk, const i64* __restrict__ offsets, u32* out,
                                                       int rec_words, int key32) {
     __shared__ u32 running[kMaxShards];
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
             }
             u64* r8 = (u64*)(rec + w8);
             r8[0] = (u64)ts[e];
-            for (int j = 0; j < ap.n_vcols; j++) r8[1 + j] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            for (int j = 0; j < rp.n; j++) r8[1 + j] = (u64)load_raw(cols, rp.src[j], e);
         }
         __syncthreads();
         if (threadIdx.x < G) {
@@ -162,14 +162,14 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
     }
 }
 
-void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan kp, AggPlan ap, int G,
+void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan wkp, RawPlan rp, int G,
                        i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32) {
-    hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, kp, ap, G, N, nblk, offsets,
+    hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, wkp, rp, G, N, nblk, offsets,
                        (u32*)out, rec_words, key32);
 }
 
 // Received records -> the owner's SoA columns (8-byte raw form for every referenced column).
-// role[c]: -1 unused, 0..7 value slot, 16 + g group-key component g. The global index of a record is
+// role[c]: -1 unused, 0..15 raw slot, 16 + g component g of the wire key (kp = the wire key plan). The global index of a record is
 // its source slice's base + its slice position; its window is that of the last global window start
 // at or before it (binary search over the all-gathered starts), W_base before the first.
 __global__ __launch_bounds__(kBlock) void k_shard_unpack(const u32* __restrict__ rec, i64 M, int rec_words, KeyPlan kp,

@@ -108,6 +108,52 @@ class ShardedQuery:
             pass
 
 
+class ShardedAggregation(ShardedQuery):
+    """Rank `rank` of `world` of a key-sharded `define aggregation ... every sec...year` (C4): the
+    same three-phase ingest as ShardedQuery; this rank's roll-up tables hold the rows of its keys."""
+
+    def __init__(self, spec: abi.AggregationSpec, rank: int, world: int, ctx: Optional[Context] = None):
+        self.spec, self.rank, self.world = spec, rank, world
+        self.ctx = ctx or default_context()
+        self._desc = spec.desc()
+        self.h = C.c_void_p()
+        self.agg = C.c_void_p()
+        _check(lib().sh_aggregation_shard_create(self.ctx.h, C.byref(self._desc), rank, world, C.byref(self.h),
+                                                 C.byref(self.agg)))
+        rb = C.c_int64()
+        _check(lib().sh_shard_record_bytes(self.h, C.byref(rb)))
+        self.record_bytes = rb.value
+
+    def table_arrays(self, duration: int) -> dict:
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_aggregation_table(self.agg, duration, C.byref(out)))
+        return abi.out_arrays(out)
+
+    def close(self):
+        if self.h:
+            lib().sh_shard_destroy(self.h)  # releases the aggregation handle too
+            self.h = None
+            self.agg = None
+
+
+def merge_tables(parts: List[dict]) -> dict:
+    """Union of the owners' rows of one duration's table, in (bucket, key, values) order. An
+    aggregation table is keyed by (AGG_TIMESTAMP, group key) (AggregationParser.initDefaultTables,
+    @PrimaryKey), so its row order carries no meaning; compare tables in this canonical order."""
+    keys = np.concatenate([p["keys"] for p in parts], axis=1)
+    vals = np.concatenate([p["vals"] for p in parts], axis=1)
+    nulls = np.concatenate([p["nulls"] for p in parts], axis=1)
+    return canonical_table({"keys": keys, "vals": vals, "nulls": nulls})
+
+
+def canonical_table(t: dict) -> dict:
+    keys, vals, nulls = t["keys"], t["vals"], t["nulls"]
+    cols = [vals.view(np.int64)[i] for i in range(vals.shape[0] - 1, -1, -1)]
+    cols += [keys[i] for i in range(keys.shape[0] - 1, -1, -1)]
+    perm = np.lexsort(cols) if keys.shape[1] else np.zeros(0, np.int64)
+    return {"keys": keys[:, perm], "vals": vals[:, perm], "nulls": nulls[:, perm]}
+
+
 def host_rows(out, order) -> dict:
     """Host sh_out + order -> out_arrays dict with an 'order' column."""
     d = abi.out_arrays(out)
@@ -162,8 +208,9 @@ class LocalShards:
     """G shards of one query in one process on one device; the exchange is a device copy.
     Drives exactly the protocol a multi-process run drives over torch.distributed."""
 
-    def __init__(self, spec: abi.QuerySpec, world: int, ctx: Optional[Context] = None):
-        self.shards = [ShardedQuery(spec, r, world, ctx) for r in range(world)]
+    def __init__(self, spec, world: int, ctx: Optional[Context] = None):
+        cls = ShardedAggregation if isinstance(spec, abi.AggregationSpec) else ShardedQuery
+        self.shards = [cls(spec, r, world, ctx) for r in range(world)]
         self.world = world
 
     def push(self, slices, send_size: int, device) -> List[dict]:
@@ -191,12 +238,24 @@ class LocalShards:
                 rbytes.append(n)
             recv = torch.cat(blocks) if sum(rbytes) else torch.empty(1, dtype=torch.uint8, device=device)
             torch.cuda.current_stream(device).synchronize()  # the library runs on its own HIP stream
+            if isinstance(s, ShardedAggregation):  # rows go to the roll-up tables
+                s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=False)
+                outs.append(None)
+                continue
             out, order = s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=True)
             outs.append(host_rows(out, order))
         return outs
 
     def advance_time(self, now: int) -> List[dict]:
+        if isinstance(self.shards[0], ShardedAggregation):
+            for s in self.shards:
+                s.advance_time(now, False)
+            return [None] * self.world
         return [host_rows(*s.advance_time(now, True)) for s in self.shards]
+
+    def tables(self, duration: int) -> dict:
+        """The merged (canonical-order) table of one duration over all owners."""
+        return merge_tables([s.table_arrays(duration) for s in self.shards])
 
     def close(self):
         for s in self.shards:
