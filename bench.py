@@ -48,7 +48,7 @@ def parse():
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
     ap.add_argument("--key-type", choices=["string", "int"], default="string",
                     help="k as a dictionary-encoded string (ids are dense key slots) or as an int (hashed)")
-    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "ext"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "c5", "ext"], default="c2",
                     help="c2 = the headline (BASELINE configs[1]); c1/c3/c4/ext = secondary single-GPU lines")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N>1 on one GPU)")
@@ -106,6 +106,9 @@ SECONDARY = {
     "c4": ("C4 define aggregation sum/avg/count/min/max group by k aggregate by ts every sec...day; one GPU's share "
            "of C4 on 8 GPUs: 125k of the 1M keys, 1.25M of the 10M events per event-time second", 25.2),
     "ext": ("externalTimeBatch(et, 1 sec) count/min/max/avg group by k, 100k keys, per-event sends", 32.4),
+    # every event is read (20 B); only the partition that armed the shared timer is aggregated (R12)
+    "c5": ("C5 partition with (k of S) begin from S#window.timeBatch(1 sec) select k, sum(v), count() group by k; "
+           "10M Zipf(1.1) keys, 1M events per event-time second per GPU, per-event sends", 20.0),
 }
 
 
@@ -138,6 +141,13 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         gen = lambda i: synth.torch_keyed_stream((i * world + rank) * B, B, 0xC4, 125_000 * world, 1_250 * world,
                                                  dev)[1]
         mk = lambda cols: (cols[2], cols)
+    elif args.workload == "c5":
+        schema = abi.Schema.parse("k string, v double, ts long")
+        spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"], aggs=[("sum", "v"), ("count", None)],
+                             partition="k", key_capacity=10_000_000)
+        send = 1
+        gen = lambda i: synth.torch_zipf_stream((i * world + rank) * B, B, 0xC5, 10_000_000, 1000 * world, dev)[1]
+        mk = lambda cols: (cols[2], cols)
     else:
         if args.workload == "c3":
             schema = abi.Schema.parse("k string, v double, ts long")
@@ -152,10 +162,10 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         send = 1
         mk = lambda cols: (cols[2], cols)
     if sliced:
-        if not agg:
-            raise SystemExit("of the secondary workloads only c4 runs on N > 1 GPUs")
-        from siddhi_amd.shard import ShardedAggregation, TorchExchange, distributed_push
-        q = ShardedAggregation(agg, rank, world, ctx)
+        if args.workload not in ("c4", "c5"):
+            raise SystemExit("of the secondary workloads only c4 and c5 run on N > 1 GPUs")
+        from siddhi_amd.shard import ShardedAggregation, ShardedQuery, TorchExchange, distributed_push
+        q = ShardedAggregation(agg, rank, world, ctx) if agg else ShardedQuery(spec, rank, world, ctx)
         ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
         send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
     else:
@@ -181,8 +191,10 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     kern_ms, t0 = 0.0, time.perf_counter()
     for i in range(args.warmup, nb):
         push(i)
-        if not agg:
-            kern_ms += q.stats().main_kernel_ms
+        if not agg and not sliced:
+            st = q.stats()
+            # C5's work is the scans over every event (R12 leaves one partition to aggregate)
+            kern_ms += st.push_ms if args.workload == "c5" else st.main_kernel_ms
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -199,14 +211,15 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     roof = None
     if kern_ms > 0:
         ach = bpe * B * args.steps / (kern_ms / 1e3) / 1e9
-        roof = {"bound": "hbm", "kernel": "main (aggregate / sliding)", "achieved": ach, "peak": HBM_PEAK_GBS,
+        kname = "whole device pipeline of the push" if args.workload == "c5" else "main (aggregate / sliding)"
+        roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms_per_step": kern_ms / args.steps,
                 "bytes_per_event": bpe}
     config = {"workload": desc, "events_per_step_per_gpu": B, "send_size": send}
     if sliced:
         config.update(parallelism=f"slice ingest x{world}, key re-shard over "
                                   f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all",
-                      keys_total=125_000 * world,
+                      keys_total=125_000 * world if agg else 10_000_000,
                       phases_ms_per_step_rank0={k: v / args.steps for k, v in phases.items()})
     print(json.dumps({"metric": METRIC, "value": B * args.steps * world / elapsed, "unit": "events/s",
                       "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

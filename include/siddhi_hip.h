@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 2
+#define SH_ABI_VERSION 3
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -256,14 +256,17 @@ int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out
  *                                                   first event, so merging the G outputs of a
  *                                                   flush by `order` yields the single-stream row
  *                                                   order of QuerySelector.processInBatchGroupBy.
- * Supported: timeBatch group-by (not partitioned), and incremental aggregations through
- * sh_aggregation_shard_create (below).                                                       */
+ * Supported: timeBatch group-by, partitioned or not (`partition with (p of S)`: R12 — every rank
+ * restricts the stream to the partition of the globally first passing event), and incremental
+ * aggregations through sh_aggregation_shard_create (below).                                  */
 typedef struct {
     int64_t n;           /* events in the slice                                              */
     int64_t n_pass;      /* events passing the filter                                        */
     int64_t max_tl;      /* max timestamp over the slice's send-last events (INT64_MIN: none) */
     int64_t first_clock; /* clock of the send of the slice's first passing event, without the
                             clock carried in (INT64_MIN: no passing event)                    */
+    int64_t first_key;   /* partitioned queries: partition key of that event (R12: the globally
+                            first one picks the only partition that ever flushes); else 0     */
 } sh_slice_summary;
 
 typedef struct {

@@ -50,8 +50,18 @@ __device__ __forceinline__ void load_items_raw(const ColSet& cs, int c, i64 base
             int4 v = q[j];
             out[4 * j] = v.x; out[4 * j + 1] = v.y; out[4 * j + 2] = v.z; out[4 * j + 3] = v.w;
         }
-    } else if (t == SH_T_LONG) {
+    } else if (t == SH_T_LONG || t == SH_T_DOUBLE) {  // DOUBLE: the bit patterns
         load_items_i64((const i64*)cs.ptr[c], base, N, out, 0);
+    } else if (t == SH_T_FLOAT && base + kItems <= N && (((size_t)((const float*)cs.ptr[c] + base)) & 15) == 0) {
+        const float4* q = (const float4*)((const float*)cs.ptr[c] + base);
+#pragma unroll
+        for (int j = 0; j < kItems / 4; j++) {
+            float4 v = q[j];
+            out[4 * j] = __double_as_longlong((double)v.x);
+            out[4 * j + 1] = __double_as_longlong((double)v.y);
+            out[4 * j + 2] = __double_as_longlong((double)v.z);
+            out[4 * j + 3] = __double_as_longlong((double)v.w);
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < kItems; j++) out[j] = base + j < N ? load_raw(cs, c, base + j) : 0;
@@ -102,8 +112,37 @@ __device__ __forceinline__ bool java_cmp(int op, int ta, i64 a, int tb, i64 b) {
 
 // FilterProcessor.process (core/query/processor/filter/FilterProcessor.java:47-60): a postfix
 // program over column refs and constants; the result must be TRUE to keep the event.
+__device__ __forceinline__ void filter_const(const FilterOpD& o, int& t, i64& v) {
+    t = o.type;
+    if (o.type == SH_T_FLOAT) v = __double_as_longlong((double)(float)o.dval);
+    else if (o.type == SH_T_DOUBLE) v = __double_as_longlong(o.dval);
+    else if (o.type == SH_T_INT) v = (i64)(int)o.ival;
+    else v = o.ival;
+}
+
+__device__ __forceinline__ bool is_leaf(const FilterProg& f, int i) {
+    return f.ops[i].op == SH_OP_COL && f.ops[i + 1].op == SH_OP_CONST && f.ops[i + 2].op >= SH_OP_GT &&
+           f.ops[i + 2].op <= SH_OP_NE;
+}
+
+// `col <cmp> const` (ops i .. i+2) in registers
+__device__ __forceinline__ bool eval_leaf(const FilterProg& f, int i, const ColSet& cs, i64 e) {
+    int tc;
+    i64 vc;
+    filter_const(f.ops[i + 1], tc, vc);
+    const int c = f.ops[i].col;
+    return java_cmp(f.ops[i + 2].op, cs.type[c], load_raw(cs, c, e), tc, vc);
+}
+
 __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& cs, i64 e) {
     if (f.n == 0) return true;
+    // register-only forms of the common programs (the branch is uniform: f is a kernel argument);
+    // the general stack machine below keeps its operand stack in scratch memory
+    if (f.n == 3 && is_leaf(f, 0)) return eval_leaf(f, 0, cs, e);
+    if (f.n == 7 && is_leaf(f, 0) && is_leaf(f, 3)) {
+        if (f.ops[6].op == SH_OP_AND) return eval_leaf(f, 0, cs, e) && eval_leaf(f, 3, cs, e);
+        if (f.ops[6].op == SH_OP_OR) return eval_leaf(f, 0, cs, e) || eval_leaf(f, 3, cs, e);
+    }
     i64 sv[16];
     int st[16];
     int sp = 0;
@@ -131,6 +170,39 @@ __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& c
         }
     }
     return sp > 0 && sv[sp - 1] != 0;
+}
+
+// The filter over one thread's kItems consecutive events: the leaf forms load their columns with
+// the blocked vector loads (16-byte loads per thread) instead of one scattered element load per item.
+__device__ __forceinline__ void leaf_items(const FilterProg& f, int i, const ColSet& cs, i64 base, i64 N,
+                                          bool (&r)[kItems]) {
+    int tc;
+    i64 vc;
+    filter_const(f.ops[i + 1], tc, vc);
+    const int c = f.ops[i].col, op = f.ops[i + 2].op, ta = cs.type[c];
+    i64 x[kItems];
+    load_items_raw(cs, c, base, N, x);
+#pragma unroll
+    for (int j = 0; j < kItems; j++) r[j] = java_cmp(op, ta, x[j], tc, vc);
+}
+
+__device__ __forceinline__ void filter_items(const FilterProg& f, const ColSet& cs, i64 base, i64 N,
+                                            bool (&pass)[kItems]) {
+    if (f.n == 3 && is_leaf(f, 0)) {
+        leaf_items(f, 0, cs, base, N, pass);
+    } else if (f.n == 7 && is_leaf(f, 0) && is_leaf(f, 3) && (f.ops[6].op == SH_OP_AND || f.ops[6].op == SH_OP_OR)) {
+        bool a[kItems], b[kItems];
+        leaf_items(f, 0, cs, base, N, a);
+        leaf_items(f, 3, cs, base, N, b);
+        const bool conj = f.ops[6].op == SH_OP_AND;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) pass[j] = conj ? (a[j] && b[j]) : (a[j] || b[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) pass[j] = base + j < N && eval_filter(f, cs, base + j);
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; j++) pass[j] = pass[j] && base + j < N;
 }
 
 // ---- group keys ---------------------------------------------------------------------------------

@@ -160,7 +160,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, RowTmp* rows, u64* row_vals,
                       u32* row_counter, unsigned char* flags, u32* rowref, i64* seg_rows,
-                      // partitioned source (P > 1)
+                      // multisplit source (always when P > 1; null: the flat kernel reads the batch)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
                       const i64* seg_off);
 size_t aggregate_own_lds(int NL, int n_fields, int n_vcols);

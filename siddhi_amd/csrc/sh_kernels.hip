@@ -23,12 +23,14 @@ __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts,
     i64 cnt = 0, tl = INT64_MIN, first = INT64_MAX, xm = INT64_MIN;
     i64 tsv[kItems];
     load_items_i64(ts, base, wp.N, tsv, INT64_MIN);
+    bool pass[kItems];
+    filter_items(f, cols, base, wp.N, pass);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
-            if (eval_filter(f, cols, e)) {
+            if (pass[i]) {
                 cnt++;
                 if (first == INT64_MAX) first = e;
                 if (blk_xm) xm = max(xm, load_raw(cols, wp.ts_col, e));
@@ -194,12 +196,12 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     i64 t[kItems];
     i64 cnt = 0, tl = INT64_MIN;
     load_items_i64(ts, base, wp.N, t, INT64_MIN);
+    filter_items(f, cols, base, wp.N, pass);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         bool in = e < wp.N;
-        pass[i] = in && eval_filter(f, cols, e);
         cnt += pass[i];
         if (in && sc.last(wp, e)) tl = max(tl, t[i]);
         sc.next();
@@ -642,7 +644,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       i64* seg_rows, const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
                       const i64* seg_off) {
     size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
-    if (P > 1) {
+    if (rec_pos) {  // multisplit records: lane-ownership kernel (P >= 1)
         lds = aggregate_own_lds(NL, ap.n_fields, ap.n_vcols);
 #define SH_AGG_OWN(VV)                                                                                           \
     hipLaunchKernelGGL((k_aggregate_own<own_rounds(VV), VV>), dim3(nseg * P), dim3(kOwnT), lds, s, segs, P, logP, NL, ap, \

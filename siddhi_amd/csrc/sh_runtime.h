@@ -145,6 +145,9 @@ struct sh_query {
     std::vector<int64_t> order_host;
 };
 
+// the filter restricted to partition key `key` (R12): base AND (pcol == key)
+int partition_filter(const FilterProg& base, int pcol, int ptype, int64_t key, FilterProg* out);
+
 // sharded owner helpers (sh_window.cpp)
 int64_t given_flush_clock(const sh_query* q, int64_t W);
 int query_push_given(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);

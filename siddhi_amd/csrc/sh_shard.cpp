@@ -37,7 +37,9 @@ struct sh_shard {
     sh_ctx* ctx = nullptr;
     sh_query_desc d{};
     int rank = 0, world = 1;
-    FilterProg fp{};
+    FilterProg fp{};     // the ingest filter (partitioned: AND partition == p0 once p0 is known)
+    FilterProg fp_orig{};
+    bool partitioned = false, p0_known = false;
     KeyPlan kp{};        // the owner query's group key
     KeyPlan wkp{};       // the key word a record carries (kp without time-bucket components)
     RawPlan rp{};        // the 8-byte raw columns a record carries
@@ -81,7 +83,6 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_INVALID, "sh_shard_create: need 0 <= rank < world <= 16");
     if (d->window != SH_WIN_TIME_BATCH)
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch group-by queries");
-    if (d->partition_col >= 0) return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest of partitioned queries");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     sh_shard* s = new sh_shard();
     s->ctx = ctx;
@@ -98,6 +99,8 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return rc;
     }
     if (kp_override) s->kp = *kp_override;
+    s->fp_orig = s->fp;
+    s->partitioned = d->partition_col >= 0;
     // wire plan: the key word holds the components that are column values; a time-bucket component
     // (aggregation roots) travels as its raw column and the owner re-derives the bucket. Owners are
     // chosen from the key word alone, so a group key keeps its owner across buckets.
@@ -136,7 +139,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     sh_query* q = s->owner;
     q->given = true;
-    if (s->kp.dense) {
+    if (q->kp.dense) {
         q->kt.dmul = (uint32_t)world;
         q->kt.dadd = (uint32_t)rank;
     }
@@ -229,6 +232,19 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     out->n_pass = s->h_info->total_pass;
     out->max_tl = s->h_info->max_tl;
     out->first_clock = s->h_info->first_pass == INT64_MAX ? INT64_MIN : s->h_info->first_clk;
+    out->first_key = 0;
+    if (s->partitioned && !s->p0_known && s->h_info->first_pass != INT64_MAX) {
+        // partition key of the slice's first passing event (PartitionStreamReceiver :176-272)
+        const int pc = s->d.partition_col;
+        const int64_t e = s->h_info->first_pass;
+        if (s->d.col_types[pc] == SH_T_LONG) {
+            HIPCHK(hipMemcpy(&out->first_key, (const char*)b->cols[pc] + e * 8, 8, hipMemcpyDeviceToHost));
+        } else {
+            int32_t k32 = 0;
+            HIPCHK(hipMemcpy(&k32, (const char*)b->cols[pc] + e * 4, 4, hipMemcpyDeviceToHost));
+            out->first_key = k32;
+        }
+    }
     return SH_OK;
 }
 
@@ -254,6 +270,19 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     }
     const int64_t clock_end = c, n_total = o;
     if (s->seq + (uint64_t)n_total >= (1ull << 40)) return sh_fail(SH_ERR_UNSUPPORTED, "stream longer than 2^40 events");
+    // R12: the partition of the stream's first passing event armed the shared timer and is the only
+    // one that ever flushes; from here on the ingest keeps only its events (the owner needs no filter)
+    if (s->partitioned && !s->p0_known) {
+        for (int r = 0; r < G; r++) {
+            if (all[r].n_pass == 0) continue;
+            const int pc = s->d.partition_col;
+            RCHK(partition_filter(s->fp_orig, pc, s->d.col_types[pc], all[r].first_key, &s->fp));
+            s->p0_known = true;
+            s->owner->p0 = all[r].first_key;
+            s->owner->p0_known = true;
+            break;
+        }
+    }
     // nextEmitTime: initialised by the first send that reaches the window (TimeBatch :266-276, 342-347)
     if (!s->e0_valid) {
         for (int r = 0; r < G; r++) {

@@ -33,12 +33,12 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
     i64 t[kItems];
     i64 tl = INT64_MIN;
     SendCursor sc(wp, base);
+    load_items_i64(ts, base, wp.N, t, INT64_MIN);
+    filter_items(f, cols, base, wp.N, pass);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         bool in = e < wp.N;
-        t[i] = in ? ts[e] : INT64_MIN;
-        pass[i] = in && eval_filter(f, cols, e);
         if (in && sc.last(wp, e)) tl = max(tl, t[i]);
         sc.next();
     }

@@ -20,12 +20,14 @@ __global__ __launch_bounds__(kBlock) void k_sl_blockagg(const i64* __restrict__ 
                                                        WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_pm) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     i64 cnt = 0, tl = INT64_MIN, pm = INT64_MIN;
+    bool pass[kItems];
+    filter_items(f, cols, base, wp.N, pass);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
             i64 t = ts[e];
-            if (eval_filter(f, cols, e)) { cnt++; pm = max(pm, t); }
+            if (pass[i]) { cnt++; pm = max(pm, t); }
             if (is_send_last(wp, e)) tl = max(tl, t);
         }
     }
@@ -76,10 +78,10 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     i64 cnt = 0, tl = INT64_MIN, pm = INT64_MIN;
+    filter_items(f, cols, base, wp.N, pass);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        pass[i] = e < wp.N && eval_filter(f, cols, e);
         if (e < wp.N) {
             i64 t = ts[e];
             cnt += pass[i];

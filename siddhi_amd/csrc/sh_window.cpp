@@ -187,6 +187,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
+    if (d->partition_col >= 0) {
+        // R12: only partition p0 is ever aggregated. Its group keys are a sparse subset of the
+        // dictionary, so they go to the hash table; grouped by the partition key alone it is one key.
+        q->kp.dense = 0;
+        if (d->n_group_by == 1 && d->group_by[0] == d->partition_col) cap = 1;
+    }
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
@@ -237,7 +243,13 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     HIPCHK(hipMemcpyAsync(q->segs.p, segs.data(), nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
     const u32* rec_pos = nullptr; const u32* rec_idx = nullptr; const u64* rec_vals = nullptr;
     int64_t rec_cap = 0;
-    if (q->P > 1) {
+    // One flat workgroup per segment walks every event of the segment, passing or not, and
+    // serialises a key's events in conflict rounds: fine for short batches, latency-bound for long
+    // windows of few keys or sparse partitions (R12 keeps one partition). Those take the compacting
+    // multisplit and the lane-ownership kernel even with one key partition.
+    const bool own = q->P > 1 || ((q->partitioned || closed_hi / nseg >= 65536) &&
+                                  aggregate_own_lds(q->NL, q->ap.n_fields, q->ap.n_vcols) <= 80 * 1024);
+    if (own) {
         RCHK(run_multisplit(q, closed_hi, b, &rec_pos, &rec_idx, &rec_vals, &rec_cap));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
         int nblk = (int)((closed_hi + kTile - 1) / kTile);
@@ -398,19 +410,22 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
 }
 
 // Restrict the query to partition key p0 (the partition that armed the shared timer, R12).
+int partition_filter(const FilterProg& base, int pcol, int ptype, int64_t key, FilterProg* out) {
+    FilterProg fp = base;
+    if (fp.n + 4 > kMaxFilterOps) return sh_fail(SH_ERR_UNSUPPORTED, "filter too long for a partitioned query");
+    fp.ops[fp.n++] = FilterOpD{SH_OP_COL, 0, pcol, 0, 0, 0.0};
+    fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, ptype, 0, 0, key, 0.0};
+    fp.ops[fp.n++] = FilterOpD{SH_OP_EQ, 0, 0, 0, 0, 0.0};
+    if (base.n > 0) fp.ops[fp.n++] = FilterOpD{SH_OP_AND, 0, 0, 0, 0, 0.0};
+    *out = fp;
+    return SH_OK;
+}
+
 int query_set_partition(sh_query* q, int64_t key) {
     int pc = q->d.partition_col;
-    int t = q->d.col_types[pc];
     q->p0 = key;
     q->p0_known = true;
-    FilterProg fp = q->fp_orig;
-    if (fp.n + 4 > kMaxFilterOps) return sh_fail(SH_ERR_UNSUPPORTED, "filter too long for a partitioned query");
-    fp.ops[fp.n++] = FilterOpD{SH_OP_COL, 0, pc, 0, 0, 0.0};
-    fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, t, 0, 0, key, 0.0};
-    fp.ops[fp.n++] = FilterOpD{SH_OP_EQ, 0, 0, 0, 0, 0.0};
-    if (q->fp_orig.n > 0) fp.ops[fp.n++] = FilterOpD{SH_OP_AND, 0, 0, 0, 0, 0.0};
-    q->fp = fp;
-    return SH_OK;
+    return partition_filter(q->fp_orig, pc, q->d.col_types[pc], key, &q->fp);
 }
 
 // sh_query_restore: a key table of the snapshot's size and room for its queued events.

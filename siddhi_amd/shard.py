@@ -24,7 +24,7 @@ import numpy as np
 from . import abi
 from .runtime import Context, _check, default_context, lib
 
-SUMMARY_WORDS = 4
+SUMMARY_WORDS = 5
 BOUND_WORDS = 4
 
 
@@ -55,14 +55,14 @@ class ShardedQuery:
         self._b = _batch(n, ts_ptr, col_ptrs, send_size)
         s = abi.SliceSummary()
         _check(lib().sh_shard_summarize(self.h, C.byref(self._b), C.byref(s)))
-        return np.array([s.n, s.n_pass, s.max_tl, s.first_clock], dtype=np.int64)
+        return np.array([s.n, s.n_pass, s.max_tl, s.first_clock, s.first_key], dtype=np.int64)
 
     def pack(self, summaries: np.ndarray, send_ptr: int, send_cap: int) -> Tuple[np.ndarray, np.ndarray]:
         """summaries: [world, 4] int64. Returns (send_bytes[world], bounds[k, 4] int64)."""
         summ = np.ascontiguousarray(summaries, dtype=np.int64).reshape(self.world, SUMMARY_WORDS)
         arr = (abi.SliceSummary * self.world)()
         for r in range(self.world):
-            arr[r].n, arr[r].n_pass, arr[r].max_tl, arr[r].first_clock = (int(x) for x in summ[r])
+            arr[r].n, arr[r].n_pass, arr[r].max_tl, arr[r].first_clock, arr[r].first_key = (int(x) for x in summ[r])
         sb = (C.c_int64 * self.world)()
         bp = C.POINTER(abi.Bound)()
         nb = C.c_int64()

@@ -94,6 +94,21 @@ def torch_draws(seed: int, start: int, n: int, width: int, device):
     return _t_mix64(z).reshape(n, width)
 
 
+def torch_zipf_stream(start: int, n: int, seed: int, keys: int, events_per_ms: int, device, s: float = 1.1):
+    """C5 on the GPU: Zipf(s) keys over [0, keys) (zipf_keys' inverse CDF, float64 on the device)
+    and uniform [0, 200) values; returns (ts, [k int32, v float64, ts int64]) torch tensors."""
+    import torch
+    d = torch_draws(seed, start, n, 2, device)
+    u = _t_lsr(d[:, 0], 11).to(torch.float64) * (2.0 ** -53)
+    a = 1.0 - s
+    hi = (keys + 1.0) ** a
+    x = (1.0 + u * (hi - 1.0)) ** (1.0 / a)
+    k = torch.clamp(torch.floor(x) - 1, max=keys - 1).to(torch.int32)
+    v = _t_lsr(d[:, 1], 11).to(torch.float64) * (2.0 ** -53) * 200.0
+    ts = T0 + torch.arange(start, start + n, dtype=torch.int64, device=device) // events_per_ms
+    return ts, [k.contiguous(), v.contiguous(), ts.clone()]
+
+
 def torch_keyed_stream(start: int, n: int, seed: int, keys: int, events_per_ms: int, device):
     """keyed_stream() on the GPU: returns (ts, [k int32, v float64, ts int64]) torch tensors."""
     import torch

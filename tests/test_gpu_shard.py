@@ -112,3 +112,25 @@ def test_sharded_dictionary_keys_round_robin_owners():
     got = run_sharded(sp, 4, pushes, 1, [[0.3, 0.5, 0.9]], advance=adv)
     ref = run_oracle(sp, pushes, 1, advance=adv)
     assert_same(got, ref, label="sharded dict x4")
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_sharded_partition_with_zipf_keys(world):
+    """C5: `partition with (k of S) begin from S#window.timeBatch(1 sec) select k, sum(v), count()
+    group by k` — R12: only the partition of the globally first passing event ever flushes; here the
+    first slices hold no passing event, so a later rank's slice decides it."""
+    sch = abi.Schema.parse("k int, v long, ts long")
+    n = 60_000  # the oracle's scheduler scans every partition per send (Scheduler.java:75-98)
+    ts = synth.T0 + np.arange(n, dtype=np.int64) // 10
+    ts[30_000:] += 7_500  # an idle gap of several windows
+    k = synth.zipf_keys(0, n, 0xC5, 1_000)
+    v = (np.arange(n, dtype=np.int64) * 7919) % 1000
+    sp = abi.QuerySpec(sch, "timeBatch", 1000, group_by=["k"], aggs=[("sum", "v"), ("count", None)],
+                       filter=(">", "ts", int(ts[int(0.5 * n / world)])), partition="k", key_capacity=1_000)
+    pushes = [(ts[:20_000], [k[:20_000], v[:20_000], ts[:20_000]]),
+              (ts[20_000:], [k[20_000:], v[20_000:], ts[20_000:]])]
+    adv = int(ts[-1]) + 5000
+    got = run_sharded(sp, world, pushes, 1, [[(g + 1) / world for g in range(world - 1)]], advance=adv)
+    ref = run_oracle(sp, pushes, 1, advance=adv)
+    assert ref["flush_offsets"].size > 5
+    assert_same(got, ref, label=f"sharded partition x{world}")
