@@ -1,12 +1,12 @@
 #!/bin/bash
-# One SQ counter pass over the C2 bench: scripts/pmc_sq.sh <tag> <counters...> (<= 8 SQ counters)
+# One SQ counter pass over the bench (C2, or BENCH_ARGS): scripts/pmc_sq.sh <tag> <counters...> (<= 8 SQ)
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc "$@" -d "$OUT/sq" -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/b.json" 2> "$OUT/err" || exit $?
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/b.json" 2> "$OUT/err" || exit $?
 python3 - "$OUT" <<'PY'
 import csv, sys, glob, collections, re
 f = glob.glob(sys.argv[1] + "/sq/**/run_counter_collection.csv", recursive=True)

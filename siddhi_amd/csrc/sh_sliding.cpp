@@ -29,13 +29,13 @@ using namespace shd;
 
 struct SlidingImpl {
     int64_t nslots = 0, rc = 0;
-    int P = 1;
+    int P = 1, logP = 0;
     int64_t pm = INT64_MIN;   // PM carried across pushes
     int64_t send_base = 0;    // global send number of the push's first send
     DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
     // per push scratch
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
-        tmp, ranks, part_off, flags, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
+        tmp, ranks, part_off, flags, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
         out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, flush_off, flush_clock;
     SlInfo* h_info = nullptr;
     sh_out dev_out{};
@@ -117,8 +117,12 @@ int sliding_create(sh_query* q) {
         return sh_fail(SH_ERR_OOM, "pinned alloc failed");
     RCHK(size_rings(q, 64));
     int P = 1;
-    while (P < 1024 && (int64_t)P * 8 < n) P <<= 1;
+    // key partitions of at most 64 local keys: one lane of k_sl_own per key (the multisplit's LDS
+    // histogram caps P at 4096; beyond that lanes own several keys)
+    while (P < 4096 && (int64_t)P * 64 < n) P <<= 1;
     s->P = P;
+    s->logP = 0;
+    while ((1 << s->logP) < P) s->logP++;
     (void)hipEventCreate(&q->ev_push0); (void)hipEventCreate(&q->ev_push1);
     (void)hipEventCreate(&q->ev_agg0); (void)hipEventCreate(&q->ev_agg1);
     return SH_OK;
@@ -130,7 +134,8 @@ void sliding_destroy(sh_query* q) {
     DevBuf* bufs[] = {&s->cnt, &s->f, &s->mm, &s->mm_has, &s->dq_head, &s->dq_len, &s->dq, &s->rhead, &s->rlen,
                       &s->rpm, &s->rval, &s->cur_send, &s->cur_first, &s->blk_pass, &s->blk_tl, &s->blk_pm,
                       &s->info, &s->rec_raw, &s->rec_slot, &s->rec_clock, &s->rec_pm, &s->rec_ts, &s->rec_vals,
-                      &s->slot_cnt, &s->counts, &s->tmp, &s->ranks, &s->part_off, &s->flags, &s->rows_ts,
+                      &s->slot_cnt, &s->counts, &s->tmp, &s->ranks, &s->part_off, &s->flags, &s->p_raw,
+                      &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
                       &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
                       &s->out_expired, &s->flush_off, &s->flush_clock};
@@ -222,9 +227,19 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
         HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
         SlRows rows{s->rows_ts.as<int64_t>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
                     s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
+        // the records in partition order
+        RCHK(s->p_raw.reserve(M * 4, false));
+        RCHK(s->p_slot.reserve(M * 4, false));
+        RCHK(s->p_clock.reserve(M * 8, false));
+        RCHK(s->p_pm.reserve(M * 8, false));
+        RCHK(s->p_ts.reserve(M * 8, false));
+        RCHK(s->p_vals.reserve((size_t)V * M * 8, false));
+        SlRecords prec{s->p_raw.as<u32>(), s->p_slot.as<u32>(), s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
+                       s->p_ts.as<int64_t>(), s->p_vals.as<u64>(), M};
+        launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
         HIPCHK(hipEventRecord(q->ev_agg0, st));
-        launch_sliding(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, rec, state_of(s), q->ap,
-                       q->d.window_param, b->send_size, s->send_base, rows, s->flags.as<unsigned char>());
+        launch_sliding_own(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, s->logP, prec, state_of(s), q->ap,
+                           q->d.window_param, b->send_size, s->send_base, rows, s->flags.as<unsigned char>());
         HIPCHK(hipEventRecord(q->ev_agg1, st));
         HIPCHK(hipGetLastError());
         // emit in rank order

@@ -405,6 +405,856 @@ __global__ __launch_bounds__(64) void k_sliding(const u32* __restrict__ rank_lis
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_sl_own: one wave per key partition, lane ownership. Local key li = slot >> logP belongs to lane
+// li & 63 (with NL <= 64 local keys every lane owns at most one key, whose state — counts, sums,
+// min/max values, ring and deque heads — stays in registers for the whole push). The partition's
+// records (event order) are taken in chunks; each chunk is split stably in LDS into 64 per-lane
+// lists, and every lane replays its key's events in order: lazy expiry from the ring head, add, row.
+// No conflict rounds. Latency is what bounds it (one dependent chain per key), so:
+//  - the next record's fields and the next ring-head entry are loaded one step ahead;
+//  - the min/max deques (MinAttributeAggregatorExecutor's LinkedList with removeFirstOccurrence)
+//    live in LDS, kDqL entries per (key, aggregator); a deque that outgrows that spills to its ring
+//    in global memory for the rest of the push (sorted input makes deques as long as the window).
+// ------------------------------------------------------------------------------------------------
+constexpr int kSlCh = 2048;
+constexpr int kSlKeyLanes = 8;  // key-owning lanes per wave of k_sl_own_d
+constexpr int kDqL = 32;
+
+template <int NA, int NV>
+struct LaneKey {
+    u32 k;  // cached slot (kNoPos: none)
+    i64 cnt, rh, rlen, cur_send, cur_first;
+    u64 f[NA], mm[NA], dqf[NA], dqb[NA];
+    i64 dqh[NA], dql[NA];
+    unsigned char mmh[NA];
+    bool spill[NA];
+    bool hvalid;
+    i64 hpm;
+    u64 hval[NV];
+    i64 hb_base;  // ring index of the first entry in the lane's LDS head cache
+    int hb_n;     // valid entries there
+};
+constexpr int kHb = 8;  // ring-head entries fetched per refill (one latency per kHb expiries)
+
+__device__ __forceinline__ bool is_mm(int kind) { return kind >= AK_MIN_L; }
+
+// v[i] with a run-time i, as a select chain over the unrolled slots (keeps v in registers)
+template <int NV>
+__device__ __forceinline__ u64 pick(const u64 (&v)[NV], int i) {
+    u64 x = v[0];
+#pragma unroll
+    for (int q = 1; q < NV; q++) x = (i == q) ? v[q] : x;
+    return x;
+}
+
+// deque storage of aggregator a for the lane's key: LDS ring (kDqL) or, spilled, the global ring
+struct DqView {
+    u64* g;
+    u64* l;
+    i64 gm;
+    bool spill;
+    __device__ __forceinline__ u64 get(i64 i) const { return spill ? g[i & gm] : l[i & (kDqL - 1)]; }
+    __device__ __forceinline__ void set(i64 i, u64 v) const {
+        if (spill) g[i & gm] = v;
+        else l[i & (kDqL - 1)] = v;
+    }
+};
+
+template <int NA, int NV>
+__device__ __forceinline__ DqView dq_view(const LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, u64* lds_dq,
+                                          const int (&mmi)[NA], int a) {
+    DqView d;
+    d.g = S.dq + ((size_t)ap.field[a] * S.nslots + L.k) * S.rc;
+    d.l = lds_dq + ((size_t)mmi[a] * 64 + threadIdx.x) * kDqL;
+    d.gm = S.rc - 1;
+    d.spill = L.spill[a];
+    return d;
+}
+
+template <int NA, int NV>
+__device__ __forceinline__ void lk_load(LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, u64* lds_dq,
+                                        const int (&mmi)[NA], u32 k) {
+    L.k = k;
+    L.cnt = S.cnt[k];
+    L.rh = S.rhead[k];
+    L.rlen = S.rlen[k];
+    L.cur_send = S.cur_send[k];
+    L.cur_first = S.cur_first[k];
+    L.hvalid = false;
+    L.hb_n = 0;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) break;
+        const int kind = ap.kind[a];
+        if (kind == AK_COUNT) continue;
+        const size_t fi = (size_t)ap.field[a] * S.nslots + k;
+        L.f[a] = S.f[fi];
+        if (is_mm(kind)) {
+            L.mm[a] = S.mm[fi];
+            L.mmh[a] = S.mm_has[fi];
+            L.dqh[a] = S.dq_head[fi];
+            L.dql[a] = S.dq_len[fi];
+            L.spill[a] = L.dql[a] >= kDqL;
+            const DqView d = dq_view(L, S, ap, lds_dq, mmi, a);
+            const i64 h = L.dqh[a], len = L.dql[a];
+            if (!d.spill)
+                for (i64 i = 0; i < len; i++) d.l[(h + i) & (kDqL - 1)] = d.g[(h + i) & d.gm];
+            if (len > 0) {
+                L.dqf[a] = d.get(h);
+                L.dqb[a] = d.get(h + len - 1);
+            }
+        }
+    }
+}
+
+template <int NA, int NV>
+__device__ __forceinline__ void lk_store(const LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, u64* lds_dq,
+                                         const int (&mmi)[NA]) {
+    const u32 k = L.k;
+    S.cnt[k] = L.cnt;
+    S.rhead[k] = L.rh;
+    S.rlen[k] = L.rlen;
+    S.cur_send[k] = L.cur_send;
+    S.cur_first[k] = L.cur_first;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) break;
+        const int kind = ap.kind[a];
+        if (kind == AK_COUNT) continue;
+        const size_t fi = (size_t)ap.field[a] * S.nslots + k;
+        S.f[fi] = L.f[a];
+        if (is_mm(kind)) {
+            S.mm[fi] = L.mm[a];
+            S.mm_has[fi] = L.mmh[a];
+            S.dq_head[fi] = L.dqh[a];
+            S.dq_len[fi] = L.dql[a];
+            const DqView d = dq_view(L, S, ap, lds_dq, mmi, a);
+            if (!d.spill)
+                for (i64 i = 0; i < L.dql[a]; i++) d.g[(L.dqh[a] + i) & d.gm] = d.l[(L.dqh[a] + i) & (kDqL - 1)];
+        }
+    }
+}
+
+// the ring head entry (index rh) into registers, from the lane's LDS cache of the next kHb
+// entries; a refill loads up to kHb entries (never past the current tail) in one round trip
+template <int NA, int NV>
+__device__ __forceinline__ void lk_head(LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, i64* hb_pm,
+                                        u64* hb_v) {
+    const int lane = threadIdx.x;
+    if (!(L.rh >= L.hb_base && L.rh < L.hb_base + L.hb_n)) {
+        const int n = (int)min<i64>(kHb, L.rlen);
+        i64 pm[kHb];
+        u64 vv[NV][kHb];
+#pragma unroll
+        for (int e = 0; e < kHb; e++) {
+            if (e < n) {
+                const i64 sl = (L.rh + e) & (S.rc - 1);
+                pm[e] = S.rpm[(size_t)L.k * S.rc + sl];
+#pragma unroll
+                for (int j = 0; j < NV; j++)
+                    if (j < ap.n_vcols) vv[j][e] = S.rval[((size_t)j * S.nslots + L.k) * S.rc + sl];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < kHb; e++) {
+            if (e < n) {
+                hb_pm[lane * kHb + e] = pm[e];
+#pragma unroll
+                for (int j = 0; j < NV; j++)
+                    if (j < ap.n_vcols) hb_v[(j * 64 + lane) * kHb + e] = vv[j][e];
+            }
+        }
+        L.hb_base = L.rh;
+        L.hb_n = n;
+    }
+    const int e = (int)(L.rh - L.hb_base);
+    L.hpm = hb_pm[lane * kHb + e];
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        if (j >= ap.n_vcols) break;
+        L.hval[j] = hb_v[(j * 64 + lane) * kHb + e];
+    }
+    L.hvalid = true;
+}
+
+// AttributeAggregatorExecutor.processRemove for every aggregator (same arithmetic as sl_remove)
+template <int NA, int NV>
+__device__ __forceinline__ void lk_remove(LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, u64* lds_dq,
+                                          const int (&mmi)[NA], const u64 (&v)[NV]) {
+    const i64 c = L.cnt - 1;
+    L.cnt = c;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) break;
+        const int kind = ap.kind[a];
+        if (kind == AK_COUNT) continue;
+        const u64 x = pick(v, ap.vcol[a]);
+        if (kind == AK_SUM_L) {
+            L.f[a] = (u64)java_d2l((double)(i64)L.f[a] - (double)(i64)x);
+        } else if (kind == AK_SUM_D || kind == AK_AVG) {
+            const double xv = (kind == AK_AVG && !(ap.vcol_type[ap.vcol[a]] == SH_T_FLOAT ||
+                                                   ap.vcol_type[ap.vcol[a]] == SH_T_DOUBLE))
+                                  ? (double)(i64)x : __longlong_as_double((i64)x);
+            double r = __longlong_as_double((i64)L.f[a]) - xv;
+            if (c == 0 && r == 0.0) r = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
+            L.f[a] = (u64)__double_as_longlong(r);
+        } else {
+            // removeFirstOccurrence(value): the front in the common case, else a scan
+            const DqView d = dq_view(L, S, ap, lds_dq, mmi, a);
+            i64 h = L.dqh[a], len = L.dql[a];
+            if (len > 0 && boxed_eq(kind, L.dqf[a], x)) {
+                h++;
+                len--;
+                if (len > 0) L.dqf[a] = d.get(h);
+            } else if (len > 1) {
+                i64 found = -1;
+                for (i64 i = 1; i < len; i++)
+                    if (boxed_eq(kind, d.get(h + i), x)) { found = i; break; }
+                if (found >= 0) {
+                    for (i64 i = found; i + 1 < len; i++) d.set(h + i, d.get(h + i + 1));
+                    len--;
+                    L.dqb[a] = d.get(h + len - 1);
+                }
+            }
+            L.dqh[a] = h;
+            L.dql[a] = len;
+            if (len > 0) { L.mm[a] = L.dqf[a]; L.mmh[a] = 1; }
+            else L.mmh[a] = 0;
+        }
+    }
+}
+
+// processAdd (same arithmetic as sl_add)
+template <int NA, int NV>
+__device__ __forceinline__ void lk_add(LaneKey<NA, NV>& L, const SlState& S, const AggPlan& ap, u64* lds_dq,
+                                       const int (&mmi)[NA], const u64 (&v)[NV]) {
+    L.cnt = L.cnt + 1;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) break;
+        const int kind = ap.kind[a];
+        if (kind == AK_COUNT) continue;
+        const u64 x = pick(v, ap.vcol[a]);
+        if (kind == AK_SUM_L) {
+            L.f[a] = (u64)((i64)L.f[a] + (i64)x);
+        } else if (kind == AK_SUM_D || kind == AK_AVG) {
+            const double xv = (kind == AK_AVG && !(ap.vcol_type[ap.vcol[a]] == SH_T_FLOAT ||
+                                                   ap.vcol_type[ap.vcol[a]] == SH_T_DOUBLE))
+                                  ? (double)(i64)x : __longlong_as_double((i64)x);
+            L.f[a] = (u64)__double_as_longlong(__longlong_as_double((i64)L.f[a]) + xv);
+        } else {
+            DqView d = dq_view(L, S, ap, lds_dq, mmi, a);
+            const i64 h = L.dqh[a];
+            i64 len = L.dql[a];
+            while (len > 0 && mm_worse(kind, L.dqb[a], x)) {
+                len--;
+                if (len > 0) L.dqb[a] = d.get(h + len - 1);
+            }
+            if (!d.spill && len == kDqL) {  // the LDS ring is full: move to the global ring
+                for (i64 i = 0; i < len; i++) d.g[(h + i) & d.gm] = d.l[(h + i) & (kDqL - 1)];
+                L.spill[a] = true;
+                d.spill = true;
+            }
+            d.set(h + len, x);
+            len++;
+            L.dqb[a] = x;
+            if (len == 1) L.dqf[a] = x;
+            L.dql[a] = len;
+            if (!L.mmh[a] || mm_worse(kind, L.mm[a], x)) { L.mm[a] = x; L.mmh[a] = 1; }
+        }
+    }
+}
+
+template <int NV>
+struct SlRec {
+    i64 clk, pm, ts;
+    u32 raw;
+    u64 v[NV];
+};
+
+template <int NV>
+__device__ __forceinline__ void sl_rec_load(SlRec<NV>& o, const SlRecords& rec, const AggPlan& ap, i64 r) {
+    o.clk = rec.clock[r];
+    o.pm = rec.pm[r];
+    o.ts = rec.ts[r];
+    o.raw = rec.raw[r];
+#pragma unroll
+    for (int q = 0; q < NV; q++) {
+        if (q >= ap.n_vcols) break;
+        o.v[q] = rec.vals[(size_t)q * rec.cap + r];
+    }
+}
+
+// Chunk split shared by the k_sl_own kernels: records [c0, c0+n) of the partition (event order)
+// into 64 stable per-lane lists (lane = (slot >> logP) & 63). Returns this lane's count and start.
+template <int KL = 64>
+__device__ __forceinline__ void sl_chunk_split(const u32* __restrict__ rank_list, const u32* __restrict__ slot, i64 c0,
+                                               int n, int logP, u32* ch_rank, u32* ch_slot, unsigned short* list,
+                                               u32* run, u32& mine_out, u32& start_out) {
+    constexpr int B = KL == 64 ? 6 : KL == 32 ? 5 : KL == 16 ? 4 : KL == 8 ? 3 : KL == 4 ? 2 : 1;
+    const int lane = threadIdx.x;
+    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    u32 mine = 0;
+    for (int g = 0; g < n; g += 64) {
+        const int j = g + lane;
+        u32 o = 0;
+        if (j < n) {
+            const u32 k = slot[c0 + j];
+            o = (k >> logP) & (KL - 1);
+            ch_rank[j] = rank_list[c0 + j];
+            ch_slot[j] = k;
+        }
+        u64 mask = __ballot(j < n);
+#pragma unroll
+        for (int bt = 0; bt < B; bt++) {
+            const u64 b = __ballot((o >> bt) & 1);
+            mask &= ((lane >> bt) & 1) ? b : ~b;
+        }
+        if (lane < KL) mine += (u32)__popcll(mask);
+    }
+    u32 incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const u32 y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const u32 start = incl - mine;
+    run[lane] = start;
+    __syncthreads();
+    for (int g = 0; g < n; g += 64) {
+        const int j = g + lane;
+        const bool ok = j < n;
+        const u32 o = ok ? ((ch_slot[j] >> logP) & (KL - 1)) : 0;
+        u64 peers = __ballot(ok);
+#pragma unroll
+        for (int bt = 0; bt < B; bt++) {
+            const bool bit = (o >> bt) & 1;
+            const u64 b = __ballot(bit);
+            peers &= bit ? b : ~b;
+        }
+        const u32 lr = (u32)__popcll(peers & lt_mask);
+        u32 base = 0;
+        if (ok) base = run[o];
+        __syncthreads();
+        if (ok) list[base + lr] = (unsigned short)j;
+        if (ok && lr == 0) run[o] = base + (u32)__popcll(peers);
+        __syncthreads();
+    }
+    mine_out = mine;
+    start_out = start;
+}
+
+// ---- k_sl_own_d: the same replay specialised for the common shape — every aggregator is count or
+// reads one DOUBLE column with sum / avg / min / max (each at most once). Sum and avg perform the
+// identical += / -= sequence (with the same canDestroy reset), so they share one running sum; the
+// min and max deques use plain double comparisons and Double.equals. Far fewer instructions per
+// event than the generic kernel, whose run-time aggregator dispatch dominated its chain latency.
+struct DFields {
+    int sum, avg, mn, mx;  // field index of each (-1: absent)
+};
+
+struct DDeque {
+    i64 h, len;
+    u64 f, b, mm;
+    bool mmh, spill;
+    bool nan;  // a NaN may be in the deque (Java comparisons with NaN are false: order no longer holds)
+};
+
+__device__ __forceinline__ bool d_eq(u64 a, u64 b) {
+    const double x = __longlong_as_double((i64)a), y = __longlong_as_double((i64)b);
+    return a == b || (x != x && y != y);
+}
+
+template <bool MIN>
+__device__ __forceinline__ bool d_worse(u64 cur, u64 x) {
+    const double c = __longlong_as_double((i64)cur), v = __longlong_as_double((i64)x);
+    return MIN ? (c > v) : (c < v);
+}
+
+__device__ __forceinline__ bool d_isnan(u64 a) {
+    const double x = __longlong_as_double((i64)a);
+    return x != x;
+}
+
+// The deque of the lane's key lives in its LDS ring `l` (kDqL entries) unless it outgrew that
+// (`spill`): then in its global ring `g`. The two paths are separate so each uses plain LDS or
+// global instructions (a pointer select would compile to FLAT accesses that wait on both counters).
+__device__ __forceinline__ void dd_load(DDeque& q, const SlState& S, int field, u32 k, u64* l) {
+    const size_t fi = (size_t)field * S.nslots + k;
+    q.mm = S.mm[fi];
+    q.mmh = S.mm_has[fi];
+    q.h = S.dq_head[fi];
+    q.len = S.dq_len[fi];
+    q.spill = q.len >= kDqL;
+    q.nan = q.spill;
+    const u64* g = S.dq + fi * S.rc;
+    const i64 gm = S.rc - 1;
+    if (!q.spill) {
+        for (i64 i = 0; i < q.len; i++) {
+            const u64 v = g[(q.h + i) & gm];
+            l[(q.h + i) & (kDqL - 1)] = v;
+            q.nan |= d_isnan(v);
+        }
+    }
+    if (q.len > 0) {
+        q.f = g[q.h & gm];
+        q.b = g[(q.h + q.len - 1) & gm];
+    }
+}
+
+__device__ __forceinline__ void dd_store(const DDeque& q, const SlState& S, int field, u32 k, const u64* l) {
+    const size_t fi = (size_t)field * S.nslots + k;
+    S.mm[fi] = q.mm;
+    S.mm_has[fi] = q.mmh;
+    S.dq_head[fi] = q.h;
+    S.dq_len[fi] = q.len;
+    u64* g = S.dq + fi * S.rc;
+    const i64 gm = S.rc - 1;
+    if (!q.spill)
+        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[(q.h + i) & (kDqL - 1)];
+}
+
+// removeFirstOccurrence(x) then minValue = peekFirst() (Min/MaxAttributeAggregatorExecutor).
+// The front is the common case. Otherwise, while no NaN is in the deque it is monotone (min:
+// non-decreasing, max: non-increasing), so an x beyond the back cannot be in it and needs no scan.
+template <bool MIN, bool GLOBAL>
+__device__ __forceinline__ void dd_remove_t(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
+    auto at = [&](i64 i) -> u64 { return GLOBAL ? g[i & gm] : l[i & (kDqL - 1)]; };
+    if (q.len > 0 && d_eq(q.f, x)) {
+        q.h++;
+        q.len--;
+        if (q.len > 0) q.f = at(q.h);
+    } else if (q.len > 1 && (q.nan || !d_worse<MIN>(x, q.b))) {
+        i64 found = -1;
+        for (i64 i = 1; i < q.len; i++)
+            if (d_eq(at(q.h + i), x)) { found = i; break; }
+        if (found >= 0) {
+            for (i64 i = found; i + 1 < q.len; i++) {
+                const u64 v = at(q.h + i + 1);
+                if (GLOBAL) g[(q.h + i) & gm] = v;
+                else l[(q.h + i) & (kDqL - 1)] = v;
+            }
+            q.len--;
+            q.b = at(q.h + q.len - 1);
+        }
+    }
+    if (q.len > 0) { q.mm = q.f; q.mmh = true; }
+    else { q.mmh = false; q.nan = q.spill; }
+}
+
+template <bool MIN>
+__device__ __forceinline__ void dd_remove(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
+    if (q.spill) dd_remove_t<MIN, true>(q, g, gm, l, x);
+    else dd_remove_t<MIN, false>(q, g, gm, l, x);
+}
+
+template <bool MIN, bool GLOBAL>
+__device__ __forceinline__ void dd_add_t(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
+    while (q.len > 0 && d_worse<MIN>(q.b, x)) {
+        q.len--;
+        if (q.len > 0) q.b = GLOBAL ? g[(q.h + q.len - 1) & gm] : l[(q.h + q.len - 1) & (kDqL - 1)];
+    }
+}
+
+template <bool MIN>
+__device__ __forceinline__ void dd_add(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
+    if (q.spill) dd_add_t<MIN, true>(q, g, gm, l, x);
+    else dd_add_t<MIN, false>(q, g, gm, l, x);
+    if (!q.spill && q.len == kDqL) {  // the LDS ring is full: move to the global ring
+        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[(q.h + i) & (kDqL - 1)];
+        q.spill = true;
+        q.nan = true;  // the global path always scans
+    }
+    if (q.spill) g[(q.h + q.len) & gm] = x;
+    else l[(q.h + q.len) & (kDqL - 1)] = x;
+    q.len++;
+    q.b = x;
+    q.nan |= d_isnan(x);
+    if (q.len == 1) q.f = x;
+    if (!q.mmh || d_worse<MIN>(q.mm, x)) { q.mm = x; q.mmh = true; }
+}
+
+template <bool HSUM, bool HMIN, bool HMAX>
+__global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_list, const i64* __restrict__ part_off,
+                                                int logP, SlRecords rec, SlState S, AggPlan ap, DFields fd, i64 T,
+                                                i64 send_size, i64 send_base, SlRows rows, unsigned char* flags) {
+    // KL key lanes per wave (one key each when the partition has <= KL local keys): few lanes keep
+    // the divergence of the per-key chains low, and the small LDS footprint (≈ 20 KB) lets many
+    // waves share a CU, which is what hides each chain's instruction latency
+    constexpr int KL = kSlKeyLanes;
+    constexpr int CH = 512;
+    __shared__ u32 ch_rank[CH];
+    __shared__ u32 ch_slot[CH];
+    __shared__ unsigned short list[CH];
+    __shared__ i64 ch_clk[CH];
+    __shared__ i64 ch_pm[CH];
+    __shared__ i64 ch_ts[CH];
+    __shared__ u32 ch_raw[CH];
+    __shared__ u64 ch_v[CH];
+    __shared__ u32 run[64];
+    __shared__ i64 hb_pm[KL * kHb];
+    __shared__ u64 hb_v[KL * kHb];
+    __shared__ u64 dq_min[KL * kDqL];
+    __shared__ u64 dq_max[KL * kDqL];
+    const int lane = threadIdx.x;
+    const int kl = lane & (KL - 1);
+    u64* lmin = dq_min + kl * kDqL;
+    u64* lmax = dq_max + kl * kDqL;
+    const i64 lo = part_off[blockIdx.x], hi = part_off[blockIdx.x + 1];
+    const i64 gm = S.rc - 1;
+    // lane state
+    u32 K = kNoPos;
+    i64 cnt = 0, rh = 0, rlen = 0, cur_send = 0, cur_first = 0, hb_base = 0;
+    int hb_n = 0;
+    u64 sum = 0;
+    DDeque qn{}, qx{};
+    u64* gmin = nullptr;
+    u64* gmax = nullptr;
+    auto store_key = [&]() {
+        S.cnt[K] = cnt;
+        S.rhead[K] = rh;
+        S.rlen[K] = rlen;
+        S.cur_send[K] = cur_send;
+        S.cur_first[K] = cur_first;
+        if (HSUM) {
+            if (fd.sum >= 0) S.f[(size_t)fd.sum * S.nslots + K] = sum;
+            if (fd.avg >= 0) S.f[(size_t)fd.avg * S.nslots + K] = sum;
+        }
+        if (HMIN) dd_store(qn, S, fd.mn, K, lmin);
+        if (HMAX) dd_store(qx, S, fd.mx, K, lmax);
+    };
+    for (i64 c0 = lo; c0 < hi; c0 += CH) {
+        const int n = (int)min<i64>(CH, hi - c0);
+        // the chunk's fields, coalesced (the records are in partition order), into LDS
+#pragma unroll 4
+        for (int g = 0; g < CH; g += 64) {
+            const int j = g + lane;
+            if (j < n) {
+                ch_clk[j] = rec.clock[c0 + j];
+                ch_pm[j] = rec.pm[c0 + j];
+                ch_ts[j] = rec.ts[c0 + j];
+                ch_raw[j] = rec.raw[c0 + j];
+                ch_v[j] = rec.vals[c0 + j];
+            }
+        }
+        u32 mine, start;
+        sl_chunk_split<KL>(rank_list, rec.slot, c0, n, logP, ch_rank, ch_slot, list, run, mine, start);
+        for (u32 i = 0; i < mine; i++) {
+            const int j = list[start + i];
+            const u32 r = ch_rank[j], k = ch_slot[j];
+            const i64 clk = ch_clk[j], pmr = ch_pm[j], tsr = ch_ts[j];
+            const u32 raw = ch_raw[j];
+            const u64 x = ch_v[j];
+            if (k != K) {
+                if (K != kNoPos) store_key();
+                K = k;
+                cnt = S.cnt[k];
+                rh = S.rhead[k];
+                rlen = S.rlen[k];
+                cur_send = S.cur_send[k];
+                cur_first = S.cur_first[k];
+                hb_n = 0;
+                if (HSUM) sum = S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k];
+                if (HMIN) { dd_load(qn, S, fd.mn, k, lmin); gmin = S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc; }
+                if (HMAX) { dd_load(qx, S, fd.mx, k, lmax); gmax = S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc; }
+            }
+            // lazy expiry: ring head events with PM + T <= clock (TimeWindowProcessor.java:132-169)
+            while (rlen > 0) {
+                if (!(rh >= hb_base && rh < hb_base + hb_n)) {  // refill the head cache
+                    const int m = (int)min<i64>(kHb, rlen);
+                    i64 pm8[kHb];
+                    u64 v8[kHb];
+#pragma unroll
+                    for (int e = 0; e < kHb; e++) {
+                        if (e < m) {
+                            const i64 sl = (rh + e) & gm;
+                            pm8[e] = S.rpm[(size_t)k * S.rc + sl];
+                            v8[e] = S.rval[(size_t)k * S.rc + sl];
+                        }
+                    }
+#pragma unroll
+                    for (int e = 0; e < kHb; e++)
+                        if (e < m) { hb_pm[kl * kHb + e] = pm8[e]; hb_v[kl * kHb + e] = v8[e]; }
+                    hb_base = rh;
+                    hb_n = m;
+                }
+                const int e = (int)(rh - hb_base);
+                if (hb_pm[kl * kHb + e] + T > clk) break;
+                const u64 y = hb_v[kl * kHb + e];
+                cnt--;
+                if (HSUM) {
+                    double rr = __longlong_as_double((i64)sum) - __longlong_as_double((i64)y);
+                    if (cnt == 0 && rr == 0.0) rr = 0.0;  // destroyed state restarts from +0.0
+                    sum = (u64)__double_as_longlong(rr);
+                }
+                if (HMIN) dd_remove<true>(qn, gmin, gm, lmin, y);
+                if (HMAX) dd_remove<false>(qx, gmax, gm, lmax, y);
+                rh++;
+                rlen--;
+            }
+            // the event joins the ring and the aggregators
+            const i64 sl = (rh + rlen) & gm;
+            S.rpm[(size_t)k * S.rc + sl] = pmr;
+            S.rval[(size_t)k * S.rc + sl] = x;
+            rlen++;
+            cnt++;
+            if (HSUM) sum = (u64)__double_as_longlong(__longlong_as_double((i64)sum) + __longlong_as_double((i64)x));
+            if (HMIN) dd_add<true>(qn, gmin, gm, lmin, x);
+            if (HMAX) dd_add<false>(qx, gmax, gm, lmax, x);
+            // output row of (send, key): first occurrence position, last event's values
+            const i64 send = send_base + (send_size > 0 ? (i64)raw / send_size : 0);
+            i64 first;
+            if (cur_send != send) { cur_send = send; cur_first = r; first = r; flags[r] = 1; }
+            else first = cur_first;
+            rows.ts[first] = tsr;
+            rows.slot[first] = k;
+            rows.send[first] = send;
+            rows.clock[first] = clk;
+            for (int a = 0; a < ap.n; a++) {
+                const int kind = ap.kind[a];
+                u64 o = 0;
+                unsigned char nl = 0;
+                if (kind == AK_COUNT) o = (u64)cnt;
+                else if (kind == AK_SUM_D) o = sum;
+                else if (kind == AK_AVG) o = (u64)__double_as_longlong(__longlong_as_double((i64)sum) / (double)cnt);
+                else if (kind == AK_MIN_D) { o = qn.mm; nl = qn.mmh ? 0 : 1; }
+                else { o = qx.mm; nl = qx.mmh ? 0 : 1; }
+                rows.vals[(size_t)a * rows.cap + first] = o;
+                rows.nulls[(size_t)a * rows.cap + first] = nl;
+            }
+        }
+        __syncthreads();
+    }
+    if (K != kNoPos) store_key();
+}
+
+template <int NA, int NV>
+__global__ __launch_bounds__(64) void k_sl_own(const u32* __restrict__ rank_list, const i64* __restrict__ part_off,
+                                              int logP, SlRecords rec, SlState S, AggPlan ap, i64 T, i64 send_size,
+                                              i64 send_base, SlRows rows, unsigned char* flags) {
+    __shared__ u32 ch_rank[kSlCh];
+    __shared__ u32 ch_slot[kSlCh];
+    __shared__ unsigned short list[kSlCh];
+    __shared__ u32 run[64];
+    __shared__ i64 hb_pm[64 * kHb];
+    __shared__ u64 hb_v[NV * 64 * kHb];
+    extern __shared__ __attribute__((aligned(16))) u64 lds_dq[];  // [min/max aggregator][lane][kDqL]
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
+    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const i64 lo = part_off[p], hi = part_off[p + 1];
+    int mmi[NA];
+    {
+        int c = 0;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            mmi[a] = c;
+            if (a < ap.n && is_mm(ap.kind[a])) c++;
+        }
+    }
+    LaneKey<NA, NV> L;
+    L.k = kNoPos;
+    L.hvalid = false;
+    L.hb_n = 0;
+    L.hb_base = 0;
+    for (i64 c0 = lo; c0 < hi; c0 += kSlCh) {
+        const int n = (int)min<i64>(kSlCh, hi - c0);
+        // per-lane counts of the chunk
+        u32 mine = 0;
+        for (int g = 0; g < n; g += 64) {
+            const int j = g + lane;
+            u32 o = 64;
+            if (j < n) {
+                const u32 r = rank_list[c0 + j];
+                const u32 k = rec.slot[c0 + j];
+                o = (k >> logP) & 63;
+                ch_rank[j] = r;
+                ch_slot[j] = k;
+            }
+            // how many of this group's records go to my lane
+            u64 mask = __ballot(j < n);
+#pragma unroll
+            for (int bt = 0; bt < 6; bt++) {
+                const u64 b = __ballot((o >> bt) & 1);
+                mask &= ((lane >> bt) & 1) ? b : ~b;
+            }
+            mine += (u32)__popcll(mask);
+        }
+        // exclusive scan of the lane counts -> list starts
+        u32 incl = mine;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const u32 start = incl - mine;
+        run[lane] = start;
+        __syncthreads();
+        // stable placement: rank among the group's same-owner records + that owner's running count
+        for (int g = 0; g < n; g += 64) {
+            const int j = g + lane;
+            const bool ok = j < n;
+            const u32 o = ok ? ((ch_slot[j] >> logP) & 63) : 0;
+            u64 peers = __ballot(ok);
+#pragma unroll
+            for (int bt = 0; bt < 6; bt++) {
+                const bool bit = (o >> bt) & 1;
+                const u64 b = __ballot(bit);
+                peers &= bit ? b : ~b;
+            }
+            const u32 lr = (u32)__popcll(peers & lt_mask);
+            u32 base = 0;
+            if (ok) base = run[o];
+            __syncthreads();
+            if (ok) list[base + lr] = (unsigned short)j;
+            if (ok && lr == 0) run[o] = base + (u32)__popcll(peers);
+            __syncthreads();
+        }
+        // replay: my key's events in order, the next record's fields loaded one step ahead
+        SlRec<NV> nx;
+        if (mine > 0) sl_rec_load(nx, rec, ap, c0 + list[start]);
+        for (u32 i = 0; i < mine; i++) {
+            const int j = list[start + i];
+            const u32 r = ch_rank[j], k = ch_slot[j];
+            const SlRec<NV> cur = nx;
+            if (i + 1 < mine) sl_rec_load(nx, rec, ap, c0 + list[start + i + 1]);
+            if (k != L.k) {
+                if (L.k != kNoPos) lk_store(L, S, ap, lds_dq, mmi);
+                lk_load(L, S, ap, lds_dq, mmi, k);
+            }
+            const i64 clk = cur.clk;
+            // lazy expiry: ring head events with PM + T <= clock (TimeWindowProcessor.java:132-169)
+            while (L.rlen > 0) {
+                if (!L.hvalid) lk_head(L, S, ap, hb_pm, hb_v);
+                if (L.hpm + T > clk) break;
+                lk_remove(L, S, ap, lds_dq, mmi, L.hval);
+                L.rh++;
+                L.rlen--;
+                L.hvalid = false;
+                if (L.rlen > 0) lk_head(L, S, ap, hb_pm, hb_v);
+            }
+            // the event joins the ring and the aggregators
+            const i64 sl = (L.rh + L.rlen) & (S.rc - 1);
+            S.rpm[(size_t)k * S.rc + sl] = cur.pm;
+#pragma unroll
+            for (int q = 0; q < NV; q++) {
+                if (q >= ap.n_vcols) break;
+                S.rval[((size_t)q * S.nslots + k) * S.rc + sl] = cur.v[q];
+            }
+            if (L.rlen == 0) {
+                L.hpm = cur.pm;
+#pragma unroll
+                for (int q = 0; q < NV; q++) {
+                    if (q >= ap.n_vcols) break;
+                    L.hval[q] = cur.v[q];
+                }
+                L.hvalid = true;
+            }
+            L.rlen++;
+            lk_add(L, S, ap, lds_dq, mmi, cur.v);
+            // output row of (send, key): first occurrence position, last event's values
+            const i64 send = send_base + (send_size > 0 ? (i64)cur.raw / send_size : 0);
+            i64 first;
+            if (L.cur_send != send) { L.cur_send = send; L.cur_first = r; first = r; flags[r] = 1; }
+            else first = L.cur_first;
+            rows.ts[first] = cur.ts;
+            rows.slot[first] = k;
+            rows.send[first] = send;
+            rows.clock[first] = clk;
+            const i64 c = L.cnt;
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                if (a >= ap.n) break;
+                const int kind = ap.kind[a];
+                u64 o;
+                unsigned char nl = 0;
+                if (kind == AK_COUNT) o = (u64)c;
+                else if (kind == AK_SUM_L || kind == AK_SUM_D) o = L.f[a];
+                else if (kind == AK_AVG) o = (u64)__double_as_longlong(__longlong_as_double((i64)L.f[a]) / (double)c);
+                else { o = L.mm[a]; nl = L.mmh[a] ? 0 : 1; }
+                rows.vals[(size_t)a * rows.cap + first] = o;
+                rows.nulls[(size_t)a * rows.cap + first] = nl;
+            }
+        }
+        __syncthreads();
+    }
+    if (L.k != kNoPos) lk_store(L, S, ap, lds_dq, mmi);
+}
+
+// rank-indexed records -> partition order (position q of the multisplit's rank list), so the
+// per-key replay reads each partition's records from one contiguous range
+__global__ __launch_bounds__(kBlock) void k_sl_gather(const u32* __restrict__ ranks, i64 M, SlRecords rec, SlRecords out,
+                                                     int nv) {
+    const i64 q = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= M) return;
+    const u32 r = ranks[q];
+    out.raw[q] = rec.raw[r];
+    out.slot[q] = rec.slot[r];
+    out.clock[q] = rec.clock[r];
+    out.pm[q] = rec.pm[r];
+    out.ts[q] = rec.ts[r];
+    for (int j = 0; j < nv; j++) out.vals[(size_t)j * out.cap + q] = rec.vals[(size_t)j * rec.cap + r];
+}
+
+void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_sl_gather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ranks, M, rec, out,
+                       nv);
+}
+
+void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
+                        SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,
+                        unsigned char* flags) {
+    // the double-column shape (C3): count + at most one each of sum / avg / min / max of one DOUBLE
+    {
+        DFields fd{-1, -1, -1, -1};
+        bool ok = ap.n_vcols == 1 && ap.vcol_type[0] == SH_T_DOUBLE;
+        for (int a = 0; ok && a < ap.n; a++) {
+            int* slotp = nullptr;
+            switch (ap.kind[a]) {
+                case AK_COUNT: continue;
+                case AK_SUM_D: slotp = &fd.sum; break;
+                case AK_AVG: slotp = &fd.avg; break;
+                case AK_MIN_D: slotp = &fd.mn; break;
+                case AK_MAX_D: slotp = &fd.mx; break;
+                default: ok = false; continue;
+            }
+            if (*slotp >= 0) ok = false;
+            else *slotp = ap.field[a];
+        }
+        if (ok) {
+            const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
+#define SH_SL_D(A, B, C)                                                                                      \
+    hipLaunchKernelGGL((k_sl_own_d<A, B, C>), dim3(P), dim3(64), 0, s, rank_list, part_off, logP, rec, S, ap, fd, T, \
+                       send_size, send_base, rows, flags)
+            if (hs && hn && hx) SH_SL_D(true, true, true);
+            else if (hs && !hn && !hx) SH_SL_D(true, false, false);
+            else if (!hs && hn && hx) SH_SL_D(false, true, true);
+            else if (hs && hn) SH_SL_D(true, true, false);
+            else if (hs && hx) SH_SL_D(true, false, true);
+            else if (hn && !hx) SH_SL_D(false, true, false);
+            else if (hx && !hn) SH_SL_D(false, false, true);
+            else SH_SL_D(false, false, false);
+#undef SH_SL_D
+            return;
+        }
+    }
+    int n_mm = 0;
+    for (int a = 0; a < ap.n; a++) n_mm += ap.kind[a] >= AK_MIN_L;
+    const size_t lds = (size_t)std::max(1, n_mm) * 64 * kDqL * 8;
+#define SH_SL_OWN(A, V)                                                                                        \
+    hipLaunchKernelGGL((k_sl_own<A, V>), dim3(P), dim3(64), lds, s, rank_list, part_off, logP, rec, S, ap, T, \
+                       send_size, send_base, rows, flags)
+    const int nv = std::max(1, ap.n_vcols);
+    if (ap.n <= 2 && nv <= 1) SH_SL_OWN(2, 1);
+    else if (ap.n <= 4 && nv <= 1) SH_SL_OWN(4, 1);
+    else if (ap.n <= 4 && nv <= 2) SH_SL_OWN(4, 2);
+    else if (nv <= 2) SH_SL_OWN(8, 2);
+    else SH_SL_OWN(8, 8);
+#undef SH_SL_OWN
+}
+
 void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, int P, SlRecords rec, SlState S,
                     AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags) {
     hipLaunchKernelGGL(k_sliding, dim3(P), dim3(64), 0, s, rank_list, part_off, P, rec, S, ap, T, send_size,

@@ -215,3 +215,21 @@ def test_sliding_no_group_by(rt):
     ts, cols = synth.keyed_stream(0, 30_000, 0xC3, 100, 5)
     spec = abi.QuerySpec(C2_SCHEMA, "time", 700, aggs=[("sum", "v"), ("max", "v"), ("count", None)])
     both(rt, spec, split_batches(C2_SCHEMA, ts, cols, [10_000], 3), label="slide-nogroup")
+
+
+def test_sliding_monotone_values_long_deques(rt):
+    """Per-key rising then falling values: the min (then max) deque grows to the whole window, past the
+    LDS deque capacity of k_sl_own, so those keys run on the spilled global deques; NaN/-0.0 mixed in
+    break the deque's order (Java comparisons with NaN are false) and Double.equals."""
+    rng = np.random.default_rng(17)
+    n = 50_000
+    ts = (np.arange(n, dtype=np.int64) // 5) + 1_000
+    k = rng.integers(0, 20, n).astype(np.int32)
+    v = np.where(np.arange(n) < n // 2, np.arange(n, dtype=np.float64), (n - np.arange(n)).astype(np.float64))
+    v[rng.integers(0, n, 40)] = np.nan
+    v[rng.integers(0, n, 40)] = -0.0
+    v[rng.integers(0, n, 40)] = 0.0
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "time", 400, group_by=["k"],
+                         aggs=[("min", "v"), ("max", "v"), ("count", None), ("sum", "v")], key_capacity=32)
+    both(rt, spec, split_batches(schema, ts, [k, v, ts.copy()], [20_000, 20_001], 1), label="monotone")
