@@ -113,9 +113,9 @@ SECONDARY = {
 
 
 def run_secondary(args, dev, rank=0, world=1, dist=None):
-    """Inputs resident in HBM, `--steps` pushes of `--batch` events (per GPU) of the workload. One
-    GPU, except C4: at N > 1 one global stream (N x the per-GPU key count and event rate) is sliced
-    across the ranks and key-sharded (ShardedAggregation over RCCL all-to-all)."""
+    """Inputs resident in HBM, `--steps` pushes of `--batch` events (per GPU) of the workload. C1, C4
+    and C5 also run at N > 1: one global stream (C4, C5: N x the per-GPU key count and event rate) is
+    sliced across the ranks and key-sharded (ShardedQuery / ShardedAggregation over RCCL all-to-all)."""
     import numpy as np
     import torch
     from siddhi_amd import abi, runtime, synth
@@ -130,7 +130,9 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         spec = abi.QuerySpec(schema, "lengthBatch", 10000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
                              filter=(">", "price", 100), key_capacity=1000)
         send = 1000
-        gen = lambda i: [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in synth.c1_stock(i * B, B)[1]]
+        # N > 1: one global stream, rank r holds slice r of every global push
+        gen = lambda i: [torch.from_numpy(np.ascontiguousarray(c)).to(dev)
+                         for c in synth.c1_stock((i * world + rank) * B, B)[1]]
         mk = lambda cols: (cols[3], cols)
     elif args.workload == "c4":
         schema = abi.Schema.parse("k string, v double, ts long")
@@ -162,8 +164,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         send = 1
         mk = lambda cols: (cols[2], cols)
     if sliced:
-        if args.workload not in ("c4", "c5"):
-            raise SystemExit("of the secondary workloads only c4 and c5 run on N > 1 GPUs")
+        if args.workload not in ("c1", "c4", "c5"):
+            raise SystemExit("of the secondary workloads only c1, c4 and c5 run on N > 1 GPUs")
         from siddhi_amd.shard import ShardedAggregation, ShardedQuery, TorchExchange, distributed_push
         q = ShardedAggregation(agg, rank, world, ctx) if agg else ShardedQuery(spec, rank, world, ctx)
         ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
@@ -219,7 +221,7 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     if sliced:
         config.update(parallelism=f"slice ingest x{world}, key re-shard over "
                                   f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all",
-                      keys_total=125_000 * world if agg else 10_000_000,
+                      keys_total=125_000 * world if agg else 1000 if args.workload == "c1" else 10_000_000,
                       phases_ms_per_step_rank0={k: v / args.steps for k, v in phases.items()})
     print(json.dumps({"metric": METRIC, "value": B * args.steps * world / elapsed, "unit": "events/s",
                       "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

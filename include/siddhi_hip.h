@@ -257,8 +257,12 @@ int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out
  *                                                   flush by `order` yields the single-stream row
  *                                                   order of QuerySelector.processInBatchGroupBy.
  * Supported: timeBatch group-by, partitioned or not (`partition with (p of S)`: R12 — every rank
- * restricts the stream to the partition of the globally first passing event), and incremental
- * aggregations through sh_aggregation_shard_create (below).                                  */
+ * restricts the stream to the partition of the globally first passing event), lengthBatch
+ * group-by (batch = global filtered index / L, LengthBatchWindowProcessor.java:206-243: the
+ * summaries' pass counts give every slice its offset; a batch's sh_bound carries the clock of the
+ * send of its L-th event, where it is flushed), and incremental aggregations through
+ * sh_aggregation_shard_create (below). Several lengthBatch batches can close in one send (same
+ * flush clock): merge owner flushes by (clock, window of their rows' `order`).               */
 typedef struct {
     int64_t n;           /* events in the slice                                              */
     int64_t n_pass;      /* events passing the filter                                        */
@@ -271,7 +275,8 @@ typedef struct {
 
 typedef struct {
     int64_t W;     /* window number that starts here                                         */
-    int64_t clock; /* playback clock of the send that opened it (the flush clock of W-1...)  */
+    int64_t clock; /* flush clock of window W-1: timeBatch, the clock of the send that opened
+                      W; lengthBatch, the clock of the send holding W-1's L-th event          */
     int64_t gidx;  /* global stream index of the first event of window W                    */
     int64_t pad;
 } sh_bound;

@@ -54,6 +54,7 @@ struct sh_shard {
     bool e0_valid = false;
     int64_t E0 = 0;
     int64_t W = 0;        // window of the last event of the stream so far
+    int64_t carry = 0;    // lengthBatch: passing events in the open batch (count, :206-243)
     uint64_t seq = 0;     // events of the stream so far (global index of the next event)
     // the push in flight (pack -> consume)
     bool packed = false;
@@ -81,8 +82,10 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_create: NULL argument");
     if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
         return sh_fail(SH_ERR_INVALID, "sh_shard_create: need 0 <= rank < world <= 16");
-    if (d->window != SH_WIN_TIME_BATCH)
-        return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch group-by queries");
+    if (d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_LENGTH_BATCH)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch / lengthBatch group-by queries");
+    if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
+        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     sh_shard* s = new sh_shard();
     s->ctx = ctx;
@@ -283,8 +286,13 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
             break;
         }
     }
+    const bool lb = s->d.window == SH_WIN_LENGTH_BATCH;
+    // passing events of the slices before each slice (lengthBatch: the global batch index)
+    std::vector<int64_t> poff(G);
+    int64_t total_pass = 0;
+    for (int r = 0; r < G; r++) { poff[r] = total_pass; total_pass += all[r].n_pass; }
     // nextEmitTime: initialised by the first send that reaches the window (TimeBatch :266-276, 342-347)
-    if (!s->e0_valid) {
+    if (!lb && !s->e0_valid) {
         for (int r = 0; r < G; r++) {
             if (all[r].n_pass == 0) continue;
             int64_t ck = std::max(cin[r], all[r].first_clock);
@@ -295,7 +303,10 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         }
     }
     const int64_t W_start = s->W;
-    const int64_t W_end = std::max(W_start, wfun_g(s, clock_end));
+    // lengthBatch: a batch is complete (and flushed in the send of its L-th event) once L passing
+    // events reached it, so every window below (carry + passes) / L closes in this push
+    const int64_t W_end = lb ? W_start + (s->carry + total_pass) / s->d.window_param
+                             : std::max(W_start, wfun_g(s, clock_end));
     if (W_end - W_start >= (1 << 23)) return sh_fail(SH_ERR_UNSUPPORTED, "more than 8M windows in one push");
     s->cur_W_base = W_start;
     s->cur_W_end = W_end;
@@ -316,7 +327,9 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         RCHK(s->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
         HIPCHK(hipMemsetAsync(s->info.p, 0, sizeof(PushInfo), st));
         WinParams wp{};
-        wp.kind = SH_WIN_TIME_BATCH;
+        wp.kind = lb ? SH_WIN_LENGTH_BATCH : SH_WIN_TIME_BATCH;
+        wp.L = s->d.window_param;
+        wp.n_pend = s->carry + poff[s->rank];
         wp.e0_valid = s->e0_valid;
         wp.E0 = s->E0;
         wp.T = s->d.window_param;
@@ -328,7 +341,8 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         wp.N = N;
         wp.send_size = b->send_size;
         PushInfo* info = s->info.as<PushInfo>();
-        launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), info, s->wkp, G, nblk,
+        launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), s->blk_pass.as<int64_t>(),
+                            info, s->wkp, G, nblk,
                             s->code.as<u32>(), s->counts.as<int64_t>(), s->bounds.as<Bound>(), max_bounds,
                             &info->n_bounds);
         HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
@@ -360,6 +374,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         s->clock_valid = true;
     }
     s->W = W_end;
+    if (lb) s->carry = (s->carry + total_pass) % s->d.window_param;
     s->seq += (uint64_t)n_total;
     s->packed = true;
     s->slice_n = -1;
@@ -478,7 +493,7 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
     if (!(s->clock_valid && now < s->clock)) {
         s->clock = now;
         s->clock_valid = true;
-        s->W = std::max(s->W, wfun_g(s, now));
+        if (s->d.window == SH_WIN_TIME_BATCH) s->W = std::max(s->W, wfun_g(s, now));
     }
     set_order(s, host_out != 0, order);
     return SH_OK;

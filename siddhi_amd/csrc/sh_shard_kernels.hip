@@ -22,8 +22,13 @@ __device__ __forceinline__ u32 owner_of(const KeyPlan& kp, u64 key, int G) {
 // code of a passing event: (W - W_base) << 4 | owner; kNoPos when it is filtered out
 constexpr int kOwnerBits = 4;
 
+// lengthBatch (LengthBatchWindowProcessor :206-243): the window of a passing event is
+// (carry + global passing events before it) / L — wp.n_pend holds the carry plus the passing events
+// of the slices before this one, blk_pass_pre the slice's tile prefix. A window start is recorded at
+// the event after every L-th passing event, with the clock of the L-th event's send (the flush clock).
 __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__ ts, ColSet cols, FilterProg f,
-                                                        WinParams wp, const i64* __restrict__ blk_tl_pre, KeyPlan kp,
+                                                        WinParams wp, const i64* __restrict__ blk_tl_pre,
+                                                        const i64* __restrict__ blk_pass_pre, KeyPlan kp,
                                                         int G, int nblk, u32* code, i64* counts, Bound* bounds,
                                                         int max_bounds, int* n_bounds) {
     __shared__ u32 hist[kMaxShards];
@@ -44,9 +49,43 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
     }
     i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
     const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
+    const bool lb = wp.kind == SH_WIN_LENGTH_BATCH;
+    if (lb) {
+        i64 cnt = 0;
+#pragma unroll
+        for (int i = 0; i < kItems; i++) cnt += pass[i];
+        i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x] + wp.n_pend;
+        SendCursor sc2(wp, base);
+#pragma unroll
+        for (int i = 0; i < kItems; i++) {
+            i64 e = base + i;
+            if (e >= wp.N) break;
+            u32 c = kNoPos;
+            if (pass[i]) {
+                const i64 Wr = pcb / wp.L;
+                if ((pcb + 1) % wp.L == 0) {
+                    const i64 tsl = sc2.s == 1 ? t[i] : ts[sc2.last_of(wp, e)];
+                    int k = atomicAdd(n_bounds, 1);
+                    if (k < max_bounds) {
+                        Bound b;
+                        b.idx = e + 1; b.W = wp.W_base + Wr + 1; b.clock = max(c0, max(pm, tsl));
+                        b.clock_prev = b.clock; b.pcb = 0; b.pad = 0;
+                        bounds[k] = b;
+                    }
+                }
+                u32 o = owner_of(kp, make_key(kp, cols, e), G);
+                c = ((u32)Wr << kOwnerBits) | o;
+                atomicAdd(&hist[o], 1u);
+                pcb++;
+            }
+            code[e] = c;
+            if (sc2.last(wp, e)) pm = max(pm, t[i]);
+            sc2.next();
+        }
+    }
     const i64 E0 = wp.E0;
     const int e0v = wp.e0_valid;
-    if (base < wp.N) {
+    if (!lb && base < wp.N) {
         SendCursor sc2(wp, base);
         i64 Wprev, clock_prev;
         if (base == 0) {
@@ -93,11 +132,11 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
 }
 
 void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
-                         const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code, i64* counts, Bound* bounds,
-                         int max_bounds, int* n_bounds) {
+                         const i64* blk_pass_pre, const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code,
+                         i64* counts, Bound* bounds, int max_bounds, int* n_bounds) {
     (void)info;
-    hipLaunchKernelGGL(k_shard_assign, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_tl_pre, kp, G, nblk, code,
-                       counts, bounds, max_bounds, n_bounds);
+    hipLaunchKernelGGL(k_shard_assign, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_tl_pre, blk_pass_pre, kp,
+                       G, nblk, code, counts, bounds, max_bounds, n_bounds);
 }
 
 // Stable multisplit by owner. Tile events are taken in kItems rounds of kBlock consecutive events;

@@ -528,7 +528,12 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         // sharded owner: the global clock closed every window below given_W_end during this push,
         // including the one this owner's last events belong to (a timer flush, Scheduler.java:171-209)
         const int64_t W_last = bounds.empty() ? q->W_open : bounds.back().W;
-        const bool close_all = q->given && q->given_W_end > W_last;
+        // lengthBatch whose L-th event is the push's last event: LengthBatchWindowProcessor flushes
+        // the batch while processing that send (:206-243), not when the next event arrives
+        const int64_t open_cnt = bounds.empty() ? q->n_pend + info.total_pass : info.total_pass - bounds.back().pcb;
+        const bool lb_full = !q->given && q->d.window == SH_WIN_LENGTH_BATCH && info.total_pass > 0 &&
+                             open_cnt == q->d.window_param;
+        const bool close_all = (q->given && q->given_W_end > W_last) || lb_full;
         if (!bounds.empty() || close_all) {
             std::vector<Segment> segs;
             std::vector<int64_t> clocks, windows;
@@ -543,7 +548,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             }
             if (close_all) {
                 segs.push_back(Segment{lo, q->n_pend + N});
-                clocks.push_back(given_flush_clock(q, wprev));
+                clocks.push_back(lb_full ? q->clock : given_flush_clock(q, wprev));
                 windows.push_back(wprev);
             }
             RCHK(run_closed(q, segs, clocks, windows, b, host_out));
@@ -552,13 +557,14 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
                 pcb_lo = info.total_pass;
                 dst_base = 0;
                 new_pend = 0;
-                q->W_open = q->given_W_end;
+                q->W_open = lb_full ? 0 : q->given_W_end;
             } else {
                 e_lo = bounds.back().idx - q->n_pend;
                 pcb_lo = bounds.back().pcb;
                 dst_base = 0;
                 new_pend = info.total_pass - pcb_lo;
-                q->W_open = bounds.back().W;
+                // lengthBatch windows are numbered relative to the open batch (W = (n_pend + pcb) / L)
+                q->W_open = (!q->given && q->d.window == SH_WIN_LENGTH_BATCH) ? 0 : bounds.back().W;
             }
         } else {
             e_lo = 0;

@@ -162,19 +162,31 @@ def host_rows(out, order) -> dict:
     return d
 
 
-def merge_owner_outputs(parts: List[dict]) -> dict:
+def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None) -> dict:
     """Merge the G owners' outputs of one global push into the single-stream output: flushes are
-    matched by flush clock (every owner flushes window w at the same global clock) and rows inside a
-    flush are ordered by the global first-occurrence index."""
-    clocks = sorted(set(int(c) for p in parts for c in p["flush_clock"]))
+    matched by flush clock (every owner flushes window w at the same global clock) and, when `bounds`
+    (the push's all-gathered window starts) is given, by the window their rows' first events fall in
+    — several lengthBatch batches can complete in one send and share its clock. Rows inside a flush
+    are ordered by the global first-occurrence index."""
+    starts = np.sort(np.asarray(bounds, np.int64).reshape(-1, BOUND_WORDS)[:, 2]) if bounds is not None \
+        else np.zeros(0, np.int64)
+
+    def fkey(p, f):
+        a = int(p["flush_offsets"][f])
+        w = int(np.searchsorted(starts, int(p["order"][a]), side="right")) if starts.size else 0
+        return (int(p["flush_clock"][f]), w)
+
+    keys = sorted(set(fkey(p, f) for p in parts for f in range(len(p["flush_clock"]))
+                      if p["flush_offsets"][f + 1] > p["flush_offsets"][f]))
     fo, fc, rows = [0], [], []
-    for ck in clocks:
+    for ky in keys:
+        ck = ky[0]
         sel = []
         for p in parts:
-            idx = np.nonzero(p["flush_clock"] == ck)[0]
-            for f in idx:
+            for f in range(len(p["flush_clock"])):
                 a, b = int(p["flush_offsets"][f]), int(p["flush_offsets"][f + 1])
-                sel.append((p, a, b))
+                if b > a and fkey(p, f) == ky:
+                    sel.append((p, a, b))
         order = np.concatenate([p["order"][a:b] for p, a, b in sel])
         perm = np.argsort(order, kind="stable")
         rows.append((sel, perm))
@@ -228,6 +240,7 @@ class LocalShards:
             counts.append(sb)
             bounds.append(bd)
         all_bounds = np.concatenate(bounds) if bounds else np.zeros((0, BOUND_WORDS), np.int64)
+        self.last_bounds = all_bounds
         outs = []
         for o, s in enumerate(self.shards):
             blocks, rbytes = [], []

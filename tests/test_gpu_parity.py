@@ -233,3 +233,16 @@ def test_sliding_monotone_values_long_deques(rt):
     spec = abi.QuerySpec(schema, "time", 400, group_by=["k"],
                          aggs=[("min", "v"), ("max", "v"), ("count", None), ("sum", "v")], key_capacity=32)
     both(rt, spec, split_batches(schema, ts, [k, v, ts.copy()], [20_000, 20_001], 1), label="monotone")
+
+
+def test_lengthbatch_batch_completing_on_the_push_end_flushes_in_that_push(rt):
+    """LengthBatchWindowProcessor flushes a batch in the send of its L-th event (:206-243): a push
+    whose last event completes a batch must emit it in that push's output, not the next one's."""
+    ts, cols = synth.c1_stock(0, 40_000)
+    spec = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 1000, group_by=["symbol"], aggs=[("sum", "volume"), ("count", None)],
+                         key_capacity=1000)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    for p in split_batches(C1_SCHEMA, ts, cols, [3_000, 3_500, 10_000, 10_001, 25_000], 500):
+        assert_same(abi.out_arrays(g.push_raw(p)), abi.out_arrays(o.push_raw(p)), label="per push")
+    g.close()
+    o.close()

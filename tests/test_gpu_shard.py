@@ -40,7 +40,8 @@ def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
             a, b = edges[g], edges[g + 1]
             slices.append((torch.from_numpy(np.ascontiguousarray(ts[a:b])).to(dev),
                            [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in cols]))
-        parts.append(merge_owner_outputs(ls.push(slices, send_size, dev)))
+        outs = ls.push(slices, send_size, dev)
+        parts.append(merge_owner_outputs(outs, ls.last_bounds))
     if advance is not None:
         parts.append(merge_owner_outputs(ls.advance_time(advance)))
     ls.close()
@@ -134,3 +135,47 @@ def test_sharded_partition_with_zipf_keys(world):
     ref = run_oracle(sp, pushes, 1, advance=adv)
     assert ref["flush_offsets"].size > 5
     assert_same(got, ref, label=f"sharded partition x{world}")
+
+
+# ---- C1 over G GPUs: lengthBatch (the batch index is global: passing events of the slices before) ----
+C1_SCHEMA = abi.Schema.parse("symbol string, price double, volume long, ts long")
+
+
+def c1_pushes(n, sizes, quantized=False):
+    ts, cols = synth.c1_stock(0, n, quantized=quantized)
+    out, a = [], 0
+    for s in sizes:
+        out.append((ts[a:a + s], [c[a:a + s] for c in cols]))
+        a += s
+    return out
+
+
+@pytest.mark.parametrize("world,send_size", [(2, 1), (3, 1000), (8, 1)])
+def test_sharded_c1_lengthbatch_matches_single_stream(world, send_size):
+    """`from StockStream[price>100]#window.lengthBatch(L) select symbol, sum(volume), avg(price) group
+    by symbol`: batch b = events whose global filtered index is in [bL, (b+1)L), flushed in the send
+    of its L-th event; owners flush batch b at that send's clock."""
+    sp = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 3000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
+                       filter=(">", "price", 100), key_capacity=1000)
+    pushes = c1_pushes(200_000, [70_000, 1000, 129_000])
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.05 * (g + 1) for g in range(world - 1)]]
+    got = run_sharded(sp, world, pushes, send_size, fr)
+    ref = run_oracle(sp, pushes, send_size)
+    assert ref["flush_offsets"].size > 20
+    assert_same(got, ref, label=f"sharded C1 x{world}")
+
+
+def test_sharded_lengthbatch_batches_ending_at_push_and_slice_ends():
+    """Batches that complete on the last event of a slice or of a push, several batches in one send
+    (send_size > L), and a quiet owner: flush clocks and row order still match the single stream."""
+    sp = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 500, group_by=["symbol"],
+                       aggs=[("sum", "volume"), ("count", None), ("max", "price")], key_capacity=1000)
+    # no filter: push sizes that are multiples of L end exactly on a batch
+    pushes = c1_pushes(30_000, [5_000, 7_250, 17_750])
+    fr = [[0.5, 0.5, 0.75]]
+    got = run_sharded(sp, 4, pushes, 2_000, fr)
+    ref = run_oracle(sp, pushes, 2_000)
+    assert_same(got, ref, label="sharded lengthBatch edges")
+    got1 = run_sharded(sp, 4, pushes, 1, [[0.1, 0.2, 0.3]])
+    ref1 = run_oracle(sp, pushes, 1)
+    assert_same(got1, ref1, label="sharded lengthBatch edges per-event")

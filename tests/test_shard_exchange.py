@@ -87,3 +87,26 @@ def test_merge_owner_outputs_orders_rows_by_first_occurrence():
     assert m["flush_clock"].tolist() == [1000, 2000]
     assert m["keys"][0].tolist() == [1, 3, 2, 1]
     assert m["order"].tolist() == [0, 5, 6, 7]
+
+
+def test_merge_owner_outputs_separates_batches_of_one_send():
+    """lengthBatch: two batches completing in one send share its flush clock; the window starts
+    (bounds) keep them apart."""
+    from siddhi_amd.shard import BOUND_WORDS, merge_owner_outputs
+
+    def part(fo, fc, order, keys):
+        n = len(order)
+        return {"flush_offsets": np.array(fo, np.int64), "flush_clock": np.array(fc, np.int64),
+                "val_types": np.array([2], np.int32), "ts": np.array(order, np.int64),
+                "expired": np.zeros(n, np.uint8), "order": np.array(order, np.int64),
+                "keys": np.array([keys], np.int64), "vals": np.array([keys], np.uint64),
+                "nulls": np.zeros((1, n), np.uint8)}
+
+    # batch 0 = events [0, 4), batch 1 = [4, 8): both closed by the same send (clock 500)
+    a = part([0, 1, 2], [500, 500], [1, 5], [10, 10])
+    b = part([0, 2, 3], [500, 500], [0, 2, 4], [11, 12, 11])
+    bounds = np.array([[1, 500, 4, 0], [2, 500, 8, 0]], np.int64).reshape(-1, BOUND_WORDS)
+    m = merge_owner_outputs([a, b], bounds)
+    assert m["flush_offsets"].tolist() == [0, 3, 5]
+    assert m["order"].tolist() == [0, 1, 2, 4, 5]
+    assert m["keys"][0].tolist() == [11, 10, 12, 11, 10]
