@@ -115,7 +115,7 @@ SECONDARY = {
 def run_secondary(args, dev, rank=0, world=1, dist=None):
     """Inputs resident in HBM, `--steps` pushes of `--batch` events (per GPU) of the workload. C1, C4
     and C5 also run at N > 1: one global stream (C4, C5: N x the per-GPU key count and event rate) is
-    sliced across the ranks and key-sharded (ShardedQuery / ShardedAggregation over RCCL all-to-all)."""
+    sliced across the ranks and key-sharded; C3 likewise with N x the keys and the event rate (ShardedQuery / ShardedAggregation over RCCL all-to-all)."""
     import numpy as np
     import torch
     from siddhi_amd import abi, runtime, synth
@@ -153,9 +153,12 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     else:
         if args.workload == "c3":
             schema = abi.Schema.parse("k string, v double, ts long")
+            # N > 1: one global stream with N x the keys and N x the event rate, sliced across the ranks
             spec = abi.QuerySpec(schema, "time", 10_000, group_by=["k"],
-                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=10_000)
-            gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC3, 10_000, 1000, dev)[1]
+                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")],
+                                 key_capacity=10_000 * world)
+            gen = lambda i: synth.torch_keyed_stream((i * world + rank) * B, B, 0xC3, 10_000 * world, 1000 * world,
+                                                     dev)[1]
         else:
             schema = abi.Schema.parse("k string, v double, ts long")
             spec = abi.QuerySpec(schema, "externalTimeBatch", 1000, group_by=["k"], ts_attr="ts",
@@ -164,8 +167,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         send = 1
         mk = lambda cols: (cols[2], cols)
     if sliced:
-        if args.workload not in ("c1", "c4", "c5"):
-            raise SystemExit("of the secondary workloads only c1, c4 and c5 run on N > 1 GPUs")
+        if args.workload not in ("c1", "c3", "c4", "c5"):
+            raise SystemExit("of the secondary workloads only c1, c3, c4 and c5 run on N > 1 GPUs")
         from siddhi_amd.shard import ShardedAggregation, ShardedQuery, TorchExchange, distributed_push
         q = ShardedAggregation(agg, rank, world, ctx) if agg else ShardedQuery(spec, rank, world, ctx)
         ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
@@ -221,7 +224,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     if sliced:
         config.update(parallelism=f"slice ingest x{world}, key re-shard over "
                                   f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all",
-                      keys_total=125_000 * world if agg else 1000 if args.workload == "c1" else 10_000_000,
+                      keys_total=125_000 * world if agg else 1000 if args.workload == "c1" else
+                      10_000 * world if args.workload == "c3" else 10_000_000,
                       phases_ms_per_step_rank0={k: v / args.steps for k, v in phases.items()})
     print(json.dumps({"metric": METRIC, "value": B * args.steps * world / elapsed, "unit": "events/s",
                       "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

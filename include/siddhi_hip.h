@@ -262,7 +262,12 @@ int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out
  * summaries' pass counts give every slice its offset; a batch's sh_bound carries the clock of the
  * send of its L-th event, where it is flushed), and incremental aggregations through
  * sh_aggregation_shard_create (below). Several lengthBatch batches can close in one send (same
- * flush clock): merge owner flushes by (clock, window of their rows' `order`).               */
+ * flush clock): merge owner flushes by (clock, window of their rows' `order`). Sliding time(T)
+ * group-by (TimeWindowProcessor.java:132-169, not partitioned): the source slice gives every passing
+ * event its send's global clock and PM (max ts over the stream's passing events up to it, the expiry
+ * key) — both travel in the record — and the owner replays its keys' windows; it emits one flush per
+ * global send, so merge owner flushes by send number ((order - push's first index) / send_size) and
+ * rows by `order`. Sliding records carry 2 extra words: at most 6 stream columns.              */
 typedef struct {
     int64_t n;           /* events in the slice                                              */
     int64_t n_pass;      /* events passing the filter                                        */
@@ -270,7 +275,9 @@ typedef struct {
     int64_t first_clock; /* clock of the send of the slice's first passing event, without the
                             clock carried in (INT64_MIN: no passing event)                    */
     int64_t first_key;   /* partitioned queries: partition key of that event (R12: the globally
-                            first one picks the only partition that ever flushes); else 0     */
+                            first one picks the only partition that ever flushes); sliding
+                            time(T): max ts over the slice's passing events (INT64_MIN: none,
+                            the slice's PM contribution); else 0                              */
 } sh_slice_summary;
 
 typedef struct {

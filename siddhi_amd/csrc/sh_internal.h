@@ -191,6 +191,9 @@ constexpr int kMaxShards = 16;
 void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
                          const i64* blk_pass_pre, const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code,
                          i64* counts, Bound* bounds, int max_bounds, int* n_bounds);
+void launch_shard_sl_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
+                            const i64* blk_tl_pre, const i64* blk_pm_pre, i64 pm0, KeyPlan kp, int G, int nblk,
+                            u32* code, i64* counts, i64* clk_out, i64* pm_out);
 // Record of one re-keyed event (4-byte words): [key u32 | key u64][slice position u32 (+pad)][ts i64]
 // [values u64...]; the owner derives the global index from the source and position, and the
 // window from the global window starts.

@@ -177,6 +177,9 @@ void agg_release_sharded(sh_aggregation* a);                     // called by sh
 int sliding_create(sh_query* q);
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
 int sliding_advance(sh_query* q, int64_t now, const sh_out** out);
+int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* const* cols, const int64_t* gclk,
+                       const int64_t* gpm, const uint64_t* gidx, int64_t raw_base, int64_t send_size,
+                       int64_t send_base, bool host_out, const sh_out** out, int64_t n_global);
 void sliding_destroy(sh_query* q);
 int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const shd::u32** rec_pos,
                    const shd::u32** rec_idx, const shd::u64** rec_vals, int64_t* rec_cap);

@@ -19,6 +19,7 @@
 #include "sh_agg.h"
 #include "sh_internal.h"
 #include "sh_runtime.h"
+#include "sh_sliding.h"
 
 using namespace shd;
 
@@ -56,6 +57,11 @@ struct sh_shard {
     int64_t W = 0;        // window of the last event of the stream so far
     int64_t carry = 0;    // lengthBatch: passing events in the open batch (count, :206-243)
     uint64_t seq = 0;     // events of the stream so far (global index of the next event)
+    // sliding time(T): PM (max ts over the stream's passing events so far) and sends so far
+    bool sliding = false;
+    int64_t sl_pm = INT64_MIN;
+    int64_t send_base = 0, cur_send_base = 0, cur_send_size = 1, cur_n = 0;
+    DevBuf sl_clk, sl_pmv;
     // the push in flight (pack -> consume)
     bool packed = false;
     int64_t cur_W_base = 0, cur_W_end = 0;
@@ -82,8 +88,12 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_create: NULL argument");
     if (world < 1 || world > kMaxShards || rank < 0 || rank >= world)
         return sh_fail(SH_ERR_INVALID, "sh_shard_create: need 0 <= rank < world <= 16");
-    if (d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_LENGTH_BATCH)
-        return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch / lengthBatch group-by queries");
+    if (d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded ingest runs timeBatch / lengthBatch / time group-by queries");
+    if (d->window == SH_WIN_TIME && (d->partition_col >= 0 || kp_override))
+        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned sliding windows are not on the GPU");
+    if (d->window == SH_WIN_TIME && d->n_cols + 2 > SH_MAX_COLS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows carry 2 extra columns: at most 6 stream columns");
     if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
@@ -122,6 +132,12 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
             s->wkp.n++;
         }
     }
+    // sliding: the send's global clock and the global PM travel as two extra raw columns
+    s->sliding = d->window == SH_WIN_TIME;
+    if (s->sliding) {
+        s->rp.src[s->rp.n++] = d->n_cols;
+        s->rp.src[s->rp.n++] = d->n_cols + 1;
+    }
     // round-robin owners for one dictionary-id component (dense ids stay dense per owner)
     s->wkp.dense = (s->wkp.n == 1 && s->wkp.type[0] == SH_T_STRID) ? 1 : 0;
     s->key32 = (s->wkp.n == 0 || (s->wkp.n == 1 && s->wkp.type[0] != SH_T_LONG)) ? 1 : 0;
@@ -146,10 +162,10 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         q->kt.dmul = (uint32_t)world;
         q->kt.dadd = (uint32_t)rank;
     }
-    s->roles.n = d->n_cols;
-    for (int c = 0; c < d->n_cols; c++) {
-        int t = d->col_types[c];
-        q->load_type[c] = (t == SH_T_FLOAT || t == SH_T_DOUBLE) ? SH_T_DOUBLE : SH_T_LONG;
+    s->roles.n = d->n_cols + (s->sliding ? 2 : 0);
+    for (int c = 0; c < s->roles.n; c++) {
+        int t = c < d->n_cols ? d->col_types[c] : SH_T_LONG;
+        if (c < d->n_cols) q->load_type[c] = (t == SH_T_FLOAT || t == SH_T_DOUBLE) ? SH_T_DOUBLE : SH_T_LONG;
         s->roles.role[c] = -1;
         for (int g = 0; g < s->wkp.n; g++) if (s->wkp.col[g] == c) s->roles.role[c] = 16 + g;
         for (int j = 0; j < s->rp.n; j++) if (s->rp.src[j] == c) s->roles.role[c] = j;
@@ -185,7 +201,8 @@ extern "C" int sh_shard_destroy(sh_shard* s) {
     if (s->agg) agg_release_sharded(s->agg);
     if (s->owner) sh_query_destroy(s->owner);
     DevBuf* bufs[] = {&s->blk_pass, &s->blk_tl, &s->blk_first, &s->info, &s->code, &s->counts, &s->tmp,
-                      &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx, &s->u_bg, &s->u_bw};
+                      &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx, &s->u_bg, &s->u_bw,
+                      &s->sl_clk, &s->sl_pmv};
     for (DevBuf* b : bufs) b->release();
     for (auto& c : s->u_cols) c.release();
     if (s->h_info) (void)hipHostFree(s->h_info);
@@ -220,6 +237,24 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     RCHK(s->blk_pass.reserve(nblk * 8, false));
     RCHK(s->blk_tl.reserve(nblk * 8, false));
     RCHK(s->blk_first.reserve(nblk * 8, false));
+    if (s->sliding) {
+        // pass count, max send-last ts, max passing ts (PM) of the slice; blk_first holds the PM prefix
+        WinParams wp{};
+        wp.kind = SH_WIN_TIME;
+        wp.N = b->n;
+        wp.send_size = b->send_size;
+        launch_sl_prefix(st, b->ts, colset(s, b), s->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                         s->blk_first.as<int64_t>(), nblk, s->info.as<SlInfo>());
+        HIPCHK(hipGetLastError());
+        SlInfo si{};
+        HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        si = *(const SlInfo*)s->h_info;
+        out->n_pass = si.total_pass;
+        out->max_tl = si.max_tl;
+        out->first_key = si.max_pm;
+        return SH_OK;
+    }
     launch_blockagg(st, b->ts, colset(s, b), s->fp, b->n, b->send_size, s->blk_pass.as<int64_t>(),
                     s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(), nblk);
     WinParams wp{};
@@ -251,6 +286,78 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     return SH_OK;
 }
 
+// Phase 2 of a sliding time(T) query: every passing event gets its send's global clock and the global
+// PM (max ts over the passing events of the stream up to it: the slices before contribute their
+// summaries' PM, carried in sh_slice_summary.first_key) and goes to its key's owner.
+static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch* b, void* send_buf,
+                        int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds,
+                        const std::vector<int64_t>& cin, const std::vector<int64_t>& off, int64_t clock_end,
+                        int64_t n_total) {
+    const int G = s->world;
+    const int64_t RB = 4 * (int64_t)s->rec_words;
+    int64_t pm_in = s->sl_pm, pm_end = s->sl_pm, sends = 0;
+    const int64_t ss = std::max<int64_t>(1, b->send_size);
+    for (int r = 0; r < G; r++) {
+        if (r < s->rank) pm_in = std::max(pm_in, all[r].first_key);
+        pm_end = std::max(pm_end, all[r].first_key);
+        sends += (all[r].n + ss - 1) / ss;
+    }
+    s->my_bounds.clear();
+    for (int r = 0; r < G; r++) send_bytes[r] = 0;
+    const int64_t N = b->n;
+    if (N > 0) {
+        hipStream_t st = s->ctx->stream;
+        int nblk = (int)((N + kTile - 1) / kTile);
+        int64_t ncnt = (int64_t)G * nblk;
+        RCHK(s->code.reserve(N * 4, false));
+        RCHK(s->counts.reserve((ncnt + 1) * 8, false));
+        RCHK(s->tmp.reserve(((ncnt + kTile) / kTile + 16) * 8, false));
+        RCHK(s->part_off.reserve((G + 1) * 8, false));
+        RCHK(s->sl_clk.reserve(N * 8, false));
+        RCHK(s->sl_pmv.reserve(N * 8, false));
+        WinParams wp{};
+        wp.kind = SH_WIN_TIME;
+        wp.clock_valid = cin[s->rank] != INT64_MIN;
+        wp.clock0 = cin[s->rank];
+        wp.N = N;
+        wp.send_size = b->send_size;
+        launch_shard_sl_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(),
+                               pm_in, s->wkp, G, nblk, s->code.as<u32>(), s->counts.as<int64_t>(),
+                               s->sl_clk.as<int64_t>(), s->sl_pmv.as<int64_t>());
+        HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
+        launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
+        ColSet cs = colset(s, b);
+        cs.ptr[cs.n] = s->sl_clk.p; cs.type[cs.n] = SH_T_LONG;
+        cs.ptr[cs.n + 1] = s->sl_pmv.p; cs.type[cs.n + 1] = SH_T_LONG;
+        cs.n += 2;
+        launch_shard_pack(st, cs, b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk, s->counts.as<int64_t>(),
+                          (unsigned char*)send_buf, s->rec_words, s->key32);
+        launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        std::vector<int64_t> po(G + 1);
+        HIPCHK(hipMemcpyAsync(po.data(), s->part_off.p, (G + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int r = 0; r < G; r++) send_bytes[r] = (po[r + 1] - po[r]) * RB;
+    }
+    s->cur_seq = (int64_t)s->seq;
+    s->cur_off = off;
+    s->cur_send_base = s->send_base;
+    s->cur_send_size = ss;
+    s->cur_n = n_total;
+    if (clock_end != INT64_MIN) {
+        s->clock = clock_end;
+        s->clock_valid = true;
+    }
+    s->sl_pm = pm_end;
+    s->send_base += sends;
+    s->seq += (uint64_t)n_total;
+    s->packed = true;
+    s->slice_n = -1;
+    *bounds = s->my_bounds.data();
+    *n_bounds = 0;
+    return SH_OK;
+}
+
 // Phase 2: global clock / nextEmitTime / windows from the G summaries, then the per-owner records.
 extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_batch* b, void* send_buf,
                              int64_t send_cap, int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds) {
@@ -273,6 +380,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     }
     const int64_t clock_end = c, n_total = o;
     if (s->seq + (uint64_t)n_total >= (1ull << 40)) return sh_fail(SH_ERR_UNSUPPORTED, "stream longer than 2^40 events");
+    if (s->sliding) return pack_sliding(s, all, b, send_buf, send_bytes, bounds, n_bounds, cin, off, clock_end, n_total);
     // R12: the partition of the stream's first passing event armed the shared timer and is the only
     // one that ever flushes; from here on the ingest keeps only its events (the owner needs no filter)
     if (s->partitioned && !s->p0_known) {
@@ -397,6 +505,49 @@ static void set_order(sh_shard* s, bool host_out, const int64_t** order) {
     *order = host_out ? q->order_host.data() : q->out_order.as<int64_t>();
 }
 
+// Phase 3 of a sliding query: unpack, then the owner's per-key replay with the records' global clock,
+// PM and stream index (one flush per global send that touched the owner's keys).
+static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, int64_t M, bool host_out,
+                           const sh_out** out, const int64_t** order) {
+    sh_query* q = s->owner;
+    hipStream_t st = s->ctx->stream;
+    const int64_t cap = std::max<int64_t>(M, 1);
+    RCHK(s->u_ts.reserve(cap * 8, false));
+    RCHK(s->u_wcol.reserve(cap * 4, false));
+    RCHK(s->u_gidx.reserve(cap * 8, false));
+    ColPtrs cp{};
+    const void* cols[SH_MAX_COLS] = {};
+    for (int c = 0; c < s->roles.n; c++) {
+        if (s->roles.role[c] < 0) continue;
+        RCHK(s->u_cols[c].reserve(cap * 8, false));
+        cp.p[c] = s->u_cols[c].as<u64>();
+        cols[c] = cp.p[c];
+    }
+    ShardSrc src{};
+    src.G = s->world;
+    src.key32 = s->key32;
+    int64_t acc = 0;
+    const int64_t RB = 4 * (int64_t)s->rec_words;
+    for (int g = 0; g < s->world; g++) {
+        src.start[g] = acc;
+        acc += recv_bytes[g] / RB;
+        src.gbase[g] = s->cur_seq + s->cur_off[g];
+    }
+    src.start[s->world] = acc;
+    if (M > 0)
+        launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->wkp, s->roles, src, nullptr,
+                            nullptr, 0, 0, s->u_ts.as<int64_t>(), cp, s->u_wcol.as<int>(), s->u_gidx.as<u64>());
+    HIPCHK(hipGetLastError());
+    const int nc = s->d.n_cols;
+    RCHK(sliding_push_given(q, M, s->u_ts.as<int64_t>(), cols, s->u_cols[nc].as<int64_t>(),
+                            s->u_cols[nc + 1].as<int64_t>(), (const uint64_t*)s->u_gidx.p, s->cur_seq,
+                            s->cur_send_size, s->cur_send_base, host_out, out, s->cur_n));
+    q->clock = s->clock;
+    q->clock_valid = s->clock_valid;
+    set_order(s, host_out, order);
+    return SH_OK;
+}
+
 // Phase 3: the owner aggregates the records of its keys (event order preserved: sources are
 // concatenated in rank order and every source run is in stream order).
 extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, const sh_bound* all_bounds,
@@ -415,6 +566,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     const int64_t M = bytes / RB;
     if (M > 0 && !recv_buf) return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL receive buffer");
     sh_query* q = s->owner;
+    if (s->sliding) return consume_sliding(s, recv_buf, recv_bytes, M, host_out != 0, out, order);
     q->gbounds.assign(all_bounds, all_bounds + n_all_bounds);
     std::sort(q->gbounds.begin(), q->gbounds.end(), [](const sh_bound& a, const sh_bound& c) { return a.gidx < c.gidx; });
     q->given_W_base = s->cur_W_base;
@@ -486,6 +638,17 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_advance_time: NULL argument");
     if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");
     sh_query* q = s->owner;
+    if (s->sliding) {
+        // expiry is lazy (applied at each key's next event): the TIMER only moves the clock
+        RCHK(sliding_advance(q, now, out));
+        if (!(s->clock_valid && now < s->clock)) {
+            s->clock = now;
+            s->clock_valid = true;
+        }
+        q->order_host.clear();
+        set_order(s, true, order);
+        return SH_OK;
+    }
     sync_owner(s);
     if (s->agg) host_out = 0;
     RCHK(query_advance(q, now, host_out != 0, out));

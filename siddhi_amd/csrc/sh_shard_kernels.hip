@@ -139,6 +139,62 @@ void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f
                        G, nblk, code, counts, bounds, max_bounds, n_bounds);
 }
 
+// Sliding time(T) (TimeWindowProcessor :132-169): the owner needs, per passing event, the global
+// clock of its send and PM = max ts over the passing events of the whole stream up to it (its expiry
+// key, sh_sliding_kernels.hip); both are prefix quantities of the slice (blk_*_pre from the sliding
+// prefix scan) continued from the slices before (wp.clock0, pm0). They travel as two extra raw
+// columns of the record; code = owner (no window bits).
+__global__ __launch_bounds__(kBlock) void k_shard_sl_assign(const i64* __restrict__ ts, ColSet cols, FilterProg f,
+                                                           WinParams wp, const i64* __restrict__ blk_tl_pre,
+                                                           const i64* __restrict__ blk_pm_pre, i64 pm0, KeyPlan kp,
+                                                           int G, int nblk, u32* code, i64* counts, i64* clk_out,
+                                                           i64* pm_out) {
+    __shared__ u32 hist[kMaxShards];
+    if (threadIdx.x < kMaxShards) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    bool pass[kItems];
+    i64 tl = INT64_MIN, pm = INT64_MIN;
+    filter_items(f, cols, base, wp.N, pass);
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        const i64 e = base + i;
+        if (e < wp.N) {
+            const i64 t = ts[e];
+            if (pass[i]) pm = max(pm, t);
+            if (is_send_last(wp, e)) tl = max(tl, t);
+        }
+    }
+    i64 cm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
+    i64 pmx = max(max(block_excl_scan(pm, MaxOp(), INT64_MIN, nullptr), blk_pm_pre[blockIdx.x]), pm0);
+    const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        const i64 e = base + i;
+        if (e >= wp.N) break;
+        const i64 t = ts[e];
+        u32 c = kNoPos;
+        if (pass[i]) {
+            pmx = max(pmx, t);
+            clk_out[e] = max(c0, max(cm, ts[send_last_of(wp, e)]));
+            pm_out[e] = pmx;
+            c = owner_of(kp, make_key(kp, cols, e), G);
+            atomicAdd(&hist[c], 1u);
+        }
+        code[e] = c;
+        if (is_send_last(wp, e)) cm = max(cm, t);
+    }
+    __syncthreads();
+    if (threadIdx.x < G) counts[(i64)threadIdx.x * nblk + blockIdx.x] = hist[threadIdx.x];
+}
+
+void launch_shard_sl_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
+                            const i64* blk_tl_pre, const i64* blk_pm_pre, i64 pm0, KeyPlan kp, int G, int nblk,
+                            u32* code, i64* counts, i64* clk_out, i64* pm_out) {
+    hipLaunchKernelGGL(k_shard_sl_assign, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_tl_pre, blk_pm_pre, pm0,
+                       kp, G, nblk, code, counts, clk_out, pm_out);
+}
+
 // Stable multisplit by owner. Tile events are taken in kItems rounds of kBlock consecutive events;
 // inside a round, the rank of an event among the same owner's events is (waves before) + (lanes
 // before), so every owner's run keeps event order. offsets = exclusive scan of counts[o][tile].

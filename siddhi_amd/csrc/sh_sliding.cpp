@@ -151,6 +151,9 @@ static int empty_out(sh_query* q, const sh_out** out) {
     return SH_OK;
 }
 
+static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
+                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out);
+
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
@@ -197,10 +200,70 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     HIPCHK(hipStreamSynchronize(st));
     RCHK(q->kt.check(st));
     SlInfo info = *s->h_info;
-    int64_t M = info.total_pass;
-    if (info.need > s->rc) {
+    RCHK(sliding_finish(q, info.total_pass, N, info.need, b->send_size, s->send_base, 0, false, host_out, out));
+    // window state moves on
+    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+    q->clock_valid = true;
+    s->pm = std::max(s->pm, info.max_pm);
+    s->send_base += b->send_size > 0 ? (N + b->send_size - 1) / b->send_size : 1;
+    q->stats.events = N;
+    return SH_OK;
+}
+
+// Sharded owner push (sh_shard.cpp): M records of this owner's keys, already filtered, in stream
+// order, with their send's global clock, the global PM and their global stream index. The push's
+// sends are numbered from send_base; raw = gidx - raw_base is the position in the global push.
+int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* const* cols, const int64_t* gclk,
+                       const int64_t* gpm, const uint64_t* gidx, int64_t raw_base, int64_t send_size,
+                       int64_t send_base, bool host_out, const sh_out** out, int64_t n_global) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    if (M < 0 || n_global >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "bad sharded sliding push");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    int V = std::max(1, q->ap.n_vcols);
+    int64_t cap = std::max<int64_t>(M, 1);
+    RCHK(s->rec_raw.reserve(cap * 4, false));
+    RCHK(s->rec_slot.reserve(cap * 4, false));
+    RCHK(s->rec_clock.reserve(cap * 8, false));
+    RCHK(s->rec_pm.reserve(cap * 8, false));
+    RCHK(s->rec_ts.reserve(cap * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    RCHK(s->info.reserve(sizeof(SlInfo), false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = cols[c]; }
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    launch_sl_records_given(st, M, ts, cs, q->kp, q->kt.dev(), q->ap, gclk, gpm, (const u64*)gidx, raw_base, rec,
+                            s->slot_cnt.as<u32>());
+    HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
+    launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
+                   (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    RCHK(q->kt.check(st));
+    RCHK(sliding_finish(q, M, cap, s->h_info->need, send_size, send_base, raw_base, true, host_out, out));
+    q->stats.events = M;
+    return SH_OK;
+}
+
+// The rest of a push once its M rank-ordered records are in place: ring growth, the per-key-partition
+// replay (launch_sliding_own), rows in rank order, one flush per send. want_order: also the global
+// stream index of every row's first event (raw_base + raw), into q->order_host / q->out_order.
+static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
+                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    int V = std::max(1, q->ap.n_vcols);
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), rec_cap};
+    if (need > s->rc) {
         int64_t nrc = s->rc;
-        while (nrc < info.need) nrc <<= 1;
+        while (nrc < need) nrc <<= 1;
         RCHK(size_rings(q, nrc));
     }
     int64_t n_rows = 0;
@@ -239,7 +302,7 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
         launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
         HIPCHK(hipEventRecord(q->ev_agg0, st));
         launch_sliding_own(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, s->logP, prec, state_of(s), q->ap,
-                           q->d.window_param, b->send_size, s->send_base, rows, s->flags.as<unsigned char>());
+                           q->d.window_param, send_size, send_base, rows, s->flags.as<unsigned char>());
         HIPCHK(hipEventRecord(q->ev_agg1, st));
         HIPCHK(hipGetLastError());
         // emit in rank order
@@ -263,10 +326,12 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
         RCHK(s->out_clock.reserve(cap * 8, false));
         RCHK(s->out_expired.reserve(cap, false));
         HIPCHK(hipMemsetAsync(s->out_expired.p, 0, cap, st));
+        if (want_order) RCHK(q->out_order.reserve(cap * 8, false));
         launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
         launch_sl_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, rows, na, q->kt.dev(),
                        q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
-                       s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>());
+                       s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(),
+                       s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr);
         HIPCHK(hipGetLastError());
     }
     // flush structure: a flush per send that produced rows (one selector output chunk per send)
@@ -287,17 +352,11 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
         HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, &n_rows, 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipGetLastError());
     }
-    // window state moves on
-    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
-    q->clock_valid = true;
-    s->pm = std::max(s->pm, info.max_pm);
-    s->send_base += b->send_size > 0 ? (N + b->send_size - 1) / b->send_size : 1;
     HIPCHK(hipEventRecord(q->ev_push1, st));
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
     q->stats.push_ms = ms;
-    q->stats.events = N;
     q->stats.main_kernel_bytes = M * (int64_t)(4 + 8 + 8 + 8 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 + 8 * q->ap.n);
     int nk = q->kp.n, na = q->ap.n;
     if (host_out) {
@@ -318,8 +377,13 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
             if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), s->out_keys.p, (size_t)nk * n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.vals.data(), s->out_vals.p, (size_t)na * n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.nulls.data(), s->out_nulls.p, (size_t)na * n_rows, hipMemcpyDeviceToHost, st));
+            if (want_order) {
+                q->order_host.resize(n_rows);
+                HIPCHK(hipMemcpyAsync(q->order_host.data(), q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, st));
+            }
             HIPCHK(hipStreamSynchronize(st));
         } else {
+            q->order_host.clear();
             o.flush_offsets.assign(1, 0);
         }
         *out = o.view(nk, na, q->vtypes);

@@ -64,7 +64,11 @@ void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off
                         unsigned char* flags);
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                    unsigned char* out_nulls, i64* out_send, i64* out_clock);
+                    unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw = nullptr,
+                    i64 raw_base = 0, i64* out_order = nullptr);
+void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, KeyPlan kp, KeyTable kt, AggPlan ap,
+                             const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
+                             u32* slot_cnt);
 void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb);
 void launch_flush_write(hipStream_t s, const i64* out_send, const i64* out_clock, i64 n_rows, const i64* blk_pre,
                         int nb, i64* flush_off, i64* flush_clock);

@@ -122,6 +122,34 @@ void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
                        blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt);
 }
 
+// Sharded owner (sh_shard.cpp): the records arrive filtered and re-keyed, with the global clock of
+// their send and the global PM computed by the source slice (sh_shard_kernels.hip k_shard_sl_assign);
+// raw = position in the global push, so send = send_base + raw / send_size as in the single stream.
+__global__ __launch_bounds__(kBlock) void k_sl_records_given(i64 M, const i64* __restrict__ ts, ColSet cols,
+                                                            KeyPlan kp, KeyTable kt, AggPlan ap,
+                                                            const i64* __restrict__ gclk, const i64* __restrict__ gpm,
+                                                            const u64* __restrict__ gidx, i64 raw_base,
+                                                            SlRecords rec, u32* slot_cnt) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= M) return;
+    const u32 pos = key_slot(kt, make_key(kp, cols, r));
+    rec.raw[r] = (u32)((i64)gidx[r] - raw_base);
+    rec.slot[r] = pos;
+    rec.clock[r] = gclk[r];
+    rec.pm[r] = gpm[r];
+    rec.ts[r] = ts[r];
+    for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], r);
+    atomicAdd(&slot_cnt[pos], 1u);
+}
+
+void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, KeyPlan kp, KeyTable kt, AggPlan ap,
+                             const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
+                             u32* slot_cnt) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_sl_records_given, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, M, ts,
+                       cols, kp, kt, ap, gclk, gpm, gidx, raw_base, rec, slot_cnt);
+}
+
 // max over slots of (ring length + new events): the ring capacity this push needs
 __global__ __launch_bounds__(kBlock) void k_sl_need(const u32* slot_cnt, const i64* rlen, i64 n, i64* out) {
     i64 m = 0;
@@ -1268,7 +1296,8 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
                                                    const i64* __restrict__ blk_pre, SlRows rows, int n_aggs,
                                                    KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys,
                                                    u64* out_vals, unsigned char* out_nulls, i64* out_send,
-                                                   i64* out_clock) {
+                                                   i64* out_clock, const u32* __restrict__ rank_raw, i64 raw_base,
+                                                   i64* out_order) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     unsigned char fl[kItems];
     i64 c = 0;
@@ -1287,6 +1316,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
         }
         out_send[r] = rows.send[j];
         out_clock[r] = rows.clock[j];
+        if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
         r++;
     }
 }
@@ -1326,9 +1356,10 @@ __global__ __launch_bounds__(kBlock) void k_flush_write(const i64* __restrict__ 
 
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                    unsigned char* out_nulls, i64* out_send, i64* out_clock) {
+                    unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw, i64 raw_base,
+                    i64* out_order) {
     hipLaunchKernelGGL(k_sl_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rows, n_aggs, kt, kp, out_cap,
-                       out_ts, out_keys, out_vals, out_nulls, out_send, out_clock);
+                       out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base, out_order);
 }
 
 void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb) {

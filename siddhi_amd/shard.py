@@ -162,17 +162,24 @@ def host_rows(out, order) -> dict:
     return d
 
 
-def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None) -> dict:
+def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None,
+                        sends: Optional[Tuple[int, int]] = None) -> dict:
     """Merge the G owners' outputs of one global push into the single-stream output: flushes are
     matched by flush clock (every owner flushes window w at the same global clock) and, when `bounds`
     (the push's all-gathered window starts) is given, by the window their rows' first events fall in
-    — several lengthBatch batches can complete in one send and share its clock. Rows inside a flush
-    are ordered by the global first-occurrence index."""
+    — several lengthBatch batches can complete in one send and share its clock. Sliding windows emit
+    one flush per send (QuerySelector output per chunk, R8) and consecutive sends can share a clock:
+    `sends` = (global index of the push's first event, send_size) keys their flushes by send number.
+    Rows inside a flush are ordered by the global first-occurrence index."""
+    if sends is not None:
+        return _merge_by_send(parts, sends)
     starts = np.sort(np.asarray(bounds, np.int64).reshape(-1, BOUND_WORDS)[:, 2]) if bounds is not None \
         else np.zeros(0, np.int64)
 
     def fkey(p, f):
         a = int(p["flush_offsets"][f])
+        if sends is not None:
+            return (int(p["flush_clock"][f]), (int(p["order"][a]) - sends[0]) // max(1, sends[1]))
         w = int(np.searchsorted(starts, int(p["order"][a]), side="right")) if starts.size else 0
         return (int(p["flush_clock"][f]), w)
 
@@ -216,6 +223,26 @@ def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None) 
     return res
 
 
+def _merge_by_send(parts: List[dict], sends: Tuple[int, int]) -> dict:
+    """One flush per send: the global row order is the order of the rows' first events (rows of an
+    earlier send come first), and a flush ends where the send number changes."""
+    seq0, ss = int(sends[0]), max(1, int(sends[1]))
+    ref = parts[0]
+    order = np.concatenate([p["order"] for p in parts])
+    clock = np.concatenate([np.repeat(p["flush_clock"], np.diff(p["flush_offsets"])) for p in parts])
+    perm = np.argsort(order, kind="stable")
+    order = order[perm]
+    send = (order - seq0) // ss
+    starts = np.flatnonzero(np.r_[True, send[1:] != send[:-1]]) if order.size else np.zeros(0, np.int64)
+    res = {"flush_offsets": np.r_[starts, order.size].astype(np.int64),
+           "flush_clock": clock[perm][starts].astype(np.int64), "val_types": ref["val_types"], "order": order}
+    for key in ("ts", "expired"):
+        res[key] = np.concatenate([p[key] for p in parts])[perm]
+    for key in ("keys", "vals", "nulls"):
+        res[key] = np.concatenate([p[key] for p in parts], axis=1)[:, perm]
+    return res
+
+
 class LocalShards:
     """G shards of one query in one process on one device; the exchange is a device copy.
     Drives exactly the protocol a multi-process run drives over torch.distributed."""
@@ -224,6 +251,7 @@ class LocalShards:
         cls = ShardedAggregation if isinstance(spec, abi.AggregationSpec) else ShardedQuery
         self.shards = [cls(spec, r, world, ctx) for r in range(world)]
         self.world = world
+        self.seq = 0  # global stream index of the next push's first event
 
     def push(self, slices, send_size: int, device) -> List[dict]:
         """slices: per rank (ts tensor, [col tensors]) on `device`. Returns per-owner host outputs."""
@@ -241,6 +269,8 @@ class LocalShards:
             bounds.append(bd)
         all_bounds = np.concatenate(bounds) if bounds else np.zeros((0, BOUND_WORDS), np.int64)
         self.last_bounds = all_bounds
+        self.last_sends = (self.seq, send_size)
+        self.seq += sum(int(ts.numel()) for ts, _ in slices)
         outs = []
         for o, s in enumerate(self.shards):
             blocks, rbytes = [], []

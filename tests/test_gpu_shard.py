@@ -41,7 +41,7 @@ def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
             slices.append((torch.from_numpy(np.ascontiguousarray(ts[a:b])).to(dev),
                            [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in cols]))
         outs = ls.push(slices, send_size, dev)
-        parts.append(merge_owner_outputs(outs, ls.last_bounds))
+        parts.append(merge_owner_outputs(outs, ls.last_bounds, ls.last_sends if sp.window == "time" else None))
     if advance is not None:
         parts.append(merge_owner_outputs(ls.advance_time(advance)))
     ls.close()
@@ -179,3 +179,41 @@ def test_sharded_lengthbatch_batches_ending_at_push_and_slice_ends():
     got1 = run_sharded(sp, 4, pushes, 1, [[0.1, 0.2, 0.3]])
     ref1 = run_oracle(sp, pushes, 1)
     assert_same(got1, ref1, label="sharded lengthBatch edges per-event")
+
+
+# ---- C3 over G GPUs: sliding time(T) (the clock and PM of every event are global: the source slice
+# computes them from the all-gathered summaries; the owner replays its keys' windows with them) ----
+def c3_spec(keys, T, filt=None, aggs=None, schema=SCHEMA, group_by=("k",)):
+    return abi.QuerySpec(schema, "time", T, group_by=list(group_by),
+                         aggs=aggs or [("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], filter=filt,
+                         key_capacity=keys)
+
+
+@pytest.mark.parametrize("world,send_size", [(2, 1), (3, 250), (8, 1)])
+def test_sharded_c3_sliding_matches_single_stream(world, send_size):
+    sp = c3_spec(2000, 1000)
+    pushes = stream_pushes(200_000, [77_777, 1, 122_222], 0xC3, 2000, 20)
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.1 * (g + 1) for g in range(world - 1)]]
+    got = run_sharded(sp, world, pushes, send_size, fr, advance=int(pushes[-1][0][-1]) + 5000)
+    ref = run_oracle(sp, pushes, send_size, advance=int(pushes[-1][0][-1]) + 5000)
+    assert ref["flush_offsets"].size > 500
+    assert_same(got, ref, label=f"sharded C3 x{world}")
+
+
+def test_sharded_sliding_filter_nonmonotone_ts_dictionary_keys():
+    """Out-of-order timestamps (PM, not ts, decides expiry), a filter, dictionary-id keys (owner =
+    id % G) and the deque quirk on few distinct values, with a quiet owner."""
+    rng = np.random.default_rng(11)
+    n = 60_000
+    ts = (np.arange(n) // 4 + rng.integers(-50, 50, n)).astype(np.int64) + 10_000
+    k = rng.integers(0, 7, n).astype(np.int32)
+    v = rng.integers(0, 6, n).astype(np.float64)
+    x = rng.integers(-10**9, 10**9, n).astype(np.int64)
+    sch = abi.Schema.parse("k string, v double, x long, ts long")
+    sp = c3_spec(16, 300, filt=(">", "x", -5 * 10**8), schema=sch,
+                 aggs=[("min", "v"), ("max", "v"), ("sum", "x"), ("count", None), ("avg", "v")])
+    full = [k, v, x, ts.copy()]
+    pushes = [(ts[:25_000], [c[:25_000] for c in full]), (ts[25_000:], [c[25_000:] for c in full])]
+    got = run_sharded(sp, 5, pushes, 7, [[0.2, 0.4, 0.6, 0.8], [0.0, 0.5, 0.5, 0.99]])
+    ref = run_oracle(sp, pushes, 7)
+    assert_same(got, ref, label="sharded sliding nonmono")

@@ -25,3 +25,28 @@ def test_empty_tables_merge():
     e = table([])
     m = merge_tables([e, e])
     assert m["keys"].shape == (2, 0)
+
+
+def owner_out(order, clocks_per_flush, flush_offsets, vals):
+    order = np.asarray(order, np.int64)
+    n = order.size
+    return {"order": order, "flush_offsets": np.asarray(flush_offsets, np.int64),
+            "flush_clock": np.asarray(clocks_per_flush, np.int64), "ts": order * 10, "expired": np.zeros(n, np.uint8),
+            "keys": order[None, :] % 5, "vals": np.asarray(vals, np.uint64)[None, :], "nulls": np.zeros((1, n), np.uint8),
+            "val_types": np.zeros(1, np.int32)}
+
+
+def test_sliding_owner_outputs_merge_per_send():
+    """Sliding windows: one flush per send (consecutive sends may share a clock); rows of a send in the
+    order of their first events across owners (siddhi_amd.shard._merge_by_send)."""
+    from siddhi_amd.shard import merge_owner_outputs
+    # push starts at global index 100, send_size 4: sends 0 = [100,104), 1 = [104,108), 2 = [108,112)
+    a = owner_out([101, 103, 109], [7, 8], [0, 2, 3], [1, 2, 3])        # sends 0 and 2
+    b = owner_out([100, 105, 106, 111], [7, 7, 8], [0, 1, 3, 4], [4, 5, 6, 7])  # sends 0, 1, 2
+    m = merge_owner_outputs([a, b], sends=(100, 4))
+    assert m["order"].tolist() == [100, 101, 103, 105, 106, 109, 111]
+    assert m["flush_offsets"].tolist() == [0, 3, 5, 7]
+    assert m["flush_clock"].tolist() == [7, 7, 8]   # sends 0 and 1 share clock 7 but stay separate flushes
+    assert m["vals"][0].tolist() == [4, 1, 2, 5, 6, 3, 7]
+    e = merge_owner_outputs([owner_out([], [], [0], []), owner_out([], [], [0], [])], sends=(0, 1))
+    assert e["flush_offsets"].tolist() == [0] and e["keys"].shape == (1, 0)
