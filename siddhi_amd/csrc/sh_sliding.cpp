@@ -117,9 +117,10 @@ int sliding_create(sh_query* q) {
         return sh_fail(SH_ERR_OOM, "pinned alloc failed");
     RCHK(size_rings(q, 64));
     int P = 1;
-    // key partitions of at most 64 local keys: one lane of k_sl_own per key (the multisplit's LDS
-    // histogram caps P at 4096; beyond that lanes own several keys)
-    while (P < 4096 && (int64_t)P * 64 < n) P <<= 1;
+    // key partitions small enough for one replay lane per key (64 for k_sl_own, kSlKeyLanes for
+    // k_sl_own_d); the multisplit's LDS histogram caps P at 4096, beyond that lanes own several keys
+    const int per = sliding_keys_per_partition(q->ap);
+    while (P < 4096 && (int64_t)P * per < n) P <<= 1;
     s->P = P;
     s->logP = 0;
     while ((1 << s->logP) < P) s->logP++;

@@ -58,6 +58,7 @@ void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* cou
                           i64* part_off);
 void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, int P, SlRecords rec, SlState S,
                     AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags);
+int sliding_keys_per_partition(AggPlan ap);
 void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv);
 void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
                         SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,

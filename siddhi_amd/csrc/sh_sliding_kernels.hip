@@ -446,7 +446,16 @@ __global__ __launch_bounds__(64) void k_sliding(const u32* __restrict__ rank_lis
 //    in global memory for the rest of the push (sorted input makes deques as long as the window).
 // ------------------------------------------------------------------------------------------------
 constexpr int kSlCh = 2048;
-constexpr int kSlKeyLanes = 8;  // key-owning lanes per wave of k_sl_own_d
+#ifndef SH_SL_KL
+#define SH_SL_KL 8
+#endif
+// records staged per chunk of k_sl_own_d. Measured on MI355X, C3 (10k keys, 16.7M events per
+// push): CH 512 -> 23.9 ms at KL 8 with CH 256, 20.2 ms at CH 128, 20.1 ms at CH 64; KL 4/8/16
+// within 10% at CH 256, KL 2 31 ms (the ~11 KB LDS footprint at CH 128 keeps ~14 waves per CU)
+#ifndef SH_SL_CH
+#define SH_SL_CH 128
+#endif
+constexpr int kSlKeyLanes = SH_SL_KL;  // key-owning lanes per wave of k_sl_own_d
 constexpr int kDqL = 32;
 
 template <int NA, int NV>
@@ -908,10 +917,10 @@ __global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_li
                                                 int logP, SlRecords rec, SlState S, AggPlan ap, DFields fd, i64 T,
                                                 i64 send_size, i64 send_base, SlRows rows, unsigned char* flags) {
     // KL key lanes per wave (one key each when the partition has <= KL local keys): few lanes keep
-    // the divergence of the per-key chains low, and the small LDS footprint (≈ 20 KB) lets many
+    // the divergence of the per-key chains low, and the small LDS footprint (≈ 11 KB) lets many
     // waves share a CU, which is what hides each chain's instruction latency
     constexpr int KL = kSlKeyLanes;
-    constexpr int CH = 512;
+    constexpr int CH = SH_SL_CH;
     __shared__ u32 ch_rank[CH];
     __shared__ u32 ch_slot[CH];
     __shared__ unsigned short list[CH];
@@ -1231,26 +1240,40 @@ void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlR
                        nv);
 }
 
+// the double-column shape (C3): count + at most one each of sum / avg / min / max of one DOUBLE
+static bool own_d_fields(const AggPlan& ap, DFields& fd) {
+    fd = DFields{-1, -1, -1, -1};
+    bool ok = ap.n_vcols == 1 && ap.vcol_type[0] == SH_T_DOUBLE;
+    for (int a = 0; ok && a < ap.n; a++) {
+        int* slotp = nullptr;
+        switch (ap.kind[a]) {
+            case AK_COUNT: continue;
+            case AK_SUM_D: slotp = &fd.sum; break;
+            case AK_AVG: slotp = &fd.avg; break;
+            case AK_MIN_D: slotp = &fd.mn; break;
+            case AK_MAX_D: slotp = &fd.mx; break;
+            default: ok = false; continue;
+        }
+        if (*slotp >= 0) ok = false;
+        else *slotp = ap.field[a];
+    }
+    return ok;
+}
+
+// keys a key partition should hold so that every key gets a lane of its own in the replay kernel
+// (k_sl_own_d: kSlKeyLanes per wave; k_sl_own: 64). A lane owning several keys switches per-key
+// state (global loads and stores) whenever consecutive records of its list change key.
+int sliding_keys_per_partition(AggPlan ap) {
+    DFields fd;
+    return own_d_fields(ap, fd) ? kSlKeyLanes : 64;
+}
+
 void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
                         SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,
                         unsigned char* flags) {
-    // the double-column shape (C3): count + at most one each of sum / avg / min / max of one DOUBLE
     {
-        DFields fd{-1, -1, -1, -1};
-        bool ok = ap.n_vcols == 1 && ap.vcol_type[0] == SH_T_DOUBLE;
-        for (int a = 0; ok && a < ap.n; a++) {
-            int* slotp = nullptr;
-            switch (ap.kind[a]) {
-                case AK_COUNT: continue;
-                case AK_SUM_D: slotp = &fd.sum; break;
-                case AK_AVG: slotp = &fd.avg; break;
-                case AK_MIN_D: slotp = &fd.mn; break;
-                case AK_MAX_D: slotp = &fd.mx; break;
-                default: ok = false; continue;
-            }
-            if (*slotp >= 0) ok = false;
-            else *slotp = ap.field[a];
-        }
+        DFields fd;
+        const bool ok = own_d_fields(ap, fd);
         if (ok) {
             const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
 #define SH_SL_D(A, B, C)                                                                                      \
