@@ -1321,16 +1321,18 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
                                                    u64* out_vals, unsigned char* out_nulls, i64* out_send,
                                                    i64* out_clock, const u32* __restrict__ rank_raw, i64 raw_base,
                                                    i64* out_order) {
-    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
-    unsigned char fl[kItems];
-    i64 c = 0;
-#pragma unroll
-    for (int i = 0; i < kItems; i++) { fl[i] = base + i < n ? flags[base + i] : 0; c += fl[i]; }
-    i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + blk_pre[blockIdx.x];
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-        if (!fl[i]) continue;
-        i64 j = base + i;
+    // striped over the tile (round it: elements tile + it * kBlock + lane), so every row read and
+    // every output column store of a wave is one contiguous run; the tile's first output row is
+    // blk_pre (k_count_flags counts whole tiles, whatever the order inside)
+    const i64 tile = (i64)blockIdx.x * kTile;
+    i64 run = blk_pre[blockIdx.x];
+    for (int it = 0; it < kItems; it++) {
+        const i64 j = tile + (i64)it * kBlock + threadIdx.x;
+        const i64 fl = j < n ? flags[j] : 0;
+        i64 tot;
+        const i64 r = run + block_excl_scan(fl, SumOp(), 0, &tot);
+        run += tot;
+        if (!fl) continue;
         out_ts[r] = rows.ts[j];
         unpack_key(kp, slot_key(kt, rows.slot[j]), out_keys + r, out_cap);
         for (int a = 0; a < n_aggs; a++) {
@@ -1340,7 +1342,6 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
         out_send[r] = rows.send[j];
         out_clock[r] = rows.clock[j];
         if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
-        r++;
     }
 }
 
