@@ -300,10 +300,11 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         RCHK(s->p_vals.reserve((size_t)V * M * 8, false));
         SlRecords prec{s->p_raw.as<u32>(), s->p_slot.as<u32>(), s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
                        s->p_ts.as<int64_t>(), s->p_vals.as<u64>(), M};
-        launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
+        // the double-column replay (k_sl_own_d) reads the records through the rank lists itself
+        if (sliding_keys_per_partition(q->ap) == 64) launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
         HIPCHK(hipEventRecord(q->ev_agg0, st));
         launch_sliding_own(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, s->logP, prec, state_of(s), q->ap,
-                           q->d.window_param, send_size, send_base, rows, s->flags.as<unsigned char>());
+                           q->d.window_param, send_size, send_base, rows, s->flags.as<unsigned char>(), rec);
         HIPCHK(hipEventRecord(q->ev_agg1, st));
         HIPCHK(hipGetLastError());
         // emit in rank order

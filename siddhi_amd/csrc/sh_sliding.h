@@ -60,9 +60,11 @@ void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, in
                     AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags);
 int sliding_keys_per_partition(AggPlan ap);
 void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv);
+// rec: the records gathered into partition order (k_sl_own); rec_by_rank: the same records in rank
+// order, read through rank_list by k_sl_own_d (sliding_keys_per_partition(ap) == 8 shapes)
 void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
                         SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,
-                        unsigned char* flags);
+                        unsigned char* flags, SlRecords rec_by_rank);
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                     unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw = nullptr,

@@ -725,7 +725,8 @@ __device__ __forceinline__ void sl_rec_load(SlRec<NV>& o, const SlRecords& rec, 
 
 // Chunk split shared by the k_sl_own kernels: records [c0, c0+n) of the partition (event order)
 // into 64 stable per-lane lists (lane = (slot >> logP) & 63). Returns this lane's count and start.
-template <int KL = 64>
+// BYRANK: slot is indexed by record rank (records not gathered into partition order).
+template <int KL = 64, bool BYRANK = false>
 __device__ __forceinline__ void sl_chunk_split(const u32* __restrict__ rank_list, const u32* __restrict__ slot, i64 c0,
                                                int n, int logP, u32* ch_rank, u32* ch_slot, unsigned short* list,
                                                u32* run, u32& mine_out, u32& start_out) {
@@ -737,9 +738,10 @@ __device__ __forceinline__ void sl_chunk_split(const u32* __restrict__ rank_list
         const int j = g + lane;
         u32 o = 0;
         if (j < n) {
-            const u32 k = slot[c0 + j];
+            const u32 rk = rank_list[c0 + j];
+            const u32 k = BYRANK ? slot[rk] : slot[c0 + j];
             o = (k >> logP) & (KL - 1);
-            ch_rank[j] = rank_list[c0 + j];
+            ch_rank[j] = rk;
             ch_slot[j] = k;
         }
         u64 mask = __ballot(j < n);
@@ -912,7 +914,9 @@ __device__ __forceinline__ void dd_add(DDeque& q, u64* g, i64 gm, u64* l, u64 x)
     if (!q.mmh || d_worse<MIN>(q.mm, x)) { q.mm = x; q.mmh = true; }
 }
 
-template <bool HSUM, bool HMIN, bool HMAX>
+// BYRANK: `rec` is the push's records in rank order (no k_sl_gather pass): the chunk's fields are
+// read through the partition's rank list, and their latency overlaps the other waves' replay
+template <bool HSUM, bool HMIN, bool HMAX, bool BYRANK>
 __global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_list, const i64* __restrict__ part_off,
                                                 int logP, SlRecords rec, SlState S, AggPlan ap, DFields fd, i64 T,
                                                 i64 send_size, i64 send_base, SlRows rows, unsigned char* flags) {
@@ -963,20 +967,38 @@ __global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_li
     };
     for (i64 c0 = lo; c0 < hi; c0 += CH) {
         const int n = (int)min<i64>(CH, hi - c0);
-        // the chunk's fields, coalesced (the records are in partition order), into LDS
+        u32 mine, start;
+        if (!BYRANK) {
+            // the chunk's fields, coalesced (the records are in partition order), into LDS
 #pragma unroll 4
-        for (int g = 0; g < CH; g += 64) {
-            const int j = g + lane;
-            if (j < n) {
-                ch_clk[j] = rec.clock[c0 + j];
-                ch_pm[j] = rec.pm[c0 + j];
-                ch_ts[j] = rec.ts[c0 + j];
-                ch_raw[j] = rec.raw[c0 + j];
-                ch_v[j] = rec.vals[c0 + j];
+            for (int g = 0; g < CH; g += 64) {
+                const int j = g + lane;
+                if (j < n) {
+                    ch_clk[j] = rec.clock[c0 + j];
+                    ch_pm[j] = rec.pm[c0 + j];
+                    ch_ts[j] = rec.ts[c0 + j];
+                    ch_raw[j] = rec.raw[c0 + j];
+                    ch_v[j] = rec.vals[c0 + j];
+                }
             }
         }
-        u32 mine, start;
-        sl_chunk_split<KL>(rank_list, rec.slot, c0, n, logP, ch_rank, ch_slot, list, run, mine, start);
+        sl_chunk_split<KL, BYRANK>(rank_list, rec.slot, c0, n, logP, ch_rank, ch_slot, list, run, mine, start);
+        if (BYRANK) {
+            // each thread fetches the fields of the records whose rank it staged in the split
+#pragma unroll 4
+            for (int g = 0; g < CH; g += 64) {
+                const int j = g + lane;
+                if (j < n) {
+                    const u32 rk = ch_rank[j];
+                    ch_clk[j] = rec.clock[rk];
+                    ch_pm[j] = rec.pm[rk];
+                    ch_ts[j] = rec.ts[rk];
+                    ch_raw[j] = rec.raw[rk];
+                    ch_v[j] = rec.vals[rk];
+                }
+            }
+            __syncthreads();
+        }
         for (u32 i = 0; i < mine; i++) {
             const int j = list[start + i];
             const u32 r = ch_rank[j], k = ch_slot[j];
@@ -1270,15 +1292,16 @@ int sliding_keys_per_partition(AggPlan ap) {
 
 void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
                         SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,
-                        unsigned char* flags) {
+                        unsigned char* flags, SlRecords rec_by_rank) {
     {
         DFields fd;
         const bool ok = own_d_fields(ap, fd);
         if (ok) {
             const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
 #define SH_SL_D(A, B, C)                                                                                      \
-    hipLaunchKernelGGL((k_sl_own_d<A, B, C>), dim3(P), dim3(64), 0, s, rank_list, part_off, logP, rec, S, ap, fd, T, \
-                       send_size, send_base, rows, flags)
+    hipLaunchKernelGGL((k_sl_own_d<A, B, C, true>), dim3(P), dim3(64), 0, s, rank_list, part_off, logP, rec_by_rank, S, \
+                       ap, fd,                                                                                \
+                       T, send_size, send_base, rows, flags)
             if (hs && hn && hx) SH_SL_D(true, true, true);
             else if (hs && !hn && !hx) SH_SL_D(true, false, false);
             else if (!hs && hn && hx) SH_SL_D(false, true, true);
