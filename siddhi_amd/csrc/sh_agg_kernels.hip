@@ -217,9 +217,16 @@ __global__ __launch_bounds__(kBlock) void k_minmax_i64(const i64* __restrict__ x
     }
 }
 
+__global__ void k_minmax_init(i64* out) {
+    out[0] = INT64_MAX;
+    out[1] = INT64_MIN;
+}
+
 void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out) {
-    const i64 init[2] = {INT64_MAX, INT64_MIN};
-    (void)hipMemcpyAsync(out, init, 16, hipMemcpyHostToDevice, s);
+    // initialised on the stream by a kernel: an async copy from a stack array may read the array
+    // after this function returned (pageable source), which made the bucket span, and with it the
+    // root key-table reservation, intermittently wrong
+    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, s, out);
     if (n <= 0) return;
     unsigned g = (unsigned)std::min<i64>(1024, (n + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_minmax_i64, dim3(g), dim3(kBlock), 0, s, x, n, out);
