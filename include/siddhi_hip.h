@@ -79,6 +79,8 @@ typedef struct {
 #define SH_WIN_TIME 3         /* core/query/processor/stream/window/TimeWindowProcessor.java        */
 #define SH_WIN_EXT_TIME_BATCH 4 /* core/query/processor/stream/window/ExternalTimeBatchWindowProcessor.java:
                                    externalTimeBatch(ts_col, T[, start]) — event-time batches, no timeout */
+#define SH_WIN_EXT_TIME 5     /* core/query/processor/stream/window/ExternalTimeWindowProcessor.java:
+                                 externalTime(ts_col, T) — sliding over the LONG attribute ts_col    */
 
 /* ---- aggregators: core/query/selector/attribute/aggregator/ [Sum,Avg,Count,Min,Max]AttributeAggregatorExecutor ---- */
 #define SH_AGG_SUM 1
@@ -120,7 +122,7 @@ typedef struct {
     int32_t expired_on;     /* insert [expired|all] events                               */
     int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`     */
     int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing)  */
-    int32_t ts_col;         /* externalTimeBatch: the LONG timestamp attribute               */
+    int32_t ts_col;         /* externalTimeBatch / externalTime: the LONG timestamp attribute  */
     int32_t start_col;      /* externalTimeBatch: LONG start-time attribute (has_start_time 2) */
 } sh_query_desc;
 

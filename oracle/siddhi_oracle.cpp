@@ -602,6 +602,31 @@ struct Query {
         selector(ps, outc);
     }
 
+    // ExternalTimeWindowProcessor.process (:126-161): sliding over the attribute ts_col; each event
+    // expires the queue head while expiredTime - currentTime + timeToKeep <= 0 (currentTime = the
+    // event's attribute, not the playback clock), expired events re-stamped with currentTime
+    void ext_time_window(PartitionState& ps, Chunk& in) {
+        const int64_t T = d.window_param;
+        Chunk outc;
+        for (OEvent& ev : in) {
+            const int64_t now = ext_attr(ev, d.ts_col);
+            while (!ps.time_queue.empty()) {
+                OEvent& x = ps.time_queue.front();
+                if (ext_attr(x, d.ts_col) - now + T <= 0) {
+                    OEvent e2 = x; e2.ts = now; e2.type = EXPIRED;
+                    ps.time_queue.pop_front();
+                    outc.push_back(e2);  // insertBeforeCurrent
+                } else break;
+            }
+            if (ev.type == CURRENT) {
+                OEvent c = ev; c.type = EXPIRED;
+                ps.time_queue.push_back(c);
+                outc.push_back(ev);
+            }
+        }
+        selector(ps, outc);
+    }
+
     // ExternalTimeBatchWindowProcessor.process (:238-311) without a timeout (no TIMER events reach it):
     // initTiming (:313-334), flushToOutputChunk (:336-383), findEndTime (:440-444), cloneAppend
     // (:446-456). Every batch an event closes is its own downstream chunk, emitted after the whole
@@ -666,6 +691,7 @@ struct Query {
     void window(PartitionState& ps, Chunk& c) {
         switch (d.window) {
             case SH_WIN_EXT_TIME_BATCH: ext_time_batch(ps, c); break;
+            case SH_WIN_EXT_TIME: ext_time_window(ps, c); break;
             case SH_WIN_NONE: { Chunk k; for (auto& e : c) if (e.type != TIMER) k.push_back(e); if (!k.empty()) selector(ps, k); break; }
             case SH_WIN_LENGTH_BATCH: length_batch(ps, c); break;
             case SH_WIN_TIME_BATCH: time_batch(ps, c); break;
@@ -1037,7 +1063,13 @@ void* or_query_create(const sh_query_desc* desc) {
         desc->n_aggs > SH_MAX_AGGS || desc->n_group_by < 0 || desc->n_group_by > SH_MAX_GROUP) {
         g_err = "invalid descriptor"; return nullptr;
     }
-    if (desc->window < SH_WIN_NONE || desc->window > SH_WIN_EXT_TIME_BATCH) { g_err = "bad window"; return nullptr; }
+    if (desc->window < SH_WIN_NONE || desc->window > SH_WIN_EXT_TIME) { g_err = "bad window"; return nullptr; }
+    // ExternalTimeWindowProcessor.init (:108-116): the timestamp must be a LONG attribute
+    if ((desc->window == SH_WIN_EXT_TIME || desc->window == SH_WIN_EXT_TIME_BATCH) &&
+        (desc->ts_col < 0 || desc->ts_col >= desc->n_cols || desc->col_types[desc->ts_col] != SH_T_LONG)) {
+        g_err = "external time windows need a long timestamp attribute";
+        return nullptr;
+    }
     Query* q = new Query();
     q->d = *desc;
     q->schema.n = desc->n_cols;
@@ -1045,7 +1077,7 @@ void* or_query_create(const sh_query_desc* desc) {
     if (desc->n_filter_ops > 0) q->filter.assign(desc->filter, desc->filter + desc->n_filter_ops);
     q->output_expects_expired = desc->expired_on != 0;
     // ProcessingMode: time window -> SLIDE; batch windows -> BATCH (RESET if streamCurrent)
-    bool slide = desc->window == SH_WIN_TIME;
+    bool slide = desc->window == SH_WIN_TIME || desc->window == SH_WIN_EXT_TIME;
     for (int a = 0; a < desc->n_aggs; a++) {
         AggDef ad;
         ad.fn = desc->aggs[a].fn; ad.col = desc->aggs[a].col;

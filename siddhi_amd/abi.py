@@ -27,7 +27,7 @@ NP_DTYPE = {INT: np.int32, LONG: np.int64, FLOAT: np.float32, DOUBLE: np.float64
 OP_COL, OP_CONST, OP_GT, OP_GE, OP_LT, OP_LE, OP_EQ, OP_NE, OP_AND, OP_OR, OP_NOT = range(1, 12)
 CMP_OPS = {">": OP_GT, ">=": OP_GE, "<": OP_LT, "<=": OP_LE, "==": OP_EQ, "!=": OP_NE}
 
-WIN_NONE, WIN_LENGTH_BATCH, WIN_TIME_BATCH, WIN_TIME, WIN_EXT_TIME_BATCH = 0, 1, 2, 3, 4
+WIN_NONE, WIN_LENGTH_BATCH, WIN_TIME_BATCH, WIN_TIME, WIN_EXT_TIME_BATCH, WIN_EXT_TIME = 0, 1, 2, 3, 4, 5
 AGG_SUM, AGG_AVG, AGG_COUNT, AGG_MIN, AGG_MAX = 1, 2, 3, 4, 5
 AGG_NAMES = {"sum": AGG_SUM, "avg": AGG_AVG, "count": AGG_COUNT, "min": AGG_MIN, "max": AGG_MAX}
 DUR_SECONDS, DUR_MINUTES, DUR_HOURS, DUR_DAYS, DUR_MONTHS, DUR_YEARS = range(6)
@@ -185,7 +185,8 @@ class QuerySpec:
         d.n_filter_ops = len(fops)
         d.filter = C.cast(arr, C.POINTER(FilterOp))
         d.window = {None: WIN_NONE, "lengthBatch": WIN_LENGTH_BATCH, "timeBatch": WIN_TIME_BATCH,
-                    "time": WIN_TIME, "externalTimeBatch": WIN_EXT_TIME_BATCH}[self.window]
+                    "time": WIN_TIME, "externalTimeBatch": WIN_EXT_TIME_BATCH,
+                    "externalTime": WIN_EXT_TIME}[self.window]
         d.window_param = self.param
         d.stream_current = int(self.stream_current)
         d.has_start_time = int(self.start_time is not None)

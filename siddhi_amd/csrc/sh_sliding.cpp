@@ -35,7 +35,7 @@ struct SlidingImpl {
     DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
     // per push scratch
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
-        tmp, ranks, part_off, flags, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
+        tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
         out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, flush_off, flush_clock;
     SlInfo* h_info = nullptr;
     sh_out dev_out{};
@@ -139,7 +139,7 @@ void sliding_destroy(sh_query* q) {
                       &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
                       &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
-                      &s->out_expired, &s->flush_off, &s->flush_clock};
+                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk};
     for (DevBuf* b : bufs) b->release();
     if (s->h_info) (void)hipHostFree(s->h_info);
     delete s;
@@ -172,7 +172,8 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     RCHK(s->blk_tl.reserve(nblk * 8, false));
     RCHK(s->blk_pm.reserve(nblk * 8, false));
     WinParams wp{};
-    wp.kind = SH_WIN_TIME;
+    wp.kind = q->d.window;  // SH_WIN_TIME or SH_WIN_EXT_TIME
+    wp.ts_col = q->d.ts_col;
     wp.clock_valid = q->clock_valid;
     wp.clock0 = q->clock;
     wp.send_size = b->send_size;
@@ -191,8 +192,11 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), N};
+    const bool ext = q->d.window == SH_WIN_EXT_TIME;
+    if (ext) RCHK(s->rec_sclk.reserve(N * 8, false));
     launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk,
+                      ext ? s->rec_sclk.as<int64_t>() : nullptr);
     HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
     launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
                    (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
@@ -333,7 +337,8 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         launch_sl_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, rows, na, q->kt.dev(),
                        q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                        s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(),
-                       s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr);
+                       s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr,
+                       q->d.window == SH_WIN_EXT_TIME ? s->rec_sclk.as<int64_t>() : nullptr);
         HIPCHK(hipGetLastError());
     }
     // flush structure: a flush per send that produced rows (one selector output chunk per send)

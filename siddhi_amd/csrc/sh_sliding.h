@@ -52,7 +52,7 @@ void launch_sl_prefix(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, W
                       i64* blk_tl, i64* blk_pm, int nblk, SlInfo* info);
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
-                       i64 pm0, SlRecords rec, u32* slot_cnt, int nblk);
+                       i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock = nullptr);
 void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* out);
 void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* counts, i64* tmp, u32* out_rank,
                           i64* part_off);
@@ -68,7 +68,7 @@ void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                     unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw = nullptr,
-                    i64 raw_base = 0, i64* out_order = nullptr);
+                    i64 raw_base = 0, i64* out_order = nullptr, const i64* clock_by_rank = nullptr);
 void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, KeyPlan kp, KeyTable kt, AggPlan ap,
                              const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
                              u32* slot_cnt);

@@ -22,12 +22,14 @@ __global__ __launch_bounds__(kBlock) void k_sl_blockagg(const i64* __restrict__ 
     i64 cnt = 0, tl = INT64_MIN, pm = INT64_MIN;
     bool pass[kItems];
     filter_items(f, cols, base, wp.N, pass);
+    // externalTime: PM runs over the timestamp attribute instead of the event timestamps
+    const bool ext = wp.kind == SH_WIN_EXT_TIME;
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
             i64 t = ts[e];
-            if (pass[i]) { cnt++; pm = max(pm, t); }
+            if (pass[i]) { cnt++; pm = max(pm, ext ? load_raw(cols, wp.ts_col, e) : t); }
             if (is_send_last(wp, e)) tl = max(tl, t);
         }
     }
@@ -74,18 +76,20 @@ void launch_sl_prefix(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, W
 __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
                                                       const i64* blk_pass_pre, const i64* blk_tl_pre,
-                                                      const i64* blk_pm_pre, i64 pm0, SlRecords rec, u32* slot_cnt) {
+                                                      const i64* blk_pm_pre, i64 pm0, SlRecords rec, u32* slot_cnt,
+                                                      i64* send_clock) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     i64 cnt = 0, tl = INT64_MIN, pm = INT64_MIN;
     filter_items(f, cols, base, wp.N, pass);
+    const bool ext = wp.kind == SH_WIN_EXT_TIME;
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
         if (e < wp.N) {
             i64 t = ts[e];
             cnt += pass[i];
-            if (pass[i]) pm = max(pm, t);
+            if (pass[i]) pm = max(pm, ext ? load_raw(cols, wp.ts_col, e) : t);
             if (is_send_last(wp, e)) tl = max(tl, t);
         }
     }
@@ -99,8 +103,13 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
         if (e >= wp.N) break;
         i64 t = ts[e];
         if (pass[i]) {
-            pmx = max(pmx, t);
-            i64 clk = max(c0, max(cm, ts[send_last_of(wp, e)]));
+            // externalTime (ExternalTimeWindowProcessor :126-161): an event expires the queue head
+            // while headTime + T <= its own attribute, so event j has left the window at event i iff
+            // PMa(j) + T <= PMa(i) (PMa = running max of the attribute): clock = PMa(i)
+            pmx = max(pmx, ext ? load_raw(cols, wp.ts_col, e) : t);
+            const i64 sclk = max(c0, max(cm, ts[send_last_of(wp, e)]));
+            i64 clk = ext ? pmx : sclk;
+            if (send_clock) send_clock[r] = sclk;  // the flush clock of an externalTime row
             u32 pos = key_slot(kt, make_key(kp, cols, e));
             rec.raw[r] = (u32)e;
             rec.slot[r] = pos;
@@ -117,9 +126,9 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
 
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
-                       i64 pm0, SlRecords rec, u32* slot_cnt, int nblk) {
+                       i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock) {
     hipLaunchKernelGGL(k_sl_records, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, kp, kt, ap, blk_pass_pre,
-                       blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt);
+                       blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
 }
 
 // Sharded owner (sh_shard.cpp): the records arrive filtered and re-keyed, with the global clock of
@@ -1343,7 +1352,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
                                                    KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys,
                                                    u64* out_vals, unsigned char* out_nulls, i64* out_send,
                                                    i64* out_clock, const u32* __restrict__ rank_raw, i64 raw_base,
-                                                   i64* out_order) {
+                                                   i64* out_order, const i64* __restrict__ clock_by_rank) {
     // striped over the tile (round it: elements tile + it * kBlock + lane), so every row read and
     // every output column store of a wave is one contiguous run; the tile's first output row is
     // blk_pre (k_count_flags counts whole tiles, whatever the order inside)
@@ -1363,7 +1372,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
             out_nulls[(size_t)a * out_cap + r] = rows.nulls[(size_t)a * rows.cap + j];
         }
         out_send[r] = rows.send[j];
-        out_clock[r] = rows.clock[j];
+        out_clock[r] = clock_by_rank ? clock_by_rank[j] : rows.clock[j];
         if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
     }
 }
@@ -1404,9 +1413,10 @@ __global__ __launch_bounds__(kBlock) void k_flush_write(const i64* __restrict__ 
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                     unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw, i64 raw_base,
-                    i64* out_order) {
+                    i64* out_order, const i64* clock_by_rank) {
     hipLaunchKernelGGL(k_sl_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rows, n_aggs, kt, kp, out_cap,
-                       out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base, out_order);
+                       out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base, out_order,
+                       clock_by_rank);
 }
 
 void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb) {

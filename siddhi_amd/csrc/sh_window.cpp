@@ -153,8 +153,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (d->n_aggs < 1 || d->n_aggs > SH_MAX_AGGS)
         return sh_fail(SH_ERR_UNSUPPORTED, "GPU path runs aggregation queries (1..8 aggregators)");
     if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME &&
-        d->window != SH_WIN_EXT_TIME_BATCH)
-        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path needs a lengthBatch, timeBatch, time or externalTimeBatch window");
+        d->window != SH_WIN_EXT_TIME_BATCH && d->window != SH_WIN_EXT_TIME)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "GPU path needs a lengthBatch, timeBatch, time, externalTimeBatch or externalTime window");
+    if (d->window == SH_WIN_EXT_TIME &&
+        (d->ts_col < 0 || d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG))
+        return sh_fail(SH_ERR_INVALID, "externalTime timestamp must be a long attribute");
     if (d->window == SH_WIN_EXT_TIME_BATCH) {
         if (d->ts_col < 0 || d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG)
             return sh_fail(SH_ERR_INVALID, "externalTimeBatch timestamp must be a long attribute");
@@ -197,7 +201,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0;
-    if (d->window == SH_WIN_TIME) {
+    if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) {
         q->kind = 1;
         if ((rc = sliding_create(q))) { delete q; return rc; }
         *out = q;

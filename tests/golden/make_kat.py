@@ -106,6 +106,16 @@ case(name="externalTimeBatch_test05_edge", source=E + ":99-141", schema="cpu int
                                                         (85, 10020), (10000, 100000)])],
      expect=dict(in_count=2, flush_sizes=[1, 1], values=[[15.0, 3], [85.0, 3]]))
 
+# ---------------------------------------------------------------- externalTime (ExternalTimeWindowTestCase)
+# sliding over the `timestamp` attribute: 804341/804342 expire at 814341, 814341/814345 at 824341
+X = "ctest/query/window/ExternalTimeWindowTestCase.java"
+case(name="externalTime_test1", source=X + ":49-95", schema="timestamp long, ip string",
+     query=dict(window="externalTime", param=5000, ts_attr="timestamp", output="all"),
+     sends=[[[B + i, t, ip]] for i, (t, ip) in enumerate([(1366335804341, "192.10.1.3"), (1366335804342, "192.10.1.4"),
+                                                          (1366335814341, "192.10.1.5"), (1366335814345, "192.10.1.6"),
+                                                          (1366335824341, "192.10.1.7")])],
+     expect=dict(in_count=5, remove_count=4))
+
 # ---------------------------------------------------------------- partitioned timeBatch (WindowPartitionTestCase)
 case(name="partition5_timeBatch", source="ctest/query/partition/WindowPartitionTestCase.java:291-348",
      schema="symbol string, price double, volume int",

@@ -80,3 +80,23 @@ def test_ext_reference_kat_on_gpu(case):
     from siddhi_amd import runtime
     schema, sp, dic, flushes = kat_runner.run_query(case, runtime.GpuQuery)
     kat_runner.check_query(case, flushes, schema, dic)
+
+
+# ---- externalTime(et, T): sliding over the attribute (ExternalTimeWindowProcessor :126-161) ----
+def ext_time_spec(T, keys, filt=None, aggs=None):
+    return abi.QuerySpec(SCH, "externalTime", T, group_by=["k"], ts_attr="et", filter=filt,
+                         aggs=aggs or [("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys)
+
+
+@pytest.mark.parametrize("send_size", [1, 64])
+def test_external_time_sliding_matches_oracle(send_size):
+    """late events (the attribute goes backwards: the head blocks, nothing newer expires past it) and
+    chunked sends; one output chunk per send."""
+    ts, cols = stream(120_000, 500, 0xE8, late_ms=700)
+    both(ext_time_spec(1500, 512), split_batches(SCH, ts, cols, [40_000, 40_001], send_size), "externalTime")
+
+
+def test_external_time_filter_sum_and_dictionary_keys():
+    ts, cols = stream(90_000, 40, 0xE9, late_ms=3000, per_ms=5)
+    sp = ext_time_spec(800, 64, filt=(">", "v", 60.0), aggs=[("sum", "v"), ("max", "v"), ("count", None)])
+    both(sp, split_batches(SCH, ts, cols, [1, 30_000, 59_998], 3), "externalTime filter")
