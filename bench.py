@@ -78,23 +78,27 @@ def cpu_baseline(args):
                       f"{t_used:.1f} s single-thread in the C++ restatement (oracle/), not stock Siddhi (no JVM)"}
 
 
+# The PMC summary the roofline's `traffic` is read from: collected on exactly the default C2
+# configuration with the current kernels (scripts/profile_bench.sh + scripts/pmc_summary.py).
+TRAFFIC_SUMMARY = "profiles/r01_c2_v7_pmc.json"
+TRAFFIC_KERNEL = "shd::k_aggregate_own"
+
+
 def measured_traffic(args, sliced):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
-    (profiles/r*_c2_*_pmc.json: FETCH_SIZE x 2 + WRITE_SIZE per launch, gfx950-corrected by
-    scripts/pmc_summary.py), valid for the default single-GPU configuration it was collected on."""
-    import glob
+    """HBM bytes per launch of the dominant kernel and of the whole push from TRAFFIC_SUMMARY
+    (FETCH_SIZE x 2 + WRITE_SIZE per launch, gfx950-corrected), valid only for the default
+    single-GPU configuration it was collected on."""
     if sliced or args.batch != 1 << 25 or args.keys != 100_000 or args.key_type != "string" or args.send_size != 1:
-        return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c2_*_pmc.json")))
-    for f in reversed(files):
-        try:
-            ks = json.load(open(f))["kernels"]
-        except (OSError, ValueError, KeyError):
-            continue
-        for name, v in ks.items():
-            if name.startswith("shd::k_aggregate_own"):
-                return v["hbm_bytes"]
-    return None
+        return None, None
+    try:
+        ks = json.load(open(os.path.join(ROOT, TRAFFIC_SUMMARY)))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    main = next((v["hbm_bytes"] for n, v in ks.items() if n.startswith(TRAFFIC_KERNEL)), None)
+    # every kernel of the push (one launch each per push; k_scan_sum runs twice)
+    push = sum(v["hbm_bytes"] * v.get("launches", 1) for v in ks.values()) / max(
+        1, next((v.get("launches", 1) for n, v in ks.items() if n.startswith(TRAFFIC_KERNEL)), 1))
+    return main, push
 
 
 # ---- secondary single-GPU workloads (BASELINE.json configs[0], [2], [3]; externalTimeBatch) ---------
@@ -130,6 +134,7 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         spec = abi.QuerySpec(schema, "lengthBatch", 10000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
                              filter=(">", "price", 100), key_capacity=1000)
         send = 1000
+        B = args.batch = B - B % send  # slices are cut at send boundaries (sh_shard_pack checks it)
         # N > 1: one global stream, rank r holds slice r of every global push
         gen = lambda i: [torch.from_numpy(np.ascontiguousarray(c)).to(dev)
                          for c in synth.c1_stock((i * world + rank) * B, B)[1]]
@@ -325,7 +330,7 @@ def main():
     # roofline of the dominant kernel (k_aggregate): algorithmic bytes per launch / its HIP-event time
     n_launch = args.steps
     ach = (C2_BYTES_PER_EVENT * B * n_launch) / (kern_ms / 1e3) / 1e9 if kern_ms > 0 else 0.0
-    traffic = measured_traffic(args, sliced)
+    traffic, push_traffic = measured_traffic(args, sliced)
     result = {
         "metric": METRIC,
         "value": total_events / elapsed,
@@ -351,7 +356,13 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_aggregate_own", "achieved": ach, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms_per_step": kern_ms / args.steps,
-                     "bytes_per_event": C2_BYTES_PER_EVENT},
+                     "bytes_per_event": C2_BYTES_PER_EVENT,
+                     # the same algorithmic bytes over the whole step's wall time (every kernel, launch
+                     # gaps and host synchronisation included), and the PMC bytes of the whole push
+                     "end_to_end": {"achieved": C2_BYTES_PER_EVENT * B * world / (elapsed / args.steps) / 1e9,
+                                    "frac": C2_BYTES_PER_EVENT * B * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
+                                    "traffic_per_step": push_traffic,
+                                    "traffic_source": TRAFFIC_SUMMARY if traffic else None}},
     }
     if sliced:
         # rank 0's wall time per step in each phase of the sharded push (summaries all-gather,

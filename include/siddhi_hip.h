@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 3
+#define SH_ABI_VERSION 4
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -173,7 +173,14 @@ typedef struct {
  * (core/query/output/ratelimit/OutputRateLimiter.java:64-104). Rows are in the reference's
  * order (first-occurrence order of the group key inside the flush, QuerySelector.java:315-374);
  * a row carries the timestamp and aggregate values of the key's last qualifying event.
- * vals are raw 8-byte slots: int64 for LONG/INT outputs, IEEE double bits for DOUBLE/FLOAT. */
+ * vals are raw 8-byte slots: int64 for LONG/INT outputs, IEEE double bits for DOUBLE/FLOAT.
+ * rep is that last qualifying event itself — the event QuerySelector.processInBatchGroupBy keeps
+ * per key in its LinkedHashMap (QuerySelector.java:315-374) and whose non-aggregated select
+ * attributes (e.g. `volume` in `select symbol, sum(price), volume`) the output event carries — as
+ * its stream index: events are numbered from 0 in arrival order over every event ever pushed into
+ * the query (filtered-out ones included; for sh_shard_* the global stream index). The Java shim
+ * keeps the events of the open window and reads the row's other attributes from rep. NULL for
+ * aggregation tables. */
 typedef struct {
     int64_t n_flushes;
     int64_t n_rows;
@@ -187,6 +194,7 @@ typedef struct {
     const int64_t* keys;          /* [n_keys][n_rows] group-by values widened to int64     */
     const uint64_t* vals;         /* [n_vals][n_rows]                                      */
     const uint8_t* nulls;         /* [n_vals][n_rows] 1 = Java null                         */
+    const int64_t* rep;           /* [n_rows] stream index of the row's representative event */
 } sh_out;
 
 /* Rows written to one duration's aggregation table (core/aggregation/IncrementalExecutor.java:

@@ -108,6 +108,7 @@ enum EvType { CURRENT = 0, EXPIRED = 1, TIMER = 2, RESET = 3 };
 struct OEvent {
     int64_t ts = 0;
     int type = CURRENT;
+    int64_t seq = -1;  // stream index (arrival order over every pushed event): sh_out.rep
     std::array<int64_t, SH_MAX_COLS> raw{};  // column values, raw 8-byte form
 };
 
@@ -344,22 +345,24 @@ int64_t key_raw(const Schema& s, const OEvent& e, int c) {
 struct OutRow {
     int64_t ts; uint8_t expired; int64_t keys[SH_MAX_GROUP];
     uint64_t vals[SH_MAX_AGGS]; uint8_t nulls[SH_MAX_AGGS];
+    int64_t rep;  // stream index of the event the row was built from
 };
 struct OutBuf {
     std::vector<int64_t> flush_offsets{0};
     std::vector<int64_t> flush_clock;
     std::vector<OutRow> rows;
     // flattened views for sh_out
-    std::vector<int64_t> ts, keys; std::vector<uint8_t> expired, nulls; std::vector<uint64_t> vals;
+    std::vector<int64_t> ts, keys, rep; std::vector<uint8_t> expired, nulls; std::vector<uint64_t> vals;
+    bool with_rep = true;  // aggregation tables carry no representative event (sh_out.rep NULL)
     sh_out out{};
     void clear() { flush_offsets.assign(1, 0); flush_clock.clear(); rows.clear(); }
     void close_flush(int64_t clock) { flush_offsets.push_back((int64_t)rows.size()); flush_clock.push_back(clock); }
     const sh_out* view(int nk, int nv, const int* vtypes) {
         int64_t n = (int64_t)rows.size();
-        ts.resize(n); expired.resize(n); keys.assign((size_t)nk * n, 0);
+        ts.resize(n); expired.resize(n); keys.assign((size_t)nk * n, 0); rep.resize(n);
         vals.assign((size_t)nv * n, 0); nulls.assign((size_t)nv * n, 0);
         for (int64_t r = 0; r < n; r++) {
-            ts[r] = rows[r].ts; expired[r] = rows[r].expired;
+            ts[r] = rows[r].ts; expired[r] = rows[r].expired; rep[r] = rows[r].rep;
             for (int k = 0; k < nk; k++) keys[k * n + r] = rows[r].keys[k];
             for (int v = 0; v < nv; v++) { vals[v * n + r] = rows[r].vals[v]; nulls[v * n + r] = rows[r].nulls[v]; }
         }
@@ -369,6 +372,7 @@ struct OutBuf {
         out.flush_offsets = flush_offsets.data(); out.flush_clock = flush_clock.data();
         out.ts = ts.data(); out.expired = expired.data(); out.keys = keys.data();
         out.vals = vals.data(); out.nulls = nulls.data();
+        out.rep = with_rep ? rep.data() : nullptr;
         return &out;
     }
 };
@@ -393,6 +397,8 @@ struct PartitionState {
     int64_t ext_end = -1, ext_start = 0, ext_last = 0;
     Chunk ext_current, ext_expired;
     bool ext_has_reset = false; OEvent ext_reset;
+    size_t index = 0;  // position in the scheduler's iteration order
+    int64_t key = 0;
 };
 
 struct Query {
@@ -408,8 +414,12 @@ struct Query {
     bool clock_set = false;
     // TimeBatchWindowProcessor.nextEmitTime is a processor field shared by all partitions (:128)
     int64_t next_emit_time = -1;
-    std::map<int64_t, std::unique_ptr<PartitionState>> parts;  // partition flow id -> state
+    int64_t seq_base = 0;  // stream index of the current push's first event
+    std::unordered_map<int64_t, std::unique_ptr<PartitionState>> parts;  // partition flow id -> state
     std::vector<int64_t> part_order;  // scheduler iteration order (insertion order)
+    // partitions whose notify queue is non-empty, by insertion index: Scheduler.onTimeChange only
+    // ever fires states with a due time (:75-87), so a scan over these equals the scan over all
+    std::map<size_t, int64_t> armed;
     OutBuf out;
 
     PartitionState& part(int64_t key) {
@@ -418,6 +428,8 @@ struct Query {
         auto ps = std::unique_ptr<PartitionState>(new PartitionState());
         ps->agg_states.resize(aggs.size());
         if (d.window == SH_WIN_EXT_TIME_BATCH && d.has_start_time == 1) ps->ext_start = d.start_time;
+        ps->index = part_order.size();
+        ps->key = key;
         PartitionState& r = *ps;
         parts.emplace(key, std::move(ps));
         part_order.push_back(key);
@@ -425,7 +437,10 @@ struct Query {
     }
 
     // Scheduler.notifyAt (core/util/Scheduler.java:107-121)
-    void notify_at(PartitionState& ps, int64_t t) { ps.notify_queue.push_back(t); }
+    void notify_at(PartitionState& ps, int64_t t) {
+        ps.notify_queue.push_back(t);
+        armed.emplace(ps.index, ps.key);
+    }
 
     // ---- selector: QuerySelector.processInBatchGroupBy (core/query/selector/QuerySelector.java:315-374)
     void selector(PartitionState& ps, const Chunk& chunk) {
@@ -436,7 +451,7 @@ struct Query {
                 if (ev.type != CURRENT && ev.type != EXPIRED) continue;
                 bool q = (ev.type == CURRENT && d.current_on) || (ev.type == EXPIRED && d.expired_on);
                 if (!q) continue;
-                OutRow row{}; row.ts = ev.ts; row.expired = ev.type == EXPIRED;
+                OutRow row{}; row.ts = ev.ts; row.expired = ev.type == EXPIRED; row.rep = ev.seq;
                 out.rows.push_back(row); any = true;
             }
             if (any) out.close_flush(clock);
@@ -449,7 +464,7 @@ struct Query {
                 GKey key;
                 for (int g = 0; g < d.n_group_by; g++) key.k[g] = key_raw(schema, ev, d.group_by[g]);
                 OutRow row{};
-                row.ts = ev.ts; row.expired = ev.type == EXPIRED;
+                row.ts = ev.ts; row.expired = ev.type == EXPIRED; row.rep = ev.seq;
                 for (int g = 0; g < d.n_group_by; g++) row.keys[g] = key.k[g];
                 for (size_t a = 0; a < aggs.size(); a++) {
                     auto& states = ps.agg_states[a];
@@ -703,9 +718,9 @@ struct Query {
     // TreeMultimap<Long, SchedulerState> with compareTo()==0: one state per distinct due time.
     void on_time_change() {
         std::map<int64_t, int64_t> sorted;  // due time -> partition key (first inserted wins)
-        for (int64_t pk : part_order) {
-            PartitionState& ps = *parts[pk];
-            if (!ps.notify_queue.empty() && ps.notify_queue.front() <= clock) sorted.emplace(ps.notify_queue.front(), pk);
+        for (auto& ak : armed) {
+            PartitionState& ps = *parts[ak.second];
+            if (!ps.notify_queue.empty() && ps.notify_queue.front() <= clock) sorted.emplace(ps.notify_queue.front(), ak.second);
         }
         for (auto& kv : sorted) {
             PartitionState& ps = *parts[kv.second];
@@ -716,6 +731,7 @@ struct Query {
                 Chunk c{timer};
                 window(ps, c);  // EntryValveProcessor -> window
             }
+            if (ps.notify_queue.empty()) armed.erase(ps.index);
         }
     }
 
@@ -739,6 +755,7 @@ struct Query {
             OEvent e;
             for (int64_t i = lo; i < hi; i++) {
                 load_event(schema, b, i, e);
+                e.seq = seq_base + i;
                 if (eval_filter(schema, filter, e)) c.push_back(e);
             }
             if (!c.empty()) window(part(0), c);
@@ -753,6 +770,7 @@ struct Query {
                 int64_t j = i;
                 while (j < hi) {
                     OEvent f; load_event(schema, b, j, f);
+                    f.seq = seq_base + j;
                     if (key_raw(schema, f, d.partition_col) != key) break;
                     if (eval_filter(schema, filter, f)) c.push_back(f);
                     j++;
@@ -1099,6 +1117,7 @@ int or_push(void* h, const sh_batch* b, const sh_out** out) {
     q->out.clear();
     int64_t step = b->send_size > 0 ? b->send_size : b->n;
     for (int64_t lo = 0; lo < b->n; lo += step) q->send(b, lo, std::min(b->n, lo + step));
+    q->seq_base += b->n;
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }
@@ -1170,6 +1189,7 @@ int or_aggregation_table(void* h, int32_t dur, const sh_out** out) {
     if (dur < 0 || dur > SH_DUR_YEARS) { g_err = "bad duration"; return SH_ERR_INVALID; }
     OutBuf& ob = a->views[dur];
     ob.clear();
+    ob.with_rep = false;
     for (const OutRow& r : a->tables[dur]) ob.rows.push_back(r);
     if (!ob.rows.empty()) ob.close_flush(a->clock);
     *out = ob.view(1 + a->d.n_group_by, (int)a->bases.size(), a->vtypes);

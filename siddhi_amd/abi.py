@@ -74,7 +74,7 @@ class Out(C.Structure):
                 ("flush_offsets", C.POINTER(C.c_int64)), ("flush_clock", C.POINTER(C.c_int64)),
                 ("ts", C.POINTER(C.c_int64)), ("expired", C.POINTER(C.c_uint8)),
                 ("keys", C.POINTER(C.c_int64)), ("vals", C.POINTER(C.c_uint64)),
-                ("nulls", C.POINTER(C.c_uint8))]
+                ("nulls", C.POINTER(C.c_uint8)), ("rep", C.POINTER(C.c_int64))]
 
 
 class SliceSummary(C.Structure):
@@ -285,6 +285,7 @@ class HostBatch:
 class Flush:
     clock: int
     rows: List[tuple]   # (ts, expired, keys tuple, values tuple with None for null)
+    reps: List[int] = field(default_factory=list)  # stream index of each row's representative event
 
 
 def decode_out(out_ptr) -> List[Flush]:
@@ -304,9 +305,11 @@ def decode_out(out_ptr) -> List[Flush]:
             if o.n_vals else np.zeros((0, n), np.uint64)
         nulls = np.ctypeslib.as_array(o.nulls, shape=(max(1, o.n_vals) * n,)).copy().reshape(max(1, o.n_vals), n) \
             if o.n_vals else np.zeros((0, n), np.uint8)
+        rep = np.ctypeslib.as_array(o.rep, shape=(n,)).copy() if o.rep else np.full(n, -1, np.int64)
     vt = [o.val_types[i] for i in range(o.n_vals)]
     for f in range(o.n_flushes):
         rows = []
+        reps = [int(rep[r]) for r in range(int(offs[f]), int(offs[f + 1]))]
         for r in range(int(offs[f]), int(offs[f + 1])):
             vs = []
             for v in range(o.n_vals):
@@ -317,7 +320,7 @@ def decode_out(out_ptr) -> List[Flush]:
                 else:
                     vs.append(int(np.array([vals[v, r]], dtype=np.uint64).view(np.int64)[0]))
             rows.append((int(ts[r]), int(exp[r]), tuple(int(keys[k, r]) for k in range(o.n_keys)), tuple(vs)))
-        flushes.append(Flush(int(clocks[f]), rows))
+        flushes.append(Flush(int(clocks[f]), rows, reps))
     return flushes
 
 
@@ -341,10 +344,11 @@ def out_arrays(out_ptr) -> Dict[str, np.ndarray]:
             if o.n_vals else np.zeros((0, n), np.uint64)
         res["nulls"] = np.ctypeslib.as_array(o.nulls, shape=(o.n_vals * n,)).copy().reshape(o.n_vals, n) \
             if o.n_vals else np.zeros((0, n), np.uint8)
+        res["rep"] = np.ctypeslib.as_array(o.rep, shape=(n,)).copy() if o.rep else np.full(n, -1, np.int64)
     else:
         res.update(ts=np.zeros(0, np.int64), expired=np.zeros(0, np.uint8),
                    keys=np.zeros((o.n_keys, 0), np.int64), vals=np.zeros((o.n_vals, 0), np.uint64),
-                   nulls=np.zeros((o.n_vals, 0), np.uint8))
+                   nulls=np.zeros((o.n_vals, 0), np.uint8), rep=np.zeros(0, np.int64))
     return res
 
 
@@ -359,7 +363,7 @@ def concat_arrays(parts: List[Dict[str, np.ndarray]]) -> Dict[str, np.ndarray]:
         base += len(p["ts"])
     res = {"flush_offsets": np.concatenate(offs), "flush_clock": np.concatenate([p["flush_clock"] for p in parts]),
            "val_types": parts[0]["val_types"]}
-    for k in ("ts", "expired"):
+    for k in ("ts", "expired", "rep"):
         res[k] = np.concatenate([p[k] for p in parts])
     for k in ("keys", "vals", "nulls"):
         res[k] = np.concatenate([p[k] for p in parts], axis=1)

@@ -193,9 +193,7 @@ static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
                                       t.n * 8, hipMemcpyDeviceToDevice, s));
         }
         HIPCHK(hipStreamSynchronize(s));
-        t.bucket.release(); t.key.release(); t.vals.release();
-        t.bucket = b2; t.key = k2; t.vals = v2;
-        b2.p = k2.p = v2.p = nullptr;
+        t.bucket = std::move(b2); t.key = std::move(k2); t.vals = std::move(v2);
         t.cap = ncap;
     }
     HIPCHK(hipMemcpyAsync(t.bucket.as<int64_t>() + t.n, rb.bucket, rb.n * 8, hipMemcpyDeviceToDevice, s));
@@ -444,7 +442,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     RCHK(a->minmax.reserve(16, false));
     HIPCHK(hipHostMalloc((void**)&a->h_minmax, 16, hipHostMallocDefault));
     RCHK(a->root_key_col.reserve(8 << 20, false));
-    HIPCHK(hipMemset(a->root_key_col.p, 0, 8 << 20));
+    HIPCHK(hipMemsetAsync(a->root_key_col.p, 0, 8 << 20, ctx->stream));
     // upper durations
     for (int dur = d->min_duration + 1; dur <= d->max_duration; dur++) {
         a->levels.emplace_back();
@@ -456,10 +454,10 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         RCHK(L.has.reserve((size_t)a->nb * L.nslots, false));
         RCHK(L.tag.reserve(L.nslots * 4, false));
         RCHK(L.first_seq.reserve(L.nslots * 4, false));
-        HIPCHK(hipMemset(L.first_seq.p, 0xFF, L.nslots * 4));
+        HIPCHK(hipMemsetAsync(L.first_seq.p, 0xFF, L.nslots * 4, ctx->stream));
         RCHK(L.dup.reserve(64, false));
-        HIPCHK(hipMemset(L.has.p, 0, (size_t)a->nb * L.nslots));
-        HIPCHK(hipMemset(L.tag.p, 0, L.nslots * 4));
+        HIPCHK(hipMemsetAsync(L.has.p, 0, (size_t)a->nb * L.nslots, ctx->stream));
+        HIPCHK(hipMemsetAsync(L.tag.p, 0, L.nslots * 4, ctx->stream));
         HIPCHK(hipHostMalloc((void**)&L.dup_host, 64, hipHostMallocDefault));
     }
     *out = a;
@@ -467,6 +465,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
 }
 
 extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, sh_aggregation** out) {
+    StreamScope _ss(ctx ? ctx->stream : nullptr);
     return agg_create(ctx, d, 0, 1, nullptr, out);
 }
 
@@ -476,6 +475,7 @@ extern "C" int sh_aggregation_create(sh_ctx* ctx, const sh_aggregation_desc* d, 
 // together hold exactly the single-stream tables' rows.
 extern "C" int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, int32_t world,
                                            sh_shard** shard, sh_aggregation** out) {
+    StreamScope _ss(ctx ? ctx->stream : nullptr);
     if (!shard) return sh_fail(SH_ERR_INVALID, "sh_aggregation_shard_create: NULL argument");
     if (d && d->n_group_by != 1) return sh_fail(SH_ERR_UNSUPPORTED, "sharded aggregations need one group-by key");
     return agg_create(ctx, d, rank, world, shard, out);
@@ -497,6 +497,7 @@ static void agg_free(sh_aggregation* a) {
 }
 
 extern "C" int sh_aggregation_destroy(sh_aggregation* a) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a) return SH_OK;
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation is released by sh_shard_destroy");
     (void)hipStreamSynchronize(a->ctx->stream);
@@ -552,12 +553,14 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
 }
 
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
     return agg_push(a, b, true);
 }
 
 extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push_device: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
     return agg_push(a, b, false);
@@ -566,6 +569,7 @@ extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) 
 
 
 extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation advances through sh_shard_advance_time");
     const sh_out* o = nullptr;
@@ -575,6 +579,7 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
 }
 
 extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out** out) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_table: NULL argument");
     if (dur < a->d.min_duration || dur > a->d.max_duration) return sh_fail(SH_ERR_INVALID, "duration not aggregated");
     TableBuf& t = a->tables[dur];
@@ -600,6 +605,8 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
         o.flush_clock.push_back(a->root->clock);
     }
     t.n = 0;
-    *out = o.view(nk, a->nb, a->btypes);
+    o.view(nk, a->nb, a->btypes);
+    o.out.rep = nullptr;  // table rows have no representative event
+    *out = &o.out;
     return SH_OK;
 }

@@ -104,7 +104,7 @@ struct WinParams {
     const int* wcol;   // sharded owner: window of every event given (W_base + wcol[e]); else null
     i64 W_base;
     int want_first_clk;  // sharded summary: report PushInfo.first_clk
-    int pad2;
+    int pcol1;           // partitioned queries: report PushInfo.first_key from column pcol1 - 1 (0: none)
     // externalTimeBatch: window of an event = bucket (from the start time E0) of the running max of
     // the ts_col attribute over the events reaching the window; xm0 = that max before the push
     int ts_col, start_col;
@@ -123,6 +123,7 @@ struct PushInfo {
     i64 max_xm;        // externalTimeBatch: max of the timestamp attribute over passing events
     int err;           // externalTimeBatch: first event before its start time
     int pad;
+    i64 first_key;     // column WinParams.pcol1 - 1 of the first passing event (partitioned queries, R12)
 };
 
 // A window boundary inside the push: first combined index of a new window.
@@ -170,10 +171,10 @@ void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i
                  u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
                  i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
                  u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
-                 i64* out_order);
+                 i64* out_order, i64 seq_base, i64* out_rep);
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
-                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx);
+                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);
 // multisplit (partitioned aggregation, P > 1)
 void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
                      i64* counts, int nblk);

@@ -136,6 +136,7 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
         info->first_clk = INT64_MIN;
         info->max_xm = tot_x;
         info->err = 0;
+        info->first_key = (wp.pcol1 > 0 && tot_mn != INT64_MAX) ? load_raw(cols, wp.pcol1 - 1, tot_mn) : 0;
         // externalTimeBatch initTiming (:313-334): the start is the constant, the start attribute or
         // the timestamp attribute of the first event reaching the window
         if (wp.kind == SH_WIN_EXT_TIME_BATCH && !wp.e0_valid && tot_mn != INT64_MAX) {
@@ -727,14 +728,21 @@ __global__ __launch_bounds__(kBlock) void k_emit_gather(const u32* __restrict__ 
                                                        const i64* __restrict__ ts, i64 out_cap, i64* out_ts,
                                                        i64* out_keys, u64* out_vals, unsigned char* out_nulls,
                                                        const u64* __restrict__ pend_gidx,
-                                                       const u64* __restrict__ new_gidx, i64* out_order) {
+                                                       const u64* __restrict__ new_gidx, i64* out_order,
+                                                       i64 seq_base, i64* out_rep) {
     i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (o >= n_rows) return;
     u32 row = perm[o];
     RowTmp t = rows[row];
     u64 k = slot_key(kt, t.pos);
     out_ts[o] = t.last < n_pend ? pend_ts[t.last] : ts[t.last - n_pend];
-    if (out_order) out_order[o] = (i64)(t.first < n_pend ? pend_gidx[t.first] : new_gidx[t.first - n_pend]);
+    // stream index of an event of the combined (queued + new) sequence
+    auto sidx = [&](u32 c) -> i64 {
+        if (c < n_pend) return (i64)pend_gidx[c];
+        return new_gidx ? (i64)new_gidx[c - n_pend] : seq_base + (i64)(c - n_pend);
+    };
+    if (out_order) out_order[o] = sidx(t.first);
+    out_rep[o] = sidx(t.last);
     unpack_key(kp, k, out_keys + o, out_cap);
     for (int a = 0; a < n_aggs; a++) {
         out_vals[(size_t)a * out_cap + o] = row_vals[(size_t)row * n_aggs + a];
@@ -746,12 +754,12 @@ void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i
                  u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
                  i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
                  u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
-                 i64* out_order) {
+                 i64* out_order, i64 seq_base, i64* out_rep) {
     hipLaunchKernelGGL(k_emit_perm, dim3(nblk), dim3(kBlock), 0, s, flags, rowref, n, blk_pre, perm);
     unsigned g = (unsigned)((n_rows + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_emit_gather, dim3(g), dim3(kBlock), 0, s, perm, n_rows, rows, row_vals, n_aggs, kt, kp,
                        n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls, pend_gidx, new_gidx,
-                       out_order);
+                       out_order, seq_base, out_rep);
 }
 
 // ================================================================================================
@@ -763,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
                                                            i64 N, i64 pcb_lo, i64 dst_base, const i64* blk_pass_pre,
                                                            int blk0, u32* pend_pos, i64* pend_ts, u64* pend_vals,
                                                            i64 pend_cap, const u64* __restrict__ new_gidx,
-                                                           u64* pend_gidx) {
+                                                           u64* pend_gidx, i64 seq_base) {
     int blk = blk0 + blockIdx.x;
     i64 base = (i64)blk * kTile + (i64)threadIdx.x * kItems;
     u32 pos[kItems];
@@ -784,7 +792,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
                 pend_pos[d] = pos[i];
                 pend_ts[d] = ts[e];
                 for (int j = 0; j < ap.n_vcols; j++) pend_vals[(size_t)j * pend_cap + d] = (u64)load_raw(cols, ap.vcol_src[j], e);
-                if (pend_gidx) pend_gidx[d] = new_gidx[e];
+                pend_gidx[d] = new_gidx ? new_gidx[e] : (u64)(seq_base + e);
             }
             pcb++;
         }
@@ -793,13 +801,13 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
 
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
-                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx) {
+                            u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base) {
     if (e_lo >= N) return;
     int blk0 = (int)(e_lo / kTile);
     int blk1 = (int)((N + kTile - 1) / kTile);
     hipLaunchKernelGGL(k_compact_pending, dim3(blk1 - blk0), dim3(kBlock), 0, s, ts, cols, new_pos, ap, e_lo, N,
                        pcb_lo, base, blk_pass_pre, blk0, pend_pos, pend_ts, pend_vals, pend_cap, new_gidx,
-                       pend_gidx);
+                       pend_gidx, seq_base);
 }
 
 }  // namespace shd

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "sh_agg.h"
 #include "sh_internal.h"
 #include "sh_runtime.h"
 
@@ -30,19 +31,26 @@ int sh_fail(int code, const std::string& msg) {
 // ---------------------------------------------------------------------------------------------
 // device buffer helpers
 // ---------------------------------------------------------------------------------------------
+thread_local hipStream_t g_stream = nullptr;
+
+// Stream-ordered growth on the calling context's stream: the copy of the kept bytes and the free of
+// the old block are queued behind the kernels that still use it. Outside any API scope (g_stream
+// null) the old block is released after a wait for the device.
 int DevBuf::reserve(size_t n, bool keep) {
     if (n <= cap) return SH_OK;
     size_t ncap = std::max(n, cap + cap / 2);
     void* np = nullptr;
-    hipError_t e = hipMalloc(&np, ncap);
-    if (e != hipSuccess) return sh_fail(SH_ERR_OOM, "hipMalloc failed: " + std::string(hipGetErrorString(e)));
+    hipError_t e = g_stream ? hipMallocAsync(&np, ncap, g_stream) : hipMalloc(&np, ncap);
+    if (e != hipSuccess) return sh_fail(SH_ERR_OOM, "device allocation failed: " + std::string(hipGetErrorString(e)));
     if (p) {
         if (keep && used) {
-            e = hipMemcpy(np, p, used, hipMemcpyDeviceToDevice);
-            if (e != hipSuccess) return sh_fail(SH_ERR_DEVICE, "hipMemcpy (grow) failed");
+            e = hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, g_stream);
+            if (e != hipSuccess) {
+                (void)(g_stream ? hipFreeAsync(np, g_stream) : hipFree(np));
+                return sh_fail(SH_ERR_DEVICE, "device copy (grow) failed");
+            }
         }
-        (void)hipDeviceSynchronize();
-        (void)hipFree(p);
+        release();
     }
     p = np;
     cap = ncap;
@@ -50,9 +58,34 @@ int DevBuf::reserve(size_t n, bool keep) {
 }
 
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+        if (g_stream) {
+            (void)hipFreeAsync(p, g_stream);
+        } else {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
+    }
     p = nullptr;
     cap = used = 0;
+}
+
+int PinnedBuf::reserve(size_t n) {
+    if (n <= cap) return SH_OK;
+    release();
+    size_t ncap = std::max<size_t>(n, 4096);
+    if (hipHostMalloc(&p, ncap, hipHostMallocDefault) != hipSuccess) {
+        p = nullptr;
+        return sh_fail(SH_ERR_OOM, "pinned host allocation failed");
+    }
+    cap = ncap;
+    return SH_OK;
+}
+
+void PinnedBuf::release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -231,7 +264,7 @@ int KeyTableHost::init_dense(int64_t capacity, uint32_t mul, uint32_t add) {
     if (rc) return rc;
     rc = ctrl.reserve(64, false);
     if (rc) return rc;
-    if (hipMemset(ctrl.p, 0, 64) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table init failed");
+    if (hipMemsetAsync(ctrl.p, 0, 64, g_stream) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table init failed");
     return SH_OK;
 }
 
@@ -243,10 +276,10 @@ int KeyTableHost::init_size(size_t ts) {
     if (rc) return rc;
     rc = ctrl.reserve(64, false);
     if (rc) return rc;
-    std::vector<u64> init(ts, kEmptyKey);
-    if (hipMemcpy(keys.p, init.data(), ts * 8, hipMemcpyHostToDevice) != hipSuccess)
+    // EMPTY sentinels written on the device, in the calling context's stream order
+    launch_fill_i64(g_stream, (int64_t*)keys.p, (int64_t)ts, (int64_t)kEmptyKey);
+    if (hipGetLastError() != hipSuccess || hipMemsetAsync(ctrl.p, 0, 64, g_stream) != hipSuccess)
         return sh_fail(SH_ERR_DEVICE, "key table init failed");
-    if (hipMemset(ctrl.p, 0, 64) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table init failed");
     return SH_OK;
 }
 

@@ -17,12 +17,52 @@ struct sh_ctx {
 
 int sh_fail(int code, const std::string& msg);
 
-// Growable device allocation. `used` is the byte count that must survive a grow (keep=true).
+// The stream of the context whose API call is running on this thread. Device buffers grow and are
+// freed in that stream's order (hipMallocAsync / hipFreeAsync), so a growth never waits on other
+// streams and never frees memory a queued kernel still reads. Every extern "C" entry point that
+// touches a context opens a StreamScope.
+extern thread_local hipStream_t g_stream;
+struct StreamScope {
+    hipStream_t prev;
+    explicit StreamScope(hipStream_t s) : prev(g_stream) { g_stream = s; }
+    ~StreamScope() { g_stream = prev; }
+    StreamScope(const StreamScope&) = delete;
+    StreamScope& operator=(const StreamScope&) = delete;
+};
+
+// Growable device allocation (move-only; released on destruction, so early error returns do not
+// leak). `used` is the byte count that must survive a grow (keep=true).
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     size_t used = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap), used(o.used) { o.p = nullptr; o.cap = o.used = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p; cap = o.cap; used = o.used;
+            o.p = nullptr; o.cap = o.used = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { release(); }
     int reserve(size_t n, bool keep);
+    void release();
+    template <typename T> T* as() const { return (T*)p; }
+};
+
+// Pinned host allocation (hipHostMalloc), move-only, freed on destruction.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { release(); }
+    int reserve(size_t n);
     void release();
     template <typename T> T* as() const { return (T*)p; }
 };
@@ -44,14 +84,14 @@ struct KeyTableHost {
 
 // Host copy of a push's output (sh_out points into these vectors).
 struct OutHost {
-    std::vector<int64_t> flush_offsets{0}, flush_clock, ts, keys;
+    std::vector<int64_t> flush_offsets{0}, flush_clock, ts, keys, rep;
     std::vector<uint8_t> expired, nulls;
     std::vector<uint64_t> vals;
     sh_out out{};
     void reset() {
         flush_offsets.assign(1, 0);
         flush_clock.clear();
-        ts.clear(); keys.clear(); expired.clear(); nulls.clear(); vals.clear();
+        ts.clear(); keys.clear(); expired.clear(); nulls.clear(); vals.clear(); rep.clear();
     }
     const sh_out* view(int n_keys, int n_vals, const int32_t* vtypes) {
         out = sh_out{};
@@ -67,6 +107,8 @@ struct OutHost {
         out.keys = keys.data();
         out.vals = vals.data();
         out.nulls = nulls.data();
+        rep.resize(ts.size(), -1);
+        out.rep = rep.data();
         return &out;
     }
 };
@@ -114,13 +156,15 @@ struct sh_query {
     int64_t W_open = 0;
     int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
     int64_t n_pend = 0, pend_cap = 0;
+    int64_t seq = 0;  // stream index of the next event pushed (sh_out.rep numbering)
     DevBuf pend_pos, pend_ts, pend_vals;
     // scratch
     DevBuf blk_pass, blk_tl, blk_first, blk_xm, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
-        out_ts, out_keys, out_vals, out_nulls, out_expired, blk_cnt;
+        out_ts, out_keys, out_vals, out_nulls, out_expired, out_rep, blk_cnt;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
     DevBuf new_pos, perm, seg_off;  // key slot per event of the push (kNoPos = filtered out); output permutation
     PushInfo* h_info = nullptr;
+    PinnedBuf h_up;  // pinned staging of small host->device uploads (segment lists)
     StagedBatch staged;
     OutHost out;
     sh_out dev_out{};
@@ -141,7 +185,7 @@ struct sh_query {
     const shd::u64* given_gidx = nullptr;
     int64_t given_W_base = 0, given_W_end = 0;
     std::vector<sh_bound> gbounds;  // this push's global window starts, sorted by gidx
-    DevBuf pend_gidx, out_order;
+    DevBuf pend_gidx, out_order;  // pend_gidx: stream index of every queued event (all modes)
     std::vector<int64_t> order_host;
 };
 

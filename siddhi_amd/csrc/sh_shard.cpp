@@ -67,7 +67,7 @@ struct sh_shard {
     int64_t cur_W_base = 0, cur_W_end = 0;
     int64_t cur_seq = 0;                  // global index of the push's first event
     std::vector<int64_t> cur_off;         // stream offset of every slice in the push
-    std::vector<int64_t> h_bg, h_bw;      // host copies of the window starts being uploaded
+    PinnedBuf h_bgw;                      // pinned copies of the window starts being uploaded
     // ingest scratch
     int64_t slice_n = -1;
     DevBuf blk_pass, blk_tl, blk_first, info, code, counts, tmp, part_off, bounds;
@@ -181,6 +181,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
 }
 
 extern "C" int sh_shard_create(sh_ctx* ctx, const sh_query_desc* d, int32_t rank, int32_t world, sh_shard** out) {
+    StreamScope _ss(ctx ? ctx->stream : nullptr);
     return shard_create(ctx, d, nullptr, rank, world, out);
 }
 
@@ -196,6 +197,7 @@ int shard_create_root(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, in
 void shard_attach_aggregation(sh_shard* s, sh_aggregation* a) { s->agg = a; }
 
 extern "C" int sh_shard_destroy(sh_shard* s) {
+    StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s) return SH_OK;
     (void)hipStreamSynchronize(s->ctx->stream);
     if (s->agg) agg_release_sharded(s->agg);
@@ -225,6 +227,7 @@ static ColSet colset(const sh_shard* s, const sh_batch* b) {
 
 // Phase 1: pass count, send clocks and the first passing send of the slice (k_blockagg + k_scan_blocks).
 extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summary* out) {
+    StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_summarize: NULL argument");
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative slice size");
     if (b->n > 0 && (b->send_size < 1 || !b->ts))
@@ -262,27 +265,18 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     wp.N = b->n;
     wp.send_size = b->send_size;
     wp.want_first_clk = 1;
+    wp.pcol1 = (s->partitioned && !s->p0_known) ? s->d.partition_col + 1 : 0;
     launch_scan_blocks(st, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(), nblk, b->ts,
-                       wp, s->info.as<PushInfo>());
+                       wp, s->info.as<PushInfo>(), nullptr, colset(s, b));
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     out->n_pass = s->h_info->total_pass;
     out->max_tl = s->h_info->max_tl;
     out->first_clock = s->h_info->first_pass == INT64_MAX ? INT64_MIN : s->h_info->first_clk;
-    out->first_key = 0;
-    if (s->partitioned && !s->p0_known && s->h_info->first_pass != INT64_MAX) {
-        // partition key of the slice's first passing event (PartitionStreamReceiver :176-272)
-        const int pc = s->d.partition_col;
-        const int64_t e = s->h_info->first_pass;
-        if (s->d.col_types[pc] == SH_T_LONG) {
-            HIPCHK(hipMemcpy(&out->first_key, (const char*)b->cols[pc] + e * 8, 8, hipMemcpyDeviceToHost));
-        } else {
-            int32_t k32 = 0;
-            HIPCHK(hipMemcpy(&k32, (const char*)b->cols[pc] + e * 4, 4, hipMemcpyDeviceToHost));
-            out->first_key = k32;
-        }
-    }
+    // partition key of the slice's first passing event (PartitionStreamReceiver :176-272), read by
+    // k_scan_blocks in the same pass
+    out->first_key = (wp.pcol1 > 0 && s->h_info->first_pass != INT64_MAX) ? s->h_info->first_key : 0;
     return SH_OK;
 }
 
@@ -361,10 +355,18 @@ static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch
 // Phase 2: global clock / nextEmitTime / windows from the G summaries, then the per-owner records.
 extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_batch* b, void* send_buf,
                              int64_t send_cap, int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds) {
+    StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !all || !b || !send_bytes || !bounds || !n_bounds)
         return sh_fail(SH_ERR_INVALID, "sh_shard_pack: NULL argument");
     if (s->slice_n != b->n || all[s->rank].n != b->n)
         return sh_fail(SH_ERR_STATE, "sh_shard_pack: call sh_shard_summarize on the same slice first");
+    // slices are cut at send boundaries: every slice but the last holds whole sends, otherwise one
+    // send's events would get different clocks / send numbers on two ranks (InputHandler.send :85-96)
+    if (b->send_size > 0)
+        for (int r = 0; r + 1 < s->world; r++)
+            if (all[r].n % b->send_size != 0)
+                return sh_fail(SH_ERR_INVALID, "sh_shard_pack: slice " + std::to_string(r) +
+                                                   " is not a whole number of sends (cut slices at send boundaries)");
     const int G = s->world;
     const int64_t RB = 4 * (int64_t)s->rec_words;
     if (b->n > 0 && (!send_buf || send_cap < b->n * RB))
@@ -552,6 +554,7 @@ static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* rec
 // concatenated in rank order and every source run is in stream order).
 extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, const sh_bound* all_bounds,
                                 int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order) {
+    StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !recv_bytes || !out || (n_all_bounds > 0 && !all_bounds))
         return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
     if (!s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
@@ -594,16 +597,15 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     }
     // the global window starts, sorted by stream index, for the per-record window lookup
     const int nb = (int)q->gbounds.size();
-    std::vector<int64_t>& bg = s->h_bg;
-    std::vector<int64_t>& bw = s->h_bw;
-    bg.resize(nb);
-    bw.resize(nb);
+    RCHK(s->h_bgw.reserve((size_t)std::max(1, nb) * 16));
+    int64_t* bg = s->h_bgw.as<int64_t>();
+    int64_t* bw = bg + std::max(1, nb);
     for (int i = 0; i < nb; i++) { bg[i] = q->gbounds[i].gidx; bw[i] = q->gbounds[i].W; }
     RCHK(s->u_bg.reserve(std::max(1, nb) * 8, false));
     RCHK(s->u_bw.reserve(std::max(1, nb) * 8, false));
     if (nb) {
-        HIPCHK(hipMemcpyAsync(s->u_bg.p, bg.data(), nb * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(s->u_bw.p, bw.data(), nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->u_bg.p, bg, nb * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->u_bw.p, bw, nb * 8, hipMemcpyHostToDevice, st));
     }
     ShardSrc src{};
     src.G = s->world;
@@ -635,6 +637,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
 
 extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out,
                                      const int64_t** order) {
+    StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_advance_time: NULL argument");
     if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");
     sh_query* q = s->owner;

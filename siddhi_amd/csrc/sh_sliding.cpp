@@ -35,9 +35,10 @@ struct SlidingImpl {
     DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
     // per push scratch
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
-        tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
-        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, flush_off, flush_clock;
+        tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_rep, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
+        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock;
     SlInfo* h_info = nullptr;
+    PinnedBuf h_up;  // pinned staging of small host->device uploads
     sh_out dev_out{};
 };
 
@@ -63,12 +64,14 @@ static SlState state_of(SlidingImpl* s) {
 
 static int alloc_zero(DevBuf& b, size_t bytes, int fill = 0) {
     RCHK(b.reserve(std::max<size_t>(bytes, 8), false));
-    if (hipMemset(b.p, fill, std::max<size_t>(bytes, 8)) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "memset failed");
+    if (hipMemsetAsync(b.p, fill, std::max<size_t>(bytes, 8), g_stream) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "memset failed");
     return SH_OK;
 }
 
 // (re)size the per-key rings and deques to capacity rc (power of two), keeping their contents
-static int size_rings(sh_query* q, int64_t new_rc) {
+// (keep = false: fresh buffers, e.g. before a restore overwrites them — the live rings may hold more
+// entries than the new capacity, so they must not be copied over)
+static int size_rings(sh_query* q, int64_t new_rc, bool keep = true) {
     SlidingImpl* s = q->sl;
     int F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols);
     int64_t n = s->nslots;
@@ -77,7 +80,7 @@ static int size_rings(sh_query* q, int64_t new_rc) {
     RCHK(rval2.reserve((size_t)V * n * new_rc * 8, false));
     RCHK(dq2.reserve((size_t)F * n * new_rc * 8, false));
     hipStream_t st = q->ctx->stream;
-    if (s->rc > 0) {
+    if (s->rc > 0 && keep) {
         launch_sl_regrow(st, (const u64*)s->rpm.p, (u64*)rpm2.p, s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, 1,
                          s->rc, new_rc, false);
         launch_sl_regrow(st, s->rval.as<u64>(), rval2.as<u64>(), s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, V,
@@ -88,9 +91,7 @@ static int size_rings(sh_query* q, int64_t new_rc) {
         HIPCHK(hipMemsetAsync(s->dq_head.p, 0, (size_t)F * n * 8, st));
         HIPCHK(hipStreamSynchronize(st));
     }
-    s->rpm.release(); s->rval.release(); s->dq.release();
-    s->rpm = rpm2; s->rval = rval2; s->dq = dq2;
-    rpm2.p = rval2.p = dq2.p = nullptr;
+    s->rpm = std::move(rpm2); s->rval = std::move(rval2); s->dq = std::move(dq2);
     s->rc = new_rc;
     return SH_OK;
 }
@@ -205,7 +206,8 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     HIPCHK(hipStreamSynchronize(st));
     RCHK(q->kt.check(st));
     SlInfo info = *s->h_info;
-    RCHK(sliding_finish(q, info.total_pass, N, info.need, b->send_size, s->send_base, 0, false, host_out, out));
+    RCHK(sliding_finish(q, info.total_pass, N, info.need, b->send_size, s->send_base, q->seq, false, host_out, out));
+    q->seq += N;
     // window state moves on
     q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
     q->clock_valid = true;
@@ -287,13 +289,14 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         int na = q->ap.n;
         RCHK(s->flags.reserve(M + 16, false));
         RCHK(s->rows_ts.reserve(M * 8, false));
+        RCHK(s->rows_rep.reserve(M * 4, false));
         RCHK(s->rows_slot.reserve(M * 4, false));
         RCHK(s->rows_send.reserve(M * 8, false));
         RCHK(s->rows_clock.reserve(M * 8, false));
         RCHK(s->rows_vals.reserve((size_t)na * M * 8, false));
         RCHK(s->rows_nulls.reserve((size_t)na * M, false));
         HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
-        SlRows rows{s->rows_ts.as<int64_t>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
+        SlRows rows{s->rows_ts.as<int64_t>(), s->rows_rep.as<u32>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
                     s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
         // the records in partition order
         RCHK(s->p_raw.reserve(M * 4, false));
@@ -331,6 +334,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         RCHK(s->out_send.reserve(cap * 8, false));
         RCHK(s->out_clock.reserve(cap * 8, false));
         RCHK(s->out_expired.reserve(cap, false));
+        RCHK(s->out_rep.reserve(cap * 8, false));
         HIPCHK(hipMemsetAsync(s->out_expired.p, 0, cap, st));
         if (want_order) RCHK(q->out_order.reserve(cap * 8, false));
         launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
@@ -338,7 +342,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
                        q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                        s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(),
                        s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr,
-                       q->d.window == SH_WIN_EXT_TIME ? s->rec_sclk.as<int64_t>() : nullptr);
+                       q->d.window == SH_WIN_EXT_TIME ? s->rec_sclk.as<int64_t>() : nullptr, s->out_rep.as<int64_t>());
         HIPCHK(hipGetLastError());
     }
     // flush structure: a flush per send that produced rows (one selector output chunk per send)
@@ -356,7 +360,9 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         launch_scan_sum(st, s->blk_cnt.as<int64_t>(), rb);
         launch_flush_write(st, s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), n_rows, s->blk_cnt.as<int64_t>(),
                            rb, s->flush_off.as<int64_t>(), s->flush_clock.as<int64_t>());
-        HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, &n_rows, 8, hipMemcpyHostToDevice, st));
+        RCHK(s->h_up.reserve(8));
+        *s->h_up.as<int64_t>() = n_rows;
+        HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, s->h_up.p, 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(q->ev_push1, st));
@@ -376,6 +382,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         o.keys.resize((size_t)nk * n_rows);
         o.vals.resize((size_t)na * n_rows);
         o.nulls.resize((size_t)na * n_rows);
+        o.rep.resize(n_rows);
         if (n_rows > 0) {
             HIPCHK(hipMemcpyAsync(o.flush_offsets.data(), s->flush_off.p, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.flush_clock.data(), s->flush_clock.p, n_flushes * 8, hipMemcpyDeviceToHost, st));
@@ -384,6 +391,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
             if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), s->out_keys.p, (size_t)nk * n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.vals.data(), s->out_vals.p, (size_t)na * n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.nulls.data(), s->out_nulls.p, (size_t)na * n_rows, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.rep.data(), s->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, st));
             if (want_order) {
                 q->order_host.resize(n_rows);
                 HIPCHK(hipMemcpyAsync(q->order_host.data(), q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, st));
@@ -409,6 +417,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         o.keys = s->out_keys.as<int64_t>();
         o.vals = s->out_vals.as<uint64_t>();
         o.nulls = s->out_nulls.as<uint8_t>();
+        o.rep = s->out_rep.as<int64_t>();
         *out = &o;
     }
     return SH_OK;
@@ -433,7 +442,8 @@ int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& 
     if (n_sc != 4) return sh_fail(SH_ERR_INVALID, "sliding snapshot layout");
     if (set) {
         if (sc[0] != s->nslots) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
-        if (new_rc != s->rc) RCHK(size_rings(q, new_rc));
+        if (new_rc <= 0 || (new_rc & (new_rc - 1))) return sh_fail(SH_ERR_INVALID, "snapshot ring capacity");
+        if (new_rc != s->rc) RCHK(size_rings(q, new_rc, false));
         s->pm = sc[2];
         s->send_base = sc[3];
     } else {

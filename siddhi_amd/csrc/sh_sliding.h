@@ -40,6 +40,7 @@ struct SlState {
 // rows indexed by the rank of the (send, key) first occurrence
 struct SlRows {
     i64* ts;
+    u32* rep;             // push index of the row's representative event (the key's last in the send)
     u32* slot;
     i64* send;
     i64* clock;
@@ -56,8 +57,6 @@ void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
 void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* out);
 void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* counts, i64* tmp, u32* out_rank,
                           i64* part_off);
-void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, int P, SlRecords rec, SlState S,
-                    AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags);
 int sliding_keys_per_partition(AggPlan ap);
 void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv);
 // rec: the records gathered into partition order (k_sl_own); rec_by_rank: the same records in rank
@@ -67,8 +66,8 @@ void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off
                         unsigned char* flags, SlRecords rec_by_rank);
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                    unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw = nullptr,
-                    i64 raw_base = 0, i64* out_order = nullptr, const i64* clock_by_rank = nullptr);
+                    unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw, i64 raw_base,
+                    i64* out_order, const i64* clock_by_rank, i64* out_rep);
 void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, KeyPlan kp, KeyTable kt, AggPlan ap,
                              const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
                              u32* slot_cnt);

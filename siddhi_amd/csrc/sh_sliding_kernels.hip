@@ -299,149 +299,6 @@ __device__ __forceinline__ bool boxed_eq(int kind, u64 a, u64 b) {
     return a == b;
 }
 
-__device__ __forceinline__ void sl_remove(const SlState& S, const AggPlan& ap, u32 k, const u64* v) {
-    i64 c = S.cnt[k] - 1;
-    S.cnt[k] = c;
-    for (int a = 0; a < ap.n; a++) {
-        int kind = ap.kind[a];
-        if (kind == AK_COUNT) continue;
-        u64 x = v[ap.vcol[a]];
-        size_t fi = (size_t)ap.field[a] * S.nslots + k;
-        switch (kind) {
-            case AK_SUM_L: S.f[fi] = (u64)java_d2l((double)(i64)S.f[fi] - (double)(i64)x); break;
-            case AK_SUM_D: case AK_AVG: {
-                double xv = (kind == AK_AVG && !(ap.vcol_type[ap.vcol[a]] == SH_T_FLOAT ||
-                                                 ap.vcol_type[ap.vcol[a]] == SH_T_DOUBLE))
-                                ? (double)(i64)x : __longlong_as_double((i64)x);
-                double r = __longlong_as_double((i64)S.f[fi]) - xv;
-                // state destroyed when count == 0 && sum == 0.0 (PartitionStateHolder.returnState):
-                // a fresh state restarts from +0.0
-                if (c == 0 && r == 0.0) r = 0.0;
-                S.f[fi] = (u64)__double_as_longlong(r);
-                break;
-            }
-            default: {
-                // removeFirstOccurrence(value) on the deque ring; then minValue = peekFirst()
-                u64* dq = S.dq + ((size_t)ap.field[a] * S.nslots + k) * S.rc;
-                i64 h = S.dq_head[fi], len = S.dq_len[fi];
-                i64 found = -1;
-                for (i64 i = 0; i < len; i++) {
-                    if (boxed_eq(kind, dq[(h + i) & (S.rc - 1)], x)) { found = i; break; }
-                }
-                if (found >= 0) {
-                    for (i64 i = found; i + 1 < len; i++) dq[(h + i) & (S.rc - 1)] = dq[(h + i + 1) & (S.rc - 1)];
-                    len--;
-                    S.dq_len[fi] = len;
-                }
-                if (len > 0) { S.mm[fi] = dq[h & (S.rc - 1)]; S.mm_has[fi] = 1; }
-                else S.mm_has[fi] = 0;
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void sl_add(const SlState& S, const AggPlan& ap, u32 k, const u64* v) {
-    i64 c = S.cnt[k] + 1;
-    S.cnt[k] = c;
-    for (int a = 0; a < ap.n; a++) {
-        int kind = ap.kind[a];
-        if (kind == AK_COUNT) continue;
-        u64 x = v[ap.vcol[a]];
-        size_t fi = (size_t)ap.field[a] * S.nslots + k;
-        switch (kind) {
-            case AK_SUM_L: S.f[fi] = (u64)((i64)S.f[fi] + (i64)x); break;
-            case AK_SUM_D: case AK_AVG: {
-                double xv = (kind == AK_AVG && !(ap.vcol_type[ap.vcol[a]] == SH_T_FLOAT ||
-                                                 ap.vcol_type[ap.vcol[a]] == SH_T_DOUBLE))
-                                ? (double)(i64)x : __longlong_as_double((i64)x);
-                S.f[fi] = (u64)__double_as_longlong(__longlong_as_double((i64)S.f[fi]) + xv);
-                break;
-            }
-            default: {
-                u64* dq = S.dq + ((size_t)ap.field[a] * S.nslots + k) * S.rc;
-                i64 h = S.dq_head[fi], len = S.dq_len[fi];
-                while (len > 0 && mm_worse(kind, dq[(h + len - 1) & (S.rc - 1)], x)) len--;
-                dq[(h + len) & (S.rc - 1)] = x;
-                S.dq_len[fi] = len + 1;
-                if (!S.mm_has[fi] || mm_worse(kind, S.mm[fi], x)) { S.mm[fi] = x; S.mm_has[fi] = 1; }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(64) void k_sliding(const u32* __restrict__ rank_list, const i64* __restrict__ part_off,
-                                                int P, SlRecords rec, SlState S, AggPlan ap, i64 T, i64 send_size,
-                                                i64 send_base, SlRows rows, unsigned char* flags) {
-    const int p = blockIdx.x;
-    const int lane = threadIdx.x;
-    const i64 lo = part_off[p], hi = part_off[p + 1];
-    for (i64 b = lo; b < hi; b += 64) {
-        i64 idx = b + lane;
-        bool pend = idx < hi;
-        u32 r = 0, k = 0;
-        if (pend) { r = rank_list[idx]; k = rec.slot[r]; }
-        while (__ballot(pend)) {
-            // lowest pending lane per key wins this round:
-            // find, for each pending lane, whether an earlier pending lane has the same key
-            bool win = pend;
-            for (int j = 0; j < 64; j++) {
-                u32 kj = __shfl(k, j, 64);
-                bool pj = __shfl((int)pend, j, 64);
-                if (j < lane && pj && kj == k) win = false;
-            }
-            if (win) {
-                i64 clk = rec.clock[r];
-                // lazy expiry: ring head events with PM + T <= clock
-                i64 h = S.rhead[k], len = S.rlen[k];
-                while (len > 0) {
-                    i64 slot = (h & (S.rc - 1));
-                    i64 pmj = S.rpm[(size_t)k * S.rc + slot];
-                    if (pmj + T > clk) break;
-                    u64 v[SH_MAX_AGGS];
-                    for (int j = 0; j < ap.n_vcols; j++) v[j] = S.rval[((size_t)j * S.nslots + k) * S.rc + slot];
-                    sl_remove(S, ap, k, v);
-                    h++; len--;
-                }
-                // add the event to the key's ring and aggregators
-                u64 v[SH_MAX_AGGS];
-                for (int j = 0; j < ap.n_vcols; j++) v[j] = rec.vals[(size_t)j * rec.cap + r];
-                i64 slot = (h + len) & (S.rc - 1);
-                S.rpm[(size_t)k * S.rc + slot] = rec.pm[r];
-                for (int j = 0; j < ap.n_vcols; j++) S.rval[((size_t)j * S.nslots + k) * S.rc + slot] = v[j];
-                len++;
-                S.rhead[k] = h; S.rlen[k] = len;
-                sl_add(S, ap, k, v);
-                // output row of (send, key): first occurrence position, last event's values
-                i64 send = send_base + (send_size > 0 ? (i64)rec.raw[r] / send_size : 0);
-                i64 first;
-                if (S.cur_send[k] != send) { S.cur_send[k] = send; S.cur_first[k] = r; first = r; flags[r] = 1; }
-                else first = S.cur_first[k];
-                rows.ts[first] = rec.ts[r];
-                rows.slot[first] = k;
-                rows.send[first] = send;
-                rows.clock[first] = clk;
-                i64 c = S.cnt[k];
-                for (int a = 0; a < ap.n; a++) {
-                    int kind = ap.kind[a];
-                    u64 o; unsigned char nl = 0;
-                    if (kind == AK_COUNT) o = (u64)c;
-                    else {
-                        size_t fi = (size_t)ap.field[a] * S.nslots + k;
-                        if (kind == AK_SUM_L || kind == AK_SUM_D) o = S.f[fi];
-                        else if (kind == AK_AVG) o = (u64)__double_as_longlong(__longlong_as_double((i64)S.f[fi]) / (double)c);
-                        else { o = S.mm[fi]; nl = S.mm_has[fi] ? 0 : 1; }
-                    }
-                    rows.vals[(size_t)a * rows.cap + first] = o;
-                    rows.nulls[(size_t)a * rows.cap + first] = nl;
-                }
-                pend = false;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __threadfence_block();
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // k_sl_own: one wave per key partition, lane ownership. Local key li = slot >> logP belongs to lane
 // li & 63 (with NL <= 64 local keys every lane owns at most one key, whose state — counts, sums,
@@ -1076,6 +933,7 @@ __global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_li
             if (cur_send != send) { cur_send = send; cur_first = r; first = r; flags[r] = 1; }
             else first = cur_first;
             rows.ts[first] = tsr;
+            rows.rep[first] = raw;
             rows.slot[first] = k;
             rows.send[first] = send;
             rows.clock[first] = clk;
@@ -1227,6 +1085,7 @@ __global__ __launch_bounds__(64) void k_sl_own(const u32* __restrict__ rank_list
             if (L.cur_send != send) { L.cur_send = send; L.cur_first = r; first = r; flags[r] = 1; }
             else first = L.cur_first;
             rows.ts[first] = cur.ts;
+            rows.rep[first] = cur.raw;
             rows.slot[first] = k;
             rows.send[first] = send;
             rows.clock[first] = clk;
@@ -1338,12 +1197,6 @@ void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off
 #undef SH_SL_OWN
 }
 
-void launch_sliding(hipStream_t s, const u32* rank_list, const i64* part_off, int P, SlRecords rec, SlState S,
-                    AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows, unsigned char* flags) {
-    hipLaunchKernelGGL(k_sliding, dim3(P), dim3(64), 0, s, rank_list, part_off, P, rec, S, ap, T, send_size,
-                       send_base, rows, flags);
-}
-
 // ------------------------------------------------------------------------------------------------
 // emit: flagged ranks -> output rows in rank order; flush starts where the send changes.
 // ------------------------------------------------------------------------------------------------
@@ -1352,7 +1205,8 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
                                                    KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys,
                                                    u64* out_vals, unsigned char* out_nulls, i64* out_send,
                                                    i64* out_clock, const u32* __restrict__ rank_raw, i64 raw_base,
-                                                   i64* out_order, const i64* __restrict__ clock_by_rank) {
+                                                   i64* out_order, const i64* __restrict__ clock_by_rank,
+                                                   i64* out_rep) {
     // striped over the tile (round it: elements tile + it * kBlock + lane), so every row read and
     // every output column store of a wave is one contiguous run; the tile's first output row is
     // blk_pre (k_count_flags counts whole tiles, whatever the order inside)
@@ -1374,6 +1228,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_emit(const unsigned char* __restr
         out_send[r] = rows.send[j];
         out_clock[r] = clock_by_rank ? clock_by_rank[j] : rows.clock[j];
         if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
+        out_rep[r] = raw_base + (i64)rows.rep[j];
     }
 }
 
@@ -1413,10 +1268,10 @@ __global__ __launch_bounds__(kBlock) void k_flush_write(const i64* __restrict__ 
 void launch_sl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlRows rows,
                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                     unsigned char* out_nulls, i64* out_send, i64* out_clock, const u32* rank_raw, i64 raw_base,
-                    i64* out_order, const i64* clock_by_rank) {
+                    i64* out_order, const i64* clock_by_rank, i64* out_rep) {
     hipLaunchKernelGGL(k_sl_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rows, n_aggs, kt, kp, out_cap,
                        out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base, out_order,
-                       clock_by_rank);
+                       clock_by_rank, out_rep);
 }
 
 void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb) {

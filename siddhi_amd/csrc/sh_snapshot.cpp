@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 2;
+constexpr uint32_t kVersion = 3;
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -100,6 +100,18 @@ uint64_t fingerprint(const sh_query* q) {
     return h;
 }
 
+// the key table's insert counter after a restore (stream-ordered, from pinned memory)
+int set_key_count(sh_query* q, int64_t nk) {
+    PinnedBuf h;
+    RCHK(h.reserve(16));
+    uint32_t* c = h.as<uint32_t>();
+    c[0] = (uint32_t)nk; c[1] = c[2] = c[3] = 0;
+    if (hipMemcpyAsync(q->kt.ctrl.p, c, 16, hipMemcpyHostToDevice, q->ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(q->ctx->stream) != hipSuccess)
+        return sh_fail(SH_ERR_DEVICE, "restore: key table counter");
+    return SH_OK;
+}
+
 }  // namespace
 
 // ---- per-kind sections (batch windows: sh_window.cpp; sliding: sh_sliding.cpp) -----------------
@@ -131,6 +143,9 @@ int batch_snapshot(sh_query* q, Writer& w) {
     RCHK(w.dev(q->pend_ts.p, n * 8, s));
     w.val<int32_t>(q->ap.n_vcols);
     for (int j = 0; j < q->ap.n_vcols; j++) RCHK(w.dev(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, n * 8, s));
+    // stream numbering (sh_out.rep): the queued events' indices and the next event's
+    RCHK(w.dev(q->pend_gidx.p, n * 8, s));
+    w.val<int64_t>(q->seq);
     return SH_OK;
 }
 
@@ -162,26 +177,30 @@ int batch_restore(sh_query* q, Reader& r) {
     }
     RCHK(query_resize_for_restore(q, size, n_pend_peek));
     RCHK(r.dev(q->kt.keys, dense ? 8 : size * 8, s));
-    uint32_t ctrl[4] = {(uint32_t)nk, 0, 0, 0};
-    if (hipMemcpy(q->kt.ctrl.p, ctrl, 16, hipMemcpyHostToDevice) != hipSuccess)
-        return sh_fail(SH_ERR_DEVICE, "restore: key table counter");
+    RCHK(set_key_count(q, nk));
     q->kt.n_keys = nk;
     const int64_t n = r.val<int64_t>();
     q->n_pend = n;
     // pending buffers were sized by query_resize_for_restore; copy the sections into them
     DevBuf tmp;
     RCHK(r.dev(tmp, 8, s));
-    if (n && hipMemcpy(q->pend_pos.p, tmp.p, n * 4, hipMemcpyDeviceToDevice) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
+    if (n && hipMemcpyAsync(q->pend_pos.p, tmp.p, n * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
     RCHK(r.dev(tmp, 8, s));
-    if (n && hipMemcpy(q->pend_ts.p, tmp.p, n * 8, hipMemcpyDeviceToDevice) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
+    if (n && hipMemcpyAsync(q->pend_ts.p, tmp.p, n * 8, hipMemcpyDeviceToDevice, s) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "restore");
     int32_t nv = r.val<int32_t>();
     if (nv != q->ap.n_vcols) { tmp.release(); return sh_fail(SH_ERR_INVALID, "snapshot does not match this query"); }
     for (int j = 0; j < nv; j++) {
         RCHK(r.dev(tmp, 8, s));
-        if (n && hipMemcpy(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, tmp.p, n * 8, hipMemcpyDeviceToDevice) !=
-                     hipSuccess)
+        if (n && (hipMemcpyAsync(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, tmp.p, n * 8,
+                                 hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess))
             return sh_fail(SH_ERR_DEVICE, "restore");
     }
+    RCHK(r.dev(tmp, 8, s));
+    if (n && (hipMemcpyAsync(q->pend_gidx.p, tmp.p, n * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+        return sh_fail(SH_ERR_DEVICE, "restore");
+    q->seq = r.val<int64_t>();
     tmp.release();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     q->p0_known = false;
@@ -190,6 +209,7 @@ int batch_restore(sh_query* q, Reader& r) {
 }
 
 extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
     if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
     Writer w;
@@ -207,6 +227,7 @@ extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* l
 }
 
 extern "C" int sh_query_restore(sh_query* q, const void* buf, int64_t len) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_query_restore: bad arguments");
     Reader r{(const uint8_t*)buf, (size_t)len};
     if (std::memcmp(buf, "SHQ1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip query snapshot");
@@ -236,6 +257,7 @@ int sliding_snapshot(sh_query* q, Writer& w) {
     RCHK(sliding_state_buffers(q, bufs, sc, 4, false, 0));
     for (int i = 0; i < 4; i++) w.val<int64_t>(sc[i]);
     for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+    w.val<int64_t>(q->seq);
     return SH_OK;
 }
 
@@ -247,9 +269,7 @@ int sliding_restore(sh_query* q, Reader& r) {
     int64_t nk = r.val<int64_t>();
     if (!r.ok || size != q->kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
     RCHK(r.dev(q->kt.keys, q->kt.dense ? 8 : size * 8, s));
-    uint32_t ctrl[4] = {(uint32_t)nk, 0, 0, 0};
-    if (hipMemcpy(q->kt.ctrl.p, ctrl, 16, hipMemcpyHostToDevice) != hipSuccess)
-        return sh_fail(SH_ERR_DEVICE, "restore: key table counter");
+    RCHK(set_key_count(q, nk));
     q->kt.n_keys = nk;
     int64_t sc[4];
     for (int i = 0; i < 4; i++) sc[i] = r.val<int64_t>();
@@ -257,6 +277,7 @@ int sliding_restore(sh_query* q, Reader& r) {
     std::vector<std::pair<DevBuf*, size_t>> bufs;
     RCHK(sliding_state_buffers(q, bufs, sc, 4, true, sc[1]));
     for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+    q->seq = r.val<int64_t>();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;
 }

@@ -66,10 +66,10 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
     RCHK(np.reserve(ncap * 4, false));
     RCHK(nt.reserve(ncap * 8, false));
     RCHK(nv.reserve(std::max(1, q->ap.n_vcols) * ncap * 8, false));
-    if (q->given) RCHK(ng.reserve(ncap * 8, false));
+    RCHK(ng.reserve(ncap * 8, false));
     hipStream_t s = q->ctx->stream;
     if (keep > 0) {
-        if (q->given) HIPCHK(hipMemcpyAsync(ng.p, q->pend_gidx.p, keep * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(ng.p, q->pend_gidx.p, keep * 8, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(np.p, q->pend_pos.p, keep * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(nt.p, q->pend_ts.p, keep * 8, hipMemcpyDeviceToDevice, s));
         for (int j = 0; j < q->ap.n_vcols; j++)
@@ -77,9 +77,7 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
                                   hipMemcpyDeviceToDevice, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    q->pend_pos.release(); q->pend_ts.release(); q->pend_vals.release(); q->pend_gidx.release();
-    q->pend_pos = np; q->pend_ts = nt; q->pend_vals = nv; q->pend_gidx = ng;
-    np.p = nt.p = nv.p = ng.p = nullptr;
+    q->pend_pos = std::move(np); q->pend_ts = std::move(nt); q->pend_vals = std::move(nv); q->pend_gidx = std::move(ng);
     q->pend_cap = ncap;
     return SH_OK;
 }
@@ -121,9 +119,7 @@ static int rekey(sh_query* q, size_t size) {
     launch_rekey(q->ctx->stream, q->n_pend, q->pend_pos.as<u32>(), q->kt.dev(), nk.dev());
     HIPCHK(hipGetLastError());
     RCHK(nk.check(q->ctx->stream));
-    q->kt.release();
-    q->kt = nk;
-    nk.keys.p = nk.ctrl.p = nullptr;
+    q->kt = std::move(nk);
     return size_partitions(q);
 }
 
@@ -138,6 +134,7 @@ int query_reserve_keys(sh_query* q, int64_t extra) {
 }
 
 extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
+    StreamScope _ss(ctx ? ctx->stream : nullptr);
     return query_create(ctx, d, nullptr, out);
 }
 
@@ -244,7 +241,11 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     HIPCHK(hipMemsetAsync(q->flags.p, 0, closed_hi, s));
     HIPCHK(hipMemsetAsync(q->seg_rows.p, 0, nseg * 8, s));
     HIPCHK(hipMemsetAsync(q->counters.p, 0, 64, s));
-    HIPCHK(hipMemcpyAsync(q->segs.p, segs.data(), nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
+    // the segment list goes up from pinned memory (an async copy from pageable memory may read it
+    // after this function returned)
+    RCHK(q->h_up.reserve((size_t)nseg * sizeof(Segment)));
+    std::memcpy(q->h_up.p, segs.data(), (size_t)nseg * sizeof(Segment));
+    HIPCHK(hipMemcpyAsync(q->segs.p, q->h_up.p, nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
     const u32* rec_pos = nullptr; const u32* rec_idx = nullptr; const u64* rec_vals = nullptr;
     int64_t rec_cap = 0;
     // One flat workgroup per segment walks every event of the segment, passing or not, and
@@ -291,6 +292,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         RCHK(q->out_vals.reserve(na * cap * 8, false));
         RCHK(q->out_nulls.reserve(na * cap, false));
         RCHK(q->out_expired.reserve(cap, false));
+        RCHK(q->out_rep.reserve(cap * 8, false));
         if (q->given) RCHK(q->out_order.reserve(cap * 8, false));
         int nblk2 = (int)((closed_hi + kTile - 1) / kTile);
         RCHK(q->blk_cnt.reserve(nblk2 * 8, false));
@@ -301,9 +303,9 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
                     q->perm.as<u32>(), n_rows, q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp,
                     q->n_pend,
                     q->pend_ts.as<int64_t>(), ts, cap, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(),
-                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>(),
-                    q->given ? q->pend_gidx.as<u64>() : nullptr, q->given && b ? q->given_gidx : nullptr,
-                    q->given ? q->out_order.as<int64_t>() : nullptr);
+                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>(), q->pend_gidx.as<u64>(),
+                    q->given && b ? q->given_gidx : nullptr, q->given ? q->out_order.as<int64_t>() : nullptr, q->seq,
+                    q->out_rep.as<int64_t>());
         HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
         HIPCHK(hipGetLastError());
         if (host_out) {
@@ -311,7 +313,9 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
             size_t nb = base + n_rows;
             q->out.ts.resize(nb);
             q->out.expired.resize(nb, 0);
+            q->out.rep.resize(nb);
             HIPCHK(hipMemcpyAsync(q->out.ts.data() + base, q->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(q->out.rep.data() + base, q->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, s));
             // keys / vals / nulls are [k][n] blocks; append per push into temporaries and interleave later
             std::vector<int64_t> k(nk * n_rows);
             std::vector<uint64_t> v(na * n_rows);
@@ -364,6 +368,7 @@ static void finish_out(sh_query* q, bool host_out, const sh_out** out) {
         o.keys = q->out_keys.as<int64_t>();
         o.vals = q->out_vals.as<uint64_t>();
         o.nulls = q->out_nulls.as<uint8_t>();
+        o.rep = q->out_rep.as<int64_t>();
         *out = &o;
     }
 }
@@ -387,10 +392,11 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
     wp.kind = SH_WIN_LENGTH_BATCH;  // no nextEmitTime initialisation in this probe
     wp.N = N;
     wp.send_size = b->send_size;
+    wp.pcol1 = q->d.partition_col + 1;
     launch_blockagg(s, b->ts, cs, q->fp_orig, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                     q->blk_first.as<int64_t>(), nblk);
     launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk, b->ts,
-                       wp, q->info.as<PushInfo>());
+                       wp, q->info.as<PushInfo>(), nullptr, cs);
     HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     int64_t first = q->h_info->first_pass;
@@ -400,16 +406,8 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
         q->clock_valid = true;
         return SH_OK;
     }
-    int pc = q->d.partition_col;
-    int t = q->d.col_types[pc];
-    int64_t key = 0;
-    if (t == SH_T_LONG) {
-        HIPCHK(hipMemcpy(&key, (const char*)b->cols[pc] + first * 8, 8, hipMemcpyDeviceToHost));
-    } else {
-        int32_t k32 = 0;
-        HIPCHK(hipMemcpy(&k32, (const char*)b->cols[pc] + first * 4, 4, hipMemcpyDeviceToHost));
-        key = k32;
-    }
+    // the partition key of that event, read by k_scan_blocks (no extra round trip)
+    const int64_t key = q->h_info->first_key;
     return query_set_partition(q, key);
 }
 
@@ -580,10 +578,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
                                q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                                q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
-                               q->given ? q->pend_gidx.as<u64>() : nullptr);
+                               q->pend_gidx.as<u64>(), q->seq);
         HIPCHK(hipGetLastError());
         q->n_pend = new_pend;
     }
+    q->seq += N;
     HIPCHK(hipEventRecord(q->ev_push1, s));
     RCHK(q->kt.check(s));
     float ms = 0;
@@ -599,6 +598,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
 // run_closed calls append (only one per push today) the layout stays [col][n_rows] because a push
 // calls run_closed at most once.
 extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
     sh_batch dev;
     RCHK(q->staged.stage(q->ctx->stream, b, q->d.n_cols, q->d.col_types, &dev));
@@ -607,6 +607,7 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
 }
 
 extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
     if (q->kind == 1) return sliding_push(q, b, false, out);
     return push_core(q, b, false, out);
@@ -638,6 +639,7 @@ static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** 
 }
 
 extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
     if (q->kind == 1) return sliding_advance(q, now, out);
     return advance_core(q, now, true, out);
@@ -649,6 +651,7 @@ int sh_advance_time_device(sh_query* q, int64_t now, const sh_out** out) {
 }
 
 extern "C" int sh_query_destroy(sh_query* q) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q) return SH_OK;
     (void)hipStreamSynchronize(q->ctx->stream);
     if (q->kind == 1) sliding_destroy(q);

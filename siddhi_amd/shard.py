@@ -214,7 +214,7 @@ def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None,
     ref = parts[0]
     res = {"flush_offsets": np.array(fo, np.int64), "flush_clock": np.array(fc, np.int64),
            "val_types": ref["val_types"]}
-    for key in ("ts", "expired", "order"):
+    for key in ("ts", "expired", "order", "rep"):
         g = gather(key)
         res[key] = np.concatenate(g) if g else np.zeros(0, ref[key].dtype)
     for key in ("keys", "vals", "nulls"):
@@ -236,7 +236,7 @@ def _merge_by_send(parts: List[dict], sends: Tuple[int, int]) -> dict:
     starts = np.flatnonzero(np.r_[True, send[1:] != send[:-1]]) if order.size else np.zeros(0, np.int64)
     res = {"flush_offsets": np.r_[starts, order.size].astype(np.int64),
            "flush_clock": clock[perm][starts].astype(np.int64), "val_types": ref["val_types"], "order": order}
-    for key in ("ts", "expired"):
+    for key in ("ts", "expired", "rep"):
         res[key] = np.concatenate([p[key] for p in parts])[perm]
     for key in ("keys", "vals", "nulls"):
         res[key] = np.concatenate([p[key] for p in parts], axis=1)[:, perm]

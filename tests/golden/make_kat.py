@@ -35,10 +35,13 @@ case(name="lengthBatch3_all_events", source="ctest/query/window/LengthBatchWindo
                  remove_order=[1, 2, 3, 4]))
 _lb4 = [["IBM", 10.0, 0], ["WSO2", 20.0, 1], ["IBM", 30.0, 0], ["WSO2", 40.0, 1], ["IBM", 50.0, 0],
         ["WSO2", 60.0, 1]]
+# `select symbol, sum(price) as sumPrice, volume`: the Java test asserts sumPrice; symbol and volume
+# are the batch's last event's (QuerySelector.processInBatchNoGroupBy keeps the chunk's last event),
+# hand-traced here as rep_cols: WSO2 / 1 (the 4th event)
 case(name="lengthBatch4_sum", source="ctest/query/window/LengthBatchWindowTestCase.java:192-234",
      schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=4, aggs=[["sum", "price"]], output="current"),
      sends=[[[B + i] + r] for i, r in enumerate(_lb4)],
-     expect=dict(in_count=1, remove_count=0, values=[[100.0]]))
+     expect=dict(in_count=1, remove_count=0, values=[[100.0]], rep_cols=[["volume", [1]], ["symbol", ["WSO2"]]]))
 case(name="lengthBatch5_expired", source="ctest/query/window/LengthBatchWindowTestCase.java:236-277",
      schema=CSE_FLOAT_INT, query=dict(window="lengthBatch", param=2, output="expired"),
      sends=[[[B + i] + r] for i, r in enumerate(_six)],

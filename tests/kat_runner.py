@@ -121,13 +121,26 @@ def check_query(case, flushes, schema, dic):
         idx, lo, hi = e["value_range"]
         for r in rows:
             assert lo <= r[3][idx] <= hi
+    # non-aggregated select attributes come from the row's representative event (sh_out.rep, the
+    # event QuerySelector keeps per key): in/remove order checks and transcribed attribute columns
+    events = [r for s in case["sends"] if isinstance(s, list) for r in s]
+    reps = [x for f in flushes for x in f.reps]
+    if "in_order" in e or "remove_order" in e or "rep_cols" in e:
+        assert len(reps) == len(rows), "output without representative events"
+
+    def attr(col, idx):
+        return events[reps[idx]][1 + schema.col(col)]
+    if "in_order" in e:
+        got = [attr(e["in_order_col"], i) for i, r in enumerate(rows) if not r[1]]
+        assert got == e["in_order"], (got, e["in_order"])
+    if "remove_order" in e:
+        got = [attr(e.get("in_order_col", "volume"), i) for i, r in enumerate(rows) if r[1]]
+        assert got == e["remove_order"], (got, e["remove_order"])
+    if "rep_cols" in e:
+        for col, want in e["rep_cols"]:
+            got = [attr(col, i) for i in range(len(rows))]
+            assert got == want, (col, got, want)
     return rows
-
-
-def order_check(case, rows_ts, sends):
-    """In/remove order checks use the volume column of the event that produced the row; rows carry
-    the event timestamp, which is unique per send in these cases."""
-    pass
 
 
 def run_aggregation(case, make_agg):

@@ -27,6 +27,7 @@ def assert_same(gpu, ora, rtol=None, label=""):
     assert np.array_equal(gpu["keys"], ora["keys"]), f"{label}: group keys / row order differ"
     assert np.array_equal(gpu["nulls"], ora["nulls"]), f"{label}: null flags differ"
     assert np.array_equal(gpu["expired"], ora["expired"]), f"{label}: expired flags differ"
+    assert np.array_equal(gpu["rep"], ora["rep"]), f"{label}: representative events differ"
     vt = ora["val_types"]
     assert np.array_equal(gpu["val_types"], vt)
     for a in range(len(vt)):

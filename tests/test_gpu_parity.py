@@ -44,6 +44,23 @@ def test_reference_kat_on_gpu(rt, case):
     assert [(f.clock, f.rows) for f in flushes] == [(f.clock, f.rows) for f in oflushes]
 
 
+# ---- the FilterTestCase1 promotion KATs through the GPU filter program (sh_device.h java_cmp) ----
+# The GPU runs aggregating windows only, so each case is wrapped as `from S[cond]#window.lengthBatch(1)
+# select count() insert into O`: every passing event completes a batch of one and emits one row, so
+# the row count is the number of events the reference's FilterProcessor let through.
+FILTER_KATS = [c for c in kat_runner.load_cases() if c.get("kind") != "aggregation" and c["query"].get("window") is None
+               and c["query"].get("filter") is not None]
+
+
+@pytest.mark.parametrize("case", FILTER_KATS, ids=[c["name"] for c in FILTER_KATS])
+def test_reference_filter_kat_on_gpu(rt, case):
+    wrapped = dict(case, query=dict(case["query"], window="lengthBatch", param=1, aggs=[["count", None]]))
+    _, _, _, flushes = kat_runner.run_query(wrapped, rt.GpuQuery)
+    rows = [r for f in flushes for r in f.rows]
+    assert len(rows) == case["expect"]["in_count"], (len(rows), case["expect"])
+    assert all(r[3] == (1,) for r in rows)
+
+
 # ---- C1: filtered lengthBatch group-by, 1k symbols --------------------------------------------------
 C1_SCHEMA = abi.Schema.parse("symbol string, price double, volume long, ts long")
 

@@ -62,6 +62,28 @@ def test_sliding_checkpoint_keeps_rings_and_deques():
     assert_same(got, ref, label="sliding ckpt")
 
 
+def test_sliding_rollback_into_a_running_query_whose_rings_grew():
+    """Restore an earlier revision into the SAME running query after its per-key rings grew past the
+    snapshot's capacity (SnapshotService.restoreRevision into a live runtime): the rings are rebuilt at
+    the snapshot's capacity, never copied over, and the query continues like the uninterrupted run."""
+    from siddhi_amd import runtime
+    ts, cols = synth.keyed_stream(0, 200_000, 0xC3, 64, 20)
+    spec = abi.QuerySpec(C2, "time", 5_000, group_by=["k"], aggs=[("count", None), ("min", "v"), ("avg", "v")],
+                         key_capacity=64)
+    pushes = split_batches(C2, ts, cols, [2_000, 150_000], 1)
+    g = runtime.GpuQuery(spec)
+    a = run_pushes(g, pushes[:1])        # ~30 events per key: small rings
+    blob = g.snapshot()
+    run_pushes(g, pushes[1:2])           # ~1500 events per key: the rings grow
+    g.restore(blob)                      # roll back into the grown query
+    b = run_pushes(g, pushes[1:])
+    g.close()
+    o = OracleQuery(spec)
+    ref = run_pushes(o, pushes)
+    o.close()
+    assert_same(abi.concat_arrays([a, b]), ref, label="sliding rollback")
+
+
 def test_partitioned_timebatch_checkpoint():
     rng = np.random.default_rng(5)
     n = 30_000

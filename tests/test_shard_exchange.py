@@ -77,6 +77,7 @@ def test_merge_owner_outputs_orders_rows_by_first_occurrence():
         return {"flush_offsets": np.array(fo, np.int64), "flush_clock": np.array(fc, np.int64),
                 "val_types": np.array([2], np.int32), "ts": np.array(order, np.int64) * 10,
                 "expired": np.zeros(n, np.uint8), "order": np.array(order, np.int64),
+                "rep": np.array(order, np.int64) + 1,
                 "keys": np.array([keys], np.int64), "vals": np.array([keys], np.uint64),
                 "nulls": np.zeros((1, n), np.uint8)}
 
@@ -87,6 +88,7 @@ def test_merge_owner_outputs_orders_rows_by_first_occurrence():
     assert m["flush_clock"].tolist() == [1000, 2000]
     assert m["keys"][0].tolist() == [1, 3, 2, 1]
     assert m["order"].tolist() == [0, 5, 6, 7]
+    assert m["rep"].tolist() == [1, 6, 7, 8]
 
 
 def test_merge_owner_outputs_separates_batches_of_one_send():
@@ -99,6 +101,7 @@ def test_merge_owner_outputs_separates_batches_of_one_send():
         return {"flush_offsets": np.array(fo, np.int64), "flush_clock": np.array(fc, np.int64),
                 "val_types": np.array([2], np.int32), "ts": np.array(order, np.int64),
                 "expired": np.zeros(n, np.uint8), "order": np.array(order, np.int64),
+                "rep": np.array(order, np.int64) + 1,
                 "keys": np.array([keys], np.int64), "vals": np.array([keys], np.uint64),
                 "nulls": np.zeros((1, n), np.uint8)}
 

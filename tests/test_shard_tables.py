@@ -31,7 +31,7 @@ def owner_out(order, clocks_per_flush, flush_offsets, vals):
     order = np.asarray(order, np.int64)
     n = order.size
     return {"order": order, "flush_offsets": np.asarray(flush_offsets, np.int64),
-            "flush_clock": np.asarray(clocks_per_flush, np.int64), "ts": order * 10, "expired": np.zeros(n, np.uint8),
+            "flush_clock": np.asarray(clocks_per_flush, np.int64), "ts": order * 10, "expired": np.zeros(n, np.uint8), "rep": order + 3,
             "keys": order[None, :] % 5, "vals": np.asarray(vals, np.uint64)[None, :], "nulls": np.zeros((1, n), np.uint8),
             "val_types": np.zeros(1, np.int32)}
 
