@@ -141,13 +141,9 @@ struct Segment {
     i64 lo, hi;
 };
 
-// Temp row written by the aggregation kernel; ordered afterwards by `first`.
-struct RowTmp {
-    u32 pos;
-    u32 first;
-    u32 last;
-    u32 pad;
-};
+// Row record of the aggregation kernels: row_words(n_aggs) u64 words — slot | count << 32,
+// first | last << 32 (combined event indices), then the aggregate values.
+__host__ __device__ constexpr int row_words(int n_aggs) { return (2 + n_aggs + 1) & ~1; }
 
 // Launchers (sh_kernels.hip).
 void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
@@ -159,19 +155,18 @@ void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr);
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
-                      AggPlan ap, RowTmp* rows, u64* row_vals,
-                      u32* row_counter, unsigned char* flags, u32* rowref, i64* seg_rows,
-                      // multisplit source (always when P > 1; null: the flat kernel reads the batch)
-                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
-                      const i64* seg_off);
-size_t aggregate_own_lds(int NL, int n_fields, int n_vcols);
+                      AggPlan ap, u64* rows, int RW, u32* row_counter, u32* first_bits, i64* seg_rows,
+                      // multisplit source (P > 1 or long windows; null: the flat kernel reads the batch)
+                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
-void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
-                 u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
-                 i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
-                 u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
-                 i64* out_order, i64 seq_base, i64* out_rep);
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre);
+// rows: row_cap bounds the grid, the row count is read on the device (the aggregation's counter)
+void launch_emit_rows(hipStream_t s, const u64* rows, int RW, i64 row_cap, const u32* n_rows_dev, const u32* bits,
+                      const u32* word_pre, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend, const i64* pend_ts,
+                      const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, const u64* pend_gidx,
+                      const u64* new_gidx, i64* out_order, i64 seq_base, i64* out_rep, u64* stage);
+size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows);
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);

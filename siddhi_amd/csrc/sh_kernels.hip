@@ -5,8 +5,8 @@
 //   k_scan_blocks   exclusive scans of those, nextEmitTime initialisation (TimeBatchWindowProcessor.process :266-276)
 //   k_boundaries    window number per event, boundary list              (LengthBatch :206-243, TimeBatch :278-340, Scheduler)
 //   k_ms_count/scatter  stable multisplit of closed-window events into key partitions (P > 1 only)
-//   k_aggregate     ordered per-key aggregation of one (window, partition) in LDS (QuerySelector.processInBatchGroupBy :315-374)
-//   k_count_flags + k_emit   rows in first-occurrence order                (LinkedHashMap insertion order)
+//   k_aggregate_*   ordered per-key aggregation of one (window, partition) (QuerySelector.processInBatchGroupBy :315-374)
+//   k_bits_* + k_emit_rows   rows in first-occurrence order: rank of the first event's bit (LinkedHashMap order)
 //   k_compact_pending        events of the still-open window carried to the next push
 #include "sh_device.h"
 
@@ -296,13 +296,17 @@ void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
 }
 
 // ================================================================================================
-// k_aggregate: one workgroup per (closed segment, key partition). Events are applied to the key's
-// LDS state strictly in event order — each step takes 256 consecutive events; lanes that share a
-// key resolve in rounds (the lowest lane of each key wins a round), so every per-key update runs
-// in the order the reference's selector runs it (QuerySelector.processInBatchGroupBy :315-374).
-// Double sums are therefore bit-identical to Java's sequential `sum += v`.
-// State starts empty because each flush chunk begins with RESET (LengthBatch :222-226,
-// TimeBatch :320-323; AttributeAggregatorExecutor.processReset :145-151).
+// Aggregation of the closed windows. One row per (window, key) with the aggregate values at the
+// key's last event, folded in event order per key (QuerySelector.processInBatchGroupBy :315-374), so
+// double sums are bit-identical to Java's sequential `sum += v`. State starts empty because each
+// flush chunk begins with RESET (LengthBatch :222-226, TimeBatch :320-323;
+// AttributeAggregatorExecutor.processReset :145-151).
+//
+// Rows are written as records of row_words(n_aggs) u64 words:
+//   w0 = key slot | event count << 32, w1 = first | last << 32 (combined event index), w2.. = values
+// and the row's first event is marked in a bitmap over the combined index space. The output position
+// of a row is the rank of that bit (k_emit_rows): first-occurrence order inside a flush, and flushes
+// in window order, because windows are consecutive index ranges.
 // ================================================================================================
 struct AggLds {
     u64* fields;  // [n_fields][NL]
@@ -321,47 +325,14 @@ __device__ __forceinline__ i64 pick(const i64 (&v)[V], int j) {
     return x;
 }
 
-template <int V>
-__device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL, u32 li, u32 idx, const i64 (&v)[V]) {
-    u32 c = L.cnt[li];
-    if (c == 0) L.first[li] = idx;
-    L.cnt[li] = c + 1;
-    L.last[li] = idx;
-#pragma unroll 1
-    for (int a = 0; a < ap.n; a++) {
-        int k = ap.kind[a];
-        if (k == AK_COUNT) continue;
-        u64* fp = L.fields + (size_t)ap.field[a] * NL + li;
-        i64 x = pick<V>(v, ap.vcol[a]);
-        switch (k) {
-            case AK_SUM_L: *fp = (u64)((c == 0 ? 0 : (i64)*fp) + x); break;  // SumAttributeAggregatorExecutor long: sum += data
-            case AK_SUM_D:                                                // double: sum += data
-            case AK_AVG: {                                               // Avg*: value += (double) data
-                double cur = c == 0 ? 0.0 : __longlong_as_double((i64)*fp);
-                double xv = (k == AK_AVG && !(ap.vcol_type[ap.vcol[a]] == SH_T_FLOAT ||
-                                              ap.vcol_type[ap.vcol[a]] == SH_T_DOUBLE))
-                                ? (double)x : __longlong_as_double(x);
-                *fp = (u64)__double_as_longlong(cur + xv);
-                break;
-            }
-            case AK_MIN_L: if (c == 0 || (i64)*fp > x) *fp = (u64)x; break;  // minValue > value
-            case AK_MAX_L: if (c == 0 || (i64)*fp < x) *fp = (u64)x; break;
-            case AK_MIN_D: if (c == 0 || __longlong_as_double((i64)*fp) > __longlong_as_double(x)) *fp = (u64)x; break;
-            case AK_MAX_D: if (c == 0 || __longlong_as_double((i64)*fp) < __longlong_as_double(x)) *fp = (u64)x; break;
-            case AK_MIN_F: if (c == 0 || (float)__longlong_as_double((i64)*fp) > (float)__longlong_as_double(x)) *fp = (u64)x; break;
-            case AK_MAX_F: if (c == 0 || (float)__longlong_as_double((i64)*fp) < (float)__longlong_as_double(x)) *fp = (u64)x; break;
-        }
-    }
-}
-
-// A key's aggregate fields held in registers while one of its events is folded (k_aggregate_own),
-// field j in register slot j: the per-event updates of apply_event, driven by the per-field op
-// table (sums: sum += x / value += (double) x; min/max: replace when the state is new or x is
-// smaller / larger in the column's type — MinAttributeAggregatorExecutor `minValue > value`).
-template <int V>
-__device__ __forceinline__ void fold_fields(const AggPlan& ap, u64 (&f)[SH_MAX_AGGS], bool first, const i64 (&v)[V]) {
+// A key's aggregate fields held in registers while one of its events is folded, field j in register
+// slot j: the per-event updates driven by the per-field op table (sums: sum += x / value += (double) x;
+// min/max: replace when the state is new or x is smaller / larger in the column's type —
+// MinAttributeAggregatorExecutor `minValue > value`).
+template <int V, int F = SH_MAX_AGGS>
+__device__ __forceinline__ void fold_fields(const AggPlan& ap, u64 (&f)[F], bool first, const i64 (&v)[V]) {
 #pragma unroll
-    for (int j = 0; j < SH_MAX_AGGS; j++) {
+    for (int j = 0; j < F; j++) {
         if (j >= ap.n_fields) break;
         const int op = ap.fop[j];
         const i64 x = pick<V>(v, ap.fvcol[j]);
@@ -392,47 +363,37 @@ __device__ __forceinline__ void fold_fields(const AggPlan& ap, u64 (&f)[SH_MAX_A
     }
 }
 
-// Row emission shared by both variants: one row per touched local key (RowTmp + values), the
-// first-occurrence flag and the row reference at the key's first event.
-__device__ __forceinline__ void emit_rows(const AggPlan& ap, AggLds& L, int NL, int logP, int p, int seg,
-                                          RowTmp* rows, u64* row_vals, u32* row_counter, unsigned char* flags,
-                                          u32* rowref, i64* seg_rows) {
-    int mine = 0;
-    for (int i = threadIdx.x; i < NL; i += blockDim.x) mine += L.cnt[i] > 0;
-    i64 tot;
-    i64 pre = block_excl_scan_any((i64)mine, &tot);
-    __shared__ u32 base_row;
-    if (threadIdx.x == 0) {
-        base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
-        if (tot) atomicAdd((unsigned long long*)&seg_rows[seg], (unsigned long long)tot);
+// The output values of a row: count, avg = value / count, the other fields as folded.
+__device__ __forceinline__ u64 agg_out(const AggPlan& ap, int a, u32 c, u64 fv) {
+    const int k = ap.kind[a];
+    if (k == AK_COUNT) return (u64)(i64)c;
+    if (k == AK_AVG) return (u64)__double_as_longlong(__longlong_as_double((i64)fv) / (double)(i64)c);
+    return fv;
+}
+
+// one row record (see above) with 16-byte stores
+template <int F = SH_MAX_AGGS>
+__device__ __forceinline__ void write_row(const AggPlan& ap, u64* row, int RW, u32 pos, u32 c, u32 first, u32 last,
+                                          const u64 (&f)[F]) {
+    u64 w[2 + SH_MAX_AGGS];
+    w[0] = (u64)pos | ((u64)c << 32);
+    w[1] = (u64)first | ((u64)last << 32);
+#pragma unroll
+    for (int a = 0; a < SH_MAX_AGGS; a++) {
+        u64 fv = f[0];
+#pragma unroll
+        for (int j = 1; j < F; j++) if (ap.field[a] == j) fv = f[j];
+        w[2 + a] = a < ap.n ? agg_out(ap, a, c, fv) : 0;
     }
-    __syncthreads();
-    u32 r = base_row + (u32)pre;
-    for (int i = threadIdx.x; i < NL; i += blockDim.x) {
-        u32 c = L.cnt[i];
-        if (!c) continue;
-        RowTmp t;
-        t.pos = ((u32)i << logP) | (u32)p;
-        t.first = L.first[i];
-        t.last = L.last[i];
-        t.pad = c;
-        rows[r] = t;
-#pragma unroll 1
-        for (int a = 0; a < ap.n; a++) {
-            u64 out;
-            int k = ap.kind[a];
-            if (k == AK_COUNT) out = (u64)(i64)c;
-            else {
-                u64 fv = L.fields[(size_t)ap.field[a] * NL + i];
-                if (k == AK_AVG) out = (u64)__double_as_longlong(__longlong_as_double((i64)fv) / (double)(i64)c);
-                else out = fv;
-            }
-            row_vals[(size_t)r * ap.n + a] = out;
-        }
-        flags[t.first] = 1;
-        rowref[t.first] = r;
-        r++;
+#pragma unroll
+    for (int i = 0; i < (2 + SH_MAX_AGGS) / 2; i++) {
+        if (2 * i >= RW) break;
+        ((ulonglong2*)row)[i] = make_ulonglong2(w[2 * i], w[2 * i + 1]);
     }
+}
+
+__device__ __forceinline__ void mark_first(u32* first_bits, u32 first) {
+    atomicOr(&first_bits[first >> 5], 1u << (first & 31));
 }
 
 __device__ __forceinline__ void lds_layout(unsigned char* smem_raw, const AggPlan& ap, int NL, AggLds& L) {
@@ -445,14 +406,29 @@ __device__ __forceinline__ void lds_layout(unsigned char* smem_raw, const AggPla
     L.owner = L.last + NL;
 }
 
-// Unpartitioned (P == 1, few keys): one workgroup per closed segment reads the events directly;
-// lanes that share a key resolve in ordered rounds (lowest lane first).
+template <int V>
+__device__ __forceinline__ void apply_event(const AggPlan& ap, AggLds& L, int NL, u32 li, u32 idx, const i64 (&v)[V]) {
+    const u32 c = L.cnt[li];
+    u64 f[SH_MAX_AGGS];
+#pragma unroll
+    for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = (j < ap.n_fields && c) ? L.fields[(size_t)j * NL + li] : 0;
+    fold_fields<V>(ap, f, c == 0, v);
+#pragma unroll
+    for (int j = 0; j < SH_MAX_AGGS; j++) if (j < ap.n_fields) L.fields[(size_t)j * NL + li] = f[j];
+    if (c == 0) L.first[li] = idx;
+    L.last[li] = idx;
+    L.cnt[li] = c + 1;
+}
+
+// Unpartitioned (P == 1, few keys, short windows): one workgroup per closed segment reads the events
+// directly; the keys' state is in LDS and lanes that share a key resolve in ordered rounds (lowest
+// lane first).
 __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __restrict__ segs, int NL, i64 n_pend,
                                                           const u32* __restrict__ pend_pos,
                                                           const u64* __restrict__ pend_vals, i64 pend_cap,
                                                           const u32* __restrict__ new_pos, ColSet cols, AggPlan ap,
-                                                          RowTmp* rows, u64* row_vals, u32* row_counter,
-                                                          unsigned char* flags, u32* rowref, i64* seg_rows) {
+                                                          u64* rows, int RW, u32* row_counter, u32* first_bits,
+                                                          i64* seg_rows) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     AggLds L;
     lds_layout(smem_raw, ap, NL, L);
@@ -498,173 +474,204 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
         }
     }
     __syncthreads();
-    emit_rows(ap, L, NL, 0, 0, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
+    int mine = 0;
+    for (int i = threadIdx.x; i < NL; i += blockDim.x) mine += L.cnt[i] > 0;
+    i64 tot;
+    i64 pre = block_excl_scan_any((i64)mine, &tot);
+    __shared__ u32 base_row;
+    if (threadIdx.x == 0) {
+        base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
+        if (tot) atomicAdd((unsigned long long*)&seg_rows[seg], (unsigned long long)tot);
+    }
+    __syncthreads();
+    u32 r = base_row + (u32)pre;
+    for (int i = threadIdx.x; i < NL; i += blockDim.x) {
+        const u32 c = L.cnt[i];
+        if (!c) continue;
+        u64 f[SH_MAX_AGGS];
+#pragma unroll
+        for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = j < ap.n_fields ? L.fields[(size_t)j * NL + i] : 0;
+        write_row(ap, rows + (size_t)r * RW, RW, (u32)i, c, L.first[i], L.last[i], f);
+        mark_first(first_bits, L.first[i]);
+        r++;
+    }
 }
 
-// Partitioned (P > 1), lane ownership: thread t of the workgroup owns the local keys li with
-// li mod 512 == t. Every chunk of CH records (event order) is split stably in LDS into 512 per-thread
-// lists: piece q (64 consecutive records, loaded by one wave) gets per-bucket counts pc[q][b] and
-// in-piece ranks from ballots over the 9 bucket bits; a per-bucket scan over the pieces and a
-// workgroup scan over the buckets give every record its slot. Thread t then folds its list in order
-// straight into the LDS state — keys owned by different lanes of a wave fall in different LDS banks,
-// and no two lanes ever touch one key, so there are no conflict rounds at all.
+// Partitioned, thread ownership with register-resident state: thread t of the workgroup owns the
+// local key t (local key = slot >> logP of key partition p = slot & (P - 1); with K == 2 also
+// t + 512, which only the hash table's sentinel slot can be) and keeps its count, first/last event and
+// aggregate fields in registers for the whole (window, partition). The partition's records (event
+// order) are taken in chunks of CH = 512 * R; wave w loads the contiguous run [w * 64R, (w + 1) * 64R)
+// of the chunk (coalesced), ranks each record among its run's records of the same owner (ballots over
+// the 9 owner bits, a wave-private running count per owner), and after one workgroup scan per chunk
+// every record has its slot in its owner's list, in event order. The owner then folds its list.
 constexpr int kOwnT = 512;
-template <int R, int V>
-__global__ __launch_bounds__(kOwnT, 2) void k_aggregate_own(const Segment* __restrict__ segs, int P, int logP, int NL,
-                                                           AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter,
-                                                           unsigned char* flags, u32* rowref, i64* seg_rows,
+template <int V, int K, int R, int F>
+__global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restrict__ seg_off, int P, int logP,
+                                                           AggPlan ap, u64* rows, int RW, u32* row_counter,
+                                                           u32* first_bits, i64* seg_rows,
                                                            const u32* __restrict__ rec_pos,
                                                            const u32* __restrict__ rec_idx,
-                                                           const u64* __restrict__ rec_vals, i64 rec_cap,
-                                                           const i64* __restrict__ seg_off) {
+                                                           const u64* __restrict__ rec_vals, i64 rec_cap) {
     constexpr int W = kOwnT / 64;
-    constexpr int NQ = W * R;        // pieces per chunk
-    constexpr int CH = 64 * NQ;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    AggLds L;
-    lds_layout(smem_raw, ap, NL, L);
-    unsigned char* stg0 = (unsigned char*)(L.owner + NL);
-    unsigned char* stg = stg0 + ((16u - ((unsigned)(size_t)stg0 & 15u)) & 15u);
-    u64* st_v = (u64*)stg;                               // [V][CH]
-    u32* st_li = (u32*)(st_v + (size_t)V * CH);          // [CH]
-    u32* st_idx = st_li + CH;                            // [CH]
-    unsigned short* pc = (unsigned short*)(st_idx + CH); // [NQ][512]: count, then in-bucket offset
-    u32* bstart = (u32*)(pc + NQ * kOwnT);               // [512]
-
+    constexpr int PW = 64 * R;   // records per wave and chunk
+    constexpr int CH = kOwnT * R;
+    __shared__ u32 st_idx[CH];
+    __shared__ u64 st_v[V][CH];
+    __shared__ unsigned char st_hi[K > 1 ? CH : 1];
+    __shared__ unsigned short wcnt[W][kOwnT];  // per wave: running count per owner, then its offset
+    __shared__ u32 bstart[kOwnT];
+    __shared__ u32 base_row;
+    constexpr u32 kNone = 0xFFFFFFFFu;
     const int seg = blockIdx.x / P;
-    const int p = blockIdx.x % P;
+    const int p = blockIdx.x - seg * P;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    for (int i = t; i < NL; i += kOwnT) L.cnt[i] = 0;
     const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
-
-    // records of chunk c0 for this lane: piece q = j * W + w holds records q*64 .. q*64+63
-    u32 li[R], idx[R], rk[R];
-    i64 v[R][V];
-    u32 nli[R], nidx[R];
-    i64 nv[R][V];
-    auto load = [&](i64 c, u32 (&a)[R], u32 (&b)[R], i64 (&vals)[R][V]) {
-        const int n = (int)min((i64)CH, hi - c);
+    u32 cnt0 = 0, fst0 = 0, lst0 = 0, cnt1 = 0, fst1 = 0, lst1 = 0;
+    u64 f0[F], f1[F];
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-            const int r = (j * W + w) * 64 + lane;
-            const bool ok = r < n;
-            a[j] = ok ? (rec_pos[c + r] >> logP) : 0xFFFFFFFFu;
-            b[j] = ok ? rec_idx[c + r] : 0;
-#pragma unroll
-            for (int x = 0; x < V; x++)
-                vals[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c + r] : 0;
-        }
-    };
-    if (lo < hi) load(lo, li, idx, v);
+    for (int j = 0; j < F; j++) { f0[j] = 0; f1[j] = 0; }
     for (i64 c0 = lo; c0 < hi; c0 += CH) {
-        // (a) the next chunk's loads are issued now and land while this chunk is split and folded
-        if (c0 + CH < hi) load(c0 + CH, nli, nidx, nv);
-        for (int i = t; i < NQ * kOwnT / 8; i += kOwnT) ((uint4*)pc)[i] = make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        // (b) in-piece rank among lanes of the same bucket (li mod 512), per-piece bucket counts
+        const int n = (int)min((i64)CH, hi - c0);
+        // (a) the wave's run of the chunk, coalesced, into registers
+        u32 li[R], ix[R];
+        i64 v[R][V];
 #pragma unroll
         for (int j = 0; j < R; j++) {
-            const bool ok = li[j] != 0xFFFFFFFFu;
+            const int r = w * PW + j * 64 + lane;
+            const bool ok = r < n;
+            li[j] = ok ? (rec_pos[c0 + r] >> logP) : kNone;
+            ix[j] = ok ? rec_idx[c0 + r] : 0;
+#pragma unroll
+            for (int x = 0; x < V; x++) v[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c0 + r] : 0;
+        }
+        // (b) rank among the run's records of the same owner (the wave's LDS operations complete in
+        // program order, so the running counts need no barrier)
+#pragma unroll
+        for (int i = lane; i < kOwnT; i += 64) wcnt[w][i] = 0;
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+            const bool ok = li[j] != kNone;
+            const u32 b = li[j] & (kOwnT - 1);
             u64 peers = __ballot(ok);
 #pragma unroll
             for (int bt = 0; bt < 9; bt++) {
-                const bool bit = ok && ((li[j] >> bt) & 1);
+                const bool bit = ok && ((b >> bt) & 1);
                 const u64 mb = __ballot(bit);
                 peers &= bit ? mb : ~mb;
             }
-            rk[j] = (u32)__popcll(peers & lt_mask);
-            if (ok && rk[j] == 0) pc[(j * W + w) * kOwnT + (li[j] & (kOwnT - 1))] = (unsigned short)__popcll(peers);
+            const u32 lr = (u32)__popcll(peers & lt_mask);
+            const u32 base = ok ? wcnt[w][b] : 0;
+            if (ok && lr == 0) wcnt[w][b] = (unsigned short)(base + __popcll(peers));
+            // local key (< 1024) and its rank (< CH <= 4096) share the register from here on
+            if (ok) li[j] |= (base + lr) << 10;
         }
         __syncthreads();
-        // (c) bucket t: offsets over the pieces, then bucket starts over the buckets
+        // (c) owner t: offsets of the waves' runs in its list, then its list's start in the chunk
         u32 tot = 0;
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-            u32 c = pc[q * kOwnT + t];
-            pc[q * kOwnT + t] = (unsigned short)tot;
+        for (int x = 0; x < W; x++) {
+            const u32 c = wcnt[x][t];
+            wcnt[x][t] = (unsigned short)tot;
             tot += c;
         }
         i64 all;
-        const u32 my_start = (u32)block_excl_scan_any((i64)tot, &all);
-        bstart[t] = my_start;
+        const u32 start = (u32)block_excl_scan_any((i64)tot, &all);
+        bstart[t] = start;
         __syncthreads();
-        // (d) place every record in its owner's list
+        // (d) every record into its owner's list
 #pragma unroll
         for (int j = 0; j < R; j++) {
-            if (li[j] == 0xFFFFFFFFu) continue;
-            const int b = li[j] & (kOwnT - 1);
-            const u32 d = bstart[b] + pc[(j * W + w) * kOwnT + b] + rk[j];
-            st_li[d] = li[j];
-            st_idx[d] = idx[j];
+            if (li[j] == kNone) continue;
+            const u32 b = li[j] & (kOwnT - 1);
+            const u32 d = bstart[b] + wcnt[w][b] + (li[j] >> 10);
+            st_idx[d] = ix[j];
 #pragma unroll
-            for (int x = 0; x < V; x++) if (x < ap.n_vcols) st_v[(size_t)x * CH + d] = (u64)v[j][x];
-        }
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            li[j] = nli[j];
-            idx[j] = nidx[j];
-#pragma unroll
-            for (int x = 0; x < V; x++) v[j][x] = nv[j][x];
+            for (int x = 0; x < V; x++) st_v[x][d] = (u64)v[j][x];
+            if (K > 1) st_hi[d] = (unsigned char)((li[j] >> 9) & 1);
         }
         __syncthreads();
-        // (e) thread t folds its list in event order into the LDS state of its keys
-        for (u32 i = my_start; i < my_start + tot; i++) {
-            const u32 k = st_li[i];
-            const u32 ix = st_idx[i];
+        // (e) the owner folds its list in event order
+        for (u32 i = start; i < start + tot; i++) {
+            const u32 e = st_idx[i];
             i64 vv[V];
 #pragma unroll
-            for (int x = 0; x < V; x++) vv[x] = x < ap.n_vcols ? (i64)st_v[(size_t)x * CH + i] : 0;
-            const u32 c = L.cnt[k];
-            u64 f[SH_MAX_AGGS];
-#pragma unroll
-            for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = (j < ap.n_fields && c) ? L.fields[(size_t)j * NL + k] : 0;
-            fold_fields<V>(ap, f, c == 0, vv);
-#pragma unroll
-            for (int j = 0; j < SH_MAX_AGGS; j++) if (j < ap.n_fields) L.fields[(size_t)j * NL + k] = f[j];
-            if (c == 0) L.first[k] = ix;
-            L.last[k] = ix;
-            L.cnt[k] = c + 1;
+            for (int x = 0; x < V; x++) vv[x] = x < ap.n_vcols ? (i64)st_v[x][i] : 0;
+            if (K > 1 && st_hi[i]) {
+                fold_fields<V, F>(ap, f1, cnt1 == 0, vv);
+                if (cnt1 == 0) fst1 = e;
+                lst1 = e;
+                cnt1++;
+            } else {
+                fold_fields<V, F>(ap, f0, cnt0 == 0, vv);
+                if (cnt0 == 0) fst0 = e;
+                lst0 = e;
+                cnt0++;
+            }
         }
     }
+    // one row per key with events
+    const int mine = (cnt0 > 0) + (K > 1 && cnt1 > 0);
+    i64 tot;
+    const i64 pre = block_excl_scan_any((i64)mine, &tot);
+    if (t == 0) {
+        base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
+        if (tot) atomicAdd((unsigned long long*)&seg_rows[seg], (unsigned long long)tot);
+    }
     __syncthreads();
-    emit_rows(ap, L, NL, logP, p, seg, rows, row_vals, row_counter, flags, rowref, seg_rows);
+    u32 r = base_row + (u32)pre;
+    if (cnt0) {
+        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
+        mark_first(first_bits, fst0);
+        r++;
+    }
+    if (K > 1 && cnt1) {
+        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)(t + kOwnT) << logP) | (u32)p, cnt1, fst1, lst1, f1);
+        mark_first(first_bits, fst1);
+    }
 }
 
-constexpr int own_rounds(int V) { return V <= 2 ? 2 : 1; }
-
-size_t aggregate_own_lds(int NL, int n_fields, int n_vcols) {
-    n_vcols = n_vcols <= 1 ? 1 : n_vcols <= 2 ? 2 : n_vcols <= 4 ? 4 : 8;
-    const int R = own_rounds(n_vcols), NQ = (kOwnT / 64) * R, CH = 64 * NQ;
-    size_t state = (size_t)NL * (8 * n_fields + 16) + 16;
-    state = (state + 15) & ~(size_t)15;
-    return state + 16 + (size_t)CH * (8 * n_vcols + 8) + (size_t)NQ * kOwnT * 2 + kOwnT * 4 + 64;
-}
+int own_keys_per_thread(int NL) { return NL <= kOwnT ? 1 : 2; }
 
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
-                      AggPlan ap, RowTmp* rows, u64* row_vals, u32* row_counter, unsigned char* flags, u32* rowref,
-                      i64* seg_rows, const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap,
-                      const i64* seg_off) {
-    size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
-    if (rec_pos) {  // multisplit records: lane-ownership kernel (P >= 1)
-        lds = aggregate_own_lds(NL, ap.n_fields, ap.n_vcols);
-#define SH_AGG_OWN(VV)                                                                                           \
-    hipLaunchKernelGGL((k_aggregate_own<own_rounds(VV), VV>), dim3(nseg * P), dim3(kOwnT), lds, s, segs, P, logP, NL, ap, \
-                       rows, row_vals, row_counter, flags, rowref, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap, seg_off)
-        if (ap.n_vcols <= 1) SH_AGG_OWN(1);
-        else if (ap.n_vcols <= 2) SH_AGG_OWN(2);
-        else if (ap.n_vcols <= 4) SH_AGG_OWN(4);
-        else SH_AGG_OWN(8);
+                      AggPlan ap, u64* rows, int RW, u32* row_counter, u32* first_bits, i64* seg_rows,
+                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off) {
+    if (rec_pos) {  // multisplit records: thread-ownership kernel
+        const int K = own_keys_per_thread(NL);
+        const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
+#define SH_AGG_OWN(VV, KK, RR, FF)                                                                             \
+    hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP, ap, rows, \
+                       RW, row_counter, first_bits, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap)
+#define SH_AGG_OWN_F(VV, KK, RR)                          \
+    do {                                                  \
+        if (F == 2) SH_AGG_OWN(VV, KK, RR, 2);            \
+        else if (F == 4) SH_AGG_OWN(VV, KK, RR, 4);       \
+        else SH_AGG_OWN(VV, KK, RR, 8);                   \
+    } while (0)
+        if (K == 1) {
+            if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
+            else if (ap.n_vcols <= 2) SH_AGG_OWN_F(2, 1, 4);
+            else if (ap.n_vcols <= 4) SH_AGG_OWN_F(4, 1, 2);
+            else SH_AGG_OWN_F(8, 1, 1);
+        } else {
+            if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 2, 8);
+            else if (ap.n_vcols <= 2) SH_AGG_OWN_F(2, 2, 4);
+            else if (ap.n_vcols <= 4) SH_AGG_OWN_F(4, 2, 2);
+            else SH_AGG_OWN_F(8, 2, 1);
+        }
+#undef SH_AGG_OWN_F
 #undef SH_AGG_OWN
     } else {
+        size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
         hipLaunchKernelGGL(k_aggregate_flat, dim3(nseg), dim3(kBlock), lds, s, segs, NL, n_pend, pend_pos, pend_vals,
-                           pend_cap, new_pos, cols, ap, rows, row_vals, row_counter, flags, rowref, seg_rows);
+                           pend_cap, new_pos, cols, ap, rows, RW, row_counter, first_bits, seg_rows);
     }
 }
 
 // ================================================================================================
-// Ordering: a row's position is the rank of its first-occurrence index among all first indices.
+// Flag counts and single-workgroup scans (also used by the sliding path's row ordering).
 // ================================================================================================
 __global__ __launch_bounds__(kBlock) void k_count_flags(const unsigned char* __restrict__ flags, i64 n, i64* blk_cnt) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
@@ -705,62 +712,126 @@ void launch_scan_sum(hipStream_t s, i64* a, int n) {
     hipLaunchKernelGGL(k_scan_sum, dim3(1), dim3(1024), 0, s, a, n);
 }
 
-// Rank of each flagged first occurrence -> perm[rank] = row (tile-local scan + tile prefix).
-__global__ __launch_bounds__(kBlock) void k_emit_perm(const unsigned char* __restrict__ flags,
-                                                     const u32* __restrict__ rowref, i64 n,
-                                                     const i64* __restrict__ blk_pre, u32* perm) {
-    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
-    unsigned char fl[kItems];
+// Exclusive prefix of the popcounts of the first-occurrence bitmap, per 32-bit word.
+__global__ __launch_bounds__(kBlock) void k_bits_tile(const u32* __restrict__ bits, i64 nw, i64* tile_sum) {
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     i64 c = 0;
 #pragma unroll
-    for (int i = 0; i < kItems; i++) { fl[i] = base + i < n ? flags[base + i] : 0; c += fl[i]; }
-    i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + blk_pre[blockIdx.x];
-#pragma unroll
-    for (int i = 0; i < kItems; i++)
-        if (fl[i]) perm[r++] = rowref[base + i];
+    for (int i = 0; i < kItems; i++) if (base + i < nw) c += __popc(bits[base + i]);
+    const i64 t = block_reduce(c, SumOp(), 0);
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = t;
 }
 
-// One output row per thread, in output order: gather the row, its last event's timestamp and key.
-__global__ __launch_bounds__(kBlock) void k_emit_gather(const u32* __restrict__ perm, i64 n_rows,
-                                                       const RowTmp* __restrict__ rows,
-                                                       const u64* __restrict__ row_vals, int n_aggs, KeyTable kt,
-                                                       KeyPlan kp, i64 n_pend, const i64* __restrict__ pend_ts,
-                                                       const i64* __restrict__ ts, i64 out_cap, i64* out_ts,
-                                                       i64* out_keys, u64* out_vals, unsigned char* out_nulls,
-                                                       const u64* __restrict__ pend_gidx,
-                                                       const u64* __restrict__ new_gidx, i64* out_order,
-                                                       i64 seq_base, i64* out_rep) {
-    i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (o >= n_rows) return;
-    u32 row = perm[o];
-    RowTmp t = rows[row];
-    u64 k = slot_key(kt, t.pos);
-    out_ts[o] = t.last < n_pend ? pend_ts[t.last] : ts[t.last - n_pend];
+__global__ __launch_bounds__(kBlock) void k_bits_pre(const u32* __restrict__ bits, i64 nw, const i64* tile_pre,
+                                                    u32* word_pre) {
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    u32 b[kItems];
+    i64 c = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; i++) { b[i] = base + i < nw ? bits[base + i] : 0; c += __popc(b[i]); }
+    i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + tile_pre[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        if (base + i < nw) word_pre[base + i] = (u32)r;
+        r += __popc(b[i]);
+    }
+}
+
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre) {
+    const int nb = (int)((nw + kTile - 1) / kTile);
+    hipLaunchKernelGGL(k_bits_tile, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum);
+    launch_scan_sum(s, tile_sum, nb);
+    hipLaunchKernelGGL(k_bits_pre, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum, word_pre);
+}
+
+// Output rows are staged as records of stage_words(nk, na, order) u64 words at their output
+// position — ts, keys, representative event, [first event], values — so the rank scatter writes
+// whole 64-byte records and the column split (k_emit_soa) reads and writes contiguous runs.
+__host__ __device__ constexpr int stage_words(int nk, int na, int order) { return (2 + nk + order + na + 1) & ~1; }
+
+// Stage 1, one row record per thread: its output position is the rank of its first event's bit; the
+// row's timestamp and representative event are those of the key's last event, the key comes from the
+// slot.
+__global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
+                                                     const u32* __restrict__ n_rows_dev,
+                                                     const u32* __restrict__ bits, const u32* __restrict__ word_pre,
+                                                     int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
+                                                     const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
+                                                     const u64* __restrict__ pend_gidx,
+                                                     const u64* __restrict__ new_gidx, int want_order, i64 seq_base,
+                                                     u64* stage) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= (i64)*n_rows_dev) return;
+    const u64* row = rows + (size_t)r * RW;
+    const ulonglong2 h = *(const ulonglong2*)row;
+    const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
+    const u32 wd = first >> 5;
+    const i64 o = (i64)word_pre[wd] + __popc(bits[wd] & ((1u << (first & 31)) - 1u));
     // stream index of an event of the combined (queued + new) sequence
     auto sidx = [&](u32 c) -> i64 {
         if (c < n_pend) return (i64)pend_gidx[c];
         return new_gidx ? (i64)new_gidx[c - n_pend] : seq_base + (i64)(c - n_pend);
     };
-    if (out_order) out_order[o] = sidx(t.first);
-    out_rep[o] = sidx(t.last);
-    unpack_key(kp, k, out_keys + o, out_cap);
-    for (int a = 0; a < n_aggs; a++) {
-        out_vals[(size_t)a * out_cap + o] = row_vals[(size_t)row * n_aggs + a];
-        out_nulls[(size_t)a * out_cap + o] = 0;
+    const int nk = kp.n, SW = stage_words(nk, n_aggs, want_order);
+    u64 w[2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1];
+    w[0] = (u64)(last < n_pend ? pend_ts[last] : ts[last - n_pend]);
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, pos), kv, 1);
+    w[1] = (u64)sidx(last);
+    w[2] = (u64)kv[0];
+    w[3] = (u64)kv[1];
+    int c = 2 + nk;
+    if (want_order) w[c++] = (u64)sidx(first);
+#pragma unroll
+    for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) w[c + a] = row[2 + a];
+    u64* dst = stage + (size_t)o * SW;
+#pragma unroll
+    for (int i = 0; i < (2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1) / 2; i++) {
+        if (2 * i >= SW) break;
+        ((ulonglong2*)dst)[i] = make_ulonglong2(w[2 * i], w[2 * i + 1]);
     }
 }
 
-void launch_emit(hipStream_t s, const unsigned char* flags, const u32* rowref, i64 n, const i64* blk_pre, int nblk,
-                 u32* perm, i64 n_rows, const RowTmp* rows, const u64* row_vals, int n_aggs, KeyTable kt, KeyPlan kp,
-                 i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys,
-                 u64* out_vals, unsigned char* out_nulls, const u64* pend_gidx, const u64* new_gidx,
-                 i64* out_order, i64 seq_base, i64* out_rep) {
-    hipLaunchKernelGGL(k_emit_perm, dim3(nblk), dim3(kBlock), 0, s, flags, rowref, n, blk_pre, perm);
-    unsigned g = (unsigned)((n_rows + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_emit_gather, dim3(g), dim3(kBlock), 0, s, perm, n_rows, rows, row_vals, n_aggs, kt, kp,
-                       n_pend, pend_ts, ts, out_cap, out_ts, out_keys, out_vals, out_nulls, pend_gidx, new_gidx,
-                       out_order, seq_base, out_rep);
+// Stage 2, one output row per thread: the staged records split into the SoA output columns.
+__global__ __launch_bounds__(kBlock) void k_emit_soa(const u64* __restrict__ stage, const u32* __restrict__ n_rows_dev,
+                                                    int nk, int n_aggs, int want_order, i64 out_cap, i64* out_ts,
+                                                    i64* out_keys, u64* out_vals, i64* out_order, i64* out_rep) {
+    const i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 n = (i64)*n_rows_dev;  // the column stride of the output: [k][n_rows] as sh_out states
+    if (o >= n) return;
+    (void)out_cap;
+    const int SW = stage_words(nk, n_aggs, want_order);
+    const u64* src = stage + (size_t)o * SW;
+    u64 w[2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1];
+#pragma unroll
+    for (int i = 0; i < (2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1) / 2; i++) {
+        if (2 * i >= SW) break;
+        const ulonglong2 v = ((const ulonglong2*)src)[i];
+        w[2 * i] = v.x;
+        w[2 * i + 1] = v.y;
+    }
+    out_ts[o] = (i64)w[0];
+    out_rep[o] = (i64)w[1];
+    for (int k = 0; k < nk; k++) out_keys[(size_t)k * n + o] = (i64)w[2 + k];
+    int c = 2 + nk;
+    if (want_order) out_order[o] = (i64)w[c++];
+    for (int a = 0; a < n_aggs; a++) out_vals[(size_t)a * n + o] = w[c + a];
 }
+
+void launch_emit_rows(hipStream_t s, const u64* rows, int RW, i64 row_cap, const u32* n_rows_dev, const u32* bits,
+                      const u32* word_pre, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend, const i64* pend_ts,
+                      const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, const u64* pend_gidx,
+                      const u64* new_gidx, i64* out_order, i64 seq_base, i64* out_rep, u64* stage) {
+    if (row_cap <= 0) return;
+    const unsigned g = (unsigned)((row_cap + kBlock - 1) / kBlock);
+    const int want_order = out_order ? 1 : 0;
+    hipLaunchKernelGGL(k_emit_rank, dim3(g), dim3(kBlock), 0, s, rows, RW, n_rows_dev, bits, word_pre, n_aggs, kt, kp,
+                       n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
+    hipLaunchKernelGGL(k_emit_soa, dim3(g), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,
+                       out_ts, out_keys, out_vals, out_order, out_rep);
+}
+
+size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows) { return (size_t)stage_words(nk, na, order) * 8 * n_rows; }
 
 // ================================================================================================
 // k_compact_pending: passing events of the open window [e_lo, N) appended to the pending buffer
@@ -840,6 +911,7 @@ __device__ __forceinline__ int xcd_tile(int nblk) {
 __global__ __launch_bounds__(kBlock) void k_ms_count(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
                                                     const u32* __restrict__ new_pos, int P, i64* counts, int nblk) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(i64)P * nblk] = 0;  // the scan's total slot
     const int tile = xcd_tile(nblk);
     if (tile >= nblk) return;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
@@ -886,8 +958,18 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     u32* stage_pos = (u32*)(stage_vals + (size_t)ap.n_vcols * kTile);
     u32* stage_idx = stage_pos + kTile;
     u32* start = stage_idx + kTile;
-    unsigned short* run = (unsigned short*)(start + P);  // [NW][P]
+    i64* gbase = (i64*)(start + P + (P & 1));                // [P] global position of the tile's run - start
+    unsigned short* run = (unsigned short*)(gbase + P);  // [NW][P]
     for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
+    // the tile's run offsets (one per partition, strided by nblk in the [p][tile] scan): their loads
+    // are issued now and land while the tile is ranked
+    constexpr int kOffRegs = 4;
+    i64 off_reg[kOffRegs];
+#pragma unroll
+    for (int k = 0; k < kOffRegs; k++) {
+        const int i = threadIdx.x + k * kBlock;
+        off_reg[k] = i < P ? offsets[(i64)i * nblk + tile] : 0;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -943,6 +1025,13 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     }
     __syncthreads();
 #pragma unroll
+    for (int k = 0; k < kOffRegs; k++) {
+        const int i = threadIdx.x + k * kBlock;
+        if (i < P) gbase[i] = off_reg[k] - (i64)start[i];
+    }
+    for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = offsets[(i64)i * nblk + tile] - (i64)start[i];
+    __syncthreads();
+#pragma unroll
     for (int r = 0; r < kItems; r++) {
         if (my_pos[r] == kNoPos) continue;
         const u32 p = my_pos[r] & (P - 1);
@@ -962,7 +1051,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     const u32 n_tile = s_total;
     for (u32 j = threadIdx.x; j < n_tile; j += kBlock) {
         const u32 pp = stage_pos[j] & (P - 1);
-        const i64 dst = offsets[(i64)pp * nblk + tile] + (j - start[pp]);
+        const i64 dst = gbase[pp] + j;
         rec_pos[dst] = stage_pos[j];
         rec_idx[dst] = stage_idx[j];
         for (int v = 0; v < ap.n_vcols; v++) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
@@ -972,7 +1061,8 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
                        i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
-    size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + (size_t)P * 2 * (kBlock / 64) + 32;
+    size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
+                 (size_t)P * 2 * (kBlock / 64) + 32;
     int grid = ((nblk + 7) >> 3) * 8;
     hipLaunchKernelGGL(k_ms_scatter, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
                        new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);

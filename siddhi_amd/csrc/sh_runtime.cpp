@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -19,7 +20,16 @@ thread_local std::string g_last_error;
 
 int sh_fail(int code, const std::string& msg) {
     g_last_error = msg;
+    SH_TRACE("error %d: %s", code, msg.c_str());
     return code;
+}
+
+bool sh_trace_on() {
+    static const bool on = [] {
+        const char* e = getenv("SH_TRACE");
+        return e && *e && *e != '0';
+    }();
+    return on;
 }
 
 #define HIPCHK(x)                                                                                          \
@@ -299,13 +309,23 @@ KeyTable KeyTableHost::dev() const {
     return kt;
 }
 
-int KeyTableHost::check(hipStream_t s) {
-    uint32_t c[4] = {0, 0, 0, 0};
-    if (hipMemcpyAsync(c, ctrl.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+int KeyTableHost::check_async(hipStream_t s, uint32_t* pinned4) {
+    if (hipMemcpyAsync(pinned4, ctrl.p, 16, hipMemcpyDeviceToHost, s) != hipSuccess)
         return sh_fail(SH_ERR_DEVICE, "key table check failed");
+    return SH_OK;
+}
+
+int KeyTableHost::check_result(const uint32_t* c) {
     n_keys = c[0];
     if (c[2] == 2) return sh_fail(SH_ERR_INVALID, "dictionary id outside [0, key_capacity): raise key_capacity");
     if (c[2]) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
     return SH_OK;
+}
+
+int KeyTableHost::check(hipStream_t s) {
+    int rc = h_ctrl.reserve(16);
+    if (rc) return rc;
+    if ((rc = check_async(s, h_ctrl.as<uint32_t>()))) return rc;
+    if (hipStreamSynchronize(s) != hipSuccess) return sh_fail(SH_ERR_DEVICE, "key table check failed");
+    return check_result(h_ctrl.as<uint32_t>());
 }

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <string>
 #include <vector>
 
@@ -16,6 +17,17 @@ struct sh_ctx {
 };
 
 int sh_fail(int code, const std::string& msg);
+
+// SH_TRACE=1 in the environment: one stderr line per pipeline step (diagnostics only)
+bool sh_trace_on();
+#define SH_TRACE(...)                                    \
+    do {                                                 \
+        if (sh_trace_on()) {                             \
+            fprintf(stderr, "[sh] " __VA_ARGS__);        \
+            fputc('\n', stderr);                         \
+            fflush(stderr);                              \
+        }                                                \
+    } while (0)
 
 // The stream of the context whose API call is running on this thread. Device buffers grow and are
 // freed in that stream's order (hipMallocAsync / hipFreeAsync), so a growth never waits on other
@@ -61,6 +73,15 @@ struct PinnedBuf {
     PinnedBuf() = default;
     PinnedBuf(const PinnedBuf&) = delete;
     PinnedBuf& operator=(const PinnedBuf&) = delete;
+    PinnedBuf(PinnedBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+    PinnedBuf& operator=(PinnedBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p; cap = o.cap;
+            o.p = nullptr; o.cap = 0;
+        }
+        return *this;
+    }
     ~PinnedBuf() { release(); }
     int reserve(size_t n);
     void release();
@@ -70,6 +91,7 @@ struct PinnedBuf {
 // Open-addressing group-key table on the device (key -> position).
 struct KeyTableHost {
     DevBuf keys, ctrl;
+    PinnedBuf h_ctrl;  // landing area of check()
     size_t size_ = 0;
     int64_t n_keys = 0;  // keys inserted so far (read back by check)
     bool dense = false;  // dictionary ids: slot = (id - dadd) / dmul, no hashing
@@ -79,6 +101,9 @@ struct KeyTableHost {
     int init_size(size_t ts);
     shd::KeyTable dev() const;
     int check(hipStream_t s);
+    // check() in two halves: queue the counter copy into pinned memory, read it after a sync
+    int check_async(hipStream_t s, uint32_t* pinned4);
+    int check_result(const uint32_t* pinned4);
     void release() { keys.release(); ctrl.release(); }
 };
 
@@ -159,17 +184,35 @@ struct sh_query {
     int64_t seq = 0;  // stream index of the next event pushed (sh_out.rep numbering)
     DevBuf pend_pos, pend_ts, pend_vals;
     // scratch
-    DevBuf blk_pass, blk_tl, blk_first, blk_xm, info, bounds, segs, seg_rows, flags, rowref, rows, row_vals, counters,
-        out_ts, out_keys, out_vals, out_nulls, out_expired, out_rep, blk_cnt;
+    DevBuf blk_pass, blk_tl, blk_first, blk_xm, info, bounds, segs, seg_rows, rows, counters, out_ts, out_keys, out_vals,
+        out_nulls, out_expired, out_rep, blk_cnt;
+    DevBuf first_bits, word_pre;  // first-occurrence bitmap of the closed events and its word prefix
+    DevBuf emit_stage;            // output rows staged at their output position (k_emit_rank)
+    const void* zeroed_nulls = nullptr;    // out_nulls / out_expired buffers already zeroed
+    const void* zeroed_expired = nullptr;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
-    DevBuf new_pos, perm, seg_off;  // key slot per event of the push (kNoPos = filtered out); output permutation
+    DevBuf new_pos, seg_off;  // key slot per event of the push (kNoPos = filtered out); segment record offsets
     PushInfo* h_info = nullptr;
-    PinnedBuf h_up;  // pinned staging of small host->device uploads (segment lists)
+    PinnedBuf h_up;    // pinned segment list of the closed windows (read by the kernels in place)
+    PinnedBuf h_tail;  // pinned landing area of the push's final copies: key-table counters, rows per segment
+    PinnedBuf h_bounds;  // pinned landing area of the push's window boundaries
+    // the multisplit of the push's events, launched before the host reads the window boundaries
+    bool ms_ready = false;
+    int ms_nblk = 0;
+    int64_t rec_cap = 0;
+    // flush bookkeeping of the closed windows, completed after the push's final synchronisation
+    struct ClosedTail {
+        bool active = false, host_done = false;
+        int nseg = 0;
+        int64_t closed_hi = 0;
+        std::vector<int64_t> clocks, windows;
+    } tail;
     StagedBatch staged;
     OutHost out;
     sh_out dev_out{};
     std::vector<int64_t> dev_flush_offsets{0}, dev_flush_clock;
     hipEvent_t ev_push0 = nullptr, ev_push1 = nullptr, ev_agg0 = nullptr, ev_agg1 = nullptr;
+    hipEvent_t ev_mid = nullptr;  // the push info and boundaries are on the host (work queued after it runs on)
     sh_stats stats{};
     int64_t agg_bytes = 0;
     // per flush of the last push: window number (internal use by the aggregation root)
@@ -225,6 +268,7 @@ int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* co
                        const int64_t* gpm, const uint64_t* gidx, int64_t raw_base, int64_t send_size,
                        int64_t send_base, bool host_out, const sh_out** out, int64_t n_global);
 void sliding_destroy(sh_query* q);
-int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const shd::u32** rec_pos,
-                   const shd::u32** rec_idx, const shd::u64** rec_vals, int64_t* rec_cap);
+// stable multisplit of the combined events [0, hi) into the query's P key partitions: records
+// (q->rec_pos / rec_idx / rec_vals, capacity q->rec_cap), per-(partition, tile) offsets in q->ms_counts
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b);
 

@@ -85,28 +85,23 @@ static int grow_pending(sh_query* q, int64_t need, int64_t keep) {
 static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_override, sh_query** out);
 int query_set_partition(sh_query* q, int64_t key);
 
-// key partitions: smallest power of two whose per-partition LDS state (plus, when partitioned, the
-// record staging of k_aggregate_own) fits the budget that keeps two workgroups per CU
+// Key partitions: the smallest power of two P that leaves at most 512 local keys per partition (the
+// aggregation kernel's threads own one local key each, state in registers), as long as the
+// multisplit's per-tile LDS (staging + per-wave partition counters) fits a CU.
 static int size_partitions(sh_query* q) {
-    const size_t budget = 80 * 1024;
-    size_t ts = q->kt.size_;
-    int P = 1;
-    auto need = [&](int p) {
-        int nl = (int)(ts / p) + 1;
-        return p == 1 ? (size_t)nl * (16 + 8 * (size_t)q->ap.n_fields) + 16
-                      : aggregate_own_lds(nl, q->ap.n_fields, q->ap.n_vcols);
-    };
-    // the multisplit's per-tile LDS (staging + per-wave partition counters) must fit one CU too
+    const size_t ts = q->kt.size_;
     auto scatter_fits = [&](int p) {
         size_t v = (size_t)std::max(1, q->ap.n_vcols);
-        return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 12 + 64 <= 160 * 1024;
+        return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 20 + 64 <= 160 * 1024;
     };
-    while (need(P) > budget && P < 16384 && scatter_fits(P << 1)) P <<= 1;
-    if (need(P) > budget) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
+    int P = 1;
+    while (ts / P > 512 && P < 16384 && scatter_fits(P << 1)) P <<= 1;
+    if (ts / P > 512) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
     q->P = P;
     q->logP = 0;
     while ((1 << q->logP) < P) q->logP++;
-    q->NL = (int)(ts / P) + 1;
+    // local keys per partition: the hash table's sentinel slot (mask + 1) adds one to partition 0
+    q->NL = (int)(ts / P) + (q->kt.dense ? 0 : 1);
     return SH_OK;
 }
 
@@ -213,12 +208,17 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if ((rc = q->info.reserve(sizeof(PushInfo), false)) || (rc = q->counters.reserve(64, false))) { delete q; return rc; }
     (void)hipEventCreate(&q->ev_push0); (void)hipEventCreate(&q->ev_push1);
     (void)hipEventCreate(&q->ev_agg0); (void)hipEventCreate(&q->ev_agg1);
+    (void)hipEventCreateWithFlags(&q->ev_mid, hipEventDisableTiming);
     *out = q;
     return SH_OK;
 }
 
 // Aggregate the closed segments [segs[i].lo, segs[i].hi) of the combined (pending + new) sequence
-// and append one flush per non-empty segment.
+// and append one flush per non-empty segment. Device output: everything is queued on the stream and
+// the flush bookkeeping (rows per segment) completes in closed_finish after the push's final
+// synchronisation. Host output synchronises here for the row copies.
+static int closed_finish(sh_query* q, bool host_out);
+
 static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::vector<int64_t>& clocks,
                       const std::vector<int64_t>& windows, const sh_batch* b, bool host_out) {
     hipStream_t s = q->ctx->stream;
@@ -232,123 +232,144 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     int64_t row_cap = 0;
     for (auto& sg : segs) row_cap += std::min<int64_t>(sg.hi - sg.lo, (int64_t)q->kt.size_ + 1);
     row_cap = std::max<int64_t>(row_cap, 1);
-    RCHK(q->flags.reserve(closed_hi + 16, false));
-    RCHK(q->rowref.reserve((closed_hi + 16) * 4, false));
-    RCHK(q->rows.reserve(row_cap * sizeof(RowTmp), false));
-    RCHK(q->row_vals.reserve(row_cap * q->ap.n * 8, false));
-    RCHK(q->segs.reserve(nseg * sizeof(Segment), false));
-    RCHK(q->seg_rows.reserve(nseg * 8, false));
-    HIPCHK(hipMemsetAsync(q->flags.p, 0, closed_hi, s));
-    HIPCHK(hipMemsetAsync(q->seg_rows.p, 0, nseg * 8, s));
-    HIPCHK(hipMemsetAsync(q->counters.p, 0, 64, s));
+    const int na = q->ap.n, nk = q->kp.n, RW = row_words(na);
+    const int64_t n_words = (closed_hi >> 5) + 1;  // first-occurrence bitmap over the combined index space
+    RCHK(q->rows.reserve((size_t)row_cap * RW * 8, false));
+    RCHK(q->first_bits.reserve((size_t)n_words * 4, false));
+    // the row counter and the rows per segment share one zeroed block
+    RCHK(q->counters.reserve(64 + (size_t)nseg * 8, false));
+    int64_t* seg_rows_dev = (int64_t*)(q->counters.as<char>() + 64);
+    HIPCHK(hipMemsetAsync(q->first_bits.p, 0, (size_t)n_words * 4, s));
+    HIPCHK(hipMemsetAsync(q->counters.p, 0, 64 + (size_t)nseg * 8, s));
     // the segment list goes up from pinned memory (an async copy from pageable memory may read it
     // after this function returned)
     RCHK(q->h_up.reserve((size_t)nseg * sizeof(Segment)));
+    RCHK(q->segs.reserve(nseg * sizeof(Segment), false));
     std::memcpy(q->h_up.p, segs.data(), (size_t)nseg * sizeof(Segment));
     HIPCHK(hipMemcpyAsync(q->segs.p, q->h_up.p, nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
-    const u32* rec_pos = nullptr; const u32* rec_idx = nullptr; const u64* rec_vals = nullptr;
-    int64_t rec_cap = 0;
+    const Segment* dsegs = q->segs.as<Segment>();
     // One flat workgroup per segment walks every event of the segment, passing or not, and
-    // serialises a key's events in conflict rounds: fine for short batches, latency-bound for long
-    // windows of few keys or sparse partitions (R12 keeps one partition). Those take the compacting
-    // multisplit and the lane-ownership kernel even with one key partition.
-    const bool own = q->P > 1 || ((q->partitioned || closed_hi / nseg >= 65536) &&
-                                  aggregate_own_lds(q->NL, q->ap.n_fields, q->ap.n_vcols) <= 80 * 1024);
+    // serialises a key's events in conflict rounds: fine for short batches of few keys. Key
+    // partitions, long windows and sparse partitions (R12 keeps one partition) take the compacting
+    // multisplit (usually launched already by push_core) and the thread-ownership kernel.
+    const bool own = q->P > 1 || q->partitioned || closed_hi / nseg >= 65536;
+    SH_TRACE("run_closed nseg=%d closed_hi=%lld row_cap=%lld own=%d P=%d NL=%d ms_ready=%d", nseg, (long long)closed_hi,
+             (long long)row_cap, (int)own, q->P, q->NL, (int)q->ms_ready);
     if (own) {
-        RCHK(run_multisplit(q, closed_hi, b, &rec_pos, &rec_idx, &rec_vals, &rec_cap));
+        if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
-        int nblk = (int)((closed_hi + kTile - 1) / kTile);
-        launch_seg_offsets(s, q->segs.as<Segment>(), nseg, q->n_pend, q->pend_pos.as<u32>(),
-                           b ? q->new_pos.as<u32>() : nullptr, q->P, q->ms_counts.as<int64_t>(), nblk,
-                           q->seg_off.as<int64_t>());
+        launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), b ? q->new_pos.as<u32>() : nullptr, q->P,
+                           q->ms_counts.as<int64_t>(), q->ms_nblk, q->seg_off.as<int64_t>());
     }
+    // (the record buffers' addresses only after run_multisplit: it may have grown them)
+    const u32* rec_pos = q->rec_pos.as<u32>();
+    const u32* rec_idx = q->rec_idx.as<u32>();
+    const u64* rec_vals = q->rec_vals.as<u64>();
     HIPCHK(hipEventRecord(q->ev_agg0, s));
-    launch_aggregate(s, q->segs.as<Segment>(), nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(),
-                     q->pend_vals.as<u64>(), q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap,
-                     q->rows.as<RowTmp>(), q->row_vals.as<u64>(), q->counters.as<u32>(), q->flags.as<unsigned char>(),
-                     q->rowref.as<u32>(), q->seg_rows.as<int64_t>(), rec_pos, rec_idx, rec_vals, rec_cap,
-                     q->seg_off.as<int64_t>());
+    launch_aggregate(s, dsegs, nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(),
+                     q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
+                     q->counters.as<u32>(), q->first_bits.as<u32>(), seg_rows_dev,
+                     own ? rec_pos : nullptr, rec_idx, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
-    std::vector<int64_t> seg_rows(nseg);
-    HIPCHK(hipMemcpyAsync(seg_rows.data(), q->seg_rows.p, nseg * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    // output columns sized for the row capacity; the emit kernels read the row count on the device
+    const int64_t cap = row_cap;
+    RCHK(q->out_ts.reserve(cap * 8, false));
+    RCHK(q->out_keys.reserve(std::max(1, nk) * cap * 8, false));
+    RCHK(q->out_vals.reserve(na * cap * 8, false));
+    RCHK(q->out_nulls.reserve(na * cap, false));
+    RCHK(q->out_expired.reserve(cap, false));
+    RCHK(q->out_rep.reserve(cap * 8, false));
+    if (q->given) RCHK(q->out_order.reserve(cap * 8, false));
+    const int nbt = (int)((n_words + kTile - 1) / kTile);
+    RCHK(q->blk_cnt.reserve((nbt + 16) * 8, false));
+    RCHK(q->word_pre.reserve((size_t)n_words * 4, false));
+    RCHK(q->emit_stage.reserve(emit_stage_bytes(nk, na, q->given ? 1 : 0, cap), false));
+    launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u32>());
+    launch_emit_rows(s, q->rows.as<u64>(), RW, cap, q->counters.as<u32>(), q->first_bits.as<u32>(),
+                     q->word_pre.as<u32>(), na, q->kt.dev(), q->kp, q->n_pend, q->pend_ts.as<int64_t>(), ts, cap,
+                     q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->pend_gidx.as<u64>(),
+                     q->given && b ? q->given_gidx : nullptr, q->given ? q->out_order.as<int64_t>() : nullptr, q->seq,
+                     q->out_rep.as<int64_t>(), q->emit_stage.as<u64>());
+    // batch-window rows always have a value (count >= 1) and are CURRENT events: the null and
+    // expired flags are zeroed once per buffer, nothing here ever sets them
+    if (q->out_nulls.p != q->zeroed_nulls) {
+        HIPCHK(hipMemsetAsync(q->out_nulls.p, 0, q->out_nulls.cap, s));
+        q->zeroed_nulls = q->out_nulls.p;
+    }
+    if (q->out_expired.p != q->zeroed_expired) {
+        HIPCHK(hipMemsetAsync(q->out_expired.p, 0, q->out_expired.cap, s));
+        q->zeroed_expired = q->out_expired.p;
+    }
+    HIPCHK(hipGetLastError());
+    // rows per segment land in pinned memory with the push's final copies
+    RCHK(q->h_tail.reserve(16 + (size_t)nseg * 8));
+    HIPCHK(hipMemcpyAsync(q->h_tail.as<char>() + 16, seg_rows_dev, nseg * 8, hipMemcpyDeviceToHost, s));
+    auto& t = q->tail;
+    t.active = true;
+    t.host_done = false;
+    t.nseg = nseg;
+    t.closed_hi = closed_hi;
+    t.clocks = clocks;
+    t.windows = windows;
+    SH_TRACE("run_closed queued");
+    if (host_out) {
+        HIPCHK(hipStreamSynchronize(s));
+        RCHK(closed_finish(q, true));
+    }
+    return SH_OK;
+}
+
+// After the stream synchronised: rows per segment -> flush offsets / clocks; host output copies.
+static int closed_finish(sh_query* q, bool host_out) {
+    auto& t = q->tail;
+    if (!t.active || t.host_done) return SH_OK;
+    t.host_done = true;
+    hipStream_t s = q->ctx->stream;
+    const int64_t* seg_rows = (const int64_t*)(q->h_tail.as<char>() + 16);
+    const int na = q->ap.n, nk = q->kp.n;
+    int64_t n_rows = 0;
+    for (int i = 0; i < t.nseg; i++) n_rows += seg_rows[i];
     float agg_ms = 0;
     (void)hipEventElapsedTime(&agg_ms, q->ev_agg0, q->ev_agg1);
     q->stats.main_kernel_ms += agg_ms;
-    int64_t n_rows = 0;
-    for (auto r : seg_rows) n_rows += r;
     // algorithmic bytes of the aggregation kernel: every closed event's referenced columns + rows out
-    {
-        int64_t ev = closed_hi;
-        int64_t per = 4 + 8 * q->ap.n_vcols;  // key + values
-        q->agg_bytes += ev * per + n_rows * (int64_t)(sizeof(RowTmp) + 8 * q->ap.n);
-    }
-    int nk = q->kp.n, na = q->ap.n;
-    if (n_rows > 0) {
-        int64_t cap = n_rows;
-        RCHK(q->out_ts.reserve(cap * 8, false));
-        RCHK(q->out_keys.reserve(std::max(1, nk) * cap * 8, false));
-        RCHK(q->out_vals.reserve(na * cap * 8, false));
-        RCHK(q->out_nulls.reserve(na * cap, false));
-        RCHK(q->out_expired.reserve(cap, false));
-        RCHK(q->out_rep.reserve(cap * 8, false));
-        if (q->given) RCHK(q->out_order.reserve(cap * 8, false));
-        int nblk2 = (int)((closed_hi + kTile - 1) / kTile);
-        RCHK(q->blk_cnt.reserve(nblk2 * 8, false));
-        launch_count_flags(s, q->flags.as<unsigned char>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2);
-        launch_scan_sum(s, q->blk_cnt.as<int64_t>(), nblk2);
-        RCHK(q->perm.reserve(cap * 4, false));
-        launch_emit(s, q->flags.as<unsigned char>(), q->rowref.as<u32>(), closed_hi, q->blk_cnt.as<int64_t>(), nblk2,
-                    q->perm.as<u32>(), n_rows, q->rows.as<RowTmp>(), q->row_vals.as<u64>(), na, q->kt.dev(), q->kp,
-                    q->n_pend,
-                    q->pend_ts.as<int64_t>(), ts, cap, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(),
-                    q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>(), q->pend_gidx.as<u64>(),
-                    q->given && b ? q->given_gidx : nullptr, q->given ? q->out_order.as<int64_t>() : nullptr, q->seq,
-                    q->out_rep.as<int64_t>());
-        HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
-        HIPCHK(hipGetLastError());
-        if (host_out) {
-            size_t base = q->out.ts.size();
-            size_t nb = base + n_rows;
-            q->out.ts.resize(nb);
-            q->out.expired.resize(nb, 0);
-            q->out.rep.resize(nb);
-            HIPCHK(hipMemcpyAsync(q->out.ts.data() + base, q->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(q->out.rep.data() + base, q->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, s));
-            // keys / vals / nulls are [k][n] blocks; append per push into temporaries and interleave later
-            std::vector<int64_t> k(nk * n_rows);
-            std::vector<uint64_t> v(na * n_rows);
-            std::vector<uint8_t> nl(na * n_rows);
-            if (nk) HIPCHK(hipMemcpyAsync(k.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
-            if (q->given) {
-                size_t ob = q->order_host.size();
-                q->order_host.resize(ob + n_rows);
-                HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
-            }
-            HIPCHK(hipMemcpyAsync(v.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(nl.data(), q->out_nulls.p, na * n_rows, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            // q->out keeps rows grouped: store column blocks per push in pending vectors, merged in finish_out
-            q->out.keys.insert(q->out.keys.end(), k.begin(), k.end());
-            q->out.vals.insert(q->out.vals.end(), v.begin(), v.end());
-            q->out.nulls.insert(q->out.nulls.end(), nl.begin(), nl.end());
+    q->agg_bytes += t.closed_hi * (int64_t)(4 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 * row_words(na));
+    if (host_out && n_rows > 0) {
+        size_t base = q->out.ts.size();
+        size_t nb = base + n_rows;
+        q->out.ts.resize(nb);
+        q->out.expired.resize(nb, 0);
+        q->out.rep.resize(nb);
+        HIPCHK(hipMemcpyAsync(q->out.ts.data() + base, q->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(q->out.rep.data() + base, q->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+        // keys / vals / nulls are [k][n_rows] blocks (a push closes windows through run_closed at most once)
+        std::vector<int64_t> k(nk * n_rows);
+        std::vector<uint64_t> v(na * n_rows);
+        if (nk) HIPCHK(hipMemcpyAsync(k.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+        if (q->given) {
+            size_t ob = q->order_host.size();
+            q->order_host.resize(ob + n_rows);
+            HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
         }
+        HIPCHK(hipMemcpyAsync(v.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        q->out.keys.insert(q->out.keys.end(), k.begin(), k.end());
+        q->out.vals.insert(q->out.vals.end(), v.begin(), v.end());
+        q->out.nulls.insert(q->out.nulls.end(), (size_t)na * n_rows, 0);
     }
     // flush bookkeeping (one flush per non-empty closed segment)
     std::vector<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
     std::vector<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
     int64_t acc = fo.back();
-    for (int i = 0; i < nseg; i++) {
+    for (int i = 0; i < t.nseg; i++) {
         if (seg_rows[i] == 0) continue;
         acc += seg_rows[i];
         fo.push_back(acc);
-        fc.push_back(clocks[i]);
-        q->flush_window.push_back(windows[i]);
+        fc.push_back(t.clocks[i]);
+        q->flush_window.push_back(t.windows[i]);
     }
-    if (!host_out) {
-        q->dev_out.n_rows = n_rows;
-    }
+    if (!host_out) q->dev_out.n_rows = n_rows;
     return SH_OK;
 }
 
@@ -453,6 +474,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     q->stats = sh_stats{};
     q->agg_bytes = 0;
     q->order_host.clear();
+    q->ms_ready = false;
+    q->tail.active = false;
     int64_t N = b->n;
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
@@ -506,9 +529,21 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
                           q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
                           q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr);
         HIPCHK(hipGetLastError());
+        // the push info and the first boundaries come back in one copy; the key partitioning of the
+        // push's events (independent of where the windows close) is queued behind it and runs while
+        // the host reads them
+        constexpr int kFirstBounds = 256;
+        const int nb0 = std::min(kFirstBounds, max_bounds);
+        RCHK(q->h_bounds.reserve((size_t)nb0 * sizeof(Bound)));
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(q->ev_mid, s));
+        // (large pushes only: a small push usually closes no window, and then the split was wasted)
+        if ((q->P > 1 || q->partitioned) && N >= (1 << 18)) RCHK(run_multisplit(q, q->n_pend + N, b));
+        SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
+        HIPCHK(hipEventSynchronize(q->ev_mid));
         PushInfo info = *q->h_info;
+        SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
         if (info.n_bounds > max_bounds) return sh_fail(SH_ERR_INVALID, "more than 4M windows closed in one push");
         if (ext && info.err)
             return sh_fail(SH_ERR_UNSUPPORTED,
@@ -516,8 +551,12 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         if (ext) q->xm = std::max(q->xm, info.max_xm);
         std::vector<Bound> bounds(info.n_bounds);
         if (info.n_bounds) {
-            HIPCHK(hipMemcpyAsync(bounds.data(), q->bounds.p, info.n_bounds * sizeof(Bound), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
+            if (info.n_bounds <= nb0) {
+                std::memcpy(bounds.data(), q->h_bounds.p, info.n_bounds * sizeof(Bound));
+            } else {
+                HIPCHK(hipMemcpyAsync(bounds.data(), q->bounds.p, info.n_bounds * sizeof(Bound), hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
         if (!q->given) {
@@ -584,7 +623,14 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     }
     q->seq += N;
     HIPCHK(hipEventRecord(q->ev_push1, s));
-    RCHK(q->kt.check(s));
+    // the push's one final synchronisation: key-table counters and rows per segment
+    RCHK(q->h_tail.reserve(16));
+    RCHK(q->kt.check_async(s, q->h_tail.as<uint32_t>()));
+    SH_TRACE("push final sync");
+    HIPCHK(hipStreamSynchronize(s));
+    SH_TRACE("push done");
+    RCHK(q->kt.check_result(q->h_tail.as<uint32_t>()));
+    RCHK(closed_finish(q, host_out));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
     q->stats.push_ms = ms;
@@ -620,6 +666,8 @@ static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** 
     q->dev_flush_clock.clear();
     q->flush_window.clear();
     q->dev_out = sh_out{};
+    q->ms_ready = false;
+    q->tail.active = false;
     // TimestampGeneratorImpl.setCurrentTimestamp only moves the clock forward (:104-122)
     if (q->clock_valid && now < q->clock) { finish_out(q, host_out, out); return SH_OK; }
     q->clock = now;
@@ -631,6 +679,8 @@ static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** 
             std::vector<int64_t> clocks{now}, windows{q->W_open};
             RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
             q->n_pend = 0;
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+            RCHK(closed_finish(q, host_out));
         }
         q->W_open = std::max(q->W_open, W);
     }
@@ -655,17 +705,10 @@ extern "C" int sh_query_destroy(sh_query* q) {
     if (!q) return SH_OK;
     (void)hipStreamSynchronize(q->ctx->stream);
     if (q->kind == 1) sliding_destroy(q);
-    DevBuf* bufs[] = {&q->pend_pos, &q->pend_ts, &q->pend_vals, &q->blk_pass, &q->blk_tl, &q->blk_first, &q->blk_xm, &q->info,
-                      &q->bounds, &q->segs, &q->seg_rows, &q->flags, &q->rowref, &q->rows, &q->row_vals,
-                      &q->counters, &q->out_ts, &q->out_keys, &q->out_vals, &q->out_nulls, &q->out_expired,
-                      &q->blk_cnt, &q->ms_counts, &q->ms_tmp, &q->rec_pos, &q->rec_idx, &q->rec_vals,
-                      &q->part_off, &q->new_pos, &q->perm, &q->seg_off, &q->pend_gidx, &q->out_order};
-    for (DevBuf* bf : bufs) bf->release();
-    for (auto& c : q->staged.cols) c.release();
-    q->staged.ts.release();
+    // device buffers are released by their destructors (stream-ordered on this context)
     q->kt.release();
     if (q->h_info) (void)hipHostFree(q->h_info);
-    hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1};
+    hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1, q->ev_mid};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     delete q;
     return SH_OK;
@@ -677,39 +720,35 @@ extern "C" int sh_query_stats(sh_query* q, sh_stats* out) {
     return SH_OK;
 }
 
-// ---- multisplit: closed events of the push into P key partitions (stable) -----------------------
-int run_multisplit(sh_query* q, int64_t closed_hi, const sh_batch* b, const u32** rec_pos, const u32** rec_idx,
-                   const u64** rec_vals, int64_t* rec_cap) {
+// ---- multisplit: the combined events into P key partitions (stable) -------------------------------
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b) {
     hipStream_t s = q->ctx->stream;
     int P = q->P;
     ColSet cs{};
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
-    int nblk = (int)((closed_hi + kTile - 1) / kTile);
+    int nblk = (int)((hi + kTile - 1) / kTile);
     int64_t ncnt = (int64_t)P * nblk;
     RCHK(q->ms_counts.reserve((ncnt + 1) * 8, false));
     RCHK(q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false));
     RCHK(q->part_off.reserve((P + 1) * 8, false));
-    int64_t cap = std::max<int64_t>(closed_hi, 1);
+    int64_t cap = std::max<int64_t>(hi, 1);
     RCHK(q->rec_pos.reserve(cap * 4, false));
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
     const u32* np = b ? q->new_pos.as<u32>() : nullptr;
-    launch_ms_count(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<int64_t>(), nblk);
+    launch_ms_count(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<int64_t>(), nblk);
     // counts are laid out [p][blk]; one exclusive scan gives every (partition, block) its offset,
     // and partition p starts at offset[p * nblk]
-    HIPCHK(hipMemsetAsync(q->ms_counts.as<int64_t>() + ncnt, 0, 8, s));
+    // (k_ms_count zeroes the total slot counts[ncnt])
     launch_scan_sum_large(s, q->ms_counts.as<int64_t>(), ncnt + 1, q->ms_tmp.as<int64_t>());
-    launch_ms_scatter(s, 0, closed_hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs,
-                      q->ap, P, q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
+    launch_ms_scatter(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
+                      q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
                       q->rec_vals.as<u64>(), cap);
-    // part_off[p] = counts[p * nblk] (exclusive); part_off[P] = total
-    launch_part_off(s, q->ms_counts.as<int64_t>(), nblk, P, q->part_off.as<int64_t>());
     HIPCHK(hipGetLastError());
-    *rec_pos = q->rec_pos.as<u32>();
-    *rec_idx = q->rec_idx.as<u32>();
-    *rec_vals = q->rec_vals.as<u64>();
-    *rec_cap = cap;
+    q->ms_ready = true;
+    q->ms_nblk = nblk;
+    q->rec_cap = cap;
     return SH_OK;
 }
 
@@ -735,12 +774,16 @@ int query_close_given(sh_query* q, bool host_out, const sh_out** out) {
     q->flush_window.clear();
     q->dev_out = sh_out{};
     q->stats = sh_stats{};
+    q->ms_ready = false;
+    q->tail.active = false;
     if (q->given_W_end > q->W_open) {
         if (q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{given_flush_clock(q, q->W_open)}, windows{q->W_open};
             RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
             q->n_pend = 0;
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+            RCHK(closed_finish(q, host_out));
         }
         q->W_open = q->given_W_end;
     }

@@ -15,7 +15,7 @@ from typing import Callable, List, Optional
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsiddhi_hip.so")
+LIB_PATH = os.environ.get("SH_LIB", os.path.join(HERE, "libsiddhi_hip.so"))
 
 _lib = None
 
