@@ -153,19 +153,25 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr);
+// Rows of one aggregation unit — (segment, key partition) for the multisplit kernel, the segment for
+// the flat one — fill the unit's own region of agg_unit_rows() row slots; unit_rows[u] = its count.
+int agg_unit_rows(int P, int NL, bool own);
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
-                      AggPlan ap, u64* rows, int RW, u32* row_counter, u32* first_bits, i64* seg_rows,
+                      AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       // multisplit source (P > 1 or long windows; null: the flat kernel reads the batch)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
-void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre);
-// rows: row_cap bounds the grid, the row count is read on the device (the aggregation's counter)
-void launch_emit_rows(hipStream_t s, const u64* rows, int RW, i64 row_cap, const u32* n_rows_dev, const u32* bits,
-                      const u32* word_pre, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend, const i64* pend_ts,
-                      const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, const u64* pend_gidx,
-                      const u64* new_gidx, i64* out_order, i64 seq_base, i64* out_rep, u64* stage);
+// word_pre = exclusive popcount prefix of the first-occurrence bitmap; *total = the bitmap's popcount
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre, u32* total);
+// rows: the aggregation units' regions; the row count (for the output columns' stride) is read on
+// the device (launch_bits_prefix's total); row_cap bounds it
+void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_rows, i64 n_units, int unit_stride,
+                      i64 row_cap, const u32* n_rows_dev, const u32* bits, const u32* word_pre, int n_aggs, KeyTable kt,
+                      KeyPlan kp, i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts,
+                      i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
+                      i64 seq_base, i64* out_rep, u64* stage);
 size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows);
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,

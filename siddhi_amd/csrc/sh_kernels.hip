@@ -427,8 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
                                                           const u32* __restrict__ pend_pos,
                                                           const u64* __restrict__ pend_vals, i64 pend_cap,
                                                           const u32* __restrict__ new_pos, ColSet cols, AggPlan ap,
-                                                          u64* rows, int RW, u32* row_counter, u32* first_bits,
-                                                          i64* seg_rows) {
+                                                          u64* rows, int RW, u32* unit_rows, u32* first_bits) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     AggLds L;
     lds_layout(smem_raw, ap, NL, L);
@@ -478,13 +477,9 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
     for (int i = threadIdx.x; i < NL; i += blockDim.x) mine += L.cnt[i] > 0;
     i64 tot;
     i64 pre = block_excl_scan_any((i64)mine, &tot);
-    __shared__ u32 base_row;
-    if (threadIdx.x == 0) {
-        base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
-        if (tot) atomicAdd((unsigned long long*)&seg_rows[seg], (unsigned long long)tot);
-    }
-    __syncthreads();
-    u32 r = base_row + (u32)pre;
+    // the segment's rows fill its own region of NL row slots
+    if (threadIdx.x == 0) unit_rows[seg] = (u32)tot;
+    u32 r = (u32)seg * (u32)NL + (u32)pre;
     for (int i = threadIdx.x; i < NL; i += blockDim.x) {
         const u32 c = L.cnt[i];
         if (!c) continue;
@@ -508,8 +503,8 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
 constexpr int kOwnT = 512;
 template <int V, int K, int R, int F>
 __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restrict__ seg_off, int P, int logP,
-                                                           AggPlan ap, u64* rows, int RW, u32* row_counter,
-                                                           u32* first_bits, i64* seg_rows,
+                                                           AggPlan ap, u64* rows, int RW, u32* unit_rows,
+                                                           u32* first_bits,
                                                            const u32* __restrict__ rec_pos,
                                                            const u32* __restrict__ rec_idx,
                                                            const u64* __restrict__ rec_vals, i64 rec_cap) {
@@ -521,7 +516,6 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     __shared__ unsigned char st_hi[K > 1 ? CH : 1];
     __shared__ unsigned short wcnt[W][kOwnT];  // per wave: running count per owner, then its offset
     __shared__ u32 bstart[kOwnT];
-    __shared__ u32 base_row;
     constexpr u32 kNone = 0xFFFFFFFFu;
     const int seg = blockIdx.x / P;
     const int p = blockIdx.x - seg * P;
@@ -592,13 +586,33 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             if (K > 1) st_hi[d] = (unsigned char)((li[j] >> 9) & 1);
         }
         __syncthreads();
-        // (e) the owner folds its list in event order
-        for (u32 i = start; i < start + tot; i++) {
-            const u32 e = st_idx[i];
+        // (e) the owner folds its list in event order; the next record's LDS loads are issued before
+        // the current one is folded, so their latency overlaps the fold
+        u32 e_nx = 0;
+        i64 v_nx[V];
+        unsigned char hi_nx = 0;
+#pragma unroll
+        for (int x = 0; x < V; x++) v_nx[x] = 0;
+        if (tot) {
+            e_nx = st_idx[start];
+#pragma unroll
+            for (int x = 0; x < V; x++) if (x < ap.n_vcols) v_nx[x] = (i64)st_v[x][start];
+            if (K > 1) hi_nx = st_hi[start];
+        }
+        for (u32 k = 0; k < tot; k++) {
+            const u32 e = e_nx;
             i64 vv[V];
 #pragma unroll
-            for (int x = 0; x < V; x++) vv[x] = x < ap.n_vcols ? (i64)st_v[x][i] : 0;
-            if (K > 1 && st_hi[i]) {
+            for (int x = 0; x < V; x++) vv[x] = v_nx[x];
+            const unsigned char hi_cur = hi_nx;
+            if (k + 1 < tot) {
+                const u32 i = start + k + 1;
+                e_nx = st_idx[i];
+#pragma unroll
+                for (int x = 0; x < V; x++) if (x < ap.n_vcols) v_nx[x] = (i64)st_v[x][i];
+                if (K > 1) hi_nx = st_hi[i];
+            }
+            if (K > 1 && hi_cur) {
                 fold_fields<V, F>(ap, f1, cnt1 == 0, vv);
                 if (cnt1 == 0) fst1 = e;
                 lst1 = e;
@@ -611,16 +625,13 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             }
         }
     }
-    // one row per key with events
+    // one row per key with events, in the unit's own region of K * 512 row slots (no global counter:
+    // a contended atomic on one address would serialise every workgroup of the launch)
     const int mine = (cnt0 > 0) + (K > 1 && cnt1 > 0);
     i64 tot;
     const i64 pre = block_excl_scan_any((i64)mine, &tot);
-    if (t == 0) {
-        base_row = tot ? atomicAdd(row_counter, (u32)tot) : 0;
-        if (tot) atomicAdd((unsigned long long*)&seg_rows[seg], (unsigned long long)tot);
-    }
-    __syncthreads();
-    u32 r = base_row + (u32)pre;
+    if (t == 0) unit_rows[blockIdx.x] = (u32)tot;
+    u32 r = (u32)blockIdx.x * (u32)(K * kOwnT) + (u32)pre;
     if (cnt0) {
         write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
         mark_first(first_bits, fst0);
@@ -634,16 +645,18 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
 
 int own_keys_per_thread(int NL) { return NL <= kOwnT ? 1 : 2; }
 
+int agg_unit_rows(int P, int NL, bool own) { return own ? own_keys_per_thread(NL) * kOwnT : NL; }
+
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
-                      AggPlan ap, u64* rows, int RW, u32* row_counter, u32* first_bits, i64* seg_rows,
+                      AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off) {
     if (rec_pos) {  // multisplit records: thread-ownership kernel
         const int K = own_keys_per_thread(NL);
         const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
 #define SH_AGG_OWN(VV, KK, RR, FF)                                                                             \
     hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP, ap, rows, \
-                       RW, row_counter, first_bits, seg_rows, rec_pos, rec_idx, rec_vals, rec_cap)
+                       RW, unit_rows, first_bits, rec_pos, rec_idx, rec_vals, rec_cap)
 #define SH_AGG_OWN_F(VV, KK, RR)                          \
     do {                                                  \
         if (F == 2) SH_AGG_OWN(VV, KK, RR, 2);            \
@@ -666,7 +679,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
     } else {
         size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
         hipLaunchKernelGGL(k_aggregate_flat, dim3(nseg), dim3(kBlock), lds, s, segs, NL, n_pend, pend_pos, pend_vals,
-                           pend_cap, new_pos, cols, ap, rows, RW, row_counter, first_bits, seg_rows);
+                           pend_cap, new_pos, cols, ap, rows, RW, unit_rows, first_bits);
     }
 }
 
@@ -723,7 +736,7 @@ __global__ __launch_bounds__(kBlock) void k_bits_tile(const u32* __restrict__ bi
 }
 
 __global__ __launch_bounds__(kBlock) void k_bits_pre(const u32* __restrict__ bits, i64 nw, const i64* tile_pre,
-                                                    u32* word_pre) {
+                                                    u32* word_pre, u32* total) {
     const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     u32 b[kItems];
     i64 c = 0;
@@ -734,14 +747,15 @@ __global__ __launch_bounds__(kBlock) void k_bits_pre(const u32* __restrict__ bit
     for (int i = 0; i < kItems; i++) {
         if (base + i < nw) word_pre[base + i] = (u32)r;
         r += __popc(b[i]);
+        if (base + i == nw - 1) *total = (u32)r;  // every row's first event has one bit: the row count
     }
 }
 
-void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre) {
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre, u32* total) {
     const int nb = (int)((nw + kTile - 1) / kTile);
     hipLaunchKernelGGL(k_bits_tile, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum);
     launch_scan_sum(s, tile_sum, nb);
-    hipLaunchKernelGGL(k_bits_pre, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum, word_pre);
+    hipLaunchKernelGGL(k_bits_pre, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum, word_pre, total);
 }
 
 // Output rows are staged as records of stage_words(nk, na, order) u64 words at their output
@@ -753,15 +767,18 @@ __host__ __device__ constexpr int stage_words(int nk, int na, int order) { retur
 // row's timestamp and representative event are those of the key's last event, the key comes from the
 // slot.
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
-                                                     const u32* __restrict__ n_rows_dev,
+                                                     const u32* __restrict__ unit_rows, i64 n_units,
+                                                     int unit_stride,
                                                      const u32* __restrict__ bits, const u32* __restrict__ word_pre,
                                                      int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
                                                      const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
                                                      const u64* __restrict__ pend_gidx,
                                                      const u64* __restrict__ new_gidx, int want_order, i64 seq_base,
                                                      u64* stage) {
+    // thread (unit, j): the j-th row of a unit's region, if the unit produced that many
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= (i64)*n_rows_dev) return;
+    const i64 u = r / unit_stride;
+    if (u >= n_units || (u32)(r - u * unit_stride) >= unit_rows[u]) return;
     const u64* row = rows + (size_t)r * RW;
     const ulonglong2 h = *(const ulonglong2*)row;
     const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
@@ -818,16 +835,18 @@ __global__ __launch_bounds__(kBlock) void k_emit_soa(const u64* __restrict__ sta
     for (int a = 0; a < n_aggs; a++) out_vals[(size_t)a * n + o] = w[c + a];
 }
 
-void launch_emit_rows(hipStream_t s, const u64* rows, int RW, i64 row_cap, const u32* n_rows_dev, const u32* bits,
-                      const u32* word_pre, int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend, const i64* pend_ts,
-                      const i64* ts, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, const u64* pend_gidx,
-                      const u64* new_gidx, i64* out_order, i64 seq_base, i64* out_rep, u64* stage) {
-    if (row_cap <= 0) return;
-    const unsigned g = (unsigned)((row_cap + kBlock - 1) / kBlock);
+void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_rows, i64 n_units, int unit_stride,
+                      i64 row_cap, const u32* n_rows_dev, const u32* bits, const u32* word_pre, int n_aggs, KeyTable kt,
+                      KeyPlan kp, i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts,
+                      i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
+                      i64 seq_base, i64* out_rep, u64* stage) {
+    if (row_cap <= 0 || n_units <= 0) return;
     const int want_order = out_order ? 1 : 0;
-    hipLaunchKernelGGL(k_emit_rank, dim3(g), dim3(kBlock), 0, s, rows, RW, n_rows_dev, bits, word_pre, n_aggs, kt, kp,
-                       n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
-    hipLaunchKernelGGL(k_emit_soa, dim3(g), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,
+    const unsigned g1 = (unsigned)((n_units * unit_stride + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, bits, word_pre,
+                       n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
+    const unsigned g2 = (unsigned)((row_cap + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_emit_soa, dim3(g2), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,
                        out_ts, out_keys, out_vals, out_order, out_rep);
 }
 
@@ -936,13 +955,14 @@ void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_
 }
 
 // Stable multisplit of one tile of kTile closed events into the P key partitions. Wave w takes
-// the tile's events [w*512, w*512+512) in 8 rounds of 64 (coalesced loads); an event's rank inside
-// its partition is the wave's running count for that partition plus its rank among the round's
-// lanes of the same partition (ballots over the partition bits). Waves never wait for each other
-// until the tile is ranked: one barrier, a scan over (partition, wave) gives every event its
-// staging slot (partition-major, event order inside a partition), and the staged tile is written
-// out as one contiguous run per partition.
-// LDS: run[4][P] (u16) | start[P] (u32) | stage_pos[kTile] | stage_idx[kTile] | stage_vals[V][kTile]
+// the tile's events [w*512, w*512+512) in 8 rounds of 64; all 8 rounds' positions and values are
+// loaded first (one memory latency per tile). An event's rank inside its partition is the wave's
+// running count for that partition plus its rank among the round's lanes of the same partition
+// (ballots over the partition bits). One barrier, a scan over (partition, wave) gives every event
+// its staging slot (partition-major, event order inside a partition), and the staged tile is
+// written out as one contiguous run per partition.
+// LDS: stage_vals[V][kTile] | stage_pos[kTile] | stage_idx[kTile] | start[P] | gbase[P] (i64) | run[4][P] (u16)
+template <int V>
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
                                                       const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
@@ -955,14 +975,38 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     unsigned char* sm = smem_raw + ((16u - ((unsigned)(size_t)smem_raw & 15u)) & 15u);
     u64* stage_vals = (u64*)sm;
-    u32* stage_pos = (u32*)(stage_vals + (size_t)ap.n_vcols * kTile);
+    u32* stage_pos = (u32*)(stage_vals + (size_t)V * kTile);
     u32* stage_idx = stage_pos + kTile;
     u32* start = stage_idx + kTile;
     i64* gbase = (i64*)(start + P + (P & 1));                // [P] global position of the tile's run - start
     unsigned short* run = (unsigned short*)(gbase + P);  // [NW][P]
-    for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
-    // the tile's run offsets (one per partition, strided by nblk in the [p][tile] scan): their loads
-    // are issued now and land while the tile is ranked
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const i64 t0 = lo + (i64)tile * kTile + (i64)w * PER_WAVE;
+    // every round's position and values, and the tile's run offsets (one per partition, strided by
+    // nblk in the [p][tile] scan), requested before anything waits on them
+    u32 my_pos[kItems];
+    u64 my_val[kItems][V];
+#pragma unroll
+    for (int r = 0; r < kItems; r++) {
+        const i64 e = t0 + (i64)r * 64 + lane;
+        u32 pos = kNoPos;
+#pragma unroll
+        for (int j = 0; j < V; j++) my_val[r][j] = 0;
+        if (e < hi) {
+            if (e < n_pend) {
+                pos = pend_pos[e];
+#pragma unroll
+                for (int j = 0; j < V; j++)
+                    if (j < ap.n_vcols) my_val[r][j] = pend_vals[(size_t)j * pend_cap + e];
+            } else {
+                pos = new_pos[e - n_pend];
+#pragma unroll
+                for (int j = 0; j < V; j++)
+                    if (j < ap.n_vcols) my_val[r][j] = (u64)load_raw(cols, ap.vcol_src[j], e - n_pend);
+            }
+        }
+        my_pos[r] = pos;
+    }
     constexpr int kOffRegs = 4;
     i64 off_reg[kOffRegs];
 #pragma unroll
@@ -970,35 +1014,28 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         const int i = threadIdx.x + k * kBlock;
         off_reg[k] = i < P ? offsets[(i64)i * nblk + tile] : 0;
     }
+    for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
     __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int bits = 0;
     while ((1 << bits) < P) bits++;
-    const i64 t0 = lo + (i64)tile * kTile + (i64)w * PER_WAVE;
     unsigned short* wrun = run + w * P;
-    u32 my_pos[kItems], my_rank[kItems];
+    u32 my_rank[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
-        const i64 e = t0 + (i64)r * 64 + lane;
-        bool ok = false;
-        u32 pos = 0;
-        if (e < hi) {
-            EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
-            ok = ev.ok;
-            pos = ev.pos;
-        }
-        const u32 p = ok ? (pos & (P - 1)) : 0;
+        const bool ok = my_pos[r] != kNoPos;
+        const u32 p = ok ? (my_pos[r] & (P - 1)) : 0;
         u64 peers = __ballot(ok);
-        for (int bt = 0; bt < bits; bt++) {
+#pragma unroll
+        for (int bt = 0; bt < 14; bt++) {
+            if (bt >= bits) break;
             const bool bit = (p >> bt) & 1;
             const u64 m = __ballot(bit);
             peers &= bit ? m : ~m;
         }
         const u32 lr = (u32)__popcll(peers & lt_mask);
-        u32 base = ok ? wrun[p] : 0;  // the wave's LDS operations complete in program order
+        const u32 base = ok ? wrun[p] : 0;  // the wave's LDS operations complete in program order
         if (ok && lr == 0) wrun[p] = (unsigned short)(base + __popcll(peers));
-        my_pos[r] = ok ? pos : kNoPos;
         my_rank[r] = base + lr;
     }
     __syncthreads();
@@ -1030,21 +1067,16 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         if (i < P) gbase[i] = off_reg[k] - (i64)start[i];
     }
     for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = offsets[(i64)i * nblk + tile] - (i64)start[i];
-    __syncthreads();
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
         if (my_pos[r] == kNoPos) continue;
         const u32 p = my_pos[r] & (P - 1);
         const u32 slot = start[p] + wrun[p] + my_rank[r];
-        const i64 e = t0 + (i64)r * 64 + lane;
         stage_pos[slot] = my_pos[r];
-        stage_idx[slot] = (u32)e;
-        if (e < n_pend) {
-            for (int j = 0; j < ap.n_vcols; j++) stage_vals[(size_t)j * kTile + slot] = pend_vals[(size_t)j * pend_cap + e];
-        } else {
-            for (int j = 0; j < ap.n_vcols; j++)
-                stage_vals[(size_t)j * kTile + slot] = (u64)load_raw(cols, ap.vcol_src[j], e - n_pend);
-        }
+        stage_idx[slot] = (u32)(t0 + (i64)r * 64 + lane);
+#pragma unroll
+        for (int j = 0; j < V; j++)
+            if (j < ap.n_vcols) stage_vals[(size_t)j * kTile + slot] = my_val[r][j];
     }
     __syncthreads();
     // write every partition's run of this tile contiguously
@@ -1054,18 +1086,27 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         const i64 dst = gbase[pp] + j;
         rec_pos[dst] = stage_pos[j];
         rec_idx[dst] = stage_idx[j];
-        for (int v = 0; v < ap.n_vcols; v++) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
+#pragma unroll
+        for (int v = 0; v < V; v++)
+            if (v < ap.n_vcols) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
     }
 }
 
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
                        i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
-    size_t lds = (size_t)ap.n_vcols * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
+    const int V = ap.n_vcols <= 1 ? 1 : ap.n_vcols <= 2 ? 2 : ap.n_vcols <= 4 ? 4 : 8;
+    size_t lds = (size_t)V * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
                  (size_t)P * 2 * (kBlock / 64) + 32;
     int grid = ((nblk + 7) >> 3) * 8;
-    hipLaunchKernelGGL(k_ms_scatter, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap,
-                       new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap);
+#define SH_MS(VV)                                                                                                   \
+    hipLaunchKernelGGL(k_ms_scatter<VV>, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap, \
+                       new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap)
+    if (V == 1) SH_MS(1);
+    else if (V == 2) SH_MS(2);
+    else if (V == 4) SH_MS(4);
+    else SH_MS(8);
+#undef SH_MS
 }
 
 // three-phase exclusive scan for long arrays

@@ -203,7 +203,7 @@ struct sh_query {
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation
     struct ClosedTail {
         bool active = false, host_done = false;
-        int nseg = 0;
+        int nseg = 0, units_per_seg = 1;
         int64_t closed_hi = 0;
         std::vector<int64_t> clocks, windows;
     } tail;

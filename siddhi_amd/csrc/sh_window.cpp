@@ -91,7 +91,8 @@ int query_set_partition(sh_query* q, int64_t key);
 static int size_partitions(sh_query* q) {
     const size_t ts = q->kt.size_;
     auto scatter_fits = [&](int p) {
-        size_t v = (size_t)std::max(1, q->ap.n_vcols);
+        const int nv = q->ap.n_vcols;
+        size_t v = nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : 8;
         return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 20 + 64 <= 160 * 1024;
     };
     int P = 1;
@@ -234,13 +235,18 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     row_cap = std::max<int64_t>(row_cap, 1);
     const int na = q->ap.n, nk = q->kp.n, RW = row_words(na);
     const int64_t n_words = (closed_hi >> 5) + 1;  // first-occurrence bitmap over the combined index space
-    RCHK(q->rows.reserve((size_t)row_cap * RW * 8, false));
+    // One flat workgroup per segment walks every event of the segment, passing or not, and
+    // serialises a key's events in conflict rounds: fine for short batches of few keys. Key
+    // partitions, long windows and sparse partitions (R12 keeps one partition) take the compacting
+    // multisplit (usually launched already by push_core) and the thread-ownership kernel.
+    const bool own = q->P > 1 || q->partitioned || closed_hi / nseg >= 65536;
+    const int64_t n_units = own ? (int64_t)nseg * q->P : nseg;
+    const int unit_stride = agg_unit_rows(q->P, q->NL, own);
+    RCHK(q->rows.reserve((size_t)n_units * unit_stride * RW * 8, false));
     RCHK(q->first_bits.reserve((size_t)n_words * 4, false));
-    // the row counter and the rows per segment share one zeroed block
-    RCHK(q->counters.reserve(64 + (size_t)nseg * 8, false));
-    int64_t* seg_rows_dev = (int64_t*)(q->counters.as<char>() + 64);
+    RCHK(q->counters.reserve(64 + (size_t)n_units * 4, false));
+    uint32_t* unit_rows = (uint32_t*)(q->counters.as<char>() + 64);  // written by every unit's workgroup
     HIPCHK(hipMemsetAsync(q->first_bits.p, 0, (size_t)n_words * 4, s));
-    HIPCHK(hipMemsetAsync(q->counters.p, 0, 64 + (size_t)nseg * 8, s));
     // the segment list goes up from pinned memory (an async copy from pageable memory may read it
     // after this function returned)
     RCHK(q->h_up.reserve((size_t)nseg * sizeof(Segment)));
@@ -252,7 +258,6 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     // serialises a key's events in conflict rounds: fine for short batches of few keys. Key
     // partitions, long windows and sparse partitions (R12 keeps one partition) take the compacting
     // multisplit (usually launched already by push_core) and the thread-ownership kernel.
-    const bool own = q->P > 1 || q->partitioned || closed_hi / nseg >= 65536;
     SH_TRACE("run_closed nseg=%d closed_hi=%lld row_cap=%lld own=%d P=%d NL=%d ms_ready=%d", nseg, (long long)closed_hi,
              (long long)row_cap, (int)own, q->P, q->NL, (int)q->ms_ready);
     if (own) {
@@ -268,7 +273,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_aggregate(s, dsegs, nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(),
                      q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
-                     q->counters.as<u32>(), q->first_bits.as<u32>(), seg_rows_dev,
+                     unit_rows, q->first_bits.as<u32>(),
                      own ? rec_pos : nullptr, rec_idx, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>());
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
@@ -285,9 +290,11 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     RCHK(q->blk_cnt.reserve((nbt + 16) * 8, false));
     RCHK(q->word_pre.reserve((size_t)n_words * 4, false));
     RCHK(q->emit_stage.reserve(emit_stage_bytes(nk, na, q->given ? 1 : 0, cap), false));
-    launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u32>());
-    launch_emit_rows(s, q->rows.as<u64>(), RW, cap, q->counters.as<u32>(), q->first_bits.as<u32>(),
-                     q->word_pre.as<u32>(), na, q->kt.dev(), q->kp, q->n_pend, q->pend_ts.as<int64_t>(), ts, cap,
+    launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u32>(),
+                       q->counters.as<u32>());
+    launch_emit_rows(s, q->rows.as<u64>(), RW, unit_rows, n_units, unit_stride, cap, q->counters.as<u32>(),
+                     q->first_bits.as<u32>(), q->word_pre.as<u32>(), na, q->kt.dev(), q->kp, q->n_pend,
+                     q->pend_ts.as<int64_t>(), ts, cap,
                      q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->pend_gidx.as<u64>(),
                      q->given && b ? q->given_gidx : nullptr, q->given ? q->out_order.as<int64_t>() : nullptr, q->seq,
                      q->out_rep.as<int64_t>(), q->emit_stage.as<u64>());
@@ -302,13 +309,14 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         q->zeroed_expired = q->out_expired.p;
     }
     HIPCHK(hipGetLastError());
-    // rows per segment land in pinned memory with the push's final copies
-    RCHK(q->h_tail.reserve(16 + (size_t)nseg * 8));
-    HIPCHK(hipMemcpyAsync(q->h_tail.as<char>() + 16, seg_rows_dev, nseg * 8, hipMemcpyDeviceToHost, s));
+    // rows per unit land in pinned memory with the push's final copies
+    RCHK(q->h_tail.reserve(16 + (size_t)n_units * 4));
+    HIPCHK(hipMemcpyAsync(q->h_tail.as<char>() + 16, unit_rows, n_units * 4, hipMemcpyDeviceToHost, s));
     auto& t = q->tail;
     t.active = true;
     t.host_done = false;
     t.nseg = nseg;
+    t.units_per_seg = own ? q->P : 1;
     t.closed_hi = closed_hi;
     t.clocks = clocks;
     t.windows = windows;
@@ -326,7 +334,10 @@ static int closed_finish(sh_query* q, bool host_out) {
     if (!t.active || t.host_done) return SH_OK;
     t.host_done = true;
     hipStream_t s = q->ctx->stream;
-    const int64_t* seg_rows = (const int64_t*)(q->h_tail.as<char>() + 16);
+    const uint32_t* unit_rows = (const uint32_t*)(q->h_tail.as<char>() + 16);
+    std::vector<int64_t> seg_rows(t.nseg, 0);
+    for (int i = 0; i < t.nseg; i++)
+        for (int u = 0; u < t.units_per_seg; u++) seg_rows[i] += unit_rows[(size_t)i * t.units_per_seg + u];
     const int na = q->ap.n, nk = q->kp.n;
     int64_t n_rows = 0;
     for (int i = 0; i < t.nseg; i++) n_rows += seg_rows[i];
