@@ -20,3 +20,4 @@ for r in rows:
 PY
 cat "$OUT/bench.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', d['value'], 'ms/step', d['ms_per_step'])"
 cat "$OUT/stats.txt"
+python3 scripts/timeline.py "$OUT/kt" > "$OUT/timeline.txt" 2>&1 && tail -1 "$OUT/timeline.txt"

@@ -134,8 +134,12 @@ __device__ __forceinline__ bool eval_leaf(const FilterProg& f, int i, const ColS
     return java_cmp(f.ops[i + 2].op, cs.type[c], load_raw(cs, c, e), tc, vc);
 }
 
+// FK narrows the program forms a kernel instance handles (filter_kind on the host): 0 no filter,
+// 1 the register-only forms below, 2 any program. The narrow instances do not carry the stack
+// machine's registers.
+template <int FK = 2>
 __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& cs, i64 e) {
-    if (f.n == 0) return true;
+    if (FK == 0 || f.n == 0) return true;
     // register-only forms of the common programs (the branch is uniform: f is a kernel argument);
     // the general stack machine below keeps its operand stack in scratch memory
     if (f.n == 3 && is_leaf(f, 0)) return eval_leaf(f, 0, cs, e);
@@ -143,6 +147,7 @@ __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& c
         if (f.ops[6].op == SH_OP_AND) return eval_leaf(f, 0, cs, e) && eval_leaf(f, 3, cs, e);
         if (f.ops[6].op == SH_OP_OR) return eval_leaf(f, 0, cs, e) || eval_leaf(f, 3, cs, e);
     }
+    if (FK < 2) return false;  // not reached: filter_kind picked FK 1 for a register form
     i64 sv[16];
     int st[16];
     int sp = 0;
@@ -186,9 +191,13 @@ __device__ __forceinline__ void leaf_items(const FilterProg& f, int i, const Col
     for (int j = 0; j < kItems; j++) r[j] = java_cmp(op, ta, x[j], tc, vc);
 }
 
+template <int FK = 2>
 __device__ __forceinline__ void filter_items(const FilterProg& f, const ColSet& cs, i64 base, i64 N,
                                             bool (&pass)[kItems]) {
-    if (f.n == 3 && is_leaf(f, 0)) {
+    if (FK == 0) {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) pass[j] = true;
+    } else if (f.n == 3 && is_leaf(f, 0)) {
         leaf_items(f, 0, cs, base, N, pass);
     } else if (f.n == 7 && is_leaf(f, 0) && is_leaf(f, 3) && (f.ops[6].op == SH_OP_AND || f.ops[6].op == SH_OP_OR)) {
         bool a[kItems], b[kItems];
@@ -199,7 +208,7 @@ __device__ __forceinline__ void filter_items(const FilterProg& f, const ColSet& 
         for (int j = 0; j < kItems; j++) pass[j] = conj ? (a[j] && b[j]) : (a[j] || b[j]);
     } else {
 #pragma unroll
-        for (int j = 0; j < kItems; j++) pass[j] = base + j < N && eval_filter(f, cs, base + j);
+        for (int j = 0; j < kItems; j++) pass[j] = base + j < N && eval_filter<FK>(f, cs, base + j);
     }
 #pragma unroll
     for (int j = 0; j < kItems; j++) pass[j] = pass[j] && base + j < N;

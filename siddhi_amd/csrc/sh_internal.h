@@ -32,6 +32,19 @@ struct FilterProg {
     FilterOpD ops[kMaxFilterOps];
 };
 
+// Which kernel instance evaluates a filter program (eval_filter's FK): 0 none, 1 `col <cmp> const`
+// or two of those joined by AND / OR (evaluated in registers), 2 anything else (the stack machine).
+inline int filter_kind(const FilterProg& f) {
+    auto leaf = [&](int i) {
+        return f.ops[i].op == SH_OP_COL && f.ops[i + 1].op == SH_OP_CONST && f.ops[i + 2].op >= SH_OP_GT &&
+               f.ops[i + 2].op <= SH_OP_NE;
+    };
+    if (f.n == 0) return 0;
+    if (f.n == 3 && leaf(0)) return 1;
+    if (f.n == 7 && leaf(0) && leaf(3) && (f.ops[6].op == SH_OP_AND || f.ops[6].op == SH_OP_OR)) return 1;
+    return 2;
+}
+
 // Stream columns of one batch (device pointers) with their SH_T_* types.
 struct ColSet {
     const void* ptr[SH_MAX_COLS];

@@ -16,6 +16,7 @@ namespace shd {
 // k_blockagg: per workgroup (kTile events, blocked kItems per thread) the number of passing events,
 // the max timestamp over send-last events and the first passing event.
 // ================================================================================================
+template <int FK>
 __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                     WinParams wp, i64* blk_pass, i64* blk_tl, i64* blk_first,
                                                     i64* blk_xm) {
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(kBlock) void k_blockagg(const i64* __restrict__ ts,
     i64 tsv[kItems];
     load_items_i64(ts, base, wp.N, tsv, INT64_MIN);
     bool pass[kItems];
-    filter_items(f, cols, base, wp.N, pass);
+    filter_items<FK>(f, cols, base, wp.N, pass);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
@@ -55,8 +56,12 @@ void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i6
     wp.N = N;
     wp.send_size = send_size;
     wp.ts_col = ts_col;
-    hipLaunchKernelGGL(k_blockagg, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first,
-                       ts_col >= 0 ? blk_xm : nullptr);
+    i64* xm = ts_col >= 0 ? blk_xm : nullptr;
+    switch (filter_kind(f)) {
+        case 0: hipLaunchKernelGGL(k_blockagg<0>, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first, xm); break;
+        case 1: hipLaunchKernelGGL(k_blockagg<1>, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first, xm); break;
+        default: hipLaunchKernelGGL(k_blockagg<2>, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass, blk_tl, blk_first, xm);
+    }
 }
 
 // ================================================================================================
@@ -189,6 +194,7 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
 //                e's send. Due timers fire before the send is processed and catch up one period
 //                each (Scheduler.sendTimerEvents :171-209), so the window boundaries sit at E0 + kT.
 // ================================================================================================
+template <bool EXT, int FK>
 __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const PushInfo* info, Bound* bounds, int max_bounds,
@@ -196,21 +202,10 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
                                                       const i64* blk_xm_pre) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
-    i64 t[kItems];
-    i64 cnt = 0, tl = INT64_MIN;
-    load_items_i64(ts, base, wp.N, t, INT64_MIN);
-    filter_items(f, cols, base, wp.N, pass);
-    SendCursor sc(wp, base);
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-        i64 e = base + i;
-        bool in = e < wp.N;
-        cnt += pass[i];
-        if (in && sc.last(wp, e)) tl = max(tl, t[i]);
-        sc.next();
-    }
+    filter_items<FK>(f, cols, base, wp.N, pass);
     // group-key slot of every passing event, looked up once for the whole pipeline
-    // (GroupByKeyGenerator.constructEventKey, QuerySelector.java:331-336)
+    // (GroupByKeyGenerator.constructEventKey, QuerySelector.java:331-336); done before the timestamps
+    // are loaded so the lookup's registers and the window pass's are not live together
     {
         u64 key[kItems];
         u32 pos[kItems];
@@ -225,13 +220,33 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         }
         key_slots<kItems>(kt, key, pass, pos);
 #pragma unroll
-        for (int i = 0; i < kItems; i++)
-            if (base + i < wp.N) new_pos[base + i] = pass[i] ? pos[i] : kNoPos;
+        for (int i = 0; i < kItems; i++) pos[i] = pass[i] ? pos[i] : kNoPos;
+        if (base + kItems <= wp.N && (((size_t)(new_pos + base)) & 15) == 0) {
+            uint4* q = (uint4*)(new_pos + base);
+            q[0] = make_uint4(pos[0], pos[1], pos[2], pos[3]);
+            q[1] = make_uint4(pos[4], pos[5], pos[6], pos[7]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < kItems; i++)
+                if (base + i < wp.N) new_pos[base + i] = pos[i];
+        }
+    }
+    i64 t[kItems];
+    i64 cnt = 0, tl = INT64_MIN;
+    load_items_i64(ts, base, wp.N, t, INT64_MIN);
+    SendCursor sc(wp, base);
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        i64 e = base + i;
+        bool in = e < wp.N;
+        cnt += pass[i];
+        if (in && sc.last(wp, e)) tl = max(tl, t[i]);
+        sc.next();
     }
     i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x];
     i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
     // externalTimeBatch: running max of the timestamp attribute over the events reaching the window
-    const bool ext = wp.kind == SH_WIN_EXT_TIME_BATCH;
+    constexpr bool ext = EXT;  // externalTimeBatch (the running max M below)
     i64 av[kItems];
     i64 M = INT64_MIN;
     if (ext) {
@@ -254,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         clock_prev = c0;
     } else {
         i64 ep = base - 1;
-        bool pp = eval_filter(f, cols, ep);
+        bool pp = eval_filter<FK>(f, cols, ep);
         i64 pcb_prev = pcb - (pp ? 1 : 0);
         // ep and base in one send: ep's clock is that send's clock; else it closed the previous send
         if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
@@ -291,8 +306,16 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre) {
-    hipLaunchKernelGGL(k_boundaries, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass_pre, blk_tl_pre,
-                       info, bounds, max_bounds, (int*)&((PushInfo*)info)->n_bounds, kp, kt, new_pos, blk_xm_pre);
+    int* nb = (int*)&((PushInfo*)info)->n_bounds;
+#define SH_BOUNDS(EXT, FK)                                                                                      \
+    hipLaunchKernelGGL((k_boundaries<EXT, FK>), dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass_pre, \
+                       blk_tl_pre, info, bounds, max_bounds, nb, kp, kt, new_pos, blk_xm_pre)
+    const int fk = filter_kind(f);
+    if (wp.kind == SH_WIN_EXT_TIME_BATCH) SH_BOUNDS(true, 2);
+    else if (fk == 0) SH_BOUNDS(false, 0);
+    else if (fk == 1) SH_BOUNDS(false, 1);
+    else SH_BOUNDS(false, 2);
+#undef SH_BOUNDS
 }
 
 // ================================================================================================
@@ -663,8 +686,11 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
         else if (F == 4) SH_AGG_OWN(VV, KK, RR, 4);       \
         else SH_AGG_OWN(VV, KK, RR, 8);                   \
     } while (0)
+        static const int r_env = getenv("SH_OWN_R") ? atoi(getenv("SH_OWN_R")) : 8;  // chunk experiment
         if (K == 1) {
-            if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
+            if (ap.n_vcols <= 1 && r_env == 4) SH_AGG_OWN_F(1, 1, 4);
+            else if (ap.n_vcols <= 1 && r_env == 2) SH_AGG_OWN_F(1, 1, 2);
+            else if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
             else if (ap.n_vcols <= 2) SH_AGG_OWN_F(2, 1, 4);
             else if (ap.n_vcols <= 4) SH_AGG_OWN_F(4, 1, 2);
             else SH_AGG_OWN_F(8, 1, 1);
@@ -765,7 +791,10 @@ __host__ __device__ constexpr int stage_words(int nk, int na, int order) { retur
 
 // Stage 1, one row record per thread: its output position is the rank of its first event's bit; the
 // row's timestamp and representative event are those of the key's last event, the key comes from the
-// slot.
+// slot. The records of a wave are then stored cooperatively through LDS: consecutive lanes write
+// consecutive 16-byte pieces of one record, so each store instruction covers whole 64-byte records
+// instead of one piece of 64 scattered ones.
+constexpr int kStageMax = 2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1;
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
                                                      const u32* __restrict__ unit_rows, i64 n_units,
                                                      int unit_stride,
@@ -775,37 +804,51 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
                                                      const u64* __restrict__ pend_gidx,
                                                      const u64* __restrict__ new_gidx, int want_order, i64 seq_base,
                                                      u64* stage) {
+    __shared__ ulonglong2 sw[kBlock][kStageMax / 2];
+    __shared__ i64 so[kBlock];
     // thread (unit, j): the j-th row of a unit's region, if the unit produced that many
-    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const int t = threadIdx.x;
+    const i64 r = (i64)blockIdx.x * kBlock + t;
     const i64 u = r / unit_stride;
-    if (u >= n_units || (u32)(r - u * unit_stride) >= unit_rows[u]) return;
-    const u64* row = rows + (size_t)r * RW;
-    const ulonglong2 h = *(const ulonglong2*)row;
-    const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
-    const u32 wd = first >> 5;
-    const i64 o = (i64)word_pre[wd] + __popc(bits[wd] & ((1u << (first & 31)) - 1u));
-    // stream index of an event of the combined (queued + new) sequence
-    auto sidx = [&](u32 c) -> i64 {
-        if (c < n_pend) return (i64)pend_gidx[c];
-        return new_gidx ? (i64)new_gidx[c - n_pend] : seq_base + (i64)(c - n_pend);
-    };
+    const bool valid = u < n_units && (u32)(r - u * unit_stride) < unit_rows[u];
     const int nk = kp.n, SW = stage_words(nk, n_aggs, want_order);
-    u64 w[2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1];
-    w[0] = (u64)(last < n_pend ? pend_ts[last] : ts[last - n_pend]);
-    i64 kv[SH_MAX_GROUP] = {0, 0};
-    unpack_key(kp, slot_key(kt, pos), kv, 1);
-    w[1] = (u64)sidx(last);
-    w[2] = (u64)kv[0];
-    w[3] = (u64)kv[1];
-    int c = 2 + nk;
-    if (want_order) w[c++] = (u64)sidx(first);
+    so[t] = -1;
+    if (valid) {
+        const u64* row = rows + (size_t)r * RW;
+        const ulonglong2 h = *(const ulonglong2*)row;
+        const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
+        const u32 wd = first >> 5;
+        const i64 o = (i64)word_pre[wd] + __popc(bits[wd] & ((1u << (first & 31)) - 1u));
+        // stream index of an event of the combined (queued + new) sequence
+        auto sidx = [&](u32 c) -> i64 {
+            if (c < n_pend) return (i64)pend_gidx[c];
+            return new_gidx ? (i64)new_gidx[c - n_pend] : seq_base + (i64)(c - n_pend);
+        };
+        u64 w[kStageMax + 1];
+        w[0] = (u64)(last < n_pend ? pend_ts[last] : ts[last - n_pend]);
+        i64 kv[SH_MAX_GROUP] = {0, 0};
+        unpack_key(kp, slot_key(kt, pos), kv, 1);
+        w[1] = (u64)sidx(last);
+        w[2] = (u64)kv[0];
+        w[3] = (u64)kv[1];
+        int c = 2 + nk;
+        if (want_order) w[c++] = (u64)sidx(first);
 #pragma unroll
-    for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) w[c + a] = row[2 + a];
-    u64* dst = stage + (size_t)o * SW;
+        for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) w[c + a] = row[2 + a];
 #pragma unroll
-    for (int i = 0; i < (2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1) / 2; i++) {
-        if (2 * i >= SW) break;
-        ((ulonglong2*)dst)[i] = make_ulonglong2(w[2 * i], w[2 * i + 1]);
+        for (int i = 0; i < kStageMax / 2; i++) {
+            if (2 * i >= SW) break;
+            sw[t][i] = make_ulonglong2(w[2 * i], w[2 * i + 1]);
+        }
+        so[t] = o;
+    }
+    __syncthreads();
+    // the wave's 64 records as SW / 2 pieces each, piece-major across lanes
+    const int pcs = SW / 2, wb = t & ~63, lane = t & 63;
+    for (int q = lane; q < 64 * pcs; q += 64) {
+        const int rec = q / pcs, pc = q - rec * pcs;
+        const i64 o = so[wb + rec];
+        if (o >= 0) ((ulonglong2*)(stage + (size_t)o * SW))[pc] = sw[wb + rec][pc];
     }
 }
 
