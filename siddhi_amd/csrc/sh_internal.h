@@ -161,6 +161,8 @@ __host__ __device__ constexpr int row_words(int n_aggs) { return (2 + n_aggs + 1
 // Launchers (sh_kernels.hip).
 void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
                      i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, i64* blk_xm = nullptr, int ts_col = -1);
+// bytes of blk_first for launch_scan_blocks: the tiles' values, then the chunk totals
+size_t scan_blocks_first_bytes(int nblk);
 void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
                         WinParams wp, PushInfo* info, i64* blk_xm = nullptr, ColSet cols = ColSet{});
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
@@ -191,14 +193,15 @@ void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);
 // multisplit (partitioned aggregation, P > 1)
 void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
-                     i64* counts, int nblk);
+                     u32* counts, int nblk);
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets, int nblk,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
+void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const i64* counts, int nblk, i64* seg_off);
+                        const u32* new_pos, int P, const u32* counts, int nblk, i64* seg_off);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 // sharded ingest (sh_shard_kernels.hip)

@@ -75,63 +75,84 @@ void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i6
 struct Scan3 {
     i64 s, m, mn, x;  // sum, max, min, second max
 };
+template <bool XM = true>
 __device__ __forceinline__ Scan3 block1024_excl(Scan3 v, Scan3* tot) {
     __shared__ i64 w_sum[16], w_max[16], w_min[16], w_x[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const i64 si = wave_incl_scan(v.s, SumOp());
     const i64 mi = wave_incl_scan(v.m, MaxOp());
     const i64 ni = wave_incl_scan(v.mn, MinOp());
-    const i64 xi = wave_incl_scan(v.x, MaxOp());
+    const i64 xi = XM ? wave_incl_scan(v.x, MaxOp()) : INT64_MIN;
     if (lane == 63) { w_sum[wv] = si; w_max[wv] = mi; w_min[wv] = ni; w_x[wv] = xi; }
     __syncthreads();
     Scan3 pre{0, INT64_MIN, INT64_MAX, INT64_MIN}, all{0, INT64_MIN, INT64_MAX, INT64_MIN};
+    // not unrolled: all 64 LDS reads in flight at once would need 128 registers per thread
+#pragma unroll 2
     for (int x = 0; x < 16; x++) {
         if (x < wv) { pre.s += w_sum[x]; pre.m = max(pre.m, w_max[x]); pre.x = max(pre.x, w_x[x]); }
         all.s += w_sum[x]; all.m = max(all.m, w_max[x]); all.mn = min(all.mn, w_min[x]); all.x = max(all.x, w_x[x]);
     }
     __syncthreads();
     i64 mex = __shfl_up(mi, 1, 64);
-    i64 xex = __shfl_up(xi, 1, 64);
+    i64 xex = XM ? __shfl_up(xi, 1, 64) : INT64_MIN;
     if (lane == 0) { mex = INT64_MIN; xex = INT64_MIN; }
     *tot = all;
     return Scan3{pre.s + si - v.s, max(pre.m, mex), 0, max(pre.x, xex)};
 }
 
-__global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk,
+// Two launches of one workgroup per chunk of 1024 tiles (thread t takes tile c*1024 + t: coalesced).
+// k_scan_chunks reduces each chunk to its totals {sum, max, min, second max}, stored after the
+// tiles' first-event column (blk_first + nblk, see scan_blocks_first_bytes); k_scan_blocks scans
+// each chunk offset by the totals of the chunks before it (uniform loads). A single workgroup looping
+// over the chunks was latency-bound: its stores sat in the same in-order counter as the next
+// chunk's loads.
+template <bool XM>
+__global__ __launch_bounds__(1024) void k_scan_chunks(const i64* blk_pass, const i64* blk_tl, i64* blk_first,
+                                                     int nblk, const i64* blk_xm) {
+    const int i = blockIdx.x * 1024 + threadIdx.x;
+    const bool in = i < nblk;
+    Scan3 v{in ? blk_pass[i] : 0, in ? blk_tl[i] : INT64_MIN, in ? blk_first[i] : INT64_MAX,
+            (XM && in) ? blk_xm[i] : INT64_MIN};
+    Scan3 all;
+    block1024_excl<XM>(v, &all);
+    if (threadIdx.x == 0) {
+        i64* ct = blk_first + nblk + 4 * (i64)blockIdx.x;
+        ct[0] = all.s; ct[1] = all.m; ct[2] = all.mn; ct[3] = all.x;
+    }
+}
+
+template <bool XM>
+__global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl, const i64* blk_first, int nblk,
                                                      const i64* __restrict__ ts, WinParams wp, PushInfo* info,
                                                      i64* blk_xm, ColSet cols) {
-    // thread t owns the contiguous tiles [t*per, t*per + per): a serial fold, ONE workgroup scan,
-    // then the serial write-back of the exclusive prefixes (16 tiles per thread at N = 2^25);
-    // 115 -> 66 us per push at N = 2^25 against 16 chained workgroup scans (bound by this one CU's
-    // memory pipe: per-thread contiguous runs are strided across lanes)
-    const int t = threadIdx.x;
-    const int per = (nblk + 1023) / 1024;
-    const int lo = min(nblk, t * per), hi = min(nblk, lo + per);
-    Scan3 v{0, INT64_MIN, INT64_MAX, INT64_MIN};
-    for (int i = lo; i < hi; i++) {
-        v.s += blk_pass[i];
-        v.m = max(v.m, blk_tl[i]);
-        v.mn = min(v.mn, blk_first[i]);
-        if (blk_xm) v.x = max(v.x, blk_xm[i]);
+    const int t = threadIdx.x, c = blockIdx.x, nch = (nblk + 1023) / 1024;
+    const int i = c * 1024 + t;
+    const bool in = i < nblk;
+    Scan3 v{in ? blk_pass[i] : 0, in ? blk_tl[i] : INT64_MIN, INT64_MAX, (XM && in) ? blk_xm[i] : INT64_MIN};
+    const i64* ct = blk_first + nblk;
+    Scan3 pre{0, INT64_MIN, INT64_MAX, INT64_MIN}, all{0, INT64_MIN, INT64_MAX, INT64_MIN};
+    for (int k = 0; k < nch; k++) {
+        const i64 a0 = ct[4 * k], a1 = ct[4 * k + 1], a2 = ct[4 * k + 2], a3 = ct[4 * k + 3];
+        if (k < c) { pre.s += a0; pre.m = max(pre.m, a1); pre.x = max(pre.x, a3); }
+        all.s += a0; all.m = max(all.m, a1); all.mn = min(all.mn, a2); all.x = max(all.x, a3);
     }
-    Scan3 all;
-    const Scan3 ex = block1024_excl(v, &all);
-    i64 rs = ex.s, rm = ex.m, rx = ex.x;
-    for (int i = lo; i < hi; i++) {
-        const i64 a = blk_pass[i], b = blk_tl[i];
-        blk_pass[i] = rs;
-        blk_tl[i] = rm;
-        rs += a;
-        rm = max(rm, b);
-        if (blk_xm) {
-            const i64 c = blk_xm[i];
-            blk_xm[i] = rx;
-            rx = max(rx, c);
-        }
+    Scan3 call;
+    const Scan3 ex = block1024_excl<XM>(v, &call);
+    const i64 my_pm = max(pre.m, ex.m);  // exclusive prefix max of tile i
+    if (in) {
+        blk_pass[i] = pre.s + ex.s;
+        blk_tl[i] = my_pm;
+        if (XM) blk_xm[i] = max(pre.x, ex.x);
     }
     const i64 tot_s = all.s, tot_m = all.m, tot_mn = all.mn, tot_x = all.x;
-    __syncthreads();
-    if (t == 0) {
+    // the push info is written by one thread: the one holding the tile of the send that carries the
+    // first passing event when that send's clock is needed, else thread 0 of chunk 0
+    const bool init_e0 = wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && !wp.wcol;
+    const bool need_clk = tot_mn != INT64_MAX && (init_e0 || wp.want_first_clk);
+    const i64 sl = wp.send_size > 0 ? wp.send_size : wp.N;
+    const i64 start = need_clk ? (tot_mn / sl) * sl : 0;
+    const int b0 = (int)(start / kTile);
+    if (need_clk ? i == b0 : i == 0) {
         info->total_pass = tot_s;
         info->max_tl = tot_m;
         info->first_pass = tot_mn;
@@ -151,27 +172,22 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
             info->e0_valid = 1;
             if (a < st || st < 0) info->err = 1;
         }
-        const bool init_e0 = wp.kind == SH_WIN_TIME_BATCH && !wp.e0_valid && !wp.wcol;
-        if (tot_mn != INT64_MAX && (init_e0 || wp.want_first_clk)) {
+        if (need_clk) {
             // clock of the send that carries the first passing event (before the carried-in clock)
-            i64 e0 = tot_mn;
-            i64 sl = wp.send_size > 0 ? wp.send_size : wp.N;
-            i64 start = (e0 / sl) * sl;
-            i64 last = min(wp.N - 1, start + sl - 1);
-            int b0 = (int)(start / kTile);
-            i64 pm = blk_tl[b0];  // now the exclusive prefix max of block b0
+            const i64 last = min(wp.N - 1, start + sl - 1);
+            i64 pm = my_pm;  // the exclusive prefix max of tile b0
             for (i64 e = (i64)b0 * kTile; e < start; e++)
                 if (is_send_last(wp, e)) pm = max(pm, ts[e]);
-            i64 c = max(pm, ts[last]);
-            info->first_clk = c;
+            i64 cl = max(pm, ts[last]);
+            info->first_clk = cl;
             if (init_e0) {
-                if (wp.clock_valid) c = max(c, wp.clock0);
+                if (wp.clock_valid) cl = max(cl, wp.clock0);
                 i64 E0;
                 if (wp.has_start) {
-                    i64 elapsed = (c - wp.start_time) % wp.T;  // Java % truncates like C++
-                    E0 = c + (wp.T - elapsed);
+                    i64 elapsed = (cl - wp.start_time) % wp.T;  // Java % truncates like C++
+                    E0 = cl + (wp.T - elapsed);
                 } else {
-                    E0 = c + wp.T;
+                    E0 = cl + wp.T;
                 }
                 info->E0 = E0;
                 info->e0_valid = 1;
@@ -180,10 +196,21 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
     }
 }
 
+size_t scan_blocks_first_bytes(int nblk) { return ((size_t)nblk + 4 * (size_t)((nblk + 1023) / 1024)) * 8; }
+
 void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
                         WinParams wp, PushInfo* info, i64* blk_xm, ColSet cols) {
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, ts, wp, info,
-                       wp.kind == SH_WIN_EXT_TIME_BATCH ? blk_xm : nullptr, cols);
+    const int nch = (nblk + 1023) / 1024;
+    if (wp.kind == SH_WIN_EXT_TIME_BATCH) {
+        hipLaunchKernelGGL(k_scan_chunks<true>, dim3(nch), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, blk_xm);
+        hipLaunchKernelGGL(k_scan_blocks<true>, dim3(nch), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, ts, wp,
+                           info, blk_xm, cols);
+    } else {
+        hipLaunchKernelGGL(k_scan_chunks<false>, dim3(nch), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk,
+                           nullptr);
+        hipLaunchKernelGGL(k_scan_blocks<false>, dim3(nch), dim3(1024), 0, s, blk_pass, blk_tl, blk_first, nblk, ts, wp,
+                           info, nullptr, cols);
+    }
 }
 
 // ================================================================================================
@@ -352,12 +379,27 @@ __device__ __forceinline__ i64 pick(const i64 (&v)[V], int j) {
 // slot j: the per-event updates driven by the per-field op table (sums: sum += x / value += (double) x;
 // min/max: replace when the state is new or x is smaller / larger in the column's type —
 // MinAttributeAggregatorExecutor `minValue > value`).
-template <int V, int F = SH_MAX_AGGS>
+// SIG != 0 is a compile-time op table (agg_sig): 4 bits per field, op + 1, so the folds of the common
+// plans carry no per-field dispatch.
+__host__ __device__ constexpr int sig_op(u32 sig, int j) { return (int)((sig >> (4 * j)) & 15u) - 1; }
+__host__ __device__ constexpr int sig_fields(u32 sig) { return sig == 0 ? 0 : 1 + sig_fields(sig >> 4); }
+constexpr u32 agg_sig3(int a, int b, int c) {
+    return (u32)(a + 1) | ((u32)(b + 1) << 4) | ((u32)(c + 1) << 8);
+}
+// the plan's op table as a signature (0 when it has no field or more than 4)
+inline u32 agg_sig(const AggPlan& ap) {
+    if (ap.n_fields < 1 || ap.n_fields > 4) return 0;
+    u32 s = 0;
+    for (int j = 0; j < ap.n_fields; j++) s |= (u32)(ap.fop[j] + 1) << (4 * j);
+    return s;
+}
+
+template <int V, int F = SH_MAX_AGGS, u32 SIG = 0>
 __device__ __forceinline__ void fold_fields(const AggPlan& ap, u64 (&f)[F], bool first, const i64 (&v)[V]) {
 #pragma unroll
     for (int j = 0; j < F; j++) {
-        if (j >= ap.n_fields) break;
-        const int op = ap.fop[j];
+        if (j >= (SIG ? sig_fields(SIG) : ap.n_fields)) break;
+        const int op = SIG ? sig_op(SIG, j) : ap.fop[j];
         const i64 x = pick<V>(v, ap.fvcol[j]);
         const u64 cur = f[j];
         u64 r;
@@ -524,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
 // the 9 owner bits, a wave-private running count per owner), and after one workgroup scan per chunk
 // every record has its slot in its owner's list, in event order. The owner then folds its list.
 constexpr int kOwnT = 512;
-template <int V, int K, int R, int F>
+template <int V, int K, int R, int F, u32 SIG>
 __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restrict__ seg_off, int P, int logP,
                                                            AggPlan ap, u64* rows, int RW, u32* unit_rows,
                                                            u32* first_bits,
@@ -537,13 +579,12 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     __shared__ u32 st_idx[CH];
     __shared__ u64 st_v[V][CH];
     __shared__ unsigned char st_hi[K > 1 ? CH : 1];
-    __shared__ unsigned short wcnt[W][kOwnT];  // per wave: running count per owner, then its offset
+    __shared__ u32 wcnt[W][kOwnT];  // per wave: running count per owner, then its offset
     __shared__ u32 bstart[kOwnT];
     constexpr u32 kNone = 0xFFFFFFFFu;
     const int seg = blockIdx.x / P;
     const int p = blockIdx.x - seg * P;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
     u32 cnt0 = 0, fst0 = 0, lst0 = 0, cnt1 = 0, fst1 = 0, lst1 = 0;
     u64 f0[F], f1[F];
@@ -563,26 +604,17 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
 #pragma unroll
             for (int x = 0; x < V; x++) v[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c0 + r] : 0;
         }
-        // (b) rank among the run's records of the same owner (the wave's LDS operations complete in
-        // program order, so the running counts need no barrier)
+        // (b) rank among the run's records of the same owner: a wave-private running count per owner,
+        // advanced by LDS atomics (the wave's rounds complete in program order; lanes of one round
+        // that share an owner get distinct ranks, in an order (e) restores)
 #pragma unroll
         for (int i = lane; i < kOwnT; i += 64) wcnt[w][i] = 0;
 #pragma unroll
         for (int j = 0; j < R; j++) {
-            const bool ok = li[j] != kNone;
-            const u32 b = li[j] & (kOwnT - 1);
-            u64 peers = __ballot(ok);
-#pragma unroll
-            for (int bt = 0; bt < 9; bt++) {
-                const bool bit = ok && ((b >> bt) & 1);
-                const u64 mb = __ballot(bit);
-                peers &= bit ? mb : ~mb;
-            }
-            const u32 lr = (u32)__popcll(peers & lt_mask);
-            const u32 base = ok ? wcnt[w][b] : 0;
-            if (ok && lr == 0) wcnt[w][b] = (unsigned short)(base + __popcll(peers));
+            if (li[j] == kNone) continue;
+            const u32 rk = atomicAdd(&wcnt[w][li[j] & (kOwnT - 1)], 1u);
             // local key (< 1024) and its rank (< CH <= 4096) share the register from here on
-            if (ok) li[j] |= (base + lr) << 10;
+            li[j] |= rk << 10;
         }
         __syncthreads();
         // (c) owner t: offsets of the waves' runs in its list, then its list's start in the chunk
@@ -590,7 +622,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
 #pragma unroll
         for (int x = 0; x < W; x++) {
             const u32 c = wcnt[x][t];
-            wcnt[x][t] = (unsigned short)tot;
+            wcnt[x][t] = tot;
             tot += c;
         }
         i64 all;
@@ -609,8 +641,33 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             if (K > 1) st_hi[d] = (unsigned char)((li[j] >> 9) & 1);
         }
         __syncthreads();
-        // (e) the owner folds its list in event order; the next record's LDS loads are issued before
-        // the current one is folded, so their latency overlaps the fold
+        // (e) the owner's list is in event order except where lanes of one round shared the owner:
+        // an insertion pass over the event indices restores it (no moves when already ordered)
+        if (tot > 1) {
+            u32 prev = st_idx[start];
+            for (u32 k = 1; k < tot; k++) {
+                const u32 e = st_idx[start + k];
+                if (e > prev) { prev = e; continue; }
+                u64 mv[V];
+#pragma unroll
+                for (int x = 0; x < V; x++) mv[x] = st_v[x][start + k];
+                const unsigned char mh = K > 1 ? st_hi[start + k] : 0;
+                u32 m = k;
+                while (m > 0 && st_idx[start + m - 1] > e) {
+                    st_idx[start + m] = st_idx[start + m - 1];
+#pragma unroll
+                    for (int x = 0; x < V; x++) st_v[x][start + m] = st_v[x][start + m - 1];
+                    if (K > 1) st_hi[start + m] = st_hi[start + m - 1];
+                    m--;
+                }
+                st_idx[start + m] = e;
+#pragma unroll
+                for (int x = 0; x < V; x++) st_v[x][start + m] = mv[x];
+                if (K > 1) st_hi[start + m] = mh;
+            }
+        }
+        // then folds it; the next record's LDS loads are issued before the current one is folded, so
+        // their latency overlaps the fold
         u32 e_nx = 0;
         i64 v_nx[V];
         unsigned char hi_nx = 0;
@@ -636,12 +693,12 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
                 if (K > 1) hi_nx = st_hi[i];
             }
             if (K > 1 && hi_cur) {
-                fold_fields<V, F>(ap, f1, cnt1 == 0, vv);
+                fold_fields<V, F, SIG>(ap, f1, cnt1 == 0, vv);
                 if (cnt1 == 0) fst1 = e;
                 lst1 = e;
                 cnt1++;
             } else {
-                fold_fields<V, F>(ap, f0, cnt0 == 0, vv);
+                fold_fields<V, F, SIG>(ap, f0, cnt0 == 0, vv);
                 if (cnt0 == 0) fst0 = e;
                 lst0 = e;
                 cnt0++;
@@ -677,20 +734,28 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
     if (rec_pos) {  // multisplit records: thread-ownership kernel
         const int K = own_keys_per_thread(NL);
         const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
-#define SH_AGG_OWN(VV, KK, RR, FF)                                                                             \
-    hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP, ap, rows, \
-                       RW, unit_rows, first_bits, rec_pos, rec_idx, rec_vals, rec_cap)
+#define SH_AGG_OWN(VV, KK, RR, FF, SG)                                                                         \
+    hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP, ap, \
+                       rows, RW, unit_rows, first_bits, rec_pos, rec_idx, rec_vals, rec_cap)
 #define SH_AGG_OWN_F(VV, KK, RR)                          \
     do {                                                  \
-        if (F == 2) SH_AGG_OWN(VV, KK, RR, 2);            \
-        else if (F == 4) SH_AGG_OWN(VV, KK, RR, 4);       \
-        else SH_AGG_OWN(VV, KK, RR, 8);                   \
+        if (F == 2) SH_AGG_OWN(VV, KK, RR, 2, 0);         \
+        else if (F == 4) SH_AGG_OWN(VV, KK, RR, 4, 0);    \
+        else SH_AGG_OWN(VV, KK, RR, 8, 0);                \
     } while (0)
-        static const int r_env = getenv("SH_OWN_R") ? atoi(getenv("SH_OWN_R")) : 8;  // chunk experiment
-        if (K == 1) {
-            if (ap.n_vcols <= 1 && r_env == 4) SH_AGG_OWN_F(1, 1, 4);
-            else if (ap.n_vcols <= 1 && r_env == 2) SH_AGG_OWN_F(1, 1, 2);
-            else if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
+        // compile-time op tables of the common plans (one value column: sum / avg, min + max + avg;
+        // two: long sum + double avg); anything else runs the table-driven fold
+        constexpr u32 kMinMaxAvgD = agg_sig3(FOP_MIN_D, FOP_MAX_D, FOP_ADD_D), kSumD = agg_sig3(FOP_ADD_D, -1, -1),
+                      kSumI = agg_sig3(FOP_ADD_I, -1, -1), kSumISumD = agg_sig3(FOP_ADD_I, FOP_ADD_D, -1);
+        const u32 sig = agg_sig(ap);
+        if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
+        else if (K == 1 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 1, 8, 2, kSumD);
+        else if (K == 1 && ap.n_vcols <= 1 && sig == kSumI) SH_AGG_OWN(1, 1, 8, 2, kSumI);
+        else if (K == 1 && ap.n_vcols == 2 && sig == kSumISumD) SH_AGG_OWN(2, 1, 4, 2, kSumISumD);
+        else if (K == 2 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 2, 8, 4, kMinMaxAvgD);
+        else if (K == 2 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 2, 8, 2, kSumD);
+        else if (K == 1) {
+            if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
             else if (ap.n_vcols <= 2) SH_AGG_OWN_F(2, 1, 4);
             else if (ap.n_vcols <= 4) SH_AGG_OWN_F(4, 1, 2);
             else SH_AGG_OWN_F(8, 1, 1);
@@ -971,7 +1036,7 @@ __device__ __forceinline__ int xcd_tile(int nblk) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_ms_count(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
-                                                    const u32* __restrict__ new_pos, int P, i64* counts, int nblk) {
+                                                    const u32* __restrict__ new_pos, int P, u32* counts, int nblk) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     if (blockIdx.x == 0 && threadIdx.x == 0) counts[(i64)P * nblk] = 0;  // the scan's total slot
     const int tile = xcd_tile(nblk);
@@ -991,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_count(i64 lo, i64 hi, i64 n_pend,
 }
 
 void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
-                     i64* counts, int nblk) {
+                     u32* counts, int nblk) {
     int grid = ((nblk + 7) >> 3) * 8;
     hipLaunchKernelGGL(k_ms_count, dim3(grid), dim3(kBlock), P * 4, s, lo, hi, n_pend, pend_pos, new_pos, P, counts,
                        nblk);
@@ -1009,7 +1074,7 @@ template <int V>
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
                                                       const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
-                                                      const i64* __restrict__ offsets, int nblk, u32* rec_pos,
+                                                      const u32* __restrict__ offsets, int nblk, u32* rec_pos,
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     const int tile = xcd_tile(nblk);
     if (tile >= nblk) return;
@@ -1055,31 +1120,24 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
 #pragma unroll
     for (int k = 0; k < kOffRegs; k++) {
         const int i = threadIdx.x + k * kBlock;
-        off_reg[k] = i < P ? offsets[(i64)i * nblk + tile] : 0;
+        off_reg[k] = i < P ? (i64)offsets[(i64)i * nblk + tile] : 0;
     }
     for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
     __syncthreads();
-    const u64 lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    int bits = 0;
-    while ((1 << bits) < P) bits++;
+    // rank = the wave's running count of its partition, advanced by LDS atomics on the 16-bit
+    // counters (two per 32-bit word); the wave's rounds complete in program order, and lanes of one
+    // round that hit the same counter receive their values in lane order on gfx950
+    // (scripts/probe/lds_atomic_order.hip) — the check after staging repairs the order if not
+    u32* wrun32 = (u32*)run;
     unsigned short* wrun = run + w * P;
     u32 my_rank[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
-        const bool ok = my_pos[r] != kNoPos;
-        const u32 p = ok ? (my_pos[r] & (P - 1)) : 0;
-        u64 peers = __ballot(ok);
-#pragma unroll
-        for (int bt = 0; bt < 14; bt++) {
-            if (bt >= bits) break;
-            const bool bit = (p >> bt) & 1;
-            const u64 m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        const u32 lr = (u32)__popcll(peers & lt_mask);
-        const u32 base = ok ? wrun[p] : 0;  // the wave's LDS operations complete in program order
-        if (ok && lr == 0) wrun[p] = (unsigned short)(base + __popcll(peers));
-        my_rank[r] = base + lr;
+        my_rank[r] = 0;
+        if (my_pos[r] == kNoPos) continue;
+        const u32 c = (u32)(w * P) + (my_pos[r] & (P - 1));
+        const u32 sh = (c & 1) * 16;
+        my_rank[r] = (atomicAdd(&wrun32[c >> 1], 1u << sh) >> sh) & 0xFFFFu;
     }
     __syncthreads();
     // partition starts in the tile (p-major), then each wave's offset inside its partition
@@ -1109,7 +1167,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
         const int i = threadIdx.x + k * kBlock;
         if (i < P) gbase[i] = off_reg[k] - (i64)start[i];
     }
-    for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = offsets[(i64)i * nblk + tile] - (i64)start[i];
+    for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = (i64)offsets[(i64)i * nblk + tile] - (i64)start[i];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
         if (my_pos[r] == kNoPos) continue;
@@ -1122,8 +1180,38 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
             if (j < ap.n_vcols) stage_vals[(size_t)j * kTile + slot] = my_val[r][j];
     }
     __syncthreads();
-    // write every partition's run of this tile contiguously
     const u32 n_tile = s_total;
+    // stability check: inside each partition's run the events must be in stream order
+    bool bad = false;
+    for (u32 j = threadIdx.x; j + 1 < n_tile; j += kBlock)
+        bad |= stage_idx[j + 1] < stage_idx[j] && ((stage_pos[j + 1] ^ stage_pos[j]) & (P - 1)) == 0;
+    if (__syncthreads_or(bad)) {
+        for (int p = threadIdx.x; p < P; p += kBlock) {
+            const u32 a = start[p], b = p + 1 < P ? start[p + 1] : n_tile;
+            for (u32 k = a + 1; k < b; k++) {
+                const u32 e = stage_idx[k], pos = stage_pos[k];
+                u64 mv[V];
+#pragma unroll
+                for (int j = 0; j < V; j++) mv[j] = j < ap.n_vcols ? stage_vals[(size_t)j * kTile + k] : 0;
+                u32 m = k;
+                while (m > a && stage_idx[m - 1] > e) {
+                    stage_idx[m] = stage_idx[m - 1];
+                    stage_pos[m] = stage_pos[m - 1];
+#pragma unroll
+                    for (int j = 0; j < V; j++)
+                        if (j < ap.n_vcols) stage_vals[(size_t)j * kTile + m] = stage_vals[(size_t)j * kTile + m - 1];
+                    m--;
+                }
+                stage_idx[m] = e;
+                stage_pos[m] = pos;
+#pragma unroll
+                for (int j = 0; j < V; j++)
+                    if (j < ap.n_vcols) stage_vals[(size_t)j * kTile + m] = mv[j];
+            }
+        }
+        __syncthreads();
+    }
+    // write every partition's run of this tile contiguously
     for (u32 j = threadIdx.x; j < n_tile; j += kBlock) {
         const u32 pp = stage_pos[j] & (P - 1);
         const i64 dst = gbase[pp] + j;
@@ -1136,7 +1224,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
 }
 
 void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const i64* offsets, int nblk,
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets, int nblk,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     const int V = ap.n_vcols <= 1 ? 1 : ap.n_vcols <= 2 ? 2 : ap.n_vcols <= 4 ? 4 : 8;
     size_t lds = (size_t)V * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
@@ -1152,31 +1240,71 @@ void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pen
 #undef SH_MS
 }
 
-// three-phase exclusive scan for long arrays
-__global__ __launch_bounds__(kBlock) void k_reduce_tiles(const i64* a, i64 n, i64* tmp) {
-    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+// three-phase exclusive scan for long arrays (i64, or u32 counts whose total stays below 2^32): each
+// thread takes kItems consecutive elements with 16-byte loads and stores
+template <typename T>
+__device__ __forceinline__ void load_run(const T* a, i64 base, i64 n, T (&v)[kItems]) {
+    constexpr int PER16 = 16 / sizeof(T);
+    if (base + kItems <= n && (((size_t)(a + base)) & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < kItems / PER16; j++) {
+            const uint4 q = ((const uint4*)(a + base))[j];
+            const T* e = (const T*)&q;
+#pragma unroll
+            for (int k = 0; k < PER16; k++) v[j * PER16 + k] = e[k];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; i++) v[i] = base + i < n ? a[base + i] : (T)0;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_reduce_tiles(const T* a, i64 n, i64* tmp) {
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    T v[kItems];
+    load_run(a, base, n, v);
     i64 s = 0;
 #pragma unroll
-    for (int i = 0; i < kItems; i++) if (base + i < n) s += a[base + i];
+    for (int i = 0; i < kItems; i++) s += (i64)v[i];
     i64 t = block_reduce(s, SumOp(), 0);
     if (threadIdx.x == 0) tmp[blockIdx.x] = t;
 }
-__global__ __launch_bounds__(kBlock) void k_scan_tiles(i64* a, i64 n, const i64* tmp) {
-    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
-    i64 v[kItems];
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(T* a, i64 n, const i64* tmp) {
+    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    T v[kItems];
+    load_run(a, base, n, v);
     i64 s = 0;
 #pragma unroll
-    for (int i = 0; i < kItems; i++) { v[i] = base + i < n ? a[base + i] : 0; s += v[i]; }
+    for (int i = 0; i < kItems; i++) s += (i64)v[i];
     i64 pre = block_excl_scan(s, SumOp(), 0, nullptr) + tmp[blockIdx.x];
+    T o[kItems];
 #pragma unroll
-    for (int i = 0; i < kItems; i++) if (base + i < n) { a[base + i] = pre; pre += v[i]; }
+    for (int i = 0; i < kItems; i++) { o[i] = (T)pre; pre += (i64)v[i]; }
+    constexpr int PER16 = 16 / sizeof(T);
+    if (base + kItems <= n && (((size_t)(a + base)) & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < kItems / PER16; j++) ((uint4*)(a + base))[j] = *(const uint4*)&o[j * PER16];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; i++) if (base + i < n) a[base + i] = o[i];
+    }
 }
 
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp) {
     int nb = (int)((n + kTile - 1) / kTile);
-    hipLaunchKernelGGL(k_reduce_tiles, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
+    hipLaunchKernelGGL(k_reduce_tiles<i64>, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
     launch_scan_sum(s, tmp, nb);
-    hipLaunchKernelGGL(k_scan_tiles, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
+    hipLaunchKernelGGL(k_scan_tiles<i64>, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
+}
+
+void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp) {
+    int nb = (int)((n + kTile - 1) / kTile);
+    hipLaunchKernelGGL(k_reduce_tiles<u32>, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
+    launch_scan_sum(s, tmp, nb);
+    hipLaunchKernelGGL(k_scan_tiles<u32>, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
 }
 
 __global__ void k_part_off(const i64* counts, int nblk, int P, i64* part_off) {
@@ -1193,7 +1321,7 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
 __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restrict__ segs, int nseg, i64 n_pend,
                                                        const u32* __restrict__ pend_pos,
                                                        const u32* __restrict__ new_pos, int P,
-                                                       const i64* __restrict__ counts, int nblk, i64* seg_off) {
+                                                       const u32* __restrict__ counts, int nblk, i64* seg_off) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int k = blockIdx.x;
     const i64 b = k < nseg ? segs[k].lo : segs[nseg - 1].hi;
@@ -1205,11 +1333,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restric
         if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < P; p += kBlock) seg_off[(i64)k * P + p] = counts[(i64)p * nblk + t] + hist[p];
+    for (int p = threadIdx.x; p < P; p += kBlock) seg_off[(i64)k * P + p] = (i64)counts[(i64)p * nblk + t] + hist[p];
 }
 
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const i64* counts, int nblk, i64* seg_off) {
+                        const u32* new_pos, int P, const u32* counts, int nblk, i64* seg_off) {
     hipLaunchKernelGGL(k_seg_offsets, dim3(nseg + 1), dim3(kBlock), P * 4, s, segs, nseg, n_pend, pend_pos, new_pos, P,
                        counts, nblk, seg_off);
 }

@@ -239,7 +239,7 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     int nblk = (int)((b->n + kTile - 1) / kTile);
     RCHK(s->blk_pass.reserve(nblk * 8, false));
     RCHK(s->blk_tl.reserve(nblk * 8, false));
-    RCHK(s->blk_first.reserve(nblk * 8, false));
+    RCHK(s->blk_first.reserve(scan_blocks_first_bytes(nblk), false));
     if (s->sliding) {
         // pass count, max send-last ts, max passing ts (PM) of the slice; blk_first holds the PM prefix
         WinParams wp{};

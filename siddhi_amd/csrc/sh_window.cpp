@@ -264,7 +264,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
         launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), b ? q->new_pos.as<u32>() : nullptr, q->P,
-                           q->ms_counts.as<int64_t>(), q->ms_nblk, q->seg_off.as<int64_t>());
+                           q->ms_counts.as<u32>(), q->ms_nblk, q->seg_off.as<int64_t>());
     }
     // (the record buffers' addresses only after run_multisplit: it may have grown them)
     const u32* rec_pos = q->rec_pos.as<u32>();
@@ -419,7 +419,7 @@ static int resolve_first_partition(sh_query* q, const sh_batch* b) {
     int nblk = (int)((N + kTile - 1) / kTile);
     RCHK(q->blk_pass.reserve(nblk * 8, false));
     RCHK(q->blk_tl.reserve(nblk * 8, false));
-    RCHK(q->blk_first.reserve(nblk * 8, false));
+    RCHK(q->blk_first.reserve(scan_blocks_first_bytes(nblk), false));
     WinParams wp{};
     wp.kind = SH_WIN_LENGTH_BATCH;  // no nextEmitTime initialisation in this probe
     wp.N = N;
@@ -501,7 +501,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         int nblk = (int)((N + kTile - 1) / kTile);
         RCHK(q->blk_pass.reserve(nblk * 8, false));
         RCHK(q->blk_tl.reserve(nblk * 8, false));
-        RCHK(q->blk_first.reserve(nblk * 8, false));
+        RCHK(q->blk_first.reserve(scan_blocks_first_bytes(nblk), false));
         WinParams wp{};
         wp.kind = q->d.window;
         wp.e0_valid = q->e0_valid;
@@ -740,7 +740,7 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b) {
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     int nblk = (int)((hi + kTile - 1) / kTile);
     int64_t ncnt = (int64_t)P * nblk;
-    RCHK(q->ms_counts.reserve((ncnt + 1) * 8, false));
+    RCHK(q->ms_counts.reserve((ncnt + 4) * 4, false));
     RCHK(q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false));
     RCHK(q->part_off.reserve((P + 1) * 8, false));
     int64_t cap = std::max<int64_t>(hi, 1);
@@ -748,13 +748,13 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b) {
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
     const u32* np = b ? q->new_pos.as<u32>() : nullptr;
-    launch_ms_count(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<int64_t>(), nblk);
-    // counts are laid out [p][blk]; one exclusive scan gives every (partition, block) its offset,
-    // and partition p starts at offset[p * nblk]
+    launch_ms_count(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<u32>(), nblk);
+    // counts (u32: a push holds fewer than 2^32 events) are laid out [p][blk]; one exclusive scan
+    // gives every (partition, block) its offset, and partition p starts at offset[p * nblk]
     // (k_ms_count zeroes the total slot counts[ncnt])
-    launch_scan_sum_large(s, q->ms_counts.as<int64_t>(), ncnt + 1, q->ms_tmp.as<int64_t>());
+    launch_scan_sum_large_u32(s, q->ms_counts.as<u32>(), ncnt + 1, q->ms_tmp.as<int64_t>());
     launch_ms_scatter(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
-                      q->ms_counts.as<int64_t>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
+                      q->ms_counts.as<u32>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
                       q->rec_vals.as<u64>(), cap);
     HIPCHK(hipGetLastError());
     q->ms_ready = true;
