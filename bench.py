@@ -36,8 +36,8 @@ C2_BYTES_PER_EVENT = 24.4  # 20 B/event in + 100k rows x 44 B pe
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1 << 25, help="events per step (per GPU)")
     ap.add_argument("--keys", type=int, default=100_000)
     ap.add_argument("--events-per-ms", type=int, default=1000)
@@ -310,14 +310,28 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     kern_ms, kern_bytes, flushes, rows = 0.0, 0, 0, 0
+    host_t = [] if os.environ.get("SH_TIMING") else None
     t0 = time.perf_counter()
     for i in range(args.warmup, nb):
+        ta = time.perf_counter()
         o = push(i).contents
+        tb = time.perf_counter()
         st = q.stats()
         kern_ms += st.main_kernel_ms
         flushes += o.n_flushes
         rows += o.n_rows
+        if host_t is not None:
+            host_t.append((tb - ta, time.perf_counter() - tb))
+    t_sync = time.perf_counter()
     torch.cuda.synchronize()
+    if host_t:
+        import statistics
+        print(f"[bench timing] loop {(t_sync - t0) * 1e3:.2f} ms, pushes {sum(a for a, _ in host_t) * 1e3:.2f} ms, "
+              f"bookkeeping {sum(b for _, b in host_t) * 1e3:.2f} ms, final sync {(time.perf_counter() - t_sync) * 1e3:.2f} ms",
+              file=sys.stderr)
+        print(f"[bench timing] push call median {statistics.median(a for a, _ in host_t) * 1e6:.1f} us, "
+              f"bookkeeping median {statistics.median(b for _, b in host_t) * 1e6:.1f} us; per push: "
+              + " ".join(f"{a * 1e6:.0f}" for a, _ in host_t), file=sys.stderr)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

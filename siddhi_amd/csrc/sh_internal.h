@@ -167,7 +167,8 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
                         WinParams wp, PushInfo* info, i64* blk_xm = nullptr, ColSet cols = ColSet{});
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr);
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr,
+                       u32* ms_counts = nullptr, int P = 1, int ms_nblk = 0, int ms_col0 = 0);
 // Rows of one aggregation unit — (segment, key partition) for the multisplit kernel, the segment for
 // the flat one — fill the unit's own region of agg_unit_rows() row slots; unit_rows[u] = its count.
 int agg_unit_rows(int P, int NL, bool own);
@@ -192,16 +193,48 @@ void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);
 // multisplit (partitioned aggregation, P > 1)
-void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
-                     u32* counts, int nblk);
-void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets, int nblk,
+// Multisplit tiles over the combined index space [0, hi) of queued + new events: tiles of kTile
+// events over [0, split) (the queued events), then tiles of kTile over [split, hi) (the push's
+// events, aligned with k_boundaries' tiles so that it can count them). split = 0: one uniform run.
+struct TileMap {
+    i64 split;
+    i64 hi;
+    int np_t;   // tiles over [0, split)
+    int nblk;   // all tiles
+};
+inline TileMap make_tile_map(i64 split, i64 hi) {
+    TileMap m;
+    m.split = split < hi ? split : hi;
+    m.hi = hi;
+    m.np_t = (int)((m.split + kTile - 1) / kTile);
+    m.nblk = m.np_t + (int)((hi - m.split + kTile - 1) / kTile);
+    return m;
+}
+__host__ __device__ inline i64 tile_lo(const TileMap& m, int t) {
+    return t < m.np_t ? (i64)t * kTile : m.split + (i64)(t - m.np_t) * kTile;
+}
+__host__ __device__ inline i64 tile_hi(const TileMap& m, int t) {
+    const i64 lo = tile_lo(m, t), end = t < m.np_t ? m.split : m.hi;
+    return lo + kTile < end ? lo + kTile : end;
+}
+// the tile holding index b (b == hi: one past the last tile, whose count column the scan's layout
+// makes the next partition's start)
+__host__ __device__ inline int tile_of(const TileMap& m, i64 b) {
+    if (b < m.split) return (int)(b / kTile);
+    return m.np_t + (int)((b - m.split) / kTile);
+}
+
+// counts the first n_count tiles of the map (k_boundaries counted the others) and zeroes the total slot
+void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+                     u32* counts);
+void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
 void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const u32* counts, int nblk, i64* seg_off);
+                        const u32* new_pos, int P, const u32* counts, TileMap m, i64* seg_off);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 // sharded ingest (sh_shard_kernels.hip)

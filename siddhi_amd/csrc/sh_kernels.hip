@@ -12,6 +12,22 @@
 
 namespace shd {
 
+// Diagnostic phase stamps (make stamps -> libsiddhi_hip_stamps.so, read by scripts/stamps.py): thread 0
+// of a workgroup records the shader clock at numbered points of a kernel. The product build has none.
+#ifdef SH_STAMPS
+constexpr int kStampKernels = 4, kStampBlocks = 32768, kStampPts = 16;
+__device__ unsigned long long g_stamps[kStampKernels * kStampBlocks * kStampPts];
+#define SH_STAMP(kern, pt)                                                                                   \
+    do {                                                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x < kStampBlocks) {                                                 \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                      \
+            g_stamps[((size_t)(kern) * kStampBlocks + blockIdx.x) * kStampPts + (pt)] = __builtin_amdgcn_s_memtime(); \
+        }                                                                                                    \
+    } while (0)
+#else
+#define SH_STAMP(kern, pt) do {} while (0)
+#endif
+
 // ================================================================================================
 // k_blockagg: per workgroup (kTile events, blocked kItems per thread) the number of passing events,
 // the max timestamp over send-last events and the first passing event.
@@ -226,7 +242,8 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
                                                       WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const PushInfo* info, Bound* bounds, int max_bounds,
                                                       int* n_bounds, KeyPlan kp, KeyTable kt, u32* new_pos,
-                                                      const i64* blk_xm_pre) {
+                                                      const i64* blk_xm_pre, u32* ms_counts, int P, int ms_nblk,
+                                                      int ms_col0) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     filter_items<FK>(f, cols, base, wp.N, pass);
@@ -256,6 +273,19 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
 #pragma unroll
             for (int i = 0; i < kItems; i++)
                 if (base + i < wp.N) new_pos[base + i] = pos[i];
+        }
+        // the multisplit's per-tile key-partition counts of this tile (k_ms_count's job for the
+        // push's events when the split runs over the whole push)
+        if (ms_counts) {
+            extern __shared__ __attribute__((aligned(16))) u32 mhist[];
+            for (int i = threadIdx.x; i < P; i += kBlock) mhist[i] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kItems; i++)
+                if (pass[i]) atomicAdd(&mhist[pos[i] & (P - 1)], 1u);
+            __syncthreads();
+            for (int i = threadIdx.x; i < P; i += kBlock)
+                ms_counts[(i64)i * ms_nblk + ms_col0 + blockIdx.x] = mhist[i];
         }
     }
     i64 t[kItems];
@@ -332,11 +362,14 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
 
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
-                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre) {
+                       int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre,
+                       u32* ms_counts, int P, int ms_nblk, int ms_col0) {
+    const size_t lds = ms_counts ? (size_t)P * 4 : 0;
     int* nb = (int*)&((PushInfo*)info)->n_bounds;
 #define SH_BOUNDS(EXT, FK)                                                                                      \
-    hipLaunchKernelGGL((k_boundaries<EXT, FK>), dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_pass_pre, \
-                       blk_tl_pre, info, bounds, max_bounds, nb, kp, kt, new_pos, blk_xm_pre)
+    hipLaunchKernelGGL((k_boundaries<EXT, FK>), dim3(nblk), dim3(kBlock), lds, s, ts, cols, f, wp, blk_pass_pre, \
+                       blk_tl_pre, info, bounds, max_bounds, nb, kp, kt, new_pos, blk_xm_pre, ms_counts, P, ms_nblk,  \
+                       ms_col0)
     const int fk = filter_kind(f);
     if (wp.kind == SH_WIN_EXT_TIME_BATCH) SH_BOUNDS(true, 2);
     else if (fk == 0) SH_BOUNDS(false, 0);
@@ -581,11 +614,13 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     __shared__ unsigned char st_hi[K > 1 ? CH : 1];
     __shared__ u32 wcnt[W][kOwnT];  // per wave: running count per owner, then its offset
     __shared__ u32 bstart[kOwnT];
+    __shared__ u32 lstart[CH / 32];  // bitmap: chunk positions where an owner's list starts
     constexpr u32 kNone = 0xFFFFFFFFu;
     const int seg = blockIdx.x / P;
     const int p = blockIdx.x - seg * P;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
+    SH_STAMP(0, 0);
     u32 cnt0 = 0, fst0 = 0, lst0 = 0, cnt1 = 0, fst1 = 0, lst1 = 0;
     u64 f0[F], f1[F];
 #pragma unroll
@@ -604,11 +639,13 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
 #pragma unroll
             for (int x = 0; x < V; x++) v[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c0 + r] : 0;
         }
+        SH_STAMP(0, 1);
         // (b) rank among the run's records of the same owner: a wave-private running count per owner,
         // advanced by LDS atomics (the wave's rounds complete in program order; lanes of one round
         // that share an owner get distinct ranks, in an order (e) restores)
 #pragma unroll
         for (int i = lane; i < kOwnT; i += 64) wcnt[w][i] = 0;
+        for (int i = t; i < CH / 32; i += kOwnT) lstart[i] = 0;
 #pragma unroll
         for (int j = 0; j < R; j++) {
             if (li[j] == kNone) continue;
@@ -617,6 +654,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             li[j] |= rk << 10;
         }
         __syncthreads();
+        SH_STAMP(0, 2);
         // (c) owner t: offsets of the waves' runs in its list, then its list's start in the chunk
         u32 tot = 0;
 #pragma unroll
@@ -628,6 +666,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         i64 all;
         const u32 start = (u32)block_excl_scan_any((i64)tot, &all);
         bstart[t] = start;
+        if (tot) atomicOr(&lstart[start >> 5], 1u << (start & 31));
         __syncthreads();
         // (d) every record into its owner's list
 #pragma unroll
@@ -641,9 +680,14 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             if (K > 1) st_hi[d] = (unsigned char)((li[j] >> 9) & 1);
         }
         __syncthreads();
-        // (e) the owner's list is in event order except where lanes of one round shared the owner:
-        // an insertion pass over the event indices restores it (no moves when already ordered)
-        if (tot > 1) {
+        SH_STAMP(0, 3);
+        // (e) the owner's list is in event order unless lanes of one round that shared the owner got
+        // their ranks out of lane order (never seen on gfx950: scripts/probe/lds_atomic_order.hip);
+        // checked in parallel over adjacent positions of one list, repaired by an insertion pass
+        bool bad = false;
+        for (int d = t; d + 1 < n; d += kOwnT)
+            bad |= !((lstart[(d + 1) >> 5] >> ((d + 1) & 31)) & 1u) && st_idx[d + 1] < st_idx[d];
+        if (__syncthreads_or(bad) && tot > 1) {
             u32 prev = st_idx[start];
             for (u32 k = 1; k < tot; k++) {
                 const u32 e = st_idx[start + k];
@@ -666,6 +710,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
                 if (K > 1) st_hi[start + m] = mh;
             }
         }
+        SH_STAMP(0, 4);
         // then folds it; the next record's LDS loads are issued before the current one is folded, so
         // their latency overlaps the fold
         u32 e_nx = 0;
@@ -705,6 +750,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             }
         }
     }
+    SH_STAMP(0, 5);
     // one row per key with events, in the unit's own region of K * 512 row slots (no global counter:
     // a contended atomic on one address would serialise every workgroup of the launch)
     const int mine = (cnt0 > 0) + (K > 1 && cnt1 > 0);
@@ -721,6 +767,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)(t + kOwnT) << logP) | (u32)p, cnt1, fst1, lst1, f1);
         mark_first(first_bits, fst1);
     }
+    SH_STAMP(0, 6);
 }
 
 int own_keys_per_thread(int NL) { return NL <= kOwnT ? 1 : 2; }
@@ -1035,31 +1082,30 @@ __device__ __forceinline__ int xcd_tile(int nblk) {
     return (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
 }
 
-__global__ __launch_bounds__(kBlock) void k_ms_count(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
-                                                    const u32* __restrict__ new_pos, int P, u32* counts, int nblk) {
+__global__ __launch_bounds__(kBlock) void k_ms_count(TileMap m, int n_count, i64 n_pend, const u32* __restrict__ pend_pos,
+                                                    const u32* __restrict__ new_pos, int P, u32* counts) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
-    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(i64)P * nblk] = 0;  // the scan's total slot
-    const int tile = xcd_tile(nblk);
-    if (tile >= nblk) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(i64)P * m.nblk] = 0;  // the scan's total slot
+    const int tile = xcd_tile(n_count);
+    if (tile >= n_count) return;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
     __syncthreads();
-    i64 t0 = lo + (i64)tile * kTile;
+    const i64 t0 = tile_lo(m, tile), t1 = tile_hi(m, tile);
     for (int r = 0; r < kItems; r++) {
         i64 e = t0 + (i64)r * kBlock + threadIdx.x;
-        if (e < hi) {
+        if (e < t1) {
             EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
             if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)i * nblk + tile] = hist[i];
+    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)i * m.nblk + tile] = hist[i];
 }
 
-void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
-                     u32* counts, int nblk) {
-    int grid = ((nblk + 7) >> 3) * 8;
-    hipLaunchKernelGGL(k_ms_count, dim3(grid), dim3(kBlock), P * 4, s, lo, hi, n_pend, pend_pos, new_pos, P, counts,
-                       nblk);
+void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+                     u32* counts) {
+    int grid = std::max(1, ((n_count + 7) >> 3) * 8);
+    hipLaunchKernelGGL(k_ms_count, dim3(grid), dim3(kBlock), P * 4, s, m, n_count, n_pend, pend_pos, new_pos, P, counts);
 }
 
 // Stable multisplit of one tile of kTile closed events into the P key partitions. Wave w takes
@@ -1071,11 +1117,12 @@ void launch_ms_count(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_
 // written out as one contiguous run per partition.
 // LDS: stage_vals[V][kTile] | stage_pos[kTile] | stage_idx[kTile] | start[P] | gbase[P] (i64) | run[4][P] (u16)
 template <int V>
-__global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pend, const u32* __restrict__ pend_pos,
+__global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
                                                       const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
-                                                      const u32* __restrict__ offsets, int nblk, u32* rec_pos,
+                                                      const u32* __restrict__ offsets, u32* rec_pos,
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
+    const int nblk = m.nblk;
     const int tile = xcd_tile(nblk);
     if (tile >= nblk) return;
     constexpr int NW = kBlock / 64;
@@ -1089,7 +1136,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     i64* gbase = (i64*)(start + P + (P & 1));                // [P] global position of the tile's run - start
     unsigned short* run = (unsigned short*)(gbase + P);  // [NW][P]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const i64 t0 = lo + (i64)tile * kTile + (i64)w * PER_WAVE;
+    const i64 t0 = tile_lo(m, tile) + (i64)w * PER_WAVE, hi = tile_hi(m, tile);
     // every round's position and values, and the tile's run offsets (one per partition, strided by
     // nblk in the [p][tile] scan), requested before anything waits on them
     u32 my_pos[kItems];
@@ -1223,16 +1270,17 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(i64 lo, i64 hi, i64 n_pen
     }
 }
 
-void launch_ms_scatter(hipStream_t s, i64 lo, i64 hi, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets, int nblk,
+void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
+    const int nblk = m.nblk;
     const int V = ap.n_vcols <= 1 ? 1 : ap.n_vcols <= 2 ? 2 : ap.n_vcols <= 4 ? 4 : 8;
     size_t lds = (size_t)V * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
                  (size_t)P * 2 * (kBlock / 64) + 32;
     int grid = ((nblk + 7) >> 3) * 8;
 #define SH_MS(VV)                                                                                                   \
-    hipLaunchKernelGGL(k_ms_scatter<VV>, dim3(grid), dim3(kBlock), lds, s, lo, hi, n_pend, pend_pos, pend_vals, pend_cap, \
-                       new_pos, cols, ap, P, offsets, nblk, rec_pos, rec_idx, rec_vals, rec_cap)
+    hipLaunchKernelGGL(k_ms_scatter<VV>, dim3(grid), dim3(kBlock), lds, s, m, n_pend, pend_pos, pend_vals, pend_cap, \
+                       new_pos, cols, ap, P, offsets, rec_pos, rec_idx, rec_vals, rec_cap)
     if (V == 1) SH_MS(1);
     else if (V == 2) SH_MS(2);
     else if (V == 4) SH_MS(4);
@@ -1321,14 +1369,15 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
 __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restrict__ segs, int nseg, i64 n_pend,
                                                        const u32* __restrict__ pend_pos,
                                                        const u32* __restrict__ new_pos, int P,
-                                                       const u32* __restrict__ counts, int nblk, i64* seg_off) {
+                                                       const u32* __restrict__ counts, TileMap m, i64* seg_off) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int k = blockIdx.x;
     const i64 b = k < nseg ? segs[k].lo : segs[nseg - 1].hi;
-    const i64 t = b / kTile;
+    const int t = tile_of(m, b);
+    const int nblk = m.nblk;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
     __syncthreads();
-    for (i64 e = t * kTile + threadIdx.x; e < b; e += kBlock) {
+    for (i64 e = tile_lo(m, t) + threadIdx.x; e < b; e += kBlock) {
         EvLoad ev = load_pos(e, n_pend, pend_pos, new_pos);
         if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
     }
@@ -1337,10 +1386,26 @@ __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restric
 }
 
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const u32* counts, int nblk, i64* seg_off) {
+                        const u32* new_pos, int P, const u32* counts, TileMap m, i64* seg_off) {
     hipLaunchKernelGGL(k_seg_offsets, dim3(nseg + 1), dim3(kBlock), P * 4, s, segs, nseg, n_pend, pend_pos, new_pos, P,
-                       counts, nblk, seg_off);
+                       counts, m, seg_off);
 }
+
+#ifdef SH_STAMPS
+}  // namespace shd
+extern "C" int sh_debug_stamps(unsigned long long* out, long long n, int clear) {
+    const long long cap = (long long)shd::kStampKernels * shd::kStampBlocks * shd::kStampPts;
+    if (n > cap) n = cap;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (clear) {
+        static unsigned long long* zero = nullptr;
+        if (!zero) zero = (unsigned long long*)calloc(cap, 8);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(shd::g_stamps), zero, cap * 8, 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace shd {
+#endif
 
 // ---- key-table rebuild: the open window's keys move to a fresh table (drops dead keys / grows) ------
 __global__ __launch_bounds__(kBlock) void k_rekey(i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt) {

@@ -14,6 +14,8 @@
 #include "sh_internal.h"
 #include "sh_runtime.h"
 
+#include <chrono>
+
 using namespace shd;
 
 thread_local std::string g_last_error;
@@ -22,6 +24,41 @@ int sh_fail(int code, const std::string& msg) {
     g_last_error = msg;
     SH_TRACE("error %d: %s", code, msg.c_str());
     return code;
+}
+
+namespace {
+struct HostTiming {
+    static constexpr int kPts = 8;
+    std::vector<double> d[kPts];
+    std::chrono::steady_clock::time_point last;
+    int last_pt = -1;
+    ~HostTiming() {
+        if (!sh_timing_on()) return;
+        for (int p = 1; p < kPts; p++) {
+            if (d[p].empty()) continue;
+            std::vector<double> v = d[p];
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, "[sh timing] ->%d: %zu x, median %.1f us, min %.1f, max %.1f\n", p, v.size(), v[v.size() / 2],
+                    v.front(), v.back());
+        }
+    }
+};
+HostTiming g_timing;
+}  // namespace
+
+bool sh_timing_on() {
+    static const bool on = getenv("SH_TIMING") != nullptr;
+    return on;
+}
+
+// point 0 starts a push; point p > 0 adds the time since the previous point to slot p
+void sh_timing_mark(int p) {
+    const auto now = std::chrono::steady_clock::now();
+    if (p > 0 && g_timing.last_pt >= 0 && p < HostTiming::kPts) {
+        g_timing.d[p].push_back(std::chrono::duration<double, std::micro>(now - g_timing.last).count());
+    }
+    g_timing.last = now;
+    g_timing.last_pt = p;
 }
 
 bool sh_trace_on() {
@@ -112,6 +149,13 @@ extern "C" int sh_init(int32_t device, sh_ctx** out) {
     HIPCHK(hipGetDeviceProperties(&prop, device));
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         return sh_fail(SH_ERR_DEVICE, std::string("built for gfx950, found ") + prop.gcnArchName);
+    // stream-ordered buffers come from the device's default pool; keep what it has reserved instead
+    // of handing it back at every synchronisation (a grown buffer's old block is reused, not re-mapped)
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     sh_ctx* c = new sh_ctx();
     c->device = device;
     c->num_cus = prop.multiProcessorCount;

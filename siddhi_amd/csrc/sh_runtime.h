@@ -29,6 +29,15 @@ bool sh_trace_on();
         }                                                \
     } while (0)
 
+// SH_TIMING=1 in the environment: host-side time between numbered points of a push, accumulated and
+// printed to stderr at exit (diagnostics only; one clock read per point otherwise skipped)
+bool sh_timing_on();
+void sh_timing_mark(int point);
+#define SH_TMARK(p)                          \
+    do {                                     \
+        if (sh_timing_on()) sh_timing_mark(p); \
+    } while (0)
+
 // The stream of the context whose API call is running on this thread. Device buffers grow and are
 // freed in that stream's order (hipMallocAsync / hipFreeAsync), so a growth never waits on other
 // streams and never frees memory a queued kernel still reads. Every extern "C" entry point that
@@ -155,6 +164,7 @@ using shd::AggPlan;
 using shd::FilterProg;
 using shd::KeyPlan;
 using shd::PushInfo;
+using shd::TileMap;
 
 struct SlidingImpl;
 
@@ -198,7 +208,7 @@ struct sh_query {
     PinnedBuf h_bounds;  // pinned landing area of the push's window boundaries
     // the multisplit of the push's events, launched before the host reads the window boundaries
     bool ms_ready = false;
-    int ms_nblk = 0;
+    TileMap ms_map{};  // tiling of the last multisplit
     int64_t rec_cap = 0;
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation
     struct ClosedTail {
@@ -270,5 +280,8 @@ int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* co
 void sliding_destroy(sh_query* q);
 // stable multisplit of the combined events [0, hi) into the query's P key partitions: records
 // (q->rec_pos / rec_idx / rec_vals, capacity q->rec_cap), per-(partition, tile) offsets in q->ms_counts
-int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b);
+// counted: k_boundaries already wrote the counts of the push's tiles (tiling make_tile_map(n_pend, hi),
+// buffers sized by reserve_ms_counts before it ran)
+int reserve_ms_counts(sh_query* q, const TileMap& m);
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted = false);
 

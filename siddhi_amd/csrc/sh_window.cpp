@@ -264,7 +264,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
         launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), b ? q->new_pos.as<u32>() : nullptr, q->P,
-                           q->ms_counts.as<u32>(), q->ms_nblk, q->seg_off.as<int64_t>());
+                           q->ms_counts.as<u32>(), q->ms_map, q->seg_off.as<int64_t>());
     }
     // (the record buffers' addresses only after run_multisplit: it may have grown them)
     const u32* rec_pos = q->rec_pos.as<u32>();
@@ -476,6 +476,7 @@ int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend) {
 }
 
 static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    SH_TMARK(0);
     hipStream_t s = q->ctx->stream;
     q->out.reset();
     q->dev_flush_offsets.assign(1, 0);
@@ -536,9 +537,15 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
         RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
         RCHK(q->new_pos.reserve((size_t)N * 4, false));
+        // large pushes split the whole push into key partitions right behind k_boundaries, which
+        // counts the push's tiles for it (a small push usually closes no window: no split then)
+        const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18);
+        const TileMap ms_map = make_tile_map(q->n_pend, q->n_pend + N);
+        if (early_split) RCHK(reserve_ms_counts(q, ms_map));
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                           q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                          q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr);
+                          q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr,
+                          early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t);
         HIPCHK(hipGetLastError());
         // the push info and the first boundaries come back in one copy; the key partitioning of the
         // push's events (independent of where the windows close) is queued behind it and runs while
@@ -549,10 +556,12 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(q->ev_mid, s));
-        // (large pushes only: a small push usually closes no window, and then the split was wasted)
-        if ((q->P > 1 || q->partitioned) && N >= (1 << 18)) RCHK(run_multisplit(q, q->n_pend + N, b));
+        SH_TMARK(1);
+        if (early_split) RCHK(run_multisplit(q, q->n_pend + N, b, true));
         SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
+        SH_TMARK(2);
         HIPCHK(hipEventSynchronize(q->ev_mid));
+        SH_TMARK(3);
         PushInfo info = *q->h_info;
         SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
         if (info.n_bounds > max_bounds) return sh_fail(SH_ERR_INVALID, "more than 4M windows closed in one push");
@@ -638,7 +647,9 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     RCHK(q->h_tail.reserve(16));
     RCHK(q->kt.check_async(s, q->h_tail.as<uint32_t>()));
     SH_TRACE("push final sync");
+    SH_TMARK(4);
     HIPCHK(hipStreamSynchronize(s));
+    SH_TMARK(5);
     SH_TRACE("push done");
     RCHK(q->kt.check_result(q->h_tail.as<uint32_t>()));
     RCHK(closed_finish(q, host_out));
@@ -648,6 +659,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     q->stats.events = N;
     q->stats.main_kernel_bytes = q->agg_bytes;
     finish_out(q, host_out, out);
+    SH_TMARK(6);
     return SH_OK;
 }
 
@@ -732,33 +744,37 @@ extern "C" int sh_query_stats(sh_query* q, sh_stats* out) {
 }
 
 // ---- multisplit: the combined events into P key partitions (stable) -------------------------------
-int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b) {
+int reserve_ms_counts(sh_query* q, const TileMap& m) {
+    const int64_t ncnt = (int64_t)q->P * m.nblk;
+    RCHK(q->ms_counts.reserve((ncnt + 4) * 4, false));
+    return q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false);
+}
+
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted) {
     hipStream_t s = q->ctx->stream;
     int P = q->P;
     ColSet cs{};
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
-    int nblk = (int)((hi + kTile - 1) / kTile);
-    int64_t ncnt = (int64_t)P * nblk;
-    RCHK(q->ms_counts.reserve((ncnt + 4) * 4, false));
-    RCHK(q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false));
+    const TileMap m = counted ? make_tile_map(q->n_pend, hi) : make_tile_map(0, hi);
+    int64_t ncnt = (int64_t)P * m.nblk;
+    RCHK(reserve_ms_counts(q, m));  // (the size k_boundaries' counts were written into: no regrowth)
     RCHK(q->part_off.reserve((P + 1) * 8, false));
     int64_t cap = std::max<int64_t>(hi, 1);
     RCHK(q->rec_pos.reserve(cap * 4, false));
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
     const u32* np = b ? q->new_pos.as<u32>() : nullptr;
-    launch_ms_count(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<u32>(), nblk);
+    // the queued events' tiles (every tile when k_boundaries did not count); also zeroes the total slot
+    launch_ms_count(s, m, counted ? m.np_t : m.nblk, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<u32>());
     // counts (u32: a push holds fewer than 2^32 events) are laid out [p][blk]; one exclusive scan
     // gives every (partition, block) its offset, and partition p starts at offset[p * nblk]
-    // (k_ms_count zeroes the total slot counts[ncnt])
     launch_scan_sum_large_u32(s, q->ms_counts.as<u32>(), ncnt + 1, q->ms_tmp.as<int64_t>());
-    launch_ms_scatter(s, 0, hi, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
-                      q->ms_counts.as<u32>(), nblk, q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
-                      q->rec_vals.as<u64>(), cap);
+    launch_ms_scatter(s, m, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
+                      q->ms_counts.as<u32>(), q->rec_pos.as<u32>(), q->rec_idx.as<u32>(), q->rec_vals.as<u64>(), cap);
     HIPCHK(hipGetLastError());
     q->ms_ready = true;
-    q->ms_nblk = nblk;
+    q->ms_map = m;
     q->rec_cap = cap;
     return SH_OK;
 }
