@@ -46,6 +46,24 @@ struct HostTiming {
 HostTiming g_timing;
 }  // namespace
 
+template <typename Q, typename W>
+static hipError_t poll_then_wait(Q query, W wait) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; it++) {
+        const hipError_t e = query();
+        if (e != hipErrorNotReady) return e;
+        if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) return wait();
+    }
+}
+
+hipError_t sh_wait_stream(hipStream_t s) {
+    return poll_then_wait([&] { return hipStreamQuery(s); }, [&] { return hipStreamSynchronize(s); });
+}
+
+hipError_t sh_wait_event(hipEvent_t e) {
+    return poll_then_wait([&] { return hipEventQuery(e); }, [&] { return hipEventSynchronize(e); });
+}
+
 bool sh_timing_on() {
     static const bool on = getenv("SH_TIMING") != nullptr;
     return on;

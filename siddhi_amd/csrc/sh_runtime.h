@@ -38,6 +38,12 @@ void sh_timing_mark(int point);
         if (sh_timing_on()) sh_timing_mark(p); \
     } while (0)
 
+// Waits that poll the stream / event instead of sleeping in the driver: a push waits for work that
+// completes within a millisecond or two, and a blocking wait's wake-up adds tens of microseconds to
+// every push. After ~20 ms of polling they fall back to the blocking call.
+hipError_t sh_wait_stream(hipStream_t s);
+hipError_t sh_wait_event(hipEvent_t e);
+
 // The stream of the context whose API call is running on this thread. Device buffers grow and are
 // freed in that stream's order (hipMallocAsync / hipFreeAsync), so a growth never waits on other
 // streams and never frees memory a queued kernel still reads. Every extern "C" entry point that

@@ -560,7 +560,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         if (early_split) RCHK(run_multisplit(q, q->n_pend + N, b, true));
         SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
         SH_TMARK(2);
-        HIPCHK(hipEventSynchronize(q->ev_mid));
+        HIPCHK(sh_wait_event(q->ev_mid));
         SH_TMARK(3);
         PushInfo info = *q->h_info;
         SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
@@ -648,7 +648,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     RCHK(q->kt.check_async(s, q->h_tail.as<uint32_t>()));
     SH_TRACE("push final sync");
     SH_TMARK(4);
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(sh_wait_stream(s));
     SH_TMARK(5);
     SH_TRACE("push done");
     RCHK(q->kt.check_result(q->h_tail.as<uint32_t>()));
