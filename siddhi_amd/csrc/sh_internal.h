@@ -135,7 +135,7 @@ struct PushInfo {
     i64 first_clk;     // clock of the first passing event's send, before the carried-in clock
     i64 max_xm;        // externalTimeBatch: max of the timestamp attribute over passing events
     int err;           // externalTimeBatch: first event before its start time
-    int pad;
+    int unsorted;      // single-pass form: a timestamp decreased (redo with the prefix passes)
     i64 first_key;     // column WinParams.pcol1 - 1 of the first passing event (partitioned queries, R12)
 };
 
@@ -165,10 +165,13 @@ void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i6
 size_t scan_blocks_first_bytes(int nblk);
 void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_first, int nblk, const i64* ts,
                         WinParams wp, PushInfo* info, i64* blk_xm = nullptr, ColSet cols = ColSet{});
+// sorted: the single-pass form for non-decreasing timestamps (timeBatch with nextEmitTime known); it
+// also scans blk_pass (nblk + 1 entries, the last zeroed) with scan_tmp and fixes the boundaries
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
-                       const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
+                       i64* blk_pass_pre, const i64* blk_tl_pre, PushInfo* info, Bound* bounds,
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre = nullptr,
-                       u32* ms_counts = nullptr, int P = 1, int ms_nblk = 0, int ms_col0 = 0);
+                       u32* ms_counts = nullptr, int P = 1, int ms_nblk = 0, int ms_col0 = 0, bool sorted = false,
+                       i64* scan_tmp = nullptr);
 // Rows of one aggregation unit — (segment, key partition) for the multisplit kernel, the segment for
 // the flat one — fill the unit's own region of agg_unit_rows() row slots; unit_rows[u] = its count.
 int agg_unit_rows(int P, int NL, bool own);

@@ -237,14 +237,22 @@ void launch_scan_blocks(hipStream_t s, i64* blk_pass, i64* blk_tl, i64* blk_firs
 //                e's send. Due timers fire before the send is processed and catch up one period
 //                each (Scheduler.sendTimerEvents :171-209), so the window boundaries sit at E0 + kT.
 // ================================================================================================
-template <bool EXT, int FK>
+// Single-pass form (SORTED, timeBatch once nextEmitTime is known): when the send-last timestamps do
+// not decrease, the clock of an event's send is max(carried-in clock, the send's own last timestamp)
+// — no prefix over earlier tiles is needed, so k_blockagg + k_scan_blocks are skipped. Every tile
+// checks that ts never decreases across its events and into the next tile's first event; a tile
+// that finds a decrease sets PushInfo.unsorted and the host redoes the window assignment with the
+// prefix passes. The tile's passing-event count goes to blk_pass[tile] and each boundary records
+// its tile and in-tile count; k_fix_bounds adds the scanned tile prefixes afterwards.
+template <bool EXT, int FK, bool SORTED>
 __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ ts, ColSet cols, FilterProg f,
-                                                      WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
-                                                      const PushInfo* info, Bound* bounds, int max_bounds,
+                                                      WinParams wp, i64* blk_pass_pre, const i64* blk_tl_pre,
+                                                      PushInfo* info, Bound* bounds, int max_bounds,
                                                       int* n_bounds, KeyPlan kp, KeyTable kt, u32* new_pos,
                                                       const i64* blk_xm_pre, u32* ms_counts, int P, int ms_nblk,
                                                       int ms_col0) {
-    i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
+    const int tile = blockIdx.x;
+    i64 base = (i64)tile * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     filter_items<FK>(f, cols, base, wp.N, pass);
     // group-key slot of every passing event, looked up once for the whole pipeline
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
                 if (pass[i]) atomicAdd(&mhist[pos[i] & (P - 1)], 1u);
             __syncthreads();
             for (int i = threadIdx.x; i < P; i += kBlock)
-                ms_counts[(i64)i * ms_nblk + ms_col0 + blockIdx.x] = mhist[i];
+                ms_counts[(i64)i * ms_nblk + ms_col0 + tile] = mhist[i];
         }
     }
     i64 t[kItems];
@@ -297,11 +305,23 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         i64 e = base + i;
         bool in = e < wp.N;
         cnt += pass[i];
-        if (in && sc.last(wp, e)) tl = max(tl, t[i]);
+        if (!SORTED && in && sc.last(wp, e)) tl = max(tl, t[i]);
         sc.next();
     }
-    i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x];
-    i64 pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
+    i64 pcb, pm = INT64_MIN;
+    if (SORTED) {
+        i64 tot_c;
+        pcb = block_excl_scan(cnt, SumOp(), 0, &tot_c);  // in-tile: the tile prefix is added later
+        if (threadIdx.x == 0) blk_pass_pre[tile] = tot_c;
+        bool down = false;
+#pragma unroll
+        for (int i = 0; i + 1 < kItems; i++) down |= base + i + 1 < wp.N && t[i + 1] < t[i];
+        if (base + kItems < wp.N) down |= ts[base + kItems] < t[kItems - 1];
+        if (down) atomicOr(&info->unsorted, 1);
+    } else {
+        pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[tile];
+        pm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[tile]);
+    }
     // externalTimeBatch: running max of the timestamp attribute over the events reaching the window
     constexpr bool ext = EXT;  // externalTimeBatch (the running max M below)
     i64 av[kItems];
@@ -311,11 +331,11 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         i64 xm = INT64_MIN;
 #pragma unroll
         for (int i = 0; i < kItems; i++) if (pass[i]) xm = max(xm, av[i]);
-        M = max(wp.xm0, max(block_excl_scan(xm, MaxOp(), INT64_MIN, nullptr), blk_xm_pre[blockIdx.x]));
+        M = max(wp.xm0, max(block_excl_scan(xm, MaxOp(), INT64_MIN, nullptr), blk_xm_pre[tile]));
     }
     const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
-    const i64 E0 = info->E0;
-    const int e0v = info->e0_valid;
+    const i64 E0 = SORTED ? wp.E0 : info->E0;
+    const int e0v = SORTED ? wp.e0_valid : info->e0_valid;
     if (base >= wp.N) return;
     const bool per_event = send_len(wp) == 1;
     SendCursor sc2(wp, base);
@@ -329,7 +349,8 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         bool pp = eval_filter<FK>(f, cols, ep);
         i64 pcb_prev = pcb - (pp ? 1 : 0);
         // ep and base in one send: ep's clock is that send's clock; else it closed the previous send
-        if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
+        if (SORTED) clock_prev = max(c0, ts[sc2.r != 0 ? sc2.last_of(wp, base) : ep]);
+        else if (sc2.r != 0) clock_prev = max(c0, max(pm, ts[sc2.last_of(wp, base)]));
         else clock_prev = max(c0, pm);
         Wprev = wp.wcol ? wp.W_base + wp.wcol[ep] : wfun(wp, E0, e0v, pcb_prev, ext ? M : clock_prev);
     }
@@ -348,34 +369,64 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
             int k = atomicAdd(n_bounds, 1);
             if (k < max_bounds) {
                 Bound b;
-                b.idx = wp.n_pend + e; b.W = W; b.clock = clk; b.clock_prev = clock_prev; b.pcb = pcb; b.pad = 0;
+                b.idx = wp.n_pend + e; b.W = W; b.clock = clk; b.clock_prev = clock_prev; b.pcb = pcb;
+                b.pad = SORTED ? tile : 0;  // (SORTED: pcb is in-tile until k_fix_bounds)
                 bounds[k] = b;
             }
         }
         Wprev = W;
         clock_prev = clk;
         pcb += pass[i];
-        if (sc2.last(wp, e)) pm = max(pm, t[i]);
+        if (!SORTED && sc2.last(wp, e)) pm = max(pm, t[i]);
         sc2.next();
     }
 }
 
+// SORTED form, after the scan of the tile counts (blk_pass[nblk] = total): the boundaries' pass
+// counts become push-relative and the push totals go to PushInfo (the clock max of a sorted push is
+// its last event's timestamp: the last event always ends a send).
+__global__ __launch_bounds__(kBlock) void k_fix_bounds(Bound* bounds, int max_bounds, const i64* blk_pass_pre,
+                                                      int nblk, const i64* __restrict__ ts, WinParams wp,
+                                                      PushInfo* info) {
+    const int n = min(info->n_bounds, max_bounds);
+    for (int k = threadIdx.x; k < n; k += kBlock) bounds[k].pcb += blk_pass_pre[bounds[k].pad];
+    if (threadIdx.x == 0) {
+        info->total_pass = blk_pass_pre[nblk];
+        info->max_tl = ts[wp.N - 1];
+        info->first_pass = blk_pass_pre[nblk] ? 0 : INT64_MAX;
+        info->E0 = wp.E0;
+        info->e0_valid = wp.e0_valid;
+        info->first_clk = INT64_MIN;
+        info->max_xm = INT64_MIN;
+    }
+}
+
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
-                       const i64* blk_pass_pre, const i64* blk_tl_pre, const PushInfo* info, Bound* bounds,
+                       i64* blk_pass_pre, const i64* blk_tl_pre, PushInfo* info, Bound* bounds,
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre,
-                       u32* ms_counts, int P, int ms_nblk, int ms_col0) {
+                       u32* ms_counts, int P, int ms_nblk, int ms_col0, bool sorted, i64* scan_tmp) {
     const size_t lds = ms_counts ? (size_t)P * 4 : 0;
-    int* nb = (int*)&((PushInfo*)info)->n_bounds;
-#define SH_BOUNDS(EXT, FK)                                                                                      \
-    hipLaunchKernelGGL((k_boundaries<EXT, FK>), dim3(nblk), dim3(kBlock), lds, s, ts, cols, f, wp, blk_pass_pre, \
-                       blk_tl_pre, info, bounds, max_bounds, nb, kp, kt, new_pos, blk_xm_pre, ms_counts, P, ms_nblk,  \
+    int* nb = &info->n_bounds;
+#define SH_BOUNDS(EXT, FK, S)                                                                                     \
+    hipLaunchKernelGGL((k_boundaries<EXT, FK, S>), dim3(nblk), dim3(kBlock), lds, s, ts, cols, f, wp, blk_pass_pre, \
+                       blk_tl_pre, info, bounds, max_bounds, nb, kp, kt, new_pos, blk_xm_pre, ms_counts, P, ms_nblk,   \
                        ms_col0)
     const int fk = filter_kind(f);
-    if (wp.kind == SH_WIN_EXT_TIME_BATCH) SH_BOUNDS(true, 2);
-    else if (fk == 0) SH_BOUNDS(false, 0);
-    else if (fk == 1) SH_BOUNDS(false, 1);
-    else SH_BOUNDS(false, 2);
+    if (wp.kind == SH_WIN_EXT_TIME_BATCH) SH_BOUNDS(true, 2, false);
+    else if (sorted) {
+        if (fk == 0) SH_BOUNDS(false, 0, true);
+        else if (fk == 1) SH_BOUNDS(false, 1, true);
+        else SH_BOUNDS(false, 2, true);
+    } else if (fk == 0) SH_BOUNDS(false, 0, false);
+    else if (fk == 1) SH_BOUNDS(false, 1, false);
+    else SH_BOUNDS(false, 2, false);
 #undef SH_BOUNDS
+    if (sorted) {
+        // blk_pass[nblk] was zeroed with the info block: the scan leaves the total there
+        launch_scan_sum_large(s, blk_pass_pre, nblk + 1, scan_tmp);
+        hipLaunchKernelGGL(k_fix_bounds, dim3(1), dim3(kBlock), 0, s, bounds, max_bounds, blk_pass_pre, nblk, ts, wp,
+                           info);
+    }
 }
 
 // ================================================================================================

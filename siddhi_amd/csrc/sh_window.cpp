@@ -529,11 +529,25 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             wp.wcol = q->given_wcol;
             wp.W_base = q->given_W_base;
         }
-        launch_blockagg(s, b->ts, cs, q->fp, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
-                        q->blk_first.as<int64_t>(), nblk, ext ? q->blk_xm.as<int64_t>() : nullptr,
-                        ext ? q->d.ts_col : -1);
-        launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk,
-                           b->ts, wp, q->info.as<PushInfo>(), ext ? q->blk_xm.as<int64_t>() : nullptr, cs);
+        // timeBatch once nextEmitTime is known: one pass assigns the windows if the timestamps do not
+        // decrease (checked by the pass itself, redone below with the prefix passes if they do);
+        // otherwise (first timeBatch push, lengthBatch, externalTimeBatch, the sharded owner's given
+        // windows) the block-aggregate + scan passes run first
+        const bool single_pass = !ext && !q->given && wp.pcol1 == 0 && wp.kind == SH_WIN_TIME_BATCH && wp.e0_valid;
+        auto prefix_passes = [&] {
+            launch_blockagg(s, b->ts, cs, q->fp, N, b->send_size, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                            q->blk_first.as<int64_t>(), nblk, ext ? q->blk_xm.as<int64_t>() : nullptr,
+                            ext ? q->d.ts_col : -1);
+            launch_scan_blocks(s, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(), q->blk_first.as<int64_t>(), nblk,
+                               b->ts, wp, q->info.as<PushInfo>(), ext ? q->blk_xm.as<int64_t>() : nullptr, cs);
+        };
+        if (single_pass) {
+            RCHK(q->blk_pass.reserve((size_t)(nblk + 1) * 8, false));
+            HIPCHK(hipMemsetAsync(q->info.p, 0, sizeof(PushInfo), s));
+            HIPCHK(hipMemsetAsync(q->blk_pass.as<int64_t>() + nblk, 0, 8, s));
+        } else {
+            prefix_passes();
+        }
         int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
         RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
         RCHK(q->new_pos.reserve((size_t)N * 4, false));
@@ -545,7 +559,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                           q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
                           q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr,
-                          early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t);
+                          early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
+                          single_pass, q->blk_tl.as<int64_t>());
         HIPCHK(hipGetLastError());
         // the push info and the first boundaries come back in one copy; the key partitioning of the
         // push's events (independent of where the windows close) is queued behind it and runs while
@@ -564,6 +579,20 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
         SH_TMARK(3);
         PushInfo info = *q->h_info;
         SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
+        if (single_pass && info.unsorted) {
+            // a timestamp decreased: the send clocks need the prefix passes after all (the key slots,
+            // the multisplit counts and the split already queued do not depend on the windows)
+            SH_TRACE("push: unsorted timestamps, window assignment redone with the prefix passes");
+            prefix_passes();
+            launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                              q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
+                              q->new_pos.as<u32>(), nullptr);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
+            HIPCHK(sh_wait_stream(s));
+            info = *q->h_info;
+        }
         if (info.n_bounds > max_bounds) return sh_fail(SH_ERR_INVALID, "more than 4M windows closed in one push");
         if (ext && info.err)
             return sh_fail(SH_ERR_UNSUPPORTED,

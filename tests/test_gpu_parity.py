@@ -150,6 +150,28 @@ def test_timebatch_small_keys_start_time_and_gaps(rt):
     both(rt, spec, pushes, label="gaps")
 
 
+@pytest.mark.parametrize("send_size", [1, 7])
+def test_timebatch_out_of_order_timestamps(rt, send_size):
+    """Later pushes (nextEmitTime known) take the single-pass window assignment, which holds only for
+    non-decreasing timestamps: jittered and stepped-back timestamps must fall back to the prefix passes
+    and still match the oracle (TimeBatchWindowProcessor :262-340 with the send clock of
+    InputHandler :85-96). Sorted pushes in between take the single pass."""
+    rng = np.random.default_rng(23)
+    n = 300_000
+    ts = (np.arange(n, dtype=np.int64) // 40) + 10_000          # 40 events / ms, sorted
+    ts[100_000:160_000] += rng.integers(-60, 60, 60_000)        # jitter inside one push
+    ts[230_000:] -= 900                                         # a step back below the clock
+    k = rng.integers(0, 5_000, n).astype(np.int32)
+    v = rng.standard_normal(n)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 500, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=5_000)
+    pushes = split_batches(schema, ts, [k, v, ts.copy()], [50_000, 100_000, 160_000, 230_000, 260_000], send_size)
+    pushes.append(("advance", int(ts.max()) + 2_000))
+    out = both(rt, spec, pushes, label="out-of-order ts")
+    assert out["flush_offsets"].size >= 10
+
+
 def test_lengthbatch_types_and_two_keys(rt):
     rng = np.random.default_rng(11)
     n = 50_000
