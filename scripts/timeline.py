@@ -5,7 +5,7 @@ import glob
 import sys
 
 d = sys.argv[1]
-first = sys.argv[2] if len(sys.argv) > 2 else "k_blockagg"
+first = sys.argv[2] if len(sys.argv) > 2 else "k_boundaries"
 f = glob.glob(d + "/**/run_kernel_trace.csv", recursive=True) + glob.glob(d + "/run_kernel_trace.csv")
 rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
