@@ -182,12 +182,13 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
-// word_pre = exclusive popcount prefix of the first-occurrence bitmap; *total = the bitmap's popcount
-void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre, u32* total);
+// word_pre[w] = exclusive popcount prefix of the first-occurrence bitmap before word w (low 32 bits)
+// with word w itself (high 32 bits); *total = the bitmap's popcount
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u64* word_pre, u32* total);
 // rows: the aggregation units' regions; the row count (for the output columns' stride) is read on
 // the device (launch_bits_prefix's total); row_cap bounds it
 void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_rows, i64 n_units, int unit_stride,
-                      i64 row_cap, const u32* n_rows_dev, const u32* bits, const u32* word_pre, int n_aggs, KeyTable kt,
+                      i64 row_cap, const u32* n_rows_dev, const u64* word_pre, int n_aggs, KeyTable kt,
                       KeyPlan kp, i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts,
                       i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
                       i64 seq_base, i64* out_rep, u64* stage);

@@ -925,7 +925,7 @@ __global__ __launch_bounds__(kBlock) void k_bits_tile(const u32* __restrict__ bi
 }
 
 __global__ __launch_bounds__(kBlock) void k_bits_pre(const u32* __restrict__ bits, i64 nw, const i64* tile_pre,
-                                                    u32* word_pre, u32* total) {
+                                                    u64* word_pre, u32* total) {
     const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     u32 b[kItems];
     i64 c = 0;
@@ -934,13 +934,13 @@ __global__ __launch_bounds__(kBlock) void k_bits_pre(const u32* __restrict__ bit
     i64 r = block_excl_scan(c, SumOp(), 0, nullptr) + tile_pre[blockIdx.x];
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
-        if (base + i < nw) word_pre[base + i] = (u32)r;
+        if (base + i < nw) word_pre[base + i] = ((u64)b[i] << 32) | (u32)r;  // the word beside its prefix
         r += __popc(b[i]);
         if (base + i == nw - 1) *total = (u32)r;  // every row's first event has one bit: the row count
     }
 }
 
-void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u32* word_pre, u32* total) {
+void launch_bits_prefix(hipStream_t s, const u32* bits, i64 nw, i64* tile_sum, u64* word_pre, u32* total) {
     const int nb = (int)((nw + kTile - 1) / kTile);
     hipLaunchKernelGGL(k_bits_tile, dim3(nb), dim3(kBlock), 0, s, bits, nw, tile_sum);
     launch_scan_sum(s, tile_sum, nb);
@@ -961,7 +961,7 @@ constexpr int kStageMax = 2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1;
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
                                                      const u32* __restrict__ unit_rows, i64 n_units,
                                                      int unit_stride,
-                                                     const u32* __restrict__ bits, const u32* __restrict__ word_pre,
+                                                     const u64* __restrict__ word_pre,
                                                      int n_aggs, KeyTable kt, KeyPlan kp, i64 n_pend,
                                                      const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
                                                      const u64* __restrict__ pend_gidx,
@@ -981,7 +981,8 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         const ulonglong2 h = *(const ulonglong2*)row;
         const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
         const u32 wd = first >> 5;
-        const i64 o = (i64)word_pre[wd] + __popc(bits[wd] & ((1u << (first & 31)) - 1u));
+        const u64 wp2 = word_pre[wd];  // one read: the bitmap word and the rows before it
+        const i64 o = (i64)(u32)wp2 + __popc((u32)(wp2 >> 32) & ((1u << (first & 31)) - 1u));
         // stream index of an event of the combined (queued + new) sequence
         auto sidx = [&](u32 c) -> i64 {
             if (c < n_pend) return (i64)pend_gidx[c];
@@ -1042,14 +1043,14 @@ __global__ __launch_bounds__(kBlock) void k_emit_soa(const u64* __restrict__ sta
 }
 
 void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_rows, i64 n_units, int unit_stride,
-                      i64 row_cap, const u32* n_rows_dev, const u32* bits, const u32* word_pre, int n_aggs, KeyTable kt,
+                      i64 row_cap, const u32* n_rows_dev, const u64* word_pre, int n_aggs, KeyTable kt,
                       KeyPlan kp, i64 n_pend, const i64* pend_ts, const i64* ts, i64 out_cap, i64* out_ts,
                       i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
                       i64 seq_base, i64* out_rep, u64* stage) {
     if (row_cap <= 0 || n_units <= 0) return;
     const int want_order = out_order ? 1 : 0;
     const unsigned g1 = (unsigned)((n_units * unit_stride + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, bits, word_pre,
+    hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, word_pre,
                        n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
     const unsigned g2 = (unsigned)((row_cap + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_emit_soa, dim3(g2), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,

@@ -288,12 +288,12 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     if (q->given) RCHK(q->out_order.reserve(cap * 8, false));
     const int nbt = (int)((n_words + kTile - 1) / kTile);
     RCHK(q->blk_cnt.reserve((nbt + 16) * 8, false));
-    RCHK(q->word_pre.reserve((size_t)n_words * 4, false));
+    RCHK(q->word_pre.reserve((size_t)n_words * 8, false));
     RCHK(q->emit_stage.reserve(emit_stage_bytes(nk, na, q->given ? 1 : 0, cap), false));
-    launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u32>(),
+    launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u64>(),
                        q->counters.as<u32>());
     launch_emit_rows(s, q->rows.as<u64>(), RW, unit_rows, n_units, unit_stride, cap, q->counters.as<u32>(),
-                     q->first_bits.as<u32>(), q->word_pre.as<u32>(), na, q->kt.dev(), q->kp, q->n_pend,
+                     q->word_pre.as<u64>(), na, q->kt.dev(), q->kp, q->n_pend,
                      q->pend_ts.as<int64_t>(), ts, cap,
                      q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->pend_gidx.as<u64>(),
                      q->given && b ? q->given_gidx : nullptr, q->given ? q->out_order.as<int64_t>() : nullptr, q->seq,
