@@ -341,6 +341,10 @@ typedef struct {
 int sh_query_stats(sh_query* q, sh_stats* out);
 /* The same for the owner pipeline of a sharded query (its last sh_shard_consume). */
 int sh_shard_stats(sh_shard* s, sh_stats* out);
+/* The same for an aggregation's last push: push_ms covers the root window and every roll-up level
+ * (IncrementalExecutor chain, core/aggregation/IncrementalExecutor.java:110-258), main_kernel_ms the
+ * root's base aggregation. */
+int sh_aggregation_stats(sh_aggregation* a, sh_stats* out);
 
 const char* sh_last_error(void);
 int32_t sh_abi_version(void);

@@ -158,6 +158,11 @@ struct sh_aggregation {
     OutHost tout;
     DevBuf root_bucket_col, root_key_col, minmax;
     int64_t* h_minmax = nullptr;
+    // device time of the last push: ev0 before the root's key reservation, ev1 after the roll-up
+    // levels' kernels are queued (read lazily by sh_aggregation_stats)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int64_t last_events = 0;
+    bool timed = false;
 };
 
 static LevelDev level_dev(Level& L, int nb) {
@@ -438,6 +443,8 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         a->bp.kind[i] = a->root->ap.kind[i];
         a->btypes[i] = a->root->vtypes[i];
     }
+    HIPCHK(hipEventCreate(&a->ev0));
+    HIPCHK(hipEventCreate(&a->ev1));
     // constant key / bucket columns for rows without them
     RCHK(a->minmax.reserve(16, false));
     HIPCHK(hipHostMalloc((void**)&a->h_minmax, 16, hipHostMallocDefault));
@@ -493,6 +500,8 @@ static void agg_free(sh_aggregation* a) {
     a->root_key_col.release();
     a->minmax.release();
     if (a->h_minmax) (void)hipHostFree(a->h_minmax);
+    if (a->ev0) (void)hipEventDestroy(a->ev0);
+    if (a->ev1) (void)hipEventDestroy(a->ev1);
     delete a;
 }
 
@@ -535,9 +544,33 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     } else {
         dev = *b;
     }
+    HIPCHK(hipEventRecord(a->ev0, a->ctx->stream));
     RCHK(agg_reserve_root(a, &dev));
     RCHK(sh_push_device(a->root, &dev, &o));
-    return agg_after_root(a, o);
+    RCHK(agg_after_root(a, o));
+    HIPCHK(hipEventRecord(a->ev1, a->ctx->stream));
+    a->last_events = dev.n;
+    a->timed = true;
+    return SH_OK;
+}
+
+// Device time of the last push: the whole pipeline (root window + every roll-up level) and the
+// root's aggregation kernel (IncrementalExecutor's base aggregation over the raw events).
+extern "C" int sh_aggregation_stats(sh_aggregation* a, sh_stats* out) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_stats: NULL argument");
+    *out = sh_stats{};
+    if (!a->timed) return SH_OK;
+    HIPCHK(hipEventSynchronize(a->ev1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, a->ev0, a->ev1));
+    sh_stats rs{};
+    RCHK(sh_query_stats(a->root, &rs));
+    out->push_ms = ms;
+    out->main_kernel_ms = rs.main_kernel_ms;
+    out->main_kernel_bytes = rs.main_kernel_bytes;
+    out->events = a->last_events;
+    return SH_OK;
 }
 
 int agg_after_root(sh_aggregation* a, const sh_out* o) {

@@ -176,6 +176,11 @@ class GpuAggregation:
     def advance_time(self, now: int):
         _check(lib().sh_aggregation_advance_time(self.h, now))
 
+    def stats(self) -> abi.Stats:
+        s = abi.Stats()
+        _check(lib().sh_aggregation_stats(self.h, C.byref(s)))
+        return s
+
     def table_raw(self, duration: int):
         out = C.POINTER(abi.Out)()
         _check(lib().sh_aggregation_table(self.h, duration, C.byref(out)))
