@@ -844,7 +844,8 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
         // compile-time op tables of the common plans (one value column: sum / avg, min + max + avg;
         // two: long sum + double avg); anything else runs the table-driven fold
         constexpr u32 kMinMaxAvgD = agg_sig3(FOP_MIN_D, FOP_MAX_D, FOP_ADD_D), kSumD = agg_sig3(FOP_ADD_D, -1, -1),
-                      kSumI = agg_sig3(FOP_ADD_I, -1, -1), kSumISumD = agg_sig3(FOP_ADD_I, FOP_ADD_D, -1);
+                      kSumI = agg_sig3(FOP_ADD_I, -1, -1), kSumISumD = agg_sig3(FOP_ADD_I, FOP_ADD_D, -1),
+                      kSumMinMaxD = agg_sig3(FOP_ADD_D, FOP_MIN_D, FOP_MAX_D);  // aggregation base values
         const u32 sig = agg_sig(ap);
         if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
         else if (K == 1 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 1, 8, 2, kSumD);
@@ -852,6 +853,8 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
         else if (K == 1 && ap.n_vcols == 2 && sig == kSumISumD) SH_AGG_OWN(2, 1, 4, 2, kSumISumD);
         else if (K == 2 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 2, 8, 4, kMinMaxAvgD);
         else if (K == 2 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 2, 8, 2, kSumD);
+        else if (K == 1 && ap.n_vcols <= 1 && sig == kSumMinMaxD) SH_AGG_OWN(1, 1, 8, 4, kSumMinMaxD);
+        else if (K == 2 && ap.n_vcols <= 1 && sig == kSumMinMaxD) SH_AGG_OWN(1, 2, 8, 4, kSumMinMaxD);
         else if (K == 1) {
             if (ap.n_vcols <= 1) SH_AGG_OWN_F(1, 1, 8);
             else if (ap.n_vcols <= 2) SH_AGG_OWN_F(2, 1, 4);

@@ -88,13 +88,22 @@ int query_set_partition(sh_query* q, int64_t key);
 // Key partitions: the smallest power of two P that leaves at most 512 local keys per partition (the
 // aggregation kernel's threads own one local key each, state in registers), as long as the
 // multisplit's per-tile LDS (staging + per-wave partition counters) fits a CU.
+static bool scatter_fits(const sh_query* q, int p) {
+    const int nv = q->ap.n_vcols;
+    size_t v = nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : 8;
+    return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 20 + 64 <= 160 * 1024;
+}
+
+// the largest key table the partitioning supports (512 local keys per partition)
+static size_t max_table_size(const sh_query* q) {
+    int P = 1;
+    while (P < 16384 && scatter_fits(q, P << 1)) P <<= 1;
+    return (size_t)P * 512;
+}
+
 static int size_partitions(sh_query* q) {
     const size_t ts = q->kt.size_;
-    auto scatter_fits = [&](int p) {
-        const int nv = q->ap.n_vcols;
-        size_t v = nv <= 1 ? 1 : nv <= 2 ? 2 : nv <= 4 ? 4 : 8;
-        return v * kTile * 8 + (size_t)kTile * 8 + (size_t)p * 20 + 64 <= 160 * 1024;
-    };
+    auto scatter_fits = [&](int p) { return ::scatter_fits(q, p); };
     int P = 1;
     while (ts / P > 512 && P < 16384 && scatter_fits(P << 1)) P <<= 1;
     if (ts / P > 512) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
@@ -123,10 +132,25 @@ int query_reserve_keys(sh_query* q, int64_t extra) {
     if (q->kt.dense) return SH_OK;  // slots are the dictionary ids themselves
     int64_t ts = (int64_t)q->kt.size_;
     if (q->kt.n_keys + extra <= ts / 2) return SH_OK;
+    auto pow2_for = [](int64_t n) {
+        size_t w = 16;
+        while ((int64_t)w < 2 * n) w <<= 1;
+        return w;
+    };
+    // the open window's keys survive the rebuild: at most min(keys so far, queued events)
     int64_t live = std::min<int64_t>(q->kt.n_keys, q->n_pend);
-    size_t want = 16;
-    while ((int64_t)want < 2 * (live + extra)) want <<= 1;
-    return rekey(q, std::max(want, q->kt_min_size));
+    bool compacted = false;
+    if (std::max(pow2_for(live + extra), q->kt_min_size) > max_table_size(q)) {
+        // that bound is too loose to fit: compact to the live keys first (the rebuild counts them)
+        RCHK(rekey(q, std::max(pow2_for(live), q->kt_min_size)));
+        live = q->kt.n_keys;
+        compacted = true;
+        SH_TRACE("reserve_keys: compacted to %lld live keys", (long long)live);
+    }
+    const size_t want = std::max(pow2_for(live + extra), q->kt_min_size);
+    SH_TRACE("reserve_keys: n_keys=%lld n_pend=%lld extra=%lld size=%lld -> %lld", (long long)q->kt.n_keys,
+             (long long)q->n_pend, (long long)extra, (long long)ts, (long long)want);
+    return compacted && want == q->kt.size_ ? SH_OK : rekey(q, want);
 }
 
 extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
