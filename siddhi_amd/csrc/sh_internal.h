@@ -278,4 +278,30 @@ void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec
                          ShardSrc src, const i64* bound_gidx, const i64* bound_W, int n_bounds, i64 W_base, i64* ts,
                          ColPtrs cols, int* wcol, u64* gidx);
 
+// ---- expired / all-events output of batch windows, pass-through batch queries (sh_expired*) ----
+// One output flush: expired rows of the previous batch [p_lo, p_lo + p_n) and/or current rows
+// [c_lo, c_lo + c_n) of the source array; tab_size > 0: merged by key through a table at tab_off.
+struct XItem {
+    i64 p_lo, p_n, c_lo, c_n, clock, tab_off, tab_size, out_base;
+};
+struct XOut {
+    i64* ts;
+    unsigned char* expired;
+    i64* keys;
+    u64* vals;
+    unsigned char* nulls;
+    i64* rep;
+};
+void launch_x_merge(hipStream_t s, const XItem* items, const i64* cum_c, const i64* cum_p, int n_items, i64 tot_c,
+                    i64 tot_p, const i64* s_keys, i64 S, int nk, u32* trow, u64* tkey, int* match, u32* keep,
+                    u32* item_matched);
+void launch_x_scatter(hipStream_t s, const XItem* items, const i64* cum, int n_items, i64 total, const i64* s_ts,
+                      const i64* s_keys, const u64* s_vals, const unsigned char* s_nulls, const i64* s_rep, i64 S,
+                      int nk, int na, u32 count_mask, const int* match, const u32* keep, const u32* rank, i64 T,
+                      XOut out);
+// pass-through rows of the closed segments: pos = exclusive prefix of passing events over [0, hi]
+void launch_pass_rows(hipStream_t s, i64 hi, i64 n_pend, const u32* new_pos, u32* pos, i64* tmp, const i64* pend_ts,
+                      const u64* pend_gidx, const i64* ts, i64 seq_base, const Segment* segs, int nseg, i64* out_ts,
+                      i64* out_rep, u32* seg_rows, u32* n_rows);
+
 }  // namespace shd

@@ -246,7 +246,21 @@ struct sh_query {
     std::vector<sh_bound> gbounds;  // this push's global window starts, sorted by gidx
     DevBuf pend_gidx, out_order;  // pend_gidx: stream index of every queued event (all modes)
     std::vector<int64_t> order_host;
+    // `expired` / `all events` output (sh_expired.cpp): the current rows of a call are turned into
+    // the output flushes; the last flushed batch is carried until its successor closes
+    bool xmode = false;
+    bool xc_valid = false;
+    int64_t xc_n = 0, xc_W = 0;
+    DevBuf xc_keys, xc_rep, xc_keys2, xc_rep2;                   // carried rows
+    DevBuf xs_ts, xs_keys, xs_vals, xs_nulls, xs_rep;            // source rows of a call
+    DevBuf x_ts, x_keys, x_vals, x_nulls, x_expired, x_rep;      // output rows
+    DevBuf x_items, x_keep, x_rank, x_match, x_tmp, x_matched, x_trow, x_tkey, pass_pos;
+    PinnedBuf x_h;
+    std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call
 };
+
+// expired / all-events output of a batch query's call (sh_expired.cpp)
+int xout_finish(sh_query* q, bool host_out, const sh_out** out);
 
 // the filter restricted to partition key `key` (R12): base AND (pcol == key)
 int partition_filter(const FilterProg& base, int pcol, int ptype, int64_t key, FilterProg* out);

@@ -96,6 +96,8 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows carry 2 extra columns: at most 6 stream columns");
     if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
+    if (d->expired_on || !d->current_on || d->n_aggs < 1)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries emit current events of aggregations (`insert into`)");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     sh_shard* s = new sh_shard();
     s->ctx = ctx;

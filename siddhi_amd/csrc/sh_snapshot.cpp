@@ -212,6 +212,7 @@ extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* l
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
     if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
+    if (q->xmode) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a query with expired / all-events output");
     Writer w;
     w.put("SHQ1", 4);
     w.val<uint32_t>(kVersion);

@@ -167,8 +167,11 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     for (int c = 0; c < d->n_cols; c++)
         if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
-    if (d->n_aggs < 1 || d->n_aggs > SH_MAX_AGGS)
-        return sh_fail(SH_ERR_UNSUPPORTED, "GPU path runs aggregation queries (1..8 aggregators)");
+    const bool batch_win = d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME_BATCH;
+    const bool pass_through = d->n_aggs == 0 && d->n_group_by == 0 && batch_win && d->partition_col < 0;
+    if ((d->n_aggs < 1 && !pass_through) || d->n_aggs > SH_MAX_AGGS)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "GPU path runs aggregation queries (1..8 aggregators) or pass-through lengthBatch/timeBatch");
     if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME &&
         d->window != SH_WIN_EXT_TIME_BATCH && d->window != SH_WIN_EXT_TIME)
         return sh_fail(SH_ERR_UNSUPPORTED,
@@ -186,8 +189,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
             return sh_fail(SH_ERR_UNSUPPORTED, "partitioned externalTimeBatch is not on the GPU");
     }
     if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
-    if (!d->current_on || d->expired_on)
-        return sh_fail(SH_ERR_UNSUPPORTED, "GPU windows emit current events only (`insert into`)");
+    if (!d->current_on && !d->expired_on) return sh_fail(SH_ERR_INVALID, "query emits neither current nor expired events");
+    if ((!d->current_on || d->expired_on) && !(batch_win && d->partition_col < 0))
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "expired / all-events output runs on lengthBatch and timeBatch (not partitioned) windows");
     if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "stream.current.event batch windows not on the GPU yet");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
@@ -218,6 +223,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0;
+    q->xmode = d->expired_on != 0;
     if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) {
         q->kind = 1;
         if ((rc = sliding_create(q))) { delete q; return rc; }
@@ -253,6 +259,49 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     const int64_t* ts = b ? b->ts : nullptr;
+    if (q->ap.n == 0) {
+        // pass-through (`select *` without aggregators or group-by): every passing event of the
+        // closed batches is a row, in stream order (QuerySelector.processNoGroupBy :161-205)
+        RCHK(q->pass_pos.reserve((size_t)(closed_hi + 1) * 4, false));
+        RCHK(q->x_tmp.reserve((size_t)((closed_hi + 1 + kTile - 1) / kTile + 16) * 8, false));
+        RCHK(q->counters.reserve(64 + (size_t)nseg * 4, false));
+        RCHK(q->h_up.reserve((size_t)nseg * sizeof(Segment)));
+        RCHK(q->segs.reserve(nseg * sizeof(Segment), false));
+        std::memcpy(q->h_up.p, segs.data(), (size_t)nseg * sizeof(Segment));
+        HIPCHK(hipMemcpyAsync(q->segs.p, q->h_up.p, nseg * sizeof(Segment), hipMemcpyHostToDevice, s));
+        const int64_t cap = std::max<int64_t>(closed_hi, 1);
+        RCHK(q->out_ts.reserve(cap * 8, false));
+        RCHK(q->out_rep.reserve(cap * 8, false));
+        RCHK(q->out_keys.reserve(8, false));
+        RCHK(q->out_vals.reserve(8, false));
+        RCHK(q->out_nulls.reserve(8, false));
+        RCHK(q->out_expired.reserve(cap, false));
+        HIPCHK(hipMemsetAsync(q->out_expired.p, 0, cap, s));
+        q->zeroed_expired = nullptr;
+        uint32_t* unit_rows = (uint32_t*)(q->counters.as<char>() + 64);
+        HIPCHK(hipEventRecord(q->ev_agg0, s));
+        launch_pass_rows(s, closed_hi, q->n_pend, b ? q->new_pos.as<u32>() : nullptr, q->pass_pos.as<u32>(),
+                         q->x_tmp.as<int64_t>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(), ts, q->seq,
+                         q->segs.as<Segment>(), nseg, q->out_ts.as<int64_t>(), q->out_rep.as<int64_t>(), unit_rows,
+                         q->counters.as<u32>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(q->ev_agg1, s));
+        RCHK(q->h_tail.reserve(16 + (size_t)nseg * 4));
+        HIPCHK(hipMemcpyAsync(q->h_tail.as<char>() + 16, unit_rows, nseg * 4, hipMemcpyDeviceToHost, s));
+        auto& t = q->tail;
+        t.active = true;
+        t.host_done = false;
+        t.nseg = nseg;
+        t.units_per_seg = 1;
+        t.closed_hi = closed_hi;
+        t.clocks = clocks;
+        t.windows = windows;
+        if (host_out) {
+            HIPCHK(hipStreamSynchronize(s));
+            RCHK(closed_finish(q, true));
+        }
+        return SH_OK;
+    }
     // row capacity: per segment at most min(len, distinct keys)
     int64_t row_cap = 0;
     for (auto& sg : segs) row_cap += std::min<int64_t>(sg.hi - sg.lo, (int64_t)q->kt.size_ + 1);
@@ -499,8 +548,11 @@ int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend) {
     return grow_pending(q, n_pend, 0);
 }
 
-static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh_out** out) {
     SH_TMARK(0);
+    // expired / all-events output: the current rows stay on the device for xout_finish
+    const bool host_out = host_out_req && !q->xmode;
+    q->x_closes.clear();
     hipStream_t s = q->ctx->stream;
     q->out.reset();
     q->dev_flush_offsets.assign(1, 0);
@@ -632,6 +684,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
             }
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
+        if (q->xmode)
+            for (auto& bd : bounds) q->x_closes.emplace_back(bd.W, bd.clock);
         if (!q->given) {
             q->e0_valid = info.e0_valid;
             q->E0 = info.E0;
@@ -711,6 +765,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out, const sh_out
     q->stats.push_ms = ms;
     q->stats.events = N;
     q->stats.main_kernel_bytes = q->agg_bytes;
+    if (q->xmode) return xout_finish(q, host_out_req, out);
     finish_out(q, host_out, out);
     SH_TMARK(6);
     return SH_OK;
@@ -735,7 +790,9 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
     return push_core(q, b, false, out);
 }
 
-static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** out) {
+static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_out** out) {
+    const bool host_out = host_out_req && !q->xmode;
+    q->x_closes.clear();
     q->out.reset();
     q->order_host.clear();
     q->dev_flush_offsets.assign(1, 0);
@@ -745,11 +802,16 @@ static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** 
     q->ms_ready = false;
     q->tail.active = false;
     // TimestampGeneratorImpl.setCurrentTimestamp only moves the clock forward (:104-122)
-    if (q->clock_valid && now < q->clock) { finish_out(q, host_out, out); return SH_OK; }
+    if (q->clock_valid && now < q->clock) {
+        if (q->xmode) return xout_finish(q, host_out_req, out);
+        finish_out(q, host_out, out);
+        return SH_OK;
+    }
     q->clock = now;
     q->clock_valid = true;
     if (q->d.window == SH_WIN_TIME_BATCH && q->e0_valid) {
         int64_t W = wfun_host(q, now);
+        if (q->xmode && W > q->W_open) q->x_closes.emplace_back(W, now);
         if (W > q->W_open && q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{now}, windows{q->W_open};
@@ -760,6 +822,7 @@ static int advance_core(sh_query* q, int64_t now, bool host_out, const sh_out** 
         }
         q->W_open = std::max(q->W_open, W);
     }
+    if (q->xmode) return xout_finish(q, host_out_req, out);
     finish_out(q, host_out, out);
     return SH_OK;
 }

@@ -28,11 +28,18 @@ def both(rt, spec, pushes, rtol=None, label=""):
     return gout
 
 
-# ---- reference KATs that the GPU path runs (aggregating lengthBatch / timeBatch, current events) ----
-GPU_KATS = [c for c in kat_runner.load_cases()
-            if c.get("kind") != "aggregation" and c["query"].get("window") in ("lengthBatch", "timeBatch", "time")
-            and c["query"].get("aggs") and c["query"].get("output", "current") == "current"
-            and not c["query"].get("stream_current")]
+# ---- reference KATs that the GPU path runs: aggregating or pass-through lengthBatch / timeBatch with
+# current, expired or all-events output; aggregating sliding time windows with current events ----
+def _gpu_runs(c):
+    q = c.get("query", {})
+    if c.get("kind") == "aggregation" or q.get("stream_current"):
+        return False
+    if q.get("window") in ("lengthBatch", "timeBatch"):
+        return bool(q.get("aggs")) or not q.get("group_by")
+    return q.get("window") == "time" and bool(q.get("aggs")) and q.get("output", "current") == "current"
+
+
+GPU_KATS = [c for c in kat_runner.load_cases() if _gpu_runs(c)]
 
 
 @pytest.mark.parametrize("case", GPU_KATS, ids=[c["name"] for c in GPU_KATS])
