@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 4
+#define SH_ABI_VERSION 5
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -330,6 +330,20 @@ int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_desc* desc, in
 /* Pinned host buffers for zero-copy packing of Event[] chunks (hipHostMalloc). */
 int sh_alloc_pinned(int64_t bytes, void** out);
 int sh_free_pinned(void* p);
+
+/* Double-buffered host ingest: the Java side packs each ComplexEventChunk micro-batch into pinned
+ * SoA buffers (sh_alloc_pinned) and hands it over as InputHandler.send(Event[]) would
+ * (InputHandler.java:85-96 -> StreamJunction.sendEvent, StreamJunction.java:104-131; the @async
+ * junction's batching, :279-316). sh_stage queues the batch's H2D copy into one of the query's two
+ * device staging slots on the context's copy stream and returns at once with a ticket;
+ * sh_push_staged(ticket) runs the push once that copy has landed, with host output as sh_push.
+ * Staging batch i+1 before pushing batch i overlaps its PCIe copy with batch i's kernels. At most
+ * two tickets are outstanding; they are pushed in staging order; a staged batch's host buffers must
+ * stay unchanged until its push returns. sh_ingest_stats: HIP-event time and bytes of the H2D copy
+ * of the last pushed batch (copy stream). */
+int sh_stage(sh_query* q, const sh_batch* batch, int32_t* ticket);
+int sh_push_staged(sh_query* q, int32_t ticket, const sh_out** out);
+int sh_ingest_stats(sh_query* q, double* h2d_ms, int64_t* h2d_bytes);
 
 /* Device timing of the last push: kernel time of the dominant kernel and of the whole push. */
 typedef struct {

@@ -387,6 +387,9 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
     lib.sh_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
     lib.sh_alloc_pinned.argtypes = [C.c_int64, P(C.c_void_p)]
+    lib.sh_stage.argtypes = [C.c_void_p, P(Batch), P(C.c_int32)]
+    lib.sh_push_staged.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
+    lib.sh_ingest_stats.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int64)]
     lib.sh_free_pinned.argtypes = [C.c_void_p]
     lib.sh_query_stats.argtypes = [C.c_void_p, P(Stats)]
     lib.sh_aggregation_stats.argtypes = [C.c_void_p, P(Stats)]
@@ -420,5 +423,5 @@ ABI_SYMBOLS = [
     "sh_alloc_pinned", "sh_free_pinned", "sh_query_stats", "sh_last_error", "sh_abi_version",
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
-    "sh_aggregation_shard_create", "sh_aggregation_stats",
+    "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
 ]

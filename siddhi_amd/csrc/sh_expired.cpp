@@ -238,8 +238,8 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
     if (host_out) {
         OutHost& o = q->out;
         o.reset();
-        o.flush_offsets = fo;
-        o.flush_clock = fc;
+        o.flush_offsets.assign(fo.begin(), fo.end());
+        o.flush_clock.assign(fc.begin(), fc.end());
         o.ts.resize(T);
         o.expired.resize(T);
         o.rep.resize(T);
@@ -261,8 +261,8 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         *out = o.view(nk, na, q->vtypes);
     } else {
         HIPCHK(hipStreamSynchronize(s));
-        q->dev_flush_offsets = fo;
-        q->dev_flush_clock = fc;
+        q->dev_flush_offsets.assign(fo.begin(), fo.end());
+        q->dev_flush_clock.assign(fc.begin(), fc.end());
         sh_out& o = q->dev_out;
         o = sh_out{};
         o.n_flushes = (int64_t)fc.size();

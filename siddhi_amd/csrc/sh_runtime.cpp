@@ -178,7 +178,9 @@ extern "C" int sh_init(int32_t device, sh_ctx** out) {
     c->device = device;
     c->num_cus = prop.multiProcessorCount;
     c->max_lds = (int)prop.sharedMemPerBlock;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
         delete c;
         return sh_fail(SH_ERR_DEVICE, "hipStreamCreate failed");
     }
@@ -189,7 +191,9 @@ extern "C" int sh_init(int32_t device, sh_ctx** out) {
 extern "C" int sh_ctx_destroy(sh_ctx* c) {
     if (!c) return SH_OK;
     (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->copy_stream);
     delete c;
     return SH_OK;
 }

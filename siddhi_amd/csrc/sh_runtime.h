@@ -3,7 +3,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <new>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -14,6 +17,7 @@ struct sh_ctx {
     int num_cus = 0;
     int max_lds = 0;
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // H2D staging of host batches (sh_stage), beside the compute stream
 };
 
 int sh_fail(int code, const std::string& msg);
@@ -122,11 +126,33 @@ struct KeyTableHost {
     void release() { keys.release(); ctrl.release(); }
 };
 
+// Host vectors in pinned memory (hipHostMalloc) without value-initialisation on resize: the row
+// arrays of a push are D2H copy targets, refilled every push, so they land at the copy engine's rate
+// instead of through a pageable bounce buffer, and a resize does not first zero them.
+template <typename T>
+struct PinnedAlloc {
+    typedef T value_type;
+    PinnedAlloc() = default;
+    template <typename U> PinnedAlloc(const PinnedAlloc<U>&) {}
+    T* allocate(size_t n) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess)
+            throw std::bad_alloc();
+        return (T*)p;
+    }
+    void deallocate(T* p, size_t) { (void)hipHostFree(p); }
+    template <typename U> void construct(U* p) { ::new ((void*)p) U; }  // default-init: no zeroing
+    template <typename U, typename... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+    template <typename U> bool operator==(const PinnedAlloc<U>&) const { return true; }
+    template <typename U> bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+template <typename T> using PinnedVec = std::vector<T, PinnedAlloc<T>>;
+
 // Host copy of a push's output (sh_out points into these vectors).
 struct OutHost {
-    std::vector<int64_t> flush_offsets{0}, flush_clock, ts, keys, rep;
-    std::vector<uint8_t> expired, nulls;
-    std::vector<uint64_t> vals;
+    PinnedVec<int64_t> flush_offsets{0}, flush_clock, ts, keys, rep;
+    PinnedVec<uint8_t> expired, nulls;
+    PinnedVec<uint64_t> vals;
     sh_out out{};
     void reset() {
         flush_offsets.assign(1, 0);
@@ -226,7 +252,7 @@ struct sh_query {
     StagedBatch staged;
     OutHost out;
     sh_out dev_out{};
-    std::vector<int64_t> dev_flush_offsets{0}, dev_flush_clock;
+    PinnedVec<int64_t> dev_flush_offsets{0}, dev_flush_clock;
     hipEvent_t ev_push0 = nullptr, ev_push1 = nullptr, ev_agg0 = nullptr, ev_agg1 = nullptr;
     hipEvent_t ev_mid = nullptr;  // the push info and boundaries are on the host (work queued after it runs on)
     sh_stats stats{};
@@ -257,7 +283,24 @@ struct sh_query {
     DevBuf x_items, x_keep, x_rank, x_match, x_tmp, x_matched, x_trow, x_tkey, pass_pos;
     PinnedBuf x_h;
     std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call
+    // double-buffered host ingest (sh_ingest.cpp): two device staging slots filled on the copy stream
+    struct Ingest {
+        StagedBatch slot[2];
+        sh_batch dev[2]{};
+        hipEvent_t copied[2]{}, consumed[2]{}, c0[2]{}, c1[2]{};
+        bool used[2]{};
+        int next_stage = 0, next_push = 0, outstanding = 0;
+        uint32_t gen = 0;
+        uint32_t ticket_gen[2]{};
+        int64_t bytes[2]{};
+        double last_h2d_ms = 0;
+        int64_t last_h2d_bytes = 0;
+    } ing;
 };
+
+// push of a batch staged on the device by sh_stage, host output (sh_window.cpp)
+int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out);
+void ingest_destroy(sh_query* q);  // (sh_ingest.cpp)
 
 // expired / all-events output of a batch query's call (sh_expired.cpp)
 int xout_finish(sh_query* q, bool host_out, const sh_out** out);

@@ -427,24 +427,24 @@ static int closed_finish(sh_query* q, bool host_out) {
         q->out.rep.resize(nb);
         HIPCHK(hipMemcpyAsync(q->out.ts.data() + base, q->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(q->out.rep.data() + base, q->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, s));
-        // keys / vals / nulls are [k][n_rows] blocks (a push closes windows through run_closed at most once)
-        std::vector<int64_t> k(nk * n_rows);
-        std::vector<uint64_t> v(na * n_rows);
-        if (nk) HIPCHK(hipMemcpyAsync(k.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+        // keys / vals / nulls are [k][n_rows] blocks straight into the pinned output vectors (a push
+        // closes windows through run_closed at most once, so they start empty)
+        if (base != 0) return sh_fail(SH_ERR_INVALID, "host output appended twice in one push");
+        q->out.keys.resize((size_t)nk * n_rows);
+        q->out.vals.resize((size_t)na * n_rows);
+        if (nk) HIPCHK(hipMemcpyAsync(q->out.keys.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
         if (q->given) {
             size_t ob = q->order_host.size();
             q->order_host.resize(ob + n_rows);
             HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
         }
-        HIPCHK(hipMemcpyAsync(v.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+        if (na) HIPCHK(hipMemcpyAsync(q->out.vals.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+        q->out.nulls.assign((size_t)na * n_rows, 0);
         HIPCHK(hipStreamSynchronize(s));
-        q->out.keys.insert(q->out.keys.end(), k.begin(), k.end());
-        q->out.vals.insert(q->out.vals.end(), v.begin(), v.end());
-        q->out.nulls.insert(q->out.nulls.end(), (size_t)na * n_rows, 0);
     }
     // flush bookkeeping (one flush per non-empty closed segment)
-    std::vector<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
-    std::vector<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
+    PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
+    PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
     int64_t acc = fo.back();
     for (int i = 0; i < t.nseg; i++) {
         if (seg_rows[i] == 0) continue;
@@ -783,6 +783,12 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     return push_core(q, &dev, true, out);
 }
 
+// a push whose batch is already on the device, with host output (sh_push_staged)
+int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out) {
+    if (q->kind == 1) return sliding_push(q, dev, true, out);
+    return push_core(q, dev, true, out);
+}
+
 extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
@@ -843,6 +849,16 @@ extern "C" int sh_query_destroy(sh_query* q) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q) return SH_OK;
     (void)hipStreamSynchronize(q->ctx->stream);
+    (void)hipStreamSynchronize(q->ctx->copy_stream);
+    {
+        // staging slots were allocated outside stream order (sh_ingest.cpp)
+        StreamScope none(nullptr);
+        for (auto& sl : q->ing.slot) {
+            sl.ts.release();
+            for (auto& c : sl.cols) c.release();
+        }
+    }
+    ingest_destroy(q);
     if (q->kind == 1) sliding_destroy(q);
     // device buffers are released by their destructors (stream-ordered on this context)
     q->kt.release();

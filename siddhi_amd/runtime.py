@@ -9,6 +9,8 @@ no CPU fallback — importing this module on a box without the built library rai
 from __future__ import annotations
 
 import ctypes as C
+
+import numpy as np
 import os
 from typing import Callable, List, Optional
 
@@ -29,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 4:
+        if L.sh_abi_version() != 5:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -114,6 +116,31 @@ class GpuQuery:
         _check(lib().sh_push_device(self.h, C.byref(b), C.byref(out)))
         return out
 
+    # -- double-buffered host ingest (sh_stage / sh_push_staged) -----------------------------
+    def stage(self, batch) -> int:
+        """Queue the H2D copy of a host batch (ideally a PinnedBatch) on the copy stream; returns the
+        ticket for push_staged. The batch must stay alive and unchanged until its push returns."""
+        t = C.c_int32()
+        _check(lib().sh_stage(self.h, C.byref(batch.b), C.byref(t)))
+        self._staged = getattr(self, "_staged", {})
+        self._staged[t.value] = batch
+        return t.value
+
+    def push_staged_raw(self, ticket: int):
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_push_staged(self.h, ticket, C.byref(out)))
+        getattr(self, "_staged", {}).pop(ticket, None)  # its copy has landed and been consumed
+        return out
+
+    def push_staged(self, ticket: int):
+        return abi.decode_out(self.push_staged_raw(ticket))
+
+    def ingest_stats(self):
+        """(H2D copy ms, bytes) of the last pushed staged batch."""
+        ms, nb = C.c_double(), C.c_int64()
+        _check(lib().sh_ingest_stats(self.h, C.byref(ms), C.byref(nb)))
+        return ms.value, nb.value
+
     def advance_time_raw(self, now: int):
         out = C.POINTER(abi.Out)()
         _check(lib().sh_advance_time(self.h, now, C.byref(out)))
@@ -193,6 +220,54 @@ class GpuAggregation:
         if self.h:
             lib().sh_aggregation_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedBatch:
+    """An sh_batch whose SoA columns live in pinned host memory (sh_alloc_pinned): what the Java shim
+    packs a ComplexEventChunk into. `fill` copies numpy columns in; `view` exposes them."""
+
+    def __init__(self, schema: abi.Schema, capacity: int, send_size: int = 0):
+        self.schema = schema
+        self.capacity = capacity
+        self._ptrs = []
+        sizes = [8] + [np.dtype(abi.NP_DTYPE[t]).itemsize for t in schema.types]
+        self.arrays = []
+        for sz, dt in zip(sizes, [np.int64] + [abi.NP_DTYPE[t] for t in schema.types]):
+            p = C.c_void_p()
+            _check(lib().sh_alloc_pinned(max(1, capacity * sz), C.byref(p)))
+            self._ptrs.append(p)
+            buf = (C.c_char * (capacity * sz)).from_address(p.value)
+            self.arrays.append(np.frombuffer(buf, dtype=dt, count=capacity))
+        self.b = abi.Batch()
+        self.b.send_size = send_size
+        self.b.ts = self._ptrs[0].value
+        for i in range(len(schema.types)):
+            self.b.cols[i] = self._ptrs[1 + i].value
+        self.b.n = 0
+
+    def fill(self, ts, cols, send_size=None):
+        n = len(ts)
+        assert n <= self.capacity
+        self.arrays[0][:n] = ts
+        for a, c in zip(self.arrays[1:], cols):
+            a[:n] = c
+        self.b.n = n
+        if send_size is not None:
+            self.b.send_size = send_size
+        return self
+
+    def close(self):
+        for p in self._ptrs:
+            if p.value:
+                lib().sh_free_pinned(p)
+        self._ptrs = []
+        self.arrays = []
 
     def __del__(self):
         try:

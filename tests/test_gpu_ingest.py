@@ -1,0 +1,73 @@
+"""Double-buffered host ingest (sh_stage / sh_push_staged): pinned SoA micro-batches copied on the
+copy stream while the previous batch is processed give exactly the output of sh_push and of the
+oracle (InputHandler.send(Event[]) per micro-batch, InputHandler.java:85-96)."""
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleQuery
+from siddhi_amd import abi, synth
+from tests.parity import assert_same, run_pushes
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = abi.Schema.parse("k string, v double, ts long")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def staged_run(rt, g, schema, ts, cols, chunk, send_size):
+    """Stage batch i+1 before pushing batch i (two pinned buffers in rotation)."""
+    bufs = [rt.PinnedBatch(schema, chunk), rt.PinnedBatch(schema, chunk)]
+    edges = list(range(0, len(ts), chunk)) + [len(ts)]
+    parts, tickets = [], []
+    for i, (a, b) in enumerate(zip(edges[:-1], edges[1:])):
+        pb = bufs[i % 2].fill(ts[a:b], [c[a:b] for c in cols], send_size)
+        tickets.append(g.stage(pb))
+        if len(tickets) == 2:
+            parts.append(abi.out_arrays(g.push_staged_raw(tickets.pop(0))))
+    while tickets:
+        parts.append(abi.out_arrays(g.push_staged_raw(tickets.pop(0))))
+    ms, nb = g.ingest_stats()
+    assert nb > 0 and ms > 0
+    for b in bufs:
+        b.close()
+    return abi.concat_arrays(parts), edges
+
+
+@pytest.mark.parametrize("window,param,chunk", [("timeBatch", 1000, 50_000), ("time", 500, 20_000),
+                                                ("lengthBatch", 3000, 1000)])
+def test_staged_ingest_matches_oracle(rt, window, param, chunk):
+    ts, cols = synth.keyed_stream(0, 200_000, 0xC2, 5_000, 100)
+    spec = abi.QuerySpec(SCHEMA, window, param, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=5_000)
+    g = rt.GpuQuery(spec)
+    gout, edges = staged_run(rt, g, SCHEMA, ts, cols, chunk, 1)
+    o = OracleQuery(spec)
+    pushes = [abi.HostBatch(SCHEMA, ts[a:b], [c[a:b] for c in cols], 1) for a, b in zip(edges[:-1], edges[1:])]
+    assert_same(gout, run_pushes(o, pushes), label=f"staged {window}")
+    g.close()
+    o.close()
+
+
+def test_staged_tickets_are_checked(rt):
+    from siddhi_amd.runtime import SiddhiError
+    ts, cols = synth.keyed_stream(0, 3_000, 0xC2, 100, 10)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 100, group_by=["k"], aggs=[("count", None)], key_capacity=128)
+    g = rt.GpuQuery(spec)
+    bs = [abi.HostBatch(SCHEMA, ts[i * 1000:(i + 1) * 1000], [c[i * 1000:(i + 1) * 1000] for c in cols], 1)
+          for i in range(3)]
+    t0 = g.stage(bs[0])
+    t1 = g.stage(bs[1])
+    with pytest.raises(SiddhiError, match="two staged"):
+        g.stage(bs[2])
+    with pytest.raises(SiddhiError, match="order they were staged"):
+        g.push_staged(t1)
+    g.push_staged(t0)
+    g.push_staged(t1)
+    with pytest.raises(SiddhiError, match="order they were staged"):
+        g.push_staged(t1)
+    g.close()
