@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -36,7 +37,8 @@ struct SlidingImpl {
     // per push scratch
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
         tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_rep, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
-        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock;
+        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock, sort_tmp,
+        key_off, g_rank, inv, rows_k;
     SlInfo* h_info = nullptr;
     PinnedBuf h_up;  // pinned staging of small host->device uploads
     sh_out dev_out{};
@@ -140,7 +142,7 @@ void sliding_destroy(sh_query* q) {
                       &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
                       &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
-                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk};
+                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk, &s->sort_tmp, &s->key_off, &s->g_rank, &s->inv, &s->rows_k};
     for (DevBuf* b : bufs) b->release();
     if (s->h_info) (void)hipHostFree(s->h_info);
     delete s;
@@ -275,18 +277,8 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     }
     int64_t n_rows = 0;
     if (M > 0) {
-        // stable split of the records by key partition
-        int P = s->P;
-        int mblk = (int)((M + kTile - 1) / kTile);
-        int64_t ncnt = (int64_t)P * mblk;
-        RCHK(s->counts.reserve((ncnt + 1) * 8, false));
-        RCHK(s->tmp.reserve(((ncnt + kTile) / kTile + 16) * 8, false));
-        RCHK(s->ranks.reserve(M * 4, false));
-        RCHK(s->part_off.reserve((P + 1) * 8, false));
-        launch_sl_multisplit(st, s->rec_slot.as<u32>(), M, P, s->counts.as<int64_t>(), s->tmp.as<int64_t>(),
-                             s->ranks.as<u32>(), s->part_off.as<int64_t>());
+        const int na = q->ap.n;
         // rows indexed by first-occurrence rank
-        int na = q->ap.n;
         RCHK(s->flags.reserve(M + 16, false));
         RCHK(s->rows_ts.reserve(M * 8, false));
         RCHK(s->rows_rep.reserve(M * 4, false));
@@ -298,20 +290,61 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
         SlRows rows{s->rows_ts.as<int64_t>(), s->rows_rep.as<u32>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
                     s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
-        // the records in partition order
-        RCHK(s->p_raw.reserve(M * 4, false));
-        RCHK(s->p_slot.reserve(M * 4, false));
-        RCHK(s->p_clock.reserve(M * 8, false));
-        RCHK(s->p_pm.reserve(M * 8, false));
-        RCHK(s->p_ts.reserve(M * 8, false));
-        RCHK(s->p_vals.reserve((size_t)V * M * 8, false));
-        SlRecords prec{s->p_raw.as<u32>(), s->p_slot.as<u32>(), s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
-                       s->p_ts.as<int64_t>(), s->p_vals.as<u64>(), M};
-        // the double-column replay (k_sl_own_d) reads the records through the rank lists itself
-        if (sliding_keys_per_partition(q->ap) == 64) launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
-        HIPCHK(hipEventRecord(q->ev_agg0, st));
-        launch_sliding_own(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, s->logP, prec, state_of(s), q->ap,
-                           q->d.window_param, send_size, send_base, rows, s->flags.as<unsigned char>(), rec);
+        // the common shape (count / sum / avg / min / max of one double column, time window): records
+        // sorted stably by key, one lane per key (k_sl_key); other shapes: key-partition replay
+        static const bool force_part = getenv("SH_SL_PARTITIONED") != nullptr;
+        const bool keyed = q->d.window == SH_WIN_TIME && sliding_keyed_ok(q->ap) && !force_part;
+        if (keyed) {
+            HIPCHK(hipEventRecord(q->ev_agg0, st));  // the sort is part of the replay's time
+            size_t tb = 0;
+            if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            RCHK(s->p_slot.reserve(M * 4, false));
+            RCHK(s->ranks.reserve(M * 4, false));
+            if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+            RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+            RCHK(s->p_clock.reserve(M * 8, false));
+            RCHK(s->p_pm.reserve(M * 8, false));
+            RCHK(s->p_ts.reserve(M * 8, false));
+            RCHK(s->p_vals.reserve(M * 8, false));
+            RCHK(s->p_raw.reserve(M * 4, false));
+            RCHK(s->g_rank.reserve(M * 4, false));
+            RCHK(s->inv.reserve(M * 4, false));
+            RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na) * 8, false));
+            launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
+                                 s->p_slot.as<u32>(), M, rec, s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
+                                 s->p_vals.as<u64>(), s->p_ts.as<int64_t>(), s->p_raw.as<u32>(), s->g_rank.as<u32>(),
+                                 s->inv.as<u32>(), state_of(s), q->ap, q->d.window_param, send_size, send_base,
+                                 s->rows_k.as<u64>(), s->flags.as<unsigned char>());
+        } else {
+            // stable split of the records by key partition
+            int P = s->P;
+            int mblk = (int)((M + kTile - 1) / kTile);
+            int64_t ncnt = (int64_t)P * mblk;
+            RCHK(s->counts.reserve((ncnt + 1) * 8, false));
+            RCHK(s->tmp.reserve(((ncnt + kTile) / kTile + 16) * 8, false));
+            RCHK(s->ranks.reserve(M * 4, false));
+            RCHK(s->part_off.reserve((P + 1) * 8, false));
+            launch_sl_multisplit(st, s->rec_slot.as<u32>(), M, P, s->counts.as<int64_t>(), s->tmp.as<int64_t>(),
+                                 s->ranks.as<u32>(), s->part_off.as<int64_t>());
+            // the records in partition order
+            RCHK(s->p_raw.reserve(M * 4, false));
+            RCHK(s->p_slot.reserve(M * 4, false));
+            RCHK(s->p_clock.reserve(M * 8, false));
+            RCHK(s->p_pm.reserve(M * 8, false));
+            RCHK(s->p_ts.reserve(M * 8, false));
+            RCHK(s->p_vals.reserve((size_t)V * M * 8, false));
+            SlRecords prec{s->p_raw.as<u32>(), s->p_slot.as<u32>(), s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
+                           s->p_ts.as<int64_t>(), s->p_vals.as<u64>(), M};
+            // the double-column replay (k_sl_own_d) reads the records through the rank lists itself
+            if (sliding_keys_per_partition(q->ap) == 64) launch_sl_gather(st, s->ranks.as<u32>(), M, rec, prec, q->ap.n_vcols);
+            HIPCHK(hipEventRecord(q->ev_agg0, st));
+            launch_sliding_own(st, s->ranks.as<u32>(), s->part_off.as<int64_t>(), P, s->logP, prec, state_of(s), q->ap,
+                               q->d.window_param, send_size, send_base, rows, s->flags.as<unsigned char>(), rec);
+        }
         HIPCHK(hipEventRecord(q->ev_agg1, st));
         HIPCHK(hipGetLastError());
         // emit in rank order
@@ -338,6 +371,14 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         HIPCHK(hipMemsetAsync(s->out_expired.p, 0, cap, st));
         if (want_order) RCHK(q->out_order.reserve(cap * 8, false));
         launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
+        if (keyed)
+            launch_slk_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, s->inv.as<u32>(),
+                            s->rows_k.as<u64>(), sliding_keyed_row_words(na), na, q->kt.dev(), q->kp, cap,
+                            s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
+                            s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(),
+                            s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr,
+                            s->out_rep.as<int64_t>());
+        else
         launch_sl_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, rows, na, q->kt.dev(),
                        q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                        s->out_nulls.as<unsigned char>(), s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(),

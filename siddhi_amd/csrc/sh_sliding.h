@@ -58,6 +58,20 @@ void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, 
 void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* counts, i64* tmp, u32* out_rank,
                           i64* part_off);
 int sliding_keys_per_partition(AggPlan ap);
+// key-sorted replay (k_sl_key) for the count / sum / avg / min / max-of-one-double shape: ranks =
+// the records' ranks sorted stably by slot (sort_slot_ranks, sh_sort.hip); key_off [nslots + 1]
+bool sliding_keyed_ok(AggPlan ap);
+int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u32* rank_out, i64 M, i64 nslots,
+                    hipStream_t s);
+void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
+                          const u32* sorted_slot, i64 M, SlRecords rec, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
+                          u32* g_raw, u32* g_rank, u32* inv, SlState S, AggPlan ap, i64 T, i64 send_size,
+                          i64 send_base, u64* rowsK, unsigned char* flags);
+int sliding_keyed_row_words(int n_aggs);
+void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, const u32* inv,
+                     const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
+                     i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
+                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep);
 void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv);
 // rec: the records gathered into partition order (k_sl_own); rec_by_rank: the same records in rank
 // order, read through rank_list by k_sl_own_d (sliding_keys_per_partition(ap) == 8 shapes)

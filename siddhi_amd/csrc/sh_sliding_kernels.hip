@@ -685,6 +685,7 @@ __device__ __forceinline__ bool d_isnan(u64 a) {
 // The deque of the lane's key lives in its LDS ring `l` (kDqL entries) unless it outgrew that
 // (`spill`): then in its global ring `g`. The two paths are separate so each uses plain LDS or
 // global instructions (a pointer select would compile to FLAT accesses that wait on both counters).
+template <int LS = 1>
 __device__ __forceinline__ void dd_load(DDeque& q, const SlState& S, int field, u32 k, u64* l) {
     const size_t fi = (size_t)field * S.nslots + k;
     q.mm = S.mm[fi];
@@ -698,7 +699,7 @@ __device__ __forceinline__ void dd_load(DDeque& q, const SlState& S, int field, 
     if (!q.spill) {
         for (i64 i = 0; i < q.len; i++) {
             const u64 v = g[(q.h + i) & gm];
-            l[(q.h + i) & (kDqL - 1)] = v;
+            l[((q.h + i) & (kDqL - 1)) * LS] = v;
             q.nan |= d_isnan(v);
         }
     }
@@ -708,6 +709,7 @@ __device__ __forceinline__ void dd_load(DDeque& q, const SlState& S, int field, 
     }
 }
 
+template <int LS = 1>
 __device__ __forceinline__ void dd_store(const DDeque& q, const SlState& S, int field, u32 k, const u64* l) {
     const size_t fi = (size_t)field * S.nslots + k;
     S.mm[fi] = q.mm;
@@ -717,15 +719,15 @@ __device__ __forceinline__ void dd_store(const DDeque& q, const SlState& S, int 
     u64* g = S.dq + fi * S.rc;
     const i64 gm = S.rc - 1;
     if (!q.spill)
-        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[(q.h + i) & (kDqL - 1)];
+        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[((q.h + i) & (kDqL - 1)) * LS];
 }
 
 // removeFirstOccurrence(x) then minValue = peekFirst() (Min/MaxAttributeAggregatorExecutor).
 // The front is the common case. Otherwise, while no NaN is in the deque it is monotone (min:
 // non-decreasing, max: non-increasing), so an x beyond the back cannot be in it and needs no scan.
-template <bool MIN, bool GLOBAL>
+template <bool MIN, bool GLOBAL, int LS = 1>
 __device__ __forceinline__ void dd_remove_t(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
-    auto at = [&](i64 i) -> u64 { return GLOBAL ? g[i & gm] : l[i & (kDqL - 1)]; };
+    auto at = [&](i64 i) -> u64 { return GLOBAL ? g[i & gm] : l[(i & (kDqL - 1)) * LS]; };
     if (q.len > 0 && d_eq(q.f, x)) {
         q.h++;
         q.len--;
@@ -738,7 +740,7 @@ __device__ __forceinline__ void dd_remove_t(DDeque& q, u64* g, i64 gm, u64* l, u
             for (i64 i = found; i + 1 < q.len; i++) {
                 const u64 v = at(q.h + i + 1);
                 if (GLOBAL) g[(q.h + i) & gm] = v;
-                else l[(q.h + i) & (kDqL - 1)] = v;
+                else l[((q.h + i) & (kDqL - 1)) * LS] = v;
             }
             q.len--;
             q.b = at(q.h + q.len - 1);
@@ -748,31 +750,31 @@ __device__ __forceinline__ void dd_remove_t(DDeque& q, u64* g, i64 gm, u64* l, u
     else { q.mmh = false; q.nan = q.spill; }
 }
 
-template <bool MIN>
+template <bool MIN, int LS = 1>
 __device__ __forceinline__ void dd_remove(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
-    if (q.spill) dd_remove_t<MIN, true>(q, g, gm, l, x);
-    else dd_remove_t<MIN, false>(q, g, gm, l, x);
+    if (q.spill) dd_remove_t<MIN, true, LS>(q, g, gm, l, x);
+    else dd_remove_t<MIN, false, LS>(q, g, gm, l, x);
 }
 
-template <bool MIN, bool GLOBAL>
+template <bool MIN, bool GLOBAL, int LS = 1>
 __device__ __forceinline__ void dd_add_t(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
     while (q.len > 0 && d_worse<MIN>(q.b, x)) {
         q.len--;
-        if (q.len > 0) q.b = GLOBAL ? g[(q.h + q.len - 1) & gm] : l[(q.h + q.len - 1) & (kDqL - 1)];
+        if (q.len > 0) q.b = GLOBAL ? g[(q.h + q.len - 1) & gm] : l[((q.h + q.len - 1) & (kDqL - 1)) * LS];
     }
 }
 
-template <bool MIN>
+template <bool MIN, int LS = 1>
 __device__ __forceinline__ void dd_add(DDeque& q, u64* g, i64 gm, u64* l, u64 x) {
-    if (q.spill) dd_add_t<MIN, true>(q, g, gm, l, x);
-    else dd_add_t<MIN, false>(q, g, gm, l, x);
+    if (q.spill) dd_add_t<MIN, true, LS>(q, g, gm, l, x);
+    else dd_add_t<MIN, false, LS>(q, g, gm, l, x);
     if (!q.spill && q.len == kDqL) {  // the LDS ring is full: move to the global ring
-        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[(q.h + i) & (kDqL - 1)];
+        for (i64 i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[((q.h + i) & (kDqL - 1)) * LS];
         q.spill = true;
         q.nan = true;  // the global path always scans
     }
     if (q.spill) g[(q.h + q.len) & gm] = x;
-    else l[(q.h + q.len) & (kDqL - 1)] = x;
+    else l[((q.h + q.len) & (kDqL - 1)) * LS] = x;
     q.len++;
     q.b = x;
     q.nan |= d_isnan(x);
@@ -932,6 +934,9 @@ __global__ __launch_bounds__(64) void k_sl_own_d(const u32* __restrict__ rank_li
             i64 first;
             if (cur_send != send) { cur_send = send; cur_first = r; first = r; flags[r] = 1; }
             else first = cur_first;
+#ifdef SH_SL_EXP_NOROWS
+            if (first != 0x7fffffff) continue;  // timing experiment only: no row stores
+#endif
             rows.ts[first] = tsr;
             rows.rep[first] = raw;
             rows.slot[first] = k;
@@ -1153,6 +1158,483 @@ static bool own_d_fields(const AggPlan& ap, DFields& fd) {
 // keys a key partition should hold so that every key gets a lane of its own in the replay kernel
 // (k_sl_own_d: kSlKeyLanes per wave; k_sl_own: 64). A lane owning several keys switches per-key
 // state (global loads and stores) whenever consecutive records of its list change key.
+// ---- key-sorted replay (k_sl_key): the records of a push sorted stably by key slot (sh_sort.hip),
+// so each key's events form one contiguous run in event order, and one lane per key walks its run.
+// The key's window is its carried ring (events of earlier pushes) followed by the run itself, so the
+// expiry head reads the run's own earlier entries instead of a ring written and read back per event;
+// only the entries still in the window at the end of the push go to the ring. Rows are written in
+// key order as one record each (full-line stores) and put in stream order by the emit kernel. ------
+constexpr int kKR = 8;    // records per replay step (fields loaded one step ahead)
+constexpr int kKH = 32;   // staged window-head entries per lane
+constexpr int kKS = 16;   // head entries staged per step (twice the step's average expiries: the
+                          // staged run does not drain into the global-memory fallback)
+constexpr int kDqK = 64;  // LDS min/max deque entries per lane (longer deques continue in global memory)
+constexpr u32 kFirstBit = 0x80000000u;
+
+// k_sl_kgather: key-order copies of the record fields; a record opens a row when it is its key's
+// first event of its send; flags / inv give the row of each opening rank (rank order, for the emit)
+__global__ __launch_bounds__(kBlock) void k_sl_kgather(const u32* __restrict__ sorted_rank,
+                                                       const u32* __restrict__ sorted_slot, i64 M, SlRecords rec,
+                                                       u32 send_size, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
+                                                       u32* g_raw, u32* g_rank, unsigned char* flags, u32* inv) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const u32 r = sorted_rank[i];
+    const u32 raw = rec.raw[r];
+    // (every event is its own send when send_size == 1; one send holds the whole push when it is 0)
+    bool first = send_size == 1 || i == 0 || sorted_slot[i - 1] != sorted_slot[i];
+    if (!first && send_size > 1) {
+        const u32 praw = rec.raw[sorted_rank[i - 1]];
+        first = praw / send_size != raw / send_size;
+    }
+    g_clk[i] = rec.clock[r];
+    g_pm[i] = rec.pm[r];
+    g_v[i] = rec.vals[r];
+    g_ts[i] = rec.ts[r];
+    g_raw[i] = raw;
+    g_rank[i] = r | (first ? kFirstBit : 0u);
+    flags[r] = first ? 1 : 0;
+    if (first) inv[r] = (u32)i;
+}
+
+__global__ void k_sl_keyoff(const u32* __restrict__ slot_cnt, i64 nslots, u32* key_off) {
+    const i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= nslots) key_off[k] = k < nslots ? slot_cnt[k] : 0u;
+}
+
+// Wait for this wave's vector-memory loads right where a rare path issued them. The replay step keeps
+// the next step's loads and this step's row stores in flight; a load result that flows out of a
+// rare branch would otherwise make the compiler wait for every outstanding vector-memory operation
+// at the merge point, on every record, taken or not (the counter retires in order).
+__device__ __forceinline__ void wait_vm_here() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
+// a lane's min or max deque (MinAttributeAggregatorExecutor's LinkedList with removeFirstOccurrence):
+// ring `l` in LDS (kDqK entries, lane-interleaved) or, once longer, ring `g` in global memory
+struct KDq {
+    int h, len;
+    u64 f, b, mm;
+    bool mmh, spill, nan;
+};
+
+// GLOBAL: the deque lives in its global ring; otherwise in LDS. Separate instances, so each uses plain
+// LDS or global instructions (no pointer select)
+template <bool MIN, bool GLOBAL, int KL>
+__device__ __forceinline__ void kdq_remove_t(KDq& q, u64* g, int gm, u64* l, u64 x) {
+    auto at = [&](int i) -> u64 {
+        if (!GLOBAL) return l[(i & (kDqK - 1)) * KL];
+        const u64 v = g[i & gm];
+        wait_vm_here();
+        return v;
+    };
+    if (q.len > 0 && d_eq(q.f, x)) {
+        q.h++;
+        q.len--;
+        if (q.len > 0) q.f = at(q.h);
+    } else if (q.len > 1 && (q.nan || !d_worse<MIN>(x, q.b))) {
+        int found = -1;
+        if (!q.nan) {
+            // NaN-free: the deque is monotone (min: non-decreasing), so the first entry not better
+            // than x is found by bisection; x is present iff that entry equals it
+            int lo = 1, hi = q.len;  // answer in [lo, hi]
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (d_worse<MIN>(x, at(q.h + mid))) lo = mid + 1;
+                else hi = mid;
+            }
+            // among numerically equal entries (0.0 / -0.0) Double.equals wants the same bits
+            for (int i = lo; i < q.len; i++) {
+                const u64 e = at(q.h + i);
+                if (d_eq(e, x)) { found = i; break; }
+                if (d_worse<MIN>(e, x)) break;  // past every entry equal to x
+            }
+        } else {
+            for (int i = 1; i < q.len; i++)
+                if (d_eq(at(q.h + i), x)) { found = i; break; }
+        }
+        if (found >= 0) {
+            for (int i = found; i + 1 < q.len; i++) {
+                const u64 v = at(q.h + i + 1);
+                if (GLOBAL) g[(q.h + i) & gm] = v;
+                else l[((q.h + i) & (kDqK - 1)) * KL] = v;
+            }
+            q.len--;
+            q.b = at(q.h + q.len - 1);
+        }
+    }
+    if (q.len > 0) { q.mm = q.f; q.mmh = true; }
+    else { q.mmh = false; q.nan = q.spill; }
+}
+
+template <bool MIN, int KL>
+__device__ __forceinline__ void kdq_remove(KDq& q, u64* g, int gm, u64* l, u64 x) {
+    if (q.spill) kdq_remove_t<MIN, true, KL>(q, g, gm, l, x);
+    else kdq_remove_t<MIN, false, KL>(q, g, gm, l, x);
+}
+
+template <bool MIN, bool GLOBAL, int KL>
+__device__ __forceinline__ void kdq_pop_t(KDq& q, const u64* g, int gm, const u64* l, u64 x) {
+    while (q.len > 0 && d_worse<MIN>(q.b, x)) {
+        q.len--;
+        if (q.len > 0) {
+            if (GLOBAL) { q.b = g[(q.h + q.len - 1) & gm]; wait_vm_here(); }
+            else q.b = l[((q.h + q.len - 1) & (kDqK - 1)) * KL];
+        }
+    }
+}
+
+template <bool MIN, int KL>
+__device__ __forceinline__ void kdq_add(KDq& q, u64* g, int gm, u64* l, u64 x) {
+    if (q.spill) kdq_pop_t<MIN, true, KL>(q, g, gm, l, x);
+    else kdq_pop_t<MIN, false, KL>(q, g, gm, l, x);
+    if (!q.spill && q.len == kDqK) {  // the LDS ring is full: the deque moves to its global ring
+        for (int i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[((q.h + i) & (kDqK - 1)) * KL];
+        q.spill = true;
+        q.nan = true;  // the global path always scans
+    }
+    if (q.spill) g[(q.h + q.len) & gm] = x;
+    else l[((q.h + q.len) & (kDqK - 1)) * KL] = x;
+    q.len++;
+    q.b = x;
+    q.nan |= d_isnan(x);
+    if (q.len == 1) q.f = x;
+    if (!q.mmh || d_worse<MIN>(q.mm, x)) { q.mm = x; q.mmh = true; }
+}
+
+template <int KL>
+__device__ __forceinline__ void kdq_load(KDq& q, const SlState& S, int field, u32 k, u64* l) {
+    const size_t fi = (size_t)field * S.nslots + k;
+    q.mm = S.mm[fi];
+    q.mmh = S.mm_has[fi];
+    q.len = (int)S.dq_len[fi];
+    q.h = (int)(S.dq_head[fi] & (S.rc - 1));
+    q.spill = q.len > kDqK;
+    q.nan = q.spill;
+    const u64* g = S.dq + fi * S.rc;
+    const int gm = (int)(S.rc - 1);
+    if (!q.spill) {
+        for (int i = 0; i < q.len; i++) {
+            const u64 v = g[(q.h + i) & gm];
+            l[((q.h + i) & (kDqK - 1)) * KL] = v;
+            q.nan |= d_isnan(v);
+        }
+    }
+    if (q.len > 0) {
+        q.f = g[q.h & gm];
+        q.b = g[(q.h + q.len - 1) & gm];
+    }
+}
+
+template <int KL>
+__device__ __forceinline__ void kdq_store(const KDq& q, const SlState& S, int field, u32 k, const u64* l) {
+    const size_t fi = (size_t)field * S.nslots + k;
+    S.mm[fi] = q.mm;
+    S.mm_has[fi] = q.mmh;
+    const int gm = (int)(S.rc - 1);
+    S.dq_head[fi] = q.h & gm;
+    S.dq_len[fi] = q.len;
+    u64* g = S.dq + fi * S.rc;
+    if (!q.spill)
+        for (int i = 0; i < q.len; i++) g[(q.h + i) & gm] = l[((q.h + i) & (kDqK - 1)) * KL];
+}
+
+// output aggregator sources of the keyed replay: 0 count, 1 sum, 2 avg, 3 min, 4 max
+struct KOut {
+    int n;
+    int src[SH_MAX_AGGS];
+};
+
+template <bool HSUM, bool HMIN, bool HMAX, int KL>
+__global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, u32 nslots, const i64* __restrict__ g_clk,
+                                              const i64* __restrict__ g_pm, const u64* __restrict__ g_v,
+                                              const i64* __restrict__ g_ts, const u32* __restrict__ g_raw,
+                                              const u32* __restrict__ g_rank, SlState S, DFields fd, KOut ko, i64 T,
+                                              u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW) {
+    __shared__ u64 dq_min[HMIN ? KL * kDqK : 1];
+    __shared__ u64 dq_max[HMAX ? KL * kDqK : 1];
+    __shared__ i64 hb_pm[KL * kKH];
+    __shared__ u64 hb_v[KL * kKH];
+    __shared__ i64 r_clk[KL * kKR];
+    __shared__ i64 r_ts[KL * kKR];
+    __shared__ u64 r_v[KL * kKR];
+    __shared__ u32 r_raw[KL * kKR];
+    __shared__ u32 r_rank[KL * kKR];
+    // KL lanes of the wave own a key each: fewer owners per wave, less divergence between their
+    // data-dependent loops (expiry, deque pops and searches)
+    const int lane = threadIdx.x;
+    const u32 k = blockIdx.x * KL + lane;
+    if (lane >= KL || k >= nslots) return;
+    const u32 a = key_off[k], b = key_off[k + 1];
+    if (a == b) return;
+    // per-lane LDS arrays interleaved (entry e of this lane at e * 64 + lane): conflict-free
+    u64* lmin = dq_min + (HMIN ? lane : 0);
+    u64* lmax = dq_max + (HMAX ? lane : 0);
+    const int gm = (int)(S.rc - 1);
+    i64* rpm = S.rpm + (size_t)k * S.rc;
+    u64* rval = S.rval + (size_t)k * S.rc;
+    i64 cnt = S.cnt[k];
+    const int rh0 = (int)(S.rhead[k] & gm), H0 = (int)S.rlen[k];
+    double sum = 0.0;
+    if (HSUM) sum = __longlong_as_double((i64)S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k]);
+    KDq qn{}, qx{};
+    u64* gmin = nullptr;
+    u64* gmax = nullptr;
+    if (HMIN) { kdq_load<KL>(qn, S, fd.mn, k, lmin); gmin = S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc; }
+    if (HMAX) { kdq_load<KL>(qx, S, fd.mx, k, lmax); gmax = S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc; }
+    // head sequence: the carried ring's H0 entries, then the run; entry j of it
+    const int n = (int)(b - a), HN = H0 + n;
+    auto head_pm = [&](int j) -> i64 { return j < H0 ? rpm[(rh0 + j) & gm] : g_pm[a + (j - H0)]; };
+    auto head_v = [&](int j) -> u64 { return j < H0 ? rval[(rh0 + j) & gm] : g_v[a + (j - H0)]; };
+    int hj = 0;      // next head entry to expire
+    int staged = 0;  // entries [.., staged) staged in the LDS ring (those >= hj and >= staged - kKH)
+    i64 h_pm[kKS];
+    u64 h_v[kKS];
+    int h_from = 0, h_to = 0;
+    auto load_heads = [&]() {
+        h_from = staged > hj ? staged : hj;
+        h_to = min(min(h_from + kKS, hj + kKH), HN);
+#pragma unroll
+        for (int q = 0; q < kKS; q++) {
+            const int j = min(h_from + q, HN - 1);
+            h_pm[q] = head_pm(j);
+            h_v[q] = head_v(j);
+        }
+    };
+    auto commit_heads = [&]() {
+#pragma unroll
+        for (int q = 0; q < kKS; q++) {
+            const int j = h_from + q;
+            if (j < h_to) { hb_pm[(j & (kKH - 1)) * KL + lane] = h_pm[q]; hb_v[(j & (kKH - 1)) * KL + lane] = h_v[q]; }
+        }
+        if (h_to > h_from) staged = h_to;
+    };
+    i64 n_clk[kKR], n_ts[kKR];
+    u64 n_v[kKR];
+    u32 n_raw[kKR], n_rank[kKR];
+    auto load_recs = [&](int o) {
+#pragma unroll
+        for (int q = 0; q < kKR; q++) {
+            const u32 i = a + (u32)min(o + q, n - 1);
+            n_clk[q] = g_clk[i];
+            n_ts[q] = g_ts[i];
+            n_v[q] = g_v[i];
+            n_raw[q] = g_raw[i];
+            n_rank[q] = g_rank[i];
+        }
+    };
+    auto commit_recs = [&]() {
+#pragma unroll
+        for (int q = 0; q < kKR; q++) {
+            r_clk[q * KL + lane] = n_clk[q];
+            r_ts[q * KL + lane] = n_ts[q];
+            r_v[q * KL + lane] = n_v[q];
+            r_raw[q * KL + lane] = n_raw[q];
+            r_rank[q * KL + lane] = n_rank[q];
+        }
+    };
+    load_recs(0);
+    load_heads();
+    commit_recs();
+    commit_heads();
+    i64 send = 0;
+    u32 row = 0;  // key-order position of the current row (its first record)
+    for (int o0 = 0; o0 < n; o0 += kKR) {
+        // the next step's records and heads go out before this step's stores (vector-memory
+        // counters complete in order: waiting for these loads never waits for the stores)
+        load_recs(o0 + kKR);
+        load_heads();
+        const int m = min(kKR, n - o0);
+        for (int q = 0; q < m; q++) {
+            const i64 clk = r_clk[q * KL + lane];
+            const int added = H0 + o0 + q;  // head entries in the window before this record
+            // lazy expiry: window events with PM + T <= clock (TimeWindowProcessor.java:132-169)
+            while (hj < added) {
+                i64 pm;
+                u64 hv;
+                if (hj < staged && hj + kKH >= staged) {
+                    pm = hb_pm[(hj & (kKH - 1)) * KL + lane];
+                    hv = hb_v[(hj & (kKH - 1)) * KL + lane];
+                } else {
+                    pm = head_pm(hj);
+                    hv = head_v(hj);
+                    wait_vm_here();
+                }
+                if (pm + T > clk) break;
+                cnt--;
+                if (HSUM) {
+                    sum = sum - __longlong_as_double((i64)hv);
+                    if (cnt == 0 && sum == 0.0) sum = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
+                }
+                if (HMIN) kdq_remove<true, KL>(qn, gmin, gm, lmin, hv);
+                if (HMAX) kdq_remove<false, KL>(qx, gmax, gm, lmax, hv);
+                hj++;
+            }
+            // the event joins the window and the aggregators
+            const u64 x = r_v[q * KL + lane];
+            cnt++;
+            if (HSUM) sum = sum + __longlong_as_double((i64)x);
+            if (HMIN) kdq_add<true, KL>(qn, gmin, gm, lmin, x);
+            if (HMAX) kdq_add<false, KL>(qx, gmax, gm, lmax, x);
+            // the row of (send, key): at its first record, with the values after this one
+            const u32 raw = r_raw[q * KL + lane];
+            if (r_rank[q * KL + lane] & kFirstBit) {
+                row = a + (u32)(o0 + q);
+                send = send_base + (send_size == 1 ? (i64)raw : send_size ? (i64)(raw / send_size) : 0);
+            }
+            u64 w[4 + SH_MAX_AGGS];
+            u32 nulls = 0;
+            w[0] = (u64)r_ts[q * KL + lane];
+            w[1] = (u64)raw | ((u64)k << 32);
+            w[2] = (u64)clk;
+#pragma unroll
+            for (int o = 0; o < SH_MAX_AGGS; o++) {
+                if (o >= ko.n) break;
+                const int src = ko.src[o];
+                u64 v = 0;
+                if (src == 0) v = (u64)cnt;
+                else if (src == 1) v = (u64)__double_as_longlong(sum);
+                else if (src == 2) v = (u64)__double_as_longlong(sum / (double)cnt);
+                else if (src == 3) { v = qn.mm; nulls |= (qn.mmh ? 0u : 1u) << o; }
+                else { v = qx.mm; nulls |= (qx.mmh ? 0u : 1u) << o; }
+                w[4 + o] = v;
+            }
+            w[3] = (u64)send | ((u64)nulls << 56);
+            ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row * RW);
+#pragma unroll
+            for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
+                if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
+        }
+        commit_recs();
+        commit_heads();
+    }
+    // the window after the push: head entries [hj, HN) become the ring (ring entries keep their
+    // place; the run's entries follow them)
+    const int keep = hj < H0 ? H0 - hj : 0;
+    const int rh = (rh0 + (hj < H0 ? hj : H0)) & gm;
+    int rlen = keep;
+    for (int j = (hj > H0 ? hj : H0); j < HN; j++) {
+        const int sl = (rh + rlen) & gm;
+        rpm[sl] = g_pm[a + (j - H0)];
+        rval[sl] = g_v[a + (j - H0)];
+        rlen++;
+    }
+    S.cnt[k] = cnt;
+    S.rhead[k] = rh;
+    S.rlen[k] = rlen;
+    S.cur_send[k] = send;
+    S.cur_first[k] = 0;
+    if (HSUM) {
+        const u64 sb = (u64)__double_as_longlong(sum);
+        if (fd.sum >= 0) S.f[(size_t)fd.sum * S.nslots + k] = sb;
+        if (fd.avg >= 0) S.f[(size_t)fd.avg * S.nslots + k] = sb;
+    }
+    if (HMIN) kdq_store<KL>(qn, S, fd.mn, k, lmin);
+    if (HMAX) kdq_store<KL>(qx, S, fd.mx, k, lmax);
+}
+
+// emit of the keyed replay: flagged ranks in stream order, each row read from its key-order record
+__global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __restrict__ flags, i64 n,
+                                                    const i64* __restrict__ blk_pre, const u32* __restrict__ inv,
+                                                    const u64* __restrict__ rowsK, int RW, int n_aggs, KeyTable kt,
+                                                    KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                                                    unsigned char* out_nulls, i64* out_send, i64* out_clock,
+                                                    const u32* __restrict__ rank_raw, i64 raw_base, i64* out_order,
+                                                    i64* out_rep) {
+    const i64 tile = (i64)blockIdx.x * kTile;
+    i64 run = blk_pre[blockIdx.x];
+    for (int it = 0; it < kItems; it++) {
+        const i64 j = tile + (i64)it * kBlock + threadIdx.x;
+        const i64 fl = j < n ? flags[j] : 0;
+        i64 tot;
+        const i64 r = run + block_excl_scan(fl, SumOp(), 0, &tot);
+        run += tot;
+        if (!fl) continue;
+        const u64* src = rowsK + (size_t)inv[j] * RW;
+        u64 w[4 + SH_MAX_AGGS];
+#pragma unroll
+        for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++) {
+            if (2 * o >= RW) break;
+            const ulonglong2 v = ((const ulonglong2*)src)[o];
+            w[2 * o] = v.x;
+            w[2 * o + 1] = v.y;
+        }
+        out_ts[r] = (i64)w[0];
+        unpack_key(kp, slot_key(kt, (u32)(w[1] >> 32)), out_keys + r, out_cap);
+        const u32 nulls = (u32)(w[3] >> 56);
+        for (int a = 0; a < n_aggs; a++) {
+            out_vals[(size_t)a * out_cap + r] = w[4 + a];
+            out_nulls[(size_t)a * out_cap + r] = (nulls >> a) & 1u;
+        }
+        out_send[r] = (i64)(w[3] & ((1ull << 56) - 1));
+        out_clock[r] = (i64)w[2];
+        if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
+        out_rep[r] = raw_base + (i64)(u32)w[1];
+    }
+}
+
+void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, const u32* inv,
+                     const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
+                     i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
+                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep) {
+    hipLaunchKernelGGL(k_slk_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, inv, rowsK, RW, n_aggs, kt, kp,
+                       out_cap, out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base,
+                       out_order, out_rep);
+}
+
+// The keyed replay is used where it measured faster than the key-partition replay (k_sl_own_d): with
+// a min or max deque (C3's count/min/max/avg: 18.5 vs 20.7 ms per 16.7M-event push on MI355X);
+// count/sum/avg alone stay on k_sl_own_d (5.5 vs 6.1 ms).
+bool sliding_keyed_ok(AggPlan ap) {
+    DFields fd;
+    return own_d_fields(ap, fd) && ap.n <= SH_MAX_AGGS && (fd.mn >= 0 || fd.mx >= 0);
+}
+
+int sliding_keyed_row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
+
+void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
+                          const u32* sorted_slot, i64 M, SlRecords rec, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
+                          u32* g_raw, u32* g_rank, u32* inv, SlState S, AggPlan ap, i64 T, i64 send_size,
+                          i64 send_base, u64* rowsK, unsigned char* flags) {
+    DFields fd;
+    own_d_fields(ap, fd);
+    KOut ko{};
+    ko.n = ap.n;
+    for (int q = 0; q < ap.n; q++) {
+        const int kind = ap.kind[q];
+        ko.src[q] = kind == AK_COUNT ? 0 : kind == AK_SUM_D ? 1 : kind == AK_AVG ? 2 : kind == AK_MIN_D ? 3 : 4;
+    }
+    const i64 n = S.nslots;
+    const u32 ss = send_size > 0 ? (u32)send_size : 0u;
+    hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
+    launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
+    hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank,
+                       sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
+    const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
+    static const int kl_env = getenv("SH_SL_KL") ? atoi(getenv("SH_SL_KL")) : 16;
+    const int KLr = kl_env == 8 || kl_env == 32 || kl_env == 64 ? kl_env : 16;
+    const unsigned grid = (unsigned)((n + KLr - 1) / KLr);
+    const int RW = sliding_keyed_row_words(ap.n);
+#define SH_SL_K1(A, B, C, KLV)                                                                                      \
+    hipLaunchKernelGGL((k_sl_key<A, B, C, KLV>), dim3(grid), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, g_ts, \
+                       g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RW)
+#define SH_SL_K(A, B, C)                                                                                            \
+    do {                                                                                                            \
+        if (KLr == 8) SH_SL_K1(A, B, C, 8);                                                                          \
+        else if (KLr == 32) SH_SL_K1(A, B, C, 32);                                                                   \
+        else if (KLr == 64) SH_SL_K1(A, B, C, 64);                                                                   \
+        else SH_SL_K1(A, B, C, 16);                                                                                  \
+    } while (0)
+    if (hs && hn && hx) SH_SL_K(true, true, true);
+    else if (hs && !hn && !hx) SH_SL_K(true, false, false);
+    else if (!hs && hn && hx) SH_SL_K(false, true, true);
+    else if (hs && hn) SH_SL_K(true, true, false);
+    else if (hs && hx) SH_SL_K(true, false, true);
+    else if (hn && !hx) SH_SL_K(false, true, false);
+    else if (hx && !hn) SH_SL_K(false, false, true);
+    else SH_SL_K(false, false, false);
+#undef SH_SL_K
+#undef SH_SL_K1
+}
+
 int sliding_keys_per_partition(AggPlan ap) {
     DFields fd;
     return own_d_fields(ap, fd) ? kSlKeyLanes : 64;

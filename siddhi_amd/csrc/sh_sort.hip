@@ -1,0 +1,31 @@
+// sh_sort.hip — stable device radix sort of the sliding window's records by key slot (rocPRIM
+// onesweep), so that every key's records of a push form one contiguous run in event order.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include "sh_internal.h"
+
+namespace shd {
+
+// bits needed for slots < nslots
+static unsigned slot_bits(i64 nslots) {
+    unsigned b = 1;
+    while (b < 32 && ((i64)1 << b) < nslots) b++;
+    return b;
+}
+
+// temp == nullptr: *bytes = the temporary storage needed. Sorts keys (slots) stably, values = the
+// records' ranks 0..M-1.
+int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u32* rank_out, i64 M, i64 nslots,
+                    hipStream_t s) {
+    rocprim::counting_iterator<u32> iota(0u);
+    hipError_t e = rocprim::radix_sort_pairs(temp, *bytes, slot, slot_out, iota, rank_out, (unsigned)M, 0u,
+                                             slot_bits(nslots), s);
+    return e == hipSuccess ? 0 : -1;
+}
+
+}  // namespace shd
