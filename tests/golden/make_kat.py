@@ -159,6 +159,55 @@ case(name="aggregation6_seconds_to_year", source="ctest/aggregation/Aggregation1
                                     [1496289953000, "IBM", 400.0, 400.0], [1496289954000, "IBM", 600.0, 600.0],
                                     [1496290016000, "IBM", 1000.0, 1000.0]]))
 
+# Retrieval KATs (`from A within ... per "<duration>"`) transcribed as the matching duration table:
+# the tests' `within` ranges cover every bucket, and a TIMER past the last bucket (added here; the Java
+# tests read the still-open buckets from the executors' in-memory state instead) moves every bucket
+# into its table with the same base values (sums, counts are associative), so the table rows equal
+# the retrieved rows. Columns the GPU does not aggregate (`price * quantity` as lastTradeValue) are
+# not transcribed.
+_t17 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+        ["WSO2", 60.0, 44.0, 200, 56, 1496289952000], ["WSO2", 100.0, 0.0, 200, 16, 1496289952000],
+        ["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+        ["IBM", 100.0, 0.0, 200, 26, 1496289954000], ["IBM", 100.0, 0.0, 200, 96, 1496289954000],
+        ["IBM", 900.0, 0.0, 200, 60, 1496289956000], ["IBM", 500.0, 0.0, 200, 7, 1496289956000],
+        ["IBM", 400.0, 0.0, 200, 9, 1496290016000], ["IBM", 600.0, 0.0, 200, 6, 1496290076000],
+        ["CISCO", 700.0, 0.0, 200, 20, 1496293676000], ["WSO2", 60.0, 44.0, 200, 56, 1496297276000],
+        ["CISCO", 800.0, 0.0, 100, 10, 1496383676000], ["CISCO", 900.0, 0.0, 100, 15, 1496470076000],
+        ["IBM", 100.0, 0.0, 200, 96, 1499062076000], ["IBM", 400.0, 0.0, 200, 9, 1501740476000],
+        ["WSO2", 60.0, 44.0, 200, 6, 1533276476000], ["WSO2", 260.0, 44.0, 200, 16, 1564812476000],
+        ["CISCO", 260.0, 44.0, 200, 16, 1596434876000], ["CISCO", 260.0, 44.0, 200, 16, 1606975676000]]
+_after_2020 = 1609459200000 + 400 * 86_400_000
+case(name="aggregation17_months", source="ctest/aggregation/Aggregation1TestCase.java:704-839",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[r[-1]] + r] for r in _t17] + [{"advance": _after_2020}],
+     expect=dict(table="month", rows=[[1496275200000, "WSO2", 65.71428571428571, 460.0],
+                                      [1496275200000, "CISCO", 800.0, 2400.0],
+                                      [1496275200000, "IBM", 433.3333333333333, 2600.0],
+                                      [1498867200000, "IBM", 100.0, 100.0], [1501545600000, "IBM", 400.0, 400.0],
+                                      [1533081600000, "WSO2", 60.0, 60.0], [1564617600000, "WSO2", 260.0, 260.0],
+                                      [1596240000000, "CISCO", 260.0, 260.0], [1606780800000, "CISCO", 260.0, 260.0]]))
+case(name="aggregation18_years", source="ctest/aggregation/Aggregation1TestCase.java:840-972",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[r[-1]] + r] for r in _t17] + [{"advance": _after_2020}],
+     expect=dict(table="year", rows=[[1483228800000, "CISCO", 800.0, 2400.0], [1483228800000, "IBM", 387.5, 3100.0],
+                                     [1483228800000, "WSO2", 65.71428571428571, 460.0],
+                                     [1514764800000, "WSO2", 60.0, 60.0], [1546300800000, "WSO2", 260.0, 260.0],
+                                     [1577836800000, "CISCO", 260.0, 520.0]]))
+_t9 = [r for i, r in enumerate(_t17) if i not in (4, 5, 21)]  # test 9 sends each WSO2 pair once, no Dec 2020 event
+case(name="aggregation9_days_no_group_by", source="ctest/aggregation/Aggregation1TestCase.java:300-428",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"], ["count", None]], group_by=[], ts="timestamp",
+                      durations=["min", "year"]),
+     sends=[[[r[-1]] + r] for r in _t9] + [{"advance": _after_2020}],
+     expect=dict(table="day", rows=[[1496275200000, 303.3333333333333, 3640.0, 12], [1496361600000, 800.0, 800.0, 1],
+                                    [1496448000000, 900.0, 900.0, 1], [1499040000000, 100.0, 100.0, 1],
+                                    [1501718400000, 400.0, 400.0, 1], [1533254400000, 60.0, 60.0, 1],
+                                    [1564790400000, 260.0, 260.0, 1], [1596412800000, 260.0, 260.0, 1]]))
+
 # ---------------------------------------------------------------- filters (FilterTestCase1): expected counts
 F = "ctest/query/FilterTestCase1.java"
 FL = "symbol string, price float, volume long"
