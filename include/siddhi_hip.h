@@ -247,6 +247,15 @@ int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* batch);
 int sh_aggregation_advance_time(sh_aggregation* a, int64_t now);
 /* Rows added to the table of `duration` since the previous call for that duration. */
 int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out);
+/* Retrieval `from A within start, end per "<per>"` (AggregationRuntime.find ->
+ * IncrementalAggregateCompileCondition.find, core/util/collection/operator/
+ * IncrementalAggregateCompileCondition.java:180-290): the `per` table's rows plus the in-memory
+ * stores of the executors `per` .. root re-bucketed to `per` (IncrementalDataAggregator.java:92-143),
+ * merged by (AGG_TIMESTAMP, key) and restricted to start <= AGG_TIMESTAMP < end. Host rows as
+ * sh_aggregation_table (keys[0] = AGG_TIMESTAMP, keys[1] = the group key, base values), ordered by
+ * (AGG_TIMESTAMP, key). The caller evaluates the select expressions (avg = sum / count, ...) and
+ * resolves `within` patterns / time strings to [start, end). */
+int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start, int64_t end, const sh_out** out);
 
 /* ---- sharded ingest across G GPUs (one process per GPU) ---------------------
  * Rank g of G holds slice g of every global micro-batch: a contiguous run of the global stream

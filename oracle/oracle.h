@@ -17,6 +17,7 @@ void or_aggregation_destroy(void* a);
 int or_aggregation_push(void* a, const sh_batch* b);
 int or_aggregation_advance_time(void* a, int64_t now);
 int or_aggregation_table(void* a, int32_t duration, const sh_out** out);
+int or_aggregation_find(void* a, int32_t per, int64_t start, int64_t end, const sh_out** out);
 #ifdef __cplusplus
 }
 #endif

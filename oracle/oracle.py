@@ -40,6 +40,7 @@ def lib():
         L.or_aggregation_push.argtypes = [C.c_void_p, P(abi.Batch)]
         L.or_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
         L.or_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(abi.Out))]
+        L.or_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(abi.Out))]
         _lib = L
     return _lib
 
@@ -111,6 +112,17 @@ class OracleAggregation:
 
     def table(self, duration: int):
         fl = abi.decode_out(self.table_raw(duration))
+        return [r for f in fl for r in f.rows]
+
+    def find_raw(self, per: int, start: int, end: int):
+        out = C.POINTER(abi.Out)()
+        rc = lib().or_aggregation_find(self.h, per, start, end, C.byref(out))
+        if rc != 0:
+            raise RuntimeError(lib().or_last_error().decode())
+        return out
+
+    def find(self, per: int, start: int, end: int):
+        fl = abi.decode_out(self.find_raw(per, start, end))
         return [r for f in fl for r in f.rows]
 
     def close(self):

@@ -915,8 +915,8 @@ struct AggRuntime {
     std::vector<std::unique_ptr<IncExec>> execs;
     int64_t clock = INT64_MIN; bool clock_set = false;
     std::deque<int64_t> notify_queue;  // root scheduler (AggregationParser.java:431-437)
-    // table rows per duration, appended on dispatch
-    std::vector<std::vector<OutRow>> tables;
+    // table rows per duration, appended on dispatch; `history` keeps every row (retrieval)
+    std::vector<std::vector<OutRow>> tables, history;
     std::vector<OutBuf> views;
     int vtypes[SH_MAX_AGGS]{};
 
@@ -1018,6 +1018,85 @@ struct AggRuntime {
             if (o.has) { if (is_fp(base_out_type(bases[i]))) std::memcpy(&r.vals[i], &o.d, 8); else r.vals[i] = (uint64_t)o.i; }
         }
         tables[dur].push_back(r);
+        history[dur].push_back(r);
+    }
+
+    // Retrieval `from A within start, end per "<per>"`: AggregationRuntime.find ->
+    // IncrementalAggregateCompileCondition.find (:180-290). The in-memory stores of the executors
+    // per .. root are re-bucketed to `per` and folded per (bucket, key) in executor order
+    // (IncrementalDataAggregator.aggregateInMemoryData :92-143), then merged with the `per` table's
+    // rows by (AGG_TIMESTAMP, key), table rows first (OutOfOrderEventsDataAggregator), restricted to
+    // start <= AGG_TIMESTAMP < end. Output order: (AGG_TIMESTAMP, key) (the reference's is a HashMap's).
+    struct Acc { std::vector<std::unique_ptr<AggState>> st; std::vector<AggOut> val; };
+    Acc new_acc() const {
+        Acc a;
+        for (auto& b : bases) {
+            AggDef ad;
+            ad.fn = b.kind == B_SUM || b.kind == B_COUNT ? SH_AGG_SUM : (b.kind == B_MIN ? SH_AGG_MIN : SH_AGG_MAX);
+            ad.in_type = b.kind == B_COUNT ? SH_T_LONG : b.type;
+            ad.track = false; ad.col = 0; ad.out_type = 0;
+            a.st.push_back(make_state(ad));
+            a.val.push_back(AggOut());
+        }
+        return a;
+    }
+    JVal as_jval(size_t i, const AggOut& o) const {
+        JVal v; v.t = base_out_type(bases[i]);
+        if (is_fp(v.t)) v.d = o.d; else v.i = o.i;
+        return v;
+    }
+    void fold(Acc& a, const std::vector<AggOut>& vals) const {
+        for (size_t i = 0; i < bases.size(); i++) if (vals[i].has) a.val[i] = a.st[i]->add(as_jval(i, vals[i]));
+    }
+    void find(int per, int64_t start, int64_t end, OutBuf& ob) {
+        typedef std::pair<int64_t, int64_t> GK;
+        std::map<GK, Acc> mem;
+        const int ip = per - d.min_duration;
+        for (int k = ip; k >= 0; k--) {
+            IncExec& ex = *execs[k];
+            for (const GKey& key : ex.order) {
+                const BaseRow& br = ex.store[key];
+                const int64_t b = start_time_of(d.ts_col >= 0 ? br.ext : ex.store_ts, per);
+                GK g(b, d.n_group_by > 0 ? br.keys[0] : 0);
+                auto it = mem.find(g);
+                if (it == mem.end()) it = mem.emplace(g, new_acc()).first;
+                fold(it->second, br.val);
+            }
+        }
+        std::map<GK, Acc> res;
+        for (const OutRow& r : history[per]) {
+            if (r.ts < start || r.ts >= end) continue;
+            GK g(r.ts, d.n_group_by > 0 ? r.keys[1] : 0);
+            auto it = res.find(g);
+            if (it == res.end()) it = res.emplace(g, new_acc()).first;
+            std::vector<AggOut> v(bases.size());
+            for (size_t i = 0; i < bases.size(); i++) {
+                v[i].has = !r.nulls[i];
+                if (is_fp(base_out_type(bases[i]))) std::memcpy(&v[i].d, &r.vals[i], 8); else v[i].i = (int64_t)r.vals[i];
+            }
+            fold(it->second, v);
+        }
+        for (auto& m : mem) {
+            if (m.first.first < start || m.first.first >= end) continue;
+            auto it = res.find(m.first);
+            if (it == res.end()) it = res.emplace(m.first, new_acc()).first;
+            fold(it->second, m.second.val);
+        }
+        ob.clear();
+        ob.with_rep = false;
+        for (auto& kv : res) {
+            OutRow r{};
+            r.ts = kv.first.first;
+            r.keys[0] = kv.first.first;
+            r.keys[1] = kv.first.second;
+            for (size_t i = 0; i < bases.size(); i++) {
+                const AggOut& o = kv.second.val[i];
+                r.nulls[i] = o.has ? 0 : 1;
+                if (o.has) { if (is_fp(base_out_type(bases[i]))) std::memcpy(&r.vals[i], &o.d, 8); else r.vals[i] = (uint64_t)o.i; }
+            }
+            ob.rows.push_back(r);
+        }
+        if (!ob.rows.empty()) ob.close_flush(clock);
     }
 
     void on_time_change() {
@@ -1166,7 +1245,8 @@ void* or_aggregation_create(const sh_aggregation_desc* desc) {
     }
     for (size_t i = 0; i + 1 < a->execs.size(); i++) a->execs[i]->next = a->execs[i + 1].get();
     a->tables.resize(SH_DUR_YEARS + 1);
-    a->views.resize(SH_DUR_YEARS + 1);
+    a->history.resize(SH_DUR_YEARS + 1);
+    a->views.resize(SH_DUR_YEARS + 2);
     return a;
 }
 
@@ -1194,6 +1274,15 @@ int or_aggregation_table(void* h, int32_t dur, const sh_out** out) {
     if (!ob.rows.empty()) ob.close_flush(a->clock);
     *out = ob.view(1 + a->d.n_group_by, (int)a->bases.size(), a->vtypes);
     a->tables[dur].clear();
+    return SH_OK;
+}
+
+int or_aggregation_find(void* h, int32_t per, int64_t start, int64_t end, const sh_out** out) {
+    AggRuntime* a = (AggRuntime*)h;
+    if (per < a->d.min_duration || per > a->d.max_duration) { g_err = "duration not aggregated"; return SH_ERR_INVALID; }
+    OutBuf& ob = a->views[SH_DUR_YEARS + 1];
+    a->find(per, start, end, ob);
+    *out = ob.view(1 + a->d.n_group_by, (int)a->bases.size(), a->vtypes);
     return SH_OK;
 }
 

@@ -25,10 +25,20 @@ struct LevelDev {
 void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
                         const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
                         int* dup_dev, int* dup_host);
-void launch_level_mark(hipStream_t s, LevelDev L, i64 n_in);
+void launch_level_mark(hipStream_t s, LevelDev L, i64 n_in, bool reset = true);
 void launch_level_count(hipStream_t s, LevelDev L, i64 n_in, i64* blk, int nblk);
 void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket, i64 store_ts, i64 n_in, i64* blk,
-                          int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals);
+                          int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals, bool clear = true);
+// retrieval (sh_aggregation_find)
+void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i64 start, i64 end, i64* bucket_out,
+                          u32* idx);
+void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst);
+void launch_find_starts(hipStream_t s, i64 n, const u32* idx, const i64* bucket, const i64* key, u32* flag);
+void launch_find_fold(hipStream_t s, i64 n, const u32* idx, const u32* flag, const u32* pre, const i64* bucket,
+                      const i64* key, const u64* vals, i64 vstride, BasePlan bp, i64 cap, i64* out_bucket,
+                      i64* out_key, u64* out_vals);
+int sort_u64_pairs(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out, i64 n,
+                   hipStream_t s);
 void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v);
 void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out);
 

@@ -132,13 +132,14 @@ void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* k
 
 // ---- extraction of a level's store (dispatch) -----------------------------------------------------
 // order[first_seq[slot]] = slot, so walking `order` visits the slots in first-arrival order
-__global__ __launch_bounds__(kBlock) void k_level_mark(LevelDev L) {
+// reset = false: the retrieval's read of the in-progress store (the store stays as it is)
+__global__ __launch_bounds__(kBlock) void k_level_mark(LevelDev L, int reset) {
     i64 p = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (p >= L.nslots) return;
     u32 f = L.first_seq[p];
     if (f != 0xFFFFFFFFu) {
         L.order[f] = (u32)p;
-        L.first_seq[p] = 0xFFFFFFFFu;
+        if (reset) L.first_seq[p] = 0xFFFFFFFFu;
     }
 }
 
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_level_count(LevelDev L, i64 n_in, i6
 
 __global__ __launch_bounds__(kBlock) void k_level_extract(LevelDev L, BasePlan bp, int has_bucket, i64 store_ts,
                                                          i64 n_in, const i64* blk_pre, i64 cap, i64* out_bucket,
-                                                         i64* out_key, u64* out_vals) {
+                                                         i64* out_key, u64* out_vals, int clear) {
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     u32 slot[kItems];
     i64 c = 0;
@@ -178,17 +179,17 @@ __global__ __launch_bounds__(kBlock) void k_level_extract(LevelDev L, BasePlan b
         }
         for (int b = 0; b < bp.n; b++) {
             out_vals[(size_t)b * cap + r] = L.vals[(size_t)b * L.nslots + p];
-            L.has[(size_t)b * L.nslots + p] = 0;
+            if (clear) L.has[(size_t)b * L.nslots + p] = 0;
         }
-        if (p <= L.kt.mask) L.kt.keys[p] = kEmptyKey;  // BaseIncrementalValueStore.clearValues (:73-78)
+        if (clear && p <= L.kt.mask) L.kt.keys[p] = kEmptyKey;  // BaseIncrementalValueStore.clearValues (:73-78)
         r++;
     }
 }
 
-void launch_level_mark(hipStream_t s, LevelDev L, i64 n_in) {
+void launch_level_mark(hipStream_t s, LevelDev L, i64 n_in, bool reset) {
     (void)hipMemsetAsync(L.order, 0xFF, (size_t)n_in * 4, s);
     unsigned g = (unsigned)((L.nslots + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_level_mark, dim3(g), dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL(k_level_mark, dim3(g), dim3(kBlock), 0, s, L, reset ? 1 : 0);
 }
 
 void launch_level_count(hipStream_t s, LevelDev L, i64 n_in, i64* blk, int nblk) {
@@ -196,9 +197,108 @@ void launch_level_count(hipStream_t s, LevelDev L, i64 n_in, i64* blk, int nblk)
 }
 
 void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket, i64 store_ts, i64 n_in, i64* blk,
-                          int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals) {
+                          int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals, bool clear) {
     hipLaunchKernelGGL(k_level_extract, dim3(nblk), dim3(kBlock), 0, s, L, bp, has_bucket, store_ts, n_in, blk, cap,
-                       out_bucket, out_key, out_vals);
+                       out_bucket, out_key, out_vals, clear ? 1 : 0);
+}
+
+// ---- retrieval (sh_aggregation_find) ---------------------------------------------------------------
+// rows re-bucketed to the `per` duration; rows outside [start, end) get bucket -1 (sorted last, dropped)
+__global__ __launch_bounds__(kBlock) void k_find_rebucket(i64 n, const i64* __restrict__ bucket_in, int per, i64 start,
+                                                         i64 end, i64* bucket_out, u32* idx) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const i64 b = start_of_dev(bucket_in[i], per);
+    bucket_out[i] = (b >= start && b < end) ? b : -1;
+    idx[i] = (u32)i;
+}
+
+__global__ __launch_bounds__(kBlock) void k_find_gather_u64(i64 n, const u32* __restrict__ idx, const i64* __restrict__ src,
+                                                           u64* dst) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) dst[i] = (u64)src[idx[i]];
+}
+
+// group starts in (bucket, key) order; out-of-range rows (bucket -1) start no group
+__global__ __launch_bounds__(kBlock) void k_find_starts(i64 n, const u32* __restrict__ idx, const i64* __restrict__ bucket,
+                                                       const i64* __restrict__ key, u32* flag) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { flag[i] = 0; return; }
+    const u32 r = idx[i];
+    bool st = bucket[r] >= 0;
+    if (st && i > 0) {
+        const u32 q = idx[i - 1];
+        st = bucket[q] != bucket[r] || key[q] != key[r];
+    }
+    flag[i] = st ? 1u : 0u;
+}
+
+// one thread per group: its rows folded in input order with the base executors' semantics
+// (sum / count: 0 + v1 + v2 ..., min / max: first value then compares; OutOfOrderEventsDataAggregator,
+// IncrementalDataAggregator)
+__global__ __launch_bounds__(kBlock) void k_find_fold(i64 n, const u32* __restrict__ idx, const u32* __restrict__ flag,
+                                                     const u32* __restrict__ pre, const i64* __restrict__ bucket,
+                                                     const i64* __restrict__ key, const u64* __restrict__ vals,
+                                                     i64 vstride, BasePlan bp, i64 cap, i64* out_bucket, i64* out_key,
+                                                     u64* out_vals) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (!flag[i]) return;  // not a group's first row
+    const u32 r = idx[i];
+    const i64 o = pre[i];
+    u64 acc[SH_MAX_AGGS];
+    for (int b = 0; b < bp.n; b++) acc[b] = vals[(size_t)b * vstride + r];
+    for (int b = 0; b < bp.n; b++)
+        if (bp.kind[b] == AK_SUM_D) acc[b] = (u64)__double_as_longlong(0.0 + __longlong_as_double((i64)acc[b]));
+    for (i64 j = i + 1; j < n && !flag[j]; j++) {
+        const u32 q = idx[j];
+        if (bucket[q] < 0) break;  // the out-of-range rows sorted last
+        for (int b = 0; b < bp.n; b++) {
+            const u64 x = vals[(size_t)b * vstride + q];
+            switch (bp.kind[b]) {
+                case AK_SUM_L: case AK_COUNT: acc[b] = (u64)((i64)acc[b] + (i64)x); break;
+                case AK_SUM_D:
+                    acc[b] = (u64)__double_as_longlong(__longlong_as_double((i64)acc[b]) + __longlong_as_double((i64)x));
+                    break;
+                case AK_MIN_L: if ((i64)acc[b] > (i64)x) acc[b] = x; break;
+                case AK_MAX_L: if ((i64)acc[b] < (i64)x) acc[b] = x; break;
+                case AK_MIN_D: if (__longlong_as_double((i64)acc[b]) > __longlong_as_double((i64)x)) acc[b] = x; break;
+                case AK_MAX_D: if (__longlong_as_double((i64)acc[b]) < __longlong_as_double((i64)x)) acc[b] = x; break;
+                case AK_MIN_F: if ((float)__longlong_as_double((i64)acc[b]) > (float)__longlong_as_double((i64)x)) acc[b] = x; break;
+                case AK_MAX_F: if ((float)__longlong_as_double((i64)acc[b]) < (float)__longlong_as_double((i64)x)) acc[b] = x; break;
+            }
+        }
+    }
+    out_bucket[o] = bucket[r];
+    out_key[o] = key[r];
+    for (int b = 0; b < bp.n; b++) out_vals[(size_t)b * cap + o] = acc[b];
+}
+
+void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i64 start, i64 end, i64* bucket_out,
+                          u32* idx) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_find_rebucket, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, bucket_in,
+                       per, start, end, bucket_out, idx);
+}
+
+void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_find_gather_u64, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, idx,
+                       src, dst);
+}
+
+void launch_find_starts(hipStream_t s, i64 n, const u32* idx, const i64* bucket, const i64* key, u32* flag) {
+    hipLaunchKernelGGL(k_find_starts, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, idx,
+                       bucket, key, flag);
+}
+
+void launch_find_fold(hipStream_t s, i64 n, const u32* idx, const u32* flag, const u32* pre, const i64* bucket,
+                      const i64* key, const u64* vals, i64 vstride, BasePlan bp, i64 cap, i64* out_bucket,
+                      i64* out_key, u64* out_vals) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_find_fold, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, idx, flag,
+                       pre, bucket, key, vals, vstride, bp, cap, out_bucket, out_key, out_vals);
 }
 
 // min / max of an int64 column (event-time span of a push -> root key-table bound)

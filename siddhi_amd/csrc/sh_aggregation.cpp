@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -126,6 +127,7 @@ struct RowBatch {
 struct TableBuf {
     DevBuf bucket, key, vals;
     int64_t n = 0, cap = 0;
+    int64_t drained = 0;  // rows [0, drained) were returned by sh_aggregation_table; all stay for retrieval
 };
 
 struct Level {
@@ -155,7 +157,10 @@ struct sh_aggregation {
     int64_t root_bucket = 0;
     std::vector<Level> levels;            // durations above the root
     TableBuf tables[SH_DUR_YEARS + 1];
-    OutHost tout;
+    OutHost tout, fout;
+    // retrieval scratch (sh_aggregation_find)
+    DevBuf m_bucket, m_key, m_vals, f_bucket, f_key, f_vals, g_bucket, g_idx, g_k64, g_k64s, g_idx1, g_idx2, g_flag,
+        g_pre, g_tmp, g_sort, v_bucket, v_key, v_vals;
     DevBuf root_bucket_col, root_key_col, minmax;
     int64_t* h_minmax = nullptr;
     // device time of the last push: ev0 before the root's key reservation, ev1 after the roll-up
@@ -619,7 +624,8 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
     hipStream_t s = a->ctx->stream;
     OutHost& o = a->tout;
     o.reset();
-    int64_t n = t.n;
+    const int64_t r0 = t.drained;
+    int64_t n = t.n - r0;
     int nk = 1 + a->d.n_group_by;
     o.ts.resize(n);
     o.expired.assign(n, 0);
@@ -627,19 +633,196 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
     o.vals.resize((size_t)a->nb * n);
     o.nulls.assign((size_t)a->nb * n, 0);
     if (n) {
-        HIPCHK(hipMemcpyAsync(o.ts.data(), t.bucket.p, n * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(o.keys.data(), t.bucket.p, n * 8, hipMemcpyDeviceToHost, s));
-        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + n, t.key.p, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(o.ts.data(), t.bucket.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(o.keys.data(), t.bucket.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
+        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + n, t.key.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
         for (int b = 0; b < a->nb; b++)
-            HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * n, (char*)t.vals.p + (size_t)b * t.cap * 8, n * 8,
+            HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * n, t.vals.as<u64>() + (size_t)b * t.cap + r0, n * 8,
                                   hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         o.flush_offsets.push_back(n);
         o.flush_clock.push_back(a->root->clock);
     }
-    t.n = 0;
+    t.drained = t.n;
     o.view(nk, a->nb, a->btypes);
     o.out.rep = nullptr;  // table rows have no representative event
+    *out = &o.out;
+    return SH_OK;
+}
+
+// ---- retrieval: `from A within start, end per "<per>"` (AggregationRuntime.find ->
+// IncrementalAggregateCompileCondition.find :180-290) ---------------------------------------------
+// The rows of the `per` table plus the in-memory stores of the executors `per` .. root
+// (IncrementalDataAggregator.aggregateInMemoryData :92-143: re-bucketed to `per` and folded per
+// (bucket, key) in executor order), merged with the table rows by (AGG_TIMESTAMP, key)
+// (OutOfOrderEventsDataAggregator: table rows first), restricted to start <= AGG_TIMESTAMP < end.
+// Rows come out in (AGG_TIMESTAMP, key) order (the reference's order is a HashMap's).
+
+// rows (bucket at their own duration, key, vals [nb][vstride]) -> grouped by (`per` bucket, key) in
+// (bucket, key) order, each group's rows folded in input order; rows outside [start, end) dropped
+static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* key, const u64* vals, int64_t n,
+                      int64_t vstride, int per, int64_t start, int64_t end, DevBuf& ob, DevBuf& ok, DevBuf& ov,
+                      int64_t* n_out) {
+    *n_out = 0;
+    if (n <= 0) return SH_OK;
+    hipStream_t s = a->ctx->stream;
+    RCHK(a->g_bucket.reserve(n * 8, false));
+    RCHK(a->g_idx.reserve(n * 4, false));
+    RCHK(a->g_k64.reserve(n * 8, false));
+    RCHK(a->g_k64s.reserve(n * 8, false));
+    RCHK(a->g_idx1.reserve(n * 4, false));
+    RCHK(a->g_idx2.reserve(n * 4, false));
+    RCHK(a->g_flag.reserve((n + 1) * 4, false));
+    RCHK(a->g_pre.reserve((n + 1) * 4, false));
+    RCHK(a->g_tmp.reserve((size_t)((n + 1 + kTile - 1) / kTile + 16) * 8, false));
+    launch_find_rebucket(s, n, bucket, per, start, end, a->g_bucket.as<int64_t>(), a->g_idx.as<u32>());
+    // (bucket, key) order, input order within a group: stable LSD sorts by key, then by bucket
+    size_t tb = 0;
+    if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, s)) return sh_fail(SH_ERR_DEVICE, "sort sizing");
+    RCHK(a->g_sort.reserve(std::max<size_t>(tb, 16), false));
+    launch_find_gather_u64(s, n, a->g_idx.as<u32>(), key, a->g_k64.as<u64>());
+    if (sort_u64_pairs(a->g_sort.p, &tb, a->g_k64.as<u64>(), a->g_k64s.as<u64>(), a->g_idx.as<u32>(), a->g_idx1.as<u32>(),
+                       n, s))
+        return sh_fail(SH_ERR_DEVICE, "retrieval sort failed");
+    launch_find_gather_u64(s, n, a->g_idx1.as<u32>(), a->g_bucket.as<int64_t>(), a->g_k64.as<u64>());
+    if (sort_u64_pairs(a->g_sort.p, &tb, a->g_k64.as<u64>(), a->g_k64s.as<u64>(), a->g_idx1.as<u32>(),
+                       a->g_idx2.as<u32>(), n, s))
+        return sh_fail(SH_ERR_DEVICE, "retrieval sort failed");
+    launch_find_starts(s, n, a->g_idx2.as<u32>(), a->g_bucket.as<int64_t>(), key, a->g_flag.as<u32>());
+    HIPCHK(hipMemcpyAsync(a->g_pre.p, a->g_flag.p, (n + 1) * 4, hipMemcpyDeviceToDevice, s));
+    launch_scan_sum_large_u32(s, a->g_pre.as<u32>(), n + 1, a->g_tmp.as<int64_t>());
+    uint32_t groups = 0;
+    HIPCHK(hipMemcpyAsync(a->h_minmax, a->g_pre.as<u32>() + n, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::memcpy(&groups, a->h_minmax, 4);
+    const int64_t cap = std::max<int64_t>(groups, 1);
+    RCHK(ob.reserve(cap * 8, false));
+    RCHK(ok.reserve(cap * 8, false));
+    RCHK(ov.reserve((size_t)a->nb * cap * 8, false));
+    launch_find_fold(s, n, a->g_idx2.as<u32>(), a->g_flag.as<u32>(), a->g_pre.as<u32>(), a->g_bucket.as<int64_t>(), key,
+                     vals, vstride, a->bp, cap, ob.as<int64_t>(), ok.as<int64_t>(), ov.as<u64>());
+    HIPCHK(hipGetLastError());
+    *n_out = groups;
+    return SH_OK;
+}
+
+extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start, int64_t end, const sh_out** out) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_find: NULL argument");
+    if (per < a->d.min_duration || per > a->d.max_duration)
+        return sh_fail(SH_ERR_INVALID, "the aggregation does not contain the `per` duration");
+    hipStream_t s = a->ctx->stream;
+    const int nb = a->nb;
+    // in-memory rows, executors `per` down to the root: sizes first
+    std::vector<int64_t> level_n;
+    int64_t total = 0;
+    for (int dur = per; dur > a->d.min_duration; dur--) {
+        Level& L = a->levels[dur - a->d.min_duration - 1];
+        level_n.push_back(L.processed ? L.n_in : 0);
+        total += level_n.back();
+    }
+    int64_t root_rows = 0;
+    RCHK(query_peek(a->root, &root_rows));
+    total += root_rows;
+    const int64_t mcap = std::max<int64_t>(total, 1);
+    RCHK(a->m_bucket.reserve(mcap * 8, false));
+    RCHK(a->m_key.reserve(mcap * 8, false));
+    RCHK(a->m_vals.reserve((size_t)nb * mcap * 8, false));
+    int64_t m = 0;
+    for (size_t i = 0; i < level_n.size(); i++) {
+        const int dur = per - (int)i;
+        Level& L = a->levels[dur - a->d.min_duration - 1];
+        const int64_t n_in = level_n[i];
+        if (n_in == 0) continue;
+        // the store's entries in first-arrival order (its insertion order), left in place
+        const int nblk = (int)((n_in + kTile - 1) / kTile);
+        RCHK(L.blk.reserve((nblk + 8) * 8, false));
+        RCHK(L.order.reserve(n_in * 4, false));
+        LevelDev D = level_dev(L, nb);
+        launch_level_mark(s, D, n_in, false);
+        launch_level_count(s, D, n_in, L.blk.as<int64_t>(), nblk);
+        std::vector<int64_t> bc(nblk);
+        HIPCHK(hipMemcpyAsync(bc.data(), L.blk.p, nblk * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int64_t entries = 0;  // distinct (bucket, key) slots; rows merged into one slot count once
+        for (auto c : bc) entries += c;
+        launch_scan_sum(s, L.blk.as<int64_t>(), nblk);
+        launch_level_extract(s, D, a->bp, a->has_bucket, L.store_ts, n_in, L.blk.as<int64_t>(), nblk, mcap,
+                             a->m_bucket.as<int64_t>() + m, a->m_key.as<int64_t>() + m, a->m_vals.as<u64>() + m, false);
+        HIPCHK(hipGetLastError());
+        m += entries;
+    }
+    if (root_rows > 0) {
+        sh_query* q = a->root;
+        const int64_t R = root_rows;
+        const int nk = q->kp.n;
+        const int64_t* keys = q->out_keys.as<int64_t>();
+        if (a->has_bucket) {
+            HIPCHK(hipMemcpyAsync(a->m_bucket.as<int64_t>() + m, keys, R * 8, hipMemcpyDeviceToDevice, s));
+            if (nk > 1) HIPCHK(hipMemcpyAsync(a->m_key.as<int64_t>() + m, keys + R, R * 8, hipMemcpyDeviceToDevice, s));
+            else HIPCHK(hipMemsetAsync(a->m_key.as<int64_t>() + m, 0, R * 8, s));
+        } else {
+            // processing time: AGG_TIMESTAMP of the root store = the open window's start
+            launch_fill_i64(s, a->m_bucket.as<int64_t>() + m, R, q->E0 + (q->W_open - 1) * a->T_root);
+            if (nk > 0) HIPCHK(hipMemcpyAsync(a->m_key.as<int64_t>() + m, keys, R * 8, hipMemcpyDeviceToDevice, s));
+            else HIPCHK(hipMemsetAsync(a->m_key.as<int64_t>() + m, 0, R * 8, s));
+        }
+        for (int b = 0; b < nb; b++)
+            HIPCHK(hipMemcpyAsync(a->m_vals.as<u64>() + (size_t)b * mcap + m, q->out_vals.as<u64>() + (size_t)b * R, R * 8,
+                                  hipMemcpyDeviceToDevice, s));
+        m += R;
+    }
+    // in-memory values per (`per` bucket, key): IncrementalDataAggregator
+    int64_t nv = 0;
+    RCHK(group_fold(a, a->m_bucket.as<int64_t>(), a->m_key.as<int64_t>(), a->m_vals.as<u64>(), m, mcap, per, INT64_MIN,
+                    INT64_MAX, a->v_bucket, a->v_key, a->v_vals, &nv));
+    // the `per` table's rows first, then the in-memory values: OutOfOrderEventsDataAggregator
+    TableBuf& t = a->tables[per];
+    const int64_t n2 = t.n + nv, cap2 = std::max<int64_t>(n2, 1);
+    RCHK(a->f_bucket.reserve(cap2 * 8, false));
+    RCHK(a->f_key.reserve(cap2 * 8, false));
+    RCHK(a->f_vals.reserve((size_t)nb * cap2 * 8, false));
+    if (t.n) {
+        HIPCHK(hipMemcpyAsync(a->f_bucket.p, t.bucket.p, t.n * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(a->f_key.p, t.key.p, t.n * 8, hipMemcpyDeviceToDevice, s));
+        for (int b = 0; b < nb; b++)
+            HIPCHK(hipMemcpyAsync(a->f_vals.as<u64>() + (size_t)b * cap2, t.vals.as<u64>() + (size_t)b * t.cap, t.n * 8,
+                                  hipMemcpyDeviceToDevice, s));
+    }
+    if (nv) {
+        HIPCHK(hipMemcpyAsync(a->f_bucket.as<int64_t>() + t.n, a->v_bucket.p, nv * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(a->f_key.as<int64_t>() + t.n, a->v_key.p, nv * 8, hipMemcpyDeviceToDevice, s));
+        const int64_t vcap = std::max<int64_t>(nv, 1);
+        for (int b = 0; b < nb; b++)
+            HIPCHK(hipMemcpyAsync(a->f_vals.as<u64>() + (size_t)b * cap2 + t.n, a->v_vals.as<u64>() + (size_t)b * vcap,
+                                  nv * 8, hipMemcpyDeviceToDevice, s));
+    }
+    int64_t nr = 0;
+    RCHK(group_fold(a, a->f_bucket.as<int64_t>(), a->f_key.as<int64_t>(), a->f_vals.as<u64>(), n2, cap2, per, start, end,
+                    a->v_bucket, a->v_key, a->v_vals, &nr));
+    // host rows: AGG_TIMESTAMP, [key], base values (as sh_aggregation_table)
+    OutHost& o = a->fout;
+    o.reset();
+    const int nk = 1 + a->d.n_group_by;
+    o.ts.resize(nr);
+    o.expired.assign(nr, 0);
+    o.keys.resize((size_t)nk * nr);
+    o.vals.resize((size_t)nb * nr);
+    o.nulls.assign((size_t)nb * nr, 0);
+    if (nr) {
+        const int64_t vcap = std::max<int64_t>(nr, 1);
+        HIPCHK(hipMemcpyAsync(o.ts.data(), a->v_bucket.p, nr * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(o.keys.data(), a->v_bucket.p, nr * 8, hipMemcpyDeviceToHost, s));
+        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + nr, a->v_key.p, nr * 8, hipMemcpyDeviceToHost, s));
+        for (int b = 0; b < nb; b++)
+            HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * nr, a->v_vals.as<u64>() + (size_t)b * vcap, nr * 8,
+                                  hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        o.flush_offsets.push_back(nr);
+        o.flush_clock.push_back(a->root->clock);
+    }
+    o.view(nk, nb, a->btypes);
+    o.out.rep = nullptr;
     *out = &o.out;
     return SH_OK;
 }

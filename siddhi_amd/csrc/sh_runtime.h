@@ -298,6 +298,8 @@ struct sh_query {
     } ing;
 };
 
+// the open window aggregated per key without closing it (sh_window.cpp; aggregation retrieval)
+int query_peek(sh_query* q, int64_t* n_rows);
 // push of a batch staged on the device by sh_stage, host output (sh_window.cpp)
 int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out);
 void ingest_destroy(sh_query* q);  // (sh_ingest.cpp)

@@ -28,4 +28,11 @@ int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u
     return e == hipSuccess ? 0 : -1;
 }
 
+// stable sort of (u64 key, u32 value) pairs over all 64 key bits (aggregation retrieval)
+int sort_u64_pairs(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out, i64 n,
+                   hipStream_t s) {
+    hipError_t e = rocprim::radix_sort_pairs(temp, *bytes, keys, keys_out, vals, vals_out, (unsigned)n, 0u, 64u, s);
+    return e == hipSuccess ? 0 : -1;
+}
+
 }  // namespace shd

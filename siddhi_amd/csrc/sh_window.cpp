@@ -783,6 +783,32 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     return push_core(q, &dev, true, out);
 }
 
+// The open window's pending events aggregated per key without closing it (the aggregation root's
+// in-memory store for a retrieval, sh_aggregation_find): device rows in q->out_* ([col][n_rows],
+// first-occurrence order); no flush is recorded and the window stays open.
+int query_peek(sh_query* q, int64_t* n_rows) {
+    *n_rows = 0;
+    if (q->n_pend == 0) return SH_OK;
+    hipStream_t s = q->ctx->stream;
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    q->flush_window.clear();
+    q->dev_out = sh_out{};
+    q->ms_ready = false;
+    q->tail.active = false;
+    std::vector<Segment> segs{Segment{0, q->n_pend}};
+    std::vector<int64_t> clocks{q->clock}, windows{q->W_open};
+    RCHK(run_closed(q, segs, clocks, windows, nullptr, false));
+    HIPCHK(hipStreamSynchronize(s));
+    RCHK(closed_finish(q, false));
+    *n_rows = q->dev_out.n_rows;
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    q->flush_window.clear();
+    q->tail.active = false;
+    return SH_OK;
+}
+
 // a push whose batch is already on the device, with host output (sh_push_staged)
 int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out) {
     if (q->kind == 1) return sliding_push(q, dev, true, out);

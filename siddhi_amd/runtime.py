@@ -213,6 +213,16 @@ class GpuAggregation:
         _check(lib().sh_aggregation_table(self.h, duration, C.byref(out)))
         return out
 
+    def find_raw(self, per: int, start: int, end: int):
+        """`from A within start, end per <per>`: table + in-memory rows, (AGG_TIMESTAMP, key) order."""
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_aggregation_find(self.h, per, start, end, C.byref(out)))
+        return out
+
+    def find(self, per: int, start: int, end: int):
+        fl = abi.decode_out(self.find_raw(per, start, end))
+        return [r for f in fl for r in f.rows]
+
     def table(self, duration: int):
         return [r for f in abi.decode_out(self.table_raw(duration)) for r in f.rows]
 

@@ -208,6 +208,50 @@ case(name="aggregation9_days_no_group_by", source="ctest/aggregation/Aggregation
                                     [1501718400000, 400.0, 400.0, 1], [1533254400000, 60.0, 60.0, 1],
                                     [1564790400000, 260.0, 260.0, 1], [1596412800000, 260.0, 260.0, 1]]))
 
+# The same retrievals through the query path (sh_aggregation_find): no closing TIMER, so the
+# latest buckets are read from the executors' in-memory stores as in the Java tests. `within` time
+# strings are resolved to [start, end) here (the Java shim's job): "2017-01-01 00:00:00" (GMT) =
+# 1483228800000, "2021-01-01 00:00:00" = 1609459200000, "2017-06-** **:**:**" = June 2017.
+_jun2017 = [1496275200000, 1498867200000]
+case(name="retrieval5_per_seconds", source="ctest/aggregation/Aggregation1TestCase.java:138-189",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "hour"]),
+     sends=[[[r[-1]] + r] for r in _t5],
+     expect=dict(find=dict(per="sec", start=_jun2017[0], end=_jun2017[1]),
+                 rows=[[1496289952000, "WSO2", 80.0, 160.0], [1496289950000, "WSO2", 60.0, 120.0],
+                       [1496289954000, "IBM", 100.0, 200.0]]))
+case(name="retrieval9_per_days", source="ctest/aggregation/Aggregation1TestCase.java:300-428",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"], ["count", None]], group_by=[], ts="timestamp",
+                      durations=["min", "year"]),
+     sends=[[[r[-1]] + r] for r in _t9],
+     expect=dict(find=dict(per="day", start=1496200000000, end=1596434876000),
+                 rows=[[1496275200000, 303.3333333333333, 3640.0, 12], [1496361600000, 800.0, 800.0, 1],
+                       [1496448000000, 900.0, 900.0, 1], [1499040000000, 100.0, 100.0, 1],
+                       [1501718400000, 400.0, 400.0, 1], [1533254400000, 60.0, 60.0, 1],
+                       [1564790400000, 260.0, 260.0, 1], [1596412800000, 260.0, 260.0, 1]]))
+case(name="retrieval17_per_months", source="ctest/aggregation/Aggregation1TestCase.java:704-839",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[r[-1]] + r] for r in _t17],
+     expect=dict(find=dict(per="month", start=1483228800000, end=1609459200000),
+                 rows=[[1496275200000, "WSO2", 65.71428571428571, 460.0], [1496275200000, "CISCO", 800.0, 2400.0],
+                       [1496275200000, "IBM", 433.3333333333333, 2600.0], [1498867200000, "IBM", 100.0, 100.0],
+                       [1501545600000, "IBM", 400.0, 400.0], [1533081600000, "WSO2", 60.0, 60.0],
+                       [1564617600000, "WSO2", 260.0, 260.0], [1596240000000, "CISCO", 260.0, 260.0],
+                       [1606780800000, "CISCO", 260.0, 260.0]]))
+case(name="retrieval18_per_years", source="ctest/aggregation/Aggregation1TestCase.java:840-972",
+     kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["avg", "price"], ["sum", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[r[-1]] + r] for r in _t17],
+     expect=dict(find=dict(per="year", start=1483228800000, end=1609459200000),
+                 rows=[[1483228800000, "CISCO", 800.0, 2400.0], [1483228800000, "IBM", 387.5, 3100.0],
+                       [1483228800000, "WSO2", 65.71428571428571, 460.0], [1514764800000, "WSO2", 60.0, 60.0],
+                       [1546300800000, "WSO2", 260.0, 260.0], [1577836800000, "CISCO", 260.0, 520.0]]))
+
 # ---------------------------------------------------------------- filters (FilterTestCase1): expected counts
 F = "ctest/query/FilterTestCase1.java"
 FL = "symbol string, price float, volume long"

@@ -176,3 +176,12 @@ def check_aggregation_table(case, spec, dic, table_rows):
     exp = [list(r) for r in e["rows"]]
     key = lambda r: (r[0], r[1]) if spec.group_by else (r[0],)
     assert sorted(got, key=key) == sorted(exp, key=key), (sorted(got, key=key), sorted(exp, key=key))
+
+
+def aggregation_rows(case, agg):
+    """The rows a case checks: a retrieval (`within ... per`, expect.find) or a duration table."""
+    e = case["expect"]
+    if "find" in e:
+        f = e["find"]
+        return agg.find(abi.DUR_NAMES[f["per"]], f["start"], f["end"])
+    return agg.table(abi.DUR_NAMES[e["table"]])

@@ -65,8 +65,15 @@ AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"
 @pytest.mark.parametrize("case", AGG_KATS, ids=[c["name"] for c in AGG_KATS])
 def test_reference_aggregation_kat_on_gpu(rt, case):
     schema, spec, dic, a = kat_runner.run_aggregation(case, rt.GpuAggregation)
-    dur = abi.DUR_NAMES[case["expect"]["table"]]
-    kat_runner.check_aggregation_table(case, spec, dic, a.table(dur))
+    kat_runner.check_aggregation_table(case, spec, dic, kat_runner.aggregation_rows(case, a))
+    if "find" in case["expect"]:
+        # the retrieval identical to the oracle's, and to itself after the tables were drained
+        _, _, _, o = kat_runner.run_aggregation(case, OracleAggregation)
+        f = case["expect"]["find"]
+        args = (abi.DUR_NAMES[f["per"]], f["start"], f["end"])
+        assert a.find(*args) == o.find(*args)
+        tables(a, spec)
+        assert a.find(*args) == o.find(*args)
     # every duration identical to the oracle (tables drain on read, so run both afresh)
     _, _, _, a = kat_runner.run_aggregation(case, rt.GpuAggregation)
     _, _, _, o = kat_runner.run_aggregation(case, OracleAggregation)
@@ -135,3 +142,42 @@ def test_long_sums_and_int_min_max(rt):
                                ts="ts", durations=("sec", "hour"), key_capacity=700)
     pushes = split_batches(schema, ts, cols, [40_000], 1000) + [("advance", int(ts[-1]) + 7_200_000)]
     both(rt, spec, pushes, "longs")
+
+
+# ---- retrieval `from A within start, end per "<per>"` (sh_aggregation_find) against the oracle ------
+def _finds(a, spans):
+    return [a.find(per, lo, hi) for per, lo, hi in spans]
+
+
+@pytest.mark.parametrize("proc_time", [False, True])
+def test_retrieval_mid_stream_matches_oracle(rt, proc_time):
+    """Retrievals between pushes: the `per` table plus the in-memory stores of every executor below it
+    (root window pending events, roll-up levels mid-bucket) with late events (IncrementalDataAggregator /
+    OutOfOrderEventsDataAggregator) — GPU = oracle at every per duration and several ranges."""
+    rng = np.random.default_rng(31)
+    n = 40_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 40, n)).astype(np.int64)
+    ext = clock - rng.integers(0, 90_000, n).astype(np.int64)
+    k = rng.integers(0, 40, n).astype(np.int32)
+    v = np.round(rng.normal(100, 30, n), 3)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("count", None), ("min", "v"), ("max", "v")], group_by=["k"],
+                               ts=None if proc_time else "ts", durations=("sec", "day"), key_capacity=64)
+    g = rt.GpuAggregation(spec)
+    o = OracleAggregation(spec)
+    lo, hi = int(ext.min()) - 86_400_000, int(clock.max()) + 86_400_000
+    mid = int(clock[n // 2])
+    spans = [(abi.DUR_NAMES[d], lo, hi) for d in ("sec", "min", "hour", "day")] + \
+            [(abi.DUR_NAMES["min"], mid - 600_000, mid), (abi.DUR_NAMES["sec"], mid, hi)]
+    cuts = [0, 7_000, 7_001, 19_000, 33_333, n]
+    for a_, b_ in zip(cuts[:-1], cuts[1:]):
+        for q in (g, o):
+            q.push(abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], ext[a_:b_]], 25))
+        gf, of = _finds(g, spans), _finds(o, spans)
+        assert gf == of, f"retrieval differs after {b_} events"
+        assert sum(len(x) for x in gf) > 0
+    for q in (g, o):
+        q.advance_time(int(clock[-1]) + 3 * 86_400_000)
+    assert _finds(g, spans) == _finds(o, spans)
+    g.close()
+    o.close()
