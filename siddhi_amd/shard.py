@@ -376,6 +376,7 @@ def distributed_push(q: ShardedQuery, ex: TorchExchange, n: int, ts_ptr: int, co
     torch.cuda.current_stream(send_buf.device).synchronize()  # recv was written on torch's stream
     t3 = time.perf_counter()
     res = q.consume(recv.data_ptr(), recv_bytes, all_bounds, host_out)
+    q.last_bounds = all_bounds  # (the merge of the owners' outputs matches flushes by these)
     if timings is not None:
         t4 = time.perf_counter()
         for k, v in (("summarize", t1 - t0), ("pack", t2 - t1), ("exchange", t3 - t2), ("consume", t4 - t3)):
