@@ -256,6 +256,12 @@ int sh_aggregation_table(sh_aggregation* a, int32_t duration, const sh_out** out
  * (AGG_TIMESTAMP, key). The caller evaluates the select expressions (avg = sum / count, ...) and
  * resolves `within` patterns / time strings to [start, end). */
 int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start, int64_t end, const sh_out** out);
+/* Checkpoint of an aggregation (SnapshotService.persist/restore, SnapshotService.java:90-296): the root
+ * window, every roll-up executor's state and store (IncrementalExecutor.java:283-317,
+ * BaseIncrementalValueStore.java:231-262) and the duration tables. Two calls as sh_query_snapshot;
+ * restores only into an aggregation created from the same descriptor. Not for sharded aggregations. */
+int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap, int64_t* len);
+int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len);
 
 /* ---- sharded ingest across G GPUs (one process per GPU) ---------------------
  * Rank g of G holds slice g of every global micro-batch: a contiguous run of the global stream

@@ -387,6 +387,8 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
     lib.sh_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
     lib.sh_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(Out))]
+    lib.sh_aggregation_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, P(C.c_int64)]
+    lib.sh_aggregation_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.sh_alloc_pinned.argtypes = [C.c_int64, P(C.c_void_p)]
     lib.sh_stage.argtypes = [C.c_void_p, P(Batch), P(C.c_int32)]
     lib.sh_push_staged.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
@@ -425,5 +427,5 @@ ABI_SYMBOLS = [
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
-    "sh_aggregation_find",
+    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore",
 ]

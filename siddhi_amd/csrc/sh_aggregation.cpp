@@ -826,3 +826,184 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
     *out = &o.out;
     return SH_OK;
 }
+
+// ---- checkpoint: State.snapshot()/restore() of an aggregation (SnapshotService.persist/restore,
+// core/util/snapshot/SnapshotService.java:90-296) — the root window (its sh_query snapshot), every
+// roll-up executor's ExecutorState (IncrementalExecutor.java:283-317: nextEmitTime,
+// startTimeOfAggregates) and BaseIncrementalValueStore (:231-262: store timestamp, processed flag,
+// the per-(bucket, key) base values), and the duration tables. A restored aggregation continues
+// exactly as the snapshotted one (same tables, same retrievals). --------------------------------------
+namespace {
+struct ABlob {
+    std::vector<uint8_t> b;
+    template <typename T> void val(const T& x) { b.insert(b.end(), (const uint8_t*)&x, (const uint8_t*)&x + sizeof(T)); }
+    int dev(const void* d, size_t n, hipStream_t s) {
+        val<uint64_t>(n);
+        size_t o = b.size();
+        b.resize(o + n);
+        if (n && (hipMemcpyAsync(b.data() + o, d, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess))
+            return sh_fail(SH_ERR_DEVICE, "aggregation snapshot: device read failed");
+        return SH_OK;
+    }
+};
+struct AReader {
+    const uint8_t* p;
+    size_t n, o = 0;
+    bool ok = true;
+    template <typename T> T val() {
+        T x{};
+        if (o + sizeof(T) > n) { ok = false; return x; }
+        std::memcpy(&x, p + o, sizeof(T));
+        o += sizeof(T);
+        return x;
+    }
+    // a device section of exactly `want` bytes into d (-1: any length, returned in *got)
+    int dev(void* d, int64_t want, hipStream_t s, uint64_t* got = nullptr) {
+        const uint64_t len = val<uint64_t>();
+        if (!ok || o + len > n || (want >= 0 && (uint64_t)want != len)) {
+            ok = false;
+            return sh_fail(SH_ERR_INVALID, "aggregation snapshot does not match this aggregation");
+        }
+        if (got) *got = len;
+        if (len && (hipMemcpyAsync(d, p + o, len, hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipStreamSynchronize(s) != hipSuccess))
+            return sh_fail(SH_ERR_DEVICE, "aggregation restore: device write failed");
+        o += len;
+        return SH_OK;
+    }
+};
+uint64_t agg_fingerprint(const sh_aggregation* a) {
+    const sh_aggregation_desc& d = a->d;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        for (size_t i = 0; i < n; i++) h = (h ^ ((const uint8_t*)p)[i]) * 1099511628211ull;
+    };
+    int32_t ints[] = {d.n_cols, d.n_group_by, d.n_aggs, d.ts_col, d.min_duration, d.max_duration, d.n_filter_ops};
+    mix(ints, sizeof(ints));
+    mix(d.col_types, sizeof(int32_t) * d.n_cols);
+    mix(d.group_by, sizeof(int32_t) * d.n_group_by);
+    mix(d.aggs, sizeof(sh_agg_spec) * d.n_aggs);
+    mix(&d.key_capacity, 8);
+    return h;
+}
+constexpr uint32_t kAggSnapVersion = 1;
+}  // namespace
+
+extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap, int64_t* len) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation");
+    hipStream_t s = a->ctx->stream;
+    ABlob w;
+    w.b.insert(w.b.end(), {'S', 'H', 'A', '1'});
+    w.val<uint32_t>(kAggSnapVersion);
+    w.val<uint64_t>(agg_fingerprint(a));
+    // the root window
+    int64_t rl = 0;
+    RCHK(sh_query_snapshot(a->root, nullptr, 0, &rl));
+    std::vector<uint8_t> rb((size_t)rl);
+    RCHK(sh_query_snapshot(a->root, rb.data(), rl, &rl));
+    w.val<int64_t>(rl);
+    w.b.insert(w.b.end(), rb.begin(), rb.end());
+    w.val<uint8_t>(a->root_init);
+    w.val<int64_t>(a->root_bucket);
+    // roll-up executors
+    w.val<uint32_t>((uint32_t)a->levels.size());
+    for (Level& L : a->levels) {
+        w.val<int64_t>(L.next_emit);
+        w.val<int64_t>(L.start);
+        w.val<int64_t>(L.store_ts);
+        w.val<uint8_t>(L.processed);
+        w.val<int64_t>(L.n_in);
+        w.val<uint32_t>(L.epoch);
+        w.val<uint64_t>(L.kt.size_);
+        RCHK(L.kt.check(s));
+        w.val<int64_t>(L.kt.n_keys);
+        RCHK(w.dev(L.kt.keys.p, L.kt.size_ * 8, s));
+        RCHK(w.dev(L.vals.p, (size_t)a->nb * L.nslots * 8, s));
+        RCHK(w.dev(L.has.p, (size_t)a->nb * L.nslots, s));
+        RCHK(w.dev(L.tag.p, (size_t)L.nslots * 4, s));
+        RCHK(w.dev(L.first_seq.p, (size_t)L.nslots * 4, s));
+    }
+    // duration tables (every row: retrievals read the whole table) and their drain cursors
+    for (int dur = a->d.min_duration; dur <= a->d.max_duration; dur++) {
+        TableBuf& t = a->tables[dur];
+        w.val<int64_t>(t.n);
+        w.val<int64_t>(t.drained);
+        RCHK(w.dev(t.bucket.p, t.n * 8, s));
+        RCHK(w.dev(t.key.p, t.n * 8, s));
+        for (int b = 0; b < a->nb; b++) RCHK(w.dev(t.vals.as<u64>() + (size_t)b * t.cap, t.n * 8, s));
+    }
+    *len = (int64_t)w.b.size();
+    if (buf) {
+        if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: buffer too small (call with buf=NULL for the size)");
+        std::memcpy(buf, w.b.data(), w.b.size());
+    }
+    return SH_OK;
+}
+
+extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "restore of a sharded aggregation");
+    if (std::memcmp(buf, "SHA1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip aggregation snapshot");
+    hipStream_t s = a->ctx->stream;
+    AReader r{(const uint8_t*)buf, (size_t)len};
+    r.o = 4;
+    if (r.val<uint32_t>() != kAggSnapVersion) return sh_fail(SH_ERR_INVALID, "snapshot version mismatch");
+    if (r.val<uint64_t>() != agg_fingerprint(a)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different aggregation");
+    const int64_t rl = r.val<int64_t>();
+    if (!r.ok || rl <= 0 || r.o + (size_t)rl > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    (void)hipStreamSynchronize(s);
+    RCHK(sh_query_restore(a->root, r.p + r.o, rl));
+    r.o += (size_t)rl;
+    a->root_init = r.val<uint8_t>();
+    a->root_bucket = r.val<int64_t>();
+    if (r.val<uint32_t>() != (uint32_t)a->levels.size() || !r.ok)
+        return sh_fail(SH_ERR_INVALID, "snapshot does not match this aggregation");
+    for (Level& L : a->levels) {
+        L.next_emit = r.val<int64_t>();
+        L.start = r.val<int64_t>();
+        L.store_ts = r.val<int64_t>();
+        L.processed = r.val<uint8_t>();
+        L.n_in = r.val<int64_t>();
+        L.epoch = r.val<uint32_t>();
+        const uint64_t ks = r.val<uint64_t>();
+        const int64_t nk = r.val<int64_t>();
+        if (!r.ok || ks != L.kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this aggregation");
+        RCHK(r.dev(L.kt.keys.p, (int64_t)ks * 8, s));
+        // the key table's insert counter (stream-ordered, from pinned memory)
+        RCHK(L.kt.h_ctrl.reserve(16));
+        uint32_t* c = L.kt.h_ctrl.as<uint32_t>();
+        c[0] = (uint32_t)nk; c[1] = c[2] = c[3] = 0;
+        HIPCHK(hipMemcpyAsync(L.kt.ctrl.p, c, 16, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        L.kt.n_keys = nk;
+        RCHK(r.dev(L.vals.p, (int64_t)a->nb * L.nslots * 8, s));
+        RCHK(r.dev(L.has.p, (int64_t)a->nb * L.nslots, s));
+        RCHK(r.dev(L.tag.p, L.nslots * 4, s));
+        RCHK(r.dev(L.first_seq.p, L.nslots * 4, s));
+    }
+    for (int dur = a->d.min_duration; dur <= a->d.max_duration; dur++) {
+        TableBuf& t = a->tables[dur];
+        const int64_t n = r.val<int64_t>(), drained = r.val<int64_t>();
+        if (!r.ok || n < 0 || drained < 0 || drained > n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        const int64_t ncap = std::max<int64_t>(n, 1024);
+        if (ncap > t.cap) {
+            DevBuf b2, k2, v2;
+            RCHK(b2.reserve(ncap * 8, false));
+            RCHK(k2.reserve(ncap * 8, false));
+            RCHK(v2.reserve((size_t)a->nb * ncap * 8, false));
+            t.bucket = std::move(b2); t.key = std::move(k2); t.vals = std::move(v2);
+            t.cap = ncap;
+        }
+        RCHK(r.dev(t.bucket.p, n * 8, s));
+        RCHK(r.dev(t.key.p, n * 8, s));
+        for (int b = 0; b < a->nb; b++) RCHK(r.dev(t.vals.as<u64>() + (size_t)b * t.cap, n * 8, s));
+        t.n = n;
+        t.drained = drained;
+    }
+    if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    return SH_OK;
+}

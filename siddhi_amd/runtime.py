@@ -223,6 +223,16 @@ class GpuAggregation:
         fl = abi.decode_out(self.find_raw(per, start, end))
         return [r for f in fl for r in f.rows]
 
+    def snapshot(self) -> bytes:
+        n = C.c_int64()
+        _check(lib().sh_aggregation_snapshot(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().sh_aggregation_snapshot(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, blob: bytes):
+        _check(lib().sh_aggregation_restore(self.h, blob, len(blob)))
+
     def table(self, duration: int):
         return [r for f in abi.decode_out(self.table_raw(duration)) for r in f.rows]
 

@@ -181,3 +181,47 @@ def test_retrieval_mid_stream_matches_oracle(rt, proc_time):
     assert _finds(g, spans) == _finds(o, spans)
     g.close()
     o.close()
+
+
+# ---- checkpoint of an aggregation (sh_aggregation_snapshot / restore) --------------------------------
+def test_aggregation_checkpoint_restores_executors_and_tables(rt):
+    """Snapshot mid-stream (root window pending, roll-up stores mid-bucket, late events); the rest of the
+    stream pushed into (a) a fresh aggregation restored from the blob and (b) the original rolled back
+    after it had moved on must give the uninterrupted oracle's tables and retrievals."""
+    rng = np.random.default_rng(47)
+    n = 30_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 50, n)).astype(np.int64)
+    ext = clock - rng.integers(0, 70_000, n).astype(np.int64)
+    k = rng.integers(0, 30, n).astype(np.int32)
+    v = np.round(rng.normal(50, 20, n), 3)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("avg", "v"), ("min", "v"), ("max", "v")], group_by=["k"],
+                               ts="ts", durations=("sec", "day"), key_capacity=64)
+    bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], ext[a_:b_]], 9)
+    cut = 13_001
+    g = rt.GpuAggregation(spec)
+    g.push(bat(0, cut))
+    blob = g.snapshot()
+    g.push(bat(cut, 20_000))  # moves on past the snapshot
+    fresh = rt.GpuAggregation(spec)
+    fresh.restore(blob)
+    g.restore(blob)  # roll back the running aggregation
+    o = OracleAggregation(spec)
+    o.push(bat(0, cut))
+    rest = [bat(cut, n), ("advance", int(clock[-1]) + 2 * 86_400_000)]
+    spans = [(abi.DUR_NAMES[d], 0, 1 << 62) for d in ("sec", "hour", "day")]
+    assert _finds(fresh, spans) == _finds(o, spans) == _finds(g, spans)
+    for x in (g, fresh, o):
+        drive(x, rest[:1])
+    assert _finds(fresh, spans) == _finds(o, spans) == _finds(g, spans)
+    for x in (g, fresh, o):
+        drive(x, rest[1:])
+    ot = tables(o, spec)
+    assert_tables_equal(tables(fresh, spec), ot, "restored")
+    assert_tables_equal(tables(g, spec), ot, "rolled back")
+    with pytest.raises(Exception, match="different aggregation|does not match"):
+        other = rt.GpuAggregation(abi.AggregationSpec(schema, [("sum", "v")], group_by=["k"], ts="ts",
+                                                      durations=("sec", "day"), key_capacity=64))
+        other.restore(blob)
+    for x in (g, fresh, o):
+        x.close()
