@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 5
+#define SH_ABI_VERSION 6
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -227,6 +227,16 @@ int sh_push(sh_query* q, const sh_batch* batch, const sh_out** out);
 int sh_push_device(sh_query* q, const sh_batch* batch, const sh_out** out);
 /* TIMER path: advance the playback clock to `now` without events (Scheduler.onTimeChange). */
 int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
+
+/* Output rate limiting `output [all|first|last] every <n> events` (core/query/output/ratelimit/event/:
+ * AllPerEvent, FirstPerEvent, LastPerEvent and, for group-by queries, FirstGroupByPerEvent /
+ * LastGroupByPerEventOutputRateLimiter.java). Set once, before the first push; every later output
+ * (push, advance_time) goes through the limiter: one flush per input flush that emits rows. */
+#define SH_RATE_NONE 0
+#define SH_RATE_ALL 1
+#define SH_RATE_FIRST 2
+#define SH_RATE_LAST 3
+int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
 
 /* Checkpoint of the query's state: State.snapshot()/restore() (core/util/snapshot/state/State.java:
  * 26-36) driven by SnapshotService.persist/restore (core/util/snapshot/SnapshotService.java:90-296)

@@ -32,6 +32,7 @@ def lib():
         L.or_query_create.argtypes = [P(abi.QueryDesc)]
         L.or_query_create.restype = C.c_void_p
         L.or_query_destroy.argtypes = [C.c_void_p]
+        L.or_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
         L.or_push.argtypes = [C.c_void_p, P(abi.Batch), P(P(abi.Out))]
         L.or_advance_time.argtypes = [C.c_void_p, C.c_int64, P(P(abi.Out))]
         L.or_aggregation_create.argtypes = [P(abi.AggregationDesc)]
@@ -53,6 +54,8 @@ class OracleQuery:
         self._desc = spec.desc()
         self.h = lib().or_query_create(C.byref(self._desc))
         if not self.h:
+            raise ValueError(lib().or_last_error().decode())
+        if spec.rate and lib().or_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])):
             raise ValueError(lib().or_last_error().decode())
 
     def push_raw(self, batch: abi.HostBatch):

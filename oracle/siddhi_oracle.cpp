@@ -378,6 +378,85 @@ struct OutBuf {
 };
 
 // ==========================================================================================
+// Output rate limiting `output [all|first|last] every N events` (OutputParser.java:288-303 picks the
+// limiter; core/query/output/ratelimit/event/*.java). Each selector output chunk (one flush here) is
+// one process() call; a call that emits rows sends one chunk with the flush's clock.
+// ==========================================================================================
+struct RateLimiter {
+    int kind = SH_RATE_NONE;
+    int64_t value = 0;
+    bool group_by = false;
+    int64_t counter = 0;                          // All/First/Last(GroupBy)PerEvent: state.counter
+    std::vector<OutRow> all_chunk;                // AllPerEvent: state.allComplexEventChunk
+    std::map<std::vector<int64_t>, int64_t> first_count;  // FirstGroupByPerEvent: groupByOutputTime
+    std::vector<std::vector<int64_t>> last_order;  // LastGroupByPerEvent: allGroupByKeyEvents (LinkedHashMap)
+    std::map<std::vector<int64_t>, OutRow> last_rows;
+    int nk = 0;
+
+    std::vector<int64_t> key_of(const OutRow& r) const { return std::vector<int64_t>(r.keys, r.keys + nk); }
+
+    void process(const OutRow* rows, int64_t n, std::vector<OutRow>& out) {
+        for (int64_t i = 0; i < n; i++) {
+            const OutRow& ev = rows[i];
+            if (kind == SH_RATE_ALL) {  // AllPerEventOutputRateLimiter.process :48-77
+                all_chunk.push_back(ev);
+                if (++counter == value) {
+                    out.insert(out.end(), all_chunk.begin(), all_chunk.end());
+                    all_chunk.clear();
+                    counter = 0;
+                }
+            } else if (kind == SH_RATE_FIRST && !group_by) {  // FirstPerEventOutputRateLimiter :48-72
+                counter++;
+                if (counter == 1) out.push_back(ev);
+                else if (counter == value) counter = 0;
+            } else if (kind == SH_RATE_LAST && !group_by) {  // LastPerEventOutputRateLimiter :47-71
+                if (++counter == value) {
+                    out.push_back(ev);
+                    counter = 0;
+                }
+            } else if (kind == SH_RATE_FIRST) {  // FirstGroupByPerEventOutputRateLimiter :48-77
+                const std::vector<int64_t> k = key_of(ev);
+                auto it = first_count.find(k);
+                if (it == first_count.end()) {
+                    first_count[k] = 1;
+                    out.push_back(ev);
+                } else if (it->second == value - 1) {
+                    first_count.erase(it);
+                } else {
+                    it->second++;
+                }
+            } else {  // LastGroupByPerEventOutputRateLimiter :51-83
+                const std::vector<int64_t> k = key_of(ev);
+                if (!last_rows.count(k)) last_order.push_back(k);
+                last_rows[k] = ev;
+                if (++counter == value) {
+                    counter = 0;
+                    for (const auto& kk : last_order) out.push_back(last_rows[kk]);
+                    last_order.clear();
+                    last_rows.clear();
+                }
+            }
+        }
+    }
+
+    // the selector's flushes of one push/advance -> the limiter's flushes
+    void apply(OutBuf& o) {
+        if (kind == SH_RATE_NONE) return;
+        std::vector<OutRow> rows;
+        rows.swap(o.rows);
+        std::vector<int64_t> off = o.flush_offsets, clk = o.flush_clock;
+        o.clear();
+        for (size_t f = 0; f < clk.size(); f++) {
+            std::vector<OutRow> chunk;
+            process(rows.data() + off[f], off[f + 1] - off[f], chunk);
+            if (chunk.empty()) continue;
+            o.rows.insert(o.rows.end(), chunk.begin(), chunk.end());
+            o.close_flush(clk[f]);
+        }
+    }
+};
+
+// ==========================================================================================
 // Window query engine
 // ==========================================================================================
 struct PartitionState {
@@ -421,6 +500,7 @@ struct Query {
     // ever fires states with a due time (:75-87), so a scan over these equals the scan over all
     std::map<size_t, int64_t> armed;
     OutBuf out;
+    RateLimiter rate;
 
     PartitionState& part(int64_t key) {
         auto it = parts.find(key);
@@ -1191,12 +1271,27 @@ void* or_query_create(const sh_query_desc* desc) {
 
 void or_query_destroy(void* h) { delete (Query*)h; }
 
+int or_query_set_output_rate(void* h, int32_t kind, int64_t n) {
+    Query* q = (Query*)h;
+    if (kind < SH_RATE_NONE || kind > SH_RATE_LAST || (kind != SH_RATE_NONE && n < 1)) {
+        g_err = "invalid output rate";
+        return SH_ERR_INVALID;
+    }
+    q->rate = RateLimiter{};
+    q->rate.kind = kind;
+    q->rate.value = n;
+    q->rate.group_by = q->d.n_group_by > 0;
+    q->rate.nk = q->d.n_group_by;
+    return SH_OK;
+}
+
 int or_push(void* h, const sh_batch* b, const sh_out** out) {
     Query* q = (Query*)h;
     q->out.clear();
     int64_t step = b->send_size > 0 ? b->send_size : b->n;
     for (int64_t lo = 0; lo < b->n; lo += step) q->send(b, lo, std::min(b->n, lo + step));
     q->seq_base += b->n;
+    q->rate.apply(q->out);
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }
@@ -1205,6 +1300,7 @@ int or_advance_time(void* h, int64_t now, const sh_out** out) {
     Query* q = (Query*)h;
     q->out.clear();
     q->set_clock(now);
+    q->rate.apply(q->out);
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }

@@ -170,6 +170,7 @@ class QuerySpec:
     output: str = "current"          # 'current' | 'all' | 'expired'
     partition: Optional[str] = None
     key_capacity: int = 0
+    rate: Optional[tuple] = None       # ('all'|'first'|'last', n): `output <kind> every n events`
     ts_attr: Optional[str] = None      # externalTimeBatch timestamp attribute
     start_attr: Optional[str] = None   # externalTimeBatch start time from this attribute
     _keep: list = field(default_factory=list, repr=False)
@@ -387,6 +388,7 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
     lib.sh_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
     lib.sh_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(Out))]
+    lib.sh_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
     lib.sh_aggregation_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, P(C.c_int64)]
     lib.sh_aggregation_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.sh_alloc_pinned.argtypes = [C.c_int64, P(C.c_void_p)]
@@ -427,5 +429,8 @@ ABI_SYMBOLS = [
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
-    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore",
+    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate",
 ]
+
+# output rate limiter kinds (SH_RATE_*)
+RATE_KINDS = {"all": 1, "first": 2, "last": 3}

@@ -304,4 +304,28 @@ void launch_pass_rows(hipStream_t s, i64 hi, i64 n_pend, const u32* new_pos, u32
                       const u64* pend_gidx, const i64* ts, i64 seq_base, const Segment* segs, int nseg, i64* out_ts,
                       i64* out_rep, u32* seg_rows, u32* n_rows);
 
+// ---- output rate limiting (sh_rate.cpp, sh_rate_kernels.hip) ----
+struct RateRows {
+    i64* ts;
+    unsigned char* expired;
+    i64* rep;
+    i64* keys;
+    u64* vals;
+    unsigned char* nulls;
+};
+void launch_rate_pos(hipStream_t s, i64 n_src, i64 n_carry, int mode, i64 N, i64 seq0, const i64* flush_off, int nf,
+                     u32* flag, int* eflush, u32* src);
+void launch_rate_clear(hipStream_t s, i64 n, u32* src, u32* flag);
+void launch_rate_pack(hipStream_t s, i64 n, const i64* keys, i64 stride, int nk, u64* skey, u32* idx);
+void launch_rate_segments(hipStream_t s, i64 n, const u64* skey, const u32* idx, i64 N, int with_win, u32* hd, u32* pos,
+                          u32* starts, i64* tmp);
+void launch_rate_first(hipStream_t s, i64 n, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
+                       const u32* idx, i64 N, u64* tk, i64* tc, u32 tmask, i64* seg_c0, u32* seg_new, u32* n_keys,
+                       const i64* flush_off, int nf, u32* flag, int* eflush);
+void launch_rate_rehash(hipStream_t s, i64 old_cap, const u64* otk, const i64* otc, u64* tk, i64* tc, u32 tmask);
+void launch_rate_last(hipStream_t s, i64 n, const u32* hd, const u32* pos, const u32* starts, const u32* idx, i64 N,
+                      i64 n_carry, const i64* flush_off, int nf, u32* flag, u32* src, int* eflush);
+void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, const u32* src, const int* eflush,
+                        RateRows in, i64 in_stride, RateRows out, i64 T, int nk, int na, int* out_flush);
+
 }  // namespace shd

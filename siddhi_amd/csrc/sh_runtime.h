@@ -283,6 +283,24 @@ struct sh_query {
     DevBuf x_items, x_keep, x_rank, x_match, x_tmp, x_matched, x_trow, x_tkey, pass_pos;
     PinnedBuf x_h;
     std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call
+    // `output [all|first|last] every N events` (sh_rate.cpp): the limiter's state across calls
+    struct Rate {
+        int kind = SH_RATE_NONE;
+        int64_t N = 0;
+        bool gb = false;          // group-by variants (FirstGroupBy / LastGroupBy)
+        int64_t seq = 0;          // rows seen (First/LastPerEvent counters)
+        int64_t nc = 0;           // carried rows (AllPerEvent chunk, LastGroupBy open window)
+        DevBuf c_ts, c_exp, c_rep, c_keys, c_vals, c_nulls;          // carried rows (stride nc)
+        DevBuf s_ts, s_exp, s_rep, s_keys, s_vals, s_nulls;          // source rows of a call
+        DevBuf o_ts, o_exp, o_rep, o_keys, o_vals, o_nulls, o_flush;  // kept rows
+        DevBuf foff, flag, pre, src, eflush, tmp, skey, skey2, idx, idx2, hd, pos, starts, seg_c0, seg_new, sort_tmp;
+        DevBuf tk, tc, tk2, tc2, n_keys;  // FirstGroupBy key -> count table
+        int64_t t_cap = 0, t_keys = 0;
+        PinnedVec<int64_t> h_off, h_clk, flush_offsets, flush_clock;
+        PinnedVec<int> h_flush;
+        PinnedBuf h_small;
+        sh_out dev_out{};
+    } rate;
     // double-buffered host ingest (sh_ingest.cpp): two device staging slots filled on the copy stream
     struct Ingest {
         StagedBatch slot[2];
@@ -306,6 +324,9 @@ void ingest_destroy(sh_query* q);  // (sh_ingest.cpp)
 
 // expired / all-events output of a batch query's call (sh_expired.cpp)
 int xout_finish(sh_query* q, bool host_out, const sh_out** out);
+// output rate limiting over a call's device output (sh_rate.cpp); flush_dev: the input's flush
+// arrays are device memory (sliding windows)
+int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, const sh_out** out);
 
 // the filter restricted to partition key `key` (R12): base AND (pcol == key)
 int partition_filter(const FilterProg& base, int pcol, int ptype, int64_t key, FilterProg* out);

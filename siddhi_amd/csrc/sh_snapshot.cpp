@@ -213,6 +213,7 @@ extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* l
     if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
     if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
     if (q->xmode) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a query with expired / all-events output");
+    if (q->rate.kind != SH_RATE_NONE) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a rate-limited query");
     Writer w;
     w.put("SHQ1", 4);
     w.val<uint32_t>(kVersion);

@@ -779,8 +779,18 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
     sh_batch dev;
     RCHK(q->staged.stage(q->ctx->stream, b, q->d.n_cols, q->d.col_types, &dev));
-    if (q->kind == 1) return sliding_push(q, &dev, true, out);
-    return push_core(q, &dev, true, out);
+    return query_push_staged(q, &dev, out);
+}
+
+// a push through the query's output rate limiter: device output, then the limiter (sh_rate.cpp)
+static int push_any(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out) {
+    if (q->rate.kind != SH_RATE_NONE) {
+        const bool sl = q->kind == 1;
+        RCHK(sl ? sliding_push(q, dev, false, out) : push_core(q, dev, false, out));
+        return rate_apply(q, *out, sl, host_out, out);
+    }
+    if (q->kind == 1) return sliding_push(q, dev, host_out, out);
+    return push_core(q, dev, host_out, out);
 }
 
 // The open window's pending events aggregated per key without closing it (the aggregation root's
@@ -811,15 +821,13 @@ int query_peek(sh_query* q, int64_t* n_rows) {
 
 // a push whose batch is already on the device, with host output (sh_push_staged)
 int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out) {
-    if (q->kind == 1) return sliding_push(q, dev, true, out);
-    return push_core(q, dev, true, out);
+    return push_any(q, dev, true, out);
 }
 
 extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
-    if (q->kind == 1) return sliding_push(q, b, false, out);
-    return push_core(q, b, false, out);
+    return push_any(q, b, false, out);
 }
 
 static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_out** out) {
@@ -863,6 +871,10 @@ extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
     if (q->kind == 1) return sliding_advance(q, now, out);
+    if (q->rate.kind != SH_RATE_NONE) {
+        RCHK(advance_core(q, now, false, out));
+        return rate_apply(q, *out, false, true, out);
+    }
     return advance_core(q, now, true, out);
 }
 

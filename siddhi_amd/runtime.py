@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 5:
+        if L.sh_abi_version() != 6:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -81,6 +81,12 @@ class GpuQuery:
         self.h = C.c_void_p()
         _check(lib().sh_query_create(self.ctx.h, C.byref(self._desc), C.byref(self.h)))
         self.callbacks: List[Callable] = []
+        if spec.rate:
+            try:
+                _check(lib().sh_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])))
+            except Exception:
+                self.close()
+                raise
 
     # -- reference-shaped API --------------------------------------------------------------
     def add_callback(self, fn: Callable[[List[tuple]], None]):

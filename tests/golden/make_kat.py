@@ -309,6 +309,71 @@ case(name="filter30_bool", source=F + ":1036-1064", schema="symbol string, price
      query=dict(window=None, filter=["!=", "available", ["bool", 1]]),
      sends=[[[B, "IBM", 55.6, True]], [[B + 1, "WSO2", 57.6, False]]], expect=dict(in_count=1))
 
+# ------------------------------------------------- output rate limiting (EventOutputRateLimitTestCase)
+# `output [all|first|last] every N events` over the selector's rows (OutputParser.java:288-303). The
+# Java tests send one event per InputHandler.send (each send is one chunk for the limiter).
+R = "ctest/query/ratelimit/EventOutputRateLimitTestCase.java"
+LOGIN = "timestamp long, ip string"
+
+
+def _ips(*ips):
+    return [[[B + i, B + i, "192.10.1." + str(x)]] for i, x in enumerate(ips)]
+
+
+def _ip(*xs):
+    return ["192.10.1." + str(x) for x in xs]
+
+
+case(name="rate1_all2", source=R + ":45-97", schema=LOGIN, query=dict(window=None, rate=["all", 2]),
+     sends=_ips(3, 3, 4, 3, 5), expect=dict(in_count=4, remove_count=0))
+case(name="rate2_default_all2", source=R + ":99-149", schema=LOGIN, query=dict(window=None, rate=["all", 2]),
+     sends=_ips(3, 3, 4, 3, 5), expect=dict(in_count=4, remove_count=0))
+case(name="rate3_all5", source=R + ":151-205", schema=LOGIN, query=dict(window=None, rate=["all", 5]),
+     sends=_ips(5, 5, 3, 9, 4, 4, 4, 30), expect=dict(in_count=5, remove_count=0))
+case(name="rate4_first2", source=R + ":207-260", schema=LOGIN, query=dict(window=None, rate=["first", 2]),
+     sends=_ips(5, 3, 9, 4, 3), expect=dict(in_count=3, remove_count=0, in_col_in=["ip", _ip(5, 9, 3)]))
+case(name="rate5_first3", source=R + ":262-314", schema=LOGIN, query=dict(window=None, rate=["first", 3]),
+     sends=_ips(5, 3, 9, 4, 3), expect=dict(in_count=2, remove_count=0, in_col_in=["ip", _ip(5, 4)]))
+case(name="rate6_last2", source=R + ":316-368", schema=LOGIN, query=dict(window=None, rate=["last", 2]),
+     sends=_ips(3, 5, 3, 4, 3), expect=dict(in_count=2, remove_count=0, in_col_in=["ip", _ip(5, 4)]))
+case(name="rate7_last4", source=R + ":370-421", schema=LOGIN, query=dict(window=None, rate=["last", 4]),
+     sends=_ips(3, 5, 3, 4, 3), expect=dict(in_count=1, remove_count=0, in_col_in=["ip", _ip(4)]))
+case(name="rate8_first5_group_by", source=R + ":423-476", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["first", 5]),
+     sends=_ips(5, 5, 3, 9, 4, 4, 4, 30), expect=dict(in_count=5, remove_count=0))
+case(name="rate9_last5_group_by", source=R + ":478-533", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["last", 5]),
+     sends=_ips(5, 5, 3, 9, 4, 4, 4, 30), expect=dict(in_count=4, remove_count=0))
+case(name="rate10_first5_group_by", source=R + ":535-590", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["first", 5]),
+     sends=_ips(5, 5, 3, 9, 4, 4, 4, 4, 4, 30), expect=dict(in_count=5, remove_count=0))
+case(name="rate11_last5_group_by", source=R + ":592-649", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["last", 5]),
+     sends=_ips(5, 5, 3, 9, 4, 4, 4, 30, 3, 30), expect=dict(in_count=7, remove_count=0))
+_r12 = _ips(5, 3, 3, 9, 3, 4, 4, 4, 30, 31, 32, 33)
+case(name="rate12_lengthBatch_last5_group_by", source=R + ":651-710", schema=LOGIN,
+     query=dict(window="lengthBatch", param=4, group_by=["ip"], aggs=[["count", None]], rate=["last", 5]),
+     sends=_r12, expect=dict(in_count=4, remove_count=0))
+case(name="rate13_lengthBatch_last2", source=R + ":712-769", schema=LOGIN,
+     query=dict(window="lengthBatch", param=4, aggs=[["count", None]], rate=["last", 2]),
+     sends=_r12, expect=dict(in_count=1, remove_count=0))
+case(name="rate14_lengthBatch_expired_last2", source=R + ":771-829", schema=LOGIN,
+     query=dict(window="lengthBatch", param=4, aggs=[["count", None]], output="expired", rate=["last", 2]),
+     sends=_r12, expect=dict(in_count=0, remove_count=1))
+case(name="rate15_lengthBatch_expired_all2", source=R + ":831-888", schema=LOGIN,
+     query=dict(window="lengthBatch", param=4, aggs=[["count", None]], output="expired", rate=["all", 2]),
+     sends=_r12, expect=dict(in_count=0, remove_count=2))
+case(name="rate16_lengthBatch_expired_all2_group_by", source=R + ":890-948", schema=LOGIN,
+     query=dict(window="lengthBatch", param=4, group_by=["ip"], aggs=[["count", None]], output="expired",
+                rate=["all", 2]),
+     sends=_r12, expect=dict(in_count=0, remove_count=4))
+case(name="rate17_first2_group_by", source=R + ":950-1006", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["first", 2]),
+     sends=_ips(5, 5, 3, 5, 5, 9, 4, 4, 4, 5, 30), expect=dict(in_count=8, remove_count=0))
+case(name="rate18_first2", source=R + ":1008-1066", schema=LOGIN, query=dict(window=None, rate=["first", 2]),
+     sends=_ips(5, 3, 5, 5, 5, 9, 4, 4, 4, 30, 5),
+     expect=dict(in_count=6, remove_count=0, in_col_in=["ip", _ip(5, 4)]))
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat_reference.json")
     with open(out, "w") as f:

@@ -57,7 +57,8 @@ def build(case, dic):
                          aggs=[tuple(x) for x in q.get("aggs", [])], filter=_conv_filter(q.get("filter"), dic),
                          start_time=q.get("start_time"), stream_current=q.get("stream_current", False),
                          output=q.get("output", "current"), partition=q.get("partition"),
-                         ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"))
+                         ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"),
+                         rate=tuple(q["rate"]) if q.get("rate") else None)
     return schema, spec
 
 
@@ -125,7 +126,7 @@ def check_query(case, flushes, schema, dic):
     # event QuerySelector keeps per key): in/remove order checks and transcribed attribute columns
     events = [r for s in case["sends"] if isinstance(s, list) for r in s]
     reps = [x for f in flushes for x in f.reps]
-    if "in_order" in e or "remove_order" in e or "rep_cols" in e:
+    if "in_order" in e or "remove_order" in e or "rep_cols" in e or "in_col_in" in e:
         assert len(reps) == len(rows), "output without representative events"
 
     def attr(col, idx):
@@ -136,6 +137,11 @@ def check_query(case, flushes, schema, dic):
     if "remove_order" in e:
         got = [attr(e.get("in_order_col", "volume"), i) for i, r in enumerate(rows) if r[1]]
         assert got == e["remove_order"], (got, e["remove_order"])
+    if "in_col_in" in e:  # the Java callback asserts every (first) in-event's attribute is one of these
+        col, allowed = e["in_col_in"]
+        for i, r in enumerate(rows):
+            if not r[1]:
+                assert attr(col, i) in allowed, (col, attr(col, i), allowed)
     if "rep_cols" in e:
         for col, want in e["rep_cols"]:
             got = [attr(col, i) for i in range(len(rows))]

@@ -1,0 +1,158 @@
+"""GPU parity of `output [all|first|last] every N events` (sh_rate.cpp / sh_rate_kernels.hip) against
+the oracle's restatement of the reference's event rate limiters (core/query/output/ratelimit/event/
+AllPerEvent, FirstPerEvent, LastPerEvent, FirstGroupByPerEvent, LastGroupByPerEventOutputRateLimiter).
+The oracle's limiters are pinned by EventOutputRateLimitTestCase (tests/golden, rate1..rate18); the
+windowed ones (rate12..16) also run on the GPU through test_gpu_parity.py, and the no-window ones run
+here as `#window.lengthBatch(1)` (one event per send: every send is one chunk either way)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle.oracle import OracleQuery
+from siddhi_amd import abi
+from tests import kat_runner
+from tests.parity import assert_same, run_pushes, split_batches
+from tests.test_gpu_parity import both
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = abi.Schema.parse("k int, v double, x long, ts long")
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def stream(n, keys, seed, step=40):
+    rng = np.random.default_rng(seed)
+    ts = np.cumsum(rng.integers(0, step, n)).astype(np.int64) + 5_000
+    k = rng.integers(0, keys, n).astype(np.int32)
+    v = rng.integers(-4000, 4000, n).astype(np.float64) / 16.0
+    x = rng.integers(-10**6, 10**6, n).astype(np.int64)
+    return ts, [k, v, x, ts.copy()]
+
+
+NOWIN_RATE_KATS = [c for c in kat_runner.load_cases()
+                   if c.get("kind") != "aggregation" and c["query"].get("rate") and c["query"].get("window") is None]
+
+
+@pytest.mark.parametrize("case", NOWIN_RATE_KATS, ids=[c["name"] for c in NOWIN_RATE_KATS])
+def test_reference_rate_kat_on_gpu(rt, case):
+    q = case["query"]
+    aggs = [["count", None]] if q.get("group_by") else []
+    wrapped = dict(case, query=dict(q, window="lengthBatch", param=1, aggs=aggs))
+    schema, _, dic, flushes = kat_runner.run_query(wrapped, rt.GpuQuery)
+    kat_runner.check_query(case, flushes, schema, dic)
+    _, _, _, oflushes = kat_runner.run_query(wrapped, OracleQuery)
+    assert [(f.clock, f.rows) for f in flushes] == [(f.clock, f.rows) for f in oflushes]
+
+
+AGGS = [("count", None), ("sum", "v"), ("max", "x")]
+KINDS = [("all", 1), ("all", 7), ("first", 1), ("first", 3), ("last", 1), ("last", 4), ("first", 50), ("last", 33)]
+
+
+@pytest.mark.parametrize("kind,n", KINDS)
+@pytest.mark.parametrize("group_by", [True, False])
+def test_lengthbatch_rate(rt, kind, n, group_by):
+    ts, cols = stream(30_000, 40, 3)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 97, group_by=["k"] if group_by else (), aggs=AGGS,
+                         key_capacity=64, rate=(kind, n))
+    out = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 500, 12_345, 12_346], 3),
+               label=f"lengthBatch {kind} {n} gb={group_by}")
+    assert out["ts"].size > 0
+
+
+@pytest.mark.parametrize("kind,n", [("all", 5), ("first", 4), ("last", 6)])
+@pytest.mark.parametrize("output", ["all", "expired"])
+def test_timebatch_expired_rate(rt, kind, n, output):
+    ts, cols = stream(40_000, 200, 5)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 600, group_by=["k"], aggs=AGGS, filter=(">", "v", -100.0),
+                         output=output, key_capacity=256, rate=(kind, n))
+    pushes = split_batches(SCHEMA, ts, cols, [2_000, 20_000, 20_001], 7)
+    pushes += [("advance", int(ts[-1]) + 300), ("advance", int(ts[-1]) + 5_000)]
+    out = both(rt, spec, pushes, label=f"timeBatch {output} {kind} {n}")
+    assert out["expired"].sum() > 0
+
+
+@pytest.mark.parametrize("kind,n", [("all", 3), ("first", 5), ("last", 2), ("first", 1)])
+@pytest.mark.parametrize("group_by", [True, False])
+def test_sliding_time_rate(rt, kind, n, group_by):
+    ts, cols = stream(20_000, 30, 11)
+    spec = abi.QuerySpec(SCHEMA, "time", 500, group_by=["k"] if group_by else (), aggs=[("sum", "v"), ("min", "x")],
+                         key_capacity=64, rate=(kind, n))
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 9_999], 4), label=f"time {kind} {n} gb={group_by}")
+
+
+@pytest.mark.parametrize("kind,n", [("all", 4), ("last", 3)])
+def test_pass_through_rate(rt, kind, n):
+    ts, cols = stream(10_000, 10, 21)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 13, filter=("<", "x", 500_000), rate=(kind, n))
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [5, 4_000], 2), label=f"pass-through {kind} {n}")
+
+
+def test_first_group_by_table_growth(rt):
+    """FirstGroupBy's key -> count table grows (rehash) while counts carry across pushes."""
+    ts, cols = stream(120_000, 50_000, 23, step=3)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 1000, group_by=["k"], aggs=[("count", None)],
+                         key_capacity=65_536, rate=("first", 3))
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [100, 1_000, 30_000, 60_000], 0), label="first gb growth")
+
+
+def _hip():
+    return C.CDLL("libamdhip64.so")
+
+
+def _dev_arrays(out_ptr):
+    """abi.out_arrays for an sh_push_device result: row arrays copied out of HBM first."""
+    o = out_ptr.contents
+    n, nk, na = o.n_rows, o.n_keys, o.n_vals
+    hip = _hip()
+    host = {}
+    for name, cnt, dt in (("ts", n, np.int64), ("expired", n, np.uint8), ("keys", nk * n, np.int64),
+                          ("vals", na * n, np.uint64), ("nulls", na * n, np.uint8), ("rep", n, np.int64)):
+        a = np.zeros(max(cnt, 1), dt)
+        src = C.cast(getattr(o, name), C.c_void_p).value
+        if cnt:
+            assert hip.hipMemcpy(C.c_void_p(a.ctypes.data), C.c_void_p(src), C.c_size_t(a.itemsize * cnt), 2) == 0
+        host[name] = a[:cnt]
+    res = {
+        "flush_offsets": np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
+        if o.n_flushes else np.zeros(1, np.int64),
+        "flush_clock": np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
+        if o.n_flushes else np.zeros(0, np.int64),
+        "val_types": np.array([o.val_types[i] for i in range(na)], np.int32),
+        "ts": host["ts"], "expired": host["expired"], "rep": host["rep"],
+        "keys": host["keys"].reshape(nk, n), "vals": host["vals"].reshape(na, n), "nulls": host["nulls"].reshape(na, n),
+    }
+    return res
+
+
+@pytest.mark.parametrize("window,param", [("lengthBatch", 50), ("timeBatch", 300)])
+def test_device_output_rate(rt, window, param):
+    """sh_push_device: the limiter's rows stay in HBM, flush metadata on the host."""
+    import torch
+    ts, cols = stream(20_000, 25, 31)
+    spec = abi.QuerySpec(SCHEMA, window, param, group_by=["k"], aggs=AGGS, key_capacity=32, rate=("last", 5))
+    g = rt.GpuQuery(spec)
+    parts = []
+    for b in split_batches(SCHEMA, ts, cols, [7_000, 7_001], 0):
+        keep = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in [b.ts] + b.cols]
+        torch.cuda.synchronize()
+        parts.append(_dev_arrays(g.push_device(len(b.ts), keep[0].data_ptr(), [t.data_ptr() for t in keep[1:]])))
+    g.close()
+    o = OracleQuery(spec)
+    ora = run_pushes(o, split_batches(SCHEMA, ts, cols, [7_000, 7_001], 0))
+    o.close()
+    assert_same(abi.concat_arrays(parts), ora, label=f"device {window}")
+
+
+def test_rate_rejects(rt):
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 100, group_by=["k"], aggs=AGGS, partition="k", rate=("all", 2))
+    with pytest.raises(rt.SiddhiError, match="partitioned"):
+        rt.GpuQuery(spec)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 10, aggs=AGGS, rate=("first", 0))
+    with pytest.raises(rt.SiddhiError, match="every >= 1"):
+        rt.GpuQuery(spec)
