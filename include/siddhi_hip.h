@@ -342,6 +342,12 @@ int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_byte
                      int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order);
 /* TIMER path of the sharded query: every rank calls it with the same `now`. */
 int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out, const int64_t** order);
+/* Checkpoint of one rank's shard (SnapshotService.persist/restore, SnapshotService.java:90-296): the
+ * global stream state every rank keeps (clock, nextEmitTime, batch count, stream index, p0) and its
+ * owner query's windows. Taken between pushes on every rank; restored into a shard created from the
+ * same descriptor, rank and world. Two calls as sh_query_snapshot. Sharded aggregations: refused. */
+int sh_shard_snapshot(sh_shard* s, void* buf, int64_t cap, int64_t* len);
+int sh_shard_restore(sh_shard* s, const void* buf, int64_t len);
 /* Key-sharded incremental aggregation (C4 across G GPUs): *shard ingests through the three phases
  * above (owner = the group key's owner; an event's time bucket travels as its raw `aggregate by`
  * column), and every owner runs the root and all roll-up levels of its keys, so the union of the G

@@ -415,6 +415,8 @@ def setup_lib_prototypes(lib, prefix: str):
                                          P(P(Out)), P(PI)]
         lib.sh_shard_stats.argtypes = [C.c_void_p, P(Stats)]
         lib.sh_shard_advance_time.argtypes = [C.c_void_p, C.c_int64, C.c_int32, P(P(Out)), P(PI)]
+        lib.sh_shard_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, PI]
+        lib.sh_shard_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     if hasattr(lib, "sh_aggregation_shard_create"):
         lib.sh_aggregation_shard_create.argtypes = [C.c_void_p, P(AggregationDesc), C.c_int32, C.c_int32,
                                                     P(C.c_void_p), P(C.c_void_p)]
@@ -430,6 +432,7 @@ ABI_SYMBOLS = [
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
     "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate",
+    "sh_shard_snapshot", "sh_shard_restore",
 ]
 
 # output rate limiter kinds (SH_RATE_*)

@@ -328,4 +328,16 @@ void launch_rate_last(hipStream_t s, i64 n, const u32* hd, const u32* pos, const
 void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, const u32* src, const int* eflush,
                         RateRows in, i64 in_stride, RateRows out, i64 T, int nk, int na, int* out_flush);
 
+// ---- stream.current.event batch windows (sh_kernels.hip, driven by sh_window.cpp) ----
+void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
+                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send);
+void launch_sc_walk(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx,
+                    const i64* chunk, const u64* pend_vals, i64 pend_cap, AggPlan ap, i64 n_old, u32* ghead, u64* sval,
+                    u32* slast);
+void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32* pre, const u32* slast, const u64* sval,
+                    const u32* pend_pos, const i64* pend_ts, const u64* pend_gidx, const i64* chunk, const i64* send,
+                    KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys, u64* out_vals, i64* out_rep,
+                    i64* out_chunk, i64* out_send);
+void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out);
+
 }  // namespace shd

@@ -1474,4 +1474,155 @@ void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_
     hipLaunchKernelGGL(k_rekey, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, pos, old_kt, new_kt);
 }
 
+
+// ================================================================================================
+// stream.current.event batch windows (sh_stream_current.cpp)
+// ================================================================================================
+// sh_sc_kernels.hip — `#window.lengthBatch(L, true)` / `#window.timeBatch(T, true)` (stream.current.event)
+// with current-events output. The window emits every arriving event at once and resets the aggregators
+// when a batch ends (LengthBatchWindowProcessor.processStreamCurrentEvents :245-274, TimeBatchWindow-
+// Processor.process :262-340 in RESET mode); the selector groups each chunk by key (QuerySelector
+// :315-374: a key's row is the value after its last event of the chunk, at its first position). A row's
+// values are therefore the running aggregates of its (window, key) up to that event.
+//
+// The pending buffer holds [the open window's earlier events | this push's passing events]; the
+// entries are stably sorted by (window, key slot), each (window, key) run is folded in event order by
+// one thread (the Java order of the double sums), and the last entry of every (chunk, key) group writes
+// the group's row values at the group's first entry. A scan over those heads gives the output order.
+
+
+// window of entry m (0 = the window open before the push; a new entry j is in window #{pcb <= j})
+// and its chunk: lengthBatch sends every event on its own (:160-182), timeBatch the whole send
+__global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
+                                                   const u32* __restrict__ pend_pos, const u64* __restrict__ pend_gidx,
+                                                   int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx,
+                                                   i64* chunk, i64* send) {
+    const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M) return;
+    u32 w = 0;
+    if (m >= n_old) {
+        const i64 j = m - n_old;
+        int lo = 0, hi = nb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pcb[mid] <= j) lo = mid + 1; else hi = mid;
+        }
+        w = (u32)lo;
+        const i64 e = (i64)pend_gidx[m] - seq0;  // the event's index in the push
+        const i64 sd = send_size > 0 ? e / send_size : 0;
+        chunk[m] = per_event ? j : sd;
+        send[m] = sd;
+    } else {
+        chunk[m] = -1;
+        send[m] = -1;
+    }
+    skey[m] = ((u64)w << 32) | (u64)pend_pos[m];
+    idx[m] = (u32)m;
+}
+
+// one thread per (window, key) run of the sorted entries
+__global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                   const u32* __restrict__ starts, const u32* __restrict__ idx,
+                                                   const i64* __restrict__ chunk, const u64* __restrict__ pend_vals,
+                                                   i64 pend_cap, AggPlan ap, i64 n_old, u32* ghead, u64* sval,
+                                                   u32* slast) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M || !hd[i]) return;
+    const i64 hi = starts[pos[i] + 1];
+    u64 f[SH_MAX_AGGS];
+#pragma unroll
+    for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = 0;
+    u32 c = 0;
+    i64 head = -1;
+    for (i64 t = i; t < hi; t++) {
+        const u32 m = idx[t];
+        i64 v[SH_MAX_AGGS];
+#pragma unroll
+        for (int j = 0; j < SH_MAX_AGGS; j++) v[j] = j < ap.n_vcols ? (i64)pend_vals[(size_t)j * pend_cap + m] : 0;
+        fold_fields<SH_MAX_AGGS>(ap, f, c == 0, v);
+        c++;
+        if ((i64)m < n_old) continue;
+        const i64 ch = chunk[m];
+        if (head < 0 || chunk[idx[t - 1]] != ch) {
+            head = m;
+            ghead[m] = 1;
+        }
+        if (t + 1 == hi || chunk[idx[t + 1]] != ch) {  // the group's last event: its row values
+#pragma unroll
+            for (int a = 0; a < SH_MAX_AGGS; a++) {
+                if (a >= ap.n) break;
+                u64 fv = f[0];
+#pragma unroll
+                for (int j = 1; j < SH_MAX_AGGS; j++) if (ap.field[a] == j) fv = f[j];
+                sval[(size_t)a * M + head] = agg_out(ap, a, c, fv);
+            }
+            slast[head] = m;
+        }
+    }
+}
+
+// rows in output order (heads of the new entries, scanned): ts / representative event of the group's
+// last event, the key of its slot, the values
+__global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32* __restrict__ ghead,
+                                                   const u32* __restrict__ pre, const u32* __restrict__ slast,
+                                                   const u64* __restrict__ sval, const u32* __restrict__ pend_pos,
+                                                   const i64* __restrict__ pend_ts, const u64* __restrict__ pend_gidx,
+                                                   const i64* __restrict__ chunk, const i64* __restrict__ send,
+                                                   KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys,
+                                                   u64* out_vals, i64* out_rep, i64* out_chunk, i64* out_send) {
+    const i64 m = n_old + (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M || !ghead[m]) return;
+    const i64 o = pre[m - n_old];
+    const u32 l = slast[m];
+    out_ts[o] = pend_ts[l];
+    out_rep[o] = (i64)pend_gidx[l];
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
+    for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
+    for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+    out_chunk[o] = chunk[m];
+    out_send[o] = send[m];
+}
+
+// the last timestamp of every send of the push (the send's playback clock before the prefix max)
+__global__ __launch_bounds__(kBlock) void k_sc_send_last(const i64* __restrict__ ts, i64 N, i64 send_size, i64 n_sends,
+                                                        i64* out) {
+    const i64 s = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n_sends) return;
+    const i64 e = send_size > 0 ? min((s + 1) * send_size, N) - 1 : N - 1;
+    out[s] = ts[e];
+}
+
+static inline unsigned sc_grid(i64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
+                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_sc_keys, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, n_old, pcb, nb, pend_pos, pend_gidx, per_event,
+                       send_size, seq0, skey, idx, chunk, send);
+}
+
+void launch_sc_walk(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx,
+                    const i64* chunk, const u64* pend_vals, i64 pend_cap, AggPlan ap, i64 n_old, u32* ghead, u64* sval,
+                    u32* slast) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_sc_walk, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, hd, pos, starts, idx, chunk, pend_vals,
+                       pend_cap, ap, n_old, ghead, sval, slast);
+}
+
+void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32* pre, const u32* slast, const u64* sval,
+                    const u32* pend_pos, const i64* pend_ts, const u64* pend_gidx, const i64* chunk, const i64* send,
+                    KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys, u64* out_vals, i64* out_rep,
+                    i64* out_chunk, i64* out_send) {
+    if (M <= n_old || T <= 0) return;
+    hipLaunchKernelGGL(k_sc_emit, dim3(sc_grid(M - n_old)), dim3(kBlock), 0, s, M, n_old, ghead, pre, slast, sval,
+                       pend_pos, pend_ts, pend_gidx, chunk, send, kt, kp, na, T, out_ts, out_keys, out_vals, out_rep,
+                       out_chunk, out_send);
+}
+
+void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out) {
+    if (n_sends <= 0) return;
+    hipLaunchKernelGGL(k_sc_send_last, dim3(sc_grid(n_sends)), dim3(kBlock), 0, s, ts, N, send_size, n_sends, out);
+}
+
 }  // namespace shd

@@ -96,6 +96,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows carry 2 extra columns: at most 6 stream columns");
     if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
+    if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "sharded stream.current.event windows are not on the GPU");
     if (d->expired_on || !d->current_on || d->n_aggs < 1)
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries emit current events of aggregations (`insert into`)");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
@@ -670,4 +671,38 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
 extern "C" int sh_shard_stats(sh_shard* s, sh_stats* out) {
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_stats: NULL argument");
     return sh_query_stats(s->owner, out);
+}
+
+// ---- checkpoint (sh_snapshot.cpp): the shard's global stream state; the owner query is snapshotted
+// by the query sections. sc = {clock_valid, clock, e0_valid, E0, W, carry, seq, sl_pm, send_base,
+// p0_known, p0, rank, world, sliding}.
+int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query** owner) {
+    if (n != 14) return sh_fail(SH_ERR_INVALID, "shard snapshot layout");
+    *owner = s->owner;
+    if (s->agg) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation: not supported");
+    if (s->packed) return sh_fail(SH_ERR_INVALID, "shard snapshot between pack and consume");
+    if (!set) {
+        const int64_t v[14] = {s->clock_valid, s->clock, s->e0_valid, s->E0, s->W, s->carry, (int64_t)s->seq,
+                               s->sl_pm, s->send_base, s->p0_known, s->owner->p0, s->rank, s->world, s->sliding};
+        for (int i = 0; i < 14; i++) sc[i] = v[i];
+        return SH_OK;
+    }
+    if (sc[11] != s->rank || sc[12] != s->world || (sc[13] != 0) != s->sliding)
+        return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different shard (rank / world / window)");
+    s->clock_valid = sc[0] != 0;
+    s->clock = sc[1];
+    s->e0_valid = sc[2] != 0;
+    s->E0 = sc[3];
+    s->W = sc[4];
+    s->carry = sc[5];
+    s->seq = (uint64_t)sc[6];
+    s->sl_pm = sc[7];
+    s->send_base = sc[8];
+    s->p0_known = sc[9] != 0;
+    s->fp = s->fp_orig;
+    if (s->p0_known) {
+        const int pc = s->d.partition_col;
+        RCHK(partition_filter(s->fp_orig, pc, s->d.col_types[pc], sc[10], &s->fp));
+    }
+    return SH_OK;
 }

@@ -283,3 +283,51 @@ int sliding_restore(sh_query* q, Reader& r) {
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;
 }
+
+// ---- sharded query (sh_shard.cpp): the shard's global stream state + its owner query -------------
+int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query** owner);
+
+extern "C" int sh_shard_snapshot(sh_shard* sd, void* buf, int64_t cap, int64_t* len) {
+    if (!sd || !len) return sh_fail(SH_ERR_INVALID, "sh_shard_snapshot: NULL argument");
+    int64_t sc[14];
+    sh_query* q = nullptr;
+    RCHK(shard_checkpoint_state(sd, sc, 14, false, &q));
+    StreamScope _ss(q->ctx->stream);
+    Writer w;
+    w.put("SHS1", 4);
+    w.val<uint32_t>(kVersion);
+    w.val<uint64_t>(fingerprint(q));
+    w.val<uint32_t>((uint32_t)q->kind);
+    for (int i = 0; i < 14; i++) w.val<int64_t>(sc[i]);
+    RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    *len = (int64_t)w.b.size();
+    if (buf) {
+        if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_shard_snapshot: buffer too small (call with buf=NULL for the size)");
+        std::memcpy(buf, w.b.data(), w.b.size());
+    }
+    return SH_OK;
+}
+
+extern "C" int sh_shard_restore(sh_shard* sd, const void* buf, int64_t len) {
+    if (!sd || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_shard_restore: bad arguments");
+    int64_t cur[14];
+    sh_query* q = nullptr;
+    RCHK(shard_checkpoint_state(sd, cur, 14, false, &q));
+    StreamScope _ss(q->ctx->stream);
+    Reader r{(const uint8_t*)buf, (size_t)len};
+    if (std::memcmp(buf, "SHS1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip shard snapshot");
+    r.o = 4;
+    if (r.val<uint32_t>() != kVersion) return sh_fail(SH_ERR_INVALID, "snapshot version mismatch");
+    if (r.val<uint64_t>() != fingerprint(q)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different query");
+    if (r.val<uint32_t>() != (uint32_t)q->kind) return sh_fail(SH_ERR_INVALID, "snapshot kind mismatch");
+    int64_t sc[14];
+    for (int i = 0; i < 14; i++) sc[i] = r.val<int64_t>();
+    if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    RCHK(shard_checkpoint_state(sd, sc, 14, true, &q));
+    (void)hipStreamSynchronize(q->ctx->stream);
+    // the owner takes its events already filtered by the ingest: keep its own (empty) filter
+    const FilterProg keep = q->fp;
+    const int rc = q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
+    q->fp = keep;
+    return rc;
+}

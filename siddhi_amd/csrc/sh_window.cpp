@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "sh_agg.h"
 #include "sh_internal.h"
 #include "sh_runtime.h"
 
@@ -193,7 +194,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if ((!d->current_on || d->expired_on) && !(batch_win && d->partition_col < 0))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch and timeBatch (not partitioned) windows");
-    if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "stream.current.event batch windows not on the GPU yet");
+    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->current_on && !d->expired_on && d->n_aggs >= 1))
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "stream.current.event runs on aggregating, non-partitioned lengthBatch/timeBatch with current "
+                       "events output");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
@@ -548,6 +552,152 @@ int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend) {
     return grow_pending(q, n_pend, 0);
 }
 
+// stream.current.event batch windows (LengthBatchWindowProcessor.processStreamCurrentEvents :245-274,
+// TimeBatchWindowProcessor RESET mode :262-340): the pending entries [0, n_old) are the open window's
+// earlier events, [n_old, M) this push's passing events (sh_kernels.hip k_sc_*). One flush per chunk:
+// every passing event for lengthBatch (:160-182 sends each event's chunk on its own), every send with
+// passing events for timeBatch; the flush clock is the send's playback clock.
+static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bounds, int64_t n_old, int64_t M,
+                   bool cv0, int64_t clock0, int64_t seq0, bool host_out) {
+    hipStream_t s = q->ctx->stream;
+    const int nk = q->kp.n, na = q->ap.n;
+    const int nb = (int)bounds.size();
+    const bool per_event = q->d.window == SH_WIN_LENGTH_BATCH;
+    const int64_t N = b->n, ss = b->send_size;
+    const int64_t n_sends = ss > 0 ? (N + ss - 1) / ss : 1;
+    RCHK(q->sc_h.reserve((size_t)std::max(nb, 1) * 8 + 64));
+    for (int i = 0; i < nb; i++) q->sc_h.as<int64_t>()[i] = bounds[i].pcb;
+    RCHK(q->sc_pcb.reserve((size_t)std::max(nb, 1) * 8, false));
+    if (nb) HIPCHK(hipMemcpyAsync(q->sc_pcb.p, q->sc_h.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
+    RCHK(q->sc_skey.reserve((size_t)M * 8, false));
+    RCHK(q->sc_skey2.reserve((size_t)M * 8, false));
+    RCHK(q->sc_idx.reserve((size_t)M * 4, false));
+    RCHK(q->sc_idx2.reserve((size_t)M * 4, false));
+    RCHK(q->sc_chunk.reserve((size_t)M * 8, false));
+    RCHK(q->sc_send.reserve((size_t)M * 8, false));
+    RCHK(q->sc_hd.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_pos.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_starts.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_ghead.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_pre.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_slast.reserve((size_t)M * 4, false));
+    RCHK(q->sc_sval.reserve((size_t)std::max(na, 1) * M * 8, false));
+    RCHK(q->sc_tmp.reserve((size_t)((M + 1 + kTile - 1) / kTile + 16) * 8, false));
+    RCHK(q->sc_sl.reserve((size_t)n_sends * 8, false));
+    launch_sc_keys(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(),
+                   per_event ? 1 : 0, ss, seq0, q->sc_skey.as<u64>(), q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(),
+                   q->sc_send.as<int64_t>());
+    size_t tb = 0;
+    if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, M, s))
+        return sh_fail(SH_ERR_DEVICE, "stream.current: sort sizing");
+    RCHK(q->sc_sort.reserve(std::max<size_t>(tb, 16), false));
+    if (sort_u64_pairs(q->sc_sort.p, &tb, q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(), q->sc_idx.as<u32>(),
+                       q->sc_idx2.as<u32>(), M, s))
+        return sh_fail(SH_ERR_DEVICE, "stream.current: sort failed");
+    launch_rate_segments(s, M, q->sc_skey2.as<u64>(), q->sc_idx2.as<u32>(), 1, 0, q->sc_hd.as<u32>(),
+                         q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_tmp.as<int64_t>());
+    HIPCHK(hipMemsetAsync(q->sc_ghead.p, 0, (size_t)(M + 1) * 4, s));
+    HIPCHK(hipEventRecord(q->ev_agg0, s));
+    launch_sc_walk(s, M, q->sc_hd.as<u32>(), q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_idx2.as<u32>(),
+                   q->sc_chunk.as<int64_t>(), q->pend_vals.as<u64>(), q->pend_cap, q->ap, n_old, q->sc_ghead.as<u32>(),
+                   q->sc_sval.as<u64>(), q->sc_slast.as<u32>());
+    HIPCHK(hipEventRecord(q->ev_agg1, s));
+    const int64_t nn = M - n_old;
+    HIPCHK(hipMemcpyAsync(q->sc_pre.p, q->sc_ghead.as<uint32_t>() + n_old, (size_t)(nn + 1) * 4, hipMemcpyDeviceToDevice, s));
+    launch_scan_sum_large_u32(s, q->sc_pre.as<u32>(), nn + 1, q->sc_tmp.as<int64_t>());
+    launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    RCHK(q->sc_h.reserve((size_t)n_sends * 8 + 64));
+    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_pre.as<uint32_t>() + nn, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t T = *q->sc_h.as<uint32_t>();
+    const int64_t TC = std::max<int64_t>(T, 1);
+    RCHK(q->out_ts.reserve(TC * 8, false));
+    RCHK(q->out_keys.reserve((size_t)std::max(1, nk) * TC * 8, false));
+    RCHK(q->out_vals.reserve((size_t)std::max(1, na) * TC * 8, false));
+    RCHK(q->out_nulls.reserve((size_t)std::max(1, na) * TC, false));
+    RCHK(q->out_expired.reserve(TC, false));
+    RCHK(q->out_rep.reserve(TC * 8, false));
+    RCHK(q->sc_ochunk.reserve(TC * 8, false));
+    RCHK(q->sc_osend.reserve(TC * 8, false));
+    HIPCHK(hipMemsetAsync(q->out_nulls.p, 0, q->out_nulls.cap, s));
+    HIPCHK(hipMemsetAsync(q->out_expired.p, 0, q->out_expired.cap, s));
+    q->zeroed_nulls = q->out_nulls.p;
+    q->zeroed_expired = q->out_expired.p;
+    launch_sc_emit(s, M, n_old, q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(), q->sc_sval.as<u64>(),
+                   q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(), q->sc_chunk.as<int64_t>(),
+                   q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T, q->out_ts.as<int64_t>(),
+                   q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->out_rep.as<int64_t>(),
+                   q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    // the sends' playback clocks (TimestampGeneratorImpl only moves forward) and every row's chunk
+    std::vector<int64_t> sl(n_sends), och(T), osd(T);
+    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::memcpy(sl.data(), q->sc_h.p, (size_t)n_sends * 8);
+    if (T) {
+        HIPCHK(hipMemcpy(och.data(), q->sc_ochunk.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(osd.data(), q->sc_osend.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+    }
+    bool cv = cv0;
+    int64_t c = clock0;
+    for (int64_t i = 0; i < n_sends; i++) {
+        c = cv ? std::max(c, sl[i]) : sl[i];
+        cv = true;
+        sl[i] = c;
+    }
+    PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
+    PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
+    fo.assign(1, 0);
+    fc.clear();
+    for (int64_t i = 0; i < T; i++) {
+        if (i + 1 == T || och[i + 1] != och[i]) {
+            fo.push_back(i + 1);
+            fc.push_back(sl[osd[i]]);
+        }
+    }
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_agg0, q->ev_agg1);
+    q->stats.main_kernel_ms += ms;
+    if (host_out) {
+        OutHost& o = q->out;
+        o.ts.resize(T);
+        o.expired.assign(T, 0);
+        o.rep.resize(T);
+        o.keys.resize((size_t)nk * T);
+        o.vals.resize((size_t)na * T);
+        o.nulls.assign((size_t)na * T, 0);
+        if (T) {
+            HIPCHK(hipMemcpyAsync(o.ts.data(), q->out_ts.p, T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(o.rep.data(), q->out_rep.p, T * 8, hipMemcpyDeviceToHost, s));
+            if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), q->out_keys.p, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
+            if (na) HIPCHK(hipMemcpyAsync(o.vals.data(), q->out_vals.p, (size_t)na * T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    } else {
+        q->dev_out.n_rows = T;
+    }
+    return SH_OK;
+}
+
+// entries [lo, lo + n) of the pending buffer moved to its front
+static int pending_to_front(sh_query* q, int64_t lo, int64_t n) {
+    if (lo == 0 || n == 0) return SH_OK;
+    hipStream_t s = q->ctx->stream;
+    DevBuf t;
+    RCHK(t.reserve((size_t)n * 8, false));
+    auto move = [&](void* base, size_t elem) -> int {
+        HIPCHK(hipMemcpyAsync(t.p, (char*)base + (size_t)lo * elem, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(base, t.p, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
+        return SH_OK;
+    };
+    RCHK(move(q->pend_pos.p, 4));
+    RCHK(move(q->pend_ts.p, 8));
+    RCHK(move(q->pend_gidx.p, 8));
+    for (int j = 0; j < q->ap.n_vcols; j++) RCHK(move(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, 8));
+    return SH_OK;
+}
+
 static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh_out** out) {
     SH_TMARK(0);
     // expired / all-events output: the current rows stay on the device for xout_finish
@@ -565,6 +715,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
     q->ms_ready = false;
     q->tail.active = false;
     int64_t N = b->n;
+    const bool cv0 = q->clock_valid;
+    const int64_t clock0 = q->clock, seq0 = q->seq;
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
     if (q->n_pend + N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
@@ -629,7 +781,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         RCHK(q->new_pos.reserve((size_t)N * 4, false));
         // large pushes split the whole push into key partitions right behind k_boundaries, which
         // counts the push's tiles for it (a small push usually closes no window: no split then)
-        const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18);
+        const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18) && !q->d.stream_current;
         const TileMap ms_map = make_tile_map(q->n_pend, q->n_pend + N);
         if (early_split) RCHK(reserve_ms_counts(q, ms_map));
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
@@ -719,7 +871,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
                 clocks.push_back(lb_full ? q->clock : given_flush_clock(q, wprev));
                 windows.push_back(wprev);
             }
-            RCHK(run_closed(q, segs, clocks, windows, b, host_out));
+            if (!q->d.stream_current) RCHK(run_closed(q, segs, clocks, windows, b, host_out));
             if (close_all) {
                 e_lo = N;
                 pcb_lo = info.total_pass;
@@ -740,12 +892,25 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             dst_base = q->n_pend;
             new_pend = q->n_pend + info.total_pass;
         }
-        RCHK(grow_pending(q, new_pend, dst_base));
-        launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
-                               q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
-                               q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
-                               q->pend_gidx.as<u64>(), q->seq);
-        HIPCHK(hipGetLastError());
+        if (q->d.stream_current) {
+            // every passing event is emitted now: all of them join the pending entries, the rows come
+            // from the open window's earlier events + these; the last window's entries stay queued
+            const int64_t n_old = q->n_pend, M = n_old + info.total_pass;
+            RCHK(grow_pending(q, M, n_old));
+            launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, 0, N, 0, n_old,
+                                   q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
+                                   q->pend_vals.as<u64>(), q->pend_cap, nullptr, q->pend_gidx.as<u64>(), q->seq);
+            HIPCHK(hipGetLastError());
+            if (M > n_old) RCHK(sc_rows(q, b, bounds, n_old, M, cv0, clock0, seq0, host_out));
+            RCHK(pending_to_front(q, M - new_pend, new_pend));
+        } else {
+            RCHK(grow_pending(q, new_pend, dst_base));
+            launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
+                                   q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
+                                   q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
+                                   q->pend_gidx.as<u64>(), q->seq);
+            HIPCHK(hipGetLastError());
+        }
         q->n_pend = new_pend;
     }
     q->seq += N;
@@ -852,7 +1017,9 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
     if (q->d.window == SH_WIN_TIME_BATCH && q->e0_valid) {
         int64_t W = wfun_host(q, now);
         if (q->xmode && W > q->W_open) q->x_closes.emplace_back(W, now);
-        if (W > q->W_open && q->n_pend > 0) {
+        if (W > q->W_open && q->n_pend > 0 && q->d.stream_current) {
+            q->n_pend = 0;  // RESET: the events were emitted as they arrived
+        } else if (W > q->W_open && q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{now}, windows{q->W_open};
             RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));

@@ -96,6 +96,17 @@ class ShardedQuery:
         _check(lib().sh_shard_stats(self.h, C.byref(st)))
         return st
 
+    def snapshot(self) -> bytes:
+        """This rank's checkpoint (sh_shard_snapshot), taken between pushes."""
+        n = C.c_int64()
+        _check(lib().sh_shard_snapshot(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().sh_shard_snapshot(self.h, buf, n.value, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def restore(self, blob: bytes):
+        _check(lib().sh_shard_restore(self.h, blob, len(blob)))
+
     def close(self):
         if self.h:
             lib().sh_shard_destroy(self.h)
@@ -295,6 +306,15 @@ class LocalShards:
                 s.advance_time(now, False)
             return [None] * self.world
         return [host_rows(*s.advance_time(now, True)) for s in self.shards]
+
+    def snapshot(self) -> List[bytes]:
+        return [s.snapshot() for s in self.shards]
+
+    def restore(self, blobs: List[bytes], seq: int):
+        """Continue from snapshot() blobs; seq = global stream index of the next event."""
+        for s, b in zip(self.shards, blobs):
+            s.restore(b)
+        self.seq = seq
 
     def tables(self, duration: int) -> dict:
         """The merged (canonical-order) table of one duration over all owners."""

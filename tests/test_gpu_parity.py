@@ -32,8 +32,10 @@ def both(rt, spec, pushes, rtol=None, label=""):
 # current, expired or all-events output; aggregating sliding time windows with current events ----
 def _gpu_runs(c):
     q = c.get("query", {})
-    if c.get("kind") == "aggregation" or q.get("stream_current"):
+    if c.get("kind") == "aggregation":
         return False
+    if q.get("stream_current"):
+        return bool(q.get("aggs")) and q.get("output", "current") == "current" and not q.get("partition")
     if q.get("window") in ("lengthBatch", "timeBatch"):
         return bool(q.get("aggs")) or not q.get("group_by")
     return q.get("window") == "time" and bool(q.get("aggs")) and q.get("output", "current") == "current"

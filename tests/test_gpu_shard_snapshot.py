@@ -1,0 +1,88 @@
+"""Checkpoint of a sharded query (sh_shard_snapshot / sh_shard_restore, SnapshotService.persist/restore):
+G shards snapshotted between two global pushes and restored into fresh shards (new device state) must
+continue exactly like the single-stream oracle does over the whole stream."""
+import numpy as np
+import pytest
+
+from siddhi_amd import abi
+from tests.parity import assert_same
+from tests.test_gpu_shard import SCHEMA, run_oracle, spec, stream_pushes
+
+pytestmark = pytest.mark.gpu
+
+
+def run_sharded_restored(sp, world, pushes, send_size, cut_at, advance=None):
+    import torch
+    from siddhi_amd.shard import LocalShards, merge_owner_outputs
+    dev = torch.device("cuda", 0)
+    ls = LocalShards(sp, world)
+    parts = []
+    for pi, (ts, cols) in enumerate(pushes):
+        if pi == cut_at:  # checkpoint, drop every shard, continue on restored ones
+            blobs, seq = ls.snapshot(), ls.seq
+            ls.close()
+            ls = LocalShards(sp, world)
+            ls.restore(blobs, seq)
+        n = len(ts)
+        units = (n + send_size - 1) // send_size
+        edges = [0] + sorted(min(n, int(units * (g + 1) / world) * send_size) for g in range(world - 1)) + [n]
+        slices = [(torch.from_numpy(np.ascontiguousarray(ts[edges[g]:edges[g + 1]])).to(dev),
+                   [torch.from_numpy(np.ascontiguousarray(c[edges[g]:edges[g + 1]])).to(dev) for c in cols])
+                  for g in range(world)]
+        outs = ls.push(slices, send_size, dev)
+        parts.append(merge_owner_outputs(outs, ls.last_bounds, ls.last_sends if sp.window == "time" else None))
+    if advance is not None:
+        parts.append(merge_owner_outputs(ls.advance_time(advance)))
+    ls.close()
+    return abi.concat_arrays(parts)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("cut_at", [1, 2])
+def test_sharded_timebatch_checkpoint(world, cut_at):
+    sp = spec(5_000)
+    pushes = stream_pushes(300_000, [90_000, 60_001, 149_999], 0xC2, 5_000, 100)
+    adv = int(pushes[-1][0][-1]) + 5000
+    got = run_sharded_restored(sp, world, pushes, 1, cut_at, advance=adv)
+    assert_same(got, run_oracle(sp, pushes, 1, advance=adv), label=f"timeBatch x{world} cut {cut_at}")
+
+
+def test_sharded_lengthbatch_checkpoint():
+    sp = abi.QuerySpec(SCHEMA, "lengthBatch", 777, group_by=["k"], aggs=[("sum", "v"), ("count", None)],
+                       key_capacity=2_000)
+    pushes = stream_pushes(120_000, [50_000, 3_333, 66_667], 7, 2_000, 50)
+    got = run_sharded_restored(sp, 2, pushes, 3, 1)
+    assert_same(got, run_oracle(sp, pushes, 3), label="lengthBatch x2")
+
+
+def test_sharded_sliding_checkpoint():
+    sp = abi.QuerySpec(SCHEMA, "time", 400, group_by=["k"], aggs=[("sum", "v"), ("max", "v")], key_capacity=1_000)
+    pushes = stream_pushes(60_000, [20_000, 20_000, 20_000], 11, 1_000, 20)
+    got = run_sharded_restored(sp, 2, pushes, 1, 2)
+    assert_same(got, run_oracle(sp, pushes, 1), label="time x2")
+
+
+def test_sharded_partitioned_checkpoint():
+    sch = abi.Schema.parse("k int, p int, v double, ts long")
+    sp = abi.QuerySpec(sch, "timeBatch", 500, group_by=["k"], aggs=[("count", None), ("avg", "v")], partition="p",
+                       key_capacity=1_000)
+    rng = np.random.default_rng(5)
+    n = 80_000
+    ts = (np.arange(n) // 30 + 10_000).astype(np.int64)
+    cols = [rng.integers(0, 500, n).astype(np.int32), rng.integers(0, 4, n).astype(np.int32),
+            rng.integers(-999, 999, n).astype(np.float64) / 8, ts.copy()]
+    pushes = [(ts[a:b], [c[a:b] for c in cols]) for a, b in ((0, 30_000), (30_000, 50_000), (50_000, n))]
+    adv = int(ts[-1]) + 2_000
+    got = run_sharded_restored(sp, 2, pushes, 1, 1, advance=adv)
+    assert_same(got, run_oracle(sp, pushes, 1, advance=adv), label="partitioned x2")
+
+
+def test_sharded_snapshot_rejects_other_rank():
+    from siddhi_amd.runtime import SiddhiError
+    from siddhi_amd.shard import ShardedQuery
+    sp = spec(100)
+    a, b = ShardedQuery(sp, 0, 2), ShardedQuery(sp, 1, 2)
+    with pytest.raises(SiddhiError, match="different shard"):
+        b.restore(a.snapshot())
+    a.close()
+    b.close()

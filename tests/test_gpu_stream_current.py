@@ -1,0 +1,70 @@
+"""GPU parity of `#window.lengthBatch(L, true)` / `#window.timeBatch(T, true)` (stream.current.event, current
+events output): every arriving event is emitted at once with its key's running aggregates since the last
+batch reset (LengthBatchWindowProcessor.processStreamCurrentEvents :245-274, TimeBatchWindowProcessor RESET
+mode :262-340, QuerySelector :315-374 grouping each chunk). The reference KAT lengthBatch11 runs in
+test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+from siddhi_amd import abi
+from tests.parity import split_batches
+from tests.test_gpu_parity import both
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = abi.Schema.parse("k int, v double, x long, ts long")
+AGGS = [("count", None), ("sum", "v"), ("min", "v"), ("max", "x"), ("avg", "x"), ("sum", "x")]
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def stream(n, keys, seed, step=40, gap_at=None):
+    rng = np.random.default_rng(seed)
+    ts = np.cumsum(rng.integers(0, step, n)).astype(np.int64) + 5_000
+    if gap_at is not None:
+        ts[gap_at:] += 20_000
+    k = rng.integers(0, keys, n).astype(np.int32)
+    v = rng.integers(-4000, 4000, n).astype(np.float64) / 16.0
+    x = rng.integers(-10**6, 10**6, n).astype(np.int64)
+    return ts, [k, v, x, ts.copy()]
+
+
+@pytest.mark.parametrize("L,cuts,send_size", [(100, [1, 777, 5_000], 3), (7, [3, 4_000], 1), (1, [10], 5),
+                                              (5_000, [2_500, 12_000], 0)])
+@pytest.mark.parametrize("group_by", [True, False])
+def test_lengthbatch_stream_current(rt, L, cuts, send_size, group_by):
+    ts, cols = stream(15_000, 60, 3)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["k"] if group_by else (), aggs=AGGS,
+                         filter=(">", "v", -180.0), stream_current=True, key_capacity=64)
+    out = both(rt, spec, split_batches(SCHEMA, ts, cols, cuts, send_size), label=f"lengthBatch({L}, true)")
+    assert out["ts"].size > 0
+
+
+@pytest.mark.parametrize("send_size", [1, 13, 0])
+@pytest.mark.parametrize("group_by", [True, False])
+def test_timebatch_stream_current(rt, send_size, group_by):
+    ts, cols = stream(30_000, 300, 7, gap_at=17_000)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 700, group_by=["k"] if group_by else (), aggs=AGGS,
+                         filter=(">", "v", -150.0), stream_current=True, key_capacity=512)
+    pushes = split_batches(SCHEMA, ts, cols, [1, 2_000, 16_999, 17_000, 25_000], send_size)
+    pushes.insert(3, ("advance", int(ts[16_999]) + 1_500))
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    out = both(rt, spec, pushes, label=f"timeBatch stream current send {send_size}")
+    assert out["flush_offsets"].size > (10 if send_size else 4)
+
+
+def test_timebatch_stream_current_start_time(rt):
+    ts, cols = stream(8_000, 20, 9)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 333, group_by=["k"], aggs=[("sum", "v"), ("count", None)],
+                         start_time=100, stream_current=True, key_capacity=32)
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [4_000], 2), label="timeBatch start")
+
+
+def test_stream_current_rejects_expired(rt):
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 4, aggs=[("count", None)], stream_current=True, output="expired")
+    with pytest.raises(rt.SiddhiError, match="stream.current"):
+        rt.GpuQuery(spec)
