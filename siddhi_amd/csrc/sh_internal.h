@@ -339,5 +339,14 @@ void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32
                     KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys, u64* out_vals, i64* out_rep,
                     i64* out_chunk, i64* out_send);
 void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out);
+void launch_scx_first(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx, u32* fe,
+                      u32* fpre, u32* lastidx);
+void launch_scx_count(hipStream_t s, i64 M, i64 n_old, const i64* pcb, const u64* skey, const u64* skey2,
+                      const u32* idx2, const u32* fpre, int cur_on, int exp_on, u32* rows, i64* rank_e);
+void launch_scx_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fe,
+                     const u32* fpre, const u32* lastidx, const u32* base, const i64* rank_e, const u64* sval,
+                     const i64* send, const i64* send_clock, const i64* pend_ts, const u64* pend_gidx, KeyTable kt,
+                     KeyPlan kp, AggPlan ap, int cur_on, int exp_on, i64 T, i64* out_ts, i64* out_keys, u64* out_vals,
+                     unsigned char* out_nulls, unsigned char* out_exp, i64* out_rep, i64* out_chunk, i64* out_send);
 
 }  // namespace shd

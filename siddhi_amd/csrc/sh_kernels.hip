@@ -1625,4 +1625,155 @@ void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64
     hipLaunchKernelGGL(k_sc_send_last, dim3(sc_grid(n_sends)), dim3(kBlock), 0, s, ts, N, send_size, n_sends, out);
 }
 
+
+// ---- lengthBatch(L, true) with expired / all-events output: the event that starts batch w + 1 (the
+// reference's count == length + 1, :249-266) carries batch w's events as EXPIRED before the RESET; the
+// selector groups that chunk by key, so batch w's keys show their empty state (count 0, the others
+// null) at their first-occurrence position, each with ts = the chunk's clock and the representative
+// event of the key's last event in w; with `all events` the new event's own row replaces its key's
+// expired row (LinkedHashMap.put) or follows them.
+__device__ __forceinline__ i64 sc_wstart(i64 w, i64 n_old, const i64* pcb) { return w == 0 ? 0 : n_old + pcb[w - 1]; }
+
+// fe[m] = 1 at the first entry (stream order) of every (window, key) run; lastidx[first] = its last entry
+__global__ __launch_bounds__(kBlock) void k_scx_first(i64 M, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                     const u32* __restrict__ starts, const u32* __restrict__ idx,
+                                                     u32* fe, u32* fpre, u32* lastidx) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > M) return;
+    if (i == M) { fpre[M] = 0; return; }
+    u32 f = 0;
+    if (hd[i]) {
+        const u32 m = idx[i];
+        fe[m] = 1;
+        lastidx[m] = idx[starts[pos[i] + 1] - 1];
+    }
+    (void)f;
+}
+
+// rows of every new entry's chunk and, at batch starts, the new event's key rank in the closing batch
+__global__ __launch_bounds__(kBlock) void k_scx_count(i64 M, i64 n_old, const i64* __restrict__ pcb,
+                                                     const u64* __restrict__ skey, const u64* __restrict__ skey2,
+                                                     const u32* __restrict__ idx2, const u32* __restrict__ fpre,
+                                                     int cur_on, int exp_on, u32* rows, i64* rank_e) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 m = n_old + j;
+    if (m > M) return;
+    if (m == M) { rows[j] = 0; return; }
+    const u64 key = skey[m];
+    const i64 w = (i64)(key >> 32);
+    i64 re = -1;
+    u32 r = cur_on ? 1u : 0u;
+    if (w >= 1 && m == sc_wstart(w, n_old, pcb)) {
+        const i64 ws0 = sc_wstart(w - 1, n_old, pcb);
+        const i64 nprev = (i64)fpre[m] - (i64)fpre[ws0];
+        // the new event's key among batch w - 1's keys: lower bound of (w - 1, slot) in the sorted keys
+        const u64 want = ((u64)(w - 1) << 32) | (key & 0xFFFFFFFFull);
+        i64 lo = 0, hi = M;
+        while (lo < hi) {
+            const i64 mid = (lo + hi) >> 1;
+            if (skey2[mid] < want) lo = mid + 1; else hi = mid;
+        }
+        if (lo < M && skey2[lo] == want) re = (i64)fpre[idx2[lo]] - (i64)fpre[ws0];
+        if (exp_on) r = (u32)nprev + ((cur_on && re < 0) ? 1u : 0u);
+    }
+    rows[j] = r;
+    rank_e[j] = re;
+}
+
+// the expired rows: one per (batch, key) run whose batch closes in this push
+__global__ __launch_bounds__(kBlock) void k_scx_expired(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
+                                                       const u64* __restrict__ skey, const u32* __restrict__ fe,
+                                                       const u32* __restrict__ fpre, const u32* __restrict__ lastidx,
+                                                       const u32* __restrict__ base, const i64* __restrict__ rank_e,
+                                                       const i64* __restrict__ send, const i64* __restrict__ send_clock,
+                                                       const u64* __restrict__ pend_gidx, KeyTable kt, KeyPlan kp,
+                                                       AggPlan ap, int cur_on, i64 T, i64* out_ts, i64* out_keys,
+                                                       u64* out_vals, unsigned char* out_nulls, unsigned char* out_exp,
+                                                       i64* out_rep, i64* out_chunk, i64* out_send) {
+    const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M || !fe[m]) return;
+    const u64 key = skey[m];
+    const i64 w = (i64)(key >> 32);
+    if (w >= nb) return;  // batch w has not closed yet
+    const i64 mb = n_old + pcb[w];  // the event starting batch w + 1
+    const i64 jb = mb - n_old;
+    const i64 rank = (i64)fpre[m] - (i64)fpre[sc_wstart(w, n_old, pcb)];
+    if (cur_on && rank == rank_e[jb]) return;  // the new event's current row takes this position
+    const i64 o = base[jb] + rank;
+    out_ts[o] = send_clock[send[mb]];
+    out_rep[o] = (i64)pend_gidx[lastidx[m]];
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
+    for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
+    for (int a = 0; a < ap.n; a++) {
+        out_vals[(size_t)a * T + o] = 0;
+        out_nulls[(size_t)a * T + o] = ap.kind[a] == AK_COUNT ? 0 : 1;
+    }
+    out_exp[o] = 1;
+    out_chunk[o] = jb;
+    out_send[o] = send[mb];
+}
+
+// the current rows (per-event chunks): at a batch start after the batch's expired rows, or in place
+// of the key's expired row
+__global__ __launch_bounds__(kBlock) void k_scx_current(i64 M, i64 n_old, const i64* __restrict__ pcb,
+                                                       const u64* __restrict__ skey, const u32* __restrict__ fpre,
+                                                       const u32* __restrict__ base, const i64* __restrict__ rank_e,
+                                                       const u64* __restrict__ sval, const i64* __restrict__ send,
+                                                       const i64* __restrict__ pend_ts, const u64* __restrict__ pend_gidx,
+                                                       KeyTable kt, KeyPlan kp, int na, int exp_on, i64 T, i64* out_ts,
+                                                       i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                                                       unsigned char* out_exp, i64* out_rep, i64* out_chunk,
+                                                       i64* out_send) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 m = n_old + j;
+    if (m >= M) return;
+    const u64 key = skey[m];
+    const i64 w = (i64)(key >> 32);
+    i64 o = base[j];
+    if (exp_on && w >= 1 && m == sc_wstart(w, n_old, pcb)) {
+        const i64 nprev = (i64)fpre[m] - (i64)fpre[sc_wstart(w - 1, n_old, pcb)];
+        o += rank_e[j] >= 0 ? rank_e[j] : nprev;
+    }
+    out_ts[o] = pend_ts[m];
+    out_rep[o] = (i64)pend_gidx[m];
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
+    for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
+    for (int a = 0; a < na; a++) {
+        out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+        out_nulls[(size_t)a * T + o] = 0;
+    }
+    out_exp[o] = 0;
+    out_chunk[o] = j;
+    out_send[o] = send[m];
+}
+
+void launch_scx_first(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx, u32* fe,
+                      u32* fpre, u32* lastidx) {
+    hipLaunchKernelGGL(k_scx_first, dim3(sc_grid(M + 1)), dim3(kBlock), 0, s, M, hd, pos, starts, idx, fe, fpre,
+                       lastidx);
+}
+
+void launch_scx_count(hipStream_t s, i64 M, i64 n_old, const i64* pcb, const u64* skey, const u64* skey2,
+                      const u32* idx2, const u32* fpre, int cur_on, int exp_on, u32* rows, i64* rank_e) {
+    hipLaunchKernelGGL(k_scx_count, dim3(sc_grid(M - n_old + 1)), dim3(kBlock), 0, s, M, n_old, pcb, skey, skey2, idx2,
+                       fpre, cur_on, exp_on, rows, rank_e);
+}
+
+void launch_scx_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fe,
+                     const u32* fpre, const u32* lastidx, const u32* base, const i64* rank_e, const u64* sval,
+                     const i64* send, const i64* send_clock, const i64* pend_ts, const u64* pend_gidx, KeyTable kt,
+                     KeyPlan kp, AggPlan ap, int cur_on, int exp_on, i64 T, i64* out_ts, i64* out_keys, u64* out_vals,
+                     unsigned char* out_nulls, unsigned char* out_exp, i64* out_rep, i64* out_chunk, i64* out_send) {
+    if (T <= 0) return;
+    if (exp_on)
+        hipLaunchKernelGGL(k_scx_expired, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, n_old, pcb, nb, skey, fe, fpre,
+                           lastidx, base, rank_e, send, send_clock, pend_gidx, kt, kp, ap, cur_on, T, out_ts, out_keys,
+                           out_vals, out_nulls, out_exp, out_rep, out_chunk, out_send);
+    if (cur_on && M > n_old)
+        hipLaunchKernelGGL(k_scx_current, dim3(sc_grid(M - n_old)), dim3(kBlock), 0, s, M, n_old, pcb, skey, fpre, base,
+                           rank_e, sval, send, pend_ts, pend_gidx, kt, kp, ap.n, exp_on, T, out_ts, out_keys, out_vals,
+                           out_nulls, out_exp, out_rep, out_chunk, out_send);
+}
 }  // namespace shd

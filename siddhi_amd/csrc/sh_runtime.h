@@ -285,8 +285,9 @@ struct sh_query {
     std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call
     // stream.current.event batch windows (sh_window.cpp sc_rows): scratch of a push
     DevBuf sc_pcb, sc_skey, sc_skey2, sc_idx, sc_idx2, sc_chunk, sc_send, sc_hd, sc_pos, sc_starts, sc_tmp, sc_ghead,
-        sc_pre, sc_sval, sc_slast, sc_ochunk, sc_osend, sc_sl, sc_sort;
-    PinnedBuf sc_h;
+        sc_pre, sc_sval, sc_slast, sc_ochunk, sc_osend, sc_sl, sc_sort, scx_fe, scx_fpre, scx_last, scx_rows, scx_rank,
+        scx_clk;
+    PinnedBuf sc_h, sc_hp, sc_ho, h_small_sc;
     // `output [all|first|last] every N events` (sh_rate.cpp): the limiter's state across calls
     struct Rate {
         int kind = SH_RATE_NONE;

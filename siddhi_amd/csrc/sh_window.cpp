@@ -194,10 +194,11 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if ((!d->current_on || d->expired_on) && !(batch_win && d->partition_col < 0))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch and timeBatch (not partitioned) windows");
-    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->current_on && !d->expired_on && d->n_aggs >= 1))
+    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1 &&
+                               (d->window == SH_WIN_LENGTH_BATCH || (d->current_on && !d->expired_on))))
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "stream.current.event runs on aggregating, non-partitioned lengthBatch/timeBatch with current "
-                       "events output");
+                       "stream.current.event runs on aggregating, non-partitioned lengthBatch (any output) or timeBatch "
+                       "(current events) windows");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
@@ -227,7 +228,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0;
-    q->xmode = d->expired_on != 0;
+    q->xmode = d->expired_on != 0 && !d->stream_current;
     if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) {
         q->kind = 1;
         if ((rc = sliding_create(q))) { delete q; return rc; }
@@ -565,10 +566,10 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     const bool per_event = q->d.window == SH_WIN_LENGTH_BATCH;
     const int64_t N = b->n, ss = b->send_size;
     const int64_t n_sends = ss > 0 ? (N + ss - 1) / ss : 1;
-    RCHK(q->sc_h.reserve((size_t)std::max(nb, 1) * 8 + 64));
-    for (int i = 0; i < nb; i++) q->sc_h.as<int64_t>()[i] = bounds[i].pcb;
+    RCHK(q->sc_hp.reserve((size_t)std::max(nb, 1) * 8 + 64));
+    for (int i = 0; i < nb; i++) q->sc_hp.as<int64_t>()[i] = bounds[i].pcb;
     RCHK(q->sc_pcb.reserve((size_t)std::max(nb, 1) * 8, false));
-    if (nb) HIPCHK(hipMemcpyAsync(q->sc_pcb.p, q->sc_h.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
+    if (nb) HIPCHK(hipMemcpyAsync(q->sc_pcb.p, q->sc_hp.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
     RCHK(q->sc_skey.reserve((size_t)M * 8, false));
     RCHK(q->sc_skey2.reserve((size_t)M * 8, false));
     RCHK(q->sc_idx.reserve((size_t)M * 4, false));
@@ -603,14 +604,59 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                    q->sc_sval.as<u64>(), q->sc_slast.as<u32>());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     const int64_t nn = M - n_old;
-    HIPCHK(hipMemcpyAsync(q->sc_pre.p, q->sc_ghead.as<uint32_t>() + n_old, (size_t)(nn + 1) * 4, hipMemcpyDeviceToDevice, s));
-    launch_scan_sum_large_u32(s, q->sc_pre.as<u32>(), nn + 1, q->sc_tmp.as<int64_t>());
+    // the sends' playback clocks: TimestampGeneratorImpl only moves forward (prefix max of send-last ts)
     launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
     HIPCHK(hipGetLastError());
     RCHK(q->sc_h.reserve((size_t)n_sends * 8 + 64));
-    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_pre.as<uint32_t>() + nn, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    const int64_t T = *q->sc_h.as<uint32_t>();
+    std::vector<int64_t> sl(n_sends);
+    {
+        const int64_t* hs = q->sc_h.as<int64_t>();
+        bool cv = cv0;
+        int64_t c = clock0;
+        for (int64_t i = 0; i < n_sends; i++) {
+            c = cv ? std::max(c, hs[i]) : hs[i];
+            cv = true;
+            sl[i] = c;
+        }
+    }
+    const bool xs = q->d.expired_on && per_event;  // lengthBatch(L, true) with expired / all events
+    const int cur_on = q->d.current_on ? 1 : 0;
+    int64_t T = 0;
+    if (xs) {
+        RCHK(q->scx_fe.reserve((size_t)(M + 1) * 4, false));
+        RCHK(q->scx_fpre.reserve((size_t)(M + 1) * 4, false));
+        RCHK(q->scx_last.reserve((size_t)M * 4, false));
+        RCHK(q->scx_rows.reserve((size_t)(nn + 1) * 4, false));
+        RCHK(q->scx_rank.reserve((size_t)std::max<int64_t>(nn, 1) * 8, false));
+        RCHK(q->scx_clk.reserve((size_t)n_sends * 8, false));
+        HIPCHK(hipMemsetAsync(q->scx_fe.p, 0, (size_t)(M + 1) * 4, s));
+        launch_scx_first(s, M, q->sc_hd.as<u32>(), q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_idx2.as<u32>(),
+                         q->scx_fe.as<u32>(), q->scx_fpre.as<u32>(), q->scx_last.as<u32>());
+        HIPCHK(hipMemcpyAsync(q->scx_fpre.p, q->scx_fe.p, (size_t)(M + 1) * 4, hipMemcpyDeviceToDevice, s));
+        launch_scan_sum_large_u32(s, q->scx_fpre.as<u32>(), M + 1, q->sc_tmp.as<int64_t>());
+        launch_scx_count(s, M, n_old, q->sc_pcb.as<int64_t>(), q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(),
+                         q->sc_idx2.as<u32>(), q->scx_fpre.as<u32>(), cur_on, 1, q->scx_rows.as<u32>(),
+                         q->scx_rank.as<int64_t>());
+        launch_scan_sum_large_u32(s, q->scx_rows.as<u32>(), nn + 1, q->sc_tmp.as<int64_t>());
+        std::memcpy(q->sc_h.p, sl.data(), (size_t)n_sends * 8);
+        HIPCHK(hipMemcpyAsync(q->scx_clk.p, q->sc_h.p, (size_t)n_sends * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipGetLastError());
+        RCHK(q->h_small_sc.reserve(64));
+        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->scx_rows.as<uint32_t>() + nn, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        T = *q->h_small_sc.as<uint32_t>();
+    } else {
+        HIPCHK(hipMemcpyAsync(q->sc_pre.p, q->sc_ghead.as<uint32_t>() + n_old, (size_t)(nn + 1) * 4,
+                              hipMemcpyDeviceToDevice, s));
+        launch_scan_sum_large_u32(s, q->sc_pre.as<u32>(), nn + 1, q->sc_tmp.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        RCHK(q->h_small_sc.reserve(64));
+        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->sc_pre.as<uint32_t>() + nn, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        T = *q->h_small_sc.as<uint32_t>();
+    }
     const int64_t TC = std::max<int64_t>(T, 1);
     RCHK(q->out_ts.reserve(TC * 8, false));
     RCHK(q->out_keys.reserve((size_t)std::max(1, nk) * TC * 8, false));
@@ -624,27 +670,32 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     HIPCHK(hipMemsetAsync(q->out_expired.p, 0, q->out_expired.cap, s));
     q->zeroed_nulls = q->out_nulls.p;
     q->zeroed_expired = q->out_expired.p;
-    launch_sc_emit(s, M, n_old, q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(), q->sc_sval.as<u64>(),
-                   q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(), q->sc_chunk.as<int64_t>(),
-                   q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T, q->out_ts.as<int64_t>(),
-                   q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->out_rep.as<int64_t>(),
-                   q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
-    HIPCHK(hipGetLastError());
-    // the sends' playback clocks (TimestampGeneratorImpl only moves forward) and every row's chunk
-    std::vector<int64_t> sl(n_sends), och(T), osd(T);
-    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::memcpy(sl.data(), q->sc_h.p, (size_t)n_sends * 8);
-    if (T) {
-        HIPCHK(hipMemcpy(och.data(), q->sc_ochunk.p, (size_t)T * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(osd.data(), q->sc_osend.p, (size_t)T * 8, hipMemcpyDeviceToHost));
+    if (xs) {
+        launch_scx_rows(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->sc_skey.as<u64>(), q->scx_fe.as<u32>(),
+                        q->scx_fpre.as<u32>(), q->scx_last.as<u32>(), q->scx_rows.as<u32>(), q->scx_rank.as<int64_t>(),
+                        q->sc_sval.as<u64>(), q->sc_send.as<int64_t>(), q->scx_clk.as<int64_t>(),
+                        q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(), q->kt.dev(), q->kp, q->ap, cur_on, 1, T,
+                        q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
+                        q->out_nulls.as<unsigned char>(), q->out_expired.as<unsigned char>(), q->out_rep.as<int64_t>(),
+                        q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
+    } else {
+        launch_sc_emit(s, M, n_old, q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(),
+                       q->sc_sval.as<u64>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(),
+                       q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T,
+                       q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
+                       q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
     }
-    bool cv = cv0;
-    int64_t c = clock0;
-    for (int64_t i = 0; i < n_sends; i++) {
-        c = cv ? std::max(c, sl[i]) : sl[i];
-        cv = true;
-        sl[i] = c;
+    HIPCHK(hipGetLastError());
+    // every row's chunk and send
+    std::vector<int64_t> och(T), osd(T);
+    if (T) {
+        RCHK(q->sc_ho.reserve((size_t)2 * T * 8 + 64));
+        int64_t* hs = q->sc_ho.as<int64_t>();
+        HIPCHK(hipMemcpyAsync(hs, q->sc_ochunk.p, (size_t)T * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hs + T, q->sc_osend.p, (size_t)T * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::memcpy(och.data(), hs, (size_t)T * 8);
+        std::memcpy(osd.data(), hs + T, (size_t)T * 8);
     }
     PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
     PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
@@ -662,12 +713,14 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     if (host_out) {
         OutHost& o = q->out;
         o.ts.resize(T);
-        o.expired.assign(T, 0);
+        o.expired.resize(T);
         o.rep.resize(T);
         o.keys.resize((size_t)nk * T);
         o.vals.resize((size_t)na * T);
-        o.nulls.assign((size_t)na * T, 0);
+        o.nulls.resize((size_t)na * T);
         if (T) {
+            HIPCHK(hipMemcpyAsync(o.expired.data(), q->out_expired.p, T, hipMemcpyDeviceToHost, s));
+            if (na) HIPCHK(hipMemcpyAsync(o.nulls.data(), q->out_nulls.p, (size_t)na * T, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(o.ts.data(), q->out_ts.p, T * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(o.rep.data(), q->out_rep.p, T * 8, hipMemcpyDeviceToHost, s));
             if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), q->out_keys.p, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
@@ -851,7 +904,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         // lengthBatch whose L-th event is the push's last event: LengthBatchWindowProcessor flushes
         // the batch while processing that send (:206-243), not when the next event arrives
         const int64_t open_cnt = bounds.empty() ? q->n_pend + info.total_pass : info.total_pass - bounds.back().pcb;
-        const bool lb_full = !q->given && q->d.window == SH_WIN_LENGTH_BATCH && info.total_pass > 0 &&
+        const bool lb_full = !q->given && !q->d.stream_current && q->d.window == SH_WIN_LENGTH_BATCH && info.total_pass > 0 &&
                              open_cnt == q->d.window_param;
         const bool close_all = (q->given && q->given_W_end > W_last) || lb_full;
         if (!bounds.empty() || close_all) {

@@ -35,7 +35,8 @@ def _gpu_runs(c):
     if c.get("kind") == "aggregation":
         return False
     if q.get("stream_current"):
-        return bool(q.get("aggs")) and q.get("output", "current") == "current" and not q.get("partition")
+        return bool(q.get("aggs")) and not q.get("partition") and (
+            q.get("output", "current") == "current" or q.get("window") == "lengthBatch")
     if q.get("window") in ("lengthBatch", "timeBatch"):
         return bool(q.get("aggs")) or not q.get("group_by")
     return q.get("window") == "time" and bool(q.get("aggs")) and q.get("output", "current") == "current"

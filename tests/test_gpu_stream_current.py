@@ -64,7 +64,21 @@ def test_timebatch_stream_current_start_time(rt):
     both(rt, spec, split_batches(SCHEMA, ts, cols, [4_000], 2), label="timeBatch start")
 
 
-def test_stream_current_rejects_expired(rt):
-    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 4, aggs=[("count", None)], stream_current=True, output="expired")
+@pytest.mark.parametrize("output", ["all", "expired"])
+@pytest.mark.parametrize("L,cuts,send_size", [(50, [1, 777, 5_000], 3), (4, [3, 4_000, 4_001], 1), (1, [10], 2),
+                                              (2_000, [2_000, 6_000], 0)])
+@pytest.mark.parametrize("group_by", [True, False])
+def test_lengthbatch_stream_current_expired(rt, output, L, cuts, send_size, group_by):
+    """Batch w + 1's first event carries batch w's keys as EXPIRED rows (empty state) in its chunk."""
+    ts, cols = stream(12_000, 40, 13)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["k"] if group_by else (), aggs=AGGS,
+                         filter=(">", "v", -180.0), stream_current=True, output=output, key_capacity=64)
+    out = both(rt, spec, split_batches(SCHEMA, ts, cols, cuts, send_size), label=f"lengthBatch({L}, true) {output}")
+    if output == "expired" or group_by:  # (without group-by, `all` shows the new event's row in the key's place)
+        assert out["expired"].sum() > 0
+
+
+def test_stream_current_rejects_timebatch_expired(rt):
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 4, aggs=[("count", None)], stream_current=True, output="expired")
     with pytest.raises(rt.SiddhiError, match="stream.current"):
         rt.GpuQuery(spec)
