@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--send-size", type=int, default=1, help="events per InputHandler.send (1 = PER_EVENT)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N > 1 slice ingest: exchange and consume each push in turn (no overlap)")
     ap.add_argument("--ingest", choices=["slice", "keyed"], default="slice",
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
     ap.add_argument("--key-type", choices=["string", "int"], default="string",
@@ -358,10 +360,12 @@ def main():
     batches = []
     if sliced:
         # rank r's slice of global push i: events [(i*N + r)*B, (i*N + r + 1)*B) of one stream
-        from siddhi_amd.shard import ShardedQuery, TorchExchange, distributed_push
+        from siddhi_amd.shard import PipelinedPush, ShardedQuery, TorchExchange, distributed_push
         q = ShardedQuery(spec, rank, world, ctx)
         ex = TorchExchange(dev if args.backend == "nccl" else torch.device("cpu"))
         send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
+        # the record exchange of push i overlaps the consume of push i - 1 (two send buffers)
+        pp = None if args.no_pipeline else PipelinedPush(q, ex, [send_buf, torch.empty_like(send_buf)])
         for i in range(nb):
             batches.append(synth.torch_keyed_stream((i * world + rank) * B, B, 0xC2, keys_total,
                                                     args.events_per_ms * world, dev))
@@ -376,15 +380,27 @@ def main():
     torch.cuda.synchronize()
 
     def push(i):
+        """The output of push i (pipelined sharded ingest: of push i - 1, None for the first)."""
         ts, cols = batches[i]
         if sliced:
+            if pp is not None:
+                r = pp.push(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size,
+                            timings=phases if timing else None)
+                return r[0] if r is not None else None
             return distributed_push(q, ex, B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size,
                                     send_buf, host_out=False, timings=phases if timing else None)[0]
         return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
 
+    def drain():
+        if sliced and pp is not None:
+            r = pp.finish()
+            return r[0] if r is not None else None
+        return None
+
     phases, timing = {}, False
     for i in range(args.warmup):
         push(i)
+    drain()
     torch.cuda.synchronize()
     timing = True
     if dist:
@@ -393,10 +409,13 @@ def main():
     kern_ms, kern_bytes, flushes, rows = 0.0, 0, 0, 0
     host_t = [] if os.environ.get("SH_TIMING") else None
     t0 = time.perf_counter()
-    for i in range(args.warmup, nb):
+    for i in range(args.warmup, nb + 1):
         ta = time.perf_counter()
-        o = push(i).contents
+        op = push(i) if i < nb else drain()  # (the pipelined ingest consumes its last push here)
         tb = time.perf_counter()
+        if op is None:
+            continue
+        o = op.contents
         st = q.stats()
         kern_ms += st.main_kernel_ms
         flushes += o.n_flushes
@@ -445,7 +464,8 @@ def main():
                    "keys_per_gpu": args.keys, "keys_total": keys_total, "events_per_step_per_gpu": B,
                    "event_rate": f"{args.events_per_ms * 1000 * (world if sliced else 1)} events per event-time second",
                    "send_size": args.send_size,
-                   "parallelism": (f"slice ingest x{world}, key re-shard over {'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all" if sliced
+                   "parallelism": (f"slice ingest x{world}, key re-shard over {'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all"
+                                   + ("" if args.no_pipeline else ", exchange of push i overlapped with consume of push i-1") if sliced
                                    else f"key-sharded x{world}"),
                    "flushes": flushes, "rows": rows},
         "roofline": {"bound": "hbm", "kernel": "k_aggregate_own", "achieved": ach, "peak": HBM_PEAK_GBS,

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "sh_agg.h"
@@ -67,6 +68,18 @@ struct sh_shard {
     int64_t cur_W_base = 0, cur_W_end = 0;
     int64_t cur_seq = 0;                  // global index of the push's first event
     std::vector<int64_t> cur_off;         // stream offset of every slice in the push
+    // packed pushes waiting for their consume, oldest first (two at most: the exchange of push i may
+    // run while push i - 1 is consumed)
+    struct InFlight {
+        int64_t W_base, W_end, seq, send_base, send_size, n;
+        std::vector<int64_t> off;
+        int64_t clock, E0;
+        bool clock_valid, e0_valid;
+    };
+    // the stream state as of the push being consumed (the ingest may already be a push ahead)
+    int64_t cur_clock = 0, cur_E0 = 0;
+    bool cur_clock_valid = false, cur_e0_valid = false;
+    std::deque<InFlight> fl;
     PinnedBuf h_bgw;                      // pinned copies of the window starts being uploaded
     // ingest scratch
     int64_t slice_n = -1;
@@ -283,6 +296,11 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     return SH_OK;
 }
 
+static sh_shard::InFlight Shard_InFlight(const sh_shard* s) {
+    return sh_shard::InFlight{s->cur_W_base, s->cur_W_end, s->cur_seq, s->cur_send_base, s->cur_send_size, s->cur_n,
+                              s->cur_off, s->clock, s->E0, s->clock_valid, s->e0_valid};
+}
+
 // Phase 2 of a sliding time(T) query: every passing event gets its send's global clock and the global
 // PM (max ts over the passing events of the stream up to it: the slices before contribute their
 // summaries' PM, carried in sh_slice_summary.first_key) and goes to its key's owner.
@@ -348,6 +366,7 @@ static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch
     s->sl_pm = pm_end;
     s->send_base += sends;
     s->seq += (uint64_t)n_total;
+    s->fl.push_back(Shard_InFlight(s));
     s->packed = true;
     s->slice_n = -1;
     *bounds = s->my_bounds.data();
@@ -363,6 +382,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         return sh_fail(SH_ERR_INVALID, "sh_shard_pack: NULL argument");
     if (s->slice_n != b->n || all[s->rank].n != b->n)
         return sh_fail(SH_ERR_STATE, "sh_shard_pack: call sh_shard_summarize on the same slice first");
+    if (s->fl.size() >= 2) return sh_fail(SH_ERR_STATE, "sh_shard_pack: two packed pushes already wait for consume");
     // slices are cut at send boundaries: every slice but the last holds whole sends, otherwise one
     // send's events would get different clocks / send numbers on two ranks (InputHandler.send :85-96)
     if (b->send_size > 0)
@@ -489,6 +509,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     s->W = W_end;
     if (lb) s->carry = (s->carry + total_pass) % s->d.window_param;
     s->seq += (uint64_t)n_total;
+    s->fl.push_back(Shard_InFlight(s));
     s->packed = true;
     s->slice_n = -1;
     *bounds = s->my_bounds.data();
@@ -498,10 +519,10 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
 
 static void sync_owner(sh_shard* s) {
     sh_query* q = s->owner;
-    q->clock = s->clock;
-    q->clock_valid = s->clock_valid;
-    q->E0 = s->E0;
-    q->e0_valid = s->e0_valid;
+    q->clock = s->cur_clock;
+    q->clock_valid = s->cur_clock_valid;
+    q->E0 = s->cur_E0;
+    q->e0_valid = s->cur_e0_valid;
 }
 
 static void set_order(sh_shard* s, bool host_out, const int64_t** order) {
@@ -547,8 +568,8 @@ static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* rec
     RCHK(sliding_push_given(q, M, s->u_ts.as<int64_t>(), cols, s->u_cols[nc].as<int64_t>(),
                             s->u_cols[nc + 1].as<int64_t>(), (const uint64_t*)s->u_gidx.p, s->cur_seq,
                             s->cur_send_size, s->cur_send_base, host_out, out, s->cur_n));
-    q->clock = s->clock;
-    q->clock_valid = s->clock_valid;
+    q->clock = s->cur_clock;
+    q->clock_valid = s->cur_clock_valid;
     set_order(s, host_out, order);
     return SH_OK;
 }
@@ -560,8 +581,23 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !recv_bytes || !out || (n_all_bounds > 0 && !all_bounds))
         return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
-    if (!s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
-    s->packed = false;
+    if (s->fl.empty()) return sh_fail(SH_ERR_STATE, "sh_shard_consume: no packed push in flight");
+    {
+        const sh_shard::InFlight f = s->fl.front();
+        s->fl.pop_front();
+        s->cur_W_base = f.W_base;
+        s->cur_W_end = f.W_end;
+        s->cur_seq = f.seq;
+        s->cur_send_base = f.send_base;
+        s->cur_send_size = f.send_size;
+        s->cur_n = f.n;
+        s->cur_off = f.off;
+        s->cur_clock = f.clock;
+        s->cur_clock_valid = f.clock_valid;
+        s->cur_E0 = f.E0;
+        s->cur_e0_valid = f.e0_valid;
+    }
+    s->packed = !s->fl.empty();
     if (s->agg) host_out = 0;  // the root's flushes feed the roll-up levels on the device
     const int64_t RB = 4 * (int64_t)s->rec_words;
     int64_t bytes = 0;
@@ -643,6 +679,11 @@ extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out,
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_advance_time: NULL argument");
     if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");
+    // nothing in flight: the consumed stream state is the ingest's
+    s->cur_clock = s->clock;
+    s->cur_clock_valid = s->clock_valid;
+    s->cur_E0 = s->E0;
+    s->cur_e0_valid = s->e0_valid;
     sh_query* q = s->owner;
     if (s->sliding) {
         // expiry is lazy (applied at each key's next event): the TIMER only moves the clock
@@ -699,6 +740,10 @@ int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query**
     s->sl_pm = sc[7];
     s->send_base = sc[8];
     s->p0_known = sc[9] != 0;
+    s->cur_clock = s->clock;
+    s->cur_clock_valid = s->clock_valid;
+    s->cur_E0 = s->E0;
+    s->cur_e0_valid = s->e0_valid;
     s->fp = s->fp_orig;
     if (s->p0_known) {
         const int pc = s->d.partition_col;

@@ -358,6 +358,22 @@ class TorchExchange:
                                     [int(x) for x in send_bytes], group=self.group)
         return recv, recv_bytes
 
+    def all_to_all_start(self, send, send_bytes: np.ndarray):
+        """all_to_all with the record payload left in flight: (recv, recv_bytes, work); work.wait()
+        before reading recv (the counts exchange is synchronous, it is 8 bytes per rank)."""
+        import torch
+        sc = torch.as_tensor(np.asarray(send_bytes, dtype=np.int64)).to(self.device)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc, group=self.group)
+        recv_bytes = rc.cpu().numpy()
+        total = int(recv_bytes.sum())
+        recv = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
+        used = int(np.asarray(send_bytes).sum())
+        send = send[:used].to(self.device)
+        work = self.dist.all_to_all_single(recv[:total], send, [int(x) for x in recv_bytes],
+                                           [int(x) for x in send_bytes], group=self.group, async_op=True)
+        return recv, recv_bytes, (work, send)
+
     def all_gather_bounds(self, bounds: np.ndarray) -> np.ndarray:
         import torch
         n = torch.tensor([len(bounds)], dtype=torch.int64, device=self.device)
@@ -403,3 +419,55 @@ def distributed_push(q: ShardedQuery, ex: TorchExchange, n: int, ts_ptr: int, co
             timings[k] = timings.get(k, 0.0) + v * 1e3
         timings["bytes_sent"] = timings.get("bytes_sent", 0) + int(np.asarray(send_bytes).sum())
     return res
+
+
+class PipelinedPush:
+    """distributed_push with the record exchange of push i in flight while push i - 1 is consumed
+    (the library keeps up to two packed pushes per shard, sh_shard_pack / sh_shard_consume FIFO).
+    push() returns the output of the previous push (None for the first); finish() the last one.
+    Two send buffers alternate: pack(i + 1) writes one while the exchange of i still reads the other."""
+
+    def __init__(self, q: ShardedQuery, ex: TorchExchange, send_bufs, host_out: bool = False):
+        self.q, self.ex, self.bufs, self.host_out = q, ex, list(send_bufs), host_out
+        self.k = 0
+        self.pending = None
+
+    def push(self, n: int, ts_ptr: int, col_ptrs: Sequence[int], send_size: int, timings: Optional[dict] = None):
+        import time
+        t0 = time.perf_counter()
+        summ = self.q.summarize(n, ts_ptr, col_ptrs, send_size)
+        all_summ = self.ex.all_gather_summaries(summ)  # (after the previous exchange on the same group)
+        buf = self.bufs[self.k % len(self.bufs)]
+        self.k += 1
+        t1 = time.perf_counter()
+        send_bytes, bounds = self.q.pack(all_summ, buf.data_ptr(), int(buf.numel()))
+        t2 = time.perf_counter()
+        all_bounds = self.ex.all_gather_bounds(bounds)  # before the payload: collectives run in order
+        recv, recv_bytes, work = self.ex.all_to_all_start(buf, send_bytes)
+        t3 = time.perf_counter()
+        res = self._consume_pending()  # push i - 1 aggregates while push i's records move
+        self.pending = (recv, recv_bytes, all_bounds, work, buf.device)
+        if timings is not None:
+            t4 = time.perf_counter()
+            for key, v in (("summarize", t1 - t0), ("pack", t2 - t1), ("exchange_start", t3 - t2),
+                           ("consume_prev", t4 - t3)):
+                timings[key] = timings.get(key, 0.0) + v * 1e3
+            timings["bytes_sent"] = timings.get("bytes_sent", 0) + int(np.asarray(send_bytes).sum())
+        return res
+
+    def finish(self):
+        return self._consume_pending()
+
+    def _consume_pending(self):
+        import torch
+        if self.pending is None:
+            return None
+        recv, recv_bytes, all_bounds, (work, _send), dev = self.pending
+        self.pending = None
+        work.wait()
+        if recv.device != dev:  # host transport (gloo)
+            recv = recv.to(dev)
+        torch.cuda.current_stream(dev).synchronize()
+        res = self.q.consume(recv.data_ptr(), recv_bytes, all_bounds, self.host_out)
+        self.q.last_bounds = all_bounds
+        return res

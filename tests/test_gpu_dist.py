@@ -38,16 +38,17 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, window, outdir):
+def _worker(rank, world, port, window, outdir, pipelined=False):
     import torch
     import torch.distributed as dist
-    from siddhi_amd.shard import ShardedQuery, TorchExchange, distributed_push, host_rows
+    from siddhi_amd.shard import PipelinedPush, ShardedQuery, TorchExchange, distributed_push, host_rows
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     q = ShardedQuery(_spec(window), rank, world)
     ex = TorchExchange(torch.device("cpu"))
     send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
+    pp = PipelinedPush(q, ex, [send_buf, torch.empty_like(send_buf)], host_out=True) if pipelined else None
     outs = []
     for i in range(N_PUSH):
         ts, cols = synth.keyed_stream(i * B, B, 0xD2, KEYS, 20)
@@ -57,9 +58,17 @@ def _worker(rank, world, port, window, outdir):
         t = torch.from_numpy(np.ascontiguousarray(ts[lo:hi])).to(dev)
         cs = [torch.from_numpy(np.ascontiguousarray(c[lo:hi])).to(dev) for c in cols]
         torch.cuda.synchronize()
+        if pp is not None:  # the output of push i - 1 comes back while push i is exchanged
+            res = pp.push(hi - lo, t.data_ptr(), [c.data_ptr() for c in cs], SEND)
+            if res is not None:
+                outs.append((host_rows(*res), q.last_bounds, ((i - 1) * B, SEND)))
+            continue
         res = distributed_push(q, ex, hi - lo, t.data_ptr(), [c.data_ptr() for c in cs], SEND, send_buf,
                                host_out=True)
         outs.append((host_rows(*res), q.last_bounds, (i * B, SEND)))
+    if pp is not None:
+        res = pp.finish()
+        outs.append((host_rows(*res), q.last_bounds, ((N_PUSH - 1) * B, SEND)))
     with open(os.path.join(outdir, f"rank{rank}.pkl"), "wb") as f:
         pickle.dump(outs, f)
     q.close()
@@ -67,12 +76,14 @@ def _worker(rank, world, port, window, outdir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("window", ["timeBatch", "time"])
-def test_two_process_sharded_push_matches_oracle(window):
+def test_two_process_sharded_push_matches_oracle(window, pipelined):
+    """pipelined: PipelinedPush, the exchange of push i overlapping the consume of push i - 1."""
     from siddhi_amd.shard import merge_owner_outputs
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), window, d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), window, d, pipelined), nprocs=world, join=True)
         per_rank = []
         for r in range(world):
             with open(os.path.join(d, f"rank{r}.pkl"), "rb") as f:
@@ -90,5 +101,5 @@ def test_two_process_sharded_push_matches_oracle(window):
         pushes.append(abi.HostBatch(SCHEMA, ts, cols, SEND))
     want = run_pushes(o, pushes)
     o.close()
-    assert_same(got, want, label=f"2-process {window}")
+    assert_same(got, want, label=f"2-process {window} pipelined={pipelined}")
     assert got["flush_offsets"].size > 5
