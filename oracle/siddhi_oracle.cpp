@@ -438,22 +438,6 @@ struct RateLimiter {
             }
         }
     }
-
-    // the selector's flushes of one push/advance -> the limiter's flushes
-    void apply(OutBuf& o) {
-        if (kind == SH_RATE_NONE) return;
-        std::vector<OutRow> rows;
-        rows.swap(o.rows);
-        std::vector<int64_t> off = o.flush_offsets, clk = o.flush_clock;
-        o.clear();
-        for (size_t f = 0; f < clk.size(); f++) {
-            std::vector<OutRow> chunk;
-            process(rows.data() + off[f], off[f + 1] - off[f], chunk);
-            if (chunk.empty()) continue;
-            o.rows.insert(o.rows.end(), chunk.begin(), chunk.end());
-            o.close_flush(clk[f]);
-        }
-    }
 };
 
 // ==========================================================================================
@@ -478,6 +462,10 @@ struct PartitionState {
     bool ext_has_reset = false; OEvent ext_reset;
     size_t index = 0;  // position in the scheduler's iteration order
     int64_t key = 0;
+    // the query's output rate limiter: one per partition instance (PartitionRuntime clones the query
+    // with its OutputRateLimiter, PartitionRuntimeImpl)
+    RateLimiter rl;
+    bool rl_init = false;
 };
 
 struct Query {
@@ -523,7 +511,20 @@ struct Query {
     }
 
     // ---- selector: QuerySelector.processInBatchGroupBy (core/query/selector/QuerySelector.java:315-374)
+    // one selector output chunk -> the partition's rate limiter -> one flush (if it sends anything)
+    void close_chunk(PartitionState& ps, size_t start) {
+        if (rate.kind == SH_RATE_NONE) { out.close_flush(clock); return; }
+        if (!ps.rl_init) { ps.rl = rate; ps.rl_init = true; }
+        std::vector<OutRow> chunk(out.rows.begin() + (int64_t)start, out.rows.end()), kept;
+        out.rows.resize(start);
+        ps.rl.process(chunk.data(), (int64_t)chunk.size(), kept);
+        if (kept.empty()) return;
+        out.rows.insert(out.rows.end(), kept.begin(), kept.end());
+        out.close_flush(clock);
+    }
+
     void selector(PartitionState& ps, const Chunk& chunk) {
+        const size_t start = out.rows.size();
         if (aggs.empty() && d.n_group_by == 0) {
             // QuerySelector.processNoGroupBy (:161-205): every qualifying event passes through
             bool any = false;
@@ -534,7 +535,7 @@ struct Query {
                 OutRow row{}; row.ts = ev.ts; row.expired = ev.type == EXPIRED; row.rep = ev.seq;
                 out.rows.push_back(row); any = true;
             }
-            if (any) out.close_flush(clock);
+            if (any) close_chunk(ps, start);
             return;
         }
         std::vector<GKey> order;
@@ -575,7 +576,7 @@ struct Query {
         }
         if (!order.empty()) {
             for (const GKey& k : order) out.rows.push_back(grouped[k]);
-            out.close_flush(clock);
+            close_chunk(ps, start);
         }
     }
 
@@ -1291,7 +1292,6 @@ int or_push(void* h, const sh_batch* b, const sh_out** out) {
     int64_t step = b->send_size > 0 ? b->send_size : b->n;
     for (int64_t lo = 0; lo < b->n; lo += step) q->send(b, lo, std::min(b->n, lo + step));
     q->seq_base += b->n;
-    q->rate.apply(q->out);
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }
@@ -1300,7 +1300,6 @@ int or_advance_time(void* h, int64_t now, const sh_out** out) {
     Query* q = (Query*)h;
     q->out.clear();
     q->set_clock(now);
-    q->rate.apply(q->out);
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }

@@ -35,9 +35,8 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     if (kind != SH_RATE_NONE && n < 1) return sh_fail(SH_ERR_INVALID, "output rate needs every >= 1 events");
     if (n > (int64_t)1 << 30) return sh_fail(SH_ERR_UNSUPPORTED, "output rate above 2^30 events");
     if (q->seq > 0 || q->clock_valid) return sh_fail(SH_ERR_INVALID, "output rate must be set before the first push");
-    // a partitioned query holds one limiter per partition instance (PartitionRuntime clones the query)
-    if (kind != SH_RATE_NONE && q->d.partition_col >= 0)
-        return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of a partitioned query");
+    // a partitioned query holds one limiter per partition instance (PartitionRuntime clones the query);
+    // the GPU's partitioned timeBatch flushes only partition p0 (R12), so its one limiter is p0's
     if (kind != SH_RATE_NONE && q->given) return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of a sharded query");
     if (kind != SH_RATE_NONE && q->kp.n > 2) return sh_fail(SH_ERR_UNSUPPORTED, "output rate with more than 2 group-by keys");
     q->rate.kind = kind;

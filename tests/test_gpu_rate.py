@@ -149,10 +149,23 @@ def test_device_output_rate(rt, window, param):
     assert_same(abi.concat_arrays(parts), ora, label=f"device {window}")
 
 
+@pytest.mark.parametrize("kind,n", [("all", 3), ("first", 2), ("last", 4)])
+def test_partitioned_timebatch_rate(rt, kind, n):
+    """One limiter per partition instance; only p0 ever flushes (R12), so the GPU's one limiter is p0's."""
+    sch = abi.Schema.parse("k int, p int, v double, ts long")
+    rng = np.random.default_rng(41)
+    m = 30_000
+    ts = (np.arange(m) // 20 + 10_000).astype(np.int64)
+    cols = [rng.integers(0, 50, m).astype(np.int32), rng.integers(0, 3, m).astype(np.int32),
+            rng.integers(-99, 99, m).astype(np.float64) / 4, ts.copy()]
+    spec = abi.QuerySpec(sch, "timeBatch", 400, group_by=["k"], aggs=[("count", None), ("sum", "v")], partition="p",
+                         key_capacity=64, rate=(kind, n))
+    pushes = split_batches(sch, ts, cols, [7_000, 20_000], 1) + [("advance", int(ts[-1]) + 1_000)]
+    out = both(rt, spec, pushes, label=f"partitioned {kind} {n}")
+    assert out["ts"].size > 0
+
+
 def test_rate_rejects(rt):
-    spec = abi.QuerySpec(SCHEMA, "timeBatch", 100, group_by=["k"], aggs=AGGS, partition="k", rate=("all", 2))
-    with pytest.raises(rt.SiddhiError, match="partitioned"):
-        rt.GpuQuery(spec)
     spec = abi.QuerySpec(SCHEMA, "lengthBatch", 10, aggs=AGGS, rate=("first", 0))
     with pytest.raises(rt.SiddhiError, match="every >= 1"):
         rt.GpuQuery(spec)
