@@ -1392,11 +1392,16 @@ __global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, 
     auto load_heads = [&]() {
         h_from = staged > hj ? staged : hj;
         h_to = min(min(h_from + kKS, hj + kKH), HN);
+        // one address select per entry (ring or run), no divergent branch per staged entry
 #pragma unroll
         for (int q = 0; q < kKS; q++) {
             const int j = min(h_from + q, HN - 1);
-            h_pm[q] = head_pm(j);
-            h_v[q] = head_v(j);
+            const bool ring = j < H0;
+            const size_t ri = (size_t)((rh0 + j) & gm), gi = (size_t)a + (size_t)(j - H0);
+            const i64* pp = ring ? rpm + ri : g_pm + gi;
+            const u64* pv = ring ? rval + ri : g_v + gi;
+            h_pm[q] = *pp;
+            h_v[q] = *pv;
         }
     };
     auto commit_heads = [&]() {
