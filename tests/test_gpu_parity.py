@@ -227,6 +227,26 @@ def c3_spec(keys=10_000, T=10_000):
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys)
 
 
+def test_sliding_key_churn_bound(rt):
+    """Sliding windows keep a key's slot for the query's lifetime (siddhi_hip.h key_capacity): churn
+    within the table's room matches the oracle push after push; a stream that keeps bringing new keys
+    past it fails loudly instead of mixing keys."""
+    from siddhi_amd.runtime import SiddhiError
+    sch = abi.Schema.parse("k long, v double, ts long")  # hashed keys (no dictionary ids)
+    n = 6_000
+    ts = (np.arange(n, dtype=np.int64) * 3 + 1_000)
+    v = (np.arange(n) % 97).astype(np.float64) / 8
+    k = (np.arange(n, dtype=np.int64) // 4) * 1_000_003  # a new key every 4 events: 1500 keys over time
+    spec = abi.QuerySpec(sch, "time", 50, group_by=["k"], aggs=[("sum", "v"), ("count", None)], key_capacity=4_096)
+    both(rt, spec, split_batches(sch, ts, [k, v, ts.copy()], [1_000, 3_000], 1), label="churn within room")
+    small = abi.QuerySpec(sch, "time", 50, group_by=["k"], aggs=[("sum", "v")], key_capacity=64)
+    g = rt.GpuQuery(small)
+    with pytest.raises(SiddhiError, match="key table full"):
+        for b in split_batches(sch, ts, [k, v, ts.copy()], [500, 1_000, 2_000, 4_000], 1):
+            g.push(b)
+    g.close()
+
+
 @pytest.mark.parametrize("send_size", [1, 250])
 def test_c3_sliding_matches_oracle(rt, send_size):
     ts, cols = synth.keyed_stream(0, 200_000, 0xC3, 2000, 20)   # 20 events/ms, 10 s window ~ 100 per key
