@@ -121,12 +121,12 @@ typedef struct {
     sh_agg_spec aggs[SH_MAX_AGGS];
     int32_t expired_on;     /* insert [expired|all] events                               */
     int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`     */
-    int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing). Batch
-                             * windows rebuild their hashed table from the live keys when it is half
-                             * full; sliding (time / externalTime) windows keep a key's slot for the
-                             * query's lifetime, so there it bounds the distinct keys EVER seen
-                             * (dictionary-id keys: the id range). Exceeding it fails the push with
-                             * "group key table full: raise key_capacity".                   */
+    int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing). Batch and
+                             * time() windows rebuild their hashed table from the live keys when it
+                             * is half full (a time() key is live while an event of it can still be
+                             * in a later window); externalTime windows keep a key's slot for the
+                             * query's lifetime; dictionary-id keys: the id range. Exceeding it
+                             * fails the push with "group key table full: raise key_capacity". */
     int32_t ts_col;         /* externalTimeBatch / externalTime: the LONG timestamp attribute  */
     int32_t start_col;      /* externalTimeBatch: LONG start-time attribute (has_start_time 2) */
 } sh_query_desc;

@@ -158,6 +158,44 @@ static int empty_out(sh_query* q, const sh_out** out) {
 static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
                           int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out);
 
+// Hashed keys of a time() window get a fresh table once more than half full: keys whose every window
+// event has expired for any later event (last PM + T <= the playback clock) are dropped — the state the
+// reference destroys (AttributeAggregatorExecutor canDestroy) — and the live keys' state moves to
+// their new slots. Same table size, so the per-slot layouts keep their strides.
+static int sliding_rekey(sh_query* q) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    const int64_t size = (int64_t)q->kt.size_, n = s->nslots;
+    if (n != size + 1) return SH_OK;
+    KeyTableHost nk;
+    RCHK(nk.init_size((size_t)size));
+    DevBuf map;
+    RCHK(map.reserve((size_t)n * 4, false));
+    launch_sl_rekey_map(st, size, q->kt.dev(), nk.dev(), s->rhead.as<int64_t>(), s->rlen.as<int64_t>(),
+                        s->rpm.as<int64_t>(), s->rc, q->d.window_param, q->clock, map.as<u32>());
+    HIPCHK(hipGetLastError());
+    RCHK(nk.check(st));
+    const int64_t F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols), rc = s->rc;
+    struct L { DevBuf* b; int64_t outer, inner; int fill; };
+    const L lay[] = {{&s->cnt, 1, 8, 0},        {&s->f, F, 8, 0},          {&s->mm, F, 8, 0},
+                     {&s->mm_has, F, 1, 0},     {&s->dq_head, F, 8, 0},    {&s->dq_len, F, 8, 0},
+                     {&s->dq, F, rc * 8, 0},    {&s->rhead, 1, 8, 0},      {&s->rlen, 1, 8, 0},
+                     {&s->rpm, 1, rc * 8, 0},   {&s->rval, V, rc * 8, 0},  {&s->cur_send, 1, 8, 0xff},
+                     {&s->cur_first, 1, 8, 0}};
+    for (const L& l : lay) {
+        DevBuf nb;
+        const size_t bytes = (size_t)l.outer * n * l.inner;
+        RCHK(nb.reserve(std::max<size_t>(bytes, 8), false));
+        HIPCHK(hipMemsetAsync(nb.p, l.fill, std::max<size_t>(bytes, 8), st));
+        launch_sl_rekey_copy(st, l.b->p, nb.p, l.outer, n, l.inner, map.as<u32>());
+        HIPCHK(hipGetLastError());
+        *l.b = std::move(nb);  // (stream-ordered release of the old buffer)
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    q->kt = std::move(nk);
+    return SH_OK;
+}
+
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
@@ -166,6 +204,9 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N == 0) return empty_out(q, out);
     if (N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
+    if (!q->kt.dense && q->kp.n > 0 && q->d.window == SH_WIN_TIME && q->clock_valid &&
+        q->kt.n_keys > (int64_t)q->kt.size_ / 2)
+        RCHK(sliding_rekey(q));
     HIPCHK(hipEventRecord(q->ev_push0, st));
     ColSet cs{};
     cs.n = q->d.n_cols;

@@ -90,5 +90,8 @@ void launch_flush_write(hipStream_t s, const i64* out_send, const i64* out_clock
                         int nb, i64* flush_off, i64* flush_clock);
 void launch_sl_regrow(hipStream_t s, const u64* old_buf, u64* new_buf, const i64* head, const i64* len, i64 nslots,
                       int nsub, i64 old_rc, i64 new_rc, bool per_sub);
+void launch_sl_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new_kt, const i64* rhead, const i64* rlen,
+                         const i64* rpm, i64 rc, i64 T, i64 bound, u32* map);
+void launch_sl_rekey_copy(hipStream_t s, const void* src, void* dst, i64 outer, i64 n, i64 inner, const u32* map);
 
 }  // namespace shd

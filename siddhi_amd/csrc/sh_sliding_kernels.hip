@@ -1792,4 +1792,55 @@ void launch_sl_regrow(hipStream_t s, const u64* old_buf, u64* new_buf, const i64
                        nslots, nsub, old_rc, new_rc, per_sub ? head : nullptr);
 }
 
+
+// ---- key-table rebuild of a sliding window (sh_sliding.cpp sliding_rekey): a key whose window holds
+// no event that can still be in it for any later event (last ring entry's PM + T <= the clock every
+// later record carries at least) is in the state the reference destroys (canDestroy): it is dropped;
+// the live keys move to a fresh table and their state follows them to the new slots --------------------
+__global__ __launch_bounds__(kBlock) void k_sl_rekey_map(i64 size, KeyTable old_kt, KeyTable new_kt,
+                                                        const i64* __restrict__ rhead, const i64* __restrict__ rlen,
+                                                        const i64* __restrict__ rpm, i64 rc, i64 T, i64 bound,
+                                                        u32* map) {
+    const i64 s = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (s > size) return;
+    if (s == size) { map[s] = (u32)size; return; }  // the spare slot keeps its place
+    map[s] = 0xFFFFFFFFu;
+    const u64 key = old_kt.keys[s];
+    if (key == kEmptyKey) return;
+    const i64 n = rlen[s];
+    if (n <= 0) return;
+    const i64 last_pm = rpm[(size_t)s * rc + ((rhead[s] + n - 1) & (rc - 1))];
+    if (last_pm + T <= bound) return;
+    map[s] = key_slot(new_kt, key);
+}
+
+// dst[o][map[s]][.] = src[o][s][.] for live slots (unit-sized words; rings keep their head offsets)
+__global__ __launch_bounds__(kBlock) void k_sl_rekey_copy(const unsigned char* __restrict__ src, unsigned char* dst,
+                                                         i64 outer, i64 n, i64 inner, int unit,
+                                                         const u32* __restrict__ map) {
+    const i64 per = inner / unit;
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= outer * n * per) return;
+    const i64 w = i % per, sl = (i / per) % n, o = i / (per * n);
+    const u32 to = map[sl];
+    if (to == 0xFFFFFFFFu) return;
+    const size_t from_off = ((size_t)o * n + sl) * inner + (size_t)w * unit;
+    const size_t to_off = ((size_t)o * n + to) * inner + (size_t)w * unit;
+    if (unit == 8) *(u64*)(dst + to_off) = *(const u64*)(src + from_off);
+    else dst[to_off] = src[from_off];
+}
+
+void launch_sl_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new_kt, const i64* rhead, const i64* rlen,
+                         const i64* rpm, i64 rc, i64 T, i64 bound, u32* map) {
+    hipLaunchKernelGGL(k_sl_rekey_map, dim3((unsigned)((size + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, size,
+                       old_kt, new_kt, rhead, rlen, rpm, rc, T, bound, map);
+}
+
+void launch_sl_rekey_copy(hipStream_t s, const void* src, void* dst, i64 outer, i64 n, i64 inner, const u32* map) {
+    const int unit = inner % 8 == 0 ? 8 : 1;
+    const i64 total = outer * n * (inner / unit);
+    if (total <= 0) return;
+    hipLaunchKernelGGL(k_sl_rekey_copy, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       (const unsigned char*)src, (unsigned char*)dst, outer, n, inner, unit, map);
+}
 }  // namespace shd

@@ -228,21 +228,27 @@ def c3_spec(keys=10_000, T=10_000):
 
 
 def test_sliding_key_churn_bound(rt):
-    """Sliding windows keep a key's slot for the query's lifetime (siddhi_hip.h key_capacity): churn
-    within the table's room matches the oracle push after push; a stream that keeps bringing new keys
-    past it fails loudly instead of mixing keys."""
+    """A time() window with hashed keys rebuilds its table from the live keys (every key whose window
+    events can no longer be in any later window is dropped, as the reference destroys its state), so a
+    stream bringing far more distinct keys over time than key_capacity matches the oracle; more keys
+    alive at once than the table holds fails loudly instead of mixing keys."""
     from siddhi_amd.runtime import SiddhiError
     sch = abi.Schema.parse("k long, v double, ts long")  # hashed keys (no dictionary ids)
     n = 6_000
     ts = (np.arange(n, dtype=np.int64) * 3 + 1_000)
     v = (np.arange(n) % 97).astype(np.float64) / 8
     k = (np.arange(n, dtype=np.int64) // 4) * 1_000_003  # a new key every 4 events: 1500 keys over time
-    spec = abi.QuerySpec(sch, "time", 50, group_by=["k"], aggs=[("sum", "v"), ("count", None)], key_capacity=4_096)
-    both(rt, spec, split_batches(sch, ts, [k, v, ts.copy()], [1_000, 3_000], 1), label="churn within room")
-    small = abi.QuerySpec(sch, "time", 50, group_by=["k"], aggs=[("sum", "v")], key_capacity=64)
-    g = rt.GpuQuery(small)
+    cuts = [500, 1_000, 2_000, 3_000, 4_000, 5_000]
+    # cap 64 (a 128-slot table): pushes of 100 events bring 25 new keys each, the table is rebuilt
+    # every few pushes (a push's own new keys must fit: the rebuild runs between pushes)
+    for cap, cc in ((4_096, cuts), (64, list(range(100, n, 100)))):
+        spec = abi.QuerySpec(sch, "time", 50, group_by=["k"], aggs=[("sum", "v"), ("count", None), ("max", "v")],
+                             key_capacity=cap)
+        both(rt, spec, split_batches(sch, ts, [k, v, ts.copy()], cc, 1), label=f"churn cap {cap}")
+    alive = abi.QuerySpec(sch, "time", 1_000_000, group_by=["k"], aggs=[("sum", "v")], key_capacity=64)
+    g = rt.GpuQuery(alive)
     with pytest.raises(SiddhiError, match="key table full"):
-        for b in split_batches(sch, ts, [k, v, ts.copy()], [500, 1_000, 2_000, 4_000], 1):
+        for b in split_batches(sch, ts, [k, v, ts.copy()], cuts, 1):
             g.push(b)
     g.close()
 
