@@ -348,5 +348,17 @@ void launch_scx_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, co
                      const i64* send, const i64* send_clock, const i64* pend_ts, const u64* pend_gidx, KeyTable kt,
                      KeyPlan kp, AggPlan ap, int cur_on, int exp_on, i64 T, i64* out_ts, i64* out_keys, u64* out_vals,
                      unsigned char* out_nulls, unsigned char* out_exp, i64* out_rep, i64* out_chunk, i64* out_send);
+void launch_scxt_count(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fpre,
+                       const u32* ghead, int cur_on, u32* rows);
+void launch_scxt_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fe,
+                      const u32* fpre, const u32* lastidx, const u32* ghead, const u32* base, const u32* slast,
+                      const u64* sval, const i64* chunk, const i64* send, const i64* bclk, const i64* pend_ts,
+                      const u64* pend_gidx, KeyTable kt, KeyPlan kp, AggPlan ap, int cur_on, i64 T, i64* out_ts,
+                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, unsigned char* out_exp, i64* out_rep,
+                      i64* out_chunk, i64* out_send);
+void launch_scx_pending_rows(hipStream_t s, i64 M, const u32* fe, const u32* fpre, const u32* lastidx,
+                             const u32* pend_pos, const u64* pend_gidx, KeyTable kt, KeyPlan kp, AggPlan ap, i64 now,
+                             i64 T, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                             unsigned char* out_exp, i64* out_rep);
 
 }  // namespace shd

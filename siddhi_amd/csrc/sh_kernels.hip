@@ -1686,8 +1686,9 @@ __global__ __launch_bounds__(kBlock) void k_scx_expired(i64 M, i64 n_old, const 
                                                        const u32* __restrict__ fpre, const u32* __restrict__ lastidx,
                                                        const u32* __restrict__ base, const i64* __restrict__ rank_e,
                                                        const i64* __restrict__ send, const i64* __restrict__ send_clock,
+                                                       const i64* __restrict__ bclk,
                                                        const u64* __restrict__ pend_gidx, KeyTable kt, KeyPlan kp,
-                                                       AggPlan ap, int cur_on, i64 T, i64* out_ts, i64* out_keys,
+                                                       AggPlan ap, int cur_on, int tb, i64 T, i64* out_ts, i64* out_keys,
                                                        u64* out_vals, unsigned char* out_nulls, unsigned char* out_exp,
                                                        i64* out_rep, i64* out_chunk, i64* out_send) {
     const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
@@ -1700,7 +1701,7 @@ __global__ __launch_bounds__(kBlock) void k_scx_expired(i64 M, i64 n_old, const 
     const i64 rank = (i64)fpre[m] - (i64)fpre[sc_wstart(w, n_old, pcb)];
     if (cur_on && rank == rank_e[jb]) return;  // the new event's current row takes this position
     const i64 o = base[jb] + rank;
-    out_ts[o] = send_clock[send[mb]];
+    out_ts[o] = tb ? bclk[w] : send_clock[send[mb]];  // (timeBatch: mb may be past the push's entries)
     out_rep[o] = (i64)pend_gidx[lastidx[m]];
     i64 kv[SH_MAX_GROUP] = {0, 0};
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
@@ -1710,8 +1711,8 @@ __global__ __launch_bounds__(kBlock) void k_scx_expired(i64 M, i64 n_old, const 
         out_nulls[(size_t)a * T + o] = ap.kind[a] == AK_COUNT ? 0 : 1;
     }
     out_exp[o] = 1;
-    out_chunk[o] = jb;
-    out_send[o] = send[mb];
+    out_chunk[o] = tb ? -(w + 1) : jb;  // timeBatch: the closing TIMER chunk precedes the send's own
+    out_send[o] = tb ? -(w + 1) : send[mb];
 }
 
 // the current rows (per-event chunks): at a batch start after the batch's expired rows, or in place
@@ -1769,11 +1770,122 @@ void launch_scx_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, co
     if (T <= 0) return;
     if (exp_on)
         hipLaunchKernelGGL(k_scx_expired, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, n_old, pcb, nb, skey, fe, fpre,
-                           lastidx, base, rank_e, send, send_clock, pend_gidx, kt, kp, ap, cur_on, T, out_ts, out_keys,
-                           out_vals, out_nulls, out_exp, out_rep, out_chunk, out_send);
+                           lastidx, base, rank_e, send, send_clock, (const i64*)nullptr, pend_gidx, kt, kp, ap, cur_on, 0, T, out_ts,
+                           out_keys, out_vals, out_nulls, out_exp, out_rep, out_chunk, out_send);
     if (cur_on && M > n_old)
         hipLaunchKernelGGL(k_scx_current, dim3(sc_grid(M - n_old)), dim3(kBlock), 0, s, M, n_old, pcb, skey, fpre, base,
                            rank_e, sval, send, pend_ts, pend_gidx, kt, kp, ap.n, exp_on, T, out_ts, out_keys, out_vals,
                            out_nulls, out_exp, out_rep, out_chunk, out_send);
+}
+
+// ---- timeBatch(T, true) with expired / all-events output: a window closes in the scheduler's TIMER
+// chunk, which runs before the crossing send's own chunk (Scheduler.onTimeChange at the send's
+// set_clock): its keys' EXPIRED rows (empty state) form a flush of their own, in the window's
+// first-occurrence order, followed by the send's CURRENT rows (one per (send, key) group) ----------
+// keys of the window that closes right before entry m (m == M: after the push's last entry), if
+// entry m - 1's window closes in this push (w < nb) and entry m starts a later window (or there is none)
+__device__ __forceinline__ i64 sc_closing_keys(i64 m, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey,
+                                               const u32* fpre) {
+    if (m < 1) return 0;
+    const i64 wp = (i64)(skey[m - 1] >> 32);
+    if (wp >= nb) return 0;
+    if (m < M && (i64)(skey[m] >> 32) <= wp) return 0;
+    return (i64)fpre[m] - (i64)fpre[sc_wstart(wp, n_old, pcb)];
+}
+
+__global__ __launch_bounds__(kBlock) void k_scxt_count(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
+                                                      const u64* __restrict__ skey, const u32* __restrict__ fpre,
+                                                      const u32* __restrict__ ghead, int cur_on, u32* rows) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 m = n_old + j;
+    if (m > M + 1) return;
+    if (m == M + 1) { rows[j] = 0; return; }  // (rows[nn] counts windows closing after the last entry)
+    u32 r = (m < M && cur_on && ghead[m]) ? 1u : 0u;
+    r += (u32)sc_closing_keys(m, M, n_old, pcb, nb, skey, fpre);
+    rows[j] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scxt_current(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
+                                                        const u64* __restrict__ skey, const u32* __restrict__ fpre,
+                                                        const u32* __restrict__ ghead, const u32* __restrict__ base,
+                                                        const u32* __restrict__ slast, const u64* __restrict__ sval,
+                                                        const i64* __restrict__ chunk, const i64* __restrict__ send,
+                                                        const i64* __restrict__ pend_ts, const u64* __restrict__ pend_gidx,
+                                                        KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts,
+                                                        i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                                                        unsigned char* out_exp, i64* out_rep, i64* out_chunk,
+                                                        i64* out_send) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 m = n_old + j;
+    if (m >= M || !ghead[m]) return;
+    const u64 key = skey[m];
+    const i64 o = base[j] + sc_closing_keys(m, M, n_old, pcb, nb, skey, fpre);
+    const u32 l = slast[m];
+    out_ts[o] = pend_ts[l];
+    out_rep[o] = (i64)pend_gidx[l];
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
+    for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
+    for (int a = 0; a < na; a++) {
+        out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+        out_nulls[(size_t)a * T + o] = 0;
+    }
+    out_exp[o] = 0;
+    out_chunk[o] = chunk[m];
+    out_send[o] = send[m];
+}
+
+// the open window closed by a TIMER without events (sh_advance_time): its keys' EXPIRED rows
+__global__ __launch_bounds__(kBlock) void k_scx_pending_rows(i64 M, const u32* __restrict__ fe,
+                                                            const u32* __restrict__ fpre, const u32* __restrict__ lastidx,
+                                                            const u32* __restrict__ pend_pos,
+                                                            const u64* __restrict__ pend_gidx, KeyTable kt, KeyPlan kp,
+                                                            AggPlan ap, i64 now, i64 T, i64* out_ts, i64* out_keys,
+                                                            u64* out_vals, unsigned char* out_nulls,
+                                                            unsigned char* out_exp, i64* out_rep) {
+    const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M || !fe[m]) return;
+    const i64 o = fpre[m];
+    out_ts[o] = now;
+    out_rep[o] = (i64)pend_gidx[lastidx[m]];
+    i64 kv[SH_MAX_GROUP] = {0, 0};
+    unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
+    for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
+    for (int a = 0; a < ap.n; a++) {
+        out_vals[(size_t)a * T + o] = 0;
+        out_nulls[(size_t)a * T + o] = ap.kind[a] == AK_COUNT ? 0 : 1;
+    }
+    out_exp[o] = 1;
+}
+
+void launch_scxt_count(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fpre,
+                       const u32* ghead, int cur_on, u32* rows) {
+    hipLaunchKernelGGL(k_scxt_count, dim3(sc_grid(M - n_old + 2)), dim3(kBlock), 0, s, M, n_old, pcb, nb, skey, fpre,
+                       ghead, cur_on, rows);
+}
+
+void launch_scxt_rows(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u64* skey, const u32* fe,
+                      const u32* fpre, const u32* lastidx, const u32* ghead, const u32* base, const u32* slast,
+                      const u64* sval, const i64* chunk, const i64* send, const i64* bclk, const i64* pend_ts,
+                      const u64* pend_gidx, KeyTable kt, KeyPlan kp, AggPlan ap, int cur_on, i64 T, i64* out_ts,
+                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, unsigned char* out_exp, i64* out_rep,
+                      i64* out_chunk, i64* out_send) {
+    if (T <= 0) return;
+    hipLaunchKernelGGL(k_scx_expired, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, n_old, pcb, nb, skey, fe, fpre, lastidx,
+                       base, (const i64*)nullptr, send, (const i64*)nullptr, bclk, pend_gidx, kt, kp, ap, 0, 1, T,
+                       out_ts, out_keys, out_vals, out_nulls, out_exp, out_rep, out_chunk, out_send);
+    if (cur_on && M > n_old)
+        hipLaunchKernelGGL(k_scxt_current, dim3(sc_grid(M - n_old)), dim3(kBlock), 0, s, M, n_old, pcb, nb, skey, fpre,
+                           ghead, base, slast, sval, chunk, send, pend_ts, pend_gidx, kt, kp, ap.n, T, out_ts, out_keys,
+                           out_vals, out_nulls, out_exp, out_rep, out_chunk, out_send);
+}
+
+void launch_scx_pending_rows(hipStream_t s, i64 M, const u32* fe, const u32* fpre, const u32* lastidx,
+                             const u32* pend_pos, const u64* pend_gidx, KeyTable kt, KeyPlan kp, AggPlan ap, i64 now,
+                             i64 T, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                             unsigned char* out_exp, i64* out_rep) {
+    if (T <= 0) return;
+    hipLaunchKernelGGL(k_scx_pending_rows, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, fe, fpre, lastidx, pend_pos,
+                       pend_gidx, kt, kp, ap, now, T, out_ts, out_keys, out_vals, out_nulls, out_exp, out_rep);
 }
 }  // namespace shd

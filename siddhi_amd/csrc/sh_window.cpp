@@ -194,11 +194,9 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if ((!d->current_on || d->expired_on) && !(batch_win && d->partition_col < 0))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch and timeBatch (not partitioned) windows");
-    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1 &&
-                               (d->window == SH_WIN_LENGTH_BATCH || (d->current_on && !d->expired_on))))
+    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1))
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "stream.current.event runs on aggregating, non-partitioned lengthBatch (any output) or timeBatch "
-                       "(current events) windows");
+                       "stream.current.event runs on aggregating, non-partitioned lengthBatch / timeBatch windows");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
@@ -621,14 +619,15 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
             sl[i] = c;
         }
     }
-    const bool xs = q->d.expired_on && per_event;  // lengthBatch(L, true) with expired / all events
+    const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
+    const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
     const int cur_on = q->d.current_on ? 1 : 0;
     int64_t T = 0;
-    if (xs) {
+    if (xs || xt) {
         RCHK(q->scx_fe.reserve((size_t)(M + 1) * 4, false));
         RCHK(q->scx_fpre.reserve((size_t)(M + 1) * 4, false));
         RCHK(q->scx_last.reserve((size_t)M * 4, false));
-        RCHK(q->scx_rows.reserve((size_t)(nn + 1) * 4, false));
+        RCHK(q->scx_rows.reserve((size_t)(nn + 2) * 4, false));
         RCHK(q->scx_rank.reserve((size_t)std::max<int64_t>(nn, 1) * 8, false));
         RCHK(q->scx_clk.reserve((size_t)n_sends * 8, false));
         HIPCHK(hipMemsetAsync(q->scx_fe.p, 0, (size_t)(M + 1) * 4, s));
@@ -636,15 +635,27 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                          q->scx_fe.as<u32>(), q->scx_fpre.as<u32>(), q->scx_last.as<u32>());
         HIPCHK(hipMemcpyAsync(q->scx_fpre.p, q->scx_fe.p, (size_t)(M + 1) * 4, hipMemcpyDeviceToDevice, s));
         launch_scan_sum_large_u32(s, q->scx_fpre.as<u32>(), M + 1, q->sc_tmp.as<int64_t>());
-        launch_scx_count(s, M, n_old, q->sc_pcb.as<int64_t>(), q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(),
-                         q->sc_idx2.as<u32>(), q->scx_fpre.as<u32>(), cur_on, 1, q->scx_rows.as<u32>(),
-                         q->scx_rank.as<int64_t>());
-        launch_scan_sum_large_u32(s, q->scx_rows.as<u32>(), nn + 1, q->sc_tmp.as<int64_t>());
-        std::memcpy(q->sc_h.p, sl.data(), (size_t)n_sends * 8);
-        HIPCHK(hipMemcpyAsync(q->scx_clk.p, q->sc_h.p, (size_t)n_sends * 8, hipMemcpyHostToDevice, s));
+        if (xs)
+            launch_scx_count(s, M, n_old, q->sc_pcb.as<int64_t>(), q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(),
+                             q->sc_idx2.as<u32>(), q->scx_fpre.as<u32>(), cur_on, 1, q->scx_rows.as<u32>(),
+                             q->scx_rank.as<int64_t>());
+        else
+            launch_scxt_count(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->sc_skey.as<u64>(), q->scx_fpre.as<u32>(),
+                              q->sc_ghead.as<u32>(), cur_on, q->scx_rows.as<u32>());
+        const int64_t nr = xs ? nn + 1 : nn + 2;  // (timeBatch: rows[nn] = windows closing after the last entry)
+        launch_scan_sum_large_u32(s, q->scx_rows.as<u32>(), nr, q->sc_tmp.as<int64_t>());
+        if (xs) {
+            std::memcpy(q->sc_h.p, sl.data(), (size_t)n_sends * 8);
+            HIPCHK(hipMemcpyAsync(q->scx_clk.p, q->sc_h.p, (size_t)n_sends * 8, hipMemcpyHostToDevice, s));
+        } else {  // timeBatch: the clock of each window start (the TIMER chunk's clock)
+            RCHK(q->scx_clk.reserve((size_t)std::max(nb, 1) * 8, false));
+            RCHK(q->sc_h.reserve((size_t)std::max<int64_t>(nb, n_sends) * 8 + 64));
+            for (int i = 0; i < nb; i++) q->sc_h.as<int64_t>()[i] = bounds[i].clock;
+            if (nb) HIPCHK(hipMemcpyAsync(q->scx_clk.p, q->sc_h.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
+        }
         HIPCHK(hipGetLastError());
         RCHK(q->h_small_sc.reserve(64));
-        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->scx_rows.as<uint32_t>() + nn, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->scx_rows.as<uint32_t>() + nr - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         T = *q->h_small_sc.as<uint32_t>();
     } else {
@@ -678,6 +689,15 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                         q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
                         q->out_nulls.as<unsigned char>(), q->out_expired.as<unsigned char>(), q->out_rep.as<int64_t>(),
                         q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
+    } else if (xt) {
+        launch_scxt_rows(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->sc_skey.as<u64>(), q->scx_fe.as<u32>(),
+                         q->scx_fpre.as<u32>(), q->scx_last.as<u32>(), q->sc_ghead.as<u32>(), q->scx_rows.as<u32>(),
+                         q->sc_slast.as<u32>(), q->sc_sval.as<u64>(), q->sc_chunk.as<int64_t>(),
+                         q->sc_send.as<int64_t>(), q->scx_clk.as<int64_t>(), q->pend_ts.as<int64_t>(),
+                         q->pend_gidx.as<u64>(), q->kt.dev(), q->kp, q->ap, cur_on, T, q->out_ts.as<int64_t>(),
+                         q->out_keys.as<int64_t>(), q->out_vals.as<u64>(), q->out_nulls.as<unsigned char>(),
+                         q->out_expired.as<unsigned char>(), q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(),
+                         q->sc_osend.as<int64_t>());
     } else {
         launch_sc_emit(s, M, n_old, q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(),
                        q->sc_sval.as<u64>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(),
@@ -704,12 +724,98 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     for (int64_t i = 0; i < T; i++) {
         if (i + 1 == T || och[i + 1] != och[i]) {
             fo.push_back(i + 1);
-            fc.push_back(sl[osd[i]]);
+            fc.push_back(osd[i] >= 0 ? sl[osd[i]] : bounds[-osd[i] - 1].clock);
         }
     }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, q->ev_agg0, q->ev_agg1);
     q->stats.main_kernel_ms += ms;
+    if (host_out) {
+        OutHost& o = q->out;
+        o.ts.resize(T);
+        o.expired.resize(T);
+        o.rep.resize(T);
+        o.keys.resize((size_t)nk * T);
+        o.vals.resize((size_t)na * T);
+        o.nulls.resize((size_t)na * T);
+        if (T) {
+            HIPCHK(hipMemcpyAsync(o.expired.data(), q->out_expired.p, T, hipMemcpyDeviceToHost, s));
+            if (na) HIPCHK(hipMemcpyAsync(o.nulls.data(), q->out_nulls.p, (size_t)na * T, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(o.ts.data(), q->out_ts.p, T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(o.rep.data(), q->out_rep.p, T * 8, hipMemcpyDeviceToHost, s));
+            if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), q->out_keys.p, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
+            if (na) HIPCHK(hipMemcpyAsync(o.vals.data(), q->out_vals.p, (size_t)na * T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    } else {
+        q->dev_out.n_rows = T;
+    }
+    return SH_OK;
+}
+
+// timeBatch(T, true) with expired output: the open window closed by a TIMER without events
+// (sh_advance_time): one flush of its keys' EXPIRED rows (empty state) at clock `now`
+static int sc_expire_pending(sh_query* q, int64_t now, bool host_out) {
+    hipStream_t s = q->ctx->stream;
+    const int64_t M = q->n_pend;
+    const int nk = q->kp.n, na = q->ap.n;
+    RCHK(q->sc_skey.reserve((size_t)M * 8, false));
+    RCHK(q->sc_skey2.reserve((size_t)M * 8, false));
+    RCHK(q->sc_idx.reserve((size_t)M * 4, false));
+    RCHK(q->sc_idx2.reserve((size_t)M * 4, false));
+    RCHK(q->sc_chunk.reserve((size_t)M * 8, false));
+    RCHK(q->sc_send.reserve((size_t)M * 8, false));
+    RCHK(q->sc_hd.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_pos.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_starts.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->sc_tmp.reserve((size_t)((M + 1 + kTile - 1) / kTile + 16) * 8, false));
+    RCHK(q->scx_fe.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->scx_fpre.reserve((size_t)(M + 1) * 4, false));
+    RCHK(q->scx_last.reserve((size_t)M * 4, false));
+    RCHK(q->sc_pcb.reserve(8, false));
+    launch_sc_keys(s, M, M, q->sc_pcb.as<int64_t>(), 0, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(), 0, 0, 0,
+                   q->sc_skey.as<u64>(), q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>());
+    size_t tb = 0;
+    if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, M, s))
+        return sh_fail(SH_ERR_DEVICE, "stream.current: sort sizing");
+    RCHK(q->sc_sort.reserve(std::max<size_t>(tb, 16), false));
+    if (sort_u64_pairs(q->sc_sort.p, &tb, q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(), q->sc_idx.as<u32>(),
+                       q->sc_idx2.as<u32>(), M, s))
+        return sh_fail(SH_ERR_DEVICE, "stream.current: sort failed");
+    launch_rate_segments(s, M, q->sc_skey2.as<u64>(), q->sc_idx2.as<u32>(), 1, 0, q->sc_hd.as<u32>(),
+                         q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_tmp.as<int64_t>());
+    HIPCHK(hipMemsetAsync(q->scx_fe.p, 0, (size_t)(M + 1) * 4, s));
+    launch_scx_first(s, M, q->sc_hd.as<u32>(), q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_idx2.as<u32>(),
+                     q->scx_fe.as<u32>(), q->scx_fpre.as<u32>(), q->scx_last.as<u32>());
+    HIPCHK(hipMemcpyAsync(q->scx_fpre.p, q->scx_fe.p, (size_t)(M + 1) * 4, hipMemcpyDeviceToDevice, s));
+    launch_scan_sum_large_u32(s, q->scx_fpre.as<u32>(), M + 1, q->sc_tmp.as<int64_t>());
+    RCHK(q->h_small_sc.reserve(64));
+    HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->scx_fpre.as<uint32_t>() + M, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t T = *q->h_small_sc.as<uint32_t>();
+    const int64_t TC = std::max<int64_t>(T, 1);
+    RCHK(q->out_ts.reserve(TC * 8, false));
+    RCHK(q->out_keys.reserve((size_t)std::max(1, nk) * TC * 8, false));
+    RCHK(q->out_vals.reserve((size_t)std::max(1, na) * TC * 8, false));
+    RCHK(q->out_nulls.reserve((size_t)std::max(1, na) * TC, false));
+    RCHK(q->out_expired.reserve(TC, false));
+    RCHK(q->out_rep.reserve(TC * 8, false));
+    q->zeroed_nulls = nullptr;
+    q->zeroed_expired = nullptr;
+    launch_scx_pending_rows(s, M, q->scx_fe.as<u32>(), q->scx_fpre.as<u32>(), q->scx_last.as<u32>(),
+                            q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(), q->kt.dev(), q->kp, q->ap, now, T,
+                            q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
+                            q->out_nulls.as<unsigned char>(), q->out_expired.as<unsigned char>(),
+                            q->out_rep.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
+    PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
+    fo.assign(1, 0);
+    fc.clear();
+    if (T) {
+        fo.push_back(T);
+        fc.push_back(now);
+    }
     if (host_out) {
         OutHost& o = q->out;
         o.ts.resize(T);
@@ -954,7 +1060,9 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
                                    q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                                    q->pend_vals.as<u64>(), q->pend_cap, nullptr, q->pend_gidx.as<u64>(), q->seq);
             HIPCHK(hipGetLastError());
-            if (M > n_old) RCHK(sc_rows(q, b, bounds, n_old, M, cv0, clock0, seq0, host_out));
+            // (a window may close with no passing event in the push: its expired rows still go out)
+            if (M > n_old || (q->d.expired_on && !bounds.empty() && n_old > 0))
+                RCHK(sc_rows(q, b, bounds, n_old, M, cv0, clock0, seq0, host_out));
             RCHK(pending_to_front(q, M - new_pend, new_pend));
         } else {
             RCHK(grow_pending(q, new_pend, dst_base));
@@ -1071,7 +1179,10 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
         int64_t W = wfun_host(q, now);
         if (q->xmode && W > q->W_open) q->x_closes.emplace_back(W, now);
         if (W > q->W_open && q->n_pend > 0 && q->d.stream_current) {
-            q->n_pend = 0;  // RESET: the events were emitted as they arrived
+            // RESET: the events were emitted as they arrived; with expired output the TIMER chunk
+            // carries the window's keys as EXPIRED rows
+            if (q->d.expired_on) RCHK(sc_expire_pending(q, now, host_out));
+            q->n_pend = 0;
         } else if (W > q->W_open && q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{now}, windows{q->W_open};

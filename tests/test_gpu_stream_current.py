@@ -78,7 +78,20 @@ def test_lengthbatch_stream_current_expired(rt, output, L, cuts, send_size, grou
         assert out["expired"].sum() > 0
 
 
-def test_stream_current_rejects_timebatch_expired(rt):
-    spec = abi.QuerySpec(SCHEMA, "timeBatch", 4, aggs=[("count", None)], stream_current=True, output="expired")
-    with pytest.raises(rt.SiddhiError, match="stream.current"):
-        rt.GpuQuery(spec)
+@pytest.mark.parametrize("output", ["all", "expired"])
+@pytest.mark.parametrize("send_size", [1, 13, 0])
+@pytest.mark.parametrize("group_by", [True, False])
+def test_timebatch_stream_current_expired(rt, output, send_size, group_by):
+    """A window closes in the scheduler's TIMER chunk before the crossing send's own chunk: a flush of
+    its keys' EXPIRED rows (also when no event of the push passes, and at advance_time)."""
+    ts, cols = stream(30_000, 300, 19, gap_at=17_000)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 700, group_by=["k"] if group_by else (), aggs=AGGS,
+                         filter=(">", "v", -150.0), stream_current=True, output=output, key_capacity=512)
+    pushes = split_batches(SCHEMA, ts, cols, [1, 2_000, 16_999, 17_000, 25_000], send_size)
+    none_pass = abi.HostBatch(SCHEMA, ts[25_000:25_100] + 900, [cols[0][:100], np.full(100, -500.0), cols[2][:100],
+                                                                 ts[25_000:25_100] + 900], send_size)
+    pushes.insert(3, ("advance", int(ts[16_999]) + 1_500))
+    pushes.insert(6, none_pass)
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    out = both(rt, spec, pushes, label=f"timeBatch stream current {output} send {send_size}")
+    assert out["expired"].sum() > 0
