@@ -197,7 +197,12 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
             launch_rate_segments(s, m, r.skey2.as<u64>(), r.idx2.as<u32>(), N, r.kind == SH_RATE_LAST ? 1 : 0,
                                  r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.tmp.as<i64>());
             if (r.kind == SH_RATE_FIRST) {
-                RCHK(grow_table(q, r.t_keys + m));
+                // the table holds distinct keys: size it by the call's segments (its distinct keys,
+                // pos[m] after the head scan), not by its rows
+                HIPCHK(hipMemcpyAsync(r.h_small.as<char>() + 16, r.pos.as<u32>() + m, 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                const int64_t n_seg = *(const uint32_t*)(r.h_small.as<char>() + 16);
+                RCHK(grow_table(q, r.t_keys + n_seg));
                 RCHK(r.seg_c0.reserve((size_t)m * 8, false));
                 RCHK(r.seg_new.reserve((size_t)m * 4, false));
                 RCHK(r.n_keys.reserve(16, false));

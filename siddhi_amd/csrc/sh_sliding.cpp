@@ -42,6 +42,15 @@ struct SlidingImpl {
     SlInfo* h_info = nullptr;
     PinnedBuf h_up;  // pinned staging of small host->device uploads
     sh_out dev_out{};
+    // `insert expired events` / `insert all events` (sh_slx_kernels.hip): the expiry queue as a FIFO
+    // of the window's events (PM and stream index, global arrival order X0 .. G0), each ring entry's
+    // arrival index, and the scheduler's pending notify times (ascending)
+    bool xm = false;
+    DevBuf rg, upm, useq, upm2, useq2, npend, npend2;
+    int64_t x0 = 0, g0 = 0, w0 = 0, n_np = 0, np_front = 0;
+    DevBuf x_sK, x_scb, x_slast, x_cK, x_cC, x_cS, x_fire, x_keep, x_idx, x_fK, x_fC, x_fS, x_blk, x_xop, x_xch,
+        x_xts, x_xclk, x_aop, x_nexp, xr_ts, xr_rep, xr_slot, xr_ch, xr_clk, xr_exp, xr_vals, xr_nulls;
+    PinnedBuf x_h;
 };
 
 static SlState state_of(SlidingImpl* s) {
@@ -81,6 +90,8 @@ static int size_rings(sh_query* q, int64_t new_rc, bool keep = true) {
     RCHK(rpm2.reserve((size_t)n * new_rc * 8, false));
     RCHK(rval2.reserve((size_t)V * n * new_rc * 8, false));
     RCHK(dq2.reserve((size_t)F * n * new_rc * 8, false));
+    DevBuf rg2;
+    if (s->xm) RCHK(rg2.reserve((size_t)n * new_rc * 8, false));
     hipStream_t st = q->ctx->stream;
     if (s->rc > 0 && keep) {
         launch_sl_regrow(st, (const u64*)s->rpm.p, (u64*)rpm2.p, s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, 1,
@@ -89,11 +100,15 @@ static int size_rings(sh_query* q, int64_t new_rc, bool keep = true) {
                          s->rc, new_rc, false);
         launch_sl_regrow(st, s->dq.as<u64>(), dq2.as<u64>(), s->dq_head.as<int64_t>(), s->dq_len.as<int64_t>(), n, F,
                          s->rc, new_rc, true);
+        if (s->xm)
+            launch_sl_regrow(st, (const u64*)s->rg.p, (u64*)rg2.p, s->rhead.as<int64_t>(), s->rlen.as<int64_t>(), n, 1,
+                             s->rc, new_rc, false);
         HIPCHK(hipMemsetAsync(s->rhead.p, 0, n * 8, st));
         HIPCHK(hipMemsetAsync(s->dq_head.p, 0, (size_t)F * n * 8, st));
         HIPCHK(hipStreamSynchronize(st));
     }
     s->rpm = std::move(rpm2); s->rval = std::move(rval2); s->dq = std::move(dq2);
+    if (s->xm) s->rg = std::move(rg2);
     s->rc = new_rc;
     return SH_OK;
 }
@@ -102,6 +117,7 @@ int sliding_create(sh_query* q) {
     if (q->partitioned) return sh_fail(SH_ERR_UNSUPPORTED, "partitioned sliding windows are not on the GPU");
     SlidingImpl* s = new SlidingImpl();
     q->sl = s;
+    s->xm = q->d.expired_on != 0 || q->ap.n == 0;  // expired output or pass-through
     s->nslots = (int64_t)q->kt.size_ + 1;
     int F = std::max(1, q->ap.n_fields);
     int64_t n = s->nslots;
@@ -142,8 +158,14 @@ void sliding_destroy(sh_query* q) {
                       &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
                       &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
-                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk, &s->sort_tmp, &s->key_off, &s->g_rank, &s->inv, &s->rows_k};
+                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk, &s->sort_tmp, &s->key_off, &s->g_rank, &s->inv, &s->rows_k,
+                      &s->rg, &s->upm, &s->useq, &s->upm2, &s->useq2, &s->npend, &s->npend2, &s->x_sK, &s->x_scb,
+                      &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
+                      &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
+                      &s->x_nexp, &s->xr_ts, &s->xr_rep, &s->xr_slot, &s->xr_ch, &s->xr_clk, &s->xr_exp,
+                      &s->xr_vals, &s->xr_nulls};
     for (DevBuf* b : bufs) b->release();
+    s->x_h.release();
     if (s->h_info) (void)hipHostFree(s->h_info);
     delete s;
     q->sl = nullptr;
@@ -157,6 +179,10 @@ static int empty_out(sh_query* q, const sh_out** out) {
 
 static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
                           int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out);
+static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out);
+static int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out);
+static int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out,
+                          const sh_out** out);
 
 // Hashed keys of a time() window get a fresh table once more than half full: keys whose every window
 // event has expired for any later event (last PM + T <= the playback clock) are dropped — the state the
@@ -171,8 +197,12 @@ static int sliding_rekey(sh_query* q) {
     RCHK(nk.init_size((size_t)size));
     DevBuf map;
     RCHK(map.reserve((size_t)n * 4, false));
-    launch_sl_rekey_map(st, size, q->kt.dev(), nk.dev(), s->rhead.as<int64_t>(), s->rlen.as<int64_t>(),
-                        s->rpm.as<int64_t>(), s->rc, q->d.window_param, q->clock, map.as<u32>());
+    if (s->xm)
+        launch_slx_rekey_map(st, size, q->kt.dev(), nk.dev(), s->rlen.as<int64_t>(), s->cnt.as<int64_t>(),
+                             s->f.as<u64>(), n, q->ap, map.as<u32>());
+    else
+        launch_sl_rekey_map(st, size, q->kt.dev(), nk.dev(), s->rhead.as<int64_t>(), s->rlen.as<int64_t>(),
+                            s->rpm.as<int64_t>(), s->rc, q->d.window_param, q->clock, map.as<u32>());
     HIPCHK(hipGetLastError());
     RCHK(nk.check(st));
     const int64_t F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols), rc = s->rc;
@@ -181,8 +211,9 @@ static int sliding_rekey(sh_query* q) {
                      {&s->mm_has, F, 1, 0},     {&s->dq_head, F, 8, 0},    {&s->dq_len, F, 8, 0},
                      {&s->dq, F, rc * 8, 0},    {&s->rhead, 1, 8, 0},      {&s->rlen, 1, 8, 0},
                      {&s->rpm, 1, rc * 8, 0},   {&s->rval, V, rc * 8, 0},  {&s->cur_send, 1, 8, 0xff},
-                     {&s->cur_first, 1, 8, 0}};
+                     {&s->cur_first, 1, 8, 0}, {&s->rg, 1, rc * 8, 0}};
     for (const L& l : lay) {
+        if (l.b == &s->rg && !s->xm) continue;
         DevBuf nb;
         const size_t bytes = (size_t)l.outer * n * l.inner;
         RCHK(nb.reserve(std::max<size_t>(bytes, 8), false));
@@ -204,9 +235,10 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N == 0) return empty_out(q, out);
     if (N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
-    if (!q->kt.dense && q->kp.n > 0 && q->d.window == SH_WIN_TIME && q->clock_valid &&
+    if (!q->kt.dense && q->kp.n > 0 && (q->d.window == SH_WIN_TIME || s->xm) && q->clock_valid &&
         q->kt.n_keys > (int64_t)q->kt.size_ / 2)
         RCHK(sliding_rekey(q));
+    if (s->xm) return slx_run(q, b, 0, host_out, out);
     HIPCHK(hipEventRecord(q->ev_push0, st));
     ColSet cs{};
     cs.n = q->d.n_cols;
@@ -429,6 +461,22 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     }
     // flush structure: a flush per send that produced rows (one selector output chunk per send)
     int64_t n_flushes = 0;
+    RCHK(sliding_flushes(q, n_rows, &n_flushes));
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.main_kernel_bytes = M * (int64_t)(4 + 8 + 8 + 8 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 + 8 * q->ap.n);
+    return sliding_output(q, n_rows, n_flushes, want_order, host_out, out);
+}
+
+// flush offsets / clocks of n_rows output rows: a flush starts where out_send (the send, or the
+// chunk in expired mode) changes; flush_off[n_flushes] = n_rows
+static int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    int64_t n_flushes = 0;
     if (n_rows > 0) {
         int rb = (int)((n_rows + kTile - 1) / kTile);
         RCHK(s->blk_cnt.reserve((rb + 16) * 8, false));
@@ -447,12 +495,15 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, s->h_up.p, 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(q->ev_push1, st));
-    HIPCHK(hipStreamSynchronize(st));
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
-    q->stats.push_ms = ms;
-    q->stats.main_kernel_bytes = M * (int64_t)(4 + 8 + 8 + 8 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 + 8 * q->ap.n);
+    *n_flushes_out = n_flushes;
+    return SH_OK;
+}
+
+// the push's rows (device arrays of stride n_rows) and flush arrays -> host vectors or the device view
+static int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out,
+                          const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
     int nk = q->kp.n, na = q->ap.n;
     if (host_out) {
         OutHost& o = q->out;
@@ -460,7 +511,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         o.flush_offsets.resize(n_flushes + 1);
         o.flush_clock.resize(n_flushes);
         o.ts.resize(n_rows);
-        o.expired.assign(n_rows, 0);
+        o.expired.resize(n_rows);
         o.keys.resize((size_t)nk * n_rows);
         o.vals.resize((size_t)na * n_rows);
         o.nulls.resize((size_t)na * n_rows);
@@ -469,6 +520,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
             HIPCHK(hipMemcpyAsync(o.flush_offsets.data(), s->flush_off.p, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.flush_clock.data(), s->flush_clock.p, n_flushes * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.ts.data(), s->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.expired.data(), s->out_expired.p, n_rows, hipMemcpyDeviceToHost, st));
             // device arrays have stride cap == n_rows
             if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), s->out_keys.p, (size_t)nk * n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.vals.data(), s->out_vals.p, (size_t)na * n_rows * 8, hipMemcpyDeviceToHost, st));
@@ -505,7 +557,287 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     return SH_OK;
 }
 
+// ---- `insert expired events` / `insert all events` (sh_slx_kernels.hip) -----------------------------
+// One push (b) or one TIMER call (b == nullptr: the playback clock moves to `now`, sh_advance_time).
+// The window's events form one expiry queue in arrival order (TimeWindowProcessor.java:132-169); every
+// event's removal point and every operation's place in the push's operation sequence come from the
+// monotone PM / clock sequences, then one lane per key replays its adds and removes in that order.
+static int read_count(sh_query* q, const int64_t* dev, int64_t* out) {
+    SlidingImpl* s = q->sl;
+    RCHK(s->x_h.reserve(64));
+    HIPCHK(hipMemcpyAsync(s->x_h.p, dev, 8, hipMemcpyDeviceToHost, q->ctx->stream));
+    HIPCHK(hipStreamSynchronize(q->ctx->stream));
+    *out = *s->x_h.as<int64_t>();
+    return SH_OK;
+}
+
+static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    const bool ext = q->d.window == SH_WIN_EXT_TIME;
+    const int64_t T = q->d.window_param;
+    const int64_t N = b ? b->n : 0;
+    const int64_t ss = b ? b->send_size : 0;
+    const int V = std::max(1, q->ap.n_vcols);
+    if (!b) {
+        // TimestampGeneratorImpl.setCurrentTimestamp: the clock only moves forward, then onTimeChange
+        if (q->clock_valid && now < q->clock) return empty_out(q, out);
+        q->clock = now;
+        q->clock_valid = true;
+        if (s->n_np == 0) return empty_out(q, out);  // no notify time pending: no TIMER
+    }
+    if (N >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 2G events");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    WinParams wp{};
+    int nblk = 0;
+    int64_t M = 0;
+    SlInfo info{};
+    const int64_t cap = std::max<int64_t>(N, 1);
+    RCHK(s->rec_raw.reserve(cap * 4, false));
+    RCHK(s->rec_slot.reserve(cap * 4, false));
+    RCHK(s->rec_clock.reserve(cap * 8, false));
+    RCHK(s->rec_pm.reserve(cap * 8, false));
+    RCHK(s->rec_ts.reserve(cap * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    if (b) {
+        for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+        nblk = (int)((N + kTile - 1) / kTile);
+        RCHK(s->blk_pass.reserve(nblk * 8, false));
+        RCHK(s->blk_tl.reserve(nblk * 8, false));
+        RCHK(s->blk_pm.reserve(nblk * 8, false));
+        wp.kind = q->d.window;
+        wp.ts_col = q->d.ts_col;
+        wp.clock_valid = q->clock_valid;
+        wp.clock0 = q->clock;
+        wp.send_size = ss;
+        wp.N = N;
+        launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                         s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+        if (ext) RCHK(s->rec_sclk.reserve(cap * 8, false));
+        launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk,
+                          ext ? s->rec_sclk.as<int64_t>() : nullptr);
+        HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
+        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
+                       (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        RCHK(q->kt.check(st));
+        info = *s->h_info;
+        M = info.total_pass;
+        if (info.need > s->rc) {
+            int64_t nrc = s->rc;
+            while (nrc < info.need) nrc <<= 1;
+            RCHK(size_rings(q, nrc));
+        }
+    }
+    // ---- the calls of the push (sends that set the clock) and which of them fire a TIMER chunk
+    int64_t nC = 0, nF = 0, n_keep = 0;
+    if (!ext) {
+        if (b) {
+            const int64_t NS = ss > 0 ? (N + ss - 1) / ss : 1;
+            const int nbS = (int)((NS + kTile - 1) / kTile);
+            RCHK(s->x_sK.reserve(NS * 8, false));
+            RCHK(s->x_scb.reserve(NS * 8, false));
+            RCHK(s->x_slast.reserve(NS * 8, false));
+            RCHK(s->x_cK.reserve(NS * 8, false));
+            RCHK(s->x_cC.reserve(NS * 8, false));
+            RCHK(s->x_cS.reserve(NS * 8, false));
+            RCHK(s->x_blk.reserve((size_t)(nbS + 2) * 8, false));
+            launch_slx_sends(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), nblk,
+                             s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>());
+            launch_slx_compact(st, 0, nullptr, s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>(),
+                               NS, s->x_blk.as<int64_t>(), s->x_cK.as<int64_t>(), s->x_cC.as<int64_t>(),
+                               s->x_cS.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + nbS, &nC));
+        } else {
+            nC = 1;
+            RCHK(s->x_cK.reserve(8, false));
+            RCHK(s->x_cC.reserve(8, false));
+            RCHK(s->x_cS.reserve(8, false));
+            RCHK(s->x_h.reserve(64));
+            int64_t* h = s->x_h.as<int64_t>();
+            h[0] = 0; h[1] = now; h[2] = 0;
+            HIPCHK(hipMemcpyAsync(s->x_cK.p, h, 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(s->x_cC.p, h + 1, 8, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(s->x_cS.p, h + 2, 8, hipMemcpyHostToDevice, st));
+        }
+        const int64_t n_cand = s->n_np + M;
+        const int64_t n_big = std::max<int64_t>({nC, n_cand, 1});
+        RCHK(s->x_fire.reserve(nC + 16, false));
+        RCHK(s->x_keep.reserve(n_cand + 16, false));
+        RCHK(s->x_idx.reserve(n_big * 8, false));
+        RCHK(s->x_fK.reserve(std::max<int64_t>(nC, 1) * 8, false));
+        RCHK(s->x_fC.reserve(std::max<int64_t>(nC, 1) * 8, false));
+        RCHK(s->x_fS.reserve(std::max<int64_t>(nC, 1) * 8, false));
+        RCHK(s->npend2.reserve(std::max<int64_t>(n_cand, 1) * 8, false));
+        RCHK(s->x_blk.reserve((size_t)((n_big + kTile - 1) / kTile + 2) * 8, false));
+        HIPCHK(hipMemsetAsync(s->x_fire.p, 0, nC + 16, st));
+        launch_slx_notify(st, s->npend.as<int64_t>(), s->n_np, rec.pm, M, s->pm, s->x_cK.as<int64_t>(),
+                          s->x_cC.as<int64_t>(), nC, T, s->x_fire.as<unsigned char>(), s->x_keep.as<unsigned char>());
+        launch_slx_compact(st, 1, s->x_fire.as<unsigned char>(), nullptr, nullptr, nullptr, nC, s->x_blk.as<int64_t>(),
+                           nullptr, nullptr, s->x_idx.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (nC + kTile - 1) / kTile, &nF));
+        launch_slx_gather_calls(st, s->x_idx.as<int64_t>(), nF, s->x_cK.as<int64_t>(), s->x_cC.as<int64_t>(),
+                                s->x_cS.as<int64_t>(), s->x_fK.as<int64_t>(), s->x_fC.as<int64_t>(),
+                                s->x_fS.as<int64_t>());
+        launch_slx_compact(st, 1, s->x_keep.as<unsigned char>(), nullptr, nullptr, nullptr, n_cand,
+                           s->x_blk.as<int64_t>(), nullptr, nullptr, s->x_idx.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (n_cand + kTile - 1) / kTile, &n_keep));
+        launch_slx_gather_pend(st, s->x_idx.as<int64_t>(), n_keep, s->npend.as<int64_t>(), s->n_np, rec.pm,
+                               s->npend2.as<int64_t>());
+        if (!b && nF == 0) {
+            // no notify time due: the clock moved, nothing expired
+            std::swap(s->npend, s->npend2);
+            s->n_np = n_keep;
+            return empty_out(q, out);
+        }
+    }
+    // ---- the window FIFO gets the push's records; expiry points and operation indices
+    const int64_t W0 = s->w0, n_u = W0 + M;
+    s->upm.used = (size_t)W0 * 8;
+    s->useq.used = (size_t)W0 * 8;
+    RCHK(s->upm.reserve(std::max<int64_t>(n_u, 1) * 8, true));
+    RCHK(s->useq.reserve(std::max<int64_t>(n_u, 1) * 8, true));
+    launch_slx_append(st, rec.pm, rec.raw, M, q->seq, s->upm.as<int64_t>() + W0, s->useq.as<int64_t>() + W0);
+    const int64_t nu1 = std::max<int64_t>(n_u, 1);
+    RCHK(s->x_xop.reserve(nu1 * 8, false));
+    RCHK(s->x_xch.reserve(nu1 * 8, false));
+    RCHK(s->x_xts.reserve(nu1 * 8, false));
+    RCHK(s->x_xclk.reserve(nu1 * 8, false));
+    RCHK(s->x_aop.reserve(cap * 8, false));
+    RCHK(s->x_nexp.reserve(8, false));
+    HIPCHK(hipMemsetAsync(s->x_nexp.p, 0, 8, st));
+    launch_slx_expiry(st, s->upm.as<int64_t>(), n_u, W0, M, rec.clock, ext ? s->rec_sclk.as<int64_t>() : nullptr,
+                      rec.raw, ss, s->x_fK.as<int64_t>(), s->x_fC.as<int64_t>(), s->x_fS.as<int64_t>(), nF, T,
+                      s->x_xop.as<u64>(), s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(),
+                      (unsigned long long*)s->x_nexp.p);
+    launch_slx_aop(st, rec.clock, M, s->upm.as<int64_t>(), n_u, W0, T, s->x_aop.as<u64>());
+    // the push's records sorted stably by key slot: each key's adds in arrival order
+    RCHK(s->ranks.reserve(cap * 4, false));
+    RCHK(s->p_slot.reserve(cap * 4, false));
+    if (M > 0 && q->ap.n > 0) {
+        size_t tb = 0;
+        if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+    }
+    RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+    RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+    launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    int64_t R = 0;
+    RCHK(read_count(q, (const int64_t*)s->x_nexp.p, &R));
+    // ---- the replay (one lane per key slot) writes one row per (chunk, key) at its operation index
+    const int64_t n_ops = M + R;
+    const int na = q->ap.n;
+    const int64_t oc = std::max<int64_t>(n_ops, 1);
+    RCHK(s->flags.reserve(oc + 16, false));
+    RCHK(s->xr_ts.reserve(oc * 8, false));
+    RCHK(s->xr_rep.reserve(oc * 8, false));
+    RCHK(s->xr_slot.reserve(oc * 4, false));
+    RCHK(s->xr_ch.reserve(oc * 8, false));
+    RCHK(s->xr_clk.reserve(oc * 8, false));
+    RCHK(s->xr_exp.reserve(oc, false));
+    RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * oc * 8, false));
+    RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * oc, false));
+    HIPCHK(hipMemsetAsync(s->flags.p, 0, oc + 16, st));
+    SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                 s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                 s->xr_nulls.as<unsigned char>(), oc};
+    HIPCHK(hipEventRecord(q->ev_agg0, st));
+    if (q->ap.n == 0)
+        launch_slx_pass(st, rec, M, s->x_aop.as<u64>(), s->x_xop.as<u64>(), s->x_xch.as<int64_t>(),
+                        s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, q->seq, ss,
+                        q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+    else
+    launch_slx_walk(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
+                    s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u,
+                    s->x0, s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on,
+                    q->d.expired_on, rows, s->flags.as<unsigned char>());
+    HIPCHK(hipEventRecord(q->ev_agg1, st));
+    HIPCHK(hipGetLastError());
+    // ---- rows in operation order, one flush per chunk
+    int64_t n_rows = 0;
+    const int fblk = (int)((n_ops + kTile - 1) / kTile);
+    if (n_ops > 0) {
+        RCHK(s->blk_cnt.reserve((size_t)(fblk + 16) * 8, false));
+        launch_count_flags(st, s->flags.as<unsigned char>(), n_ops, s->blk_cnt.as<int64_t>(), fblk);
+        HIPCHK(hipMemsetAsync(s->blk_cnt.as<int64_t>() + fblk, 0, 8, st));
+        launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk + 1);
+        RCHK(read_count(q, s->blk_cnt.as<int64_t>() + fblk, &n_rows));
+    }
+    float kms = 0;
+    (void)hipEventElapsedTime(&kms, q->ev_agg0, q->ev_agg1);
+    q->stats.main_kernel_ms = kms;
+    {
+        const int64_t rcap = std::max<int64_t>(n_rows, 1);
+        RCHK(s->out_ts.reserve(rcap * 8, false));
+        RCHK(s->out_keys.reserve((size_t)std::max(1, q->kp.n) * rcap * 8, false));
+        RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * rcap * 8, false));
+        RCHK(s->out_nulls.reserve((size_t)std::max(na, 1) * rcap, false));
+        RCHK(s->out_send.reserve(rcap * 8, false));
+        RCHK(s->out_clock.reserve(rcap * 8, false));
+        RCHK(s->out_expired.reserve(rcap, false));
+        RCHK(s->out_rep.reserve(rcap * 8, false));
+        if (n_rows > 0)
+            launch_slx_emit(st, s->flags.as<unsigned char>(), n_ops, s->blk_cnt.as<int64_t>(), fblk, rows, na,
+                            q->kt.dev(), q->kp, rcap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(),
+                            s->out_vals.as<u64>(), s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
+                            s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());
+        HIPCHK(hipGetLastError());
+    }
+    int64_t n_flushes = 0;
+    RCHK(sliding_flushes(q, n_rows, &n_flushes));
+    // ---- the state moves on: unexpired FIFO tail, pending notify times, counters, clock
+    const int64_t new_w = n_u - R;
+    RCHK(s->upm2.reserve(std::max<int64_t>(new_w, 1) * 8, false));
+    RCHK(s->useq2.reserve(std::max<int64_t>(new_w, 1) * 8, false));
+    launch_slx_shift(st, s->upm.as<int64_t>(), s->useq.as<int64_t>(), R, new_w, s->upm2.as<int64_t>(),
+                     s->useq2.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    std::swap(s->upm, s->upm2);
+    std::swap(s->useq, s->useq2);
+    if (!ext) {
+        std::swap(s->npend, s->npend2);
+        s->n_np = n_keep;
+    }
+    s->x0 += R;
+    s->g0 += M;
+    s->w0 = new_w;
+    if (b) {
+        q->seq += N;
+        q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+        q->clock_valid = true;
+        s->pm = std::max(s->pm, info.max_pm);
+        s->send_base += ss > 0 ? (N + ss - 1) / ss : 1;
+        q->stats.events = N;
+    }
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.main_kernel_bytes = n_ops * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
+    return sliding_output(q, n_rows, n_flushes, false, host_out || !b, out);
+}
+
 int sliding_advance(sh_query* q, int64_t now, const sh_out** out) {
+    // expired output: the TIMER chunk's expired events (Scheduler.onTimeChange -> the window)
+    if (q->sl->xm && q->d.window == SH_WIN_TIME) return slx_run(q, nullptr, now, true, out);
     // expiry is applied lazily at each key's next event; with current-events-only output the
     // timer path changes no visible result, only the clock (TimestampGeneratorImpl :104-122)
     if (!q->clock_valid || now >= q->clock) {

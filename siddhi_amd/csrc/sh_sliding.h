@@ -94,4 +94,49 @@ void launch_sl_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new_
                          const i64* rpm, i64 rc, i64 T, i64 bound, u32* map);
 void launch_sl_rekey_copy(hipStream_t s, const void* src, void* dst, i64 outer, i64 n, i64 inner, const u32* map);
 
+// ---- expired / all-events output of time / externalTime windows (sh_slx_kernels.hip) ----
+// rows indexed by operation index (the position of the row's first qualifying operation)
+struct SlxRows {
+    i64* ts;
+    i64* rep;
+    u32* slot;
+    i64* ch;   // chunk: 2 * send (timer chunk before the send) or 2 * send + 1 (the send's own chunk)
+    i64* clk;  // flush clock of the chunk
+    unsigned char* exp;
+    u64* vals;
+    unsigned char* nulls;
+    i64 cap;
+};
+void launch_slx_sends(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_pass_pre,
+                      const i64* blk_tl_pre, int nblk, i64* sK, i64* scb, i64* slast);
+// kind 0: the calls among n sends -> (oK, oC, oS); kind 1: indices of the set flags -> oS.
+// blk: (n + kTile - 1) / kTile + 1 entries; blk[last] = the count
+void launch_slx_compact(hipStream_t s, int kind, const unsigned char* flags, const i64* sK, const i64* scb,
+                        const i64* slast, i64 n, i64* blk, i64* oK, i64* oC, i64* oS);
+void launch_slx_notify(hipStream_t s, const i64* pend, i64 n_pend, const i64* pm, i64 M, i64 pm0, const i64* cK,
+                       const i64* cC, i64 nC, i64 T, unsigned char* fire, unsigned char* keep);
+void launch_slx_gather_calls(hipStream_t s, const i64* idx, i64 n, const i64* cK, const i64* cC, const i64* cS, i64* fK,
+                             i64* fC, i64* fS);
+void launch_slx_gather_pend(hipStream_t s, const i64* idx, i64 n, const i64* pend, i64 n_pend, const i64* pm,
+                            i64* out);
+void launch_slx_append(hipStream_t s, const i64* pm, const u32* raw, i64 M, i64 seq_base, i64* upm, i64* useq);
+void launch_slx_expiry(hipStream_t s, const i64* upm, i64 n_u, i64 W0, i64 M, const i64* rclk, const i64* rsclk,
+                       const u32* raw, i64 send_size, const i64* fK, const i64* fC, const i64* fS, i64 nF, i64 T,
+                       u64* xop, i64* xch, i64* xts, i64* xclk, unsigned long long* n_exp);
+void launch_slx_aop(hipStream_t s, const i64* rclk, i64 M, const i64* upm, i64 n_u, i64 W0, i64 T, u64* aop);
+void launch_slx_keyoff(hipStream_t s, const u32* slot_cnt, i64 nslots, u32* key_off, i64* tmp);
+void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                     const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
+                     i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
+                     int exp_on, SlxRows rows, unsigned char* flags);
+void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
+                     const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
+                     SlxRows rows, unsigned char* flags);
+void launch_slx_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
+                     int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                     unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
+void launch_slx_shift(hipStream_t s, const i64* upm, const i64* useq, i64 from, i64 n, i64* opm, i64* oseq);
+void launch_slx_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new_kt, const i64* rlen, const i64* cnt,
+                          const u64* f, i64 nslots, AggPlan ap, u32* map);
+
 }  // namespace shd

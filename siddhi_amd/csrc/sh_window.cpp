@@ -169,10 +169,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     for (int c = 0; c < d->n_cols; c++)
         if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
     const bool batch_win = d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME_BATCH;
-    const bool pass_through = d->n_aggs == 0 && d->n_group_by == 0 && batch_win && d->partition_col < 0;
+    const bool pass_through = d->n_aggs == 0 && d->n_group_by == 0 && d->partition_col < 0 &&
+                              (batch_win || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME);
     if ((d->n_aggs < 1 && !pass_through) || d->n_aggs > SH_MAX_AGGS)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "GPU path runs aggregation queries (1..8 aggregators) or pass-through lengthBatch/timeBatch");
+                       "GPU path runs aggregation queries (1..8 aggregators) or pass-through lengthBatch / timeBatch / "
+                       "time / externalTime windows");
     if (d->window != SH_WIN_LENGTH_BATCH && d->window != SH_WIN_TIME_BATCH && d->window != SH_WIN_TIME &&
         d->window != SH_WIN_EXT_TIME_BATCH && d->window != SH_WIN_EXT_TIME)
         return sh_fail(SH_ERR_UNSUPPORTED,
@@ -191,9 +193,11 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
     if (!d->current_on && !d->expired_on) return sh_fail(SH_ERR_INVALID, "query emits neither current nor expired events");
-    if ((!d->current_on || d->expired_on) && !(batch_win && d->partition_col < 0))
+    const bool sliding_win = d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME;
+    if ((!d->current_on || d->expired_on) && !((batch_win || sliding_win) && d->partition_col < 0))
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "expired / all-events output runs on lengthBatch and timeBatch (not partitioned) windows");
+                       "expired / all-events output runs on lengthBatch, timeBatch, time and externalTime "
+                       "(not partitioned) windows");
     if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "stream.current.event runs on aggregating, non-partitioned lengthBatch / timeBatch windows");

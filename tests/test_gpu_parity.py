@@ -28,8 +28,8 @@ def both(rt, spec, pushes, rtol=None, label=""):
     return gout
 
 
-# ---- reference KATs that the GPU path runs: aggregating or pass-through lengthBatch / timeBatch with
-# current, expired or all-events output; aggregating sliding time windows with current events ----
+# ---- reference KATs that the GPU path runs: aggregating or pass-through lengthBatch / timeBatch /
+# time / externalTime windows with current, expired or all-events output ----
 def _gpu_runs(c):
     q = c.get("query", {})
     if c.get("kind") == "aggregation":
@@ -39,7 +39,9 @@ def _gpu_runs(c):
             q.get("output", "current") == "current" or q.get("window") == "lengthBatch")
     if q.get("window") in ("lengthBatch", "timeBatch"):
         return bool(q.get("aggs")) or not q.get("group_by")
-    return q.get("window") == "time" and bool(q.get("aggs")) and q.get("output", "current") == "current"
+    if q.get("window") in ("time", "externalTime"):
+        return not q.get("partition") and (bool(q.get("aggs")) or not q.get("group_by"))
+    return False
 
 
 GPU_KATS = [c for c in kat_runner.load_cases() if _gpu_runs(c)]
