@@ -1,0 +1,365 @@
+// sh_plane.cpp — `partition with (p of S) begin from S[cond]#window.lengthBatch(L) | time(T) select
+// [p,] aggs [group by p] insert [current|all|expired] events into O; end` on the GPU.
+//
+// PartitionStreamReceiver.receive (core/partition/PartitionStreamReceiver.java:176-272) gives every
+// partition its own window and aggregator states (PartitionRuntimeImpl.initPartition :346-367). With
+// the group key equal to the partition key (or no group-by) a selector chunk holds one key, so each
+// partition is an independent sequential machine: one GPU lane per partition replays it
+// (sh_plane_kernels.hip). Every chunk yields at most one row and is its own flush:
+//  * lengthBatch: each batch a partition completes (LengthBatchWindowProcessor.processFullBatchEvents
+//    :206-243), at its L-th event's position in the stream;
+//  * time: each run of consecutive same-partition events of a send (the receiver's chunk), and each
+//    TIMER call the Scheduler fires for the partition (Scheduler.onTimeChange :71-104). Which partition
+//    fires at which call is the Scheduler's own logic — notify times per partition, a TreeMultimap keyed
+//    by due time whose equal keys keep only the first-created partition's state — and runs here on the
+//    host over the device-computed notify registrations; the windows and aggregators stay on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "sh_sliding_impl.h"
+
+using namespace shd;
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t _e = (x);                                                                               \
+        if (_e != hipSuccess) return sh_fail(SH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+#define RCHK(x)            \
+    do {                   \
+        int _r = (x);      \
+        if (_r) return _r; \
+    } while (0)
+
+static int fill(DevBuf& b, size_t bytes, int v) {
+    RCHK(b.reserve(std::max<size_t>(bytes, 8), false));
+    HIPCHK(hipMemsetAsync(b.p, v, std::max<size_t>(bytes, 8), g_stream));
+    return SH_OK;
+}
+
+int plane_create(sh_query* q) {
+    SlidingImpl* s = q->sl;
+    s->lane = q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
+    s->nk_out = q->d.n_group_by;
+    const size_t n = (size_t)s->nslots;
+    RCHK(fill(s->pl_last_ts, n * 8, 0x80));  // lastTimestamp = Long.MIN_VALUE (0x8080... < any real ts)
+    RCHK(fill(s->pl_last_seq, n * 8, 0));
+    RCHK(fill(s->pl_prev_seq, n * 8, 0xff));  // -1: no batch flushed yet
+    RCHK(fill(s->pl_first, n * 8, 0xff));     // creation order: none yet
+    if (s->lane == 2 && !s->rg.p) RCHK(s->rg.reserve(n * s->rc * 8, false));
+    return SH_OK;
+}
+
+// host copy of n i64 from the device
+static int d2h(sh_query* q, std::vector<int64_t>& v, const void* dev, int64_t n) {
+    v.resize((size_t)std::max<int64_t>(n, 0));
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(v.data(), dev, (size_t)n * 8, hipMemcpyDeviceToHost, q->ctx->stream));
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+    }
+    return SH_OK;
+}
+
+static int h2d(sh_query* q, DevBuf& b, const std::vector<int64_t>& v) {
+    RCHK(b.reserve(std::max<size_t>(v.size(), 1) * 8, false));
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), v.size() * 8, hipMemcpyHostToDevice, q->ctx->stream));
+    HIPCHK(hipStreamSynchronize(q->ctx->stream));  // v is pageable and may be freed after the call
+    return SH_OK;
+}
+
+struct Firing {
+    int64_t send, clock, K;
+    uint32_t slot;
+};
+
+// Scheduler.onTimeChange at one call (clock c): the armed partitions whose front notify time is due,
+// one per distinct due time (TreeMultimap<Long, SchedulerState> with compareTo() == 0 keeps the first
+// put, i.e. the first-created partition), each popping all of its due times (sendTimerEvents :171-209).
+static void sched_call(SlidingImpl* s, int64_t send, int64_t c, int64_t K, std::vector<Firing>& out) {
+    std::vector<std::tuple<int64_t, uint64_t, uint32_t>> win;
+    int64_t last = 0;
+    bool any = false;
+    for (auto it = s->pl_armed.begin(); it != s->pl_armed.end() && std::get<0>(*it) <= c; ++it) {
+        if (!any || std::get<0>(*it) != last) win.push_back(*it);
+        last = std::get<0>(*it);
+        any = true;
+    }
+    for (auto& w : win) {
+        s->pl_armed.erase(w);
+        const uint32_t slot = std::get<2>(w);
+        auto& pend = s->pl_pend[slot];
+        while (!pend.empty() && pend.front() <= c) pend.pop_front();
+        out.push_back(Firing{send, c, K, slot});
+        if (pend.empty()) s->pl_pend.erase(slot);
+        else s->pl_armed.insert(std::make_tuple(pend.front(), std::get<1>(w), slot));
+    }
+}
+
+// Scheduler.notifyAt (:107-121): the time joins the partition's queue; a partition with a due time is armed
+static void sched_register(SlidingImpl* s, uint32_t slot, int64_t t, uint64_t ckey) {
+    auto& pend = s->pl_pend[slot];
+    if (pend.empty()) s->pl_armed.insert(std::make_tuple(t, ckey, slot));
+    pend.push_back(t);
+}
+
+// Lane pass of the push: records of M passing events sorted by slot (b == null: a TIMER call at `now`).
+static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    const bool tm = s->lane == 2, sched = tm && q->d.expired_on;
+    const int64_t N = b ? b->n : 0, ss = b ? b->send_size : 0, T = q->d.window_param;
+    const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    if (!b) {
+        if (q->clock_valid && now < q->clock) return empty_out(q, out);
+        q->clock = now;
+        q->clock_valid = true;
+        if (!sched || s->pl_armed.empty() || std::get<0>(*s->pl_armed.begin()) > now) return empty_out(q, out);
+    }
+    if (N >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 2G events");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    const int64_t cap = std::max<int64_t>(N, 1);
+    RCHK(s->rec_raw.reserve(cap * 4, false));
+    RCHK(s->rec_slot.reserve(cap * 4, false));
+    RCHK(s->rec_clock.reserve(cap * 8, false));
+    RCHK(s->rec_pm.reserve(cap * 8, false));
+    RCHK(s->rec_ts.reserve(cap * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    WinParams wp{};
+    int nblk = 0;
+    int64_t M = 0;
+    SlInfo info{};
+    if (b) {
+        for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+        nblk = (int)((N + kTile - 1) / kTile);
+        RCHK(s->blk_pass.reserve(nblk * 8, false));
+        RCHK(s->blk_tl.reserve(nblk * 8, false));
+        RCHK(s->blk_pm.reserve(nblk * 8, false));
+        wp.kind = SH_WIN_TIME;  // the clock / pass-count prefix of the sliding path
+        wp.clock_valid = q->clock_valid;
+        wp.clock0 = q->clock;
+        wp.send_size = ss;
+        wp.N = N;
+        launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                         s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+        launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+        if (sched)
+            launch_pl_first_seen(st, cs, q->kp, q->kt.dev(), N, q->seq, (unsigned long long*)s->pl_first.p);
+        HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
+        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
+                       (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        RCHK(q->kt.check(st));
+        info = *s->h_info;
+        M = info.total_pass;
+        if (tm && info.need > s->rc) {
+            int64_t nrc = s->rc;
+            while (nrc < info.need) nrc <<= 1;
+            RCHK(size_rings(q, nrc));
+        }
+    }
+    // each partition's records in stream order
+    RCHK(s->ranks.reserve(cap * 4, false));
+    RCHK(s->p_slot.reserve(cap * 4, false));
+    if (M > 0) {
+        size_t tb = 0;
+        if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+    }
+    RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+    RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+    launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
+    HIPCHK(hipGetLastError());
+
+    // ---- time windows with expired output: the Scheduler's TIMER calls per partition
+    std::vector<Firing> fire;
+    if (sched) {
+        std::vector<int64_t> calls_s, calls_c, calls_k, reg_r;
+        if (b) {
+            const int64_t NS = ss > 0 ? (N + ss - 1) / ss : 1;
+            const int nbS = (int)((NS + kTile - 1) / kTile);
+            RCHK(s->x_sK.reserve(NS * 8, false));
+            RCHK(s->x_scb.reserve(NS * 8, false));
+            RCHK(s->x_slast.reserve(NS * 8, false));
+            RCHK(s->x_cK.reserve(NS * 8, false));
+            RCHK(s->x_cC.reserve(NS * 8, false));
+            RCHK(s->x_cS.reserve(NS * 8, false));
+            RCHK(s->x_blk.reserve((size_t)((std::max(NS, M) + kTile - 1) / kTile + 2) * 8, false));
+            launch_slx_sends(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), nblk,
+                             s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>());
+            launch_slx_compact(st, 0, nullptr, s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>(),
+                               NS, s->x_blk.as<int64_t>(), s->x_cK.as<int64_t>(), s->x_cC.as<int64_t>(),
+                               s->x_cS.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            int64_t nC = 0;
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + nbS, &nC));
+            RCHK(d2h(q, calls_s, s->x_cS.p, nC));
+            RCHK(d2h(q, calls_c, s->x_cC.p, nC));
+            RCHK(d2h(q, calls_k, s->x_cK.p, nC));
+            // notify registrations: the records that raise their partition's lastTimestamp
+            RCHK(s->pl_reg.reserve(cap + 16, false));
+            launch_pl_notify(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec.ts, s->pl_last_ts.as<int64_t>(),
+                             s->pl_reg.as<unsigned char>());
+            RCHK(s->x_idx.reserve(cap * 8, false));
+            launch_slx_compact(st, 1, s->pl_reg.as<unsigned char>(), nullptr, nullptr, nullptr, M,
+                               s->x_blk.as<int64_t>(), nullptr, nullptr, s->x_idx.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            int64_t n_reg = 0;
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + (M + kTile - 1) / kTile, &n_reg));
+            RCHK(d2h(q, reg_r, s->x_idx.p, n_reg));
+        } else {
+            calls_s.push_back(0);
+            calls_c.push_back(now);
+            calls_k.push_back(0);
+        }
+        std::vector<uint32_t> raw(M), slot(M);
+        std::vector<int64_t> tsv(M), first;
+        if (!reg_r.empty()) {
+            HIPCHK(hipMemcpyAsync(raw.data(), rec.raw, M * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(slot.data(), rec.slot, M * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(tsv.data(), rec.ts, M * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        RCHK(d2h(q, first, s->pl_first.p, s->nslots));
+        // replay the Scheduler: registrations of a send happen after that send's call
+        size_t j = 0;
+        for (size_t c = 0; c < calls_s.size(); c++) {
+            for (; j < reg_r.size(); j++) {
+                const uint32_t r = (uint32_t)reg_r[j];
+                const int64_t snd = ss > 0 ? (int64_t)raw[r] / ss : 0;
+                if (snd >= calls_s[c]) break;
+                sched_register(s, slot[r], tsv[r] + T, (uint64_t)first[slot[r]]);
+            }
+            if (!s->pl_armed.empty() && std::get<0>(*s->pl_armed.begin()) <= calls_c[c])
+                sched_call(s, calls_s[c], calls_c[c], calls_k[c], fire);
+        }
+        for (; j < reg_r.size(); j++) {
+            const uint32_t r = (uint32_t)reg_r[j];
+            sched_register(s, slot[r], tsv[r] + T, (uint64_t)first[slot[r]]);
+        }
+    }
+    const int64_t nF = (int64_t)fire.size();
+    if (nF > 0) {
+        // per partition its firings in order; positions K + t in the push's output order
+        std::vector<int64_t> fsend(nF), order(nF), toff(s->nslots + 1, 0), tsend(nF), tclk(nF), tpos(nF);
+        for (int64_t t = 0; t < nF; t++) { fsend[t] = fire[t].send; toff[fire[t].slot + 1]++; }
+        for (int64_t k = 0; k < s->nslots; k++) toff[k + 1] += toff[k];
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t c) { return fire[a].slot < fire[c].slot; });
+        for (int64_t i = 0; i < nF; i++) {
+            const Firing& f = fire[order[i]];
+            tsend[i] = f.send;
+            tclk[i] = f.clock;
+            tpos[i] = f.K + order[i];
+        }
+        RCHK(h2d(q, s->pl_toff, toff));
+        RCHK(h2d(q, s->pl_tsend, tsend));
+        RCHK(h2d(q, s->pl_tclk, tclk));
+        RCHK(h2d(q, s->pl_tpos, tpos));
+        RCHK(h2d(q, s->pl_fsend, fsend));
+    }
+    // ---- the lanes
+    const int64_t n_pos = M + nF, pc = std::max<int64_t>(n_pos, 1);
+    RCHK(s->flags.reserve(pc + 16, false));
+    RCHK(s->xr_ts.reserve(pc * 8, false));
+    RCHK(s->xr_rep.reserve(pc * 8, false));
+    RCHK(s->xr_slot.reserve(pc * 4, false));
+    RCHK(s->xr_ch.reserve(pc * 8, false));
+    RCHK(s->xr_clk.reserve(pc * 8, false));
+    RCHK(s->xr_exp.reserve(pc, false));
+    RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * pc * 8, false));
+    RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * pc, false));
+    HIPCHK(hipMemsetAsync(s->flags.p, 0, pc + 16, st));
+    SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                 s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                 s->xr_nulls.as<unsigned char>(), pc};
+    HIPCHK(hipEventRecord(q->ev_agg0, st));
+    if (!tm) {
+        launch_pl_walk_lb(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, T, q->seq, state_of(s),
+                          s->pl_last_ts.as<int64_t>(), s->pl_last_seq.as<int64_t>(), s->pl_prev_seq.as<int64_t>(), q->ap,
+                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+    } else {
+        if (b) {
+            RCHK(s->pl_start.reserve(cap + 16, false));
+            RCHK(s->pl_run.reserve(cap * 8, false));
+            RCHK(s->x_blk.reserve((size_t)((N + kTile - 1) / kTile + 2) * 8, false));
+            launch_pl_runs(st, cs, q->d.partition_col, N, ss, s->pl_start.as<unsigned char>(), s->x_blk.as<int64_t>(),
+                           s->pl_run.as<int64_t>());
+        }
+        launch_pl_walk_tm(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->pl_run.as<int64_t>(), T, q->seq,
+                          ss, nF ? s->pl_toff.as<int64_t>() : nullptr, s->pl_tsend.as<int64_t>(), s->pl_tclk.as<int64_t>(),
+                          s->pl_tpos.as<int64_t>(), s->pl_fsend.as<int64_t>(), nF, state_of(s), s->rg.as<int64_t>(), q->ap,
+                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+    }
+    HIPCHK(hipEventRecord(q->ev_agg1, st));
+    HIPCHK(hipGetLastError());
+    // ---- rows in position order, one flush each
+    int64_t n_rows = 0;
+    const int fblk = (int)((n_pos + kTile - 1) / kTile);
+    if (n_pos > 0) {
+        RCHK(s->blk_cnt.reserve((size_t)(fblk + 16) * 8, false));
+        launch_count_flags(st, s->flags.as<unsigned char>(), n_pos, s->blk_cnt.as<int64_t>(), fblk);
+        HIPCHK(hipMemsetAsync(s->blk_cnt.as<int64_t>() + fblk, 0, 8, st));
+        launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk + 1);
+        RCHK(read_count(q, s->blk_cnt.as<int64_t>() + fblk, &n_rows));
+    }
+    float kms = 0;
+    (void)hipEventElapsedTime(&kms, q->ev_agg0, q->ev_agg1);
+    q->stats.main_kernel_ms = kms;
+    {
+        const int64_t rcap = std::max<int64_t>(n_rows, 1);
+        RCHK(s->out_ts.reserve(rcap * 8, false));
+        RCHK(s->out_keys.reserve((size_t)std::max(1, q->kp.n) * rcap * 8, false));
+        RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * rcap * 8, false));
+        RCHK(s->out_nulls.reserve((size_t)std::max(na, 1) * rcap, false));
+        RCHK(s->out_send.reserve(rcap * 8, false));
+        RCHK(s->out_clock.reserve(rcap * 8, false));
+        RCHK(s->out_expired.reserve(rcap, false));
+        RCHK(s->out_rep.reserve(rcap * 8, false));
+        if (n_rows > 0)
+            launch_pl_emit(st, s->flags.as<unsigned char>(), n_pos, s->blk_cnt.as<int64_t>(), fblk, rows, na, s->nk_out,
+                           q->kt.dev(), q->kp, rcap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(),
+                           s->out_vals.as<u64>(), s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
+                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());
+        HIPCHK(hipGetLastError());
+    }
+    int64_t n_flushes = 0;
+    RCHK(sliding_flushes(q, n_rows, &n_flushes));
+    if (b) {
+        q->seq += N;
+        q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+        q->clock_valid = true;
+        q->stats.events = N;
+    }
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
+    return sliding_output(q, n_rows, n_flushes, false, host_out || !b, out);
+}
+
+int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
+    if (b->n == 0) return empty_out(q, out);
+    return plane_run(q, b, 0, host_out, out);
+}
+
+int plane_advance(sh_query* q, int64_t now, const sh_out** out) { return plane_run(q, nullptr, now, true, out); }

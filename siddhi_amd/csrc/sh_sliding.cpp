@@ -28,32 +28,9 @@ using namespace shd;
         if (_r) return _r; \
     } while (0)
 
-struct SlidingImpl {
-    int64_t nslots = 0, rc = 0;
-    int P = 1, logP = 0;
-    int64_t pm = INT64_MIN;   // PM carried across pushes
-    int64_t send_base = 0;    // global send number of the push's first send
-    DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
-    // per push scratch
-    DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
-        tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_rep, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
-        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock, sort_tmp,
-        key_off, g_rank, inv, rows_k;
-    SlInfo* h_info = nullptr;
-    PinnedBuf h_up;  // pinned staging of small host->device uploads
-    sh_out dev_out{};
-    // `insert expired events` / `insert all events` (sh_slx_kernels.hip): the expiry queue as a FIFO
-    // of the window's events (PM and stream index, global arrival order X0 .. G0), each ring entry's
-    // arrival index, and the scheduler's pending notify times (ascending)
-    bool xm = false;
-    DevBuf rg, upm, useq, upm2, useq2, npend, npend2;
-    int64_t x0 = 0, g0 = 0, w0 = 0, n_np = 0, np_front = 0;
-    DevBuf x_sK, x_scb, x_slast, x_cK, x_cC, x_cS, x_fire, x_keep, x_idx, x_fK, x_fC, x_fS, x_blk, x_xop, x_xch,
-        x_xts, x_xclk, x_aop, x_nexp, xr_ts, xr_rep, xr_slot, xr_ch, xr_clk, xr_exp, xr_vals, xr_nulls;
-    PinnedBuf x_h;
-};
+#include "sh_sliding_impl.h"
 
-static SlState state_of(SlidingImpl* s) {
+SlState state_of(SlidingImpl* s) {
     SlState S;
     S.nslots = s->nslots;
     S.rc = s->rc;
@@ -82,7 +59,7 @@ static int alloc_zero(DevBuf& b, size_t bytes, int fill = 0) {
 // (re)size the per-key rings and deques to capacity rc (power of two), keeping their contents
 // (keep = false: fresh buffers, e.g. before a restore overwrites them — the live rings may hold more
 // entries than the new capacity, so they must not be copied over)
-static int size_rings(sh_query* q, int64_t new_rc, bool keep = true) {
+int size_rings(sh_query* q, int64_t new_rc, bool keep) {
     SlidingImpl* s = q->sl;
     int F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols);
     int64_t n = s->nslots;
@@ -117,7 +94,9 @@ int sliding_create(sh_query* q) {
     if (q->partitioned) return sh_fail(SH_ERR_UNSUPPORTED, "partitioned sliding windows are not on the GPU");
     SlidingImpl* s = new SlidingImpl();
     q->sl = s;
-    s->xm = q->d.expired_on != 0 || q->ap.n == 0;  // expired output or pass-through
+    const bool plane = q->d.partition_col >= 0;  // partitioned lengthBatch / time keyed by the partition
+    // expired output, pass-through, and the partition lanes' time windows keep each ring entry's 2nd word
+    s->xm = q->d.expired_on != 0 || q->ap.n == 0 || (plane && q->d.window == SH_WIN_TIME);
     s->nslots = (int64_t)q->kt.size_ + 1;
     int F = std::max(1, q->ap.n_fields);
     int64_t n = s->nslots;
@@ -145,6 +124,7 @@ int sliding_create(sh_query* q) {
     while ((1 << s->logP) < P) s->logP++;
     (void)hipEventCreate(&q->ev_push0); (void)hipEventCreate(&q->ev_push1);
     (void)hipEventCreate(&q->ev_agg0); (void)hipEventCreate(&q->ev_agg1);
+    if (plane) RCHK(plane_create(q));
     return SH_OK;
 }
 
@@ -163,7 +143,9 @@ void sliding_destroy(sh_query* q) {
                       &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
                       &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
                       &s->x_nexp, &s->xr_ts, &s->xr_rep, &s->xr_slot, &s->xr_ch, &s->xr_clk, &s->xr_exp,
-                      &s->xr_vals, &s->xr_nulls};
+                      &s->xr_vals, &s->xr_nulls, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_first,
+                      &s->pl_start, &s->pl_run, &s->pl_reg, &s->pl_toff, &s->pl_tsend, &s->pl_tclk, &s->pl_tpos,
+                      &s->pl_fsend};
     for (DevBuf* b : bufs) b->release();
     s->x_h.release();
     if (s->h_info) (void)hipHostFree(s->h_info);
@@ -171,7 +153,7 @@ void sliding_destroy(sh_query* q) {
     q->sl = nullptr;
 }
 
-static int empty_out(sh_query* q, const sh_out** out) {
+int empty_out(sh_query* q, const sh_out** out) {
     q->out.reset();
     *out = q->out.view(q->kp.n, q->ap.n, q->vtypes);
     return SH_OK;
@@ -180,9 +162,6 @@ static int empty_out(sh_query* q, const sh_out** out) {
 static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
                           int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out);
 static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out);
-static int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out);
-static int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out,
-                          const sh_out** out);
 
 // Hashed keys of a time() window get a fresh table once more than half full: keys whose every window
 // event has expired for any later event (last PM + T <= the playback clock) are dropped — the state the
@@ -229,6 +208,7 @@ static int sliding_rekey(sh_query* q) {
 
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
+    if (s->lane) return plane_push(q, b, host_out, out);
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
     int64_t N = b->n;
@@ -473,7 +453,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
 
 // flush offsets / clocks of n_rows output rows: a flush starts where out_send (the send, or the
 // chunk in expired mode) changes; flush_off[n_flushes] = n_rows
-static int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out) {
+int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
     int64_t n_flushes = 0;
@@ -500,11 +480,11 @@ static int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out) 
 }
 
 // the push's rows (device arrays of stride n_rows) and flush arrays -> host vectors or the device view
-static int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out,
-                          const sh_out** out) {
+int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out,
+                   const sh_out** out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
-    int nk = q->kp.n, na = q->ap.n;
+    int nk = s->nk_out >= 0 ? s->nk_out : q->kp.n, na = q->ap.n;
     if (host_out) {
         OutHost& o = q->out;
         o.reset();
@@ -562,7 +542,7 @@ static int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool w
 // The window's events form one expiry queue in arrival order (TimeWindowProcessor.java:132-169); every
 // event's removal point and every operation's place in the push's operation sequence come from the
 // monotone PM / clock sequences, then one lane per key replays its adds and removes in that order.
-static int read_count(sh_query* q, const int64_t* dev, int64_t* out) {
+int read_count(sh_query* q, const int64_t* dev, int64_t* out) {
     SlidingImpl* s = q->sl;
     RCHK(s->x_h.reserve(64));
     HIPCHK(hipMemcpyAsync(s->x_h.p, dev, 8, hipMemcpyDeviceToHost, q->ctx->stream));
@@ -762,12 +742,13 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     if (q->ap.n == 0)
         launch_slx_pass(st, rec, M, s->x_aop.as<u64>(), s->x_xop.as<u64>(), s->x_xch.as<int64_t>(),
                         s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, q->seq, ss,
-                        q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+                        q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
+                        ext ? s->rec_sclk.as<int64_t>() : nullptr);
     else
     launch_slx_walk(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
                     s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u,
                     s->x0, s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on,
-                    q->d.expired_on, rows, s->flags.as<unsigned char>());
+                    q->d.expired_on, rows, s->flags.as<unsigned char>(), ext ? s->rec_sclk.as<int64_t>() : nullptr);
     HIPCHK(hipEventRecord(q->ev_agg1, st));
     HIPCHK(hipGetLastError());
     // ---- rows in operation order, one flush per chunk
@@ -836,6 +817,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
 }
 
 int sliding_advance(sh_query* q, int64_t now, const sh_out** out) {
+    if (q->sl->lane) return plane_advance(q, now, out);
     // expired output: the TIMER chunk's expired events (Scheduler.onTimeChange -> the window)
     if (q->sl->xm && q->d.window == SH_WIN_TIME) return slx_run(q, nullptr, now, true, out);
     // expiry is applied lazily at each key's next event; with current-events-only output the

@@ -128,15 +128,33 @@ void launch_slx_keyoff(hipStream_t s, const u32* slot_cnt, i64 nslots, u32* key_
 void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
                      const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
                      i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
-                     int exp_on, SlxRows rows, unsigned char* flags);
+                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk);
 void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
                      const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
-                     SlxRows rows, unsigned char* flags);
+                     SlxRows rows, unsigned char* flags, const i64* rsclk);
 void launch_slx_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
                      int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                      unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
 void launch_slx_shift(hipStream_t s, const i64* upm, const i64* useq, i64 from, i64 n, i64* opm, i64* oseq);
 void launch_slx_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new_kt, const i64* rlen, const i64* cnt,
                           const u64* f, i64 nslots, AggPlan ap, u32* map);
+
+// ---- partitioned lengthBatch / time windows keyed by the partition (sh_plane_kernels.hip) ----
+void launch_pl_walk_lb(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec, i64 L,
+                       i64 seq_base, SlState S, i64* last_ts, i64* last_seq, i64* prev_seq, AggPlan ap, int cur_on,
+                       int exp_on, SlxRows rows, unsigned char* flags);
+void launch_pl_runs(hipStream_t s, ColSet cols, int pcol, i64 N, i64 send_size, unsigned char* start, i64* blk,
+                    i64* run);
+void launch_pl_first_seen(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64 seq_base,
+                          unsigned long long* first_seen);
+void launch_pl_notify(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, const i64* ts, i64* last_ts,
+                      unsigned char* reg);
+void launch_pl_walk_tm(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                       const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
+                       const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, AggPlan ap,
+                       int cur_on, int exp_on, SlxRows rows, unsigned char* flags);
+void launch_pl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
+                    int n_aggs, int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                    unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
 
 }  // namespace shd

@@ -1,0 +1,61 @@
+// sh_sliding_impl.h — host state of a query of kind 1 (sh_sliding.cpp: time / externalTime windows;
+// sh_plane.cpp: partitioned lengthBatch / time windows keyed by the partition).
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <set>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "sh_runtime.h"
+#include "sh_sliding.h"
+
+using shd::SlInfo;
+
+struct SlidingImpl {
+    int64_t nslots = 0, rc = 0;
+    int P = 1, logP = 0;
+    int64_t pm = INT64_MIN;   // PM carried across pushes
+    int64_t send_base = 0;    // global send number of the push's first send
+    DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
+    // per push scratch
+    DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
+        tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_rep, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
+        out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock, sort_tmp,
+        key_off, g_rank, inv, rows_k;
+    SlInfo* h_info = nullptr;
+    PinnedBuf h_up;  // pinned staging of small host->device uploads
+    sh_out dev_out{};
+
+    // `insert expired events` / `insert all events` (sh_slx_kernels.hip): the expiry queue as a FIFO
+    // of the window's events (PM and stream index, global arrival order X0 .. G0), each ring entry's
+    // arrival index, and the scheduler's pending notify times (ascending)
+    bool xm = false;
+    DevBuf rg, upm, useq, upm2, useq2, npend, npend2;
+    int64_t x0 = 0, g0 = 0, w0 = 0, n_np = 0, np_front = 0;
+    DevBuf x_sK, x_scb, x_slast, x_cK, x_cC, x_cS, x_fire, x_keep, x_idx, x_fK, x_fC, x_fS, x_blk, x_xop, x_xch,
+        x_xts, x_xclk, x_aop, x_nexp, xr_ts, xr_rep, xr_slot, xr_ch, xr_clk, xr_exp, xr_vals, xr_nulls;
+    PinnedBuf x_h;
+    // partitioned windows keyed by the partition (sh_plane.cpp): lane = 1 lengthBatch, 2 time; per slot the
+    // open batch's last event, the last flushed batch's last event (expired rows), lastTimestamp, the
+    // partition's creation order; host side the Scheduler's pending notify times per partition
+    int lane = 0;
+    int nk_out = -1;  // output key columns (0: no group-by, the partition key is internal)
+    DevBuf pl_last_ts, pl_last_seq, pl_prev_seq, pl_first, pl_start, pl_run, pl_reg, pl_toff, pl_tsend, pl_tclk,
+        pl_tpos, pl_fsend;
+    std::unordered_map<uint32_t, std::deque<int64_t>> pl_pend;
+    std::set<std::tuple<int64_t, uint64_t, uint32_t>> pl_armed;  // (front notify time, creation order, slot)
+};
+
+
+// shared by sh_sliding.cpp and sh_plane.cpp
+shd::SlState state_of(SlidingImpl* s);
+int size_rings(sh_query* q, int64_t new_rc, bool keep = true);
+int empty_out(sh_query* q, const sh_out** out);
+int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out);
+int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out, const sh_out** out);
+int read_count(sh_query* q, const int64_t* dev, int64_t* out);
+int plane_create(sh_query* q);
+int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
+int plane_advance(sh_query* q, int64_t now, const sh_out** out);

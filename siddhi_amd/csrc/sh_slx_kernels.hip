@@ -325,7 +325,7 @@ __global__ __launch_bounds__(64) void k_slx_walk(const u32* __restrict__ key_off
                                                  const i64* __restrict__ xts, const i64* __restrict__ xclk,
                                                  const i64* __restrict__ useq, i64 n_u, i64 X0, i64 G0, i64 seq_base,
                                                  i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on, int exp_on,
-                                                 SlxRows rows, unsigned char* flags) {
+                                                 SlxRows rows, unsigned char* flags, const i64* __restrict__ rsclk) {
     const u32 k = blockIdx.x * 64 + threadIdx.x;
     if (k >= nslots) return;
     const u32 lo = key_off[k], hi = key_off[k + 1];
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(64) void k_slx_walk(const u32* __restrict__ key_off
             const i64 send = send_size > 0 ? (i64)rec.raw[r] / send_size : 0;
             ch = 2 * send + 1;
             ts_row = rec.ts[r];
-            clk = rec.clock[r];
+            clk = rsclk ? rsclk[r] : rec.clock[r];  // externalTime: the send's playback clock
             rep = seq_base + (i64)rec.raw[r];
             is_exp = false;
             ai++;
@@ -533,13 +533,13 @@ __global__ __launch_bounds__(64) void k_slx_walk(const u32* __restrict__ key_off
 void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
                      const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
                      i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
-                     int exp_on, SlxRows rows, unsigned char* flags) {
+                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk) {
     const unsigned grid = (unsigned)((nslots + 63) / 64);
     if (grid == 0) return;
 #define SH_SLX_W(A, V)                                                                                            \
     hipLaunchKernelGGL((k_slx_walk<A, V>), dim3(grid), dim3(64), 0, s, key_off, sorted_rank, (u32)nslots, rec, aop, \
                        xop, xch, xts, xclk, useq, n_u, X0, G0, seq_base, send_size, S, rg, ap, cur_on, exp_on, rows,  \
-                       flags)
+                       flags, rsclk)
     const int nv = ap.n_vcols < 1 ? 1 : ap.n_vcols;
     if (ap.n <= 4 && nv <= 1) SH_SLX_W(4, 1);
     else if (nv <= 2) SH_SLX_W(8, 2);
@@ -553,7 +553,8 @@ __global__ __launch_bounds__(kBlock) void k_slx_pass(SlRecords rec, i64 M, const
                                                     const u64* __restrict__ xop, const i64* __restrict__ xch,
                                                     const i64* __restrict__ xts, const i64* __restrict__ xclk,
                                                     const i64* __restrict__ useq, i64 n_u, i64 seq_base, i64 send_size,
-                                                    int cur_on, int exp_on, SlxRows rows, unsigned char* flags) {
+                                                    int cur_on, int exp_on, SlxRows rows, unsigned char* flags,
+                                                    const i64* __restrict__ rsclk) {
     const i64 t = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (t < M) {
         if (!cur_on) return;
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void k_slx_pass(SlRecords rec, i64 M, const
         rows.rep[op] = seq_base + (i64)rec.raw[t];
         rows.slot[op] = 0;
         rows.ch[op] = 2 * send + 1;
-        rows.clk[op] = rec.clock[t];
+        rows.clk[op] = rsclk ? rsclk[t] : rec.clock[t];
         rows.exp[op] = 0;
         flags[op] = 1;
     } else if (t < M + n_u) {
@@ -582,11 +583,11 @@ __global__ __launch_bounds__(kBlock) void k_slx_pass(SlRecords rec, i64 M, const
 
 void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
                      const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
-                     SlxRows rows, unsigned char* flags) {
+                     SlxRows rows, unsigned char* flags, const i64* rsclk) {
     const i64 n = M + n_u;
     if (n <= 0) return;
     hipLaunchKernelGGL(k_slx_pass, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, aop, xop, xch,
-                       xts, xclk, useq, n_u, seq_base, send_size, cur_on, exp_on, rows, flags);
+                       xts, xclk, useq, n_u, seq_base, send_size, cur_on, exp_on, rows, flags, rsclk);
 }
 
 // per slot key offsets of the slot-sorted records (exclusive scan of the per-slot counts)

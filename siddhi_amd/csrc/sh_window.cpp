@@ -194,15 +194,21 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
     if (!d->current_on && !d->expired_on) return sh_fail(SH_ERR_INVALID, "query emits neither current nor expired events");
     const bool sliding_win = d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME;
-    if ((!d->current_on || d->expired_on) && !((batch_win || sliding_win) && d->partition_col < 0))
+    // partitioned lengthBatch / time keyed by the partition (no group-by, or group by the partition
+    // key): one lane per partition (sh_plane.cpp)
+    const bool plane = d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
+                       (d->n_group_by == 0 || (d->n_group_by == 1 && d->group_by[0] == d->partition_col));
+    if ((!d->current_on || d->expired_on) && !((batch_win || sliding_win) && d->partition_col < 0) && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "expired / all-events output runs on lengthBatch, timeBatch, time and externalTime "
-                       "(not partitioned) windows");
+                       "expired / all-events output runs on lengthBatch, timeBatch, time and externalTime windows "
+                       "(partitioned: lengthBatch / time grouped by the partition key)");
     if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "stream.current.event runs on aggregating, non-partitioned lengthBatch / timeBatch windows");
-    if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH)
-        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned GPU queries support timeBatch");
+    if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "partitioned GPU queries support timeBatch, and lengthBatch / time with no group-by or "
+                       "grouped by the partition key");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
                                   d->col_types[d->partition_col] == SH_T_LONG || d->col_types[d->partition_col] == SH_T_STRID)))
         return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/string column");
@@ -212,15 +218,17 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     q->d = *d;
     q->d.filter = nullptr;
     int rc;
+    const int32_t pkey[1] = {d->partition_col};
     if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, q->fp)) ||
         (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, q->ap, q->vtypes)) ||
-        (!kp_override && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->kp)))) {
+        (!kp_override && plane && (rc = compile_keys(1, pkey, d->n_cols, d->col_types, q->kp))) ||
+        (!kp_override && !plane && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->kp)))) {
         delete q;
         return rc;
     }
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
-    if (d->partition_col >= 0) {
+    if (d->partition_col >= 0 && !plane) {
         // R12: only partition p0 is ever aggregated. Its group keys are a sparse subset of the
         // dictionary, so they go to the hash table; grouped by the partition key alone it is one key.
         q->kp.dense = 0;
@@ -229,9 +237,9 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
-    q->partitioned = d->partition_col >= 0;
+    q->partitioned = d->partition_col >= 0 && !plane;
     q->xmode = d->expired_on != 0 && !d->stream_current;
-    if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) {
+    if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME || plane) {
         q->kind = 1;
         if ((rc = sliding_create(q))) { delete q; return rc; }
         *out = q;

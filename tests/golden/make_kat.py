@@ -130,6 +130,31 @@ case(name="partition5_timeBatch", source="ctest/query/partition/WindowPartitionT
      expect=dict(in_count_max=7, remove_count=0, min_in_count=1, partition_values={"IBM": 370.0, "WSO2": 2200.0,
                                                                                     "ORACLE": 75.6}))
 
+# partitioned lengthBatch(2) without group-by, `insert all events`: IBM's first batch (70, 100) and
+# WSO2's (700, 1000) complete; IBM 200 stays open. Two events, 170.0 then 1700.0 (sum of the floats).
+case(name="partition2_lengthBatch_all", source="ctest/query/partition/WindowPartitionTestCase.java:96-139",
+     schema="symbol string, price float, volume int",
+     query=dict(window="lengthBatch", param=2, partition="symbol", aggs=[["sum", "price"]], output="all"),
+     sends=[[[B + i] + r] for i, r in enumerate([["IBM", 70.0, 100], ["WSO2", 700.0, 100], ["IBM", 100.0, 100],
+                                                ["IBM", 200.0, 100], ["WSO2", 1000.0, 100]])],
+     expect=dict(total_count=2, values=[[170.0], [1700.0]], rep_cols=[["symbol", ["IBM", "WSO2"]]]))
+
+# partitioned time(1 sec) without group-by, `insert all events`, `default(sum(price), 0.0)`: the Java test
+# sleeps between sends and lets the wall-clock scheduler expire each partition's events 1 s after they
+# arrived; in playback those scheduler calls are TIMER calls at B+1000 (IBM 70), B+1100 (WSO2 700),
+# B+1200 (IBM 100), B+4200 and B+4300. WSO2 rows: 700, 0.0, 1000, 0.0; IBM rows: 70, 170, 100, 0.0,
+# 200, 0.0 (the callback counts them by symbol); default() turns the null sums into 0.0 (None here).
+case(name="partition3_time_all", source="ctest/query/partition/WindowPartitionTestCase.java:141-216",
+     schema="symbol string, price float, volume int",
+     query=dict(window="time", param=1000, partition="symbol", aggs=[["sum", "price"]], output="all"),
+     sends=[[[B, "IBM", 70.0, 100]], [[B + 100, "WSO2", 700.0, 100]], [[B + 200, "IBM", 100.0, 200]],
+            {"advance": B + 1000}, {"advance": B + 1100}, {"advance": B + 1200},
+            [[B + 3200, "IBM", 200.0, 300]], [[B + 3300, "WSO2", 1000.0, 100]],
+            {"advance": B + 4200}, {"advance": B + 4300}],
+     expect=dict(total_count=10, values=[[70.0], [700.0], [170.0], [100.0], [None], [None], [200.0], [1000.0],
+                                         [None], [None]],
+                 rep_cols=[["symbol", ["IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "WSO2"]]]))
+
 # ---------------------------------------------------------------- incremental aggregation (Aggregation1TestCase)
 AGG_SCHEMA = "symbol string, price float, lastClosingPrice float, volume long, quantity int, timestamp long"
 _t5 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],

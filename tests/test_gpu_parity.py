@@ -40,7 +40,9 @@ def _gpu_runs(c):
     if q.get("window") in ("lengthBatch", "timeBatch"):
         return bool(q.get("aggs")) or not q.get("group_by")
     if q.get("window") in ("time", "externalTime"):
-        return not q.get("partition") and (bool(q.get("aggs")) or not q.get("group_by"))
+        if q.get("partition"):  # the partition lanes: no group-by or grouped by the partition key
+            return bool(q.get("aggs")) and q.get("group_by", []) in ([], [q["partition"]])
+        return bool(q.get("aggs")) or not q.get("group_by")
     return False
 
 

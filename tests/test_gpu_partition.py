@@ -1,0 +1,81 @@
+"""GPU parity of `partition with (p of S)` around lengthBatch(L) and time(T) windows grouped by the
+partition key or without group-by (sh_plane.cpp: one lane per partition), against the oracle's
+restatement of PartitionStreamReceiver.receive (:176-272: runs of equal partition keys per send, one
+window / aggregator state per partition), LengthBatchWindowProcessor (:153-243), TimeWindowProcessor
+(:132-169) and the Scheduler's TIMER calls per partition (Scheduler.java:71-104, 171-209, including
+its TreeMultimap tie rule: of several partitions due at the same time only the first-created fires).
+The reference KATs (WindowPartitionTestCase partition2 lengthBatch, partition3 time) run in
+test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+from siddhi_amd import abi, synth
+from tests.parity import split_batches
+from tests.test_gpu_sliding_expired import both
+
+pytestmark = pytest.mark.gpu
+
+SCHEMA = abi.Schema.parse("p int, v double, x long, ts long")
+AGGS = [("count", None), ("sum", "v"), ("min", "v"), ("max", "x"), ("avg", "x"), ("sum", "x")]
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from siddhi_amd import runtime
+    return runtime
+
+
+def stream(n, parts, seed, step=3, runs=False, zipf=False):
+    rng = np.random.default_rng(seed)
+    ts = (np.cumsum(rng.integers(0, step, n)) + 10_000).astype(np.int64)
+    if zipf:
+        p = (synth.zipf_keys(0, n, seed, parts) % parts).astype(np.int32)
+    else:
+        p = rng.integers(0, parts, n).astype(np.int32)
+    if runs:  # runs of equal partition keys (the receiver's chunks hold several events)
+        p = np.repeat(p[: (n + 3) // 4], 4)[:n]
+    v = rng.integers(-400, 400, n).astype(np.float64) / 8.0
+    x = rng.integers(-50, 50, n).astype(np.int64)
+    return ts, [p, v, x, ts.copy()]
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("L,group", [(1, True), (3, False), (100, True)])
+def test_partitioned_lengthbatch(rt, output, L, group):
+    ts, cols = stream(30_000, 200, 41, runs=True)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["p"] if group else [], aggs=AGGS, partition="p",
+                         filter=(">", "v", -30.0), output=output, key_capacity=256)
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 7_777, 20_000], 5), f"plb {L} {output}")
+    assert ref["ts"].size > 0
+
+
+def test_partitioned_lengthbatch_zipf_100k_partitions(rt):
+    ts, cols = stream(2_000_000, 1_000_000, 43, zipf=True)  # ~231k distinct partitions
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 3, group_by=["p"], aggs=[("count", None), ("sum", "v"), ("max", "x")],
+                         partition="p", output="all", key_capacity=1_000_000)
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000], 1), "plb zipf")
+    assert len(np.unique(cols[0])) > 100_000 and ref["ts"].size > 10_000
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("send_size", [1, 6])
+def test_partitioned_time(rt, output, send_size):
+    """ms timestamps shared by many partitions: several partitions are due at the same TIMER call"""
+    ts, cols = stream(30_000, 60, 47, step=2, runs=send_size > 1)
+    spec = abi.QuerySpec(SCHEMA, "time", 150, group_by=["p"], aggs=AGGS, partition="p", filter=(">", "v", -40.0),
+                         output=output, key_capacity=64)
+    pushes = split_batches(SCHEMA, ts, cols, [1, 5_000, 18_000], send_size)
+    pushes.insert(3, ("advance", int(ts[17_999]) + 100))
+    pushes.append(("advance", int(ts[-1]) + 120))
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    ref = both(rt, spec, pushes, f"ptime {output} {send_size}")
+    assert ref["ts"].size > 0
+
+
+def test_partitioned_time_no_group_by_zipf(rt):
+    ts, cols = stream(300_000, 100_000, 53, step=2, zipf=True)
+    spec = abi.QuerySpec(SCHEMA, "time", 500, aggs=[("sum", "v"), ("count", None)], partition="p", output="all",
+                         key_capacity=100_000)
+    pushes = split_batches(SCHEMA, ts, cols, [100_000, 200_000], 1) + [("advance", int(ts[-1]) + 1_000)]
+    ref = both(rt, spec, pushes, "ptime zipf")
+    assert ref["expired"].sum() > 0
