@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 6
+#define SH_ABI_VERSION 7
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -235,12 +235,17 @@ int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
 
 /* Output rate limiting `output [all|first|last] every <n> events` (core/query/output/ratelimit/event/:
  * AllPerEvent, FirstPerEvent, LastPerEvent and, for group-by queries, FirstGroupByPerEvent /
- * LastGroupByPerEventOutputRateLimiter.java). Set once, before the first push; every later output
- * (push, advance_time) goes through the limiter: one flush per input flush that emits rows. */
+ * LastGroupByPerEventOutputRateLimiter.java) and `output first every <n> milliseconds`
+ * (core/query/output/ratelimit/time/FirstPerTimeOutputRateLimiter.java:54-78, for group-by queries
+ * FirstGroupByPerTimeOutputRateLimiter.java:54-80: they read the playback clock, so they are
+ * deterministic; the all/last time limiters arm a wall-clock schedule and are not offered). Set once,
+ * before the first push; every later output (push, advance_time) goes through the limiter: one flush
+ * per input flush that emits rows. */
 #define SH_RATE_NONE 0
 #define SH_RATE_ALL 1
 #define SH_RATE_FIRST 2
 #define SH_RATE_LAST 3
+#define SH_RATE_FIRST_TIME 4
 int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
 
 /* Checkpoint of the query's state: State.snapshot()/restore() (core/util/snapshot/state/State.java:

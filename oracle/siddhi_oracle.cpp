@@ -393,9 +393,33 @@ struct RateLimiter {
     std::map<std::vector<int64_t>, OutRow> last_rows;
     int nk = 0;
 
+    bool has_out_time = false;                     // FirstPerTime: state.outputTime != null
+    int64_t out_time = 0;
+    std::map<std::vector<int64_t>, int64_t> first_time;  // FirstGroupByPerTime: groupByOutputTime
+
     std::vector<int64_t> key_of(const OutRow& r) const { return std::vector<int64_t>(r.keys, r.keys + nk); }
 
-    void process(const OutRow* rows, int64_t n, std::vector<OutRow>& out) {
+    // one selector output chunk at playback clock `now`
+    void process(const OutRow* rows, int64_t n, std::vector<OutRow>& out, int64_t now) {
+        if (kind == SH_RATE_FIRST_TIME) {
+            if (!group_by) {  // FirstPerTimeOutputRateLimiter.process :54-78: the chunk's first event
+                if (n > 0 && (!has_out_time || out_time + value <= now)) {
+                    has_out_time = true;
+                    out_time = now;
+                    out.push_back(rows[0]);
+                }
+                return;
+            }
+            for (int64_t i = 0; i < n; i++) {  // FirstGroupByPerTimeOutputRateLimiter.process :54-80
+                const std::vector<int64_t> k = key_of(rows[i]);
+                auto it = first_time.find(k);
+                if (it == first_time.end() || it->second + value <= now) {
+                    first_time[k] = now;
+                    out.push_back(rows[i]);
+                }
+            }
+            return;
+        }
         for (int64_t i = 0; i < n; i++) {
             const OutRow& ev = rows[i];
             if (kind == SH_RATE_ALL) {  // AllPerEventOutputRateLimiter.process :48-77
@@ -517,7 +541,7 @@ struct Query {
         if (!ps.rl_init) { ps.rl = rate; ps.rl_init = true; }
         std::vector<OutRow> chunk(out.rows.begin() + (int64_t)start, out.rows.end()), kept;
         out.rows.resize(start);
-        ps.rl.process(chunk.data(), (int64_t)chunk.size(), kept);
+        ps.rl.process(chunk.data(), (int64_t)chunk.size(), kept, clock);
         if (kept.empty()) return;
         out.rows.insert(out.rows.end(), kept.begin(), kept.end());
         out.close_flush(clock);
@@ -1274,7 +1298,7 @@ void or_query_destroy(void* h) { delete (Query*)h; }
 
 int or_query_set_output_rate(void* h, int32_t kind, int64_t n) {
     Query* q = (Query*)h;
-    if (kind < SH_RATE_NONE || kind > SH_RATE_LAST || (kind != SH_RATE_NONE && n < 1)) {
+    if (kind < SH_RATE_NONE || kind > SH_RATE_FIRST_TIME || (kind != SH_RATE_NONE && n < (kind == SH_RATE_FIRST_TIME ? 0 : 1))) {
         g_err = "invalid output rate";
         return SH_ERR_INVALID;
     }

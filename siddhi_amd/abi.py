@@ -170,7 +170,8 @@ class QuerySpec:
     output: str = "current"          # 'current' | 'all' | 'expired'
     partition: Optional[str] = None
     key_capacity: int = 0
-    rate: Optional[tuple] = None       # ('all'|'first'|'last', n): `output <kind> every n events`
+    rate: Optional[tuple] = None       # ('all'|'first'|'last', n): `output <kind> every n events`;
+                                       # ('first_time', ms): `output first every <ms> milliseconds`
     ts_attr: Optional[str] = None      # externalTimeBatch timestamp attribute
     start_attr: Optional[str] = None   # externalTimeBatch start time from this attribute
     _keep: list = field(default_factory=list, repr=False)
@@ -436,4 +437,4 @@ ABI_SYMBOLS = [
 ]
 
 # output rate limiter kinds (SH_RATE_*)
-RATE_KINDS = {"all": 1, "first": 2, "last": 3}
+RATE_KINDS = {"all": 1, "first": 2, "last": 3, "first_time": 4}

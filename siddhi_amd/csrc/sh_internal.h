@@ -325,6 +325,12 @@ void launch_rate_first(hipStream_t s, i64 n, const u32* hd, const u32* pos, cons
 void launch_rate_rehash(hipStream_t s, i64 old_cap, const u64* otk, const i64* otc, u64* tk, i64* tc, u32 tmask);
 void launch_rate_last(hipStream_t s, i64 n, const u32* hd, const u32* pos, const u32* starts, const u32* idx, i64 N,
                       i64 n_carry, const i64* flush_off, int nf, u32* flag, u32* src, int* eflush);
+void launch_rate_ftime_rows(hipStream_t s, i64 n, const i64* foff, int nf, const unsigned char* chosen, u32* flag,
+                            int* eflush, u32* src);
+void launch_rate_ftime_walk(hipStream_t s, i64 n, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
+                            const u32* idx, const i64* foff, const i64* fclk, int nf, i64 T, u64* tk, i64* tt, u32 tmask,
+                            u32* flag, u32* n_new);
+void launch_rate_ftime_rehash(hipStream_t s, i64 old_cap, const u64* otk, const i64* ott, u64* tk, i64* tt, u32 tmask);
 void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, const u32* src, const int* eflush,
                         RateRows in, i64 in_stride, RateRows out, i64 T, int nk, int na, int* out_flush);
 

@@ -353,7 +353,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
     (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
     q->stats.push_ms = ms;
     q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
-    return sliding_output(q, n_rows, n_flushes, false, host_out || !b, out);
+    return sliding_output(q, n_rows, n_flushes, false, host_out, out);
 }
 
 int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
@@ -362,4 +362,6 @@ int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out
     return plane_run(q, b, 0, host_out, out);
 }
 
-int plane_advance(sh_query* q, int64_t now, const sh_out** out) { return plane_run(q, nullptr, now, true, out); }
+int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out) {
+    return plane_run(q, nullptr, now, host_out, out);
+}

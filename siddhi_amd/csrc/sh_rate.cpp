@@ -31,13 +31,18 @@ using namespace shd;
 
 extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_output_rate: NULL query");
-    if (kind < SH_RATE_NONE || kind > SH_RATE_LAST) return sh_fail(SH_ERR_INVALID, "unknown output rate kind");
-    if (kind != SH_RATE_NONE && n < 1) return sh_fail(SH_ERR_INVALID, "output rate needs every >= 1 events");
+    if (kind < SH_RATE_NONE || kind > SH_RATE_FIRST_TIME) return sh_fail(SH_ERR_INVALID, "unknown output rate kind");
+    if (kind != SH_RATE_NONE && kind != SH_RATE_FIRST_TIME && n < 1)
+        return sh_fail(SH_ERR_INVALID, "output rate needs every >= 1 events");
+    if (kind == SH_RATE_FIRST_TIME && n < 0) return sh_fail(SH_ERR_INVALID, "output rate needs a time >= 0");
     if (n > (int64_t)1 << 30) return sh_fail(SH_ERR_UNSUPPORTED, "output rate above 2^30 events");
     if (q->seq > 0 || q->clock_valid) return sh_fail(SH_ERR_INVALID, "output rate must be set before the first push");
     // a partitioned query holds one limiter per partition instance (PartitionRuntime clones the query);
     // the GPU's partitioned timeBatch flushes only partition p0 (R12), so its one limiter is p0's
     if (kind != SH_RATE_NONE && q->given) return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of a sharded query");
+    // the partition lanes (sh_plane.cpp) would need one limiter per partition instance
+    if (kind != SH_RATE_NONE && q->kind == 1 && q->d.partition_col >= 0)
+        return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of partitioned lengthBatch / time windows");
     if (kind != SH_RATE_NONE && q->kp.n > 2) return sh_fail(SH_ERR_UNSUPPORTED, "output rate with more than 2 group-by keys");
     q->rate.kind = kind;
     q->rate.N = n;
@@ -46,6 +51,33 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     q->rate.nc = 0;
     q->rate.t_cap = 0;
     q->rate.t_keys = 0;
+    q->rate.ft_has = false;
+    q->rate.ft_cap = 0;
+    q->rate.ft_keys = 0;
+    return SH_OK;
+}
+
+// `output first every <t>` group-by table: room for `need` keys at load <= 1/2
+static int grow_ftime_table(sh_query* q, int64_t need) {
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    int64_t cap = 64;
+    while (cap < 2 * need) cap <<= 1;
+    if (cap > ((int64_t)1 << 31)) return sh_fail(SH_ERR_UNSUPPORTED, "output rate: too many group keys");
+    if (cap <= r.ft_cap) return SH_OK;
+    RCHK(r.ftk2.reserve((size_t)cap * 8, false));
+    RCHK(r.ftt2.reserve((size_t)cap * 8, false));
+    // kEmptyKey (0x8000000000000001) in every slot
+    std::vector<uint64_t> empty((size_t)cap, kEmptyKey);
+    HIPCHK(hipMemcpyAsync(r.ftk2.p, empty.data(), (size_t)cap * 8, hipMemcpyHostToDevice, s));
+    if (r.ft_cap > 0)
+        launch_rate_ftime_rehash(s, r.ft_cap, r.ftk.as<u64>(), r.ftt.as<i64>(), r.ftk2.as<u64>(), r.ftt2.as<i64>(),
+                                 (u32)(cap - 1));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));  // `empty` is pageable host memory
+    std::swap(r.ftk, r.ftk2);
+    std::swap(r.ftt, r.ftt2);
+    r.ft_cap = cap;
     return SH_OK;
 }
 
@@ -172,7 +204,57 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
     RCHK(r.eflush.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
     RCHK(r.tmp.reserve((size_t)((S + 1 + kTile - 1) / kTile + 16) * 8, false));
     RCHK(r.h_small.reserve(64));
-    if (!r.gb) {
+    if (r.kind == SH_RATE_FIRST_TIME && !r.gb) {
+        // FirstPerTimeOutputRateLimiter :54-78, flush by flush in order (a flush = one process() chunk)
+        std::vector<unsigned char> chosen((size_t)std::max(nf, 1), 0);
+        for (int f = 0; f < nf; f++) {
+            if (r.h_off[f + 1] <= r.h_off[f]) continue;
+            if (!r.ft_has || r.ft_last + N <= r.h_clk[f]) {
+                chosen[f] = 1;
+                r.ft_has = true;
+                r.ft_last = r.h_clk[f];
+            }
+        }
+        RCHK(r.chosen.reserve(chosen.size(), false));
+        HIPCHK(hipMemcpyAsync(r.chosen.p, chosen.data(), chosen.size(), hipMemcpyHostToDevice, s));
+        launch_rate_ftime_rows(s, S, foff, nf, r.chosen.as<unsigned char>(), r.flag.as<u32>(), r.eflush.as<int>(),
+                               r.src.as<u32>());
+        HIPCHK(hipStreamSynchronize(s));  // `chosen` is pageable host memory
+    } else if (r.kind == SH_RATE_FIRST_TIME) {
+        // FirstGroupByPerTimeOutputRateLimiter :54-80: rows sorted stably by key, one walker per key
+        RCHK(r.fclk.reserve((size_t)std::max(nf, 1) * 8, false));
+        if (nf) HIPCHK(hipMemcpyAsync(r.fclk.p, r.h_clk.data(), (size_t)nf * 8, hipMemcpyHostToDevice, s));
+        launch_rate_ftime_rows(s, S, foff, nf, nullptr, r.flag.as<u32>(), r.eflush.as<int>(), r.src.as<u32>());
+        const int64_t m = S;
+        RCHK(r.skey.reserve((size_t)m * 8, false));
+        RCHK(r.skey2.reserve((size_t)m * 8, false));
+        RCHK(r.idx.reserve((size_t)m * 4, false));
+        RCHK(r.idx2.reserve((size_t)m * 4, false));
+        RCHK(r.hd.reserve((size_t)(m + 1) * 4, false));
+        RCHK(r.pos.reserve((size_t)(m + 1) * 4, false));
+        RCHK(r.starts.reserve((size_t)(m + 1) * 4, false));
+        RCHK(r.tmp.reserve((size_t)((m + 1 + kTile - 1) / kTile + 16) * 8, false));
+        launch_rate_pack(s, m, src.keys, sstride, nk, r.skey.as<u64>(), r.idx.as<u32>());
+        size_t tb = 0;
+        if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, m, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
+        RCHK(r.sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_u64_pairs(r.sort_tmp.p, &tb, r.skey.as<u64>(), r.skey2.as<u64>(), r.idx.as<u32>(), r.idx2.as<u32>(), m, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
+        launch_rate_segments(s, m, r.skey2.as<u64>(), r.idx2.as<u32>(), 1, 0, r.hd.as<u32>(), r.pos.as<u32>(),
+                             r.starts.as<u32>(), r.tmp.as<i64>());
+        HIPCHK(hipMemcpyAsync(r.h_small.as<char>() + 16, r.pos.as<u32>() + m, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        RCHK(grow_ftime_table(q, r.ft_keys + *(const uint32_t*)(r.h_small.as<char>() + 16)));
+        RCHK(r.n_keys.reserve(16, false));
+        HIPCHK(hipMemsetAsync(r.n_keys.p, 0, 4, s));
+        launch_rate_ftime_walk(s, m, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.skey2.as<u64>(),
+                               r.idx2.as<u32>(), foff, r.fclk.as<i64>(), nf, N, r.ftk.as<u64>(), r.ftt.as<i64>(),
+                               (u32)(r.ft_cap - 1), r.flag.as<u32>(), r.n_keys.as<u32>());
+        HIPCHK(hipMemcpyAsync(r.h_small.as<char>() + 24, r.n_keys.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        r.ft_keys += *(const uint32_t*)(r.h_small.as<char>() + 24);
+    } else if (!r.gb) {
         launch_rate_pos(s, S, nc, r.kind, N, r.seq, foff, nf, r.flag.as<u32>(), r.eflush.as<int>(), r.src.as<u32>());
     } else {
         launch_rate_clear(s, S, r.src.as<u32>(), r.flag.as<u32>());

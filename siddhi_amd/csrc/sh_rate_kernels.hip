@@ -275,4 +275,89 @@ void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, c
                        out, T, nk, na, out_flush);
 }
 
+// ---- `output first every <t>` (core/query/output/ratelimit/time/): the playback clock of the chunk
+// (the input flush) decides. FirstPerTimeOutputRateLimiter.process :54-78 sends a chunk's FIRST event
+// when no output happened yet or outputTime + t <= now (chosen per flush on the host, in order), then
+// outputTime = now. Every row also gets its emitting flush and source index here.
+__global__ __launch_bounds__(kBlock) void k_rate_ftime_rows(i64 n, const i64* __restrict__ foff, int nf,
+                                                           const unsigned char* __restrict__ chosen, u32* flag,
+                                                           int* eflush, u32* src) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { flag[n] = 0; return; }
+    const int f = rate_flush_of(foff, nf, i);
+    eflush[i] = f;
+    src[i] = (u32)i;
+    flag[i] = chosen ? (chosen[f] && foff[f] == i) : 0u;
+}
+
+void launch_rate_ftime_rows(hipStream_t s, i64 n, const i64* foff, int nf, const unsigned char* chosen, u32* flag,
+                            int* eflush, u32* src) {
+    hipLaunchKernelGGL(k_rate_ftime_rows, dim3(grid_of(n + 1)), dim3(kBlock), 0, s, n, foff, nf, chosen, flag, eflush,
+                       src);
+}
+
+// FirstGroupByPerTimeOutputRateLimiter.process :54-80: per group key the time of its last output row
+// (groupByOutputTime); a row is sent when its key has none or that time + t <= the chunk's clock. One
+// thread per key segment of the call (rows of one key in stream order); the key -> time table keeps
+// the keys of earlier calls (tk == kEmptyKey: free; a thread only ever claims or reads its own key's slot).
+__global__ __launch_bounds__(kBlock) void k_rate_ftime_walk(i64 n, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                           const u32* __restrict__ starts, const u64* __restrict__ skey,
+                                                           const u32* __restrict__ idx, const i64* __restrict__ foff,
+                                                           const i64* __restrict__ fclk, int nf, i64 T, u64* tk, i64* tt,
+                                                           u32 tmask, u32* flag, u32* n_new) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || !hd[i]) return;
+    const u32 g = pos[i];
+    const i64 end = starts[g + 1];
+    const u64 key = skey[i];
+    u32 h = (u32)mix64(key) & tmask;
+    bool has = true;
+    for (;;) {
+        const u64 k0 = tk[h];
+        if (k0 == key) break;
+        if (k0 == kEmptyKey) {
+            const u64 old = atomicCAS(&tk[h], kEmptyKey, key);
+            if (old == kEmptyKey) { has = false; atomicAdd(n_new, 1u); break; }
+            if (old == key) break;
+        }
+        h = (h + 1) & tmask;
+    }
+    i64 last = has ? tt[h] : 0;
+    for (i64 j = i; j < end; j++) {
+        const u32 r = idx[j];
+        const i64 c = fclk[rate_flush_of(foff, nf, r)];
+        if (!has || last + T <= c) {
+            flag[r] = 1;
+            has = true;
+            last = c;
+        }
+    }
+    tt[h] = last;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rate_ftime_rehash(i64 old_cap, const u64* __restrict__ otk,
+                                                             const i64* __restrict__ ott, u64* tk, i64* tt, u32 tmask) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= old_cap) return;
+    const u64 key = otk[i];
+    if (key == kEmptyKey) return;
+    u32 h = (u32)mix64(key) & tmask;
+    while (atomicCAS(&tk[h], kEmptyKey, key) != kEmptyKey) h = (h + 1) & tmask;
+    tt[h] = ott[i];
+}
+
+void launch_rate_ftime_walk(hipStream_t s, i64 n, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
+                            const u32* idx, const i64* foff, const i64* fclk, int nf, i64 T, u64* tk, i64* tt, u32 tmask,
+                            u32* flag, u32* n_new) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_rate_ftime_walk, dim3(grid_of(n)), dim3(kBlock), 0, s, n, hd, pos, starts, skey, idx, foff, fclk,
+                       nf, T, tk, tt, tmask, flag, n_new);
+}
+
+void launch_rate_ftime_rehash(hipStream_t s, i64 old_cap, const u64* otk, const i64* ott, u64* tk, i64* tt, u32 tmask) {
+    if (old_cap <= 0) return;
+    hipLaunchKernelGGL(k_rate_ftime_rehash, dim3(grid_of(old_cap)), dim3(kBlock), 0, s, old_cap, otk, ott, tk, tt, tmask);
+}
+
 }  // namespace shd

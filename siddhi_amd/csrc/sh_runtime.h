@@ -301,6 +301,11 @@ struct sh_query {
         DevBuf foff, flag, pre, src, eflush, tmp, skey, skey2, idx, idx2, hd, pos, starts, seg_c0, seg_new, sort_tmp;
         DevBuf tk, tc, tk2, tc2, n_keys;  // FirstGroupBy key -> count table
         int64_t t_cap = 0, t_keys = 0;
+        // `output first every <t>`: outputTime (no group-by) / the key -> last output time table
+        bool ft_has = false;
+        int64_t ft_last = 0;
+        DevBuf ftk, ftt, ftk2, ftt2, fclk, chosen;
+        int64_t ft_cap = 0, ft_keys = 0;
         PinnedVec<int64_t> h_off, h_clk, flush_offsets, flush_clock;
         PinnedVec<int> h_flush;
         PinnedBuf h_small;
@@ -364,7 +369,7 @@ void agg_release_sharded(sh_aggregation* a);                     // called by sh
 // sliding time window (sh_sliding.cpp)
 int sliding_create(sh_query* q);
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
-int sliding_advance(sh_query* q, int64_t now, const sh_out** out);
+int sliding_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out = true);
 int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* const* cols, const int64_t* gclk,
                        const int64_t* gpm, const uint64_t* gidx, int64_t raw_base, int64_t send_size,
                        int64_t send_base, bool host_out, const sh_out** out, int64_t n_global);

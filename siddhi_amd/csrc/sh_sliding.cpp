@@ -813,13 +813,13 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
     q->stats.push_ms = ms;
     q->stats.main_kernel_bytes = n_ops * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
-    return sliding_output(q, n_rows, n_flushes, false, host_out || !b, out);
+    return sliding_output(q, n_rows, n_flushes, false, host_out, out);
 }
 
-int sliding_advance(sh_query* q, int64_t now, const sh_out** out) {
-    if (q->sl->lane) return plane_advance(q, now, out);
+int sliding_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out) {
+    if (q->sl->lane) return plane_advance(q, now, out, host_out);
     // expired output: the TIMER chunk's expired events (Scheduler.onTimeChange -> the window)
-    if (q->sl->xm && q->d.window == SH_WIN_TIME) return slx_run(q, nullptr, now, true, out);
+    if (q->sl->xm && q->d.window == SH_WIN_TIME) return slx_run(q, nullptr, now, host_out, out);
     // expiry is applied lazily at each key's next event; with current-events-only output the
     // timer path changes no visible result, only the clock (TimestampGeneratorImpl :104-122)
     if (!q->clock_valid || now >= q->clock) {

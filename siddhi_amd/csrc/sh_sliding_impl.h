@@ -58,4 +58,4 @@ int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_ord
 int read_count(sh_query* q, const int64_t* dev, int64_t* out);
 int plane_create(sh_query* q);
 int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
-int plane_advance(sh_query* q, int64_t now, const sh_out** out);
+int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out);

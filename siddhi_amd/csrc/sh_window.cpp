@@ -1213,7 +1213,11 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
 extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
-    if (q->kind == 1) return sliding_advance(q, now, out);
+    if (q->kind == 1) {
+        if (q->rate.kind == SH_RATE_NONE) return sliding_advance(q, now, out, true);
+        RCHK(sliding_advance(q, now, out, false));  // the TIMER chunks' rows reach the limiter too
+        return rate_apply(q, *out, true, true, out);
+    }
     if (q->rate.kind != SH_RATE_NONE) {
         RCHK(advance_core(q, now, false, out));
         return rate_apply(q, *out, false, true, out);

@@ -399,6 +399,25 @@ case(name="rate18_first2", source=R + ":1008-1066", schema=LOGIN, query=dict(win
      sends=_ips(5, 3, 5, 5, 5, 9, 4, 4, 4, 30, 5),
      expect=dict(in_count=6, remove_count=0, in_col_in=["ip", _ip(5, 4)]))
 
+# `output first every 1 sec` (TimeOutputRateLimitTestCase): FirstPerTime / FirstGroupByPerTime read the
+# TimestampGenerator, so in playback the clock of each send decides; the Java tests' sends land at
+# t, t (+ ms), then 1100 ms later, then 2200 ms later (Thread.sleep between them).
+T_ = "ctest/query/ratelimit/TimeOutputRateLimitTestCase.java"
+
+
+def _tips(*pairs):
+    return [[[B + dt, B + dt, "192.10.1." + str(x)]] for dt, x in pairs]
+
+
+case(name="trate4_first_every_1s", source=T_ + ":223-280", schema=LOGIN,
+     query=dict(window=None, rate=["first_time", 1000]),
+     sends=_tips((0, 5), (0, 3), (1100, 9), (1100, 4), (2200, 30)),
+     expect=dict(in_count=3, remove_count=0, in_col_in=["ip", _ip(5, 9, 30)]))
+case(name="trate6_first_every_1s_group_by", source=T_ + ":341-398", schema=LOGIN,
+     query=dict(window=None, group_by=["ip"], rate=["first_time", 1000]),
+     sends=_tips((0, 5), (0, 5), (0, 3), (0, 9), (0, 4), (1100, 4), (1100, 4), (1100, 30)),
+     expect=dict(in_count=6, remove_count=0))
+
 if __name__ == "__main__":
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat_reference.json")
     with open(out, "w") as f:

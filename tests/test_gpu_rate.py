@@ -51,7 +51,8 @@ def test_reference_rate_kat_on_gpu(rt, case):
 
 
 AGGS = [("count", None), ("sum", "v"), ("max", "x")]
-KINDS = [("all", 1), ("all", 7), ("first", 1), ("first", 3), ("last", 1), ("last", 4), ("first", 50), ("last", 33)]
+KINDS = [("all", 1), ("all", 7), ("first", 1), ("first", 3), ("last", 1), ("last", 4), ("first", 50), ("last", 33),
+         ("first_time", 0), ("first_time", 700)]
 
 
 @pytest.mark.parametrize("kind,n", KINDS)
@@ -169,3 +170,21 @@ def test_rate_rejects(rt):
     spec = abi.QuerySpec(SCHEMA, "lengthBatch", 10, aggs=AGGS, rate=("first", 0))
     with pytest.raises(rt.SiddhiError, match="every >= 1"):
         rt.GpuQuery(spec)
+
+
+# `output first every <t>` (FirstPerTime / FirstGroupByPerTimeOutputRateLimiter): the chunk's playback
+# clock decides, also for the sliding windows' per-send chunks and TIMER chunks (expired output)
+@pytest.mark.parametrize("window,param,output", [("time", 300, "current"), ("time", 300, "all"),
+                                                 ("timeBatch", 500, "all"), ("externalTime", 250, "expired")])
+@pytest.mark.parametrize("group_by", [True, False])
+@pytest.mark.parametrize("t", [1, 900])
+def test_first_every_time(rt, window, param, output, group_by, t):
+    ts, cols = stream(20_000, 30, 9, step=8)
+    kw = {"ts_attr": "x"} if window == "externalTime" else {}
+    if window == "externalTime":
+        cols[2] = cols[3].copy()  # the attribute clock
+    spec = abi.QuerySpec(SCHEMA, window, param, group_by=["k"] if group_by else (), aggs=AGGS, output=output,
+                         key_capacity=64, rate=("first_time", t), **kw)
+    pushes = split_batches(SCHEMA, ts, cols, [3_000, 11_111], 2) + [("advance", int(ts[-1]) + 2_000)]
+    out = both(rt, spec, pushes, label=f"{window} {output} first every {t} gb={group_by}")
+    assert out["ts"].size > 0

@@ -1,5 +1,6 @@
 """CPU check of the oracle's output rate limiters: oracle(query with `output ... every n events`) must
-equal a direct Python transcription of the five Java limiters (core/query/output/ratelimit/event/*)
+equal a direct Python transcription of the five Java event limiters (core/query/output/ratelimit/event/*)
+and of the two `output first every <t>` limiters (ratelimit/time/First[GroupBy]PerTimeOutputRateLimiter)
 applied flush by flush to oracle(query without it), on random streams. Complements the 18
 EventOutputRateLimitTestCase KATs that pin the counts."""
 import numpy as np
@@ -15,9 +16,23 @@ SCHEMA = abi.Schema.parse("k int, v double, ts long")
 def py_limit(flushes, kind, n, group_by):
     """flushes: list of (clock, [rows]) with row = (key tuple, payload). Returns the limited flushes."""
     out, counter, chunk, counts, last = [], 0, [], {}, {}
+    out_time = None
     for clock, rows in flushes:
         sent = []
+        if kind == "first_time" and not group_by:  # FirstPerTimeOutputRateLimiter.process :54-78
+            if rows and (out_time is None or out_time + n <= clock):
+                out_time = clock
+                sent.append(rows[0][1])
+            if sent:
+                out.append((clock, sent))
+            continue
         for key, row in rows:
+            if kind == "first_time":  # FirstGroupByPerTimeOutputRateLimiter.process :54-80
+                t = counts.get(key)
+                if t is None or t + n <= clock:
+                    counts[key] = clock
+                    sent.append(row)
+                continue
             if kind == "all":  # AllPerEventOutputRateLimiter.process :48-77
                 chunk.append(row)
                 counter += 1
@@ -70,7 +85,8 @@ def flushes_of(a):
     return res
 
 
-@pytest.mark.parametrize("kind,n", [("all", 1), ("all", 4), ("first", 1), ("first", 3), ("last", 1), ("last", 5)])
+@pytest.mark.parametrize("kind,n", [("all", 1), ("all", 4), ("first", 1), ("first", 3), ("last", 1), ("last", 5),
+                                    ("first_time", 0), ("first_time", 37)])
 @pytest.mark.parametrize("window,param,output", [("lengthBatch", 7, "current"), ("timeBatch", 50, "all"),
                                                  ("time", 40, "current")])
 @pytest.mark.parametrize("group_by", [True, False])
