@@ -19,6 +19,11 @@ constexpr int kItems = 8;             // events per thread in the scan-type pass
 constexpr int kTile = kBlock * kItems;  // events per workgroup in the scan-type passes
 constexpr u64 kEmptyKey = 0x8000000000000001ull;  // open-addressing EMPTY sentinel
 constexpr u32 kNoPos = 0xFFFFFFFFu;              // event filtered out (no key slot)
+// Packed multisplit record (one u32 per event): local key (< 1024) << 22 | the low 22 bits of the
+// combined event index. The aggregation restores the index from its segment's start, so a packed
+// split serves every closed segment shorter than 2^22 events (longer ones re-split wide).
+constexpr int kPackIdxBits = 22;
+constexpr u32 kPackIdxMask = (1u << kPackIdxBits) - 1u;
 
 // Filter program (postfix), evaluated per event on device. Mirrors sh_filter_op.
 struct FilterOpD {
@@ -179,7 +184,8 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       // multisplit source (P > 1 or long windows; null: the flat kernel reads the batch)
-                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off);
+                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
+                      bool pack = false);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
 // word_pre[w] = exclusive popcount prefix of the first-occurrence bitmap before word w (low 32 bits)
@@ -232,8 +238,8 @@ __host__ __device__ inline int tile_of(const TileMap& m, i64 b) {
 void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
                      u32* counts);
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets,
-                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap);
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
+                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap, bool pack);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
 void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);

@@ -650,10 +650,10 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
 // the 9 owner bits, a wave-private running count per owner), and after one workgroup scan per chunk
 // every record has its slot in its owner's list, in event order. The owner then folds its list.
 constexpr int kOwnT = 512;
-template <int V, int K, int R, int F, u32 SIG>
+template <int V, int K, int R, int F, u32 SIG, bool PACK>
 __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restrict__ seg_off, int P, int logP,
                                                            AggPlan ap, u64* rows, int RW, u32* unit_rows,
-                                                           u32* first_bits,
+                                                           u32* first_bits, const Segment* __restrict__ segs,
                                                            const u32* __restrict__ rec_pos,
                                                            const u32* __restrict__ rec_idx,
                                                            const u64* __restrict__ rec_vals, i64 rec_cap) {
@@ -671,6 +671,8 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     const int p = blockIdx.x - seg * P;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
+    // packed records: the low kPackIdxBits of the event index, which lies in [seg_lo, seg_lo + 2^bits)
+    const u32 seg_lo = PACK ? (u32)segs[seg].lo : 0u;
     SH_STAMP(0, 0);
     u32 cnt0 = 0, fst0 = 0, lst0 = 0, cnt1 = 0, fst1 = 0, lst1 = 0;
     u64 f0[F], f1[F];
@@ -685,8 +687,14 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         for (int j = 0; j < R; j++) {
             const int r = w * PW + j * 64 + lane;
             const bool ok = r < n;
-            li[j] = ok ? (rec_pos[c0 + r] >> logP) : kNone;
-            ix[j] = ok ? rec_idx[c0 + r] : 0;
+            if (PACK) {
+                const u32 wd = ok ? rec_idx[c0 + r] : 0u;
+                li[j] = ok ? (wd >> kPackIdxBits) : kNone;
+                ix[j] = seg_lo + (((wd & kPackIdxMask) - seg_lo) & kPackIdxMask);
+            } else {
+                li[j] = ok ? (rec_pos[c0 + r] >> logP) : kNone;
+                ix[j] = ok ? rec_idx[c0 + r] : 0;
+            }
 #pragma unroll
             for (int x = 0; x < V; x++) v[j][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c0 + r] : 0;
         }
@@ -828,13 +836,22 @@ int agg_unit_rows(int P, int NL, bool own) { return own ? own_keys_per_thread(NL
 void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int logP, int NL, i64 n_pend,
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
-                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off) {
-    if (rec_pos) {  // multisplit records: thread-ownership kernel
+                      const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
+                      bool pack) {
+    if (rec_idx) {  // multisplit records: thread-ownership kernel
         const int K = own_keys_per_thread(NL);
         const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
-#define SH_AGG_OWN(VV, KK, RR, FF, SG)                                                                         \
-    hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP, ap, \
-                       rows, RW, unit_rows, first_bits, rec_pos, rec_idx, rec_vals, rec_cap)
+#define SH_AGG_OWN(VV, KK, RR, FF, SG)                                                                          \
+    do {                                                                                                        \
+        if (pack)                                                                                               \
+            hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, true>), dim3(nseg * P), dim3(kOwnT), 0, s,   \
+                               seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
+                               rec_vals, rec_cap);                                                              \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, false>), dim3(nseg * P), dim3(kOwnT), 0, s,  \
+                               seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
+                               rec_vals, rec_cap);                                                              \
+    } while (0)
 #define SH_AGG_OWN_F(VV, KK, RR)                          \
     do {                                                  \
         if (F == 2) SH_AGG_OWN(VV, KK, RR, 2, 0);         \
@@ -1171,11 +1188,11 @@ void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u3
 // its staging slot (partition-major, event order inside a partition), and the staged tile is
 // written out as one contiguous run per partition.
 // LDS: stage_vals[V][kTile] | stage_pos[kTile] | stage_idx[kTile] | start[P] | gbase[P] (i64) | run[4][P] (u16)
-template <int V>
+template <int V, bool PACK>
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
                                                       const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
-                                                      const u32* __restrict__ offsets, u32* rec_pos,
+                                                      int logP, const u32* __restrict__ offsets, u32* rec_pos,
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     const int nblk = m.nblk;
     const int tile = xcd_tile(nblk);
@@ -1317,8 +1334,12 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
     for (u32 j = threadIdx.x; j < n_tile; j += kBlock) {
         const u32 pp = stage_pos[j] & (P - 1);
         const i64 dst = gbase[pp] + j;
-        rec_pos[dst] = stage_pos[j];
-        rec_idx[dst] = stage_idx[j];
+        if (PACK) {
+            rec_idx[dst] = ((stage_pos[j] >> logP) << kPackIdxBits) | (stage_idx[j] & kPackIdxMask);
+        } else {
+            rec_pos[dst] = stage_pos[j];
+            rec_idx[dst] = stage_idx[j];
+        }
 #pragma unroll
         for (int v = 0; v < V; v++)
             if (v < ap.n_vcols) rec_vals[(size_t)v * rec_cap + dst] = stage_vals[(size_t)v * kTile + j];
@@ -1326,16 +1347,24 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
 }
 
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, const u32* offsets,
-                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap) {
+                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
+                       u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap, bool pack) {
     const int nblk = m.nblk;
     const int V = ap.n_vcols <= 1 ? 1 : ap.n_vcols <= 2 ? 2 : ap.n_vcols <= 4 ? 4 : 8;
     size_t lds = (size_t)V * kTile * 8 + (size_t)kTile * 8 + (size_t)P * 4 + 4 + (size_t)P * 8 +
                  (size_t)P * 2 * (kBlock / 64) + 32;
     int grid = ((nblk + 7) >> 3) * 8;
 #define SH_MS(VV)                                                                                                   \
-    hipLaunchKernelGGL(k_ms_scatter<VV>, dim3(grid), dim3(kBlock), lds, s, m, n_pend, pend_pos, pend_vals, pend_cap, \
-                       new_pos, cols, ap, P, offsets, rec_pos, rec_idx, rec_vals, rec_cap)
+    do {                                                                                                            \
+        if (pack)                                                                                                   \
+            hipLaunchKernelGGL((k_ms_scatter<VV, true>), dim3(grid), dim3(kBlock), lds, s, m, n_pend, pend_pos,       \
+                               pend_vals, pend_cap, new_pos, cols, ap, P, logP, offsets, rec_pos, rec_idx, rec_vals,  \
+                               rec_cap);                                                                            \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_ms_scatter<VV, false>), dim3(grid), dim3(kBlock), lds, s, m, n_pend, pend_pos,      \
+                               pend_vals, pend_cap, new_pos, cols, ap, P, logP, offsets, rec_pos, rec_idx, rec_vals,  \
+                               rec_cap);                                                                            \
+    } while (0)
     if (V == 1) SH_MS(1);
     else if (V == 2) SH_MS(2);
     else if (V == 4) SH_MS(4);

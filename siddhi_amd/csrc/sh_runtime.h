@@ -240,6 +240,7 @@ struct sh_query {
     PinnedBuf h_bounds;  // pinned landing area of the push's window boundaries
     // the multisplit of the push's events, launched before the host reads the window boundaries
     bool ms_ready = false;
+    bool rec_packed = false;  // the split wrote packed records (rec_idx only)
     TileMap ms_map{};  // tiling of the last multisplit
     int64_t rec_cap = 0;
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation
@@ -379,5 +380,5 @@ void sliding_destroy(sh_query* q);
 // counted: k_boundaries already wrote the counts of the push's tiles (tiling make_tile_map(n_pend, hi),
 // buffers sized by reserve_ms_counts before it ran)
 int reserve_ms_counts(sh_query* q, const TileMap& m);
-int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted = false);
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted = false, bool wide = false);
 

@@ -349,7 +349,11 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     SH_TRACE("run_closed nseg=%d closed_hi=%lld row_cap=%lld own=%d P=%d NL=%d ms_ready=%d", nseg, (long long)closed_hi,
              (long long)row_cap, (int)own, q->P, q->NL, (int)q->ms_ready);
     if (own) {
-        if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b));
+        // a packed split (kPackIdxBits of event index per record) serves segments up to 2^22 events
+        bool long_seg = false;
+        for (auto& sg : segs) long_seg |= sg.hi - sg.lo > (int64_t)kPackIdxMask + 1;
+        if (q->ms_ready && q->rec_packed && long_seg) q->ms_ready = false;
+        if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b, false, long_seg));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
         launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), b ? q->new_pos.as<u32>() : nullptr, q->P,
                            q->ms_counts.as<u32>(), q->ms_map, q->seg_off.as<int64_t>());
@@ -362,7 +366,8 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     launch_aggregate(s, dsegs, nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(),
                      q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
                      unit_rows, q->first_bits.as<u32>(),
-                     own ? rec_pos : nullptr, rec_idx, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>());
+                     rec_pos, own ? rec_idx : nullptr, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>(),
+                     q->rec_packed);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     // output columns sized for the row capacity; the emit kernels read the row count on the device
@@ -1267,7 +1272,7 @@ int reserve_ms_counts(sh_query* q, const TileMap& m) {
     return q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false);
 }
 
-int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted) {
+int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted, bool wide) {
     hipStream_t s = q->ctx->stream;
     int P = q->P;
     ColSet cs{};
@@ -1278,7 +1283,9 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted) {
     RCHK(reserve_ms_counts(q, m));  // (the size k_boundaries' counts were written into: no regrowth)
     RCHK(q->part_off.reserve((P + 1) * 8, false));
     int64_t cap = std::max<int64_t>(hi, 1);
-    RCHK(q->rec_pos.reserve(cap * 4, false));
+    // packed records (local key | low index bits in one word) unless a segment may be too long
+    const bool pack = !wide && q->NL <= 1024;
+    if (!pack) RCHK(q->rec_pos.reserve(cap * 4, false));
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
     const u32* np = b ? q->new_pos.as<u32>() : nullptr;
@@ -1288,9 +1295,11 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted) {
     // gives every (partition, block) its offset, and partition p starts at offset[p * nblk]
     launch_scan_sum_large_u32(s, q->ms_counts.as<u32>(), ncnt + 1, q->ms_tmp.as<int64_t>());
     launch_ms_scatter(s, m, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
-                      q->ms_counts.as<u32>(), q->rec_pos.as<u32>(), q->rec_idx.as<u32>(), q->rec_vals.as<u64>(), cap);
+                      q->logP, q->ms_counts.as<u32>(), pack ? nullptr : q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
+                      q->rec_vals.as<u64>(), cap, pack);
     HIPCHK(hipGetLastError());
     q->ms_ready = true;
+    q->rec_packed = pack;
     q->ms_map = m;
     q->rec_cap = cap;
     return SH_OK;

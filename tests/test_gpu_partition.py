@@ -40,9 +40,10 @@ def stream(n, parts, seed, step=3, runs=False, zipf=False):
 
 
 @pytest.mark.parametrize("output", ["current", "all", "expired"])
-@pytest.mark.parametrize("L,group", [(1, True), (3, False), (100, True)])
-def test_partitioned_lengthbatch(rt, output, L, group):
-    ts, cols = stream(30_000, 200, 41, runs=True)
+@pytest.mark.parametrize("L,group,parts", [(1, True, 200), (3, False, 200), (100, True, 40)])
+def test_partitioned_lengthbatch(rt, output, L, group, parts):
+    """(L = 100 over 40 partitions: several batches per partition, so expired rows exist)"""
+    ts, cols = stream(30_000, parts, 41, runs=True)
     spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["p"] if group else [], aggs=AGGS, partition="p",
                          filter=(">", "v", -30.0), output=output, key_capacity=256)
     ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 7_777, 20_000], 5), f"plb {L} {output}")
