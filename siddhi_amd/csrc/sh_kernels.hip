@@ -273,10 +273,17 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
         key_slots<kItems>(kt, key, pass, pos);
 #pragma unroll
         for (int i = 0; i < kItems; i++) pos[i] = pass[i] ? pos[i] : kNoPos;
-        if (base + kItems <= wp.N && (((size_t)(new_pos + base)) & 15) == 0) {
-            uint4* q = (uint4*)(new_pos + base);
-            q[0] = make_uint4(pos[0], pos[1], pos[2], pos[3]);
-            q[1] = make_uint4(pos[4], pos[5], pos[6], pos[7]);
+        const i64 tile0 = (i64)tile * kTile;
+        if (tile0 + kTile <= wp.N && (((size_t)(new_pos + tile0)) & 15) == 0) {
+            // transposed through LDS so every store instruction covers whole lines (a thread's own
+            // 32-byte run would leave each 16-byte store half a line, written back twice)
+            __shared__ uint4 tp[kTile / 4];
+            tp[threadIdx.x * 2] = make_uint4(pos[0], pos[1], pos[2], pos[3]);
+            tp[threadIdx.x * 2 + 1] = make_uint4(pos[4], pos[5], pos[6], pos[7]);
+            __syncthreads();
+            uint4* q = (uint4*)(new_pos + tile0);
+            q[threadIdx.x] = tp[threadIdx.x];
+            q[threadIdx.x + kBlock] = tp[threadIdx.x + kBlock];
         } else {
 #pragma unroll
             for (int i = 0; i < kItems; i++)
@@ -817,6 +824,21 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     const i64 pre = block_excl_scan_any((i64)mine, &tot);
     if (t == 0) unit_rows[blockIdx.x] = (u32)tot;
     u32 r = (u32)blockIdx.x * (u32)(K * kOwnT) + (u32)pre;
+    if (K == 1 && (size_t)kOwnT * RW * 8 <= sizeof(st_v)) {
+        // the unit's rows are one contiguous run: staged in LDS (the record staging is free now),
+        // then stored with whole-line writes instead of each thread's strided 16-byte pieces
+        u64* stg = &st_v[0][0];
+        __syncthreads();
+        if (cnt0) write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
+        if (cnt0) mark_first(first_bits, fst0);
+        __syncthreads();
+        const int n2 = (int)tot * RW / 2;
+        ulonglong2* dst = (ulonglong2*)(rows + (size_t)blockIdx.x * (K * kOwnT) * RW);
+        const ulonglong2* src = (const ulonglong2*)stg;
+        for (int i = t; i < n2; i += kOwnT) dst[i] = src[i];
+        SH_STAMP(0, 6);
+        return;
+    }
     if (cnt0) {
         write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
         mark_first(first_bits, fst0);
@@ -991,7 +1013,11 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
     __shared__ i64 so[kBlock];
     // thread (unit, j): the j-th row of a unit's region, if the unit produced that many
     const int t = threadIdx.x;
-    const i64 r = (i64)blockIdx.x * kBlock + t;
+    // XCD-aware: each XCD takes a contiguous run of blocks (a few windows), so the random reads of
+    // its rows' last-event timestamps stay inside a window-sized range its own L2 holds
+    const int nb = gridDim.x, per = (nb + 7) >> 3;
+    const int lb = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    const i64 r = (i64)lb * kBlock + t;
     const i64 u = r / unit_stride;
     const bool valid = u < n_units && (u32)(r - u * unit_stride) < unit_rows[u];
     const int nk = kp.n, SW = stage_words(nk, n_aggs, want_order);
@@ -1069,7 +1095,8 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
                       i64 seq_base, i64* out_rep, u64* stage) {
     if (row_cap <= 0 || n_units <= 0) return;
     const int want_order = out_order ? 1 : 0;
-    const unsigned g1 = (unsigned)((n_units * unit_stride + kBlock - 1) / kBlock);
+    // (rounded to a multiple of 8 for the XCD-aware block order; surplus blocks find no row)
+    const unsigned g1 = (unsigned)(((n_units * unit_stride + kBlock - 1) / kBlock + 7) / 8 * 8);
     hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, word_pre,
                        n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
     const unsigned g2 = (unsigned)((row_cap + kBlock - 1) / kBlock);

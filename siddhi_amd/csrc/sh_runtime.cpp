@@ -98,20 +98,25 @@ bool sh_trace_on() {
 // ---------------------------------------------------------------------------------------------
 thread_local hipStream_t g_stream = nullptr;
 
-// Stream-ordered growth on the calling context's stream: the copy of the kept bytes and the free of
-// the old block are queued behind the kernels that still use it. Outside any API scope (g_stream
-// null) the old block is released after a wait for the device.
+// Growth on the calling context's stream, with plain (not stream-ordered) allocations: the stream is
+// drained before the old block is copied and freed. hipMallocAsync / hipFreeAsync pool reuse was seen
+// to hand a block back while a copy out of it was still pending (the sliding window's FIFO came back
+// corrupted at C3 size, nondeterministically); growth is rare (x1.5 steps), so two waits per growth
+// cost nothing in steady state. Outside any API scope (g_stream null) the whole device is drained.
+static hipError_t drain() { return g_stream ? hipStreamSynchronize(g_stream) : hipDeviceSynchronize(); }
+
 int DevBuf::reserve(size_t n, bool keep) {
     if (n <= cap) return SH_OK;
     size_t ncap = std::max(n, cap + cap / 2);
     void* np = nullptr;
-    hipError_t e = g_stream ? hipMallocAsync(&np, ncap, g_stream) : hipMalloc(&np, ncap);
+    hipError_t e = hipMalloc(&np, ncap);
     if (e != hipSuccess) return sh_fail(SH_ERR_OOM, "device allocation failed: " + std::string(hipGetErrorString(e)));
     if (p) {
         if (keep && used) {
             e = hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, g_stream);
             if (e != hipSuccess) {
-                (void)(g_stream ? hipFreeAsync(np, g_stream) : hipFree(np));
+                (void)drain();
+                (void)hipFree(np);
                 return sh_fail(SH_ERR_DEVICE, "device copy (grow) failed");
             }
         }
@@ -124,12 +129,8 @@ int DevBuf::reserve(size_t n, bool keep) {
 
 void DevBuf::release() {
     if (p) {
-        if (g_stream) {
-            (void)hipFreeAsync(p, g_stream);
-        } else {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(p);
-        }
+        (void)drain();  // kernels and copies queued on the block have finished
+        (void)hipFree(p);
     }
     p = nullptr;
     cap = used = 0;

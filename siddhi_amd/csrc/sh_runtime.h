@@ -48,10 +48,9 @@ void sh_timing_mark(int point);
 hipError_t sh_wait_stream(hipStream_t s);
 hipError_t sh_wait_event(hipEvent_t e);
 
-// The stream of the context whose API call is running on this thread. Device buffers grow and are
-// freed in that stream's order (hipMallocAsync / hipFreeAsync), so a growth never waits on other
-// streams and never frees memory a queued kernel still reads. Every extern "C" entry point that
-// touches a context opens a StreamScope.
+// The stream of the context whose API call is running on this thread. A device buffer's growth or
+// release drains that stream before the old block is freed, so no queued kernel or copy still reads
+// it (DevBuf::reserve). Every extern "C" entry point that touches a context opens a StreamScope.
 extern thread_local hipStream_t g_stream;
 struct StreamScope {
     hipStream_t prev;
