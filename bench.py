@@ -83,6 +83,45 @@ def cpu_baseline(args):
                       f"{t_used:.1f} s single-thread in the C++ restatement (oracle/), not stock Siddhi (no JVM)"}
 
 
+def _cpu_shard_worker(job):
+    """All-cores baseline, one worker: its key-hash shard (id % P == i) of the C2 sample stream through
+    its own oracle runtime (P runtimes on disjoint key-hash shards). Only push_raw is timed."""
+    key_type, keys, epm, send_size, seconds, P, i = job
+    from oracle.oracle import OracleQuery
+    from siddhi_amd import abi, synth
+    schema = abi.Schema.parse(f"k {key_type}, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys)
+    q = OracleQuery(spec)
+    n_done, t_used, pos, chunk = 0, 0.0, 0, 1_000_000
+    while t_used < seconds and pos < 400_000_000:
+        ts, cols = synth.keyed_stream(pos, chunk, 0xC2, keys, epm)
+        m = (cols[0] % P) == i
+        b = abi.HostBatch(schema, ts[m], [c[m] for c in cols], send_size)
+        t0 = time.perf_counter()
+        q.push_raw(b)
+        t_used += time.perf_counter() - t0
+        n_done += int(m.sum())
+        pos += chunk
+    q.close()
+    return n_done, t_used, pos
+
+
+def cpu_baseline_all_cores(args, pool, P):
+    """P oracle runtimes in parallel worker processes (started before the GPU was touched), each on
+    its key-hash shard; rate = the shards' events / the slowest shard's push time."""
+    t0 = time.perf_counter()
+    res = pool.map(_cpu_shard_worker, [(args.key_type, args.keys, args.events_per_ms, args.send_size,
+                                        max(1.0, args.cpu_seconds / 4), P, i) for i in range(P)])
+    wall = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    t = max(r[1] for r in res)
+    return {"value": n / t, "unit": "events/s", "cores": P, "kind": "port",
+            "sample": f"{n} events: the first {max(r[2] for r in res)} events (at most) of the same C2 stream split into {P} "
+                      f"key-hash shards (id % {P}), each through its own oracle runtime in its own process; "
+                      f"slowest shard {t:.1f} s of push time ({wall:.1f} s wall with stream generation)"}
+
+
 # The PMC summary the roofline's `traffic` is read from: collected on exactly the default C2
 # configuration with the current kernels (scripts/profile_bench.sh + scripts/pmc_summary.py).
 TRAFFIC_SUMMARY = "profiles/r02_c2_v2_pmc.json"
@@ -322,6 +361,17 @@ def run_host(args, dev):
 
 def main():
     args = parse()
+    # all-cores CPU baseline workers: started before anything touches the GPU (rank 0, N = 1 only)
+    pool, P = None, 0
+    if (not args.no_cpu_baseline and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.workload == "c2"
+            and not args.host):
+        import multiprocessing as mp
+        P = max(2, min(15, os.cpu_count() or 2))
+        # the workers run the oracle only: they must not load a HIP runtime (siddhi_amd binds one at
+        # import), or each would hold the GPU open next to this process
+        os.environ["SIDDHI_AMD_BIND_HIP"] = "0"
+        pool = mp.get_context("spawn").Pool(P)
+        os.environ.pop("SIDDHI_AMD_BIND_HIP", None)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -485,6 +535,10 @@ def main():
         result["config"]["phases_ms_per_step_rank0"] = {k: v / args.steps for k, v in phases.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
+        if pool is not None:
+            result["cpu_baseline_all_cores"] = cpu_baseline_all_cores(args, pool, P)
+            pool.close()
+            pool.join()
     if rank == 0:
         print(json.dumps(result), flush=True)
     q.close()

@@ -591,6 +591,7 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
 }
 
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
+    SH_RANGE("sh_aggregation_push");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
@@ -598,6 +599,7 @@ extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
 }
 
 extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) {
+    SH_RANGE("sh_aggregation_push_device");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !b) return sh_fail(SH_ERR_INVALID, "sh_aggregation_push_device: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation ingests through sh_shard_*");
@@ -607,6 +609,7 @@ extern "C" int sh_aggregation_push_device(sh_aggregation* a, const sh_batch* b) 
 
 
 extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
+    SH_RANGE("sh_aggregation_advance_time");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation advances through sh_shard_advance_time");
@@ -617,6 +620,7 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
 }
 
 extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out** out) {
+    SH_RANGE("sh_aggregation_table");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_table: NULL argument");
     if (dur < a->d.min_duration || dur > a->d.max_duration) return sh_fail(SH_ERR_INVALID, "duration not aggregated");
@@ -707,6 +711,7 @@ static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* k
 }
 
 extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start, int64_t end, const sh_out** out) {
+    SH_RANGE("sh_aggregation_find");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_find: NULL argument");
     if (per < a->d.min_duration || per > a->d.max_duration)
@@ -890,12 +895,8 @@ uint64_t agg_fingerprint(const sh_aggregation* a) {
 constexpr uint32_t kAggSnapVersion = 1;
 }  // namespace
 
-extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap, int64_t* len) {
-    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
-    if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
-    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation");
+static int agg_snapshot_blob(sh_aggregation* a, ABlob& w) {
     hipStream_t s = a->ctx->stream;
-    ABlob w;
     w.b.insert(w.b.end(), {'S', 'H', 'A', '1'});
     w.val<uint32_t>(kAggSnapVersion);
     w.val<uint64_t>(agg_fingerprint(a));
@@ -935,6 +936,16 @@ extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap
         RCHK(w.dev(t.key.p, t.n * 8, s));
         for (int b = 0; b < a->nb; b++) RCHK(w.dev(t.vals.as<u64>() + (size_t)b * t.cap, t.n * 8, s));
     }
+    return SH_OK;
+}
+
+extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap, int64_t* len) {
+    SH_RANGE("sh_aggregation_snapshot");
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation");
+    ABlob w;
+    RCHK(agg_snapshot_blob(a, w));
     *len = (int64_t)w.b.size();
     if (buf) {
         if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: buffer too small (call with buf=NULL for the size)");
@@ -943,11 +954,8 @@ extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap
     return SH_OK;
 }
 
-extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len) {
-    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
-    if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
-    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "restore of a sharded aggregation");
-    if (std::memcmp(buf, "SHA1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip aggregation snapshot");
+static int agg_restore_blob(sh_aggregation* a, const void* buf, int64_t len) {
+    if (len < 20 || std::memcmp(buf, "SHA1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip aggregation snapshot");
     hipStream_t s = a->ctx->stream;
     AReader r{(const uint8_t*)buf, (size_t)len};
     r.o = 4;
@@ -1006,4 +1014,22 @@ extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_
     }
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;
+}
+
+// All or nothing: the aggregation's current state is snapshotted first and put back when the blob
+// fails part-way (the root window, an executor or a table section), keeping the first error.
+extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len) {
+    SH_RANGE("sh_aggregation_restore");
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "restore of a sharded aggregation");
+    ABlob backup;
+    const bool have = agg_snapshot_blob(a, backup) == SH_OK;
+    const int rc = agg_restore_blob(a, buf, len);
+    if (rc != SH_OK && have) {
+        const std::string msg = sh_last_error();
+        (void)agg_restore_blob(a, backup.b.data(), (int64_t)backup.b.size());
+        return sh_fail(rc, msg);
+    }
+    return rc;
 }

@@ -217,22 +217,38 @@ __device__ __forceinline__ void filter_items(const FilterProg& f, const ColSet& 
 // ---- group keys ---------------------------------------------------------------------------------
 // GroupByKeyGenerator.constructEventKey (core/query/selector/GroupByKeyGenerator.java:63-73) keys
 // by the values' string form; for the integral key columns string equality is value equality.
+// Floating-point keys: String.valueOf(double / float) names every value apart (0.0 and -0.0 too)
+// except NaN, whose payloads all print "NaN" — so the key is the value's bits with NaN made canonical.
+// A float alone is keyed by its value widened to double (an injective map); as one of two 32-bit
+// components by its own (canonical) bits.
 __device__ __forceinline__ i64 key_part(const KeyPlan& kp, const ColSet& cs, int g, i64 e) {
     i64 v = load_raw(cs, kp.col[g], e);
+    const int t = kp.type[g];
+    if (t == SH_T_FLOAT || t == SH_T_DOUBLE) return __longlong_as_double(v) != __longlong_as_double(v) ? 0x7FF8000000000000ll : v;
     // aggregation time bucket: getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69)
     if (kp.div[g] > 0) v = v / kp.div[g];
     return v;
 }
 
+__device__ __forceinline__ u32 key_part32(const KeyPlan& kp, const ColSet& cs, int g, i64 e) {
+    if (kp.type[g] == SH_T_FLOAT) {
+        const float f = ((const float*)cs.ptr[kp.col[g]])[e];
+        return f != f ? 0x7FC00000u : __float_as_uint(f);
+    }
+    return (u32)key_part(kp, cs, g, e);
+}
+
 __device__ __forceinline__ u64 make_key(const KeyPlan& kp, const ColSet& cs, i64 e) {
     if (kp.n == 0) return 0;
     if (kp.n == 1) return (u64)key_part(kp, cs, 0, e);
-    u64 a = (u64)(u32)key_part(kp, cs, 0, e);
-    u64 b = (u64)(u32)key_part(kp, cs, 1, e);
+    u64 a = (u64)key_part32(kp, cs, 0, e);
+    u64 b = (u64)key_part32(kp, cs, 1, e);
     return (a << 32) | b;
 }
 
+// a component as sh_out reports it: int64 widening; floats as the bits of the value widened to double
 __device__ __forceinline__ i64 unpack_part(const KeyPlan& kp, int g, u32 x) {
+    if (kp.type[g] == SH_T_FLOAT) return __double_as_longlong((double)__uint_as_float(x));
     return kp.div[g] > 0 ? (i64)x * kp.div[g] : (i64)(int)x;
 }
 

@@ -47,6 +47,7 @@ void ingest_destroy(sh_query* q) {
 }
 
 extern "C" int sh_stage(sh_query* q, const sh_batch* b, int32_t* ticket) {
+    SH_RANGE("sh_stage");
     if (!q || !b || !ticket) return sh_fail(SH_ERR_INVALID, "sh_stage: NULL argument");
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (b->n > 0 && !b->ts) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
@@ -80,6 +81,7 @@ extern "C" int sh_stage(sh_query* q, const sh_batch* b, int32_t* ticket) {
 }
 
 extern "C" int sh_push_staged(sh_query* q, int32_t ticket, const sh_out** out) {
+    SH_RANGE("sh_push_staged");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_push_staged: NULL argument");
     auto& g = q->ing;

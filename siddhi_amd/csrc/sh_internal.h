@@ -159,9 +159,40 @@ struct Segment {
     i64 lo, hi;
 };
 
+// Key slot of a push event: from the key-slot column k_boundaries wrote (np), or — dictionary keys
+// that are their own slots, no filter (k_boundaries then writes no slot column) — the key column
+// itself, clamped to the table (an id outside it has already failed the push).
+struct PosSrc {
+    const u32* np;
+    const int* key;
+    u32 mask;
+    int pad;
+};
+__host__ __device__ inline u32 pos_at(const PosSrc& ps, i64 x) {
+    if (ps.np) return ps.np[x];
+    const u32 id = (u32)ps.key[x];
+    return id > ps.mask ? ps.mask : id;
+}
+__host__ __device__ inline bool pos_any(const PosSrc& ps) { return ps.np || ps.key; }
+
 // Row record of the aggregation kernels: row_words(n_aggs) u64 words — slot | count << 32,
-// first | last << 32 (combined event indices), then the aggregate values.
-__host__ __device__ constexpr int row_words(int n_aggs) { return (2 + n_aggs + 1) & ~1; }
+// first | last << 32 (combined event indices), the last event's timestamp and stream index (read by
+// the aggregation kernel itself, so the emission only permutes whole records), then the values.
+__host__ __device__ constexpr int row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
+// where a row's last-event timestamp and stream index come from (combined index space)
+struct EvSrc {
+    i64 n_pend;
+    const i64* pend_ts;
+    const i64* ts;
+    const u64* pend_gidx;
+    const u64* new_gidx;  // sharded owner: global stream index of every new event; else seq_base + e
+    i64 seq_base;
+};
+__host__ __device__ inline i64 ev_ts(const EvSrc& es, u32 c) { return c < es.n_pend ? es.pend_ts[c] : es.ts[c - es.n_pend]; }
+__host__ __device__ inline i64 ev_seq(const EvSrc& es, u32 c) {
+    if (c < es.n_pend) return (i64)es.pend_gidx[c];
+    return es.new_gidx ? (i64)es.new_gidx[c - es.n_pend] : es.seq_base + (i64)(c - es.n_pend);
+}
 
 // Launchers (sh_kernels.hip).
 void launch_blockagg(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, i64 N, i64 send_size,
@@ -185,7 +216,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       // multisplit source (P > 1 or long windows; null: the flat kernel reads the batch)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
-                      bool pack = false);
+                      bool pack, EvSrc es);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
 // word_pre[w] = exclusive popcount prefix of the first-occurrence bitmap before word w (low 32 bits)
@@ -199,9 +230,23 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
                       i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
                       i64 seq_base, i64* out_rep, u64* stage);
 size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows);
-void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
+void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, PosSrc new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);
+// small pushes that close no window (sh_window.cpp try_small_push): one workgroup of kSmallT threads
+constexpr int kSmallT = 1024;
+constexpr int kSmallMax = kSmallT * kItems;
+struct SmallRes {
+    i64 total_pass;  // passing events appended to the open window
+    i64 max_tl;      // the push's last timestamp (its clock; timestamps are non-decreasing here)
+    int fallback;    // a window closes / timestamps decrease: nothing appended, run the full pipeline
+    int pad;
+    u32 ctrl[4];     // the key table's control words after the lookups (KeyTableHost::check_result)
+    u64 token;       // written last: the host waits for it
+};
+void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt,
+                       AggPlan ap, u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap, u64* pend_gidx,
+                       i64 seq_base, SmallRes* res, u64 token);
 // multisplit (partitioned aggregation, P > 1)
 // Multisplit tiles over the combined index space [0, hi) of queued + new events: tiles of kTile
 // events over [0, split) (the queued events), then tiles of kTile over [split, hi) (the push's
@@ -235,16 +280,19 @@ __host__ __device__ inline int tile_of(const TileMap& m, i64 b) {
 }
 
 // counts the first n_count tiles of the map (k_boundaries counted the others) and zeroes the total slot
-void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, PosSrc new_pos, int P,
                      u32* counts);
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
+                       i64 pend_cap, PosSrc new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap, bool pack);
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp);
+// the multisplit's [tile][partition] count matrix -> record offsets in place (row nblk: partition ends)
+size_t ms_offsets_tmp_bytes(int nblk, int P);
+void launch_ms_offsets(hipStream_t s, u32* counts, int nblk, int P, i64* tmp);
 void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const u32* counts, TileMap m, i64* seg_off);
+                        PosSrc new_pos, int P, const u32* counts, TileMap m, i64* seg_off);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 // sharded ingest (sh_shard_kernels.hip)

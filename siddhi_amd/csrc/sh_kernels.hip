@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     {
         u64 key[kItems];
         u32 pos[kItems];
-        if (kp.n == 1 && kp.div[0] == 0) {
+        if (kp.n == 1 && kp.div[0] == 0 && kp.type[0] != SH_T_FLOAT && kp.type[0] != SH_T_DOUBLE) {
             i64 raw[kItems];
             load_items_raw(cols, kp.col[0], base, wp.N, raw);
 #pragma unroll
@@ -274,7 +274,9 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
 #pragma unroll
         for (int i = 0; i < kItems; i++) pos[i] = pass[i] ? pos[i] : kNoPos;
         const i64 tile0 = (i64)tile * kTile;
-        if (tile0 + kTile <= wp.N && (((size_t)(new_pos + tile0)) & 15) == 0) {
+        if (!new_pos) {
+            // dictionary keys are their own slots (PosSrc reads the key column): no slot column
+        } else if (tile0 + kTile <= wp.N && (((size_t)(new_pos + tile0)) & 15) == 0) {
             // transposed through LDS so every store instruction covers whole lines (a thread's own
             // 32-byte run would leave each 16-byte store half a line, written back twice)
             __shared__ uint4 tp[kTile / 4];
@@ -299,8 +301,9 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
             for (int i = 0; i < kItems; i++)
                 if (pass[i]) atomicAdd(&mhist[pos[i] & (P - 1)], 1u);
             __syncthreads();
+            // the tile's row of the [tile][partition] count matrix: one contiguous store per tile
             for (int i = threadIdx.x; i < P; i += kBlock)
-                ms_counts[(i64)i * ms_nblk + ms_col0 + tile] = mhist[i];
+                ms_counts[(i64)(ms_col0 + tile) * P + i] = mhist[i];
         }
     }
     i64 t[kItems];
@@ -530,19 +533,21 @@ __device__ __forceinline__ u64 agg_out(const AggPlan& ap, int a, u32 c, u64 fv) 
 // one row record (see above) with 16-byte stores
 template <int F = SH_MAX_AGGS>
 __device__ __forceinline__ void write_row(const AggPlan& ap, u64* row, int RW, u32 pos, u32 c, u32 first, u32 last,
-                                          const u64 (&f)[F]) {
-    u64 w[2 + SH_MAX_AGGS];
+                                          const u64 (&f)[F], const EvSrc& es) {
+    u64 w[4 + SH_MAX_AGGS];
     w[0] = (u64)pos | ((u64)c << 32);
     w[1] = (u64)first | ((u64)last << 32);
+    w[2] = (u64)ev_ts(es, last);
+    w[3] = (u64)ev_seq(es, last);
 #pragma unroll
     for (int a = 0; a < SH_MAX_AGGS; a++) {
         u64 fv = f[0];
 #pragma unroll
         for (int j = 1; j < F; j++) if (ap.field[a] == j) fv = f[j];
-        w[2 + a] = a < ap.n ? agg_out(ap, a, c, fv) : 0;
+        w[4 + a] = a < ap.n ? agg_out(ap, a, c, fv) : 0;
     }
 #pragma unroll
-    for (int i = 0; i < (2 + SH_MAX_AGGS) / 2; i++) {
+    for (int i = 0; i < (4 + SH_MAX_AGGS) / 2; i++) {
         if (2 * i >= RW) break;
         ((ulonglong2*)row)[i] = make_ulonglong2(w[2 * i], w[2 * i + 1]);
     }
@@ -583,7 +588,8 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
                                                           const u32* __restrict__ pend_pos,
                                                           const u64* __restrict__ pend_vals, i64 pend_cap,
                                                           const u32* __restrict__ new_pos, ColSet cols, AggPlan ap,
-                                                          u64* rows, int RW, u32* unit_rows, u32* first_bits) {
+                                                          u64* rows, int RW, u32* unit_rows, u32* first_bits,
+                                                          EvSrc es) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     AggLds L;
     lds_layout(smem_raw, ap, NL, L);
@@ -642,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void k_aggregate_flat(const Segment* __rest
         u64 f[SH_MAX_AGGS];
 #pragma unroll
         for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = j < ap.n_fields ? L.fields[(size_t)j * NL + i] : 0;
-        write_row(ap, rows + (size_t)r * RW, RW, (u32)i, c, L.first[i], L.last[i], f);
+        write_row(ap, rows + (size_t)r * RW, RW, (u32)i, c, L.first[i], L.last[i], f, es);
         mark_first(first_bits, L.first[i]);
         r++;
     }
@@ -663,7 +669,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
                                                            u32* first_bits, const Segment* __restrict__ segs,
                                                            const u32* __restrict__ rec_pos,
                                                            const u32* __restrict__ rec_idx,
-                                                           const u64* __restrict__ rec_vals, i64 rec_cap) {
+                                                           const u64* __restrict__ rec_vals, i64 rec_cap, EvSrc es) {
     constexpr int W = kOwnT / 64;
     constexpr int PW = 64 * R;   // records per wave and chunk
     constexpr int CH = kOwnT * R;
@@ -829,7 +835,7 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         // then stored with whole-line writes instead of each thread's strided 16-byte pieces
         u64* stg = &st_v[0][0];
         __syncthreads();
-        if (cnt0) write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
+        if (cnt0) write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es);
         if (cnt0) mark_first(first_bits, fst0);
         __syncthreads();
         const int n2 = (int)tot * RW / 2;
@@ -840,12 +846,12 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         return;
     }
     if (cnt0) {
-        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0);
+        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es);
         mark_first(first_bits, fst0);
         r++;
     }
     if (K > 1 && cnt1) {
-        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)(t + kOwnT) << logP) | (u32)p, cnt1, fst1, lst1, f1);
+        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)(t + kOwnT) << logP) | (u32)p, cnt1, fst1, lst1, f1, es);
         mark_first(first_bits, fst1);
     }
     SH_STAMP(0, 6);
@@ -859,7 +865,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
-                      bool pack) {
+                      bool pack, EvSrc es) {
     if (rec_idx) {  // multisplit records: thread-ownership kernel
         const int K = own_keys_per_thread(NL);
         const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
@@ -868,11 +874,11 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
         if (pack)                                                                                               \
             hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, true>), dim3(nseg * P), dim3(kOwnT), 0, s,   \
                                seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
-                               rec_vals, rec_cap);                                                              \
+                               rec_vals, rec_cap, es);                                                          \
         else                                                                                                    \
             hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, false>), dim3(nseg * P), dim3(kOwnT), 0, s,  \
                                seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
-                               rec_vals, rec_cap);                                                              \
+                               rec_vals, rec_cap, es);                                                          \
     } while (0)
 #define SH_AGG_OWN_F(VV, KK, RR)                          \
     do {                                                  \
@@ -910,7 +916,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
     } else {
         size_t lds = (size_t)NL * (8 * ap.n_fields + 16) + 16;
         hipLaunchKernelGGL(k_aggregate_flat, dim3(nseg), dim3(kBlock), lds, s, segs, NL, n_pend, pend_pos, pend_vals,
-                           pend_cap, new_pos, cols, ap, rows, RW, unit_rows, first_bits);
+                           pend_cap, new_pos, cols, ap, rows, RW, unit_rows, first_bits, es);
     }
 }
 
@@ -1025,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
     if (valid) {
         const u64* row = rows + (size_t)r * RW;
         const ulonglong2 h = *(const ulonglong2*)row;
-        const u32 pos = (u32)h.x, first = (u32)h.y, last = (u32)(h.y >> 32);
+        const u32 pos = (u32)h.x, first = (u32)h.y;
         const u32 wd = first >> 5;
         const u64 wp2 = word_pre[wd];  // one read: the bitmap word and the rows before it
         const i64 o = (i64)(u32)wp2 + __popc((u32)(wp2 >> 32) & ((1u << (first & 31)) - 1u));
@@ -1035,16 +1041,17 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
             return new_gidx ? (i64)new_gidx[c - n_pend] : seq_base + (i64)(c - n_pend);
         };
         u64 w[kStageMax + 1];
-        w[0] = (u64)(last < n_pend ? pend_ts[last] : ts[last - n_pend]);
+        const ulonglong2 tr = *(const ulonglong2*)(row + 2);  // the last event's timestamp and stream index
+        w[0] = tr.x;
         i64 kv[SH_MAX_GROUP] = {0, 0};
         unpack_key(kp, slot_key(kt, pos), kv, 1);
-        w[1] = (u64)sidx(last);
+        w[1] = tr.y;
         w[2] = (u64)kv[0];
         w[3] = (u64)kv[1];
         int c = 2 + nk;
         if (want_order) w[c++] = (u64)sidx(first);
 #pragma unroll
-        for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) w[c + a] = row[2 + a];
+        for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) w[c + a] = row[4 + a];
 #pragma unroll
         for (int i = 0; i < kStageMax / 2; i++) {
             if (2 * i >= SW) break;
@@ -1111,7 +1118,7 @@ size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows) { return (size_t)
 // (the window's queued events, LengthBatch WindowState.currentEventQueue / TimeBatch queue).
 // ================================================================================================
 __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restrict__ ts, ColSet cols,
-                                                           const u32* __restrict__ new_pos, AggPlan ap, i64 e_lo,
+                                                           PosSrc new_pos, AggPlan ap, i64 e_lo,
                                                            i64 N, i64 pcb_lo, i64 dst_base, const i64* blk_pass_pre,
                                                            int blk0, u32* pend_pos, i64* pend_ts, u64* pend_vals,
                                                            i64 pend_cap, const u64* __restrict__ new_gidx,
@@ -1123,7 +1130,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        pos[i] = e < N ? new_pos[e] : kNoPos;
+        pos[i] = e < N ? pos_at(new_pos, e) : kNoPos;
         cnt += pos[i] != kNoPos;
     }
     i64 pcb = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blk];
@@ -1143,7 +1150,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_pending(const i64* __restric
     }
 }
 
-void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, const u32* new_pos, AggPlan ap, i64 e_lo,
+void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, PosSrc new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base) {
     if (e_lo >= N) return;
@@ -1169,8 +1176,8 @@ struct EvLoad {
 };
 
 // combined index space: pending events [0, n_pend), then the push's events
-__device__ __forceinline__ EvLoad load_pos(i64 e, i64 n_pend, const u32* pend_pos, const u32* new_pos) {
-    u32 p = e < n_pend ? pend_pos[e] : new_pos[e - n_pend];
+__device__ __forceinline__ EvLoad load_pos(i64 e, i64 n_pend, const u32* pend_pos, const PosSrc& new_pos) {
+    u32 p = e < n_pend ? pend_pos[e] : pos_at(new_pos, e - n_pend);
     return EvLoad{p != kNoPos, p};
 }
 
@@ -1182,9 +1189,8 @@ __device__ __forceinline__ int xcd_tile(int nblk) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_ms_count(TileMap m, int n_count, i64 n_pend, const u32* __restrict__ pend_pos,
-                                                    const u32* __restrict__ new_pos, int P, u32* counts) {
+                                                    PosSrc new_pos, int P, u32* counts) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
-    if (blockIdx.x == 0 && threadIdx.x == 0) counts[(i64)P * m.nblk] = 0;  // the scan's total slot
     const int tile = xcd_tile(n_count);
     if (tile >= n_count) return;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
@@ -1198,10 +1204,10 @@ __global__ __launch_bounds__(kBlock) void k_ms_count(TileMap m, int n_count, i64
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)i * m.nblk + tile] = hist[i];
+    for (int i = threadIdx.x; i < P; i += kBlock) counts[(i64)tile * P + i] = hist[i];
 }
 
-void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, const u32* new_pos, int P,
+void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, PosSrc new_pos, int P,
                      u32* counts) {
     int grid = std::max(1, ((n_count + 7) >> 3) * 8);
     hipLaunchKernelGGL(k_ms_count, dim3(grid), dim3(kBlock), P * 4, s, m, n_count, n_pend, pend_pos, new_pos, P, counts);
@@ -1218,7 +1224,7 @@ void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u3
 template <int V, bool PACK>
 __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, const u32* __restrict__ pend_pos,
                                                       const u64* __restrict__ pend_vals, i64 pend_cap,
-                                                      const u32* __restrict__ new_pos, ColSet cols, AggPlan ap, int P,
+                                                      PosSrc new_pos, ColSet cols, AggPlan ap, int P,
                                                       int logP, const u32* __restrict__ offsets, u32* rec_pos,
                                                       u32* rec_idx, u64* rec_vals, i64 rec_cap) {
     const int nblk = m.nblk;
@@ -1253,7 +1259,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
                 for (int j = 0; j < V; j++)
                     if (j < ap.n_vcols) my_val[r][j] = pend_vals[(size_t)j * pend_cap + e];
             } else {
-                pos = new_pos[e - n_pend];
+                pos = pos_at(new_pos, e - n_pend);
 #pragma unroll
                 for (int j = 0; j < V; j++)
                     if (j < ap.n_vcols) my_val[r][j] = (u64)load_raw(cols, ap.vcol_src[j], e - n_pend);
@@ -1266,7 +1272,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
 #pragma unroll
     for (int k = 0; k < kOffRegs; k++) {
         const int i = threadIdx.x + k * kBlock;
-        off_reg[k] = i < P ? (i64)offsets[(i64)i * nblk + tile] : 0;
+        off_reg[k] = i < P ? (i64)offsets[(i64)tile * P + i] : 0;
     }
     for (int i = threadIdx.x; i < NW * P; i += kBlock) run[i] = 0;
     __syncthreads();
@@ -1313,7 +1319,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
         const int i = threadIdx.x + k * kBlock;
         if (i < P) gbase[i] = off_reg[k] - (i64)start[i];
     }
-    for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = (i64)offsets[(i64)i * nblk + tile] - (i64)start[i];
+    for (int i = threadIdx.x + kOffRegs * kBlock; i < P; i += kBlock) gbase[i] = (i64)offsets[(i64)tile * P + i] - (i64)start[i];
 #pragma unroll
     for (int r = 0; r < kItems; r++) {
         if (my_pos[r] == kNoPos) continue;
@@ -1374,7 +1380,7 @@ __global__ __launch_bounds__(kBlock) void k_ms_scatter(TileMap m, i64 n_pend, co
 }
 
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
-                       i64 pend_cap, const u32* new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
+                       i64 pend_cap, PosSrc new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap, bool pack) {
     const int nblk = m.nblk;
     const int V = ap.n_vcols <= 1 ? 1 : ap.n_vcols <= 2 ? 2 : ap.n_vcols <= 4 ? 4 : 8;
@@ -1475,17 +1481,79 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
     hipLaunchKernelGGL(k_part_off, dim3((P + 1 + 255) / 256), dim3(256), 0, s, counts, nblk, P, part_off);
 }
 
+// Record offsets of the [tile][partition] count matrix, in place: offset(t, p) = (records of the
+// partitions before p) + (records of p in the tiles before t) — the stable multisplit's layout
+// (partition-major, tile order inside a partition). Row nblk gets each partition's end. Three passes
+// over coalesced rows: per block of kColT tiles the per-partition sums, per partition the exclusive
+// scan over the blocks (+ its total), the scan of the totals over the partitions, then the rows.
+constexpr int kColT = 64;
+__global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c, int nblk, int P, i64* bsum) {
+    const int b = blockIdx.y;
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    const int t0 = b * kColT, t1 = min(nblk, t0 + kColT);
+    i64 acc = 0;
+    for (int t = t0; t < t1; t++) acc += c[(i64)t * P + p];
+    bsum[(i64)b * P + p] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P, i64* total) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    i64 run = 0;
+    for (int b = 0; b < nb; b++) {
+        const i64 x = bsum[(i64)b * P + p];
+        bsum[(i64)b * P + p] = run;
+        run += x;
+    }
+    total[p] = run;
+}
+
+__global__ __launch_bounds__(kBlock) void k_col_apply(u32* c, int nblk, int P, const i64* __restrict__ bpre,
+                                                     const i64* __restrict__ base, const i64* __restrict__ total) {
+    const int b = blockIdx.y;
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    const int t0 = b * kColT, t1 = min(nblk, t0 + kColT);
+    i64 run = base[p] + bpre[(i64)b * P + p];
+    for (int t = t0; t < t1; t++) {
+        const u32 x = c[(i64)t * P + p];
+        c[(i64)t * P + p] = (u32)run;
+        run += x;
+    }
+    if (t1 == nblk) c[(i64)nblk * P + p] = (u32)(base[p] + total[p]);
+}
+
+size_t ms_offsets_tmp_bytes(int nblk, int P) {
+    const size_t nb = (size_t)(nblk + kColT - 1) / kColT;
+    return (nb * P + 2 * (size_t)P + 16) * 8;
+}
+
+void launch_ms_offsets(hipStream_t s, u32* counts, int nblk, int P, i64* tmp) {
+    const int nb = (nblk + kColT - 1) / kColT;
+    i64* bsum = tmp;
+    i64* total = tmp + (size_t)nb * P;
+    i64* base = total + P;
+    const dim3 g((P + kBlock - 1) / kBlock, nb);
+    if (nblk > 0) hipLaunchKernelGGL(k_col_reduce, g, dim3(kBlock), 0, s, counts, nblk, P, bsum);
+    hipLaunchKernelGGL(k_col_blocks, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, s, bsum, nb, P, total);
+    (void)hipMemcpyAsync(base, total, (size_t)P * 8, hipMemcpyDeviceToDevice, s);
+    launch_scan_sum(s, base, P);
+    if (nblk > 0) hipLaunchKernelGGL(k_col_apply, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, base, total);
+    else hipLaunchKernelGGL(k_col_apply, dim3((P + kBlock - 1) / kBlock, 1), dim3(kBlock), 0, s, counts, nblk, P, bsum,
+                            base, total);
+}
+
 // Record offset of every segment boundary in every partition's list: boundary b lies in tile
 // t = b / kTile; offset = (scanned count of p before tile t) + (p-records of tile t before b).
 __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restrict__ segs, int nseg, i64 n_pend,
                                                        const u32* __restrict__ pend_pos,
-                                                       const u32* __restrict__ new_pos, int P,
+                                                       PosSrc new_pos, int P,
                                                        const u32* __restrict__ counts, TileMap m, i64* seg_off) {
     extern __shared__ __attribute__((aligned(16))) u32 hist[];
     const int k = blockIdx.x;
     const i64 b = k < nseg ? segs[k].lo : segs[nseg - 1].hi;
     const int t = tile_of(m, b);
-    const int nblk = m.nblk;
     for (int i = threadIdx.x; i < P; i += kBlock) hist[i] = 0;
     __syncthreads();
     for (i64 e = tile_lo(m, t) + threadIdx.x; e < b; e += kBlock) {
@@ -1493,11 +1561,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_offsets(const Segment* __restric
         if (ev.ok) atomicAdd(&hist[ev.pos & (P - 1)], 1u);
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < P; p += kBlock) seg_off[(i64)k * P + p] = (i64)counts[(i64)p * nblk + t] + hist[p];
+    for (int p = threadIdx.x; p < P; p += kBlock) seg_off[(i64)k * P + p] = (i64)counts[(i64)t * P + p] + hist[p];
 }
 
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
-                        const u32* new_pos, int P, const u32* counts, TileMap m, i64* seg_off) {
+                        PosSrc new_pos, int P, const u32* counts, TileMap m, i64* seg_off) {
     hipLaunchKernelGGL(k_seg_offsets, dim3(nseg + 1), dim3(kBlock), P * 4, s, segs, nseg, n_pend, pend_pos, new_pos, P,
                        counts, m, seg_off);
 }
@@ -1944,4 +2012,96 @@ void launch_scx_pending_rows(hipStream_t s, i64 M, const u32* fe, const u32* fpr
     hipLaunchKernelGGL(k_scx_pending_rows, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, fe, fpre, lastidx, pend_pos,
                        pend_gidx, kt, kp, ap, now, T, out_ts, out_keys, out_vals, out_nulls, out_exp, out_rep);
 }
+}  // namespace shd
+
+namespace shd {
+
+// ================================================================================================
+// Small pushes (send(Event[n]) with n <= kSmallMax): the common case closes no window — the events
+// only join the open window's queue (LengthBatch currentEventQueue / TimeBatch queue). One workgroup
+// does what k_boundaries + k_compact_pending do for it: the filter, the key slots, the window test
+// (timeBatch: the push's last send clock still below nextEmitTime, timestamps non-decreasing;
+// lengthBatch: the queue stays below L) and the append, then reports to pinned host memory, so the
+// host learns the outcome without a stream synchronisation. Any push that closes a window (or has
+// decreasing timestamps) appends nothing and reports `fallback`: the full pipeline runs it.
+// ================================================================================================
+template <int FK>
+__global__ __launch_bounds__(kSmallT) void k_small_push(const i64* __restrict__ ts, ColSet cols, FilterProg f,
+                                                       WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
+                                                       u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap,
+                                                       u64* pend_gidx, i64 seq_base, SmallRes* res, u64 token) {
+    const int t = threadIdx.x;
+    const i64 base = (i64)t * kItems;
+    bool pass[kItems];
+    filter_items<FK>(f, cols, base, wp.N, pass);
+    u32 pos[kItems];
+    {
+        u64 key[kItems];
+#pragma unroll
+        for (int i = 0; i < kItems; i++) key[i] = pass[i] ? make_key(kp, cols, base + i) : 0;
+        key_slots<kItems>(kt, key, pass, pos);
+    }
+    i64 tv[kItems];
+    load_items_i64(ts, base, wp.N, tv, INT64_MAX);
+    bool down = false;
+    i64 cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kItems; i++) {
+        cnt += pass[i];
+        if (i + 1 < kItems) down |= base + i + 1 < wp.N && tv[i + 1] < tv[i];
+    }
+    if (base + kItems < wp.N) down |= ts[base + kItems] < tv[kItems - 1];
+    i64 tot;
+    i64 pre = block_excl_scan_any(cnt, &tot);
+    const bool any_down = __syncthreads_or(down);
+    bool fallback = any_down;
+    if (wp.kind == SH_WIN_LENGTH_BATCH) {
+        fallback |= wp.n_pend + tot >= wp.L;
+    } else {
+        // sorted: the last send's clock is the push's largest; its window must still be the open one
+        const i64 clk = max(wp.clock_valid ? wp.clock0 : INT64_MIN, ts[wp.N - 1]);
+        fallback |= wfun(wp, wp.E0, wp.e0_valid, 0, clk) > wp.W_open;
+    }
+    if (!fallback) {
+#pragma unroll
+        for (int i = 0; i < kItems; i++) {
+            if (!pass[i]) continue;
+            const i64 e = base + i, d = wp.n_pend + pre;
+            pend_pos[d] = pos[i];
+            pend_ts[d] = tv[i];
+            for (int j = 0; j < ap.n_vcols; j++) pend_vals[(size_t)j * pend_cap + d] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            pend_gidx[d] = (u64)(seq_base + e);
+            pre++;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        __threadfence();
+        SmallRes r;
+        r.total_pass = tot;
+        r.max_tl = ts[wp.N - 1];
+        r.fallback = fallback ? 1 : 0;
+        r.pad = 0;
+        const volatile u32* c = (const volatile u32*)kt.n_keys;  // the key table's control words
+        for (int i = 0; i < 4; i++) r.ctrl[i] = c[i];
+        res->total_pass = r.total_pass;
+        res->max_tl = r.max_tl;
+        res->fallback = r.fallback;
+        for (int i = 0; i < 4; i++) res->ctrl[i] = r.ctrl[i];
+        __threadfence_system();
+        ((volatile u64*)&res->token)[0] = token;
+        __threadfence_system();
+    }
+}
+
+void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt,
+                       AggPlan ap, u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap, u64* pend_gidx,
+                       i64 seq_base, SmallRes* res, u64 token) {
+    switch (filter_kind(f)) {
+        case 0: hipLaunchKernelGGL(k_small_push<0>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token); break;
+        case 1: hipLaunchKernelGGL(k_small_push<1>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token); break;
+        default: hipLaunchKernelGGL(k_small_push<2>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token);
+    }
+}
+
 }  // namespace shd

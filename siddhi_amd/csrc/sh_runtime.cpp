@@ -310,13 +310,15 @@ int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* t
     for (int g = 0; g < n_group; g++) {
         int c = group[g];
         if (c < 0 || c >= n_cols) return sh_fail(SH_ERR_INVALID, "group-by column out of range");
-        if (!integral(types[c]))
-            return sh_fail(SH_ERR_UNSUPPORTED, "GPU group-by supports int/long/string(dictionary id)/bool keys");
+        if (!integral(types[c]) && types[c] != SH_T_FLOAT && types[c] != SH_T_DOUBLE)
+            return sh_fail(SH_ERR_INVALID, "unknown group-by column type");
         kp.col[g] = c;
         kp.type[g] = types[c];
     }
-    if (n_group == 2 && (kp.type[0] == SH_T_LONG || kp.type[1] == SH_T_LONG))
-        return sh_fail(SH_ERR_UNSUPPORTED, "two group-by columns must both be 32-bit");
+    // one column of any type, or two 32-bit ones (int / string id / bool / float): the key is one u64
+    if (n_group == 2 && (kp.type[0] == SH_T_LONG || kp.type[1] == SH_T_LONG || kp.type[0] == SH_T_DOUBLE ||
+                         kp.type[1] == SH_T_DOUBLE))
+        return sh_fail(SH_ERR_UNSUPPORTED, "two group-by columns must both be 32-bit (int, string, bool, float)");
     // string keys arrive as dictionary ids the host assigns densely from 0: the id is the slot
     kp.dense = n_group == 1 && kp.type[0] == SH_T_STRID;
     return SH_OK;

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -47,6 +48,16 @@ void sh_timing_mark(int point);
 // every push. After ~20 ms of polling they fall back to the blocking call.
 hipError_t sh_wait_stream(hipStream_t s);
 hipError_t sh_wait_event(hipEvent_t e);
+
+// A roctx range around every data-path C-ABI call (rocprofv3 --marker-trace shows the calls next to
+// their kernels; without a profiler attached a push/pop is a table lookup in librocprofiler-sdk-roctx).
+struct ShRange {
+    explicit ShRange(const char* n) { roctxRangePush(n); }
+    ~ShRange() { roctxRangePop(); }
+    ShRange(const ShRange&) = delete;
+    ShRange& operator=(const ShRange&) = delete;
+};
+#define SH_RANGE(name) ShRange _sh_range(name)
 
 // The stream of the context whose API call is running on this thread. A device buffer's growth or
 // release drains that stream before the old block is freed, so no queued kernel or copy still reads
@@ -186,6 +197,7 @@ int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* t
 // Host batch staged to the device (sh_push): one DevBuf per column + timestamps.
 struct StagedBatch {
     DevBuf ts, cols[SH_MAX_COLS];
+    DevBuf blk;  // one block when the host batch is one contiguous region (PinnedBatch layout)
     int stage(hipStream_t s, const sh_batch* b, int n_cols, const int32_t* types, sh_batch* dev);
 };
 
@@ -239,7 +251,12 @@ struct sh_query {
     PinnedBuf h_bounds;  // pinned landing area of the push's window boundaries
     // the multisplit of the push's events, launched before the host reads the window boundaries
     bool ms_ready = false;
-    bool rec_packed = false;  // the split wrote packed records (rec_idx only)
+    bool rec_packed = false;
+    bool direct_pos = false;
+    // small-push fast path (try_small_push): the kernel's report in coherent pinned host memory
+    shd::SmallRes* small_res = nullptr;
+    shd::SmallRes* small_res_dev = nullptr;
+    uint64_t small_token = 0;  // this push's key slots are read from the key column (pos_src)  // the split wrote packed records (rec_idx only)
     TileMap ms_map{};  // tiling of the last multisplit
     int64_t rec_cap = 0;
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation

@@ -156,7 +156,14 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     // round-robin owners for one dictionary-id component (dense ids stay dense per owner)
     s->wkp.dense = (s->wkp.n == 1 && s->wkp.type[0] == SH_T_STRID) ? 1 : 0;
-    s->key32 = (s->wkp.n == 0 || (s->wkp.n == 1 && s->wkp.type[0] != SH_T_LONG)) ? 1 : 0;
+    // floating-point keys travel as the 64-bit pattern of the value widened to double
+    const bool wide1 = s->wkp.n == 1 && (s->wkp.type[0] == SH_T_LONG || s->wkp.type[0] == SH_T_DOUBLE ||
+                                         s->wkp.type[0] == SH_T_FLOAT);
+    s->key32 = (s->wkp.n == 0 || (s->wkp.n == 1 && !wide1)) ? 1 : 0;
+    if (s->wkp.n == 2 && (s->wkp.type[0] == SH_T_FLOAT || s->wkp.type[1] == SH_T_FLOAT)) {
+        delete s;
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries: a float group-by column must be the only one");
+    }
     s->rec_words = (s->key32 ? 4 : 6) + 2 * s->rp.n;
     // the owner runs the same query over the records it receives: no filter (applied at ingest),
     // 8-byte raw columns, windows given per event
@@ -243,6 +250,7 @@ static ColSet colset(const sh_shard* s, const sh_batch* b) {
 
 // Phase 1: pass count, send clocks and the first passing send of the slice (k_blockagg + k_scan_blocks).
 extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summary* out) {
+    SH_RANGE("sh_shard_summarize");
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_summarize: NULL argument");
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative slice size");
@@ -377,6 +385,7 @@ static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch
 // Phase 2: global clock / nextEmitTime / windows from the G summaries, then the per-owner records.
 extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_batch* b, void* send_buf,
                              int64_t send_cap, int64_t* send_bytes, const sh_bound** bounds, int64_t* n_bounds) {
+    SH_RANGE("sh_shard_pack");
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !all || !b || !send_bytes || !bounds || !n_bounds)
         return sh_fail(SH_ERR_INVALID, "sh_shard_pack: NULL argument");
@@ -578,6 +587,7 @@ static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* rec
 // concatenated in rank order and every source run is in stream order).
 extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_bytes, const sh_bound* all_bounds,
                                 int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order) {
+    SH_RANGE("sh_shard_consume");
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !recv_bytes || !out || (n_all_bounds > 0 && !all_bounds))
         return sh_fail(SH_ERR_INVALID, "sh_shard_consume: NULL argument");
@@ -676,6 +686,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
 
 extern "C" int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out,
                                      const int64_t** order) {
+    SH_RANGE("sh_shard_advance_time");
     StreamScope _ss(s && s->ctx ? s->ctx->stream : nullptr);
     if (!s || !out) return sh_fail(SH_ERR_INVALID, "sh_shard_advance_time: NULL argument");
     if (s->packed) return sh_fail(SH_ERR_STATE, "sh_shard_advance_time: a packed push is still in flight");

@@ -215,9 +215,14 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N == 0) return empty_out(q, out);
     if (N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
+    // hysteresis: after a rebuild that kept many live keys, the next one waits until size/8 more keys
+    // arrived (capped at 7/8 full), instead of copying every slot's state on every push
+    const int64_t tsz = (int64_t)q->kt.size_;
     if (!q->kt.dense && q->kp.n > 0 && (q->d.window == SH_WIN_TIME || s->xm) && q->clock_valid &&
-        q->kt.n_keys > (int64_t)q->kt.size_ / 2)
+        q->kt.n_keys > std::max<int64_t>(tsz / 2, s->rekey_floor)) {
         RCHK(sliding_rekey(q));
+        s->rekey_floor = std::min<int64_t>(q->kt.n_keys + tsz / 8, tsz * 7 / 8);
+    }
     if (s->xm) return slx_run(q, b, 0, host_out, out);
     HIPCHK(hipEventRecord(q->ev_push0, st));
     ColSet cs{};
@@ -851,5 +856,26 @@ int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& 
             {&s->dq_head, F * n * 8},  {&s->dq_len, F * n * 8},    {&s->dq, F * n * rc * 8}, {&s->rhead, n * 8},
             {&s->rlen, n * 8},         {&s->rpm, n * rc * 8},      {&s->rval, V * n * rc * 8},
             {&s->cur_send, n * 8},     {&s->cur_first, n * 8}};
+    return SH_OK;
+}
+
+// Checkpoint of the expiry FIFO of `insert expired / all events` and pass-through sliding windows
+// (sh_slx_kernels.hip): arrival indices X0 / G0, the unexpired FIFO (PM, stream index), the pending
+// notify times and each ring entry's arrival index. sc = {x0, g0, w0, n_np, np_front}. The partition
+// lanes (sh_plane.cpp) keep host-side scheduler state and are not checkpointed (lane != 0).
+int sliding_fifo_state(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* sc, bool set, int* kind) {
+    SlidingImpl* s = q->sl;
+    *kind = s->lane ? 2 : s->xm ? 1 : 0;
+    bufs.clear();
+    if (*kind != 1) return SH_OK;
+    if (set) {
+        if (sc[2] < 0 || sc[3] < 0) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+        s->x0 = sc[0]; s->g0 = sc[1]; s->w0 = sc[2]; s->n_np = sc[3]; s->np_front = sc[4];
+    } else {
+        sc[0] = s->x0; sc[1] = s->g0; sc[2] = s->w0; sc[3] = s->n_np; sc[4] = s->np_front;
+    }
+    const size_t n = (size_t)s->nslots, rc = (size_t)s->rc;
+    bufs = {{&s->rg, n * rc * 8}, {&s->upm, (size_t)s->w0 * 8}, {&s->useq, (size_t)s->w0 * 8},
+            {&s->npend, (size_t)s->n_np * 8}};
     return SH_OK;
 }

@@ -18,6 +18,7 @@ struct SlidingImpl {
     int P = 1, logP = 0;
     int64_t pm = INT64_MIN;   // PM carried across pushes
     int64_t send_base = 0;    // global send number of the push's first send
+    int64_t rekey_floor = 0;  // key count above which the next key-table rebuild runs (hysteresis)
     DevBuf cnt, f, mm, mm_has, dq_head, dq_len, dq, rhead, rlen, rpm, rval, cur_send, cur_first;
     // per push scratch
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,

@@ -1536,6 +1536,185 @@ __global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, 
     if (HMAX) kdq_store<KL>(qx, S, fd.mx, k, lmax);
 }
 
+// ---- one wave per key (round 3): the 64 lanes of a wave share one key's run, 64 records at a time.
+// Everything per record that does not depend on the running aggregates is computed lane-parallel:
+// the expiry prefix (the heads with PM + T <= the record's clock form a prefix, PM and the clock both
+// being non-decreasing along a key's events — one binary search per lane over the staged heads), the
+// count, the row position and the row stores. Only the Java-order double sum and the min / max deques
+// (MinAttributeAggregatorExecutor's LinkedList, removeFirstOccurrence included) run sequentially, in
+// lane 0, over values staged in LDS. With a wave per key a SIMD holds several keys' waves, whose
+// sequential parts interleave (the lane-per-key kernel left most SIMDs without a wave: ~0.6 per SIMD at
+// C3's 10k keys). TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
+constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)
+
+template <bool HSUM, bool HMIN, bool HMAX>
+__global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, const i64* __restrict__ g_clk,
+                                               const i64* __restrict__ g_pm, const u64* __restrict__ g_v,
+                                               const i64* __restrict__ g_ts, const u32* __restrict__ g_raw,
+                                               const u32* __restrict__ g_rank, SlState S, DFields fd, KOut ko, i64 T,
+                                               u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW) {
+    __shared__ u64 dq_min[HMIN ? kDqK : 1];
+    __shared__ u64 dq_max[HMAX ? kDqK : 1];
+    __shared__ i64 s_pm[kWS];
+    __shared__ u64 s_hv[kWS];
+    __shared__ u64 s_x[64];
+    __shared__ int s_e[64];
+    __shared__ u64 s_sum[64], s_mn[64], s_mx[64];
+    __shared__ i64 s_cnt[64];
+    __shared__ unsigned char s_fl[64];
+    __shared__ int s_hj;
+    const u32 k = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (k >= nslots) return;
+    const u32 a = key_off[k], b = key_off[k + 1];
+    if (a == b) return;
+    const int gm = (int)(S.rc - 1);
+    const i64* rpm = S.rpm + (size_t)k * S.rc;
+    const u64* rval = S.rval + (size_t)k * S.rc;
+    const int rh0 = (int)(S.rhead[k] & gm), H0 = (int)S.rlen[k];
+    const int n = (int)(b - a), HN = H0 + n;
+    auto head_pm = [&](int h) -> i64 { return h < H0 ? rpm[(rh0 + h) & gm] : g_pm[a + (h - H0)]; };
+    auto head_v = [&](int h) -> u64 { return h < H0 ? rval[(rh0 + h) & gm] : g_v[a + (h - H0)]; };
+    // lane 0's running state
+    i64 cnt = 0;
+    double sum = 0.0;
+    KDq qn{}, qx{};
+    u64* gmin = HMIN ? S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc : nullptr;
+    u64* gmax = HMAX ? S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc : nullptr;
+    if (lane == 0) {
+        cnt = S.cnt[k];
+        if (HSUM) sum = __longlong_as_double((i64)S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k]);
+        if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
+        if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
+    }
+    int hj = 0;         // heads expired so far
+    int open_row = 0;   // key-order index of the (send, key) row open at the chunk start
+    i64 last_send = 0;
+    for (int o0 = 0; o0 < n; o0 += 64) {
+        const int m = min(64, n - o0);
+        const bool in = lane < m;
+        const u32 i = a + (u32)(o0 + min(lane, m - 1));
+        const i64 clk = g_clk[i];
+        const u64 x = g_v[i];
+        const i64 ts = g_ts[i];
+        const u32 raw = g_raw[i];
+        const u32 rk = g_rank[i];
+        const int hb = hj;
+        for (int q = lane; q < kWS; q += 64) {
+            const int h = hb + q;
+            if (h < HN) { s_pm[q] = head_pm(h); s_hv[q] = head_v(h); }
+        }
+        s_x[lane] = x;
+        __syncthreads();
+        // heads expired before this record: the first h in [hb, added) whose PM + T exceeds its clock
+        int lo = hb, hi = in ? H0 + o0 + lane : hb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const i64 pm = mid - hb < kWS ? s_pm[mid - hb] : head_pm(mid);
+            if (pm + T <= clk) lo = mid + 1;
+            else hi = mid;
+        }
+        if (in) s_e[lane] = lo;
+        __syncthreads();
+        if (lane == 0) {
+            int h = hb;
+            for (int q = 0; q < m; q++) {
+                const int e = max(s_e[q], h);
+                for (; h < e; h++) {  // expired heads leave, oldest first (processRemove)
+                    const u64 v = h - hb < kWS ? s_hv[h - hb] : head_v(h);
+                    cnt--;
+                    if (HSUM) {
+                        sum = sum - __longlong_as_double((i64)v);
+                        if (cnt == 0 && sum == 0.0) sum = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
+                    }
+                    if (HMIN) kdq_remove<true, 1>(qn, gmin, gm, dq_min, v);
+                    if (HMAX) kdq_remove<false, 1>(qx, gmax, gm, dq_max, v);
+                }
+                const u64 xq = s_x[q];  // the event joins the window (processAdd)
+                cnt++;
+                if (HSUM) sum = sum + __longlong_as_double((i64)xq);
+                if (HMIN) kdq_add<true, 1>(qn, gmin, gm, dq_min, xq);
+                if (HMAX) kdq_add<false, 1>(qx, gmax, gm, dq_max, xq);
+                s_cnt[q] = cnt;
+                s_sum[q] = (u64)__double_as_longlong(sum);
+                s_mn[q] = qn.mm;
+                s_mx[q] = qx.mm;
+                s_fl[q] = (unsigned char)((qn.mmh ? 1 : 0) | (qx.mmh ? 2 : 0));
+            }
+            s_hj = h;
+        }
+        __syncthreads();
+        hj = s_hj;
+        // the row of (send, key): opened by the group's first record (its key-order position), written
+        // with the values after the group's last record of this chunk (a later chunk overwrites it)
+        const bool first = in && (rk & kFirstBit);
+        int grp = first ? o0 + lane : -1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int up = __shfl_up(grp, d, 64);
+            if (lane >= d) grp = max(grp, up);
+        }
+        grp = max(grp, open_row);
+        const bool next_first = lane + 1 < m ? ((__shfl_down(rk, 1, 64) & kFirstBit) != 0) : true;
+        const i64 send = send_base + (send_size == 1 ? (i64)raw : send_size ? (i64)(raw / send_size) : 0);
+        if (in && next_first) {
+            u64 w[4 + SH_MAX_AGGS];
+            u32 nulls = 0;
+            const i64 c = s_cnt[lane];
+            const u64 sb = s_sum[lane];
+            const unsigned char fl = s_fl[lane];
+            w[0] = (u64)ts;
+            w[1] = (u64)raw | ((u64)k << 32);
+            w[2] = (u64)clk;
+#pragma unroll
+            for (int o = 0; o < SH_MAX_AGGS; o++) {
+                if (o >= ko.n) break;
+                const int src = ko.src[o];
+                u64 v = 0;
+                if (src == 0) v = (u64)c;
+                else if (src == 1) v = sb;
+                else if (src == 2) v = (u64)__double_as_longlong(__longlong_as_double((i64)sb) / (double)c);
+                else if (src == 3) { v = s_mn[lane]; nulls |= ((fl & 1) ? 0u : 1u) << o; }
+                else { v = s_mx[lane]; nulls |= ((fl & 2) ? 0u : 1u) << o; }
+                w[4 + o] = v;
+            }
+            w[3] = (u64)send | ((u64)nulls << 56);
+            ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)(a + (u32)grp) * RW);
+#pragma unroll
+            for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
+                if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
+        }
+        open_row = __shfl(grp, m - 1, 64);
+        last_send = __shfl(send, m - 1, 64);
+        __syncthreads();  // the staging arrays are refilled by the next chunk
+    }
+    // the window after the push: heads [hj, HN) — ring entries keep their place, the run's follow
+    const int keep = hj < H0 ? H0 - hj : 0;
+    const int rh = (rh0 + (hj < H0 ? hj : H0)) & gm;
+    const int j0 = hj > H0 ? hj : H0;
+    i64* wpm = S.rpm + (size_t)k * S.rc;
+    u64* wval = S.rval + (size_t)k * S.rc;
+    for (int j = j0 + lane; j < HN; j += 64) {
+        const int sl = (rh + keep + (j - j0)) & gm;
+        wpm[sl] = g_pm[a + (j - H0)];
+        wval[sl] = g_v[a + (j - H0)];
+    }
+    if (lane == 0) {
+        S.cnt[k] = cnt;
+        S.rhead[k] = rh;
+        S.rlen[k] = keep + (HN - j0);
+        S.cur_send[k] = last_send;
+        S.cur_first[k] = 0;
+        if (HSUM) {
+            const u64 sb = (u64)__double_as_longlong(sum);
+            if (fd.sum >= 0) S.f[(size_t)fd.sum * S.nslots + k] = sb;
+            if (fd.avg >= 0) S.f[(size_t)fd.avg * S.nslots + k] = sb;
+        }
+        if (HMIN) kdq_store<1>(qn, S, fd.mn, k, dq_min);
+        if (HMAX) kdq_store<1>(qx, S, fd.mx, k, dq_max);
+    }
+}
+
 // emit of the keyed replay: flagged ranks in stream order, each row read from its key-order record
 __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __restrict__ flags, i64 n,
                                                     const i64* __restrict__ blk_pre, const u32* __restrict__ inv,
@@ -1614,6 +1793,23 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank,
                        sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
+    static const bool lane_per_key = getenv("SH_SL_LANE_PER_KEY") != nullptr;  // the round-2 kernel
+    if (!lane_per_key) {
+        const int RWw = sliding_keyed_row_words(ap.n);
+#define SH_SL_W(A, B, C)                                                                                           \
+    hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, \
+                       g_ts, g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RWw)
+        if (hs && hn && hx) SH_SL_W(true, true, true);
+        else if (hs && !hn && !hx) SH_SL_W(true, false, false);
+        else if (!hs && hn && hx) SH_SL_W(false, true, true);
+        else if (hs && hn) SH_SL_W(true, true, false);
+        else if (hs && hx) SH_SL_W(true, false, true);
+        else if (hn && !hx) SH_SL_W(false, true, false);
+        else if (hx && !hn) SH_SL_W(false, false, true);
+        else SH_SL_W(false, false, false);
+#undef SH_SL_W
+        return;
+    }
     static const int kl_env = getenv("SH_SL_KL") ? atoi(getenv("SH_SL_KL")) : 16;
     const int KLr = kl_env == 8 || kl_env == 32 || kl_env == 64 ? kl_env : 16;
     const unsigned grid = (unsigned)((n + KLr - 1) / KLr);

@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 3;
+constexpr uint32_t kVersion = 4;  // 4: expired-output, pass-through sliding and rate-limiter state
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -145,6 +145,17 @@ int batch_snapshot(sh_query* q, Writer& w) {
     for (int j = 0; j < q->ap.n_vcols; j++) RCHK(w.dev(q->pend_vals.as<char>() + (size_t)j * q->pend_cap * 8, n * 8, s));
     // stream numbering (sh_out.rep): the queued events' indices and the next event's
     RCHK(w.dev(q->pend_gidx.p, n * 8, s));
+    // expired / all-events output: the last flushed batch's keys and representative events, carried
+    // until the batch after it closes (sh_expired.cpp)
+    w.val<uint8_t>(q->xmode);
+    if (q->xmode) {
+        const int64_t xn = q->xc_valid ? q->xc_n : 0;
+        w.val<uint8_t>(q->xc_valid);
+        w.val<int64_t>(xn);
+        w.val<int64_t>(q->xc_W);
+        RCHK(w.dev(q->xc_keys.p, (size_t)q->kp.n * xn * 8, s));
+        RCHK(w.dev(q->xc_rep.p, (size_t)xn * 8, s));
+    }
     w.val<int64_t>(q->seq);
     return SH_OK;
 }
@@ -200,6 +211,15 @@ int batch_restore(sh_query* q, Reader& r) {
     if (n && (hipMemcpyAsync(q->pend_gidx.p, tmp.p, n * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
               hipStreamSynchronize(s) != hipSuccess))
         return sh_fail(SH_ERR_DEVICE, "restore");
+    if ((bool)r.val<uint8_t>() != q->xmode || !r.ok) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    if (q->xmode) {
+        q->xc_valid = r.val<uint8_t>();
+        q->xc_n = r.val<int64_t>();
+        q->xc_W = r.val<int64_t>();
+        if (!r.ok || q->xc_n < 0) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        RCHK(r.dev(q->xc_keys, 8, s));
+        RCHK(r.dev(q->xc_rep, 8, s));
+    }
     q->seq = r.val<int64_t>();
     tmp.release();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
@@ -208,18 +228,79 @@ int batch_restore(sh_query* q, Reader& r) {
     return SH_OK;
 }
 
-extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len) {
-    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
-    if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
+// Output rate limiter (sh_rate.cpp; the reference limiters' State: counters, the carried rows of an
+// open group, the FirstGroupBy key -> count table, `first every <t>`'s output time / key table)
+static int rate_snapshot(sh_query* q, Writer& w) {
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    const int nk = q->kp.n, na = q->ap.n;
+    w.val<int32_t>(r.kind);
+    w.val<int64_t>(r.N);
+    if (r.kind == SH_RATE_NONE) return SH_OK;
+    w.val<int64_t>(r.seq);
+    w.val<int64_t>(r.nc);
+    const size_t n = (size_t)r.nc;
+    RCHK(w.dev(r.c_ts.p, n * 8, s));
+    RCHK(w.dev(r.c_exp.p, n, s));
+    RCHK(w.dev(r.c_rep.p, n * 8, s));
+    RCHK(w.dev(r.c_keys.p, (size_t)nk * n * 8, s));
+    RCHK(w.dev(r.c_vals.p, (size_t)na * n * 8, s));
+    RCHK(w.dev(r.c_nulls.p, (size_t)na * n, s));
+    w.val<int64_t>(r.t_cap);
+    w.val<int64_t>(r.t_keys);
+    RCHK(w.dev(r.tk.p, (size_t)r.t_cap * 8, s));
+    RCHK(w.dev(r.tc.p, (size_t)r.t_cap * 8, s));
+    w.val<uint8_t>(r.ft_has);
+    w.val<int64_t>(r.ft_last);
+    w.val<int64_t>(r.ft_cap);
+    w.val<int64_t>(r.ft_keys);
+    RCHK(w.dev(r.ftk.p, (size_t)r.ft_cap * 8, s));
+    RCHK(w.dev(r.ftt.p, (size_t)r.ft_cap * 8, s));
+    return SH_OK;
+}
+
+static int rate_restore(sh_query* q, Reader& rd) {
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    const int32_t kind = rd.val<int32_t>();
+    const int64_t N = rd.val<int64_t>();
+    if (!rd.ok || kind != r.kind || N != r.N)
+        return sh_fail(SH_ERR_INVALID, "snapshot's output rate limiting differs from this query's (set it before restoring)");
+    if (kind == SH_RATE_NONE) return SH_OK;
+    r.seq = rd.val<int64_t>();
+    r.nc = rd.val<int64_t>();
+    if (!rd.ok || r.nc < 0) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    for (DevBuf* b : {&r.c_ts, &r.c_exp, &r.c_rep, &r.c_keys, &r.c_vals, &r.c_nulls}) RCHK(rd.dev(*b, 8, s));
+    r.t_cap = rd.val<int64_t>();
+    r.t_keys = rd.val<int64_t>();
+    RCHK(rd.dev(r.tk, 8, s));
+    RCHK(rd.dev(r.tc, 8, s));
+    r.ft_has = rd.val<uint8_t>();
+    r.ft_last = rd.val<int64_t>();
+    r.ft_cap = rd.val<int64_t>();
+    r.ft_keys = rd.val<int64_t>();
+    RCHK(rd.dev(r.ftk, 8, s));
+    RCHK(rd.dev(r.ftt, 8, s));
+    if (!rd.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    return SH_OK;
+}
+
+static int query_snapshot_blob(sh_query* q, Writer& w) {
     if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
-    if (q->xmode) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a query with expired / all-events output");
-    if (q->rate.kind != SH_RATE_NONE) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a rate-limited query");
-    Writer w;
     w.put("SHQ1", 4);
     w.val<uint32_t>(kVersion);
     w.val<uint64_t>(fingerprint(q));
     w.val<uint32_t>((uint32_t)q->kind);
     RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    return rate_snapshot(q, w);
+}
+
+extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len) {
+    SH_RANGE("sh_query_snapshot");
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
+    if (!q || !len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: NULL argument");
+    Writer w;
+    RCHK(query_snapshot_blob(q, w));
     *len = (int64_t)w.b.size();
     if (buf) {
         if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_query_snapshot: buffer too small (call with buf=NULL for the size)");
@@ -228,9 +309,8 @@ extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* l
     return SH_OK;
 }
 
-extern "C" int sh_query_restore(sh_query* q, const void* buf, int64_t len) {
-    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
-    if (!q || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_query_restore: bad arguments");
+static int query_restore_blob(sh_query* q, const void* buf, int64_t len) {
+    if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "restore of a sharded owner: restore the sh_shard instead");
     Reader r{(const uint8_t*)buf, (size_t)len};
     if (std::memcmp(buf, "SHQ1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip query snapshot");
     r.o = 4;
@@ -238,13 +318,39 @@ extern "C" int sh_query_restore(sh_query* q, const void* buf, int64_t len) {
     if (r.val<uint64_t>() != fingerprint(q)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different query");
     if (r.val<uint32_t>() != (uint32_t)q->kind) return sh_fail(SH_ERR_INVALID, "snapshot kind mismatch");
     (void)hipStreamSynchronize(q->ctx->stream);
-    return q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
+    RCHK(q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r));
+    return rate_restore(q, r);
+}
+
+// A restore either applies the whole blob or leaves the query as it was: the current state is
+// snapshotted first and put back when the blob fails part-way (truncated, wrong sections, device
+// error), keeping the first failure's message.
+template <class Snap, class Rest>
+static int restore_or_roll_back(Snap snap, Rest rest, const void* buf, int64_t len) {
+    Writer backup;
+    const bool have = snap(backup) == SH_OK;
+    const int rc = rest(buf, len);
+    if (rc != SH_OK && have) {
+        const std::string msg = sh_last_error();
+        (void)rest(backup.b.data(), (int64_t)backup.b.size());
+        return sh_fail(rc, msg);
+    }
+    return rc;
+}
+
+extern "C" int sh_query_restore(sh_query* q, const void* buf, int64_t len) {
+    SH_RANGE("sh_query_restore");
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
+    if (!q || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_query_restore: bad arguments");
+    return restore_or_roll_back([&](Writer& w) { return query_snapshot_blob(q, w); },
+                                [&](const void* b, int64_t n) { return query_restore_blob(q, b, n); }, buf, len);
 }
 
 // ---- sliding window (state in SlidingImpl, sh_sliding.cpp) ---------------------------------------
 struct SlidingImpl;
 int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* scalars, int n_scalars,
                           bool set, int64_t new_rc);
+int sliding_fifo_state(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* sc, bool set, int* kind);
 
 int sliding_snapshot(sh_query* q, Writer& w) {
     hipStream_t s = q->ctx->stream;
@@ -259,6 +365,16 @@ int sliding_snapshot(sh_query* q, Writer& w) {
     RCHK(sliding_state_buffers(q, bufs, sc, 4, false, 0));
     for (int i = 0; i < 4; i++) w.val<int64_t>(sc[i]);
     for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+    // the expiry FIFO of expired / all-events output and pass-through windows
+    int64_t fs[5] = {0, 0, 0, 0, 0};
+    int fk = 0;
+    RCHK(sliding_fifo_state(q, bufs, fs, false, &fk));
+    if (fk == 2) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of partitioned lengthBatch / time windows");
+    w.val<int32_t>(fk);
+    if (fk == 1) {
+        for (int i = 0; i < 5; i++) w.val<int64_t>(fs[i]);
+        for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+    }
     w.val<int64_t>(q->seq);
     return SH_OK;
 }
@@ -279,6 +395,16 @@ int sliding_restore(sh_query* q, Reader& r) {
     std::vector<std::pair<DevBuf*, size_t>> bufs;
     RCHK(sliding_state_buffers(q, bufs, sc, 4, true, sc[1]));
     for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+    int64_t fs[5] = {0, 0, 0, 0, 0};
+    int fk = 0;
+    RCHK(sliding_fifo_state(q, bufs, fs, false, &fk));
+    if (r.val<int32_t>() != fk || !r.ok) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    if (fk == 1) {
+        for (int i = 0; i < 5; i++) fs[i] = r.val<int64_t>();
+        if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        RCHK(sliding_fifo_state(q, bufs, fs, true, &fk));
+        for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+    }
     q->seq = r.val<int64_t>();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;
@@ -287,19 +413,26 @@ int sliding_restore(sh_query* q, Reader& r) {
 // ---- sharded query (sh_shard.cpp): the shard's global stream state + its owner query -------------
 int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query** owner);
 
+static int shard_snapshot_blob(sh_shard* sd, sh_query* q, Writer& w) {
+    int64_t sc[14];
+    RCHK(shard_checkpoint_state(sd, sc, 14, false, &q));
+    w.put("SHS1", 4);
+    w.val<uint32_t>(kVersion);
+    w.val<uint64_t>(fingerprint(q));
+    w.val<uint32_t>((uint32_t)q->kind);
+    for (int i = 0; i < 14; i++) w.val<int64_t>(sc[i]);
+    return q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w);
+}
+
 extern "C" int sh_shard_snapshot(sh_shard* sd, void* buf, int64_t cap, int64_t* len) {
+    SH_RANGE("sh_shard_snapshot");
     if (!sd || !len) return sh_fail(SH_ERR_INVALID, "sh_shard_snapshot: NULL argument");
     int64_t sc[14];
     sh_query* q = nullptr;
     RCHK(shard_checkpoint_state(sd, sc, 14, false, &q));
     StreamScope _ss(q->ctx->stream);
     Writer w;
-    w.put("SHS1", 4);
-    w.val<uint32_t>(kVersion);
-    w.val<uint64_t>(fingerprint(q));
-    w.val<uint32_t>((uint32_t)q->kind);
-    for (int i = 0; i < 14; i++) w.val<int64_t>(sc[i]);
-    RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    RCHK(shard_snapshot_blob(sd, q, w));
     *len = (int64_t)w.b.size();
     if (buf) {
         if (cap < *len) return sh_fail(SH_ERR_INVALID, "sh_shard_snapshot: buffer too small (call with buf=NULL for the size)");
@@ -308,14 +441,11 @@ extern "C" int sh_shard_snapshot(sh_shard* sd, void* buf, int64_t cap, int64_t* 
     return SH_OK;
 }
 
-extern "C" int sh_shard_restore(sh_shard* sd, const void* buf, int64_t len) {
-    if (!sd || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_shard_restore: bad arguments");
-    int64_t cur[14];
-    sh_query* q = nullptr;
-    RCHK(shard_checkpoint_state(sd, cur, 14, false, &q));
-    StreamScope _ss(q->ctx->stream);
+// The owner's windows are restored before the rank's global stream state is applied, and both only
+// after the blob's header checked out; a failure part-way rolls the shard back (restore_or_roll_back).
+static int shard_restore_blob(sh_shard* sd, sh_query* q, const void* buf, int64_t len) {
     Reader r{(const uint8_t*)buf, (size_t)len};
-    if (std::memcmp(buf, "SHS1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip shard snapshot");
+    if (len < 20 || std::memcmp(buf, "SHS1", 4) != 0) return sh_fail(SH_ERR_INVALID, "not a siddhi_hip shard snapshot");
     r.o = 4;
     if (r.val<uint32_t>() != kVersion) return sh_fail(SH_ERR_INVALID, "snapshot version mismatch");
     if (r.val<uint64_t>() != fingerprint(q)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different query");
@@ -323,11 +453,22 @@ extern "C" int sh_shard_restore(sh_shard* sd, const void* buf, int64_t len) {
     int64_t sc[14];
     for (int i = 0; i < 14; i++) sc[i] = r.val<int64_t>();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
-    RCHK(shard_checkpoint_state(sd, sc, 14, true, &q));
     (void)hipStreamSynchronize(q->ctx->stream);
     // the owner takes its events already filtered by the ingest: keep its own (empty) filter
     const FilterProg keep = q->fp;
     const int rc = q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
     q->fp = keep;
-    return rc;
+    RCHK(rc);
+    return shard_checkpoint_state(sd, sc, 14, true, &q);
+}
+
+extern "C" int sh_shard_restore(sh_shard* sd, const void* buf, int64_t len) {
+    SH_RANGE("sh_shard_restore");
+    if (!sd || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_shard_restore: bad arguments");
+    int64_t cur[14];
+    sh_query* q = nullptr;
+    RCHK(shard_checkpoint_state(sd, cur, 14, false, &q));
+    StreamScope _ss(q->ctx->stream);
+    return restore_or_roll_back([&](Writer& w) { return shard_snapshot_blob(sd, q, w); },
+                                [&](const void* b, int64_t n) { return shard_restore_blob(sd, q, b, n); }, buf, len);
 }

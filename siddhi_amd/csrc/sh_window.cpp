@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -41,6 +43,27 @@ int StagedBatch::stage(hipStream_t s, const sh_batch* b, int n_cols, const int32
     *dev = *b;
     size_t n = (size_t)b->n;
     if (n == 0) return SH_OK;
+    // a host batch laid out as one region — ts[n], then each column's n values, every run 16-byte
+    // aligned (the pinned layout the shim packs) — goes over in ONE copy
+    {
+        auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+        const char* base = (const char*)b->ts;
+        size_t off = a16(n * 8), offs[SH_MAX_COLS] = {};
+        bool contig = true;
+        for (int c = 0; c < n_cols && contig; c++) {
+            if (!b->cols[c]) continue;
+            contig = (const char*)b->cols[c] == base + off;
+            offs[c] = off;
+            off = a16(off + n * type_size(types[c]));
+        }
+        if (contig) {
+            RCHK(blk.reserve(off, false));
+            HIPCHK(hipMemcpyAsync(blk.p, base, off, hipMemcpyHostToDevice, s));
+            dev->ts = blk.as<int64_t>();
+            for (int c = 0; c < n_cols; c++) dev->cols[c] = b->cols[c] ? blk.as<char>() + offs[c] : nullptr;
+            return SH_OK;
+        }
+    }
     RCHK(ts.reserve(n * 8, false));
     HIPCHK(hipMemcpyAsync(ts.p, b->ts, n * 8, hipMemcpyHostToDevice, s));
     dev->ts = ts.as<int64_t>();
@@ -106,8 +129,11 @@ static int size_partitions(sh_query* q) {
     const size_t ts = q->kt.size_;
     auto scatter_fits = [&](int p) { return ::scatter_fits(q, p); };
     int P = 1;
-    while (ts / P > 512 && P < 16384 && scatter_fits(P << 1)) P <<= 1;
-    if (ts / P > 512) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
+    // local keys per partition: at most 512 (one per thread of k_aggregate_own) or, for experiments,
+    // 1024 (two per thread) — SH_PART_KEYS
+    static const size_t nl_max = getenv("SH_PART_KEYS") && atoi(getenv("SH_PART_KEYS")) == 1024 ? 1024 : 512;
+    while (ts / P > nl_max && P < 16384 && scatter_fits(P << 1)) P <<= 1;
+    if (ts / P > nl_max) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
     q->P = P;
     q->logP = 0;
     while ((1 << q->logP) < P) q->logP++;
@@ -263,6 +289,29 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
 // and append one flush per non-empty segment. Device output: everything is queued on the stream and
 // the flush bookkeeping (rows per segment) completes in closed_finish after the push's final
 // synchronisation. Host output synchronises here for the row copies.
+// Where the push's key slots come from (PosSrc): dictionary ids that are their own slots, with no
+// filter and no consumer of the slot column but the multisplit path, are read from the key column.
+static bool want_direct_pos(const sh_query* q) {
+    static const bool off = getenv("SH_NO_DIRECT_POS") != nullptr;  // A/B switch for profiling
+    if (off) return false;
+    const int kc = q->kp.n == 1 ? q->kp.col[0] : -1;
+    return q->kt.dense && q->kt.dmul == 1 && q->kt.dadd == 0 && kc >= 0 && q->kp.div[0] == 0 &&
+           (q->load_type[kc] == SH_T_STRID || q->load_type[kc] == SH_T_INT) && filter_kind(q->fp) == 0 &&
+           !q->xmode && !q->d.stream_current && q->ap.n > 0 && q->P > 1 && !q->partitioned && !q->given;
+}
+
+static PosSrc pos_src(const sh_query* q, const sh_batch* b) {
+    PosSrc ps{};
+    if (!b) return ps;
+    if (q->direct_pos) {
+        ps.key = (const int*)b->cols[q->kp.col[0]];
+        ps.mask = q->kt.dev().mask;
+    } else {
+        ps.np = q->new_pos.as<u32>();
+    }
+    return ps;
+}
+
 static int closed_finish(sh_query* q, bool host_out);
 
 static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::vector<int64_t>& clocks,
@@ -355,7 +404,7 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
         if (q->ms_ready && q->rec_packed && long_seg) q->ms_ready = false;
         if (!q->ms_ready) RCHK(run_multisplit(q, closed_hi, b, false, long_seg));
         RCHK(q->seg_off.reserve((size_t)(nseg + 1) * q->P * 8, false));
-        launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), b ? q->new_pos.as<u32>() : nullptr, q->P,
+        launch_seg_offsets(s, dsegs, nseg, q->n_pend, q->pend_pos.as<u32>(), pos_src(q, b), q->P,
                            q->ms_counts.as<u32>(), q->ms_map, q->seg_off.as<int64_t>());
     }
     // (the record buffers' addresses only after run_multisplit: it may have grown them)
@@ -367,7 +416,9 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
                      q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
                      unit_rows, q->first_bits.as<u32>(),
                      rec_pos, own ? rec_idx : nullptr, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>(),
-                     q->rec_packed);
+                     q->rec_packed,
+                     EvSrc{q->n_pend, q->pend_ts.as<int64_t>(), ts, q->pend_gidx.as<u64>(),
+                           q->given && b ? q->given_gidx : nullptr, q->seq});
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     // output columns sized for the row capacity; the emit kernels read the row count on the device
@@ -874,6 +925,71 @@ static int pending_to_front(sh_query* q, int64_t lo, int64_t n) {
     return SH_OK;
 }
 
+// Small pushes that close no window — most calls of send(Event[n]) with small n: one kernel
+// (k_small_push) appends the passing events to the open window and reports through coherent pinned
+// memory, which the host polls instead of synchronising the stream. A push that would close a window
+// (or whose timestamps decrease) is reported back untouched and runs through the full pipeline.
+static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
+    *done = false;
+    const int64_t N = b->n;
+    if (N <= 0 || N > kSmallMax || q->kind != 0 || q->xmode || q->d.stream_current || q->partitioned || q->given ||
+        q->rate.kind != SH_RATE_NONE || q->ap.n == 0)
+        return SH_OK;
+    const int w = q->d.window;
+    if (!(w == SH_WIN_LENGTH_BATCH || (w == SH_WIN_TIME_BATCH && q->e0_valid && q->clock_valid))) return SH_OK;
+    if (!q->small_res) {
+        if (hipHostMalloc((void**)&q->small_res, sizeof(SmallRes), hipHostMallocCoherent | hipHostMallocMapped) !=
+                hipSuccess ||
+            hipHostGetDevicePointer((void**)&q->small_res_dev, q->small_res, 0) != hipSuccess)
+            return sh_fail(SH_ERR_OOM, "pinned allocation failed");
+        std::memset(q->small_res, 0, sizeof(SmallRes));
+    }
+    RCHK(grow_pending(q, q->n_pend + N, q->n_pend));
+    hipStream_t s = q->ctx->stream;
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b->cols[c]; }
+    WinParams wp{};
+    wp.kind = w;
+    wp.e0_valid = q->e0_valid;
+    wp.clock_valid = q->clock_valid;
+    wp.L = wp.T = q->d.window_param;
+    wp.E0 = q->E0;
+    wp.clock0 = q->clock;
+    wp.W_open = q->W_open;
+    wp.n_pend = q->n_pend;
+    wp.send_size = b->send_size;
+    wp.N = N;
+    const uint64_t token = ++q->small_token;
+    HIPCHK(hipEventRecord(q->ev_push0, s));
+    launch_small_push(s, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
+                      q->pend_vals.as<u64>(), q->pend_cap, q->pend_gidx.as<u64>(), q->seq, q->small_res_dev, token);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(q->ev_push1, s));
+    volatile SmallRes* r = q->small_res;
+    for (int spin = 0; *(volatile uint64_t*)&r->token != token; spin++) {
+        if ((spin & 1023) == 1023) {  // every ~1000 polls: is the stream still running?
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) {
+                if (*(volatile uint64_t*)&r->token != token) return sh_fail(SH_ERR_DEVICE, "small push: no report");
+                break;
+            }
+            if (e != hipErrorNotReady) return sh_fail(SH_ERR_DEVICE, std::string("small push: ") + hipGetErrorString(e));
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    uint32_t ctrl[4];
+    for (int i = 0; i < 4; i++) ctrl[i] = r->ctrl[i];
+    if (r->fallback) return SH_OK;  // nothing was appended (the key lookups it made are kept)
+    RCHK(q->kt.check_result(ctrl));
+    q->n_pend += r->total_pass;
+    q->seq += N;
+    q->clock = std::max(q->clock, (int64_t)r->max_tl);
+    q->stats.events = N;
+    *done = true;
+    return SH_OK;
+}
+
 static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh_out** out) {
     SH_TMARK(0);
     // expired / all-events output: the current rows stay on the device for xout_finish
@@ -897,6 +1013,14 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
     if (q->n_pend + N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
     if (N > 0 && !q->internal_keys && q->kt.n_keys > (int64_t)q->kt.size_ / 2) RCHK(query_reserve_keys(q, 0));
+    {
+        bool done = false;
+        RCHK(try_small_push(q, b, &done));
+        if (done) {
+            finish_out(q, host_out, out);
+            return SH_OK;
+        }
+    }
     HIPCHK(hipEventRecord(q->ev_push0, s));
     if (N > 0 && q->partitioned && !q->p0_known) RCHK(resolve_first_partition(q, b));
     if (N > 0 && !(q->partitioned && !q->p0_known)) {
@@ -954,7 +1078,9 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         }
         int max_bounds = (int)std::min<int64_t>(N + 1, 1 << 22);
         RCHK(q->bounds.reserve((size_t)max_bounds * sizeof(Bound), false));
-        RCHK(q->new_pos.reserve((size_t)N * 4, false));
+        q->direct_pos = want_direct_pos(q);
+        if (!q->direct_pos) RCHK(q->new_pos.reserve((size_t)N * 4, false));
+        u32* slot_col = q->direct_pos ? nullptr : q->new_pos.as<u32>();
         // large pushes split the whole push into key partitions right behind k_boundaries, which
         // counts the push's tiles for it (a small push usually closes no window: no split then)
         const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18) && !q->d.stream_current;
@@ -962,7 +1088,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         if (early_split) RCHK(reserve_ms_counts(q, ms_map));
         launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                           q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                          q->new_pos.as<u32>(), ext ? q->blk_xm.as<int64_t>() : nullptr,
+                          slot_col, ext ? q->blk_xm.as<int64_t>() : nullptr,
                           early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
                           single_pass, q->blk_tl.as<int64_t>());
         HIPCHK(hipGetLastError());
@@ -990,7 +1116,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             prefix_passes();
             launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
                               q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                              q->new_pos.as<u32>(), nullptr);
+                              slot_col, nullptr);
             HIPCHK(hipGetLastError());
             HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
@@ -1073,7 +1199,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             // from the open window's earlier events + these; the last window's entries stay queued
             const int64_t n_old = q->n_pend, M = n_old + info.total_pass;
             RCHK(grow_pending(q, M, n_old));
-            launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, 0, N, 0, n_old,
+            launch_compact_pending(s, b->ts, cs, pos_src(q, b), q->ap, 0, N, 0, n_old,
                                    q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                                    q->pend_vals.as<u64>(), q->pend_cap, nullptr, q->pend_gidx.as<u64>(), q->seq);
             HIPCHK(hipGetLastError());
@@ -1083,7 +1209,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             RCHK(pending_to_front(q, M - new_pend, new_pend));
         } else {
             RCHK(grow_pending(q, new_pend, dst_base));
-            launch_compact_pending(s, b->ts, cs, q->new_pos.as<u32>(), q->ap, e_lo, N, pcb_lo, dst_base,
+            launch_compact_pending(s, b->ts, cs, pos_src(q, b), q->ap, e_lo, N, pcb_lo, dst_base,
                                    q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                                    q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
                                    q->pend_gidx.as<u64>(), q->seq);
@@ -1118,6 +1244,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
 // run_closed calls append (only one per push today) the layout stays [col][n_rows] because a push
 // calls run_closed at most once.
 extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
+    SH_RANGE("sh_push");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
     sh_batch dev;
@@ -1168,6 +1295,7 @@ int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out) {
 }
 
 extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out) {
+    SH_RANGE("sh_push_device");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
     return push_any(q, b, false, out);
@@ -1216,6 +1344,7 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
 }
 
 extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
+    SH_RANGE("sh_advance_time");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
     if (q->kind == 1) {
@@ -1253,6 +1382,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     // device buffers are released by their destructors (stream-ordered on this context)
     q->kt.release();
     if (q->h_info) (void)hipHostFree(q->h_info);
+    if (q->small_res) (void)hipHostFree(q->small_res);
     hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1, q->ev_mid};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     delete q;
@@ -1267,9 +1397,9 @@ extern "C" int sh_query_stats(sh_query* q, sh_stats* out) {
 
 // ---- multisplit: the combined events into P key partitions (stable) -------------------------------
 int reserve_ms_counts(sh_query* q, const TileMap& m) {
-    const int64_t ncnt = (int64_t)q->P * m.nblk;
+    const int64_t ncnt = (int64_t)q->P * (m.nblk + 1);  // [tile][partition] + the partition-end row
     RCHK(q->ms_counts.reserve((ncnt + 4) * 4, false));
-    return q->ms_tmp.reserve(((ncnt + kTile - 1) / kTile + 16) * 8, false);
+    return q->ms_tmp.reserve(ms_offsets_tmp_bytes(m.nblk, q->P), false);
 }
 
 int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted, bool wide) {
@@ -1279,7 +1409,6 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted, boo
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     const TileMap m = counted ? make_tile_map(q->n_pend, hi) : make_tile_map(0, hi);
-    int64_t ncnt = (int64_t)P * m.nblk;
     RCHK(reserve_ms_counts(q, m));  // (the size k_boundaries' counts were written into: no regrowth)
     RCHK(q->part_off.reserve((P + 1) * 8, false));
     int64_t cap = std::max<int64_t>(hi, 1);
@@ -1288,12 +1417,12 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted, boo
     if (!pack) RCHK(q->rec_pos.reserve(cap * 4, false));
     RCHK(q->rec_idx.reserve(cap * 4, false));
     RCHK(q->rec_vals.reserve(std::max(1, q->ap.n_vcols) * cap * 8, false));
-    const u32* np = b ? q->new_pos.as<u32>() : nullptr;
+    const PosSrc np = pos_src(q, b);
     // the queued events' tiles (every tile when k_boundaries did not count); also zeroes the total slot
     launch_ms_count(s, m, counted ? m.np_t : m.nblk, q->n_pend, q->pend_pos.as<u32>(), np, P, q->ms_counts.as<u32>());
     // counts (u32: a push holds fewer than 2^32 events) are laid out [p][blk]; one exclusive scan
     // gives every (partition, block) its offset, and partition p starts at offset[p * nblk]
-    launch_scan_sum_large_u32(s, q->ms_counts.as<u32>(), ncnt + 1, q->ms_tmp.as<int64_t>());
+    launch_ms_offsets(s, q->ms_counts.as<u32>(), m.nblk, P, q->ms_tmp.as<int64_t>());
     launch_ms_scatter(s, m, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, np, cs, q->ap, P,
                       q->logP, q->ms_counts.as<u32>(), pack ? nullptr : q->rec_pos.as<u32>(), q->rec_idx.as<u32>(),
                       q->rec_vals.as<u64>(), cap, pack);

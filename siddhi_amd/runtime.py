@@ -255,34 +255,53 @@ class GpuAggregation:
 
 
 class PinnedBatch:
-    """An sh_batch whose SoA columns live in pinned host memory (sh_alloc_pinned): what the Java shim
-    packs a ComplexEventChunk into. `fill` copies numpy columns in; `view` exposes them."""
+    """An sh_batch whose SoA columns live in one pinned host block (sh_alloc_pinned): what the Java shim
+    packs a ComplexEventChunk into. For n events the block holds ts[n], then every column's n values,
+    each run 16-byte aligned — one contiguous region, so sh_stage moves it with a single H2D copy.
+    `fill` copies numpy columns in (laying the block out for their length); `arrays` are the views."""
 
     def __init__(self, schema: abi.Schema, capacity: int, send_size: int = 0):
         self.schema = schema
         self.capacity = capacity
+        self._dts = [np.dtype(np.int64)] + [np.dtype(abi.NP_DTYPE[t]) for t in schema.types]
         self._ptrs = []
-        sizes = [8] + [np.dtype(abi.NP_DTYPE[t]).itemsize for t in schema.types]
-        self.arrays = []
-        for sz, dt in zip(sizes, [np.int64] + [abi.NP_DTYPE[t] for t in schema.types]):
-            p = C.c_void_p()
-            _check(lib().sh_alloc_pinned(max(1, capacity * sz), C.byref(p)))
-            self._ptrs.append(p)
-            buf = (C.c_char * (capacity * sz)).from_address(p.value)
-            self.arrays.append(np.frombuffer(buf, dtype=dt, count=capacity))
+        p = C.c_void_p()
+        _check(lib().sh_alloc_pinned(max(1, self._span(capacity)), C.byref(p)))
+        self._ptrs.append(p)
         self.b = abi.Batch()
         self.b.send_size = send_size
-        self.b.ts = self._ptrs[0].value
-        for i in range(len(schema.types)):
-            self.b.cols[i] = self._ptrs[1 + i].value
+        self._layout(capacity)
         self.b.n = 0
+
+    @staticmethod
+    def _a16(x):
+        return (x + 15) & ~15
+
+    def _span(self, n):
+        off = 0
+        for dt in self._dts:
+            off = self._a16(off + n * dt.itemsize)
+        return off
+
+    def _layout(self, n):
+        base, off = self._ptrs[0].value, 0
+        self.arrays = []
+        for dt in self._dts:
+            buf = (C.c_char * max(1, n * dt.itemsize)).from_address(base + off)
+            self.arrays.append(np.frombuffer(buf, dtype=dt, count=n))
+            if len(self.arrays) == 1:
+                self.b.ts = base + off
+            else:
+                self.b.cols[len(self.arrays) - 2] = base + off
+            off = self._a16(off + n * dt.itemsize)
 
     def fill(self, ts, cols, send_size=None):
         n = len(ts)
         assert n <= self.capacity
-        self.arrays[0][:n] = ts
+        self._layout(n)
+        self.arrays[0][:] = ts
         for a, c in zip(self.arrays[1:], cols):
-            a[:n] = c
+            a[:] = c
         self.b.n = n
         if send_size is not None:
             self.b.send_size = send_size

@@ -225,3 +225,31 @@ def test_aggregation_checkpoint_restores_executors_and_tables(rt):
         other.restore(blob)
     for x in (g, fresh, o):
         x.close()
+
+
+def test_aggregation_truncated_blob_rolls_back(rt):
+    """sh_aggregation_restore from a truncated blob fails part-way (after the root window or inside an
+    executor / table section) and rolls the aggregation back to its state before the call."""
+    rng = np.random.default_rng(5)
+    n = 20_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 40, n)).astype(np.int64)
+    k = rng.integers(0, 20, n).astype(np.int32)
+    v = np.round(rng.normal(10, 3, n), 2)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("max", "v")], group_by=["k"], ts="ts",
+                               durations=("sec", "hour"), key_capacity=32)
+    bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], clock[a_:b_]], 1)
+    g, o = rt.GpuAggregation(spec), OracleAggregation(spec)
+    for x in (g, o):
+        x.push(bat(0, 8_000))
+    blob = g.snapshot()
+    for x in (g, o):
+        x.push(bat(8_000, 12_000))
+    for cut in (30, len(blob) // 2, len(blob) - 3):
+        with pytest.raises(Exception, match="truncated|does not match|restore"):
+            g.restore(blob[:cut])
+    for x in (g, o):
+        drive(x, [bat(12_000, n), ("advance", int(clock[-1]) + 7_200_000)])
+    assert_tables_equal(tables(g, spec), tables(o, spec), "after failed restores")
+    for x in (g, o):
+        x.close()

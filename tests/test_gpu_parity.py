@@ -257,6 +257,26 @@ def test_sliding_key_churn_bound(rt):
     g.close()
 
 
+@pytest.mark.parametrize("output", ["current", "all"])
+def test_sliding_many_live_keys_rebuild_hysteresis(rt, output):
+    """More than half of a time() window's hashed key table stays live across many pushes: the rebuild
+    keeps every key (none can be dropped), and the hysteresis (next rebuild only after size/8 more
+    keys) must not change the output — 40 pushes, ~80 of 128 slots live, a few new keys per push."""
+    sch = abi.Schema.parse("k long, v double, ts long")
+    n = 12_000
+    rng = np.random.default_rng(11)
+    ts = (np.arange(n, dtype=np.int64) * 2 + 5_000)
+    # 70 long-lived keys plus a slowly moving band of short-lived ones
+    hot = rng.integers(0, 70, n)
+    band = 1_000 + np.arange(n) // 150
+    k = np.where(rng.random(n) < 0.8, hot, band).astype(np.int64) * 7_919
+    v = rng.integers(-200, 200, n).astype(np.float64) / 4
+    spec = abi.QuerySpec(sch, "time", 400, group_by=["k"], aggs=[("sum", "v"), ("count", None), ("min", "v")],
+                         key_capacity=64, output=output)
+    both(rt, spec, split_batches(sch, ts, [k, v, ts.copy()], list(range(300, n, 300)), 1),
+         label=f"live keys {output}")
+
+
 @pytest.mark.parametrize("send_size", [1, 250])
 def test_c3_sliding_matches_oracle(rt, send_size):
     ts, cols = synth.keyed_stream(0, 200_000, 0xC3, 2000, 20)   # 20 events/ms, 10 s window ~ 100 per key

@@ -86,3 +86,31 @@ def test_sharded_snapshot_rejects_other_rank():
         b.restore(a.snapshot())
     a.close()
     b.close()
+
+
+def test_truncated_shard_blob_leaves_shard_unchanged():
+    """sh_shard_restore from a truncated blob fails without touching the shard: the rank's global
+    stream state is applied only after its owner restored, and a failure rolls both back."""
+    import torch
+    from siddhi_amd.shard import LocalShards, merge_owner_outputs
+    sp = spec(4_000)
+    pushes = stream_pushes(90_000, [30_000, 30_000, 30_000], 0xC2, 4_000, 100)
+    dev = torch.device("cuda", 0)
+    ls = LocalShards(sp, 2)
+    parts = []
+    for pi, (ts, cols) in enumerate(pushes):
+        if pi == 1:
+            blobs = ls.snapshot()
+            for g, sh in enumerate(ls.shards):
+                for cut in (40, len(blobs[g]) // 2, len(blobs[g]) - 5):
+                    with pytest.raises(Exception, match="truncated|does not match|restore"):
+                        sh.restore(blobs[g][:cut])
+        n = len(ts)
+        half = (n // 2)
+        slices = [(torch.from_numpy(np.ascontiguousarray(ts[a:b])).to(dev),
+                   [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in cols])
+                  for a, b in ((0, half), (half, n))]
+        outs = ls.push(slices, 1, dev)
+        parts.append(merge_owner_outputs(outs, ls.last_bounds, None))
+    ls.close()
+    assert_same(abi.concat_arrays(parts), run_oracle(sp, pushes, 1), label="shard after failed restores")

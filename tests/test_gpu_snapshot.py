@@ -111,3 +111,64 @@ def test_restore_into_a_different_query_fails_loudly():
         h.restore(blob)
     with pytest.raises(runtime.SiddhiError):
         runtime.GpuQuery(a).restore(blob[:40])
+
+
+@pytest.mark.parametrize("window", ["timeBatch", "time"])
+def test_truncated_blob_leaves_query_unchanged(window):
+    """A restore from a truncated blob fails and leaves the query exactly as it was (sh_query_restore
+    snapshots the current state first and rolls back): the query, restored from a blob cut at several
+    points after it moved on, continues identically to the uninterrupted oracle."""
+    from siddhi_amd import runtime
+    ts, cols = synth.keyed_stream(0, 200_000, 0xC2, 5_000, 50, quantized=True)
+    spec = abi.QuerySpec(C2, window, 700, group_by=["k"], aggs=[("count", None), ("min", "v"), ("sum", "v")],
+                         key_capacity=5_000)
+    pushes = split_batches(C2, ts, cols, [60_000, 120_000], 1)
+    g = runtime.GpuQuery(spec)
+    a = run_pushes(g, pushes[:1])
+    blob = g.snapshot()
+    b = run_pushes(g, pushes[1:2])  # moves on past the snapshot
+    for cut in (24, len(blob) // 3, len(blob) - 9):
+        with pytest.raises(Exception, match="truncated|does not match|restore"):
+            g.restore(blob[:cut])
+    c = run_pushes(g, pushes[2:])
+    g.close()
+    o = OracleQuery(spec)
+    ref = run_pushes(o, pushes)
+    o.close()
+    assert_same(abi.concat_arrays([a, b, c]), ref, label=f"{window} after failed restores")
+
+
+# ---- checkpoints of the state that round 2 refused: expired / all-events output (the carried batch,
+# the sliding expiry FIFO), pass-through sliding windows and every output rate limiter ------------------
+def _xstream(n=120_000, keys=3_000, per_ms=40):
+    ts, cols = synth.keyed_stream(0, n, 0xE5, keys, per_ms, quantized=True)
+    return ts, cols
+
+
+@pytest.mark.parametrize("window,param,output,group", [
+    ("timeBatch", 500, "all", True), ("lengthBatch", 4_000, "expired", True), ("timeBatch", 700, "all", False),
+    ("time", 400, "all", True), ("time", 300, "expired", False), ("time", 250, "current", None)])
+def test_expired_output_checkpoint(window, param, output, group):
+    """(group None: `select *` pass-through, whose sliding form keeps the expiry FIFO too)"""
+    ts, cols = _xstream()
+    aggs = [] if group is None else [("count", None), ("min", "v"), ("sum", "v")]
+    spec = abi.QuerySpec(C2, window, param, group_by=["k"] if group else [], aggs=aggs, output=output,
+                         key_capacity=3_000)
+    pushes = split_batches(C2, ts, cols, [40_000, 41_000, 90_000], 1)
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    for cut in (1, 3):
+        got, ref, _ = checkpointed(spec, pushes, cut)
+        assert_same(got, ref, label=f"{window} {output} ckpt at {cut}")
+
+
+@pytest.mark.parametrize("rate", [("all", 7), ("first", 5), ("last", 6), ("first_time", 300)])
+@pytest.mark.parametrize("group", [True, False])
+def test_rate_limited_checkpoint(rate, group):
+    """the limiter's counters, carried rows and key tables travel in the blob (restored into a query
+    with the same `output ... every`)"""
+    ts, cols = _xstream(80_000, 500, 20)
+    spec = abi.QuerySpec(C2, "lengthBatch", 900, group_by=["k"] if group else [],
+                         aggs=[("count", None), ("max", "v")], rate=rate, key_capacity=500)
+    pushes = split_batches(C2, ts, cols, [20_011, 50_000], 3)
+    got, ref, _ = checkpointed(spec, pushes, 1)
+    assert_same(got, ref, label=f"rate {rate} group {group} ckpt")
