@@ -41,5 +41,7 @@ int sort_u64_pairs(void* temp, size_t* bytes, const u64* keys, u64* keys_out, co
                    hipStream_t s);
 void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v);
 void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out);
+// time buckets of the root's queued events, relative to `ref` (out[0] = min, out[1] = max)
+void launch_pend_bucket_range(hipStream_t s, const u32* pos, i64 n, KeyTable kt, u32 ref, i64* out);
 
 }  // namespace shd

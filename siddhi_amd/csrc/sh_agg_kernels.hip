@@ -332,6 +332,29 @@ void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out) {
     hipLaunchKernelGGL(k_minmax_i64, dim3(g), dim3(kBlock), 0, s, x, n, out);
 }
 
+__global__ __launch_bounds__(kBlock) void k_pend_bucket_range(const u32* __restrict__ pos, i64 n, KeyTable kt,
+                                                              u32 ref, i64* out) {
+    i64 lo = INT64_MAX, hi = INT64_MIN;
+    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
+        const i64 d = (i64)(int)((u32)(slot_key(kt, pos[i]) >> 32) - ref);
+        lo = d < lo ? d : lo;
+        hi = d > hi ? d : hi;
+    }
+    lo = block_reduce(lo, MinOp(), INT64_MAX);
+    hi = block_reduce(hi, MaxOp(), INT64_MIN);
+    if (threadIdx.x == 0) {
+        atomicMin((long long*)&out[0], (long long)lo);
+        atomicMax((long long*)&out[1], (long long)hi);
+    }
+}
+
+void launch_pend_bucket_range(hipStream_t s, const u32* pos, i64 n, KeyTable kt, u32 ref, i64* out) {
+    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, s, out);
+    if (n <= 0) return;
+    const i64 g = std::min<i64>((n + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL(k_pend_bucket_range, dim3((unsigned)g), dim3(kBlock), 0, s, pos, n, kt, ref, out);
+}
+
 __global__ __launch_bounds__(kBlock) void k_fill_i64(i64* p, i64 n, i64 v) {
     i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) p[i] = v;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -168,6 +169,10 @@ struct sh_aggregation {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int64_t last_events = 0;
     bool timed = false;
+    // band keys for the root (KeyTable::lk): (bucket, dictionary id) slots by arithmetic while the live
+    // buckets fit `band_rows` consecutive buckets; the open-addressing table otherwise
+    bool band_ok = false;
+    uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
 };
 
 static LevelDev level_dev(Level& L, int nb) {
@@ -442,6 +447,27 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         shard_attach_aggregation(a->shard, a);
         *shard = a->shard;
     }
+    if (a->has_bucket && d->n_group_by == 1 && d->col_types[d->group_by[0]] == SH_T_STRID) {
+        // ids per bucket row: the GPU's share of the dictionary (sharded owners hold the ids = rank mod G)
+        const int64_t cap = rd.key_capacity, per = shard ? (cap + world - 1) / world : cap;
+        static const char* env_rows = getenv("SH_AGG_BAND_ROWS");  // A/B switch (0 = hash keys only)
+        uint32_t lk = 4, rows = env_rows ? (uint32_t)atoi(env_rows) : 8u;
+        while (((int64_t)1 << lk) < per) lk++;
+        while (rows > 4 && ((int64_t)rows << lk) > (8 << 20)) rows >>= 1;
+        if (rows >= 2 && ((int64_t)rows << lk) <= (8 << 20)) {
+            a->band_ok = true;
+            a->band_lk = lk;
+            a->band_rows = rows;
+            a->band_mul = shard ? (uint32_t)world : 1u;
+            a->band_add = shard ? (uint32_t)rank : 0u;
+            sh_query* q = a->root;
+            q->band_keys = true;
+            q->band_lk = lk;
+            q->band_rows = rows;
+            q->band_mul = a->band_mul;
+            q->band_add = a->band_add;
+        }
+    }
     a->nb = a->root->ap.n;
     a->bp.n = a->nb;
     for (int i = 0; i < a->nb; i++) {
@@ -525,6 +551,38 @@ void agg_release_sharded(sh_aggregation* a) { agg_free(a); }
 
 // Room in the root's key table for this push: (event-time bucket, key) pairs are bounded by
 // min(N, keys x buckets spanned); closed buckets' keys are dropped by the rebuild.
+// Band keys (KeyTable::lk): the push's buckets [lo, hi] and the queued events' buckets must lie in
+// band_rows consecutive buckets; the band is re-based (the queued events' slots re-derived) when the
+// push runs past it, and the root falls back to the open-addressing table while they do not fit.
+static int band_reserve(sh_aggregation* a, int64_t lo, int64_t hi, int64_t bound) {
+    sh_query* q = a->root;
+    const int64_t R = a->band_rows;
+    if (q->kt.lk && lo >= q->kt.band_base && hi < q->kt.band_base + R) return SH_OK;
+    int64_t ulo = lo, uhi = hi;
+    if (hi - lo < R && q->n_pend > 0) {
+        hipStream_t s = a->ctx->stream;
+        launch_pend_bucket_range(s, q->pend_pos.as<u32>(), q->n_pend, q->kt.dev(), (u32)lo, a->minmax.as<int64_t>());
+        HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(sh_wait_stream(s));
+        ulo = std::min(ulo, lo + a->h_minmax[0]);
+        uhi = std::max(uhi, lo + a->h_minmax[1]);
+    }
+    if (uhi - ulo < R) {
+        KeyTableHost nk;
+        RCHK(nk.init_band(a->band_lk, a->band_rows, ulo, a->band_mul, a->band_add));
+        SH_TRACE("aggregation root: key band [%lld, %lld)", (long long)ulo, (long long)(ulo + R));
+        return query_swap_keys(q, nk);
+    }
+    if (q->kt.lk) {
+        // buckets too far apart for the band: the open-addressing table, sized for the queued keys too
+        KeyTableHost nk;
+        RCHK(nk.init(std::min<int64_t>(q->n_pend, (int64_t)q->kt.size_) + bound));
+        SH_TRACE("aggregation root: buckets [%lld, %lld] leave the band", (long long)ulo, (long long)uhi);
+        RCHK(query_swap_keys(q, nk));
+    }
+    return query_reserve_keys(q, bound);
+}
+
 int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
     int64_t N = dev->n;
     if (N <= 0) return SH_OK;
@@ -534,9 +592,12 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
         hipStream_t s = a->ctx->stream;
         launch_minmax_i64(s, (const int64_t*)dev->cols[a->d.ts_col], N, a->minmax.as<int64_t>());
         HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        int64_t nb = a->h_minmax[1] / a->T_root - a->h_minmax[0] / a->T_root + 1;
+        HIPCHK(sh_wait_stream(s));
+        // the key's bucket component: ts / T truncated (sh_device.h key_part)
+        const int64_t lo = a->h_minmax[0] / a->T_root, hi = a->h_minmax[1] / a->T_root;
+        int64_t nb = hi - lo + 1;
         bound = (nb > 0 && keys <= N / nb) ? keys * nb : N;
+        if (a->band_ok) return band_reserve(a, lo, hi, bound);
     }
     return query_reserve_keys(a->root, bound);
 }

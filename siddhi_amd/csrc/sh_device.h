@@ -292,6 +292,13 @@ __device__ __forceinline__ bool probe_step(const KeyTable& kt, u64 key, u64 k, u
 __device__ __forceinline__ u32 dense_slot(const KeyTable& kt, u64 key) {
     u32 id = (u32)key;
     u32 s = kt.dmul == 1 ? id - kt.dadd : (id - kt.dadd) / kt.dmul;
+    if (kt.lk) {
+        // band: the bucket's row (the host placed every live bucket inside the band) and the id's slot
+        const u32 row = (u32)(key >> 32) - kt.b0;
+        if (row >= kt.rows) { atomicExch(kt.overflow, 3); return 0; }
+        if ((int)id < 0 || (s >> kt.lk) != 0) { atomicExch(kt.overflow, 2); return 0; }
+        return (row << kt.lk) | s;
+    }
     if ((i64)key < 0 || s > kt.mask) { atomicExch(kt.overflow, 2); return 0; }
     return s;
 }
@@ -342,6 +349,10 @@ __device__ __forceinline__ void key_slots(const KeyTable& kt, const u64* key, co
 }
 
 __device__ __forceinline__ u64 slot_key(const KeyTable& kt, u32 pos) {
+    if (kt.lk) {
+        const u32 s = pos & ((1u << kt.lk) - 1u);
+        return ((u64)(kt.b0 + (pos >> kt.lk)) << 32) | (u64)(s * kt.dmul + kt.dadd);
+    }
     if (kt.dense) return (u64)(pos * kt.dmul + kt.dadd);
     return pos > kt.mask ? kEmptyKey : kt.keys[pos];
 }

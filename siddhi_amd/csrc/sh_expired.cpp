@@ -49,7 +49,11 @@ static int copy_cols(hipStream_t s, void* dst, size_t dst_stride, const void* sr
 int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
     hipStream_t s = q->ctx->stream;
     const int nk = q->kp.n, na = q->ap.n;
-    const bool lb = q->d.window == SH_WIN_LENGTH_BATCH;
+    // lengthBatch and externalTimeBatch never close an empty batch: the expired copies of flush j go
+    // out with flush j + 1 (ExternalTimeBatchWindowProcessor.flushToOutputChunk :336-383), stamped
+    // with the attribute time that closed it (its running max, x_stamps) instead of the clock
+    const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
+    const bool lb = q->d.window == SH_WIN_LENGTH_BATCH || ext;
     const int m = (int)q->dev_flush_clock.size();
     const int64_t nr = q->dev_flush_offsets.back();
     const int64_t nc = q->xc_valid ? q->xc_n : 0;
@@ -96,6 +100,7 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         const It& it = kv.second;
         XItem x{};
         x.clock = it.clock;
+        x.xts = ext && kv.first >= 0 && kv.first < (int64_t)q->x_stamps.size() ? q->x_stamps[kv.first] : it.clock;
         if (it.p >= 0) { x.p_lo = src[it.p].lo; x.p_n = src[it.p].n; }
         if (it.c >= 0 && q->d.current_on) { x.c_lo = src[it.c].lo; x.c_n = src[it.c].n; }
         if (x.p_n + x.c_n == 0) continue;

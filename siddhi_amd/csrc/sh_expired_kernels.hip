@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kBlock) void k_x_scatter(const XItem* items, const 
             x_copy_current(m, o, S, T, nk, na, s_ts, s_keys, s_vals, s_nulls, s_rep, out);
             return;
         }
-        out.ts[o] = it.clock;
+        out.ts[o] = it.xts;
         out.expired[o] = 1;
         out.rep[o] = s_rep[r];
         for (int kk = 0; kk < nk; kk++) out.keys[(size_t)kk * T + o] = s_keys[(size_t)kk * S + r];

@@ -101,7 +101,9 @@ struct KeyTable {
     // dense mode (dictionary ids): slot = (id - dadd) / dmul, no probing, no table
     int dense;
     u32 dmul, dadd;
-    int pad;
+    // band mode (dense, lk > 0): an aggregation root's (time bucket, dictionary id) keys; bucket b
+    // owns slot row b - b0 of 2^lk slots, rows in [0, rows), so slot = (row << lk) | id slot
+    u32 lk, b0, rows;
 };
 
 // Window assignment for one push (see DESIGN.md "Window assignment").
@@ -337,6 +339,8 @@ void launch_shard_unpack(hipStream_t s, const unsigned char* rec, i64 M, int rec
 // [c_lo, c_lo + c_n) of the source array; tab_size > 0: merged by key through a table at tab_off.
 struct XItem {
     i64 p_lo, p_n, c_lo, c_n, clock, tab_off, tab_size, out_base;
+    i64 xts;  // timestamp of the expired rows (the flush clock; externalTimeBatch: the attribute time)
+    i64 pad;
 };
 struct XOut {
     i64* ts;

@@ -380,7 +380,9 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
             if (k < max_bounds) {
                 Bound b;
                 b.idx = wp.n_pend + e; b.W = W; b.clock = clk; b.clock_prev = clock_prev; b.pcb = pcb;
-                b.pad = SORTED ? tile : 0;  // (SORTED: pcb is in-tile until k_fix_bounds)
+                // (SORTED: pcb is in-tile until k_fix_bounds; externalTimeBatch: the attribute max M at
+                // the closing event, the expired rows' timestamp)
+                b.pad = SORTED ? tile : ext ? M : 0;
                 bounds[k] = b;
             }
         }

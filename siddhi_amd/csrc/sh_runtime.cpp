@@ -335,6 +335,7 @@ int KeyTableHost::init_dense(int64_t capacity, uint32_t mul, uint32_t add) {
     size_t ts = 16;
     while ((int64_t)ts < capacity) ts <<= 1;
     dense = true;
+    lk = 0;
     dmul = mul;
     dadd = add;
     size_ = ts;
@@ -347,8 +348,19 @@ int KeyTableHost::init_dense(int64_t capacity, uint32_t mul, uint32_t add) {
     return SH_OK;
 }
 
+int KeyTableHost::init_band(uint32_t lg, uint32_t nrows, int64_t base, uint32_t mul, uint32_t add) {
+    int rc = init_dense((int64_t)nrows << lg, mul, add);
+    if (rc) return rc;
+    lk = lg;
+    rows = nrows;
+    band_base = base;
+    b0 = (uint32_t)base;
+    return SH_OK;
+}
+
 int KeyTableHost::init_size(size_t ts) {
     dense = false;
+    lk = 0;
     size_ = ts;
     n_keys = 0;
     int rc = keys.reserve(ts * 8, false);
@@ -374,7 +386,9 @@ KeyTable KeyTableHost::dev() const {
     kt.dense = dense ? 1 : 0;
     kt.dmul = dmul;
     kt.dadd = dadd;
-    kt.pad = 0;
+    kt.lk = lk;
+    kt.b0 = b0;
+    kt.rows = rows;
     return kt;
 }
 
@@ -387,6 +401,7 @@ int KeyTableHost::check_async(hipStream_t s, uint32_t* pinned4) {
 int KeyTableHost::check_result(const uint32_t* c) {
     n_keys = c[0];
     if (c[2] == 2) return sh_fail(SH_ERR_INVALID, "dictionary id outside [0, key_capacity): raise key_capacity");
+    if (c[2] == 3) return sh_fail(SH_ERR_DEVICE, "aggregation time bucket outside the root key band");
     if (c[2]) return sh_fail(SH_ERR_INVALID, "group key table full: raise key_capacity");
     return SH_OK;
 }

@@ -125,8 +125,12 @@ struct KeyTableHost {
     int64_t n_keys = 0;  // keys inserted so far (read back by check)
     bool dense = false;  // dictionary ids: slot = (id - dadd) / dmul, no hashing
     uint32_t dmul = 1, dadd = 0;
+    // band mode (KeyTable::lk): rows of 2^lk slots for the time buckets [b0, b0 + rows)
+    uint32_t lk = 0, b0 = 0, rows = 0;
+    int64_t band_base = 0;  // b0 before truncation to 32 bits
     int init(int64_t capacity);
     int init_dense(int64_t capacity, uint32_t mul, uint32_t add);
+    int init_band(uint32_t lk, uint32_t rows, int64_t base, uint32_t mul, uint32_t add);
     int init_size(size_t ts);
     shd::KeyTable dev() const;
     int check(hipStream_t s);
@@ -134,6 +138,12 @@ struct KeyTableHost {
     int check_async(hipStream_t s, uint32_t* pinned4);
     int check_result(const uint32_t* pinned4);
     void release() { keys.release(); ctrl.release(); }
+};
+
+// a band key table's shape (snapshot / restore)
+struct KeyBand {
+    uint32_t lk = 0, rows = 0;
+    int64_t base = 0;
 };
 
 // Host vectors in pinned memory (hipHostMalloc) without value-initialisation on resize: the row
@@ -253,6 +263,9 @@ struct sh_query {
     bool ms_ready = false;
     bool rec_packed = false;
     bool direct_pos = false;
+    // an aggregation root whose key table may switch to band mode (sh_aggregation.cpp band_reserve)
+    bool band_keys = false;
+    uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
     // small-push fast path (try_small_push): the kernel's report in coherent pinned host memory
     shd::SmallRes* small_res = nullptr;
     shd::SmallRes* small_res_dev = nullptr;
@@ -300,6 +313,7 @@ struct sh_query {
     DevBuf x_items, x_keep, x_rank, x_match, x_tmp, x_matched, x_trow, x_tkey, pass_pos;
     PinnedBuf x_h;
     std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call
+    std::vector<int64_t> x_stamps;  // externalTimeBatch: attribute time (running max) closing flush j
     // stream.current.event batch windows (sh_window.cpp sc_rows): scratch of a push
     DevBuf sc_pcb, sc_skey, sc_skey2, sc_idx, sc_idx2, sc_chunk, sc_send, sc_hd, sc_pos, sc_starts, sc_tmp, sc_ghead,
         sc_pre, sc_sval, sc_slast, sc_ochunk, sc_osend, sc_sl, sc_sort, scx_fe, scx_fpre, scx_last, scx_rows, scx_rank,
@@ -366,6 +380,8 @@ int query_advance(sh_query* q, int64_t now, bool host_out, const sh_out** out);
 
 // make room for `extra` new keys in a batch query's table (rebuild / grow; batch windows only)
 int query_reserve_keys(sh_query* q, int64_t extra);
+// move the queued events' key slots into table `nk` (any mode to any mode) and make it the query's
+int query_swap_keys(sh_query* q, KeyTableHost& nk);
 
 // internal constructor for the aggregation root: a batch query with a prepared key plan
 int sh_query_create_internal(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, sh_query** out);

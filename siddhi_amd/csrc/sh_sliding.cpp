@@ -133,7 +133,7 @@ void sliding_destroy(sh_query* q) {
     if (!s) return;
     DevBuf* bufs[] = {&s->cnt, &s->f, &s->mm, &s->mm_has, &s->dq_head, &s->dq_len, &s->dq, &s->rhead, &s->rlen,
                       &s->rpm, &s->rval, &s->cur_send, &s->cur_first, &s->blk_pass, &s->blk_tl, &s->blk_pm,
-                      &s->info, &s->rec_raw, &s->rec_slot, &s->rec_clock, &s->rec_pm, &s->rec_ts, &s->rec_vals,
+                      &s->info, &s->rec_raw, &s->rec_slot, &s->rec_clock, &s->rec_pm, &s->rec_ts, &s->rec_vals, &s->rec_aos,
                       &s->slot_cnt, &s->counts, &s->tmp, &s->ranks, &s->part_off, &s->flags, &s->p_raw,
                       &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
@@ -206,6 +206,14 @@ static int sliding_rekey(sh_query* q) {
     return SH_OK;
 }
 
+// the key-sorted replay with 48-byte records (k_sl_wkey<AOS>): time windows of the count / sum / avg
+// / min / max-of-one-double shape with a min or max (sliding_keyed_ok)
+static bool keyed_aos(const sh_query* q) {
+    static const bool off = getenv("SH_SL_PARTITIONED") != nullptr || getenv("SH_SL_LANE_PER_KEY") != nullptr ||
+                            getenv("SH_SL_NO_AOS") != nullptr;
+    return !off && q->d.window == SH_WIN_TIME && sliding_keyed_ok(q->ap);
+}
+
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     if (s->lane) return plane_push(q, b, host_out, out);
@@ -253,6 +261,10 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), N};
+    if (keyed_aos(q)) {
+        RCHK(s->rec_aos.reserve((size_t)N * kSlAosWords * 8, false));
+        rec.aos = s->rec_aos.as<u64>();
+    }
     const bool ext = q->d.window == SH_WIN_EXT_TIME;
     if (ext) RCHK(s->rec_sclk.reserve(N * 8, false));
     launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
@@ -304,6 +316,10 @@ int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* co
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = cols[c]; }
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    if (keyed_aos(q)) {
+        RCHK(s->rec_aos.reserve((size_t)cap * kSlAosWords * 8, false));
+        rec.aos = s->rec_aos.as<u64>();
+    }
     launch_sl_records_given(st, M, ts, cs, q->kp, q->kt.dev(), q->ap, gclk, gpm, (const u64*)gidx, raw_base, rec,
                             s->slot_cnt.as<u32>());
     HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
@@ -328,6 +344,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     int V = std::max(1, q->ap.n_vcols);
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), rec_cap};
+    if (keyed_aos(q)) rec.aos = s->rec_aos.as<u64>();
     if (need > s->rc) {
         int64_t nrc = s->rc;
         while (nrc < need) nrc <<= 1;

@@ -17,7 +17,11 @@ struct SlRecords {
     i64* ts;
     u64* vals;    // [n_vcols][cap]
     i64 cap;
+    // keyed replay (k_sl_wkey): one 48-byte record per event instead of the clock / pm / ts / vals
+    // columns — {clock, pm, ts, value, raw, 0} — so the key-order walk reads each record as one line
+    u64* aos = nullptr;
 };
+constexpr int kSlAosWords = 6;
 
 // persistent per-key state (indexed by key slot)
 struct SlState {

@@ -113,10 +113,17 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
             u32 pos = key_slot(kt, make_key(kp, cols, e));
             rec.raw[r] = (u32)e;
             rec.slot[r] = pos;
-            rec.clock[r] = clk;
-            rec.pm[r] = pmx;
-            rec.ts[r] = t;
-            for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            if (rec.aos) {
+                ulonglong2* o = (ulonglong2*)(rec.aos + (size_t)r * kSlAosWords);
+                o[0] = make_ulonglong2((u64)clk, (u64)pmx);
+                o[1] = make_ulonglong2((u64)t, (u64)load_raw(cols, ap.vcol_src[0], e));
+                o[2] = make_ulonglong2((u64)e, 0ull);
+            } else {
+                rec.clock[r] = clk;
+                rec.pm[r] = pmx;
+                rec.ts[r] = t;
+                for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            }
             atomicAdd(&slot_cnt[pos], 1u);
             r++;
         }
@@ -142,12 +149,20 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_given(i64 M, const i64* _
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (r >= M) return;
     const u32 pos = key_slot(kt, make_key(kp, cols, r));
-    rec.raw[r] = (u32)((i64)gidx[r] - raw_base);
+    const u32 raw = (u32)((i64)gidx[r] - raw_base);
+    rec.raw[r] = raw;
     rec.slot[r] = pos;
-    rec.clock[r] = gclk[r];
-    rec.pm[r] = gpm[r];
-    rec.ts[r] = ts[r];
-    for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], r);
+    if (rec.aos) {
+        ulonglong2* o = (ulonglong2*)(rec.aos + (size_t)r * kSlAosWords);
+        o[0] = make_ulonglong2((u64)gclk[r], (u64)gpm[r]);
+        o[1] = make_ulonglong2((u64)ts[r], (u64)load_raw(cols, ap.vcol_src[0], r));
+        o[2] = make_ulonglong2((u64)raw, 0ull);
+    } else {
+        rec.clock[r] = gclk[r];
+        rec.pm[r] = gpm[r];
+        rec.ts[r] = ts[r];
+        for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], r);
+    }
     atomicAdd(&slot_cnt[pos], 1u);
 }
 
@@ -1547,12 +1562,18 @@ __global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, 
 // C3's 10k keys). TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
 constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)
 
-template <bool HSUM, bool HMIN, bool HMAX>
+// AOS: the records are read in key order through the sort's rank list from the 48-byte records
+// (SlRecords.aos), the lanes write the key-order (PM, value) columns the window-head reads use, and
+// the first-record flags / key-order positions the emit needs (what k_sl_kgather did in a pass of
+// its own, with five scattered 8-byte reads per record).
+template <bool HSUM, bool HMIN, bool HMAX, bool AOS>
 __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, const i64* __restrict__ g_clk,
-                                               const i64* __restrict__ g_pm, const u64* __restrict__ g_v,
+                                               i64* __restrict__ g_pm, u64* __restrict__ g_v,
                                                const i64* __restrict__ g_ts, const u32* __restrict__ g_raw,
                                                const u32* __restrict__ g_rank, SlState S, DFields fd, KOut ko, i64 T,
-                                               u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW) {
+                                               u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
+                                               const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
+                                               unsigned char* __restrict__ flags, u32* __restrict__ inv) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ i64 s_pm[kWS];
@@ -1590,15 +1611,43 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     int hj = 0;         // heads expired so far
     int open_row = 0;   // key-order index of the (send, key) row open at the chunk start
     i64 last_send = 0;
+    u32 prev_raw = 0;   // (AOS) the previous chunk's last record
     for (int o0 = 0; o0 < n; o0 += 64) {
         const int m = min(64, n - o0);
         const bool in = lane < m;
         const u32 i = a + (u32)(o0 + min(lane, m - 1));
-        const i64 clk = g_clk[i];
-        const u64 x = g_v[i];
-        const i64 ts = g_ts[i];
-        const u32 raw = g_raw[i];
-        const u32 rk = g_rank[i];
+        i64 clk, ts;
+        u64 x;
+        u32 raw, rk;
+        if (AOS) {
+            const u32 r = sorted_rank[i];
+            const ulonglong2* rp = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
+            const ulonglong2 w0 = rp[0], w1 = rp[1], w2 = rp[2];
+            clk = (i64)w0.x;
+            ts = (i64)w1.x;
+            x = w1.y;
+            raw = (u32)w2.x;
+            // a record opens a row when it is its key's first of its send (every record per-event)
+            u32 pr = __shfl_up(raw, 1, 64);
+            if (lane == 0) pr = prev_raw;
+            const bool fst = send_size == 1 || (o0 + lane == 0) || (send_size == 0 ? false : pr / send_size != raw / send_size);
+            rk = r | (fst ? kFirstBit : 0u);
+            if (in) {
+                g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
+                g_v[i] = x;
+                flags[r] = fst ? 1 : 0;
+                if (fst) inv[r] = i;
+            }
+            prev_raw = __shfl(raw, m - 1, 64);
+            __threadfence_block();  // this chunk's own records may expire within it
+            __syncthreads();
+        } else {
+            clk = g_clk[i];
+            x = g_v[i];
+            ts = g_ts[i];
+            raw = g_raw[i];
+            rk = g_rank[i];
+        }
         const int hb = hj;
         for (int q = lane; q < kWS; q += 64) {
             const int h = hb + q;
@@ -1655,7 +1704,9 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             if (lane >= d) grp = max(grp, up);
         }
         grp = max(grp, open_row);
-        const bool next_first = lane + 1 < m ? ((__shfl_down(rk, 1, 64) & kFirstBit) != 0) : true;
+        // (the shuffle runs on every lane: a lane may only read a lane that executes it)
+        const u32 rk_next = __shfl_down(rk, 1, 64);
+        const bool next_first = lane + 1 < m ? (rk_next & kFirstBit) != 0 : true;
         const i64 send = send_base + (send_size == 1 ? (i64)raw : send_size ? (i64)(raw / send_size) : 0);
         if (in && next_first) {
             u64 w[4 + SH_MAX_AGGS];
@@ -1790,15 +1841,22 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     const u32 ss = send_size > 0 ? (u32)send_size : 0u;
     hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
     launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
-    hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank,
-                       sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
     static const bool lane_per_key = getenv("SH_SL_LANE_PER_KEY") != nullptr;  // the round-2 kernel
     if (!lane_per_key) {
         const int RWw = sliding_keyed_row_words(ap.n);
-#define SH_SL_W(A, B, C)                                                                                           \
-    hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, \
-                       g_ts, g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RWw)
+        const bool AO = rec.aos != nullptr;
+        if (!AO)
+            hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                               sorted_rank, sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
+#define SH_SL_W1(A, B, C, D)                                                                                          \
+    hipLaunchKernelGGL((k_sl_wkey<A, B, C, D>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, \
+                       g_ts, g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RWw, sorted_rank, rec.aos, flags, inv)
+#define SH_SL_W(A, B, C)                 \
+    do {                                 \
+        if (AO) SH_SL_W1(A, B, C, true); \
+        else SH_SL_W1(A, B, C, false);   \
+    } while (0)
         if (hs && hn && hx) SH_SL_W(true, true, true);
         else if (hs && !hn && !hx) SH_SL_W(true, false, false);
         else if (!hs && hn && hx) SH_SL_W(false, true, true);
@@ -1808,8 +1866,11 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
         else if (hx && !hn) SH_SL_W(false, false, true);
         else SH_SL_W(false, false, false);
 #undef SH_SL_W
+#undef SH_SL_W1
         return;
     }
+    hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank,
+                       sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
     static const int kl_env = getenv("SH_SL_KL") ? atoi(getenv("SH_SL_KL")) : 16;
     const int KLr = kl_env == 8 || kl_env == 32 || kl_env == 64 ? kl_env : 16;
     const unsigned grid = (unsigned)((n + KLr - 1) / KLr);

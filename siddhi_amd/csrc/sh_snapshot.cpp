@@ -131,8 +131,14 @@ int batch_snapshot(sh_query* q, Writer& w) {
     w.val<uint8_t>(q->p0_known);
     w.val<int64_t>(q->p0);
     // group-key table: the queued events refer to its slots
-    w.val<uint8_t>(q->kt.dense);
+    // key mode: 0 open addressing, 1 dictionary ids, 2 band (an aggregation root's (bucket, id) rows)
+    w.val<uint8_t>(q->kt.lk ? 2 : q->kt.dense ? 1 : 0);
     w.val<uint64_t>(q->kt.size_);
+    if (q->kt.lk) {
+        w.val<uint32_t>(q->kt.lk);
+        w.val<uint32_t>(q->kt.rows);
+        w.val<int64_t>(q->kt.band_base);
+    }
     RCHK(q->kt.check(s));
     w.val<int64_t>(q->kt.n_keys);
     RCHK(w.dev(q->kt.keys.p, q->kt.dense ? 0 : q->kt.size_ * 8, s));
@@ -160,7 +166,7 @@ int batch_snapshot(sh_query* q, Writer& w) {
     return SH_OK;
 }
 
-int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend);
+int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend, const KeyBand* band);
 int query_set_partition(sh_query* q, int64_t p0);
 
 int batch_restore(sh_query* q, Reader& r) {
@@ -173,10 +179,20 @@ int batch_restore(sh_query* q, Reader& r) {
     q->xm = r.val<int64_t>();
     bool p0k = r.val<uint8_t>();
     int64_t p0 = r.val<int64_t>();
-    bool dense = r.val<uint8_t>();
+    const int mode = r.val<uint8_t>();
     uint64_t size = r.val<uint64_t>();
+    KeyBand band{};
+    if (mode == 2) {
+        band.lk = r.val<uint32_t>();
+        band.rows = r.val<uint32_t>();
+        band.base = r.val<int64_t>();
+    }
     int64_t nk = r.val<int64_t>();
-    if (!r.ok || dense != q->kt.dense) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    // a band-keyed root may be in either of its modes; any other query in the one it was created with
+    const bool fits = q->band_keys ? (mode == 0 || (mode == 2 && band.lk == q->band_lk && band.rows == q->band_rows))
+                                   : mode == (q->kt.dense ? 1 : 0);
+    if (!r.ok || !fits) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    const bool dense = mode != 0;
     // table of the snapshot's size, then its keys
     int64_t n_pend_peek;
     {
@@ -186,7 +202,7 @@ int batch_restore(sh_query* q, Reader& r) {
         n_pend_peek = t.val<int64_t>();
         if (!t.ok || n_pend_peek < 0) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     }
-    RCHK(query_resize_for_restore(q, size, n_pend_peek));
+    RCHK(query_resize_for_restore(q, size, n_pend_peek, mode == 2 ? &band : nullptr));
     RCHK(r.dev(q->kt.keys, dense ? 8 : size * 8, s));
     RCHK(set_key_count(q, nk));
     q->kt.n_keys = nk;
@@ -264,7 +280,8 @@ static int rate_restore(sh_query* q, Reader& rd) {
     hipStream_t s = q->ctx->stream;
     const int32_t kind = rd.val<int32_t>();
     const int64_t N = rd.val<int64_t>();
-    if (!rd.ok || kind != r.kind || N != r.N)
+    if (!rd.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    if (kind != r.kind || N != r.N)
         return sh_fail(SH_ERR_INVALID, "snapshot's output rate limiting differs from this query's (set it before restoring)");
     if (kind == SH_RATE_NONE) return SH_OK;
     r.seq = rd.val<int64_t>();

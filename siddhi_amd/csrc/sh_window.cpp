@@ -145,14 +145,18 @@ static int size_partitions(sh_query* q) {
 // Move the open window's keys into a fresh table of `size` slots: keys of closed windows are dead
 // (their group states were destroyed on flush, R9), so the rebuild drops them; the pending events'
 // slot positions are remapped.
-static int rekey(sh_query* q, size_t size) {
-    KeyTableHost nk;
-    RCHK(nk.init_size(size));
+int query_swap_keys(sh_query* q, KeyTableHost& nk) {
     launch_rekey(q->ctx->stream, q->n_pend, q->pend_pos.as<u32>(), q->kt.dev(), nk.dev());
     HIPCHK(hipGetLastError());
     RCHK(nk.check(q->ctx->stream));
     q->kt = std::move(nk);
     return size_partitions(q);
+}
+
+static int rekey(sh_query* q, size_t size) {
+    KeyTableHost nk;
+    RCHK(nk.init_size(size));
+    return query_swap_keys(q, nk);
 }
 
 int query_reserve_keys(sh_query* q, int64_t extra) {
@@ -196,7 +200,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
     const bool batch_win = d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME_BATCH;
     const bool pass_through = d->n_aggs == 0 && d->n_group_by == 0 && d->partition_col < 0 &&
-                              (batch_win || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME);
+                              (batch_win || d->window == SH_WIN_EXT_TIME_BATCH || d->window == SH_WIN_TIME ||
+                               d->window == SH_WIN_EXT_TIME);
     if ((d->n_aggs < 1 && !pass_through) || d->n_aggs > SH_MAX_AGGS)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "GPU path runs aggregation queries (1..8 aggregators) or pass-through lengthBatch / timeBatch / "
@@ -224,10 +229,11 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // key): one lane per partition (sh_plane.cpp)
     const bool plane = d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
                        (d->n_group_by == 0 || (d->n_group_by == 1 && d->group_by[0] == d->partition_col));
-    if ((!d->current_on || d->expired_on) && !((batch_win || sliding_win) && d->partition_col < 0) && !plane)
+    if ((!d->current_on || d->expired_on) &&
+        !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "expired / all-events output runs on lengthBatch, timeBatch, time and externalTime windows "
-                       "(partitioned: lengthBatch / time grouped by the partition key)");
+                       "expired / all-events output runs on lengthBatch, timeBatch, externalTimeBatch, time and "
+                       "externalTime windows (partitioned: lengthBatch / time grouped by the partition key)");
     if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "stream.current.event runs on aggregating, non-partitioned lengthBatch / timeBatch windows");
@@ -607,10 +613,14 @@ int query_set_partition(sh_query* q, int64_t key) {
 }
 
 // sh_query_restore: a key table of the snapshot's size and room for its queued events.
-int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend) {
-    if (q->kt.dense) {
+int query_resize_for_restore(sh_query* q, size_t table_size, int64_t n_pend, const KeyBand* band) {
+    if (band) {
+        q->kt.release();
+        RCHK(q->kt.init_band(band->lk, band->rows, band->base, q->band_mul, q->band_add));
         if (table_size != q->kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
-    } else if (table_size != q->kt.size_) {
+    } else if (q->kt.dense && !q->kt.lk) {
+        if (table_size != q->kt.size_) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    } else if (table_size != q->kt.size_ || q->kt.lk) {
         q->kt.release();
         RCHK(q->kt.init_size(table_size));
     }
@@ -995,6 +1005,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
     // expired / all-events output: the current rows stay on the device for xout_finish
     const bool host_out = host_out_req && !q->xmode;
     q->x_closes.clear();
+    q->x_stamps.clear();
     hipStream_t s = q->ctx->stream;
     q->out.reset();
     q->dev_flush_offsets.assign(1, 0);
@@ -1138,8 +1149,13 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             }
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
-        if (q->xmode)
-            for (auto& bd : bounds) q->x_closes.emplace_back(bd.W, bd.clock);
+        if (q->xmode) {
+            q->x_stamps.clear();
+            for (auto& bd : bounds) {
+                q->x_closes.emplace_back(bd.W, bd.clock);
+                q->x_stamps.push_back(bd.pad);  // (externalTimeBatch: the attribute max at the close)
+            }
+        }
         if (!q->given) {
             q->e0_valid = info.e0_valid;
             q->E0 = info.E0;

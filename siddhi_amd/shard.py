@@ -329,18 +329,24 @@ class TorchExchange:
     """The three collectives of a sharded push over torch.distributed (nccl = RCCL on ROCm, or gloo).
     Tensors live on `device` (a CUDA device for nccl, CPU for gloo)."""
 
-    def __init__(self, device, group=None):
+    def __init__(self, device, group=None, separate_control: bool = True):
+        """separate_control: the small collectives (slice summaries, window starts, record counts) run
+        on a communicator of their own (dist.new_group, collective over `group`'s ranks), so the next
+        push's summary all-gather does not queue behind the previous push's record all-to-all still
+        in flight on the data communicator (PipelinedPush)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.device = device
         self.world = dist.get_world_size(group)
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        self.ctrl = dist.new_group(ranks=ranks) if separate_control else group
 
     def all_gather_summaries(self, summary: np.ndarray) -> np.ndarray:
         import torch
         t = torch.as_tensor(summary, dtype=torch.int64).to(self.device)
         out = torch.empty(self.world * SUMMARY_WORDS, dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        self.dist.all_gather_into_tensor(out, t, group=self.ctrl)
         return out.cpu().numpy().reshape(self.world, SUMMARY_WORDS)
 
     def all_to_all(self, send, send_bytes: np.ndarray):
@@ -348,7 +354,7 @@ class TorchExchange:
         import torch
         sc = torch.as_tensor(np.asarray(send_bytes, dtype=np.int64)).to(self.device)
         rc = torch.empty_like(sc)
-        self.dist.all_to_all_single(rc, sc, group=self.group)
+        self.dist.all_to_all_single(rc, sc, group=self.ctrl)
         recv_bytes = rc.cpu().numpy()
         total = int(recv_bytes.sum())
         recv = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
@@ -364,7 +370,7 @@ class TorchExchange:
         import torch
         sc = torch.as_tensor(np.asarray(send_bytes, dtype=np.int64)).to(self.device)
         rc = torch.empty_like(sc)
-        self.dist.all_to_all_single(rc, sc, group=self.group)
+        self.dist.all_to_all_single(rc, sc, group=self.ctrl)
         recv_bytes = rc.cpu().numpy()
         total = int(recv_bytes.sum())
         recv = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
@@ -378,7 +384,7 @@ class TorchExchange:
         import torch
         n = torch.tensor([len(bounds)], dtype=torch.int64, device=self.device)
         ns = torch.empty(self.world, dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(ns, n, group=self.group)
+        self.dist.all_gather_into_tensor(ns, n, group=self.ctrl)
         counts = ns.cpu().numpy()
         mx = int(counts.max())
         if mx == 0:
@@ -387,7 +393,7 @@ class TorchExchange:
         pad[:len(bounds)] = bounds
         t = torch.as_tensor(pad).to(self.device)
         out = torch.empty(self.world * mx * BOUND_WORDS, dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(out, t.reshape(-1), group=self.group)
+        self.dist.all_gather_into_tensor(out, t.reshape(-1), group=self.ctrl)
         allb = out.cpu().numpy().reshape(self.world, mx, BOUND_WORDS)
         return np.concatenate([allb[r, :counts[r]] for r in range(self.world)])
 
@@ -436,13 +442,13 @@ class PipelinedPush:
         import time
         t0 = time.perf_counter()
         summ = self.q.summarize(n, ts_ptr, col_ptrs, send_size)
-        all_summ = self.ex.all_gather_summaries(summ)  # (after the previous exchange on the same group)
+        all_summ = self.ex.all_gather_summaries(summ)  # control communicator: not behind push i - 1's payload
         buf = self.bufs[self.k % len(self.bufs)]
         self.k += 1
         t1 = time.perf_counter()
         send_bytes, bounds = self.q.pack(all_summ, buf.data_ptr(), int(buf.numel()))
         t2 = time.perf_counter()
-        all_bounds = self.ex.all_gather_bounds(bounds)  # before the payload: collectives run in order
+        all_bounds = self.ex.all_gather_bounds(bounds)
         recv, recv_bytes, work = self.ex.all_to_all_start(buf, send_bytes)
         t3 = time.perf_counter()
         res = self._consume_pending()  # push i - 1 aggregates while push i's records move

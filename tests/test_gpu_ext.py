@@ -40,10 +40,10 @@ def stream(n, keys, seed, late_ms=0, per_ms=20, start_ms=5_000):
     return ts, [cols[0], cols[1], et.astype(np.int64), st, ts.copy()]
 
 
-def spec(T=1000, start=None, start_attr=None, filt=None, keys=1000, aggs=None):
-    return abi.QuerySpec(SCH, "externalTimeBatch", T, group_by=["k"], ts_attr="et", start_time=start,
-                         start_attr=start_attr, filter=filt, key_capacity=keys,
-                         aggs=aggs or [("count", None), ("sum", "v"), ("min", "v"), ("max", "et")])
+def spec(T=1000, start=None, start_attr=None, filt=None, keys=1000, aggs=None, output="current", group=True):
+    return abi.QuerySpec(SCH, "externalTimeBatch", T, group_by=["k"] if group else [], ts_attr="et", start_time=start,
+                         start_attr=start_attr, filter=filt, key_capacity=keys, output=output,
+                         aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "et")] if aggs is None else aggs)
 
 
 @pytest.mark.parametrize("send_size", [1, 64])
@@ -100,3 +100,19 @@ def test_external_time_filter_sum_and_dictionary_keys():
     ts, cols = stream(90_000, 40, 0xE9, late_ms=3000, per_ms=5)
     sp = ext_time_spec(800, 64, filt=(">", "v", 60.0), aggs=[("sum", "v"), ("max", "v"), ("count", None)])
     both(sp, split_batches(SCH, ts, cols, [1, 30_000, 59_998], 3), "externalTime filter")
+
+
+@pytest.mark.parametrize("output,group", [("all", True), ("expired", True), ("all", False), ("expired", None)])
+def test_ext_expired_and_all_events(output, group):
+    """ExternalTimeBatchWindowProcessor.flushToOutputChunk (:336-383): the flush closing batch X carries
+    batch X-1's events as EXPIRED (stamped with the attribute time that closed X: the running max of
+    `et`), then RESET, then X's events; batches are never empty, so X-1 is the previous flush. Late
+    events, bucket gaps (an idle stretch of event time) and batches carried across pushes.
+    group None: `select *` pass-through."""
+    ts, cols = stream(90_000, 20_000, 0xE7, late_ms=1_500)
+    cols[2] = cols[2] + (np.arange(len(ts)) >= 50_000) * 7_000  # a gap of several empty buckets
+    aggs = [] if group is None else None
+    got = both(spec(T=700, output=output, group=bool(group), aggs=aggs, keys=20_000),
+               split_batches(SCH, ts, cols, [20_000, 20_001, 64_000], 5), f"ext {output} {group}")
+    if group is not False:  # (without group-by a chunk is one row: the current one replaces the expired)
+        assert got["expired"].sum() > 1000
