@@ -55,6 +55,27 @@ extern "C" int sh_stage(sh_query* q, const sh_batch* b, int32_t* ticket) {
     if (g.outstanding >= 2) return sh_fail(SH_ERR_INVALID, "sh_stage: two staged batches are waiting for sh_push_staged");
     RCHK(ingest_init(q));
     const int slot = g.next_stage;
+    // a small batch in pinned host memory that the small-push kernel can take: no copy at all, the
+    // kernel reads it over PCIe in place (hipHostGetDevicePointer refuses pageable memory)
+    g.zc[slot] = false;
+    if (query_small_eligible(q, b->n)) {
+        sh_batch dv = *b;
+        bool ok = hipHostGetDevicePointer((void**)&dv.ts, (void*)b->ts, 0) == hipSuccess;
+        for (int c = 0; c < q->d.n_cols && ok; c++)
+            if (b->cols[c]) ok = hipHostGetDevicePointer((void**)&dv.cols[c], (void*)b->cols[c], 0) == hipSuccess;
+        (void)hipGetLastError();
+        if (ok) {
+            g.zc[slot] = true;
+            g.host[slot] = *b;
+            g.dev[slot] = dv;
+            g.bytes[slot] = 0;
+            g.ticket_gen[slot] = ++g.gen;
+            g.next_stage ^= 1;
+            g.outstanding++;
+            *ticket = (int32_t)((g.ticket_gen[slot] << 1) | (uint32_t)slot);
+            return SH_OK;
+        }
+    }
     hipStream_t cs = q->ctx->copy_stream;
     // the slot's previous batch must have been consumed by its push before it is overwritten
     if (g.used[slot]) HIPCHK(hipStreamWaitEvent(cs, g.consumed[slot], 0));
@@ -89,9 +110,18 @@ extern "C" int sh_push_staged(sh_query* q, int32_t ticket, const sh_out** out) {
     if (g.outstanding == 0 || slot != g.next_push || (uint32_t)ticket >> 1 != g.ticket_gen[slot])
         return sh_fail(SH_ERR_INVALID, "sh_push_staged: tickets are pushed once, in the order they were staged");
     hipStream_t s = q->ctx->stream;
-    HIPCHK(hipStreamWaitEvent(s, g.copied[slot], 0));
     g.outstanding--;
     g.next_push ^= 1;
+    if (g.zc[slot]) {
+        // read in place; staged on this stream only if the push leaves the small-push path
+        q->zc_host = &g.host[slot];
+        const int rc = query_push_staged(q, &g.dev[slot], out);
+        q->zc_host = nullptr;
+        g.last_h2d_ms = 0;
+        g.last_h2d_bytes = 0;
+        return rc;
+    }
+    HIPCHK(hipStreamWaitEvent(s, g.copied[slot], 0));
     const int rc = query_push_staged(q, &g.dev[slot], out);
     // the slot is free for the next sh_stage once the kernels that read it have run
     HIPCHK(hipEventRecord(g.consumed[slot], s));

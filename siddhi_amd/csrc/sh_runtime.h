@@ -263,6 +263,9 @@ struct sh_query {
     bool ms_ready = false;
     bool rec_packed = false;
     bool direct_pos = false;
+    // set during a zero-copy staged push: the host batch, staged on the compute stream if the push
+    // leaves the small-push path (sh_ingest.cpp)
+    const sh_batch* zc_host = nullptr;
     // an aggregation root whose key table may switch to band mode (sh_aggregation.cpp band_reserve)
     bool band_keys = false;
     uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
@@ -352,6 +355,10 @@ struct sh_query {
         uint32_t gen = 0;
         uint32_t ticket_gen[2]{};
         int64_t bytes[2]{};
+        // zero-copy slot: a small pinned batch the small-push kernel reads in place over PCIe (host[]
+        // is copied on the compute stream only if the push needs the full pipeline)
+        bool zc[2]{};
+        sh_batch host[2]{};
         double last_h2d_ms = 0;
         int64_t last_h2d_bytes = 0;
     } ing;
@@ -361,6 +368,8 @@ struct sh_query {
 int query_peek(sh_query* q, int64_t* n_rows);
 // push of a batch staged on the device by sh_stage, host output (sh_window.cpp)
 int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out);
+// a push the small-push kernel can take whole (no window state that forces the full pipeline)
+bool query_small_eligible(const sh_query* q, int64_t n);
 void ingest_destroy(sh_query* q);  // (sh_ingest.cpp)
 
 // expired / all-events output of a batch query's call (sh_expired.cpp)

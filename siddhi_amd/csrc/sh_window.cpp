@@ -939,14 +939,19 @@ static int pending_to_front(sh_query* q, int64_t lo, int64_t n) {
 // (k_small_push) appends the passing events to the open window and reports through coherent pinned
 // memory, which the host polls instead of synchronising the stream. A push that would close a window
 // (or whose timestamps decrease) is reported back untouched and runs through the full pipeline.
+bool query_small_eligible(const sh_query* q, int64_t N) {
+    if (N <= 0 || N > kSmallMax || q->kind != 0 || q->xmode || q->d.stream_current || q->partitioned || q->given ||
+        q->rate.kind != SH_RATE_NONE || q->ap.n == 0)
+        return false;
+    const int w = q->d.window;
+    return w == SH_WIN_LENGTH_BATCH || (w == SH_WIN_TIME_BATCH && q->e0_valid && q->clock_valid);
+}
+
 static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     *done = false;
     const int64_t N = b->n;
-    if (N <= 0 || N > kSmallMax || q->kind != 0 || q->xmode || q->d.stream_current || q->partitioned || q->given ||
-        q->rate.kind != SH_RATE_NONE || q->ap.n == 0)
-        return SH_OK;
+    if (!query_small_eligible(q, N)) return SH_OK;
     const int w = q->d.window;
-    if (!(w == SH_WIN_LENGTH_BATCH || (w == SH_WIN_TIME_BATCH && q->e0_valid && q->clock_valid))) return SH_OK;
     if (!q->small_res) {
         if (hipHostMalloc((void**)&q->small_res, sizeof(SmallRes), hipHostMallocCoherent | hipHostMallocMapped) !=
                 hipSuccess ||
@@ -971,11 +976,9 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     wp.send_size = b->send_size;
     wp.N = N;
     const uint64_t token = ++q->small_token;
-    HIPCHK(hipEventRecord(q->ev_push0, s));
     launch_small_push(s, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                       q->pend_vals.as<u64>(), q->pend_cap, q->pend_gidx.as<u64>(), q->seq, q->small_res_dev, token);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(q->ev_push1, s));
     volatile SmallRes* r = q->small_res;
     for (int spin = 0; *(volatile uint64_t*)&r->token != token; spin++) {
         if ((spin & 1023) == 1023) {  // every ~1000 polls: is the stream still running?
@@ -1031,6 +1034,13 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             finish_out(q, host_out, out);
             return SH_OK;
         }
+    }
+    sh_batch zc_dev;
+    if (q->zc_host) {
+        // a zero-copy batch that needs the full pipeline: on the device first
+        RCHK(q->staged.stage(s, q->zc_host, q->d.n_cols, q->d.col_types, &zc_dev));
+        q->zc_host = nullptr;
+        b = &zc_dev;
     }
     HIPCHK(hipEventRecord(q->ev_push0, s));
     if (N > 0 && q->partitioned && !q->p0_known) RCHK(resolve_first_partition(q, b));

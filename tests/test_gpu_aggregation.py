@@ -98,6 +98,41 @@ def test_c4_event_time_rollups(rt, send_size):
     assert n > 0
 
 
+STR_SCHEMA = abi.Schema.parse("k string, v double, ts long")
+
+
+@pytest.mark.parametrize("send_size", [1, 500])
+def test_c4_string_keys_band_rollups(rt, send_size):
+    """Dictionary keys under `aggregate by`: the root keys (bucket, id) by arithmetic in a band of
+    consecutive buckets, re-based as the stream moves on (sh_aggregation.cpp band_reserve)."""
+    ts, cols = synth.keyed_stream(1_700_000_000_000 - 15_000, 200_000, 0xC4, 2_000, 5)
+    pushes = split_batches(STR_SCHEMA, ts, cols, [33_333, 100_000, 150_001], send_size)
+    pushes.append(("advance", int(ts[-1]) + 3_600_000 * 30))
+    spec = abi.AggregationSpec(STR_SCHEMA, [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                               group_by=["k"], ts="ts", durations=("sec", "day"), key_capacity=2_000)
+    assert both(rt, spec, pushes, "C4 band", checkpoints=(0, 1, 2)) > 0
+
+
+def test_band_keys_fall_back_and_return(rt):
+    """A push whose event times spread over 30 s of sec buckets leaves the band for the open-addressing
+    table; once the queued events' buckets fit again the root returns to band keys. Tables equal the
+    oracle's after every push."""
+    rng = np.random.default_rng(21)
+    n = 90_000
+    clock = 1_700_000_000_000 + np.arange(n, dtype=np.int64) // 10  # 10 events per ms: pushes span 1-2 s
+    lag = np.zeros(n, np.int64)
+    lag[30_000:50_000] = rng.integers(0, 30_000, 20_000)
+    ext = clock - lag
+    k = rng.integers(0, 3_000, n).astype(np.int32)
+    v = np.round(rng.normal(50, 20, n), 2)
+    spec = abi.AggregationSpec(STR_SCHEMA, [("sum", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                               group_by=["k"], ts="ts", durations=("sec", "hour"), key_capacity=3_000)
+    cuts = [0, 10_000, 30_000, 50_000, 70_000, n]
+    pushes = [abi.HostBatch(STR_SCHEMA, clock[a:b], [k[a:b], v[a:b], ext[a:b]], 1) for a, b in zip(cuts, cuts[1:])]
+    pushes.append(("advance", int(clock[-1]) + 2 * 3_600_000))
+    both(rt, spec, pushes, "band fallback", checkpoints=(0, 1, 2, 3, 4))
+
+
 def test_processing_time_rollups_without_aggregate_by(rt):
     ts, cols = synth.keyed_stream(1_600_000_000_000, 100_000, 7, 300, 2)
     pushes = split_batches(C4_SCHEMA, ts, cols, [10_000, 60_000], 100)
@@ -184,17 +219,21 @@ def test_retrieval_mid_stream_matches_oracle(rt, proc_time):
 
 
 # ---- checkpoint of an aggregation (sh_aggregation_snapshot / restore) --------------------------------
-def test_aggregation_checkpoint_restores_executors_and_tables(rt):
+@pytest.mark.parametrize("ktype,lag", [("int", 70_000), ("string", 70_000), ("string", 1_000)])
+def test_aggregation_checkpoint_restores_executors_and_tables(rt, ktype, lag):
     """Snapshot mid-stream (root window pending, roll-up stores mid-bucket, late events); the rest of the
     stream pushed into (a) a fresh aggregation restored from the blob and (b) the original rolled back
-    after it had moved on must give the uninterrupted oracle's tables and retrievals."""
+    after it had moved on must give the uninterrupted oracle's tables and retrievals. String keys with
+    short lags snapshot the root in band mode, with 70 s lags in its open-addressing mode."""
     rng = np.random.default_rng(47)
     n = 30_000
     clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 50, n)).astype(np.int64)
-    ext = clock - rng.integers(0, 70_000, n).astype(np.int64)
+    if lag < 10_000:
+        clock = 1_706_745_000_000 + np.arange(n, dtype=np.int64) // 4  # pushes span a few sec buckets
+    ext = clock - rng.integers(0, lag, n).astype(np.int64)
     k = rng.integers(0, 30, n).astype(np.int32)
     v = np.round(rng.normal(50, 20, n), 3)
-    schema = abi.Schema.parse("k int, v double, ts long")
+    schema = abi.Schema.parse(f"k {ktype}, v double, ts long")
     spec = abi.AggregationSpec(schema, [("sum", "v"), ("avg", "v"), ("min", "v"), ("max", "v")], group_by=["k"],
                                ts="ts", durations=("sec", "day"), key_capacity=64)
     bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], ext[a_:b_]], 9)
@@ -227,7 +266,8 @@ def test_aggregation_checkpoint_restores_executors_and_tables(rt):
         x.close()
 
 
-def test_aggregation_truncated_blob_rolls_back(rt):
+@pytest.mark.parametrize("ktype", ["int", "string"])
+def test_aggregation_truncated_blob_rolls_back(rt, ktype):
     """sh_aggregation_restore from a truncated blob fails part-way (after the root window or inside an
     executor / table section) and rolls the aggregation back to its state before the call."""
     rng = np.random.default_rng(5)
@@ -235,7 +275,7 @@ def test_aggregation_truncated_blob_rolls_back(rt):
     clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 40, n)).astype(np.int64)
     k = rng.integers(0, 20, n).astype(np.int32)
     v = np.round(rng.normal(10, 3, n), 2)
-    schema = abi.Schema.parse("k int, v double, ts long")
+    schema = abi.Schema.parse(f"k {ktype}, v double, ts long")
     spec = abi.AggregationSpec(schema, [("sum", "v"), ("max", "v")], group_by=["k"], ts="ts",
                                durations=("sec", "hour"), key_capacity=32)
     bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], clock[a_:b_]], 1)
