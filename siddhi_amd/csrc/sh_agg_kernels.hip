@@ -76,58 +76,74 @@ __global__ __launch_bounds__(kBlock) void k_level_lookup(i64 n, const i64* __res
 
 __device__ __forceinline__ void level_fold(const LevelDev& L, const BasePlan& bp, u32 pos, const u64* vin,
                                            i64 stride, i64 i) {
+    u64* rec = L.vals + (size_t)pos * L.vs;  // the slot's values and has-mask share a line
+    const u64 has = rec[bp.n];
     for (int b = 0; b < bp.n; b++) {
         u64 x = vin[(size_t)b * stride + i];
-        size_t fi = (size_t)b * L.nslots + pos;
-        bool first = !L.has[fi];
-        u64 cur = L.vals[fi];
+        const bool first = !((has >> b) & 1);
+        u64 cur = rec[b], r = cur;
         switch (bp.kind[b]) {
-            case AK_SUM_L: case AK_COUNT: L.vals[fi] = (u64)((first ? 0 : (i64)cur) + (i64)x); break;  // sum += v
+            case AK_SUM_L: case AK_COUNT: r = (u64)((first ? 0 : (i64)cur) + (i64)x); break;  // sum += v
             case AK_SUM_D:
-                L.vals[fi] = (u64)__double_as_longlong((first ? 0.0 : __longlong_as_double((i64)cur)) +
-                                                       __longlong_as_double((i64)x));
+                r = (u64)__double_as_longlong((first ? 0.0 : __longlong_as_double((i64)cur)) + __longlong_as_double((i64)x));
                 break;
-            case AK_MIN_L: if (first || (i64)cur > (i64)x) L.vals[fi] = x; break;
-            case AK_MAX_L: if (first || (i64)cur < (i64)x) L.vals[fi] = x; break;
-            case AK_MIN_D: if (first || __longlong_as_double((i64)cur) > __longlong_as_double((i64)x)) L.vals[fi] = x; break;
-            case AK_MAX_D: if (first || __longlong_as_double((i64)cur) < __longlong_as_double((i64)x)) L.vals[fi] = x; break;
-            case AK_MIN_F: if (first || (float)__longlong_as_double((i64)cur) > (float)__longlong_as_double((i64)x)) L.vals[fi] = x; break;
-            case AK_MAX_F: if (first || (float)__longlong_as_double((i64)cur) < (float)__longlong_as_double((i64)x)) L.vals[fi] = x; break;
+            case AK_MIN_L: if (first || (i64)cur > (i64)x) r = x; break;
+            case AK_MAX_L: if (first || (i64)cur < (i64)x) r = x; break;
+            case AK_MIN_D: if (first || __longlong_as_double((i64)cur) > __longlong_as_double((i64)x)) r = x; break;
+            case AK_MAX_D: if (first || __longlong_as_double((i64)cur) < __longlong_as_double((i64)x)) r = x; break;
+            case AK_MIN_F: if (first || (float)__longlong_as_double((i64)cur) > (float)__longlong_as_double((i64)x)) r = x; break;
+            case AK_MAX_F: if (first || (float)__longlong_as_double((i64)cur) < (float)__longlong_as_double((i64)x)) r = x; break;
         }
-        L.has[fi] = 1;
+        rec[b] = r;
     }
+    rec[bp.n] = (1ull << bp.n) - 1;
 }
 
-// rows with distinct slots: fold in parallel
-__global__ __launch_bounds__(kBlock) void k_level_fold_par(i64 n, const u32* __restrict__ slots,
-                                                          const u64* __restrict__ vin, i64 stride, LevelDev L,
-                                                          BasePlan bp) {
+// The merge of one batch of rows: rows with distinct slots fold in parallel; when the lookup saw two
+// rows share a slot (late events) one lane folds them all in row order. The choice is made on the
+// device from the lookup's flag, so the host does not wait between the two kernels.
+__global__ __launch_bounds__(kBlock) void k_level_fold(i64 n, const u32* __restrict__ slots,
+                                                      const u64* __restrict__ vin, i64 stride, LevelDev L,
+                                                      BasePlan bp, const int* __restrict__ dup) {
+    if (*dup) {
+        if (blockIdx.x != 0 || threadIdx.x != 0) return;
+        for (i64 i = 0; i < n; i++) level_fold(L, bp, slots[i], vin, stride, i);
+        return;
+    }
     i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     level_fold(L, bp, slots[i], vin, stride, i);
 }
 
-// rows sharing a slot within one dispatch (late events): fold in row order, one lane
-__global__ void k_level_fold_seq(i64 n, const u32* __restrict__ slots, const u64* __restrict__ vin, i64 stride,
-                                 LevelDev L, BasePlan bp) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    for (i64 i = 0; i < n; i++) level_fold(L, bp, slots[i], vin, stride, i);
-}
+__global__ void k_zero_int(int* p) { *p = 0; }
 
 void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
                         const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
-                        int* dup_dev, int* dup_host) {
+                        int* dup_dev) {
     if (n == 0) return;
     unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
-    (void)hipMemsetAsync(dup_dev, 0, 4, s);
+    hipLaunchKernelGGL(k_zero_int, dim3(1), dim3(1), 0, s, dup_dev);
     hipLaunchKernelGGL(k_level_lookup, dim3(g), dim3(kBlock), 0, s, n, bucket_in, key_in, has_bucket, dur, L, epoch,
                        seq0, slots, dup_dev);
-    (void)hipMemcpyAsync(dup_host, dup_dev, 4, hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    if (*dup_host)
-        hipLaunchKernelGGL(k_level_fold_seq, dim3(1), dim3(64), 0, s, n, slots, vin, stride, L, bp);
-    else
-        hipLaunchKernelGGL(k_level_fold_par, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp);
+    hipLaunchKernelGGL(k_level_fold, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp, dup_dev);
+}
+
+__global__ __launch_bounds__(kBlock) void k_table_append(i64 n, const i64* __restrict__ bucket,
+                                                        const i64* __restrict__ key, const u64* __restrict__ vals,
+                                                        i64 vstride, int nb, i64* t_bucket, i64* t_key, u64* t_vals,
+                                                        i64 t_cap) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    t_bucket[i] = bucket[i];
+    t_key[i] = key[i];
+    for (int b = 0; b < nb; b++) t_vals[(size_t)b * t_cap + i] = vals[(size_t)b * vstride + i];
+}
+
+void launch_table_append(hipStream_t s, i64 n, const i64* bucket, const i64* key, const u64* vals, i64 vstride,
+                         int nb, i64* t_bucket, i64* t_key, u64* t_vals, i64 t_cap) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_table_append, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, bucket,
+                       key, vals, vstride, nb, t_bucket, t_key, t_vals, t_cap);
 }
 
 // ---- extraction of a level's store (dispatch) -----------------------------------------------------
@@ -177,10 +193,9 @@ __global__ __launch_bounds__(kBlock) void k_level_extract(LevelDev L, BasePlan b
             out_bucket[r] = store_ts;
             out_key[r] = (i64)k;
         }
-        for (int b = 0; b < bp.n; b++) {
-            out_vals[(size_t)b * cap + r] = L.vals[(size_t)b * L.nslots + p];
-            if (clear) L.has[(size_t)b * L.nslots + p] = 0;
-        }
+        u64* rec = L.vals + (size_t)p * L.vs;
+        for (int b = 0; b < bp.n; b++) out_vals[(size_t)b * cap + r] = rec[b];
+        if (clear) rec[bp.n] = 0;
         if (clear && p <= L.kt.mask) L.kt.keys[p] = kEmptyKey;  // BaseIncrementalValueStore.clearValues (:73-78)
         r++;
     }
@@ -302,18 +317,41 @@ void launch_find_fold(hipStream_t s, i64 n, const u32* idx, const u32* flag, con
 }
 
 // min / max of an int64 column (event-time span of a push -> root key-table bound)
-__global__ __launch_bounds__(kBlock) void k_minmax_i64(const i64* __restrict__ x, i64 n, i64* out) {
+// min / max of an i64 column in two passes: per-block partials (16-byte loads), then one block
+// folds them (a single pair of global atomics hit by every block serialised at the L2)
+constexpr int kMinmaxBlocks = 512;
+__global__ __launch_bounds__(kBlock) void k_minmax_i64(const i64* __restrict__ x, i64 n, i64* part) {
     i64 lo = INT64_MAX, hi = INT64_MIN;
-    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
-        i64 v = x[i];
-        lo = v < lo ? v : lo;
-        hi = v > hi ? v : hi;
+    const i64 n2 = n >> 1;
+    const longlong2* x2 = (const longlong2*)x;
+    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n2; i += (i64)gridDim.x * kBlock) {
+        const longlong2 v = x2[i];
+        lo = min(lo, (i64)min(v.x, v.y));
+        hi = max(hi, (i64)max(v.x, v.y));
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        lo = min(lo, x[n - 1]);
+        hi = max(hi, x[n - 1]);
     }
     lo = block_reduce(lo, MinOp(), INT64_MAX);
     hi = block_reduce(hi, MaxOp(), INT64_MIN);
     if (threadIdx.x == 0) {
-        atomicMin((long long*)&out[0], (long long)lo);
-        atomicMax((long long*)&out[1], (long long)hi);
+        part[2 * blockIdx.x] = lo;
+        part[2 * blockIdx.x + 1] = hi;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_minmax_final(const i64* __restrict__ part, int nb, i64* out) {
+    i64 lo = INT64_MAX, hi = INT64_MIN;
+    for (int i = threadIdx.x; i < nb; i += kBlock) {
+        lo = min(lo, part[2 * i]);
+        hi = max(hi, part[2 * i + 1]);
+    }
+    lo = block_reduce(lo, MinOp(), INT64_MAX);
+    hi = block_reduce(hi, MaxOp(), INT64_MIN);
+    if (threadIdx.x == 0) {
+        out[0] = lo;
+        out[1] = hi;
     }
 }
 
@@ -322,14 +360,34 @@ __global__ void k_minmax_init(i64* out) {
     out[1] = INT64_MIN;
 }
 
+size_t minmax_scratch_bytes() { return 16 + (size_t)kMinmaxBlocks * 16; }
+
+// a column that is not 16-byte aligned: scalar loads
+__global__ __launch_bounds__(kBlock) void k_minmax_i64_s(const i64* __restrict__ x, i64 n, i64* part) {
+    i64 lo = INT64_MAX, hi = INT64_MIN;
+    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
+        lo = min(lo, x[i]);
+        hi = max(hi, x[i]);
+    }
+    lo = block_reduce(lo, MinOp(), INT64_MAX);
+    hi = block_reduce(hi, MaxOp(), INT64_MIN);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = lo;
+        part[2 * blockIdx.x + 1] = hi;
+    }
+}
+
 void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out) {
-    // initialised on the stream by a kernel: an async copy from a stack array may read the array
-    // after this function returned (pageable source), which made the bucket span, and with it the
-    // root key-table reservation, intermittently wrong
-    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, s, out);
-    if (n <= 0) return;
-    unsigned g = (unsigned)std::min<i64>(1024, (n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_minmax_i64, dim3(g), dim3(kBlock), 0, s, x, n, out);
+    if (n <= 0) {
+        hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, s, out);
+        return;
+    }
+    const unsigned g = (unsigned)std::max<i64>(1, std::min<i64>(kMinmaxBlocks, (n / 2 + kBlock - 1) / kBlock));
+    if (((uintptr_t)x & 15) == 0)
+        hipLaunchKernelGGL(k_minmax_i64, dim3(g), dim3(kBlock), 0, s, x, n, out + 2);
+    else
+        hipLaunchKernelGGL(k_minmax_i64_s, dim3(g), dim3(kBlock), 0, s, x, n, out + 2);
+    hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(kBlock), 0, s, out + 2, (int)g, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_pend_bucket_range(const u32* __restrict__ pos, i64 n, KeyTable kt,

@@ -137,11 +137,12 @@ struct Level {
     int64_t next_emit = -1, start = -1, store_ts = -1;
     bool processed = false;
     KeyTableHost kt;
-    DevBuf vals, has, tag, first_seq, order, slots, dup, blk, out_bucket, out_key, out_vals;
+    DevBuf vals, tag, first_seq, order, slots, dup, blk, out_bucket, out_key, out_vals;
     int64_t n_in = 0;  // rows merged since the last dispatch
     int64_t nslots = 0;
     uint32_t epoch = 0;
     int* dup_host = nullptr;
+    uint32_t* chk = nullptr;  // pinned landing area of the key table's counters (checked after a sync)
 };
 
 struct sh_aggregation {
@@ -173,18 +174,33 @@ struct sh_aggregation {
     // buckets fit `band_rows` consecutive buckets; the open-addressing table otherwise
     bool band_ok = false;
     uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
+    bool chk_pending = false;  // level key-table counters queued to pinned memory, not yet verified
 };
+
+// The levels' key-table overflow checks are queued with each merge and verified after the next
+// synchronisation the aggregation makes anyway (a full table still fails the call loudly, one sync
+// later, instead of stalling the stream after every merge).
+static int agg_verify(sh_aggregation* a) {
+    if (!a->chk_pending) return SH_OK;
+    a->chk_pending = false;
+    for (auto& L : a->levels) RCHK(L.kt.check_result(L.chk));
+    return SH_OK;
+}
+
+static int agg_sync(sh_aggregation* a) {
+    HIPCHK(sh_wait_stream(a->ctx->stream));
+    return agg_verify(a);
+}
 
 static LevelDev level_dev(Level& L, int nb) {
     LevelDev D;
     D.kt = L.kt.dev();
     D.nslots = L.nslots;
     D.vals = L.vals.as<u64>();
-    D.has = L.has.as<unsigned char>();
+    D.vs = nb + 1;
     D.tag = L.tag.as<u32>();
     D.first_seq = L.first_seq.as<u32>();
     D.order = L.order.as<u32>();
-    (void)nb;
     return D;
 }
 
@@ -211,11 +227,9 @@ static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
         t.bucket = std::move(b2); t.key = std::move(k2); t.vals = std::move(v2);
         t.cap = ncap;
     }
-    HIPCHK(hipMemcpyAsync(t.bucket.as<int64_t>() + t.n, rb.bucket, rb.n * 8, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(t.key.as<int64_t>() + t.n, rb.key, rb.n * 8, hipMemcpyDeviceToDevice, s));
-    for (int b = 0; b < a->nb; b++)
-        HIPCHK(hipMemcpyAsync(t.vals.as<u64>() + (size_t)b * t.cap + t.n, rb.vals + (size_t)b * rb.cap, rb.n * 8,
-                              hipMemcpyDeviceToDevice, s));
+    launch_table_append(s, rb.n, rb.bucket, rb.key, rb.vals, rb.cap, a->nb, t.bucket.as<int64_t>() + t.n,
+                        t.key.as<int64_t>() + t.n, t.vals.as<u64>() + t.n, t.cap);
+    HIPCHK(hipGetLastError());
     t.n = need;
     return SH_OK;
 }
@@ -237,7 +251,7 @@ static int level_dispatch(sh_aggregation* a, size_t li, int64_t start_of_new) {
         launch_level_count(s, D, n_in, L.blk.as<int64_t>(), nblk);
         std::vector<int64_t> bc(nblk);
         HIPCHK(hipMemcpyAsync(bc.data(), L.blk.p, nblk * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        RCHK(agg_sync(a));
         int64_t n = 0;
         for (auto c : bc) n += c;
         int64_t cap = std::max<int64_t>(n, 1);
@@ -277,10 +291,11 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
         L.epoch++;
         if (L.n_in + rb.n >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "too many rows in one roll-up bucket");
         launch_level_merge(s, rb.n, rb.bucket, rb.key, a->has_bucket, L.dur, rb.vals, rb.cap, level_dev(L, a->nb),
-                           a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>(), L.dup_host);
+                           a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>());
         L.n_in += rb.n;
         HIPCHK(hipGetLastError());
-        RCHK(L.kt.check(s));
+        RCHK(L.kt.check_async(s, L.chk));
+        a->chk_pending = true;
         L.processed = true;
     }
     return SH_OK;
@@ -477,7 +492,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     HIPCHK(hipEventCreate(&a->ev0));
     HIPCHK(hipEventCreate(&a->ev1));
     // constant key / bucket columns for rows without them
-    RCHK(a->minmax.reserve(16, false));
+    RCHK(a->minmax.reserve(minmax_scratch_bytes(), false));
     HIPCHK(hipHostMalloc((void**)&a->h_minmax, 16, hipHostMallocDefault));
     RCHK(a->root_key_col.reserve(8 << 20, false));
     HIPCHK(hipMemsetAsync(a->root_key_col.p, 0, 8 << 20, ctx->stream));
@@ -488,15 +503,16 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         L.dur = dur;
         RCHK(L.kt.init(std::max<int64_t>(2 * rd.key_capacity, 64)));
         L.nslots = (int64_t)L.kt.size_ + 1;
-        RCHK(L.vals.reserve((size_t)a->nb * L.nslots * 8, false));
-        RCHK(L.has.reserve((size_t)a->nb * L.nslots, false));
+        RCHK(L.vals.reserve((size_t)(a->nb + 1) * L.nslots * 8, false));
         RCHK(L.tag.reserve(L.nslots * 4, false));
         RCHK(L.first_seq.reserve(L.nslots * 4, false));
         HIPCHK(hipMemsetAsync(L.first_seq.p, 0xFF, L.nslots * 4, ctx->stream));
         RCHK(L.dup.reserve(64, false));
-        HIPCHK(hipMemsetAsync(L.has.p, 0, (size_t)a->nb * L.nslots, ctx->stream));
+        HIPCHK(hipMemsetAsync(L.vals.p, 0, (size_t)(a->nb + 1) * L.nslots * 8, ctx->stream));
         HIPCHK(hipMemsetAsync(L.tag.p, 0, L.nslots * 4, ctx->stream));
         HIPCHK(hipHostMalloc((void**)&L.dup_host, 64, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&L.chk, 16, hipHostMallocDefault));
+        std::memset(L.chk, 0, 16);
     }
     *out = a;
     return SH_OK;
@@ -521,10 +537,11 @@ extern "C" int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_des
 
 static void agg_free(sh_aggregation* a) {
     for (auto& L : a->levels) {
-        DevBuf* bufs[] = {&L.vals, &L.has, &L.tag, &L.first_seq, &L.order, &L.slots, &L.dup, &L.blk, &L.out_bucket, &L.out_key, &L.out_vals};
+        DevBuf* bufs[] = {&L.vals, &L.tag, &L.first_seq, &L.order, &L.slots, &L.dup, &L.blk, &L.out_bucket, &L.out_key, &L.out_vals};
         for (auto* b : bufs) b->release();
         L.kt.release();
         if (L.dup_host) (void)hipHostFree(L.dup_host);
+        if (L.chk) (void)hipHostFree(L.chk);
     }
     for (auto& t : a->tables) { t.bucket.release(); t.key.release(); t.vals.release(); }
     a->root_bucket_col.release();
@@ -592,7 +609,7 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
         hipStream_t s = a->ctx->stream;
         launch_minmax_i64(s, (const int64_t*)dev->cols[a->d.ts_col], N, a->minmax.as<int64_t>());
         HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(sh_wait_stream(s));
+        RCHK(agg_sync(a));
         // the key's bucket component: ts / T truncated (sh_device.h key_part)
         const int64_t lo = a->h_minmax[0] / a->T_root, hi = a->h_minmax[1] / a->T_root;
         int64_t nb = hi - lo + 1;
@@ -704,7 +721,7 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
         for (int b = 0; b < a->nb; b++)
             HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * n, t.vals.as<u64>() + (size_t)b * t.cap + r0, n * 8,
                                   hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        RCHK(agg_sync(a));
         o.flush_offsets.push_back(n);
         o.flush_clock.push_back(a->root->clock);
     }
@@ -758,7 +775,7 @@ static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* k
     launch_scan_sum_large_u32(s, a->g_pre.as<u32>(), n + 1, a->g_tmp.as<int64_t>());
     uint32_t groups = 0;
     HIPCHK(hipMemcpyAsync(a->h_minmax, a->g_pre.as<u32>() + n, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    RCHK(agg_sync(a));
     std::memcpy(&groups, a->h_minmax, 4);
     const int64_t cap = std::max<int64_t>(groups, 1);
     RCHK(ob.reserve(cap * 8, false));
@@ -809,7 +826,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
         launch_level_count(s, D, n_in, L.blk.as<int64_t>(), nblk);
         std::vector<int64_t> bc(nblk);
         HIPCHK(hipMemcpyAsync(bc.data(), L.blk.p, nblk * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        RCHK(agg_sync(a));
         int64_t entries = 0;  // distinct (bucket, key) slots; rows merged into one slot count once
         for (auto c : bc) entries += c;
         launch_scan_sum(s, L.blk.as<int64_t>(), nblk);
@@ -883,7 +900,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
         for (int b = 0; b < nb; b++)
             HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * nr, a->v_vals.as<u64>() + (size_t)b * vcap, nr * 8,
                                   hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        RCHK(agg_sync(a));
         o.flush_offsets.push_back(nr);
         o.flush_clock.push_back(a->root->clock);
     }
@@ -953,7 +970,7 @@ uint64_t agg_fingerprint(const sh_aggregation* a) {
     mix(&d.key_capacity, 8);
     return h;
 }
-constexpr uint32_t kAggSnapVersion = 1;
+constexpr uint32_t kAggSnapVersion = 2;  // 2: level stores as [slot][base + has-mask] records
 }  // namespace
 
 static int agg_snapshot_blob(sh_aggregation* a, ABlob& w) {
@@ -983,8 +1000,7 @@ static int agg_snapshot_blob(sh_aggregation* a, ABlob& w) {
         RCHK(L.kt.check(s));
         w.val<int64_t>(L.kt.n_keys);
         RCHK(w.dev(L.kt.keys.p, L.kt.size_ * 8, s));
-        RCHK(w.dev(L.vals.p, (size_t)a->nb * L.nslots * 8, s));
-        RCHK(w.dev(L.has.p, (size_t)a->nb * L.nslots, s));
+        RCHK(w.dev(L.vals.p, (size_t)(a->nb + 1) * L.nslots * 8, s));
         RCHK(w.dev(L.tag.p, (size_t)L.nslots * 4, s));
         RCHK(w.dev(L.first_seq.p, (size_t)L.nslots * 4, s));
     }
@@ -1049,8 +1065,7 @@ static int agg_restore_blob(sh_aggregation* a, const void* buf, int64_t len) {
         HIPCHK(hipMemcpyAsync(L.kt.ctrl.p, c, 16, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
         L.kt.n_keys = nk;
-        RCHK(r.dev(L.vals.p, (int64_t)a->nb * L.nslots * 8, s));
-        RCHK(r.dev(L.has.p, (int64_t)a->nb * L.nslots, s));
+        RCHK(r.dev(L.vals.p, (int64_t)(a->nb + 1) * L.nslots * 8, s));
         RCHK(r.dev(L.tag.p, L.nslots * 4, s));
         RCHK(r.dev(L.first_seq.p, L.nslots * 4, s));
     }
