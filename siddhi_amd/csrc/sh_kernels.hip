@@ -253,11 +253,13 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
                                                       int ms_col0) {
     const int tile = blockIdx.x;
     i64 base = (i64)tile * kTile + (i64)threadIdx.x * kItems;
+    // the timestamps are loaded first, so their latency overlaps the filter, key and histogram work
+    i64 t[kItems];
+    load_items_i64(ts, base, wp.N, t, INT64_MIN);
     bool pass[kItems];
     filter_items<FK>(f, cols, base, wp.N, pass);
     // group-key slot of every passing event, looked up once for the whole pipeline
-    // (GroupByKeyGenerator.constructEventKey, QuerySelector.java:331-336); done before the timestamps
-    // are loaded so the lookup's registers and the window pass's are not live together
+    // (GroupByKeyGenerator.constructEventKey, QuerySelector.java:331-336)
     {
         u64 key[kItems];
         u32 pos[kItems];
@@ -306,9 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
                 ms_counts[(i64)(ms_col0 + tile) * P + i] = mhist[i];
         }
     }
-    i64 t[kItems];
     i64 cnt = 0, tl = INT64_MIN;
-    load_items_i64(ts, base, wp.N, t, INT64_MIN);
     SendCursor sc(wp, base);
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
@@ -1007,7 +1007,15 @@ __host__ __device__ constexpr int stage_words(int nk, int na, int order) { retur
 // slot. The records of a wave are then stored cooperatively through LDS: consecutive lanes write
 // consecutive 16-byte pieces of one record, so each store instruction covers whole 64-byte records
 // instead of one piece of 64 scattered ones.
+// DIRECT: the row's fields go straight to the SoA output columns at its rank (no staged record and
+// no k_emit_soa pass; the partial-line writes of a window's rows are merged in L2).
 constexpr int kStageMax = 2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1;
+struct EmitOut {
+    const u32* n_rows;
+    i64 *ts, *keys, *order, *rep;
+    u64* vals;
+};
+template <bool DIRECT>
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
                                                      const u32* __restrict__ unit_rows, i64 n_units,
                                                      int unit_stride,
@@ -1016,7 +1024,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
                                                      const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
                                                      const u64* __restrict__ pend_gidx,
                                                      const u64* __restrict__ new_gidx, int want_order, i64 seq_base,
-                                                     u64* stage) {
+                                                     u64* stage, EmitOut eo) {
     __shared__ ulonglong2 sw[kBlock][kStageMax / 2];
     __shared__ i64 so[kBlock];
     // thread (unit, j): the j-th row of a unit's region, if the unit produced that many
@@ -1048,6 +1056,16 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         i64 kv[SH_MAX_GROUP] = {0, 0};
         unpack_key(kp, slot_key(kt, pos), kv, 1);
         w[1] = tr.y;
+        if (DIRECT) {
+            const i64 n = (i64)*eo.n_rows;
+            eo.ts[o] = (i64)tr.x;
+            eo.rep[o] = (i64)tr.y;
+            for (int k = 0; k < nk; k++) eo.keys[(size_t)k * n + o] = kv[k];
+            if (want_order) eo.order[o] = sidx(first);
+#pragma unroll
+            for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) eo.vals[(size_t)a * n + o] = row[4 + a];
+            return;
+        }
         w[2] = (u64)kv[0];
         w[3] = (u64)kv[1];
         int c = 2 + nk;
@@ -1061,6 +1079,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         }
         so[t] = o;
     }
+    if (DIRECT) return;
     __syncthreads();
     // the wave's 64 records as SW / 2 pieces each, piece-major across lanes
     const int pcs = SW / 2, wb = t & ~63, lane = t & 63;
@@ -1106,8 +1125,17 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
     const int want_order = out_order ? 1 : 0;
     // (rounded to a multiple of 8 for the XCD-aware block order; surplus blocks find no row)
     const unsigned g1 = (unsigned)(((n_units * unit_stride + kBlock - 1) / kBlock + 7) / 8 * 8);
-    hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, word_pre,
-                       n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
+    static const bool direct = getenv("SH_EMIT_DIRECT") != nullptr;  // A/B switch
+    const EmitOut eo{n_rows_dev, out_ts, out_keys, out_order, out_rep, out_vals};
+    if (direct) {
+        hipLaunchKernelGGL(k_emit_rank<true>, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride,
+                           word_pre, n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base,
+                           stage, eo);
+        return;
+    }
+    hipLaunchKernelGGL(k_emit_rank<false>, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride,
+                       word_pre, n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage,
+                       eo);
     const unsigned g2 = (unsigned)((row_cap + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_emit_soa, dim3(g2), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,
                        out_ts, out_keys, out_vals, out_order, out_rep);
@@ -1488,7 +1516,7 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
 // (partition-major, tile order inside a partition). Row nblk gets each partition's end. Three passes
 // over coalesced rows: per block of kColT tiles the per-partition sums, per partition the exclusive
 // scan over the blocks (+ its total), the scan of the totals over the partitions, then the rows.
-constexpr int kColT = 64;
+constexpr int kColT = 16;
 __global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c, int nblk, int P, i64* bsum) {
     const int b = blockIdx.y;
     const int p = blockIdx.x * kBlock + threadIdx.x;
@@ -1499,16 +1527,20 @@ __global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c
     bsum[(i64)b * P + p] = acc;
 }
 
+// one workgroup per partition: the exclusive scan of its column of block sums, kBlock blocks at a
+// time (a thread per column walking every block serialised nb dependent loads: 63 us at C2 size)
 __global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P, i64* total) {
-    const int p = blockIdx.x * kBlock + threadIdx.x;
-    if (p >= P) return;
+    const int p = blockIdx.x;
     i64 run = 0;
-    for (int b = 0; b < nb; b++) {
-        const i64 x = bsum[(i64)b * P + p];
-        bsum[(i64)b * P + p] = run;
-        run += x;
+    for (int b0 = 0; b0 < nb; b0 += kBlock) {
+        const int b = b0 + threadIdx.x;
+        const i64 x = b < nb ? bsum[(i64)b * P + p] : 0;
+        i64 tot;
+        const i64 pre = block_excl_scan(x, SumOp(), 0, &tot);
+        if (b < nb) bsum[(i64)b * P + p] = run + pre;
+        run += tot;
     }
-    total[p] = run;
+    if (threadIdx.x == 0) total[p] = run;
 }
 
 __global__ __launch_bounds__(kBlock) void k_col_apply(u32* c, int nblk, int P, const i64* __restrict__ bpre,
@@ -1538,7 +1570,7 @@ void launch_ms_offsets(hipStream_t s, u32* counts, int nblk, int P, i64* tmp) {
     i64* base = total + P;
     const dim3 g((P + kBlock - 1) / kBlock, nb);
     if (nblk > 0) hipLaunchKernelGGL(k_col_reduce, g, dim3(kBlock), 0, s, counts, nblk, P, bsum);
-    hipLaunchKernelGGL(k_col_blocks, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, s, bsum, nb, P, total);
+    hipLaunchKernelGGL(k_col_blocks, dim3(P), dim3(kBlock), 0, s, bsum, nb, P, total);
     (void)hipMemcpyAsync(base, total, (size_t)P * 8, hipMemcpyDeviceToDevice, s);
     launch_scan_sum(s, base, P);
     if (nblk > 0) hipLaunchKernelGGL(k_col_apply, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, base, total);

@@ -1562,6 +1562,13 @@ __global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, 
 // C3's 10k keys). TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
 constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)
 
+// lane l's value of a 64-bit register (l wave-uniform)
+__device__ __forceinline__ u64 rl64(u64 v, int l) {
+    const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, l);
+    const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), l);
+    return ((u64)hi << 32) | lo;
+}
+
 // AOS: the records are read in key order through the sort's rank list from the 48-byte records
 // (SlRecords.aos), the lanes write the key-order (PM, value) columns the window-head reads use, and
 // the first-record flags / key-order positions the emit needs (what k_sl_kgather did in a pass of
@@ -1577,13 +1584,6 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ i64 s_pm[kWS];
-    __shared__ u64 s_hv[kWS];
-    __shared__ u64 s_x[64];
-    __shared__ int s_e[64];
-    __shared__ u64 s_sum[64], s_mn[64], s_mx[64];
-    __shared__ i64 s_cnt[64];
-    __shared__ unsigned char s_fl[64];
-    __shared__ int s_hj;
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= nslots) return;
@@ -1596,13 +1596,13 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     const int n = (int)(b - a), HN = H0 + n;
     auto head_pm = [&](int h) -> i64 { return h < H0 ? rpm[(rh0 + h) & gm] : g_pm[a + (h - H0)]; };
     auto head_v = [&](int h) -> u64 { return h < H0 ? rval[(rh0 + h) & gm] : g_v[a + (h - H0)]; };
-    // lane 0's running state
+    // the running state: the same in every lane (the sequential part runs wave-uniform)
     i64 cnt = 0;
     double sum = 0.0;
     KDq qn{}, qx{};
     u64* gmin = HMIN ? S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc : nullptr;
     u64* gmax = HMAX ? S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc : nullptr;
-    if (lane == 0) {
+    {
         cnt = S.cnt[k];
         if (HSUM) sum = __longlong_as_double((i64)S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k]);
         if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
@@ -1649,11 +1649,11 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             rk = g_rank[i];
         }
         const int hb = hj;
-        for (int q = lane; q < kWS; q += 64) {
-            const int h = hb + q;
-            if (h < HN) { s_pm[q] = head_pm(h); s_hv[q] = head_v(h); }
-        }
-        s_x[lane] = x;
+        // the next kWS window heads: PM in LDS (the lanes' binary searches), values in two registers
+        // per lane (entry d in lane d & 63 of hv0 / hv1, read back with readlane by the sequential part)
+        u64 hv0 = 0, hv1 = 0;
+        if (hb + lane < HN) { s_pm[lane] = head_pm(hb + lane); hv0 = head_v(hb + lane); }
+        if (hb + 64 + lane < HN) { s_pm[64 + lane] = head_pm(hb + 64 + lane); hv1 = head_v(hb + 64 + lane); }
         __syncthreads();
         // heads expired before this record: the first h in [hb, added) whose PM + T exceeds its clock
         int lo = hb, hi = in ? H0 + o0 + lane : hb;
@@ -1663,14 +1663,20 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             if (pm + T <= clk) lo = mid + 1;
             else hi = mid;
         }
-        if (in) s_e[lane] = lo;
-        __syncthreads();
-        if (lane == 0) {
+        // The order-dependent part, run by the whole wave in lockstep on wave-uniform values (so the
+        // compiler keeps the running state scalar): each record's expiry point and value, and the
+        // expiring heads' values, come from other lanes' registers by readlane instead of LDS, and
+        // record q's results land in lane q's registers (a select, no LDS store).
+        i64 r_cnt = 0;
+        u64 r_sum = 0, r_mn = 0, r_mx = 0;
+        u32 r_fl = 0;
+        {
             int h = hb;
             for (int q = 0; q < m; q++) {
-                const int e = max(s_e[q], h);
+                const int e = max(__builtin_amdgcn_readlane(lo, q), h);
                 for (; h < e; h++) {  // expired heads leave, oldest first (processRemove)
-                    const u64 v = h - hb < kWS ? s_hv[h - hb] : head_v(h);
+                    const int d = h - hb;
+                    const u64 v = d < 64 ? rl64(hv0, d) : d < kWS ? rl64(hv1, d - 64) : head_v(h);
                     cnt--;
                     if (HSUM) {
                         sum = sum - __longlong_as_double((i64)v);
@@ -1679,21 +1685,21 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                     if (HMIN) kdq_remove<true, 1>(qn, gmin, gm, dq_min, v);
                     if (HMAX) kdq_remove<false, 1>(qx, gmax, gm, dq_max, v);
                 }
-                const u64 xq = s_x[q];  // the event joins the window (processAdd)
+                const u64 xq = rl64(x, q);  // the event joins the window (processAdd)
                 cnt++;
                 if (HSUM) sum = sum + __longlong_as_double((i64)xq);
                 if (HMIN) kdq_add<true, 1>(qn, gmin, gm, dq_min, xq);
                 if (HMAX) kdq_add<false, 1>(qx, gmax, gm, dq_max, xq);
-                s_cnt[q] = cnt;
-                s_sum[q] = (u64)__double_as_longlong(sum);
-                s_mn[q] = qn.mm;
-                s_mx[q] = qx.mm;
-                s_fl[q] = (unsigned char)((qn.mmh ? 1 : 0) | (qx.mmh ? 2 : 0));
+                if (lane == q) {
+                    r_cnt = cnt;
+                    r_sum = (u64)__double_as_longlong(sum);
+                    r_mn = qn.mm;
+                    r_mx = qx.mm;
+                    r_fl = (qn.mmh ? 1u : 0u) | (qx.mmh ? 2u : 0u);
+                }
             }
-            s_hj = h;
+            hj = h;
         }
-        __syncthreads();
-        hj = s_hj;
         // the row of (send, key): opened by the group's first record (its key-order position), written
         // with the values after the group's last record of this chunk (a later chunk overwrites it)
         const bool first = in && (rk & kFirstBit);
@@ -1711,9 +1717,9 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         if (in && next_first) {
             u64 w[4 + SH_MAX_AGGS];
             u32 nulls = 0;
-            const i64 c = s_cnt[lane];
-            const u64 sb = s_sum[lane];
-            const unsigned char fl = s_fl[lane];
+            const i64 c = r_cnt;
+            const u64 sb = r_sum;
+            const u32 fl = r_fl;
             w[0] = (u64)ts;
             w[1] = (u64)raw | ((u64)k << 32);
             w[2] = (u64)clk;
@@ -1725,8 +1731,8 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                 if (src == 0) v = (u64)c;
                 else if (src == 1) v = sb;
                 else if (src == 2) v = (u64)__double_as_longlong(__longlong_as_double((i64)sb) / (double)c);
-                else if (src == 3) { v = s_mn[lane]; nulls |= ((fl & 1) ? 0u : 1u) << o; }
-                else { v = s_mx[lane]; nulls |= ((fl & 2) ? 0u : 1u) << o; }
+                else if (src == 3) { v = r_mn; nulls |= ((fl & 1) ? 0u : 1u) << o; }
+                else { v = r_mx; nulls |= ((fl & 2) ? 0u : 1u) << o; }
                 w[4 + o] = v;
             }
             w[3] = (u64)send | ((u64)nulls << 56);

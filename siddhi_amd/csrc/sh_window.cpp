@@ -298,8 +298,9 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
 // Where the push's key slots come from (PosSrc): dictionary ids that are their own slots, with no
 // filter and no consumer of the slot column but the multisplit path, are read from the key column.
 static bool want_direct_pos(const sh_query* q) {
-    static const bool off = getenv("SH_NO_DIRECT_POS") != nullptr;  // A/B switch for profiling
-    if (off) return false;
+    // opt-in (SH_DIRECT_POS=1): measured slower on MI355X — k_ms_scatter 290 vs 236 us per C2 push
+    // reading the key column instead of the slot column k_boundaries writes (profiles/r03_c2_v3*)
+    if (!getenv("SH_DIRECT_POS")) return false;
     const int kc = q->kp.n == 1 ? q->kp.col[0] : -1;
     return q->kt.dense && q->kt.dmul == 1 && q->kt.dadd == 0 && kc >= 0 && q->kp.div[0] == 0 &&
            (q->load_type[kc] == SH_T_STRID || q->load_type[kc] == SH_T_INT) && filter_kind(q->fp) == 0 &&
@@ -960,6 +961,7 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
         std::memset(q->small_res, 0, sizeof(SmallRes));
     }
     RCHK(grow_pending(q, q->n_pend + N, q->n_pend));
+    SH_TMARK(1);
     hipStream_t s = q->ctx->stream;
     ColSet cs{};
     cs.n = q->d.n_cols;
@@ -979,6 +981,7 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     launch_small_push(s, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
                       q->pend_vals.as<u64>(), q->pend_cap, q->pend_gidx.as<u64>(), q->seq, q->small_res_dev, token);
     HIPCHK(hipGetLastError());
+    SH_TMARK(2);
     volatile SmallRes* r = q->small_res;
     for (int spin = 0; *(volatile uint64_t*)&r->token != token; spin++) {
         if ((spin & 1023) == 1023) {  // every ~1000 polls: is the stream still running?
@@ -991,6 +994,7 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    SH_TMARK(3);
     uint32_t ctrl[4];
     for (int i = 0; i < 4; i++) ctrl[i] = r->ctrl[i];
     if (r->fallback) return SH_OK;  // nothing was appended (the key lookups it made are kept)

@@ -119,9 +119,12 @@ def test_c2_timebatch_matches_oracle(rt, send_size):
 C2S_SCHEMA = abi.Schema.parse("k string, v double, ts long")
 
 
-@pytest.mark.parametrize("send_size", [1, 1000])
-def test_c2_dictionary_keys_dense_slots(rt, send_size):
-    """k as a dictionary-encoded string: ids are the key slots (no hashing); same output as the oracle."""
+@pytest.mark.parametrize("send_size,direct", [(1, False), (1000, False), (1, True)])
+def test_c2_dictionary_keys_dense_slots(rt, send_size, direct, monkeypatch):
+    """k as a dictionary-encoded string: ids are the key slots (no hashing); same output as the oracle.
+    direct: the opt-in path that reads the slots from the key column (SH_DIRECT_POS, no slot column)."""
+    if direct:
+        monkeypatch.setenv("SH_DIRECT_POS", "1")
     ts, cols = synth.keyed_stream(0, 600_000, 0xC2, 100_000, 100)
     spec = abi.QuerySpec(C2S_SCHEMA, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=100_000)
