@@ -71,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void k_level_lookup(i64 n, const i64* __res
     slot_out[i] = pos;
     atomicMin(&L.first_seq[pos], seq0 + (u32)i);
     u32 old = atomicExch(&L.tag[pos], epoch);
-    if (old == epoch) atomicExch(dup, 1);
+    if (old == epoch) atomicExch(dup, (int)epoch);  // this merge's epoch: no reset between merges
 }
 
 __device__ __forceinline__ void level_fold(const LevelDev& L, const BasePlan& bp, u32 pos, const u64* vin,
@@ -104,8 +104,8 @@ __device__ __forceinline__ void level_fold(const LevelDev& L, const BasePlan& bp
 // device from the lookup's flag, so the host does not wait between the two kernels.
 __global__ __launch_bounds__(kBlock) void k_level_fold(i64 n, const u32* __restrict__ slots,
                                                       const u64* __restrict__ vin, i64 stride, LevelDev L,
-                                                      BasePlan bp, const int* __restrict__ dup) {
-    if (*dup) {
+                                                      BasePlan bp, const int* __restrict__ dup, u32 epoch) {
+    if (*dup == (int)epoch) {
         if (blockIdx.x != 0 || threadIdx.x != 0) return;
         for (i64 i = 0; i < n; i++) level_fold(L, bp, slots[i], vin, stride, i);
         return;
@@ -115,17 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_level_fold(i64 n, const u32* __restr
     level_fold(L, bp, slots[i], vin, stride, i);
 }
 
-__global__ void k_zero_int(int* p) { *p = 0; }
-
 void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
                         const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
                         int* dup_dev) {
     if (n == 0) return;
     unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_zero_int, dim3(1), dim3(1), 0, s, dup_dev);
     hipLaunchKernelGGL(k_level_lookup, dim3(g), dim3(kBlock), 0, s, n, bucket_in, key_in, has_bucket, dur, L, epoch,
                        seq0, slots, dup_dev);
-    hipLaunchKernelGGL(k_level_fold, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp, dup_dev);
+    hipLaunchKernelGGL(k_level_fold, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp, dup_dev, epoch);
 }
 
 __global__ __launch_bounds__(kBlock) void k_table_append(i64 n, const i64* __restrict__ bucket,

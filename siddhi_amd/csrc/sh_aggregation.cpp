@@ -143,6 +143,7 @@ struct Level {
     uint32_t epoch = 0;
     int* dup_host = nullptr;
     uint32_t* chk = nullptr;  // pinned landing area of the key table's counters (checked after a sync)
+    bool dirty = false;       // merged into since its counters were last fetched
 };
 
 struct sh_aggregation {
@@ -294,8 +295,7 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
                            a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>());
         L.n_in += rb.n;
         HIPCHK(hipGetLastError());
-        RCHK(L.kt.check_async(s, L.chk));
-        a->chk_pending = true;
+        L.dirty = true;  // its key-table counters are fetched once per push (agg_after_root)
         L.processed = true;
     }
     return SH_OK;
@@ -508,6 +508,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         RCHK(L.first_seq.reserve(L.nslots * 4, false));
         HIPCHK(hipMemsetAsync(L.first_seq.p, 0xFF, L.nslots * 4, ctx->stream));
         RCHK(L.dup.reserve(64, false));
+        HIPCHK(hipMemsetAsync(L.dup.p, 0, 64, ctx->stream));
         HIPCHK(hipMemsetAsync(L.vals.p, 0, (size_t)(a->nb + 1) * L.nslots * 8, ctx->stream));
         HIPCHK(hipMemsetAsync(L.tag.p, 0, L.nslots * 4, ctx->stream));
         HIPCHK(hipHostMalloc((void**)&L.dup_host, 64, hipHostMallocDefault));
@@ -665,7 +666,15 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
     RCHK(pass_root_flushes(a, o));
-    return catch_up(a);
+    RCHK(catch_up(a));
+    // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
+    for (auto& L : a->levels) {
+        if (!L.dirty) continue;
+        RCHK(L.kt.check_async(a->ctx->stream, L.chk));
+        L.dirty = false;
+        a->chk_pending = true;
+    }
+    return SH_OK;
 }
 
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
@@ -694,7 +703,15 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     const sh_out* o = nullptr;
     RCHK(sh_advance_time_device(a->root, now, &o));
     RCHK(pass_root_flushes(a, o));
-    return catch_up(a);
+    RCHK(catch_up(a));
+    // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
+    for (auto& L : a->levels) {
+        if (!L.dirty) continue;
+        RCHK(L.kt.check_async(a->ctx->stream, L.chk));
+        L.dirty = false;
+        a->chk_pending = true;
+    }
+    return SH_OK;
 }
 
 extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out** out) {

@@ -246,9 +246,11 @@ struct SmallRes {
     u32 ctrl[4];     // the key table's control words after the lookups (KeyTableHost::check_result)
     u64 token;       // written last: the host waits for it
 };
+// force: the host established that the push closes no window and its timestamps do not decrease
+// (an asynchronous small push), so the kernel appends without re-checking
 void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt,
                        AggPlan ap, u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap, u64* pend_gidx,
-                       i64 seq_base, SmallRes* res, u64 token);
+                       i64 seq_base, SmallRes* res, u64 token, bool force = false);
 // multisplit (partitioned aggregation, P > 1)
 // Multisplit tiles over the combined index space [0, hi) of queued + new events: tiles of kTile
 // events over [0, split) (the queued events), then tiles of kTile over [split, hi) (the push's
@@ -295,6 +297,7 @@ void launch_scan_sum_large_u32(hipStream_t s, u32* a, i64 n, i64* tmp);
 void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* part_off);
 void launch_seg_offsets(hipStream_t s, const Segment* segs, int nseg, i64 n_pend, const u32* pend_pos,
                         PosSrc new_pos, int P, const u32* counts, TileMap m, i64* seg_off);
+void launch_zero2(hipStream_t s, void* a, int na, void* b, int nb);
 void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_kt);
 
 // sharded ingest (sh_shard_kernels.hip)

@@ -394,6 +394,16 @@ __global__ __launch_bounds__(kBlock) void k_boundaries(const i64* __restrict__ t
     }
 }
 
+// two small regions zeroed by one launch (the push's info block and the tile-count tail)
+__global__ void k_zero2(unsigned char* a, int na, unsigned char* b, int nb) {
+    for (int i = threadIdx.x; i < na; i += blockDim.x) a[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) b[i] = 0;
+}
+
+void launch_zero2(hipStream_t s, void* a, int na, void* b, int nb) {
+    hipLaunchKernelGGL(k_zero2, dim3(1), dim3(256), 0, s, (unsigned char*)a, na, (unsigned char*)b, nb);
+}
+
 // SORTED form, after the scan of the tile counts (blk_pass[nblk] = total): the boundaries' pass
 // counts become push-relative and the push totals go to PushInfo (the clock max of a sorted push is
 // its last event's timestamp: the last event always ends a send).
@@ -894,7 +904,9 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       kSumI = agg_sig3(FOP_ADD_I, -1, -1), kSumISumD = agg_sig3(FOP_ADD_I, FOP_ADD_D, -1),
                       kSumMinMaxD = agg_sig3(FOP_ADD_D, FOP_MIN_D, FOP_MAX_D);  // aggregation base values
         const u32 sig = agg_sig(ap);
-        if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
+        static const bool r4 = getenv("SH_OWN_R4") != nullptr;  // A/B: half-size chunks, 3 workgroups per CU
+        if (r4 && K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 4, 4, kMinMaxAvgD);
+        else if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
         else if (K == 1 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 1, 8, 2, kSumD);
         else if (K == 1 && ap.n_vcols <= 1 && sig == kSumI) SH_AGG_OWN(1, 1, 8, 2, kSumI);
         else if (K == 1 && ap.n_vcols == 2 && sig == kSumISumD) SH_AGG_OWN(2, 1, 4, 2, kSumISumD);
@@ -1007,15 +1019,7 @@ __host__ __device__ constexpr int stage_words(int nk, int na, int order) { retur
 // slot. The records of a wave are then stored cooperatively through LDS: consecutive lanes write
 // consecutive 16-byte pieces of one record, so each store instruction covers whole 64-byte records
 // instead of one piece of 64 scattered ones.
-// DIRECT: the row's fields go straight to the SoA output columns at its rank (no staged record and
-// no k_emit_soa pass; the partial-line writes of a window's rows are merged in L2).
 constexpr int kStageMax = 2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1;
-struct EmitOut {
-    const u32* n_rows;
-    i64 *ts, *keys, *order, *rep;
-    u64* vals;
-};
-template <bool DIRECT>
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
                                                      const u32* __restrict__ unit_rows, i64 n_units,
                                                      int unit_stride,
@@ -1024,7 +1028,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
                                                      const i64* __restrict__ pend_ts, const i64* __restrict__ ts,
                                                      const u64* __restrict__ pend_gidx,
                                                      const u64* __restrict__ new_gidx, int want_order, i64 seq_base,
-                                                     u64* stage, EmitOut eo) {
+                                                     u64* stage) {
     __shared__ ulonglong2 sw[kBlock][kStageMax / 2];
     __shared__ i64 so[kBlock];
     // thread (unit, j): the j-th row of a unit's region, if the unit produced that many
@@ -1056,16 +1060,6 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         i64 kv[SH_MAX_GROUP] = {0, 0};
         unpack_key(kp, slot_key(kt, pos), kv, 1);
         w[1] = tr.y;
-        if (DIRECT) {
-            const i64 n = (i64)*eo.n_rows;
-            eo.ts[o] = (i64)tr.x;
-            eo.rep[o] = (i64)tr.y;
-            for (int k = 0; k < nk; k++) eo.keys[(size_t)k * n + o] = kv[k];
-            if (want_order) eo.order[o] = sidx(first);
-#pragma unroll
-            for (int a = 0; a < SH_MAX_AGGS; a++) if (a < n_aggs) eo.vals[(size_t)a * n + o] = row[4 + a];
-            return;
-        }
         w[2] = (u64)kv[0];
         w[3] = (u64)kv[1];
         int c = 2 + nk;
@@ -1079,7 +1073,6 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         }
         so[t] = o;
     }
-    if (DIRECT) return;
     __syncthreads();
     // the wave's 64 records as SW / 2 pieces each, piece-major across lanes
     const int pcs = SW / 2, wb = t & ~63, lane = t & 63;
@@ -1125,17 +1118,8 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
     const int want_order = out_order ? 1 : 0;
     // (rounded to a multiple of 8 for the XCD-aware block order; surplus blocks find no row)
     const unsigned g1 = (unsigned)(((n_units * unit_stride + kBlock - 1) / kBlock + 7) / 8 * 8);
-    static const bool direct = getenv("SH_EMIT_DIRECT") != nullptr;  // A/B switch
-    const EmitOut eo{n_rows_dev, out_ts, out_keys, out_order, out_rep, out_vals};
-    if (direct) {
-        hipLaunchKernelGGL(k_emit_rank<true>, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride,
-                           word_pre, n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base,
-                           stage, eo);
-        return;
-    }
-    hipLaunchKernelGGL(k_emit_rank<false>, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride,
-                       word_pre, n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage,
-                       eo);
+    hipLaunchKernelGGL(k_emit_rank, dim3(g1), dim3(kBlock), 0, s, rows, RW, unit_rows, n_units, unit_stride, word_pre,
+                       n_aggs, kt, kp, n_pend, pend_ts, ts, pend_gidx, new_gidx, want_order, seq_base, stage);
     const unsigned g2 = (unsigned)((row_cap + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_emit_soa, dim3(g2), dim3(kBlock), 0, s, stage, n_rows_dev, kp.n, n_aggs, want_order, out_cap,
                        out_ts, out_keys, out_vals, out_order, out_rep);
@@ -2063,7 +2047,8 @@ template <int FK>
 __global__ __launch_bounds__(kSmallT) void k_small_push(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                        WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
                                                        u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap,
-                                                       u64* pend_gidx, i64 seq_base, SmallRes* res, u64 token) {
+                                                       u64* pend_gidx, i64 seq_base, SmallRes* res, u64 token,
+                                                       int force) {
     const int t = threadIdx.x;
     const i64 base = (i64)t * kItems;
     bool pass[kItems];
@@ -2096,6 +2081,7 @@ __global__ __launch_bounds__(kSmallT) void k_small_push(const i64* __restrict__ 
         const i64 clk = max(wp.clock_valid ? wp.clock0 : INT64_MIN, ts[wp.N - 1]);
         fallback |= wfun(wp, wp.E0, wp.e0_valid, 0, clk) > wp.W_open;
     }
+    if (force) fallback = false;
     if (!fallback) {
 #pragma unroll
         for (int i = 0; i < kItems; i++) {
@@ -2130,11 +2116,12 @@ __global__ __launch_bounds__(kSmallT) void k_small_push(const i64* __restrict__ 
 
 void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt,
                        AggPlan ap, u32* pend_pos, i64* pend_ts, u64* pend_vals, i64 pend_cap, u64* pend_gidx,
-                       i64 seq_base, SmallRes* res, u64 token) {
+                       i64 seq_base, SmallRes* res, u64 token, bool force) {
+    const int fo = force ? 1 : 0;
     switch (filter_kind(f)) {
-        case 0: hipLaunchKernelGGL(k_small_push<0>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token); break;
-        case 1: hipLaunchKernelGGL(k_small_push<1>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token); break;
-        default: hipLaunchKernelGGL(k_small_push<2>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token);
+        case 0: hipLaunchKernelGGL(k_small_push<0>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token, fo); break;
+        case 1: hipLaunchKernelGGL(k_small_push<1>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token, fo); break;
+        default: hipLaunchKernelGGL(k_small_push<2>, dim3(1), dim3(kSmallT), 0, s, ts, cols, f, wp, kp, kt, ap, pend_pos, pend_ts, pend_vals, pend_cap, pend_gidx, seq_base, res, token, fo);
     }
 }
 

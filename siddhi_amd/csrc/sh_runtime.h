@@ -272,7 +272,17 @@ struct sh_query {
     // small-push fast path (try_small_push): the kernel's report in coherent pinned host memory
     shd::SmallRes* small_res = nullptr;
     shd::SmallRes* small_res_dev = nullptr;
-    uint64_t small_token = 0;  // this push's key slots are read from the key column (pos_src)  // the split wrote packed records (rec_idx only)
+    uint64_t small_token = 0;
+    // asynchronous small pushes (sh_window.cpp small_async): the batch is copied into one of
+    // kZcRing pinned slots the kernel reads in place, and the call returns without waiting; the
+    // kernel's report (key-table counters) is verified by the next call that finds it, or waits for it
+    static constexpr int kZcRing = 8;
+    char* zc_ring = nullptr;      // pinned, mapped: kZcRing slots of zc_slot bytes
+    char* zc_ring_dev = nullptr;
+    size_t zc_slot = 0;
+    uint64_t zc_tok[kZcRing]{};   // token of the kernel that reads each slot
+    int zc_next = 0;
+    uint64_t async_tok = 0;       // last asynchronous push not yet verified (0: none)
     TileMap ms_map{};  // tiling of the last multisplit
     int64_t rec_cap = 0;
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation

@@ -948,6 +948,116 @@ bool query_small_eligible(const sh_query* q, int64_t N) {
     return w == SH_WIN_LENGTH_BATCH || (w == SH_WIN_TIME_BATCH && q->e0_valid && q->clock_valid);
 }
 
+// The last asynchronous small push's report: verified once its token has arrived (wait: spin for
+// it). Reports arrive in launch order and the key table's overflow flag is sticky, so any later
+// report covers the earlier pushes too.
+static int small_verify(sh_query* q, bool wait) {
+    if (!q->async_tok) return SH_OK;
+    volatile SmallRes* r = q->small_res;
+    hipStream_t s = q->ctx->stream;
+    for (int spin = 0; *(volatile uint64_t*)&r->token < q->async_tok; spin++) {
+        if (!wait) return SH_OK;
+        if ((spin & 1023) == 1023) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) {
+                if (*(volatile uint64_t*)&r->token < q->async_tok) return sh_fail(SH_ERR_DEVICE, "small push: no report");
+                break;
+            }
+            if (e != hipErrorNotReady) return sh_fail(SH_ERR_DEVICE, std::string("small push: ") + hipGetErrorString(e));
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    uint32_t ctrl[4];
+    for (int i = 0; i < 4; i++) ctrl[i] = r->ctrl[i];
+    q->async_tok = 0;
+    return q->kt.check_result(ctrl);
+}
+
+// Asynchronous small push (InputHandler.send returning once the junction has the events,
+// StreamJunction :104-131): a zero-copy batch of a query without a filter whose timestamps do not
+// decrease and that closes no window — the host checks both on the pinned batch itself — is copied
+// into a pinned ring slot (the caller may reuse its buffer as soon as the call returns), the append
+// kernel is queued and the call returns at once. Its report is verified by a later call.
+static int small_async(sh_query* q, bool* done) {
+    const sh_batch* hb = q->zc_host;
+    const int64_t N = hb->n;
+    if (filter_kind(q->fp) != 0 || getenv("SH_NO_ASYNC_SMALL")) return SH_OK;
+    const int64_t* hts = hb->ts;
+    for (int64_t i = 1; i < N; i++)
+        if (hts[i] < hts[i - 1]) return SH_OK;
+    const int64_t clk = q->clock_valid ? std::max(q->clock, hts[N - 1]) : hts[N - 1];
+    if (q->d.window == SH_WIN_LENGTH_BATCH ? q->n_pend + N >= q->d.window_param : wfun_host(q, clk) > q->W_open)
+        return SH_OK;
+    const int nc = q->d.n_cols;
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    if (!q->zc_ring) {
+        size_t sl = a16((size_t)kSmallMax * 8);
+        for (int c = 0; c < nc; c++) sl += a16((size_t)kSmallMax * type_size(q->d.col_types[c]));
+        if (hipHostMalloc((void**)&q->zc_ring, sl * sh_query::kZcRing, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&q->zc_ring_dev, q->zc_ring, 0) != hipSuccess) {
+            q->zc_ring = nullptr;
+            return sh_fail(SH_ERR_OOM, "pinned allocation failed");
+        }
+        q->zc_slot = sl;
+    }
+    volatile SmallRes* r = q->small_res;
+    hipStream_t s = q->ctx->stream;
+    const int slot = q->zc_next;
+    // the slot's previous reader has finished (reports arrive in launch order)
+    for (int spin = 0; *(volatile uint64_t*)&r->token < q->zc_tok[slot]; spin++) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) return sh_fail(SH_ERR_DEVICE, std::string("small push: ") + hipGetErrorString(e));
+        }
+    }
+    char* hbase = q->zc_ring + (size_t)slot * q->zc_slot;
+    char* dbase = q->zc_ring_dev + (size_t)slot * q->zc_slot;
+    sh_batch dv = *hb;
+    size_t off = 0;
+    std::memcpy(hbase, hts, (size_t)N * 8);
+    dv.ts = (const int64_t*)dbase;
+    off = a16((size_t)kSmallMax * 8);
+    ColSet cs{};
+    cs.n = nc;
+    for (int c = 0; c < nc; c++) {
+        const size_t ts_ = type_size(q->d.col_types[c]);
+        cs.type[c] = q->load_type[c];
+        cs.ptr[c] = nullptr;
+        if (hb->cols[c]) {
+            std::memcpy(hbase + off, hb->cols[c], (size_t)N * ts_);
+            cs.ptr[c] = dbase + off;
+        }
+        off += a16((size_t)kSmallMax * ts_);
+    }
+    WinParams wp{};
+    wp.kind = q->d.window;
+    wp.e0_valid = q->e0_valid;
+    wp.clock_valid = q->clock_valid;
+    wp.L = wp.T = q->d.window_param;
+    wp.E0 = q->E0;
+    wp.clock0 = q->clock;
+    wp.W_open = q->W_open;
+    wp.n_pend = q->n_pend;
+    wp.send_size = hb->send_size;
+    wp.N = N;
+    const uint64_t token = ++q->small_token;
+    launch_small_push(s, dv.ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
+                      q->pend_vals.as<u64>(), q->pend_cap, q->pend_gidx.as<u64>(), q->seq, q->small_res_dev, token,
+                      true);
+    HIPCHK(hipGetLastError());
+    q->zc_tok[slot] = token;
+    q->zc_next = (slot + 1) % sh_query::kZcRing;
+    q->async_tok = token;
+    q->n_pend += N;  // no filter: every event joins the open window
+    q->seq += N;
+    q->clock = clk;
+    q->clock_valid = true;
+    q->stats.events = N;
+    *done = true;
+    return SH_OK;
+}
+
 static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     *done = false;
     const int64_t N = b->n;
@@ -961,6 +1071,10 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
         std::memset(q->small_res, 0, sizeof(SmallRes));
     }
     RCHK(grow_pending(q, q->n_pend + N, q->n_pend));
+    if (q->zc_host) {
+        RCHK(small_async(q, done));
+        if (*done) return SH_OK;
+    }
     SH_TMARK(1);
     hipStream_t s = q->ctx->stream;
     ColSet cs{};
@@ -1033,11 +1147,13 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
     if (N > 0 && !q->internal_keys && q->kt.n_keys > (int64_t)q->kt.size_ / 2) RCHK(query_reserve_keys(q, 0));
     {
         bool done = false;
+        RCHK(small_verify(q, false));
         RCHK(try_small_push(q, b, &done));
         if (done) {
             finish_out(q, host_out, out);
             return SH_OK;
         }
+        RCHK(small_verify(q, true));  // the full pipeline reads the state the queued appends left
     }
     sh_batch zc_dev;
     if (q->zc_host) {
@@ -1096,8 +1212,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         };
         if (single_pass) {
             RCHK(q->blk_pass.reserve((size_t)(nblk + 1) * 8, false));
-            HIPCHK(hipMemsetAsync(q->info.p, 0, sizeof(PushInfo), s));
-            HIPCHK(hipMemsetAsync(q->blk_pass.as<int64_t>() + nblk, 0, 8, s));
+            launch_zero2(s, q->info.p, (int)sizeof(PushInfo), q->blk_pass.as<int64_t>() + nblk, 8);
+            HIPCHK(hipGetLastError());
         } else {
             prefix_passes();
         }
@@ -1332,6 +1448,7 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
 }
 
 static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_out** out) {
+    RCHK(small_verify(q, true));
     const bool host_out = host_out_req && !q->xmode;
     q->x_closes.clear();
     q->out.reset();
@@ -1413,6 +1530,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     q->kt.release();
     if (q->h_info) (void)hipHostFree(q->h_info);
     if (q->small_res) (void)hipHostFree(q->small_res);
+    if (q->zc_ring) (void)hipHostFree(q->zc_ring);
     hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1, q->ev_mid};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     delete q;

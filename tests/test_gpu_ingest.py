@@ -75,3 +75,50 @@ def test_staged_tickets_are_checked(rt):
     with pytest.raises(SiddhiError, match="order they were staged"):
         g.push_staged(t1)
     g.close()
+
+
+def test_async_small_push_reports_errors_on_the_next_call(rt):
+    """A staged small push that closes no window returns before its kernel ran (the batch was copied
+    into the library's pinned ring); a dictionary id beyond the key capacity in it is reported by the
+    next call that synchronises — loudly, one call late."""
+    from siddhi_amd.runtime import SiddhiError
+    ts, cols = synth.keyed_stream(0, 3_000, 0xC2, 100, 10)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 100_000, group_by=["k"], aggs=[("count", None)], key_capacity=128)
+    g = rt.GpuQuery(spec)
+    pb = [rt.PinnedBatch(SCHEMA, 1000), rt.PinnedBatch(SCHEMA, 1000)]
+    g.push_staged(g.stage(pb[0].fill(ts[:1000], [c[:1000] for c in cols], 1)))  # opens the window
+    bad = cols[0][1000:2000].copy()
+    bad[500] = 5_000  # outside [0, key_capacity)
+    g.push_staged(g.stage(pb[1].fill(ts[1000:2000], [bad, cols[1][1000:2000], cols[2][1000:2000]], 1)))
+    with pytest.raises(SiddhiError, match="dictionary id"):
+        g.advance_time(int(ts[-1]) + 1_000_000)
+    for b in pb:
+        b.close()
+    g.close()
+
+
+def test_async_small_pushes_then_unstaged_pushes_and_advance(rt):
+    """Asynchronous small pushes interleaved with ordinary pushes and a TIMER: the same rows as the
+    oracle (the queued appends land before the next call's work on the stream)."""
+    ts, cols = synth.keyed_stream(0, 60_000, 0xC2, 2_000, 20)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 700, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=2_000)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    bufs = [rt.PinnedBatch(SCHEMA, 1000) for _ in range(2)]
+    parts, want = [], []
+    for i, a in enumerate(range(0, 60_000, 1000)):
+        sl = slice(a, a + 1000)
+        hb = abi.HostBatch(SCHEMA, ts[sl], [c[sl] for c in cols], 1)
+        if i % 7 == 3:
+            parts.append(abi.out_arrays(g.push_raw(hb)))
+        else:
+            parts.append(abi.out_arrays(g.push_staged_raw(g.stage(bufs[i % 2].fill(ts[sl], [c[sl] for c in cols], 1)))))
+        want.append(abi.out_arrays(o.push_raw(hb)))
+        if i == 30:
+            parts.append(abi.out_arrays(g.advance_time_raw(int(ts[a + 999]) + 3)))
+            want.append(abi.out_arrays(o.advance_time_raw(int(ts[a + 999]) + 3)))
+    assert_same(abi.concat_arrays(parts), abi.concat_arrays(want), label="async small pushes")
+    for b in bufs:
+        b.close()
+    g.close()
+    o.close()
