@@ -990,8 +990,10 @@ uint64_t agg_fingerprint(const sh_aggregation* a) {
 constexpr uint32_t kAggSnapVersion = 2;  // 2: level stores as [slot][base + has-mask] records
 }  // namespace
 
+static int agg_state_write(sh_aggregation* a, ABlob& w);
+static int agg_state_read(sh_aggregation* a, AReader& r);
+
 static int agg_snapshot_blob(sh_aggregation* a, ABlob& w) {
-    hipStream_t s = a->ctx->stream;
     w.b.insert(w.b.end(), {'S', 'H', 'A', '1'});
     w.val<uint32_t>(kAggSnapVersion);
     w.val<uint64_t>(agg_fingerprint(a));
@@ -1002,6 +1004,13 @@ static int agg_snapshot_blob(sh_aggregation* a, ABlob& w) {
     RCHK(sh_query_snapshot(a->root, rb.data(), rl, &rl));
     w.val<int64_t>(rl);
     w.b.insert(w.b.end(), rb.begin(), rb.end());
+    return agg_state_write(a, w);
+}
+
+// Everything of an aggregation beyond its root window: the root bucket cursor, the roll-up executors
+// and the duration tables (the sharded form appends this to the shard's blob).
+static int agg_state_write(sh_aggregation* a, ABlob& w) {
+    hipStream_t s = a->ctx->stream;
     w.val<uint8_t>(a->root_init);
     w.val<int64_t>(a->root_bucket);
     // roll-up executors
@@ -1037,7 +1046,7 @@ extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap
     SH_RANGE("sh_aggregation_snapshot");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
-    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is checkpointed by sh_shard_snapshot");
     ABlob w;
     RCHK(agg_snapshot_blob(a, w));
     *len = (int64_t)w.b.size();
@@ -1060,6 +1069,11 @@ static int agg_restore_blob(sh_aggregation* a, const void* buf, int64_t len) {
     (void)hipStreamSynchronize(s);
     RCHK(sh_query_restore(a->root, r.p + r.o, rl));
     r.o += (size_t)rl;
+    return agg_state_read(a, r);
+}
+
+static int agg_state_read(sh_aggregation* a, AReader& r) {
+    hipStream_t s = a->ctx->stream;
     a->root_init = r.val<uint8_t>();
     a->root_bucket = r.val<int64_t>();
     if (r.val<uint32_t>() != (uint32_t)a->levels.size() || !r.ok)
@@ -1109,13 +1123,31 @@ static int agg_restore_blob(sh_aggregation* a, const void* buf, int64_t len) {
     return SH_OK;
 }
 
+// The sharded aggregation's sections after the shard's blob (sh_snapshot.cpp shard_snapshot_blob):
+// the aggregation's fingerprint, then agg_state_write's sections.
+int agg_shard_state_write(sh_aggregation* a, std::vector<uint8_t>& out) {
+    ABlob w;
+    w.val<uint64_t>(agg_fingerprint(a));
+    RCHK(agg_state_write(a, w));
+    out = std::move(w.b);
+    return SH_OK;
+}
+
+int agg_shard_state_read(sh_aggregation* a, const uint8_t* p, size_t n) {
+    AReader r{p, n};
+    if (r.val<uint64_t>() != agg_fingerprint(a) || !r.ok)
+        return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different aggregation");
+    a->chk_pending = false;
+    return agg_state_read(a, r);
+}
+
 // All or nothing: the aggregation's current state is snapshotted first and put back when the blob
 // fails part-way (the root window, an executor or a table section), keeping the first error.
 extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len) {
     SH_RANGE("sh_aggregation_restore");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
-    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "restore of a sharded aggregation");
+    if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is restored by sh_shard_restore");
     ABlob backup;
     const bool have = agg_snapshot_blob(a, backup) == SH_OK;
     const int rc = agg_restore_blob(a, buf, len);

@@ -728,10 +728,11 @@ extern "C" int sh_shard_stats(sh_shard* s, sh_stats* out) {
 // ---- checkpoint (sh_snapshot.cpp): the shard's global stream state; the owner query is snapshotted
 // by the query sections. sc = {clock_valid, clock, e0_valid, E0, W, carry, seq, sl_pm, send_base,
 // p0_known, p0, rank, world, sliding}.
+sh_aggregation* shard_aggregation(sh_shard* s) { return s->agg; }
+
 int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query** owner) {
     if (n != 14) return sh_fail(SH_ERR_INVALID, "shard snapshot layout");
     *owner = s->owner;
-    if (s->agg) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded aggregation: not supported");
     if (s->packed) return sh_fail(SH_ERR_INVALID, "shard snapshot between pack and consume");
     if (!set) {
         const int64_t v[14] = {s->clock_valid, s->clock, s->e0_valid, s->E0, s->W, s->carry, (int64_t)s->seq,

@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 4;  // 4: expired-output, pass-through sliding and rate-limiter state
+constexpr uint32_t kVersion = 5;  // 5: band key mode, sharded aggregation sections
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -428,7 +428,11 @@ int sliding_restore(sh_query* q, Reader& r) {
 }
 
 // ---- sharded query (sh_shard.cpp): the shard's global stream state + its owner query -------------
+// (a sharded aggregation's roll-up executors and tables follow as one length-prefixed section)
 int shard_checkpoint_state(sh_shard* s, int64_t* sc, int n, bool set, sh_query** owner);
+sh_aggregation* shard_aggregation(sh_shard* s);
+int agg_shard_state_write(sh_aggregation* a, std::vector<uint8_t>& out);
+int agg_shard_state_read(sh_aggregation* a, const uint8_t* p, size_t n);
 
 static int shard_snapshot_blob(sh_shard* sd, sh_query* q, Writer& w) {
     int64_t sc[14];
@@ -438,7 +442,16 @@ static int shard_snapshot_blob(sh_shard* sd, sh_query* q, Writer& w) {
     w.val<uint64_t>(fingerprint(q));
     w.val<uint32_t>((uint32_t)q->kind);
     for (int i = 0; i < 14; i++) w.val<int64_t>(sc[i]);
-    return q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w);
+    RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    sh_aggregation* a = shard_aggregation(sd);
+    w.val<uint8_t>(a ? 1 : 0);
+    if (a) {
+        std::vector<uint8_t> ab;
+        RCHK(agg_shard_state_write(a, ab));
+        w.val<uint64_t>(ab.size());
+        w.put(ab.data(), ab.size());
+    }
+    return SH_OK;
 }
 
 extern "C" int sh_shard_snapshot(sh_shard* sd, void* buf, int64_t cap, int64_t* len) {
@@ -476,6 +489,15 @@ static int shard_restore_blob(sh_shard* sd, sh_query* q, const void* buf, int64_
     const int rc = q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
     q->fp = keep;
     RCHK(rc);
+    sh_aggregation* a = shard_aggregation(sd);
+    const bool has_agg = r.val<uint8_t>() != 0;
+    if (!r.ok || has_agg != (a != nullptr)) return sh_fail(SH_ERR_INVALID, "snapshot does not match this shard");
+    if (a) {
+        const uint64_t n = r.val<uint64_t>();
+        if (!r.ok || r.o + n > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        RCHK(agg_shard_state_read(a, r.p + r.o, (size_t)n));
+        r.o += n;
+    }
     return shard_checkpoint_state(sd, sc, 14, true, &q);
 }
 

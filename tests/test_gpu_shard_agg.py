@@ -109,3 +109,40 @@ def test_sharded_processing_time_rollups():
                                durations=("sec", "hour"), key_capacity=300)
     res = run_both(spec, 2, split(ts, cols, [30_000, 70_000]), 100, [[0.6]], [int(ts[-1]) + 90_000_000])
     assert_tables(res, "proc-time x2")
+
+
+@pytest.mark.parametrize("key_type", ["int", "string"])
+def test_sharded_aggregation_checkpoint(key_type):
+    """sh_shard_snapshot of a key-sharded aggregation carries each owner's root window, roll-up
+    executors and tables: G owners snapshotted between two global pushes and restored into fresh
+    owners (a truncated blob refused first, leaving the owner as it was) end with the oracle's tables."""
+    import torch
+    from siddhi_amd.shard import LocalShards, canonical_table
+    dev = torch.device("cuda", 0)
+    world = 3
+    schema = abi.Schema.parse(f"k {key_type}, v double, ts long")
+    ts, cols = synth.keyed_stream(1_700_000_000_000 - 15_000, 180_000, 0xC4, 2_000, 5)
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                               group_by=["k"], ts="ts", durations=("sec", "hour"), key_capacity=2_000)
+    pushes = split(ts, cols, [70_000, 50_000, 60_000])
+    fr = [(g + 1) / world for g in range(world - 1)]
+    ls = LocalShards(spec, world)
+    o = OracleAggregation(spec)
+    for i, (t, c) in enumerate(pushes):
+        if i == 2:
+            blobs, seq = ls.snapshot(), ls.seq
+            with pytest.raises(Exception, match="truncated|does not match|restore"):
+                ls.shards[0].restore(blobs[0][:len(blobs[0]) - 7])
+            ls.close()
+            ls = LocalShards(spec, world)
+            ls.restore(blobs, seq)
+        ls.push(cut_slices(t, c, world, fr, 1, dev), 1, dev)
+        o.push(abi.HostBatch(spec.schema, t, c, 1))
+    end = int(ts[-1]) + 3 * 3_600_000
+    ls.advance_time(end)
+    o.advance_time(end)
+    res = {d: (ls.tables(d), canonical_table(abi.out_arrays(o.table_raw(d))))
+           for d in range(abi.DUR_SECONDS, abi.DUR_HOURS + 1)}
+    ls.close()
+    o.close()
+    assert assert_tables(res, f"checkpointed C4 x{world} {key_type}") > 2_000
