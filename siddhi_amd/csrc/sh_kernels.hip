@@ -545,12 +545,14 @@ __device__ __forceinline__ u64 agg_out(const AggPlan& ap, int a, u32 c, u64 fv) 
 // one row record (see above) with 16-byte stores
 template <int F = SH_MAX_AGGS>
 __device__ __forceinline__ void write_row(const AggPlan& ap, u64* row, int RW, u32 pos, u32 c, u32 first, u32 last,
-                                          const u64 (&f)[F], const EvSrc& es) {
+                                          const u64 (&f)[F], const EvSrc& es, bool have_last = false,
+                                          i64 last_ts = 0, i64 last_seq = 0) {
     u64 w[4 + SH_MAX_AGGS];
     w[0] = (u64)pos | ((u64)c << 32);
     w[1] = (u64)first | ((u64)last << 32);
-    w[2] = (u64)ev_ts(es, last);
-    w[3] = (u64)ev_seq(es, last);
+    // the last event's timestamp and stream index (prefetched by the caller when it could)
+    w[2] = (u64)(have_last ? last_ts : ev_ts(es, last));
+    w[3] = (u64)(have_last ? last_seq : ev_seq(es, last));
 #pragma unroll
     for (int a = 0; a < SH_MAX_AGGS; a++) {
         u64 fv = f[0];
@@ -700,6 +702,8 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     const u32 seg_lo = PACK ? (u32)segs[seg].lo : 0u;
     SH_STAMP(0, 0);
     u32 cnt0 = 0, fst0 = 0, lst0 = 0, cnt1 = 0, fst1 = 0, lst1 = 0;
+    i64 pf_ts = 0, pf_seq = 0;
+    bool pf = false;
     u64 f0[F], f1[F];
 #pragma unroll
     for (int j = 0; j < F; j++) { f0[j] = 0; f1[j] = 0; }
@@ -795,6 +799,15 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
             }
         }
         SH_STAMP(0, 4);
+        // the unit's last chunk: the owner's last event is its list's last entry (one key per owner
+        // when K == 1), so the random reads of that event's timestamp and stream index for the row
+        // are issued now and complete while the list is folded
+        if (K == 1 && c0 + CH >= hi && tot) {
+            const u32 el = st_idx[start + tot - 1];
+            pf_ts = ev_ts(es, el);
+            pf_seq = ev_seq(es, el);
+            pf = true;
+        }
         // then folds it; the next record's LDS loads are issued before the current one is folded, so
         // their latency overlaps the fold
         u32 e_nx = 0;
@@ -847,7 +860,9 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         // then stored with whole-line writes instead of each thread's strided 16-byte pieces
         u64* stg = &st_v[0][0];
         __syncthreads();
-        if (cnt0) write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es);
+        if (cnt0)
+            write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es, pf, pf_ts,
+                         pf_seq);
         if (cnt0) mark_first(first_bits, fst0);
         __syncthreads();
         const int n2 = (int)tot * RW / 2;
@@ -858,7 +873,8 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
         return;
     }
     if (cnt0) {
-        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es);
+        write_row<F>(ap, rows + (size_t)r * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es, pf, pf_ts,
+                     pf_seq);
         mark_first(first_bits, fst0);
         r++;
     }
@@ -1500,9 +1516,11 @@ void launch_part_off(hipStream_t s, const i64* counts, int nblk, int P, i64* par
 // over coalesced rows: per block of kColT tiles the per-partition sums, per partition the exclusive
 // scan over the blocks (+ its total), the scan of the totals over the partitions, then the rows.
 constexpr int kColT = 16;
-__global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c, int nblk, int P, i64* bsum) {
+__global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c, int nblk, int P, i64* bsum,
+                                                      u32* ticket) {
     const int b = blockIdx.y;
     const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (b == 0 && p == 0) *ticket = 0;  // k_col_blocks' completion count
     if (p >= P) return;
     const int t0 = b * kColT, t1 = min(nblk, t0 + kColT);
     i64 acc = 0;
@@ -1510,9 +1528,11 @@ __global__ __launch_bounds__(kBlock) void k_col_reduce(const u32* __restrict__ c
     bsum[(i64)b * P + p] = acc;
 }
 
-// one workgroup per partition: the exclusive scan of its column of block sums, kBlock blocks at a
-// time (a thread per column walking every block serialised nb dependent loads: 63 us at C2 size)
-__global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P, i64* total) {
+// One workgroup per partition: the exclusive scan of its column of block sums, kBlock blocks at a
+// time (a thread per column walking every block serialised nb dependent loads: 63 us at C2 size).
+// The last workgroup to finish also turns the partitions' totals into their bases (an exclusive scan
+// over P), so no separate copy + scan launches.
+__global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P, i64* total, i64* base, u32* ticket) {
     const int p = blockIdx.x;
     i64 run = 0;
     for (int b0 = 0; b0 < nb; b0 += kBlock) {
@@ -1523,7 +1543,24 @@ __global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P,
         if (b < nb) bsum[(i64)b * P + p] = run + pre;
         run += tot;
     }
-    if (threadIdx.x == 0) total[p] = run;
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        total[p] = run;
+        __threadfence();
+        last = atomicAdd(ticket, 1u) == (u32)(P - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    i64 carry = 0;
+    for (int q0 = 0; q0 < P; q0 += kBlock) {
+        const int q = q0 + threadIdx.x;
+        const i64 x = q < P ? __atomic_load_n(&total[q], __ATOMIC_RELAXED) : 0;
+        i64 tot;
+        const i64 pre = block_excl_scan(x, SumOp(), 0, &tot);
+        if (q < P) base[q] = carry + pre;
+        carry += tot;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_col_apply(u32* c, int nblk, int P, const i64* __restrict__ bpre,
@@ -1542,20 +1579,20 @@ __global__ __launch_bounds__(kBlock) void k_col_apply(u32* c, int nblk, int P, c
 }
 
 size_t ms_offsets_tmp_bytes(int nblk, int P) {
-    const size_t nb = (size_t)(nblk + kColT - 1) / kColT;
+    const size_t nb = (size_t)(std::max(nblk, 1) + kColT - 1) / kColT;
     return (nb * P + 2 * (size_t)P + 16) * 8;
 }
 
 void launch_ms_offsets(hipStream_t s, u32* counts, int nblk, int P, i64* tmp) {
-    const int nb = (nblk + kColT - 1) / kColT;
+    const int nb = (std::max(nblk, 1) + kColT - 1) / kColT;
     i64* bsum = tmp;
     i64* total = tmp + (size_t)nb * P;
     i64* base = total + P;
+    u32* ticket = (u32*)(base + P);
     const dim3 g((P + kBlock - 1) / kBlock, nb);
-    if (nblk > 0) hipLaunchKernelGGL(k_col_reduce, g, dim3(kBlock), 0, s, counts, nblk, P, bsum);
-    hipLaunchKernelGGL(k_col_blocks, dim3(P), dim3(kBlock), 0, s, bsum, nb, P, total);
-    (void)hipMemcpyAsync(base, total, (size_t)P * 8, hipMemcpyDeviceToDevice, s);
-    launch_scan_sum(s, base, P);
+    // (nblk == 0: the reduce pass still runs — zero block sums over no tiles — and zeroes the ticket)
+    hipLaunchKernelGGL(k_col_reduce, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, ticket);
+    hipLaunchKernelGGL(k_col_blocks, dim3(P), dim3(kBlock), 0, s, bsum, nb, P, total, base, ticket);
     if (nblk > 0) hipLaunchKernelGGL(k_col_apply, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, base, total);
     else hipLaunchKernelGGL(k_col_apply, dim3((P + kBlock - 1) / kBlock, 1), dim3(kBlock), 0, s, counts, nblk, P, bsum,
                             base, total);
