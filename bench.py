@@ -50,8 +50,11 @@ def parse():
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
     ap.add_argument("--key-type", choices=["string", "int"], default="string",
                     help="k as a dictionary-encoded string (ids are dense key slots) or as an int (hashed)")
-    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "c5", "ext"], default="c2",
-                    help="c2 = the headline (BASELINE configs[1]); c1/c3/c4/ext = secondary single-GPU lines")
+    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "c5", "ext", "c2all", "c2cur", "c3all"],
+                    default="c2",
+                    help="c2 = the headline (BASELINE configs[1]); c1/c3/c4/ext = secondary single-GPU lines; "
+                         "c2all / c3all = C2 / C3 with `insert all events` (expired rows too), c2cur = C2 with "
+                         "timeBatch(1 sec, true) (stream.current.event)")
     ap.add_argument("--host", action="store_true",
                     help="C2 from pinned host batches: double-buffered sh_stage / sh_push_staged, rows copied back "
                          "(PCIe-inclusive rate, H2D GB/s, per-call latency); never the headline value")
@@ -154,6 +157,12 @@ SECONDARY = {
     "c4": ("C4 define aggregation sum/avg/count/min/max group by k aggregate by ts every sec...day; one GPU's share "
            "of C4 on 8 GPUs: 125k of the 1M keys, 1.25M of the 10M events per event-time second", 25.2),
     "ext": ("externalTimeBatch(et, 1 sec) count/min/max/avg group by k, 100k keys, per-event sends", 32.4),
+    # output modes on the C2 / C3 streams (algorithmic bytes: the input plus the extra rows written)
+    "c2all": ("C2 with `insert all events`: every flush also re-emits the previous batch's keys as EXPIRED rows "
+              "(count 0, other aggregators null)", 28.8),
+    "c2cur": ("C2 on timeBatch(1 sec, true) (stream.current.event): a row per passing event with its key's running "
+              "aggregates since the batch reset", 64.0),
+    "c3all": ("C3 with `insert all events`: every expired event re-stamped and emitted before the current one", 168.0),
     # every event is read (20 B); only the partition that armed the shared timer is aggregated (R12)
     "c5": ("C5 partition with (k of S) begin from S#window.timeBatch(1 sec) select k, sum(v), count() group by k; "
            "10M Zipf(1.1) keys, 1M events per event-time second per GPU, per-event sends", 20.0),
@@ -208,6 +217,19 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
                                  key_capacity=10_000 * world)
             gen = lambda i: synth.torch_keyed_stream((i * world + rank) * B, B, 0xC3, 10_000 * world, 1000 * world,
                                                      dev)[1]
+        elif args.workload == "c3all":
+            schema = abi.Schema.parse("k string, v double, ts long")
+            spec = abi.QuerySpec(schema, "time", 10_000, group_by=["k"],
+                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")],
+                                 key_capacity=10_000, output="all")
+            gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC3, 10_000, 1000, dev)[1]
+        elif args.workload in ("c2all", "c2cur"):
+            schema = abi.Schema.parse("k string, v double, ts long")
+            spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
+                                 aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=100_000,
+                                 output="all" if args.workload == "c2all" else "current",
+                                 stream_current=args.workload == "c2cur")
+            gen = lambda i: synth.torch_keyed_stream(i * B, B, 0xC2, 100_000, 1000, dev)[1]
         else:
             schema = abi.Schema.parse("k string, v double, ts long")
             spec = abi.QuerySpec(schema, "externalTimeBatch", 1000, group_by=["k"], ts_attr="ts",
@@ -249,7 +271,7 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
             st = q.stats()
             # C5's work is the scans over every event (R12 leaves one partition to aggregate); C4's the
             # root window and every roll-up level
-            kern_ms += st.push_ms if args.workload in ("c4", "c5") else st.main_kernel_ms
+            kern_ms += st.push_ms if args.workload in ("c4", "c5", "c2all", "c2cur", "c3all") else st.main_kernel_ms
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -266,7 +288,7 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     roof = None
     if kern_ms > 0:
         ach = bpe * B * args.steps / (kern_ms / 1e3) / 1e9
-        kname = ("whole device pipeline of the push" if args.workload == "c5" else
+        kname = ("whole device pipeline of the push" if args.workload in ("c5", "c2all", "c2cur", "c3all") else
                  "whole device pipeline of the push (root window + sec..day roll-up levels)" if args.workload == "c4"
                  else "main (aggregate / sliding)")
         roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,
