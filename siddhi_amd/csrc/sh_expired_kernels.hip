@@ -65,23 +65,37 @@ __global__ __launch_bounds__(kBlock) void k_x_probe(const XItem* items, const i6
                                                     const i64* s_keys, i64 S, int nk, const u32* trow, const u64* tkey,
                                                     int* match, u32* keep, u32* item_matched) {
     const i64 g = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (g >= total) return;
-    const int i = x_find(cum, n_items + 1, g);
-    const XItem it = items[i];
-    const i64 r = it.p_lo + (g - cum[i]);
-    const u64 key = x_packed_key(s_keys, S, nk, r);
-    const u32 mask = (u32)it.tab_size - 1;
-    u32 h = (u32)mix64(key) & mask;
-    int m = -1;
-    for (;;) {
-        const u32 t = trow[it.tab_off + h];
-        if (t == kXEmpty) break;
-        if (tkey[it.tab_off + h] == key) { m = (int)t; break; }
-        h = (h + 1) & mask;
+    const bool valid = g < total;
+    int i = 0;
+    bool mt = false;
+    if (valid) {
+        i = x_find(cum, n_items + 1, g);
+        const XItem it = items[i];
+        const i64 r = it.p_lo + (g - cum[i]);
+        const u64 key = x_packed_key(s_keys, S, nk, r);
+        const u32 mask = (u32)it.tab_size - 1;
+        u32 h = (u32)mix64(key) & mask;
+        int m = -1;
+        for (;;) {
+            const u32 t = trow[it.tab_off + h];
+            if (t == kXEmpty) break;
+            if (tkey[it.tab_off + h] == key) { m = (int)t; break; }
+            h = (h + 1) & mask;
+        }
+        match[r] = m;
+        if (m >= 0) {
+            keep[m] = 0;
+            mt = true;
+        }
     }
-    match[r] = m;
-    if (m >= 0) {
-        keep[m] = 0;
+    // the matched count per flush: one atomic per wave when the wave's rows belong to one flush (the
+    // usual case: a flush has ~100k rows) — a per-row atomic on a few counters serialised at the L2
+    const int i0 = __shfl(i, 0, 64);  // lane 0 holds the wave's smallest g: valid if any lane is
+    const u64 same = __ballot(!valid || i == i0);
+    if (same == ~0ull) {
+        const u64 b = __ballot(mt);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(&item_matched[i0], (u32)__popcll(b));
+    } else if (mt) {
         atomicAdd(&item_matched[i], 1u);
     }
 }

@@ -266,6 +266,7 @@ struct sh_query {
     // set during a zero-copy staged push: the host batch, staged on the compute stream if the push
     // leaves the small-push path (sh_ingest.cpp)
     const sh_batch* zc_host = nullptr;
+    std::vector<int64_t> sc_sl_host;  // stream.current: the sends' clocks (host scratch, kept)
     // an aggregation root whose key table may switch to band mode (sh_aggregation.cpp band_reserve)
     bool band_keys = false;
     uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;

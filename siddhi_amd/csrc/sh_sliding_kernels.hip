@@ -1556,8 +1556,9 @@ __global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, 
 // the expiry prefix (the heads with PM + T <= the record's clock form a prefix, PM and the clock both
 // being non-decreasing along a key's events — one binary search per lane over the staged heads), the
 // count, the row position and the row stores. Only the Java-order double sum and the min / max deques
-// (MinAttributeAggregatorExecutor's LinkedList, removeFirstOccurrence included) run sequentially, in
-// lane 0, over values staged in LDS. With a wave per key a SIMD holds several keys' waves, whose
+// (MinAttributeAggregatorExecutor's LinkedList, removeFirstOccurrence included) run sequentially, by
+// the whole wave in lockstep on wave-uniform state, reading the records' values and expiry points from
+// the lanes' registers (readlane). With a wave per key a SIMD holds several keys' waves, whose
 // sequential parts interleave (the lane-per-key kernel left most SIMDs without a wave: ~0.6 per SIMD at
 // C3's 10k keys). TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
 constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)

@@ -687,7 +687,10 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     RCHK(q->sc_h.reserve((size_t)n_sends * 8 + 64));
     HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    std::vector<int64_t> sl(n_sends);
+    // (host scratch kept by the query: a fresh 8-byte-per-send vector per push faulted in its pages —
+    // hundreds of MB per C2-sized push)
+    std::vector<int64_t>& sl = q->sc_sl_host;
+    sl.resize((size_t)n_sends);
     {
         const int64_t* hs = q->sc_h.as<int64_t>();
         bool cv = cv0;
@@ -786,20 +789,23 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     }
     HIPCHK(hipGetLastError());
     // every row's chunk and send
-    std::vector<int64_t> och(T), osd(T);
+    const int64_t* och = nullptr;
+    const int64_t* osd = nullptr;
     if (T) {
         RCHK(q->sc_ho.reserve((size_t)2 * T * 8 + 64));
         int64_t* hs = q->sc_ho.as<int64_t>();
         HIPCHK(hipMemcpyAsync(hs, q->sc_ochunk.p, (size_t)T * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(hs + T, q->sc_osend.p, (size_t)T * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        std::memcpy(och.data(), hs, (size_t)T * 8);
-        std::memcpy(osd.data(), hs + T, (size_t)T * 8);
+        och = hs;  // read in place from the pinned landing area
+        osd = hs + T;
     }
     PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
     PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
     fo.assign(1, 0);
     fc.clear();
+    fo.reserve((size_t)T + 1);  // (one pinned allocation, not a doubling series)
+    fc.reserve((size_t)T);
     for (int64_t i = 0; i < T; i++) {
         if (i + 1 == T || och[i + 1] != och[i]) {
             fo.push_back(i + 1);

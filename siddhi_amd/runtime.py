@@ -109,15 +109,24 @@ class GpuQuery:
     def push(self, batch: abi.HostBatch):
         return abi.decode_out(self.push_raw(batch))
 
-    def push_device(self, n: int, ts_ptr: int, col_ptrs: List[int], send_size: int = 0):
-        """Device-resident batch (HBM pointers, e.g. torch tensors' data_ptr()). Returns the sh_out
-        pointer: flush metadata on the host, row arrays in device memory."""
+    @staticmethod
+    def device_batch(n: int, ts_ptr: int, col_ptrs: List[int], send_size: int = 0) -> abi.Batch:
+        """An sh_batch descriptor of device-resident columns, built once and pushed any number of times
+        (what a host shim keeps per buffer instead of rebuilding it per call)."""
         b = abi.Batch()
         b.n = n
         b.send_size = send_size
         b.ts = ts_ptr
         for i, p in enumerate(col_ptrs):
             b.cols[i] = p
+        return b
+
+    def push_device(self, n: int, ts_ptr: int, col_ptrs: List[int], send_size: int = 0):
+        """Device-resident batch (HBM pointers, e.g. torch tensors' data_ptr()). Returns the sh_out
+        pointer: flush metadata on the host, row arrays in device memory."""
+        return self.push_device_batch(self.device_batch(n, ts_ptr, col_ptrs, send_size))
+
+    def push_device_batch(self, b: abi.Batch):
         out = C.POINTER(abi.Out)()
         _check(lib().sh_push_device(self.h, C.byref(b), C.byref(out)))
         return out
