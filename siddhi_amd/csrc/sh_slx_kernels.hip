@@ -263,14 +263,12 @@ void launch_slx_append(hipStream_t s, const i64* pm, const u32* raw, i64 M, i64 
 // its arrival whose clock reaches PM + T: an event point i (record i, clock rclk[i]; points of the
 // push's records start at local index max(0, u - W0 + 1)) or a firing call f (fK[f] records before
 // it). The timer of call f precedes event point fK[f]. Operation index = u + records before the point.
-__global__ __launch_bounds__(kBlock) void k_slx_expiry(const i64* __restrict__ upm, i64 n_u, i64 W0, i64 M,
-                                                      const i64* __restrict__ rclk, const i64* __restrict__ rsclk,
-                                                      const u32* __restrict__ raw, i64 send_size,
-                                                      const i64* __restrict__ fK, const i64* __restrict__ fC,
-                                                      const i64* __restrict__ fS, i64 nF, i64 T, u64* xop, i64* xch,
-                                                      i64* xts, i64* xclk, unsigned long long* n_exp) {
-    const i64 u = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (u >= n_u) return;
+// one event's expiry point (see above); true when it has one
+__device__ __forceinline__ bool slx_expiry_one(i64 u, const i64* __restrict__ upm, i64 W0, i64 M,
+                                               const i64* __restrict__ rclk, const i64* __restrict__ rsclk,
+                                               const u32* __restrict__ raw, i64 send_size, const i64* __restrict__ fK,
+                                               const i64* __restrict__ fC, const i64* __restrict__ fS, i64 nF, i64 T,
+                                               u64* xop, i64* xch, i64* xts, i64* xclk) {
     const i64 th = sat_add(upm[u], T);
     const i64 lo_i = max((i64)0, u - W0 + 1);
     const i64 ie = lb_ge(rclk, lo_i, M, th);
@@ -288,7 +286,22 @@ __global__ __launch_bounds__(kBlock) void k_slx_expiry(const i64* __restrict__ u
         xclk[u] = rsclk ? rsclk[ie] : rclk[ie];
     }
     xop[u] = op;
-    if (op != kNoOp) atomicMax(n_exp, (unsigned long long)(u + 1));
+    return op != kNoOp;
+}
+
+__global__ __launch_bounds__(kBlock) void k_slx_expiry(const i64* __restrict__ upm, i64 n_u, i64 W0, i64 M,
+                                                      const i64* __restrict__ rclk, const i64* __restrict__ rsclk,
+                                                      const u32* __restrict__ raw, i64 send_size,
+                                                      const i64* __restrict__ fK, const i64* __restrict__ fC,
+                                                      const i64* __restrict__ fS, i64 nF, i64 T, u64* xop, i64* xch,
+                                                      i64* xts, i64* xclk, unsigned long long* n_exp) {
+    const i64 u = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const bool has = u < n_u && slx_expiry_one(u, upm, W0, M, rclk, rsclk, raw, send_size, fK, fC, fS, nF, T, xop,
+                                               xch, xts, xclk);
+    // n_exp = 1 + the last event with an expiry point: one atomic per wave, from its highest such lane
+    // (u grows with the lane) — one atomic per event on one address serialised at the L2
+    const u64 b = __ballot(has);
+    if (b && (int)(threadIdx.x & 63) == 63 - (int)__clzll(b)) atomicMax(n_exp, (unsigned long long)(u + 1));
 }
 
 void launch_slx_expiry(hipStream_t s, const i64* upm, i64 n_u, i64 W0, i64 M, const i64* rclk, const i64* rsclk,
