@@ -885,160 +885,6 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     SH_STAMP(0, 6);
 }
 
-// k_aggregate_own with the record values left in global memory (GV): the chunk's records are ranked
-// into owner lists of (event index, chunk position) only — the values are read back by their owner,
-// eight loads issued together, from the record array the wave just read (L2-resident) — so the
-// workgroup needs 32 KB of LDS instead of 67 KB and a CU holds four of them instead of two. One key
-// per thread (K = 1), packed records. The 32 KB region holds the lists while the chunks are folded
-// and then stages the unit's rows for whole-line stores.
-template <int V, int F, u32 SIG>
-__global__ __launch_bounds__(kOwnT, 4) void k_aggregate_gv(const i64* __restrict__ seg_off, int P, int logP,
-                                                          AggPlan ap, u64* rows, int RW, u32* unit_rows,
-                                                          u32* first_bits, const Segment* __restrict__ segs,
-                                                          const u32* __restrict__ rec_idx,
-                                                          const u64* __restrict__ rec_vals, i64 rec_cap, EvSrc es) {
-    constexpr int R = 8;
-    constexpr int W = kOwnT / 64;
-    constexpr int PW = 64 * R;
-    constexpr int CH = kOwnT * R;
-    // [st_idx u32 CH | st_pos u16 CH | wcnt u16 W x kOwnT] = 32 KB, then the rows' staging area
-    __shared__ __attribute__((aligned(16))) unsigned char big[CH * 4 + CH * 2 + W * kOwnT * 2];
-    static_assert(sizeof(big) >= (size_t)kOwnT * 8 * 8, "row staging needs kOwnT rows of up to 8 words");
-    u32* st_idx = (u32*)big;
-    unsigned short* st_pos = (unsigned short*)(big + CH * 4);
-    unsigned short* wcnt = (unsigned short*)(big + CH * 6);
-    u32* wcnt32 = (u32*)wcnt;
-    __shared__ u32 bstart[kOwnT];
-    __shared__ u32 lstart[CH / 32];
-    constexpr u32 kNone = 0xFFFFFFFFu;
-    const int seg = blockIdx.x / P;
-    const int p = blockIdx.x - seg * P;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const i64 lo = seg_off[(i64)seg * P + p], hi = seg_off[(i64)(seg + 1) * P + p];
-    const u32 seg_lo = (u32)segs[seg].lo;
-    u32 cnt0 = 0, fst0 = 0, lst0 = 0;
-    i64 pf_ts = 0, pf_seq = 0;
-    bool pf = false;
-    u64 f0[F];
-#pragma unroll
-    for (int j = 0; j < F; j++) f0[j] = 0;
-    for (i64 c0 = lo; c0 < hi; c0 += CH) {
-        const int n = (int)min((i64)CH, hi - c0);
-        u32 li[R], ix[R];
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            const int r = w * PW + j * 64 + lane;
-            const bool ok = r < n;
-            const u32 wd = ok ? rec_idx[c0 + r] : 0u;
-            li[j] = ok ? (wd >> kPackIdxBits) : kNone;
-            ix[j] = seg_lo + (((wd & kPackIdxMask) - seg_lo) & kPackIdxMask);
-        }
-        for (int i = t; i < W * kOwnT / 2; i += kOwnT) wcnt32[i] = 0;
-        for (int i = t; i < CH / 32; i += kOwnT) lstart[i] = 0;
-        __syncthreads();
-        // rank among the wave's records of the same owner: 16-bit running counts, two per word
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            if (li[j] == kNone) continue;
-            const u32 c = (u32)(w * kOwnT) + (li[j] & (kOwnT - 1));
-            const u32 sh = (c & 1) * 16;
-            const u32 rk = (atomicAdd(&wcnt32[c >> 1], 1u << sh) >> sh) & 0xFFFFu;
-            li[j] = (li[j] & (kOwnT - 1)) | (rk << 10);
-        }
-        __syncthreads();
-        u32 tot = 0;
-#pragma unroll
-        for (int x = 0; x < W; x++) {
-            const u32 c = wcnt[x * kOwnT + t];
-            wcnt[x * kOwnT + t] = (unsigned short)tot;
-            tot += c;
-        }
-        i64 all;
-        const u32 start = (u32)block_excl_scan_any((i64)tot, &all);
-        bstart[t] = start;
-        if (tot) atomicOr(&lstart[start >> 5], 1u << (start & 31));
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-            if (li[j] == kNone) continue;
-            const u32 b = li[j] & (kOwnT - 1);
-            const u32 d = bstart[b] + wcnt[w * kOwnT + b] + (li[j] >> 10);
-            st_idx[d] = ix[j];
-            st_pos[d] = (unsigned short)(w * PW + j * 64 + lane);
-        }
-        __syncthreads();
-        // the owner's list in event order (repaired if lanes of one round got ranks out of lane order)
-        bool bad = false;
-        for (int d = t; d + 1 < n; d += kOwnT)
-            bad |= !((lstart[(d + 1) >> 5] >> ((d + 1) & 31)) & 1u) && st_idx[d + 1] < st_idx[d];
-        if (__syncthreads_or(bad) && tot > 1) {
-            u32 prev = st_idx[start];
-            for (u32 k = 1; k < tot; k++) {
-                const u32 e = st_idx[start + k];
-                if (e > prev) { prev = e; continue; }
-                const unsigned short mp = st_pos[start + k];
-                u32 m = k;
-                while (m > 0 && st_idx[start + m - 1] > e) {
-                    st_idx[start + m] = st_idx[start + m - 1];
-                    st_pos[start + m] = st_pos[start + m - 1];
-                    m--;
-                }
-                st_idx[start + m] = e;
-                st_pos[start + m] = mp;
-            }
-        }
-        if (c0 + CH >= hi && tot) {  // the unit's last chunk: the row's last-event reads, early
-            const u32 el = st_idx[start + tot - 1];
-            pf_ts = ev_ts(es, el);
-            pf_seq = ev_seq(es, el);
-            pf = true;
-        }
-        // fold the list: eight records' values requested together from the record array
-        for (u32 k0 = 0; k0 < tot; k0 += 8) {
-            u32 e8[8];
-            i64 v8[8][V];
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const bool ok = k0 + q < tot;
-                const u32 i = start + k0 + (ok ? q : 0);
-                e8[q] = st_idx[i];
-                const u32 r = st_pos[i];
-#pragma unroll
-                for (int x = 0; x < V; x++)
-                    v8[q][x] = (ok && x < ap.n_vcols) ? (i64)rec_vals[(size_t)x * rec_cap + c0 + r] : 0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                if (k0 + q >= tot) break;
-                i64 vv[V];
-#pragma unroll
-                for (int x = 0; x < V; x++) vv[x] = v8[q][x];
-                fold_fields<V, F, SIG>(ap, f0, cnt0 == 0, vv);
-                if (cnt0 == 0) fst0 = e8[q];
-                lst0 = e8[q];
-                cnt0++;
-            }
-        }
-        __syncthreads();  // the lists are rebuilt by the next chunk
-    }
-    const int mine = cnt0 > 0;
-    i64 tot;
-    const i64 pre = block_excl_scan_any((i64)mine, &tot);
-    if (t == 0) unit_rows[blockIdx.x] = (u32)tot;
-    // the unit's rows staged in the list area, then stored as whole lines
-    u64* stg = (u64*)big;
-    if (cnt0) {
-        write_row<F>(ap, stg + (size_t)pre * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es, pf, pf_ts,
-                     pf_seq);
-        mark_first(first_bits, fst0);
-    }
-    __syncthreads();
-    const int n2 = (int)tot * RW / 2;
-    ulonglong2* dst = (ulonglong2*)(rows + (size_t)blockIdx.x * kOwnT * RW);
-    const ulonglong2* src = (const ulonglong2*)stg;
-    for (int i = t; i < n2; i += kOwnT) dst[i] = src[i];
-}
-
 int own_keys_per_thread(int NL) { return NL <= kOwnT ? 1 : 2; }
 
 int agg_unit_rows(int P, int NL, bool own) { return own ? own_keys_per_thread(NL) * kOwnT : NL; }
@@ -1075,11 +921,9 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       kSumMinMaxD = agg_sig3(FOP_ADD_D, FOP_MIN_D, FOP_MAX_D);  // aggregation base values
         const u32 sig = agg_sig(ap);
         // (R = 4 — half-size chunks, 3 workgroups per CU — measured 349 vs 287 us per C2 push)
-        static const bool gv = getenv("SH_FOLD_GV") != nullptr;  // A/B: values left in global memory
-        if (gv && pack && K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD && RW <= 8)
-            hipLaunchKernelGGL((k_aggregate_gv<1, 4, kMinMaxAvgD>), dim3(nseg * P), dim3(kOwnT), 0, s, seg_off, P, logP,
-                               ap, rows, RW, unit_rows, first_bits, segs, rec_idx, rec_vals, rec_cap, es);
-        else if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
+        // (values left in global memory and read back by their owner — 32 KB of LDS, four workgroups
+        // per CU — measured 334 vs 310 us)
+        if (K == 1 && ap.n_vcols <= 1 && sig == kMinMaxAvgD) SH_AGG_OWN(1, 1, 8, 4, kMinMaxAvgD);
         else if (K == 1 && ap.n_vcols <= 1 && sig == kSumD) SH_AGG_OWN(1, 1, 8, 2, kSumD);
         else if (K == 1 && ap.n_vcols <= 1 && sig == kSumI) SH_AGG_OWN(1, 1, 8, 2, kSumI);
         else if (K == 1 && ap.n_vcols == 2 && sig == kSumISumD) SH_AGG_OWN(2, 1, 4, 2, kSumISumD);
