@@ -131,9 +131,63 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
     }
 }
 
+// The common case of k_sl_records — no filter, one event per send, time(T) — with the tile's events
+// taken lane-strided (round i: events tile + i * kBlock + lane), so consecutive lanes write consecutive
+// records (whole lines; the thread-contiguous form stored 48-byte records 8 apart per lane, and PMC saw
+// 2.3x the record bytes written). Every event passes and ends its own send, so its clock and PM are the
+// running maximum of the timestamps (a block max-scan per round, carried across rounds).
+__global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict__ ts, ColSet cols, WinParams wp,
+                                                          KeyPlan kp, KeyTable kt, AggPlan ap,
+                                                          const i64* blk_pass_pre, const i64* blk_tl_pre,
+                                                          const i64* blk_pm_pre, i64 pm0, SlRecords rec,
+                                                          u32* slot_cnt, i64* send_clock) {
+    const i64 tile0 = (i64)blockIdx.x * kTile;
+    const i64 r0 = blk_pass_pre[blockIdx.x];
+    i64 carry_cm = blk_tl_pre[blockIdx.x];
+    i64 carry_pm = max(blk_pm_pre[blockIdx.x], pm0);
+    const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
+    for (int it = 0; it < kItems; it++) {
+        const i64 e = tile0 + (i64)it * kBlock + threadIdx.x;
+        const bool in = e < wp.N;
+        const i64 t = in ? ts[e] : INT64_MIN;
+        const u32 pos = in ? key_slot(kt, make_key(kp, cols, e)) : 0u;
+        const u64 v = in ? (u64)load_raw(cols, ap.vcol_src[0], e) : 0ull;
+        i64 tot;
+        const i64 incl = max(block_excl_scan(t, MaxOp(), INT64_MIN, &tot), t);
+        if (in) {
+            const i64 pmx = max(carry_pm, incl);
+            const i64 sclk = max(c0, max(carry_cm, incl));
+            const i64 r = r0 + (i64)it * kBlock + threadIdx.x;
+            if (send_clock) send_clock[r] = sclk;
+            rec.raw[r] = (u32)e;
+            rec.slot[r] = pos;
+            if (rec.aos) {
+                ulonglong2* o = (ulonglong2*)(rec.aos + (size_t)r * kSlAosWords);
+                o[0] = make_ulonglong2((u64)sclk, (u64)pmx);
+                o[1] = make_ulonglong2((u64)t, v);
+                o[2] = make_ulonglong2((u64)e, 0ull);
+            } else {
+                rec.clock[r] = sclk;
+                rec.pm[r] = pmx;
+                rec.ts[r] = t;
+                for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
+            }
+            atomicAdd(&slot_cnt[pos], 1u);
+        }
+        carry_pm = max(carry_pm, tot);
+        carry_cm = max(carry_cm, tot);
+    }
+}
+
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
                        i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock) {
+    if (filter_kind(f) == 0 && wp.send_size == 1 && wp.kind == SH_WIN_TIME && ap.n_vcols >= 1 &&
+        getenv("SH_SL_RECORDS_SEQ")) {
+        hipLaunchKernelGGL(k_sl_records_seq, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap, blk_pass_pre,
+                           blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
+        return;
+    }
     hipLaunchKernelGGL(k_sl_records, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, kp, kt, ap, blk_pass_pre,
                        blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
 }
