@@ -148,6 +148,24 @@ def measured_traffic(args, sliced):
     return main, push
 
 
+GOLDEN_DIGEST = "tests/golden/c2_bench_digest.json"
+
+
+def output_digest_check(args, arrays):
+    """SHA-256 of the first warm-up push's canonical output (siddhi_amd.digest; computed outside the timed
+    region) against the CPU restatement's digest of the same stream (tests/golden/make_c2_digest.py).
+    Only the default configuration has a golden digest."""
+    from siddhi_amd import digest
+    gold = json.load(open(os.path.join(ROOT, GOLDEN_DIGEST)))
+    cfg = gold["config"]
+    if (args.batch, args.keys, args.events_per_ms, args.send_size, args.key_type) != (
+            cfg["events_per_push"], cfg["keys"], cfg["events_per_ms"], cfg["send_size"], "string"):
+        return None
+    got = digest.output_digest(arrays)
+    return {"match": got == gold["push0"]["sha256"], "sha256": got, "rows": int(arrays["ts"].size),
+            "expected": gold["push0"]["sha256"], "source": GOLDEN_DIGEST + " (oracle/ on the same stream)"}
+
+
 # ---- secondary single-GPU workloads (BASELINE.json configs[0], [2], [3]; externalTimeBatch) ---------
 SECONDARY = {
     # name: (description, algorithmic bytes per event from SURVEY.md §8d)
@@ -473,8 +491,12 @@ def main():
         return None
 
     phases, timing = {}, False
+    digest_check = None
     for i in range(args.warmup):
-        push(i)
+        op = push(i)
+        if i == 0 and not sliced and world == 1 and op is not None:
+            torch.cuda.synchronize()
+            digest_check = output_digest_check(args, runtime.device_out_arrays(op))
     drain()
     torch.cuda.synchronize()
     timing = True
@@ -554,6 +576,9 @@ def main():
                                     "traffic_per_step": push_traffic,
                                     "traffic_source": TRAFFIC_SUMMARY if traffic else None}},
     }
+    if digest_check is not None:
+        result["output_sha256_match"] = digest_check["match"]
+        result["output_check"] = digest_check
     if sliced:
         # rank 0's wall time per step in each phase of the sharded push (summaries all-gather,
         # pack, record all-to-all over RCCL, owner pipeline) and its bytes sent per step

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 7
+#define SH_ABI_VERSION 8
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -247,6 +247,18 @@ int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
 #define SH_RATE_LAST 3
 #define SH_RATE_FIRST_TIME 4
 int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
+
+/* The text of dictionary ids [first_id, first_id + n) of string column `col`, as UTF-16 code units (what a
+ * java.lang.String holds): id first_id + i is units[offsets[i] .. offsets[i + 1]) (offsets has n + 1
+ * entries). May be called again to extend the range as the shim's dictionary grows; an id keeps its text.
+ * Needed where the reference's output depends on the string itself, not only on equality: the partition
+ * key of `partition with (k of S)` around a `time` window with expired / all-events output, whose
+ * Scheduler fires, of several partitions due at the same time, the first in java.util.HashMap<String, …>
+ * iteration order (String.hashCode, String.compareTo; Scheduler.java:71-104,363-366,
+ * PartitionStateHolder.java:36-83). A push that needs an id without text fails (SH_ERR_INVALID).
+ * Replaces nothing in the reference: the Java shim calls it when it assigns dictionary ids. */
+int sh_query_set_strings(sh_query* q, int32_t col, int64_t first_id, int64_t n, const uint16_t* units,
+                         const int64_t* offsets);
 
 /* Checkpoint of the query's state: State.snapshot()/restore() (core/util/snapshot/state/State.java:
  * 26-36) driven by SnapshotService.persist/restore (core/util/snapshot/SnapshotService.java:90-296)

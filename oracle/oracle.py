@@ -33,6 +33,7 @@ def lib():
         L.or_query_create.restype = C.c_void_p
         L.or_query_destroy.argtypes = [C.c_void_p]
         L.or_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+        L.or_query_set_strings.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
         L.or_push.argtypes = [C.c_void_p, P(abi.Batch), P(P(abi.Out))]
         L.or_advance_time.argtypes = [C.c_void_p, C.c_int64, P(P(abi.Out))]
         L.or_aggregation_create.argtypes = [P(abi.AggregationDesc)]
@@ -56,6 +57,12 @@ class OracleQuery:
         if not self.h:
             raise ValueError(lib().or_last_error().decode())
         if spec.rate and lib().or_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])):
+            raise ValueError(lib().or_last_error().decode())
+        for col, names in (spec.strings or {}).items():
+            self.set_strings(col, names)
+
+    def set_strings(self, col, names, first_id=0):
+        if abi.apply_strings(lib().or_query_set_strings, self.h, self.spec, col, list(names), first_id):
             raise ValueError(lib().or_last_error().decode())
 
     def push_raw(self, batch: abi.HostBatch):

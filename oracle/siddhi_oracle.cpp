@@ -15,6 +15,7 @@
 
 #include "../include/siddhi_hip.h"
 #include "oracle.h"
+#include "jhashmap.h"
 
 #include <algorithm>
 #include <array>
@@ -25,6 +26,8 @@
 #include <list>
 #include <map>
 #include <memory>
+#include <set>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -484,8 +487,11 @@ struct PartitionState {
     int64_t ext_end = -1, ext_start = 0, ext_last = 0;
     Chunk ext_current, ext_expired;
     bool ext_has_reset = false; OEvent ext_reset;
-    size_t index = 0;  // position in the scheduler's iteration order
     int64_t key = 0;
+    // the partition flow id: String.valueOf of the partition key (ValuePartitionExecutor.execute :34-40)
+    std::u16string flow_id;
+    bool front_indexed = false;  // (front due time, key) is in Query::fronts
+    int64_t indexed_front = 0;
     // the query's output rate limiter: one per partition instance (PartitionRuntime clones the query
     // with its OutputRateLimiter, PartitionRuntimeImpl)
     RateLimiter rl;
@@ -507,12 +513,45 @@ struct Query {
     int64_t next_emit_time = -1;
     int64_t seq_base = 0;  // stream index of the current push's first event
     std::unordered_map<int64_t, std::unique_ptr<PartitionState>> parts;  // partition flow id -> state
-    std::vector<int64_t> part_order;  // scheduler iteration order (insertion order)
-    // partitions whose notify queue is non-empty, by insertion index: Scheduler.onTimeChange only
-    // ever fires states with a due time (:75-87), so a scan over these equals the scan over all
-    std::map<size_t, int64_t> armed;
+    // Scheduler.stateHolder (PartitionSyncStateHolder -> PartitionStateHolder.states, a
+    // HashMap<String, …> keyed by the partition flow id, :36): the partitions whose notify queue is
+    // non-empty, in java.util.HashMap order (jhashmap.h); fronts = their due times, to skip calls
+    // with nothing due (onTimeChange then puts nothing into its TreeMultimap)
+    jhm::HashMap<int64_t> sched_states;
+    std::set<std::pair<int64_t, int64_t>> fronts;
+    // text of dictionary ids per string column (sh_query_set_strings), UTF-16 as Java holds it
+    std::unordered_map<int, std::vector<std::u16string>> strings;
+    std::unordered_map<int, std::vector<uint8_t>> has_string;
     OutBuf out;
     RateLimiter rate;
+
+    // the scheduler's tie rule decides output only for partitioned time windows with expired output
+    bool tie_rule_matters() const {
+        return d.partition_col >= 0 && d.window == SH_WIN_TIME && d.expired_on;
+    }
+
+    // String.valueOf(partition key): Integer/Long.toString, Boolean.toString, the string itself
+    std::u16string flow_id_of(int64_t key) const {
+        const int c = d.partition_col;
+        if (c < 0) return std::u16string();
+        switch (schema.types[c]) {
+            case SH_T_INT: case SH_T_LONG: return jhm::decimal(key);
+            case SH_T_BOOL: return key ? u"true" : u"false";
+            case SH_T_STRID: {
+                auto it = strings.find(c);
+                if (it != strings.end() && key >= 0 && key < (int64_t)it->second.size() && has_string.at(c)[(size_t)key])
+                    return it->second[(size_t)key];
+                break;
+            }
+            default: break;
+        }
+        if (tie_rule_matters())
+            throw std::runtime_error(schema.types[c] == SH_T_STRID
+                                         ? "partition key string id " + std::to_string(key) +
+                                               " has no text (sh_query_set_strings): the Scheduler's tie rule needs it"
+                                         : "float / double partition keys of time windows with expired output are not restated");
+        return jhm::decimal(key);  // order irrelevant to the output: any stable text
+    }
 
     PartitionState& part(int64_t key) {
         auto it = parts.find(key);
@@ -520,18 +559,25 @@ struct Query {
         auto ps = std::unique_ptr<PartitionState>(new PartitionState());
         ps->agg_states.resize(aggs.size());
         if (d.window == SH_WIN_EXT_TIME_BATCH && d.has_start_time == 1) ps->ext_start = d.start_time;
-        ps->index = part_order.size();
         ps->key = key;
+        ps->flow_id = flow_id_of(key);
         PartitionState& r = *ps;
         parts.emplace(key, std::move(ps));
-        part_order.push_back(key);
         return r;
     }
 
-    // Scheduler.notifyAt (core/util/Scheduler.java:107-121)
+    // Scheduler.notifyAt (core/util/Scheduler.java:113-127): stateHolder.getState() is
+    // states.computeIfAbsent(partitionFlowId, …) (PartitionStateHolder.java:46), then the time joins
+    // the state's queue; returnState keeps it (the queue is not empty)
     void notify_at(PartitionState& ps, int64_t t) {
+        sched_states.compute_if_absent(ps.flow_id, ps.key);
         ps.notify_queue.push_back(t);
-        armed.emplace(ps.index, ps.key);
+        index_front(ps);
+    }
+    void index_front(PartitionState& ps) {
+        if (ps.front_indexed) fronts.erase({ps.indexed_front, ps.key});
+        ps.front_indexed = !ps.notify_queue.empty();
+        if (ps.front_indexed) fronts.insert({ps.indexed_front = ps.notify_queue.front(), ps.key});
     }
 
     // ---- selector: QuerySelector.processInBatchGroupBy (core/query/selector/QuerySelector.java:315-374)
@@ -820,13 +866,17 @@ struct Query {
     }
 
     // Scheduler.onTimeChange (core/util/Scheduler.java:71-104) + sendTimerEvents (:171-209).
-    // TreeMultimap<Long, SchedulerState> with compareTo()==0: one state per distinct due time.
+    // getAllStates() is walked in HashMap order and every due state is put into a
+    // TreeMultimap<Long, SchedulerState> whose values compare equal (:363-366): per distinct due time
+    // only the first state put is kept. returnAllStates (PartitionStateHolder.java:132-161) then
+    // removes, in iteration order, the states whose queue is empty (canDestroy, :343-346).
     void on_time_change() {
-        std::map<int64_t, int64_t> sorted;  // due time -> partition key (first inserted wins)
-        for (auto& ak : armed) {
-            PartitionState& ps = *parts[ak.second];
-            if (!ps.notify_queue.empty() && ps.notify_queue.front() <= clock) sorted.emplace(ps.notify_queue.front(), ak.second);
-        }
+        if (fronts.empty() || fronts.begin()->first > clock) return;
+        std::map<int64_t, int64_t> sorted;  // due time -> partition key (first put wins)
+        sched_states.for_each([&](const std::u16string&, int64_t key) {
+            PartitionState& ps = *parts[key];
+            if (!ps.notify_queue.empty() && ps.notify_queue.front() <= clock) sorted.emplace(ps.notify_queue.front(), key);
+        });
         for (auto& kv : sorted) {
             PartitionState& ps = *parts[kv.second];
             while (!ps.notify_queue.empty() && ps.notify_queue.front() - clock <= 0) {
@@ -836,8 +886,13 @@ struct Query {
                 Chunk c{timer};
                 window(ps, c);  // EntryValveProcessor -> window
             }
-            if (ps.notify_queue.empty()) armed.erase(ps.index);
+            index_front(ps);
         }
+        std::vector<std::u16string> gone;
+        sched_states.for_each([&](const std::u16string& k, int64_t key) {
+            if (parts[key]->notify_queue.empty()) gone.push_back(k);
+        });
+        for (auto& k : gone) sched_states.remove(k);
     }
 
     void set_clock(int64_t ts) {
@@ -1296,6 +1351,25 @@ void* or_query_create(const sh_query_desc* desc) {
 
 void or_query_destroy(void* h) { delete (Query*)h; }
 
+int or_query_set_strings(void* h, int32_t col, int64_t first_id, int64_t n, const uint16_t* units,
+                         const int64_t* offsets) {
+    Query* q = (Query*)h;
+    if (col < 0 || col >= q->d.n_cols || q->d.col_types[col] != SH_T_STRID || first_id < 0 || n < 0 ||
+        (n > 0 && (!units || !offsets))) {
+        g_err = "sh_query_set_strings: bad column or range";
+        return SH_ERR_INVALID;
+    }
+    auto& v = q->strings[col];
+    auto& has = q->has_string[col];
+    if ((int64_t)v.size() < first_id + n) { v.resize((size_t)(first_id + n)); has.resize((size_t)(first_id + n), 0); }
+    for (int64_t i = 0; i < n; i++) {
+        if (offsets[i + 1] < offsets[i]) { g_err = "sh_query_set_strings: offsets decrease"; return SH_ERR_INVALID; }
+        v[(size_t)(first_id + i)].assign((const char16_t*)units + offsets[i], (const char16_t*)units + offsets[i + 1]);
+        has[(size_t)(first_id + i)] = 1;
+    }
+    return SH_OK;
+}
+
 int or_query_set_output_rate(void* h, int32_t kind, int64_t n) {
     Query* q = (Query*)h;
     if (kind < SH_RATE_NONE || kind > SH_RATE_FIRST_TIME || (kind != SH_RATE_NONE && n < (kind == SH_RATE_FIRST_TIME ? 0 : 1))) {
@@ -1314,7 +1388,12 @@ int or_push(void* h, const sh_batch* b, const sh_out** out) {
     Query* q = (Query*)h;
     q->out.clear();
     int64_t step = b->send_size > 0 ? b->send_size : b->n;
-    for (int64_t lo = 0; lo < b->n; lo += step) q->send(b, lo, std::min(b->n, lo + step));
+    try {
+        for (int64_t lo = 0; lo < b->n; lo += step) q->send(b, lo, std::min(b->n, lo + step));
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SH_ERR_INVALID;
+    }
     q->seq_base += b->n;
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
@@ -1323,7 +1402,12 @@ int or_push(void* h, const sh_batch* b, const sh_out** out) {
 int or_advance_time(void* h, int64_t now, const sh_out** out) {
     Query* q = (Query*)h;
     q->out.clear();
-    q->set_clock(now);
+    try {
+        q->set_clock(now);
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SH_ERR_INVALID;
+    }
     *out = q->out.view(q->d.n_group_by, (int)q->aggs.size(), q->vtypes);
     return SH_OK;
 }

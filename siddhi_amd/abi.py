@@ -172,6 +172,7 @@ class QuerySpec:
     key_capacity: int = 0
     rate: Optional[tuple] = None       # ('all'|'first'|'last', n): `output <kind> every n events`;
                                        # ('first_time', ms): `output first every <ms> milliseconds`
+    strings: Optional[dict] = None     # {string column: [text of id 0, 1, ...]} (sh_query_set_strings)
     ts_attr: Optional[str] = None      # externalTimeBatch timestamp attribute
     start_attr: Optional[str] = None   # externalTimeBatch start time from this attribute
     _keep: list = field(default_factory=list, repr=False)
@@ -390,6 +391,7 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
     lib.sh_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(Out))]
     lib.sh_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+    lib.sh_query_set_strings.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
     lib.sh_aggregation_snapshot.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, P(C.c_int64)]
     lib.sh_aggregation_restore.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
     lib.sh_alloc_pinned.argtypes = [C.c_int64, P(C.c_void_p)]
@@ -433,8 +435,24 @@ ABI_SYMBOLS = [
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
     "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate",
-    "sh_shard_snapshot", "sh_shard_restore",
+    "sh_shard_snapshot", "sh_shard_restore", "sh_query_set_strings",
 ]
+
+
+def encode_strings(names):
+    """UTF-16 code units + offsets (n + 1) of `names`: the sh_query_set_strings layout (a Java String's chars)."""
+    parts = [np.frombuffer(str(s).encode("utf-16-le"), dtype=np.uint16) for s in names]
+    offs = np.zeros(len(parts) + 1, dtype=np.int64)
+    if parts:
+        offs[1:] = np.cumsum([p.size for p in parts])
+    units = np.concatenate(parts) if parts and offs[-1] > 0 else np.zeros(1, dtype=np.uint16)
+    return np.ascontiguousarray(units), offs
+
+
+def apply_strings(fn, h, spec, col, names, first_id=0):
+    """fn = the library's set_strings entry point; registers `names` as ids first_id.. of column `col`."""
+    units, offs = encode_strings(names)
+    return fn(h, spec.schema.col(col), first_id, len(names), units.ctypes.data, offs.ctypes.data)
 
 # output rate limiter kinds (SH_RATE_*)
 RATE_KINDS = {"all": 1, "first": 2, "last": 3, "first_time": 4}

@@ -11,8 +11,9 @@
 //  * time: each run of consecutive same-partition events of a send (the receiver's chunk), and each
 //    TIMER call the Scheduler fires for the partition (Scheduler.onTimeChange :71-104). Which partition
 //    fires at which call is the Scheduler's own logic — notify times per partition, a TreeMultimap keyed
-//    by due time whose equal keys keep only the first-created partition's state — and runs here on the
-//    host over the device-computed notify registrations; the windows and aggregators stay on the GPU.
+//    by due time whose equal keys keep only the first state met while walking PartitionStateHolder.states,
+//    a java.util.HashMap<String, …> (sh_jmap.h) — and runs here on the host over the device-computed
+//    notify registrations; the windows and aggregators stay on the GPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,7 +50,7 @@ int plane_create(sh_query* q) {
     RCHK(fill(s->pl_last_ts, n * 8, 0x80));  // lastTimestamp = Long.MIN_VALUE (0x8080... < any real ts)
     RCHK(fill(s->pl_last_seq, n * 8, 0));
     RCHK(fill(s->pl_prev_seq, n * 8, 0xff));  // -1: no batch flushed yet
-    RCHK(fill(s->pl_first, n * 8, 0xff));     // creation order: none yet
+    RCHK(fill(s->pl_key, n * 8, 0));
     if (s->lane == 2 && !s->rg.p) RCHK(s->rg.reserve(n * s->rc * 8, false));
     return SH_OK;
 }
@@ -76,34 +77,85 @@ struct Firing {
     uint32_t slot;
 };
 
-// Scheduler.onTimeChange at one call (clock c): the armed partitions whose front notify time is due,
-// one per distinct due time (TreeMultimap<Long, SchedulerState> with compareTo() == 0 keeps the first
-// put, i.e. the first-created partition), each popping all of its due times (sendTimerEvents :171-209).
-static void sched_call(SlidingImpl* s, int64_t send, int64_t c, int64_t K, std::vector<Firing>& out) {
-    std::vector<std::tuple<int64_t, uint64_t, uint32_t>> win;
-    int64_t last = 0;
-    bool any = false;
-    for (auto it = s->pl_armed.begin(); it != s->pl_armed.end() && std::get<0>(*it) <= c; ++it) {
-        if (!any || std::get<0>(*it) != last) win.push_back(*it);
-        last = std::get<0>(*it);
-        any = true;
-    }
-    for (auto& w : win) {
-        s->pl_armed.erase(w);
-        const uint32_t slot = std::get<2>(w);
-        auto& pend = s->pl_pend[slot];
-        while (!pend.empty() && pend.front() <= c) pend.pop_front();
-        out.push_back(Firing{send, c, K, slot});
-        if (pend.empty()) s->pl_pend.erase(slot);
-        else s->pl_armed.insert(std::make_tuple(pend.front(), std::get<1>(w), slot));
+// String.valueOf(partition key) (ValuePartitionExecutor.execute :34-40): Integer / Long.toString,
+// Boolean.toString, or the string itself (its UTF-16 text from sh_query_set_strings)
+static int flow_id(sh_query* q, int64_t key, std::u16string* out) {
+    const int c = q->d.partition_col;
+    switch (q->d.col_types[c]) {
+        case SH_T_INT:
+        case SH_T_LONG: {
+            const std::string d = std::to_string(key);
+            out->assign(d.begin(), d.end());
+            return SH_OK;
+        }
+        case SH_T_BOOL: *out = key ? u"true" : u"false"; return SH_OK;
+        case SH_T_STRID: {
+            auto it = q->strings.find(c);
+            if (it != q->strings.end() && key >= 0 && key < (int64_t)it->second.size() && q->strings_set[c][(size_t)key]) {
+                *out = it->second[(size_t)key];
+                return SH_OK;
+            }
+            return sh_fail(SH_ERR_INVALID, "partition key string id " + std::to_string(key) +
+                                               " has no text: the Scheduler's tie rule orders partitions by "
+                                               "String.hashCode (call sh_query_set_strings)");
+        }
+        default: return sh_fail(SH_ERR_UNSUPPORTED, "float / double partition keys of time windows with expired output");
     }
 }
 
-// Scheduler.notifyAt (:107-121): the time joins the partition's queue; a partition with a due time is armed
-static void sched_register(SlidingImpl* s, uint32_t slot, int64_t t, uint64_t ckey) {
+// Scheduler.onTimeChange at one call (clock c). getAllStates() is walked in HashMap order and each due
+// state is put into a TreeMultimap<Long, SchedulerState> whose values compare equal: per distinct due time
+// the first state met fires, popping all of its due times (sendTimerEvents :171-209); returnAllStates then
+// removes the emptied states (canDestroy :343-346) through the iterator, in iteration order.
+static void sched_call(SlidingImpl* s, int64_t send, int64_t c, int64_t K, std::vector<Firing>& out) {
+    std::vector<std::pair<int64_t, uint32_t>> win;  // (due time, slot) per distinct due time
+    int64_t best = 0;
+    for (auto it = s->pl_armed.begin(); it != s->pl_armed.end() && it->first <= c; ++it) {
+        int64_t r = 0;
+        s->pl_states.rank(s->pl_flow[it->second], &r);
+        if (win.empty() || win.back().first != it->first) {
+            win.push_back(*it);
+            best = r;
+        } else if (r < best) {
+            win.back() = *it;
+            best = r;
+        }
+    }
+    std::vector<std::pair<int64_t, uint32_t>> gone;  // (HashMap rank, slot) of the emptied states
+    for (auto& w : win) {
+        s->pl_armed.erase(w);
+        const uint32_t slot = w.second;
+        auto& pend = s->pl_pend[slot];
+        while (!pend.empty() && pend.front() <= c) pend.pop_front();
+        out.push_back(Firing{send, c, K, slot});
+        if (pend.empty()) {
+            s->pl_pend.erase(slot);
+            int64_t r = 0;
+            s->pl_states.rank(s->pl_flow[slot], &r);
+            gone.emplace_back(r, slot);
+        } else {
+            s->pl_armed.insert(std::make_pair(pend.front(), slot));
+        }
+    }
+    std::sort(gone.begin(), gone.end());
+    for (auto& g : gone) s->pl_states.erase(s->pl_flow[g.second]);
+}
+
+// Scheduler.notifyAt (:113-127): stateHolder.getState() = states.computeIfAbsent(flow id) (a resize
+// check even for a present key), then the time joins the partition's queue
+static int sched_register(sh_query* q, uint32_t slot, int64_t t, const std::vector<int64_t>& slot_key) {
+    SlidingImpl* s = q->sl;
+    auto fl = s->pl_flow.find(slot);
+    if (fl == s->pl_flow.end()) {
+        std::u16string name;
+        RCHK(flow_id(q, slot_key[slot], &name));
+        fl = s->pl_flow.emplace(slot, std::move(name)).first;
+    }
+    s->pl_states.touch(fl->second, slot);
     auto& pend = s->pl_pend[slot];
-    if (pend.empty()) s->pl_armed.insert(std::make_tuple(t, ckey, slot));
+    if (pend.empty()) s->pl_armed.insert(std::make_pair(t, slot));
     pend.push_back(t);
+    return SH_OK;
 }
 
 // Lane pass of the push: records of M passing events sorted by slot (b == null: a TIMER call at `now`).
@@ -118,7 +170,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
         if (q->clock_valid && now < q->clock) return empty_out(q, out);
         q->clock = now;
         q->clock_valid = true;
-        if (!sched || s->pl_armed.empty() || std::get<0>(*s->pl_armed.begin()) > now) return empty_out(q, out);
+        if (!sched || s->pl_armed.empty() || s->pl_armed.begin()->first > now) return empty_out(q, out);
     }
     if (N >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 2G events");
     HIPCHK(hipEventRecord(q->ev_push0, st));
@@ -154,8 +206,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
                          s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
         launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
                           s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
-        if (sched)
-            launch_pl_first_seen(st, cs, q->kp, q->kt.dev(), N, q->seq, (unsigned long long*)s->pl_first.p);
+        if (sched) launch_pl_slot_key(st, cs, q->kp, q->kt.dev(), N, s->pl_key.as<int64_t>());
         HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
         launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
                        (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
@@ -229,14 +280,14 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
             calls_k.push_back(0);
         }
         std::vector<uint32_t> raw(M), slot(M);
-        std::vector<int64_t> tsv(M), first;
+        std::vector<int64_t> tsv(M), slot_key;
         if (!reg_r.empty()) {
             HIPCHK(hipMemcpyAsync(raw.data(), rec.raw, M * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(slot.data(), rec.slot, M * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(tsv.data(), rec.ts, M * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
         }
-        RCHK(d2h(q, first, s->pl_first.p, s->nslots));
+        if (!reg_r.empty()) RCHK(d2h(q, slot_key, s->pl_key.p, s->nslots));
         // replay the Scheduler: registrations of a send happen after that send's call
         size_t j = 0;
         for (size_t c = 0; c < calls_s.size(); c++) {
@@ -244,14 +295,14 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
                 const uint32_t r = (uint32_t)reg_r[j];
                 const int64_t snd = ss > 0 ? (int64_t)raw[r] / ss : 0;
                 if (snd >= calls_s[c]) break;
-                sched_register(s, slot[r], tsv[r] + T, (uint64_t)first[slot[r]]);
+                RCHK(sched_register(q, slot[r], tsv[r] + T, slot_key));
             }
-            if (!s->pl_armed.empty() && std::get<0>(*s->pl_armed.begin()) <= calls_c[c])
+            if (!s->pl_armed.empty() && s->pl_armed.begin()->first <= calls_c[c])
                 sched_call(s, calls_s[c], calls_c[c], calls_k[c], fire);
         }
         for (; j < reg_r.size(); j++) {
             const uint32_t r = (uint32_t)reg_r[j];
-            sched_register(s, slot[r], tsv[r] + T, (uint64_t)first[slot[r]]);
+            RCHK(sched_register(q, slot[r], tsv[r] + T, slot_key));
         }
     }
     const int64_t nF = (int64_t)fire.size();

@@ -227,22 +227,22 @@ void launch_pl_runs(hipStream_t s, ColSet cols, int pcol, i64 N, i64 send_size, 
     hipLaunchKernelGGL(k_pl_run_id, dim3(nb), dim3(kBlock), 0, s, start, N, blk, run);
 }
 
-// ---- creation order of the partitions: the stream index of a partition's first event, filtered or
-// not (PartitionRuntimeImpl.initPartition runs for every run, :346-367); it orders the Scheduler's
-// states (ties of TreeMultimap keys keep the first-created state, Scheduler.java:71-104) ------------------
-__global__ __launch_bounds__(kBlock) void k_pl_first_seen(ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64 seq_base,
-                                                         unsigned long long* first_seen) {
+// ---- the partition key of every slot, as sh_out reports it (int64 widening): the host names the
+// partition String.valueOf(key) for the Scheduler's HashMap order (sh_jmap.h). Every event of a slot
+// carries the same key, so concurrent stores write one value -------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_pl_slot_key(ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64* slot_key) {
     const i64 e = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (e >= N) return;
-    const u32 slot = key_slot(kt, make_key(kp, cols, e));
-    atomicMin(&first_seen[slot], (unsigned long long)(seq_base + e));
+    const u64 key = make_key(kp, cols, e);
+    i64 v;
+    unpack_key(kp, key, &v, 0);
+    slot_key[key_slot(kt, key)] = v;
 }
 
-void launch_pl_first_seen(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64 seq_base,
-                          unsigned long long* first_seen) {
+void launch_pl_slot_key(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64* slot_key) {
     if (N <= 0) return;
-    hipLaunchKernelGGL(k_pl_first_seen, dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, kp, kt,
-                       N, seq_base, first_seen);
+    hipLaunchKernelGGL(k_pl_slot_key, dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, kp, kt, N,
+                       slot_key);
 }
 
 // ---- notify registrations of partitioned time windows: Scheduler.notifyAt(ts + T) whenever an event

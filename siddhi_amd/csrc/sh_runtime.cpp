@@ -213,6 +213,33 @@ extern "C" int sh_free_pinned(void* p) {
 extern "C" const char* sh_last_error(void) { return g_last_error.c_str(); }
 extern "C" int32_t sh_abi_version(void) { return SH_ABI_VERSION; }
 
+extern "C" int sh_query_set_strings(sh_query* q, int32_t col, int64_t first_id, int64_t n, const uint16_t* units,
+                                    const int64_t* offsets) {
+    if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: NULL query");
+    if (col < 0 || col >= q->d.n_cols || q->d.col_types[col] != SH_T_STRID)
+        return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: not a string column");
+    if (first_id < 0 || n < 0 || first_id + n > ((int64_t)1 << 31) || (n > 0 && (!units || !offsets)))
+        return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: bad id range");
+    for (int64_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i] || offsets[i] < 0)
+            return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: offsets must be non-decreasing");
+    auto& v = q->strings[col];
+    auto& set = q->strings_set[col];
+    if ((int64_t)v.size() < first_id + n) {
+        v.resize((size_t)(first_id + n));
+        set.resize((size_t)(first_id + n), 0);
+    }
+    for (int64_t i = 0; i < n; i++) {
+        const size_t id = (size_t)(first_id + i);
+        if (set[id] && v[id].compare(0, std::u16string::npos, (const char16_t*)units + offsets[i],
+                                     (size_t)(offsets[i + 1] - offsets[i])) != 0)
+            return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: id " + std::to_string(id) + " already has another text");
+        v[id].assign((const char16_t*)units + offsets[i], (const char16_t*)units + offsets[i + 1]);
+        set[id] = 1;
+    }
+    return SH_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // descriptor compilation
 // ---------------------------------------------------------------------------------------------

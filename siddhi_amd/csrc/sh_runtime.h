@@ -9,6 +9,7 @@
 #include <new>
 #include <utility>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "sh_internal.h"
@@ -224,6 +225,9 @@ struct SlidingImpl;
 struct sh_query {
     int kind = 0;            // 0 = batch window (lengthBatch/timeBatch), 1 = sliding time window
     SlidingImpl* sl = nullptr;
+    // text of dictionary ids per string column (sh_query_set_strings), UTF-16 as Java holds it
+    std::unordered_map<int, std::vector<std::u16string>> strings;
+    std::unordered_map<int, std::vector<char>> strings_set;
     // partitioned timeBatch (R12): only the first partition key ever flushes
     bool partitioned = false, p0_known = false;
     int64_t p0 = 0;

@@ -143,7 +143,7 @@ void sliding_destroy(sh_query* q) {
                       &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
                       &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
                       &s->x_nexp, &s->xr_ts, &s->xr_rep, &s->xr_slot, &s->xr_ch, &s->xr_clk, &s->xr_exp,
-                      &s->xr_vals, &s->xr_nulls, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_first,
+                      &s->xr_vals, &s->xr_nulls, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_key,
                       &s->pl_start, &s->pl_run, &s->pl_reg, &s->pl_toff, &s->pl_tsend, &s->pl_tclk, &s->pl_tpos,
                       &s->pl_fsend};
     for (DevBuf* b : bufs) b->release();

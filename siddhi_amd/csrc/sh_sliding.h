@@ -149,8 +149,7 @@ void launch_pl_walk_lb(hipStream_t s, const u32* key_off, const u32* sorted_rank
                        int exp_on, SlxRows rows, unsigned char* flags);
 void launch_pl_runs(hipStream_t s, ColSet cols, int pcol, i64 N, i64 send_size, unsigned char* start, i64* blk,
                     i64* run);
-void launch_pl_first_seen(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64 seq_base,
-                          unsigned long long* first_seen);
+void launch_pl_slot_key(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64* slot_key);
 void launch_pl_notify(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, const i64* ts, i64* last_ts,
                       unsigned char* reg);
 void launch_pl_walk_tm(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "sh_runtime.h"
+#include "sh_jmap.h"
 #include "sh_sliding.h"
 
 using shd::SlInfo;
@@ -40,13 +41,17 @@ struct SlidingImpl {
     PinnedBuf x_h;
     // partitioned windows keyed by the partition (sh_plane.cpp): lane = 1 lengthBatch, 2 time; per slot the
     // open batch's last event, the last flushed batch's last event (expired rows), lastTimestamp, the
-    // partition's creation order; host side the Scheduler's pending notify times per partition
+    // partition key; host side the Scheduler: pending notify times per partition, the armed partitions by
+    // front due time, and PartitionStateHolder.states in java.util.HashMap order (sh_jmap.h) over the
+    // partitions' String.valueOf(key)
     int lane = 0;
     int nk_out = -1;  // output key columns (0: no group-by, the partition key is internal)
-    DevBuf pl_last_ts, pl_last_seq, pl_prev_seq, pl_first, pl_start, pl_run, pl_reg, pl_toff, pl_tsend, pl_tclk,
+    DevBuf pl_last_ts, pl_last_seq, pl_prev_seq, pl_key, pl_start, pl_run, pl_reg, pl_toff, pl_tsend, pl_tclk,
         pl_tpos, pl_fsend;
     std::unordered_map<uint32_t, std::deque<int64_t>> pl_pend;
-    std::set<std::tuple<int64_t, uint64_t, uint32_t>> pl_armed;  // (front notify time, creation order, slot)
+    std::set<std::pair<int64_t, uint32_t>> pl_armed;  // (front notify time, slot)
+    shj::JavaStringMap pl_states;
+    std::unordered_map<uint32_t, std::u16string> pl_flow;  // slot -> String.valueOf(partition key)
 };
 
 

@@ -31,10 +31,37 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 7:
+        if L.sh_abi_version() != 8:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
+
+
+def device_out_arrays(out_ptr):
+    """abi.out_arrays for an sh_push_device result: its row arrays are copied out of HBM (hipMemcpy, a
+    synchronising copy) into host arrays; flush offsets / clocks are already on the host."""
+    o = out_ptr.contents
+    n, nk, na = o.n_rows, o.n_keys, o.n_vals
+    hip = C.CDLL("libamdhip64.so")
+    host = {}
+    for name, cnt, dt in (("ts", n, np.int64), ("expired", n, np.uint8), ("keys", nk * n, np.int64),
+                          ("vals", na * n, np.uint64), ("nulls", na * n, np.uint8), ("rep", n, np.int64)):
+        a = np.zeros(max(cnt, 1), dt)
+        src = C.cast(getattr(o, name), C.c_void_p).value
+        if cnt:
+            rc = hip.hipMemcpy(C.c_void_p(a.ctypes.data), C.c_void_p(src), C.c_size_t(a.itemsize * cnt), 2)
+            if rc != 0:
+                raise SiddhiError(abi.SH_ERR_DEVICE, f"hipMemcpy of output column {name} failed ({rc})")
+        host[name] = a[:cnt]
+    return {
+        "flush_offsets": np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
+        if o.n_flushes else np.zeros(1, np.int64),
+        "flush_clock": np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
+        if o.n_flushes else np.zeros(0, np.int64),
+        "val_types": np.array([o.val_types[i] for i in range(na)], np.int32),
+        "ts": host["ts"], "expired": host["expired"], "rep": host["rep"],
+        "keys": host["keys"].reshape(nk, n), "vals": host["vals"].reshape(na, n), "nulls": host["nulls"].reshape(na, n),
+    }
 
 
 class SiddhiError(RuntimeError):
@@ -81,12 +108,18 @@ class GpuQuery:
         self.h = C.c_void_p()
         _check(lib().sh_query_create(self.ctx.h, C.byref(self._desc), C.byref(self.h)))
         self.callbacks: List[Callable] = []
-        if spec.rate:
-            try:
+        try:
+            if spec.rate:
                 _check(lib().sh_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])))
-            except Exception:
-                self.close()
-                raise
+            for col, names in (spec.strings or {}).items():
+                self.set_strings(col, names)
+        except Exception:
+            self.close()
+            raise
+
+    def set_strings(self, col: str, names, first_id: int = 0):
+        """The text of string column `col`'s dictionary ids first_id.. (sh_query_set_strings)."""
+        _check(abi.apply_strings(lib().sh_query_set_strings, self.h, self.spec, col, list(names), first_id))
 
     # -- reference-shaped API --------------------------------------------------------------
     def add_callback(self, fn: Callable[[List[tuple]], None]):

@@ -155,6 +155,30 @@ case(name="partition3_time_all", source="ctest/query/partition/WindowPartitionTe
                                          [None], [None]],
                  rep_cols=[["symbol", ["IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "WSO2"]]]))
 
+# Scheduler tie rule, hand-traced (no reference test pins it; ctest/query/partition/WindowPartitionTestCase.java:
+# 141-216 is the query shape). Five partitions are due at the same time B+1000; Scheduler.onTimeChange
+# (core/util/Scheduler.java:71-104) walks PartitionStateHolder.states (HashMap<String, …>,
+# PartitionStateHolder.java:36,46) and its TreeMultimap keeps ONE state per due time (values compare
+# equal, :363-366), so each later send's call fires the next one, in HashMap iteration order:
+#   String.hashCode   "WSO2" = 2674079 = 0x28CD9F   spread ^ (h >>> 16) = 0x28CDB7 -> bin 7 of 16
+#                     "IBM"  = 72276   = 0x11A54    spread 0x11A55    -> bin 5
+#                     "ORACLE" = 0x8B70F17E         spread 0x8B707A0E -> bin 14
+#                     "Aa" = 65*31+97 = 2112 = "BB" = 66*31+66 (0x840, spread 0x840) -> bin 0
+#   computeIfAbsent links a new key at the HEAD of its bin (JDK 8), so bin 0 reads BB, Aa.
+#   Iteration: BB, Aa, IBM, WSO2, ORACLE (creation order was WSO2, IBM, ORACLE, Aa, BB).
+# Each expiry empties its partition (sum null); the x partitions register B+2000.. and are never due.
+_tie = [["WSO2", 700.0, 1], ["IBM", 70.0, 2], ["ORACLE", 75.0, 3], ["Aa", 1.0, 4], ["BB", 2.0, 5]]
+case(name="partition_tie_hashmap_order", source="hand-traced: core/util/Scheduler.java:71-104,363-366, "
+     "core/util/snapshot/state/PartitionStateHolder.java:36-83 (java.util.HashMap JDK 8)",
+     schema="symbol string, price float, volume int",
+     query=dict(window="time", param=1000, partition="symbol", aggs=[["sum", "price"]], output="all"),
+     sends=[[[B] + r] for r in _tie] + [[[B + 1000 + i, f"x{i + 1}", 10.0 * (i + 1), 10 + i]] for i in range(5)],
+     expect=dict(total_count=15,
+                 values=[[700.0], [70.0], [75.0], [1.0], [2.0], [None], [10.0], [None], [20.0], [None], [30.0],
+                         [None], [40.0], [None], [50.0]],
+                 rep_cols=[["symbol", ["WSO2", "IBM", "ORACLE", "Aa", "BB", "BB", "x1", "Aa", "x2", "IBM", "x3",
+                                       "WSO2", "x4", "ORACLE", "x5"]]]))
+
 # ---------------------------------------------------------------- incremental aggregation (Aggregation1TestCase)
 AGG_SCHEMA = "symbol string, price float, lastClosingPrice float, volume long, quantity int, timestamp long"
 _t5 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],

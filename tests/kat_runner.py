@@ -76,6 +76,13 @@ def run_query(case, make_query):
     """make_query(spec) -> object with push(HostBatch) and advance_time(now) returning flushes."""
     dic = Dict()
     schema, spec = build(case, dic)
+    # the shim's dictionary holds every string it has seen; a string partition key's text goes with it
+    # (sh_query_set_strings: the Scheduler's HashMap order hashes the partition key's String)
+    for s in case["sends"]:
+        if isinstance(s, list):
+            batch_of(schema, s, dic)
+    if spec.partition and schema.types[schema.col(spec.partition)] == abi.STRID:
+        spec.strings = {spec.partition: [dic.name(i) for i in range(len(dic.ids))]}
     q = make_query(spec)
     flushes = []
     for s in case["sends"]:

@@ -3,7 +3,9 @@ partition key or without group-by (sh_plane.cpp: one lane per partition), agains
 restatement of PartitionStreamReceiver.receive (:176-272: runs of equal partition keys per send, one
 window / aggregator state per partition), LengthBatchWindowProcessor (:153-243), TimeWindowProcessor
 (:132-169) and the Scheduler's TIMER calls per partition (Scheduler.java:71-104, 171-209, including
-its TreeMultimap tie rule: of several partitions due at the same time only the first-created fires).
+its TreeMultimap tie rule: of several partitions due at the same time only the first met while walking
+PartitionStateHolder.states fires — java.util.HashMap<String, …> order of String.valueOf(partition key),
+restated twice and independently: oracle/jhashmap.h and siddhi_amd/csrc/sh_jmap.h).
 The reference KATs (WindowPartitionTestCase partition2 lengthBatch, partition3 time) run in
 test_gpu_parity.py."""
 import numpy as np
@@ -80,3 +82,44 @@ def test_partitioned_time_no_group_by_zipf(rt):
     pushes = split_batches(SCHEMA, ts, cols, [100_000, 200_000], 1) + [("advance", int(ts[-1]) + 1_000)]
     ref = both(rt, spec, pushes, "ptime zipf")
     assert ref["expired"].sum() > 0
+
+
+def _same_hash_strings(k):
+    """2^k distinct strings of one String.hashCode ("Aa" and "BB" both hash to 2112): one HashMap bin at
+    every capacity, so ties among them are ordered inside a red-black tree bin once 8 share it."""
+    out = [""]
+    for _ in range(k):
+        out = [x + y for x in out for y in ("Aa", "BB")]
+    return out
+
+
+def test_partitioned_time_string_keys_tree_bins(rt):
+    """String partition keys: 32 of equal hashCode (a tree bin as soon as 8 are armed on a table of >= 64
+    bins) among 300 others; ties at every ms; partitions drained, removed and re-inserted all the time"""
+    names = _same_hash_strings(5) + [f"sym{i}" for i in range(300)]
+    rng = np.random.default_rng(71)
+    n = 40_000
+    ts = (np.cumsum(rng.integers(0, 2, n)) + 50_000).astype(np.int64)
+    hot = rng.random(n) < 0.5
+    pid = np.where(hot, rng.integers(0, 32, n), rng.integers(32, len(names), n)).astype(np.int32)
+    v = rng.integers(-400, 400, n).astype(np.float64) / 8.0
+    x = rng.integers(-50, 50, n).astype(np.int64)
+    schema = abi.Schema.parse("p string, v double, x long, ts long")
+    cols = [pid, v, x, ts.copy()]
+    spec = abi.QuerySpec(schema, "time", 120, aggs=[("count", None), ("sum", "v"), ("max", "x")], partition="p",
+                         output="all", key_capacity=512, strings={"p": names})
+    pushes = split_batches(schema, ts, cols, [3_000, 20_000], 1) + [("advance", int(ts[-1]) + 60),
+                                                                     ("advance", int(ts[-1]) + 1_000)]
+    ref = both(rt, spec, pushes, "ptime tree bins")
+    assert ref["expired"].sum() > 1000
+
+
+def test_partition_key_without_text_fails_loudly(rt):
+    schema = abi.Schema.parse("p string, v double, ts long")
+    spec = abi.QuerySpec(schema, "time", 100, aggs=[("sum", "v")], partition="p", output="all", key_capacity=16)
+    g = rt.GpuQuery(spec)
+    g.set_strings("p", ["a", "b"])
+    b = abi.HostBatch.from_rows(schema, [(1000, 0, 1.0, 1000), (1000, 2, 2.0, 1000)], 1)
+    with pytest.raises(rt.SiddhiError, match="no text"):
+        g.push(b)
+    g.close()

@@ -4,7 +4,6 @@ AllPerEvent, FirstPerEvent, LastPerEvent, FirstGroupByPerEvent, LastGroupByPerEv
 The oracle's limiters are pinned by EventOutputRateLimitTestCase (tests/golden, rate1..rate18); the
 windowed ones (rate12..16) also run on the GPU through test_gpu_parity.py, and the no-window ones run
 here as `#window.lengthBatch(1)` (one event per send: every send is one chunk either way)."""
-import ctypes as C
 
 import numpy as np
 import pytest
@@ -102,33 +101,9 @@ def test_first_group_by_table_growth(rt):
     both(rt, spec, split_batches(SCHEMA, ts, cols, [100, 1_000, 30_000, 60_000], 0), label="first gb growth")
 
 
-def _hip():
-    return C.CDLL("libamdhip64.so")
-
-
 def _dev_arrays(out_ptr):
-    """abi.out_arrays for an sh_push_device result: row arrays copied out of HBM first."""
-    o = out_ptr.contents
-    n, nk, na = o.n_rows, o.n_keys, o.n_vals
-    hip = _hip()
-    host = {}
-    for name, cnt, dt in (("ts", n, np.int64), ("expired", n, np.uint8), ("keys", nk * n, np.int64),
-                          ("vals", na * n, np.uint64), ("nulls", na * n, np.uint8), ("rep", n, np.int64)):
-        a = np.zeros(max(cnt, 1), dt)
-        src = C.cast(getattr(o, name), C.c_void_p).value
-        if cnt:
-            assert hip.hipMemcpy(C.c_void_p(a.ctypes.data), C.c_void_p(src), C.c_size_t(a.itemsize * cnt), 2) == 0
-        host[name] = a[:cnt]
-    res = {
-        "flush_offsets": np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
-        if o.n_flushes else np.zeros(1, np.int64),
-        "flush_clock": np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
-        if o.n_flushes else np.zeros(0, np.int64),
-        "val_types": np.array([o.val_types[i] for i in range(na)], np.int32),
-        "ts": host["ts"], "expired": host["expired"], "rep": host["rep"],
-        "keys": host["keys"].reshape(nk, n), "vals": host["vals"].reshape(na, n), "nulls": host["nulls"].reshape(na, n),
-    }
-    return res
+    from siddhi_amd import runtime
+    return runtime.device_out_arrays(out_ptr)
 
 
 @pytest.mark.parametrize("window,param", [("lengthBatch", 50), ("timeBatch", 300)])
