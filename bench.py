@@ -352,7 +352,7 @@ def run_host(args, dev):
         pb = runtime.PinnedBatch(schema, B, args.send_size)
         for a, t in zip(pb.arrays, [ts] + cols):
             torch.from_numpy(a).copy_(t)  # D2H into the pinned SoA buffers (outside the timed region)
-        pb.b.n = B
+        pb.set_n(B)
         bufs.append(pb)
     torch.cuda.synchronize()
 

@@ -288,6 +288,7 @@ struct sh_query {
     uint64_t zc_tok[kZcRing]{};   // token of the kernel that reads each slot
     int zc_next = 0;
     uint64_t async_tok = 0;       // last asynchronous push not yet verified (0: none)
+    int64_t async_keys = 0;       // events of the unverified asynchronous pushes (a bound on their new keys)
     TileMap ms_map{};  // tiling of the last multisplit
     int64_t rec_cap = 0;
     // flush bookkeeping of the closed windows, completed after the push's final synchronisation
@@ -404,6 +405,7 @@ int query_advance(sh_query* q, int64_t now, bool host_out, const sh_out** out);
 
 // make room for `extra` new keys in a batch query's table (rebuild / grow; batch windows only)
 int query_reserve_keys(sh_query* q, int64_t extra);
+int query_drain_async(sh_query* q);
 // move the queued events' key slots into table `nk` (any mode to any mode) and make it the query's
 int query_swap_keys(sh_query* q, KeyTableHost& nk);
 

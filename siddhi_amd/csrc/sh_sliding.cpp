@@ -208,11 +208,7 @@ static int sliding_rekey(sh_query* q) {
 
 // the key-sorted replay with 48-byte records (k_sl_wkey<AOS>): time windows of the count / sum / avg
 // / min / max-of-one-double shape with a min or max (sliding_keyed_ok)
-static bool keyed_aos(const sh_query* q) {
-    static const bool off = getenv("SH_SL_PARTITIONED") != nullptr || getenv("SH_SL_LANE_PER_KEY") != nullptr ||
-                            getenv("SH_SL_NO_AOS") != nullptr;
-    return !off && q->d.window == SH_WIN_TIME && sliding_keyed_ok(q->ap);
-}
+static bool keyed_aos(const sh_query* q) { return q->d.window == SH_WIN_TIME && sliding_keyed_ok(q->ap); }
 
 int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
@@ -367,8 +363,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
                     s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
         // the common shape (count / sum / avg / min / max of one double column, time window): records
         // sorted stably by key, one lane per key (k_sl_key); other shapes: key-partition replay
-        static const bool force_part = getenv("SH_SL_PARTITIONED") != nullptr;
-        const bool keyed = q->d.window == SH_WIN_TIME && sliding_keyed_ok(q->ap) && !force_part;
+        const bool keyed = keyed_aos(q);
         if (keyed) {
             HIPCHK(hipEventRecord(q->ev_agg0, st));  // the sort is part of the replay's time
             size_t tb = 0;
@@ -381,19 +376,13 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
                 return sh_fail(SH_ERR_DEVICE, "radix sort failed");
             RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
             RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
-            RCHK(s->p_clock.reserve(M * 8, false));
             RCHK(s->p_pm.reserve(M * 8, false));
-            RCHK(s->p_ts.reserve(M * 8, false));
             RCHK(s->p_vals.reserve(M * 8, false));
-            RCHK(s->p_raw.reserve(M * 4, false));
-            RCHK(s->g_rank.reserve(M * 4, false));
             RCHK(s->inv.reserve(M * 4, false));
             RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na) * 8, false));
             launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
-                                 s->p_slot.as<u32>(), M, rec, s->p_clock.as<int64_t>(), s->p_pm.as<int64_t>(),
-                                 s->p_vals.as<u64>(), s->p_ts.as<int64_t>(), s->p_raw.as<u32>(), s->g_rank.as<u32>(),
-                                 s->inv.as<u32>(), state_of(s), q->ap, q->d.window_param, send_size, send_base,
-                                 s->rows_k.as<u64>(), s->flags.as<unsigned char>());
+                                 rec, s->p_pm.as<int64_t>(), s->p_vals.as<u64>(), s->inv.as<u32>(), state_of(s), q->ap,
+                                 q->d.window_param, send_size, send_base, s->rows_k.as<u64>(), s->flags.as<unsigned char>());
         } else {
             // stable split of the records by key partition
             int P = s->P;

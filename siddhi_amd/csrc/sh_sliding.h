@@ -68,9 +68,8 @@ bool sliding_keyed_ok(AggPlan ap);
 int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u32* rank_out, i64 M, i64 nslots,
                     hipStream_t s);
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
-                          const u32* sorted_slot, i64 M, SlRecords rec, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
-                          u32* g_raw, u32* g_rank, u32* inv, SlState S, AggPlan ap, i64 T, i64 send_size,
-                          i64 send_base, u64* rowsK, unsigned char* flags);
+                          SlRecords rec, i64* g_pm, u64* g_v, u32* inv, SlState S, AggPlan ap, i64 T,
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags);
 int sliding_keyed_row_words(int n_aggs);
 void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, const u32* inv,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,

@@ -1227,44 +1227,13 @@ static bool own_d_fields(const AggPlan& ap, DFields& fd) {
 // keys a key partition should hold so that every key gets a lane of its own in the replay kernel
 // (k_sl_own_d: kSlKeyLanes per wave; k_sl_own: 64). A lane owning several keys switches per-key
 // state (global loads and stores) whenever consecutive records of its list change key.
-// ---- key-sorted replay (k_sl_key): the records of a push sorted stably by key slot (sh_sort.hip),
-// so each key's events form one contiguous run in event order, and one lane per key walks its run.
-// The key's window is its carried ring (events of earlier pushes) followed by the run itself, so the
-// expiry head reads the run's own earlier entries instead of a ring written and read back per event;
-// only the entries still in the window at the end of the push go to the ring. Rows are written in
-// key order as one record each (full-line stores) and put in stream order by the emit kernel. ------
-constexpr int kKR = 8;    // records per replay step (fields loaded one step ahead)
-constexpr int kKH = 32;   // staged window-head entries per lane
-constexpr int kKS = 16;   // head entries staged per step (twice the step's average expiries: the
-                          // staged run does not drain into the global-memory fallback)
+// ---- key-sorted replay: the records of a push sorted stably by key slot (sh_sort.hip), so each key's
+// events form one contiguous run in event order, walked by one wave per key (k_sl_wkey). The key's
+// window is its carried ring (events of earlier pushes) followed by the run itself; only the entries
+// still in the window at the end of the push go to the ring. Rows are written in key order as one record
+// each (full-line stores) and put in stream order by the emit kernel. ------------------------------------
 constexpr int kDqK = 64;  // LDS min/max deque entries per lane (longer deques continue in global memory)
 constexpr u32 kFirstBit = 0x80000000u;
-
-// k_sl_kgather: key-order copies of the record fields; a record opens a row when it is its key's
-// first event of its send; flags / inv give the row of each opening rank (rank order, for the emit)
-__global__ __launch_bounds__(kBlock) void k_sl_kgather(const u32* __restrict__ sorted_rank,
-                                                       const u32* __restrict__ sorted_slot, i64 M, SlRecords rec,
-                                                       u32 send_size, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
-                                                       u32* g_raw, u32* g_rank, unsigned char* flags, u32* inv) {
-    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M) return;
-    const u32 r = sorted_rank[i];
-    const u32 raw = rec.raw[r];
-    // (every event is its own send when send_size == 1; one send holds the whole push when it is 0)
-    bool first = send_size == 1 || i == 0 || sorted_slot[i - 1] != sorted_slot[i];
-    if (!first && send_size > 1) {
-        const u32 praw = rec.raw[sorted_rank[i - 1]];
-        first = praw / send_size != raw / send_size;
-    }
-    g_clk[i] = rec.clock[r];
-    g_pm[i] = rec.pm[r];
-    g_v[i] = rec.vals[r];
-    g_ts[i] = rec.ts[r];
-    g_raw[i] = raw;
-    g_rank[i] = r | (first ? kFirstBit : 0u);
-    flags[r] = first ? 1 : 0;
-    if (first) inv[r] = (u32)i;
-}
 
 __global__ void k_sl_keyoff(const u32* __restrict__ slot_cnt, i64 nslots, u32* key_off) {
     const i64 k = (i64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1412,209 +1381,29 @@ struct KOut {
     int src[SH_MAX_AGGS];
 };
 
-template <bool HSUM, bool HMIN, bool HMAX, int KL>
-__global__ __launch_bounds__(64) void k_sl_key(const u32* __restrict__ key_off, u32 nslots, const i64* __restrict__ g_clk,
-                                              const i64* __restrict__ g_pm, const u64* __restrict__ g_v,
-                                              const i64* __restrict__ g_ts, const u32* __restrict__ g_raw,
-                                              const u32* __restrict__ g_rank, SlState S, DFields fd, KOut ko, i64 T,
-                                              u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW) {
-    __shared__ u64 dq_min[HMIN ? KL * kDqK : 1];
-    __shared__ u64 dq_max[HMAX ? KL * kDqK : 1];
-    __shared__ i64 hb_pm[KL * kKH];
-    __shared__ u64 hb_v[KL * kKH];
-    __shared__ i64 r_clk[KL * kKR];
-    __shared__ i64 r_ts[KL * kKR];
-    __shared__ u64 r_v[KL * kKR];
-    __shared__ u32 r_raw[KL * kKR];
-    __shared__ u32 r_rank[KL * kKR];
-    // KL lanes of the wave own a key each: fewer owners per wave, less divergence between their
-    // data-dependent loops (expiry, deque pops and searches)
-    const int lane = threadIdx.x;
-    const u32 k = blockIdx.x * KL + lane;
-    if (lane >= KL || k >= nslots) return;
-    const u32 a = key_off[k], b = key_off[k + 1];
-    if (a == b) return;
-    // per-lane LDS arrays interleaved (entry e of this lane at e * 64 + lane): conflict-free
-    u64* lmin = dq_min + (HMIN ? lane : 0);
-    u64* lmax = dq_max + (HMAX ? lane : 0);
-    const int gm = (int)(S.rc - 1);
-    i64* rpm = S.rpm + (size_t)k * S.rc;
-    u64* rval = S.rval + (size_t)k * S.rc;
-    i64 cnt = S.cnt[k];
-    const int rh0 = (int)(S.rhead[k] & gm), H0 = (int)S.rlen[k];
-    double sum = 0.0;
-    if (HSUM) sum = __longlong_as_double((i64)S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k]);
-    KDq qn{}, qx{};
-    u64* gmin = nullptr;
-    u64* gmax = nullptr;
-    if (HMIN) { kdq_load<KL>(qn, S, fd.mn, k, lmin); gmin = S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc; }
-    if (HMAX) { kdq_load<KL>(qx, S, fd.mx, k, lmax); gmax = S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc; }
-    // head sequence: the carried ring's H0 entries, then the run; entry j of it
-    const int n = (int)(b - a), HN = H0 + n;
-    auto head_pm = [&](int j) -> i64 { return j < H0 ? rpm[(rh0 + j) & gm] : g_pm[a + (j - H0)]; };
-    auto head_v = [&](int j) -> u64 { return j < H0 ? rval[(rh0 + j) & gm] : g_v[a + (j - H0)]; };
-    int hj = 0;      // next head entry to expire
-    int staged = 0;  // entries [.., staged) staged in the LDS ring (those >= hj and >= staged - kKH)
-    i64 h_pm[kKS];
-    u64 h_v[kKS];
-    int h_from = 0, h_to = 0;
-    auto load_heads = [&]() {
-        h_from = staged > hj ? staged : hj;
-        h_to = min(min(h_from + kKS, hj + kKH), HN);
-        // one address select per entry (ring or run), no divergent branch per staged entry
-#pragma unroll
-        for (int q = 0; q < kKS; q++) {
-            const int j = min(h_from + q, HN - 1);
-            const bool ring = j < H0;
-            const size_t ri = (size_t)((rh0 + j) & gm), gi = (size_t)a + (size_t)(j - H0);
-            const i64* pp = ring ? rpm + ri : g_pm + gi;
-            const u64* pv = ring ? rval + ri : g_v + gi;
-            h_pm[q] = *pp;
-            h_v[q] = *pv;
-        }
-    };
-    auto commit_heads = [&]() {
-#pragma unroll
-        for (int q = 0; q < kKS; q++) {
-            const int j = h_from + q;
-            if (j < h_to) { hb_pm[(j & (kKH - 1)) * KL + lane] = h_pm[q]; hb_v[(j & (kKH - 1)) * KL + lane] = h_v[q]; }
-        }
-        if (h_to > h_from) staged = h_to;
-    };
-    i64 n_clk[kKR], n_ts[kKR];
-    u64 n_v[kKR];
-    u32 n_raw[kKR], n_rank[kKR];
-    auto load_recs = [&](int o) {
-#pragma unroll
-        for (int q = 0; q < kKR; q++) {
-            const u32 i = a + (u32)min(o + q, n - 1);
-            n_clk[q] = g_clk[i];
-            n_ts[q] = g_ts[i];
-            n_v[q] = g_v[i];
-            n_raw[q] = g_raw[i];
-            n_rank[q] = g_rank[i];
-        }
-    };
-    auto commit_recs = [&]() {
-#pragma unroll
-        for (int q = 0; q < kKR; q++) {
-            r_clk[q * KL + lane] = n_clk[q];
-            r_ts[q * KL + lane] = n_ts[q];
-            r_v[q * KL + lane] = n_v[q];
-            r_raw[q * KL + lane] = n_raw[q];
-            r_rank[q * KL + lane] = n_rank[q];
-        }
-    };
-    load_recs(0);
-    load_heads();
-    commit_recs();
-    commit_heads();
-    i64 send = 0;
-    u32 row = 0;  // key-order position of the current row (its first record)
-    for (int o0 = 0; o0 < n; o0 += kKR) {
-        // the next step's records and heads go out before this step's stores (vector-memory
-        // counters complete in order: waiting for these loads never waits for the stores)
-        load_recs(o0 + kKR);
-        load_heads();
-        const int m = min(kKR, n - o0);
-        for (int q = 0; q < m; q++) {
-            const i64 clk = r_clk[q * KL + lane];
-            const int added = H0 + o0 + q;  // head entries in the window before this record
-            // lazy expiry: window events with PM + T <= clock (TimeWindowProcessor.java:132-169)
-            while (hj < added) {
-                i64 pm;
-                u64 hv;
-                if (hj < staged && hj + kKH >= staged) {
-                    pm = hb_pm[(hj & (kKH - 1)) * KL + lane];
-                    hv = hb_v[(hj & (kKH - 1)) * KL + lane];
-                } else {
-                    pm = head_pm(hj);
-                    hv = head_v(hj);
-                    wait_vm_here();
-                }
-                if (pm + T > clk) break;
-                cnt--;
-                if (HSUM) {
-                    sum = sum - __longlong_as_double((i64)hv);
-                    if (cnt == 0 && sum == 0.0) sum = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
-                }
-                if (HMIN) kdq_remove<true, KL>(qn, gmin, gm, lmin, hv);
-                if (HMAX) kdq_remove<false, KL>(qx, gmax, gm, lmax, hv);
-                hj++;
-            }
-            // the event joins the window and the aggregators
-            const u64 x = r_v[q * KL + lane];
-            cnt++;
-            if (HSUM) sum = sum + __longlong_as_double((i64)x);
-            if (HMIN) kdq_add<true, KL>(qn, gmin, gm, lmin, x);
-            if (HMAX) kdq_add<false, KL>(qx, gmax, gm, lmax, x);
-            // the row of (send, key): at its first record, with the values after this one
-            const u32 raw = r_raw[q * KL + lane];
-            if (r_rank[q * KL + lane] & kFirstBit) {
-                row = a + (u32)(o0 + q);
-                send = send_base + (send_size == 1 ? (i64)raw : send_size ? (i64)(raw / send_size) : 0);
-            }
-            u64 w[4 + SH_MAX_AGGS];
-            u32 nulls = 0;
-            w[0] = (u64)r_ts[q * KL + lane];
-            w[1] = (u64)raw | ((u64)k << 32);
-            w[2] = (u64)clk;
-#pragma unroll
-            for (int o = 0; o < SH_MAX_AGGS; o++) {
-                if (o >= ko.n) break;
-                const int src = ko.src[o];
-                u64 v = 0;
-                if (src == 0) v = (u64)cnt;
-                else if (src == 1) v = (u64)__double_as_longlong(sum);
-                else if (src == 2) v = (u64)__double_as_longlong(sum / (double)cnt);
-                else if (src == 3) { v = qn.mm; nulls |= (qn.mmh ? 0u : 1u) << o; }
-                else { v = qx.mm; nulls |= (qx.mmh ? 0u : 1u) << o; }
-                w[4 + o] = v;
-            }
-            w[3] = (u64)send | ((u64)nulls << 56);
-            ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row * RW);
-#pragma unroll
-            for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
-                if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
-        }
-        commit_recs();
-        commit_heads();
-    }
-    // the window after the push: head entries [hj, HN) become the ring (ring entries keep their
-    // place; the run's entries follow them)
-    const int keep = hj < H0 ? H0 - hj : 0;
-    const int rh = (rh0 + (hj < H0 ? hj : H0)) & gm;
-    int rlen = keep;
-    for (int j = (hj > H0 ? hj : H0); j < HN; j++) {
-        const int sl = (rh + rlen) & gm;
-        rpm[sl] = g_pm[a + (j - H0)];
-        rval[sl] = g_v[a + (j - H0)];
-        rlen++;
-    }
-    S.cnt[k] = cnt;
-    S.rhead[k] = rh;
-    S.rlen[k] = rlen;
-    S.cur_send[k] = send;
-    S.cur_first[k] = 0;
-    if (HSUM) {
-        const u64 sb = (u64)__double_as_longlong(sum);
-        if (fd.sum >= 0) S.f[(size_t)fd.sum * S.nslots + k] = sb;
-        if (fd.avg >= 0) S.f[(size_t)fd.avg * S.nslots + k] = sb;
-    }
-    if (HMIN) kdq_store<KL>(qn, S, fd.mn, k, lmin);
-    if (HMAX) kdq_store<KL>(qx, S, fd.mx, k, lmax);
-}
-
 // ---- one wave per key (round 3): the 64 lanes of a wave share one key's run, 64 records at a time.
 // Everything per record that does not depend on the running aggregates is computed lane-parallel:
 // the expiry prefix (the heads with PM + T <= the record's clock form a prefix, PM and the clock both
 // being non-decreasing along a key's events — one binary search per lane over the staged heads), the
-// count, the row position and the row stores. Only the Java-order double sum and the min / max deques
-// (MinAttributeAggregatorExecutor's LinkedList, removeFirstOccurrence included) run sequentially, by
-// the whole wave in lockstep on wave-uniform state, reading the records' values and expiry points from
-// the lanes' registers (readlane). With a wave per key a SIMD holds several keys' waves, whose
-// sequential parts interleave (the lane-per-key kernel left most SIMDs without a wave: ~0.6 per SIMD at
-// C3's 10k keys). TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
+// count, the row position and the row stores. The Java-order double sum runs sequentially, by the whole
+// wave in lockstep on wave-uniform state, reading the records' values and expiry points from the lanes'
+// registers (readlane). With a wave per key a SIMD holds several keys' waves, whose sequential parts
+// interleave. TimeWindowProcessor.java:132-169; QuerySelector.processInBatchGroupBy :315-374.
+//
+// Min / max off the sequential chain (round 4). MinAttributeAggregatorExecutor (:187-236) keeps a
+// LinkedList deque: processAdd pops the back while it is strictly worse, processRemove calls
+// removeFirstOccurrence(value) and reads the front. The expiring event is the window's oldest, so when it
+// is in the deque it is the front and leaves; the result differs from the window's true minimum only if
+// it was popped earlier and a bit-equal value sits in the deque (the reference's quirk), or once a NaN
+// breaks the order. While neither can happen the deque after every event is the monotone deque of the
+// window and minValue is the window's range minimum (the older entry on ties, which the front and the
+// strict `minValue > value` both keep). So per chunk the lanes check that no expiring head meets a
+// bit-equal value among the deque (entries carry their window index) or the chunk's records and that no
+// NaN is in sight, then compute each record's result in parallel: the first deque entry at or after the
+// record's first unexpired head, against the leftmost best of the chunk's records in its window. The
+// deque after the chunk is the old entries still unexpired and not worse than the chunk's best, then the
+// chunk's suffix bests. A chunk that fails the check or would outgrow the LDS ring runs the sequential
+// deque (kdq_*), and its key stays sequential for the rest of the push (the indices are not kept there).
 constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)
 
 // lane l's value of a 64-bit register (l wave-uniform)
@@ -1624,21 +1413,190 @@ __device__ __forceinline__ u64 rl64(u64 v, int l) {
     return ((u64)hi << 32) | lo;
 }
 
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    const u32 lo = (u32)__shfl((int)(u32)v, src, 64), hi = (u32)__shfl((int)(u32)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+
+// a (value, present) pair's leftmost-best combination: the right one only when strictly better
+template <bool MIN>
+__device__ __forceinline__ void best_comb(u64& bv, bool& bh, u64 v, bool h) {
+    if (h && (!bh || d_worse<MIN>(bv, v))) { bv = v; bh = true; }
+}
+
+// The window indices of the deque loaded from the carried state: it must be the suffix-best chain of
+// the carried ring (no quirk in its history), entry by entry, with minValue at its front; false leaves
+// the key sequential.
+template <bool MIN>
+__device__ bool dq_index_init(const KDq& q, const u64* dv, int* di, const u64* rval, int rh0, int gm, int H0,
+                              int lane) {
+    if (q.spill || q.nan) return false;
+    if (q.len == 0) return H0 == 0;
+    if (!q.mmh || q.mm != dv[q.h & (kDqK - 1)]) return false;
+    int seen = 0;      // chain entries found in the blocks after the current one
+    u64 after = 0;     // best value after the current block
+    bool after_h = false, ok = true;
+    for (int b1 = H0; b1 > 0 && ok; b1 -= 64) {
+        const int b0 = b1 - 64 > 0 ? b1 - 64 : 0, h = b0 + lane;
+        const bool in = h < b1;
+        const u64 v = in ? rval[(rh0 + h) & gm] : 0;
+        if (__any(in && d_isnan(v))) return false;
+        // inclusive suffix best over the block's lanes (a numeric best: all the membership test needs)
+        u64 t = v;
+        bool th = in;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int src = lane + d < 64 ? lane + d : lane;
+            const u64 ov = shfl64(t, src);
+            const bool oh = lane + d < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+            if (oh && (!th || d_worse<MIN>(t, ov))) { t = ov; th = true; }
+        }
+        // best strictly after h: the next lane's suffix, then the later blocks
+        const int nx = lane + 1 < 64 ? lane + 1 : lane;
+        u64 nb = shfl64(t, nx);
+        bool nh = lane + 1 < 64 && __shfl(th ? 1 : 0, nx, 64) != 0;
+        if (after_h && (!nh || d_worse<MIN>(nb, after))) { nb = after; nh = true; }
+        const bool member = in && !(nh && d_worse<MIN>(v, nb));
+        const unsigned long long bal = __ballot(member);
+        const int above = lane == 63 ? 0 : __popcll(bal >> (lane + 1));
+        const int pos = q.len - 1 - seen - above;
+        bool bad = false;
+        if (member) {
+            if (pos < 0) bad = true;
+            else {
+                const int sl = (q.h + pos) & (kDqK - 1);
+                if (dv[sl] != v) bad = true;
+                else di[sl] = h;
+            }
+        }
+        ok = !__any(bad);
+        seen += __popcll(bal);
+        const u64 bv = shfl64(t, 0);
+        const bool bh = __shfl(th ? 1 : 0, 0, 64) != 0;
+        if (bh && (!after_h || d_worse<MIN>(after, bv))) { after = bv; after_h = true; }
+    }
+    return ok && seen == q.len;
+}
+
+// per lane: the result after its record — the first deque entry at or after lo_eff against the chunk's
+// records [max(lo_eff, S), S + lane] (leftmost best)
+template <bool MIN>
+__device__ __forceinline__ u64 par_best(const KDq& q, const u64* dv, const int* di, const u64* sx, u64 x, int lo_eff,
+                                         int S, bool in_from0, int lane) {
+    int a = 0, b = q.len;
+    while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (di[(q.h + mid) & (kDqK - 1)] < lo_eff) a = mid + 1;
+        else b = mid;
+    }
+    u64 pv = a < q.len ? dv[(q.h + a) & (kDqK - 1)] : 0;
+    bool ph = a < q.len;
+    u64 cv;
+    bool ch;
+    if (in_from0) {
+        // every lane's range starts at the chunk's first record: an inclusive prefix scan
+        cv = x;
+        ch = true;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u64 ov = shfl64(cv, lane >= d ? lane - d : lane);
+            const bool oh = lane >= d;
+            // left operand (earlier lanes) wins ties
+            if (oh && !d_worse<MIN>(ov, cv)) cv = ov;
+        }
+    } else {
+        ch = false;
+        cv = 0;
+        for (int j = lo_eff - S > 0 ? lo_eff - S : 0; j <= lane; j++) best_comb<MIN>(cv, ch, sx[j], true);
+    }
+    best_comb<MIN>(pv, ph, cv, ch);
+    return pv;
+}
+
+// the deque after the chunk (see above); false when it would not fit the LDS ring (nothing written)
+struct DqPlan {
+    int i0, i1, n_new;
+};
+template <bool MIN>
+__device__ __forceinline__ DqPlan dq_plan(const KDq& q, const u64* dv, const int* di, u64 x, bool in, int S,
+                                          int lo_end, int m, int lane, bool& surv) {
+    // chunk's best over all its records
+    u64 cb = x;
+    bool chh = in;
+    u64 sb = x;  // suffix best strictly after the lane
+    bool sbh = false;
+    {
+        u64 t = x;
+        bool th = in;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {  // inclusive suffix scan
+            const int src = lane + d < 64 ? lane + d : lane;
+            const u64 ov = shfl64(t, src);
+            const bool oh = lane + d < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+            if (oh && (!th || d_worse<MIN>(t, ov))) { t = ov; th = true; }
+        }
+        cb = shfl64(t, 0);
+        chh = __shfl(th ? 1 : 0, 0, 64) != 0;
+        const int src = lane + 1 < 64 ? lane + 1 : lane;
+        sb = shfl64(t, src);
+        sbh = lane + 1 < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+    }
+    surv = in && S + lane >= lo_end && !(sbh && d_worse<MIN>(x, sb));
+    DqPlan p;
+    int a = 0, b = q.len;
+    while (a < b) {
+        const int mid = (a + b) >> 1;
+        if (di[(q.h + mid) & (kDqK - 1)] < lo_end) a = mid + 1;
+        else b = mid;
+    }
+    p.i0 = a;
+    int c = a;
+    if (chh)
+        while (c < q.len && !d_worse<MIN>(dv[(q.h + c) & (kDqK - 1)], cb)) c++;
+    else
+        c = q.len;
+    p.i1 = c;
+    p.n_new = __popcll(__ballot(surv));
+    (void)m;
+    return p;
+}
+
+template <bool MIN>
+__device__ __forceinline__ void dq_commit(KDq& q, u64* dv, int* di, const DqPlan& p, u64 x, bool surv, int S,
+                                          int lane, u64 last_best) {
+    const unsigned long long bal = __ballot(surv);
+    const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (surv) {
+        const int sl = (q.h + p.i1 + rank) & (kDqK - 1);
+        dv[sl] = x;
+        di[sl] = S + lane;
+    }
+    __syncthreads();
+    q.h += p.i0;
+    q.len = p.i1 - p.i0 + p.n_new;
+    if (q.len > 0) {
+        q.f = dv[q.h & (kDqK - 1)];
+        q.b = dv[(q.h + q.len - 1) & (kDqK - 1)];
+    }
+    q.mm = last_best;
+    q.mmh = true;
+}
+
 // AOS: the records are read in key order through the sort's rank list from the 48-byte records
-// (SlRecords.aos), the lanes write the key-order (PM, value) columns the window-head reads use, and
-// the first-record flags / key-order positions the emit needs (what k_sl_kgather did in a pass of
-// its own, with five scattered 8-byte reads per record).
-template <bool HSUM, bool HMIN, bool HMAX, bool AOS>
-__global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, const i64* __restrict__ g_clk,
-                                               i64* __restrict__ g_pm, u64* __restrict__ g_v,
-                                               const i64* __restrict__ g_ts, const u32* __restrict__ g_raw,
-                                               const u32* __restrict__ g_rank, SlState S, DFields fd, KOut ko, i64 T,
+// (SlRecords.aos); the lanes write the key-order (PM, value) columns the window-head reads use, and
+// the first-record flags / key-order positions the emit needs.
+template <bool HSUM, bool HMIN, bool HMAX>
+__global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, i64* __restrict__ g_pm,
+                                               u64* __restrict__ g_v, SlState S, DFields fd, KOut ko, i64 T,
                                                u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
                                                unsigned char* __restrict__ flags, u32* __restrict__ inv) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
+    __shared__ int di_min[HMIN ? kDqK : 1];
+    __shared__ int di_max[HMAX ? kDqK : 1];
     __shared__ i64 s_pm[kWS];
+    __shared__ u64 s_x[64];
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= nslots) return;
@@ -1663,10 +1621,16 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
         if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
     }
+    __syncthreads();
+    // the parallel min / max needs the deque entries' window indices
+    bool par = HMIN || HMAX;
+    if (HMIN && par) par = dq_index_init<true>(qn, dq_min, di_min, rval, rh0, gm, H0, lane);
+    if (HMAX && par) par = dq_index_init<false>(qx, dq_max, di_max, rval, rh0, gm, H0, lane);
+    __syncthreads();
     int hj = 0;         // heads expired so far
     int open_row = 0;   // key-order index of the (send, key) row open at the chunk start
     i64 last_send = 0;
-    u32 prev_raw = 0;   // (AOS) the previous chunk's last record
+    u32 prev_raw = 0;   // the previous chunk's last record
     for (int o0 = 0; o0 < n; o0 += 64) {
         const int m = min(64, n - o0);
         const bool in = lane < m;
@@ -1674,7 +1638,7 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         i64 clk, ts;
         u64 x;
         u32 raw, rk;
-        if (AOS) {
+        {
             const u32 r = sorted_rank[i];
             const ulonglong2* rp = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
             const ulonglong2 w0 = rp[0], w1 = rp[1], w2 = rp[2];
@@ -1693,15 +1657,10 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                 flags[r] = fst ? 1 : 0;
                 if (fst) inv[r] = i;
             }
+            s_x[lane] = x;
             prev_raw = __shfl(raw, m - 1, 64);
             __threadfence_block();  // this chunk's own records may expire within it
             __syncthreads();
-        } else {
-            clk = g_clk[i];
-            x = g_v[i];
-            ts = g_ts[i];
-            raw = g_raw[i];
-            rk = g_rank[i];
         }
         const int hb = hj;
         // the next kWS window heads: PM in LDS (the lanes' binary searches), values in two registers
@@ -1718,13 +1677,69 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             if (pm + T <= clk) lo = mid + 1;
             else hi = mid;
         }
+        // the effective expiry point of each record: the running max over the earlier lanes
+        int lo_eff = in ? lo : hb;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int up = __shfl_up(lo_eff, d, 64);
+            if (lane >= d) lo_eff = max(lo_eff, up);
+        }
+        const int Sx = H0 + o0;  // window index of the chunk's first record
+        u64 r_mn = 0, r_mx = 0;
+        u32 r_fl = 0;
+        bool pc = par;  // this chunk's min / max in parallel
+        DqPlan pn{}, px{};
+        bool sn = false, sx_ = false;
+        if (pc) {
+            const int lo_end = __builtin_amdgcn_readlane(lo_eff, m - 1);
+            const int ne = lo_end - hb;
+            pc = ne <= kWS && !__any(in && d_isnan(x));
+            if (pc) {
+                // the quirk check: an expiring head meeting a bit-equal value of another event among the
+                // deque entries or the chunk's records
+                bool dirty = false;
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int d = lane + 64 * t;
+                    if (d >= ne) continue;
+                    const u64 v = t ? hv1 : hv0;
+                    const int idx = hb + d;
+                    if (HMIN)
+                        for (int e = 0; e < qn.len; e++) {
+                            const int sl = (qn.h + e) & (kDqK - 1);
+                            dirty |= dq_min[sl] == v && di_min[sl] != idx;
+                        }
+                    if (HMAX)
+                        for (int e = 0; e < qx.len; e++) {
+                            const int sl = (qx.h + e) & (kDqK - 1);
+                            dirty |= dq_max[sl] == v && di_max[sl] != idx;
+                        }
+                    for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
+                }
+                pc = !__any(dirty);
+            }
+            if (pc) {
+                const bool from0 = !__any(in && lo_eff > Sx);
+                if (HMIN) r_mn = par_best<true>(qn, dq_min, di_min, s_x, x, lo_eff, Sx, from0, lane);
+                if (HMAX) r_mx = par_best<false>(qx, dq_max, di_max, s_x, x, lo_eff, Sx, from0, lane);
+                if (HMIN) pn = dq_plan<true>(qn, dq_min, di_min, x, in, Sx, lo_end, m, lane, sn);
+                if (HMAX) px = dq_plan<false>(qx, dq_max, di_max, x, in, Sx, lo_end, m, lane, sx_);
+                pc = (!HMIN || pn.i1 - pn.i0 + pn.n_new <= kDqK) && (!HMAX || px.i1 - px.i0 + px.n_new <= kDqK);
+            }
+            if (pc) {
+                if (HMIN) dq_commit<true>(qn, dq_min, di_min, pn, x, sn, Sx, lane, rl64(r_mn, m - 1));
+                if (HMAX) dq_commit<false>(qx, dq_max, di_max, px, x, sx_, Sx, lane, rl64(r_mx, m - 1));
+                r_fl = 3;
+            } else {
+                par = false;  // the sequential deque takes over for the rest of the push
+            }
+        }
         // The order-dependent part, run by the whole wave in lockstep on wave-uniform values (so the
         // compiler keeps the running state scalar): each record's expiry point and value, and the
         // expiring heads' values, come from other lanes' registers by readlane instead of LDS, and
         // record q's results land in lane q's registers (a select, no LDS store).
         i64 r_cnt = 0;
-        u64 r_sum = 0, r_mn = 0, r_mx = 0;
-        u32 r_fl = 0;
+        u64 r_sum = 0;
         {
             int h = hb;
             for (int q = 0; q < m; q++) {
@@ -1737,20 +1752,26 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                         sum = sum - __longlong_as_double((i64)v);
                         if (cnt == 0 && sum == 0.0) sum = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
                     }
-                    if (HMIN) kdq_remove<true, 1>(qn, gmin, gm, dq_min, v);
-                    if (HMAX) kdq_remove<false, 1>(qx, gmax, gm, dq_max, v);
+                    if (!pc) {
+                        if (HMIN) kdq_remove<true, 1>(qn, gmin, gm, dq_min, v);
+                        if (HMAX) kdq_remove<false, 1>(qx, gmax, gm, dq_max, v);
+                    }
                 }
                 const u64 xq = rl64(x, q);  // the event joins the window (processAdd)
                 cnt++;
                 if (HSUM) sum = sum + __longlong_as_double((i64)xq);
-                if (HMIN) kdq_add<true, 1>(qn, gmin, gm, dq_min, xq);
-                if (HMAX) kdq_add<false, 1>(qx, gmax, gm, dq_max, xq);
+                if (!pc) {
+                    if (HMIN) kdq_add<true, 1>(qn, gmin, gm, dq_min, xq);
+                    if (HMAX) kdq_add<false, 1>(qx, gmax, gm, dq_max, xq);
+                }
                 if (lane == q) {
                     r_cnt = cnt;
                     r_sum = (u64)__double_as_longlong(sum);
-                    r_mn = qn.mm;
-                    r_mx = qx.mm;
-                    r_fl = (qn.mmh ? 1u : 0u) | (qx.mmh ? 2u : 0u);
+                    if (!pc) {
+                        r_mn = qn.mm;
+                        r_mx = qx.mm;
+                        r_fl = (qn.mmh ? 1u : 0u) | (qx.mmh ? 2u : 0u);
+                    }
                 }
             }
             hj = h;
@@ -1887,9 +1908,8 @@ bool sliding_keyed_ok(AggPlan ap) {
 int sliding_keyed_row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
 
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
-                          const u32* sorted_slot, i64 M, SlRecords rec, i64* g_clk, i64* g_pm, u64* g_v, i64* g_ts,
-                          u32* g_raw, u32* g_rank, u32* inv, SlState S, AggPlan ap, i64 T, i64 send_size,
-                          i64 send_base, u64* rowsK, unsigned char* flags) {
+                          SlRecords rec, i64* g_pm, u64* g_v, u32* inv, SlState S, AggPlan ap, i64 T,
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags) {
     DFields fd;
     own_d_fields(ap, fd);
     KOut ko{};
@@ -1903,59 +1923,19 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
     launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
-    static const bool lane_per_key = getenv("SH_SL_LANE_PER_KEY") != nullptr;  // the round-2 kernel
-    if (!lane_per_key) {
-        const int RWw = sliding_keyed_row_words(ap.n);
-        const bool AO = rec.aos != nullptr;
-        if (!AO)
-            hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                               sorted_rank, sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
-#define SH_SL_W1(A, B, C, D)                                                                                          \
-    hipLaunchKernelGGL((k_sl_wkey<A, B, C, D>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, \
-                       g_ts, g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RWw, sorted_rank, rec.aos, flags, inv)
-#define SH_SL_W(A, B, C)                 \
-    do {                                 \
-        if (AO) SH_SL_W1(A, B, C, true); \
-        else SH_SL_W1(A, B, C, false);   \
-    } while (0)
-        if (hs && hn && hx) SH_SL_W(true, true, true);
-        else if (hs && !hn && !hx) SH_SL_W(true, false, false);
-        else if (!hs && hn && hx) SH_SL_W(false, true, true);
-        else if (hs && hn) SH_SL_W(true, true, false);
-        else if (hs && hx) SH_SL_W(true, false, true);
-        else if (hn && !hx) SH_SL_W(false, true, false);
-        else if (hx && !hn) SH_SL_W(false, false, true);
-        else SH_SL_W(false, false, false);
-#undef SH_SL_W
-#undef SH_SL_W1
-        return;
-    }
-    hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank,
-                       sorted_slot, M, rec, ss, g_clk, g_pm, g_v, g_ts, g_raw, g_rank, flags, inv);
-    static const int kl_env = getenv("SH_SL_KL") ? atoi(getenv("SH_SL_KL")) : 16;
-    const int KLr = kl_env == 8 || kl_env == 32 || kl_env == 64 ? kl_env : 16;
-    const unsigned grid = (unsigned)((n + KLr - 1) / KLr);
     const int RW = sliding_keyed_row_words(ap.n);
-#define SH_SL_K1(A, B, C, KLV)                                                                                      \
-    hipLaunchKernelGGL((k_sl_key<A, B, C, KLV>), dim3(grid), dim3(64), 0, s, key_off, (u32)n, g_clk, g_pm, g_v, g_ts, \
-                       g_raw, g_rank, S, fd, ko, T, ss, send_base, rowsK, RW)
-#define SH_SL_K(A, B, C)                                                                                            \
-    do {                                                                                                            \
-        if (KLr == 8) SH_SL_K1(A, B, C, 8);                                                                          \
-        else if (KLr == 32) SH_SL_K1(A, B, C, 32);                                                                   \
-        else if (KLr == 64) SH_SL_K1(A, B, C, 64);                                                                   \
-        else SH_SL_K1(A, B, C, 16);                                                                                  \
-    } while (0)
-    if (hs && hn && hx) SH_SL_K(true, true, true);
-    else if (hs && !hn && !hx) SH_SL_K(true, false, false);
-    else if (!hs && hn && hx) SH_SL_K(false, true, true);
-    else if (hs && hn) SH_SL_K(true, true, false);
-    else if (hs && hx) SH_SL_K(true, false, true);
-    else if (hn && !hx) SH_SL_K(false, true, false);
-    else if (hx && !hn) SH_SL_K(false, false, true);
-    else SH_SL_K(false, false, false);
-#undef SH_SL_K
-#undef SH_SL_K1
+#define SH_SL_W(A, B, C)                                                                                            \
+    hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_pm, g_v, S, fd, ko, \
+                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags, inv)
+    if (hs && hn && hx) SH_SL_W(true, true, true);
+    else if (hs && !hn && !hx) SH_SL_W(true, false, false);
+    else if (!hs && hn && hx) SH_SL_W(false, true, true);
+    else if (hs && hn) SH_SL_W(true, true, false);
+    else if (hs && hx) SH_SL_W(true, false, true);
+    else if (hn && !hx) SH_SL_W(false, true, false);
+    else if (hx && !hn) SH_SL_W(false, false, true);
+    else SH_SL_W(false, false, false);
+#undef SH_SL_W
 }
 
 int sliding_keys_per_partition(AggPlan ap) {

@@ -304,6 +304,7 @@ static int rate_restore(sh_query* q, Reader& rd) {
 
 static int query_snapshot_blob(sh_query* q, Writer& w) {
     if (q->given) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of a sharded owner: snapshot the sh_shard instead");
+    RCHK(query_drain_async(q));
     w.put("SHQ1", 4);
     w.val<uint32_t>(kVersion);
     w.val<uint64_t>(fingerprint(q));
@@ -334,6 +335,7 @@ static int query_restore_blob(sh_query* q, const void* buf, int64_t len) {
     if (r.val<uint32_t>() != kVersion) return sh_fail(SH_ERR_INVALID, "snapshot version mismatch");
     if (r.val<uint64_t>() != fingerprint(q)) return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different query");
     if (r.val<uint32_t>() != (uint32_t)q->kind) return sh_fail(SH_ERR_INVALID, "snapshot kind mismatch");
+    RCHK(query_drain_async(q));  // a queued report must not land on the restored counters
     (void)hipStreamSynchronize(q->ctx->stream);
     RCHK(q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r));
     return rate_restore(q, r);

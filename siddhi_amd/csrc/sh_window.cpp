@@ -48,17 +48,18 @@ int StagedBatch::stage(hipStream_t s, const sh_batch* b, int n_cols, const int32
     {
         auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
         const char* base = (const char*)b->ts;
-        size_t off = a16(n * 8), offs[SH_MAX_COLS] = {};
+        size_t off = a16(n * 8), offs[SH_MAX_COLS] = {}, end = n * 8;
         bool contig = true;
         for (int c = 0; c < n_cols && contig; c++) {
             if (!b->cols[c]) continue;
             contig = (const char*)b->cols[c] == base + off;
             offs[c] = off;
-            off = a16(off + n * type_size(types[c]));
+            end = off + n * type_size(types[c]);  // the copy stops at the last column's last value
+            off = a16(end);
         }
         if (contig) {
             RCHK(blk.reserve(off, false));
-            HIPCHK(hipMemcpyAsync(blk.p, base, off, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(blk.p, base, end, hipMemcpyHostToDevice, s));
             dev->ts = blk.as<int64_t>();
             for (int c = 0; c < n_cols; c++) dev->cols[c] = b->cols[c] ? blk.as<char>() + offs[c] : nullptr;
             return SH_OK;
@@ -976,8 +977,13 @@ static int small_verify(sh_query* q, bool wait) {
     uint32_t ctrl[4];
     for (int i = 0; i < 4; i++) ctrl[i] = r->ctrl[i];
     q->async_tok = 0;
+    q->async_keys = 0;
     return q->kt.check_result(ctrl);
 }
+
+// every queued asynchronous small push verified (snapshot, restore and destroy read or replace the
+// state its report describes)
+int query_drain_async(sh_query* q) { return small_verify(q, true); }
 
 // Asynchronous small push (InputHandler.send returning once the junction has the events,
 // StreamJunction :104-131): a zero-copy batch of a query without a filter whose timestamps do not
@@ -988,6 +994,9 @@ static int small_async(sh_query* q, bool* done) {
     const sh_batch* hb = q->zc_host;
     const int64_t N = hb->n;
     if (filter_kind(q->fp) != 0 || getenv("SH_NO_ASYNC_SMALL")) return SH_OK;
+    // a hashed key table may take at most one new key per event: only while that bound stays within
+    // the table's half (the growth threshold, checked on verified counts) is the push queued unverified
+    if (!q->kt.dense && q->kt.n_keys + q->async_keys + N > (int64_t)q->kt.size_ / 2) return SH_OK;
     const int64_t* hts = hb->ts;
     for (int64_t i = 1; i < N; i++)
         if (hts[i] < hts[i - 1]) return SH_OK;
@@ -1055,6 +1064,7 @@ static int small_async(sh_query* q, bool* done) {
     q->zc_tok[slot] = token;
     q->zc_next = (slot + 1) % sh_query::kZcRing;
     q->async_tok = token;
+    q->async_keys += N;
     q->n_pend += N;  // no filter: every event joins the open window
     q->seq += N;
     q->clock = clk;
@@ -1150,10 +1160,14 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
     if (N < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (N > 0 && (!b->ts)) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
     if (q->n_pend + N >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 4G events");
-    if (N > 0 && !q->internal_keys && q->kt.n_keys > (int64_t)q->kt.size_ / 2) RCHK(query_reserve_keys(q, 0));
+    RCHK(small_verify(q, false));
+    if (N > 0 && !q->internal_keys && q->kt.n_keys + q->async_keys > (int64_t)q->kt.size_ / 2) {
+        // unverified asynchronous pushes may have added keys: their report first, then the growth check
+        RCHK(small_verify(q, true));
+        if (q->kt.n_keys > (int64_t)q->kt.size_ / 2) RCHK(query_reserve_keys(q, 0));
+    }
     {
         bool done = false;
-        RCHK(small_verify(q, false));
         RCHK(try_small_push(q, b, &done));
         if (done) {
             finish_out(q, host_out, out);
@@ -1520,6 +1534,7 @@ int sh_advance_time_device(sh_query* q, int64_t now, const sh_out** out) {
 extern "C" int sh_query_destroy(sh_query* q) {
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q) return SH_OK;
+    (void)small_verify(q, true);  // the queued appends read the ring and pending buffers freed below
     (void)hipStreamSynchronize(q->ctx->stream);
     (void)hipStreamSynchronize(q->ctx->copy_stream);
     {

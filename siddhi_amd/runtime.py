@@ -300,7 +300,9 @@ class PinnedBatch:
     """An sh_batch whose SoA columns live in one pinned host block (sh_alloc_pinned): what the Java shim
     packs a ComplexEventChunk into. For n events the block holds ts[n], then every column's n values,
     each run 16-byte aligned — one contiguous region, so sh_stage moves it with a single H2D copy.
-    `fill` copies numpy columns in (laying the block out for their length); `arrays` are the views."""
+    `fill` copies numpy columns in (laying the block out for their length); `arrays` are the views of the
+    current layout and are valid only until the next `fill` / `set_n` re-lays the block out. A caller that
+    writes `arrays` directly (laid out for the capacity at construction) calls `set_n(n)` afterwards."""
 
     def __init__(self, schema: abi.Schema, capacity: int, send_size: int = 0):
         self.schema = schema
@@ -327,6 +329,7 @@ class PinnedBatch:
 
     def _layout(self, n):
         base, off = self._ptrs[0].value, 0
+        self._laid = n
         self.arrays = []
         for dt in self._dts:
             buf = (C.c_char * max(1, n * dt.itemsize)).from_address(base + off)
@@ -336,6 +339,17 @@ class PinnedBatch:
             else:
                 self.b.cols[len(self.arrays) - 2] = base + off
             off = self._a16(off + n * dt.itemsize)
+
+    def set_n(self, n: int):
+        """The batch holds the first n events written into `arrays`: the columns move to their places in
+        the n-event layout (nothing moves when the block is already laid out for n)."""
+        assert n <= self.capacity
+        if n != self._laid:
+            keep = [a[:n].copy() for a in self.arrays]
+            self._layout(n)
+            for a, k in zip(self.arrays, keep):
+                a[:] = k
+        self.b.n = n
 
     def fill(self, ts, cols, send_size=None):
         n = len(ts)

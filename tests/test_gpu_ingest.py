@@ -122,3 +122,33 @@ def test_async_small_pushes_then_unstaged_pushes_and_advance(rt):
         b.close()
     g.close()
     o.close()
+
+
+def test_async_small_pushes_hashed_keys_grow_the_table(rt):
+    """int group keys (a hashed, growable key table): asynchronous small pushes that bring ever new keys.
+    A push is queued unverified only while the verified key count plus one key per queued event stays
+    within half the table; past that the reports are waited for and the table grows first. Also a
+    snapshot and restore right after queued pushes (the reports are drained first)."""
+    schema = abi.Schema.parse("k int, v double, ts long")
+    n = 120_000
+    rng = np.random.default_rng(5)
+    ts = (np.arange(n) // 2 + 1_000).astype(np.int64)  # 4,000 events per window
+    k = (np.arange(n) * 7 + rng.integers(0, 3, n)).astype(np.int32)  # mostly new keys: dead keys pile up
+    v = rng.integers(-100, 100, n).astype(np.float64)
+    cols = [k, v, ts.copy()]
+    spec = abi.QuerySpec(schema, "timeBatch", 2_000, group_by=["k"], aggs=[("count", None), ("sum", "v")],
+                         key_capacity=5_000)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    bufs = [rt.PinnedBatch(schema, 1000) for _ in range(2)]
+    parts, want = [], []
+    for i, a in enumerate(range(0, n, 1000)):
+        sl = slice(a, a + 1000)
+        parts.append(abi.out_arrays(g.push_staged_raw(g.stage(bufs[i % 2].fill(ts[sl], [c[sl] for c in cols], 1)))))
+        want.append(abi.out_arrays(o.push_raw(abi.HostBatch(schema, ts[sl], [c[sl] for c in cols], 1))))
+        if i == 40:
+            g.restore(g.snapshot())
+    assert_same(abi.concat_arrays(parts), abi.concat_arrays(want), label="async hashed keys")
+    for b in bufs:
+        b.close()
+    g.close()
+    o.close()
