@@ -465,8 +465,8 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     if (a->has_bucket && d->n_group_by == 1 && d->col_types[d->group_by[0]] == SH_T_STRID) {
         // ids per bucket row: the GPU's share of the dictionary (sharded owners hold the ids = rank mod G)
         const int64_t cap = rd.key_capacity, per = shard ? (cap + world - 1) / world : cap;
-        static const char* env_rows = getenv("SH_AGG_BAND_ROWS");  // A/B switch (0 = hash keys only)
-        uint32_t lk = 4, rows = env_rows ? (uint32_t)atoi(env_rows) : 8u;
+        // (A/B switch SH_AGG_BAND_ROWS, 0 = hash keys only)
+        uint32_t lk = 4, rows = (uint32_t)std::max(0, Tuning::from_env().agg_band_rows);
         while (((int64_t)1 << lk) < per) lk++;
         while (rows > 4 && ((int64_t)rows << lk) > (8 << 20)) rows >>= 1;
         if (rows >= 2 && ((int64_t)rows << lk) <= (8 << 20)) {

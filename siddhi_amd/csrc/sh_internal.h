@@ -129,6 +129,7 @@ struct WinParams {
     // the ts_col attribute over the events reaching the window; xm0 = that max before the push
     int ts_col, start_col;
     i64 xm0;
+    int rec_seq;  // sliding records: the lane-strided form (k_sl_records_seq) where it applies
 };
 
 // Result of the block-aggregate scan (written by k_scan_blocks, read back by the host).

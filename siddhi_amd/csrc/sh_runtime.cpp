@@ -213,6 +213,17 @@ extern "C" int sh_free_pinned(void* p) {
 extern "C" const char* sh_last_error(void) { return g_last_error.c_str(); }
 extern "C" int32_t sh_abi_version(void) { return SH_ABI_VERSION; }
 
+Tuning Tuning::from_env() {
+    Tuning t;
+    auto on = [](const char* n) { const char* v = getenv(n); return v && *v && strcmp(v, "0") != 0; };
+    t.direct_pos = on("SH_DIRECT_POS");
+    t.part_keys_1024 = getenv("SH_PART_KEYS") && atoi(getenv("SH_PART_KEYS")) == 1024;
+    t.no_async_small = on("SH_NO_ASYNC_SMALL");
+    t.sl_records_seq = on("SH_SL_RECORDS_SEQ");
+    if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
+    return t;
+}
+
 extern "C" int sh_query_set_strings(sh_query* q, int32_t col, int64_t first_id, int64_t n, const uint16_t* units,
                                     const int64_t* offsets) {
     if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_strings: NULL query");

@@ -222,8 +222,18 @@ using shd::TileMap;
 
 struct SlidingImpl;
 
+// A/B switches of the measured alternatives, read from the environment once per query,
+// when it is created, so a process can run queries with different settings side by side:
+// SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n
+struct Tuning {
+    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false;
+    int agg_band_rows = 8;
+    static Tuning from_env();
+};
+
 struct sh_query {
-    int kind = 0;            // 0 = batch window (lengthBatch/timeBatch), 1 = sliding time window
+    int kind = 0;
+    Tuning tune = Tuning::from_env();            // 0 = batch window (lengthBatch/timeBatch), 1 = sliding time window
     SlidingImpl* sl = nullptr;
     // text of dictionary ids per string column (sh_query_set_strings), UTF-16 as Java holds it
     std::unordered_map<int, std::vector<std::u16string>> strings;

@@ -243,6 +243,7 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     wp.clock0 = q->clock;
     wp.send_size = b->send_size;
     wp.N = N;
+    wp.rec_seq = q->tune.sl_records_seq;
     launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                      s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
     // records of all passing events (capacity N; the exact count is known after the prefix scan)

@@ -182,8 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
                        i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock) {
-    if (filter_kind(f) == 0 && wp.send_size == 1 && wp.kind == SH_WIN_TIME && ap.n_vcols >= 1 &&
-        getenv("SH_SL_RECORDS_SEQ")) {
+    if (filter_kind(f) == 0 && wp.send_size == 1 && wp.kind == SH_WIN_TIME && ap.n_vcols >= 1 && wp.rec_seq) {
         hipLaunchKernelGGL(k_sl_records_seq, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap, blk_pass_pre,
                            blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
         return;

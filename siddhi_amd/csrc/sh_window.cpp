@@ -132,7 +132,7 @@ static int size_partitions(sh_query* q) {
     int P = 1;
     // local keys per partition: at most 512 (one per thread of k_aggregate_own) or, for experiments,
     // 1024 (two per thread) — SH_PART_KEYS
-    static const size_t nl_max = getenv("SH_PART_KEYS") && atoi(getenv("SH_PART_KEYS")) == 1024 ? 1024 : 512;
+    const size_t nl_max = q->tune.part_keys_1024 ? 1024 : 512;
     while (ts / P > nl_max && P < 16384 && scatter_fits(P << 1)) P <<= 1;
     if (ts / P > nl_max) return sh_fail(SH_ERR_UNSUPPORTED, "key capacity too large for one GPU (shard the query over GPUs)");
     q->P = P;
@@ -301,7 +301,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
 static bool want_direct_pos(const sh_query* q) {
     // opt-in (SH_DIRECT_POS=1): measured slower on MI355X — k_ms_scatter 290 vs 236 us per C2 push
     // reading the key column instead of the slot column k_boundaries writes (profiles/r03_c2_v3*)
-    if (!getenv("SH_DIRECT_POS")) return false;
+    if (!q->tune.direct_pos) return false;
     const int kc = q->kp.n == 1 ? q->kp.col[0] : -1;
     return q->kt.dense && q->kt.dmul == 1 && q->kt.dadd == 0 && kc >= 0 && q->kp.div[0] == 0 &&
            (q->load_type[kc] == SH_T_STRID || q->load_type[kc] == SH_T_INT) && filter_kind(q->fp) == 0 &&
@@ -993,7 +993,7 @@ int query_drain_async(sh_query* q) { return small_verify(q, true); }
 static int small_async(sh_query* q, bool* done) {
     const sh_batch* hb = q->zc_host;
     const int64_t N = hb->n;
-    if (filter_kind(q->fp) != 0 || getenv("SH_NO_ASYNC_SMALL")) return SH_OK;
+    if (filter_kind(q->fp) != 0 || q->tune.no_async_small) return SH_OK;
     // a hashed key table may take at most one new key per event: only while that bound stays within
     // the table's half (the growth threshold, checked on verified counts) is the push queued unverified
     if (!q->kt.dense && q->kt.n_keys + q->async_keys + N > (int64_t)q->kt.size_ / 2) return SH_OK;
