@@ -19,6 +19,7 @@
 // Nodes are slots of a pool addressed by int32 (-1 = null); a node's payload is the partition's slot.
 #pragma once
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -88,6 +89,75 @@ class JavaStringMap {
         for (int32_t e = bins_[b]; e != it->second; e = nd_[e].next) ++pos;
         *r = ((int64_t)b << 32) | pos;
         return true;
+    }
+
+    // the whole table (nodes, links, free list), so a checkpoint restores the iteration order exactly
+    void save(std::vector<uint8_t>& out) const {
+        auto put = [&](const void* p, size_t n) { out.insert(out.end(), (const uint8_t*)p, (const uint8_t*)p + n); };
+        const int32_t hdr[4] = {count_, threshold_, (int32_t)bins_.size(), (int32_t)nd_.size()};
+        put(hdr, sizeof(hdr));
+        put(bins_.data(), bins_.size() * 4);
+        for (const N& z : nd_) {
+            const int32_t w[7] = {z.hash, (int32_t)z.slot, z.next, z.prev, z.up, z.lo, z.hi};
+            const uint8_t fl = (z.tree ? 1 : 0) | (z.red ? 2 : 0);
+            const uint32_t len = (uint32_t)z.key.size();
+            put(w, sizeof(w));
+            put(&fl, 1);
+            put(&len, 4);
+            put(z.key.data(), len * 2);
+        }
+        const int32_t nf = (int32_t)free_.size();
+        put(&nf, 4);
+        put(free_.data(), free_.size() * 4);
+    }
+
+    bool load(const uint8_t* p, size_t n) {
+        size_t o = 0;
+        auto get = [&](void* d, size_t k) {
+            if (o + k > n) return false;
+            std::memcpy(d, p + o, k);
+            o += k;
+            return true;
+        };
+        int32_t hdr[4];
+        if (!get(hdr, sizeof(hdr)) || hdr[2] < 0 || hdr[3] < 0 || (hdr[2] & (hdr[2] - 1))) return false;
+        JavaStringMap m;
+        m.count_ = hdr[0];
+        m.threshold_ = hdr[1];
+        m.bins_.resize((size_t)hdr[2]);
+        if (!get(m.bins_.data(), m.bins_.size() * 4)) return false;
+        m.nd_.resize((size_t)hdr[3]);
+        for (N& z : m.nd_) {
+            int32_t w[7];
+            uint8_t fl;
+            uint32_t len;
+            if (!get(w, sizeof(w)) || !get(&fl, 1) || !get(&len, 4) || len > (1u << 24)) return false;
+            z.hash = w[0]; z.slot = (uint32_t)w[1]; z.next = w[2]; z.prev = w[3]; z.up = w[4]; z.lo = w[5]; z.hi = w[6];
+            z.tree = fl & 1;
+            z.red = (fl & 2) != 0;
+            z.key.resize(len);
+            if (!get(&z.key[0], (size_t)len * 2)) return false;
+        }
+        int32_t nf;
+        if (!get(&nf, 4) || nf < 0 || nf > hdr[3]) return false;
+        m.free_.resize((size_t)nf);
+        if (!get(m.free_.data(), m.free_.size() * 4)) return false;
+        std::vector<char> is_free(m.nd_.size(), 0);
+        for (int32_t f : m.free_) {
+            if (f < 0 || f >= hdr[3]) return false;
+            is_free[(size_t)f] = 1;
+        }
+        for (size_t i = 0; i < m.nd_.size(); i++)
+            if (!is_free[i]) m.by_key_[m.nd_[i].key] = (int32_t)i;
+        if ((int32_t)m.by_key_.size() != m.count_) return false;
+        *this = std::move(m);
+        return true;
+    }
+
+    template <class F>
+    void visit_keys(F f) const {
+        for (int32_t head : bins_)
+            for (int32_t e = head; e != NIL; e = nd_[e].next) f(nd_[e].slot, nd_[e].key);
     }
 
     template <class F>

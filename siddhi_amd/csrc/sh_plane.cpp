@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -344,7 +345,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
     if (!tm) {
         launch_pl_walk_lb(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, T, q->seq, state_of(s),
                           s->pl_last_ts.as<int64_t>(), s->pl_last_seq.as<int64_t>(), s->pl_prev_seq.as<int64_t>(), q->ap,
-                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+                          q->d.current_on, q->d.expired_on, q->d.stream_current, rows, s->flags.as<unsigned char>());
     } else {
         if (b) {
             RCHK(s->pl_start.reserve(cap + 16, false));
@@ -415,4 +416,78 @@ int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out
 
 int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out) {
     return plane_run(q, nullptr, now, host_out, out);
+}
+
+// ---- checkpoint of the partition lanes (sh_snapshot.cpp): per slot the lanes' device state beside the
+// sliding state buffers, and on the host the Scheduler — every partition's pending notify times and
+// PartitionStateHolder.states as a java.util.HashMap structure (its iteration order is its history) ----
+void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs) {
+    SlidingImpl* s = q->sl;
+    const size_t n = (size_t)s->nslots;
+    bufs = {{&s->pl_last_ts, n * 8}, {&s->pl_last_seq, n * 8}, {&s->pl_prev_seq, n * 8}, {&s->pl_key, n * 8}};
+    if (s->lane == 2) bufs.push_back({&s->rg, n * (size_t)s->rc * 8});
+}
+
+void plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
+    SlidingImpl* s = q->sl;
+    auto put = [&](const void* p, size_t k) { out.insert(out.end(), (const uint8_t*)p, (const uint8_t*)p + k); };
+    // pending notify times by slot, in slot order (the armed set is their fronts)
+    std::vector<uint32_t> slots;
+    for (auto& kv : s->pl_pend) slots.push_back(kv.first);
+    std::sort(slots.begin(), slots.end());
+    const uint64_t np = slots.size();
+    put(&np, 8);
+    for (uint32_t sl : slots) {
+        const auto& d = s->pl_pend[sl];
+        const uint64_t len = d.size();
+        put(&sl, 4);
+        put(&len, 8);
+        for (int64_t t : d) put(&t, 8);
+    }
+    std::vector<uint8_t> m;
+    s->pl_states.save(m);
+    const uint64_t ml = m.size();
+    put(&ml, 8);
+    put(m.data(), m.size());
+}
+
+int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
+    SlidingImpl* s = q->sl;
+    size_t o = 0;
+    auto get = [&](void* d, size_t k) {
+        if (o + k > n) return false;
+        std::memcpy(d, p + o, k);
+        o += k;
+        return true;
+    };
+    std::unordered_map<uint32_t, std::deque<int64_t>> pend;
+    std::set<std::pair<int64_t, uint32_t>> armed;
+    uint64_t np = 0;
+    if (!get(&np, 8) || np > (uint64_t)s->nslots) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    for (uint64_t i = 0; i < np; i++) {
+        uint32_t sl;
+        uint64_t len;
+        if (!get(&sl, 4) || !get(&len, 8) || sl >= (uint64_t)s->nslots || len == 0 || len > n)
+            return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        auto& d = pend[sl];
+        for (uint64_t j = 0; j < len; j++) {
+            int64_t t;
+            if (!get(&t, 8)) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+            d.push_back(t);
+        }
+        armed.insert(std::make_pair(d.front(), sl));
+    }
+    uint64_t ml = 0;
+    if (!get(&ml, 8) || o + ml > n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    shj::JavaStringMap m;
+    if (!m.load(p + o, (size_t)ml)) return sh_fail(SH_ERR_INVALID, "snapshot: scheduler state unreadable");
+    o += ml;
+    std::unordered_map<uint32_t, std::u16string> flow;
+    m.visit_keys([&](uint32_t slot, const std::u16string& k) { flow[slot] = k; });
+    s->pl_pend = std::move(pend);
+    s->pl_armed = std::move(armed);
+    s->pl_states = std::move(m);
+    s->pl_flow = std::move(flow);
+    *used = o;
+    return SH_OK;
 }

@@ -88,11 +88,18 @@ __device__ __forceinline__ void p_write_row(SlxRows rows, const AggPlan& ap, i64
 // batch's events as EXPIRED: the key's row then is that batch removed again (count 0, the others
 // null), re-stamped with the flush clock and represented by its last event — unless current events
 // follow, whose row replaces it (LinkedHashMap.put keeps one row per key). ----------------------------
+//
+// lengthBatch(L, true) (stream.current.event, processStreamCurrentEvents :245-274): every event is a chunk
+// of its own and emits the partition's running aggregates; the (L + 1)-th event of a batch starts the
+// next one — its chunk is [the previous batch's events as EXPIRED, RESET, the event], and the selector
+// without group-by (or grouped by the partition key: one key) keeps the chunk's last qualifying event
+// (processInBatchNoGroupBy :271-313): the current one, or with `insert expired events` the batch's last
+// event removed again (count 0, the others null, stamped with the send's clock).
 template <int NA, int NV>
 __global__ __launch_bounds__(64) void k_pl_walk_lb(const u32* __restrict__ key_off, const u32* __restrict__ sorted_rank,
                                                    u32 nslots, SlRecords rec, i64 L, i64 seq_base, SlState S,
                                                    i64* last_ts, i64* last_seq, i64* prev_seq, AggPlan ap, int cur_on,
-                                                   int exp_on, SlxRows rows, unsigned char* flags) {
+                                                   int exp_on, int sc, SlxRows rows, unsigned char* flags) {
     const u32 k = blockIdx.x * 64 + threadIdx.x;
     if (k >= nslots) return;
     const u32 lo = key_off[k], hi = key_off[k + 1];
@@ -110,6 +117,8 @@ __global__ __launch_bounds__(64) void k_pl_walk_lb(const u32* __restrict__ key_o
     }
     for (u32 i = lo; i < hi; i++) {
         const u32 r = sorted_rank[i];
+        const bool newb = sc && cnt == L;  // (stream.current) this event starts the next batch
+        if (newb) cnt = 0;
         if (cnt == 0) {  // RESET: the batch starts from fresh states
 #pragma unroll
             for (int a = 0; a < NA; a++) { f[a] = 0; mm[a] = 0; mmh[a] = 0; }
@@ -134,6 +143,23 @@ __global__ __launch_bounds__(64) void k_pl_walk_lb(const u32* __restrict__ key_o
             }
         }
         lts = rec.ts[r];
+        if (sc) {
+            u64 rv[NA];
+            unsigned char rn[NA];
+            if (cur_on) {
+                p_row_vals<NA>(ap, cnt, f, mm, mmh, rv, rn);
+                p_write_row<NA>(rows, ap, r, lts, seq_base + (i64)rec.raw[r], k, rec.clock[r], 0, rv, rn);
+                flags[r] = 1;
+            } else if (newb) {
+                const u64 z[NA] = {};
+                const unsigned char zh[NA] = {};
+                p_row_vals<NA>(ap, 0, z, z, zh, rv, rn);
+                p_write_row<NA>(rows, ap, r, rec.clock[r], lseq, k, rec.clock[r], 1, rv, rn);
+                flags[r] = 1;
+            }
+            lseq = seq_base + (i64)rec.raw[r];
+            continue;
+        }
         lseq = seq_base + (i64)rec.raw[r];
         if (cnt == L) {
             u64 rv[NA];
@@ -168,12 +194,12 @@ __global__ __launch_bounds__(64) void k_pl_walk_lb(const u32* __restrict__ key_o
 
 void launch_pl_walk_lb(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec, i64 L,
                        i64 seq_base, SlState S, i64* last_ts, i64* last_seq, i64* prev_seq, AggPlan ap, int cur_on,
-                       int exp_on, SlxRows rows, unsigned char* flags) {
+                       int exp_on, int sc, SlxRows rows, unsigned char* flags) {
     const unsigned grid = (unsigned)((nslots + 63) / 64);
     if (!grid) return;
 #define SH_PL_LB(A, V)                                                                                               \
     hipLaunchKernelGGL((k_pl_walk_lb<A, V>), dim3(grid), dim3(64), 0, s, key_off, sorted_rank, (u32)nslots, rec, L,  \
-                       seq_base, S, last_ts, last_seq, prev_seq, ap, cur_on, exp_on, rows, flags)
+                       seq_base, S, last_ts, last_seq, prev_seq, ap, cur_on, exp_on, sc, rows, flags)
     const int nv = ap.n_vcols < 1 ? 1 : ap.n_vcols;
     if (ap.n <= 4 && nv <= 1) SH_PL_LB(4, 1);
     else if (nv <= 2) SH_PL_LB(8, 2);

@@ -145,7 +145,7 @@ void launch_slx_rekey_map(hipStream_t s, i64 size, KeyTable old_kt, KeyTable new
 // ---- partitioned lengthBatch / time windows keyed by the partition (sh_plane_kernels.hip) ----
 void launch_pl_walk_lb(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec, i64 L,
                        i64 seq_base, SlState S, i64* last_ts, i64* last_seq, i64* prev_seq, AggPlan ap, int cur_on,
-                       int exp_on, SlxRows rows, unsigned char* flags);
+                       int exp_on, int sc, SlxRows rows, unsigned char* flags);
 void launch_pl_runs(hipStream_t s, ColSet cols, int pcol, i64 N, i64 send_size, unsigned char* start, i64* blk,
                     i64* run);
 void launch_pl_slot_key(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64* slot_key);

@@ -65,3 +65,6 @@ int read_count(sh_query* q, const int64_t* dev, int64_t* out);
 int plane_create(sh_query* q);
 int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
 int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out);
+void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs);
+void plane_host_save(sh_query* q, std::vector<uint8_t>& out);
+int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used);

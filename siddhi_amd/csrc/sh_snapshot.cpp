@@ -370,6 +370,9 @@ struct SlidingImpl;
 int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* scalars, int n_scalars,
                           bool set, int64_t new_rc);
 int sliding_fifo_state(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* sc, bool set, int* kind);
+void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs);
+void plane_host_save(sh_query* q, std::vector<uint8_t>& out);
+int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used);
 
 int sliding_snapshot(sh_query* q, Writer& w) {
     hipStream_t s = q->ctx->stream;
@@ -388,11 +391,18 @@ int sliding_snapshot(sh_query* q, Writer& w) {
     int64_t fs[5] = {0, 0, 0, 0, 0};
     int fk = 0;
     RCHK(sliding_fifo_state(q, bufs, fs, false, &fk));
-    if (fk == 2) return sh_fail(SH_ERR_UNSUPPORTED, "snapshot of partitioned lengthBatch / time windows");
     w.val<int32_t>(fk);
     if (fk == 1) {
         for (int i = 0; i < 5; i++) w.val<int64_t>(fs[i]);
         for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+    } else if (fk == 2) {
+        // the partition lanes: their per-slot device state and the host-side Scheduler
+        plane_state_buffers(q, bufs);
+        for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
+        std::vector<uint8_t> hs;
+        plane_host_save(q, hs);
+        w.val<uint64_t>(hs.size());
+        w.put(hs.data(), hs.size());
     }
     w.val<int64_t>(q->seq);
     return SH_OK;
@@ -423,6 +433,14 @@ int sliding_restore(sh_query* q, Reader& r) {
         if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
         RCHK(sliding_fifo_state(q, bufs, fs, true, &fk));
         for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+    } else if (fk == 2) {
+        plane_state_buffers(q, bufs);
+        for (auto& b : bufs) RCHK(r.dev(*b.first, b.second, s));
+        const uint64_t hn = r.val<uint64_t>();
+        if (!r.ok || r.o + hn > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        size_t used = 0;
+        RCHK(plane_host_load(q, r.p + r.o, (size_t)hn, &used));
+        r.o += hn;
     }
     q->seq = r.val<int64_t>();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");

@@ -235,9 +235,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch, timeBatch, externalTimeBatch, time and "
                        "externalTime windows (partitioned: lengthBatch / time grouped by the partition key)");
-    if (d->stream_current && !(batch_win && d->partition_col < 0 && d->n_aggs >= 1))
+    // (partitioned: lengthBatch lanes, every event its own chunk of one key)
+    if (d->stream_current &&
+        !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH))))
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "stream.current.event runs on aggregating, non-partitioned lengthBatch / timeBatch windows");
+                       "stream.current.event runs on aggregating lengthBatch / timeBatch windows (partitioned: "
+                       "lengthBatch with no group-by or grouped by the partition key)");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "partitioned GPU queries support timeBatch, and lengthBatch / time with no group-by or "

@@ -155,6 +155,18 @@ case(name="partition3_time_all", source="ctest/query/partition/WindowPartitionTe
                                          [None], [None]],
                  rep_cols=[["symbol", ["IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "IBM", "WSO2", "IBM", "WSO2"]]]))
 
+# partitioned lengthBatch(2, true) (stream.current.event), no group-by, `insert all events`: every event
+# emits its partition's running sum; the third WSO2 and the third IBM event start a new batch (the chunk
+# [expired batch, RESET, event] keeps only its last event, processInBatchNoGroupBy).
+case(name="partition_lengthBatch_stream_current_all", source="ctest/query/partition/PartitionTestCase2.java:681-736",
+     schema="ts long, symbol string, price int",
+     query=dict(window="lengthBatch", param=2, partition="symbol", stream_current=True, aggs=[["sum", "price"]],
+                output="all"),
+     sends=[[[B + i] + r] for i, r in enumerate([[100, "IBM", 700], [101, "WSO2", 60], [101, "WSO2", 60],
+                                                [1134, "WSO2", 60], [100, "IBM", 700], [1145, "IBM", 700]])],
+     expect=dict(total_count=6, values=[[700], [60], [120], [60], [1400], [700]],
+                 rep_cols=[["symbol", ["IBM", "WSO2", "WSO2", "WSO2", "IBM", "IBM"]]]))
+
 # Scheduler tie rule, hand-traced (no reference test pins it; ctest/query/partition/WindowPartitionTestCase.java:
 # 141-216 is the query shape). Five partitions are due at the same time B+1000; Scheduler.onTimeChange
 # (core/util/Scheduler.java:71-104) walks PartitionStateHolder.states (HashMap<String, …>,

@@ -35,8 +35,10 @@ def _gpu_runs(c):
     if c.get("kind") == "aggregation":
         return False
     if q.get("stream_current"):
-        return bool(q.get("aggs")) and not q.get("partition") and (
-            q.get("output", "current") == "current" or q.get("window") == "lengthBatch")
+        if q.get("partition"):  # the lengthBatch lanes: no group-by or grouped by the partition key
+            return (q.get("window") == "lengthBatch" and bool(q.get("aggs"))
+                    and q.get("group_by", []) in ([], [q["partition"]]))
+        return bool(q.get("aggs")) and (q.get("output", "current") == "current" or q.get("window") == "lengthBatch")
     if q.get("window") in ("lengthBatch", "timeBatch"):
         return bool(q.get("aggs")) or not q.get("group_by")
     if q.get("window") in ("time", "externalTime"):

@@ -123,3 +123,17 @@ def test_partition_key_without_text_fails_loudly(rt):
     with pytest.raises(rt.SiddhiError, match="no text"):
         g.push(b)
     g.close()
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("L,group,parts,zipf", [(1, False, 50, False), (2, True, 300, False), (7, False, 40, False),
+                                               (3, True, 200_000, True)])
+def test_partitioned_lengthbatch_stream_current(rt, output, L, group, parts, zipf):
+    """lengthBatch(L, true) under `partition with`: a row per event (the partition's running aggregates),
+    the (L + 1)-th event of a batch resetting it (PartitionTestCase2.java:681-736's shape at scale)"""
+    ts, cols = stream(60_000 if not zipf else 400_000, parts, 61, runs=not zipf, zipf=zipf)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["p"] if group else [], aggs=AGGS, partition="p",
+                         filter=(">", "v", -30.0), output=output, stream_current=True,
+                         key_capacity=max(256, parts))
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 17_777, 40_000], 3), f"plb sc {L} {output}")
+    assert ref["ts"].size > 0

@@ -172,3 +172,26 @@ def test_rate_limited_checkpoint(rate, group):
     pushes = split_batches(C2, ts, cols, [20_011, 50_000], 3)
     got, ref, _ = checkpointed(spec, pushes, 1)
     assert_same(got, ref, label=f"rate {rate} group {group} ckpt")
+
+
+@pytest.mark.parametrize("window,param,output,sc", [("lengthBatch", 5, "all", False), ("lengthBatch", 3, "current", True),
+                                                    ("time", 120, "all", False), ("time", 300, "expired", False)])
+@pytest.mark.parametrize("cut", [1, 2])
+def test_partition_lanes_checkpoint(window, param, output, sc, cut):
+    """The partition lanes (sh_plane.cpp): per-partition window / aggregator state, and for time windows the
+    host-side Scheduler — pending notify times per partition and PartitionStateHolder.states' HashMap
+    structure (string partition keys, many of one hash: tree bins) — restored into a fresh query."""
+    from tests.test_gpu_partition import _same_hash_strings
+    schema = abi.Schema.parse("p string, v double, ts long")
+    names = _same_hash_strings(4) + [f"sym{i}" for i in range(200)]
+    rng = np.random.default_rng(17 + cut)
+    n = 60_000
+    ts = (np.cumsum(rng.integers(0, 2, n)) + 10_000).astype(np.int64)
+    p = np.where(rng.random(n) < 0.4, rng.integers(0, 16, n), rng.integers(16, len(names), n)).astype(np.int32)
+    v = rng.integers(-400, 400, n).astype(np.float64) / 8.0
+    spec = abi.QuerySpec(schema, window, param, aggs=[("count", None), ("sum", "v"), ("max", "v")], partition="p",
+                         output=output, stream_current=sc, key_capacity=256, strings={"p": names})
+    pushes = split_batches(schema, ts, [p, v, ts.copy()], [20_000, 41_000], 1)
+    pushes.append(("advance", int(ts[-1]) + 1_000))
+    got, ref, _ = checkpointed(spec, pushes, cut)
+    assert_same(got, ref, label=f"lanes ckpt {window} {output}")
