@@ -145,6 +145,7 @@ struct PushInfo {
     int err;           // externalTimeBatch: first event before its start time
     int unsorted;      // single-pass form: a timestamp decreased (redo with the prefix passes)
     i64 first_key;     // column WinParams.pcol1 - 1 of the first passing event (partitioned queries, R12)
+    int ms_overflow;   // k_split_sweep: a partition bucket overflowed (the host redoes the split)
 };
 
 // A window boundary inside the push: first combined index of a new window.
@@ -287,6 +288,13 @@ __host__ __device__ inline int tile_of(const TileMap& m, i64 b) {
 // counts the first n_count tiles of the map (k_boundaries counted the others) and zeroes the total slot
 void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, PosSrc new_pos, int P,
                      u32* counts);
+size_t split_sweep_lds(int n_vcols, int P);
+void launch_split_sweep(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals, i64 pend_cap,
+                        const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
+                        int P, int logP, i64 cap_p, u32* status, u32* ticket, u32* ms_off, u32* rec_idx, u64* rec_vals,
+                        i64 rec_cap, u32* new_pos, i64* blk_pass_pre, PushInfo* info, Bound* bounds, int max_bounds);
+void launch_fix_bounds(hipStream_t s, Bound* bounds, int max_bounds, const i64* blk_pass_pre, int nblk, const i64* ts,
+                       WinParams wp, PushInfo* info);
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
                        i64 pend_cap, PosSrc new_pos, ColSet cols, AggPlan ap, int P, int logP, const u32* offsets,
                        u32* rec_pos, u32* rec_idx, u64* rec_vals, i64 rec_cap, bool pack);

@@ -423,6 +423,11 @@ __global__ __launch_bounds__(kBlock) void k_fix_bounds(Bound* bounds, int max_bo
     }
 }
 
+void launch_fix_bounds(hipStream_t s, Bound* bounds, int max_bounds, const i64* blk_pass_pre, int nblk, const i64* ts,
+                       WinParams wp, PushInfo* info) {
+    hipLaunchKernelGGL(k_fix_bounds, dim3(1), dim3(kBlock), 0, s, bounds, max_bounds, blk_pass_pre, nblk, ts, wp, info);
+}
+
 void launch_boundaries(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                        i64* blk_pass_pre, const i64* blk_tl_pre, PushInfo* info, Bound* bounds,
                        int max_bounds, int nblk, KeyPlan kp, KeyTable kt, u32* new_pos, const i64* blk_xm_pre,

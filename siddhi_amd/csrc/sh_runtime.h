@@ -224,9 +224,10 @@ struct SlidingImpl;
 
 // A/B switches of the measured alternatives, read from the environment once per query,
 // when it is created, so a process can run queries with different settings side by side:
-// SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n
+// SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n,
+// SH_NO_SWEEP=1 (the two-pass split instead of k_split_sweep)
 struct Tuning {
-    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false;
+    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, no_sweep = false;
     int agg_band_rows = 8;
     static Tuning from_env();
 };
@@ -268,6 +269,8 @@ struct sh_query {
     const void* zeroed_nulls = nullptr;    // out_nulls / out_expired buffers already zeroed
     const void* zeroed_expired = nullptr;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
+    DevBuf sw_status;          // k_split_sweep: look-back status words [tile][partition] + the tile ticket
+    bool sweep_off = false;    // a bucket overflowed once: this query keeps the counting split
     DevBuf new_pos, seg_off;  // key slot per event of the push (kNoPos = filtered out); segment record offsets
     PushInfo* h_info = nullptr;
     PinnedBuf h_up;    // pinned segment list of the closed windows (read by the kernels in place)

@@ -301,14 +301,18 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
 // synchronisation. Host output synchronises here for the row copies.
 // Where the push's key slots come from (PosSrc): dictionary ids that are their own slots, with no
 // filter and no consumer of the slot column but the multisplit path, are read from the key column.
-static bool want_direct_pos(const sh_query* q) {
-    // opt-in (SH_DIRECT_POS=1): measured slower on MI355X — k_ms_scatter 290 vs 236 us per C2 push
-    // reading the key column instead of the slot column k_boundaries writes (profiles/r03_c2_v3*)
-    if (!q->tune.direct_pos) return false;
+static bool direct_pos_ok(const sh_query* q) {
     const int kc = q->kp.n == 1 ? q->kp.col[0] : -1;
     return q->kt.dense && q->kt.dmul == 1 && q->kt.dadd == 0 && kc >= 0 && q->kp.div[0] == 0 &&
            (q->load_type[kc] == SH_T_STRID || q->load_type[kc] == SH_T_INT) && filter_kind(q->fp) == 0 &&
            !q->xmode && !q->d.stream_current && q->ap.n > 0 && q->P > 1 && !q->partitioned && !q->given;
+}
+
+static bool want_direct_pos(const sh_query* q) {
+    // opt-in (SH_DIRECT_POS=1) for the two-pass split: measured slower on MI355X — k_ms_scatter 290 vs
+    // 236 us per C2 push reading the key column instead of the slot column k_boundaries writes
+    // (profiles/r03_c2_v3*); the one-sweep split (k_split_sweep) writes no slot column where it may
+    return q->tune.direct_pos && direct_pos_ok(q);
 }
 
 static PosSrc pos_src(const sh_query* q, const sh_batch* b) {
@@ -1250,11 +1254,41 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18) && !q->d.stream_current;
         const TileMap ms_map = make_tile_map(q->n_pend, q->n_pend + N);
         if (early_split) RCHK(reserve_ms_counts(q, ms_map));
-        launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
-                          q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                          slot_col, ext ? q->blk_xm.as<int64_t>() : nullptr,
-                          early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
-                          single_pass, q->blk_tl.as<int64_t>());
+        // the one-sweep form (k_split_sweep): window assignment and the split in one pass over the push,
+        // records in fixed-capacity partition buckets
+        const int64_t total_ev = q->n_pend + N;
+        const int64_t cap_p = (total_ev + q->P - 1) / q->P + (total_ev + q->P - 1) / q->P / 4 + 4096;
+        const bool sweep = single_pass && early_split && b->send_size == 1 && !q->sweep_off && !q->partitioned &&
+                           q->P > 1 && q->NL <= 1024 && total_ev < (1 << 29) && (int64_t)q->P * cap_p < (1ll << 31) &&
+                           q->P <= 4096 && !q->tune.no_sweep;
+        if (sweep) {
+            q->direct_pos = direct_pos_ok(q);
+            slot_col = q->direct_pos ? nullptr : q->new_pos.as<u32>();
+            const size_t st_bytes = (size_t)ms_map.nblk * q->P * 4;
+            RCHK(q->sw_status.reserve(st_bytes + 64, false));
+            HIPCHK(hipMemsetAsync(q->sw_status.p, 0, st_bytes + 64, s));
+            const int64_t rec_cap = (int64_t)q->P * cap_p;
+            RCHK(q->rec_idx.reserve((size_t)rec_cap * 4, false));
+            RCHK(q->rec_vals.reserve((size_t)std::max(1, q->ap.n_vcols) * rec_cap * 8, false));
+            const int nblk_new = ms_map.nblk - ms_map.np_t;
+            launch_split_sweep(s, ms_map, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, b->ts,
+                               cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->P, q->logP, cap_p, q->sw_status.as<u32>(),
+                               (u32*)(q->sw_status.as<char>() + st_bytes), q->ms_counts.as<u32>(), q->rec_idx.as<u32>(),
+                               q->rec_vals.as<u64>(), rec_cap, slot_col, q->blk_pass.as<int64_t>(),
+                               q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds);
+            launch_fix_bounds(s, q->bounds.as<Bound>(), max_bounds, q->blk_pass.as<int64_t>(), nblk_new, b->ts, wp,
+                              q->info.as<PushInfo>());
+            q->ms_ready = true;
+            q->rec_packed = true;
+            q->ms_map = ms_map;
+            q->rec_cap = rec_cap;
+        } else {
+            launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                              q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
+                              slot_col, ext ? q->blk_xm.as<int64_t>() : nullptr,
+                              early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
+                              single_pass, q->blk_tl.as<int64_t>());
+        }
         HIPCHK(hipGetLastError());
         // the push info and the first boundaries come back in one copy; the key partitioning of the
         // push's events (independent of where the windows close) is queued behind it and runs while
@@ -1266,13 +1300,24 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(q->ev_mid, s));
         SH_TMARK(1);
-        if (early_split) RCHK(run_multisplit(q, q->n_pend + N, b, true));
+        if (early_split && !sweep) RCHK(run_multisplit(q, q->n_pend + N, b, true));
         SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
         SH_TMARK(2);
         HIPCHK(sh_wait_event(q->ev_mid));
         SH_TMARK(3);
         PushInfo info = *q->h_info;
         SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
+        if (sweep && info.ms_overflow) {
+            // a partition bucket overflowed (skewed keys): the counting split runs in run_closed, and
+            // for this query from now on
+            SH_TRACE("push: split-sweep bucket overflow, counting split");
+            q->sweep_off = true;
+            q->ms_ready = false;
+            if (!q->direct_pos) {
+                // the slot column may have been skipped where the sweep read dictionary ids directly:
+                // it was written (slot_col) unless direct reads are valid, so nothing to redo
+            }
+        }
         if (single_pass && info.unsorted) {
             // a timestamp decreased: the send clocks need the prefix passes after all (the key slots,
             // the multisplit counts and the split already queued do not depend on the windows)
