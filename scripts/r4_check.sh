@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_sliding_minmax.py tests/test_gpu_snapshot.py tests/test_gpu_partition.py \
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_snapshot.py::test_partition_lanes_checkpoint tests/test_gpu_partition.py \
   tests/test_gpu_headline.py tests/test_gpu_ingest.py "tests/test_gpu_parity.py::test_reference_kat_on_gpu" \
   "tests/test_gpu_parity.py::test_c3_sliding_dictionary_keys" tests/test_gpu_parity.py::test_c2_split_sweep_and_counting_split tests/test_gpu_parity.py::test_c2_split_sweep_bucket_overflow_falls_back tests/test_gpu_scale.py::test_c3_time_10s_10k_keys_1k_resident_per_key \
   > gpurun_out/r4_t1.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error|error" gpurun_out/r4_t1.log | head -20; tail -30 gpurun_out/r4_t1.log; exit 1; }

@@ -220,7 +220,7 @@ Tuning Tuning::from_env() {
     t.part_keys_1024 = getenv("SH_PART_KEYS") && atoi(getenv("SH_PART_KEYS")) == 1024;
     t.no_async_small = on("SH_NO_ASYNC_SMALL");
     t.sl_records_seq = on("SH_SL_RECORDS_SEQ");
-    t.no_sweep = on("SH_NO_SWEEP");
+    t.sweep = on("SH_SWEEP");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
     return t;
 }

@@ -225,9 +225,9 @@ struct SlidingImpl;
 // A/B switches of the measured alternatives, read from the environment once per query,
 // when it is created, so a process can run queries with different settings side by side:
 // SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n,
-// SH_NO_SWEEP=1 (the two-pass split instead of k_split_sweep)
+// SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower)
 struct Tuning {
-    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, no_sweep = false;
+    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
     int agg_band_rows = 8;
     static Tuning from_env();
 };

@@ -155,7 +155,9 @@ void sliding_destroy(sh_query* q) {
 
 int empty_out(sh_query* q, const sh_out** out) {
     q->out.reset();
-    *out = q->out.view(q->kp.n, q->ap.n, q->vtypes);
+    // (the partition lanes without group-by report no key column: the partition key is internal)
+    const int nk = q->sl && q->sl->nk_out >= 0 ? q->sl->nk_out : q->kp.n;
+    *out = q->out.view(nk, q->ap.n, q->vtypes);
     return SH_OK;
 }
 

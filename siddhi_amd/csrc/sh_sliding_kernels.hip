@@ -1445,15 +1445,18 @@ __device__ bool dq_index_init(const KDq& q, const u64* dv, int* di, const u64* r
         bool th = in;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
+            // (every lane runs every shuffle: a lane that skipped one would leave its source register stale)
             const int src = lane + d < 64 ? lane + d : lane;
             const u64 ov = shfl64(t, src);
-            const bool oh = lane + d < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+            const int oth = __shfl(th ? 1 : 0, src, 64);
+            const bool oh = lane + d < 64 && oth != 0;
             if (oh && (!th || d_worse<MIN>(t, ov))) { t = ov; th = true; }
         }
         // best strictly after h: the next lane's suffix, then the later blocks
         const int nx = lane + 1 < 64 ? lane + 1 : lane;
         u64 nb = shfl64(t, nx);
-        bool nh = lane + 1 < 64 && __shfl(th ? 1 : 0, nx, 64) != 0;
+        const int nth = __shfl(th ? 1 : 0, nx, 64);
+        bool nh = lane + 1 < 64 && nth != 0;
         if (after_h && (!nh || d_worse<MIN>(nb, after))) { nb = after; nh = true; }
         const bool member = in && !(nh && d_worse<MIN>(v, nb));
         const unsigned long long bal = __ballot(member);
@@ -1529,16 +1532,19 @@ __device__ __forceinline__ DqPlan dq_plan(const KDq& q, const u64* dv, const int
         bool th = in;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {  // inclusive suffix scan
+            // (every lane runs every shuffle: a lane that skipped one would leave its source register stale)
             const int src = lane + d < 64 ? lane + d : lane;
             const u64 ov = shfl64(t, src);
-            const bool oh = lane + d < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+            const int oth = __shfl(th ? 1 : 0, src, 64);
+            const bool oh = lane + d < 64 && oth != 0;
             if (oh && (!th || d_worse<MIN>(t, ov))) { t = ov; th = true; }
         }
         cb = shfl64(t, 0);
         chh = __shfl(th ? 1 : 0, 0, 64) != 0;
         const int src = lane + 1 < 64 ? lane + 1 : lane;
         sb = shfl64(t, src);
-        sbh = lane + 1 < 64 && __shfl(th ? 1 : 0, src, 64) != 0;
+        const int sth = __shfl(th ? 1 : 0, src, 64);
+        sbh = lane + 1 < 64 && sth != 0;
     }
     surv = in && S + lane >= lo_end && !(sbh && d_worse<MIN>(x, sb));
     DqPlan p;

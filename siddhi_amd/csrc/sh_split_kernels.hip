@@ -145,11 +145,24 @@ __global__ __launch_bounds__(kBlock) void k_split_sweep(TileMap m, i64 n_pend, c
             st_publish(me, kStIncl | c);
         } else {
             st_publish(me, kStAgg | c);
-            for (int t = tile - 1;; t--) {
-                u32 v;
-                while (((v = st_poll(status + (size_t)t * P + p)) & ~kStVal) == 0) __builtin_amdgcn_s_sleep(1);
-                pre += v & kStVal;
-                if ((v & ~kStVal) == kStIncl || t == 0) break;
+            // predecessors read kLb at a time (independent loads, one latency per batch), summed back to
+            // the first inclusive prefix; a not-yet-published one is polled again from there
+            constexpr int kLb = 16;
+            int t = tile - 1;
+            for (bool done = false; !done;) {
+                u32 v[kLb];
+#pragma unroll
+                for (int j = 0; j < kLb; j++) v[j] = t - j >= 0 ? st_poll(status + (size_t)(t - j) * P + p) : kStIncl;
+                int j = 0;
+                for (; j < kLb; j++) {
+                    const u32 fl = v[j] & ~kStVal;
+                    if (fl == 0) break;
+                    pre += v[j] & kStVal;
+                    if (fl == kStIncl) { done = true; break; }
+                }
+                if (done) break;
+                t -= j;
+                if (j < kLb) __builtin_amdgcn_s_sleep(1);
             }
             st_publish(me, kStIncl | ((pre + c) & kStVal));
         }

@@ -358,9 +358,9 @@ def test_lengthbatch_batch_completing_on_the_push_end_flushes_in_that_push(rt):
 def test_c2_split_sweep_and_counting_split(rt, sweep, key_type, keys, filt, monkeypatch):
     """timeBatch at C2 shape (per-event sends, pushes of >= 2^18 events): the one-sweep window
     assignment + multisplit (k_split_sweep, decoupled look-back into partition buckets) and the two-pass
-    form (SH_NO_SWEEP=1) both give the oracle's rows; the third push carries a decreasing timestamp (the
-    sweep's sortedness check hands over to the prefix passes)."""
-    monkeypatch.setenv("SH_NO_SWEEP", "0" if sweep == "1" else "1")
+    form (the default; SH_SWEEP=1 selects the sweep) both give the oracle's rows; the third push carries a
+    decreasing timestamp (the sweep's sortedness check hands over to the prefix passes)."""
+    monkeypatch.setenv("SH_SWEEP", sweep)
     schema = abi.Schema.parse(f"k {key_type}, v double, ts long")
     ts, cols = synth.keyed_stream(0, 1_400_000, 0xC2, keys, 1000)
     ts = ts.copy()
@@ -371,9 +371,10 @@ def test_c2_split_sweep_and_counting_split(rt, sweep, key_type, keys, filt, monk
     both(rt, spec, split_batches(schema, ts, cols, [300_000, 700_000, 1_100_000], 1), label=f"sweep {sweep}")
 
 
-def test_c2_split_sweep_bucket_overflow_falls_back(rt):
+def test_c2_split_sweep_bucket_overflow_falls_back(rt, monkeypatch):
     """A hot key (a quarter of the events) overflows its partition bucket: the push redoes the split with
     the counting passes and the query keeps them; output = oracle."""
+    monkeypatch.setenv("SH_SWEEP", "1")
     schema = abi.Schema.parse("k string, v double, ts long")
     ts, cols = synth.keyed_stream(0, 1_200_000, 0xC2, 50_000, 1000)
     k = cols[0].copy()
