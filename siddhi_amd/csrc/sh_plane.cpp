@@ -45,7 +45,7 @@ static int fill(DevBuf& b, size_t bytes, int v) {
 
 int plane_create(sh_query* q) {
     SlidingImpl* s = q->sl;
-    s->lane = q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
+    s->lane = q->gkp.n > 0 ? 3 : q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
     s->nk_out = q->d.n_group_by;
     const size_t n = (size_t)s->nslots;
     RCHK(fill(s->pl_last_ts, n * 8, 0x80));  // lastTimestamp = Long.MIN_VALUE (0x8080... < any real ts)
@@ -159,9 +159,236 @@ static int sched_register(sh_query* q, uint32_t slot, int64_t t, const std::vect
     return SH_OK;
 }
 
+// bits needed for values < n
+static int bits_for(int64_t n) {
+    int b = 1;
+    while (b < 62 && ((int64_t)1 << b) < n) b++;
+    return b;
+}
+
+// a record set with room for n records; `keep` records of `from` are copied over (column strides change)
+static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64_t keep, int V) {
+    hipStream_t st = q->ctx->stream;
+    if (to.cap < n) {
+        const int64_t cap = std::max<int64_t>(n, to.cap + to.cap / 2);
+        PgBufs nb;
+        RCHK(nb.ps.reserve(cap * 4, false));
+        RCHK(nb.gs.reserve(cap * 4, false));
+        RCHK(nb.ts.reserve(cap * 8, false));
+        RCHK(nb.seq.reserve(cap * 8, false));
+        RCHK(nb.clk.reserve(cap * 8, false));
+        RCHK(nb.vals.reserve((size_t)V * cap * 8, false));
+        RCHK(nb.prev.reserve(cap, false));
+        nb.cap = cap;
+        to = std::move(nb);
+    }
+    if (keep > 0 && &to != &from) {
+        HIPCHK(hipMemcpyAsync(to.ps.p, from.ps.p, keep * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.gs.p, from.gs.p, keep * 4, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.ts.p, from.ts.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.seq.p, from.seq.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.clk.p, from.clk.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.prev.p, from.prev.p, keep, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpy2DAsync(to.vals.p, to.cap * 8, from.vals.p, from.cap * 8, keep * 8, V, hipMemcpyDeviceToDevice, st));
+    }
+    return SH_OK;
+}
+
+// Lane 3: partitioned lengthBatch(L) grouped by columns other than the partition key, by sorting
+// (sh_plane_group_kernels.hip). The records carried from earlier pushes (every partition's open batch
+// and, with expired output, its last completed batch) precede the push's own in one combined array.
+static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    const int64_t N = b->n, ss = b->send_size, L = q->d.window_param;
+    const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    if (N >= (int64_t)0x3FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 1G events");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    const int64_t cap = std::max<int64_t>(N, 1);
+    RCHK(s->rec_raw.reserve(cap * 4, false));
+    RCHK(s->rec_slot.reserve(cap * 4, false));
+    RCHK(s->rec_clock.reserve(cap * 8, false));
+    RCHK(s->rec_pm.reserve(cap * 8, false));
+    RCHK(s->rec_ts.reserve(cap * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    RCHK(s->pg_prevcnt.reserve(s->nslots * 4, false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    HIPCHK(hipMemsetAsync(s->pg_prevcnt.p, 0, s->nslots * 4, st));
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    const int nblk = (int)((N + kTile - 1) / kTile);
+    RCHK(s->blk_pass.reserve(nblk * 8, false));
+    RCHK(s->blk_tl.reserve(nblk * 8, false));
+    RCHK(s->blk_pm.reserve(nblk * 8, false));
+    WinParams wp{};
+    wp.kind = SH_WIN_TIME;  // the clock / pass-count prefix of the sliding path
+    wp.clock_valid = q->clock_valid;
+    wp.clock0 = q->clock;
+    wp.send_size = ss;
+    wp.N = N;
+    launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                     s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+    launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    RCHK(q->kt.check(st));
+    const SlInfo info = *s->h_info;
+    const int64_t M = info.total_pass, n_old = s->pg_n, n = n_old + M;
+    int64_t n_rows = 0, n_flushes = 0;
+    if (M > 0) {
+        if (n >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "partition lanes: more than 2G carried + new events");
+        // ---- combined records: carried, then the push's
+        if (s->pg[0].cap < n) {
+            RCHK(pg_grow(q, s->pg[1], s->pg[0], n, n_old, V));
+            std::swap(s->pg[0], s->pg[1]);
+        }
+        const PgRecs C = s->pg[0].view();
+        launch_pg_append(st, rec, M, n_old, q->seq, cs, q->gkp, q->gkt.dev(), V, C, s->slot_cnt.as<u32>(),
+                         s->pg_prevcnt.as<u32>());
+        HIPCHK(hipGetLastError());
+        // ---- every partition's records in stream order
+        RCHK(s->ranks.reserve(n * 4, false));
+        RCHK(s->p_slot.reserve(n * 4, false));
+        size_t tb = 0;
+        if (sort_slot_ranks(nullptr, &tb, C.ps, nullptr, nullptr, n, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_slot_ranks(s->sort_tmp.p, &tb, C.ps, s->p_slot.as<u32>(), s->ranks.as<u32>(), n, s->nslots, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+        RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+        launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
+        // ---- entries keyed (chunk, group slot)
+        const int gbits = bits_for((int64_t)q->gkt.size_ + 2), cbits = bits_for(n + 1);
+        const unsigned ebits = (unsigned)(gbits + cbits);
+        if (ebits > 64) return sh_fail(SH_ERR_UNSUPPORTED, "partition lanes: entry key wider than 64 bits");
+        const u64 none = ebits == 64 ? ~0ull : ((1ull << ebits) - 1);
+        const int64_t ne_cap = 2 * n;
+        RCHK(s->pg_ekey.reserve(ne_cap * 8, false));
+        RCHK(s->pg_ekey2.reserve(ne_cap * 8, false));
+        RCHK(s->pg_eval.reserve(ne_cap * 4, false));
+        RCHK(s->pg_eval2.reserve(ne_cap * 4, false));
+        RCHK(s->pg_keep.reserve(n + 16, false));
+        RCHK(s->pg_cnt.reserve(64, false));
+        HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 8, st));
+        launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L, q->d.current_on,
+                         q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
+                         s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>());
+        HIPCHK(hipGetLastError());
+        RCHK(q->gkt.check(st));
+        int64_t n_e = 0;
+        RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
+        if (n_e > 0) {
+            tb = 0;
+            if (sort_u64_pairs_bits(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_cap,
+                                    ebits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (sort_u64_pairs_bits(s->sort_tmp.p, &tb, s->pg_ekey.as<u64>(), s->pg_ekey2.as<u64>(), s->pg_eval.as<u32>(),
+                                    s->pg_eval2.as<u32>(), ne_cap, ebits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            // ---- segments = rows
+            RCHK(s->pg_head.reserve(n_e + 16, false));
+            RCHK(s->pg_seg.reserve(n_e * 8, false));
+            RCHK(s->x_blk.reserve((size_t)((n_e + kTile - 1) / kTile + 2) * 8, false));
+            launch_pg_heads(st, s->pg_ekey2.as<u64>(), n_e, s->pg_head.as<unsigned char>());
+            launch_slx_compact(st, 1, s->pg_head.as<unsigned char>(), nullptr, nullptr, nullptr, n_e,
+                               s->x_blk.as<int64_t>(), nullptr, nullptr, s->pg_seg.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + (n_e + kTile - 1) / kTile, &n_rows));
+            const int64_t rc = std::max<int64_t>(n_rows, 1);
+            RCHK(s->xr_ts.reserve(rc * 8, false));
+            RCHK(s->xr_rep.reserve(rc * 8, false));
+            RCHK(s->xr_slot.reserve(rc * 4, false));
+            RCHK(s->xr_ch.reserve(rc * 8, false));
+            RCHK(s->xr_clk.reserve(rc * 8, false));
+            RCHK(s->xr_exp.reserve(rc, false));
+            RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * rc * 8, false));
+            RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * rc, false));
+            RCHK(s->pg_rkey.reserve(rc * 8, false));
+            RCHK(s->pg_rkey2.reserve(rc * 8, false));
+            RCHK(s->pg_order.reserve(rc * 4, false));
+            SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                         s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                         s->xr_nulls.as<unsigned char>(), rc};
+            HIPCHK(hipEventRecord(q->ev_agg0, st));
+            launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
+                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>());
+            HIPCHK(hipEventRecord(q->ev_agg1, st));
+            // ---- rows in (chunk, first entry) order
+            const unsigned rbits = (unsigned)(32 + cbits);
+            tb = 0;
+            if (sort_u64_iota_bits(nullptr, &tb, s->pg_rkey.as<u64>(), nullptr, nullptr, n_rows, rbits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (sort_u64_iota_bits(s->sort_tmp.p, &tb, s->pg_rkey.as<u64>(), s->pg_rkey2.as<u64>(), s->pg_order.as<u32>(),
+                                   n_rows, rbits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            RCHK(s->out_ts.reserve(rc * 8, false));
+            RCHK(s->out_keys.reserve((size_t)std::max(1, q->gkp.n) * rc * 8, false));
+            RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * rc * 8, false));
+            RCHK(s->out_nulls.reserve((size_t)std::max(na, 1) * rc, false));
+            RCHK(s->out_send.reserve(rc * 8, false));
+            RCHK(s->out_clock.reserve(rc * 8, false));
+            RCHK(s->out_expired.reserve(rc, false));
+            RCHK(s->out_rep.reserve(rc * 8, false));
+            launch_pg_emit(st, s->pg_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, rc,
+                           s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
+                           s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
+                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            float kms = 0;
+            (void)hipEventSynchronize(q->ev_agg1);
+            (void)hipEventElapsedTime(&kms, q->ev_agg0, q->ev_agg1);
+            q->stats.main_kernel_ms = kms;
+        }
+        // one flush per chunk (out_send = the completing event's stream index)
+        RCHK(sliding_flushes(q, n_rows, &n_flushes));
+        // ---- carry the open batches (and the last completed ones) in stream order
+        RCHK(s->x_idx.reserve(n * 8, false));
+        RCHK(s->x_blk.reserve((size_t)((n + kTile - 1) / kTile + 2) * 8, false));
+        launch_slx_compact(st, 1, s->pg_keep.as<unsigned char>(), nullptr, nullptr, nullptr, n, s->x_blk.as<int64_t>(),
+                           nullptr, nullptr, s->x_idx.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        int64_t n_keep = 0;
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (n + kTile - 1) / kTile, &n_keep));
+        RCHK(pg_grow(q, s->pg[1], s->pg[1], std::max<int64_t>(n_keep, 1), 0, V));
+        launch_pg_gather(st, s->x_idx.as<int64_t>(), n_keep, s->pg_keep.as<unsigned char>(), C, s->pg[1].view(), V);
+        HIPCHK(hipGetLastError());
+        std::swap(s->pg[0], s->pg[1]);
+        s->pg_n = n_keep;
+    }
+    q->seq += N;
+    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+    q->clock_valid = true;
+    q->stats.events = N;
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
+    return sliding_output(q, n_rows, n_flushes, false, host_out, out);
+}
+
 // Lane pass of the push: records of M passing events sorted by slot (b == null: a TIMER call at `now`).
 static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
+    if (s->lane == 3) {
+        if (b) return plane_run_group(q, b, host_out, out);
+        if (!q->clock_valid || now >= q->clock) {
+            q->clock = now;
+            q->clock_valid = true;
+        }
+        return empty_out(q, out);
+    }
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
     const bool tm = s->lane == 2, sched = tm && q->d.expired_on;
@@ -428,7 +655,93 @@ void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& b
     if (s->lane == 2) bufs.push_back({&s->rg, n * (size_t)s->rc * 8});
 }
 
-void plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
+// lane 3: the group key table and the carried records (in stream order)
+static int pg_save(sh_query* q, std::vector<uint8_t>& out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    auto put = [&](const void* p, size_t k) { out.insert(out.end(), (const uint8_t*)p, (const uint8_t*)p + k); };
+    auto dev = [&](const void* p, size_t k) -> int {
+        const size_t o = out.size();
+        out.resize(o + k);
+        if (k) {
+            HIPCHK(hipMemcpyAsync(out.data() + o, p, k, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        return SH_OK;
+    };
+    RCHK(q->gkt.check(st));
+    const uint64_t gsize = q->gkt.size_;
+    const int64_t gnk = q->gkt.n_keys, n = s->pg_n;
+    const int V = std::max(1, q->ap.n_vcols);
+    put(&gsize, 8);
+    put(&gnk, 8);
+    RCHK(dev(q->gkt.keys.p, q->gkt.dense ? 0 : gsize * 8));
+    put(&n, 8);
+    const PgBufs& B = s->pg[0];
+    RCHK(dev(B.ps.p, n * 4));
+    RCHK(dev(B.gs.p, n * 4));
+    RCHK(dev(B.ts.p, n * 8));
+    RCHK(dev(B.seq.p, n * 8));
+    RCHK(dev(B.clk.p, n * 8));
+    RCHK(dev(B.prev.p, n));
+    for (int v = 0; v < V; v++) RCHK(dev(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
+    return SH_OK;
+}
+
+static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    size_t o = 0;
+    auto get = [&](void* d, size_t k) {
+        if (o + k > len) return false;
+        std::memcpy(d, p + o, k);
+        o += k;
+        return true;
+    };
+    uint64_t gsize = 0;
+    int64_t gnk = 0, n = 0;
+    if (!get(&gsize, 8) || !get(&gnk, 8) || gsize != q->gkt.size_ || gnk < 0 || gnk > (int64_t)gsize + 1)
+        return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    const size_t kb = q->gkt.dense ? 0 : gsize * 8;
+    if (o + kb + 8 > len) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    const uint8_t* keys = p + o;
+    o += kb;
+    get(&n, 8);
+    const int V = std::max(1, q->ap.n_vcols);
+    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V) > len)
+        return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    // validated: now replace the state
+    if (kb) HIPCHK(hipMemcpyAsync(q->gkt.keys.p, keys, kb, hipMemcpyHostToDevice, st));
+    {
+        PinnedBuf h;
+        RCHK(h.reserve(16));
+        uint32_t* c = h.as<uint32_t>();
+        c[0] = (uint32_t)gnk; c[1] = c[2] = c[3] = 0;
+        HIPCHK(hipMemcpyAsync(q->gkt.ctrl.p, c, 16, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    q->gkt.n_keys = gnk;
+    RCHK(pg_grow(q, s->pg[0], s->pg[0], std::max<int64_t>(n, 1), 0, V));
+    const PgBufs& B = s->pg[0];
+    auto up = [&](void* d, size_t k) -> int {
+        if (k) HIPCHK(hipMemcpyAsync(d, p + o, k, hipMemcpyHostToDevice, st));
+        o += k;
+        return SH_OK;
+    };
+    RCHK(up(B.ps.p, n * 4));
+    RCHK(up(B.gs.p, n * 4));
+    RCHK(up(B.ts.p, n * 8));
+    RCHK(up(B.seq.p, n * 8));
+    RCHK(up(B.clk.p, n * 8));
+    RCHK(up(B.prev.p, n));
+    for (int v = 0; v < V; v++) RCHK(up(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
+    HIPCHK(hipStreamSynchronize(st));  // the blob may be freed after the call
+    s->pg_n = n;
+    *used = o;
+    return SH_OK;
+}
+
+int plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
     SlidingImpl* s = q->sl;
     auto put = [&](const void* p, size_t k) { out.insert(out.end(), (const uint8_t*)p, (const uint8_t*)p + k); };
     // pending notify times by slot, in slot order (the armed set is their fronts)
@@ -449,6 +762,7 @@ void plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
     const uint64_t ml = m.size();
     put(&ml, 8);
     put(m.data(), m.size());
+    return s->lane == 3 ? pg_save(q, out) : SH_OK;
 }
 
 int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
@@ -482,6 +796,12 @@ int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
     shj::JavaStringMap m;
     if (!m.load(p + o, (size_t)ml)) return sh_fail(SH_ERR_INVALID, "snapshot: scheduler state unreadable");
     o += ml;
+    size_t pg_used = 0;
+    if (s->lane == 3) {
+        // (the lanes of lane 3 carry no Scheduler: its part above is empty)
+        RCHK(pg_load(q, p + o, n - o, &pg_used));
+        o += pg_used;
+    }
     std::unordered_map<uint32_t, std::u16string> flow;
     m.visit_keys([&](uint32_t slot, const std::u16string& k) { flow[slot] = k; });
     s->pl_pend = std::move(pend);

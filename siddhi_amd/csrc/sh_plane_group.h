@@ -1,0 +1,39 @@
+// sh_plane_group.h — partitioned lengthBatch grouped by a key other than the partition key
+// (sh_plane_group_kernels.hip, driven by sh_plane.cpp).
+#pragma once
+#include "sh_sliding.h"
+
+namespace shd {
+
+// records carried between pushes (the partitions' open batches and, with expired output, their last
+// completed batch) followed by the push's own: the combined order is stream order
+struct PgRecs {
+    u32* ps;             // partition slot
+    u32* gs;             // group slot
+    i64* ts;
+    i64* seq;            // stream index of the event
+    i64* clk;            // playback clock of the event's send
+    u64* vals;           // [n_vcols][cap]
+    unsigned char* prev; // carried as the partition's last completed batch
+    i64 cap;
+};
+
+void launch_pg_append(hipStream_t s, SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols, KeyPlan gkp,
+                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt);
+void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, PgRecs C, i64 n, i64 L,
+                      int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval, unsigned char* keep,
+                      unsigned long long* n_entries);
+void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head);
+void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key);
+void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
+                    i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
+void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char* keep, PgRecs C, PgRecs D, int nv);
+// stable sort of (u64 key, u32 value) pairs over key bits [0, end_bit)
+int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
+                        i64 n, unsigned end_bit, hipStream_t s);
+int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,
+                       unsigned end_bit, hipStream_t s);
+
+}  // namespace shd

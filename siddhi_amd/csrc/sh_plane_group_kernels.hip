@@ -1,0 +1,281 @@
+// sh_plane_group_kernels.hip — `partition with (p of S) begin from S#window.lengthBatch(L) select g…,
+// aggs group by g… insert [current|all|expired] events into O; end` with a group key other than the
+// partition key, on gfx950.
+//
+// Every partition owns its own lengthBatch window (PartitionRuntimeImpl.initPartition :346-367). A batch
+// the partition completes is one selector chunk (LengthBatchWindowProcessor.processFullBatchEvents
+// :206-243): [the previous batch's events as EXPIRED, RESET, the batch's L events], and
+// QuerySelector.processInBatchGroupBy (:315-374) keeps one row per group key in first-insertion order
+// (LinkedHashMap.put). The RESET clears every group state, so a group's current row folds only its own
+// events of the batch; its expired row is its previous-batch events removed again (count 0, the others
+// null). Nothing here is sequential per partition: a partition's batches are fixed windows of L events
+// of its run in stream order, so
+//   1. the records of the push are appended to the carried ones (the partitions' open batches and,
+//      with expired output, their last completed batch) and sorted stably by partition slot;
+//   2. every sorted position knows its batch from its offset in the run (k_pg_assign) and emits up to
+//      two entries — EXPIRED into the chunk of the next batch, CURRENT into its own — keyed
+//      (chunk, group slot), where a chunk is named by the combined index of the event completing it;
+//   3. the entries are sorted stably by that key (rocPRIM), a segment is one output row (k_pg_fold);
+//   4. the rows are sorted by (chunk, first entry) and written in that order (k_pg_emit).
+// The records of incomplete batches (and the last completed batch, for expired output) are carried to
+// the next push in stream order (k_pg_assign marks them, k_pg_gather compacts them).
+#include "sh_device.h"
+#include "sh_sliding.h"
+#include "sh_plane_group.h"
+
+namespace shd {
+
+namespace {
+
+__device__ __forceinline__ bool g_worse(int kind, u64 cur, u64 v) {
+    switch (kind) {
+        case AK_MIN_L: return (i64)cur > (i64)v;
+        case AK_MAX_L: return (i64)cur < (i64)v;
+        case AK_MIN_D: return __longlong_as_double((i64)cur) > __longlong_as_double((i64)v);
+        case AK_MAX_D: return __longlong_as_double((i64)cur) < __longlong_as_double((i64)v);
+        case AK_MIN_F: return (float)__longlong_as_double((i64)cur) > (float)__longlong_as_double((i64)v);
+        default: return (float)__longlong_as_double((i64)cur) < (float)__longlong_as_double((i64)v);
+    }
+}
+
+__device__ __forceinline__ double g_num(const AggPlan& ap, int a, u64 x) {
+    return (ap.kind[a] == AK_AVG && !is_fp(ap.vcol_type[ap.vcol[a]])) ? (double)(i64)x : __longlong_as_double((i64)x);
+}
+
+}  // namespace
+
+// ---- 1. the push's records appended after the n_old carried ones (partition slot from the records
+// kernel, group slot looked up here), and the carried ones counted into the per-partition totals ----
+__global__ __launch_bounds__(kBlock) void k_pg_append(SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols,
+                                                     KeyPlan gkp, KeyTable gkt, int nv, PgRecs C) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= M) return;
+    const i64 c = n_old + r;
+    const u32 e = rec.raw[r];
+    C.ps[c] = rec.slot[r];
+    C.gs[c] = key_slot(gkt, make_key(gkp, cols, e));
+    C.ts[c] = rec.ts[r];
+    C.seq[c] = seq_base + (i64)e;
+    C.clk[c] = rec.clock[r];
+    C.prev[c] = 0;
+    for (int v = 0; v < nv; v++) C.vals[(size_t)v * C.cap + c] = rec.vals[(size_t)v * rec.cap + r];
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_count_old(PgRecs C, i64 n_old, u32* slot_cnt, u32* prev_cnt) {
+    const i64 c = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n_old) return;
+    const u32 p = C.ps[c];
+    atomicAdd(&slot_cnt[p], 1u);
+    if (C.prev[c]) atomicAdd(&prev_cnt[p], 1u);
+}
+
+void launch_pg_append(hipStream_t s, SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols, KeyPlan gkp,
+                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt) {
+    if (M > 0)
+        hipLaunchKernelGGL(k_pg_append, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, n_old,
+                           seq_base, cols, gkp, gkt, nv, C);
+    if (n_old > 0)
+        hipLaunchKernelGGL(k_pg_count_old, dim3((unsigned)((n_old + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, C,
+                           n_old, slot_cnt, prev_cnt);
+}
+
+// ---- 2. batch of every sorted position. Partition p's run [lo, hi) of the sorted order holds its
+// np carried previous-batch records first, then its open batch and the push's events in stream order.
+// Position j = i - lo - np >= 0 is in batch j / L, complete iff the run holds all of it; the chunk of
+// batch b is named by the combined index of its last event. Entries (2 per position, key ~0 = none):
+//   [2i]     EXPIRED of position i into the chunk of the following batch (expired output only);
+//   [2i + 1] CURRENT of position i into its own batch's chunk (current output only);
+// value = i | (1 << 31) for CURRENT. keep[c]: 1 = carried as the last completed batch, 2 = open batch.
+__global__ __launch_bounds__(kBlock) void k_pg_assign(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                     const u32* __restrict__ prev_cnt, PgRecs C, i64 n, i64 L,
+                                                     int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval,
+                                                     unsigned char* keep, unsigned long long* n_entries) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    int made = 0;
+    if (i < n) {
+        const u32 c = ranks[i];
+        const u32 p = C.ps[c];
+        const i64 lo = key_off[p], hi = key_off[p + 1], np = prev_cnt[p];
+        const i64 run = hi - lo - np, nfull = run / L;
+        const i64 j = i - lo - np;
+        const u64 g = C.gs[c];
+        u64 kx = none, kc = none;
+        unsigned char kp = 0;
+        if (j < 0) {
+            // a carried record of the last completed batch: EXPIRED into batch 0's chunk, else kept
+            if (nfull > 0) kx = ((u64)ranks[lo + np + L - 1] << gbits) | g;
+            else kp = 1;
+        } else {
+            const i64 b = j / L;
+            if (b < nfull) {
+                if (cur_on) kc = ((u64)ranks[lo + np + (b + 1) * L - 1] << gbits) | g;
+                if (exp_on) {
+                    if (b + 1 < nfull) kx = ((u64)ranks[lo + np + (b + 2) * L - 1] << gbits) | g;
+                    else kp = 1;
+                }
+            } else {
+                kp = 2;
+            }
+        }
+        if (!exp_on) kx = none;
+        ekey[2 * i] = kx;
+        ekey[2 * i + 1] = kc;
+        eval[2 * i] = (u32)i;
+        eval[2 * i + 1] = (u32)i | 0x80000000u;
+        keep[c] = kp;
+        made = (kx != none) + (kc != none);
+    }
+    const i64 tot = block_reduce((i64)made, SumOp(), 0);
+    if (threadIdx.x == 0 && tot) atomicAdd(n_entries, (unsigned long long)tot);
+}
+
+void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, PgRecs C, i64 n, i64 L,
+                      int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval, unsigned char* keep,
+                      unsigned long long* n_entries) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_pg_assign, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
+                       prev_cnt, C, n, L, cur_on, exp_on, gbits, none, ekey, eval, keep, n_entries);
+}
+
+// segment heads of the sorted entries
+__global__ __launch_bounds__(kBlock) void k_pg_heads(const u64* __restrict__ key, i64 n, unsigned char* head) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) head[j] = j == 0 || key[j] != key[j - 1];
+}
+
+void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_pg_heads, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key, n, head);
+}
+
+// ---- 3. one row per (chunk, group) segment. EXPIRED entries come first (the previous batch), then
+// CURRENT ones, each in stream order. With current entries the row is the group's last current event
+// carrying the fold of the group's current events (the RESET cleared the state); with expired entries
+// only, the last expired event with the state emptied (count 0, the others null), stamped with the
+// chunk's clock. Row order key: (chunk, the segment's first sorted position).
+template <int NA>
+__global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_start, i64 n_seg, i64 n_e,
+                                               const u64* __restrict__ ekey, const u32* __restrict__ eval,
+                                               const u32* __restrict__ ranks, PgRecs C, AggPlan ap, int gbits,
+                                               SlxRows rows, u64* row_key) {
+    const i64 sidx = (i64)blockIdx.x * 64 + threadIdx.x;
+    if (sidx >= n_seg) return;
+    const i64 lo = seg_start[sidx], hi = sidx + 1 < n_seg ? seg_start[sidx + 1] : n_e;
+    const u64 key = ekey[lo];
+    const u32 chunk = (u32)(key >> gbits);
+    const u32 g = (u32)(key & ((1ull << gbits) - 1));
+    u64 f[NA], mm[NA];
+    unsigned char mmh[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) { f[a] = 0; mm[a] = 0; mmh[a] = 0; }
+    i64 cnt = 0, last_c = -1, last_x = -1;
+    for (i64 t = lo; t < hi; t++) {
+        const u32 v = eval[t];
+        const u32 c = ranks[v & 0x7FFFFFFFu];
+        if (!(v >> 31)) { last_x = c; continue; }
+        last_c = c;
+        cnt++;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            if (kind == AK_COUNT) continue;
+            const u64 x = C.vals[(size_t)ap.vcol[a] * C.cap + c];
+            if (kind == AK_SUM_L) f[a] = (u64)((i64)f[a] + (i64)x);
+            else if (kind == AK_SUM_D || kind == AK_AVG)
+                f[a] = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) + g_num(ap, a, x));
+            else {
+                const bool take = !mmh[a] || g_worse(kind, mm[a], x);
+                mm[a] = take ? x : mm[a];
+                mmh[a] = 1;
+            }
+        }
+    }
+    const bool cur = last_c >= 0;
+    const i64 rc = cur ? last_c : last_x;
+    rows.ts[sidx] = cur ? C.ts[rc] : C.clk[chunk];
+    rows.rep[sidx] = C.seq[rc];
+    rows.slot[sidx] = g;
+    rows.ch[sidx] = C.seq[chunk];
+    rows.clk[sidx] = C.clk[chunk];
+    rows.exp[sidx] = cur ? 0 : 1;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) continue;
+        const int kind = ap.kind[a];
+        u64 rv = 0;
+        unsigned char rn = 0;
+        if (kind == AK_COUNT) rv = (u64)cnt;
+        else if (kind == AK_SUM_L || kind == AK_SUM_D) { rn = cnt == 0; rv = cnt == 0 ? 0 : f[a]; }
+        else if (kind == AK_AVG) {
+            rn = cnt == 0;
+            if (cnt) rv = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) / (double)cnt);
+        } else { rn = mmh[a] ? 0 : 1; rv = mmh[a] ? mm[a] : 0; }
+        rows.vals[(size_t)a * rows.cap + sidx] = rv;
+        rows.nulls[(size_t)a * rows.cap + sidx] = rn;
+    }
+    row_key[sidx] = ((u64)chunk << 32) | (u64)(eval[lo] & 0x7FFFFFFFu);
+}
+
+void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key) {
+    if (n_seg <= 0) return;
+    const unsigned grid = (unsigned)((n_seg + 63) / 64);
+    if (ap.n <= 4) hipLaunchKernelGGL(k_pg_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks,
+                                      C, ap, gbits, rows, row_key);
+    else hipLaunchKernelGGL(k_pg_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks, C, ap,
+                            gbits, rows, row_key);
+}
+
+// ---- 4. the rows in (chunk, first entry) order -> the push's output columns
+__global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ order, i64 n, SlxRows rows, int n_aggs,
+                                                   int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
+                                                   i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                                                   unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n) return;
+    const u32 j = order[r];
+    out_ts[r] = rows.ts[j];
+    if (nk > 0) unpack_key(kp, slot_key(kt, rows.slot[j]), out_keys + r, out_cap);
+    for (int a = 0; a < n_aggs; a++) {
+        out_vals[(size_t)a * out_cap + r] = rows.vals[(size_t)a * rows.cap + j];
+        out_nulls[(size_t)a * out_cap + r] = rows.nulls[(size_t)a * rows.cap + j];
+    }
+    out_exp[r] = rows.exp[j];
+    out_ch[r] = rows.ch[j];
+    out_clock[r] = rows.clk[j];
+    out_rep[r] = rows.rep[j];
+}
+
+void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
+                    i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
+                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_pg_emit, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, order, n, rows,
+                       n_aggs, nk, kt, kp, out_cap, out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock,
+                       out_rep);
+}
+
+// ---- carried records: the kept ones (keep != 0) of the combined order, gathered in that (stream)
+// order into the other buffer set
+__global__ __launch_bounds__(kBlock) void k_pg_gather(const i64* __restrict__ idx, i64 n, const unsigned char* keep,
+                                                     PgRecs C, PgRecs D, int nv) {
+    const i64 k = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= n) return;
+    const i64 c = idx[k];
+    D.ps[k] = C.ps[c];
+    D.gs[k] = C.gs[c];
+    D.ts[k] = C.ts[c];
+    D.seq[k] = C.seq[c];
+    D.clk[k] = C.clk[c];
+    D.prev[k] = keep[c] == 1;
+    for (int v = 0; v < nv; v++) D.vals[(size_t)v * D.cap + k] = C.vals[(size_t)v * C.cap + c];
+}
+
+void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char* keep, PgRecs C, PgRecs D, int nv) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_pg_gather, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, idx, n, keep, C,
+                           D, nv);
+}
+
+}  // namespace shd

@@ -250,6 +250,10 @@ struct sh_query {
     KeyPlan kp{};
     int32_t vtypes[SH_MAX_AGGS]{};
     KeyTableHost kt;
+    // partitioned lengthBatch grouped by other columns (sh_plane.cpp, lane 3): kp / kt key the
+    // partitions, gkp / gkt the output groups
+    KeyPlan gkp{};
+    KeyTableHost gkt;
     int P = 1, logP = 0, NL = 0;
     // playback clock + window state
     bool clock_valid = false;

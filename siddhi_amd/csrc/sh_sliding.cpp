@@ -138,7 +138,7 @@ void sliding_destroy(sh_query* q) {
                       &s->p_slot, &s->p_clock, &s->p_pm, &s->p_ts, &s->p_vals, &s->rows_ts,
                       &s->rows_slot, &s->rows_send, &s->rows_clock, &s->rows_vals, &s->rows_nulls, &s->blk_cnt,
                       &s->out_ts, &s->out_keys, &s->out_vals, &s->out_nulls, &s->out_send, &s->out_clock,
-                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->rec_sclk, &s->sort_tmp, &s->key_off, &s->g_rank, &s->inv, &s->rows_k,
+                      &s->out_expired, &s->flush_off, &s->flush_clock, &s->iota, &s->rec_sclk, &s->sort_tmp, &s->key_off, &s->g_rank, &s->inv, &s->rows_k,
                       &s->rg, &s->upm, &s->useq, &s->upm2, &s->useq2, &s->npend, &s->npend2, &s->x_sK, &s->x_scb,
                       &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
                       &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
@@ -455,7 +455,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     }
     // flush structure: a flush per send that produced rows (one selector output chunk per send)
     int64_t n_flushes = 0;
-    RCHK(sliding_flushes(q, n_rows, &n_flushes));
+    RCHK(sliding_flushes(q, n_rows, &n_flushes, send_size == 1));
     HIPCHK(hipEventRecord(q->ev_push1, st));
     HIPCHK(hipStreamSynchronize(st));
     float ms = 0;
@@ -467,9 +467,26 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
 
 // flush offsets / clocks of n_rows output rows: a flush starts where out_send (the send, or the
 // chunk in expired mode) changes; flush_off[n_flushes] = n_rows
-int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out) {
+int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out, bool per_row) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
+    s->fo = s->flush_off.as<int64_t>();
+    s->fc = s->flush_clock.as<int64_t>();
+    if (per_row) {
+        // one row per send (per-event sends): every row is a flush of its own, so the offsets are the
+        // identity (a persistent iota) and the clocks the rows' own
+        if (s->iota_n < n_rows + 1) {
+            const int64_t n = std::max<int64_t>(n_rows + 1, s->iota_n * 2);
+            RCHK(s->iota.reserve((size_t)n * 8, false));
+            launch_iota_i64(st, s->iota.as<int64_t>(), n);
+            HIPCHK(hipGetLastError());
+            s->iota_n = n;
+        }
+        s->fo = s->iota.as<int64_t>();
+        s->fc = s->out_clock.as<int64_t>();
+        *n_flushes_out = n_rows;
+        return SH_OK;
+    }
     int64_t n_flushes = 0;
     if (n_rows > 0) {
         int rb = (int)((n_rows + kTile - 1) / kTile);
@@ -511,8 +528,8 @@ int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_ord
         o.nulls.resize((size_t)na * n_rows);
         o.rep.resize(n_rows);
         if (n_rows > 0) {
-            HIPCHK(hipMemcpyAsync(o.flush_offsets.data(), s->flush_off.p, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(o.flush_clock.data(), s->flush_clock.p, n_flushes * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.flush_offsets.data(), s->fo, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(o.flush_clock.data(), s->fc, n_flushes * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.ts.data(), s->out_ts.p, n_rows * 8, hipMemcpyDeviceToHost, st));
             HIPCHK(hipMemcpyAsync(o.expired.data(), s->out_expired.p, n_rows, hipMemcpyDeviceToHost, st));
             // device arrays have stride cap == n_rows
@@ -538,8 +555,8 @@ int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_ord
         o.n_keys = nk;
         o.n_vals = na;
         for (int i = 0; i < na; i++) o.val_types[i] = q->vtypes[i];
-        o.flush_offsets = s->flush_off.as<int64_t>();
-        o.flush_clock = s->flush_clock.as<int64_t>();
+        o.flush_offsets = const_cast<int64_t*>(s->fo);
+        o.flush_clock = const_cast<int64_t*>(s->fc);
         o.ts = s->out_ts.as<int64_t>();
         o.expired = s->out_expired.as<uint8_t>();
         o.keys = s->out_keys.as<int64_t>();

@@ -89,6 +89,7 @@ void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, K
                              const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
                              u32* slot_cnt);
 void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* blk_cnt, int nb);
+void launch_iota_i64(hipStream_t s, i64* a, i64 n);
 void launch_flush_write(hipStream_t s, const i64* out_send, const i64* out_clock, i64 n_rows, const i64* blk_pre,
                         int nb, i64* flush_off, i64* flush_clock);
 void launch_sl_regrow(hipStream_t s, const u64* old_buf, u64* new_buf, const i64* head, const i64* len, i64 nslots,

@@ -11,8 +11,19 @@
 #include "sh_runtime.h"
 #include "sh_jmap.h"
 #include "sh_sliding.h"
+#include "sh_plane_group.h"
 
 using shd::SlInfo;
+
+// lane 3 (partitioned lengthBatch grouped by other columns): a set of carried / combined records
+struct PgBufs {
+    DevBuf ps, gs, ts, seq, clk, vals, prev;
+    int64_t cap = 0;
+    shd::PgRecs view() const {
+        return shd::PgRecs{ps.as<uint32_t>(), gs.as<uint32_t>(), ts.as<int64_t>(), seq.as<int64_t>(), clk.as<int64_t>(),
+                           vals.as<shd::u64>(), prev.as<unsigned char>(), cap};
+    }
+};
 
 struct SlidingImpl {
     int64_t nslots = 0, rc = 0;
@@ -29,6 +40,12 @@ struct SlidingImpl {
     SlInfo* h_info = nullptr;
     PinnedBuf h_up;  // pinned staging of small host->device uploads
     sh_out dev_out{};
+    // the push's flush offsets / clocks: flush_off / flush_clock, or (a row per send) the persistent
+    // identity `iota` and the rows' own clocks
+    DevBuf iota;
+    int64_t iota_n = 0;
+    const int64_t* fo = nullptr;
+    const int64_t* fc = nullptr;
 
     // `insert expired events` / `insert all events` (sh_slx_kernels.hip): the expiry queue as a FIFO
     // of the window's events (PM and stream index, global arrival order X0 .. G0), each ring entry's
@@ -52,6 +69,12 @@ struct SlidingImpl {
     std::set<std::pair<int64_t, uint32_t>> pl_armed;  // (front notify time, slot)
     shj::JavaStringMap pl_states;
     std::unordered_map<uint32_t, std::u16string> pl_flow;  // slot -> String.valueOf(partition key)
+    // lane 3: the carried records (pg[0], pg_n of them in stream order), the compaction target pg[1],
+    // and the push's entry / segment / row scratch
+    PgBufs pg[2];
+    int64_t pg_n = 0;
+    DevBuf pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
+        pg_cnt;
 };
 
 
@@ -59,12 +82,12 @@ struct SlidingImpl {
 shd::SlState state_of(SlidingImpl* s);
 int size_rings(sh_query* q, int64_t new_rc, bool keep = true);
 int empty_out(sh_query* q, const sh_out** out);
-int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out);
+int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out, bool per_row = false);
 int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_order, bool host_out, const sh_out** out);
 int read_count(sh_query* q, const int64_t* dev, int64_t* out);
 int plane_create(sh_query* q);
 int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out);
 int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out);
 void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs);
-void plane_host_save(sh_query* q, std::vector<uint8_t>& out);
+int plane_host_save(sh_query* q, std::vector<uint8_t>& out);
 int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used);

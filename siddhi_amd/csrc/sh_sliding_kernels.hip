@@ -2068,6 +2068,15 @@ void launch_flush_starts(hipStream_t s, const i64* out_send, i64 n_rows, i64* bl
     hipLaunchKernelGGL(k_flush_starts, dim3(nb), dim3(kBlock), 0, s, out_send, n_rows, blk_cnt);
 }
 
+__global__ __launch_bounds__(kBlock) void k_iota_i64(i64* a, i64 n) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) a[i] = i;
+}
+
+void launch_iota_i64(hipStream_t s, i64* a, i64 n) {
+    if (n > 0) hipLaunchKernelGGL(k_iota_i64, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a, n);
+}
+
 void launch_flush_write(hipStream_t s, const i64* out_send, const i64* out_clock, i64 n_rows, const i64* blk_pre,
                         int nb, i64* flush_off, i64* flush_clock) {
     hipLaunchKernelGGL(k_flush_write, dim3(nb), dim3(kBlock), 0, s, out_send, out_clock, n_rows, blk_pre, flush_off,

@@ -371,7 +371,7 @@ int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& 
                           bool set, int64_t new_rc);
 int sliding_fifo_state(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs, int64_t* sc, bool set, int* kind);
 void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& bufs);
-void plane_host_save(sh_query* q, std::vector<uint8_t>& out);
+int plane_host_save(sh_query* q, std::vector<uint8_t>& out);
 int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used);
 
 int sliding_snapshot(sh_query* q, Writer& w) {
@@ -400,7 +400,7 @@ int sliding_snapshot(sh_query* q, Writer& w) {
         plane_state_buffers(q, bufs);
         for (auto& b : bufs) RCHK(w.dev(b.first->p, b.second, s));
         std::vector<uint8_t> hs;
-        plane_host_save(q, hs);
+        RCHK(plane_host_save(q, hs));
         w.val<uint64_t>(hs.size());
         w.put(hs.data(), hs.size());
     }

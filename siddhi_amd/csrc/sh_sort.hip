@@ -35,4 +35,20 @@ int sort_u64_pairs(void* temp, size_t* bytes, const u64* keys, u64* keys_out, co
     return e == hipSuccess ? 0 : -1;
 }
 
+// the same over key bits [0, end_bit) only (the partition lanes' (chunk, group) entry keys)
+int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
+                        i64 n, unsigned end_bit, hipStream_t s) {
+    hipError_t e =
+        rocprim::radix_sort_pairs(temp, *bytes, keys, keys_out, vals, vals_out, (unsigned)n, 0u, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}
+
+// stable sort of u64 keys over bits [0, end_bit), values = the keys' input positions
+int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,
+                       unsigned end_bit, hipStream_t s) {
+    rocprim::counting_iterator<u32> iota(0u);
+    hipError_t e = rocprim::radix_sort_pairs(temp, *bytes, keys, keys_out, iota, vals_out, (unsigned)n, 0u, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}
+
 }  // namespace shd

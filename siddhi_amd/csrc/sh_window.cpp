@@ -228,13 +228,17 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     const bool sliding_win = d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME;
     // partitioned lengthBatch / time keyed by the partition (no group-by, or group by the partition
     // key): one lane per partition (sh_plane.cpp)
-    const bool plane = d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
-                       (d->n_group_by == 0 || (d->n_group_by == 1 && d->group_by[0] == d->partition_col));
+    const bool by_partition = d->n_group_by == 0 || (d->n_group_by == 1 && d->group_by[0] == d->partition_col);
+    // ... and partitioned lengthBatch grouped by other columns: (partition, group) rows by sorting (lane 3)
+    const bool plane_group = d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
+                             !d->stream_current && d->n_aggs >= 1;
+    const bool plane = (d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
+                        by_partition) || plane_group;
     if ((!d->current_on || d->expired_on) &&
         !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch, timeBatch, externalTimeBatch, time and "
-                       "externalTime windows (partitioned: lengthBatch / time grouped by the partition key)");
+                       "externalTime windows (partitioned: lengthBatch, and time grouped by the partition key)");
     // (partitioned: lengthBatch lanes, every event its own chunk of one key)
     if (d->stream_current &&
         !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH))))
@@ -243,8 +247,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
                        "lengthBatch with no group-by or grouped by the partition key)");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "partitioned GPU queries support timeBatch, and lengthBatch / time with no group-by or "
-                       "grouped by the partition key");
+                       "partitioned GPU queries support timeBatch, lengthBatch, and time with no group-by or "
+                       "grouped by the partition key (lengthBatch(L, true) likewise)");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
                                   d->col_types[d->partition_col] == SH_T_LONG || d->col_types[d->partition_col] == SH_T_STRID)))
         return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/string column");
@@ -263,6 +267,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return rc;
     }
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
+    if (plane_group && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
+        delete q;
+        return rc;
+    }
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (d->n_group_by == 0 ? 1 : (1 << 16));
     if (d->partition_col >= 0 && !plane) {
         // R12: only partition p0 is ever aggregated. Its group keys are a sparse subset of the
@@ -271,6 +279,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->n_group_by == 1 && d->group_by[0] == d->partition_col) cap = 1;
     }
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
+    if (plane_group && (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0 && !plane;
@@ -1598,6 +1607,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     if (q->kind == 1) sliding_destroy(q);
     // device buffers are released by their destructors (stream-ordered on this context)
     q->kt.release();
+    q->gkt.release();
     if (q->h_info) (void)hipHostFree(q->h_info);
     if (q->small_res) (void)hipHostFree(q->small_res);
     if (q->zc_ring) (void)hipHostFree(q->zc_ring);

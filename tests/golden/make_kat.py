@@ -191,6 +191,28 @@ case(name="partition_tie_hashmap_order", source="hand-traced: core/util/Schedule
                  rep_cols=[["symbol", ["WSO2", "IBM", "ORACLE", "Aa", "BB", "BB", "x1", "Aa", "x2", "IBM", "x3",
                                        "WSO2", "x4", "ORACLE", "x5"]]]))
 
+# partitioned lengthBatch(3) grouped by a column other than the partition key, `insert all events`,
+# hand-traced (no reference test pins this shape; ctest/query/partition/WindowPartitionTestCase.java:96-139
+# is the query form). Every completed batch of a partition is one chunk [previous batch EXPIRED, RESET,
+# batch] (LengthBatchWindowProcessor.processFullBatchEvents :206-243) and processInBatchGroupBy
+# (QuerySelector.java:315-374) keeps one row per side in first-insertion order (LinkedHashMap.put):
+#   IBM batch 0 = buy 10, sell 20, buy 30   -> buy 40 (rep: buy 30), sell 20
+#   WSO2 batch 0 = buy 1, sell 2, sell 3     -> buy 1, sell 5
+#   IBM batch 1 = sell 5, sell 6, sell 7: chunk [EXPIRED buy 10, sell 20, buy 30, RESET, sell 5, 6, 7]:
+#     buy first met as EXPIRED -> its last expired event with the state emptied (sum null);
+#     sell first met as EXPIRED, then replaced by its last CURRENT row -> sell 18, at the EXPIRED position
+case(name="partition_lengthBatch_group_by_other_all", source="hand-traced: core/query/selector/QuerySelector.java:315-374, "
+     "core/query/processor/stream/window/LengthBatchWindowProcessor.java:206-243",
+     schema="symbol string, side string, price int",
+     query=dict(window="lengthBatch", param=3, partition="symbol", group_by=["side"], aggs=[["sum", "price"]],
+                output="all"),
+     sends=[[[B + i] + r] for i, r in enumerate([["IBM", "buy", 10], ["IBM", "sell", 20], ["WSO2", "buy", 1],
+                                                ["IBM", "buy", 30], ["WSO2", "sell", 2], ["WSO2", "sell", 3],
+                                                ["IBM", "sell", 5], ["IBM", "sell", 6], ["IBM", "sell", 7]])],
+     expect=dict(total_count=6, values=[[40], [20], [1], [5], [None], [18]],
+                 rep_cols=[["symbol", ["IBM", "IBM", "WSO2", "WSO2", "IBM", "IBM"]],
+                           ["side", ["buy", "sell", "buy", "sell", "buy", "sell"]]]))
+
 # ---------------------------------------------------------------- incremental aggregation (Aggregation1TestCase)
 AGG_SCHEMA = "symbol string, price float, lastClosingPrice float, volume long, quantity int, timestamp long"
 _t5 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", 70.0, 0.0, 40, 10, 1496289950000],

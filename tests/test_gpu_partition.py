@@ -137,3 +137,50 @@ def test_partitioned_lengthbatch_stream_current(rt, output, L, group, parts, zip
                          key_capacity=max(256, parts))
     ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 17_777, 40_000], 3), f"plb sc {L} {output}")
     assert ref["ts"].size > 0
+
+
+# ---- lane 3: partitioned lengthBatch grouped by columns other than the partition key --------------------
+GSCHEMA = abi.Schema.parse("p int, g int, v double, x long, ts long")
+
+
+def gstream(n, parts, groups, seed, runs=False, zipf=False):
+    ts, (p, v, x, ts2) = stream(n, parts, seed, runs=runs, zipf=zipf)
+    rng = np.random.default_rng(seed + 1)
+    g = rng.integers(0, groups, n).astype(np.int32)
+    return ts, [p, g, v, x, ts2]
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("L,group_by,parts,runs", [(1, ["g"], 50, False), (4, ["g"], 30, True),
+                                                   (37, ["g", "x"], 12, False), (5, ["x", "p"], 80, True)])
+def test_partitioned_lengthbatch_group_by_other(rt, output, L, group_by, parts, runs):
+    """Every completed batch of a partition is one chunk [previous batch EXPIRED, RESET, batch] whose
+    rows are one per group key in first-insertion order (QuerySelector.processInBatchGroupBy :315-374);
+    pushes cut batches open and send sizes put several partitions' batches into one send."""
+    ts, cols = gstream(30_000, parts, 7, 61, runs=runs)
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", L, group_by=group_by, aggs=AGGS, partition="p",
+                         filter=(">", "v", -30.0), output=output, key_capacity=1024)
+    ref = both(rt, spec, split_batches(GSCHEMA, ts, cols, [1, 9_001, 9_002, 21_000], 3), f"plg {L} {group_by} {output}")
+    assert ref["ts"].size > 0
+    if output != "current" and L > 1:
+        assert ref["expired"].sum() > 0
+
+
+def test_partitioned_lengthbatch_group_by_other_long_batches(rt):
+    """L larger than a push: batches stay open across pushes (carried records) before completing"""
+    ts, cols = gstream(40_000, 6, 20, 67)
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", 2_500, group_by=["g"], aggs=AGGS, partition="p", output="all",
+                         key_capacity=64)
+    pushes = split_batches(GSCHEMA, ts, cols, [700, 1_500, 8_000, 8_100, 30_000], 1)
+    ref = both(rt, spec, pushes, "plg long")
+    assert ref["expired"].sum() > 0
+
+
+def test_partitioned_lengthbatch_zipf_100k_partitions_second_group_column(rt):
+    """>= 100k Zipf partitions, grouped by (partition, a second column)"""
+    ts, cols = gstream(2_000_000, 1_000_000, 5, 73, zipf=True)
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", 3, group_by=["p", "g"],
+                         aggs=[("count", None), ("sum", "v"), ("max", "x")], partition="p", output="all",
+                         key_capacity=1 << 21)
+    ref = both(rt, spec, split_batches(GSCHEMA, ts, cols, [700_000], 1), "plg zipf")
+    assert len(np.unique(cols[0])) > 100_000 and ref["ts"].size > 10_000

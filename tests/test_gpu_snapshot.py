@@ -195,3 +195,17 @@ def test_partition_lanes_checkpoint(window, param, output, sc, cut):
     pushes.append(("advance", int(ts[-1]) + 1_000))
     got, ref, _ = checkpointed(spec, pushes, cut)
     assert_same(got, ref, label=f"lanes ckpt {window} {output}")
+
+
+@pytest.mark.parametrize("output", ["current", "all"])
+@pytest.mark.parametrize("cut", [1, 2])
+def test_partition_group_lanes_checkpoint(output, cut):
+    """lane 3 (partitioned lengthBatch grouped by another column): the carried open and last completed
+    batches and the group key table, restored into a fresh query"""
+    from tests.test_gpu_partition import GSCHEMA, gstream
+    ts, cols = gstream(60_000, 40, 9, 19 + cut)
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", 50, group_by=["g"], aggs=[("count", None), ("sum", "v"), ("min", "x")],
+                         partition="p", output=output, key_capacity=128)
+    pushes = split_batches(GSCHEMA, ts, cols, [20_000, 41_000], 1)
+    got, ref, _ = checkpointed(spec, pushes, cut)
+    assert_same(got, ref, label=f"group lanes ckpt {output}")
