@@ -404,6 +404,19 @@ void launch_rate_ftime_rehash(hipStream_t s, i64 old_cap, const u64* otk, const 
 void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, const u32* src, const int* eflush,
                         RateRows in, i64 in_stride, RateRows out, i64 T, int nk, int na, int* out_flush);
 
+// one limiter per partition instance (the partition lanes' rows carry their partition slot)
+void launch_ratep_pack(hipStream_t s, i64 S, i64 nc, const u32* c_part, const u32* in_part, u64* skey, u32* idx);
+void launch_ratep_flags(hipStream_t s, i64 S, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
+                        const u32* idx, int mode, i64 N, i64 nc, i64* pseq, const i64* flush_off, int nf, u32* flag,
+                        int* eflush, u32* src, u32* keep);
+void launch_ratep_fparts(hipStream_t s, int nf, const i64* foff, const u32* in_part, u32 none, u64* fkey, u32* fidx);
+void launch_ratep_ftime(hipStream_t s, int nf, const u32* hd, const u32* pos, const u32* starts, const u64* fkey,
+                        const u32* fidx, const i64* fclk, u32 none, i64 T, unsigned char* has, i64* last,
+                        unsigned char* chosen);
+void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, u64* okey, u32* olist);
+void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey, RateRows in, i64 in_stride,
+                         const u32* in_part, RateRows out, int nk, int na, int* out_flush, u32* out_part);
+
 // ---- stream.current.event batch windows (sh_kernels.hip, driven by sh_window.cpp) ----
 void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
                     int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send);

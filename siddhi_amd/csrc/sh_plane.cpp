@@ -315,12 +315,14 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             RCHK(s->pg_rkey.reserve(rc * 8, false));
             RCHK(s->pg_rkey2.reserve(rc * 8, false));
             RCHK(s->pg_order.reserve(rc * 4, false));
+            RCHK(s->pg_rpart.reserve(rc * 4, false));
+            RCHK(s->out_part.reserve(rc * 4, false));
             SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
                          s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
                          s->xr_nulls.as<unsigned char>(), rc};
             HIPCHK(hipEventRecord(q->ev_agg0, st));
             launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
-                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>());
+                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>());
             HIPCHK(hipEventRecord(q->ev_agg1, st));
             // ---- rows in (chunk, first entry) order
             const unsigned rbits = (unsigned)(32 + cbits);
@@ -342,7 +344,8 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             launch_pg_emit(st, s->pg_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, rc,
                            s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                            s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
-                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());
+                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(),
+                           s->pg_rpart.as<u32>(), s->out_part.as<u32>());
             HIPCHK(hipGetLastError());
             float kms = 0;
             (void)hipEventSynchronize(q->ev_agg1);
@@ -377,6 +380,11 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
     return sliding_output(q, n_rows, n_flushes, false, host_out, out);
 }
+
+int64_t plane_slots(sh_query* q) { return q->sl->nslots; }
+// key columns of the query's output rows (the lanes without group-by keep the partition key internal)
+int query_out_keys(sh_query* q) { return q->kind == 1 && q->sl && q->sl->nk_out >= 0 ? q->sl->nk_out : q->kp.n; }
+const u32* plane_out_part(sh_query* q) { return q->sl->out_part.as<u32>(); }
 
 // Lane pass of the push: records of M passing events sorted by slot (b == null: a TIMER call at `now`).
 static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
@@ -611,11 +619,13 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
         RCHK(s->out_clock.reserve(rcap * 8, false));
         RCHK(s->out_expired.reserve(rcap, false));
         RCHK(s->out_rep.reserve(rcap * 8, false));
+        RCHK(s->out_part.reserve(rcap * 4, false));
         if (n_rows > 0)
             launch_pl_emit(st, s->flags.as<unsigned char>(), n_pos, s->blk_cnt.as<int64_t>(), fblk, rows, na, s->nk_out,
                            q->kt.dev(), q->kp, rcap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(),
                            s->out_vals.as<u64>(), s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
-                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());
+                           s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(),
+                           s->out_part.as<u32>());
         HIPCHK(hipGetLastError());
     }
     int64_t n_flushes = 0;

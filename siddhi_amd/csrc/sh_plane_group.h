@@ -25,10 +25,11 @@ void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const
                       unsigned long long* n_entries);
 void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head);
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
-                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key);
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part);
 void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
                     i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
-                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
+                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep, const u32* row_part,
+                    u32* out_part);
 void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char* keep, PgRecs C, PgRecs D, int nv);
 // stable sort of (u64 key, u32 value) pairs over key bits [0, end_bit)
 int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,

@@ -157,7 +157,7 @@ template <int NA>
 __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_start, i64 n_seg, i64 n_e,
                                                const u64* __restrict__ ekey, const u32* __restrict__ eval,
                                                const u32* __restrict__ ranks, PgRecs C, AggPlan ap, int gbits,
-                                               SlxRows rows, u64* row_key) {
+                                               SlxRows rows, u64* row_key, u32* row_part) {
     const i64 sidx = (i64)blockIdx.x * 64 + threadIdx.x;
     if (sidx >= n_seg) return;
     const i64 lo = seg_start[sidx], hi = sidx + 1 < n_seg ? seg_start[sidx + 1] : n_e;
@@ -199,6 +199,7 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
     rows.ch[sidx] = C.seq[chunk];
     rows.clk[sidx] = C.clk[chunk];
     rows.exp[sidx] = cur ? 0 : 1;
+    row_part[sidx] = C.ps[chunk];
 #pragma unroll
     for (int a = 0; a < NA; a++) {
         if (a >= ap.n) continue;
@@ -218,20 +219,21 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
 }
 
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
-                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key) {
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part) {
     if (n_seg <= 0) return;
     const unsigned grid = (unsigned)((n_seg + 63) / 64);
     if (ap.n <= 4) hipLaunchKernelGGL(k_pg_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks,
-                                      C, ap, gbits, rows, row_key);
+                                      C, ap, gbits, rows, row_key, row_part);
     else hipLaunchKernelGGL(k_pg_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks, C, ap,
-                            gbits, rows, row_key);
+                            gbits, rows, row_key, row_part);
 }
 
 // ---- 4. the rows in (chunk, first entry) order -> the push's output columns
 __global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ order, i64 n, SlxRows rows, int n_aggs,
                                                    int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                                                    i64* out_keys, u64* out_vals, unsigned char* out_nulls,
-                                                   unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+                                                   unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep,
+                                                   const u32* __restrict__ row_part, u32* out_part) {
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (r >= n) return;
     const u32 j = order[r];
@@ -245,15 +247,17 @@ __global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ orde
     out_ch[r] = rows.ch[j];
     out_clock[r] = rows.clk[j];
     out_rep[r] = rows.rep[j];
+    out_part[r] = row_part[j];
 }
 
 void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
                     i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
-                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep, const u32* row_part,
+                    u32* out_part) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_pg_emit, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, order, n, rows,
                        n_aggs, nk, kt, kp, out_cap, out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock,
-                       out_rep);
+                       out_rep, row_part, out_part);
 }
 
 // ---- carried records: the kept ones (keep != 0) of the combined order, gathered in that (stream)

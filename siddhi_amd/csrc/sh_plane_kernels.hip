@@ -510,7 +510,7 @@ __global__ __launch_bounds__(kBlock) void k_pl_emit(const unsigned char* __restr
                                                    const i64* __restrict__ blk_pre, SlxRows rows, int n_aggs, int nk,
                                                    KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys,
                                                    u64* out_vals, unsigned char* out_nulls, unsigned char* out_exp,
-                                                   i64* out_ch, i64* out_clock, i64* out_rep) {
+                                                   i64* out_ch, i64* out_clock, i64* out_rep, u32* out_part) {
     const i64 tile = (i64)blockIdx.x * kTile;
     i64 acc = blk_pre[blockIdx.x];
     for (int it = 0; it < kItems; it++) {
@@ -530,15 +530,17 @@ __global__ __launch_bounds__(kBlock) void k_pl_emit(const unsigned char* __restr
         out_ch[r] = j;
         out_clock[r] = rows.clk[j];
         out_rep[r] = rows.rep[j];
+        out_part[r] = rows.slot[j];
     }
 }
 
 void launch_pl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
                     int n_aggs, int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                    unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+                    unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep,
+                    u32* out_part) {
     if (nblk <= 0) return;
     hipLaunchKernelGGL(k_pl_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rows, n_aggs, nk, kt, kp, out_cap,
-                       out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock, out_rep);
+                       out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock, out_rep, out_part);
 }
 
 }  // namespace shd

@@ -14,9 +14,14 @@
 #include <vector>
 
 #include "sh_agg.h"
+#include "sh_plane_group.h"
 #include "sh_runtime.h"
 
 using namespace shd;
+
+// the partition lanes (sh_plane.cpp): partition slots, and the partition slot of every output row
+int64_t plane_slots(sh_query* q);
+const u32* plane_out_part(sh_query* q);
 
 #define HIPCHK(x)                                                                                          \
     do {                                                                                                   \
@@ -40,13 +45,35 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     // a partitioned query holds one limiter per partition instance (PartitionRuntime clones the query);
     // the GPU's partitioned timeBatch flushes only partition p0 (R12), so its one limiter is p0's
     if (kind != SH_RATE_NONE && q->given) return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of a sharded query");
-    // the partition lanes (sh_plane.cpp) would need one limiter per partition instance
-    if (kind != SH_RATE_NONE && q->kind == 1 && q->d.partition_col >= 0)
-        return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of partitioned lengthBatch / time windows");
     if (kind != SH_RATE_NONE && q->kp.n > 2) return sh_fail(SH_ERR_UNSUPPORTED, "output rate with more than 2 group-by keys");
+    // the partition lanes (sh_plane.cpp): one limiter per partition instance. Grouped by the partition
+    // key, a partition's limiter sees one key, so the keyed First variants equal the global keyed ones
+    // (their state is per key) and LastGroupBy is the positional LastPerEvent of the partition.
+    const bool lanes = q->kind == 1 && q->d.partition_col >= 0;
+    bool gb = (lanes ? q->d.n_group_by > 0 : q->kp.n > 0) && kind != SH_RATE_ALL;
+    bool part = false;
+    if (lanes && kind != SH_RATE_NONE) {
+        if (gb && q->gkp.n > 0)
+            return sh_fail(SH_ERR_UNSUPPORTED,
+                           "output first / last every of a partitioned lengthBatch grouped by other columns (per-partition "
+                           "keyed limiters): `output all every`, or no group-by");
+        part = kind == SH_RATE_ALL || kind == SH_RATE_LAST || !gb;
+        if (part) gb = false;
+        const int64_t np = plane_slots(q);
+        auto& r = q->rate;
+        RCHK(r.pseq.reserve((size_t)np * 8, false));
+        RCHK(r.pft_has.reserve((size_t)np, false));
+        RCHK(r.pft_last.reserve((size_t)np * 8, false));
+        HIPCHK(hipMemsetAsync(r.pseq.p, 0, (size_t)np * 8, q->ctx->stream));
+        HIPCHK(hipMemsetAsync(r.pft_has.p, 0, (size_t)np, q->ctx->stream));
+        HIPCHK(hipMemsetAsync(r.pft_last.p, 0, (size_t)np * 8, q->ctx->stream));
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        r.nparts = np;
+    }
+    q->rate.part = part;
     q->rate.kind = kind;
     q->rate.N = n;
-    q->rate.gb = q->kp.n > 0 && kind != SH_RATE_ALL;
+    q->rate.gb = gb;
     q->rate.seq = 0;
     q->rate.nc = 0;
     q->rate.t_cap = 0;
@@ -139,6 +166,69 @@ static int grow_table(sh_query* q, int64_t need) {
     return SH_OK;
 }
 
+// the kept rows (o, T of them, o_flush = their emitting input flushes) -> output flushes and the
+// host or device view
+static int rate_finish(sh_query* q, const RateRows& o, int64_t T, int nk, int na, bool host_out, const sh_out** out) {
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    // output flushes: runs of equal emitting flush
+    r.h_flush.resize(std::max<int64_t>(T, 1));
+    if (T > 0) HIPCHK(hipMemcpyAsync(r.h_flush.data(), r.o_flush.p, (size_t)T * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    r.flush_offsets.assign(1, 0);
+    r.flush_clock.clear();
+    for (int64_t i = 0; i < T; i++) {
+        if (i + 1 == T || r.h_flush[i + 1] != r.h_flush[i]) {
+            r.flush_offsets.push_back(i + 1);
+            r.flush_clock.push_back(r.h_clk[r.h_flush[i]]);
+        }
+    }
+    if (host_out) {
+        OutHost& ho = q->out;
+        ho.reset();
+        ho.flush_offsets.assign(r.flush_offsets.begin(), r.flush_offsets.end());
+        ho.flush_clock.assign(r.flush_clock.begin(), r.flush_clock.end());
+        ho.ts.resize(T);
+        ho.expired.resize(T);
+        ho.rep.resize(T);
+        ho.keys.resize((size_t)nk * T);
+        ho.vals.resize((size_t)na * T);
+        ho.nulls.resize((size_t)na * T);
+        if (T > 0) {
+            HIPCHK(hipMemcpyAsync(ho.ts.data(), o.ts, T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(ho.expired.data(), o.expired, T, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(ho.rep.data(), o.rep, T * 8, hipMemcpyDeviceToHost, s));
+            if (nk) HIPCHK(hipMemcpyAsync(ho.keys.data(), o.keys, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
+            if (na) {
+                HIPCHK(hipMemcpyAsync(ho.vals.data(), o.vals, (size_t)na * T * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(ho.nulls.data(), o.nulls, (size_t)na * T, hipMemcpyDeviceToHost, s));
+            }
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        *out = ho.view(nk, na, q->vtypes);
+    } else {
+        sh_out& d = r.dev_out;
+        d = sh_out{};
+        d.n_flushes = (int64_t)r.flush_clock.size();
+        d.n_rows = T;
+        d.n_keys = nk;
+        d.n_vals = na;
+        for (int i = 0; i < na; i++) d.val_types[i] = q->vtypes[i];
+        d.flush_offsets = r.flush_offsets.data();
+        d.flush_clock = r.flush_clock.data();
+        d.ts = o.ts;
+        d.expired = o.expired;
+        d.keys = o.keys;
+        d.vals = (const uint64_t*)o.vals;
+        d.nulls = o.nulls;
+        d.rep = o.rep;
+        *out = &d;
+    }
+    return SH_OK;
+}
+
+static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, bool host_out, const sh_out** out);
+
 int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, const sh_out** out) {
     auto& r = q->rate;
     hipStream_t s = q->ctx->stream;
@@ -178,6 +268,7 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
     RCHK(r.foff.reserve((size_t)(nf + 1) * 8, false));
     HIPCHK(hipMemcpyAsync(r.foff.p, r.h_off.data(), (size_t)(nf + 1) * 8, hipMemcpyHostToDevice, s));
     const i64* foff = r.foff.as<i64>();
+    if (r.part) return rate_part(q, in, foff, nf, host_out, out);
 
     // the source rows: [carried rows | this call's rows]
     const bool carries = r.kind == SH_RATE_ALL || (r.kind == SH_RATE_LAST && r.gb);
@@ -333,58 +424,156 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
         r.nc = nn;
     }
     r.seq += n;
-    // output flushes: runs of equal emitting flush
-    r.h_flush.resize(std::max<int64_t>(T, 1));
-    if (T > 0) HIPCHK(hipMemcpyAsync(r.h_flush.data(), r.o_flush.p, (size_t)T * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    r.flush_offsets.assign(1, 0);
-    r.flush_clock.clear();
-    for (int64_t i = 0; i < T; i++) {
-        if (i + 1 == T || r.h_flush[i + 1] != r.h_flush[i]) {
-            r.flush_offsets.push_back(i + 1);
-            r.flush_clock.push_back(r.h_clk[r.h_flush[i]]);
-        }
+    return rate_finish(q, o, T, nk, na, host_out, out);
+}
+
+static unsigned bits_of(int64_t n) {  // bits needed for values < n
+    unsigned b = 1;
+    while (b < 63 && ((int64_t)1 << b) < n) b++;
+    return b;
+}
+
+// One limiter per partition instance (PartitionRuntimeImpl clones the query and its OutputRateLimiter):
+// `output all / first / last every N events` and `output first every <t>` without group-by run on each
+// partition's own row sequence. A flush of the lanes is one chunk of one partition, so the rows a
+// flush emits come from one partition; the kept rows leave ordered by their emitting flush.
+static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, bool host_out, const sh_out** out) {
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    const int nk = (int)in->n_keys, na = (int)in->n_vals;
+    const int64_t n = in->n_rows, N = r.N;
+    const u32* in_part = plane_out_part(q);
+    const bool carries = r.kind == SH_RATE_ALL;
+    const int64_t nc = carries ? r.nc : 0, S = nc + n;
+    RateRows inr{(i64*)in->ts, (unsigned char*)in->expired, (i64*)in->rep, (i64*)in->keys, (u64*)in->vals,
+                 (unsigned char*)in->nulls};
+    RateRows src = inr;
+    int64_t sstride = n;
+    const u32* sp = in_part;
+    if (nc > 0) {
+        RCHK(reserve_set(r.s_ts, r.s_exp, r.s_rep, r.s_keys, r.s_vals, r.s_nulls, S, nk, na, &src));
+        RateRows car{r.c_ts.as<i64>(), r.c_exp.as<unsigned char>(), r.c_rep.as<i64>(), r.c_keys.as<i64>(),
+                     r.c_vals.as<u64>(), r.c_nulls.as<unsigned char>()};
+        RCHK(copy_rows(s, src, S, car, nc, 0, nc, nk, na));
+        RateRows tail = src;
+        tail.ts += nc; tail.expired += nc; tail.rep += nc; tail.keys += nc; tail.vals += nc; tail.nulls += nc;
+        RCHK(copy_rows(s, tail, S, inr, n, 0, n, nk, na));
+        sstride = S;
+        RCHK(r.s_part.reserve((size_t)S * 4, false));
+        HIPCHK(hipMemcpyAsync(r.s_part.p, r.c_part.p, (size_t)nc * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(r.s_part.as<u32>() + nc, in_part, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+        sp = r.s_part.as<u32>();
     }
-    if (host_out) {
-        OutHost& ho = q->out;
-        ho.reset();
-        ho.flush_offsets.assign(r.flush_offsets.begin(), r.flush_offsets.end());
-        ho.flush_clock.assign(r.flush_clock.begin(), r.flush_clock.end());
-        ho.ts.resize(T);
-        ho.expired.resize(T);
-        ho.rep.resize(T);
-        ho.keys.resize((size_t)nk * T);
-        ho.vals.resize((size_t)na * T);
-        ho.nulls.resize((size_t)na * T);
-        if (T > 0) {
-            HIPCHK(hipMemcpyAsync(ho.ts.data(), o.ts, T * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(ho.expired.data(), o.expired, T, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(ho.rep.data(), o.rep, T * 8, hipMemcpyDeviceToHost, s));
-            if (nk) HIPCHK(hipMemcpyAsync(ho.keys.data(), o.keys, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
-            if (na) {
-                HIPCHK(hipMemcpyAsync(ho.vals.data(), o.vals, (size_t)na * T * 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipMemcpyAsync(ho.nulls.data(), o.nulls, (size_t)na * T, hipMemcpyDeviceToHost, s));
-            }
-            HIPCHK(hipStreamSynchronize(s));
-        }
-        *out = ho.view(nk, na, q->vtypes);
+    const int64_t m = std::max<int64_t>(S, nf);
+    RCHK(r.flag.reserve((size_t)(S + 1) * 4, false));
+    RCHK(r.keep.reserve((size_t)(S + 1) * 4, false));
+    RCHK(r.pre.reserve((size_t)(S + 1) * 4, false));
+    RCHK(r.src.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
+    RCHK(r.eflush.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
+    RCHK(r.tmp.reserve((size_t)((m + 1 + kTile - 1) / kTile + 16) * 8, false));
+    RCHK(r.skey.reserve((size_t)std::max<int64_t>(m, 1) * 8, false));
+    RCHK(r.skey2.reserve((size_t)std::max<int64_t>(m, 1) * 8, false));
+    RCHK(r.idx.reserve((size_t)std::max<int64_t>(m, 1) * 4, false));
+    RCHK(r.idx2.reserve((size_t)std::max<int64_t>(m, 1) * 4, false));
+    RCHK(r.hd.reserve((size_t)(m + 1) * 4, false));
+    RCHK(r.pos.reserve((size_t)(m + 1) * 4, false));
+    RCHK(r.starts.reserve((size_t)(m + 1) * 4, false));
+    RCHK(r.h_small.reserve(64));
+    const unsigned pbits = bits_of(r.nparts + 1);
+    size_t tb = 0;
+    if (r.kind == SH_RATE_FIRST_TIME) {
+        // the partitions' flushes in order, one walker per partition
+        RCHK(r.fclk.reserve((size_t)std::max(nf, 1) * 8, false));
+        RCHK(r.chosen.reserve((size_t)std::max(nf, 1), false));
+        if (nf) HIPCHK(hipMemcpyAsync(r.fclk.p, r.h_clk.data(), (size_t)nf * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(r.chosen.p, 0, (size_t)std::max(nf, 1), s));
+        const u32 none = (u32)r.nparts;
+        launch_ratep_fparts(s, nf, foff, in_part, none, r.skey.as<u64>(), r.idx.as<u32>());
+        if (sort_u64_pairs_bits(nullptr, &tb, r.skey.as<u64>(), nullptr, r.idx.as<u32>(), nullptr, nf, pbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
+        RCHK(r.sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_u64_pairs_bits(r.sort_tmp.p, &tb, r.skey.as<u64>(), r.skey2.as<u64>(), r.idx.as<u32>(), r.idx2.as<u32>(),
+                                nf, pbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
+        launch_rate_segments(s, nf, r.skey2.as<u64>(), r.idx2.as<u32>(), 1, 0, r.hd.as<u32>(), r.pos.as<u32>(),
+                             r.starts.as<u32>(), r.tmp.as<i64>());
+        launch_ratep_ftime(s, nf, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.skey2.as<u64>(), r.idx2.as<u32>(),
+                           r.fclk.as<i64>(), none, N, r.pft_has.as<unsigned char>(), r.pft_last.as<i64>(),
+                           r.chosen.as<unsigned char>());
+        launch_rate_ftime_rows(s, S, foff, nf, r.chosen.as<unsigned char>(), r.flag.as<u32>(), r.eflush.as<int>(),
+                               r.src.as<u32>());
     } else {
-        sh_out& d = r.dev_out;
-        d = sh_out{};
-        d.n_flushes = (int64_t)r.flush_clock.size();
-        d.n_rows = T;
-        d.n_keys = nk;
-        d.n_vals = na;
-        for (int i = 0; i < na; i++) d.val_types[i] = q->vtypes[i];
-        d.flush_offsets = r.flush_offsets.data();
-        d.flush_clock = r.flush_clock.data();
-        d.ts = o.ts;
-        d.expired = o.expired;
-        d.keys = o.keys;
-        d.vals = (const uint64_t*)o.vals;
-        d.nulls = o.nulls;
-        d.rep = o.rep;
-        *out = &d;
+        // every row's ordinal in its partition's sequence (carried rows first)
+        launch_ratep_pack(s, S, nc, r.c_part.as<u32>(), in_part, r.skey.as<u64>(), r.idx.as<u32>());
+        if (sort_u64_pairs_bits(nullptr, &tb, r.skey.as<u64>(), nullptr, r.idx.as<u32>(), nullptr, S, pbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
+        RCHK(r.sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_u64_pairs_bits(r.sort_tmp.p, &tb, r.skey.as<u64>(), r.skey2.as<u64>(), r.idx.as<u32>(), r.idx2.as<u32>(),
+                                S, pbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
+        launch_rate_segments(s, S, r.skey2.as<u64>(), r.idx2.as<u32>(), 1, 0, r.hd.as<u32>(), r.pos.as<u32>(),
+                             r.starts.as<u32>(), r.tmp.as<i64>());
+        launch_ratep_flags(s, S, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.skey2.as<u64>(), r.idx2.as<u32>(),
+                           r.kind, N, nc, r.pseq.as<i64>(), foff, nf, r.flag.as<u32>(), r.eflush.as<int>(), r.src.as<u32>(),
+                           r.keep.as<u32>());
     }
-    return SH_OK;
+    HIPCHK(hipGetLastError());
+    // kept rows, ordered by their emitting flush (stable: a group leaves in its own order)
+    HIPCHK(hipMemcpyAsync(r.pre.p, r.flag.p, (size_t)(S + 1) * 4, hipMemcpyDeviceToDevice, s));
+    launch_scan_sum_large_u32(s, r.pre.as<u32>(), S + 1, r.tmp.as<i64>());
+    HIPCHK(hipMemcpyAsync(r.h_small.p, r.pre.as<u32>() + S, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t T = *r.h_small.as<uint32_t>();
+    const int64_t tc = std::max<int64_t>(T, 1);
+    RCHK(r.okey.reserve((size_t)tc * 8, false));
+    RCHK(r.okey2.reserve((size_t)tc * 8, false));
+    RCHK(r.olist.reserve((size_t)tc * 4, false));
+    RCHK(r.olist2.reserve((size_t)tc * 4, false));
+    launch_ratep_list(s, S, r.flag.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), r.okey.as<u64>(), r.olist.as<u32>());
+    if (T > 0) {
+        const unsigned fbits = bits_of((int64_t)nf + 1);
+        tb = 0;
+        if (sort_u64_pairs_bits(nullptr, &tb, r.okey.as<u64>(), nullptr, r.olist.as<u32>(), nullptr, T, fbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
+        RCHK(r.sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_u64_pairs_bits(r.sort_tmp.p, &tb, r.okey.as<u64>(), r.okey2.as<u64>(), r.olist.as<u32>(),
+                                r.olist2.as<u32>(), T, fbits, s))
+            return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
+    }
+    RateRows o{};
+    RCHK(reserve_set(r.o_ts, r.o_exp, r.o_rep, r.o_keys, r.o_vals, r.o_nulls, T, nk, na, &o));
+    RCHK(r.o_flush.reserve((size_t)tc * 4, false));
+    launch_ratep_gather(s, T, r.olist2.as<u32>(), r.okey2.as<u64>(), src, sstride, sp, o, nk, na, r.o_flush.as<int>(),
+                        nullptr);
+    HIPCHK(hipGetLastError());
+    if (carries) {
+        // the partitions' open groups wait for their next rows (source order kept)
+        HIPCHK(hipMemcpyAsync(r.pre.p, r.keep.p, (size_t)(S + 1) * 4, hipMemcpyDeviceToDevice, s));
+        launch_scan_sum_large_u32(s, r.pre.as<u32>(), S + 1, r.tmp.as<i64>());
+        HIPCHK(hipMemcpyAsync(r.h_small.as<char>() + 8, r.pre.as<u32>() + S, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int64_t nn = *(const uint32_t*)(r.h_small.as<char>() + 8);
+        if (nn > 0) {
+            RCHK(r.olist.reserve((size_t)nn * 4, false));
+            RCHK(r.okey.reserve((size_t)nn * 8, false));
+            launch_ratep_list(s, S, r.keep.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), r.okey.as<u64>(),
+                              r.olist.as<u32>());
+            RateRows c2{};
+            DevBuf t_ts, t_exp, t_rep, t_keys, t_vals, t_nulls;
+            RCHK(reserve_set(t_ts, t_exp, t_rep, t_keys, t_vals, t_nulls, nn, nk, na, &c2));
+            RCHK(r.t_part.reserve((size_t)nn * 4, false));
+            launch_ratep_gather(s, nn, r.olist.as<u32>(), nullptr, src, sstride, sp, c2, nk, na, nullptr, r.t_part.as<u32>());
+            HIPCHK(hipGetLastError());
+            std::swap(r.c_ts, t_ts);
+            std::swap(r.c_exp, t_exp);
+            std::swap(r.c_rep, t_rep);
+            std::swap(r.c_keys, t_keys);
+            std::swap(r.c_vals, t_vals);
+            std::swap(r.c_nulls, t_nulls);
+            std::swap(r.c_part, r.t_part);
+        }
+        r.nc = nn;
+    }
+    r.seq += n;
+    return rate_finish(q, o, T, nk, na, host_out, out);
 }

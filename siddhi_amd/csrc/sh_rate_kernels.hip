@@ -360,4 +360,160 @@ void launch_rate_ftime_rehash(hipStream_t s, i64 old_cap, const u64* otk, const 
     hipLaunchKernelGGL(k_rate_ftime_rehash, dim3(grid_of(old_cap)), dim3(kBlock), 0, s, old_cap, otk, ott, tk, tt, tmask);
 }
 
+// ---- one limiter per partition instance (PartitionRuntimeImpl clones the query, so each partition
+// has its own OutputRateLimiter): the partition lanes' rows carry their partition slot. Rows sorted
+// stably by partition (carried rows first) give every row its ordinal within its partition's
+// sequence; the positional limiters run on those ordinals with a per-partition counter. ---------------
+__global__ __launch_bounds__(kBlock) void k_ratep_pack(i64 S, i64 nc, const u32* __restrict__ c_part,
+                                                      const u32* __restrict__ in_part, u64* skey, u32* idx) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S) return;
+    skey[i] = i < nc ? c_part[i] : in_part[i - nc];
+    idx[i] = (u32)i;
+}
+
+// per sorted position i (segment = one partition's rows in source order): ordinal o, the partition's
+// row count tot. ALL: complete groups of N leave at their last row (keep = the open group's rows);
+// FIRST / LAST: the partition's running count pseq decides.
+__global__ __launch_bounds__(kBlock) void k_ratep_flags(i64 S, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                       const u32* __restrict__ starts, const u64* __restrict__ skey,
+                                                       const u32* __restrict__ idx, int mode, i64 N, i64 nc,
+                                                       const i64* __restrict__ pseq, const i64* __restrict__ flush_off,
+                                                       int nf, u32* flag, int* eflush, u32* src, u32* keep) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > S) return;
+    if (i == S) { flag[S] = 0; keep[S] = 0; return; }
+    const u32 g = pos[i] + hd[i] - 1;
+    const i64 lo = starts[g], o = i - lo, tot = (i64)starts[g + 1] - lo;
+    const u32 r = idx[i];
+    u32 f = 0, k = 0;
+    i64 at = r;
+    if (mode == SH_RATE_ALL) {
+        if (o < tot / N * N) {
+            f = 1;
+            at = idx[lo + (o / N + 1) * N - 1];
+        } else {
+            k = 1;
+        }
+    } else {
+        const i64 sq = pseq[skey[i]] + o;
+        f = mode == SH_RATE_FIRST ? (N == 1 ? sq == 0 : sq % N == 0) : (sq % N == N - 1);
+    }
+    flag[r] = f;
+    keep[r] = k;
+    src[r] = r;
+    eflush[r] = f ? rate_flush_of(flush_off, nf, at - nc) : 0;
+}
+
+// after the flags: the partitions' counters advance by their rows of the call (FIRST with N == 1 keeps
+// the count growing: only the partition's very first row is ever sent)
+__global__ __launch_bounds__(kBlock) void k_ratep_advance(i64 S, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                         const u32* __restrict__ starts, const u64* __restrict__ skey,
+                                                         int mode, i64 N, i64* pseq) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S || !hd[i]) return;
+    const u32 g = pos[i];
+    const i64 tot = (i64)starts[g + 1] - i;
+    const i64 v = pseq[skey[i]] + tot;
+    pseq[skey[i]] = (mode == SH_RATE_FIRST && N == 1) ? v : v % N;
+}
+
+// `output first every <t>` without group-by, per partition: a flush (one chunk, one partition) sends its
+// first row when the partition has no output time yet or that time + t <= the flush's clock. Flushes
+// sorted stably by partition; one thread walks a partition's flushes in order.
+__global__ __launch_bounds__(kBlock) void k_ratep_fparts(int nf, const i64* __restrict__ foff, const u32* __restrict__ in_part,
+                                                        u32 none, u64* fkey, u32* fidx) {
+    const int f = blockIdx.x * kBlock + threadIdx.x;
+    if (f >= nf) return;
+    fkey[f] = foff[f + 1] > foff[f] ? in_part[foff[f]] : none;
+    fidx[f] = (u32)f;
+}
+
+__global__ __launch_bounds__(kBlock) void k_ratep_ftime(int nf, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                       const u32* __restrict__ starts, const u64* __restrict__ fkey,
+                                                       const u32* __restrict__ fidx, const i64* __restrict__ fclk, u32 none,
+                                                       i64 T, unsigned char* has, i64* last, unsigned char* chosen) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nf || !hd[i]) return;
+    const u32 g = pos[i];
+    const u64 p = fkey[i];
+    if (p == none) return;
+    unsigned char h = has[p];
+    i64 t = last[p];
+    for (u32 j = (u32)i; j < starts[g + 1]; j++) {
+        const u32 f = fidx[j];
+        if (!h || t + T <= fclk[f]) {
+            chosen[f] = 1;
+            h = 1;
+            t = fclk[f];
+        }
+    }
+    has[p] = h;
+    last[p] = t;
+}
+
+// flagged source rows -> (emitting flush, source index) lists, in source order
+__global__ __launch_bounds__(kBlock) void k_ratep_list(i64 S, const u32* __restrict__ flag, const u32* __restrict__ pre,
+                                                      const int* __restrict__ eflush, u64* okey, u32* olist) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S || !flag[i]) return;
+    okey[pre[i]] = (u64)(u32)eflush[i];
+    olist[pre[i]] = (u32)i;
+}
+
+// rows of a list (source indices) -> a row set of stride T; out_flush from okey when given
+__global__ __launch_bounds__(kBlock) void k_ratep_gather(i64 T, const u32* __restrict__ list, const u64* __restrict__ okey,
+                                                        RateRows in, i64 in_stride, const u32* __restrict__ in_part,
+                                                        RateRows out, int nk, int na, int* out_flush, u32* out_part) {
+    const i64 o = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (o >= T) return;
+    const u32 s = list[o];
+    out.ts[o] = in.ts[s];
+    out.expired[o] = in.expired[s];
+    out.rep[o] = in.rep[s];
+    for (int k = 0; k < nk; k++) out.keys[(size_t)k * T + o] = in.keys[(size_t)k * in_stride + s];
+    for (int a = 0; a < na; a++) {
+        out.vals[(size_t)a * T + o] = in.vals[(size_t)a * in_stride + s];
+        out.nulls[(size_t)a * T + o] = in.nulls[(size_t)a * in_stride + s];
+    }
+    if (out_flush) out_flush[o] = (int)okey[o];
+    if (out_part) out_part[o] = in_part[s];
+}
+
+void launch_ratep_pack(hipStream_t s, i64 S, i64 nc, const u32* c_part, const u32* in_part, u64* skey, u32* idx) {
+    if (S > 0) hipLaunchKernelGGL(k_ratep_pack, dim3(grid_of(S)), dim3(kBlock), 0, s, S, nc, c_part, in_part, skey, idx);
+}
+
+void launch_ratep_flags(hipStream_t s, i64 S, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
+                        const u32* idx, int mode, i64 N, i64 nc, i64* pseq, const i64* flush_off, int nf, u32* flag,
+                        int* eflush, u32* src, u32* keep) {
+    hipLaunchKernelGGL(k_ratep_flags, dim3(grid_of(S + 1)), dim3(kBlock), 0, s, S, hd, pos, starts, skey, idx, mode, N, nc,
+                       pseq, flush_off, nf, flag, eflush, src, keep);
+    if (mode != SH_RATE_ALL && S > 0)
+        hipLaunchKernelGGL(k_ratep_advance, dim3(grid_of(S)), dim3(kBlock), 0, s, S, hd, pos, starts, skey, mode, N, pseq);
+}
+
+void launch_ratep_fparts(hipStream_t s, int nf, const i64* foff, const u32* in_part, u32 none, u64* fkey, u32* fidx) {
+    if (nf > 0) hipLaunchKernelGGL(k_ratep_fparts, dim3(grid_of(nf)), dim3(kBlock), 0, s, nf, foff, in_part, none, fkey, fidx);
+}
+
+void launch_ratep_ftime(hipStream_t s, int nf, const u32* hd, const u32* pos, const u32* starts, const u64* fkey,
+                        const u32* fidx, const i64* fclk, u32 none, i64 T, unsigned char* has, i64* last,
+                        unsigned char* chosen) {
+    if (nf > 0)
+        hipLaunchKernelGGL(k_ratep_ftime, dim3(grid_of(nf)), dim3(kBlock), 0, s, nf, hd, pos, starts, fkey, fidx, fclk, none,
+                           T, has, last, chosen);
+}
+
+void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, u64* okey, u32* olist) {
+    if (S > 0) hipLaunchKernelGGL(k_ratep_list, dim3(grid_of(S)), dim3(kBlock), 0, s, S, flag, pre, eflush, okey, olist);
+}
+
+void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey, RateRows in, i64 in_stride,
+                         const u32* in_part, RateRows out, int nk, int na, int* out_flush, u32* out_part) {
+    if (T > 0)
+        hipLaunchKernelGGL(k_ratep_gather, dim3(grid_of(T)), dim3(kBlock), 0, s, T, list, okey, in, in_stride, in_part, out,
+                           nk, na, out_flush, out_part);
+}
+
 }  // namespace shd

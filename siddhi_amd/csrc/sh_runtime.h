@@ -373,6 +373,11 @@ struct sh_query {
         int64_t ft_last = 0;
         DevBuf ftk, ftt, ftk2, ftt2, fclk, chosen;
         int64_t ft_cap = 0, ft_keys = 0;
+        // one limiter per partition instance (the partition lanes): per partition slot the running row
+        // count (First/LastPerEvent) and `first every <t>`'s output time; the carried rows' partitions
+        bool part = false;
+        int64_t nparts = 0;
+        DevBuf c_part, s_part, t_part, pseq, pft_has, pft_last, keep, okey, okey2, olist, olist2;
         PinnedVec<int64_t> h_off, h_clk, flush_offsets, flush_clock;
         PinnedVec<int> h_flush;
         PinnedBuf h_small;

@@ -158,6 +158,7 @@ void launch_pl_walk_tm(hipStream_t s, const u32* key_off, const u32* sorted_rank
                        int cur_on, int exp_on, SlxRows rows, unsigned char* flags);
 void launch_pl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
                     int n_aggs, int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
-                    unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
+                    unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep,
+                    u32* out_part);
 
 }  // namespace shd

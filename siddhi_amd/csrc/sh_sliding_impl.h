@@ -73,7 +73,8 @@ struct SlidingImpl {
     // and the push's entry / segment / row scratch
     PgBufs pg[2];
     int64_t pg_n = 0;
-    DevBuf pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
+    DevBuf out_part;  // the lanes' output rows: partition slot of each (per-partition rate limiters)
+    DevBuf pg_rpart, pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
         pg_cnt;
 };
 

@@ -244,12 +244,14 @@ int batch_restore(sh_query* q, Reader& r) {
     return SH_OK;
 }
 
+int query_out_keys(sh_query* q);
+
 // Output rate limiter (sh_rate.cpp; the reference limiters' State: counters, the carried rows of an
 // open group, the FirstGroupBy key -> count table, `first every <t>`'s output time / key table)
 static int rate_snapshot(sh_query* q, Writer& w) {
     auto& r = q->rate;
     hipStream_t s = q->ctx->stream;
-    const int nk = q->kp.n, na = q->ap.n;
+    const int nk = query_out_keys(q), na = q->ap.n;
     w.val<int32_t>(r.kind);
     w.val<int64_t>(r.N);
     if (r.kind == SH_RATE_NONE) return SH_OK;
@@ -272,6 +274,13 @@ static int rate_snapshot(sh_query* q, Writer& w) {
     w.val<int64_t>(r.ft_keys);
     RCHK(w.dev(r.ftk.p, (size_t)r.ft_cap * 8, s));
     RCHK(w.dev(r.ftt.p, (size_t)r.ft_cap * 8, s));
+    if (r.part) {  // one limiter per partition: the carried rows' partitions and every partition's state
+        const size_t np = (size_t)r.nparts;
+        RCHK(w.dev(r.c_part.p, n * 4, s));
+        RCHK(w.dev(r.pseq.p, np * 8, s));
+        RCHK(w.dev(r.pft_has.p, np, s));
+        RCHK(w.dev(r.pft_last.p, np * 8, s));
+    }
     return SH_OK;
 }
 
@@ -298,6 +307,12 @@ static int rate_restore(sh_query* q, Reader& rd) {
     r.ft_keys = rd.val<int64_t>();
     RCHK(rd.dev(r.ftk, 8, s));
     RCHK(rd.dev(r.ftt, 8, s));
+    if (r.part) {
+        RCHK(rd.dev(r.c_part, 8, s));
+        RCHK(rd.dev(r.pseq, 8, s));
+        RCHK(rd.dev(r.pft_has, 8, s));
+        RCHK(rd.dev(r.pft_last, 8, s));
+    }
     if (!rd.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;
 }

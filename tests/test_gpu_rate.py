@@ -163,3 +163,44 @@ def test_first_every_time(rt, window, param, output, group_by, t):
     pushes = split_batches(SCHEMA, ts, cols, [3_000, 11_111], 2) + [("advance", int(ts[-1]) + 2_000)]
     out = both(rt, spec, pushes, label=f"{window} {output} first every {t} gb={group_by}")
     assert out["ts"].size > 0
+
+
+# ---- one limiter per partition instance on the partition lanes (sh_rate.cpp rate_part) ----------------
+PSCHEMA = abi.Schema.parse("p int, g int, v double, x long, ts long")
+PKINDS = [("all", 1), ("all", 3), ("first", 1), ("first", 2), ("last", 1), ("last", 3), ("first_time", 0),
+          ("first_time", 90)]
+
+
+def pstream(n, parts, seed):
+    rng = np.random.default_rng(seed)
+    ts = np.cumsum(rng.integers(0, 4, n)).astype(np.int64) + 5_000
+    p = rng.integers(0, parts, n).astype(np.int32)
+    g = rng.integers(0, 5, n).astype(np.int32)
+    v = rng.integers(-4000, 4000, n).astype(np.float64) / 16.0
+    x = rng.integers(-10**6, 10**6, n).astype(np.int64)
+    return ts, [p, g, v, x, ts.copy()]
+
+
+@pytest.mark.parametrize("kind,n", PKINDS)
+@pytest.mark.parametrize("window,param,group_by,output", [("lengthBatch", 3, [], "all"), ("lengthBatch", 4, ["p"], "current"),
+                                                         ("time", 60, ["p"], "all"), ("lengthBatch", 5, ["g"], "all")])
+def test_partition_lanes_rate(rt, kind, n, window, param, group_by, output):
+    """`partition with (p of S)` clones the query with its OutputRateLimiter per partition: each
+    partition's rows are counted (and, for `first every <t>`, timed) on their own"""
+    if group_by == ["g"] and kind != "all":
+        pytest.skip("keyed limiters of lane 3 are refused (test_partition_lanes_keyed_rate_refused_for_other_group_keys)")
+    ts, cols = pstream(20_000, 37, 7)
+    spec = abi.QuerySpec(PSCHEMA, window, param, group_by=group_by, aggs=[("count", None), ("sum", "v")],
+                         partition="p", output=output, key_capacity=64, rate=(kind, n))
+    pushes = split_batches(PSCHEMA, ts, cols, [1, 3_000, 11_111], 1)
+    if window == "time":
+        pushes.append(("advance", int(ts[-1]) + 1_000))
+    out = both(rt, spec, pushes, label=f"lanes {window} {group_by} {kind} {n}")
+    assert out["ts"].size > 0
+
+
+def test_partition_lanes_keyed_rate_refused_for_other_group_keys(rt):
+    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 5, group_by=["g"], aggs=[("count", None)], partition="p",
+                         key_capacity=64, rate=("last", 3))
+    with pytest.raises(rt.SiddhiError, match="grouped by other columns"):
+        rt.GpuQuery(spec)
