@@ -50,7 +50,7 @@ def parse():
                     help="N>1: slice = one global stream re-keyed over RCCL all-to-all; keyed = per-rank streams")
     ap.add_argument("--key-type", choices=["string", "int"], default="string",
                     help="k as a dictionary-encoded string (ids are dense key slots) or as an int (hashed)")
-    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "c5", "ext", "c2all", "c2cur", "c3all"],
+    ap.add_argument("--workload", choices=["c2", "c1", "c3", "c4", "c5", "ext", "c2all", "c2cur", "c3all", "plb", "plg"],
                     default="c2",
                     help="c2 = the headline (BASELINE configs[1]); c1/c3/c4/ext = secondary single-GPU lines; "
                          "c2all / c3all = C2 / C3 with `insert all events` (expired rows too), c2cur = C2 with "
@@ -184,6 +184,11 @@ SECONDARY = {
     # every event is read (20 B); only the partition that armed the shared timer is aggregated (R12)
     "c5": ("C5 partition with (k of S) begin from S#window.timeBatch(1 sec) select k, sum(v), count() group by k; "
            "10M Zipf(1.1) keys, 1M events per event-time second per GPU, per-event sends", 20.0),
+    # partition lanes (sh_plane*): input 20 B (+ 4 B group column) and the rows of the completed batches
+    "plb": ("partition with (k of S) begin from S#window.lengthBatch(16) select k, sum(v), count(), max(v) group by k; "
+            "C5's 10M Zipf(1.1) keys, per-event sends (one lane per partition)", 22.8),
+    "plg": ("partition with (k of S) begin from S#window.lengthBatch(16) select g, sum(v), count(), max(v) group by g; "
+            "C5's 10M Zipf(1.1) partition keys, 8 groups, per-event sends (sorted chunks, lane 3)", 43.0),
 }
 
 
@@ -225,6 +230,19 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
                              partition="k", key_capacity=10_000_000)
         send = 1
         gen = lambda i: synth.torch_zipf_stream((i * world + rank) * B, B, 0xC5, 10_000_000, 1000 * world, dev)[1]
+        mk = lambda cols: (cols[2], cols)
+    elif args.workload in ("plb", "plg"):
+        g = args.workload == "plg"
+        schema = abi.Schema.parse("k string, v double, ts long, g int" if g else "k string, v double, ts long")
+        spec = abi.QuerySpec(schema, "lengthBatch", 16, group_by=["g"] if g else ["k"],
+                             aggs=[("sum", "v"), ("count", None), ("max", "v")], partition="k", key_capacity=10_000_000)
+        send = 1
+
+        def gen(i):
+            cols = synth.torch_zipf_stream(i * B, B, 0xC5, 10_000_000, 1000, dev)[1]
+            if g:
+                cols.append(((cols[2] * 7 + torch.arange(B, device=dev)) % 8).to(torch.int32).contiguous())
+            return cols
         mk = lambda cols: (cols[2], cols)
     else:
         if args.workload == "c3":
@@ -289,7 +307,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
             st = q.stats()
             # C5's work is the scans over every event (R12 leaves one partition to aggregate); C4's the
             # root window and every roll-up level
-            kern_ms += st.push_ms if args.workload in ("c4", "c5", "c2all", "c2cur", "c3all") else st.main_kernel_ms
+            kern_ms += (st.push_ms if args.workload in ("c4", "c5", "c2all", "c2cur", "c3all", "plb", "plg")
+                        else st.main_kernel_ms)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -306,7 +325,7 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     roof = None
     if kern_ms > 0:
         ach = bpe * B * args.steps / (kern_ms / 1e3) / 1e9
-        kname = ("whole device pipeline of the push" if args.workload in ("c5", "c2all", "c2cur", "c3all") else
+        kname = ("whole device pipeline of the push" if args.workload in ("c5", "c2all", "c2cur", "c3all", "plb", "plg") else
                  "whole device pipeline of the push (root window + sec..day roll-up levels)" if args.workload == "c4"
                  else "main (aggregate / sliding)")
         roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,

@@ -15,11 +15,18 @@ timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -
   > gpurun_out/r4p_lane3.log 2>&1; rc=$?
 tail -15 gpurun_out/r4p_lane3.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "lane3 tests rc=$rc"; exit 1; fi
+for w in plb plg; do
+  timeout -k 10 300 python -u bench.py --workload $w --steps 5 --warmup 2 > gpurun_out/r4p_$w.json 2>gpurun_out/r4p_$w.err || { echo "$w bench failed"; tail -5 gpurun_out/r4p_$w.err; exit 1; }
+  cat gpurun_out/r4p_$w.json
+done
+SH_PL_SORT=1 timeout -k 10 300 python -u bench.py --workload plb --steps 5 --warmup 2 > gpurun_out/r4p_plb_sorted.json 2>gpurun_out/r4p_plbs.err || { echo "plb sorted bench failed"; tail -5 gpurun_out/r4p_plbs.err; exit 1; }
+cat gpurun_out/r4p_plb_sorted.json
 for v in 0 1 0 1; do
   SH_SL_RECORDS_SEQ=$v timeout -k 10 300 python -u bench.py --workload c3 --steps 5 --warmup 2 > gpurun_out/r4p_c3seq_$v.json 2>/dev/null || { echo c3 seq bench failed; exit 1; }
   python3 -c "import json;d=json.load(open('gpurun_out/r4p_c3seq_$v.json'));print('records_seq=$v', round(d['value']/1e9,3), 'Gev/s', round(d['ms_per_step'],2), 'ms')"
 done
-timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 3 > gpurun_out/r4p_c4.json 2>/dev/null && cat gpurun_out/r4p_c4.json
+timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 3 > gpurun_out/r4p_c4.json 2>/dev/null || { echo c4 bench failed; exit 1; }
+cat gpurun_out/r4p_c4.json
 for w in c2 c3 c4; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4p_$w -o $w -- python3 bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r4p_$w.log 2>&1 || { echo "$w prof failed"; tail gpurun_out/r4p_$w.log; exit 1; }
 done

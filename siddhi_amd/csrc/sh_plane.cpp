@@ -45,7 +45,7 @@ static int fill(DevBuf& b, size_t bytes, int v) {
 
 int plane_create(sh_query* q) {
     SlidingImpl* s = q->sl;
-    s->lane = q->gkp.n > 0 ? 3 : q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
+    s->lane = q->plane_sorted ? 3 : q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
     s->nk_out = q->d.n_group_by;
     const size_t n = (size_t)s->nslots;
     RCHK(fill(s->pl_last_ts, n * 8, 0x80));  // lastTimestamp = Long.MIN_VALUE (0x8080... < any real ts)

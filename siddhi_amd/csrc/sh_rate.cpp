@@ -53,7 +53,7 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     bool gb = (lanes ? q->d.n_group_by > 0 : q->kp.n > 0) && kind != SH_RATE_ALL;
     bool part = false;
     if (lanes && kind != SH_RATE_NONE) {
-        if (gb && q->gkp.n > 0)
+        if (gb && q->group_other)
             return sh_fail(SH_ERR_UNSUPPORTED,
                            "output first / last every of a partitioned lengthBatch grouped by other columns (per-partition "
                            "keyed limiters): `output all every`, or no group-by");

@@ -221,6 +221,7 @@ Tuning Tuning::from_env() {
     t.no_async_small = on("SH_NO_ASYNC_SMALL");
     t.sl_records_seq = on("SH_SL_RECORDS_SEQ");
     t.sweep = on("SH_SWEEP");
+    t.pl_sort = on("SH_PL_SORT");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
     return t;
 }

@@ -228,6 +228,7 @@ struct SlidingImpl;
 // SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower)
 struct Tuning {
     bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
+    bool pl_sort = false;  // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
     int agg_band_rows = 8;
     static Tuning from_env();
 };
@@ -254,6 +255,8 @@ struct sh_query {
     // partitions, gkp / gkt the output groups
     KeyPlan gkp{};
     KeyTableHost gkt;
+    bool plane_sorted = false;  // lane 3 (also for lengthBatch keyed by the partition with Tuning::pl_sort)
+    bool group_other = false;   // ... grouped by columns other than the partition key
     int P = 1, logP = 0, NL = 0;
     // playback clock + window state
     bool clock_valid = false;

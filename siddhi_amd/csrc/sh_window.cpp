@@ -267,7 +267,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return rc;
     }
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
-    if (plane_group && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
+    // lane 3: grouped by other columns, or (opt-in, SH_PL_SORT=1) lengthBatch keyed by the partition —
+    // the sorted chunks have no per-partition sequential walk, so a hot partition does not serialise
+    q->group_other = plane_group;
+    q->plane_sorted = plane_group || (plane && !kp_override && d->window == SH_WIN_LENGTH_BATCH && !d->stream_current &&
+                                      q->tune.pl_sort);
+    if (q->plane_sorted && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
         delete q;
         return rc;
     }
@@ -279,7 +284,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->n_group_by == 1 && d->group_by[0] == d->partition_col) cap = 1;
     }
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
-    if (plane_group && (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(cap))) { delete q; return rc; }
+    if (q->plane_sorted && (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(q->gkp.n ? cap : 1))) {
+        delete q;
+        return rc;
+    }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0 && !plane;

@@ -184,3 +184,25 @@ def test_partitioned_lengthbatch_zipf_100k_partitions_second_group_column(rt):
                          key_capacity=1 << 21)
     ref = both(rt, spec, split_batches(GSCHEMA, ts, cols, [700_000], 1), "plg zipf")
     assert len(np.unique(cols[0])) > 100_000 and ref["ts"].size > 10_000
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("L,group", [(1, True), (3, False), (100, True)])
+def test_partitioned_lengthbatch_sorted_lanes(rt, monkeypatch, output, L, group):
+    """SH_PL_SORT=1: lengthBatch keyed by the partition (or without group-by) on the sorted chunks of
+    lane 3 instead of one sequential lane per partition — the same rows"""
+    monkeypatch.setenv("SH_PL_SORT", "1")
+    ts, cols = stream(30_000, 40 if L == 100 else 200, 41, runs=True)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["p"] if group else [], aggs=AGGS, partition="p",
+                         filter=(">", "v", -30.0), output=output, key_capacity=256)
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 7_777, 20_000], 5), f"plb sorted {L} {output}")
+    assert ref["ts"].size > 0
+
+
+def test_partitioned_lengthbatch_sorted_lanes_zipf(rt, monkeypatch):
+    monkeypatch.setenv("SH_PL_SORT", "1")
+    ts, cols = stream(2_000_000, 1_000_000, 43, zipf=True)
+    spec = abi.QuerySpec(SCHEMA, "lengthBatch", 3, group_by=["p"], aggs=[("count", None), ("sum", "v"), ("max", "x")],
+                         partition="p", output="all", key_capacity=1_000_000)
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000], 1), "plb sorted zipf")
+    assert ref["ts"].size > 10_000
