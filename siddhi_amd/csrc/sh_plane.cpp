@@ -53,6 +53,12 @@ int plane_create(sh_query* q) {
     RCHK(fill(s->pl_prev_seq, n * 8, 0xff));  // -1: no batch flushed yet
     RCHK(fill(s->pl_key, n * 8, 0));
     if (s->lane == 2 && !s->rg.p) RCHK(s->rg.reserve(n * s->rc * 8, false));
+    if (q->d.window == SH_WIN_EXT_TIME_BATCH) {
+        RCHK(fill(s->pg_M, n * 8, 0));
+        RCHK(fill(s->pg_start, n * 8, 0));
+        RCHK(fill(s->pg_has, n, 0));
+        RCHK(fill(s->pg_bopen, n * 8, 0));
+    }
     return SH_OK;
 }
 
@@ -179,6 +185,7 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         RCHK(nb.clk.reserve(cap * 8, false));
         RCHK(nb.vals.reserve((size_t)V * cap * 8, false));
         RCHK(nb.prev.reserve(cap, false));
+        RCHK(nb.x.reserve(cap * 8, false));
         nb.cap = cap;
         to = std::move(nb);
     }
@@ -189,20 +196,23 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         HIPCHK(hipMemcpyAsync(to.seq.p, from.seq.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.clk.p, from.clk.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.prev.p, from.prev.p, keep, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.x.p, from.x.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpy2DAsync(to.vals.p, to.cap * 8, from.vals.p, from.cap * 8, keep * 8, V, hipMemcpyDeviceToDevice, st));
     }
     return SH_OK;
 }
 
-// Lane 3: partitioned lengthBatch(L) grouped by columns other than the partition key, by sorting
-// (sh_plane_group_kernels.hip). The records carried from earlier pushes (every partition's open batch
-// and, with expired output, its last completed batch) precede the push's own in one combined array.
+// Lane 3: partitioned lengthBatch(L) grouped by columns other than the partition key, and partitioned
+// externalTimeBatch, by sorting (sh_plane_group_kernels.hip). The records carried from earlier pushes
+// (every partition's open batch and, with expired output, its last completed batch) precede the push's
+// own in one combined array.
 static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
     const int64_t N = b->n, ss = b->send_size, L = q->d.window_param;
     const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
     if (N >= (int64_t)0x3FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 1G events");
     HIPCHK(hipEventRecord(q->ev_push0, st));
     const int64_t cap = std::max<int64_t>(N, 1);
@@ -214,8 +224,10 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
     RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
     RCHK(s->pg_prevcnt.reserve(s->nslots * 4, false));
+    RCHK(s->pg_pendcnt.reserve(s->nslots * 4, false));
     HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
     HIPCHK(hipMemsetAsync(s->pg_prevcnt.p, 0, s->nslots * 4, st));
+    HIPCHK(hipMemsetAsync(s->pg_pendcnt.p, 0, s->nslots * 4, st));
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
     ColSet cs{};
@@ -250,8 +262,18 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             std::swap(s->pg[0], s->pg[1]);
         }
         const PgRecs C = s->pg[0].view();
+        if (ext) {
+            RCHK(s->pg_xs.reserve(n * 8, false));
+            RCHK(s->pg_xv.reserve(n * 8, false));
+            RCHK(s->pg_ms.reserve(n * 8, false));
+            RCHK(s->pg_cts.reserve(n * 8, false));
+            RCHK(s->pg_err.reserve(64, false));
+            HIPCHK(hipMemsetAsync(s->pg_err.p, 0, 8, st));
+        }
         launch_pg_append(st, rec, M, n_old, q->seq, cs, q->gkp, q->gkt.dev(), V, C, s->slot_cnt.as<u32>(),
-                         s->pg_prevcnt.as<u32>());
+                         s->pg_prevcnt.as<u32>(), ext ? q->d.ts_col : -1,
+                         ext && q->d.has_start_time == 2 ? q->d.start_col : -1, s->pg_xs.as<int64_t>(),
+                         s->pg_pendcnt.as<u32>());
         HIPCHK(hipGetLastError());
         // ---- every partition's records in stream order
         RCHK(s->ranks.reserve(n * 4, false));
@@ -278,11 +300,41 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
         RCHK(s->pg_keep.reserve(n + 16, false));
         RCHK(s->pg_cnt.reserve(64, false));
         HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 8, st));
-        launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L, q->d.current_on,
-                         q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
-                         s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>());
+        PgExt X{};
+        if (ext) {
+            // the attribute's running max along every partition's run (rocPRIM scan by key)
+            X = PgExt{s->pg_M.as<int64_t>(), s->pg_start.as<int64_t>(), s->pg_has.as<unsigned char>(),
+                      s->pg_bopen.as<int64_t>(), q->d.has_start_time, q->d.ts_col, q->d.start_col, q->d.start_time,
+                      q->d.window_param};
+            tb = 0;
+            if (launch_pg_ext_scan(st, s->ranks.as<u32>(), s->p_slot.as<u32>(), C, n, s->pg_xv.as<int64_t>(),
+                                   s->pg_ms.as<int64_t>(), nullptr, &tb))
+                return sh_fail(SH_ERR_DEVICE, "scan sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (launch_pg_ext_scan(st, s->ranks.as<u32>(), s->p_slot.as<u32>(), C, n, s->pg_xv.as<int64_t>(),
+                                   s->pg_ms.as<int64_t>(), s->sort_tmp.p, &tb))
+                return sh_fail(SH_ERR_DEVICE, "scan failed");
+            launch_pg_assign_ext(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
+                                 s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, n,
+                                 q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
+                                 s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>(), s->pg_cts.as<int64_t>(),
+                                 s->pg_err.as<int>());
+            launch_pg_ext_state(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
+                                s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, s->nslots);
+        } else {
+            launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L,
+                             q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
+                             s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>());
+        }
         HIPCHK(hipGetLastError());
         RCHK(q->gkt.check(st));
+        if (ext) {
+            int64_t err = 0;
+            RCHK(read_count(q, s->pg_err.as<int64_t>(), &err));
+            if ((int32_t)err)
+                return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch: a partition's first event is before its start time "
+                                                   "(not on the GPU)");
+        }
         int64_t n_e = 0;
         RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
         if (n_e > 0) {
@@ -322,7 +374,8 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                          s->xr_nulls.as<unsigned char>(), rc};
             HIPCHK(hipEventRecord(q->ev_agg0, st));
             launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
-                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>());
+                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
+                           ext ? s->pg_cts.as<int64_t>() : nullptr);
             HIPCHK(hipEventRecord(q->ev_agg1, st));
             // ---- rows in (chunk, first entry) order
             const unsigned rbits = (unsigned)(32 + cbits);
@@ -663,6 +716,10 @@ void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& b
     const size_t n = (size_t)s->nslots;
     bufs = {{&s->pl_last_ts, n * 8}, {&s->pl_last_seq, n * 8}, {&s->pl_prev_seq, n * 8}, {&s->pl_key, n * 8}};
     if (s->lane == 2) bufs.push_back({&s->rg, n * (size_t)s->rc * 8});
+    if (q->d.window == SH_WIN_EXT_TIME_BATCH)
+        for (auto b : {std::make_pair(&s->pg_M, n * 8), std::make_pair(&s->pg_start, n * 8), std::make_pair(&s->pg_has, n),
+                       std::make_pair(&s->pg_bopen, n * 8)})
+            bufs.push_back(b);
 }
 
 // lane 3: the group key table and the carried records (in stream order)
@@ -695,6 +752,7 @@ static int pg_save(sh_query* q, std::vector<uint8_t>& out) {
     RCHK(dev(B.clk.p, n * 8));
     RCHK(dev(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(dev(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
+    RCHK(dev(B.x.p, n * 8));
     return SH_OK;
 }
 
@@ -718,7 +776,7 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     o += kb;
     get(&n, 8);
     const int V = std::max(1, q->ap.n_vcols);
-    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V) > len)
+    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V + 8) > len)
         return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     // validated: now replace the state
     if (kb) HIPCHK(hipMemcpyAsync(q->gkt.keys.p, keys, kb, hipMemcpyHostToDevice, st));
@@ -745,6 +803,7 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     RCHK(up(B.clk.p, n * 8));
     RCHK(up(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(up(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
+    RCHK(up(B.x.p, n * 8));
     HIPCHK(hipStreamSynchronize(st));  // the blob may be freed after the call
     s->pg_n = n;
     *used = o;

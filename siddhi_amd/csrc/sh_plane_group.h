@@ -16,16 +16,42 @@ struct PgRecs {
     u64* vals;           // [n_vcols][cap]
     unsigned char* prev; // carried as the partition's last completed batch
     i64 cap;
+    i64* x;              // externalTimeBatch: the timestamp attribute
+};
+
+// externalTimeBatch under `partition with` (ExternalTimeBatchWindowProcessor.process :238-311 per
+// partition): per partition slot the running max of the attribute (lastCurrentEventTime), the start,
+// and the bucket (M - start) / T of its open batch
+struct PgExt {
+    i64* M;
+    i64* start;
+    unsigned char* has;
+    i64* bopen;
+    int has_start;       // 0: first event's attribute, 1: constant, 2: start attribute
+    int xcol, scol;
+    i64 start_time, T;
 };
 
 void launch_pg_append(hipStream_t s, SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols, KeyPlan gkp,
-                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt);
+                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt, int xcol = -1, int scol = -1,
+                      i64* xs = nullptr, u32* pend_cnt = nullptr);
+// externalTimeBatch: the attribute in sorted order, its running max per partition run (rocPRIM
+// scan-by-key), the entries, then the partitions' state
+int launch_pg_ext_scan(hipStream_t s, const u32* ranks, const u32* p_sorted, PgRecs C, i64 n, i64* xv, i64* ms,
+                       void* temp, size_t* temp_bytes);
+void launch_pg_assign_ext(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                          PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 n, int cur_on, int exp_on, int gbits,
+                          u64 none, u64* ekey, u32* eval, unsigned char* keep, unsigned long long* n_entries, i64* chunk_ts,
+                          int* err);
+void launch_pg_ext_state(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                         PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 nslots);
 void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, PgRecs C, i64 n, i64 L,
                       int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval, unsigned char* keep,
                       unsigned long long* n_entries);
 void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head);
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
-                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part);
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,
+                    const i64* chunk_ts = nullptr);
 void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
                     i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
                     unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep, const u32* row_part,

@@ -19,6 +19,8 @@
 //   4. the rows are sorted by (chunk, first entry) and written in that order (k_pg_emit).
 // The records of incomplete batches (and the last completed batch, for expired output) are carried to
 // the next push in stream order (k_pg_assign marks them, k_pg_gather compacts them).
+#include <rocprim/device/device_scan_by_key.hpp>
+
 #include "sh_device.h"
 #include "sh_sliding.h"
 #include "sh_plane_group.h"
@@ -47,11 +49,16 @@ __device__ __forceinline__ double g_num(const AggPlan& ap, int a, u64 x) {
 // ---- 1. the push's records appended after the n_old carried ones (partition slot from the records
 // kernel, group slot looked up here), and the carried ones counted into the per-partition totals ----
 __global__ __launch_bounds__(kBlock) void k_pg_append(SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols,
-                                                     KeyPlan gkp, KeyTable gkt, int nv, PgRecs C) {
+                                                     KeyPlan gkp, KeyTable gkt, int nv, PgRecs C, int xcol, int scol,
+                                                     i64* xs) {
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (r >= M) return;
     const i64 c = n_old + r;
     const u32 e = rec.raw[r];
+    if (xcol >= 0) {
+        C.x[c] = load_raw(cols, xcol, e);
+        xs[c] = scol >= 0 ? load_raw(cols, scol, e) : 0;
+    }
     C.ps[c] = rec.slot[r];
     C.gs[c] = key_slot(gkt, make_key(gkp, cols, e));
     C.ts[c] = rec.ts[r];
@@ -61,22 +68,188 @@ __global__ __launch_bounds__(kBlock) void k_pg_append(SlRecords rec, i64 M, i64 
     for (int v = 0; v < nv; v++) C.vals[(size_t)v * C.cap + c] = rec.vals[(size_t)v * rec.cap + r];
 }
 
-__global__ __launch_bounds__(kBlock) void k_pg_count_old(PgRecs C, i64 n_old, u32* slot_cnt, u32* prev_cnt) {
+__global__ __launch_bounds__(kBlock) void k_pg_count_old(PgRecs C, i64 n_old, u32* slot_cnt, u32* prev_cnt,
+                                                        u32* pend_cnt) {
     const i64 c = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (c >= n_old) return;
     const u32 p = C.ps[c];
     atomicAdd(&slot_cnt[p], 1u);
     if (C.prev[c]) atomicAdd(&prev_cnt[p], 1u);
+    else if (pend_cnt) atomicAdd(&pend_cnt[p], 1u);
 }
 
 void launch_pg_append(hipStream_t s, SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols, KeyPlan gkp,
-                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt) {
+                      KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt, int xcol, int scol, i64* xs,
+                      u32* pend_cnt) {
     if (M > 0)
         hipLaunchKernelGGL(k_pg_append, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, n_old,
-                           seq_base, cols, gkp, gkt, nv, C);
+                           seq_base, cols, gkp, gkt, nv, C, xcol, scol, xs);
     if (n_old > 0)
         hipLaunchKernelGGL(k_pg_count_old, dim3((unsigned)((n_old + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, C,
-                           n_old, slot_cnt, prev_cnt);
+                           n_old, slot_cnt, prev_cnt, pend_cnt);
+}
+
+// ---- externalTimeBatch (ExternalTimeBatchWindowProcessor.process :238-311 per partition): an event
+// appends while its attribute t < endTime, else it flushes the batch and sets endTime =
+// findEndTime(lastCurrentEventTime) (:297, :440-444) = start + T((M - start) / T + 1), M the running max
+// of t. So an event starts a new batch exactly when (M - start) / T grows: the bucket of a partition's
+// running max names its batch, and the event crossing into a higher bucket closes the batch before it
+// (that event is the chunk's name; the expired rows are stamped with M there, flushToOutputChunk :341-348).
+__global__ __launch_bounds__(kBlock) void k_pg_xgather(const u32* __restrict__ ranks, PgRecs C, i64 n, i64* xv) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) xv[i] = C.x[ranks[i]];
+}
+
+struct MaxI64 {
+    __device__ __host__ i64 operator()(i64 a, i64 b) const { return a > b ? a : b; }
+};
+
+int launch_pg_ext_scan(hipStream_t s, const u32* ranks, const u32* p_sorted, PgRecs C, i64 n, i64* xv, i64* ms,
+                       void* temp, size_t* temp_bytes) {
+    if (temp && n > 0)
+        hipLaunchKernelGGL(k_pg_xgather, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ranks, C, n, xv);
+    const hipError_t e = rocprim::inclusive_scan_by_key(temp, *temp_bytes, p_sorted, xv, ms, (size_t)n, MaxI64(),
+                                                        rocprim::equal_to<u32>(), s);
+    return e == hipSuccess ? 0 : -1;
+}
+
+namespace {
+// a partition's run: [lo, lo + np) carried previous batch, [lo + np, a) carried open batch (bucket
+// bopen), [a, hi) the push's events
+struct ExtRun {
+    i64 lo, hi, np, a, Mcar, start, bopen;
+    bool has;
+};
+
+__device__ __forceinline__ ExtRun ext_run(const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                                          const PgRecs& C, const i64* xs, const PgExt& X, u32 p) {
+    ExtRun R;
+    R.lo = key_off[p];
+    R.hi = key_off[p + 1];
+    R.np = prev_cnt[p];
+    R.a = R.lo + R.np + pend_cnt[p];
+    R.has = X.has[p] != 0;
+    R.Mcar = R.has ? X.M[p] : INT64_MIN;
+    R.bopen = X.bopen[p];
+    if (R.has) {
+        R.start = X.start[p];
+    } else if (R.a >= R.hi) {
+        R.start = 0;  // no event of the partition yet
+    } else {
+        // initTiming (:313-334) at the partition's first event
+        const u32 c = ranks[R.a];
+        R.start = X.has_start == 1 ? X.start_time : X.has_start == 2 ? xs[c] : C.x[c];
+    }
+    return R;
+}
+
+// bucket of sorted position pos >= R.a (the push's events); -1 flags an event before the start
+__device__ __forceinline__ i64 ext_bucket(const ExtRun& R, const PgExt& X, const i64* ms, i64 pos, i64* m_out) {
+    const i64 m = max(R.Mcar, ms[pos]);
+    if (m_out) *m_out = m;
+    return m < R.start ? -1 : (m - R.start) / X.T;
+}
+
+__device__ __forceinline__ i64 ext_b(const ExtRun& R, const PgExt& X, const i64* ms, i64 pos) {
+    return pos < R.a ? R.bopen : ext_bucket(R, X, ms, pos, nullptr);
+}
+
+// first position in [from, R.hi) whose bucket exceeds b (buckets do not decrease along the run)
+__device__ __forceinline__ i64 ext_after(const ExtRun& R, const PgExt& X, const i64* ms, i64 from, i64 b) {
+    i64 lo = from, hi = R.hi;
+    while (lo < hi) {
+        const i64 mid = (lo + hi) >> 1;
+        if (ext_b(R, X, ms, mid) > b) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void k_pg_assign_ext(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                         const u32* __restrict__ prev_cnt, const u32* __restrict__ pend_cnt,
+                                                         PgRecs C, const i64* __restrict__ xs, const i64* __restrict__ ms,
+                                                         PgExt X, i64 n, int cur_on, int exp_on, int gbits, u64 none,
+                                                         u64* ekey, u32* eval, unsigned char* keep,
+                                                         unsigned long long* n_entries, i64* chunk_ts, int* err) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    int made = 0;
+    if (i < n) {
+        const u32 c = ranks[i];
+        const u32 p = C.ps[c];
+        const ExtRun R = ext_run(key_off, ranks, prev_cnt, pend_cnt, C, xs, X, p);
+        const u64 g = C.gs[c];
+        u64 kx = none, kc = none;
+        unsigned char kp = 0;
+        if (i >= R.a) {
+            i64 m;
+            if (ext_bucket(R, X, ms, i, &m) < 0 || R.start < 0) atomicExch(err, 1);
+            chunk_ts[c] = m;  // lastCurrentEventTime once this event is in (the expired rows' stamp)
+        }
+        if (i < R.lo + R.np) {
+            // the last completed batch: EXPIRED into the chunk that closes the open batch, else kept
+            const i64 x2 = ext_after(R, X, ms, R.lo + R.np, R.bopen);
+            if (x2 < R.hi) kx = ((u64)ranks[x2] << gbits) | g;
+            else kp = 1;
+        } else {
+            const i64 b = ext_b(R, X, ms, i);
+            const i64 x1 = ext_after(R, X, ms, i + 1, b);  // the event closing this batch
+            if (x1 < R.hi) {
+                if (cur_on) kc = ((u64)ranks[x1] << gbits) | g;
+                if (exp_on) {
+                    const i64 x2 = ext_after(R, X, ms, x1 + 1, ext_b(R, X, ms, x1));
+                    if (x2 < R.hi) kx = ((u64)ranks[x2] << gbits) | g;
+                    else kp = 1;
+                }
+            } else {
+                kp = 2;
+            }
+        }
+        if (!exp_on) kx = none;
+        ekey[2 * i] = kx;
+        ekey[2 * i + 1] = kc;
+        eval[2 * i] = (u32)i;
+        eval[2 * i + 1] = (u32)i | 0x80000000u;
+        keep[c] = kp;
+        made = (kx != none) + (kc != none);
+    }
+    const i64 tot = block_reduce((i64)made, SumOp(), 0);
+    if (threadIdx.x == 0 && tot) atomicAdd(n_entries, (unsigned long long)tot);
+}
+
+void launch_pg_assign_ext(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                          PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 n, int cur_on, int exp_on, int gbits,
+                          u64 none, u64* ekey, u32* eval, unsigned char* keep, unsigned long long* n_entries, i64* chunk_ts,
+                          int* err) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_pg_assign_ext, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
+                       prev_cnt, pend_cnt, C, xs, ms, X, n, cur_on, exp_on, gbits, none, ekey, eval, keep, n_entries,
+                       chunk_ts, err);
+}
+
+// after the entries: every partition with events in the push keeps its running max, start and the
+// bucket of its open batch
+__global__ __launch_bounds__(kBlock) void k_pg_ext_state(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                        const u32* __restrict__ prev_cnt, const u32* __restrict__ pend_cnt,
+                                                        PgRecs C, const i64* __restrict__ xs, const i64* __restrict__ ms,
+                                                        PgExt X, i64 nslots) {
+    const i64 p = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= nslots) return;
+    const ExtRun R = ext_run(key_off, ranks, prev_cnt, pend_cnt, C, xs, X, (u32)p);
+    if (R.a >= R.hi) return;  // no event of the push
+    i64 m;
+    const i64 b = ext_bucket(R, X, ms, R.hi - 1, &m);
+    X.M[p] = m;
+    X.start[p] = R.start;
+    X.has[p] = 1;
+    X.bopen[p] = b;
+}
+
+void launch_pg_ext_state(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                         PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 nslots) {
+    if (nslots > 0)
+        hipLaunchKernelGGL(k_pg_ext_state, dim3((unsigned)((nslots + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off,
+                           ranks, prev_cnt, pend_cnt, C, xs, ms, X, nslots);
 }
 
 // ---- 2. batch of every sorted position. Partition p's run [lo, hi) of the sorted order holds its
@@ -157,7 +330,8 @@ template <int NA>
 __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_start, i64 n_seg, i64 n_e,
                                                const u64* __restrict__ ekey, const u32* __restrict__ eval,
                                                const u32* __restrict__ ranks, PgRecs C, AggPlan ap, int gbits,
-                                               SlxRows rows, u64* row_key, u32* row_part) {
+                                               SlxRows rows, u64* row_key, u32* row_part,
+                                               const i64* __restrict__ chunk_ts) {
     const i64 sidx = (i64)blockIdx.x * 64 + threadIdx.x;
     if (sidx >= n_seg) return;
     const i64 lo = seg_start[sidx], hi = sidx + 1 < n_seg ? seg_start[sidx + 1] : n_e;
@@ -193,7 +367,7 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
     }
     const bool cur = last_c >= 0;
     const i64 rc = cur ? last_c : last_x;
-    rows.ts[sidx] = cur ? C.ts[rc] : C.clk[chunk];
+    rows.ts[sidx] = cur ? C.ts[rc] : chunk_ts ? chunk_ts[chunk] : C.clk[chunk];
     rows.rep[sidx] = C.seq[rc];
     rows.slot[sidx] = g;
     rows.ch[sidx] = C.seq[chunk];
@@ -219,13 +393,14 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
 }
 
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
-                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part) {
+                    const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,
+                    const i64* chunk_ts) {
     if (n_seg <= 0) return;
     const unsigned grid = (unsigned)((n_seg + 63) / 64);
     if (ap.n <= 4) hipLaunchKernelGGL(k_pg_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks,
-                                      C, ap, gbits, rows, row_key, row_part);
+                                      C, ap, gbits, rows, row_key, row_part, chunk_ts);
     else hipLaunchKernelGGL(k_pg_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks, C, ap,
-                            gbits, rows, row_key, row_part);
+                            gbits, rows, row_key, row_part, chunk_ts);
 }
 
 // ---- 4. the rows in (chunk, first entry) order -> the push's output columns
@@ -273,6 +448,7 @@ __global__ __launch_bounds__(kBlock) void k_pg_gather(const i64* __restrict__ id
     D.seq[k] = C.seq[c];
     D.clk[k] = C.clk[c];
     D.prev[k] = keep[c] == 1;
+    if (C.x) D.x[k] = C.x[c];
     for (int v = 0; v < nv; v++) D.vals[(size_t)v * D.cap + k] = C.vals[(size_t)v * C.cap + c];
 }
 

@@ -17,11 +17,11 @@ using shd::SlInfo;
 
 // lane 3 (partitioned lengthBatch grouped by other columns): a set of carried / combined records
 struct PgBufs {
-    DevBuf ps, gs, ts, seq, clk, vals, prev;
+    DevBuf ps, gs, ts, seq, clk, vals, prev, x;
     int64_t cap = 0;
     shd::PgRecs view() const {
         return shd::PgRecs{ps.as<uint32_t>(), gs.as<uint32_t>(), ts.as<int64_t>(), seq.as<int64_t>(), clk.as<int64_t>(),
-                           vals.as<shd::u64>(), prev.as<unsigned char>(), cap};
+                           vals.as<shd::u64>(), prev.as<unsigned char>(), cap, x.as<int64_t>()};
     }
 };
 
@@ -74,6 +74,8 @@ struct SlidingImpl {
     PgBufs pg[2];
     int64_t pg_n = 0;
     DevBuf out_part;  // the lanes' output rows: partition slot of each (per-partition rate limiters)
+    // externalTimeBatch lanes: per partition slot the running max, start, started flag, open bucket
+    DevBuf pg_M, pg_start, pg_has, pg_bopen, pg_pendcnt, pg_xs, pg_xv, pg_ms, pg_cts, pg_err;
     DevBuf pg_rpart, pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
         pg_cnt;
 };

@@ -220,8 +220,6 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->has_start_time == 2 &&
             (d->start_col < 0 || d->start_col >= d->n_cols || d->col_types[d->start_col] != SH_T_LONG))
             return sh_fail(SH_ERR_INVALID, "externalTimeBatch start time attribute must be long");
-        if (d->partition_col >= 0)
-            return sh_fail(SH_ERR_UNSUPPORTED, "partitioned externalTimeBatch is not on the GPU");
     }
     if (d->window_param <= 0) return sh_fail(SH_ERR_INVALID, "window length/period must be > 0");
     if (!d->current_on && !d->expired_on) return sh_fail(SH_ERR_INVALID, "query emits neither current nor expired events");
@@ -230,8 +228,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // key): one lane per partition (sh_plane.cpp)
     const bool by_partition = d->n_group_by == 0 || (d->n_group_by == 1 && d->group_by[0] == d->partition_col);
     // ... and partitioned lengthBatch grouped by other columns: (partition, group) rows by sorting (lane 3)
-    const bool plane_group = d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
-                             !d->stream_current && d->n_aggs >= 1;
+    // (and partitioned externalTimeBatch, any group-by: the same sorted chunks with batches by attribute time)
+    const bool plane_ext = d->partition_col >= 0 && d->window == SH_WIN_EXT_TIME_BATCH && d->n_aggs >= 1;
+    const bool plane_group = (d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
+                              !d->stream_current && d->n_aggs >= 1) || plane_ext;
     const bool plane = (d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
                         by_partition) || plane_group;
     if ((!d->current_on || d->expired_on) &&
@@ -247,7 +247,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
                        "lengthBatch with no group-by or grouped by the partition key)");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "partitioned GPU queries support timeBatch, lengthBatch, and time with no group-by or "
+                       "partitioned GPU queries support timeBatch, lengthBatch, externalTimeBatch, and time with no group-by or "
                        "grouped by the partition key (lengthBatch(L, true) likewise)");
     if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
                                   d->col_types[d->partition_col] == SH_T_LONG || d->col_types[d->partition_col] == SH_T_STRID)))
@@ -269,7 +269,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     // lane 3: grouped by other columns, or (opt-in, SH_PL_SORT=1) lengthBatch keyed by the partition —
     // the sorted chunks have no per-partition sequential walk, so a hot partition does not serialise
-    q->group_other = plane_group;
+    q->group_other = plane_group && !by_partition;
     q->plane_sorted = plane_group || (plane && !kp_override && d->window == SH_WIN_LENGTH_BATCH && !d->stream_current &&
                                       q->tune.pl_sort);
     if (q->plane_sorted && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {

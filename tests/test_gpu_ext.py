@@ -116,3 +116,38 @@ def test_ext_expired_and_all_events(output, group):
                split_batches(SCH, ts, cols, [20_000, 20_001, 64_000], 5), f"ext {output} {group}")
     if group is not False:  # (without group-by a chunk is one row: the current one replaces the expired)
         assert got["expired"].sum() > 1000
+
+
+# ---- `partition with (p of S)` around externalTimeBatch: every partition's own event-time batches
+# (the sorted partition lanes, sh_plane_group_kernels.hip) ----------------------------------------------
+PSCH = abi.Schema.parse("p int, k string, v double, et long, st long, ts long")
+
+
+def pstream(n, parts, seed, late_ms=0):
+    ts, cols = stream(n, 50, seed, late_ms=late_ms, per_ms=5)
+    rng = np.random.default_rng(seed + 7)
+    p = rng.integers(0, parts, n).astype(np.int32)
+    # each partition's event time starts at its own offset (its first event sets its start)
+    et = cols[2] + (p.astype(np.int64) % 7) * 333
+    st = cols[3] + (p.astype(np.int64) % 5) * 101
+    return ts, [p, cols[0], cols[1], et, st, cols[4]]
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("group_by,start,start_attr,late", [(["p"], None, None, 0), (["k"], 1_000, None, 800),
+                                                            ([], None, "st", 0), (["k", "p"], None, None, 400)])
+def test_partitioned_ext(output, group_by, start, start_attr, late):
+    ts, cols = pstream(60_000, 37, 0xE5, late_ms=late)
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 700, group_by=group_by, ts_attr="et", start_time=start,
+                       start_attr=start_attr, partition="p", key_capacity=4096, output=output,
+                       aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "et")])
+    both(sp, split_batches(PSCH, ts, cols, [1, 20_000, 20_001, 41_000], 3), f"pext {group_by} {output}")
+
+
+def test_partitioned_ext_checkpoint():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = pstream(40_000, 23, 0xE6, late_ms=300)
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 500, group_by=["k"], ts_attr="et", partition="p", key_capacity=4096,
+                       output="all", aggs=[("count", None), ("sum", "v"), ("max", "v")])
+    got, ref, _ = checkpointed(sp, split_batches(PSCH, ts, cols, [15_000, 30_000], 1), 1)
+    assert_same(got, ref, label="pext ckpt")
