@@ -5,14 +5,15 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_sliding_minmax.py \
   "tests/test_gpu_parity.py::test_c3_sliding_dictionary_keys" tests/test_gpu_scale.py::test_c3_time_10s_10k_keys_1k_resident_per_key \
-  tests/test_gpu_snapshot.py tests/test_gpu_ext.py -k "not group_lanes and not lanes_rate and not partitioned_ext" > gpurun_out/r4p_t.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r4p_t.log; exit 1; }
+  tests/test_gpu_snapshot.py tests/test_gpu_ext.py -k "not group_lanes and not lanes_rate and not partitioned_ext and not partitioned_external" > gpurun_out/r4p_t.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r4p_t.log; exit 1; }
 tail -1 gpurun_out/r4p_t.log
 # partition lanes grouped by another column (lane 3): assertion failures are reported, faults end the run
 timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_partition.py \
   tests/test_gpu_snapshot.py::test_partition_group_lanes_checkpoint "tests/test_gpu_parity.py::test_reference_kat_on_gpu[partition_lengthBatch_group_by_other_all]" \
   tests/test_gpu_rate.py::test_partition_lanes_rate tests/test_gpu_rate.py::test_partition_lanes_keyed_rate_refused_for_other_group_keys \
   tests/test_gpu_snapshot.py::test_partition_lanes_rate_checkpoint "tests/test_gpu_ext.py::test_partitioned_ext" \
-  tests/test_gpu_ext.py::test_partitioned_ext_checkpoint \
+  tests/test_gpu_ext.py::test_partitioned_ext_checkpoint tests/test_gpu_ext.py::test_partitioned_external_time \
+  tests/test_gpu_ext.py::test_partitioned_external_time_checkpoint \
   > gpurun_out/r4p_lane3.log 2>&1; rc=$?
 tail -15 gpurun_out/r4p_lane3.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "lane3 tests rc=$rc"; exit 1; fi

@@ -452,7 +452,9 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
     }
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
-    const bool tm = s->lane == 2, sched = tm && q->d.expired_on;
+    // (externalTime lanes: the window runs on the timestamp attribute, no TIMER calls reach it)
+    const bool xt = q->d.window == SH_WIN_EXT_TIME;
+    const bool tm = s->lane == 2, sched = tm && q->d.expired_on && !xt;
     const int64_t N = b ? b->n : 0, ss = b ? b->send_size : 0, T = q->d.window_param;
     const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
     if (!b) {
@@ -641,11 +643,16 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
             RCHK(s->x_blk.reserve((size_t)((N + kTile - 1) / kTile + 2) * 8, false));
             launch_pl_runs(st, cs, q->d.partition_col, N, ss, s->pl_start.as<unsigned char>(), s->x_blk.as<int64_t>(),
                            s->pl_run.as<int64_t>());
+            if (xt) {
+                RCHK(s->pl_x.reserve(cap * 8, false));
+                launch_pl_xattr(st, cs, q->d.ts_col, rec.raw, M, s->pl_x.as<int64_t>());
+            }
         }
         launch_pl_walk_tm(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->pl_run.as<int64_t>(), T, q->seq,
                           ss, nF ? s->pl_toff.as<int64_t>() : nullptr, s->pl_tsend.as<int64_t>(), s->pl_tclk.as<int64_t>(),
                           s->pl_tpos.as<int64_t>(), s->pl_fsend.as<int64_t>(), nF, state_of(s), s->rg.as<int64_t>(), q->ap,
-                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>());
+                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
+                          xt && b ? s->pl_x.as<int64_t>() : nullptr);
     }
     HIPCHK(hipEventRecord(q->ev_agg1, st));
     HIPCHK(hipGetLastError());
@@ -705,7 +712,7 @@ int plane_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out
 }
 
 int plane_advance(sh_query* q, int64_t now, const sh_out** out, bool host_out) {
-    return plane_run(q, nullptr, now, host_out, out);
+    return plane_run(q, nullptr, now, host_out, out);  // (externalTime: only the clock moves)
 }
 
 // ---- checkpoint of the partition lanes (sh_snapshot.cpp): per slot the lanes' device state beside the

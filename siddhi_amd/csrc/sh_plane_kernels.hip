@@ -265,6 +265,16 @@ __global__ __launch_bounds__(kBlock) void k_pl_slot_key(ColSet cols, KeyPlan kp,
     slot_key[key_slot(kt, key)] = v;
 }
 
+// externalTime lanes: every record's timestamp attribute
+__global__ __launch_bounds__(kBlock) void k_pl_xattr(ColSet cols, int xcol, const u32* __restrict__ raw, i64 M, i64* x) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r < M) x[r] = load_raw(cols, xcol, raw[r]);
+}
+
+void launch_pl_xattr(hipStream_t s, ColSet cols, int xcol, const u32* raw, i64 M, i64* x) {
+    if (M > 0) hipLaunchKernelGGL(k_pl_xattr, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, xcol, raw, M, x);
+}
+
 void launch_pl_slot_key(hipStream_t s, ColSet cols, KeyPlan kp, KeyTable kt, i64 N, i64* slot_key) {
     if (N <= 0) return;
     hipLaunchKernelGGL(k_pl_slot_key, dim3((unsigned)((N + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, kp, kt, N,
@@ -308,7 +318,7 @@ __global__ __launch_bounds__(64) void k_pl_walk_tm(const u32* __restrict__ key_o
                                                    const i64* __restrict__ t_send, const i64* __restrict__ t_clk,
                                                    const i64* __restrict__ t_pos, const i64* __restrict__ f_send,
                                                    i64 nF, SlState S, i64* rseq, AggPlan ap, int cur_on, int exp_on,
-                                                   SlxRows rows, unsigned char* flags) {
+                                                   SlxRows rows, unsigned char* flags, const i64* __restrict__ xattr) {
     const u32 k = blockIdx.x * 64 + threadIdx.x;
     if (k >= nslots) return;
     const u32 lo = key_off[k], hi = key_off[k + 1];
@@ -349,8 +359,9 @@ __global__ __launch_bounds__(64) void k_pl_walk_tm(const u32* __restrict__ key_o
             clk = now;
         } else {
             r = sorted_rank[i];
-            now = rec.clock[r];
-            clk = now;
+            clk = rec.clock[r];
+            // externalTime (ExternalTimeWindowProcessor :126-161): `now` is the event's attribute
+            now = xattr ? xattr[r] : clk;
             const i64 rn_ = run[rec.raw[r]];
             if (rn_ != cur_run) {
                 cur_run = rn_;
@@ -431,7 +442,7 @@ __global__ __launch_bounds__(64) void k_pl_walk_tm(const u32* __restrict__ key_o
 #pragma unroll
             for (int q = 0; q < NV; q++) v[q] = q < ap.n_vcols ? rec.vals[(size_t)q * rec.cap + r] : 0;
             const i64 sl = (rh + rlen) & rm;
-            S.rpm[(size_t)k * rc + sl] = rec.ts[r];
+            S.rpm[(size_t)k * rc + sl] = xattr ? xattr[r] : rec.ts[r];
             rseq[(size_t)k * rc + sl] = seq_base + (i64)rec.raw[r];
 #pragma unroll
             for (int q = 0; q < NV; q++)
@@ -490,13 +501,13 @@ __global__ __launch_bounds__(64) void k_pl_walk_tm(const u32* __restrict__ key_o
 void launch_pl_walk_tm(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
                        const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
                        const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, AggPlan ap,
-                       int cur_on, int exp_on, SlxRows rows, unsigned char* flags) {
+                       int cur_on, int exp_on, SlxRows rows, unsigned char* flags, const i64* xattr) {
     const unsigned grid = (unsigned)((nslots + 63) / 64);
     if (!grid) return;
 #define SH_PL_TM(A, V)                                                                                               \
     hipLaunchKernelGGL((k_pl_walk_tm<A, V>), dim3(grid), dim3(64), 0, s, key_off, sorted_rank, (u32)nslots, rec, run, \
                        T, seq_base, send_size, t_off, t_send, t_clk, t_pos, f_send, nF, S, rseq, ap, cur_on, exp_on,  \
-                       rows, flags)
+                       rows, flags, xattr)
     const int nv = ap.n_vcols < 1 ? 1 : ap.n_vcols;
     if (ap.n <= 4 && nv <= 1) SH_PL_TM(4, 1);
     else if (nv <= 2) SH_PL_TM(8, 2);

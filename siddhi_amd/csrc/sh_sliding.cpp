@@ -96,7 +96,7 @@ int sliding_create(sh_query* q) {
     q->sl = s;
     const bool plane = q->d.partition_col >= 0;  // partitioned lengthBatch / time keyed by the partition
     // expired output, pass-through, and the partition lanes' time windows keep each ring entry's 2nd word
-    s->xm = q->d.expired_on != 0 || q->ap.n == 0 || (plane && q->d.window == SH_WIN_TIME);
+    s->xm = q->d.expired_on != 0 || q->ap.n == 0 || (plane && (q->d.window == SH_WIN_TIME || q->d.window == SH_WIN_EXT_TIME));
     s->nslots = (int64_t)q->kt.size_ + 1;
     int F = std::max(1, q->ap.n_fields);
     int64_t n = s->nslots;

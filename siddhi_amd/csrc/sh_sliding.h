@@ -155,7 +155,8 @@ void launch_pl_notify(hipStream_t s, const u32* key_off, const u32* sorted_rank,
 void launch_pl_walk_tm(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
                        const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
                        const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, AggPlan ap,
-                       int cur_on, int exp_on, SlxRows rows, unsigned char* flags);
+                       int cur_on, int exp_on, SlxRows rows, unsigned char* flags, const i64* xattr = nullptr);
+void launch_pl_xattr(hipStream_t s, ColSet cols, int xcol, const u32* raw, i64 M, i64* x);
 void launch_pl_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
                     int n_aggs, int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                     unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep,

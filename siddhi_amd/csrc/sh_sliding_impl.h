@@ -64,7 +64,7 @@ struct SlidingImpl {
     int lane = 0;
     int nk_out = -1;  // output key columns (0: no group-by, the partition key is internal)
     DevBuf pl_last_ts, pl_last_seq, pl_prev_seq, pl_key, pl_start, pl_run, pl_reg, pl_toff, pl_tsend, pl_tclk,
-        pl_tpos, pl_fsend;
+        pl_tpos, pl_fsend, pl_x;
     std::unordered_map<uint32_t, std::deque<int64_t>> pl_pend;
     std::set<std::pair<int64_t, uint32_t>> pl_armed;  // (front notify time, slot)
     shj::JavaStringMap pl_states;

@@ -232,7 +232,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     const bool plane_ext = d->partition_col >= 0 && d->window == SH_WIN_EXT_TIME_BATCH && d->n_aggs >= 1;
     const bool plane_group = (d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
                               !d->stream_current && d->n_aggs >= 1) || plane_ext;
-    const bool plane = (d->partition_col >= 0 && (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME) &&
+    const bool plane = (d->partition_col >= 0 &&
+                        (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
                         by_partition) || plane_group;
     if ((!d->current_on || d->expired_on) &&
         !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane)

@@ -151,3 +151,24 @@ def test_partitioned_ext_checkpoint():
                        output="all", aggs=[("count", None), ("sum", "v"), ("max", "v")])
     got, ref, _ = checkpointed(sp, split_batches(PSCH, ts, cols, [15_000, 30_000], 1), 1)
     assert_same(got, ref, label="pext ckpt")
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("group,late,send_size", [(True, 0, 1), (False, 600, 4), (True, 900, 1)])
+def test_partitioned_external_time(output, group, late, send_size):
+    """`partition with` around externalTime(et, T): one lane per partition whose queue expires by the
+    event's attribute (ExternalTimeWindowProcessor :126-161 per partition state)"""
+    ts, cols = pstream(40_000, 29, 0xE8, late_ms=late)
+    sp = abi.QuerySpec(PSCH, "externalTime", 400, group_by=["p"] if group else [], ts_attr="et", partition="p",
+                       key_capacity=64, output=output, aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "et")])
+    pushes = split_batches(PSCH, ts, cols, [1, 12_000, 30_000], send_size) + [("advance", int(ts[-1]) + 5_000)]
+    both(sp, pushes, f"pxt {group} {output}")
+
+
+def test_partitioned_external_time_checkpoint():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = pstream(30_000, 17, 0xE9, late_ms=300)
+    sp = abi.QuerySpec(PSCH, "externalTime", 300, group_by=["p"], ts_attr="et", partition="p", key_capacity=64,
+                       output="all", aggs=[("count", None), ("sum", "v"), ("max", "v")])
+    got, ref, _ = checkpointed(sp, split_batches(PSCH, ts, cols, [10_000, 20_000], 1), 1)
+    assert_same(got, ref, label="pxt ckpt")
