@@ -53,6 +53,12 @@ int plane_create(sh_query* q) {
     RCHK(fill(s->pl_prev_seq, n * 8, 0xff));  // -1: no batch flushed yet
     RCHK(fill(s->pl_key, n * 8, 0));
     if (s->lane == 2 && !s->rg.p) RCHK(s->rg.reserve(n * s->rc * 8, false));
+    if (q->group_other && s->lane == 2) {
+        // (partition, group) states of the time lanes grouped by other columns: count and sums
+        s->pg_st_n = (int64_t)q->pgkt.size_ + 1;
+        RCHK(fill(s->pg_st_cnt, (size_t)s->pg_st_n * 8, 0));
+        RCHK(fill(s->pg_st_f, (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n * 8, 0));
+    }
     if (q->d.window == SH_WIN_EXT_TIME_BATCH) {
         RCHK(fill(s->pg_M, n * 8, 0));
         RCHK(fill(s->pg_start, n * 8, 0));
@@ -434,6 +440,133 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     return sliding_output(q, n_rows, n_flushes, false, host_out, out);
 }
 
+// Time / externalTime lanes grouped by other columns (sh_plane_group_kernels.hip, k_pg_walk_ops /
+// k_pg_replay): the partitions' walks write their add / remove operations, the operations sorted stably
+// by (partition, group) state are replayed one thread per state, rows sorted by (chunk, first operation).
+static int group_time_rows(sh_query* q, const ColSet* cs, SlRecords rec, int64_t M, int64_t nF, int64_t T, int64_t ss,
+                           bool xt, int64_t* n_rows_out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    const int nv = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    const int64_t np = s->nslots;
+    if (cs && M > 0) {
+        launch_pg_rec_group(st, rec, M, *cs, q->gkp, q->gkt.dev(), nv);
+        HIPCHK(hipGetLastError());
+    }
+    // every partition's operation region
+    RCHK(s->pg_room.reserve((size_t)(np + 1) * 8, false));
+    RCHK(s->tmp.reserve((size_t)((np + 1 + kTile - 1) / kTile + 16) * 8, false));
+    HIPCHK(hipMemsetAsync(s->pg_room.as<int64_t>() + np, 0, 8, st));
+    launch_pg_ops_room(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), np, s->pg_room.as<int64_t>());
+    launch_scan_sum_large(st, s->pg_room.as<int64_t>(), np + 1, s->tmp.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    int64_t ocap = 0;
+    RCHK(read_count(q, s->pg_room.as<int64_t>() + np, &ocap));
+    RCHK(q->gkt.check(st));
+    if (ocap >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "partition lanes: more than 4G window operations");
+    const int64_t oc = std::max<int64_t>(ocap, 1);
+    RCHK(s->op_pos.reserve(oc * 8, false));
+    RCHK(s->op_pg.reserve(oc * 4, false));
+    RCHK(s->op_kind.reserve(oc, false));
+    RCHK(s->op_seq.reserve(oc * 8, false));
+    RCHK(s->op_ts.reserve(oc * 8, false));
+    RCHK(s->op_clk.reserve(oc * 8, false));
+    RCHK(s->op_vals.reserve((size_t)nv * oc * 8, false));
+    RCHK(s->pg_ocnt.reserve((size_t)np * 4, false));
+    HIPCHK(hipMemsetAsync(s->op_pg.p, 0xff, oc * 4, st));
+    HIPCHK(hipMemsetAsync(s->pg_ocnt.p, 0, (size_t)np * 4, st));
+    PgOps O{s->op_pos.as<int64_t>(), s->op_pg.as<u32>(), s->op_kind.as<unsigned char>(), s->op_seq.as<int64_t>(),
+            s->op_ts.as<int64_t>(), s->op_clk.as<int64_t>(), s->op_vals.as<u64>(), oc};
+    HIPCHK(hipEventRecord(q->ev_agg0, st));
+    launch_pg_walk_ops(st, s->key_off.as<u32>(), s->ranks.as<u32>(), np, rec, s->pl_run.as<int64_t>(), T, q->seq, ss,
+                       nF ? s->pl_toff.as<int64_t>() : nullptr, s->pl_tsend.as<int64_t>(), s->pl_tclk.as<int64_t>(),
+                       s->pl_tpos.as<int64_t>(), s->pl_fsend.as<int64_t>(), nF, state_of(s), s->rg.as<int64_t>(), nv,
+                       xt ? s->pl_x.as<int64_t>() : nullptr, q->pgkt.dev(), s->pg_room.as<int64_t>(), O,
+                       s->pg_ocnt.as<u32>());
+    HIPCHK(hipGetLastError());
+    RCHK(q->pgkt.check(st));
+    RCHK(s->pg_cnt.reserve(64, false));
+    HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 16, st));
+    launch_pg_sum_u32(st, s->pg_ocnt.as<u32>(), np, s->pg_cnt.as<unsigned long long>());
+    int64_t n_ops = 0;
+    RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_ops));
+    int64_t n_rows = 0;
+    if (n_ops > 0) {
+        // operations by state slot, each state's in its partition's order
+        RCHK(s->pg_skey.reserve(oc * 4, false));
+        RCHK(s->pg_sidx.reserve(oc * 4, false));
+        size_t tb = 0;
+        if (sort_slot_ranks(nullptr, &tb, O.pg, nullptr, nullptr, ocap, (int64_t)1 << 32, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_slot_ranks(s->sort_tmp.p, &tb, O.pg, s->pg_skey.as<u32>(), s->pg_sidx.as<u32>(), ocap, (int64_t)1 << 32, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        RCHK(s->pg_head.reserve(n_ops + 16, false));
+        RCHK(s->pg_seg.reserve(n_ops * 8, false));
+        RCHK(s->x_blk.reserve((size_t)((n_ops + kTile - 1) / kTile + 2) * 8, false));
+        launch_pg_heads32(st, s->pg_skey.as<u32>(), n_ops, s->pg_head.as<unsigned char>());
+        launch_slx_compact(st, 1, s->pg_head.as<unsigned char>(), nullptr, nullptr, nullptr, n_ops, s->x_blk.as<int64_t>(),
+                           nullptr, nullptr, s->pg_seg.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        int64_t n_seg = 0;
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (n_ops + kTile - 1) / kTile, &n_seg));
+        // replay: at most one row per operation
+        const int64_t rc = n_ops;
+        RCHK(s->xr_ts.reserve(rc * 8, false));
+        RCHK(s->xr_rep.reserve(rc * 8, false));
+        RCHK(s->xr_slot.reserve(rc * 4, false));
+        RCHK(s->xr_ch.reserve(rc * 8, false));
+        RCHK(s->xr_clk.reserve(rc * 8, false));
+        RCHK(s->xr_exp.reserve(rc, false));
+        RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * rc * 8, false));
+        RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * rc, false));
+        RCHK(s->pg_rkey.reserve(rc * 8, false));
+        RCHK(s->pg_rkey2.reserve(rc * 8, false));
+        RCHK(s->pg_order.reserve(rc * 4, false));
+        RCHK(s->pg_rpart.reserve(rc * 4, false));
+        SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                     s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                     s->xr_nulls.as<unsigned char>(), rc};
+        HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 16, st));
+        launch_pg_replay(st, s->pg_seg.as<int64_t>(), n_seg, n_ops, s->pg_skey.as<u32>(), s->pg_sidx.as<u32>(), O,
+                         q->pgkt.dev(), s->pg_st_cnt.as<int64_t>(), s->pg_st_f.as<u64>(), s->pg_st_n, q->ap, q->d.current_on,
+                         q->d.expired_on, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
+                         (unsigned int*)s->pg_cnt.p);
+        HIPCHK(hipGetLastError());
+        RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_rows));
+        n_rows &= 0xFFFFFFFFll;
+        if (n_rows > 0) {
+            // rows in (chunk, first operation) order
+            int pbits = 1;
+            while (pbits < 31 && ((int64_t)1 << pbits) <= M + nF) pbits++;
+            size_t tb2 = 0;
+            if (sort_u64_iota_bits(nullptr, &tb2, s->pg_rkey.as<u64>(), nullptr, nullptr, n_rows, 32 + pbits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb2, 16), false));
+            if (sort_u64_iota_bits(s->sort_tmp.p, &tb2, s->pg_rkey.as<u64>(), s->pg_rkey2.as<u64>(), s->pg_order.as<u32>(),
+                                   n_rows, 32 + pbits, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        }
+        const int64_t rcap = std::max<int64_t>(n_rows, 1);
+        RCHK(s->out_ts.reserve(rcap * 8, false));
+        RCHK(s->out_keys.reserve((size_t)std::max(1, q->gkp.n) * rcap * 8, false));
+        RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * rcap * 8, false));
+        RCHK(s->out_nulls.reserve((size_t)std::max(na, 1) * rcap, false));
+        RCHK(s->out_send.reserve(rcap * 8, false));
+        RCHK(s->out_clock.reserve(rcap * 8, false));
+        RCHK(s->out_expired.reserve(rcap, false));
+        RCHK(s->out_rep.reserve(rcap * 8, false));
+        RCHK(s->out_part.reserve(rcap * 4, false));
+        launch_pg_emit(st, s->pg_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, rcap,
+                       s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
+                       s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(), s->out_send.as<int64_t>(),
+                       s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(), s->pg_rpart.as<u32>(), s->out_part.as<u32>());
+        HIPCHK(hipGetLastError());
+    }
+    *n_rows_out = n_rows;
+    return SH_OK;
+}
+
 int64_t plane_slots(sh_query* q) { return q->sl->nslots; }
 // key columns of the query's output rows (the lanes without group-by keep the partition key internal)
 int query_out_keys(sh_query* q) { return q->kind == 1 && q->sl && q->sl->nk_out >= 0 ? q->sl->nk_out : q->kp.n; }
@@ -455,8 +588,9 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
     // (externalTime lanes: the window runs on the timestamp attribute, no TIMER calls reach it)
     const bool xt = q->d.window == SH_WIN_EXT_TIME;
     const bool tm = s->lane == 2, sched = tm && q->d.expired_on && !xt;
+    const bool grp = tm && q->group_other;  // time lanes grouped by other columns (operations, then states)
     const int64_t N = b ? b->n : 0, ss = b ? b->send_size : 0, T = q->d.window_param;
-    const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    const int V = std::max(1, q->ap.n_vcols) + (grp ? 1 : 0), na = q->ap.n;
     if (!b) {
         if (q->clock_valid && now < q->clock) return empty_out(q, out);
         q->clock = now;
@@ -648,16 +782,38 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
                 launch_pl_xattr(st, cs, q->d.ts_col, rec.raw, M, s->pl_x.as<int64_t>());
             }
         }
-        launch_pl_walk_tm(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->pl_run.as<int64_t>(), T, q->seq,
-                          ss, nF ? s->pl_toff.as<int64_t>() : nullptr, s->pl_tsend.as<int64_t>(), s->pl_tclk.as<int64_t>(),
-                          s->pl_tpos.as<int64_t>(), s->pl_fsend.as<int64_t>(), nF, state_of(s), s->rg.as<int64_t>(), q->ap,
-                          q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
-                          xt && b ? s->pl_x.as<int64_t>() : nullptr);
+        if (!grp)
+            launch_pl_walk_tm(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->pl_run.as<int64_t>(), T,
+                              q->seq, ss, nF ? s->pl_toff.as<int64_t>() : nullptr, s->pl_tsend.as<int64_t>(),
+                              s->pl_tclk.as<int64_t>(), s->pl_tpos.as<int64_t>(), s->pl_fsend.as<int64_t>(), nF, state_of(s),
+                              s->rg.as<int64_t>(), q->ap, q->d.current_on, q->d.expired_on, rows,
+                              s->flags.as<unsigned char>(), xt && b ? s->pl_x.as<int64_t>() : nullptr);
+    }
+    int64_t n_rows = 0;
+    if (grp) {
+        RCHK(group_time_rows(q, b ? &cs : nullptr, rec, M, nF, T, ss, xt && b, &n_rows));
+        HIPCHK(hipEventRecord(q->ev_agg1, st));
+        int64_t n_flushes = 0;
+        RCHK(sliding_flushes(q, n_rows, &n_flushes));
+        if (b) {
+            q->seq += N;
+            q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+            q->clock_valid = true;
+            q->stats.events = N;
+        }
+        HIPCHK(hipEventRecord(q->ev_push1, st));
+        HIPCHK(hipStreamSynchronize(st));
+        float ms = 0, kms = 0;
+        (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+        (void)hipEventElapsedTime(&kms, q->ev_agg0, q->ev_agg1);
+        q->stats.push_ms = ms;
+        q->stats.main_kernel_ms = kms;
+        q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
+        return sliding_output(q, n_rows, n_flushes, false, host_out, out);
     }
     HIPCHK(hipEventRecord(q->ev_agg1, st));
     HIPCHK(hipGetLastError());
     // ---- rows in position order, one flush each
-    int64_t n_rows = 0;
     const int fblk = (int)((n_pos + kTile - 1) / kTile);
     if (n_pos > 0) {
         RCHK(s->blk_cnt.reserve((size_t)(fblk + 16) * 8, false));
@@ -727,6 +883,50 @@ void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& b
         for (auto b : {std::make_pair(&s->pg_M, n * 8), std::make_pair(&s->pg_start, n * 8), std::make_pair(&s->pg_has, n),
                        std::make_pair(&s->pg_bopen, n * 8)})
             bufs.push_back(b);
+    if (q->group_other && s->lane == 2) {
+        bufs.push_back({&s->pg_st_cnt, (size_t)s->pg_st_n * 8});
+        bufs.push_back({&s->pg_st_f, (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n * 8});
+    }
+}
+
+// a key table's size, key count and keys (hashed tables; a dense table is its size alone)
+static int table_save(sh_query* q, KeyTableHost& kt, std::vector<uint8_t>& out) {
+    hipStream_t st = q->ctx->stream;
+    RCHK(kt.check(st));
+    const uint64_t size = kt.size_;
+    const int64_t nk = kt.n_keys;
+    const size_t kb = kt.dense ? 0 : size * 8;
+    const size_t o = out.size();
+    out.resize(o + 16 + kb);
+    std::memcpy(out.data() + o, &size, 8);
+    std::memcpy(out.data() + o + 8, &nk, 8);
+    if (kb) {
+        HIPCHK(hipMemcpyAsync(out.data() + o + 16, kt.keys.p, kb, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    return SH_OK;
+}
+
+static int table_load(sh_query* q, KeyTableHost& kt, const uint8_t* p, size_t len, size_t* used) {
+    hipStream_t st = q->ctx->stream;
+    uint64_t size = 0;
+    int64_t nk = 0;
+    if (len < 16) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    std::memcpy(&size, p, 8);
+    std::memcpy(&nk, p + 8, 8);
+    const size_t kb = kt.dense ? 0 : size * 8;
+    if (size != kt.size_ || nk < 0 || nk > (int64_t)size + 1) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+    if (16 + kb > len) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    if (kb) HIPCHK(hipMemcpyAsync(kt.keys.p, p + 16, kb, hipMemcpyHostToDevice, st));
+    PinnedBuf h;
+    RCHK(h.reserve(16));
+    uint32_t* c = h.as<uint32_t>();
+    c[0] = (uint32_t)nk; c[1] = c[2] = c[3] = 0;
+    HIPCHK(hipMemcpyAsync(kt.ctrl.p, c, 16, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    kt.n_keys = nk;
+    *used = 16 + kb;
+    return SH_OK;
 }
 
 // lane 3: the group key table and the carried records (in stream order)
@@ -838,6 +1038,10 @@ int plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
     const uint64_t ml = m.size();
     put(&ml, 8);
     put(m.data(), m.size());
+    if (s->lane == 2 && q->group_other) {
+        RCHK(table_save(q, q->gkt, out));
+        RCHK(table_save(q, q->pgkt, out));
+    }
     return s->lane == 3 ? pg_save(q, out) : SH_OK;
 }
 
@@ -872,6 +1076,13 @@ int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
     shj::JavaStringMap m;
     if (!m.load(p + o, (size_t)ml)) return sh_fail(SH_ERR_INVALID, "snapshot: scheduler state unreadable");
     o += ml;
+    if (s->lane == 2 && q->group_other) {
+        size_t u = 0;
+        RCHK(table_load(q, q->gkt, p + o, n - o, &u));
+        o += u;
+        RCHK(table_load(q, q->pgkt, p + o, n - o, &u));
+        o += u;
+    }
     size_t pg_used = 0;
     if (s->lane == 3) {
         // (the lanes of lane 3 carry no Scheduler: its part above is empty)

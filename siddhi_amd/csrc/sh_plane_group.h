@@ -60,6 +60,28 @@ void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char*
 // stable sort of (u64 key, u32 value) pairs over key bits [0, end_bit)
 int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
                         i64 n, unsigned end_bit, hipStream_t s);
+// time / externalTime windows grouped by other columns: the partitions' operations in order
+struct PgOps {
+    i64* pos;            // chunk position (the lanes' output position of the point)
+    u32* pg;             // (partition, group) state slot; 0xFFFFFFFF = no operation
+    unsigned char* kind; // 1 add (CURRENT), 2 remove (EXPIRED)
+    i64* seq;
+    i64* ts;             // the row timestamp: the event's (add) or the point's clock / attribute (remove)
+    i64* clk;
+    u64* vals;           // [n_vcols][cap]
+    i64 cap;
+};
+void launch_pg_ops_room(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* room);
+void launch_pg_rec_group(hipStream_t s, SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt, int nv);
+void launch_pg_walk_ops(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                        const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
+                        const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, int nv,
+                        const i64* xattr, KeyTable pgkt, const i64* obase, PgOps O, u32* o_cnt);
+void launch_pg_replay(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
+                      PgOps O, KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on, int exp_on,
+                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows);
+void launch_pg_heads32(hipStream_t s, const u32* key, i64 n, unsigned char* head);
+void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* out);
 int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,
                        unsigned end_bit, hipStream_t s);
 

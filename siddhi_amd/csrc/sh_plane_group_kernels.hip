@@ -458,4 +458,273 @@ void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char*
                            D, nv);
 }
 
+// ==== time / externalTime windows under `partition with`, grouped by other columns ==========================
+// TimeWindowProcessor (:132-169) per partition: at every point of the partition (a run of its events in a
+// send, or a TIMER call the Scheduler fires for it) the queue head expires while ts + T <= now, then the
+// event joins. Each EXPIRED / CURRENT event updates its group's aggregator state (partition, group) in
+// chunk order and the selector keeps one row per group per chunk (QuerySelector :315-374). Stage 1: one
+// lane per partition walks its points exactly like the time lanes but, instead of folding, writes the
+// partition's operations (add / remove, group, event) in order into its own region of an operation list.
+// Stage 2: the operations sorted stably by (partition, group) state slot; one thread per state replays
+// its operations in order (the double sums in Java's add / remove order) and emits a row per chunk:
+// placed at the chunk's first qualifying operation, valued after its last one.
+template <int NV>
+__global__ __launch_bounds__(64) void k_pg_walk_ops(const u32* __restrict__ key_off, const u32* __restrict__ sorted_rank,
+                                                   u32 nslots, SlRecords rec, const i64* __restrict__ run, i64 T,
+                                                   i64 seq_base, i64 send_size, const i64* __restrict__ t_off,
+                                                   const i64* __restrict__ t_send, const i64* __restrict__ t_clk,
+                                                   const i64* __restrict__ t_pos, const i64* __restrict__ f_send, i64 nF,
+                                                   SlState S, i64* rseq, int nv, const i64* __restrict__ xattr,
+                                                   KeyTable pgkt, const i64* __restrict__ obase, PgOps O, u32* o_cnt) {
+    const u32 k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= nslots) return;
+    const u32 lo = key_off[k], hi = key_off[k + 1];
+    const i64 tlo = t_off ? t_off[k] : 0, thi = t_off ? t_off[k + 1] : 0;
+    if (lo == hi && tlo == thi) return;
+    const i64 rc = S.rc, rm = rc - 1;
+    i64 rh = S.rhead[k], rlen = S.rlen[k];
+    i64 o = obase[k];
+    const i64 o0 = o;
+    u32 i = lo;
+    i64 t = tlo;
+    i64 cur_run = -1, run_pos = 0;
+    const int gcol = nv;  // the group slot travels as the last value column
+    while (i < hi || t < thi) {
+        const i64 rsend = i < hi ? (send_size > 0 ? (i64)rec.raw[sorted_rank[i]] / send_size : 0) : INT64_MAX;
+        const bool timer = t < thi && t_send[t] <= rsend;
+        i64 now, pos, clk;
+        u32 r = 0;
+        if (timer) {
+            now = t_clk[t];
+            pos = t_pos[t];
+            clk = now;
+        } else {
+            r = sorted_rank[i];
+            clk = rec.clock[r];
+            now = xattr ? xattr[r] : clk;
+            const i64 rn_ = run[rec.raw[r]];
+            if (rn_ != cur_run) {
+                cur_run = rn_;
+                i64 lo2 = 0, hi2 = nF;
+                while (lo2 < hi2) {
+                    const i64 m = (lo2 + hi2) >> 1;
+                    if (f_send[m] <= rsend) lo2 = m + 1;
+                    else hi2 = m;
+                }
+                run_pos = (i64)r + lo2;
+            }
+            pos = run_pos;
+        }
+        while (rlen > 0) {
+            const i64 sl = rh & rm;
+            if (S.rpm[(size_t)k * rc + sl] - now + T > 0) break;
+            const u32 g = (u32)S.rval[((size_t)gcol * S.nslots + k) * rc + sl];
+            O.pos[o] = pos;
+            O.pg[o] = key_slot(pgkt, ((u64)k << 32) | g);
+            O.kind[o] = 2;
+            O.seq[o] = rseq[(size_t)k * rc + sl];
+            O.ts[o] = now;
+            O.clk[o] = clk;
+#pragma unroll
+            for (int q = 0; q < NV; q++)
+                if (q < nv) O.vals[(size_t)q * O.cap + o] = S.rval[((size_t)q * S.nslots + k) * rc + sl];
+            o++;
+            rh++;
+            rlen--;
+        }
+        if (timer) {
+            t++;
+            continue;
+        }
+        {
+            const i64 sl = (rh + rlen) & rm;
+            const u32 g = (u32)rec.vals[(size_t)gcol * rec.cap + r];
+            S.rpm[(size_t)k * rc + sl] = xattr ? xattr[r] : rec.ts[r];
+            rseq[(size_t)k * rc + sl] = seq_base + (i64)rec.raw[r];
+            for (int q = 0; q <= nv; q++) S.rval[((size_t)q * S.nslots + k) * rc + sl] = rec.vals[(size_t)q * rec.cap + r];
+            rlen++;
+            O.pos[o] = pos;
+            O.pg[o] = key_slot(pgkt, ((u64)k << 32) | g);
+            O.kind[o] = 1;
+            O.seq[o] = seq_base + (i64)rec.raw[r];
+            O.ts[o] = rec.ts[r];
+            O.clk[o] = clk;
+#pragma unroll
+            for (int q = 0; q < NV; q++)
+                if (q < nv) O.vals[(size_t)q * O.cap + o] = rec.vals[(size_t)q * rec.cap + r];
+            o++;
+            i++;
+        }
+    }
+    S.rhead[k] = rh;
+    S.rlen[k] = rlen;
+    o_cnt[k] = (u32)(o - o0);
+}
+
+void launch_pg_walk_ops(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                        const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
+                        const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, int nv,
+                        const i64* xattr, KeyTable pgkt, const i64* obase, PgOps O, u32* o_cnt) {
+    const unsigned grid = (unsigned)((nslots + 63) / 64);
+    if (!grid) return;
+    if (nv <= 1)
+        hipLaunchKernelGGL(k_pg_walk_ops<1>, dim3(grid), dim3(64), 0, s, key_off, sorted_rank, (u32)nslots, rec, run, T,
+                           seq_base, send_size, t_off, t_send, t_clk, t_pos, f_send, nF, S, rseq, nv, xattr, pgkt, obase, O,
+                           o_cnt);
+    else
+        hipLaunchKernelGGL(k_pg_walk_ops<8>, dim3(grid), dim3(64), 0, s, key_off, sorted_rank, (u32)nslots, rec, run, T,
+                           seq_base, send_size, t_off, t_send, t_clk, t_pos, f_send, nF, S, rseq, nv, xattr, pgkt, obase, O,
+                           o_cnt);
+}
+
+// each partition's operation region: room for its queued events' removes and its new events' adds and
+// removes
+__global__ __launch_bounds__(kBlock) void k_pg_ops_room(const u32* __restrict__ slot_cnt, const i64* __restrict__ rlen,
+                                                       i64 n, i64* room) {
+    const i64 k = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (k < n) room[k] = rlen[k] + 2 * (i64)slot_cnt[k];
+}
+
+void launch_pg_ops_room(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* room) {
+    if (n > 0) hipLaunchKernelGGL(k_pg_ops_room, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, slot_cnt, rlen, n, room);
+}
+
+// the group slot of every record, as its extra value column
+__global__ __launch_bounds__(kBlock) void k_pg_rec_group(SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt,
+                                                        int nv) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r < M) rec.vals[(size_t)nv * rec.cap + r] = key_slot(gkt, make_key(gkp, cols, rec.raw[r]));
+}
+
+void launch_pg_rec_group(hipStream_t s, SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt, int nv) {
+    if (M > 0) hipLaunchKernelGGL(k_pg_rec_group, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, cols, gkp, gkt, nv);
+}
+
+// stage 2: one thread per (partition, group) state replays its operations (sorted stably by state slot)
+template <int NA>
+__global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_start, i64 n_seg, i64 n_ops,
+                                                 const u32* __restrict__ skey, const u32* __restrict__ sidx, PgOps O,
+                                                 KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on,
+                                                 int exp_on, SlxRows rows, u64* row_key, u32* row_part,
+                                                 unsigned int* n_rows) {
+    const i64 sg = (i64)blockIdx.x * 64 + threadIdx.x;
+    if (sg >= n_seg) return;
+    const i64 lo = seg_start[sg], hi = sg + 1 < n_seg ? seg_start[sg + 1] : n_ops;
+    const u32 pg = skey[lo];
+    const u64 pk = slot_key(pgkt, pg);
+    i64 cnt = st_cnt[pg];
+    u64 f[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        f[a] = 0;
+        if (a < ap.n && ap.kind[a] != AK_COUNT) f[a] = st_f[(size_t)ap.field[a] * st_n + pg];
+    }
+    i64 chunk = -1, first = -1, q_ts = 0, q_seq = 0, q_clk = 0;
+    unsigned char q_exp = 0;
+    u64 rv[NA];
+    unsigned char rn[NA];
+    auto flush_row = [&]() {
+        if (first < 0) return;
+        const u32 slot = atomicAdd(n_rows, 1u);
+        rows.ts[slot] = q_ts;
+        rows.rep[slot] = q_seq;
+        rows.slot[slot] = (u32)pk;
+        rows.ch[slot] = chunk;
+        rows.clk[slot] = q_clk;
+        rows.exp[slot] = q_exp;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            rows.vals[(size_t)a * rows.cap + slot] = rv[a];
+            rows.nulls[(size_t)a * rows.cap + slot] = rn[a];
+        }
+        row_key[slot] = ((u64)chunk << 32) | (u64)(u32)first;
+        row_part[slot] = (u32)(pk >> 32);
+    };
+    for (i64 j = lo; j < hi; j++) {
+        const u32 oi = sidx[j];
+        const i64 pos = O.pos[oi];
+        if (pos != chunk) {
+            flush_row();
+            chunk = pos;
+            first = -1;
+        }
+        const bool add = O.kind[oi] == 1;
+        add ? cnt++ : cnt--;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            if (kind == AK_COUNT) continue;
+            const u64 x = O.vals[(size_t)ap.vcol[a] * O.cap + oi];
+            if (kind == AK_SUM_L) {
+                f[a] = add ? (u64)((i64)f[a] + (i64)x) : (u64)java_d2l((double)(i64)f[a] - (double)(i64)x);
+            } else {
+                const double v = g_num(ap, a, x);
+                double rr = __longlong_as_double((i64)f[a]) + (add ? v : -v);
+                if (!add && cnt == 0 && rr == 0.0) rr = 0.0;
+                f[a] = (u64)__double_as_longlong(rr);
+            }
+        }
+        if ((add && cur_on) || (!add && exp_on)) {
+            if (first < 0) first = oi;
+            q_ts = O.ts[oi];
+            q_seq = O.seq[oi];
+            q_clk = O.clk[oi];
+            q_exp = add ? 0 : 1;
+#pragma unroll
+            for (int a = 0; a < NA; a++) {
+                rv[a] = 0;
+                rn[a] = 0;
+                if (a >= ap.n) continue;
+                const int kind = ap.kind[a];
+                if (kind == AK_COUNT) rv[a] = (u64)cnt;
+                else if (kind == AK_SUM_L || kind == AK_SUM_D) { rn[a] = cnt == 0; rv[a] = cnt == 0 ? 0 : f[a]; }
+                else {
+                    rn[a] = cnt == 0;
+                    if (cnt) rv[a] = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) / (double)cnt);
+                }
+            }
+        }
+    }
+    flush_row();
+    st_cnt[pg] = cnt;
+#pragma unroll
+    for (int a = 0; a < NA; a++)
+        if (a < ap.n && ap.kind[a] != AK_COUNT) st_f[(size_t)ap.field[a] * st_n + pg] = f[a];
+}
+
+void launch_pg_replay(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
+                      PgOps O, KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on, int exp_on,
+                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows) {
+    if (n_seg <= 0) return;
+    const unsigned grid = (unsigned)((n_seg + 63) / 64);
+    if (ap.n <= 4)
+        hipLaunchKernelGGL(k_pg_replay<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_ops, skey, sidx, O, pgkt, st_cnt,
+                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows);
+    else
+        hipLaunchKernelGGL(k_pg_replay<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_ops, skey, sidx, O, pgkt, st_cnt,
+                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows);
+}
+
+// sorted operation keys: heads of the (partition, group) runs among the first n valid ones
+__global__ __launch_bounds__(kBlock) void k_pg_heads32(const u32* __restrict__ key, i64 n, unsigned char* head) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) head[j] = j == 0 || key[j] != key[j - 1];
+}
+
+void launch_pg_heads32(hipStream_t s, const u32* key, i64 n, unsigned char* head) {
+    if (n > 0) hipLaunchKernelGGL(k_pg_heads32, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key, n, head);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_sum_u32(const u32* __restrict__ a, i64 n, unsigned long long* out) {
+    const i64 k = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 t = block_reduce(k < n ? (i64)a[k] : 0, SumOp(), 0);
+    if (threadIdx.x == 0 && t) atomicAdd(out, (unsigned long long)t);
+}
+
+void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* out) {
+    if (n > 0) hipLaunchKernelGGL(k_pg_sum_u32, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a, n, out);
+}
+
 }  // namespace shd

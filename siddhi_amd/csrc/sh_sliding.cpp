@@ -59,9 +59,16 @@ static int alloc_zero(DevBuf& b, size_t bytes, int fill = 0) {
 // (re)size the per-key rings and deques to capacity rc (power of two), keeping their contents
 // (keep = false: fresh buffers, e.g. before a restore overwrites them — the live rings may hold more
 // entries than the new capacity, so they must not be copied over)
+// value columns of a ring entry: the aggregated ones, plus the group slot on time lanes grouped by
+// other columns (sh_plane.cpp)
+int ring_vcols(const sh_query* q) {
+    return std::max(1, q->ap.n_vcols) +
+           (q->group_other && (q->d.window == SH_WIN_TIME || q->d.window == SH_WIN_EXT_TIME) ? 1 : 0);
+}
+
 int size_rings(sh_query* q, int64_t new_rc, bool keep) {
     SlidingImpl* s = q->sl;
-    int F = std::max(1, q->ap.n_fields), V = std::max(1, q->ap.n_vcols);
+    int F = std::max(1, q->ap.n_fields), V = ring_vcols(q);
     int64_t n = s->nslots;
     DevBuf rpm2, rval2, dq2;
     RCHK(rpm2.reserve((size_t)n * new_rc * 8, false));
@@ -880,7 +887,7 @@ int sliding_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& 
         sc[0] = s->nslots; sc[1] = s->rc; sc[2] = s->pm; sc[3] = s->send_base;
     }
     const size_t n = (size_t)s->nslots, rc = (size_t)s->rc;
-    const size_t F = (size_t)std::max(1, q->ap.n_fields), V = (size_t)std::max(1, q->ap.n_vcols);
+    const size_t F = (size_t)std::max(1, q->ap.n_fields), V = (size_t)ring_vcols(q);
     bufs = {{&s->cnt, n * 8},          {&s->f, F * n * 8},         {&s->mm, F * n * 8},      {&s->mm_has, F * n},
             {&s->dq_head, F * n * 8},  {&s->dq_len, F * n * 8},    {&s->dq, F * n * rc * 8}, {&s->rhead, n * 8},
             {&s->rlen, n * 8},         {&s->rpm, n * rc * 8},      {&s->rval, V * n * rc * 8},

@@ -76,6 +76,9 @@ struct SlidingImpl {
     DevBuf out_part;  // the lanes' output rows: partition slot of each (per-partition rate limiters)
     // externalTimeBatch lanes: per partition slot the running max, start, started flag, open bucket
     DevBuf pg_M, pg_start, pg_has, pg_bopen, pg_pendcnt, pg_xs, pg_xv, pg_ms, pg_cts, pg_err;
+    // time lanes grouped by other columns: operation lists, their sort, the (partition, group) states
+    DevBuf pg_room, op_pos, op_pg, op_kind, op_seq, op_ts, op_clk, op_vals, pg_ocnt, pg_skey, pg_sidx, pg_st_cnt, pg_st_f;
+    int64_t pg_st_n = 0;
     DevBuf pg_rpart, pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
         pg_cnt;
 };

@@ -232,9 +232,13 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     const bool plane_ext = d->partition_col >= 0 && d->window == SH_WIN_EXT_TIME_BATCH && d->n_aggs >= 1;
     const bool plane_group = (d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
                               !d->stream_current && d->n_aggs >= 1) || plane_ext;
+    // ... and time / externalTime grouped by other columns: the time lanes' operations, replayed per
+    // (partition, group) state (count / sum / avg)
+    const bool plane_time_group = d->partition_col >= 0 && (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
+                                  !by_partition && d->n_aggs >= 1;
     const bool plane = (d->partition_col >= 0 &&
                         (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
-                        by_partition) || plane_group;
+                        by_partition) || plane_group || plane_time_group;
     if ((!d->current_on || d->expired_on) &&
         !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
@@ -270,7 +274,20 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (kp_override) { q->kp = *kp_override; q->internal_keys = true; }
     // lane 3: grouped by other columns, or (opt-in, SH_PL_SORT=1) lengthBatch keyed by the partition —
     // the sorted chunks have no per-partition sequential walk, so a hot partition does not serialise
-    q->group_other = plane_group && !by_partition;
+    q->group_other = (plane_group && !by_partition) || plane_time_group;
+    if (plane_time_group) {
+        for (int a = 0; a < q->ap.n; a++)
+            if (q->ap.kind[a] >= AK_MIN_L) {
+                delete q;
+                return sh_fail(SH_ERR_UNSUPPORTED,
+                               "partitioned time / externalTime windows grouped by other columns: count / sum / avg "
+                               "(min / max keep a deque per (partition, group) state)");
+            }
+        if ((rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
+            delete q;
+            return rc;
+        }
+    }
     q->plane_sorted = plane_group || (plane && !kp_override && d->window == SH_WIN_LENGTH_BATCH && !d->stream_current &&
                                       q->tune.pl_sort);
     if (q->plane_sorted && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
@@ -285,10 +302,12 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->n_group_by == 1 && d->group_by[0] == d->partition_col) cap = 1;
     }
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
-    if (q->plane_sorted && (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(q->gkp.n ? cap : 1))) {
+    if ((q->plane_sorted || plane_time_group) &&
+        (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(q->gkp.n ? cap : 1))) {
         delete q;
         return rc;
     }
+    if (plane_time_group && (rc = q->pgkt.init(4 * cap))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0 && !plane;
@@ -1617,6 +1636,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     // device buffers are released by their destructors (stream-ordered on this context)
     q->kt.release();
     q->gkt.release();
+    q->pgkt.release();
     if (q->h_info) (void)hipHostFree(q->h_info);
     if (q->small_res) (void)hipHostFree(q->small_res);
     if (q->zc_ring) (void)hipHostFree(q->zc_ring);

@@ -172,3 +172,11 @@ def test_partitioned_external_time_checkpoint():
                        output="all", aggs=[("count", None), ("sum", "v"), ("max", "v")])
     got, ref, _ = checkpointed(sp, split_batches(PSCH, ts, cols, [10_000, 20_000], 1), 1)
     assert_same(got, ref, label="pxt ckpt")
+
+
+@pytest.mark.parametrize("output", ["current", "all"])
+def test_partitioned_external_time_group_by_other(output):
+    ts, cols = pstream(40_000, 29, 0xEA, late_ms=500)
+    sp = abi.QuerySpec(PSCH, "externalTime", 400, group_by=["k"], ts_attr="et", partition="p", key_capacity=128,
+                       output=output, aggs=[("count", None), ("sum", "v"), ("avg", "et")])
+    both(sp, split_batches(PSCH, ts, cols, [1, 12_000, 30_000], 3), f"pxt group {output}")

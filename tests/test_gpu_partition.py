@@ -208,3 +208,37 @@ def test_partitioned_lengthbatch_walk_lanes_zipf(rt, monkeypatch):
                          partition="p", output="all", key_capacity=1_000_000)
     ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000], 1), "plb walk zipf")
     assert ref["ts"].size > 10_000
+
+
+# ---- time / externalTime lanes grouped by other columns (operations per partition, replayed per
+# (partition, group) state) -----------------------------------------------------------------------------
+GAGGS = [("count", None), ("sum", "v"), ("avg", "x"), ("sum", "x")]
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("send_size,group_by", [(1, ["g"]), (6, ["g", "h"]), (1, ["h", "p"])])
+def test_partitioned_time_group_by_other(rt, output, send_size, group_by):
+    ts, cols = gstream(30_000, 40, 6, 79, runs=send_size > 1)
+    spec = abi.QuerySpec(GSCHEMA, "time", 150, group_by=group_by, aggs=GAGGS, partition="p", filter=(">", "v", -40.0),
+                         output=output, key_capacity=512)
+    pushes = split_batches(GSCHEMA, ts, cols, [1, 5_000, 18_000], send_size)
+    pushes.insert(3, ("advance", int(ts[17_999]) + 100))
+    pushes.append(("advance", int(ts[-1]) + 120))
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    ref = both(rt, spec, pushes, f"ptime group {group_by} {output} {send_size}")
+    assert ref["ts"].size > 0
+
+
+def test_partitioned_time_group_by_other_zipf(rt):
+    ts, cols = gstream(300_000, 100_000, 4, 83, zipf=True)
+    spec = abi.QuerySpec(GSCHEMA, "time", 400, group_by=["g"], aggs=[("sum", "v"), ("count", None)], partition="p",
+                         output="all", key_capacity=100_000)
+    pushes = split_batches(GSCHEMA, ts, cols, [100_000, 200_000], 1) + [("advance", int(ts[-1]) + 1_000)]
+    ref = both(rt, spec, pushes, "ptime group zipf")
+    assert ref["expired"].sum() > 0
+
+
+def test_partitioned_time_group_by_other_min_max_refused(rt):
+    spec = abi.QuerySpec(GSCHEMA, "time", 150, group_by=["g"], aggs=[("min", "v")], partition="p", key_capacity=64)
+    with pytest.raises(rt.SiddhiError, match="count / sum / avg"):
+        rt.GpuQuery(spec)

@@ -221,3 +221,16 @@ def test_partition_lanes_rate_checkpoint(rate):
     pushes = split_batches(PSCHEMA, ts, cols, [10_000, 20_001], 1)
     got, ref, _ = checkpointed(spec, pushes, 1)
     assert_same(got, ref, label=f"lanes rate ckpt {rate}")
+
+
+@pytest.mark.parametrize("cut", [1, 2])
+def test_partition_time_group_lanes_checkpoint(cut):
+    """time lanes grouped by other columns: the rings (with each entry's group), the (partition, group)
+    states and both key tables, and the Scheduler, restored into a fresh query"""
+    from tests.test_gpu_partition import GSCHEMA, gstream
+    ts, cols = gstream(50_000, 30, 5, 29 + cut)
+    spec = abi.QuerySpec(GSCHEMA, "time", 200, group_by=["g"], aggs=[("count", None), ("sum", "v")], partition="p",
+                         output="all", key_capacity=128)
+    pushes = split_batches(GSCHEMA, ts, cols, [15_000, 33_000], 1) + [("advance", int(ts[-1]) + 1_000)]
+    got, ref, _ = checkpointed(spec, pushes, cut)
+    assert_same(got, ref, label=f"time group lanes ckpt {cut}")
