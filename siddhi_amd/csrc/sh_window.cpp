@@ -307,7 +307,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         delete q;
         return rc;
     }
-    if (plane_time_group && (rc = q->pgkt.init(4 * cap))) { delete q; return rc; }
+    // (partition, group) pairs: room for four per group key, at least 64k
+    if (plane_time_group && (rc = q->pgkt.init(std::max<int64_t>(4 * cap, 1 << 16)))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     q->partitioned = d->partition_col >= 0 && !plane;
