@@ -68,10 +68,11 @@ bool sliding_keyed_ok(AggPlan ap);
 int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u32* rank_out, i64 M, i64 nslots,
                     hipStream_t s);
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
-                          SlRecords rec, i64* g_pm, u64* g_v, u32* inv, SlState S, AggPlan ap, i64 T,
+                          SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
                           i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags);
 int sliding_keyed_row_words(int n_aggs);
-void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, const u32* inv,
+// rowsK: the keyed replay's rows at the stream rank of their first record
+void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
                      const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep);

@@ -1595,7 +1595,7 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                                                u64* __restrict__ g_v, SlState S, DFields fd, KOut ko, i64 T,
                                                u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
-                                               unsigned char* __restrict__ flags, u32* __restrict__ inv) {
+                                               unsigned char* __restrict__ flags) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ int di_min[HMIN ? kDqK : 1];
@@ -1660,7 +1660,6 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                 g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
                 g_v[i] = x;
                 flags[r] = fst ? 1 : 0;
-                if (fst) inv[r] = i;
             }
             s_x[lane] = x;
             prev_raw = __shfl(raw, m - 1, 64);
@@ -1817,7 +1816,10 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                 w[4 + o] = v;
             }
             w[3] = (u64)send | ((u64)nulls << 56);
-            ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)(a + (u32)grp) * RW);
+            // the row lands at the stream rank of its first record, so the emission reads the rows in
+            // stream order (whole lines) instead of gathering them from key order
+            const u32 row_rank = grp == o0 + lane ? (rk & ~kFirstBit) : sorted_rank[a + (u32)grp];
+            ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row_rank * RW);
 #pragma unroll
             for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
                 if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
@@ -1853,9 +1855,9 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     }
 }
 
-// emit of the keyed replay: flagged ranks in stream order, each row read from its key-order record
+// emit of the keyed replay: flagged ranks in stream order, each row read from its record at that rank
 __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __restrict__ flags, i64 n,
-                                                    const i64* __restrict__ blk_pre, const u32* __restrict__ inv,
+                                                    const i64* __restrict__ blk_pre,
                                                     const u64* __restrict__ rowsK, int RW, int n_aggs, KeyTable kt,
                                                     KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                                                     unsigned char* out_nulls, i64* out_send, i64* out_clock,
@@ -1870,7 +1872,7 @@ __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __rest
         const i64 r = run + block_excl_scan(fl, SumOp(), 0, &tot);
         run += tot;
         if (!fl) continue;
-        const u64* src = rowsK + (size_t)inv[j] * RW;
+        const u64* src = rowsK + (size_t)j * RW;
         u64 w[4 + SH_MAX_AGGS];
 #pragma unroll
         for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++) {
@@ -1886,18 +1888,18 @@ __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __rest
             out_vals[(size_t)a * out_cap + r] = w[4 + a];
             out_nulls[(size_t)a * out_cap + r] = (nulls >> a) & 1u;
         }
-        out_send[r] = (i64)(w[3] & ((1ull << 56) - 1));
+        if (out_send) out_send[r] = (i64)(w[3] & ((1ull << 56) - 1));  // (per-event sends: the flushes are the rows)
         out_clock[r] = (i64)w[2];
         if (out_order) out_order[r] = raw_base + (i64)rank_raw[j];
         out_rep[r] = raw_base + (i64)(u32)w[1];
     }
 }
 
-void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, const u32* inv,
+void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
                      const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep) {
-    hipLaunchKernelGGL(k_slk_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, inv, rowsK, RW, n_aggs, kt, kp,
+    hipLaunchKernelGGL(k_slk_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rowsK, RW, n_aggs, kt, kp,
                        out_cap, out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base,
                        out_order, out_rep);
 }
@@ -1913,7 +1915,7 @@ bool sliding_keyed_ok(AggPlan ap) {
 int sliding_keyed_row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
 
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
-                          SlRecords rec, i64* g_pm, u64* g_v, u32* inv, SlState S, AggPlan ap, i64 T,
+                          SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
                           i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags) {
     DFields fd;
     own_d_fields(ap, fd);
@@ -1931,7 +1933,7 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     const int RW = sliding_keyed_row_words(ap.n);
 #define SH_SL_W(A, B, C)                                                                                            \
     hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_pm, g_v, S, fd, ko, \
-                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags, inv)
+                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags)
     if (hs && hn && hx) SH_SL_W(true, true, true);
     else if (hs && !hn && !hx) SH_SL_W(true, false, false);
     else if (!hs && hn && hx) SH_SL_W(false, true, true);
