@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 P=/tmp/r4c3 && rm -rf $P && mkdir -p $P
 timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread -m gpu tests/test_gpu_sliding_minmax.py \
-  tests/test_gpu_sliding.py "tests/test_gpu_parity.py::test_c3_sliding_dictionary_keys" \
+  tests/test_gpu_parity.py -k "sliding or c3 or minmax or ext" tests/test_gpu_ext.py \
   tests/test_gpu_scale.py::test_c3_time_10s_10k_keys_1k_resident_per_key > gpurun_out/r4c3_t.log 2>&1 || { tail -30 gpurun_out/r4c3_t.log; exit 1; }
 tail -2 gpurun_out/r4c3_t.log
 timeout -k 10 300 python -u bench.py --workload c3 --steps 5 --warmup 2 > gpurun_out/r4c3_bench.json 2>$P/b.err || { tail $P/b.err; exit 1; }
