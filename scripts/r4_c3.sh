@@ -22,5 +22,7 @@ head -8 gpurun_out/r4c3_kernel_stats.txt
 for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $ctr -d $P/$ctr -o run --output-format csv -- python3 bench.py --workload c3 --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2>$P/$ctr.err || { echo "$ctr failed"; exit 1; }
 done
-python3 scripts/pmc_summary.py "$(ls $P/FETCH_SIZE/*/run_counter_collection.csv | head -1)" "$(ls $P/WRITE_SIZE/*/run_counter_collection.csv | head -1)" > gpurun_out/r4c3_pmc.json
+F=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" $P/FETCH_SIZE)
+W=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" $P/WRITE_SIZE)
+python3 scripts/pmc_summary.py "$F" "$W" > gpurun_out/r4c3_pmc.json
 echo done
