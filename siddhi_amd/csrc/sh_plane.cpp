@@ -56,8 +56,13 @@ int plane_create(sh_query* q) {
     if (q->group_other && s->lane == 2) {
         // (partition, group) states of the time lanes grouped by other columns: count and sums
         s->pg_st_n = (int64_t)q->pgkt.size_ + 1;
+        const size_t F = (size_t)std::max(1, q->ap.n_fields);
         RCHK(fill(s->pg_st_cnt, (size_t)s->pg_st_n * 8, 0));
-        RCHK(fill(s->pg_st_f, (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n * 8, 0));
+        RCHK(fill(s->pg_st_f, F * s->pg_st_n * 8, 0));
+        RCHK(fill(s->pg_dq_off, F * s->pg_st_n * 8, 0));
+        RCHK(fill(s->pg_dq_len, F * s->pg_st_n * 8, 0));
+        RCHK(fill(s->pg_dq_pool, 64, 0));
+        s->pg_dq_words = 0;
     }
     if (q->d.window == SH_WIN_EXT_TIME_BATCH) {
         RCHK(fill(s->pg_M, n * 8, 0));
@@ -443,6 +448,27 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
 // Time / externalTime lanes grouped by other columns (sh_plane_group_kernels.hip, k_pg_walk_ops /
 // k_pg_replay): the partitions' walks write their add / remove operations, the operations sorted stably
 // by (partition, group) state are replayed one thread per state, rows sorted by (chunk, first operation).
+// the min / max fields of the grouped time lanes' states and their deque pool
+static PgDeques pg_deques(sh_query* q) {
+    SlidingImpl* s = q->sl;
+    PgDeques D{};
+    for (int a = 0; a < q->ap.n; a++) {
+        if (q->ap.kind[a] < AK_MIN_L) continue;
+        bool seen = false;
+        for (int f = 0; f < D.nf; f++) seen |= D.field[f] == q->ap.field[a];
+        if (!seen) D.field[D.nf++] = q->ap.field[a];
+    }
+    D.n = s->pg_st_n;
+    D.pool = s->pg_dq_pool.as<u64>();
+    D.off = s->pg_dq_off.as<int64_t>();
+    D.len = s->pg_dq_len.as<int64_t>();
+    D.scratch = s->pg_dq_scr.as<u64>();
+    D.new_at = s->pg_dq_at.as<int64_t>();
+    D.new_len = s->pg_dq_nlen.as<int64_t>();
+    D.active = s->pg_dq_act.as<unsigned char>();
+    return D;
+}
+
 static int group_time_rows(sh_query* q, const ColSet* cs, SlRecords rec, int64_t M, int64_t nF, int64_t T, int64_t ss,
                            bool xt, int64_t* n_rows_out) {
     SlidingImpl* s = q->sl;
@@ -528,11 +554,47 @@ static int group_time_rows(sh_query* q, const ColSet* cs, SlRecords rec, int64_t
                      s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
                      s->xr_nulls.as<unsigned char>(), rc};
         HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 16, st));
+        PgDeques D = pg_deques(q);
+        if (D.nf > 0) {
+            // every segment's scratch: its carried deques plus one entry per add of the push
+            const size_t FN = (size_t)std::max(1, q->ap.n_fields) * D.n;
+            RCHK(s->pg_dq_need.reserve((size_t)(n_seg + 1) * 8, false));
+            RCHK(s->tmp.reserve((size_t)((std::max<int64_t>(n_seg + 1, (int64_t)FN + 1) + kTile - 1) / kTile + 16) * 8, false));
+            launch_pg_dq_need(st, s->pg_seg.as<int64_t>(), n_seg, n_ops, s->pg_skey.as<u32>(), s->pg_sidx.as<u32>(), O, D,
+                              s->pg_dq_need.as<int64_t>());
+            launch_scan_sum_large(st, s->pg_dq_need.as<int64_t>(), n_seg + 1, s->tmp.as<int64_t>());
+            int64_t scr = 0;
+            RCHK(read_count(q, s->pg_dq_need.as<int64_t>() + n_seg, &scr));
+            RCHK(s->pg_dq_scr.reserve((size_t)std::max<int64_t>(scr, 1) * 8, false));
+            RCHK(s->pg_dq_at.reserve(FN * 8, false));
+            RCHK(s->pg_dq_nlen.reserve(FN * 8, false));
+            RCHK(s->pg_dq_act.reserve((size_t)D.n, false));
+            HIPCHK(hipMemsetAsync(s->pg_dq_act.p, 0, (size_t)D.n, st));
+            D = pg_deques(q);
+        }
         launch_pg_replay(st, s->pg_seg.as<int64_t>(), n_seg, n_ops, s->pg_skey.as<u32>(), s->pg_sidx.as<u32>(), O,
                          q->pgkt.dev(), s->pg_st_cnt.as<int64_t>(), s->pg_st_f.as<u64>(), s->pg_st_n, q->ap, q->d.current_on,
                          q->d.expired_on, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
-                         (unsigned int*)s->pg_cnt.p);
+                         (unsigned int*)s->pg_cnt.p, D, s->pg_dq_need.as<int64_t>());
         HIPCHK(hipGetLastError());
+        if (D.nf > 0) {
+            // the deques back into a fresh pool, (field, state)-major
+            const int64_t tot = (int64_t)D.nf * D.n;
+            RCHK(s->pg_dq_lens.reserve((size_t)(tot + 1) * 8, false));
+            RCHK(s->tmp.reserve((size_t)((tot + 1 + kTile - 1) / kTile + 16) * 8, false));
+            launch_pg_dq_len(st, D, s->pg_dq_lens.as<int64_t>());
+            launch_scan_sum_large(st, s->pg_dq_lens.as<int64_t>(), tot + 1, s->tmp.as<int64_t>());
+            int64_t words = 0;
+            RCHK(read_count(q, s->pg_dq_lens.as<int64_t>() + tot, &words));
+            RCHK(s->pg_dq_pool2.reserve((size_t)std::max<int64_t>(words, 8) * 8, false));
+            RCHK(s->pg_dq_off2.reserve((size_t)std::max(1, q->ap.n_fields) * D.n * 8, false));
+            launch_pg_dq_pool(st, D, s->pg_dq_lens.as<int64_t>(), s->pg_dq_pool2.as<u64>(), s->pg_dq_off2.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(st));  // the old pool is released below
+            std::swap(s->pg_dq_pool, s->pg_dq_pool2);
+            std::swap(s->pg_dq_off, s->pg_dq_off2);
+            s->pg_dq_words = words;
+        }
         RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_rows));
         n_rows &= 0xFFFFFFFFll;
         if (n_rows > 0) {
@@ -884,8 +946,11 @@ void plane_state_buffers(sh_query* q, std::vector<std::pair<DevBuf*, size_t>>& b
                        std::make_pair(&s->pg_bopen, n * 8)})
             bufs.push_back(b);
     if (q->group_other && s->lane == 2) {
+        const size_t FN = (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n;
         bufs.push_back({&s->pg_st_cnt, (size_t)s->pg_st_n * 8});
-        bufs.push_back({&s->pg_st_f, (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n * 8});
+        bufs.push_back({&s->pg_st_f, FN * 8});
+        bufs.push_back({&s->pg_dq_off, FN * 8});
+        bufs.push_back({&s->pg_dq_len, FN * 8});
     }
 }
 
@@ -1041,6 +1106,15 @@ int plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
     if (s->lane == 2 && q->group_other) {
         RCHK(table_save(q, q->gkt, out));
         RCHK(table_save(q, q->pgkt, out));
+        // the min / max deque pool
+        const uint64_t w = (uint64_t)s->pg_dq_words;
+        const size_t o = out.size();
+        out.resize(o + 8 + w * 8);
+        std::memcpy(out.data() + o, &w, 8);
+        if (w) {
+            HIPCHK(hipMemcpyAsync(out.data() + o + 8, s->pg_dq_pool.p, w * 8, hipMemcpyDeviceToHost, q->ctx->stream));
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        }
     }
     return s->lane == 3 ? pg_save(q, out) : SH_OK;
 }
@@ -1082,6 +1156,13 @@ int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
         o += u;
         RCHK(table_load(q, q->pgkt, p + o, n - o, &u));
         o += u;
+        uint64_t w = 0;
+        if (!get(&w, 8) || w > (n - o) / 8) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        RCHK(s->pg_dq_pool.reserve((size_t)std::max<uint64_t>(w, 8) * 8, false));
+        if (w) HIPCHK(hipMemcpyAsync(s->pg_dq_pool.p, p + o, w * 8, hipMemcpyHostToDevice, q->ctx->stream));
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        s->pg_dq_words = (int64_t)w;
+        o += w * 8;
     }
     size_t pg_used = 0;
     if (s->lane == 3) {

@@ -77,9 +77,27 @@ void launch_pg_walk_ops(hipStream_t s, const u32* key_off, const u32* sorted_ran
                         const i64* run, i64 T, i64 seq_base, i64 send_size, const i64* t_off, const i64* t_send,
                         const i64* t_clk, const i64* t_pos, const i64* f_send, i64 nF, SlState S, i64* rseq, int nv,
                         const i64* xattr, KeyTable pgkt, const i64* obase, PgOps O, u32* o_cnt);
+// min / max deques of the (partition, group) states: pool[off[f * n + s], + len[f * n + s]) for the
+// min / max fields field[0 .. nf)
+struct PgDeques {
+    int nf;
+    int field[SH_MAX_AGGS];
+    i64 n;               // states
+    u64* pool;
+    i64* off;
+    i64* len;
+    u64* scratch;        // the push's working areas
+    i64* new_at;         // after the replay: scratch index / length of an active state's deque
+    i64* new_len;
+    unsigned char* active;
+};
+void launch_pg_dq_need(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
+                       PgOps O, PgDeques D, i64* need);
 void launch_pg_replay(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
                       PgOps O, KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on, int exp_on,
-                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows);
+                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows, PgDeques D, const i64* scr_off);
+void launch_pg_dq_len(hipStream_t s, PgDeques D, i64* out_len);
+void launch_pg_dq_pool(hipStream_t s, PgDeques D, const i64* off_out, u64* pool_out, i64* new_off);
 void launch_pg_heads32(hipStream_t s, const u32* key, i64 n, unsigned char* head);
 void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* out);
 int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,

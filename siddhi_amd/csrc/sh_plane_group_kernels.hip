@@ -600,13 +600,51 @@ void launch_pg_rec_group(hipStream_t s, SlRecords rec, i64 M, ColSet cols, KeyPl
     if (M > 0) hipLaunchKernelGGL(k_pg_rec_group, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, cols, gkp, gkt, nv);
 }
 
-// stage 2: one thread per (partition, group) state replays its operations (sorted stably by state slot)
+// stage 2: one thread per (partition, group) state replays its operations (sorted stably by state slot).
+// Min / max keep MinAttributeAggregatorExecutor's deque (:86-236, removeFirstOccurrence on expiry) per
+// state: carried between pushes in a pool (PgDeques: per (field, state) offset and length), worked on in
+// the segment's own scratch area — room for its carried entries plus one per add of the push — and
+// gathered back into a fresh pool afterwards (k_pg_dq_pool).
+__device__ __forceinline__ bool g_eq(int kind, u64 a, u64 b) {
+    if (kind == AK_MIN_L || kind == AK_MAX_L) return a == b;
+    const double x = __longlong_as_double((i64)a), y = __longlong_as_double((i64)b);
+    if (kind == AK_MIN_F || kind == AK_MAX_F) {
+        const float fx = (float)x, fy = (float)y;
+        if (fx != fx && fy != fy) return true;
+        return __float_as_uint(fx) == __float_as_uint(fy);
+    }
+    if (x != x && y != y) return true;
+    return a == b;
+}
+
+// scratch words a segment needs: per min / max field its carried deque plus its adds
+__global__ __launch_bounds__(kBlock) void k_pg_dq_need(const i64* __restrict__ seg_start, i64 n_seg, i64 n_ops,
+                                                      const u32* __restrict__ skey, const u32* __restrict__ sidx, PgOps O,
+                                                      PgDeques D, i64* need) {
+    const i64 sg = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (sg > n_seg) return;
+    if (sg == n_seg) { need[sg] = 0; return; }
+    const i64 lo = seg_start[sg], hi = sg + 1 < n_seg ? seg_start[sg + 1] : n_ops;
+    const u32 pg = skey[lo];
+    i64 adds = 0;
+    for (i64 j = lo; j < hi; j++) adds += O.kind[sidx[j]] == 1;
+    i64 w = 0;
+    for (int f = 0; f < D.nf; f++) w += D.len[(size_t)D.field[f] * D.n + pg] + adds;
+    need[sg] = w;
+}
+
+void launch_pg_dq_need(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
+                       PgOps O, PgDeques D, i64* need) {
+    hipLaunchKernelGGL(k_pg_dq_need, dim3((unsigned)((n_seg + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, seg_start,
+                       n_seg, n_ops, skey, sidx, O, D, need);
+}
+
 template <int NA>
 __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_start, i64 n_seg, i64 n_ops,
                                                  const u32* __restrict__ skey, const u32* __restrict__ sidx, PgOps O,
                                                  KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on,
                                                  int exp_on, SlxRows rows, u64* row_key, u32* row_part,
-                                                 unsigned int* n_rows) {
+                                                 unsigned int* n_rows, PgDeques D, const i64* __restrict__ scr_off) {
     const i64 sg = (i64)blockIdx.x * 64 + threadIdx.x;
     if (sg >= n_seg) return;
     const i64 lo = seg_start[sg], hi = sg + 1 < n_seg ? seg_start[sg + 1] : n_ops;
@@ -614,15 +652,41 @@ __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_st
     const u64 pk = slot_key(pgkt, pg);
     i64 cnt = st_cnt[pg];
     u64 f[NA];
+    // min / max: the deque of aggregator a in scratch [dqb[a] + dqh[a], + dql[a])
+    i64 dqb[NA], dqh[NA], dql[NA];
+    i64 adds = 0;
+    if (D.nf > 0)
+        for (i64 j = lo; j < hi; j++) adds += O.kind[sidx[j]] == 1;
+    i64 base = D.nf > 0 ? scr_off[sg] : 0;
 #pragma unroll
     for (int a = 0; a < NA; a++) {
         f[a] = 0;
-        if (a < ap.n && ap.kind[a] != AK_COUNT) f[a] = st_f[(size_t)ap.field[a] * st_n + pg];
+        dqb[a] = dqh[a] = dql[a] = 0;
+        if (a >= ap.n) continue;
+        const int kind = ap.kind[a];
+        if (kind == AK_COUNT) continue;
+        if (kind >= AK_MIN_L) {
+            // (aggregators of one field share its deque: the first one loads it)
+            int first = a;
+            for (int b = 0; b < a; b++)
+                if (ap.kind[b] >= AK_MIN_L && ap.field[b] == ap.field[a]) { first = b; break; }
+            if (first != a) { dqb[a] = dqb[first]; dql[a] = dql[first]; continue; }
+            const size_t fi = (size_t)ap.field[a] * D.n + pg;
+            const i64 L = D.len[fi];
+            dqb[a] = base;
+            for (i64 e = 0; e < L; e++) D.scratch[base + e] = D.pool[D.off[fi] + e];
+            dql[a] = L;
+            base += L + adds;
+        } else {
+            f[a] = st_f[(size_t)ap.field[a] * st_n + pg];
+        }
     }
     i64 chunk = -1, first = -1, q_ts = 0, q_seq = 0, q_clk = 0;
     unsigned char q_exp = 0;
     u64 rv[NA];
     unsigned char rn[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) { rv[a] = 0; rn[a] = 0; }
     auto flush_row = [&]() {
         if (first < 0) return;
         const u32 slot = atomicAdd(n_rows, 1u);
@@ -657,7 +721,34 @@ __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_st
             const int kind = ap.kind[a];
             if (kind == AK_COUNT) continue;
             const u64 x = O.vals[(size_t)ap.vcol[a] * O.cap + oi];
-            if (kind == AK_SUM_L) {
+            if (kind >= AK_MIN_L) {
+                bool owner = true;
+                for (int b = 0; b < a; b++)
+                    if (ap.kind[b] >= AK_MIN_L && ap.field[b] == ap.field[a]) owner = false;
+                if (!owner) continue;  // the field's deque moves once per operation
+                u64* d = D.scratch + dqb[a];
+                i64 h = dqh[a], len = dql[a];
+                if (add) {
+                    // MinAttributeAggregatorExecutor.processAdd: drop worse entries from the back
+                    while (len > 0 && g_worse(kind, d[h + len - 1], x)) len--;
+                    d[h + len] = x;
+                    len++;
+                } else {
+                    // processRemove: removeFirstOccurrence(value)
+                    i64 found = -1;
+                    for (i64 e = 0; e < len; e++)
+                        if (g_eq(kind, d[h + e], x)) { found = e; break; }
+                    if (found == 0) { h++; len--; }
+                    else if (found > 0) {
+                        for (i64 e = found; e + 1 < len; e++) d[h + e] = d[h + e + 1];
+                        len--;
+                    }
+                }
+                dqh[a] = h;
+                dql[a] = len;
+                for (int b = a + 1; b < NA; b++)
+                    if (b < ap.n && ap.kind[b] >= AK_MIN_L && ap.field[b] == ap.field[a]) { dqh[b] = h; dql[b] = len; }
+            } else if (kind == AK_SUM_L) {
                 f[a] = add ? (u64)((i64)f[a] + (i64)x) : (u64)java_d2l((double)(i64)f[a] - (double)(i64)x);
             } else {
                 const double v = g_num(ap, a, x);
@@ -680,9 +771,12 @@ __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_st
                 const int kind = ap.kind[a];
                 if (kind == AK_COUNT) rv[a] = (u64)cnt;
                 else if (kind == AK_SUM_L || kind == AK_SUM_D) { rn[a] = cnt == 0; rv[a] = cnt == 0 ? 0 : f[a]; }
-                else {
+                else if (kind == AK_AVG) {
                     rn[a] = cnt == 0;
                     if (cnt) rv[a] = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) / (double)cnt);
+                } else {
+                    rn[a] = dql[a] > 0 ? 0 : 1;
+                    rv[a] = dql[a] > 0 ? D.scratch[dqb[a] + dqh[a]] : 0;
                 }
             }
         }
@@ -690,21 +784,69 @@ __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_st
     flush_row();
     st_cnt[pg] = cnt;
 #pragma unroll
-    for (int a = 0; a < NA; a++)
-        if (a < ap.n && ap.kind[a] != AK_COUNT) st_f[(size_t)ap.field[a] * st_n + pg] = f[a];
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n || ap.kind[a] == AK_COUNT) continue;
+        if (ap.kind[a] >= AK_MIN_L) {
+            const size_t fi = (size_t)ap.field[a] * D.n + pg;
+            D.new_at[fi] = dqb[a] + dqh[a];
+            D.new_len[fi] = dql[a];
+        } else {
+            st_f[(size_t)ap.field[a] * st_n + pg] = f[a];
+        }
+    }
+    if (D.nf > 0) D.active[pg] = 1;
 }
 
 void launch_pg_replay(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops, const u32* skey, const u32* sidx,
                       PgOps O, KeyTable pgkt, i64* st_cnt, u64* st_f, i64 st_n, AggPlan ap, int cur_on, int exp_on,
-                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows) {
+                      SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows, PgDeques D, const i64* scr_off) {
     if (n_seg <= 0) return;
     const unsigned grid = (unsigned)((n_seg + 63) / 64);
     if (ap.n <= 4)
         hipLaunchKernelGGL(k_pg_replay<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_ops, skey, sidx, O, pgkt, st_cnt,
-                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows);
+                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows, D, scr_off);
     else
         hipLaunchKernelGGL(k_pg_replay<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_ops, skey, sidx, O, pgkt, st_cnt,
-                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows);
+                           st_f, st_n, ap, cur_on, exp_on, rows, row_key, row_part, n_rows, D, scr_off);
+}
+
+// the deques after the push, (field, state)-major, into a fresh pool: lengths (then their scan) ...
+__global__ __launch_bounds__(kBlock) void k_pg_dq_len(PgDeques D, i64* out_len) {
+    const i64 t = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 total = (i64)D.nf * D.n;
+    if (t > total) return;
+    if (t == total) { out_len[t] = 0; return; }
+    const i64 fi = (i64)D.field[t / D.n] * D.n + t % D.n;
+    out_len[t] = D.active[t % D.n] ? D.new_len[fi] : D.len[fi];
+}
+
+// ... and the copies (pool_out gets every state's deque at off_out[t])
+__global__ __launch_bounds__(kBlock) void k_pg_dq_pool(PgDeques D, const i64* __restrict__ off_out, u64* pool_out,
+                                                      i64* new_off) {
+    const i64 t = (i64)blockIdx.x * kBlock + threadIdx.x;
+    const i64 total = (i64)D.nf * D.n;
+    if (t >= total) return;
+    const i64 st = t % D.n;
+    const i64 fi = (i64)D.field[t / D.n] * D.n + st;
+    const bool act = D.active[st] != 0;
+    const i64 L = act ? D.new_len[fi] : D.len[fi];
+    const u64* src = act ? D.scratch + D.new_at[fi] : D.pool + D.off[fi];
+    u64* dst = pool_out + off_out[t];
+    for (i64 e = 0; e < L; e++) dst[e] = src[e];
+    new_off[fi] = off_out[t];
+    D.len[fi] = L;
+}
+
+void launch_pg_dq_len(hipStream_t s, PgDeques D, i64* out_len) {
+    const i64 total = (i64)D.nf * D.n;
+    hipLaunchKernelGGL(k_pg_dq_len, dim3((unsigned)((total + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, D, out_len);
+}
+
+void launch_pg_dq_pool(hipStream_t s, PgDeques D, const i64* off_out, u64* pool_out, i64* new_off) {
+    const i64 total = (i64)D.nf * D.n;
+    if (total > 0)
+        hipLaunchKernelGGL(k_pg_dq_pool, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, D, off_out,
+                           pool_out, new_off);
 }
 
 // sorted operation keys: heads of the (partition, group) runs among the first n valid ones

@@ -79,6 +79,10 @@ struct SlidingImpl {
     // time lanes grouped by other columns: operation lists, their sort, the (partition, group) states
     DevBuf pg_room, op_pos, op_pg, op_kind, op_seq, op_ts, op_clk, op_vals, pg_ocnt, pg_skey, pg_sidx, pg_st_cnt, pg_st_f;
     int64_t pg_st_n = 0;
+    // their min / max deques: a pool with per (field, state) offsets / lengths, the push's scratch
+    DevBuf pg_dq_pool, pg_dq_pool2, pg_dq_off, pg_dq_off2, pg_dq_len, pg_dq_scr, pg_dq_at, pg_dq_nlen, pg_dq_act,
+        pg_dq_need, pg_dq_lens;
+    int64_t pg_dq_words = 0;
     DevBuf pg_rpart, pg_prevcnt, pg_ekey, pg_ekey2, pg_eval, pg_eval2, pg_keep, pg_head, pg_seg, pg_rkey, pg_rkey2, pg_order,
         pg_cnt;
 };

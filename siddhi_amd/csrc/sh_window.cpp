@@ -276,13 +276,6 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // the sorted chunks have no per-partition sequential walk, so a hot partition does not serialise
     q->group_other = (plane_group && !by_partition) || plane_time_group;
     if (plane_time_group) {
-        for (int a = 0; a < q->ap.n; a++)
-            if (q->ap.kind[a] >= AK_MIN_L) {
-                delete q;
-                return sh_fail(SH_ERR_UNSUPPORTED,
-                               "partitioned time / externalTime windows grouped by other columns: count / sum / avg "
-                               "(min / max keep a deque per (partition, group) state)");
-            }
         if ((rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
             delete q;
             return rc;

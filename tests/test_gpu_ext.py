@@ -178,5 +178,5 @@ def test_partitioned_external_time_checkpoint():
 def test_partitioned_external_time_group_by_other(output):
     ts, cols = pstream(40_000, 29, 0xEA, late_ms=500)
     sp = abi.QuerySpec(PSCH, "externalTime", 400, group_by=["k"], ts_attr="et", partition="p", key_capacity=128,
-                       output=output, aggs=[("count", None), ("sum", "v"), ("avg", "et")])
+                       output=output, aggs=[("count", None), ("sum", "v"), ("avg", "et"), ("min", "v"), ("max", "et")])
     both(sp, split_batches(PSCH, ts, cols, [1, 12_000, 30_000], 3), f"pxt group {output}")

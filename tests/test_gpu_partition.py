@@ -238,7 +238,17 @@ def test_partitioned_time_group_by_other_zipf(rt):
     assert ref["expired"].sum() > 0
 
 
-def test_partitioned_time_group_by_other_min_max_refused(rt):
-    spec = abi.QuerySpec(GSCHEMA, "time", 150, group_by=["g"], aggs=[("min", "v")], partition="p", key_capacity=64)
-    with pytest.raises(rt.SiddhiError, match="count / sum / avg"):
-        rt.GpuQuery(spec)
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("send_size", [1, 5])
+def test_partitioned_time_group_by_other_min_max(rt, output, send_size):
+    """min / max per (partition, group) state: MinAttributeAggregatorExecutor's deque with
+    removeFirstOccurrence (values repeat: the quirk fires), carried between pushes in a pool"""
+    ts, cols = gstream(40_000, 25, 4, 89, runs=send_size > 1)
+    spec = abi.QuerySpec(GSCHEMA, "time", 120, group_by=["g"],
+                         aggs=[("min", "v"), ("max", "v"), ("max", "x"), ("count", None), ("min", "h")], partition="p",
+                         filter=(">", "v", -45.0), output=output, key_capacity=256)
+    pushes = split_batches(GSCHEMA, ts, cols, [1, 9_000, 9_001, 25_000], send_size)
+    pushes.insert(3, ("advance", int(ts[8_999]) + 60))
+    pushes.append(("advance", int(ts[-1]) + 5_000))
+    ref = both(rt, spec, pushes, f"ptime group minmax {output} {send_size}")
+    assert ref["ts"].size > 0

@@ -229,7 +229,8 @@ def test_partition_time_group_lanes_checkpoint(cut):
     states and both key tables, and the Scheduler, restored into a fresh query"""
     from tests.test_gpu_partition import GSCHEMA, gstream
     ts, cols = gstream(50_000, 30, 5, 29 + cut)
-    spec = abi.QuerySpec(GSCHEMA, "time", 200, group_by=["g"], aggs=[("count", None), ("sum", "v")], partition="p",
+    spec = abi.QuerySpec(GSCHEMA, "time", 200, group_by=["g"], aggs=[("count", None), ("sum", "v"), ("min", "v"),
+                                                                     ("max", "x")], partition="p",
                          output="all", key_capacity=128)
     pushes = split_batches(GSCHEMA, ts, cols, [15_000, 33_000], 1) + [("advance", int(ts[-1]) + 1_000)]
     got, ref, _ = checkpointed(spec, pushes, cut)
