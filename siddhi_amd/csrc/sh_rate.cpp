@@ -53,10 +53,17 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     bool gb = (lanes ? q->d.n_group_by > 0 : q->kp.n > 0) && kind != SH_RATE_ALL;
     bool part = false;
     if (lanes && kind != SH_RATE_NONE) {
-        if (gb && q->group_other)
+        // grouped by other columns, each partition's keyed First limiter is the global one keyed by
+        // (partition, group key) — one 32-bit group column packs beside the partition slot
+        const int gc = q->d.n_group_by == 1 ? q->d.group_by[0] : -1;
+        const bool k32 = gc >= 0 && (q->d.col_types[gc] == SH_T_INT || q->d.col_types[gc] == SH_T_STRID ||
+                                     q->d.col_types[gc] == SH_T_BOOL);
+        if (gb && q->group_other && !((kind == SH_RATE_FIRST || kind == SH_RATE_FIRST_TIME) && k32))
             return sh_fail(SH_ERR_UNSUPPORTED,
-                           "output first / last every of a partitioned lengthBatch grouped by other columns (per-partition "
-                           "keyed limiters): `output all every`, or no group-by");
+                           "output last every (or first every with a long / floating / two-column group key) of a "
+                           "partitioned window grouped by other columns: `output all every`, `output first every` by one "
+                           "int / string group column, or no group-by");
+        q->rate.pkey = gb && q->group_other;
         part = kind == SH_RATE_ALL || kind == SH_RATE_LAST || !gb;
         if (part) gb = false;
         const int64_t np = plane_slots(q);
@@ -70,6 +77,7 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
         HIPCHK(hipStreamSynchronize(q->ctx->stream));
         r.nparts = np;
     }
+    if (!lanes) q->rate.pkey = false;
     q->rate.part = part;
     q->rate.kind = kind;
     q->rate.N = n;
@@ -325,7 +333,8 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
         RCHK(r.pos.reserve((size_t)(m + 1) * 4, false));
         RCHK(r.starts.reserve((size_t)(m + 1) * 4, false));
         RCHK(r.tmp.reserve((size_t)((m + 1 + kTile - 1) / kTile + 16) * 8, false));
-        launch_rate_pack(s, m, src.keys, sstride, nk, r.skey.as<u64>(), r.idx.as<u32>());
+        if (r.pkey) launch_ratep_pkey(s, m, src.keys, plane_out_part(q), r.skey.as<u64>(), r.idx.as<u32>());
+        else launch_rate_pack(s, m, src.keys, sstride, nk, r.skey.as<u64>(), r.idx.as<u32>());
         size_t tb = 0;
         if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, m, s))
             return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
@@ -359,7 +368,8 @@ int rate_apply(sh_query* q, const sh_out* in, bool flush_dev, bool host_out, con
             RCHK(r.pos.reserve((size_t)(m + 1) * 4, false));
             RCHK(r.starts.reserve((size_t)(m + 1) * 4, false));
             RCHK(r.tmp.reserve((size_t)((m + 1 + kTile - 1) / kTile + 16) * 8, false));
-            launch_rate_pack(s, m, src.keys, sstride, nk, r.skey.as<u64>(), r.idx.as<u32>());
+            if (r.pkey) launch_ratep_pkey(s, m, src.keys, plane_out_part(q), r.skey.as<u64>(), r.idx.as<u32>());
+            else launch_rate_pack(s, m, src.keys, sstride, nk, r.skey.as<u64>(), r.idx.as<u32>());
             size_t tb = 0;
             if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, m, s))
                 return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");

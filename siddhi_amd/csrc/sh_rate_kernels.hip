@@ -480,6 +480,19 @@ __global__ __launch_bounds__(kBlock) void k_ratep_gather(i64 T, const u32* __res
     if (out_part) out_part[o] = in_part[s];
 }
 
+// (partition slot, 32-bit group key) as one sort key: the per-partition keyed limiters as one keyed limiter
+__global__ __launch_bounds__(kBlock) void k_ratep_pkey(i64 n, const i64* __restrict__ keys, const u32* __restrict__ part,
+                                                      u64* skey, u32* idx) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    skey[i] = ((u64)part[i] << 32) | (u64)(u32)keys[i];
+    idx[i] = (u32)i;
+}
+
+void launch_ratep_pkey(hipStream_t s, i64 n, const i64* keys, const u32* part, u64* skey, u32* idx) {
+    if (n > 0) hipLaunchKernelGGL(k_ratep_pkey, dim3(grid_of(n)), dim3(kBlock), 0, s, n, keys, part, skey, idx);
+}
+
 void launch_ratep_pack(hipStream_t s, i64 S, i64 nc, const u32* c_part, const u32* in_part, u64* skey, u32* idx) {
     if (S > 0) hipLaunchKernelGGL(k_ratep_pack, dim3(grid_of(S)), dim3(kBlock), 0, s, S, nc, c_part, in_part, skey, idx);
 }

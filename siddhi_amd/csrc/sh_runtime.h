@@ -380,6 +380,7 @@ struct sh_query {
         // one limiter per partition instance (the partition lanes): per partition slot the running row
         // count (First/LastPerEvent) and `first every <t>`'s output time; the carried rows' partitions
         bool part = false;
+        bool pkey = false;  // keyed First limiters of lanes grouped by other columns: key = (partition, group)
         int64_t nparts = 0;
         DevBuf c_part, s_part, t_part, pseq, pft_has, pft_last, keep, okey, okey2, olist, olist2;
         PinnedVec<int64_t> h_off, h_clk, flush_offsets, flush_clock;
