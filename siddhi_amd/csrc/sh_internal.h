@@ -407,6 +407,12 @@ void launch_rate_gather(hipStream_t s, i64 n, const u32* flag, const u32* pre, c
 // one limiter per partition instance (the partition lanes' rows carry their partition slot)
 void launch_ratep_pack(hipStream_t s, i64 S, i64 nc, const u32* c_part, const u32* in_part, u64* skey, u32* idx);
 void launch_ratep_pkey(hipStream_t s, i64 n, const i64* keys, const u32* part, u64* skey, u32* idx);
+void launch_ratep_last_keyed(hipStream_t s, i64 S, const u32* hd, const u32* pos, const u32* starts, const u32* idx, i64 N,
+                             const i64* keys, i64 kstride, const u32* sp, i64* ord, u32* cidx, u32* keep, u64* skey,
+                             u32* sidx);
+void launch_ratep_last_keyed_rows(hipStream_t s, i64 S, const u64* skey, const u32* idx, const u32* cidx, const i64* ord,
+                                  i64 N, i64 nc, const i64* flush_off, int nf, u32* hd, u32* pos, u32* flag, u32* src,
+                                  int* eflush);
 void launch_ratep_flags(hipStream_t s, i64 S, const u32* hd, const u32* pos, const u32* starts, const u64* skey,
                         const u32* idx, int mode, i64 N, i64 nc, i64* pseq, const i64* flush_off, int nf, u32* flag,
                         int* eflush, u32* src, u32* keep);

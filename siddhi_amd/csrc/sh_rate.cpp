@@ -58,12 +58,13 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
         const int gc = q->d.n_group_by == 1 ? q->d.group_by[0] : -1;
         const bool k32 = gc >= 0 && (q->d.col_types[gc] == SH_T_INT || q->d.col_types[gc] == SH_T_STRID ||
                                      q->d.col_types[gc] == SH_T_BOOL);
-        if (gb && q->group_other && !((kind == SH_RATE_FIRST || kind == SH_RATE_FIRST_TIME) && k32))
+        if (gb && q->group_other && !k32)
             return sh_fail(SH_ERR_UNSUPPORTED,
-                           "output last every (or first every with a long / floating / two-column group key) of a "
-                           "partitioned window grouped by other columns: `output all every`, `output first every` by one "
-                           "int / string group column, or no group-by");
+                           "keyed output rate limiting of a partitioned window grouped by a long / floating / two-column "
+                           "key: `output all every`, a limiter keyed by one int / string group column, or no group-by");
         q->rate.pkey = gb && q->group_other;
+        // LastGroupBy grouped by other columns: the per-partition positional windows, keyed inside them
+        q->rate.lkey = kind == SH_RATE_LAST && gb && q->group_other;
         part = kind == SH_RATE_ALL || kind == SH_RATE_LAST || !gb;
         if (part) gb = false;
         const int64_t np = plane_slots(q);
@@ -77,7 +78,7 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
         HIPCHK(hipStreamSynchronize(q->ctx->stream));
         r.nparts = np;
     }
-    if (!lanes) q->rate.pkey = false;
+    if (!lanes) q->rate.pkey = q->rate.lkey = false;
     q->rate.part = part;
     q->rate.kind = kind;
     q->rate.N = n;
@@ -453,7 +454,7 @@ static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, boo
     const int nk = (int)in->n_keys, na = (int)in->n_vals;
     const int64_t n = in->n_rows, N = r.N;
     const u32* in_part = plane_out_part(q);
-    const bool carries = r.kind == SH_RATE_ALL;
+    const bool carries = r.kind == SH_RATE_ALL || r.lkey;
     const int64_t nc = carries ? r.nc : 0, S = nc + n;
     RateRows inr{(i64*)in->ts, (unsigned char*)in->expired, (i64*)in->rep, (i64*)in->keys, (u64*)in->vals,
                  (unsigned char*)in->nulls};
@@ -523,9 +524,35 @@ static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, boo
             return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
         launch_rate_segments(s, S, r.skey2.as<u64>(), r.idx2.as<u32>(), 1, 0, r.hd.as<u32>(), r.pos.as<u32>(),
                              r.starts.as<u32>(), r.tmp.as<i64>());
-        launch_ratep_flags(s, S, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.skey2.as<u64>(), r.idx2.as<u32>(),
-                           r.kind, N, nc, r.pseq.as<i64>(), foff, nf, r.flag.as<u32>(), r.eflush.as<int>(), r.src.as<u32>(),
-                           r.keep.as<u32>());
+        if (r.lkey) {
+            // windows of N rows per partition; inside a complete one, per group key its last row at its
+            // first row's place (LastGroupByPerEventOutputRateLimiter :51-83)
+            RCHK(r.lk_ord.reserve((size_t)std::max<int64_t>(S, 1) * 8, false));
+            RCHK(r.lk_cidx.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
+            RCHK(r.lk_key.reserve((size_t)std::max<int64_t>(S, 1) * 8, false));
+            RCHK(r.lk_key2.reserve((size_t)std::max<int64_t>(S, 1) * 8, false));
+            RCHK(r.lk_idx.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
+            RCHK(r.lk_idx2.reserve((size_t)std::max<int64_t>(S, 1) * 4, false));
+            launch_ratep_last_keyed(s, S, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.idx2.as<u32>(), N, src.keys,
+                                    sstride, sp, r.lk_ord.as<i64>(), r.lk_cidx.as<u32>(), r.keep.as<u32>(),
+                                    r.lk_key.as<u64>(), r.lk_idx.as<u32>());
+            tb = 0;
+            if (sort_u64_pairs(nullptr, &tb, r.lk_key.as<u64>(), nullptr, r.lk_idx.as<u32>(), nullptr, S, s))
+                return sh_fail(SH_ERR_DEVICE, "output rate: sort sizing");
+            RCHK(r.sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (sort_u64_pairs(r.sort_tmp.p, &tb, r.lk_key.as<u64>(), r.lk_key2.as<u64>(), r.lk_idx.as<u32>(),
+                               r.lk_idx2.as<u32>(), S, s))
+                return sh_fail(SH_ERR_DEVICE, "output rate: sort failed");
+            // (src = identity first: only the runs' first rows get another source)
+            launch_rate_clear(s, S, r.src.as<u32>(), r.flag.as<u32>());
+            launch_ratep_last_keyed_rows(s, S, r.lk_key2.as<u64>(), r.lk_idx2.as<u32>(), r.lk_cidx.as<u32>(),
+                                         r.lk_ord.as<i64>(), N, nc, foff, nf, r.hd.as<u32>(), r.pos.as<u32>(),
+                                         r.flag.as<u32>(), r.src.as<u32>(), r.eflush.as<int>());
+        } else {
+            launch_ratep_flags(s, S, r.hd.as<u32>(), r.pos.as<u32>(), r.starts.as<u32>(), r.skey2.as<u64>(),
+                               r.idx2.as<u32>(), r.kind, N, nc, r.pseq.as<i64>(), foff, nf, r.flag.as<u32>(),
+                               r.eflush.as<int>(), r.src.as<u32>(), r.keep.as<u32>());
+        }
     }
     HIPCHK(hipGetLastError());
     // kept rows, ordered by their emitting flush (stable: a group leaves in its own order)

@@ -493,6 +493,71 @@ void launch_ratep_pkey(hipStream_t s, i64 n, const i64* keys, const u32* part, u
     if (n > 0) hipLaunchKernelGGL(k_ratep_pkey, dim3(grid_of(n)), dim3(kBlock), 0, s, n, keys, part, skey, idx);
 }
 
+// LastGroupByPerEvent per partition instance (grouped by another column): every row's ordinal in its
+// partition's sequence (carried rows first) names its window of N; rows of complete windows are keyed
+// (partition, group key) for the second sort, the open window's rows are carried
+__global__ __launch_bounds__(kBlock) void k_ratep_lk_ord(i64 S, const u32* __restrict__ hd, const u32* __restrict__ pos,
+                                                        const u32* __restrict__ starts, const u32* __restrict__ idx, i64 N,
+                                                        const i64* __restrict__ keys, i64 kstride, const u32* __restrict__ sp,
+                                                        i64* ord, u32* cidx, u32* keep, u64* skey, u32* sidx) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > S) return;
+    if (i == S) { keep[S] = 0; return; }
+    const u32 g = pos[i] + hd[i] - 1;
+    const i64 lo = starts[g], o = i - lo, tot = (i64)starts[g + 1] - lo;
+    const u32 r = idx[i];
+    ord[r] = o;
+    const bool complete = o < tot / N * N;
+    keep[r] = complete ? 0u : 1u;
+    cidx[r] = complete ? idx[lo + (o / N + 1) * N - 1] : 0u;
+    skey[r] = complete ? (((u64)sp[r] << 32) | (u64)(u32)keys[r]) : ~0ull;
+    sidx[r] = r;
+}
+
+// heads of the (partition, key, window) runs of the key-sorted rows (source order inside a run)
+__global__ __launch_bounds__(kBlock) void k_ratep_lk_heads(i64 n, const u64* __restrict__ skey, const u32* __restrict__ idx,
+                                                          const i64* __restrict__ ord, i64 N, u32* hd, u32* pos) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (j > n) return;
+    u32 h = 0;
+    if (j < n && skey[j] != ~0ull)
+        h = j == 0 || skey[j] != skey[j - 1] || ord[idx[j]] / N != ord[idx[j - 1]] / N;
+    hd[j] = h;
+    pos[j] = h;
+}
+
+// per run: the flag at its first row, the data of its last row, emitted by the window's completing row
+__global__ __launch_bounds__(kBlock) void k_ratep_lk_rows(i64 n, const u64* __restrict__ skey, const u32* __restrict__ hd,
+                                                         const u32* __restrict__ idx, const u32* __restrict__ cidx,
+                                                         const i64* __restrict__ ord, i64 N, i64 nc,
+                                                         const i64* __restrict__ flush_off, int nf, u32* flag, u32* src,
+                                                         int* eflush) {
+    const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n || !hd[j]) return;
+    i64 e = j + 1;
+    while (e < n && !hd[e] && skey[e] != ~0ull) e++;
+    const u32 r = idx[j];
+    flag[r] = 1;
+    src[r] = idx[e - 1];
+    eflush[r] = rate_flush_of(flush_off, nf, (i64)cidx[r] - nc);
+}
+
+void launch_ratep_last_keyed(hipStream_t s, i64 S, const u32* hd, const u32* pos, const u32* starts, const u32* idx, i64 N,
+                             const i64* keys, i64 kstride, const u32* sp, i64* ord, u32* cidx, u32* keep, u64* skey,
+                             u32* sidx) {
+    hipLaunchKernelGGL(k_ratep_lk_ord, dim3(grid_of(S + 1)), dim3(kBlock), 0, s, S, hd, pos, starts, idx, N, keys, kstride,
+                       sp, ord, cidx, keep, skey, sidx);
+}
+
+void launch_ratep_last_keyed_rows(hipStream_t s, i64 S, const u64* skey, const u32* idx, const u32* cidx, const i64* ord,
+                                  i64 N, i64 nc, const i64* flush_off, int nf, u32* hd, u32* pos, u32* flag, u32* src,
+                                  int* eflush) {
+    hipLaunchKernelGGL(k_ratep_lk_heads, dim3(grid_of(S + 1)), dim3(kBlock), 0, s, S, skey, idx, ord, N, hd, pos);
+    if (S > 0)
+        hipLaunchKernelGGL(k_ratep_lk_rows, dim3(grid_of(S)), dim3(kBlock), 0, s, S, skey, hd, idx, cidx, ord, N, nc,
+                           flush_off, nf, flag, src, eflush);
+}
+
 void launch_ratep_pack(hipStream_t s, i64 S, i64 nc, const u32* c_part, const u32* in_part, u64* skey, u32* idx) {
     if (S > 0) hipLaunchKernelGGL(k_ratep_pack, dim3(grid_of(S)), dim3(kBlock), 0, s, S, nc, c_part, in_part, skey, idx);
 }

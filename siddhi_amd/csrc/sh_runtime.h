@@ -381,6 +381,8 @@ struct sh_query {
         // count (First/LastPerEvent) and `first every <t>`'s output time; the carried rows' partitions
         bool part = false;
         bool pkey = false;  // keyed First limiters of lanes grouped by other columns: key = (partition, group)
+        bool lkey = false;  // keyed Last of lanes grouped by other columns (per-partition windows, keyed inside)
+        DevBuf lk_ord, lk_cidx, lk_key, lk_key2, lk_idx, lk_idx2;
         int64_t nparts = 0;
         DevBuf c_part, s_part, t_part, pseq, pft_has, pft_last, keep, okey, okey2, olist, olist2;
         PinnedVec<int64_t> h_off, h_clk, flush_offsets, flush_clock;

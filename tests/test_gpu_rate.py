@@ -188,9 +188,6 @@ def pstream(n, parts, seed):
 def test_partition_lanes_rate(rt, kind, n, window, param, group_by, output):
     """`partition with (p of S)` clones the query with its OutputRateLimiter per partition: each
     partition's rows are counted (and, for `first every <t>`, timed) on their own"""
-    if group_by == ["g"] and kind == "last":
-        pytest.skip("keyed Last limiters of lanes grouped by other columns are refused "
-                    "(test_partition_lanes_keyed_rate_refused_for_other_group_keys)")
     ts, cols = pstream(20_000, 37, 7)
     spec = abi.QuerySpec(PSCHEMA, window, param, group_by=group_by, aggs=[("count", None), ("sum", "v")],
                          partition="p", output=output, key_capacity=64, rate=(kind, n))
@@ -201,8 +198,8 @@ def test_partition_lanes_rate(rt, kind, n, window, param, group_by, output):
     assert out["ts"].size > 0
 
 
-def test_partition_lanes_keyed_rate_refused_for_other_group_keys(rt):
-    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 5, group_by=["g"], aggs=[("count", None)], partition="p",
+def test_partition_lanes_keyed_rate_refused_for_long_group_keys(rt):
+    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 5, group_by=["x"], aggs=[("count", None)], partition="p",
                          key_capacity=64, rate=("last", 3))
-    with pytest.raises(rt.SiddhiError, match="grouped by other columns"):
+    with pytest.raises(rt.SiddhiError, match="long / floating / two-column"):
         rt.GpuQuery(spec)

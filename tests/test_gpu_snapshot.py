@@ -211,13 +211,14 @@ def test_partition_group_lanes_checkpoint(output, cut):
     assert_same(got, ref, label=f"group lanes ckpt {output}")
 
 
-@pytest.mark.parametrize("rate", [("all", 3), ("first", 2), ("first_time", 50)])
-def test_partition_lanes_rate_checkpoint(rate):
+@pytest.mark.parametrize("rate,group_by", [(("all", 3), []), (("first", 2), []), (("first_time", 50), []),
+                                           (("last", 4), ["g"]), (("first", 3), ["g"])])
+def test_partition_lanes_rate_checkpoint(rate, group_by):
     """per-partition limiters: counters, output times and carried rows with their partitions"""
     from tests.test_gpu_rate import PSCHEMA, pstream
     ts, cols = pstream(30_000, 23, 13)
-    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 3, aggs=[("count", None), ("sum", "v")], partition="p", output="all",
-                         key_capacity=64, rate=rate)
+    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 3, group_by=group_by, aggs=[("count", None), ("sum", "v")], partition="p",
+                         output="all", key_capacity=64, rate=rate)
     pushes = split_batches(PSCHEMA, ts, cols, [10_000, 20_001], 1)
     got, ref, _ = checkpointed(spec, pushes, 1)
     assert_same(got, ref, label=f"lanes rate ckpt {rate}")
