@@ -420,7 +420,8 @@ void launch_ratep_fparts(hipStream_t s, int nf, const i64* foff, const u32* in_p
 void launch_ratep_ftime(hipStream_t s, int nf, const u32* hd, const u32* pos, const u32* starts, const u64* fkey,
                         const u32* fidx, const i64* fclk, u32 none, i64 T, unsigned char* has, i64* last,
                         unsigned char* chosen);
-void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, u64* okey, u32* olist);
+void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, const u32* src, u64* okey,
+                       u32* olist);
 void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey, RateRows in, i64 in_stride,
                          const u32* in_part, RateRows out, int nk, int na, int* out_flush, u32* out_part);
 

@@ -566,7 +566,8 @@ static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, boo
     RCHK(r.okey2.reserve((size_t)tc * 8, false));
     RCHK(r.olist.reserve((size_t)tc * 4, false));
     RCHK(r.olist2.reserve((size_t)tc * 4, false));
-    launch_ratep_list(s, S, r.flag.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), r.okey.as<u64>(), r.olist.as<u32>());
+    launch_ratep_list(s, S, r.flag.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), r.src.as<u32>(), r.okey.as<u64>(),
+                      r.olist.as<u32>());
     if (T > 0) {
         const unsigned fbits = bits_of((int64_t)nf + 1);
         tb = 0;
@@ -593,7 +594,7 @@ static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, boo
         if (nn > 0) {
             RCHK(r.olist.reserve((size_t)nn * 4, false));
             RCHK(r.okey.reserve((size_t)nn * 8, false));
-            launch_ratep_list(s, S, r.keep.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), r.okey.as<u64>(),
+            launch_ratep_list(s, S, r.keep.as<u32>(), r.pre.as<u32>(), r.eflush.as<int>(), nullptr, r.okey.as<u64>(),
                               r.olist.as<u32>());
             RateRows c2{};
             DevBuf t_ts, t_exp, t_rep, t_keys, t_vals, t_nulls;

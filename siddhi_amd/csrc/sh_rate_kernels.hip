@@ -452,13 +452,15 @@ __global__ __launch_bounds__(kBlock) void k_ratep_ftime(int nf, const u32* __res
     last[p] = t;
 }
 
-// flagged source rows -> (emitting flush, source index) lists, in source order
+// flagged source rows -> (emitting flush, row to show) lists, in source order (src: the row whose data
+// the flagged place shows; null = itself)
 __global__ __launch_bounds__(kBlock) void k_ratep_list(i64 S, const u32* __restrict__ flag, const u32* __restrict__ pre,
-                                                      const int* __restrict__ eflush, u64* okey, u32* olist) {
+                                                      const int* __restrict__ eflush, const u32* __restrict__ src,
+                                                      u64* okey, u32* olist) {
     const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= S || !flag[i]) return;
     okey[pre[i]] = (u64)(u32)eflush[i];
-    olist[pre[i]] = (u32)i;
+    olist[pre[i]] = src ? src[i] : (u32)i;
 }
 
 // rows of a list (source indices) -> a row set of stride T; out_flush from okey when given
@@ -583,8 +585,9 @@ void launch_ratep_ftime(hipStream_t s, int nf, const u32* hd, const u32* pos, co
                            T, has, last, chosen);
 }
 
-void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, u64* okey, u32* olist) {
-    if (S > 0) hipLaunchKernelGGL(k_ratep_list, dim3(grid_of(S)), dim3(kBlock), 0, s, S, flag, pre, eflush, okey, olist);
+void launch_ratep_list(hipStream_t s, i64 S, const u32* flag, const u32* pre, const int* eflush, const u32* src, u64* okey,
+                       u32* olist) {
+    if (S > 0) hipLaunchKernelGGL(k_ratep_list, dim3(grid_of(S)), dim3(kBlock), 0, s, S, flag, pre, eflush, src, okey, olist);
 }
 
 void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey, RateRows in, i64 in_stride,
