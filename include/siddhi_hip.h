@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 8
+#define SH_ABI_VERSION 9
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -247,6 +247,16 @@ int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
 #define SH_RATE_LAST 3
 #define SH_RATE_FIRST_TIME 4
 int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
+
+/* externalTimeBatch's fourth parameter, the scheduler timeout in milliseconds
+ * (ExternalTimeBatchWindowProcessor.java:196-207, `externalTimeBatch(ts, 1 sec, 0, 6 sec)`): when the
+ * playback clock passes the last scheduled time (clock of the window's first event, of every batch
+ * crossing and of every timeout, + ms) the open batch goes out so far (:256-275) — again whole, with
+ * its new events, at a later timeout or at its crossing (appendToOutputChunk, :385-438). Replaces the
+ * Java window's timeout argument. Set once, before the first push, on an unpartitioned
+ * externalTimeBatch query with current-events output (all events without group-by: every emission
+ * ends in current events, QuerySelector.processInBatchNoGroupBy keeps that row). ms == 0 is no timeout. */
+int sh_query_set_ext_timeout(sh_query* q, int64_t ms);
 
 /* The text of dictionary ids [first_id, first_id + n) of string column `col`, as UTF-16 code units (what a
  * java.lang.String holds): id first_id + i is units[offsets[i] .. offsets[i + 1]) (offsets has n + 1

@@ -33,6 +33,7 @@ def lib():
         L.or_query_create.restype = C.c_void_p
         L.or_query_destroy.argtypes = [C.c_void_p]
         L.or_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+        L.or_query_set_ext_timeout.argtypes = [C.c_void_p, C.c_int64]
         L.or_query_set_strings.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
         L.or_push.argtypes = [C.c_void_p, P(abi.Batch), P(P(abi.Out))]
         L.or_advance_time.argtypes = [C.c_void_p, C.c_int64, P(P(abi.Out))]
@@ -57,6 +58,8 @@ class OracleQuery:
         if not self.h:
             raise ValueError(lib().or_last_error().decode())
         if spec.rate and lib().or_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])):
+            raise ValueError(lib().or_last_error().decode())
+        if spec.timeout and lib().or_query_set_ext_timeout(self.h, int(spec.timeout)):
             raise ValueError(lib().or_last_error().decode())
         for col, names in (spec.strings or {}).items():
             self.set_strings(col, names)

@@ -485,6 +485,8 @@ struct PartitionState {
     // ExternalTimeBatchWindowProcessor.WindowState (:495-517): endTime = -1, startTime = the constant
     // start (commonStartTime, 0 when absent), lastCurrentEventTime = 0 (Java default)
     int64_t ext_end = -1, ext_start = 0, ext_last = 0;
+    int64_t ext_sched = 0;     // lastScheduledTime (timeout form)
+    bool ext_flushed = false;  // flushed (timeout form)
     Chunk ext_current, ext_expired;
     bool ext_has_reset = false; OEvent ext_reset;
     int64_t key = 0;
@@ -511,6 +513,7 @@ struct Query {
     bool clock_set = false;
     // TimeBatchWindowProcessor.nextEmitTime is a processor field shared by all partitions (:128)
     int64_t next_emit_time = -1;
+    int64_t ext_timeout = 0;  // externalTimeBatch(ts, T, start, timeout): schedulerTimeout
     int64_t seq_base = 0;  // stream index of the current push's first event
     std::unordered_map<int64_t, std::unique_ptr<PartitionState>> parts;  // partition flow id -> state
     // Scheduler.stateHolder (PartitionSyncStateHolder -> PartitionStateHolder.states, a
@@ -802,6 +805,8 @@ struct Query {
         int64_t elapsed = (current - start) % T;  // Java % truncates like C++
         return current + (T - elapsed);
     }
+    // the expired chunk exists when expired events are output or a timeout is set (WindowState :507-517)
+    bool ext_keeps_expired() const { return output_expects_expired || ext_timeout > 0; }
     void ext_flush(PartitionState& ps, std::vector<Chunk>& outs, int64_t current_time) {
         Chunk c;
         if (output_expects_expired && !ps.ext_expired.empty()) {
@@ -812,12 +817,34 @@ struct Query {
             ps.ext_reset.ts = current_time;
             c.push_back(ps.ext_reset);
             ps.ext_has_reset = false;
-            if (output_expects_expired)
+            if (ext_keeps_expired())
                 for (auto& e : ps.ext_current) { OEvent x = e; x.type = EXPIRED; ps.ext_expired.push_back(x); }
             for (auto& e : ps.ext_current) c.push_back(e);
         }
         ps.ext_current.clear();
         if (!c.empty()) outs.push_back(std::move(c));
+    }
+    // appendToOutputChunk (:385-438): after a timeout flush the batch goes out again, whole — its
+    // flushed part re-sent as CURRENT behind a RESET (expired copies first when expired events are
+    // output), then the new events; the expired chunk keeps growing until the batch's real flush
+    void ext_append(PartitionState& ps, std::vector<Chunk>& outs, int64_t current_time) {
+        if (ps.ext_current.empty()) return;
+        Chunk c, sent;
+        for (const auto& x : ps.ext_expired) {
+            if (output_expects_expired) { OEvent e = x; e.ts = current_time; c.push_back(e); }
+            OEvent s2 = x; s2.type = CURRENT; sent.push_back(s2);
+        }
+        OEvent r = ps.ext_reset; r.type = RESET; r.ts = current_time;
+        c.push_back(r);
+        for (auto& e : sent) c.push_back(e);
+        for (auto& e : ps.ext_current) { OEvent x = e; x.type = EXPIRED; ps.ext_expired.push_back(x); }
+        for (auto& e : ps.ext_current) c.push_back(e);
+        ps.ext_current.clear();
+        outs.push_back(std::move(c));
+    }
+    void ext_schedule(PartitionState& ps) {
+        ps.ext_sched = clock + ext_timeout;
+        notify_at(ps, ps.ext_sched);
     }
     void ext_append(PartitionState& ps, const OEvent& ev) {
         ps.ext_current.push_back(ev);
@@ -826,7 +853,7 @@ struct Query {
     void ext_time_batch(PartitionState& ps, Chunk& in) {
         if (in.empty()) return;
         const int64_t T = d.window_param;
-        if (ps.ext_end < 0) {
+        if (ps.ext_end < 0 && in.front().type == CURRENT) {
             const OEvent& f = in.front();
             if (d.has_start_time == 1) {
                 ps.ext_end = find_end_time(ext_attr(f, d.ts_col), ps.ext_start, T);
@@ -837,18 +864,39 @@ struct Query {
                 ps.ext_start = ext_attr(f, d.ts_col);
                 ps.ext_end = ps.ext_start + T;
             }
+            if (ext_timeout > 0) ext_schedule(ps);  // initTiming :328-332
         }
         std::vector<Chunk> outs;
         for (OEvent& ev : in) {
+            if (ev.type == TIMER) {
+                // :256-275: the timeout of the last scheduled time flushes the batch so far (once; a
+                // later timeout re-sends it whole with its new events), then reschedules
+                if (ext_timeout > 0 && ps.ext_sched <= ev.ts) {
+                    if (!ps.ext_flushed) {
+                        ext_flush(ps, outs, ps.ext_last);
+                        ps.ext_flushed = true;
+                    } else {
+                        ext_append(ps, outs, ps.ext_last);
+                    }
+                    ext_schedule(ps);
+                }
+                continue;
+            }
             if (ev.type != CURRENT) continue;
             int64_t t = ext_attr(ev, d.ts_col);
             if (ps.ext_last < t) ps.ext_last = t;
             if (t < ps.ext_end) {
                 ext_append(ps, ev);
             } else {
-                ext_flush(ps, outs, ps.ext_last);
+                if (ps.ext_flushed) {
+                    ext_append(ps, outs, ps.ext_last);
+                    ps.ext_flushed = false;
+                } else {
+                    ext_flush(ps, outs, ps.ext_last);
+                }
                 ps.ext_end = find_end_time(ps.ext_last, ps.ext_start, T);
                 ext_append(ps, ev);
+                if (ext_timeout > 0) ext_schedule(ps);
             }
         }
         for (auto& c : outs) selector(ps, c);
@@ -1367,6 +1415,17 @@ int or_query_set_strings(void* h, int32_t col, int64_t first_id, int64_t n, cons
         v[(size_t)(first_id + i)].assign((const char16_t*)units + offsets[i], (const char16_t*)units + offsets[i + 1]);
         has[(size_t)(first_id + i)] = 1;
     }
+    return SH_OK;
+}
+
+// externalTimeBatch's 4th parameter (ExternalTimeBatchWindowProcessor :196-207): scheduler timeout (ms)
+int or_query_set_ext_timeout(void* h, int64_t ms) {
+    Query* q = (Query*)h;
+    if (q->d.window != SH_WIN_EXT_TIME_BATCH || ms < 0) {
+        g_err = "a timeout needs an externalTimeBatch window and >= 0 ms";
+        return SH_ERR_INVALID;
+    }
+    q->ext_timeout = ms;
     return SH_OK;
 }
 

@@ -177,17 +177,29 @@ __device__ __forceinline__ bool pass_at(i64 c, i64 n_pend, const u32* new_pos) {
     return c < n_pend || new_pos[c - n_pend] != kNoPos;
 }
 
-__global__ __launch_bounds__(kBlock) void k_pass_flags(i64 hi, i64 n_pend, const u32* new_pos, u32* f) {
+// (segments sorted and disjoint; they cover [0, hi) but where an externalTimeBatch timeout left a
+// batch's events out: those are in no segment)
+__device__ __forceinline__ bool in_segs(i64 c, const Segment* segs, int nseg) {
+    int a = 0, b = nseg;  // first segment with lo > c
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if (segs[m].lo <= c) a = m + 1; else b = m;
+    }
+    return a > 0 && c < segs[a - 1].hi;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pass_flags(i64 hi, i64 n_pend, const u32* new_pos, const Segment* segs,
+                                                       int nseg, u32* f) {
     const i64 c = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (c > hi) return;
-    f[c] = c < hi && pass_at(c, n_pend, new_pos) ? 1u : 0u;
+    f[c] = c < hi && pass_at(c, n_pend, new_pos) && in_segs(c, segs, nseg) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kBlock) void k_pass_rows(i64 hi, i64 n_pend, const u32* new_pos, const u32* pos,
                                                       const i64* pend_ts, const u64* pend_gidx, const i64* ts,
                                                       i64 seq_base, i64* out_ts, i64* out_rep) {
     const i64 c = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (c >= hi || !pass_at(c, n_pend, new_pos)) return;
+    if (c >= hi || pos[c + 1] == pos[c]) return;  // (not passing, or in no segment)
     const i64 o = pos[c];
     out_ts[o] = c < n_pend ? pend_ts[c] : ts[c - n_pend];
     out_rep[o] = c < n_pend ? (i64)pend_gidx[c] : seq_base + (c - n_pend);
@@ -203,7 +215,7 @@ void launch_pass_rows(hipStream_t s, i64 hi, i64 n_pend, const u32* new_pos, u32
                       const u64* pend_gidx, const i64* ts, i64 seq_base, const Segment* segs, int nseg, i64* out_ts,
                       i64* out_rep, u32* seg_rows, u32* n_rows) {
     const unsigned g = (unsigned)((hi + 1 + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_pass_flags, dim3(g), dim3(kBlock), 0, s, hi, n_pend, new_pos, pos);
+    hipLaunchKernelGGL(k_pass_flags, dim3(g), dim3(kBlock), 0, s, hi, n_pend, new_pos, segs, nseg, pos);
     launch_scan_sum_large_u32(s, pos, hi + 1, tmp);
     hipLaunchKernelGGL(k_pass_rows, dim3(g), dim3(kBlock), 0, s, hi, n_pend, new_pos, pos, pend_ts, pend_gidx, ts,
                        seq_base, out_ts, out_rep);

@@ -2168,4 +2168,36 @@ void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
     }
 }
 
+// ---- externalTimeBatch timeout: where the push's clock passes lastScheduledTime --------------------
+// First send whose last event's timestamp reaches L (InputHandler.send sets the clock from it, and
+// every earlier send's clock stays below L): out[0] = its index (u64 max: none).
+__global__ __launch_bounds__(kBlock) void k_xt_first_send(const i64* __restrict__ ts, i64 N, i64 send_size, i64 L,
+                                                          unsigned long long* out) {
+    const i64 n_sends = send_size > 0 ? (N + send_size - 1) / send_size : 1;
+    for (i64 j = (i64)blockIdx.x * kBlock + threadIdx.x; j < n_sends; j += (i64)gridDim.x * kBlock) {
+        const i64 last = send_size > 0 ? min((j + 1) * send_size, N) - 1 : N - 1;
+        if (ts[last] >= L) atomicMin(out, (unsigned long long)j);
+    }
+}
+
+// passing events of the push in [0, hi): the open batch's events before a timeout's send
+__global__ __launch_bounds__(kBlock) void k_xt_count_pass(ColSet cols, FilterProg f, i64 hi, unsigned long long* out) {
+    i64 c = 0;
+    for (i64 e = (i64)blockIdx.x * kBlock + threadIdx.x; e < hi; e += (i64)gridDim.x * kBlock) c += eval_filter(f, cols, e);
+    c = block_reduce(c, [](i64 a, i64 b) { return a + b; }, 0);
+    if (threadIdx.x == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
+void launch_xt_first_send(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 L, unsigned long long* out) {
+    const i64 n_sends = send_size > 0 ? (N + send_size - 1) / send_size : 1;
+    const unsigned g = (unsigned)std::min<i64>((n_sends + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(k_xt_first_send, dim3(std::max(1u, g)), dim3(kBlock), 0, s, ts, N, send_size, L, out);
+}
+
+void launch_xt_count_pass(hipStream_t s, ColSet cols, FilterProg f, i64 hi, unsigned long long* out) {
+    if (hi <= 0) return;
+    const unsigned g = (unsigned)std::min<i64>((hi + kBlock - 1) / kBlock, 2048);
+    hipLaunchKernelGGL(k_xt_count_pass, dim3(g), dim3(kBlock), 0, s, cols, f, hi, out);
+}
+
 }  // namespace shd

@@ -266,6 +266,14 @@ struct sh_query {
     int64_t E0 = 0;
     int64_t W_open = 0;
     int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
+    // externalTimeBatch timeout (sh_query_set_ext_timeout): lastScheduledTime, and the open batch's
+    // passing events since its last emission (the window's currentEventChunk is empty when 0)
+    int64_t xt_timeout = 0;
+    bool xt_Lvalid = false;
+    int64_t xt_L = 0;
+    int64_t xt_nnew = 0;
+    DevBuf xt_dev;
+    PinnedBuf xt_host;
     int64_t n_pend = 0, pend_cap = 0;
     int64_t seq = 0;  // stream index of the next event pushed (sh_out.rep numbering)
     DevBuf pend_pos, pend_ts, pend_vals;

@@ -163,6 +163,12 @@ int batch_snapshot(sh_query* q, Writer& w) {
         RCHK(w.dev(q->xc_rep.p, (size_t)xn * 8, s));
     }
     w.val<int64_t>(q->seq);
+    // externalTimeBatch timeout: lastScheduledTime and the open batch's events not yet sent
+    if (q->xt_timeout > 0) {
+        w.val<uint8_t>(q->xt_Lvalid);
+        w.val<int64_t>(q->xt_L);
+        w.val<int64_t>(q->xt_nnew);
+    }
     return SH_OK;
 }
 
@@ -237,6 +243,11 @@ int batch_restore(sh_query* q, Reader& r) {
         RCHK(r.dev(q->xc_rep, 8, s));
     }
     q->seq = r.val<int64_t>();
+    if (q->xt_timeout > 0) {
+        q->xt_Lvalid = r.val<uint8_t>();
+        q->xt_L = r.val<int64_t>();
+        q->xt_nnew = r.val<int64_t>();
+    }
     tmp.release();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     q->p0_known = false;

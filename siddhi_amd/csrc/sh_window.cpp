@@ -546,18 +546,40 @@ static int closed_finish(sh_query* q, bool host_out) {
         HIPCHK(hipMemcpyAsync(q->out.rep.data() + base, q->out_rep.p, n_rows * 8, hipMemcpyDeviceToHost, s));
         // keys / vals / nulls are [k][n_rows] blocks straight into the pinned output vectors (a push
         // closes windows through run_closed at most once, so they start empty)
-        if (base != 0) return sh_fail(SH_ERR_INVALID, "host output appended twice in one push");
-        q->out.keys.resize((size_t)nk * n_rows);
-        q->out.vals.resize((size_t)na * n_rows);
-        if (nk) HIPCHK(hipMemcpyAsync(q->out.keys.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
-        if (q->given) {
-            size_t ob = q->order_host.size();
-            q->order_host.resize(ob + n_rows);
-            HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+        if (base != 0 && (q->xt_timeout == 0 || q->given))
+            return sh_fail(SH_ERR_INVALID, "host output appended twice in one push");
+        if (base != 0) {
+            // (an externalTimeBatch timeout's later run: its [k][n_rows] blocks join the earlier rows)
+            PinnedVec<int64_t> nkeys((size_t)nk * n_rows);
+            PinnedVec<uint64_t> nvals((size_t)na * n_rows);
+            if (nk) HIPCHK(hipMemcpyAsync(nkeys.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+            if (na) HIPCHK(hipMemcpyAsync(nvals.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            auto join = [&](auto& v, const auto& add, int nc) {
+                std::remove_reference_t<decltype(v)> old(v);
+                v.resize((size_t)nc * nb);
+                for (int k = 0; k < nc; k++) {
+                    std::copy(old.begin() + (size_t)k * base, old.begin() + (size_t)(k + 1) * base, v.begin() + (size_t)k * nb);
+                    std::copy(add.begin() + (size_t)k * n_rows, add.begin() + (size_t)(k + 1) * n_rows,
+                              v.begin() + (size_t)k * nb + base);
+                }
+            };
+            join(q->out.keys, nkeys, nk);
+            join(q->out.vals, nvals, na);
+            q->out.nulls.assign((size_t)na * nb, 0);
+        } else {
+            q->out.keys.resize((size_t)nk * n_rows);
+            q->out.vals.resize((size_t)na * n_rows);
+            if (nk) HIPCHK(hipMemcpyAsync(q->out.keys.data(), q->out_keys.p, nk * n_rows * 8, hipMemcpyDeviceToHost, s));
+            if (q->given) {
+                size_t ob = q->order_host.size();
+                q->order_host.resize(ob + n_rows);
+                HIPCHK(hipMemcpyAsync(q->order_host.data() + ob, q->out_order.p, n_rows * 8, hipMemcpyDeviceToHost, s));
+            }
+            if (na) HIPCHK(hipMemcpyAsync(q->out.vals.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
+            q->out.nulls.assign((size_t)na * n_rows, 0);
+            HIPCHK(hipStreamSynchronize(s));
         }
-        if (na) HIPCHK(hipMemcpyAsync(q->out.vals.data(), q->out_vals.p, na * n_rows * 8, hipMemcpyDeviceToHost, s));
-        q->out.nulls.assign((size_t)na * n_rows, 0);
-        HIPCHK(hipStreamSynchronize(s));
     }
     // flush bookkeeping (one flush per non-empty closed segment)
     PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
@@ -1112,6 +1134,167 @@ static int small_async(sh_query* q, bool* done) {
     return SH_OK;
 }
 
+// ---- externalTimeBatch timeout (ExternalTimeBatchWindowProcessor.process :256-305) -----------------
+// lastScheduledTime L is the clock of the window's first event, of every batch crossing and of every
+// timeout, + the timeout. A timeout fires where the clock reaches L: at the start of the first send
+// whose last event reaches L (Scheduler timers run before the send's events). It sends the open batch
+// so far, when it holds events not yet sent (flushToOutputChunk the first time, appendToOutputChunk —
+// the batch again, whole — after that); a crossing sends the batch likewise, and nothing when a
+// timeout already sent all of it. Every emission aggregates the open batch from its first event.
+extern "C" int sh_query_set_ext_timeout(sh_query* q, int64_t ms) {
+    if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_timeout: NULL query");
+    if (q->d.window != SH_WIN_EXT_TIME_BATCH || ms < 0)
+        return sh_fail(SH_ERR_INVALID, "a timeout needs an externalTimeBatch window and >= 0 ms");
+    if (q->seq != 0 || q->n_pend != 0 || q->clock_valid)
+        return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_timeout: set it before the first push");
+    if (ms == 0) { q->xt_timeout = 0; return SH_OK; }
+    if (q->kind != 0 || q->d.partition_col >= 0 || q->given || q->internal_keys)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "externalTimeBatch timeout runs on unpartitioned queries (the partitions' timeouts fire in "
+                       "the Scheduler's HashMap order)");
+    if (!q->d.current_on || (q->d.expired_on && (q->d.n_group_by > 0 || q->ap.n == 0)))
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "externalTimeBatch timeout runs with current-events output (all events: aggregating, no "
+                       "group-by)");
+    q->xt_timeout = ms;
+    // every emission ends in the batch's current events: processInBatchNoGroupBy's one row is CURRENT
+    q->xmode = false;
+    return SH_OK;
+}
+
+namespace {
+struct XtEmit {
+    Segment seg;
+    int64_t clock, window;
+};
+}  // namespace
+
+// The timeout due where the push's clock reaches L: its send's first event (push index), that send's
+// clock, and the push's passing events before it.
+static int xt_probe(sh_query* q, const sh_batch* b, int64_t L, int64_t* f, int64_t* clk, int64_t* pcb) {
+    hipStream_t s = q->ctx->stream;
+    const int64_t N = b->n, ss = b->send_size;
+    RCHK(q->xt_dev.reserve(16, false));
+    RCHK(q->xt_host.reserve(16));
+    auto* d = q->xt_dev.as<unsigned long long>();
+    int64_t* h = q->xt_host.as<int64_t>();
+    HIPCHK(hipMemsetAsync(d, 0xFF, 8, s));
+    launch_xt_first_send(s, b->ts, N, ss, L, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t j = (uint64_t)h[0];
+    if (j == ~0ull) return sh_fail(SH_ERR_INVALID, "externalTimeBatch timeout: no send reaches the scheduled time");
+    *f = ss > 0 ? (int64_t)j * ss : 0;
+    const int64_t last = ss > 0 ? std::min<int64_t>(((int64_t)j + 1) * ss, N) - 1 : N - 1;
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b->cols[c]; }
+    HIPCHK(hipMemsetAsync(d + 1, 0, 8, s));
+    launch_xt_count_pass(s, cs, q->fp, *f, d + 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h + 1, d + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h, b->ts + last, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *clk = h[0];
+    *pcb = h[1];
+    return SH_OK;
+}
+
+// The push's emissions in stream order: timeouts and the crossings (bounds) that have events to send.
+static int xt_plan(sh_query* q, const sh_batch* b, const PushInfo& info, const std::vector<Bound>& bounds,
+                   int64_t clock0, bool cv0, std::vector<XtEmit>& em) {
+    const int64_t T = q->xt_timeout;
+    if (!q->xt_Lvalid && info.total_pass > 0) {
+        // initTiming (:313-334): scheduled from the clock of the window's first event's send
+        q->xt_L = (cv0 ? std::max(clock0, info.first_clk) : info.first_clk) + T;
+        q->xt_Lvalid = true;
+    }
+    const int64_t nnew0 = q->xt_nnew;
+    bool sent = false;
+    int64_t last_pcb = 0, lo = 0, w = q->W_open;
+    auto nnew_at = [&](int64_t pcb) { return (sent ? 0 : nnew0) + pcb - last_pcb; };
+    auto timeouts = [&](int64_t clk) -> int {
+        while (q->xt_Lvalid && clk >= q->xt_L) {
+            int64_t f, cf, pf;
+            RCHK(xt_probe(q, b, q->xt_L, &f, &cf, &pf));
+            if (nnew_at(pf) > 0) em.push_back(XtEmit{Segment{lo, q->n_pend + f}, cf, w});
+            sent = true;
+            last_pcb = pf;
+            q->xt_L = cf + T;
+        }
+        return SH_OK;
+    };
+    for (const Bound& bd : bounds) {
+        RCHK(timeouts(bd.clock));
+        if (nnew_at(bd.pcb) > 0) em.push_back(XtEmit{Segment{lo, bd.idx}, bd.clock, w});
+        sent = true;
+        last_pcb = bd.pcb;
+        lo = bd.idx;
+        w = bd.W;
+        q->xt_L = bd.clock + T;
+    }
+    RCHK(timeouts(cv0 ? std::max(clock0, info.max_tl) : info.max_tl));
+    q->xt_nnew = nnew_at(info.total_pass);
+    return SH_OK;
+}
+
+// Host rows of the push (q->out) as its device output.
+static int xt_upload(sh_query* q) {
+    hipStream_t s = q->ctx->stream;
+    const int64_t n = (int64_t)q->out.ts.size();
+    const int nk = q->kp.n, na = q->ap.n;
+    const int64_t cap = std::max<int64_t>(n, 1);
+    RCHK(q->out_ts.reserve(cap * 8, false));
+    RCHK(q->out_rep.reserve(cap * 8, false));
+    RCHK(q->out_keys.reserve(std::max(1, nk) * cap * 8, false));
+    RCHK(q->out_vals.reserve(std::max(1, na) * cap * 8, false));
+    RCHK(q->out_nulls.reserve(std::max(1, na) * cap, false));
+    RCHK(q->out_expired.reserve(cap, false));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(q->out_ts.p, q->out.ts.data(), n * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(q->out_rep.p, q->out.rep.data(), n * 8, hipMemcpyHostToDevice, s));
+        if (nk) HIPCHK(hipMemcpyAsync(q->out_keys.p, q->out.keys.data(), (size_t)nk * n * 8, hipMemcpyHostToDevice, s));
+        if (na) HIPCHK(hipMemcpyAsync(q->out_vals.p, q->out.vals.data(), (size_t)na * n * 8, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipMemsetAsync(q->out_nulls.p, 0, q->out_nulls.cap, s));
+    HIPCHK(hipMemsetAsync(q->out_expired.p, 0, q->out_expired.cap, s));
+    q->zeroed_nulls = q->out_nulls.p;
+    q->zeroed_expired = q->out_expired.p;
+    HIPCHK(hipStreamSynchronize(s));
+    q->dev_flush_offsets.assign(1, 0);
+    q->dev_flush_clock.clear();
+    for (size_t i = 1; i < q->out.flush_offsets.size(); i++) q->dev_flush_offsets.push_back(q->out.flush_offsets[i]);
+    for (size_t i = 0; i < q->out.flush_clock.size(); i++) q->dev_flush_clock.push_back(q->out.flush_clock[i]);
+    q->dev_out.n_rows = n;
+    q->out.reset();
+    return SH_OK;
+}
+
+// The emissions, in runs of disjoint segments (a timeout's segment overlaps its batch's later ones):
+// one run goes out like any push's closed batches; several collect host rows run by run.
+static int xt_emit(sh_query* q, const std::vector<XtEmit>& em, const sh_batch* b, bool host_out) {
+    if (em.empty()) return SH_OK;
+    std::vector<std::vector<XtEmit>> runs;
+    for (const XtEmit& e : em) {
+        if (runs.empty() || e.seg.lo < runs.back().back().seg.hi) runs.emplace_back();
+        runs.back().push_back(e);
+    }
+    for (size_t i = 0; i < runs.size(); i++) {
+        std::vector<Segment> segs;
+        std::vector<int64_t> clocks, windows;
+        for (const XtEmit& e : runs[i]) {
+            segs.push_back(e.seg);
+            clocks.push_back(e.clock);
+            windows.push_back(e.window);
+        }
+        if (i) q->ms_ready = false;  // (the split of the first run may not reach this run's events)
+        RCHK(run_closed(q, segs, clocks, windows, b, runs.size() == 1 ? host_out : true));
+    }
+    if (runs.size() > 1 && !host_out) RCHK(xt_upload(q));
+    return SH_OK;
+}
+
 static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     *done = false;
     const int64_t N = b->n;
@@ -1402,6 +1585,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         const bool lb_full = !q->given && !q->d.stream_current && q->d.window == SH_WIN_LENGTH_BATCH && info.total_pass > 0 &&
                              open_cnt == q->d.window_param;
         const bool close_all = (q->given && q->given_W_end > W_last) || lb_full;
+        if (q->xt_timeout > 0) {
+            std::vector<XtEmit> em;
+            RCHK(xt_plan(q, b, info, bounds, clock0, cv0, em));
+            RCHK(xt_emit(q, em, b, host_out));
+        }
         if (!bounds.empty() || close_all) {
             std::vector<Segment> segs;
             std::vector<int64_t> clocks, windows;
@@ -1419,7 +1607,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
                 clocks.push_back(lb_full ? q->clock : given_flush_clock(q, wprev));
                 windows.push_back(wprev);
             }
-            if (!q->d.stream_current) RCHK(run_closed(q, segs, clocks, windows, b, host_out));
+            if (!q->d.stream_current && q->xt_timeout == 0) RCHK(run_closed(q, segs, clocks, windows, b, host_out));
             if (close_all) {
                 e_lo = N;
                 pcb_lo = info.total_pass;
@@ -1567,6 +1755,18 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
     }
     q->clock = now;
     q->clock_valid = true;
+    if (q->xt_timeout > 0 && q->xt_Lvalid && now >= q->xt_L) {
+        // an externalTimeBatch timeout: the open batch, if it holds events not yet sent (:256-275)
+        if (q->xt_nnew > 0 && q->n_pend > 0) {
+            std::vector<Segment> segs{Segment{0, q->n_pend}};
+            std::vector<int64_t> clocks{now}, windows{q->W_open};
+            RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+            RCHK(closed_finish(q, host_out));
+        }
+        q->xt_nnew = 0;
+        q->xt_L = now + q->xt_timeout;
+    }
     if (q->d.window == SH_WIN_TIME_BATCH && q->e0_valid) {
         int64_t W = wfun_host(q, now);
         if (q->xmode && W > q->W_open) q->x_closes.emplace_back(W, now);

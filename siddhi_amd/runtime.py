@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 8:
+        if L.sh_abi_version() != 9:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -111,6 +111,8 @@ class GpuQuery:
         try:
             if spec.rate:
                 _check(lib().sh_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])))
+            if spec.timeout:
+                _check(lib().sh_query_set_ext_timeout(self.h, int(spec.timeout)))
             for col, names in (spec.strings or {}).items():
                 self.set_strings(col, names)
         except Exception:

@@ -20,6 +20,7 @@ def case(**kw):
 
 CSE_FLOAT_INT = "symbol string, price float, volume int"
 B = 1_000_000  # base timestamp for transcribed wall-clock sends
+LOGIN = "timestamp long, ip string"
 
 # ---------------------------------------------------------------- lengthBatch (LengthBatchWindowTestCase)
 _six = [["IBM", 700.0, 1], ["WSO2", 60.5, 2], ["IBM", 700.0, 3], ["WSO2", 60.5, 4], ["IBM", 700.0, 5],
@@ -108,6 +109,79 @@ case(name="externalTimeBatch_test05_edge", source=E + ":99-141", schema="cpu int
      sends=[[[B + i, c, t]] for i, (c, t) in enumerate([(15, 0), (15, 10), (15, 20), (85, 10000), (85, 10010),
                                                         (85, 10020), (10000, 100000)])],
      expect=dict(in_count=2, flush_sizes=[1, 1], values=[[15.0, 3], [85.0, 3]]))
+
+# externalTimeBatch(ts, T, start, timeout): the wall-clock tests send at w ms (Thread.sleep between
+# sends), so each send's event timestamp is B + w and the scheduler's timeout timers fire as the
+# clock passes them (ExternalTimeBatchWindowProcessor.process :256-275); a final advance stands for
+# the last sleep
+_sched = [10000, 11000, 12000, 13000, 14000, 15000, 16500, 17000, 18000, 19000, 20100, 20500, 22000, 25000,
+          32000, 33000]
+case(name="externalTimeBatch_scheduler_last_batch", source=E + ":325-392", schema="currentTime long, value int",
+     query=dict(window="externalTimeBatch", param=5000, ts_attr="currentTime", start_time=0, timeout=6000,
+                output="current"),
+     sends=[[[B + 100 * i, t, i + 1]] for i, t in enumerate(_sched)] + [{"advance": B + 1500 + 6000}],
+     expect=dict(flush_count=5, flush_first_col=["value", [1, 6, 11, 14, 15]]))
+
+
+def _login(*ws):
+    """(wall ms, timestamp attribute, ip suffix) sends of the LoginEvents tests."""
+    return [[[B + w, t, "192.10.1." + str(x)]] for w, t, x in ws]
+
+
+_L0 = 1366335800000
+_t4 = [(0, 4341, 3), (0, 4342, 4), (0, 14341, 5), (0, 14345, 6), (0, 24341, 7)]
+case(name="externalTimeBatch_w1_timeout", source=E + ":394-440", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=6000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(w, _L0 + t, x) for w, t, x in _t4]) + [{"advance": B + 1000}],
+     expect=dict(in_count=2, remove_count=0))
+case(name="externalTimeBatch_w2", source=E + ":442-490", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, x) for t, x in [(4341, 3), (4342, 4), (5340, 4), (14341, 5), (14345, 6),
+                                                 (24341, 7)]]),
+     expect=dict(in_count=2, remove_count=0))
+case(name="externalTimeBatch_w3", source=E + ":492-540", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, x) for t, x in [(4341, 3), (4342, 4), (5341, 4), (14341, 5), (14345, 6),
+                                                 (24341, 7)]]),
+     expect=dict(in_count=3, remove_count=0))
+case(name="externalTimeBatch_w4_timeout", source=E + ":542-591", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=6000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, x) for t, x in [(4341, 3), (4999, 4), (5000, 4), (5999, 5), (6000, 6),
+                                                 (6001, 6), (24341, 7)]]) + [{"advance": B + 1000}],
+     expect=dict(in_count=3, remove_count=0))
+_w5 = [(4341, 3), (4599, 4), (4600, 5), (4607, 6)]
+_w6 = _w5 + [(5599, 4), (5600, 5), (5607, 6)]
+case(name="externalTimeBatch_w5_timeout", source=E + ":593-640", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=3000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, x) for t, x in _w5]) + [{"advance": B + 5000}],
+     expect=dict(in_count=1, remove_count=0))
+case(name="externalTimeBatch_w6_timeout", source=E + ":642-691", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=3000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, x) for t, x in _w6]) + [{"advance": B + 5000}],
+     expect=dict(in_count=2, remove_count=0))
+case(name="externalTimeBatch_w7_timeout_resend", source=E + ":693-747", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=2000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*([(0, _L0 + t, x) for t, x in _w6] + [(3000, _L0 + 5606, 7), (3000, _L0 + 5605, 8),
+                                                          (6000, _L0 + 6606, 9), (6000, _L0 + 6690, 10)]))
+     + [{"advance": B + 9000}],
+     expect=dict(in_count=4, remove_count=0))
+_w8 = ([(0, _L0 + t, x) for t, x in _w6] + [(2100, _L0 + 5606, 7), (2100, _L0 + 5605, 8), (4200, _L0 + 5606, 91),
+                                           (4200, _L0 + 5605, 92), (4200, _L0 + 6606, 9), (4200, _L0 + 6690, 10)])
+case(name="externalTimeBatch_w8_timeout_counts", source=E + ":749-815", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=2000,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*_w8) + [{"advance": B + 7200}],
+     expect=dict(in_count=5, remove_count=0, values=[[4], [3], [5], [7], [2]]))
+case(name="externalTimeBatch_w10_timeout_current", source=E + ":884-950", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=2000,
+                aggs=[["count", None]], output="current"),
+     sends=_login(*_w8) + [{"advance": B + 7200}],
+     expect=dict(in_count=5, remove_count=0, values=[[4], [3], [5], [7], [2]]))
 
 # ---------------------------------------------------------------- externalTime (ExternalTimeWindowTestCase)
 # sliding over the `timestamp` attribute: 804341/804342 expire at 814341, 814341/814345 at 824341
@@ -396,7 +470,6 @@ case(name="filter30_bool", source=F + ":1036-1064", schema="symbol string, price
 # `output [all|first|last] every N events` over the selector's rows (OutputParser.java:288-303). The
 # Java tests send one event per InputHandler.send (each send is one chunk for the limiter).
 R = "ctest/query/ratelimit/EventOutputRateLimitTestCase.java"
-LOGIN = "timestamp long, ip string"
 
 
 def _ips(*ips):

@@ -57,7 +57,7 @@ def build(case, dic):
                          aggs=[tuple(x) for x in q.get("aggs", [])], filter=_conv_filter(q.get("filter"), dic),
                          start_time=q.get("start_time"), stream_current=q.get("stream_current", False),
                          output=q.get("output", "current"), partition=q.get("partition"),
-                         ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"),
+                         ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"), timeout=q.get("timeout"),
                          rate=tuple(q["rate"]) if q.get("rate") else None)
     return schema, spec
 

@@ -180,3 +180,104 @@ def test_partitioned_external_time_group_by_other(output):
     sp = abi.QuerySpec(PSCH, "externalTime", 400, group_by=["k"], ts_attr="et", partition="p", key_capacity=128,
                        output=output, aggs=[("count", None), ("sum", "v"), ("avg", "et"), ("min", "v"), ("max", "et")])
     both(sp, split_batches(PSCH, ts, cols, [1, 12_000, 30_000], 3), f"pxt group {output}")
+
+
+# ---- externalTimeBatch(et, T, start, timeout): the scheduler timeout sends the open batch so far
+# (ExternalTimeBatchWindowProcessor.process :256-305, appendToOutputChunk :385-438) --------------------
+def tstream(n, seed, pause_p=1 / 3000, per_ms=20, keys=50, late_ms=0):
+    """arrival clock `ts` mostly 0-2 ms apart with rare pauses of 2-9 s (each fires a 1.5 s timeout:
+    several per batch, some just before a crossing); event time `et` 1 ms per `per_ms` events."""
+    ts0, cols = stream(n, keys, seed, late_ms=late_ms, per_ms=per_ms)
+    rng = np.random.default_rng(seed + 11)
+    gaps = rng.integers(0, 3, n) + (rng.random(n) < pause_p) * rng.integers(2_000, 9_000, n)
+    ts = 1_000_000 + np.cumsum(gaps).astype(np.int64)
+    cols[4] = ts.copy()
+    return ts, cols
+
+
+def tspec(output="current", group=True, aggs=None, filt=None, timeout=1500, T=1000, start=0):
+    sp = spec(T=T, start=start, filt=filt, keys=64, output=output, group=group,
+              aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "et"), ("avg", "v")] if aggs is None else aggs)
+    sp.timeout = timeout
+    return sp
+
+
+def with_advances(pushes, ts, every=2):
+    """advance_time between some pushes: past the next timeout (+4 s) or barely (+1 ms)"""
+    out, clock = [], None
+    for i, p in enumerate(pushes):
+        out.append(p)
+        clock = int(p.ts[-1]) if clock is None else max(clock, int(p.ts[-1]))
+        if i % every == 0:
+            clock += 4_000 if i % 4 == 0 else 1
+            out.append(("advance", clock))
+    return out
+
+
+@pytest.mark.parametrize("send_size", [1, 7, 0])
+def test_ext_timeout_group_by(send_size):
+    ts, cols = tstream(80_000, 0xF1)
+    pushes = split_batches(SCH, ts, cols, [1, 9_000, 9_001, 30_000, 52_345, 60_000], send_size)
+    got = both(tspec(), with_advances(pushes, ts), f"ext timeout {send_size}")
+    assert got["flush_offsets"].size > (5 if send_size == 0 else 20)
+
+
+@pytest.mark.parametrize("output,group,aggs", [("all", False, None), ("current", False, [("count", None), ("avg", "v")]),
+                                               ("current", None, [])])
+def test_ext_timeout_no_group_by(output, group, aggs):
+    """all events without group-by: every emission ends in the batch's current events, so each flush is
+    one CURRENT row; `select *` (group None) re-sends a timed-out batch's events at its next emission"""
+    ts, cols = tstream(40_000, 0xF2, late_ms=300)
+    got = both(tspec(output=output, group=bool(group), aggs=aggs),
+               with_advances(split_batches(SCH, ts, cols, [10_000, 20_000, 30_000], 3), ts), f"ext timeout {output}")
+    assert got["expired"].sum() == 0
+
+
+def test_ext_timeout_filter_late_and_attribute_start():
+    ts, cols = tstream(60_000, 0xF3, late_ms=2_000, pause_p=1 / 1500)
+    sp = tspec(filt=(">", "v", 30.0), timeout=800, T=2500, start=None)
+    sp.start_attr = "st"
+    both(sp, with_advances(split_batches(SCH, ts, cols, [20_000, 40_000], 5), ts, every=1), "ext timeout filter")
+
+
+def test_ext_timeout_fires_then_crossing_sends_nothing():
+    """a timeout sends the whole batch; the event that then crosses into the next batch finds nothing
+    new (appendToOutputChunk with an empty current chunk emits nothing) — across an advance_time"""
+    n = 40
+    ts = 1_000_000 + np.arange(n, dtype=np.int64)
+    et = 5_000 + np.arange(n, dtype=np.int64) * 10  # 100 events per 1 s batch: batch 0 = events 0..39
+    et[20:] += 1_000                                  # event 20 crosses into the next batch
+    cols = [np.zeros(n, np.int32), np.arange(n, dtype=np.float64), et, np.full(n, 4_321, np.int64), ts.copy()]
+    pushes = [abi.HostBatch(SCH, ts[:20], [c[:20] for c in cols], 1), ("advance", int(ts[19]) + 2_000),
+              abi.HostBatch(SCH, ts[20:] + 2_000, [c[20:] for c in cols], 1), ("advance", int(ts[-1]) + 9_000)]
+    pushes[2].cols[4][:] = pushes[2].ts
+    from siddhi_amd import runtime
+    sp = tspec(group=False, aggs=[("count", None)])
+    g, o = runtime.GpuQuery(sp), OracleQuery(sp)
+    got, ref = run_pushes(g, pushes), run_pushes(o, pushes)
+    g.close()
+    o.close()
+    assert_same(got, ref, label="ext timeout then crossing")
+    assert got["vals"][0].tolist() == [20, 20]
+    assert got["flush_clock"].tolist() == [int(ts[19]) + 2_000, int(ts[-1]) + 9_000]
+
+
+def test_ext_timeout_checkpoint():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = tstream(50_000, 0xF4)
+    pushes = with_advances(split_batches(SCH, ts, cols, [12_000, 25_000, 37_000], 1), ts)
+    for cut in (2, 5):
+        got, ref, _ = checkpointed(tspec(), pushes, cut)
+        assert_same(got, ref, label=f"ext timeout ckpt {cut}")
+
+
+@pytest.mark.parametrize("kw", [dict(output="all"), dict(output="expired")])
+def test_ext_timeout_refused_with_expired_rows(kw):
+    from siddhi_amd import runtime
+    with pytest.raises(runtime.SiddhiError, match="timeout"):
+        runtime.GpuQuery(tspec(**kw))
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
+                       aggs=[("count", None)])
+    sp.timeout = 1000
+    with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
+        runtime.GpuQuery(sp)
