@@ -297,13 +297,18 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         push(i)
     torch.cuda.synchronize()
     timing = True
+    # an aggregation's device time is summed by the library from per-push HIP events, read after the
+    # loop (its per-push stats would wait for every push)
+    agg_timed = agg is not None and not sliced
+    if agg_timed:
+        q.timing(reset=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     kern_ms, t0 = 0.0, time.perf_counter()
     for i in range(args.warmup, nb):
         push(i)
-        if not sliced:
+        if not sliced and not agg_timed:
             st = q.stats()
             # C5's work is the scans over every event (R12 leaves one partition to aggregate); C4's the
             # root window and every roll-up level
@@ -314,6 +319,9 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if agg_timed:
+        kern_ms, n_timed = q.timing()
+        assert n_timed == args.steps, (n_timed, args.steps)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

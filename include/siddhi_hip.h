@@ -334,7 +334,12 @@ int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_t len);
  * event its send's global clock and PM (max ts over the stream's passing events up to it, the expiry
  * key) — both travel in the record — and the owner replays its keys' windows; it emits one flush per
  * global send, so merge owner flushes by send number ((order - push's first index) / send_size) and
- * rows by `order`. Sliding records carry 2 extra words: at most 6 stream columns.              */
+ * rows by `order`. Sliding records carry 2 extra words: at most 6 stream columns.
+ * `insert expired events` / `insert all events` of the batch windows: an owner's flush closing global
+ * window W holds the expired rows of its keys of W-1 and the current rows of W; a row's `order` is
+ * the first occurrence of its key in W-1 where it takes an expired row's place (LinkedHashMap.put,
+ * QuerySelector.processInBatchGroupBy :315-374), else in W — so merge owner flushes by (clock,
+ * sh_shard_flush_windows) and rows by `order`.                                                  */
 typedef struct {
     int64_t n;           /* events in the slice                                              */
     int64_t n_pass;      /* events passing the filter                                        */
@@ -374,6 +379,9 @@ int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t* recv_byte
                      int64_t n_all_bounds, int32_t host_out, const sh_out** out, const int64_t** order);
 /* TIMER path of the sharded query: every rank calls it with the same `now`. */
 int sh_shard_advance_time(sh_shard* s, int64_t now, int32_t host_out, const sh_out** out, const int64_t** order);
+/* The window each flush of the last consume / advance closes (host array of *n entries, valid until the
+ * next call; n = 0 for sliding windows): the G owners' flushes of one global flush share (clock, window). */
+int sh_shard_flush_windows(sh_shard* s, const int64_t** windows, int64_t* n);
 /* Checkpoint of one rank's shard (SnapshotService.persist/restore, SnapshotService.java:90-296): the
  * global stream state every rank keeps (clock, nextEmitTime, batch count, stream index, p0) and its
  * owner query's windows. Taken between pushes on every rank; restored into a shard created from the
@@ -422,6 +430,10 @@ int sh_shard_stats(sh_shard* s, sh_stats* out);
  * (IncrementalExecutor chain, core/aggregation/IncrementalExecutor.java:110-258), main_kernel_ms the
  * root's base aggregation. */
 int sh_aggregation_stats(sh_aggregation* a, sh_stats* out);
+/* HIP-event device time of the whole pipeline summed over every push since the last reset, read
+ * without a wait per push (sh_aggregation_stats waits for the last push): pushes still running are
+ * waited for by this call. reset != 0 zeroes the sum after reading it. */
+int sh_aggregation_timing(sh_aggregation* a, double* total_ms, int64_t* pushes, int32_t reset);
 
 const char* sh_last_error(void);
 int32_t sh_abi_version(void);

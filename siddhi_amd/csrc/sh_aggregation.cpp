@@ -171,6 +171,12 @@ struct sh_aggregation {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int64_t last_events = 0;
     bool timed = false;
+    // every push's device time, summed without a wait per push (sh_aggregation_timing): a ring of
+    // event pairs, each read once its push has completed (at the latest when the ring wraps)
+    static constexpr int kRing = 64;
+    hipEvent_t r0[kRing] = {}, r1[kRing] = {};
+    int64_t r_next = 0, r_done = 0, r_pushes = 0;
+    double r_ms = 0;
     // band keys for the root (KeyTable::lk): (bucket, dictionary id) slots by arithmetic while the live
     // buckets fit `band_rows` consecutive buckets; the open-addressing table otherwise
     bool band_ok = false;
@@ -551,6 +557,10 @@ static void agg_free(sh_aggregation* a) {
     if (a->h_minmax) (void)hipHostFree(a->h_minmax);
     if (a->ev0) (void)hipEventDestroy(a->ev0);
     if (a->ev1) (void)hipEventDestroy(a->ev1);
+    for (int i = 0; i < sh_aggregation::kRing; i++) {
+        if (a->r0[i]) (void)hipEventDestroy(a->r0[i]);
+        if (a->r1[i]) (void)hipEventDestroy(a->r1[i]);
+    }
     delete a;
 }
 
@@ -620,6 +630,20 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
     return query_reserve_keys(a->root, bound);
 }
 
+// the oldest timed pushes' device time into the sum, down to `keep` still outstanding
+static int ring_collect(sh_aggregation* a, int64_t keep) {
+    while (a->r_next - a->r_done > keep) {
+        const int k = (int)(a->r_done % sh_aggregation::kRing);
+        HIPCHK(hipEventSynchronize(a->r1[k]));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, a->r0[k], a->r1[k]));
+        a->r_ms += ms;
+        a->r_pushes++;
+        a->r_done++;
+    }
+    return SH_OK;
+}
+
 static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     const sh_out* o = nullptr;
     sh_batch dev;
@@ -628,13 +652,40 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     } else {
         dev = *b;
     }
+    RCHK(ring_collect(a, sh_aggregation::kRing - 1));
+    const int rk = (int)(a->r_next % sh_aggregation::kRing);
+    if (!a->r0[rk]) {
+        HIPCHK(hipEventCreate(&a->r0[rk]));
+        HIPCHK(hipEventCreate(&a->r1[rk]));
+    }
     HIPCHK(hipEventRecord(a->ev0, a->ctx->stream));
+    HIPCHK(hipEventRecord(a->r0[rk], a->ctx->stream));
+    SH_TMARK(0);
     RCHK(agg_reserve_root(a, &dev));
+    SH_TMARK(7);  // (the root's push marks 0..6 follow)
     RCHK(sh_push_device(a->root, &dev, &o));
     RCHK(agg_after_root(a, o));
+    SH_TMARK(8);
     HIPCHK(hipEventRecord(a->ev1, a->ctx->stream));
+    HIPCHK(hipEventRecord(a->r1[rk], a->ctx->stream));
+    a->r_next++;
     a->last_events = dev.n;
     a->timed = true;
+    return SH_OK;
+}
+
+// Device time summed over every push since the last reset, without a wait per push: the pushes still
+// running are waited for here. reset != 0 zeroes the sum after reading it.
+extern "C" int sh_aggregation_timing(sh_aggregation* a, double* total_ms, int64_t* pushes, int32_t reset) {
+    StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
+    if (!a || !total_ms || !pushes) return sh_fail(SH_ERR_INVALID, "sh_aggregation_timing: NULL argument");
+    RCHK(ring_collect(a, 0));
+    *total_ms = a->r_ms;
+    *pushes = a->r_pushes;
+    if (reset) {
+        a->r_ms = 0;
+        a->r_pushes = 0;
+    }
     return SH_OK;
 }
 

@@ -53,7 +53,10 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
     // out with flush j + 1 (ExternalTimeBatchWindowProcessor.flushToOutputChunk :336-383), stamped
     // with the attribute time that closed it (its running max, x_stamps) instead of the clock
     const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
-    const bool lb = q->d.window == SH_WIN_LENGTH_BATCH || ext;
+    // (a sharded owner's lengthBatch windows are global batches: they close at the global window
+    // starts, like timeBatch windows; its rows carry their global order)
+    const bool lb = (q->d.window == SH_WIN_LENGTH_BATCH && !q->given) || ext;
+    const bool ord = q->given;
     const int m = (int)q->dev_flush_clock.size();
     const int64_t nr = q->dev_flush_offsets.back();
     const int64_t nc = q->xc_valid ? q->xc_n : 0;
@@ -95,6 +98,7 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
     }
     const bool merge_ok = !(nk == 0 && na == 0);  // pass-through rows are never merged
     std::vector<XItem> items;
+    std::vector<int64_t> item_w;
     int64_t tab_total = 0;
     for (auto& kv : plan) {
         const It& it = kv.second;
@@ -112,6 +116,7 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
             tab_total += ts;
         }
         items.push_back(x);
+        item_w.push_back(kv.first);
     }
     const int ni = (int)items.size();
     // the source array: [carried rows] + [this call's current rows]
@@ -122,10 +127,13 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         RCHK(q->xs_keys.reserve((size_t)NK * S * 8, false));
         RCHK(q->xs_vals.reserve((size_t)NA * S * 8, false));
         RCHK(q->xs_nulls.reserve((size_t)NA * S, false));
+        if (ord) RCHK(q->xs_order.reserve(S * 8, false));
         if (nc) {
             RCHK(copy_cols(s, q->xs_keys.p, S, q->xc_keys.p, nc, nc, nk, 8));
             RCHK(copy_cols(s, q->xs_rep.p, S, q->xc_rep.p, nc, nc, 1, 8));
+            if (ord) RCHK(copy_cols(s, q->xs_order.p, S, q->xc_order.p, nc, nc, 1, 8));
         }
+        if (nr && ord) RCHK(copy_cols(s, q->xs_order.as<int64_t>() + nc, S, q->out_order.p, nr, nr, 1, 8));
         if (nr) {
             RCHK(copy_cols(s, q->xs_ts.as<int64_t>() + nc, S, q->out_ts.p, nr, nr, 1, 8));
             RCHK(copy_cols(s, q->xs_rep.as<int64_t>() + nc, S, q->out_rep.p, nr, nr, 1, 8));
@@ -209,8 +217,10 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         RCHK(q->x_nulls.reserve((size_t)NA * TC, false));
         uint32_t count_mask = 0;
         for (int a = 0; a < na; a++) if (q->ap.kind[a] == AK_COUNT) count_mask |= 1u << a;
+        if (ord) RCHK(q->x_order.reserve(TC * 8, false));
         XOut xo{q->x_ts.as<int64_t>(), q->x_expired.as<unsigned char>(), q->x_keys.as<int64_t>(), q->x_vals.as<u64>(),
-                q->x_nulls.as<unsigned char>(), q->x_rep.as<int64_t>()};
+                q->x_nulls.as<unsigned char>(), q->x_rep.as<int64_t>(), ord ? q->x_order.as<int64_t>() : nullptr,
+                ord ? q->xs_order.as<int64_t>() : nullptr};
         launch_x_scatter(s, d_items, d_cum_o, ni, cum_o[ni], q->xs_ts.as<int64_t>(), q->xs_keys.as<int64_t>(),
                          q->xs_vals.as<u64>(), q->xs_nulls.as<unsigned char>(), q->xs_rep.as<int64_t>(), S, nk, na,
                          count_mask, q->x_match.as<int>(), q->x_keep.as<uint32_t>(), q->x_rank.as<uint32_t>(), T, xo);
@@ -228,17 +238,24 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         RCHK(copy_cols(s, q->xc_rep2.p, ps.n, q->xs_rep.as<int64_t>() + ps.lo, S, ps.n, 1, 8));
         std::swap(q->xc_keys, q->xc_keys2);
         std::swap(q->xc_rep, q->xc_rep2);
+        if (ord) {
+            RCHK(q->xc_order2.reserve((size_t)std::max<int64_t>(ps.n, 1) * 8, false));
+            RCHK(copy_cols(s, q->xc_order2.p, ps.n, q->xs_order.as<int64_t>() + ps.lo, S, ps.n, 1, 8));
+            std::swap(q->xc_order, q->xc_order2);
+        }
         q->xc_valid = true;
         q->xc_n = ps.n;
         q->xc_W = ps.W;
     }
-    // output flushes
+    // output flushes, and the window each closes (a sharded merge matches the owners' flushes by it)
     std::vector<int64_t> fo(1, 0), fc;
+    q->flush_window.clear();
     for (int i = 0; i < ni; i++) {
         const int64_t next = i + 1 < ni ? items[i + 1].out_base : T;
         if (next == items[i].out_base) continue;
         fo.push_back(next);
         fc.push_back(items[i].clock);
+        q->flush_window.push_back(item_w[i]);
     }
     if (host_out) {
         OutHost& o = q->out;
@@ -251,6 +268,10 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         o.keys.resize((size_t)nk * T);
         o.vals.resize((size_t)na * T);
         o.nulls.resize((size_t)na * T);
+        if (ord) {
+            q->order_host.resize(T);
+            if (T > 0) HIPCHK(hipMemcpyAsync(q->order_host.data(), q->x_order.p, T * 8, hipMemcpyDeviceToHost, s));
+        }
         if (T > 0) {
             HIPCHK(hipMemcpyAsync(o.ts.data(), q->x_ts.p, T * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(o.expired.data(), q->x_expired.p, T, hipMemcpyDeviceToHost, s));

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_x_scatter(const XItem* items, const 
         const i64 r = it.p_lo + k;
         const i64 o = it.out_base + k;
         const int m = it.tab_size > 0 ? match[r] : -1;
+        if (out.order) out.order[o] = out.s_order[r];  // (a merged current row takes this place)
         if (m >= 0) {
             x_copy_current(m, o, S, T, nk, na, s_ts, s_keys, s_vals, s_nulls, s_rep, out);
             return;
@@ -147,6 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_x_scatter(const XItem* items, const 
     const i64 r = it.c_lo + (k - it.p_n);
     if (!keep[r]) return;
     const i64 o = it.out_base + it.p_n + (i64)(rank[r] - rank[it.c_lo]);
+    if (out.order) out.order[o] = out.s_order[r];
     x_copy_current(r, o, S, T, nk, na, s_ts, s_keys, s_vals, s_nulls, s_rep, out);
 }
 

@@ -361,6 +361,8 @@ struct XOut {
     u64* vals;
     unsigned char* nulls;
     i64* rep;
+    i64* order;            // sharded owner: the rows' global order (else null)
+    const i64* s_order;    // ... and the source rows' order
 };
 void launch_x_merge(hipStream_t s, const XItem* items, const i64* cum_c, const i64* cum_p, int n_items, i64 tot_c,
                     i64 tot_p, const i64* s_keys, i64 S, int nk, u32* trow, u64* tkey, int* match, u32* keep,

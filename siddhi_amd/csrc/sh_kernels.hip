@@ -1570,6 +1570,29 @@ __global__ __launch_bounds__(kBlock) void k_col_blocks(i64* bsum, int nb, int P,
     }
 }
 
+// Many partitions over few block rows (C4's band-keyed roots: 16k partitions, ~64 rows): a thread per
+// partition walks its column (coalesced across the partitions; the rows are loaded 8 at a time) and
+// the partitions' totals are scanned by k_scan_sum — k_col_blocks' one workgroup per partition plus
+// its last workgroup's P / kBlock serial block scans cost ~95 us there.
+__global__ __launch_bounds__(kBlock) void k_col_walk(i64* __restrict__ bsum, int nb, int P, i64* __restrict__ total,
+                                                    i64* __restrict__ base) {
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= P) return;
+    i64 run = 0;
+    for (int b0 = 0; b0 < nb; b0 += 8) {
+        i64 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = b0 + k < nb ? bsum[(i64)(b0 + k) * P + p] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (b0 + k < nb) bsum[(i64)(b0 + k) * P + p] = run;
+            run += x[k];
+        }
+    }
+    total[p] = run;
+    base[p] = run;  // (exclusive-scanned in place next)
+}
+
 __global__ __launch_bounds__(kBlock) void k_col_apply(u32* c, int nblk, int P, const i64* __restrict__ bpre,
                                                      const i64* __restrict__ base, const i64* __restrict__ total) {
     const int b = blockIdx.y;
@@ -1599,7 +1622,12 @@ void launch_ms_offsets(hipStream_t s, u32* counts, int nblk, int P, i64* tmp) {
     const dim3 g((P + kBlock - 1) / kBlock, nb);
     // (nblk == 0: the reduce pass still runs — zero block sums over no tiles — and zeroes the ticket)
     hipLaunchKernelGGL(k_col_reduce, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, ticket);
-    hipLaunchKernelGGL(k_col_blocks, dim3(P), dim3(kBlock), 0, s, bsum, nb, P, total, base, ticket);
+    if (P >= 2048 && nb <= 256) {
+        hipLaunchKernelGGL(k_col_walk, dim3((P + kBlock - 1) / kBlock), dim3(kBlock), 0, s, bsum, nb, P, total, base);
+        launch_scan_sum(s, base, P);
+    } else {
+        hipLaunchKernelGGL(k_col_blocks, dim3(P), dim3(kBlock), 0, s, bsum, nb, P, total, base, ticket);
+    }
     if (nblk > 0) hipLaunchKernelGGL(k_col_apply, g, dim3(kBlock), 0, s, counts, nblk, P, bsum, base, total);
     else hipLaunchKernelGGL(k_col_apply, dim3((P + kBlock - 1) / kBlock, 1), dim3(kBlock), 0, s, counts, nblk, P, bsum,
                             base, total);

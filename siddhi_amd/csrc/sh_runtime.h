@@ -358,6 +358,9 @@ struct sh_query {
     DevBuf xc_keys, xc_rep, xc_keys2, xc_rep2;                   // carried rows
     DevBuf xs_ts, xs_keys, xs_vals, xs_nulls, xs_rep;            // source rows of a call
     DevBuf x_ts, x_keys, x_vals, x_nulls, x_expired, x_rep;      // output rows
+    // sharded owner (given): the rows' global order (a row at an expired row's place keeps its order:
+    // the previous batch's first occurrence), carried with the last flushed batch
+    DevBuf xc_order, xc_order2, xs_order, x_order;
     DevBuf x_items, x_keep, x_rank, x_match, x_tmp, x_matched, x_trow, x_tkey, pass_pos;
     PinnedBuf x_h;
     std::vector<std::pair<int64_t, int64_t>> x_closes;  // (window start W, clock) seen by the call

@@ -110,8 +110,9 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
     if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "sharded stream.current.event windows are not on the GPU");
-    if (d->expired_on || !d->current_on || d->n_aggs < 1)
-        return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries emit current events of aggregations (`insert into`)");
+    if (d->n_aggs < 1) return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries run aggregations");
+    if (d->window == SH_WIN_TIME && (d->expired_on || !d->current_on))
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows emit current events (`insert into`)");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
     sh_shard* s = new sh_shard();
     s->ctx = ctx;
@@ -537,7 +538,17 @@ static void sync_owner(sh_shard* s) {
 static void set_order(sh_shard* s, bool host_out, const int64_t** order) {
     if (!order) return;
     sh_query* q = s->owner;
-    *order = host_out ? q->order_host.data() : q->out_order.as<int64_t>();
+    *order = host_out ? q->order_host.data() : q->xmode ? q->x_order.as<int64_t>() : q->out_order.as<int64_t>();
+}
+
+// The window every flush of the last consume / advance closes (batch windows; none for sliding ones):
+// the owners' flushes of one global flush carry the same (clock, window), whatever rows they hold.
+extern "C" int sh_shard_flush_windows(sh_shard* s, const int64_t** windows, int64_t* n) {
+    if (!s || !windows || !n) return sh_fail(SH_ERR_INVALID, "sh_shard_flush_windows: NULL argument");
+    sh_query* q = s->owner;
+    *n = s->sliding ? 0 : (int64_t)q->flush_window.size();
+    *windows = q->flush_window.data();
+    return SH_OK;
 }
 
 // Phase 3 of a sliding query: unpack, then the owner's per-key replay with the records' global clock,

@@ -161,6 +161,7 @@ int batch_snapshot(sh_query* q, Writer& w) {
         w.val<int64_t>(q->xc_W);
         RCHK(w.dev(q->xc_keys.p, (size_t)q->kp.n * xn * 8, s));
         RCHK(w.dev(q->xc_rep.p, (size_t)xn * 8, s));
+        if (q->given) RCHK(w.dev(q->xc_order.p, (size_t)xn * 8, s));  // (a sharded owner's rows' global order)
     }
     w.val<int64_t>(q->seq);
     // externalTimeBatch timeout: lastScheduledTime and the open batch's events not yet sent
@@ -241,6 +242,7 @@ int batch_restore(sh_query* q, Reader& r) {
         if (!r.ok || q->xc_n < 0) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
         RCHK(r.dev(q->xc_keys, 8, s));
         RCHK(r.dev(q->xc_rep, 8, s));
+        if (q->given) RCHK(r.dev(q->xc_order, 8, s));
     }
     q->seq = r.val<int64_t>();
     if (q->xt_timeout > 0) {

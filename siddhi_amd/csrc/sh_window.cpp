@@ -1358,6 +1358,8 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     return SH_OK;
 }
 
+static void given_closes(sh_query* q);
+
 static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh_out** out) {
     SH_TMARK(0);
     // expired / all-events output: the current rows stay on the device for xout_finish
@@ -1564,9 +1566,13 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         }
         if (q->xmode) {
             q->x_stamps.clear();
-            for (auto& bd : bounds) {
-                q->x_closes.emplace_back(bd.W, bd.clock);
-                q->x_stamps.push_back(bd.pad);  // (externalTimeBatch: the attribute max at the close)
+            if (q->given) {
+                given_closes(q);
+            } else {
+                for (auto& bd : bounds) {
+                    q->x_closes.emplace_back(bd.W, bd.clock);
+                    q->x_stamps.push_back(bd.pad);  // (externalTimeBatch: the attribute max at the close)
+                }
             }
         }
         if (!q->given) {
@@ -1886,6 +1892,13 @@ int run_multisplit(sh_query* q, int64_t hi, const sh_batch* b, bool counted, boo
 }
 
 // ---- sharded owner (given windows) ------------------------------------------------------------
+// expired / all-events output: the global window starts of the push close the owner's batches (its
+// own events may start none of them)
+static void given_closes(sh_query* q) {
+    q->x_closes.clear();
+    for (const sh_bound& b : q->gbounds) q->x_closes.emplace_back(b.W, b.clock);
+}
+
 // Flush clock of window W: the clock of the first global window start above W in this push (the
 // send whose clock fired the timer, Scheduler.sendTimerEvents :171-209).
 int64_t given_flush_clock(const sh_query* q, int64_t W) {
@@ -1899,7 +1912,9 @@ int query_push_given(sh_query* q, const sh_batch* b, bool host_out, const sh_out
 }
 
 // No events reached this owner in the push: close its open window if the global clock moved past it.
-int query_close_given(sh_query* q, bool host_out, const sh_out** out) {
+int query_close_given(sh_query* q, bool host_out_req, const sh_out** out) {
+    const bool host_out = host_out_req && !q->xmode;
+    if (q->xmode) given_closes(q);
     q->out.reset();
     q->order_host.clear();
     q->dev_flush_offsets.assign(1, 0);
@@ -1920,6 +1935,7 @@ int query_close_given(sh_query* q, bool host_out, const sh_out** out) {
         }
         q->W_open = q->given_W_end;
     }
+    if (q->xmode) return xout_finish(q, host_out_req, out);
     finish_out(q, host_out, out);
     return SH_OK;
 }

@@ -258,6 +258,12 @@ class GpuAggregation:
         _check(lib().sh_aggregation_stats(self.h, C.byref(s)))
         return s
 
+    def timing(self, reset: bool = False):
+        """(device ms summed over the pushes since the last reset, pushes) — sh_aggregation_timing."""
+        ms, n = C.c_double(), C.c_int64()
+        _check(lib().sh_aggregation_timing(self.h, C.byref(ms), C.byref(n), int(reset)))
+        return ms.value, n.value
+
     def table_raw(self, duration: int):
         out = C.POINTER(abi.Out)()
         _check(lib().sh_aggregation_table(self.h, duration, C.byref(out)))

@@ -83,13 +83,20 @@ class ShardedQuery:
         order = C.POINTER(C.c_int64)()
         _check(lib().sh_shard_consume(self.h, recv_ptr, rb, barr, len(bd), int(host_out), C.byref(out),
                                       C.byref(order)))
-        return out, order
+        return out, order, self.flush_windows()
 
     def advance_time(self, now: int, host_out: bool = True):
         out = C.POINTER(abi.Out)()
         order = C.POINTER(C.c_int64)()
         _check(lib().sh_shard_advance_time(self.h, now, int(host_out), C.byref(out), C.byref(order)))
-        return out, order
+        return out, order, self.flush_windows()
+
+    def flush_windows(self) -> np.ndarray:
+        """The window each flush of the last consume / advance closes (sh_shard_flush_windows)."""
+        w = C.POINTER(C.c_int64)()
+        n = C.c_int64()
+        _check(lib().sh_shard_flush_windows(self.h, C.byref(w), C.byref(n)))
+        return np.ctypeslib.as_array(w, shape=(n.value,)).copy() if n.value else np.zeros(0, np.int64)
 
     def stats(self) -> abi.Stats:
         st = abi.Stats()
@@ -165,11 +172,13 @@ def canonical_table(t: dict) -> dict:
     return {"keys": keys[:, perm], "vals": vals[:, perm], "nulls": nulls[:, perm]}
 
 
-def host_rows(out, order) -> dict:
-    """Host sh_out + order -> out_arrays dict with an 'order' column."""
+def host_rows(out, order, windows=None) -> dict:
+    """Host sh_out + order (+ the flushes' windows) -> out_arrays dict with an 'order' column."""
     d = abi.out_arrays(out)
     n = int(out.contents.n_rows)
     d["order"] = np.ctypeslib.as_array(order, shape=(n,)).copy() if n else np.zeros(0, np.int64)
+    if windows is not None and len(windows) == len(d["flush_clock"]) and len(windows):
+        d["window"] = np.asarray(windows, np.int64)
     return d
 
 
@@ -191,6 +200,8 @@ def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None,
         a = int(p["flush_offsets"][f])
         if sends is not None:
             return (int(p["flush_clock"][f]), (int(p["order"][a]) - sends[0]) // max(1, sends[1]))
+        if "window" in p:  # the window the owner's flush closes (sh_shard_flush_windows)
+            return (int(p["flush_clock"][f]), int(p["window"][f]))
         w = int(np.searchsorted(starts, int(p["order"][a]), side="right")) if starts.size else 0
         return (int(p["flush_clock"][f]), w)
 
@@ -296,8 +307,8 @@ class LocalShards:
                 s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=False)
                 outs.append(None)
                 continue
-            out, order = s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=True)
-            outs.append(host_rows(out, order))
+            out, order, windows = s.consume(recv.data_ptr(), rbytes, all_bounds, host_out=True)
+            outs.append(host_rows(out, order, windows))
         return outs
 
     def advance_time(self, now: int) -> List[dict]:

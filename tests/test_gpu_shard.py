@@ -217,3 +217,34 @@ def test_sharded_sliding_filter_nonmonotone_ts_dictionary_keys():
     got = run_sharded(sp, 5, pushes, 7, [[0.2, 0.4, 0.6, 0.8], [0.0, 0.5, 0.5, 0.99]])
     ref = run_oracle(sp, pushes, 7)
     assert_same(got, ref, label="sharded sliding nonmono")
+
+
+# ---- `insert expired events` / `insert all events` over G GPUs: an owner's flush closing global window
+# W carries its keys' expired rows of W-1 (order: their first occurrence in W-1) and its current rows
+# of W; the merge matches owner flushes by (clock, window) (sh_shard_flush_windows) ----------------------
+@pytest.mark.parametrize("output,world", [("all", 2), ("expired", 3), ("all", 8)])
+def test_sharded_timebatch_expired_and_all_events(output, world):
+    sp = abi.QuerySpec(SCHEMA, "timeBatch", 1000, group_by=["k"],
+                       aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=3_000,
+                       output=output)
+    pushes = stream_pushes(240_000, [90_000, 1, 149_999], 0xE1, 3_000, 40)
+    # an idle stretch: windows that close empty (their close carries only the expired rows)
+    pushes[2] = (pushes[2][0] + (np.arange(len(pushes[2][0])) >= 70_000) * 4_500, pushes[2][1])
+    pushes[2][1][2] = pushes[2][0].copy()
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.07 * (g + 1) for g in range(world - 1)]]
+    adv = int(pushes[-1][0][-1]) + 5_000
+    got = run_sharded(sp, world, pushes, 1, fr, advance=adv)
+    ref = run_oracle(sp, pushes, 1, advance=adv)
+    assert ref["expired"].sum() > 1_000
+    assert_same(got, ref, label=f"sharded {output} x{world}")
+
+
+@pytest.mark.parametrize("output", ["all", "expired"])
+def test_sharded_lengthbatch_expired_and_all_events(output):
+    sp = abi.QuerySpec(C1_SCHEMA, "lengthBatch", 2_000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
+                       filter=(">", "price", 100), key_capacity=1000, output=output)
+    pushes = c1_pushes(120_000, [50_000, 1000, 69_000])
+    got = run_sharded(sp, 4, pushes, 10, [[0.25, 0.5, 0.75], [0.0, 0.0, 0.5], [0.1, 0.2, 0.3]])
+    ref = run_oracle(sp, pushes, 10)
+    assert ref["expired"].sum() > 100
+    assert_same(got, ref, label=f"sharded lengthBatch {output}")

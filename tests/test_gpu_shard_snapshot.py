@@ -114,3 +114,14 @@ def test_truncated_shard_blob_leaves_shard_unchanged():
         parts.append(merge_owner_outputs(outs, ls.last_bounds, None))
     ls.close()
     assert_same(abi.concat_arrays(parts), run_oracle(sp, pushes, 1), label="shard after failed restores")
+
+
+@pytest.mark.parametrize("window,output", [("timeBatch", "all"), ("lengthBatch", "expired")])
+def test_sharded_expired_output_checkpoint(window, output):
+    """the carried batch (its keys, representative events and global order) survives the checkpoint"""
+    sp = abi.QuerySpec(SCHEMA, window, 1000 if window == "timeBatch" else 1_500, group_by=["k"],
+                       aggs=[("count", None), ("sum", "v")], key_capacity=2_000, output=output)
+    pushes = stream_pushes(120_000, [50_000, 3_333, 66_667], 0xE5, 2_000, 40)
+    adv = int(pushes[-1][0][-1]) + 5000 if window == "timeBatch" else None
+    got = run_sharded_restored(sp, 3, pushes, 1, 1, advance=adv)
+    assert_same(got, run_oracle(sp, pushes, 1, advance=adv), label=f"{window} {output} ckpt")
