@@ -611,16 +611,20 @@ static int band_reserve(sh_aggregation* a, int64_t lo, int64_t hi, int64_t bound
     return query_reserve_keys(q, bound);
 }
 
-int agg_reserve_root(sh_aggregation* a, const sh_batch* dev) {
+int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side) {
     int64_t N = dev->n;
     if (N <= 0) return SH_OK;
     int64_t keys = a->d.n_group_by ? std::max<int64_t>(1, a->d.key_capacity > 0 ? a->d.key_capacity : (1 << 16)) : 1;
     int64_t bound = std::min(N, keys);
     if (a->has_bucket) {
-        hipStream_t s = a->ctx->stream;
+        // side: a caller's device batch (ready when the call is made) is probed on the side stream, so
+        // the wait does not take in the previous push's roll-up kernels still running on the compute
+        // stream, and this push's kernels queue behind them without a gap
+        hipStream_t s = side ? a->ctx->copy_stream : a->ctx->stream;
         launch_minmax_i64(s, (const int64_t*)dev->cols[a->d.ts_col], N, a->minmax.as<int64_t>());
         HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
-        RCHK(agg_sync(a));
+        if (side) HIPCHK(sh_wait_stream(s));
+        else RCHK(agg_sync(a));
         // the key's bucket component: ts / T truncated (sh_device.h key_part)
         const int64_t lo = a->h_minmax[0] / a->T_root, hi = a->h_minmax[1] / a->T_root;
         int64_t nb = hi - lo + 1;
@@ -661,9 +665,10 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     HIPCHK(hipEventRecord(a->ev0, a->ctx->stream));
     HIPCHK(hipEventRecord(a->r0[rk], a->ctx->stream));
     SH_TMARK(0);
-    RCHK(agg_reserve_root(a, &dev));
+    RCHK(agg_reserve_root(a, &dev, !host));
     SH_TMARK(7);  // (the root's push marks 0..6 follow)
     RCHK(sh_push_device(a->root, &dev, &o));
+    RCHK(agg_verify(a));  // (the root's push synchronised the stream: the last push's level checks are in)
     RCHK(agg_after_root(a, o));
     SH_TMARK(8);
     HIPCHK(hipEventRecord(a->ev1, a->ctx->stream));

@@ -460,7 +460,7 @@ int shard_create_root(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, in
                       sh_shard** out, sh_query** owner);
 void shard_attach_aggregation(sh_shard* s, sh_aggregation* a);
 // (sh_aggregation.cpp)
-int agg_reserve_root(sh_aggregation* a, const sh_batch* dev);    // key room before the root's push
+int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side = false);  // key room before the root's push
 int agg_after_root(sh_aggregation* a, const sh_out* root_out);  // root flushes -> roll-up levels
 void agg_release_sharded(sh_aggregation* a);                     // called by sh_shard_destroy
 

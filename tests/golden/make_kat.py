@@ -183,6 +183,16 @@ case(name="externalTimeBatch_w10_timeout_current", source=E + ":884-950", schema
      sends=_login(*_w8) + [{"advance": B + 7200}],
      expect=dict(in_count=5, remove_count=0, values=[[4], [3], [5], [7], [2]]))
 
+# test17: externalTimeBatch(timestamp, 1 sec, 0, 100, false) — the 100 ms timeout sends the last
+# batch during the final sleep; `select timestamp` shows each row's last event (not replaced: % 100 != 0)
+_t17x = [4341, 4342, 5341, 14341, 14345, 24341, 24351, 24441]
+case(name="externalTimeBatch_w17_timeout_not_replaced", source=E + ":1272-1330", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=100,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, 3 + i) for i, t in enumerate(_t17x)]) + [{"advance": B + 1000}],
+     expect=dict(in_count=4, remove_count=0, values=[[2], [1], [2], [3]],
+                 rep_cols=[["timestamp", [_L0 + 4342, _L0 + 5341, _L0 + 14345, _L0 + 24441]]]))
+
 # ---------------------------------------------------------------- externalTime (ExternalTimeWindowTestCase)
 # sliding over the `timestamp` attribute: 804341/804342 expire at 814341, 814341/814345 at 824341
 X = "ctest/query/window/ExternalTimeWindowTestCase.java"
