@@ -1495,6 +1495,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_tiles(T* a, i64 n, const i64* t
 }
 
 void launch_scan_sum_large(hipStream_t s, i64* a, i64 n, i64* tmp) {
+    if (n <= 16384) {  // (one workgroup's loop: one launch instead of three, e.g. a push's tile counts)
+        launch_scan_sum(s, a, (int)n);
+        return;
+    }
     int nb = (int)((n + kTile - 1) / kTile);
     hipLaunchKernelGGL(k_reduce_tiles<i64>, dim3(nb), dim3(kBlock), 0, s, a, n, tmp);
     launch_scan_sum(s, tmp, nb);
