@@ -73,11 +73,27 @@ void launch_sl_prefix(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, W
 // s_records: passing events -> rank-indexed records {raw idx, slot, clock, PM, ts, values} and the
 // per-slot count of new events (for ring sizing).
 // ------------------------------------------------------------------------------------------------
+// The per-slot count through a workgroup table in LDS: the tile's events add to their slot's LDS
+// counter and each distinct slot of the tile makes one global atomic at the end. A Zipf-hot key
+// (partition lanes over 10M Zipf keys: the hottest holds ~10% of the events) otherwise sends millions
+// of same-address atomics into one L2 channel, which serialises them (43 ms per 33.5M-event push).
+constexpr int kSlotTab = 2 * kTile;  // at most kTile distinct slots per tile: never full
+__device__ __forceinline__ void slot_tab_add(u32* tk, u32* tc, u32 pos) {
+    u32 h = (pos * 2654435761u) & (kSlotTab - 1);
+    for (;;) {
+        const u32 old = atomicCAS(&tk[h], 0xFFFFFFFFu, pos);
+        if (old == 0xFFFFFFFFu || old == pos) { atomicAdd(&tc[h], 1u); return; }
+        h = (h + 1) & (kSlotTab - 1);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                       WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
                                                       const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                       const i64* blk_pm_pre, i64 pm0, SlRecords rec, u32* slot_cnt,
                                                       i64* send_clock) {
+    __shared__ u32 tk[kSlotTab], tc[kSlotTab];
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
     i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
     bool pass[kItems];
     i64 cnt = 0, tl = INT64_MIN, pm = INT64_MIN;
@@ -100,9 +116,11 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
-        if (e >= wp.N) break;
-        i64 t = ts[e];
-        if (pass[i]) {
+        const bool in = e < wp.N;
+        const bool valid = in && pass[i];
+        u32 pos = 0;
+        i64 t = in ? ts[e] : 0;
+        if (valid) {
             // externalTime (ExternalTimeWindowProcessor :126-161): an event expires the queue head
             // while headTime + T <= its own attribute, so event j has left the window at event i iff
             // PMa(j) + T <= PMa(i) (PMa = running max of the attribute): clock = PMa(i)
@@ -110,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
             const i64 sclk = max(c0, max(cm, ts[send_last_of(wp, e)]));
             i64 clk = ext ? pmx : sclk;
             if (send_clock) send_clock[r] = sclk;  // the flush clock of an externalTime row
-            u32 pos = key_slot(kt, make_key(kp, cols, e));
+            pos = key_slot(kt, make_key(kp, cols, e));
             rec.raw[r] = (u32)e;
             rec.slot[r] = pos;
             if (rec.aos) {
@@ -124,11 +142,14 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
                 rec.ts[r] = t;
                 for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
             }
-            atomicAdd(&slot_cnt[pos], 1u);
+            slot_tab_add(tk, tc, pos);
             r++;
         }
-        if (is_send_last(wp, e)) cm = max(cm, t);
+        if (in && is_send_last(wp, e)) cm = max(cm, t);
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock)
+        if (tc[i]) atomicAdd(&slot_cnt[tk[i]], tc[i]);
 }
 
 // The common case of k_sl_records — no filter, one event per send, time(T) — with the tile's events
@@ -141,6 +162,8 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
                                                           const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                           const i64* blk_pm_pre, i64 pm0, SlRecords rec,
                                                           u32* slot_cnt, i64* send_clock) {
+    __shared__ u32 tk[kSlotTab], tc[kSlotTab];
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
     const i64 tile0 = (i64)blockIdx.x * kTile;
     const i64 r0 = blk_pass_pre[blockIdx.x];
     i64 carry_cm = blk_tl_pre[blockIdx.x];
@@ -172,11 +195,14 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
                 rec.ts[r] = t;
                 for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
             }
-            atomicAdd(&slot_cnt[pos], 1u);
+            slot_tab_add(tk, tc, pos);
         }
         carry_pm = max(carry_pm, tot);
         carry_cm = max(carry_cm, tot);
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock)
+        if (tc[i]) atomicAdd(&slot_cnt[tk[i]], tc[i]);
 }
 
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
@@ -194,13 +220,10 @@ void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
 // Sharded owner (sh_shard.cpp): the records arrive filtered and re-keyed, with the global clock of
 // their send and the global PM computed by the source slice (sh_shard_kernels.hip k_shard_sl_assign);
 // raw = position in the global push, so send = send_base + raw / send_size as in the single stream.
-__global__ __launch_bounds__(kBlock) void k_sl_records_given(i64 M, const i64* __restrict__ ts, ColSet cols,
-                                                            KeyPlan kp, KeyTable kt, AggPlan ap,
-                                                            const i64* __restrict__ gclk, const i64* __restrict__ gpm,
-                                                            const u64* __restrict__ gidx, i64 raw_base,
-                                                            SlRecords rec, u32* slot_cnt) {
-    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= M) return;
+__device__ __forceinline__ void sl_record_given(i64 r, const i64* __restrict__ ts, ColSet cols, KeyPlan kp, KeyTable kt,
+                                                AggPlan ap, const i64* __restrict__ gclk, const i64* __restrict__ gpm,
+                                                const u64* __restrict__ gidx, i64 raw_base, SlRecords rec, u32* tk,
+                                                u32* tc) {
     const u32 pos = key_slot(kt, make_key(kp, cols, r));
     const u32 raw = (u32)((i64)gidx[r] - raw_base);
     rec.raw[r] = raw;
@@ -216,8 +239,24 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_given(i64 M, const i64* _
         rec.ts[r] = ts[r];
         for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], r);
     }
-    atomicAdd(&slot_cnt[pos], 1u);
+    slot_tab_add(tk, tc, pos);
 }
+
+__global__ __launch_bounds__(kBlock) void k_sl_records_given(i64 M, const i64* __restrict__ ts, ColSet cols,
+                                                            KeyPlan kp, KeyTable kt, AggPlan ap,
+                                                            const i64* __restrict__ gclk, const i64* __restrict__ gpm,
+                                                            const u64* __restrict__ gidx, i64 raw_base,
+                                                            SlRecords rec, u32* slot_cnt) {
+    __shared__ u32 tk[kSlotTab], tc[kSlotTab];
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
+    __syncthreads();
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r < M) sl_record_given(r, ts, cols, kp, kt, ap, gclk, gpm, gidx, raw_base, rec, tk, tc);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSlotTab; i += kBlock)
+        if (tc[i]) atomicAdd(&slot_cnt[tk[i]], tc[i]);
+}
+
 
 void launch_sl_records_given(hipStream_t s, i64 M, const i64* ts, ColSet cols, KeyPlan kp, KeyTable kt, AggPlan ap,
                              const i64* gclk, const i64* gpm, const u64* gidx, i64 raw_base, SlRecords rec,
