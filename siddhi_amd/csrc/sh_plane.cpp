@@ -254,6 +254,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     wp.clock0 = q->clock;
     wp.send_size = ss;
     wp.N = N;
+    wp.rec_seq = q->tune.sl_records_seq;  // (the lane-strided records where they apply, as the sliding path)
     launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                      s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
     launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
@@ -350,12 +351,13 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
         RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
         if (n_e > 0) {
             tb = 0;
-            if (sort_u64_pairs_bits(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_cap,
+            const int64_t ne_sort = q->d.expired_on ? ne_cap : n;  // (current only: one entry per event)
+            if (sort_u64_pairs_bits(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_sort,
                                     ebits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
             RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
             if (sort_u64_pairs_bits(s->sort_tmp.p, &tb, s->pg_ekey.as<u64>(), s->pg_ekey2.as<u64>(), s->pg_eval.as<u32>(),
-                                    s->pg_eval2.as<u32>(), ne_cap, ebits, st))
+                                    s->pg_eval2.as<u32>(), ne_sort, ebits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort failed");
             // ---- segments = rows
             RCHK(s->pg_head.reserve(n_e + 16, false));
@@ -689,6 +691,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
         wp.clock0 = q->clock;
         wp.send_size = ss;
         wp.N = N;
+        wp.rec_seq = q->tune.sl_records_seq;
         launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                          s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
         launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),

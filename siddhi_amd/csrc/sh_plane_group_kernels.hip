@@ -206,10 +206,15 @@ __global__ __launch_bounds__(kBlock) void k_pg_assign_ext(const u32* __restrict_
             }
         }
         if (!exp_on) kx = none;
-        ekey[2 * i] = kx;
-        ekey[2 * i + 1] = kc;
-        eval[2 * i] = (u32)i;
-        eval[2 * i + 1] = (u32)i | 0x80000000u;
+        if (exp_on) {
+            ekey[2 * i] = kx;
+            ekey[2 * i + 1] = kc;
+            eval[2 * i] = (u32)i;
+            eval[2 * i + 1] = (u32)i | 0x80000000u;
+        } else {  // current rows only: one entry per event (the sort takes n entries, not 2n)
+            ekey[i] = kc;
+            eval[i] = (u32)i | 0x80000000u;
+        }
         keep[c] = kp;
         made = (kx != none) + (kc != none);
     }
@@ -291,10 +296,15 @@ __global__ __launch_bounds__(kBlock) void k_pg_assign(const u32* __restrict__ ke
             }
         }
         if (!exp_on) kx = none;
-        ekey[2 * i] = kx;
-        ekey[2 * i + 1] = kc;
-        eval[2 * i] = (u32)i;
-        eval[2 * i + 1] = (u32)i | 0x80000000u;
+        if (exp_on) {
+            ekey[2 * i] = kx;
+            ekey[2 * i + 1] = kc;
+            eval[2 * i] = (u32)i;
+            eval[2 * i + 1] = (u32)i | 0x80000000u;
+        } else {  // current rows only: one entry per event (the sort takes n entries, not 2n)
+            ekey[i] = kc;
+            eval[i] = (u32)i | 0x80000000u;
+        }
         keep[c] = kp;
         made = (kx != none) + (kc != none);
     }
