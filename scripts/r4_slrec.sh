@@ -2,7 +2,7 @@
 # wave-aggregated slot counts: sliding + partition parity, then the lane benches
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -q -x -rf --timeout 300 --timeout-method thread -m gpu tests/test_gpu_partition.py \
+timeout -k 10 900 python -u -m pytest -q -x -rf --timeout 300 --timeout-method thread -m gpu tests/test_gpu_partition.py tests/test_gpu_aggregation.py \
   tests/test_gpu_ext.py tests/test_gpu_sliding_minmax.py tests/test_gpu_parity.py tests/test_gpu_snapshot.py tests/test_gpu_rate.py tests/test_gpu_shard.py tests/test_gpu_shard_snapshot.py tests/test_gpu_scale.py > gpurun_out/r4s_tests.log 2>&1 || { tail -30 gpurun_out/r4s_tests.log; exit 1; }
 tail -2 gpurun_out/r4s_tests.log
 for w in plb plg c3; do

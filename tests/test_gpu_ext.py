@@ -281,3 +281,13 @@ def test_ext_timeout_refused_with_expired_rows(kw):
     sp.timeout = 1000
     with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
         runtime.GpuQuery(sp)
+
+
+@pytest.mark.parametrize("rate", [("all", 3), ("last", 2)])
+def test_ext_timeout_through_rate_limiter(rate):
+    """the timeouts' emissions reach the output rate limiter like any flush (device rows of several
+    runs uploaded as one push's output)"""
+    ts, cols = tstream(40_000, 0xF6)
+    sp = tspec()
+    sp.rate = rate
+    both(sp, with_advances(split_batches(SCH, ts, cols, [10_000, 25_000], 1), ts), f"ext timeout rate {rate}")
