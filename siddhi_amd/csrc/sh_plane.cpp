@@ -334,7 +334,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             launch_pg_ext_state(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
                                 s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, s->nslots);
         } else {
-            launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L,
+            launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->p_slot.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L,
                              q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
                              s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>());
         }

@@ -45,9 +45,9 @@ void launch_pg_assign_ext(hipStream_t s, const u32* key_off, const u32* ranks, c
                           int* err);
 void launch_pg_ext_state(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
                          PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 nslots);
-void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, PgRecs C, i64 n, i64 L,
-                      int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval, unsigned char* keep,
-                      unsigned long long* n_entries);
+void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* p_sorted, const u32* prev_cnt,
+                      PgRecs C, i64 n, i64 L, int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval,
+                      unsigned char* keep, unsigned long long* n_entries);
 void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head);
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
                     const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,

@@ -265,6 +265,7 @@ void launch_pg_ext_state(hipStream_t s, const u32* key_off, const u32* ranks, co
 //   [2i + 1] CURRENT of position i into its own batch's chunk (current output only);
 // value = i | (1 << 31) for CURRENT. keep[c]: 1 = carried as the last completed batch, 2 = open batch.
 __global__ __launch_bounds__(kBlock) void k_pg_assign(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                     const u32* __restrict__ p_sorted,
                                                      const u32* __restrict__ prev_cnt, PgRecs C, i64 n, i64 L,
                                                      int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval,
                                                      unsigned char* keep, unsigned long long* n_entries) {
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_pg_assign(const u32* __restrict__ ke
     int made = 0;
     if (i < n) {
         const u32 c = ranks[i];
-        const u32 p = C.ps[c];
+        const u32 p = p_sorted[i];  // (= C.ps[c]: the sort's keys, read coalesced instead of through c)
         const i64 lo = key_off[p], hi = key_off[p + 1], np = prev_cnt[p];
         const i64 run = hi - lo - np, nfull = run / L;
         const i64 j = i - lo - np;
@@ -312,12 +313,12 @@ __global__ __launch_bounds__(kBlock) void k_pg_assign(const u32* __restrict__ ke
     if (threadIdx.x == 0 && tot) atomicAdd(n_entries, (unsigned long long)tot);
 }
 
-void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, PgRecs C, i64 n, i64 L,
-                      int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval, unsigned char* keep,
-                      unsigned long long* n_entries) {
+void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* p_sorted, const u32* prev_cnt,
+                      PgRecs C, i64 n, i64 L, int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval,
+                      unsigned char* keep, unsigned long long* n_entries) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_pg_assign, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
-                       prev_cnt, C, n, L, cur_on, exp_on, gbits, none, ekey, eval, keep, n_entries);
+                       p_sorted, prev_cnt, C, n, L, cur_on, exp_on, gbits, none, ekey, eval, keep, n_entries);
 }
 
 // segment heads of the sorted entries
