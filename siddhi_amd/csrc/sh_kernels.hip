@@ -2200,6 +2200,37 @@ void launch_small_push(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
     }
 }
 
+// ---- stream.current.event flushes on the device: a flush ends where the row's chunk changes; its
+// clock is its send's playback clock (the running max of the sends' last timestamps, with the clock
+// carried in) or, for a TIMER chunk (osd < 0), its window start's clock ---------------------------------
+__global__ __launch_bounds__(kBlock) void k_sc_flush_flags(i64 T, const i64* __restrict__ och, u32* flag) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i > T) return;
+    flag[i] = i < T && (i + 1 == T || och[i + 1] != och[i]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sc_flushes(i64 T, const i64* __restrict__ osd, const u32* __restrict__ pre,
+                                                      const i64* __restrict__ slp, int cv0, i64 clock0,
+                                                      const i64* __restrict__ bclk, i64* fo1, i64* fc) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= T || pre[i + 1] == pre[i]) return;
+    const u32 k = pre[i];
+    const i64 sd = osd[i];
+    fo1[k] = i + 1;
+    fc[k] = sd >= 0 ? (cv0 ? max(clock0, slp[sd]) : slp[sd]) : bclk[-sd - 1];
+}
+
+void launch_sc_flush_flags(hipStream_t s, i64 T, const i64* och, u32* flag) {
+    hipLaunchKernelGGL(k_sc_flush_flags, dim3((unsigned)((T + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, T, och, flag);
+}
+
+void launch_sc_flushes(hipStream_t s, i64 T, const i64* osd, const u32* pre, const i64* slp, int cv0, i64 clock0,
+                       const i64* bclk, i64* fo1, i64* fc) {
+    if (T <= 0) return;
+    hipLaunchKernelGGL(k_sc_flushes, dim3((unsigned)((T + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, T, osd, pre, slp,
+                       cv0, clock0, bclk, fo1, fc);
+}
+
 // ---- externalTimeBatch timeout: where the push's clock passes lastScheduledTime --------------------
 // First send whose last event's timestamp reaches L (InputHandler.send sets the clock from it, and
 // every earlier send's clock stays below L): out[0] = its index (u64 max: none).

@@ -272,6 +272,8 @@ struct sh_query {
     bool xt_Lvalid = false;
     int64_t xt_L = 0;
     int64_t xt_nnew = 0;
+    // stream.current.event flushes built on the device (sc_rows): send clocks, flags, offsets, clocks
+    DevBuf sc_slp, sc_fflag, sc_fo, sc_fc, sc_bclk;
     DevBuf xt_dev;
     PinnedBuf xt_host;
     int64_t n_pend = 0, pend_cap = 0;

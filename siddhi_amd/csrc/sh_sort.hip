@@ -6,6 +6,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "sh_internal.h"
 
@@ -49,6 +50,11 @@ int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out
     rocprim::counting_iterator<u32> iota(0u);
     hipError_t e = rocprim::radix_sort_pairs(temp, *bytes, keys, keys_out, iota, vals_out, (unsigned)n, 0u, end_bit, s);
     return e == hipSuccess ? 0 : -1;
+}
+
+// inclusive running maximum (the playback clock over the sends' last timestamps)
+int scan_max_i64(void* temp, size_t* bytes, const i64* in, i64* out, i64 n, hipStream_t s) {
+    return rocprim::inclusive_scan(temp, *bytes, in, out, (size_t)n, rocprim::maximum<i64>(), s) != hipSuccess;
 }
 
 }  // namespace shd

@@ -745,14 +745,16 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     // the sends' playback clocks: TimestampGeneratorImpl only moves forward (prefix max of send-last ts)
     launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
     HIPCHK(hipGetLastError());
-    RCHK(q->sc_h.reserve((size_t)n_sends * 8 + 64));
-    HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
+    const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
     // (host scratch kept by the query: a fresh 8-byte-per-send vector per push faulted in its pages —
     // hundreds of MB per C2-sized push)
     std::vector<int64_t>& sl = q->sc_sl_host;
-    sl.resize((size_t)n_sends);
-    {
+    if (xs || xt) {
+        RCHK(q->sc_h.reserve((size_t)n_sends * 8 + 64));
+        HIPCHK(hipMemcpyAsync(q->sc_h.p, q->sc_sl.p, (size_t)n_sends * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        sl.resize((size_t)n_sends);
         const int64_t* hs = q->sc_h.as<int64_t>();
         bool cv = cv0;
         int64_t c = clock0;
@@ -761,9 +763,16 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
             cv = true;
             sl[i] = c;
         }
+    } else {
+        // current rows only: the sends' clocks stay on the device (the flushes are built there too)
+        size_t stb = 0;
+        RCHK(q->sc_slp.reserve((size_t)n_sends * 8, false));
+        if (scan_max_i64(nullptr, &stb, q->sc_sl.as<int64_t>(), q->sc_slp.as<int64_t>(), n_sends, s))
+            return sh_fail(SH_ERR_DEVICE, "stream.current: scan sizing");
+        RCHK(q->sc_sort.reserve(std::max<size_t>(stb, 16), false));
+        if (scan_max_i64(q->sc_sort.p, &stb, q->sc_sl.as<int64_t>(), q->sc_slp.as<int64_t>(), n_sends, s))
+            return sh_fail(SH_ERR_DEVICE, "stream.current: scan failed");
     }
-    const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
-    const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
     const int cur_on = q->d.current_on ? 1 : 0;
     int64_t T = 0;
     if (xs || xt) {
@@ -849,10 +858,41 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                        q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
     }
     HIPCHK(hipGetLastError());
+    PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
+    PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
+    fo.assign(1, 0);
+    fc.clear();
+    if (!(xs || xt)) {
+        // a flush ends where the row's chunk changes: flags, their scan, the offsets and clocks
+        RCHK(q->sc_bclk.reserve((size_t)std::max(nb, 1) * 8, false));
+        RCHK(q->sc_h.reserve((size_t)std::max(nb, 1) * 8 + 64));
+        for (int i = 0; i < nb; i++) q->sc_h.as<int64_t>()[i] = bounds[i].clock;
+        if (nb) HIPCHK(hipMemcpyAsync(q->sc_bclk.p, q->sc_h.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
+        RCHK(q->sc_fflag.reserve((size_t)(T + 1) * 4, false));
+        RCHK(q->sc_tmp.reserve((size_t)((T + 1 + kTile - 1) / kTile + 16) * 8, false));
+        launch_sc_flush_flags(s, T, q->sc_ochunk.as<int64_t>(), q->sc_fflag.as<u32>());
+        launch_scan_sum_large_u32(s, q->sc_fflag.as<u32>(), T + 1, q->sc_tmp.as<int64_t>());
+        RCHK(q->h_small_sc.reserve(64));
+        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->sc_fflag.as<uint32_t>() + T, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int64_t nf = *q->h_small_sc.as<uint32_t>();
+        RCHK(q->sc_fo.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
+        RCHK(q->sc_fc.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
+        launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), q->sc_fflag.as<u32>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0,
+                          clock0, q->sc_bclk.as<int64_t>(), q->sc_fo.as<int64_t>(), q->sc_fc.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        fo.resize((size_t)nf + 1);
+        fc.resize((size_t)nf);
+        if (nf) {
+            HIPCHK(hipMemcpyAsync(fo.data() + 1, q->sc_fo.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(fc.data(), q->sc_fc.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+    }
     // every row's chunk and send
     const int64_t* och = nullptr;
     const int64_t* osd = nullptr;
-    if (T) {
+    if (T && (xs || xt)) {
         RCHK(q->sc_ho.reserve((size_t)2 * T * 8 + 64));
         int64_t* hs = q->sc_ho.as<int64_t>();
         HIPCHK(hipMemcpyAsync(hs, q->sc_ochunk.p, (size_t)T * 8, hipMemcpyDeviceToHost, s));
@@ -861,16 +901,14 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         och = hs;  // read in place from the pinned landing area
         osd = hs + T;
     }
-    PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
-    PinnedVec<int64_t>& fc = host_out ? q->out.flush_clock : q->dev_flush_clock;
-    fo.assign(1, 0);
-    fc.clear();
-    fo.reserve((size_t)T + 1);  // (one pinned allocation, not a doubling series)
-    fc.reserve((size_t)T);
-    for (int64_t i = 0; i < T; i++) {
-        if (i + 1 == T || och[i + 1] != och[i]) {
-            fo.push_back(i + 1);
-            fc.push_back(osd[i] >= 0 ? sl[osd[i]] : bounds[-osd[i] - 1].clock);
+    if (xs || xt) {
+        fo.reserve((size_t)T + 1);  // (one pinned allocation, not a doubling series)
+        fc.reserve((size_t)T);
+        for (int64_t i = 0; i < T; i++) {
+            if (i + 1 == T || och[i + 1] != och[i]) {
+                fo.push_back(i + 1);
+                fc.push_back(osd[i] >= 0 ? sl[osd[i]] : bounds[-osd[i] - 1].clock);
+            }
         }
     }
     float ms = 0;
