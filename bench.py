@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--send-size", type=int, default=1, help="events per InputHandler.send (1 = PER_EVENT)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-fed (PCIe) leg of the default line")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1 slice ingest: exchange and consume each push in turn (no overlap)")
     ap.add_argument("--ingest", choices=["slice", "keyed"], default="slice",
@@ -149,21 +150,25 @@ def measured_traffic(args, sliced):
 
 
 GOLDEN_DIGEST = "tests/golden/c2_bench_digest.json"
+C1_GOLDEN_DIGEST = "tests/golden/c1_bench_digest.json"
 
 
-def output_digest_check(args, arrays):
+def output_digest_check(args, arrays, golden=GOLDEN_DIGEST, c1_batch=None):
     """SHA-256 of the first warm-up push's canonical output (siddhi_amd.digest; computed outside the timed
-    region) against the CPU restatement's digest of the same stream (tests/golden/make_c2_digest.py).
-    Only the default configuration has a golden digest."""
+    region) against the CPU restatement's digest of the same stream (tests/golden/make_c2_digest.py,
+    make_c1_digest.py). Only the default configurations have a golden digest."""
     from siddhi_amd import digest
-    gold = json.load(open(os.path.join(ROOT, GOLDEN_DIGEST)))
+    gold = json.load(open(os.path.join(ROOT, golden)))
     cfg = gold["config"]
-    if (args.batch, args.keys, args.events_per_ms, args.send_size, args.key_type) != (
+    if c1_batch is not None:
+        if c1_batch != cfg["events_per_push"]:
+            return None
+    elif (args.batch, args.keys, args.events_per_ms, args.send_size, args.key_type) != (
             cfg["events_per_push"], cfg["keys"], cfg["events_per_ms"], cfg["send_size"], "string"):
         return None
     got = digest.output_digest(arrays)
     return {"match": got == gold["push0"]["sha256"], "sha256": got, "rows": int(arrays["ts"].size),
-            "expected": gold["push0"]["sha256"], "source": GOLDEN_DIGEST + " (oracle/ on the same stream)"}
+            "expected": gold["push0"]["sha256"], "source": golden + " (oracle/ on the same stream)"}
 
 
 # ---- secondary single-GPU workloads (BASELINE.json configs[0], [2], [3]; externalTimeBatch) ---------
@@ -293,8 +298,12 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
                                     host_out=False, timings=phases if timing else None)
         return q.push_device(B, ts.data_ptr(), [c.data_ptr() for c in cols], send)
 
+    digest_check = None
     for i in range(args.warmup):
-        push(i)
+        op = push(i)
+        if i == 0 and args.workload == "c1" and not sliced:
+            torch.cuda.synchronize()
+            digest_check = output_digest_check(args, runtime.device_out_arrays(op), C1_GOLDEN_DIGEST, B)
     torch.cuda.synchronize()
     timing = True
     # an aggregation's device time is summed by the library from per-push HIP events, read after the
@@ -351,39 +360,43 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
                       "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
                       "vs_baseline": None, "dtype": "f64",
                       "data": "synthetic SplitMix64 stream (SURVEY.md §8d seeds), resident in HBM",
-                      "config": config, "roofline": roof}), flush=True)
+                      "config": config, "roofline": roof,
+                      **({"output_sha256_match": digest_check["match"], "output_check": digest_check}
+                         if digest_check else {})}), flush=True)
     q.close()
 
 
 PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link (MI355X_MICROARCH.md)
+H2D_BYTES_PER_EVENT = 20  # the columns the C2 query reads: ts 8 + k 4 + v 8 (the unread `ts` attribute is NULL)
 
 
-def run_host(args, dev):
+def host_leg(args, dev, B, steps, warmup, ctx=None):
     """C2 from host memory, as the Java shim would drive it: every micro-batch packed into pinned SoA
-    buffers, its H2D copy staged on the copy stream while the previous batch is processed
-    (sh_stage / sh_push_staged), output rows copied back to the host. Reports the PCIe-inclusive event
-    rate, the copy engine's H2D GB/s (HIP events on the copy stream) and the per-call latency."""
-    import statistics
-    import numpy as np
+    buffers (only the columns the query reads: the `ts` attribute column is passed as NULL), its H2D
+    copy staged on the copy stream while the previous batch is processed (sh_stage / sh_push_staged),
+    output rows copied back to the host. Returns the PCIe-inclusive event rate, the copy engine's H2D
+    GB/s (HIP events on the copy stream) and the per-call latency."""
     import torch
     from siddhi_amd import abi, runtime, synth
-    ctx = runtime.Context(dev.index)
+    ctx = ctx or runtime.Context(dev.index)
     schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=args.keys)
-    B, nb = args.batch, args.warmup + args.steps
+    nb = warmup + steps
     q = runtime.GpuQuery(spec, ctx)
-    bufs = []
+    bufs = []  # one pinned batch per call: consecutive slices of one stream
     for i in range(nb):
         ts, cols = synth.torch_keyed_stream(i * B, B, 0xC2, args.keys, args.events_per_ms, dev)
         pb = runtime.PinnedBatch(schema, B, args.send_size)
         for a, t in zip(pb.arrays, [ts] + cols):
             torch.from_numpy(a).copy_(t)  # D2H into the pinned SoA buffers (outside the timed region)
         pb.set_n(B)
+        pb.b.cols[2] = None  # the query does not read the `ts` attribute: 20 B/event cross PCIe
         bufs.append(pb)
     torch.cuda.synchronize()
 
     lat, h2d_ms, h2d_bytes, rows = [], 0.0, 0, 0
+
     def run(lo, hi, timed):
         nonlocal h2d_ms, h2d_bytes, rows
         tickets = [q.stage(bufs[lo])]
@@ -398,32 +411,55 @@ def run_host(args, dev):
                 h2d_ms += ms
                 h2d_bytes += nbytes
                 rows += o.n_rows
-    run(0, args.warmup, False)
+    run(0, warmup, False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.warmup, nb, True)
+    run(warmup, nb, True)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    h2d = h2d_bytes / (h2d_ms / 1e3) / 1e9 if h2d_ms > 0 else 0.0
+    h2d = h2d_bytes / (h2d_ms / 1e3) / 1e9 if h2d_ms > 0 else None
     lat_ms = sorted(x * 1e3 for x in lat)
+    rate = B * steps / elapsed
+    for b in bufs:
+        b.close()
+    q.close()
+    return {"events_per_s": rate, "events_per_call": B, "calls": steps, "ms_per_call": elapsed * 1e3 / steps,
+            "h2d_bytes_per_event": H2D_BYTES_PER_EVENT, "h2d_bytes_per_call": h2d_bytes / steps,
+            "h2d_copy_GBps": h2d, "peak_GBps": PCIE_PEAK_GBS,
+            "frac": h2d / PCIE_PEAK_GBS if h2d else None,
+            # the host-fed event rate's input bytes over the link peak (the copy overlaps the kernels)
+            "end_to_end_frac": rate * H2D_BYTES_PER_EVENT / 1e9 / PCIE_PEAK_GBS, "rows_copied_back": rows,
+            "call_latency_ms": {"p50": lat_ms[len(lat_ms) // 2], "p99": lat_ms[int(0.99 * (len(lat_ms) - 1))],
+                                "max": lat_ms[-1]}}
+
+
+def pcie_line(args, dev, ctx):
+    """The driver line's `pcie` object (the H2D roofline fraction): the C2 stream fed from
+    pinned host batches of 2^25 events (bandwidth) and of 1000 events (send(Event[1000]) latency)."""
+    big = host_leg(args, dev, 1 << 25, 5, 1, ctx)
+    small = host_leg(args, dev, 1000, 400, 40, ctx)
+    return {"source": "C2 from pinned host SoA batches (sh_stage / sh_push_staged, double-buffered H2D on the "
+                      "copy stream, output rows copied back); never the headline value",
+            "bulk": big, "send_1000": small,
+            "events_per_s": big["events_per_s"], "h2d_copy_GBps": big["h2d_copy_GBps"],
+            "peak_GBps": PCIE_PEAK_GBS, "frac": big["frac"], "end_to_end_frac": big["end_to_end_frac"],
+            "p50_ms_at_1000": small["call_latency_ms"]["p50"], "p99_ms_at_1000": small["call_latency_ms"]["p99"]}
+
+
+def run_host(args, dev):
+    """`--host`: the host-fed leg alone, as its own JSON line."""
+    r = host_leg(args, dev, args.batch, args.steps, args.warmup)
     print(json.dumps({
-        "metric": METRIC, "value": B * args.steps / elapsed, "unit": "events/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+        "metric": METRIC, "value": r["events_per_s"], "unit": "events/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": r["ms_per_call"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic SplitMix64 stream seed 0xC2 packed into pinned host SoA buffers before the timed region",
         "config": {"workload": "C2 timeBatch(1 sec) count/min/max/avg group by k from HOST batches "
                                "(PCIe-inclusive: H2D of every batch, D2H of every output row; not the HBM headline)",
-                   "key_type": args.key_type, "keys": args.keys, "events_per_call": B, "send_size": args.send_size,
-                   "ingest": "double-buffered sh_stage / sh_push_staged (copy stream + compute stream)",
-                   "rows": rows},
-        "pcie": {"h2d_bytes_per_step": h2d_bytes / args.steps, "h2d_copy_GBps": h2d, "peak_GBps": PCIE_PEAK_GBS,
-                 "frac": h2d / PCIE_PEAK_GBS,
-                 "call_latency_ms": {"p50": statistics.median(lat_ms), "p99": lat_ms[int(0.99 * (len(lat_ms) - 1))],
-                                     "max": lat_ms[-1]}},
-    }), flush=True)
-    for b in bufs:
-        b.close()
-    q.close()
+                   "key_type": args.key_type, "keys": args.keys, "events_per_call": args.batch,
+                   "send_size": args.send_size,
+                   "ingest": "double-buffered sh_stage / sh_push_staged (copy stream + compute stream)"},
+        "pcie": r}), flush=True)
 
 
 def main():
@@ -610,6 +646,8 @@ def main():
         # rank 0's wall time per step in each phase of the sharded push (summaries all-gather,
         # pack, record all-to-all over RCCL, owner pipeline) and its bytes sent per step
         result["config"]["phases_ms_per_step_rank0"] = {k: v / args.steps for k, v in phases.items()}
+    if rank == 0 and world == 1 and not sliced and not args.no_pcie:
+        result["pcie"] = pcie_line(args, dev, ctx)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
         if pool is not None:

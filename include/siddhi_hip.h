@@ -78,7 +78,8 @@ typedef struct {
 #define SH_WIN_TIME_BATCH 2   /* core/query/processor/stream/window/TimeBatchWindowProcessor.java   */
 #define SH_WIN_TIME 3         /* core/query/processor/stream/window/TimeWindowProcessor.java        */
 #define SH_WIN_EXT_TIME_BATCH 4 /* core/query/processor/stream/window/ExternalTimeBatchWindowProcessor.java:
-                                   externalTimeBatch(ts_col, T[, start]) — event-time batches, no timeout */
+                                   externalTimeBatch(ts_col, T[, start[, timeout]]) — event-time batches;
+                                   the timeout through sh_query_set_ext_timeout */
 #define SH_WIN_EXT_TIME 5     /* core/query/processor/stream/window/ExternalTimeWindowProcessor.java:
                                  externalTime(ts_col, T) — sliding over the LONG attribute ts_col    */
 
@@ -165,7 +166,10 @@ typedef struct {
  *   send_size > 0 : consecutive sends of send_size events (the last may be shorter);
  *   send_size == 0: one send of all n events.
  * Columns are SoA, column c holds n values of col_types[c] (int32 for INT/STRID, uint8 BOOL).
- * For sh_push the pointers are host memory; for sh_push_device they are device memory.    */
+ * For sh_push the pointers are host memory; for sh_push_device they are device memory. A column
+ * the query does not read (not in the filter, group-by, partition key, aggregators or time
+ * attributes) may be NULL: the shim packs only what the query reads; a NULL column the query reads
+ * fails the call (SH_ERR_INVALID) before anything runs (sh_push, sh_push_device, sh_stage). */
 typedef struct {
     int64_t n;
     int64_t send_size;
@@ -385,7 +389,8 @@ int sh_shard_flush_windows(sh_shard* s, const int64_t** windows, int64_t* n);
 /* Checkpoint of one rank's shard (SnapshotService.persist/restore, SnapshotService.java:90-296): the
  * global stream state every rank keeps (clock, nextEmitTime, batch count, stream index, p0) and its
  * owner query's windows. Taken between pushes on every rank; restored into a shard created from the
- * same descriptor, rank and world. Two calls as sh_query_snapshot. Sharded aggregations: refused. */
+ * same descriptor, rank and world. Two calls as sh_query_snapshot. A sharded aggregation's shard
+ * (sh_aggregation_shard_create) also carries its roll-up executors and duration tables. */
 int sh_shard_snapshot(sh_shard* s, void* buf, int64_t cap, int64_t* len);
 int sh_shard_restore(sh_shard* s, const void* buf, int64_t len);
 /* Key-sharded incremental aggregation (C4 across G GPUs): *shard ingests through the three phases

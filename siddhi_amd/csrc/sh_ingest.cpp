@@ -51,6 +51,7 @@ extern "C" int sh_stage(sh_query* q, const sh_batch* b, int32_t* ticket) {
     if (!q || !b || !ticket) return sh_fail(SH_ERR_INVALID, "sh_stage: NULL argument");
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (b->n > 0 && !b->ts) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
+    RCHK(check_batch_cols(q, b));
     auto& g = q->ing;
     if (g.outstanding >= 2) return sh_fail(SH_ERR_INVALID, "sh_stage: two staged batches are waiting for sh_push_staged");
     RCHK(ingest_init(q));

@@ -343,6 +343,9 @@ struct sh_query {
     size_t kt_min_size = 0;      // table size at creation (rebuilds never shrink below it)
     // column widths as loaded by the kernels (the sharded owner reads 8-byte raw columns)
     int32_t load_type[SH_MAX_COLS]{};
+    // columns the query reads (filter, group-by, partition key, aggregators, time attributes): a batch
+    // may leave the others NULL — the shim packs only what the query reads (20 B/event for C2)
+    uint32_t cols_used = 0;
     // sharded owner (sh_shard.cpp): windows given per event, flush clocks from the global
     // window starts, global stream index carried per pending event and reported per row
     bool given = false;
@@ -422,6 +425,8 @@ struct sh_query {
     } ing;
 };
 
+// every column the query reads has a pointer in `b` (SH_ERR_INVALID otherwise)
+int check_batch_cols(const sh_query* q, const sh_batch* b);
 // the open window aggregated per key without closing it (sh_window.cpp; aggregation retrieval)
 int query_peek(sh_query* q, int64_t* n_rows);
 // push of a batch staged on the device by sh_stage, host output (sh_window.cpp)

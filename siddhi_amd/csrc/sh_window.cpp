@@ -304,6 +304,17 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (plane_time_group && (rc = q->pgkt.init(std::max<int64_t>(4 * cap, 1 << 16)))) { delete q; return rc; }
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
+    {
+        uint32_t m = 0;
+        auto use = [&](int c) { if (c >= 0 && c < d->n_cols) m |= 1u << c; };
+        for (int i = 0; i < d->n_filter_ops; i++) if (d->filter[i].op == SH_OP_COL) use(d->filter[i].col);
+        for (int i = 0; i < d->n_group_by; i++) use(d->group_by[i]);
+        for (int i = 0; i < d->n_aggs; i++) if (d->aggs[i].fn != SH_AGG_COUNT) use(d->aggs[i].col);
+        use(d->partition_col);
+        if (d->window == SH_WIN_EXT_TIME_BATCH || d->window == SH_WIN_EXT_TIME) use(d->ts_col);
+        if (d->window == SH_WIN_EXT_TIME_BATCH && d->has_start_time == 2) use(d->start_col);
+        q->cols_used = m;
+    }
     q->partitioned = d->partition_col >= 0 && !plane;
     q->xmode = d->expired_on != 0 && !d->stream_current;
     if (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME || plane) {
@@ -1721,10 +1732,19 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
 // The host-output path stores keys/vals/nulls as [col][n] blocks per segment batch; when several
 // run_closed calls append (only one per push today) the layout stays [col][n_rows] because a push
 // calls run_closed at most once.
+int check_batch_cols(const sh_query* q, const sh_batch* b) {
+    if (b->n <= 0) return SH_OK;
+    for (int c = 0; c < q->d.n_cols; c++)
+        if ((q->cols_used >> c & 1) && !b->cols[c])
+            return sh_fail(SH_ERR_INVALID, "batch column " + std::to_string(c) + " is NULL but the query reads it");
+    return SH_OK;
+}
+
 extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     SH_RANGE("sh_push");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
+    RCHK(check_batch_cols(q, b));
     sh_batch dev;
     RCHK(q->staged.stage(q->ctx->stream, b, q->d.n_cols, q->d.col_types, &dev));
     return query_push_staged(q, &dev, out);
@@ -1776,6 +1796,7 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
     SH_RANGE("sh_push_device");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
+    RCHK(check_batch_cols(q, b));
     return push_any(q, b, false, out);
 }
 

@@ -41,3 +41,32 @@ def test_headline_c2_bench_path_matches_golden_digest():
         assert digest.output_digest(a) == gold[name]["sha256"], name
         del ts, cols
     q.close()
+
+
+def test_c1_bench_path_matches_golden_digest():
+    """C1 (BASELINE.json configs[0]) exactly as `bench.py --workload c1` runs it: two sh_push_device calls of
+    33,554,000 events (send(Event[1000])) through the filtered lengthBatch(10000) group-by; the second push
+    starts with the batch carried across the push boundary. Golden: tests/golden/make_c1_digest.py."""
+    import numpy as np
+    import torch
+    from siddhi_amd import runtime
+    gold = json.load(open(os.path.join(HERE, "golden", "c1_bench_digest.json")))
+    cfg = gold["config"]
+    B = cfg["events_per_push"]
+    schema = abi.Schema.parse("symbol string, price double, volume long, ts long")
+    spec = abi.QuerySpec(schema, "lengthBatch", 10000, group_by=["symbol"], aggs=[("sum", "volume"), ("avg", "price")],
+                         filter=(">", "price", 100), key_capacity=1000)
+    dev = torch.device("cuda", 0)
+    q = runtime.GpuQuery(spec)
+    parts = []
+    for i, name in enumerate(("push0", "push01")):
+        cols = [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in synth.c1_stock(i * B, B)[1]]
+        torch.cuda.synchronize()
+        out = q.push_device(B, cols[3].data_ptr(), [c.data_ptr() for c in cols], cfg["send_size"])
+        torch.cuda.synchronize()
+        parts.append(runtime.device_out_arrays(out))
+        a = abi.concat_arrays(parts)
+        assert a["ts"].size == gold[name]["rows"] and a["flush_clock"].size == gold[name]["flushes"]
+        assert digest.output_digest(a) == gold[name]["sha256"], name
+        del cols
+    q.close()

@@ -152,3 +152,44 @@ def test_async_small_pushes_hashed_keys_grow_the_table(rt):
         b.close()
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("chunk", [1000, 60_000])
+def test_unread_columns_may_be_null(rt, chunk):
+    """The shim packs only the columns the query reads (20 B/event for C2: the `ts` attribute column is not
+    read by `select k, count(), min(v), max(v), avg(v)`): a NULL pointer for it gives the oracle's output,
+    staged (zero-copy small batches and copied ones) and through sh_push; a NULL column the query reads is
+    refused before anything runs."""
+    from siddhi_amd.runtime import SiddhiError
+    ts, cols = synth.keyed_stream(0, 240_000, 0xC2, 5_000, 100)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=5_000)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    bufs = [rt.PinnedBatch(SCHEMA, chunk), rt.PinnedBatch(SCHEMA, chunk)]
+    parts, want, tickets = [], [], []
+    edges = list(range(0, len(ts), chunk)) + [len(ts)]
+    for i, (a, b) in enumerate(zip(edges[:-1], edges[1:])):
+        want.append(abi.out_arrays(o.push_raw(abi.HostBatch(SCHEMA, ts[a:b], [c[a:b] for c in cols], 1))))
+        if i % 5 == 4:
+            while tickets:
+                parts.append(abi.out_arrays(g.push_staged_raw(tickets.pop(0))))
+            hb = abi.HostBatch(SCHEMA, ts[a:b], [c[a:b] for c in cols], 1)
+            hb.b.cols[2] = None
+            parts.append(abi.out_arrays(g.push_raw(hb)))
+            continue
+        pb = bufs[i % 2].fill(ts[a:b], [c[a:b] for c in cols], 1)
+        pb.b.cols[2] = None
+        tickets.append(g.stage(pb))
+        if len(tickets) == 2:
+            parts.append(abi.out_arrays(g.push_staged_raw(tickets.pop(0))))
+    while tickets:
+        parts.append(abi.out_arrays(g.push_staged_raw(tickets.pop(0))))
+    assert_same(abi.concat_arrays(parts), abi.concat_arrays(want), label=f"null unread column {chunk}")
+    hb = abi.HostBatch(SCHEMA, ts[:100] + 10**9, [c[:100] for c in cols], 1)
+    hb.b.cols[1] = None  # v is read by min / max / avg
+    with pytest.raises(SiddhiError, match="column 1 is NULL"):
+        g.push_raw(hb)
+    for b in bufs:
+        b.close()
+    g.close()
+    o.close()

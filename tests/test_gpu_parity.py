@@ -94,6 +94,16 @@ def test_c1_lengthbatch_matches_oracle(rt, send_size, cuts):
     assert out["flush_offsets"].size >= 15
 
 
+@pytest.mark.parametrize("send_size,cuts", [(1000, [4_000_000]), (1, [3_333_331, 6_666_667]), (0, [5_000_000])])
+def test_c1_full_size_matches_oracle(rt, send_size, cuts):
+    """C1 at its configuration size (BASELINE.json configs[0]: 10M events, 1k symbols) through sh_push in
+    the three send modes: send(Event[1000]), per-event sends, one send per push."""
+    ts, cols = synth.c1_stock(0, 10_000_000)
+    pushes = split_batches(C1_SCHEMA, ts, cols, cuts, send_size)
+    out = both(rt, c1_spec(), pushes, label=f"C1-10M-{send_size}")
+    assert out["flush_offsets"].size > 400
+
+
 def test_c1_quantized_prices(rt):
     ts, cols = synth.c1_stock(0, 120_000, quantized=True)
     both(rt, c1_spec(L=777), split_batches(C1_SCHEMA, ts, cols, [50_000], 1000), label="C1q")
