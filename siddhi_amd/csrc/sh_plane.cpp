@@ -471,12 +471,59 @@ static PgDeques pg_deques(sh_query* q) {
     return D;
 }
 
+// Room in the (partition, group) pair table for the push's new pairs (at most one per add, M) before
+// the walk inserts them: the walk advances every partition's ring, so a table that overflowed there
+// would fail the push after the query state changed. When the table could pass half full, the live
+// states move to a fresh table sized for them plus M (dead pairs dropped, PartitionStateHolder's
+// returnState), and the state arrays follow (sh_plane_group_kernels.hip k_pg_rehash).
+static int pg_reserve_pairs(sh_query* q, int64_t M) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    if (q->pgkt.n_keys + M <= (int64_t)q->pgkt.size_ / 2) return SH_OK;
+    const int F = std::max(1, q->ap.n_fields);
+    const int64_t on = s->pg_st_n;
+    RCHK(s->pg_cnt.reserve(64, false));
+    HIPCHK(hipMemsetAsync(s->pg_cnt.p, 0, 8, st));
+    launch_pg_count_live(st, q->pgkt.dev(), on, s->pg_st_cnt.as<int64_t>(), s->pg_st_f.as<u64>(),
+                         s->pg_dq_len.as<int64_t>(), F, (unsigned long long*)s->pg_cnt.p);
+    HIPCHK(hipGetLastError());
+    int64_t live = 0;
+    RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &live));
+    size_t ts = std::max<size_t>(q->pg_min_size, 16);
+    while ((int64_t)ts < 2 * (live + M)) ts <<= 1;
+    if (ts > ((size_t)1 << 31)) return sh_fail(SH_ERR_UNSUPPORTED, "partition lanes: more than 2^30 (partition, group) states");
+    KeyTableHost nk;
+    RCHK(nk.init_size(ts));
+    const int64_t nn = (int64_t)ts + 1;
+    DevBuf ncnt, nf, ndqo, ndql;
+    RCHK(fill(ncnt, (size_t)nn * 8, 0));
+    RCHK(fill(nf, (size_t)F * nn * 8, 0));
+    RCHK(fill(ndqo, (size_t)F * nn * 8, 0));
+    RCHK(fill(ndql, (size_t)F * nn * 8, 0));
+    launch_pg_rehash(st, q->pgkt.dev(), on, s->pg_st_cnt.as<int64_t>(), s->pg_st_f.as<u64>(), s->pg_dq_off.as<int64_t>(),
+                     s->pg_dq_len.as<int64_t>(), F, nk.dev(), nn, ncnt.as<int64_t>(), nf.as<u64>(), ndqo.as<int64_t>(),
+                     ndql.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    RCHK(nk.check(st));
+    HIPCHK(hipStreamSynchronize(st));  // the old arrays are released below
+    SH_TRACE("pg_reserve_pairs: %lld pairs (%lld live) in %zu slots -> %zu slots", (long long)q->pgkt.n_keys,
+             (long long)live, q->pgkt.size_, ts);
+    q->pgkt = std::move(nk);
+    s->pg_st_n = nn;
+    s->pg_st_cnt = std::move(ncnt);
+    s->pg_st_f = std::move(nf);
+    s->pg_dq_off = std::move(ndqo);
+    s->pg_dq_len = std::move(ndql);
+    return SH_OK;
+}
+
 static int group_time_rows(sh_query* q, const ColSet* cs, SlRecords rec, int64_t M, int64_t nF, int64_t T, int64_t ss,
                            bool xt, int64_t* n_rows_out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
     const int nv = std::max(1, q->ap.n_vcols), na = q->ap.n;
     const int64_t np = s->nslots;
+    RCHK(pg_reserve_pairs(q, M));
     if (cs && M > 0) {
         launch_pg_rec_group(st, rec, M, *cs, q->gkp, q->gkt.dev(), nv);
         HIPCHK(hipGetLastError());
@@ -975,7 +1022,7 @@ static int table_save(sh_query* q, KeyTableHost& kt, std::vector<uint8_t>& out) 
     return SH_OK;
 }
 
-static int table_load(sh_query* q, KeyTableHost& kt, const uint8_t* p, size_t len, size_t* used) {
+static int table_load(sh_query* q, KeyTableHost& kt, const uint8_t* p, size_t len, size_t* used, bool resizable = false) {
     hipStream_t st = q->ctx->stream;
     uint64_t size = 0;
     int64_t nk = 0;
@@ -983,6 +1030,9 @@ static int table_load(sh_query* q, KeyTableHost& kt, const uint8_t* p, size_t le
     std::memcpy(&size, p, 8);
     std::memcpy(&nk, p + 8, 8);
     const size_t kb = kt.dense ? 0 : size * 8;
+    if (resizable && !kt.dense && size != kt.size_ && size >= 16 && (size & (size - 1)) == 0 && size <= ((uint64_t)1 << 31) &&
+        16 + kb <= len)
+        RCHK(kt.init_size(size));  // a pair table that grew after the query was created
     if (size != kt.size_ || nk < 0 || nk > (int64_t)size + 1) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
     if (16 + kb > len) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     if (kb) HIPCHK(hipMemcpyAsync(kt.keys.p, p + 16, kb, hipMemcpyHostToDevice, st));
@@ -1157,8 +1207,16 @@ int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
         size_t u = 0;
         RCHK(table_load(q, q->gkt, p + o, n - o, &u));
         o += u;
-        RCHK(table_load(q, q->pgkt, p + o, n - o, &u));
+        RCHK(table_load(q, q->pgkt, p + o, n - o, &u, true));
         o += u;
+        // the state arrays were restored at the blob's size (sh_snapshot.cpp): they must match the table's
+        if (s->pg_st_n != (int64_t)q->pgkt.size_ + 1) {
+            s->pg_st_n = (int64_t)q->pgkt.size_ + 1;
+            const size_t FN = (size_t)std::max(1, q->ap.n_fields) * s->pg_st_n;
+            if (s->pg_st_cnt.cap < (size_t)s->pg_st_n * 8 || s->pg_st_f.cap < FN * 8 || s->pg_dq_off.cap < FN * 8 ||
+                s->pg_dq_len.cap < FN * 8)
+                return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+        }
         uint64_t w = 0;
         if (!get(&w, 8) || w > (n - o) / 8) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
         RCHK(s->pg_dq_pool.reserve((size_t)std::max<uint64_t>(w, 8) * 8, false));

@@ -98,6 +98,12 @@ void launch_pg_replay(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_ops,
                       SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows, PgDeques D, const i64* scr_off);
 void launch_pg_dq_len(hipStream_t s, PgDeques D, i64* out_len);
 void launch_pg_dq_pool(hipStream_t s, PgDeques D, const i64* off_out, u64* pool_out, i64* new_off);
+// rebuild of the pair table: live states counted, then moved into a fresh table (state arrays of n slots,
+// the last the sentinel; F fields, field-major)
+void launch_pg_count_live(hipStream_t s, KeyTable kt, i64 n, const i64* cnt, const u64* f, const i64* dql, int F,
+                          unsigned long long* n_live);
+void launch_pg_rehash(hipStream_t s, KeyTable okt, i64 on, const i64* cnt, const u64* f, const i64* dqo, const i64* dql,
+                      int F, KeyTable nkt, i64 nn, i64* ncnt, u64* nf, i64* ndqo, i64* ndql);
 void launch_pg_heads32(hipStream_t s, const u32* key, i64 n, unsigned char* head);
 void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* out);
 int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,

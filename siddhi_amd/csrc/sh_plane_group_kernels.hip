@@ -880,4 +880,55 @@ void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* o
     if (n > 0) hipLaunchKernelGGL(k_pg_sum_u32, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a, n, out);
 }
 
+// ---- rebuild of the (partition, group) pair table (time lanes grouped by other columns) -----------
+// PartitionStateHolder drops a group's state once every aggregator can be destroyed (returnState /
+// canDestroy); here a state that is all zero — count, fields and deque lengths — is exactly what a fresh
+// pair starts from, so the rebuild keeps the others and drops those. Slot n - 1 is the table's sentinel
+// (mask + 1), which maps to the new table's sentinel.
+__device__ __forceinline__ bool pg_live(i64 n, i64 s, const i64* cnt, const u64* f, const i64* dql, int F) {
+    bool live = cnt[s] != 0;
+    for (int j = 0; j < F && !live; j++) live = f[(size_t)j * n + s] != 0 || dql[(size_t)j * n + s] != 0;
+    return live;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_count_live(KeyTable kt, i64 n, const i64* __restrict__ cnt,
+                                                         const u64* __restrict__ f, const i64* __restrict__ dql, int F,
+                                                         unsigned long long* n_live) {
+    const i64 s = (i64)blockIdx.x * kBlock + threadIdx.x;
+    bool live = false;
+    if (s < n && (s == n - 1 || kt.keys[s] != kEmptyKey)) live = pg_live(n, s, cnt, f, dql, F);
+    const unsigned long long b = __ballot(live);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_live, (unsigned long long)__popcll(b));
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_rehash(KeyTable okt, i64 on, const i64* __restrict__ cnt,
+                                                     const u64* __restrict__ f, const i64* __restrict__ dqo,
+                                                     const i64* __restrict__ dql, int F, KeyTable nkt, i64 nn,
+                                                     i64* ncnt, u64* nf, i64* ndqo, i64* ndql) {
+    const i64 s = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= on) return;
+    const bool sentinel = s == on - 1;
+    if (!sentinel && okt.keys[s] == kEmptyKey) return;
+    if (!pg_live(on, s, cnt, f, dql, F)) return;
+    const i64 d = sentinel ? nn - 1 : (i64)key_slot(nkt, okt.keys[s]);
+    ncnt[d] = cnt[s];
+    for (int j = 0; j < F; j++) {
+        nf[(size_t)j * nn + d] = f[(size_t)j * on + s];
+        ndqo[(size_t)j * nn + d] = dqo[(size_t)j * on + s];
+        ndql[(size_t)j * nn + d] = dql[(size_t)j * on + s];
+    }
+}
+
+void launch_pg_count_live(hipStream_t s, KeyTable kt, i64 n, const i64* cnt, const u64* f, const i64* dql, int F,
+                          unsigned long long* n_live) {
+    hipLaunchKernelGGL(k_pg_count_live, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, kt, n, cnt, f,
+                       dql, F, n_live);
+}
+
+void launch_pg_rehash(hipStream_t s, KeyTable okt, i64 on, const i64* cnt, const u64* f, const i64* dqo, const i64* dql,
+                      int F, KeyTable nkt, i64 nn, i64* ncnt, u64* nf, i64* ndqo, i64* ndql) {
+    hipLaunchKernelGGL(k_pg_rehash, dim3((unsigned)((on + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, okt, on, cnt, f,
+                       dqo, dql, F, nkt, nn, ncnt, nf, ndqo, ndql);
+}
+
 }  // namespace shd

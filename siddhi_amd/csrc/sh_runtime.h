@@ -257,6 +257,7 @@ struct sh_query {
     KeyTableHost gkt;
     bool plane_sorted = false;  // lane 3 (also for lengthBatch keyed by the partition with Tuning::pl_sort)
     KeyTableHost pgkt;          // time lanes grouped by other columns: (partition slot, group slot) -> state
+    size_t pg_min_size = 0;     // its size at creation (a rebuild never shrinks below it)
     bool group_other = false;   // ... grouped by columns other than the partition key
     int P = 1, logP = 0, NL = 0;
     // playback clock + window state

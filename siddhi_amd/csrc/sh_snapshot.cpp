@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 5;  // 5: band key mode, sharded aggregation sections
+constexpr uint32_t kVersion = 6;  // 5: band key mode, sharded aggregation sections; 6: timeout / limiter in the fingerprint
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -89,6 +89,10 @@ uint64_t fingerprint(const sh_query* q) {
     h = fnv(h, &d.start_time, 8);
     h = fnv(h, d.group_by, sizeof(int32_t) * d.n_group_by);
     h = fnv(h, d.aggs, sizeof(sh_agg_spec) * d.n_aggs);
+    // set after creation but part of the blob's layout: the externalTimeBatch timeout (its scheduler
+    // section) and the output rate limiter's kind / per-partition form (their sections)
+    const int64_t extra[] = {q->xt_timeout, q->rate.kind, q->rate.N, q->rate.part, q->rate.pkey, q->rate.lkey};
+    h = fnv(h, extra, sizeof(extra));
     h = fnv(h, &q->fp_orig.n, sizeof(int));
     for (int i = 0; i < q->fp_orig.n; i++) {
         const FilterOpD& o = q->fp_orig.ops[i];

@@ -302,6 +302,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     // (partition, group) pairs: room for four per group key, at least 64k
     if (plane_time_group && (rc = q->pgkt.init(std::max<int64_t>(4 * cap, 1 << 16)))) { delete q; return rc; }
+    q->pg_min_size = q->pgkt.size_;
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];
     {

@@ -252,3 +252,31 @@ def test_partitioned_time_group_by_other_min_max(rt, output, send_size):
     pushes.append(("advance", int(ts[-1]) + 5_000))
     ref = both(rt, spec, pushes, f"ptime group minmax {output} {send_size}")
     assert ref["ts"].size > 0
+
+
+def test_partitioned_time_group_by_other_pair_churn(rt):
+    """Many more (partition, group) pairs over the stream than the pair table holds at creation (400 x 400
+    pairs, key_capacity 400: 64k pairs fit at half load), few alive at once: emptied states are dropped
+    (PartitionStateHolder.returnState) when the table is rebuilt before a push could overfill it. Min / max
+    deques ride along. A snapshot taken after the rebuilds restores into a fresh query (the pair table at
+    the blob's size) and continues like the oracle."""
+    from oracle.oracle import OracleQuery
+    from tests.parity import assert_same, run_pushes
+    from siddhi_amd import abi as _abi
+    ts, cols = gstream(400_000, 400, 400, 97)
+    spec = abi.QuerySpec(GSCHEMA, "time", 100, group_by=["g"], aggs=[("count", None), ("sum", "v"), ("max", "v")],
+                         partition="p", output="all", key_capacity=400)
+    pushes = split_batches(GSCHEMA, ts, cols, [50_000, 120_000, 200_000, 290_000, 330_000], 1)
+    g = rt.GpuQuery(spec)
+    part1 = run_pushes(g, pushes[:4])
+    blob = g.snapshot()
+    g.close()
+    g2 = rt.GpuQuery(spec)
+    g2.restore(blob)
+    part2 = run_pushes(g2, pushes[4:] + [("advance", int(ts[-1]) + 1_000)])
+    g2.close()
+    o = OracleQuery(spec)
+    want = run_pushes(o, pushes + [("advance", int(ts[-1]) + 1_000)])
+    o.close()
+    assert_same(_abi.concat_arrays([part1, part2]), want, label="pair churn")
+    assert want["expired"].sum() > 0

@@ -236,3 +236,31 @@ def test_partition_time_group_lanes_checkpoint(cut):
     pushes = split_batches(GSCHEMA, ts, cols, [15_000, 33_000], 1) + [("advance", int(ts[-1]) + 1_000)]
     got, ref, _ = checkpointed(spec, pushes, cut)
     assert_same(got, ref, label=f"time group lanes ckpt {cut}")
+
+
+@pytest.mark.parametrize("window,group_by", [("time", []), ("lengthBatch", []), ("time", ["g"]), ("lengthBatch", ["g"])])
+def test_truncated_partition_lane_blob_leaves_query_unchanged(window, group_by):
+    """Partition lanes (one lane per partition, lane 3, the grouped time lanes): a truncated blob cut in the
+    device section, in the host Scheduler section and in the pair / group tables fails and the query — it
+    has moved on past the snapshot — continues identically to the uninterrupted oracle (the restore rolls
+    back to the state it snapshotted first)."""
+    from siddhi_amd import runtime
+    from tests.test_gpu_partition import GSCHEMA, gstream
+    ts, cols = gstream(45_000, 60, 9, 23)
+    spec = abi.QuerySpec(GSCHEMA, window, 120 if window == "time" else 7, group_by=group_by,
+                         aggs=[("count", None), ("sum", "v"), ("max", "v")], partition="p", output="all",
+                         key_capacity=128)
+    pushes = split_batches(GSCHEMA, ts, cols, [15_000, 30_000], 1) + [("advance", int(ts[-1]) + 1_000)]
+    g = runtime.GpuQuery(spec)
+    a = run_pushes(g, pushes[:1])
+    blob = g.snapshot()
+    b = run_pushes(g, pushes[1:2])
+    for cut in (24, len(blob) // 4, len(blob) // 2, len(blob) - 40, len(blob) - 3):
+        with pytest.raises(Exception, match="truncated|does not match|restore|unreadable"):
+            g.restore(blob[:cut])
+    c = run_pushes(g, pushes[2:])
+    g.close()
+    o = OracleQuery(spec)
+    ref = run_pushes(o, pushes)
+    o.close()
+    assert_same(abi.concat_arrays([a, b, c]), ref, label=f"lanes {window} {group_by} after failed restores")
