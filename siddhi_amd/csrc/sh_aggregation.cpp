@@ -182,6 +182,17 @@ struct sh_aggregation {
     bool band_ok = false;
     uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
     bool chk_pending = false;  // level key-table counters queued to pinned memory, not yet verified
+    // band re-bases swap the root's table with this spare (init_band reuses its buffers: no hipMalloc /
+    // hipFree, whose implicit device synchronisation cost ~0.2 ms per push)
+    KeyTableHost band_spare;
+    // the queued events' bucket range after the last device push, measured behind it on the stream
+    // (k_pend_bucket_range, read at the next push once ev_pr completed): the next push places its band
+    // from it without a probe round trip
+    bool pr_valid = false;
+    int64_t pr_b0 = 0;
+    hipEvent_t ev_pr = nullptr;
+    DevBuf pr_dev;
+    int64_t* h_pr = nullptr;
 };
 
 // The levels' key-table overflow checks are queued with each merge and verified after the next
@@ -555,6 +566,10 @@ static void agg_free(sh_aggregation* a) {
     a->root_key_col.release();
     a->minmax.release();
     if (a->h_minmax) (void)hipHostFree(a->h_minmax);
+    a->band_spare.release();
+    a->pr_dev.release();
+    if (a->h_pr) (void)hipHostFree(a->h_pr);
+    if (a->ev_pr) (void)hipEventDestroy(a->ev_pr);
     if (a->ev0) (void)hipEventDestroy(a->ev0);
     if (a->ev1) (void)hipEventDestroy(a->ev1);
     for (int i = 0; i < sh_aggregation::kRing; i++) {
@@ -582,24 +597,98 @@ void agg_release_sharded(sh_aggregation* a) { agg_free(a); }
 // Band keys (KeyTable::lk): the push's buckets [lo, hi] and the queued events' buckets must lie in
 // band_rows consecutive buckets; the band is re-based (the queued events' slots re-derived) when the
 // push runs past it, and the root falls back to the open-addressing table while they do not fit.
+// The queued events' bucket range: from the measurement queued behind the last device push (pr_valid),
+// else probed now (one round trip).
+static int pend_range(sh_aggregation* a, int64_t* lo, int64_t* hi) {
+    sh_query* q = a->root;
+    if (a->pr_valid) {
+        HIPCHK(sh_wait_event(a->ev_pr));
+        *lo = a->pr_b0 + a->h_pr[0];
+        *hi = a->pr_b0 + a->h_pr[1];
+        return SH_OK;
+    }
+    hipStream_t s = a->ctx->stream;
+    const u32 ref = q->kt.lk ? q->kt.b0 : 0u;
+    const int64_t base = q->kt.lk ? q->kt.band_base : 0;
+    launch_pend_bucket_range(s, q->pend_pos.as<u32>(), q->n_pend, q->kt.dev(), ref, a->minmax.as<int64_t>());
+    HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(sh_wait_stream(s));
+    *lo = base + a->h_minmax[0];
+    *hi = base + a->h_minmax[1];
+    return SH_OK;
+}
+
+// After a device push of a band-keyed root: the queued events' bucket range, measured on the stream
+// (no wait) and read by the next push.
+static int pend_range_queue(sh_aggregation* a) {
+    sh_query* q = a->root;
+    a->pr_valid = false;
+    if (!a->band_ok || !q->kt.lk || q->n_pend <= 0) return SH_OK;
+    hipStream_t s = a->ctx->stream;
+    if (!a->ev_pr) HIPCHK(hipEventCreateWithFlags(&a->ev_pr, hipEventDisableTiming));
+    if (!a->h_pr) HIPCHK(hipHostMalloc((void**)&a->h_pr, 16, hipHostMallocDefault));
+    RCHK(a->pr_dev.reserve(16, false));
+    launch_pend_bucket_range(s, q->pend_pos.as<u32>(), q->n_pend, q->kt.dev(), q->kt.b0, a->pr_dev.as<int64_t>());
+    HIPCHK(hipMemcpyAsync(a->h_pr, a->pr_dev.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(a->ev_pr, s));
+    a->pr_b0 = q->kt.band_base;
+    a->pr_valid = true;
+    return SH_OK;
+}
+
+// A device push of a band-keyed root without the probe round trip: the band is placed from the queued
+// events' range (or the clock's bucket) and the push validates it — k_boundaries flags any bucket
+// outside the band and push_core returns kRetryBand at its first synchronisation, before anything was
+// committed; the push is then probed and pushed again. Returns 1 when the speculative push was taken.
+static int spec_push(sh_aggregation* a, const sh_batch* dev, const sh_out** o, int* taken) {
+    sh_query* q = a->root;
+    *taken = 0;
+    const int64_t R = a->band_rows;
+    if (!a->band_ok || !a->has_bucket || !q->kt.lk || dev->n < (1 << 16) || a->shard || !q->clock_valid) return SH_OK;
+    int64_t b0;
+    if (q->n_pend > 0) {
+        if (!a->pr_valid) return SH_OK;
+        int64_t plo, phi;
+        RCHK(pend_range(a, &plo, &phi));
+        if (phi - plo >= R || plo < 0) return SH_OK;
+        b0 = plo;
+    } else {
+        if (q->clock < 0) return SH_OK;
+        b0 = q->clock / a->T_root;
+    }
+    if (b0 != q->kt.band_base) {
+        RCHK(a->band_spare.init_band(a->band_lk, a->band_rows, b0, a->band_mul, a->band_add));
+        RCHK(query_swap_keys(q, a->band_spare));
+    }
+    q->band_spec = true;
+    const int rc = sh_push_device(q, dev, o);
+    q->band_spec = false;
+    if (rc == kRetryBand) {
+        // the overflow word of the band the push left: cleared before the probed push
+        HIPCHK(hipMemsetAsync((char*)q->kt.ctrl.p + 8, 0, 8, a->ctx->stream));
+        a->pr_valid = false;
+        return SH_OK;
+    }
+    RCHK(rc);
+    *taken = 1;
+    return SH_OK;
+}
+
 static int band_reserve(sh_aggregation* a, int64_t lo, int64_t hi, int64_t bound) {
     sh_query* q = a->root;
     const int64_t R = a->band_rows;
     if (q->kt.lk && lo >= q->kt.band_base && hi < q->kt.band_base + R) return SH_OK;
     int64_t ulo = lo, uhi = hi;
     if (hi - lo < R && q->n_pend > 0) {
-        hipStream_t s = a->ctx->stream;
-        launch_pend_bucket_range(s, q->pend_pos.as<u32>(), q->n_pend, q->kt.dev(), (u32)lo, a->minmax.as<int64_t>());
-        HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
-        HIPCHK(sh_wait_stream(s));
-        ulo = std::min(ulo, lo + a->h_minmax[0]);
-        uhi = std::max(uhi, lo + a->h_minmax[1]);
+        int64_t plo = 0, phi = 0;
+        RCHK(pend_range(a, &plo, &phi));
+        ulo = std::min(ulo, plo);
+        uhi = std::max(uhi, phi);
     }
     if (uhi - ulo < R) {
-        KeyTableHost nk;
-        RCHK(nk.init_band(a->band_lk, a->band_rows, ulo, a->band_mul, a->band_add));
+        RCHK(a->band_spare.init_band(a->band_lk, a->band_rows, ulo, a->band_mul, a->band_add));
         SH_TRACE("aggregation root: key band [%lld, %lld)", (long long)ulo, (long long)(ulo + R));
-        return query_swap_keys(q, nk);
+        return query_swap_keys(q, a->band_spare);
     }
     if (q->kt.lk) {
         // buckets too far apart for the band: the open-addressing table, sized for the queued keys too
@@ -665,10 +754,16 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     HIPCHK(hipEventRecord(a->ev0, a->ctx->stream));
     HIPCHK(hipEventRecord(a->r0[rk], a->ctx->stream));
     SH_TMARK(0);
-    RCHK(agg_reserve_root(a, &dev, !host));
-    SH_TMARK(7);  // (the root's push marks 0..6 follow)
-    RCHK(sh_push_device(a->root, &dev, &o));
+    int taken = 0;
+    if (!host) RCHK(spec_push(a, &dev, &o, &taken));
+    if (!taken) {
+        a->pr_valid = a->pr_valid && a->root->n_pend > 0;
+        RCHK(agg_reserve_root(a, &dev, !host));
+        SH_TMARK(7);  // (the root's push marks 0..6 follow)
+        RCHK(sh_push_device(a->root, &dev, &o));
+    }
     RCHK(agg_verify(a));  // (the root's push synchronised the stream: the last push's level checks are in)
+    RCHK(pend_range_queue(a));
     RCHK(agg_after_root(a, o));
     SH_TMARK(8);
     HIPCHK(hipEventRecord(a->ev1, a->ctx->stream));
@@ -757,6 +852,7 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation advances through sh_shard_advance_time");
     const sh_out* o = nullptr;
+    a->pr_valid = false;  // (the TIMER may flush the queued events)
     RCHK(sh_advance_time_device(a->root, now, &o));
     RCHK(pass_root_flushes(a, o));
     RCHK(catch_up(a));
@@ -1123,6 +1219,7 @@ static int agg_restore_blob(sh_aggregation* a, const void* buf, int64_t len) {
     const int64_t rl = r.val<int64_t>();
     if (!r.ok || rl <= 0 || r.o + (size_t)rl > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     (void)hipStreamSynchronize(s);
+    a->pr_valid = false;
     RCHK(sh_query_restore(a->root, r.p + r.o, rl));
     r.o += (size_t)rl;
     return agg_state_read(a, r);

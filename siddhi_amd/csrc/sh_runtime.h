@@ -305,6 +305,10 @@ struct sh_query {
     std::vector<int64_t> sc_sl_host;  // stream.current: the sends' clocks (host scratch, kept)
     // an aggregation root whose key table may switch to band mode (sh_aggregation.cpp band_reserve)
     bool band_keys = false;
+    // the band was placed without probing the push (sh_aggregation.cpp agg_push): a push one of whose
+    // buckets falls outside it returns kRetryBand at its first synchronisation, before any state changed
+    bool band_spec = false;
+    PinnedBuf h_spec;
     uint32_t band_lk = 0, band_rows = 0, band_mul = 1, band_add = 0;
     // small-push fast path (try_small_push): the kernel's report in coherent pinned host memory
     shd::SmallRes* small_res = nullptr;
@@ -426,6 +430,9 @@ struct sh_query {
     } ing;
 };
 
+// push_core's return when a speculatively placed key band missed one of the push's buckets (nothing of
+// the push was committed; the aggregation probes the push and pushes again)
+constexpr int kRetryBand = 17;
 // every column the query reads has a pointer in `b` (SH_ERR_INVALID otherwise)
 int check_batch_cols(const sh_query* q, const sh_batch* b);
 // the open window aggregated per key without closing it (sh_window.cpp; aggregation retrieval)

@@ -146,11 +146,13 @@ static int size_partitions(sh_query* q) {
 // Move the open window's keys into a fresh table of `size` slots: keys of closed windows are dead
 // (their group states were destroyed on flush, R9), so the rebuild drops them; the pending events'
 // slot positions are remapped.
+// On return `nk` holds the old table (a caller may keep it as a spare: no allocation next time). A band
+// target (arithmetic slots, the caller placed every queued bucket inside it) is not read back: no sync.
 int query_swap_keys(sh_query* q, KeyTableHost& nk) {
     launch_rekey(q->ctx->stream, q->n_pend, q->pend_pos.as<u32>(), q->kt.dev(), nk.dev());
     HIPCHK(hipGetLastError());
-    RCHK(nk.check(q->ctx->stream));
-    q->kt = std::move(nk);
+    if (!nk.lk) RCHK(nk.check(q->ctx->stream));
+    std::swap(q->kt, nk);
     return size_partitions(q);
 }
 
@@ -1565,6 +1567,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         RCHK(q->h_bounds.reserve((size_t)nb0 * sizeof(Bound)));
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
+        if (q->band_spec) {
+            // (a speculatively placed band: its overflow word comes back with the push info)
+            RCHK(q->h_spec.reserve(16));
+            RCHK(q->kt.check_async(s, q->h_spec.as<uint32_t>()));
+        }
         HIPCHK(hipEventRecord(q->ev_mid, s));
         SH_TMARK(1);
         if (early_split && !sweep) RCHK(run_multisplit(q, q->n_pend + N, b, true));
@@ -1574,6 +1581,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         SH_TMARK(3);
         PushInfo info = *q->h_info;
         SH_TRACE("push info: pass=%lld bounds=%d", (long long)info.total_pass, info.n_bounds);
+        if (q->band_spec && q->h_spec.as<uint32_t>()[2] == 3) {
+            SH_TRACE("push: a bucket outside the speculative key band, retried after a probe");
+            return kRetryBand;
+        }
         if (sweep && info.ms_overflow) {
             // a partition bucket overflowed (skewed keys): the counting split runs in run_closed, and
             // for this query from now on

@@ -293,3 +293,50 @@ def test_aggregation_truncated_blob_rolls_back(rt, ktype):
     assert_tables_equal(tables(g, spec), tables(o, spec), "after failed restores")
     for x in (g, o):
         x.close()
+
+
+def test_device_pushes_speculative_band(rt):
+    """Device pushes of a band-keyed root place the band from the queued events' bucket range measured
+    behind the previous push (no probe round trip); k_boundaries validates it and a push with a bucket
+    outside the band is probed and pushed again before anything was committed. Pushes of in-order events
+    (the speculation holds), pushes with events up to 40 s late (retried), a push after a TIMER and a push
+    after a checkpoint restore: every table equal to the oracle's (host pushes of the same events)."""
+    import torch
+    rng = np.random.default_rng(33)
+    n = 1_200_000
+    clock = 1_700_000_000_000 + np.arange(n, dtype=np.int64) // 200  # 200 events per ms: 100k events span 0.5 s
+    lag = np.zeros(n, np.int64)
+    lag[500_000:520_000] = rng.integers(0, 40_000, 20_000)
+    lag[900_000:900_050] = 3_000
+    ext = clock - lag
+    k = rng.integers(0, 4_000, n).astype(np.int32)
+    v = np.round(rng.normal(50, 20, n), 2)
+    spec = abi.AggregationSpec(STR_SCHEMA, [("sum", "v"), ("avg", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                               group_by=["k"], ts="ts", durations=("sec", "hour"), key_capacity=4_000)
+    cuts = [0, 100_000, 200_000, 330_000, 480_000, 600_000, 700_000, 800_000, 1_000_000, n]
+    dev = torch.device("cuda", 0)
+    g, o = rt.GpuAggregation(spec), OracleAggregation(spec)
+    for i, (a, b) in enumerate(zip(cuts, cuts[1:])):
+        cols = [torch.from_numpy(np.ascontiguousarray(x[a:b])).to(dev) for x in (k, v, ext)]
+        t = torch.from_numpy(np.ascontiguousarray(clock[a:b])).to(dev)
+        torch.cuda.synchronize()
+        g.push_device(b - a, t.data_ptr(), [c.data_ptr() for c in cols], 1)
+        o.push(abi.HostBatch(STR_SCHEMA, clock[a:b], [k[a:b], v[a:b], ext[a:b]], 1))
+        if i == 3:
+            now = int(clock[b - 1]) + 1_500
+            g.advance_time(now)
+            o.advance_time(now)
+        if i == 5:
+            blob = g.snapshot()
+            g.close()
+            g = rt.GpuAggregation(spec)
+            g.restore(blob)
+        if i in (2, 6):
+            assert_tables_equal(tables(g, spec), tables(o, spec), f"spec band@{i}")
+        del cols, t
+    now = int(clock[-1]) + 2 * 3_600_000
+    g.advance_time(now)
+    o.advance_time(now)
+    assert_tables_equal(tables(g, spec), tables(o, spec), "spec band end")
+    g.close()
+    o.close()
