@@ -185,6 +185,12 @@ struct sh_aggregation {
     // band re-bases swap the root's table with this spare (init_band reuses its buffers: no hipMalloc /
     // hipFree, whose implicit device synchronisation cost ~0.2 ms per push)
     KeyTableHost band_spare;
+    // the roll-up levels (merges, dispatches, upper-duration tables) run on their own stream: a push's
+    // level kernels overlap the next push's root window instead of delaying it. They read the root's
+    // rows from the root duration's table (appended on the compute stream, ev_tab), never the root's
+    // output buffers, which the next push overwrites.
+    hipStream_t lstream = nullptr;
+    hipEvent_t ev_tab = nullptr, ev_lchk = nullptr;
     // the queued events' bucket range after the last device push, measured behind it on the stream
     // (k_pend_bucket_range, read at the next push once ev_pr completed): the next push places its band
     // from it without a probe round trip
@@ -201,14 +207,19 @@ struct sh_aggregation {
 static int agg_verify(sh_aggregation* a) {
     if (!a->chk_pending) return SH_OK;
     a->chk_pending = false;
+    HIPCHK(sh_wait_event(a->ev_lchk));
     for (auto& L : a->levels) RCHK(L.kt.check_result(L.chk));
     return SH_OK;
 }
 
 static int agg_sync(sh_aggregation* a) {
     HIPCHK(sh_wait_stream(a->ctx->stream));
+    if (a->lstream) HIPCHK(sh_wait_stream(a->lstream));
     return agg_verify(a);
 }
+
+// the stream of the roll-up levels' work
+static hipStream_t lvl(const sh_aggregation* a) { return a->lstream ? a->lstream : a->ctx->stream; }
 
 static LevelDev level_dev(Level& L, int nb) {
     LevelDev D;
@@ -226,9 +237,11 @@ static LevelDev level_dev(Level& L, int nb) {
 static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
     if (rb.n == 0) return SH_OK;
     TableBuf& t = a->tables[dur];
-    hipStream_t s = a->ctx->stream;
+    hipStream_t s = dur == a->d.min_duration ? a->ctx->stream : lvl(a);
     int64_t need = t.n + rb.n;
     if (need > t.cap) {
+        // (both streams drained: level merges may still read the root table's old block)
+        RCHK(agg_sync(a));
         int64_t ncap = std::max<int64_t>(need, std::max<int64_t>(1024, t.cap * 2));
         DevBuf b2, k2, v2;
         RCHK(b2.reserve(ncap * 8, false));
@@ -242,6 +255,7 @@ static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
                                       t.n * 8, hipMemcpyDeviceToDevice, s));
         }
         HIPCHK(hipStreamSynchronize(s));
+        StreamScope _sc(s);
         t.bucket = std::move(b2); t.key = std::move(k2); t.vals = std::move(v2);
         t.cap = ncap;
     }
@@ -258,7 +272,8 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
 // dispatchEvent (:201-258) + cleanBaseIncrementalValueStore (:260-266)
 static int level_dispatch(sh_aggregation* a, size_t li, int64_t start_of_new) {
     Level& L = a->levels[li];
-    hipStream_t s = a->ctx->stream;
+    hipStream_t s = lvl(a);
+    StreamScope _sc(s);
     if (L.processed) {
         int64_t n_in = L.n_in;
         int nblk = (int)((n_in + kTile - 1) / kTile);
@@ -304,7 +319,8 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
         if (li + 1 < a->levels.size()) RCHK(level_timer(a, li + 1, L.start));
     }
     if (rb.n > 0) {
-        hipStream_t s = a->ctx->stream;
+        hipStream_t s = lvl(a);
+        StreamScope _sc(s);
         RCHK(L.slots.reserve(rb.n * 4, false));
         L.epoch++;
         if (L.n_in + rb.n >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "too many rows in one roll-up bucket");
@@ -377,9 +393,22 @@ static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
             launch_fill_i64(a->ctx->stream, a->root_bucket_col.as<int64_t>(), rb.n, s_f);
             rb.bucket = a->root_bucket_col.as<int64_t>();
         }
+        const int64_t n0 = a->tables[a->d.min_duration].n;
         RCHK(table_append(a, a->d.min_duration, rb));
         if (!a->levels.empty()) {
-            RCHK(level_rows(a, 0, rb, s_f));
+            // the level stream reads the rows from the root table's copy, once it is written
+            const TableBuf& t = a->tables[a->d.min_duration];
+            RowBatch tb;
+            tb.n = rb.n;
+            tb.cap = t.cap;
+            tb.bucket = t.bucket.as<int64_t>() + n0;
+            tb.key = t.key.as<int64_t>() + n0;
+            tb.vals = t.vals.as<u64>() + n0;
+            if (a->lstream && rb.n > 0) {
+                HIPCHK(hipEventRecord(a->ev_tab, a->ctx->stream));
+                HIPCHK(hipStreamWaitEvent(a->lstream, a->ev_tab, 0));
+            }
+            RCHK(level_rows(a, 0, rb.n > 0 ? tb : rb, s_f));
             RCHK(level_timer(a, 0, s_f + T));
         }
         a->root_bucket = s_f + T;
@@ -508,6 +537,9 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     }
     HIPCHK(hipEventCreate(&a->ev0));
     HIPCHK(hipEventCreate(&a->ev1));
+    HIPCHK(hipStreamCreateWithFlags(&a->lstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&a->ev_tab, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&a->ev_lchk, hipEventDisableTiming));
     // constant key / bucket columns for rows without them
     RCHK(a->minmax.reserve(minmax_scratch_bytes(), false));
     HIPCHK(hipHostMalloc((void**)&a->h_minmax, 16, hipHostMallocDefault));
@@ -554,6 +586,7 @@ extern "C" int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_des
 }
 
 static void agg_free(sh_aggregation* a) {
+    if (a->lstream) (void)hipStreamSynchronize(a->lstream);
     for (auto& L : a->levels) {
         DevBuf* bufs[] = {&L.vals, &L.tag, &L.first_seq, &L.order, &L.slots, &L.dup, &L.blk, &L.out_bucket, &L.out_key, &L.out_vals};
         for (auto* b : bufs) b->release();
@@ -570,6 +603,12 @@ static void agg_free(sh_aggregation* a) {
     a->pr_dev.release();
     if (a->h_pr) (void)hipHostFree(a->h_pr);
     if (a->ev_pr) (void)hipEventDestroy(a->ev_pr);
+    if (a->ev_tab) (void)hipEventDestroy(a->ev_tab);
+    if (a->ev_lchk) (void)hipEventDestroy(a->ev_lchk);
+    if (a->lstream) {
+        (void)hipStreamSynchronize(a->lstream);
+        (void)hipStreamDestroy(a->lstream);
+    }
     if (a->ev0) (void)hipEventDestroy(a->ev0);
     if (a->ev1) (void)hipEventDestroy(a->ev1);
     for (int i = 0; i < sh_aggregation::kRing; i++) {
@@ -766,8 +805,13 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     RCHK(pend_range_queue(a));
     RCHK(agg_after_root(a, o));
     SH_TMARK(8);
-    HIPCHK(hipEventRecord(a->ev1, a->ctx->stream));
-    HIPCHK(hipEventRecord(a->r1[rk], a->ctx->stream));
+    // the push's end: its root work (compute stream) and its level work (level stream)
+    if (a->lstream) {
+        HIPCHK(hipEventRecord(a->ev_tab, a->ctx->stream));
+        HIPCHK(hipStreamWaitEvent(a->lstream, a->ev_tab, 0));
+    }
+    HIPCHK(hipEventRecord(a->ev1, lvl(a)));
+    HIPCHK(hipEventRecord(a->r1[rk], lvl(a)));
     a->r_next++;
     a->last_events = dev.n;
     a->timed = true;
@@ -794,6 +838,7 @@ extern "C" int sh_aggregation_timing(sh_aggregation* a, double* total_ms, int64_
 extern "C" int sh_aggregation_stats(sh_aggregation* a, sh_stats* out) {
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_stats: NULL argument");
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     *out = sh_stats{};
     if (!a->timed) return SH_OK;
     HIPCHK(hipEventSynchronize(a->ev1));
@@ -821,10 +866,11 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
     // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
     for (auto& L : a->levels) {
         if (!L.dirty) continue;
-        RCHK(L.kt.check_async(a->ctx->stream, L.chk));
+        RCHK(L.kt.check_async(lvl(a), L.chk));
         L.dirty = false;
         a->chk_pending = true;
     }
+    if (a->chk_pending) HIPCHK(hipEventRecord(a->ev_lchk, lvl(a)));
     return SH_OK;
 }
 
@@ -859,10 +905,11 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
     for (auto& L : a->levels) {
         if (!L.dirty) continue;
-        RCHK(L.kt.check_async(a->ctx->stream, L.chk));
+        RCHK(L.kt.check_async(lvl(a), L.chk));
         L.dirty = false;
         a->chk_pending = true;
     }
+    if (a->chk_pending) HIPCHK(hipEventRecord(a->ev_lchk, lvl(a)));
     return SH_OK;
 }
 
@@ -870,6 +917,7 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
     SH_RANGE("sh_aggregation_table");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_table: NULL argument");
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (dur < a->d.min_duration || dur > a->d.max_duration) return sh_fail(SH_ERR_INVALID, "duration not aggregated");
     TableBuf& t = a->tables[dur];
     hipStream_t s = a->ctx->stream;
@@ -961,6 +1009,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
     SH_RANGE("sh_aggregation_find");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_find: NULL argument");
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (per < a->d.min_duration || per > a->d.max_duration)
         return sh_fail(SH_ERR_INVALID, "the aggregation does not contain the `per` duration");
     hipStream_t s = a->ctx->stream;
@@ -1198,6 +1247,7 @@ extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap
     SH_RANGE("sh_aggregation_snapshot");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is checkpointed by sh_shard_snapshot");
     ABlob w;
     RCHK(agg_snapshot_blob(a, w));
@@ -1279,6 +1329,7 @@ static int agg_state_read(sh_aggregation* a, AReader& r) {
 // The sharded aggregation's sections after the shard's blob (sh_snapshot.cpp shard_snapshot_blob):
 // the aggregation's fingerprint, then agg_state_write's sections.
 int agg_shard_state_write(sh_aggregation* a, std::vector<uint8_t>& out) {
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     ABlob w;
     w.val<uint64_t>(agg_fingerprint(a));
     RCHK(agg_state_write(a, w));
@@ -1287,6 +1338,7 @@ int agg_shard_state_write(sh_aggregation* a, std::vector<uint8_t>& out) {
 }
 
 int agg_shard_state_read(sh_aggregation* a, const uint8_t* p, size_t n) {
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     AReader r{p, n};
     if (r.val<uint64_t>() != agg_fingerprint(a) || !r.ok)
         return sh_fail(SH_ERR_INVALID, "snapshot was taken from a different aggregation");
@@ -1300,6 +1352,7 @@ extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_
     SH_RANGE("sh_aggregation_restore");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
+    if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is restored by sh_shard_restore");
     ABlob backup;
     const bool have = agg_snapshot_blob(a, backup) == SH_OK;
