@@ -1,0 +1,32 @@
+#!/bin/bash
+# round-5 C3: key-ordered records (k_sl_kgather), flag-free per-event rows, whole-line record stores
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+P=/tmp/r5c3
+rm -rf $P && mkdir -p $P
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_sliding_minmax.py \
+  "tests/test_gpu_scale.py::test_c3_time_10s_10k_keys_1k_resident_per_key" tests/test_gpu_shard.py \
+  "tests/test_gpu_parity.py" > gpurun_out/r5c3_tests.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error|error" gpurun_out/r5c3_tests.log | head -20; tail -30 gpurun_out/r5c3_tests.log; exit 1; }
+tail -3 gpurun_out/r5c3_tests.log
+for kg in 1 0; do
+  SH_SL_KGATHER=$kg timeout -k 10 300 python -u bench.py --workload c3 --steps 5 --warmup 2 > gpurun_out/r5c3_kg$kg.json 2>gpurun_out/r5c3.err || { echo "c3 failed"; tail -5 gpurun_out/r5c3.err; exit 1; }
+  echo "kgather=$kg $(python3 -c "import json;d=json.load(open('gpurun_out/r5c3_kg$kg.json'));print(d['value'], d['ms_per_step'])")"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/c3 -o run -- python3 bench.py --workload c3 --steps 3 --warmup 1 > /dev/null 2>$P/c3.err || { echo "c3 prof failed"; tail -5 $P/c3.err; exit 1; }
+python3 - $P/c3 > gpurun_out/r5c3_kernel_stats.txt <<'PY'
+import csv, sys, glob
+f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)
+for r in csv.DictReader(open(f[0])):
+    if "at::native" in r["Name"]:
+        continue
+    print(f"{r['Name'].split('(')[0][:70]:70s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:9.1f} us")
+PY
+head -14 gpurun_out/r5c3_kernel_stats.txt
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $ctr -d $P/c3_$ctr -o run --output-format csv -- python3 bench.py --workload c3 --steps 2 --warmup 1 > /dev/null 2>$P/c3_$ctr.err || { echo "c3 $ctr failed"; exit 1; }
+done
+python3 scripts/pmc_summary.py "$(ls $P/c3_FETCH_SIZE/*/run_counter_collection.csv $P/c3_FETCH_SIZE/run_counter_collection.csv 2>/dev/null | head -1)" \
+  "$(ls $P/c3_WRITE_SIZE/*/run_counter_collection.csv $P/c3_WRITE_SIZE/run_counter_collection.csv 2>/dev/null | head -1)" > gpurun_out/r5c3_pmc.json || echo "pmc summary failed"
+head -c 1500 gpurun_out/r5c3_pmc.json
+echo done

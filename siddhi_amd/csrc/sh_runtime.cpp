@@ -227,6 +227,7 @@ Tuning Tuning::from_env() {
     // C5's Zipf partitions (one sequential lane per partition serialises the hot one); SH_PL_SORT=0 walks
     t.pl_sort = !getenv("SH_PL_SORT") || on("SH_PL_SORT");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
+    t.sl_kgather = !getenv("SH_SL_KGATHER") || on("SH_SL_KGATHER");
     return t;
 }
 

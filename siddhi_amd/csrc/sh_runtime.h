@@ -225,10 +225,11 @@ struct SlidingImpl;
 // A/B switches of the measured alternatives, read from the environment once per query,
 // when it is created, so a process can run queries with different settings side by side:
 // SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n,
-// SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower)
+// SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower), SH_SL_KGATHER=0
 struct Tuning {
     bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
     bool pl_sort = true;   // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
+    bool sl_kgather = true;  // keyed sliding replay over key-ordered records (k_sl_kgather); SH_SL_KGATHER=0: rank list
     int agg_band_rows = 8;
     static Tuning from_env();
 };

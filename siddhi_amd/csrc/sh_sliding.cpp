@@ -359,6 +359,10 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     int64_t n_rows = 0;
     if (M > 0) {
         const int na = q->ap.n;
+        const bool keyed = keyed_aos(q);
+        // per-event sends through the keyed replay: every record opens its own row, so there are no
+        // first-occurrence flags to write, count or scan (n_rows = M)
+        const bool all_rows = keyed && send_size == 1;
         // rows indexed by first-occurrence rank
         RCHK(s->flags.reserve(M + 16, false));
         RCHK(s->rows_ts.reserve(M * 8, false));
@@ -368,12 +372,11 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         RCHK(s->rows_clock.reserve(M * 8, false));
         RCHK(s->rows_vals.reserve((size_t)na * M * 8, false));
         RCHK(s->rows_nulls.reserve((size_t)na * M, false));
-        HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
+        if (!all_rows) HIPCHK(hipMemsetAsync(s->flags.p, 0, M, st));
         SlRows rows{s->rows_ts.as<int64_t>(), s->rows_rep.as<u32>(), s->rows_slot.as<u32>(), s->rows_send.as<int64_t>(),
                     s->rows_clock.as<int64_t>(), s->rows_vals.as<u64>(), s->rows_nulls.as<unsigned char>(), M};
         // the common shape (count / sum / avg / min / max of one double column, time window): records
         // sorted stably by key, one lane per key (k_sl_key); other shapes: key-partition replay
-        const bool keyed = keyed_aos(q);
         if (keyed) {
             HIPCHK(hipEventRecord(q->ev_agg0, st));  // the sort is part of the replay's time
             size_t tb = 0;
@@ -389,9 +392,12 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
             RCHK(s->p_pm.reserve(M * 8, false));
             RCHK(s->p_vals.reserve(M * 8, false));
             RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na) * 8, false));
+            if (q->tune.sl_kgather) RCHK(s->rec_aosk.reserve((size_t)M * kSlAosWords * 8, false));
             launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
                                  rec, s->p_pm.as<int64_t>(), s->p_vals.as<u64>(), state_of(s), q->ap,
-                                 q->d.window_param, send_size, send_base, s->rows_k.as<u64>(), s->flags.as<unsigned char>());
+                                 q->d.window_param, send_size, send_base, s->rows_k.as<u64>(),
+                                 all_rows ? nullptr : s->flags.as<unsigned char>(),
+                                 q->tune.sl_kgather ? s->rec_aosk.as<u64>() : nullptr, M);
         } else {
             // stable split of the records by key partition
             int P = s->P;
@@ -423,14 +429,15 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         // emit in rank order
         int fblk = (int)((M + kTile - 1) / kTile);
         RCHK(s->blk_cnt.reserve((fblk + 16) * 8, false));
-        launch_count_flags(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk);
-        std::vector<int64_t> bc(fblk);
-        HIPCHK(hipMemcpyAsync(bc.data(), s->blk_cnt.p, fblk * 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, q->ev_agg0, q->ev_agg1);
-        q->stats.main_kernel_ms = ms;
-        for (auto c : bc) n_rows += c;
+        if (all_rows) {
+            n_rows = M;
+        } else {
+            launch_count_flags(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk);
+            std::vector<int64_t> bc(fblk);
+            HIPCHK(hipMemcpyAsync(bc.data(), s->blk_cnt.p, fblk * 8, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (auto c : bc) n_rows += c;
+        }
         int nk = q->kp.n;
         int64_t cap = std::max<int64_t>(n_rows, 1);
         RCHK(s->out_ts.reserve(cap * 8, false));
@@ -443,9 +450,9 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         RCHK(s->out_rep.reserve(cap * 8, false));
         HIPCHK(hipMemsetAsync(s->out_expired.p, 0, cap, st));
         if (want_order) RCHK(q->out_order.reserve(cap * 8, false));
-        launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
+        if (!all_rows) launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
         if (keyed)
-            launch_slk_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk,
+            launch_slk_emit(st, all_rows ? nullptr : s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk,
                             s->rows_k.as<u64>(), sliding_keyed_row_words(na), na, q->kt.dev(), q->kp, cap,
                             s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                             s->out_nulls.as<unsigned char>(), send_size == 1 ? nullptr : s->out_send.as<int64_t>(),
@@ -468,6 +475,11 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
     float ms = 0;
     (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
     q->stats.push_ms = ms;
+    if (M > 0) {
+        float ams = 0;
+        (void)hipEventElapsedTime(&ams, q->ev_agg0, q->ev_agg1);
+        q->stats.main_kernel_ms = ams;
+    }
     q->stats.main_kernel_bytes = M * (int64_t)(4 + 8 + 8 + 8 + 8 * q->ap.n_vcols) + n_rows * (int64_t)(8 + 8 * q->ap.n);
     return sliding_output(q, n_rows, n_flushes, want_order, host_out, out);
 }

@@ -69,9 +69,11 @@ int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u
                     hipStream_t s);
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
                           SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
-                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags);
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags, u64* aosk = nullptr,
+                          i64 M = 0);
 int sliding_keyed_row_words(int n_aggs);
-// rowsK: the keyed replay's rows at the stream rank of their first record
+// rowsK: the keyed replay's rows at the stream rank of their first record (flags NULL: per-event sends,
+// every rank holds a row)
 void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,

@@ -163,12 +163,16 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
                                                           const i64* blk_pm_pre, i64 pm0, SlRecords rec,
                                                           u32* slot_cnt, i64* send_clock) {
     __shared__ u32 tk[kSlotTab], tc[kSlotTab];
+    // the wave's 64 records staged in LDS, then stored as contiguous 16-byte pieces (each store
+    // instruction covers 1 KB of whole lines instead of one piece of 64 records 48 bytes apart)
+    __shared__ ulonglong2 stg[kBlock * 3];
     for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
     const i64 tile0 = (i64)blockIdx.x * kTile;
     const i64 r0 = blk_pass_pre[blockIdx.x];
     i64 carry_cm = blk_tl_pre[blockIdx.x];
     i64 carry_pm = max(blk_pm_pre[blockIdx.x], pm0);
     const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
+    const int lane = threadIdx.x & 63, wb = threadIdx.x & ~63;
     for (int it = 0; it < kItems; it++) {
         const i64 e = tile0 + (i64)it * kBlock + threadIdx.x;
         const bool in = e < wp.N;
@@ -177,19 +181,36 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
         const u64 v = in ? (u64)load_raw(cols, ap.vcol_src[0], e) : 0ull;
         i64 tot;
         const i64 incl = max(block_excl_scan(t, MaxOp(), INT64_MIN, &tot), t);
-        if (in) {
+        if (rec.aos) {
+            // (every event of the tile passes: record r0 + it * kBlock + thread; the wave's run is whole
+            // records r_w .. r_w + 63, fewer at the push's end)
+            const i64 pmx = max(carry_pm, incl);
+            const i64 sclk = max(c0, max(carry_cm, incl));
+            const i64 r = r0 + (i64)it * kBlock + threadIdx.x;
+            if (in) {
+                if (send_clock) send_clock[r] = sclk;
+                rec.raw[r] = (u32)e;
+                rec.slot[r] = pos;
+                slot_tab_add(tk, tc, pos);
+            }
+            stg[threadIdx.x * 3 + 0] = make_ulonglong2((u64)sclk, (u64)pmx);
+            stg[threadIdx.x * 3 + 1] = make_ulonglong2((u64)t, v);
+            stg[threadIdx.x * 3 + 2] = make_ulonglong2((u64)e, 0ull);
+            __syncthreads();
+            const i64 rw = r0 + (i64)it * kBlock + wb;  // the wave's first record
+            const i64 ew = tile0 + (i64)it * kBlock + wb;
+            const int nw = (int)max((i64)0, min((i64)64, wp.N - ew));
+            ulonglong2* dst = (ulonglong2*)(rec.aos + (size_t)rw * kSlAosWords);
+            for (int q = lane; q < nw * 3; q += 64) dst[q] = stg[wb * 3 + q];
+            __syncthreads();
+        } else if (in) {
             const i64 pmx = max(carry_pm, incl);
             const i64 sclk = max(c0, max(carry_cm, incl));
             const i64 r = r0 + (i64)it * kBlock + threadIdx.x;
             if (send_clock) send_clock[r] = sclk;
             rec.raw[r] = (u32)e;
             rec.slot[r] = pos;
-            if (rec.aos) {
-                ulonglong2* o = (ulonglong2*)(rec.aos + (size_t)r * kSlAosWords);
-                o[0] = make_ulonglong2((u64)sclk, (u64)pmx);
-                o[1] = make_ulonglong2((u64)t, v);
-                o[2] = make_ulonglong2((u64)e, 0ull);
-            } else {
+            {
                 rec.clock[r] = sclk;
                 rec.pm[r] = pmx;
                 rec.ts[r] = t;
@@ -1634,7 +1655,7 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                                                u64* __restrict__ g_v, SlState S, DFields fd, KOut ko, i64 T,
                                                u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
-                                               unsigned char* __restrict__ flags) {
+                                               unsigned char* __restrict__ flags, const u64* __restrict__ aosk) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ int di_min[HMIN ? kDqK : 1];
@@ -1651,8 +1672,13 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     const u64* rval = S.rval + (size_t)k * S.rc;
     const int rh0 = (int)(S.rhead[k] & gm), H0 = (int)S.rlen[k];
     const int n = (int)(b - a), HN = H0 + n;
-    auto head_pm = [&](int h) -> i64 { return h < H0 ? rpm[(rh0 + h) & gm] : g_pm[a + (h - H0)]; };
-    auto head_v = [&](int h) -> u64 { return h < H0 ? rval[(rh0 + h) & gm] : g_v[a + (h - H0)]; };
+    // aosk: the records already in key order (k_sl_kgather), their PM and value read in place; otherwise
+    // they are read through the sort's rank list and the key-order PM / value columns written here
+    const bool kord = aosk != nullptr;
+    auto run_pm = [&](u32 j) -> i64 { return kord ? (i64)aosk[(size_t)j * kSlAosWords + 1] : g_pm[j]; };
+    auto run_v = [&](u32 j) -> u64 { return kord ? aosk[(size_t)j * kSlAosWords + 3] : g_v[j]; };
+    auto head_pm = [&](int h) -> i64 { return h < H0 ? rpm[(rh0 + h) & gm] : run_pm(a + (u32)(h - H0)); };
+    auto head_v = [&](int h) -> u64 { return h < H0 ? rval[(rh0 + h) & gm] : run_v(a + (u32)(h - H0)); };
     // the running state: the same in every lane (the sequential part runs wave-uniform)
     i64 cnt = 0;
     double sum = 0.0;
@@ -1683,9 +1709,10 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         u64 x;
         u32 raw, rk;
         {
-            const u32 r = sorted_rank[i];
-            const ulonglong2* rp = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
+            const u32 r0 = kord ? 0u : sorted_rank[i];
+            const ulonglong2* rp = (const ulonglong2*)(kord ? aosk + (size_t)i * kSlAosWords : aos + (size_t)r0 * kSlAosWords);
             const ulonglong2 w0 = rp[0], w1 = rp[1], w2 = rp[2];
+            const u32 r = kord ? (u32)w2.y : r0;  // the record's stream rank
             clk = (i64)w0.x;
             ts = (i64)w1.x;
             x = w1.y;
@@ -1696,9 +1723,11 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             const bool fst = send_size == 1 || (o0 + lane == 0) || (send_size == 0 ? false : pr / send_size != raw / send_size);
             rk = r | (fst ? kFirstBit : 0u);
             if (in) {
-                g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
-                g_v[i] = x;
-                flags[r] = fst ? 1 : 0;
+                if (!kord) {
+                    g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
+                    g_v[i] = x;
+                }
+                if (flags) flags[r] = fst ? 1 : 0;  // (per-event sends: every record opens its row, no flags)
             }
             s_x[lane] = x;
             prev_raw = __shfl(raw, m - 1, 64);
@@ -1857,7 +1886,9 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
             w[3] = (u64)send | ((u64)nulls << 56);
             // the row lands at the stream rank of its first record, so the emission reads the rows in
             // stream order (whole lines) instead of gathering them from key order
-            const u32 row_rank = grp == o0 + lane ? (rk & ~kFirstBit) : sorted_rank[a + (u32)grp];
+            const u32 row_rank = grp == o0 + lane ? (rk & ~kFirstBit)
+                                 : kord ? (u32)aosk[(size_t)(a + (u32)grp) * kSlAosWords + 5]
+                                        : sorted_rank[a + (u32)grp];
             ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row_rank * RW);
 #pragma unroll
             for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
@@ -1875,8 +1906,8 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     u64* wval = S.rval + (size_t)k * S.rc;
     for (int j = j0 + lane; j < HN; j += 64) {
         const int sl = (rh + keep + (j - j0)) & gm;
-        wpm[sl] = g_pm[a + (j - H0)];
-        wval[sl] = g_v[a + (j - H0)];
+        wpm[sl] = run_pm(a + (u32)(j - H0));
+        wval[sl] = run_v(a + (u32)(j - H0));
     }
     if (lane == 0) {
         S.cnt[k] = cnt;
@@ -1903,14 +1934,19 @@ __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __rest
                                                     const u32* __restrict__ rank_raw, i64 raw_base, i64* out_order,
                                                     i64* out_rep) {
     const i64 tile = (i64)blockIdx.x * kTile;
-    i64 run = blk_pre[blockIdx.x];
+    i64 run = flags ? blk_pre[blockIdx.x] : tile;
     for (int it = 0; it < kItems; it++) {
         const i64 j = tile + (i64)it * kBlock + threadIdx.x;
-        const i64 fl = j < n ? flags[j] : 0;
-        i64 tot;
-        const i64 r = run + block_excl_scan(fl, SumOp(), 0, &tot);
-        run += tot;
-        if (!fl) continue;
+        i64 r = j;
+        if (flags) {
+            const i64 fl = j < n ? flags[j] : 0;
+            i64 tot;
+            r = run + block_excl_scan(fl, SumOp(), 0, &tot);
+            run += tot;
+            if (!fl) continue;
+        } else if (j >= n) {
+            continue;  // (per-event sends: every record's rank holds a row)
+        }
         const u64* src = rowsK + (size_t)j * RW;
         u64 w[4 + SH_MAX_AGGS];
 #pragma unroll
@@ -1953,9 +1989,25 @@ bool sliding_keyed_ok(AggPlan ap) {
 
 int sliding_keyed_row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
 
+// The 48-byte records in key order (sorted_rank[i] = the stream rank of key-order record i), each
+// carrying its stream rank in its last word: the replay then streams every key's run instead of
+// chasing the rank list with random reads (r04: 11.3 GB of HBM traffic per C3 push in k_sl_wkey).
+__global__ __launch_bounds__(kBlock) void k_sl_kgather(const u32* __restrict__ sorted_rank, i64 M,
+                                                      const u64* __restrict__ aos, u64* __restrict__ aosk) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const u32 r = sorted_rank[i];
+    const ulonglong2* src = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
+    const ulonglong2 w0 = src[0], w1 = src[1], w2 = src[2];
+    ulonglong2* dst = (ulonglong2*)(aosk + (size_t)i * kSlAosWords);
+    dst[0] = w0;
+    dst[1] = w1;
+    dst[2] = make_ulonglong2(w2.x, (u64)r);
+}
+
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
                           SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
-                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags) {
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags, u64* aosk, i64 M) {
     DFields fd;
     own_d_fields(ap, fd);
     KOut ko{};
@@ -1970,9 +2022,12 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
     const int RW = sliding_keyed_row_words(ap.n);
+    if (aosk && M > 0)
+        hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank, M,
+                           rec.aos, aosk);
 #define SH_SL_W(A, B, C)                                                                                            \
     hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_pm, g_v, S, fd, ko, \
-                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags)
+                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags, aosk)
     if (hs && hn && hx) SH_SL_W(true, true, true);
     else if (hs && !hn && !hx) SH_SL_W(true, false, false);
     else if (!hs && hn && hx) SH_SL_W(false, true, true);
