@@ -227,7 +227,9 @@ Tuning Tuning::from_env() {
     // C5's Zipf partitions (one sequential lane per partition serialises the hot one); SH_PL_SORT=0 walks
     t.pl_sort = !getenv("SH_PL_SORT") || on("SH_PL_SORT");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
-    t.sl_kgather = !getenv("SH_SL_KGATHER") || on("SH_SL_KGATHER");
+    // the gather of the records into key order costs more than the replay saves (C3 3.01e9 vs 3.36e9
+    // events/s: k_sl_kgather 1.32 ms moving 7.1 GB, k_sl_wkey 6.4 -> 6.1 ms; profiles/r05_c3_*)
+    t.sl_kgather = on("SH_SL_KGATHER");
     return t;
 }
 

@@ -229,7 +229,7 @@ struct SlidingImpl;
 struct Tuning {
     bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
     bool pl_sort = true;   // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
-    bool sl_kgather = true;  // keyed sliding replay over key-ordered records (k_sl_kgather); SH_SL_KGATHER=0: rank list
+    bool sl_kgather = false;  // keyed sliding replay over key-ordered records (k_sl_kgather, SH_SL_KGATHER=1): measured slower
     int agg_band_rows = 8;
     static Tuning from_env();
 };
