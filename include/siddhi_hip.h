@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 9
+#define SH_ABI_VERSION 10
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -261,6 +261,17 @@ int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
  * externalTimeBatch query with current-events output (all events without group-by: every emission
  * ends in current events, QuerySelector.processInBatchNoGroupBy keeps that row). ms == 0 is no timeout. */
 int sh_query_set_ext_timeout(sh_query* q, int64_t ms);
+
+/* externalTimeBatch's fifth parameter, replaceTimestampWithBatchEndTime (ExternalTimeBatchWindowProcessor.java:
+ * 210-220, cloneAppend :446-456; `externalTimeBatch(ts, 1 sec, 0, 100, true)`): the window's copy of every event
+ * carries its batch's end time in the timestamp attribute (ts_col), so the output events built from the rows'
+ * representative events show the batch end, not the sent value. sh_query_rep_ts_attr returns that attribute for
+ * every row of the last output (host array, valid until the next call on the query); the shim writes it into
+ * the row's select attributes. Set once, before the first push, on an unpartitioned externalTimeBatch query;
+ * aggregators and group keys over the timestamp attribute (which would fold the replaced values) are refused
+ * (SH_ERR_UNSUPPORTED). Replaces the Java window's fifth argument. */
+int sh_query_set_ext_replace_ts(sh_query* q, int32_t on);
+int sh_query_rep_ts_attr(sh_query* q, const int64_t** values, int64_t* n);
 
 /* The text of dictionary ids [first_id, first_id + n) of string column `col`, as UTF-16 code units (what a
  * java.lang.String holds): id first_id + i is units[offsets[i] .. offsets[i + 1]) (offsets has n + 1

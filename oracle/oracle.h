@@ -12,6 +12,8 @@ void* or_query_create(const sh_query_desc* desc);
 void or_query_destroy(void* q);
 int or_query_set_output_rate(void* q, int32_t kind, int64_t n);
 int or_query_set_ext_timeout(void* q, int64_t ms);
+int or_query_set_ext_replace_ts(void* q, int32_t on);
+int or_query_rep_ts_attr(void* q, const int64_t** values, int64_t* n);
 int or_query_set_strings(void* q, int32_t col, int64_t first_id, int64_t n, const uint16_t* units,
                          const int64_t* offsets);
 int or_push(void* q, const sh_batch* b, const sh_out** out);

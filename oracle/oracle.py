@@ -34,6 +34,8 @@ def lib():
         L.or_query_destroy.argtypes = [C.c_void_p]
         L.or_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
         L.or_query_set_ext_timeout.argtypes = [C.c_void_p, C.c_int64]
+        L.or_query_set_ext_replace_ts.argtypes = [C.c_void_p, C.c_int32]
+        L.or_query_rep_ts_attr.argtypes = [C.c_void_p, P(P(C.c_int64)), P(C.c_int64)]
         L.or_query_set_strings.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
         L.or_push.argtypes = [C.c_void_p, P(abi.Batch), P(P(abi.Out))]
         L.or_advance_time.argtypes = [C.c_void_p, C.c_int64, P(P(abi.Out))]
@@ -61,6 +63,8 @@ class OracleQuery:
             raise ValueError(lib().or_last_error().decode())
         if spec.timeout and lib().or_query_set_ext_timeout(self.h, int(spec.timeout)):
             raise ValueError(lib().or_last_error().decode())
+        if spec.replace_ts and lib().or_query_set_ext_replace_ts(self.h, 1):
+            raise ValueError(lib().or_last_error().decode())
         for col, names in (spec.strings or {}).items():
             self.set_strings(col, names)
 
@@ -87,6 +91,13 @@ class OracleQuery:
 
     def advance_time(self, now: int):
         return abi.decode_out(self.advance_time_raw(now))
+
+    def rep_ts_attr(self):
+        """The timestamp attribute of every row's representative event in the last output."""
+        import numpy as np
+        v, n = C.POINTER(C.c_int64)(), C.c_int64()
+        lib().or_query_rep_ts_attr(self.h, C.byref(v), C.byref(n))
+        return np.ctypeslib.as_array(v, shape=(n.value,)).copy() if n.value else np.zeros(0, np.int64)
 
     def close(self):
         if self.h:

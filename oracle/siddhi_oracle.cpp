@@ -349,23 +349,24 @@ struct OutRow {
     int64_t ts; uint8_t expired; int64_t keys[SH_MAX_GROUP];
     uint64_t vals[SH_MAX_AGGS]; uint8_t nulls[SH_MAX_AGGS];
     int64_t rep;  // stream index of the event the row was built from
+    int64_t rep_attr;  // externalTimeBatch: that event's timestamp attribute as the window holds it
 };
 struct OutBuf {
     std::vector<int64_t> flush_offsets{0};
     std::vector<int64_t> flush_clock;
     std::vector<OutRow> rows;
     // flattened views for sh_out
-    std::vector<int64_t> ts, keys, rep; std::vector<uint8_t> expired, nulls; std::vector<uint64_t> vals;
+    std::vector<int64_t> ts, keys, rep, rep_attr; std::vector<uint8_t> expired, nulls; std::vector<uint64_t> vals;
     bool with_rep = true;  // aggregation tables carry no representative event (sh_out.rep NULL)
     sh_out out{};
     void clear() { flush_offsets.assign(1, 0); flush_clock.clear(); rows.clear(); }
     void close_flush(int64_t clock) { flush_offsets.push_back((int64_t)rows.size()); flush_clock.push_back(clock); }
     const sh_out* view(int nk, int nv, const int* vtypes) {
         int64_t n = (int64_t)rows.size();
-        ts.resize(n); expired.resize(n); keys.assign((size_t)nk * n, 0); rep.resize(n);
+        ts.resize(n); expired.resize(n); keys.assign((size_t)nk * n, 0); rep.resize(n); rep_attr.resize(n);
         vals.assign((size_t)nv * n, 0); nulls.assign((size_t)nv * n, 0);
         for (int64_t r = 0; r < n; r++) {
-            ts[r] = rows[r].ts; expired[r] = rows[r].expired; rep[r] = rows[r].rep;
+            ts[r] = rows[r].ts; expired[r] = rows[r].expired; rep[r] = rows[r].rep; rep_attr[r] = rows[r].rep_attr;
             for (int k = 0; k < nk; k++) keys[k * n + r] = rows[r].keys[k];
             for (int v = 0; v < nv; v++) { vals[v * n + r] = rows[r].vals[v]; nulls[v * n + r] = rows[r].nulls[v]; }
         }
@@ -514,6 +515,7 @@ struct Query {
     // TimeBatchWindowProcessor.nextEmitTime is a processor field shared by all partitions (:128)
     int64_t next_emit_time = -1;
     int64_t ext_timeout = 0;  // externalTimeBatch(ts, T, start, timeout): schedulerTimeout
+    bool ext_replace = false;  // externalTimeBatch(ts, T, start, timeout, true): replaceTimestampWithBatchEndTime
     int64_t seq_base = 0;  // stream index of the current push's first event
     std::unordered_map<int64_t, std::unique_ptr<PartitionState>> parts;  // partition flow id -> state
     // Scheduler.stateHolder (PartitionSyncStateHolder -> PartitionStateHolder.states, a
@@ -606,6 +608,7 @@ struct Query {
                 bool q = (ev.type == CURRENT && d.current_on) || (ev.type == EXPIRED && d.expired_on);
                 if (!q) continue;
                 OutRow row{}; row.ts = ev.ts; row.expired = ev.type == EXPIRED; row.rep = ev.seq;
+                row.rep_attr = d.window == SH_WIN_EXT_TIME_BATCH ? ev.raw[d.ts_col] : 0;
                 out.rows.push_back(row); any = true;
             }
             if (any) close_chunk(ps, start);
@@ -619,6 +622,7 @@ struct Query {
                 for (int g = 0; g < d.n_group_by; g++) key.k[g] = key_raw(schema, ev, d.group_by[g]);
                 OutRow row{};
                 row.ts = ev.ts; row.expired = ev.type == EXPIRED; row.rep = ev.seq;
+                row.rep_attr = d.window == SH_WIN_EXT_TIME_BATCH ? ev.raw[d.ts_col] : 0;
                 for (int g = 0; g < d.n_group_by; g++) row.keys[g] = key.k[g];
                 for (size_t a = 0; a < aggs.size(); a++) {
                     auto& states = ps.agg_states[a];
@@ -846,8 +850,11 @@ struct Query {
         ps.ext_sched = clock + ext_timeout;
         notify_at(ps, ps.ext_sched);
     }
+    // cloneAppend (:446-456): the window's copy carries endTime in the timestamp attribute when
+    // replaceTimestampWithBatchEndTime is set (the RESET event is a copy of the original)
     void ext_append(PartitionState& ps, const OEvent& ev) {
         ps.ext_current.push_back(ev);
+        if (ext_replace) ps.ext_current.back().raw[d.ts_col] = ps.ext_end;
         if (!ps.ext_has_reset) { ps.ext_reset = ev; ps.ext_reset.type = RESET; ps.ext_has_reset = true; }
     }
     void ext_time_batch(PartitionState& ps, Chunk& in) {
@@ -1426,6 +1433,26 @@ int or_query_set_ext_timeout(void* h, int64_t ms) {
         return SH_ERR_INVALID;
     }
     q->ext_timeout = ms;
+    return SH_OK;
+}
+
+// externalTimeBatch's 5th parameter (ExternalTimeBatchWindowProcessor :210-220): replaceTimestampWithBatchEndTime
+int or_query_set_ext_replace_ts(void* h, int32_t on) {
+    Query* q = (Query*)h;
+    if (q->d.window != SH_WIN_EXT_TIME_BATCH) {
+        g_err = "replaceTimestampWithBatchEndTime needs an externalTimeBatch window";
+        return SH_ERR_INVALID;
+    }
+    q->ext_replace = on != 0;
+    return SH_OK;
+}
+
+// the timestamp attribute of every row's representative event in the last output (the batch end time
+// under replaceTimestampWithBatchEndTime)
+int or_query_rep_ts_attr(void* h, const int64_t** values, int64_t* n) {
+    Query* q = (Query*)h;
+    *values = q->out.rep_attr.data();
+    *n = (int64_t)q->out.rep_attr.size();
     return SH_OK;
 }
 

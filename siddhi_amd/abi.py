@@ -176,6 +176,7 @@ class QuerySpec:
     ts_attr: Optional[str] = None      # externalTimeBatch timestamp attribute
     start_attr: Optional[str] = None   # externalTimeBatch start time from this attribute
     timeout: Optional[int] = None      # externalTimeBatch(ts, T, start, timeout): scheduler timeout (ms)
+    replace_ts: bool = False           # externalTimeBatch(..., timeout, true): replaceTimestampWithBatchEndTime
     _keep: list = field(default_factory=list, repr=False)
 
     def desc(self) -> QueryDesc:
@@ -369,6 +370,8 @@ def concat_arrays(parts: List[Dict[str, np.ndarray]]) -> Dict[str, np.ndarray]:
            "val_types": parts[0]["val_types"]}
     for k in ("ts", "expired", "rep"):
         res[k] = np.concatenate([p[k] for p in parts])
+    if all("rep_attr" in p for p in parts):
+        res["rep_attr"] = np.concatenate([p["rep_attr"] for p in parts])
     for k in ("keys", "vals", "nulls"):
         res[k] = np.concatenate([p[k] for p in parts], axis=1)
     return res
@@ -393,6 +396,8 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(Out))]
     lib.sh_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
     lib.sh_query_set_ext_timeout.argtypes = [C.c_void_p, C.c_int64]
+    lib.sh_query_set_ext_replace_ts.argtypes = [C.c_void_p, C.c_int32]
+    lib.sh_query_rep_ts_attr.argtypes = [C.c_void_p, P(P(C.c_int64)), P(C.c_int64)]
     lib.sh_aggregation_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
     lib.sh_shard_flush_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.sh_query_set_strings.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p]
@@ -438,7 +443,7 @@ ABI_SYMBOLS = [
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
-    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate", "sh_query_set_ext_timeout", "sh_aggregation_timing", "sh_shard_flush_windows",
+    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate", "sh_query_set_ext_timeout", "sh_query_set_ext_replace_ts", "sh_query_rep_ts_attr", "sh_aggregation_timing", "sh_shard_flush_windows",
     "sh_shard_snapshot", "sh_shard_restore", "sh_query_set_strings",
 ]
 

@@ -271,6 +271,12 @@ struct sh_query {
     // externalTimeBatch timeout (sh_query_set_ext_timeout): lastScheduledTime, and the open batch's
     // passing events since its last emission (the window's currentEventChunk is empty when 0)
     int64_t xt_timeout = 0;
+    // replaceTimestampWithBatchEndTime (sh_query_set_ext_replace_ts): the stream index of the first event
+    // of the last windows, with their number (a row's representative event lies in the last window that
+    // starts at or before it), and the batch end times of the last output's rows
+    bool xt_replace = false;
+    std::vector<std::pair<int64_t, int64_t>> xr_starts;
+    std::vector<int64_t> xr_rep, xr_vals;
     bool xt_Lvalid = false;
     int64_t xt_L = 0;
     int64_t xt_nnew = 0;

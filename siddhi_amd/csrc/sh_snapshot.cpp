@@ -30,7 +30,7 @@ using namespace shd;
 
 namespace {
 
-constexpr uint32_t kVersion = 6;  // 5: band key mode, sharded aggregation sections; 6: timeout / limiter in the fingerprint
+constexpr uint32_t kVersion = 7;  // 5: band key mode, sharded aggregation sections; 6: timeout / limiter in the fingerprint; 7: replaceTimestampWithBatchEndTime
 
 struct Writer {
     std::vector<uint8_t> b;
@@ -91,7 +91,8 @@ uint64_t fingerprint(const sh_query* q) {
     h = fnv(h, d.aggs, sizeof(sh_agg_spec) * d.n_aggs);
     // set after creation but part of the blob's layout: the externalTimeBatch timeout (its scheduler
     // section) and the output rate limiter's kind / per-partition form (their sections)
-    const int64_t extra[] = {q->xt_timeout, q->rate.kind, q->rate.N, q->rate.part, q->rate.pkey, q->rate.lkey};
+    const int64_t extra[] = {q->xt_timeout, q->rate.kind, q->rate.N, q->rate.part, q->rate.pkey, q->rate.lkey,
+                             q->xt_replace};
     h = fnv(h, extra, sizeof(extra));
     h = fnv(h, &q->fp_orig.n, sizeof(int));
     for (int i = 0; i < q->fp_orig.n; i++) {
@@ -174,6 +175,12 @@ int batch_snapshot(sh_query* q, Writer& w) {
         w.val<int64_t>(q->xt_L);
         w.val<int64_t>(q->xt_nnew);
     }
+    // replaceTimestampWithBatchEndTime: the last windows' first events (the batch of a later row's
+    // representative event)
+    if (q->xt_replace) {
+        w.val<uint64_t>(q->xr_starts.size());
+        for (auto& e : q->xr_starts) { w.val<int64_t>(e.first); w.val<int64_t>(e.second); }
+    }
     return SH_OK;
 }
 
@@ -253,6 +260,15 @@ int batch_restore(sh_query* q, Reader& r) {
         q->xt_Lvalid = r.val<uint8_t>();
         q->xt_L = r.val<int64_t>();
         q->xt_nnew = r.val<int64_t>();
+    }
+    if (q->xt_replace) {
+        const uint64_t ns = r.val<uint64_t>();
+        if (!r.ok || ns > 64) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        q->xr_starts.clear();
+        for (uint64_t i = 0; i < ns; i++) {
+            const int64_t a = r.val<int64_t>(), b = r.val<int64_t>();
+            q->xr_starts.emplace_back(a, b);
+        }
     }
     tmp.release();
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");

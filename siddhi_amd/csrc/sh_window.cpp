@@ -1625,6 +1625,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             }
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
+        if (q->xt_replace)  // (the windows start at new events: stream index = seq0 + combined index - queued)
+            for (auto& bd : bounds) q->xr_starts.emplace_back(seq0 + std::max<int64_t>(0, bd.idx - q->n_pend), bd.W);
         if (q->xmode) {
             q->x_stamps.clear();
             if (q->given) {
@@ -1763,7 +1765,71 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
 }
 
 // a push through the query's output rate limiter: device output, then the limiter (sh_rate.cpp)
+// replaceTimestampWithBatchEndTime: the timestamp attribute the window wrote into every row's
+// representative event — the end time E0 + T (W + 1) of its batch W (ExternalTimeBatchWindowProcessor
+// cloneAppend :446-456, findEndTime :440-444) — for sh_query_rep_ts_attr
+static int rep_attr_finish(sh_query* q, const sh_out* o, bool host) {
+    if (!q->xt_replace) return SH_OK;
+    const int64_t n = o->n_rows;
+    q->xr_rep.resize((size_t)n);
+    q->xr_vals.resize((size_t)n);
+    if (n) {
+        if (host) {
+            std::memcpy(q->xr_rep.data(), o->rep, (size_t)n * 8);
+        } else {
+            HIPCHK(hipMemcpyAsync(q->xr_rep.data(), o->rep, (size_t)n * 8, hipMemcpyDeviceToHost, q->ctx->stream));
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        }
+    }
+    const auto& st = q->xr_starts;
+    const int64_t T = q->d.window_param;
+    for (int64_t i = 0; i < n; i++) {
+        auto it = std::upper_bound(st.begin(), st.end(), q->xr_rep[i],
+                                   [](int64_t v, const std::pair<int64_t, int64_t>& e) { return v < e.first; });
+        const int64_t W = it == st.begin() ? 0 : std::prev(it)->second;
+        q->xr_vals[i] = q->E0 + T * (W + 1);
+    }
+    // later rows lie in the open batch or the one before it (expired rows)
+    if (q->xr_starts.size() > 4) q->xr_starts.erase(q->xr_starts.begin(), q->xr_starts.end() - 4);
+    return SH_OK;
+}
+
+extern "C" int sh_query_set_ext_replace_ts(sh_query* q, int32_t on) {
+    if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_replace_ts: NULL query");
+    if (q->d.window != SH_WIN_EXT_TIME_BATCH)
+        return sh_fail(SH_ERR_INVALID, "replaceTimestampWithBatchEndTime needs an externalTimeBatch window");
+    if (q->seq != 0 || q->n_pend != 0 || q->clock_valid)
+        return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_replace_ts: set it before the first push");
+    if (!on) { q->xt_replace = false; return SH_OK; }
+    if (q->kind != 0 || q->d.partition_col >= 0 || q->given || q->internal_keys)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "replaceTimestampWithBatchEndTime runs on unpartitioned externalTimeBatch queries");
+    for (int i = 0; i < q->d.n_group_by; i++)
+        if (q->d.group_by[i] == q->d.ts_col)
+            return sh_fail(SH_ERR_UNSUPPORTED, "replaceTimestampWithBatchEndTime with a group-by on the timestamp attribute");
+    for (int i = 0; i < q->d.n_aggs; i++)
+        if (q->d.aggs[i].fn != SH_AGG_COUNT && q->d.aggs[i].col == q->d.ts_col)
+            return sh_fail(SH_ERR_UNSUPPORTED,
+                           "replaceTimestampWithBatchEndTime with an aggregator over the timestamp attribute");
+    q->xt_replace = true;
+    return SH_OK;
+}
+
+extern "C" int sh_query_rep_ts_attr(sh_query* q, const int64_t** values, int64_t* n) {
+    if (!q || !values || !n) return sh_fail(SH_ERR_INVALID, "sh_query_rep_ts_attr: NULL argument");
+    if (!q->xt_replace) return sh_fail(SH_ERR_INVALID, "sh_query_rep_ts_attr: replaceTimestampWithBatchEndTime is not set");
+    *values = q->xr_vals.data();
+    *n = (int64_t)q->xr_vals.size();
+    return SH_OK;
+}
+
+static int push_any_core(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out);
 static int push_any(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out) {
+    RCHK(push_any_core(q, dev, host_out, out));
+    return rep_attr_finish(q, *out, host_out);
+}
+
+static int push_any_core(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out) {
     if (q->rate.kind != SH_RATE_NONE) {
         const bool sl = q->kind == 1;
         RCHK(sl ? sliding_push(q, dev, false, out) : push_core(q, dev, false, out));
@@ -1867,10 +1933,16 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
     return SH_OK;
 }
 
+static int advance_any(sh_query* q, int64_t now, const sh_out** out);
 extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
     SH_RANGE("sh_advance_time");
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !out) return sh_fail(SH_ERR_INVALID, "sh_advance_time: NULL argument");
+    RCHK(advance_any(q, now, out));
+    return rep_attr_finish(q, *out, true);
+}
+
+static int advance_any(sh_query* q, int64_t now, const sh_out** out) {
     if (q->kind == 1) {
         if (q->rate.kind == SH_RATE_NONE) return sliding_advance(q, now, out, true);
         RCHK(sliding_advance(q, now, out, false));  // the TIMER chunks' rows reach the limiter too

@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 9:
+        if L.sh_abi_version() != 10:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -113,6 +113,8 @@ class GpuQuery:
                 _check(lib().sh_query_set_output_rate(self.h, abi.RATE_KINDS[spec.rate[0]], int(spec.rate[1])))
             if spec.timeout:
                 _check(lib().sh_query_set_ext_timeout(self.h, int(spec.timeout)))
+            if spec.replace_ts:
+                _check(lib().sh_query_set_ext_replace_ts(self.h, 1))
             for col, names in (spec.strings or {}).items():
                 self.set_strings(col, names)
         except Exception:
@@ -203,6 +205,13 @@ class GpuQuery:
         s = abi.Stats()
         _check(lib().sh_query_stats(self.h, C.byref(s)))
         return s
+
+    def rep_ts_attr(self):
+        """replaceTimestampWithBatchEndTime: the timestamp attribute of every row's representative event in
+        the last output — its batch's end time (sh_query_rep_ts_attr)."""
+        v, n = C.POINTER(C.c_int64)(), C.c_int64()
+        _check(lib().sh_query_rep_ts_attr(self.h, C.byref(v), C.byref(n)))
+        return np.ctypeslib.as_array(v, shape=(n.value,)).copy() if n.value else np.zeros(0, np.int64)
 
     def snapshot(self) -> bytes:
         """State.snapshot(): the query's device state as bytes (sh_query_snapshot)."""

@@ -192,6 +192,16 @@ case(name="externalTimeBatch_w17_timeout_not_replaced", source=E + ":1272-1330",
      sends=_login(*[(0, _L0 + t, 3 + i) for i, t in enumerate(_t17x)]) + [{"advance": B + 1000}],
      expect=dict(in_count=4, remove_count=0, values=[[2], [1], [2], [3]],
                  rep_cols=[["timestamp", [_L0 + 4342, _L0 + 5341, _L0 + 14345, _L0 + 24441]]]))
+# test16: the same with replaceTimestampWithBatchEndTime = true (5th parameter, :210-220): cloneAppend
+# (:446-456) writes the batch's endTime into every kept event's timestamp attribute, so each row's
+# `timestamp` is its batch end (% 100 == 0): 805000, 806000 (the crossing event gets the new endTime),
+# 815000 and, at the timeout, 825000
+case(name="externalTimeBatch_w16_timeout_replaced", source=E + ":1214-1270", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_time=0, timeout=100,
+                replace_ts=True, aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, 3 + i) for i, t in enumerate(_t17x)]) + [{"advance": B + 1000}],
+     expect=dict(in_count=4, remove_count=0, values=[[2], [1], [2], [3]],
+                 rep_cols=[["timestamp", [_L0 + 5000, _L0 + 6000, _L0 + 15000, _L0 + 25000]]]))
 
 # ---------------------------------------------------------------- externalTime (ExternalTimeWindowTestCase)
 # sliding over the `timestamp` attribute: 804341/804342 expire at 814341, 814341/814345 at 824341

@@ -58,6 +58,7 @@ def build(case, dic):
                          start_time=q.get("start_time"), stream_current=q.get("stream_current", False),
                          output=q.get("output", "current"), partition=q.get("partition"),
                          ts_attr=q.get("ts_attr"), start_attr=q.get("start_attr"), timeout=q.get("timeout"),
+                         replace_ts=q.get("replace_ts", False),
                          rate=tuple(q["rate"]) if q.get("rate") else None)
     return schema, spec
 
@@ -86,10 +87,15 @@ def run_query(case, make_query):
     q = make_query(spec)
     flushes = []
     for s in case["sends"]:
-        if isinstance(s, dict):
-            flushes += q.advance_time(s["advance"])
-        else:
-            flushes += q.push(batch_of(schema, s, dic))
+        fl = q.advance_time(s["advance"]) if isinstance(s, dict) else q.push(batch_of(schema, s, dic))
+        if spec.replace_ts:
+            # replaceTimestampWithBatchEndTime: the representative events' timestamp attribute as the
+            # window holds it (the batch end time), per row of this call
+            ra, o = list(q.rep_ts_attr()), 0
+            for f in fl:
+                f.rep_attrs = ra[o:o + len(f.rows)]
+                o += len(f.rows)
+        flushes += fl
     return schema, spec, dic, flushes
 
 
@@ -136,7 +142,12 @@ def check_query(case, flushes, schema, dic):
     if "in_order" in e or "remove_order" in e or "rep_cols" in e or "in_col_in" in e:
         assert len(reps) == len(rows), "output without representative events"
 
+    replaced = [x for f in flushes for x in getattr(f, "rep_attrs", [])]
+    ts_attr = case["query"].get("ts_attr") if case["query"].get("replace_ts") else None
+
     def attr(col, idx):
+        if col == ts_attr:
+            return int(replaced[idx])
         return events[reps[idx]][1 + schema.col(col)]
     if "in_order" in e:
         got = [attr(e["in_order_col"], i) for i, r in enumerate(rows) if not r[1]]

@@ -11,11 +11,14 @@ from siddhi_amd import abi
 def run_pushes(q, pushes):
     """pushes: list of HostBatch or ('advance', now). Returns concatenated out_arrays."""
     parts = []
+    replace = getattr(getattr(q, "spec", None), "replace_ts", False)
     for p in pushes:
         if isinstance(p, tuple) and p[0] == "advance":
             parts.append(abi.out_arrays(q.advance_time_raw(p[1])))
         else:
             parts.append(abi.out_arrays(q.push_raw(p)))
+        if replace:  # the batch end time in every row's representative event (replaceTimestampWithBatchEndTime)
+            parts[-1]["rep_attr"] = q.rep_ts_attr()
     return abi.concat_arrays(parts)
 
 
@@ -28,6 +31,8 @@ def assert_same(gpu, ora, rtol=None, label=""):
     assert np.array_equal(gpu["nulls"], ora["nulls"]), f"{label}: null flags differ"
     assert np.array_equal(gpu["expired"], ora["expired"]), f"{label}: expired flags differ"
     assert np.array_equal(gpu["rep"], ora["rep"]), f"{label}: representative events differ"
+    if "rep_attr" in ora:
+        assert np.array_equal(gpu["rep_attr"], ora["rep_attr"]), f"{label}: replaced timestamp attributes differ"
     vt = ora["val_types"]
     assert np.array_equal(gpu["val_types"], vt)
     for a in range(len(vt)):

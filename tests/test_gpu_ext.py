@@ -291,3 +291,67 @@ def test_ext_timeout_through_rate_limiter(rate):
     sp = tspec()
     sp.rate = rate
     both(sp, with_advances(split_batches(SCH, ts, cols, [10_000, 25_000], 1), ts), f"ext timeout rate {rate}")
+
+
+# ---- replaceTimestampWithBatchEndTime (the 5th parameter; ExternalTimeBatchWindowProcessor :210-220,
+# cloneAppend :446-456): every row's representative event carries its batch's end time ------------------
+RAGGS = [("count", None), ("sum", "v"), ("min", "v")]
+
+
+@pytest.mark.parametrize("output,group,timeout", [("current", True, 0), ("all", True, 0), ("expired", True, 0),
+                                                  ("all", False, 0), ("current", True, 1500), ("all", False, 1500)])
+def test_ext_replace_timestamp_with_batch_end(output, group, timeout):
+    """the rows' replaced timestamp attribute (sh_query_rep_ts_attr) equals the oracle's — batch ends of
+    current rows, of expired rows (the previous batch) and of timeout emissions — with late events, gaps
+    of several empty buckets and pushes cut inside batches; rows otherwise unchanged"""
+    if timeout:
+        ts, cols = tstream(60_000, 0xF7, late_ms=500)
+    else:
+        ts, cols = stream(60_000, 3_000, 0xF8, late_ms=1_200)
+        cols[2] = cols[2] + (np.arange(len(ts)) >= 30_000) * 5_000
+    sp = spec(T=800, start=0 if timeout else None, keys=3_000, output=output, group=group, aggs=RAGGS)
+    sp.replace_ts = True
+    if timeout:
+        sp.timeout = timeout
+    pushes = split_batches(SCH, ts, cols, [1, 15_000, 15_001, 41_000], 1 if timeout else 3)
+    if timeout:
+        pushes = with_advances(pushes, ts)
+    got = both(sp, pushes, f"ext replace {output} {group} {timeout}")
+    assert np.all(got["rep_attr"] % 800 == 0) or not timeout  # (start 0: every batch end is a multiple of T)
+
+
+def test_ext_replace_timestamp_device_output_and_checkpoint():
+    """device output (sh_push_device: the representative events are read back for the attribute) and a
+    checkpoint taken between batches that restores into a fresh query"""
+    import torch
+    from siddhi_amd import runtime
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = stream(40_000, 500, 0xF9, late_ms=300)
+    sp = spec(T=600, keys=500, output="all", aggs=RAGGS)
+    sp.replace_ts = True
+    got, ref, _ = checkpointed(sp, split_batches(SCH, ts, cols, [9_000, 22_000], 1), 1)
+    assert_same(got, ref, label="ext replace ckpt")
+    g, o = runtime.GpuQuery(sp), OracleQuery(sp)
+    dev = torch.device("cuda", 0)
+    t = torch.from_numpy(ts).to(dev)
+    dc = [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols]
+    torch.cuda.synchronize()
+    out = g.push_device(len(ts), t.data_ptr(), [c.data_ptr() for c in dc], 1)
+    a = runtime.device_out_arrays(out)
+    b = abi.out_arrays(o.push_raw(abi.HostBatch(SCH, ts, cols, 1)))
+    assert np.array_equal(a["rep"], b["rep"]) and np.array_equal(g.rep_ts_attr(), o.rep_ts_attr())
+    g.close()
+    o.close()
+
+
+def test_ext_replace_timestamp_refusals():
+    from siddhi_amd import runtime
+    sp = spec(T=600, keys=64, aggs=[("count", None), ("max", "et")])
+    sp.replace_ts = True
+    with pytest.raises(runtime.SiddhiError, match="aggregator over the timestamp"):
+        runtime.GpuQuery(sp)
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
+                       aggs=[("count", None)])
+    sp.replace_ts = True
+    with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
+        runtime.GpuQuery(sp)
