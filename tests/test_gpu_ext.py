@@ -309,7 +309,7 @@ def test_ext_replace_timestamp_with_batch_end(output, group, timeout):
     else:
         ts, cols = stream(60_000, 3_000, 0xF8, late_ms=1_200)
         cols[2] = cols[2] + (np.arange(len(ts)) >= 30_000) * 5_000
-    sp = spec(T=800, start=0 if timeout else None, keys=3_000, output=output, group=group, aggs=RAGGS)
+    sp = spec(T=800 if timeout else 300, start=0 if timeout else None, keys=3_000, output=output, group=group, aggs=RAGGS)
     sp.replace_ts = True
     if timeout:
         sp.timeout = timeout
