@@ -220,7 +220,7 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       // multisplit source (P > 1 or long windows; null: the flat kernel reads the batch)
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
-                      bool pack, EvSrc es);
+                      bool pack, EvSrc es, bool dense_rows = false);
 void launch_count_flags(hipStream_t s, const unsigned char* flags, i64 n, i64* blk_cnt, int nblk);
 void launch_scan_sum(hipStream_t s, i64* a, int n);
 // word_pre[w] = exclusive popcount prefix of the first-occurrence bitmap before word w (low 32 bits)
@@ -234,6 +234,12 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
                       i64* out_keys, u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order,
                       i64 seq_base, i64* out_rep, u64* stage);
 size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows);
+// dense rows (launch_aggregate dense_rows, multisplit units): one-pass emission from the bitmap words
+void launch_emit_gather(hipStream_t s, const u64* word_pre, i64 nw, const Segment* segs, int nseg, int P, int logP,
+                        int unit_stride, const u64* rows, int RW, PosSrc ps, const u32* pend_pos, i64 n_pend,
+                        const u32* n_rows_dev, int n_aggs, KeyTable kt, KeyPlan kp, i64* out_ts, i64* out_keys,
+                        u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order, i64 seq_base,
+                        i64* out_rep);
 void launch_compact_pending(hipStream_t s, const i64* ts, ColSet cols, PosSrc new_pos, AggPlan ap, i64 e_lo,
                             i64 N, i64 pcb_lo, i64 base, const i64* blk_pass_pre, u32* pend_pos, i64* pend_ts,
                             u64* pend_vals, i64 pend_cap, const u64* new_gidx, u64* pend_gidx, i64 seq_base);

@@ -688,7 +688,8 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
                                                            u32* first_bits, const Segment* __restrict__ segs,
                                                            const u32* __restrict__ rec_pos,
                                                            const u32* __restrict__ rec_idx,
-                                                           const u64* __restrict__ rec_vals, i64 rec_cap, EvSrc es) {
+                                                           const u64* __restrict__ rec_vals, i64 rec_cap, EvSrc es,
+                                                           int dense) {
     constexpr int W = kOwnT / 64;
     constexpr int PW = 64 * R;   // records per wave and chunk
     constexpr int CH = kOwnT * R;
@@ -859,6 +860,42 @@ __global__ __launch_bounds__(kOwnT, 4) void k_aggregate_own(const i64* __restric
     i64 tot;
     const i64 pre = block_excl_scan_any((i64)mine, &tot);
     if (t == 0) unit_rows[blockIdx.x] = (u32)tot;
+    if (dense) {
+        // rows at their local key's slot of the unit (K * kOwnT rows, holes where a key had no event):
+        // the emission finds a row from its first event's key slot, no rank scatter (k_emit_gather)
+        const u64 base = (u64)blockIdx.x * (u64)(K * kOwnT);
+        if (K == 1 && (size_t)kOwnT * RW * 8 <= sizeof(st_v)) {
+            u64* stg = &st_v[0][0];
+            __shared__ unsigned char has[kOwnT];
+            __syncthreads();
+            has[t] = cnt0 > 0;
+            if (cnt0) {
+                write_row<F>(ap, stg + (size_t)t * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es, pf, pf_ts,
+                             pf_seq);
+                mark_first(first_bits, fst0);
+            }
+            __syncthreads();
+            const int h = RW / 2, n2 = kOwnT * h;
+            ulonglong2* dst = (ulonglong2*)(rows + base * RW);
+            const ulonglong2* src = (const ulonglong2*)stg;
+            for (int i = t; i < n2; i += kOwnT)
+                if (has[i / h]) dst[i] = src[i];
+            SH_STAMP(0, 6);
+            return;
+        }
+        if (cnt0) {
+            write_row<F>(ap, rows + (base + (u64)t) * RW, RW, ((u32)t << logP) | (u32)p, cnt0, fst0, lst0, f0, es, pf,
+                         pf_ts, pf_seq);
+            mark_first(first_bits, fst0);
+        }
+        if (K > 1 && cnt1) {
+            write_row<F>(ap, rows + (base + (u64)(t + kOwnT)) * RW, RW, ((u32)(t + kOwnT) << logP) | (u32)p, cnt1, fst1,
+                         lst1, f1, es);
+            mark_first(first_bits, fst1);
+        }
+        SH_STAMP(0, 6);
+        return;
+    }
     u32 r = (u32)blockIdx.x * (u32)(K * kOwnT) + (u32)pre;
     if (K == 1 && (size_t)kOwnT * RW * 8 <= sizeof(st_v)) {
         // the unit's rows are one contiguous run: staged in LDS (the record staging is free now),
@@ -898,7 +935,8 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
                       const u32* pend_pos, const u64* pend_vals, i64 pend_cap, const u32* new_pos, ColSet cols,
                       AggPlan ap, u64* rows, int RW, u32* unit_rows, u32* first_bits,
                       const u32* rec_pos, const u32* rec_idx, const u64* rec_vals, i64 rec_cap, const i64* seg_off,
-                      bool pack, EvSrc es) {
+                      bool pack, EvSrc es, bool dense_rows) {
+    const int dense = dense_rows ? 1 : 0;
     if (rec_idx) {  // multisplit records: thread-ownership kernel
         const int K = own_keys_per_thread(NL);
         const int F = ap.n_fields <= 2 ? 2 : ap.n_fields <= 4 ? 4 : 8;
@@ -907,11 +945,11 @@ void launch_aggregate(hipStream_t s, const Segment* segs, int nseg, int P, int l
         if (pack)                                                                                               \
             hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, true>), dim3(nseg * P), dim3(kOwnT), 0, s,   \
                                seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
-                               rec_vals, rec_cap, es);                                                          \
+                               rec_vals, rec_cap, es, dense);                                                   \
         else                                                                                                    \
             hipLaunchKernelGGL((k_aggregate_own<VV, KK, RR, FF, SG, false>), dim3(nseg * P), dim3(kOwnT), 0, s,  \
                                seg_off, P, logP, ap, rows, RW, unit_rows, first_bits, segs, rec_pos, rec_idx,    \
-                               rec_vals, rec_cap, es);                                                          \
+                               rec_vals, rec_cap, es, dense);                                                   \
     } while (0)
 #define SH_AGG_OWN_F(VV, KK, RR)                          \
     do {                                                  \
@@ -1148,6 +1186,77 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
 }
 
 size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows) { return (size_t)stage_words(nk, na, order) * 8 * n_rows; }
+
+// One-pass emission for rows the fold left at their key's slot (dense rows, k_aggregate_own `dense`):
+// one thread per first-occurrence bitmap word (32 events of the combined index space). Each set bit is
+// a row's first event e: its rank is the word's prefix plus the bits below it; its segment (the closed
+// window holding e) and key slot (the slot column, or the dictionary id) name the unit and the local
+// key, so the row is read where the fold wrote it and its columns are stored at the rank directly.
+// Consecutive threads cover consecutive events, so a wave's stores fill one contiguous run of output
+// positions per column. Replaces the rank scatter of whole records and the column split
+// (k_emit_rank + k_emit_soa): one read of every row instead of two, no staged copy.
+__global__ __launch_bounds__(kBlock) void k_emit_gather(const u64* __restrict__ word_pre, i64 nw,
+                                                       const Segment* __restrict__ segs, int nseg, int P, int logP,
+                                                       int unit_stride, const u64* __restrict__ rows, int RW,
+                                                       PosSrc ps, const u32* __restrict__ pend_pos, i64 n_pend,
+                                                       const u32* __restrict__ n_rows_dev, int n_aggs, KeyTable kt,
+                                                       KeyPlan kp, i64* out_ts, i64* out_keys, u64* out_vals,
+                                                       const u64* __restrict__ pend_gidx,
+                                                       const u64* __restrict__ new_gidx, i64* out_order, i64 seq_base,
+                                                       i64* out_rep) {
+    const i64 w = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (w >= nw) return;
+    const u64 wp = word_pre[w];
+    u32 bits = (u32)(wp >> 32);
+    if (!bits) return;
+    i64 o = (i64)(u32)wp;
+    const i64 n = (i64)*n_rows_dev;  // the output columns' stride ([k][n_rows])
+    const i64 e0 = w * 32;
+    // the segment holding the word's first set event (segments are consecutive, sorted by lo)
+    int lo = 0, hi = nseg - 1;
+    const i64 ef = e0 + __ffs(bits) - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].lo <= ef) lo = mid;
+        else hi = mid - 1;
+    }
+    int sg = lo;
+    const int nk = kp.n;
+    while (bits) {
+        const int b = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const i64 e = e0 + b;
+        while (sg + 1 < nseg && e >= segs[sg].hi) sg++;
+        const u32 slot = e < n_pend ? pend_pos[e] : pos_at(ps, e - n_pend);
+        const i64 unit = (i64)sg * P + (slot & (u32)(P - 1));
+        const u64* row = rows + ((size_t)unit * unit_stride + (slot >> logP)) * RW;
+        const ulonglong2 h0 = ((const ulonglong2*)row)[1];  // the last event's timestamp and stream index
+        out_ts[o] = (i64)h0.x;
+        out_rep[o] = (i64)h0.y;
+        i64 kv[SH_MAX_GROUP] = {0, 0};
+        unpack_key(kp, slot_key(kt, slot), kv, 1);
+        for (int k = 0; k < nk; k++) out_keys[(size_t)k * n + o] = kv[k];
+        if (out_order) {
+            const i64 si = e < n_pend ? (i64)pend_gidx[e] : new_gidx ? (i64)new_gidx[e - n_pend] : seq_base + (e - n_pend);
+            out_order[o] = si;
+        }
+#pragma unroll
+        for (int a = 0; a < SH_MAX_AGGS; a++)
+            if (a < n_aggs) out_vals[(size_t)a * n + o] = row[4 + a];
+        o++;
+    }
+}
+
+void launch_emit_gather(hipStream_t s, const u64* word_pre, i64 nw, const Segment* segs, int nseg, int P, int logP,
+                        int unit_stride, const u64* rows, int RW, PosSrc ps, const u32* pend_pos, i64 n_pend,
+                        const u32* n_rows_dev, int n_aggs, KeyTable kt, KeyPlan kp, i64* out_ts, i64* out_keys,
+                        u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order, i64 seq_base,
+                        i64* out_rep) {
+    if (nw <= 0 || nseg <= 0) return;
+    hipLaunchKernelGGL(k_emit_gather, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, word_pre, nw,
+                       segs, nseg, P, logP, unit_stride, rows, RW, ps, pend_pos, n_pend, n_rows_dev, n_aggs, kt, kp,
+                       out_ts, out_keys, out_vals, pend_gidx, new_gidx, out_order, seq_base, out_rep);
+}
 
 // ================================================================================================
 // k_compact_pending: passing events of the open window [e_lo, N) appended to the pending buffer

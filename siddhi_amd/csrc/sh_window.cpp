@@ -241,11 +241,16 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     const bool plane = (d->partition_col >= 0 &&
                         (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
                         by_partition) || plane_group || plane_time_group;
+    // partitioned timeBatch (R12): only the partition that armed the shared nextEmitTime ever flushes, with
+    // its own expired queue (TimeBatchWindowProcessor.process :262-340 per partition state), so its expired
+    // / all-events output is the unpartitioned form over that partition's events
+    const bool r12_batch = d->partition_col >= 0 && d->window == SH_WIN_TIME_BATCH && !d->stream_current && !plane;
     if ((!d->current_on || d->expired_on) &&
-        !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane)
+        !((batch_win || sliding_win || d->window == SH_WIN_EXT_TIME_BATCH) && d->partition_col < 0) && !plane &&
+        !r12_batch)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "expired / all-events output runs on lengthBatch, timeBatch, externalTimeBatch, time and "
-                       "externalTime windows (partitioned: lengthBatch, and time grouped by the partition key)");
+                       "externalTime windows (partitioned: timeBatch, lengthBatch, and time grouped by the partition key)");
     // (partitioned: lengthBatch lanes, every event its own chunk of one key)
     if (d->stream_current &&
         !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH))))
@@ -471,6 +476,8 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     const u32* rec_pos = q->rec_pos.as<u32>();
     const u32* rec_idx = q->rec_idx.as<u32>();
     const u64* rec_vals = q->rec_vals.as<u64>();
+    // multisplit units leave every row at its key's slot and one pass emits them (k_emit_gather)
+    const bool gather = own && q->tune.emit_gather;
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_aggregate(s, dsegs, nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(),
                      q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
@@ -478,7 +485,8 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
                      rec_pos, own ? rec_idx : nullptr, rec_vals, (int64_t)q->rec_cap, q->seg_off.as<int64_t>(),
                      q->rec_packed,
                      EvSrc{q->n_pend, q->pend_ts.as<int64_t>(), ts, q->pend_gidx.as<u64>(),
-                           q->given && b ? q->given_gidx : nullptr, q->seq});
+                           q->given && b ? q->given_gidx : nullptr, q->seq},
+                     gather);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     // output columns sized for the row capacity; the emit kernels read the row count on the device
@@ -493,9 +501,16 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     const int nbt = (int)((n_words + kTile - 1) / kTile);
     RCHK(q->blk_cnt.reserve((nbt + 16) * 8, false));
     RCHK(q->word_pre.reserve((size_t)n_words * 8, false));
-    RCHK(q->emit_stage.reserve(emit_stage_bytes(nk, na, q->given ? 1 : 0, cap), false));
+    if (!gather) RCHK(q->emit_stage.reserve(emit_stage_bytes(nk, na, q->given ? 1 : 0, cap), false));
     launch_bits_prefix(s, q->first_bits.as<u32>(), n_words, q->blk_cnt.as<int64_t>(), q->word_pre.as<u64>(),
                        q->counters.as<u32>());
+    if (gather)
+        launch_emit_gather(s, q->word_pre.as<u64>(), n_words, dsegs, nseg, q->P, q->logP, unit_stride, q->rows.as<u64>(),
+                           RW, pos_src(q, b), q->pend_pos.as<u32>(), q->n_pend, q->counters.as<u32>(), na, q->kt.dev(),
+                           q->kp, q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
+                           q->pend_gidx.as<u64>(), q->given && b ? q->given_gidx : nullptr,
+                           q->given ? q->out_order.as<int64_t>() : nullptr, q->seq, q->out_rep.as<int64_t>());
+    else
     launch_emit_rows(s, q->rows.as<u64>(), RW, unit_rows, n_units, unit_stride, cap, q->counters.as<u32>(),
                      q->word_pre.as<u64>(), na, q->kt.dev(), q->kp, q->n_pend,
                      q->pend_ts.as<int64_t>(), ts, cap,

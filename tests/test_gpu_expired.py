@@ -83,3 +83,27 @@ def test_pass_through(rt, window, param, output):
     pushes = split_batches(SCHEMA, ts, cols, [1, 7_000, 12_000], 4) + [("advance", int(ts[-1]) + 2_000)]
     out = both(rt, spec, pushes, label=f"pass-through {window} {output}")
     assert out["ts"].size > 0
+
+
+PSCHEMA = abi.Schema.parse("k int, p int, v double, x long, ts long")
+
+
+@pytest.mark.parametrize("output", ["all", "expired"])
+@pytest.mark.parametrize("group_by,send_size", [(["k"], 1), (["p"], 7), ([], 1), (["k", "p"], 3)])
+def test_partitioned_timebatch_expired_output(rt, output, group_by, send_size):
+    """`partition with (p of S)` around timeBatch with expired / all-events output: nextEmitTime is shared
+    by the partitions and only the partition that armed it flushes (R12, TimeBatchWindowProcessor.process
+    :262-340), emitting its previous batch as EXPIRED then its current batch — also across empty windows
+    and with the first passing event of a later push"""
+    rng = np.random.default_rng(77)
+    n = 40_000
+    ts = np.cumsum(rng.integers(0, 30, n)).astype(np.int64) + 5_000
+    ts[22_000:] += 9_000  # empty windows
+    cols = [rng.integers(0, 60, n).astype(np.int32), rng.integers(0, 4, n).astype(np.int32),
+            rng.integers(-4000, 4000, n).astype(np.float64) / 16.0, rng.integers(-10**6, 10**6, n).astype(np.int64),
+            ts.copy()]
+    spec = abi.QuerySpec(PSCHEMA, "timeBatch", 700, group_by=group_by, aggs=AGGS, partition="p", output=output,
+                         filter=(">", "v", -120.0), key_capacity=256)
+    pushes = split_batches(PSCHEMA, ts, cols, [1, 9_000, 30_000], send_size) + [("advance", int(ts[-1]) + 3_000)]
+    ref = both(rt, spec, pushes, label=f"p timeBatch {output} {group_by}")
+    assert ref["expired"].sum() > 0
