@@ -1187,14 +1187,16 @@ void launch_emit_rows(hipStream_t s, const u64* rows, int RW, const u32* unit_ro
 
 size_t emit_stage_bytes(int nk, int na, int order, i64 n_rows) { return (size_t)stage_words(nk, na, order) * 8 * n_rows; }
 
-// One-pass emission for rows the fold left at their key's slot (dense rows, k_aggregate_own `dense`):
-// one thread per first-occurrence bitmap word (32 events of the combined index space). Each set bit is
-// a row's first event e: its rank is the word's prefix plus the bits below it; its segment (the closed
-// window holding e) and key slot (the slot column, or the dictionary id) name the unit and the local
-// key, so the row is read where the fold wrote it and its columns are stored at the rank directly.
-// Consecutive threads cover consecutive events, so a wave's stores fill one contiguous run of output
-// positions per column. Replaces the rank scatter of whole records and the column split
-// (k_emit_rank + k_emit_soa): one read of every row instead of two, no staged copy.
+// One-pass emission for rows the fold left at their key's slot (dense rows, k_aggregate_own `dense`).
+// A wave takes 512 events of the combined index space (16 words of the first-occurrence bitmap): every
+// set bit is a row's first event e. The lanes load the key slots of their 8 events (the slot column or
+// the dictionary ids, coalesced) and compact the set ones into LDS in event order; the chunk's rows have
+// consecutive output ranks from the first word's prefix. Then each lane takes every 64th entry: its
+// segment (the closed window holding e) and slot name the unit and local key, the row is read where the
+// fold wrote it and its columns are stored at the rank — consecutive lanes, consecutive ranks. Replaces
+// the rank scatter of whole records and the column split (k_emit_rank + k_emit_soa): one read of every
+// row instead of two, no staged copy.
+constexpr int kGatherEv = 512;  // events per wave
 __global__ __launch_bounds__(kBlock) void k_emit_gather(const u64* __restrict__ word_pre, i64 nw,
                                                        const Segment* __restrict__ segs, int nseg, int P, int logP,
                                                        int unit_stride, const u64* __restrict__ rows, int RW,
@@ -1204,46 +1206,72 @@ __global__ __launch_bounds__(kBlock) void k_emit_gather(const u64* __restrict__ 
                                                        const u64* __restrict__ pend_gidx,
                                                        const u64* __restrict__ new_gidx, i64* out_order, i64 seq_base,
                                                        i64* out_rep) {
-    const i64 w = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (w >= nw) return;
-    const u64 wp = word_pre[w];
-    u32 bits = (u32)(wp >> 32);
-    if (!bits) return;
-    i64 o = (i64)(u32)wp;
-    const i64 n = (i64)*n_rows_dev;  // the output columns' stride ([k][n_rows])
-    const i64 e0 = w * 32;
-    // the segment holding the word's first set event (segments are consecutive, sorted by lo)
-    int lo = 0, hi = nseg - 1;
-    const i64 ef = e0 + __ffs(bits) - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (segs[mid].lo <= ef) lo = mid;
+    __shared__ u32 ent_e[kBlock / 64][kGatherEv], ent_s[kBlock / 64][kGatherEv];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const i64 e_base = ((i64)blockIdx.x * (kBlock / 64) + wv) * kGatherEv;
+    const i64 n_ev = nw * 32;
+    const bool act = e_base < n_ev;
+    const i64 w0 = e_base >> 5;
+    // the lane's 8 events: bits (lane & 3) * 8 .. + 8 of word w0 + lane / 4
+    const i64 w = w0 + (lane >> 2);
+    u32 bits8 = 0;
+    if (act && w < nw) bits8 = ((u32)(word_pre[w] >> 32) >> ((lane & 3) * 8)) & 0xFFu;
+    const int cnt = __popc(bits8);
+    int pre = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int up = __shfl_up(pre, d, 64);
+        if (lane >= d) pre += up;
+    }
+    const int total = __shfl(pre, 63, 64);
+    pre -= cnt;
+    for (int k = 0; bits8; k++) {
+        const int b = __ffs(bits8) - 1;
+        bits8 &= bits8 - 1;
+        const int off = lane * 8 + b;
+        const i64 e = e_base + off;
+        ent_e[wv][pre + k] = (u32)off;
+        ent_s[wv][pre + k] = e < n_pend ? pend_pos[e] : pos_at(ps, e - n_pend);
+    }
+    __syncthreads();
+    if (!act || total == 0) return;
+    const i64 o0 = (i64)(u32)word_pre[w0];  // the rank of the chunk's first row
+    const i64 n = (i64)*n_rows_dev;         // the output columns' stride ([k][n_rows])
+    // the segment holding the chunk's first event (segments are consecutive, sorted by lo)
+    int s0 = 0, hi = nseg - 1;
+    while (s0 < hi) {
+        const int mid = (s0 + hi + 1) >> 1;
+        if (segs[mid].lo <= e_base) s0 = mid;
         else hi = mid - 1;
     }
-    int sg = lo;
     const int nk = kp.n;
-    while (bits) {
-        const int b = __ffs(bits) - 1;
-        bits &= bits - 1;
-        const i64 e = e0 + b;
+    for (int j = lane; j < total; j += 64) {
+        const i64 e = e_base + ent_e[wv][j];
+        const u32 slot = ent_s[wv][j];
+        int sg = s0;
         while (sg + 1 < nseg && e >= segs[sg].hi) sg++;
-        const u32 slot = e < n_pend ? pend_pos[e] : pos_at(ps, e - n_pend);
         const i64 unit = (i64)sg * P + (slot & (u32)(P - 1));
         const u64* row = rows + ((size_t)unit * unit_stride + (slot >> logP)) * RW;
         const ulonglong2 h0 = ((const ulonglong2*)row)[1];  // the last event's timestamp and stream index
+        u64 av[SH_MAX_AGGS];
+#pragma unroll
+        for (int a = 0; a < SH_MAX_AGGS / 2; a++) {
+            if (2 * a >= n_aggs) break;
+            const ulonglong2 v = ((const ulonglong2*)row)[2 + a];
+            av[2 * a] = v.x;
+            av[2 * a + 1] = v.y;
+        }
+        const i64 o = o0 + j;
         out_ts[o] = (i64)h0.x;
         out_rep[o] = (i64)h0.y;
         i64 kv[SH_MAX_GROUP] = {0, 0};
         unpack_key(kp, slot_key(kt, slot), kv, 1);
         for (int k = 0; k < nk; k++) out_keys[(size_t)k * n + o] = kv[k];
-        if (out_order) {
-            const i64 si = e < n_pend ? (i64)pend_gidx[e] : new_gidx ? (i64)new_gidx[e - n_pend] : seq_base + (e - n_pend);
-            out_order[o] = si;
-        }
+        if (out_order)
+            out_order[o] = e < n_pend ? (i64)pend_gidx[e] : new_gidx ? (i64)new_gidx[e - n_pend] : seq_base + (e - n_pend);
 #pragma unroll
         for (int a = 0; a < SH_MAX_AGGS; a++)
-            if (a < n_aggs) out_vals[(size_t)a * n + o] = row[4 + a];
-        o++;
+            if (a < n_aggs) out_vals[(size_t)a * n + o] = av[a];
     }
 }
 
@@ -1253,7 +1281,8 @@ void launch_emit_gather(hipStream_t s, const u64* word_pre, i64 nw, const Segmen
                         u64* out_vals, const u64* pend_gidx, const u64* new_gidx, i64* out_order, i64 seq_base,
                         i64* out_rep) {
     if (nw <= 0 || nseg <= 0) return;
-    hipLaunchKernelGGL(k_emit_gather, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, word_pre, nw,
+    const i64 per_block = (i64)(kBlock / 64) * kGatherEv / 32;  // words per block
+    hipLaunchKernelGGL(k_emit_gather, dim3((unsigned)((nw + per_block - 1) / per_block)), dim3(kBlock), 0, s, word_pre, nw,
                        segs, nseg, P, logP, unit_stride, rows, RW, ps, pend_pos, n_pend, n_rows_dev, n_aggs, kt, kp,
                        out_ts, out_keys, out_vals, pend_gidx, new_gidx, out_order, seq_base, out_rep);
 }
