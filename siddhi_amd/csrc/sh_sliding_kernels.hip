@@ -1759,7 +1759,12 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         const int Sx = H0 + o0;  // window index of the chunk's first record
         u64 r_mn = 0, r_mx = 0;
         u32 r_fl = 0;
+#ifdef SH_WK_NOPAR
+        bool pc = false;  // (timing experiment only)
+        par = false;
+#else
         bool pc = par;  // this chunk's min / max in parallel
+#endif
         DqPlan pn{}, px{};
         bool sn = false, sx_ = false;
         if (pc) {
@@ -1812,6 +1817,12 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         // record q's results land in lane q's registers (a select, no LDS store).
         i64 r_cnt = 0;
         u64 r_sum = 0;
+#ifdef SH_WK_NOSEQ
+        // (timing experiment only: the order-dependent chain skipped, results wrong)
+        hj = max(hb, __builtin_amdgcn_readlane(lo_eff, m - 1));
+        r_cnt = 1;
+        if (false)
+#endif
         {
             int h = hb;
             for (int q = 0; q < m; q++) {
@@ -1862,7 +1873,11 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         const u32 rk_next = __shfl_down(rk, 1, 64);
         const bool next_first = lane + 1 < m ? (rk_next & kFirstBit) != 0 : true;
         const i64 send = send_base + (send_size == 1 ? (i64)raw : send_size ? (i64)(raw / send_size) : 0);
+#ifdef SH_WK_NOROWS
+        if (false) {  // (timing experiment only: no row stores)
+#else
         if (in && next_first) {
+#endif
             u64 w[4 + SH_MAX_AGGS];
             u32 nulls = 0;
             const i64 c = r_cnt;
