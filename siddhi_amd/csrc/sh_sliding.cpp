@@ -391,7 +391,7 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
             RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
             RCHK(s->p_pm.reserve(M * 8, false));
             RCHK(s->p_vals.reserve(M * 8, false));
-            RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na) * 8, false));
+            RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na, all_rows) * 8, false));
             if (q->tune.sl_kgather) RCHK(s->rec_aosk.reserve((size_t)M * kSlAosWords * 8, false));
             launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
                                  rec, s->p_pm.as<int64_t>(), s->p_vals.as<u64>(), state_of(s), q->ap,
@@ -453,12 +453,12 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         if (!all_rows) launch_scan_sum(st, s->blk_cnt.as<int64_t>(), fblk);
         if (keyed)
             launch_slk_emit(st, all_rows ? nullptr : s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk,
-                            s->rows_k.as<u64>(), sliding_keyed_row_words(na), na, q->kt.dev(), q->kp, cap,
+                            s->rows_k.as<u64>(), sliding_keyed_row_words(na, all_rows), na, q->kt.dev(), q->kp, cap,
                             s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                             s->out_nulls.as<unsigned char>(), send_size == 1 ? nullptr : s->out_send.as<int64_t>(),
                             s->out_clock.as<int64_t>(),
                             s->rec_raw.as<u32>(), raw_base, want_order ? q->out_order.as<int64_t>() : nullptr,
-                            s->out_rep.as<int64_t>());
+                            s->out_rep.as<int64_t>(), rec.aos, rec.slot);
         else
         launch_sl_emit(st, s->flags.as<unsigned char>(), M, s->blk_cnt.as<int64_t>(), fblk, rows, na, q->kt.dev(),
                        q->kp, cap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),

@@ -71,13 +71,15 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
                           SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
                           i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags, u64* aosk = nullptr,
                           i64 M = 0);
-int sliding_keyed_row_words(int n_aggs);
+// compact: per-event sends (no flags), the row holds its values only
+int sliding_keyed_row_words(int n_aggs, bool compact = false);
 // rowsK: the keyed replay's rows at the stream rank of their first record (flags NULL: per-event sends,
 // every rank holds a row)
 void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
-                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep);
+                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep, const u64* aos = nullptr,
+                     const u32* rank_slot = nullptr);
 void launch_sl_gather(hipStream_t s, const u32* ranks, i64 M, SlRecords rec, SlRecords out, int nv);
 // rec: the records gathered into partition order (k_sl_own); rec_by_rank: the same records in rank
 // order, read through rank_list by k_sl_own_d (sliding_keys_per_partition(ap) == 8 shapes)

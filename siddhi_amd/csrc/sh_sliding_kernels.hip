@@ -1662,6 +1662,10 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
     __shared__ int di_max[HMAX ? kDqK : 1];
     __shared__ i64 s_pm[kWS];
     __shared__ u64 s_x[64];
+    // the order-dependent sum chain of a chunk as one operation list (kWS removes + 64 adds at most)
+    __shared__ u64 s_op[kWS + 64];
+    __shared__ int s_lo[64];
+    __shared__ unsigned char s_fl[kWS + 64];
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= nslots) return;
@@ -1817,13 +1821,78 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
         // record q's results land in lane q's registers (a select, no LDS store).
         i64 r_cnt = 0;
         u64 r_sum = 0;
+        // Fast chain: with the min / max handled in parallel (or none), what stays sequential is the
+        // Java-order double sum. Record q's removes are the heads [lo_eff(q-1), lo_eff(q)) and its add
+        // follows them, so every operation's place in the chunk's list is known in parallel: add q at
+        // (lo_eff(q) - hb) + q, head d at d + #{q : lo_eff(q) <= hb + d}. The lanes write the values
+        // (a remove as the negated value: a - b is a + (-b) exactly in IEEE 754), the counts are
+        // closed-form, and the wave then only adds the list up in order, reading it from LDS with a
+        // uniform address (no readlane per value), capturing the running sum after each add.
+        const int R = __builtin_amdgcn_readlane(lo_eff, m - 1) - hb;  // heads expiring in the chunk
+        const bool fast = (pc || (!HMIN && !HMAX)) && R <= kWS;
+        if (fast) {
+            const int nops = R + m;
+            if (in) s_lo[lane] = lo_eff;
+            for (int j = lane; j < nops; j += 64) s_fl[j] = 0;
+            __syncthreads();
+            const int ap_q = (lo_eff - hb) + lane;  // this lane's add (lanes < m)
+            if (in) {
+                s_op[ap_q] = x;
+                s_fl[ap_q] = 1;
+            }
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const int d = lane + 64 * t;
+                if (d >= R) continue;
+                // adds before head d: the records whose expiry point is at or below it
+                int lo2 = 0, hi2 = m;
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (s_lo[mid] <= hb + d) lo2 = mid + 1;
+                    else hi2 = mid;
+                }
+                s_op[d + lo2] = (t ? hv1 : hv0) ^ 0x8000000000000000ull;  // -v
+                // the count after this remove: zero -> the sum restarts from +0.0 (canDestroy)
+                if (cnt + lo2 - (d + 1) == 0) s_fl[d + lo2] = 2;
+            }
+            __syncthreads();
+            u64 adm[3], czm[3];
+#pragma unroll
+            for (int wd = 0; wd < 3; wd++) {
+                const int j = wd * 64 + lane;
+                const unsigned char fv = j < nops ? s_fl[j] : 0;
+                adm[wd] = __ballot(fv == 1);
+                czm[wd] = __ballot(fv == 2);
+            }
+            if (HSUM) {
+                double sm = sum;
+                int q = 0;
+                for (int j = 0; j < nops; j++) {
+                    sm = sm + __longlong_as_double((i64)s_op[j]);
+                    const int wd = j >> 6;
+                    const u64 bit = 1ull << (j & 63);
+                    const u64 cz = wd == 0 ? czm[0] : wd == 1 ? czm[1] : czm[2];
+                    const u64 ad = wd == 0 ? adm[0] : wd == 1 ? adm[1] : adm[2];
+                    if (cz & bit) sm = sm == 0.0 ? 0.0 : sm;
+                    if (ad & bit) {
+                        r_sum = lane == q ? (u64)__double_as_longlong(sm) : r_sum;
+                        q++;
+                    }
+                }
+                sum = sm;
+            }
+            r_cnt = cnt + (lane + 1) - (lo_eff - hb);
+            cnt = cnt + m - R;
+            hj = hb + R;
+            __syncthreads();  // (s_op / s_lo / s_fl are refilled by the next chunk)
+        }
 #ifdef SH_WK_NOSEQ
         // (timing experiment only: the order-dependent chain skipped, results wrong)
         hj = max(hb, __builtin_amdgcn_readlane(lo_eff, m - 1));
         r_cnt = 1;
         if (false)
 #endif
-        {
+        if (!fast) {
             int h = hb;
             for (int q = 0; q < m; q++) {
                 const int e = max(__builtin_amdgcn_readlane(lo, q), h);
@@ -1905,9 +1974,18 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                                  : kord ? (u32)aosk[(size_t)(a + (u32)grp) * kSlAosWords + 5]
                                         : sorted_rank[a + (u32)grp];
             ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row_rank * RW);
+            if (!flags) {
+                // per-event sends: every record's row follows its own add (count >= 1, no nulls) and the
+                // emission takes ts / clock / event / slot from the stream-order records, so the row is
+                // its values alone — half the bytes of the random stores (r05: 2.4 ms of the replay)
 #pragma unroll
-            for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
-                if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
+                for (int o = 0; o < SH_MAX_AGGS / 2; o++)
+                    if (2 * o < RW) dst[o] = make_ulonglong2(w[4 + 2 * o], w[4 + 2 * o + 1]);
+            } else {
+#pragma unroll
+                for (int o = 0; o < (4 + SH_MAX_AGGS) / 2; o++)
+                    if (2 * o < RW) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
+            }
         }
         open_row = __shfl(grp, m - 1, 64);
         last_send = __shfl(send, m - 1, 64);
@@ -1947,8 +2025,29 @@ __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __rest
                                                     KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                                                     unsigned char* out_nulls, i64* out_send, i64* out_clock,
                                                     const u32* __restrict__ rank_raw, i64 raw_base, i64* out_order,
-                                                    i64* out_rep) {
+                                                    i64* out_rep, const u64* __restrict__ aos,
+                                                    const u32* __restrict__ rank_slot) {
     const i64 tile = (i64)blockIdx.x * kTile;
+    if (!flags) {
+        // per-event sends: row j is record j's (compact: values only); the rest from the record itself
+        for (int it = 0; it < kItems; it++) {
+            const i64 j = tile + (i64)it * kBlock + threadIdx.x;
+            if (j >= n) continue;
+            const ulonglong2* rp = (const ulonglong2*)(aos + (size_t)j * kSlAosWords);
+            const ulonglong2 w0 = rp[0], w1 = rp[1], w2 = rp[2];
+            const u64* src = rowsK + (size_t)j * RW;
+            out_ts[j] = (i64)w1.x;
+            unpack_key(kp, slot_key(kt, rank_slot[j]), out_keys + j, out_cap);
+            for (int a = 0; a < n_aggs; a++) {
+                out_vals[(size_t)a * out_cap + j] = src[a];
+                out_nulls[(size_t)a * out_cap + j] = 0;
+            }
+            out_clock[j] = (i64)w0.x;
+            if (out_order) out_order[j] = raw_base + (i64)rank_raw[j];
+            out_rep[j] = raw_base + (i64)(u32)w2.x;
+        }
+        return;
+    }
     i64 run = flags ? blk_pre[blockIdx.x] : tile;
     for (int it = 0; it < kItems; it++) {
         const i64 j = tile + (i64)it * kBlock + threadIdx.x;
@@ -1988,10 +2087,11 @@ __global__ __launch_bounds__(kBlock) void k_slk_emit(const unsigned char* __rest
 void launch_slk_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk,
                      const u64* rowsK, int RW, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                      i64* out_keys, u64* out_vals, unsigned char* out_nulls, i64* out_send, i64* out_clock,
-                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep) {
+                     const u32* rank_raw, i64 raw_base, i64* out_order, i64* out_rep, const u64* aos,
+                     const u32* rank_slot) {
     hipLaunchKernelGGL(k_slk_emit, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rowsK, RW, n_aggs, kt, kp,
                        out_cap, out_ts, out_keys, out_vals, out_nulls, out_send, out_clock, rank_raw, raw_base,
-                       out_order, out_rep);
+                       out_order, out_rep, aos, rank_slot);
 }
 
 // The keyed replay is used where it measured faster than the key-partition replay (k_sl_own_d): with
@@ -2002,7 +2102,7 @@ bool sliding_keyed_ok(AggPlan ap) {
     return own_d_fields(ap, fd) && ap.n <= SH_MAX_AGGS && (fd.mn >= 0 || fd.mx >= 0);
 }
 
-int sliding_keyed_row_words(int n_aggs) { return (4 + n_aggs + 1) & ~1; }
+int sliding_keyed_row_words(int n_aggs, bool compact) { return compact ? (n_aggs + 1) & ~1 : (4 + n_aggs + 1) & ~1; }
 
 // The 48-byte records in key order (sorted_rank[i] = the stream rank of key-order record i), each
 // carrying its stream rank in its last word: the replay then streams every key's run instead of
@@ -2036,7 +2136,7 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
     launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
-    const int RW = sliding_keyed_row_words(ap.n);
+    const int RW = sliding_keyed_row_words(ap.n, flags == nullptr);
     if (aosk && M > 0)
         hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank, M,
                            rec.aos, aosk);
