@@ -468,7 +468,10 @@ __global__ __launch_bounds__(64) void k_pl_walk_tm(const u32* __restrict__ key_o
                     while (len > 0 && p_worse(kind, d[(h + len - 1) & rm], x)) len--;
                     d[(h + len) & rm] = x;
                     dql[a] = len + 1;
-                    mm[a] = len == 0 ? x : d[h & rm];
+                    // minValue = value when strictly better (MinAttributeAggregatorExecutor.processAdd :187):
+                    // the deque's front except past a NaN, which no comparison pops
+                    const bool take = !mmh[a] || p_worse(kind, mm[a], x);
+                    mm[a] = take ? x : mm[a];  // (a select: see k_slx_walk)
                     mmh[a] = 1;
                 }
             }

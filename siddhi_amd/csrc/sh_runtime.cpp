@@ -229,6 +229,7 @@ Tuning Tuning::from_env() {
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
     // the gather of the records into key order costs more than the replay saves (C3 3.01e9 vs 3.36e9
     // events/s: k_sl_kgather 1.32 ms moving 7.1 GB, k_sl_wkey 6.4 -> 6.1 ms; profiles/r05_c3_*)
+    t.slx_wave = !getenv("SH_SLX_WAVE") || on("SH_SLX_WAVE");
     t.sl_kgather = on("SH_SL_KGATHER");
     t.emit_gather = !getenv("SH_EMIT_GATHER") || on("SH_EMIT_GATHER");
     return t;

@@ -230,6 +230,7 @@ struct Tuning {
     bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
     bool pl_sort = true;   // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
     bool emit_gather = true;  // dense fold rows + one-pass emission (k_emit_gather); SH_EMIT_GATHER=0: rank scatter
+    bool slx_wave = true;     // expired / all-events sliding replay with a wave per key (k_slx_wkey); SH_SLX_WAVE=0: a lane per key
     bool sl_kgather = false;  // keyed sliding replay over key-ordered records (k_sl_kgather, SH_SL_KGATHER=1): measured slower
     int agg_band_rows = 8;
     static Tuning from_env();

@@ -798,10 +798,11 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
                         q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
                         ext ? s->rec_sclk.as<int64_t>() : nullptr);
     else
-    launch_slx_walk(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
-                    s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u,
-                    s->x0, s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on,
-                    q->d.expired_on, rows, s->flags.as<unsigned char>(), ext ? s->rec_sclk.as<int64_t>() : nullptr);
+        (q->tune.slx_wave && slx_keyed_ok(q->ap) ? launch_slx_wkey : launch_slx_walk)(
+            st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
+            s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, s->x0,
+            s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on, q->d.expired_on, rows,
+            s->flags.as<unsigned char>(), ext ? s->rec_sclk.as<int64_t>() : nullptr);
     HIPCHK(hipEventRecord(q->ev_agg1, st));
     HIPCHK(hipGetLastError());
     // ---- rows in operation order, one flush per chunk

@@ -138,6 +138,13 @@ void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, 
                      const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
                      i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
                      int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk);
+// the same replay with one wave per key (sh_sliding_kernels.hip) for the count / sum / avg / min / max of
+// one double column shape (slx_keyed_ok)
+bool slx_keyed_ok(AggPlan ap);
+void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                     const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
+                     i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
+                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk);
 void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
                      const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
                      SlxRows rows, unsigned char* flags, const i64* rsclk);

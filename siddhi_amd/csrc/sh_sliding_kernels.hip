@@ -2159,6 +2159,398 @@ int sliding_keys_per_partition(AggPlan ap) {
     return own_d_fields(ap, fd) ? kSlKeyLanes : 64;
 }
 
+// ---- `insert expired / all events`, one wave per key (round 5) ----------------------------------------
+// k_slx_walk gives every key one lane that merges its adds and removes one dependent load at a time
+// (c3all: 148 ms per push). Here the 64 lanes of a wave take a key's next 64 operations at once: the
+// next 64 adds (its records in arrival order, each with its operation index aop) and the next 64
+// removes (its FIFO entries, each with the operation index xop of its expiry point, kNoOp when it
+// stays) are staged, and every staged operation finds its place in the merged order by a binary
+// search over the other list; the first 64 places form the chunk. Per operation t the window is the
+// FIFO range [head(t), end(t)), both counted by ballots, so the count is closed-form; the Java-order
+// double sum is one operation list added up from LDS (a remove as the negated value, the canDestroy
+// restart where the count reaches 0); the min / max is the range best of [head(t), end(t)) while the
+// reference's deque quirk cannot show (the same check and deque bookkeeping as k_sl_wkey), else the
+// deque runs sequentially for the rest of the push. Rows: one per (chunk, key), opened by its first
+// qualifying operation (the row's place = that operation's index) and holding the values after its last
+// one — the lanes are segmented by their chunk, a row still open at the chunk's end is written and
+// overwritten by the next chunk. TimeWindowProcessor.java:132-169; QuerySelector.java:315-374.
+constexpr u64 kSlxNoOp = ~0ull;
+
+template <bool HSUM, bool HMIN, bool HMAX>
+__global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off, u32 nslots,
+                                                const u32* __restrict__ sorted_rank, SlRecords rec,
+                                                const u64* __restrict__ aop, const u64* __restrict__ xop,
+                                                const i64* __restrict__ xch, const i64* __restrict__ xts,
+                                                const i64* __restrict__ xclk, const i64* __restrict__ useq, i64 n_u,
+                                                i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S,
+                                                i64* __restrict__ rg, DFields fd, KOut ko, int cur_on, int exp_on,
+                                                SlxRows rows, unsigned char* __restrict__ flags,
+                                                const i64* __restrict__ rsclk) {
+    __shared__ u64 dq_min[HMIN ? kDqK : 1];
+    __shared__ u64 dq_max[HMAX ? kDqK : 1];
+    __shared__ int di_min[HMIN ? kDqK : 1];
+    __shared__ int di_max[HMAX ? kDqK : 1];
+    __shared__ u64 s_aop[64], s_ax[64], s_xop[64], s_xx[64], s_val[64];
+    __shared__ u64 s_pbn[HMIN ? 64 : 1], s_pbx[HMAX ? 64 : 1];
+    __shared__ u32 s_ar[64];
+    __shared__ i64 s_xu[64];
+    __shared__ int s_sel[64];
+    const u32 k = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (k >= nslots) return;
+    const u32 lo = key_off[k];
+    const int A = (int)(key_off[k + 1] - lo);
+    const int H0 = (int)S.rlen[k];
+    if (A == 0 && H0 == 0) return;
+    const int gm = (int)(S.rc - 1);
+    const int rh0 = (int)(S.rhead[k] & gm);
+    const size_t kr = (size_t)k * S.rc;
+    const int HN = H0 + A;
+    i64 cnt = S.cnt[k];
+    double sum = 0.0;
+    if (HSUM) sum = __longlong_as_double((i64)S.f[(size_t)(fd.sum >= 0 ? fd.sum : fd.avg) * S.nslots + k]);
+    KDq qn{}, qx{};
+    u64* gmin = HMIN ? S.dq + ((size_t)fd.mn * S.nslots + k) * S.rc : nullptr;
+    u64* gmax = HMAX ? S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc : nullptr;
+    if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
+    if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
+    __syncthreads();
+    bool par = HMIN || HMAX;
+    if (HMIN && par) par = dq_index_init<true>(qn, dq_min, di_min, S.rval + kr, rh0, gm, H0, lane);
+    if (HMAX && par) par = dq_index_init<false>(qx, dq_max, di_max, S.rval + kr, rh0, gm, H0, lane);
+    __syncthreads();
+    const u64 le = (2ull << lane) - 1ull;  // lanes <= this one (lane 63: all)
+    int ia = 0, ie = 0;                    // adds / FIFO entries consumed
+    i64 row_ch = -1, row_op = 0;           // the (chunk, key) row open at the chunk start
+    for (;;) {
+        // ---- stage the next 64 adds and the next 64 FIFO entries
+        u64 a_op = kSlxNoOp, a_x = 0, x_op = kSlxNoOp, x_x = 0;
+        u32 a_r = 0;
+        i64 x_u = -1;
+        if (ia + lane < A) {
+            a_r = sorted_rank[lo + (u32)(ia + lane)];
+            a_op = aop[a_r];
+            a_x = rec.vals[a_r];
+        }
+        const int p = ie + lane;
+        if (p < HN) {
+            if (p < H0) {
+                const size_t sl = kr + (size_t)((rh0 + p) & gm);
+                x_u = rg[sl] - X0;
+                x_x = S.rval[sl];
+            } else {
+                const u32 r = sorted_rank[lo + (u32)(p - H0)];
+                x_u = G0 + (i64)r - X0;
+                x_x = rec.vals[r];
+            }
+            if (x_u >= 0 && x_u < n_u) x_op = xop[x_u];
+        }
+        if (!__any(a_op != kSlxNoOp || x_op != kSlxNoOp)) break;
+        s_aop[lane] = a_op;
+        s_ax[lane] = a_x;
+        s_ar[lane] = a_r;
+        s_xop[lane] = x_op;
+        s_xx[lane] = x_x;
+        s_xu[lane] = x_u;
+        __syncthreads();
+        // ---- places in the merged order (both lists ascend; kNoOp pads the ends)
+        int pa = 64, px = 64;
+        if (a_op != kSlxNoOp) {
+            int l2 = 0, h2 = 64;
+            while (l2 < h2) {
+                const int mid = (l2 + h2) >> 1;
+                if (s_xop[mid] < a_op) l2 = mid + 1;
+                else h2 = mid;
+            }
+            pa = lane + l2;
+        }
+        if (x_op != kSlxNoOp) {
+            int l2 = 0, h2 = 64;
+            while (l2 < h2) {
+                const int mid = (l2 + h2) >> 1;
+                if (s_aop[mid] < x_op) l2 = mid + 1;
+                else h2 = mid;
+            }
+            px = lane + l2;
+        }
+        if (pa < 64) s_sel[pa] = lane;
+        if (px < 64) s_sel[px] = 64 | lane;
+        const int na_c = __popcll(__ballot(pa < 64)), nx_c = __popcll(__ballot(px < 64));
+        const int m = na_c + nx_c;
+        __syncthreads();
+        // ---- this lane's operation
+        const bool in = lane < m;
+        const int sel = in ? s_sel[lane] : 0;
+        const bool is_add = in && !(sel & 64);
+        const int si = sel & 63;
+        const u64 op = in ? (is_add ? s_aop[si] : s_xop[si]) : 0;
+        const u64 val = is_add ? s_ax[si] : s_xx[si];
+        const u32 r = s_ar[si];
+        const i64 u = s_xu[si];
+        const u64 am = __ballot(is_add), xm = __ballot(in && !is_add);
+        const int adds_le = __popcll(am & le), rems_le = __popcll(xm & le);
+        i64 r_cnt = cnt + adds_le - rems_le;
+        const int S0 = H0 + ia;        // window index of the chunk's first add
+        const int h_t = ie + rems_le;  // window head after this operation
+        const int h_end = ie + nx_c;
+        u64 r_sum = 0, r_mn = 0, r_mx = 0;
+        u32 r_fl = 0;
+        bool pc = par;
+        if (pc) {
+            // min / max in parallel: no NaN, no expiring value meeting a bit-equal one of another event
+            const bool ain = lane < na_c;  // add-space lane c = add ia + c (its staged lane)
+            pc = !__any(ain && d_isnan(a_x));
+            if (pc) {
+                bool dirty = false;
+                if (lane < nx_c) {
+                    const int idx = ie + lane;
+                    const u64 v = x_x;
+                    if (HMIN)
+                        for (int e = 0; e < qn.len; e++) {
+                            const int sl = (qn.h + e) & (kDqK - 1);
+                            dirty |= dq_min[sl] == v && di_min[sl] != idx;
+                        }
+                    if (HMAX)
+                        for (int e = 0; e < qx.len; e++) {
+                            const int sl = (qx.h + e) & (kDqK - 1);
+                            dirty |= dq_max[sl] == v && di_max[sl] != idx;
+                        }
+                    for (int c = 0; c < na_c; c++) dirty |= s_ax[c] == v && S0 + c != idx;
+                }
+                pc = !__any(dirty);
+            }
+            DqPlan pn{}, px_{};
+            bool sn = false, sx = false;
+            if (pc) {
+                const bool from0 = h_end <= S0;  // no add of the chunk leaves within it
+                if (from0) {
+                    // leftmost-best prefix of the chunk's adds
+                    u64 bn = a_x, bx = a_x;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const int src = lane >= d ? lane - d : lane;
+                        const u64 on = shfl64(bn, src), ox = shfl64(bx, src);
+                        if (lane >= d) {
+                            if (!d_worse<true>(on, bn)) bn = on;
+                            if (!d_worse<false>(ox, bx)) bx = ox;
+                        }
+                    }
+                    if (HMIN) s_pbn[lane] = bn;
+                    if (HMAX) s_pbx[lane] = bx;
+                }
+                __syncthreads();
+                if (in) {
+                    const int c0 = h_t - S0 > 0 ? h_t - S0 : 0;
+                    auto best = [&](const KDq& q, const u64* dv, const int* di, const u64* pb, bool MINB) -> u64 {
+                        int a = 0, b = q.len;
+                        while (a < b) {
+                            const int mid = (a + b) >> 1;
+                            if (di[(q.h + mid) & (kDqK - 1)] < h_t) a = mid + 1;
+                            else b = mid;
+                        }
+                        u64 bv = a < q.len ? dv[(q.h + a) & (kDqK - 1)] : 0;
+                        bool bh = a < q.len;
+                        u64 cv = 0;
+                        bool chh = false;
+                        if (from0) {
+                            if (adds_le > 0) { cv = pb[adds_le - 1]; chh = true; }
+                        } else {
+                            for (int c = c0; c < adds_le; c++) {
+                                const u64 v = s_ax[c];
+                                if (!chh || (MINB ? d_worse<true>(cv, v) : d_worse<false>(cv, v))) { cv = v; chh = true; }
+                            }
+                        }
+                        if (chh && (!bh || (MINB ? d_worse<true>(bv, cv) : d_worse<false>(bv, cv)))) bv = cv;
+                        return bv;
+                    };
+                    if (HMIN) r_mn = best(qn, dq_min, di_min, s_pbn, true);
+                    if (HMAX) r_mx = best(qx, dq_max, di_max, s_pbx, false);
+                    r_fl = r_cnt > 0 ? 3u : 0u;
+                }
+                if (HMIN) pn = dq_plan<true>(qn, dq_min, di_min, a_x, ain, S0, h_end, na_c, lane, sn);
+                if (HMAX) px_ = dq_plan<false>(qx, dq_max, di_max, a_x, ain, S0, h_end, na_c, lane, sx);
+                pc = (!HMIN || pn.i1 - pn.i0 + pn.n_new <= kDqK) && (!HMAX || px_.i1 - px_.i0 + px_.n_new <= kDqK);
+            }
+            if (pc) {
+                const bool live = cnt + na_c - nx_c > 0;
+                if (HMIN) {
+                    dq_commit<true>(qn, dq_min, di_min, pn, a_x, sn, S0, lane, rl64(r_mn, m - 1));
+                    qn.mmh = live && qn.len > 0;
+                }
+                if (HMAX) {
+                    dq_commit<false>(qx, dq_max, di_max, px_, a_x, sx, S0, lane, rl64(r_mx, m - 1));
+                    qx.mmh = live && qx.len > 0;
+                }
+            } else {
+                par = false;  // the sequential deque takes over for the rest of the push
+            }
+        }
+        if (pc || (!HMIN && !HMAX)) {
+            // the sum as one operation list: adds, negated removes, canDestroy restarts
+            if (HSUM) {
+                if (in) s_val[lane] = is_add ? val : val ^ 0x8000000000000000ull;
+                const u64 czm = __ballot(in && !is_add && r_cnt == 0);
+                __syncthreads();
+                double sm = sum;
+                for (int j = 0; j < m; j++) {
+                    sm = sm + __longlong_as_double((i64)s_val[j]);
+                    if ((czm >> j) & 1ull) sm = sm == 0.0 ? 0.0 : sm;
+                    r_sum = lane == j ? (u64)__double_as_longlong(sm) : r_sum;
+                }
+                sum = sm;
+            }
+        } else {
+            // sequential: every operation in order on wave-uniform state
+            if (in) s_val[lane] = val;
+            __syncthreads();
+            i64 c = cnt;
+            for (int j = 0; j < m; j++) {
+                const bool ad = !(s_sel[j] & 64);
+                const u64 v = s_val[j];
+                if (ad) {
+                    c++;
+                    if (HSUM) sum = sum + __longlong_as_double((i64)v);
+                    if (HMIN) kdq_add<true, 1>(qn, gmin, gm, dq_min, v);
+                    if (HMAX) kdq_add<false, 1>(qx, gmax, gm, dq_max, v);
+                } else {
+                    c--;
+                    if (HSUM) {
+                        sum = sum - __longlong_as_double((i64)v);
+                        if (c == 0 && sum == 0.0) sum = 0.0;  // destroyed state restarts from +0.0 (canDestroy)
+                    }
+                    if (HMIN) kdq_remove<true, 1>(qn, gmin, gm, dq_min, v);
+                    if (HMAX) kdq_remove<false, 1>(qx, gmax, gm, dq_max, v);
+                }
+                if (lane == j) {
+                    r_sum = (u64)__double_as_longlong(sum);
+                    r_mn = qn.mm;
+                    r_mx = qx.mm;
+                    r_fl = (qn.mmh ? 1u : 0u) | (qx.mmh ? 2u : 0u);
+                }
+            }
+        }
+        cnt += na_c - nx_c;
+        ia += na_c;
+        ie += nx_c;
+        // ---- rows: lanes segmented by their chunk among the qualifying operations
+        i64 ch = 0;
+        if (in) ch = is_add ? 2 * (send_size > 0 ? (i64)rec.raw[r] / send_size : 0) + 1 : xch[u];
+        const bool qual = in && (is_add ? cur_on : exp_on);
+        const u64 qm = __ballot(qual);
+        const u64 qb = qm & (le >> 1);  // qualifying lanes before this one
+        const int pl = qb ? 63 - __clzll(qb) : lane;
+        const i64 pch = (i64)shfl64((u64)ch, pl);
+        const i64 prev_ch = qb ? pch : row_ch;
+        const bool start = qual && ch != prev_ch;
+        if (start) flags[op] = 1;
+        const u64 stm = __ballot(start) & le;
+        const int sl = stm ? 63 - __clzll(stm) : lane;
+        const u64 sop = shfl64(op, sl);
+        const i64 my_row = stm ? (i64)sop : row_op;
+        const u64 qa = qm & ~le;  // qualifying lanes after this one
+        const int nl = qa ? __ffsll((long long)qa) - 1 : lane;
+        const i64 nch = (i64)shfl64((u64)ch, nl);
+        const bool end = qual && (!qa || nch != ch);
+        if (end) {
+            i64 ts, rep, clk;
+            if (is_add) {
+                ts = rec.ts[r];
+                rep = seq_base + (i64)rec.raw[r];
+                clk = rsclk ? rsclk[r] : rec.clock[r];
+            } else {
+                ts = xts[u];
+                rep = useq[u];
+                clk = xclk[u];
+            }
+            rows.ts[my_row] = ts;
+            rows.rep[my_row] = rep;
+            rows.slot[my_row] = k;
+            rows.ch[my_row] = ch;
+            rows.clk[my_row] = clk;
+            rows.exp[my_row] = is_add ? 0 : 1;
+#pragma unroll
+            for (int o = 0; o < SH_MAX_AGGS; o++) {
+                if (o >= ko.n) break;
+                const int src = ko.src[o];
+                u64 v = 0;
+                unsigned char nul = 0;
+                if (src == 0) v = (u64)r_cnt;
+                else if (src == 1) { nul = r_cnt == 0; v = r_sum; }
+                else if (src == 2) {
+                    nul = r_cnt == 0;
+                    if (!nul) v = (u64)__double_as_longlong(__longlong_as_double((i64)r_sum) / (double)r_cnt);
+                } else if (src == 3) { nul = (r_fl & 1u) ? 0 : 1; v = r_mn; }
+                else { nul = (r_fl & 2u) ? 0 : 1; v = r_mx; }
+                rows.vals[(size_t)o * rows.cap + my_row] = nul ? 0 : v;
+                rows.nulls[(size_t)o * rows.cap + my_row] = nul;
+            }
+        }
+        if (qm) {  // (wave-uniform)
+            const int lq = 63 - __clzll(qm);
+            row_ch = (i64)shfl64((u64)ch, lq);
+            row_op = (i64)shfl64((u64)my_row, lq);
+        }
+        __syncthreads();  // the staging arrays are refilled by the next chunk
+    }
+    // ---- the window after the push: FIFO [ie, HN) — ring entries keep their place, new ones follow
+    const int keep = ie < H0 ? H0 - ie : 0;
+    const int rh = (rh0 + (ie < H0 ? ie : H0)) & gm;
+    const int j0 = ie > H0 ? ie : H0;
+    for (int j = j0 + lane; j < HN; j += 64) {
+        const size_t sl = kr + (size_t)((rh + keep + (j - j0)) & gm);
+        const u32 r = sorted_rank[lo + (u32)(j - H0)];
+        S.rpm[sl] = rec.pm[r];
+        S.rval[sl] = rec.vals[r];
+        rg[sl] = G0 + (i64)r;
+    }
+    if (lane == 0) {
+        S.cnt[k] = cnt;
+        S.rhead[k] = rh;
+        S.rlen[k] = keep + (HN - j0);
+        if (HSUM) {
+            const u64 sb = (u64)__double_as_longlong(sum);
+            if (fd.sum >= 0) S.f[(size_t)fd.sum * S.nslots + k] = sb;
+            if (fd.avg >= 0) S.f[(size_t)fd.avg * S.nslots + k] = sb;
+        }
+        if (HMIN) kdq_store<1>(qn, S, fd.mn, k, dq_min);
+        if (HMAX) kdq_store<1>(qx, S, fd.mx, k, dq_max);
+    }
+}
+
+bool slx_keyed_ok(AggPlan ap) {
+    DFields fd;
+    return own_d_fields(ap, fd) && ap.n <= SH_MAX_AGGS;
+}
+
+void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
+                     const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
+                     i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
+                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk) {
+    if (nslots <= 0) return;
+    DFields fd;
+    own_d_fields(ap, fd);
+    KOut ko{};
+    ko.n = ap.n;
+    for (int q = 0; q < ap.n; q++) {
+        const int kind = ap.kind[q];
+        ko.src[q] = kind == AK_COUNT ? 0 : kind == AK_SUM_D ? 1 : kind == AK_AVG ? 2 : kind == AK_MIN_D ? 3 : 4;
+    }
+    const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
+#define SH_SLX_K(A, B, C)                                                                                          \
+    hipLaunchKernelGGL((k_slx_wkey<A, B, C>), dim3((unsigned)nslots), dim3(64), 0, s, key_off, (u32)nslots,       \
+                       sorted_rank, rec, aop, xop, xch, xts, xclk, useq, n_u, X0, G0, seq_base, send_size, S, rg, fd, \
+                       ko, cur_on, exp_on, rows, flags, rsclk)
+    if (hs && hn && hx) SH_SLX_K(true, true, true);
+    else if (hs && !hn && !hx) SH_SLX_K(true, false, false);
+    else if (!hs && hn && hx) SH_SLX_K(false, true, true);
+    else if (hs && hn) SH_SLX_K(true, true, false);
+    else if (hs && hx) SH_SLX_K(true, false, true);
+    else if (hn && !hx) SH_SLX_K(false, true, false);
+    else if (hx && !hn) SH_SLX_K(false, false, true);
+    else SH_SLX_K(false, false, false);
+#undef SH_SLX_K
+}
+
 void launch_sliding_own(hipStream_t s, const u32* rank_list, const i64* part_off, int P, int logP, SlRecords rec,
                         SlState S, AggPlan ap, i64 T, i64 send_size, i64 send_base, SlRows rows,
                         unsigned char* flags, SlRecords rec_by_rank) {

@@ -482,8 +482,14 @@ __global__ __launch_bounds__(64) void k_slx_walk(const u32* __restrict__ key_off
                     while (len > 0 && x_worse(kind, d[(h + len - 1) & rm], x)) len--;
                     d[(h + len) & rm] = x;
                     dql[a] = len + 1;
-                    // the running min/max is the deque's front (a value the add did not pop stays first)
-                    mm[a] = len == 0 ? x : d[h & rm];
+                    // minValue = value when strictly better (MinAttributeAggregatorExecutor.processAdd): the
+                    // deque's front except past a NaN, which no comparison pops
+                    {
+                        // (a select, not a conditional store: hipcc for gfx950 dropped the store of the
+                        // `if` form in this divergent branch — r05, tests/test_gpu_sliding_expired.py)
+                        const bool take = !mmh[a] || x_worse(kind, mm[a], x);
+                        mm[a] = take ? x : mm[a];
+                    }
                     mmh[a] = 1;
                 }
             }

@@ -75,6 +75,18 @@ def test_partitioned_time(rt, output, send_size):
     assert ref["ts"].size > 0
 
 
+@pytest.mark.parametrize("output", ["current", "all"])
+def test_partitioned_time_min_max_with_nan(rt, output):
+    """NaN values: no comparison pops them from the deque, so minValue is no longer the deque's front
+    (MinAttributeAggregatorExecutor.processAdd :178-190 keeps `minValue > value`)"""
+    ts, cols = stream(20_000, 8, 61, step=2)
+    rng = np.random.default_rng(62)
+    cols[1][rng.random(20_000) < 0.01] = np.nan
+    spec = abi.QuerySpec(SCHEMA, "time", 120, group_by=["p"], aggs=[("min", "v"), ("max", "v"), ("count", None)],
+                         partition="p", output=output, key_capacity=16)
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [6_000], 1) + [("advance", int(ts[-1]) + 200)], f"ptime nan {output}")
+
+
 def test_partitioned_time_no_group_by_zipf(rt):
     ts, cols = stream(300_000, 100_000, 53, step=2, zipf=True)
     spec = abi.QuerySpec(SCHEMA, "time", 500, aggs=[("sum", "v"), ("count", None)], partition="p", output="all",

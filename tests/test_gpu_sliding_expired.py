@@ -141,3 +141,80 @@ def test_c3_size_all_events(rt):
     assert n_exp > 1_000_000
     g.close()
     o.close()
+
+
+# ---- the wave-per-key replay (k_slx_wkey, round 5) against the oracle, and the lane walk it replaced
+# (SH_SLX_WAVE=0) on the same streams: count / sum / avg / min / max of one double column
+
+DAGGS = [("count", None), ("sum", "v"), ("min", "v"), ("max", "v"), ("avg", "v")]
+
+
+def dstream(n, keys, seed, step=6, distinct=True, nan_at=None, gap_at=None):
+    ts, cols = stream(n, keys, seed, step=step, gap_at=gap_at)
+    rng = np.random.default_rng(seed + 1)
+    if distinct:  # no repeated values: the parallel min / max path
+        cols[1] = rng.standard_normal(n) * 100.0
+    if nan_at is not None:
+        cols[1][nan_at] = np.nan
+    return ts, cols
+
+
+@pytest.mark.parametrize("wave", ["1", "0"])
+@pytest.mark.parametrize("output", ["all", "expired"])
+@pytest.mark.parametrize("distinct", [True, False])
+def test_wave_replay(rt, monkeypatch, wave, output, distinct):
+    """repeated values (the deque quirk: chunks fall back to the sequential deque) or distinct ones
+    (parallel range bests), TIMER calls, a gap that drains the window (counts 0, nulls), a filter"""
+    monkeypatch.setenv("SH_SLX_WAVE", wave)
+    ts, cols = dstream(40_000, 150, 41, distinct=distinct, gap_at=25_000)
+    spec = abi.QuerySpec(SCHEMA, "time", 500, group_by=["k"], aggs=DAGGS, filter=(">", "x", -45), output=output,
+                         key_capacity=256)
+    pushes = split_batches(SCHEMA, ts, cols, [1, 3_000, 24_999, 25_000, 31_000], 1)
+    pushes.insert(4, ("advance", int(ts[24_999]) + 250))
+    pushes.append(("advance", int(ts[-1]) + 300))
+    pushes.append(("advance", int(ts[-1]) + 10_000))
+    ref = both(rt, spec, pushes, f"wave={wave} {output} distinct={distinct}")
+    assert ref["expired"].sum() > 0 and ref["nulls"].any()
+
+
+@pytest.mark.parametrize("wave", ["1", "0"])
+@pytest.mark.parametrize("T,keys", [(30, 3), (5_000, 20), (200, 1)])
+def test_wave_replay_window_sizes(rt, monkeypatch, wave, T, keys):
+    """short windows (a chunk's own adds expire within it), long ones (deques past the LDS ring), one
+    key (every operation of the stream in one wave); send sizes 3"""
+    monkeypatch.setenv("SH_SLX_WAVE", wave)
+    ts, cols = dstream(30_000, keys, 43, step=3)
+    spec = abi.QuerySpec(SCHEMA, "time", T, group_by=["k"], aggs=[("max", "v"), ("avg", "v"), ("min", "v")],
+                         output="all", key_capacity=64)
+    pushes = split_batches(SCHEMA, ts, cols, [7_000, 7_001, 19_000], 3) + [("advance", int(ts[-1]) + T + 1)]
+    both(rt, spec, pushes, f"wave={wave} T={T} keys={keys}")
+
+
+@pytest.mark.parametrize("wave", ["1", "0"])
+def test_wave_replay_nan_sorted_values_and_sum_only(rt, monkeypatch, wave):
+    """a NaN breaks the deque's order (sequential from there); ascending / descending value runs (the
+    deque holds the whole window, spilling past the LDS ring); sum / count only (no deque)"""
+    monkeypatch.setenv("SH_SLX_WAVE", wave)
+    n = 24_000
+    ts, cols = dstream(n, 4, 47, step=2, nan_at=[9_000, 9_001])
+    cols[1][12_000:16_000] = np.arange(4_000, dtype=np.float64)          # ascending: max deque length 1,
+    cols[1][16_000:20_000] = -np.arange(4_000, dtype=np.float64) * 0.5    # min deque grows
+    spec = abi.QuerySpec(SCHEMA, "time", 2_000, group_by=["k"], aggs=DAGGS, output="all", key_capacity=16)
+    pushes = split_batches(SCHEMA, ts, cols, [5_000, 11_000, 17_000], 1) + [("advance", int(ts[-1]) + 5_000)]
+    both(rt, spec, pushes, f"wave={wave} nan / runs")
+    spec = abi.QuerySpec(SCHEMA, "time", 700, group_by=["k"], aggs=[("sum", "v"), ("count", None)],
+                         output="expired", key_capacity=16)
+    ts, cols = stream(n, 6, 53, step=2)  # eighths: exact cancellations reach 0.0 (canDestroy restarts)
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [8_000], 1) + [("advance", int(ts[-1]) + 800)],
+         f"wave={wave} sum only")
+
+
+@pytest.mark.parametrize("wave", ["1", "0"])
+def test_wave_replay_external_time(rt, monkeypatch, wave):
+    monkeypatch.setenv("SH_SLX_WAVE", wave)
+    ts, cols = dstream(30_000, 40, 59, step=5)
+    rng = np.random.default_rng(6)
+    cols[3] = cols[3] - (rng.random(30_000) < 0.1) * rng.integers(0, 600, 30_000)
+    spec = abi.QuerySpec(SCHEMA, "externalTime", 400, group_by=["k"], ts_attr="et", output="all", aggs=DAGGS,
+                         key_capacity=64)
+    both(rt, spec, split_batches(SCHEMA, ts, cols, [10_000, 10_001], 16), f"wave={wave} externalTime")
