@@ -150,7 +150,7 @@ void sliding_destroy(sh_query* q) {
                       &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
                       &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
                       &s->x_nexp, &s->xr_ts, &s->xr_rep, &s->xr_slot, &s->xr_ch, &s->xr_clk, &s->xr_exp,
-                      &s->xr_vals, &s->xr_nulls, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_key,
+                      &s->xr_vals, &s->xr_nulls, &s->xr_aos, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_key,
                       &s->pl_start, &s->pl_run, &s->pl_reg, &s->pl_toff, &s->pl_tsend, &s->pl_tclk, &s->pl_tpos,
                       &s->pl_fsend};
     for (DevBuf* b : bufs) b->release();
@@ -651,6 +651,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
         wp.clock0 = q->clock;
         wp.send_size = ss;
         wp.N = N;
+        wp.rec_seq = q->tune.sl_records_seq;  // (lane-strided records where they apply)
         launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                          s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
         if (ext) RCHK(s->rec_sclk.reserve(cap * 8, false));
@@ -778,19 +779,29 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     const int64_t n_ops = M + R;
     const int na = q->ap.n;
     const int64_t oc = std::max<int64_t>(n_ops, 1);
+    // the wave-per-key replay writes one record per row; the lane walk and pass-through write columns
+    const bool wave = na > 0 && q->tune.slx_wave && slx_keyed_ok(q->ap);
     RCHK(s->flags.reserve(oc + 16, false));
-    RCHK(s->xr_ts.reserve(oc * 8, false));
-    RCHK(s->xr_rep.reserve(oc * 8, false));
-    RCHK(s->xr_slot.reserve(oc * 4, false));
-    RCHK(s->xr_ch.reserve(oc * 8, false));
-    RCHK(s->xr_clk.reserve(oc * 8, false));
-    RCHK(s->xr_exp.reserve(oc, false));
-    RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * oc * 8, false));
-    RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * oc, false));
+    SlxRows rows{};
+    rows.cap = oc;
+    if (wave) {
+        rows.rw = slx_row_words(na);
+        RCHK(s->xr_aos.reserve((size_t)oc * rows.rw * 8, false));
+        rows.aos = s->xr_aos.as<u64>();
+    } else {
+        RCHK(s->xr_ts.reserve(oc * 8, false));
+        RCHK(s->xr_rep.reserve(oc * 8, false));
+        RCHK(s->xr_slot.reserve(oc * 4, false));
+        RCHK(s->xr_ch.reserve(oc * 8, false));
+        RCHK(s->xr_clk.reserve(oc * 8, false));
+        RCHK(s->xr_exp.reserve(oc, false));
+        RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * oc * 8, false));
+        RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * oc, false));
+        rows = SlxRows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                       s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                       s->xr_nulls.as<unsigned char>(), oc};
+    }
     HIPCHK(hipMemsetAsync(s->flags.p, 0, oc + 16, st));
-    SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
-                 s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
-                 s->xr_nulls.as<unsigned char>(), oc};
     HIPCHK(hipEventRecord(q->ev_agg0, st));
     if (q->ap.n == 0)
         launch_slx_pass(st, rec, M, s->x_aop.as<u64>(), s->x_xop.as<u64>(), s->x_xch.as<int64_t>(),
@@ -798,7 +809,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
                         q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
                         ext ? s->rec_sclk.as<int64_t>() : nullptr);
     else
-        (q->tune.slx_wave && slx_keyed_ok(q->ap) ? launch_slx_wkey : launch_slx_walk)(
+        (wave ? launch_slx_wkey : launch_slx_walk)(
             st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
             s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, s->x0,
             s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on, q->d.expired_on, rows,
@@ -829,7 +840,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
         RCHK(s->out_expired.reserve(rcap, false));
         RCHK(s->out_rep.reserve(rcap * 8, false));
         if (n_rows > 0)
-            launch_slx_emit(st, s->flags.as<unsigned char>(), n_ops, s->blk_cnt.as<int64_t>(), fblk, rows, na,
+            (wave ? launch_slx_emit_aos : launch_slx_emit)(st, s->flags.as<unsigned char>(), n_ops, s->blk_cnt.as<int64_t>(), fblk, rows, na,
                             q->kt.dev(), q->kp, rcap, s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(),
                             s->out_vals.as<u64>(), s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
                             s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>());

@@ -115,7 +115,13 @@ struct SlxRows {
     u64* vals;
     unsigned char* nulls;
     i64 cap;
+    // k_slx_wkey: one record of rw words per row instead of the columns above — {ts, rep, ch, clk,
+    // slot | exp << 32 | nulls << 40, values...} — one contiguous store per row (r05: the eight column
+    // stores per row were 23 of the replay's 34 ms in c3all)
+    u64* aos = nullptr;
+    int rw = 0;
 };
+constexpr int slx_row_words(int n_aggs) { return (5 + n_aggs + 1) & ~1; }
 void launch_slx_sends(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_pass_pre,
                       const i64* blk_tl_pre, int nblk, i64* sK, i64* scb, i64* slast);
 // kind 0: the calls among n sends -> (oK, oC, oS); kind 1: indices of the set flags -> oS.
@@ -148,6 +154,10 @@ void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, 
 void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
                      const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
                      SlxRows rows, unsigned char* flags, const i64* rsclk);
+// emission from the row records of k_slx_wkey (SlxRows.aos)
+void launch_slx_emit_aos(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
+                         int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                         unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);
 void launch_slx_emit(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
                      int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
                      unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep);

@@ -2215,7 +2215,14 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
     if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
     if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
     __syncthreads();
+#ifdef SH_XW_SEQ
+    bool par = false;  // (timing experiment only: the sequential deque throughout)
+#else
     bool par = HMIN || HMAX;
+#endif
+#ifdef SH_XW_NOROWS
+    u64 xw_chk = 0;
+#endif
     if (HMIN && par) par = dq_index_init<true>(qn, dq_min, di_min, S.rval + kr, rh0, gm, H0, lane);
     if (HMAX && par) par = dq_index_init<false>(qx, dq_max, di_max, S.rval + kr, rh0, gm, H0, lane);
     __syncthreads();
@@ -2392,11 +2399,15 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
                 const u64 czm = __ballot(in && !is_add && r_cnt == 0);
                 __syncthreads();
                 double sm = sum;
+#ifdef SH_XW_NOSUM
+                r_sum = s_val[lane] ^ czm;  // (timing experiment only: no sum chain)
+#else
                 for (int j = 0; j < m; j++) {
                     sm = sm + __longlong_as_double((i64)s_val[j]);
                     if ((czm >> j) & 1ull) sm = sm == 0.0 ? 0.0 : sm;
                     r_sum = lane == j ? (u64)__double_as_longlong(sm) : r_sum;
                 }
+#endif
                 sum = sm;
             }
         } else {
@@ -2462,28 +2473,39 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
                 rep = useq[u];
                 clk = xclk[u];
             }
-            rows.ts[my_row] = ts;
-            rows.rep[my_row] = rep;
-            rows.slot[my_row] = k;
-            rows.ch[my_row] = ch;
-            rows.clk[my_row] = clk;
-            rows.exp[my_row] = is_add ? 0 : 1;
+            u64 w[6 + SH_MAX_AGGS];
+            u64 nulls = 0;
+            w[0] = (u64)ts;
+            w[1] = (u64)rep;
+            w[2] = (u64)ch;
+            w[3] = (u64)clk;
 #pragma unroll
             for (int o = 0; o < SH_MAX_AGGS; o++) {
-                if (o >= ko.n) break;
+                w[5 + o] = 0;
+                if (o >= ko.n) continue;
                 const int src = ko.src[o];
                 u64 v = 0;
-                unsigned char nul = 0;
+                bool nul = false;
                 if (src == 0) v = (u64)r_cnt;
                 else if (src == 1) { nul = r_cnt == 0; v = r_sum; }
                 else if (src == 2) {
                     nul = r_cnt == 0;
                     if (!nul) v = (u64)__double_as_longlong(__longlong_as_double((i64)r_sum) / (double)r_cnt);
-                } else if (src == 3) { nul = (r_fl & 1u) ? 0 : 1; v = r_mn; }
-                else { nul = (r_fl & 2u) ? 0 : 1; v = r_mx; }
-                rows.vals[(size_t)o * rows.cap + my_row] = nul ? 0 : v;
-                rows.nulls[(size_t)o * rows.cap + my_row] = nul;
+                } else if (src == 3) { nul = (r_fl & 1u) == 0; v = r_mn; }
+                else { nul = (r_fl & 2u) == 0; v = r_mx; }
+                w[5 + o] = nul ? 0 : v;
+                nulls |= (u64)(nul ? 1 : 0) << o;
             }
+            w[4] = (u64)k | ((u64)(is_add ? 0 : 1) << 32) | (nulls << 40);
+#ifdef SH_XW_NOROWS
+#pragma unroll
+            for (int o = 0; o < 5 + SH_MAX_AGGS; o++) xw_chk += w[o] ^ (u64)my_row;  // (timing experiment only)
+#else
+            ulonglong2* dst = (ulonglong2*)(rows.aos + (size_t)my_row * rows.rw);
+#pragma unroll
+            for (int o = 0; o < (6 + SH_MAX_AGGS) / 2; o++)
+                if (2 * o < rows.rw) dst[o] = make_ulonglong2(w[2 * o], w[2 * o + 1]);
+#endif
         }
         if (qm) {  // (wave-uniform)
             const int lq = 63 - __clzll(qm);
@@ -2503,6 +2525,9 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         S.rval[sl] = rec.vals[r];
         rg[sl] = G0 + (i64)r;
     }
+#ifdef SH_XW_NOROWS
+    if (xw_chk == 0x5A5A5A5A5A5A5A5Aull) flags[0] = 2;
+#endif
     if (lane == 0) {
         S.cnt[k] = cnt;
         S.rhead[k] = rh;
@@ -2515,6 +2540,46 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         if (HMIN) kdq_store<1>(qn, S, fd.mn, k, dq_min);
         if (HMAX) kdq_store<1>(qx, S, fd.mx, k, dq_max);
     }
+}
+
+// emission from the row records: flagged operation indices in order, each row read as one record
+__global__ __launch_bounds__(kBlock) void k_slx_emit_aos(const unsigned char* __restrict__ flags, i64 n,
+                                                        const i64* __restrict__ blk_pre, const u64* __restrict__ rows,
+                                                        int rw, int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap,
+                                                        i64* out_ts, i64* out_keys, u64* out_vals,
+                                                        unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch,
+                                                        i64* out_clock, i64* out_rep) {
+    const i64 tile = (i64)blockIdx.x * kTile;
+    i64 run = blk_pre[blockIdx.x];
+    for (int it = 0; it < kItems; it++) {
+        const i64 j = tile + (i64)it * kBlock + threadIdx.x;
+        const i64 fl = j < n ? flags[j] : 0;
+        i64 tot;
+        const i64 r = run + block_excl_scan(fl, SumOp(), 0, &tot);
+        run += tot;
+        if (!fl) continue;
+        const ulonglong2* src = (const ulonglong2*)(rows + (size_t)j * rw);
+        const ulonglong2 a0 = src[0], a1 = src[1], a2 = src[2];
+        out_ts[r] = (i64)a0.x;
+        out_rep[r] = (i64)a0.y;
+        out_ch[r] = (i64)a1.x;
+        out_clock[r] = (i64)a1.y;
+        const u64 meta = a2.x;
+        unpack_key(kp, slot_key(kt, (u32)meta), out_keys + r, out_cap);
+        out_exp[r] = (unsigned char)((meta >> 32) & 1);
+        for (int a = 0; a < n_aggs; a++) {
+            out_vals[(size_t)a * out_cap + r] = a == 0 ? a2.y : rows[(size_t)j * rw + 5 + a];
+            out_nulls[(size_t)a * out_cap + r] = (unsigned char)((meta >> (40 + a)) & 1);
+        }
+    }
+}
+
+void launch_slx_emit_aos(hipStream_t s, const unsigned char* flags, i64 n, const i64* blk_pre, int nblk, SlxRows rows,
+                         int n_aggs, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals,
+                         unsigned char* out_nulls, unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep) {
+    if (nblk <= 0) return;
+    hipLaunchKernelGGL(k_slx_emit_aos, dim3(nblk), dim3(kBlock), 0, s, flags, n, blk_pre, rows.aos, rows.rw, n_aggs, kt,
+                       kp, out_cap, out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock, out_rep);
 }
 
 bool slx_keyed_ok(AggPlan ap) {
