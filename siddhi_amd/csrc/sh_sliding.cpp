@@ -150,7 +150,7 @@ void sliding_destroy(sh_query* q) {
                       &s->x_slast, &s->x_cK, &s->x_cC, &s->x_cS, &s->x_fire, &s->x_keep, &s->x_idx, &s->x_fK,
                       &s->x_fC, &s->x_fS, &s->x_blk, &s->x_xop, &s->x_xch, &s->x_xts, &s->x_xclk, &s->x_aop,
                       &s->x_nexp, &s->xr_ts, &s->xr_rep, &s->xr_slot, &s->xr_ch, &s->xr_clk, &s->xr_exp,
-                      &s->xr_vals, &s->xr_nulls, &s->xr_aos, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_key,
+                      &s->xr_vals, &s->xr_nulls, &s->xr_aos, &s->x_xa, &s->x_xx, &s->x_bnd, &s->pl_last_ts, &s->pl_last_seq, &s->pl_prev_seq, &s->pl_key,
                       &s->pl_start, &s->pl_run, &s->pl_reg, &s->pl_toff, &s->pl_tsend, &s->pl_tclk, &s->pl_tpos,
                       &s->pl_fsend};
     for (DevBuf* b : bufs) b->release();
@@ -746,18 +746,30 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     RCHK(s->useq.reserve(std::max<int64_t>(n_u, 1) * 8, true));
     launch_slx_append(st, rec.pm, rec.raw, M, q->seq, s->upm.as<int64_t>() + W0, s->useq.as<int64_t>() + W0);
     const int64_t nu1 = std::max<int64_t>(n_u, 1);
-    RCHK(s->x_xop.reserve(nu1 * 8, false));
-    RCHK(s->x_xch.reserve(nu1 * 8, false));
-    RCHK(s->x_xts.reserve(nu1 * 8, false));
-    RCHK(s->x_xclk.reserve(nu1 * 8, false));
-    RCHK(s->x_aop.reserve(cap * 8, false));
+    const int na = q->ap.n;
+    // the wave-per-key replay reads one record per add (xa) and per window position (xx) and writes one
+    // record per row; the lane walk and pass-through use the columns
+    const bool wave = na > 0 && q->tune.slx_wave && slx_keyed_ok(q->ap);
+    if (wave) {
+        RCHK(s->x_xa.reserve((size_t)cap * kXaWords * 8, false));
+        RCHK(s->x_xx.reserve((size_t)nu1 * kXaWords * 8, false));
+    } else {
+        RCHK(s->x_xop.reserve(nu1 * 8, false));
+        RCHK(s->x_xch.reserve(nu1 * 8, false));
+        RCHK(s->x_xts.reserve(nu1 * 8, false));
+        RCHK(s->x_xclk.reserve(nu1 * 8, false));
+        RCHK(s->x_aop.reserve(cap * 8, false));
+    }
     RCHK(s->x_nexp.reserve(8, false));
+    RCHK(s->x_bnd.reserve((size_t)(3 * (nu1 / kBlock + 2) + cap / kBlock + 2) * 8, false));
     HIPCHK(hipMemsetAsync(s->x_nexp.p, 0, 8, st));
-    launch_slx_expiry(st, s->upm.as<int64_t>(), n_u, W0, M, rec.clock, ext ? s->rec_sclk.as<int64_t>() : nullptr,
-                      rec.raw, ss, s->x_fK.as<int64_t>(), s->x_fC.as<int64_t>(), s->x_fS.as<int64_t>(), nF, T,
-                      s->x_xop.as<u64>(), s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(),
-                      (unsigned long long*)s->x_nexp.p);
-    launch_slx_aop(st, rec.clock, M, s->upm.as<int64_t>(), n_u, W0, T, s->x_aop.as<u64>());
+    const int64_t* rsclk = ext ? s->rec_sclk.as<int64_t>() : nullptr;
+    launch_slx_expiry(st, s->upm.as<int64_t>(), n_u, W0, M, rec.clock, rsclk, rec.raw, ss, s->x_fK.as<int64_t>(),
+                      s->x_fC.as<int64_t>(), s->x_fS.as<int64_t>(), nF, T, s->x_xop.as<u64>(), s->x_xch.as<int64_t>(),
+                      s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), (unsigned long long*)s->x_nexp.p,
+                      wave ? s->x_xx.as<u64>() : nullptr, s->useq.as<int64_t>(), rec.vals, s->x_bnd.as<int64_t>());
+    launch_slx_aop(st, rec.clock, M, s->upm.as<int64_t>(), n_u, W0, T, s->x_aop.as<u64>(),
+                   wave ? s->x_xa.as<u64>() : nullptr, rec, rsclk, s->x_bnd.as<int64_t>() + 3 * (nu1 / kBlock + 2));
     // the push's records sorted stably by key slot: each key's adds in arrival order
     RCHK(s->ranks.reserve(cap * 4, false));
     RCHK(s->p_slot.reserve(cap * 4, false));
@@ -777,10 +789,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     RCHK(read_count(q, (const int64_t*)s->x_nexp.p, &R));
     // ---- the replay (one lane per key slot) writes one row per (chunk, key) at its operation index
     const int64_t n_ops = M + R;
-    const int na = q->ap.n;
     const int64_t oc = std::max<int64_t>(n_ops, 1);
-    // the wave-per-key replay writes one record per row; the lane walk and pass-through write columns
-    const bool wave = na > 0 && q->tune.slx_wave && slx_keyed_ok(q->ap);
     RCHK(s->flags.reserve(oc + 16, false));
     SlxRows rows{};
     rows.cap = oc;
@@ -808,12 +817,15 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
                         s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, q->seq, ss,
                         q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(),
                         ext ? s->rec_sclk.as<int64_t>() : nullptr);
+    else if (wave)
+        launch_slx_wkey(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, s->x_xa.as<u64>(), s->x_xx.as<u64>(),
+                        n_u, s->x0, s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on,
+                        q->d.expired_on, rows, s->flags.as<unsigned char>());
     else
-        (wave ? launch_slx_wkey : launch_slx_walk)(
-            st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(), s->x_xop.as<u64>(),
-            s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(), s->useq.as<int64_t>(), n_u, s->x0,
-            s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap, q->d.current_on, q->d.expired_on, rows,
-            s->flags.as<unsigned char>(), ext ? s->rec_sclk.as<int64_t>() : nullptr);
+        launch_slx_walk(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->nslots, rec, s->x_aop.as<u64>(),
+                        s->x_xop.as<u64>(), s->x_xch.as<int64_t>(), s->x_xts.as<int64_t>(), s->x_xclk.as<int64_t>(),
+                        s->useq.as<int64_t>(), n_u, s->x0, s->g0, q->seq, ss, state_of(s), s->rg.as<int64_t>(), q->ap,
+                        q->d.current_on, q->d.expired_on, rows, s->flags.as<unsigned char>(), rsclk);
     HIPCHK(hipEventRecord(q->ev_agg1, st));
     HIPCHK(hipGetLastError());
     // ---- rows in operation order, one flush per chunk

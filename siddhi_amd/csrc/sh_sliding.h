@@ -135,10 +135,15 @@ void launch_slx_gather_calls(hipStream_t s, const i64* idx, i64 n, const i64* cK
 void launch_slx_gather_pend(hipStream_t s, const i64* idx, i64 n, const i64* pend, i64 n_pend, const i64* pm,
                             i64* out);
 void launch_slx_append(hipStream_t s, const i64* pm, const u32* raw, i64 M, i64 seq_base, i64* upm, i64* useq);
+// xx (nullable): the record form for k_slx_wkey instead of the xop / xch / xts / xclk columns (useq and
+// the records' first value column fill it)
 void launch_slx_expiry(hipStream_t s, const i64* upm, i64 n_u, i64 W0, i64 M, const i64* rclk, const i64* rsclk,
                        const u32* raw, i64 send_size, const i64* fK, const i64* fC, const i64* fS, i64 nF, i64 T,
-                       u64* xop, i64* xch, i64* xts, i64* xclk, unsigned long long* n_exp);
-void launch_slx_aop(hipStream_t s, const i64* rclk, i64 M, const i64* upm, i64 n_u, i64 W0, i64 T, u64* aop);
+                       u64* xop, i64* xch, i64* xts, i64* xclk, unsigned long long* n_exp, u64* xx,
+                       const i64* useq, const u64* rvals, i64* bnd);  // bnd: 3 * (n_u / kBlock + 2) words
+// xa (nullable): the record form for k_slx_wkey, from rec and (externalTime) the sends' clocks
+void launch_slx_aop(hipStream_t s, const i64* rclk, i64 M, const i64* upm, i64 n_u, i64 W0, i64 T, u64* aop,
+                    u64* xa, SlRecords rec, const i64* rsclk, i64* bnd);  // bnd: M / kBlock + 2 words
 void launch_slx_keyoff(hipStream_t s, const u32* slot_cnt, i64 nslots, u32* key_off, i64* tmp);
 void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
                      const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
@@ -147,10 +152,12 @@ void launch_slx_walk(hipStream_t s, const u32* key_off, const u32* sorted_rank, 
 // the same replay with one wave per key (sh_sliding_kernels.hip) for the count / sum / avg / min / max of
 // one double column shape (slx_keyed_ok)
 bool slx_keyed_ok(AggPlan ap);
-void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
-                     const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
-                     i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
-                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk);
+// xa: per record {aop, value, ts, clock, raw, pm}; xx: per window position {xop, value (this push's
+// records), ts, clock, event, chunk} (k_slx_aop / k_slx_expiry with their record outputs)
+constexpr int kXaWords = 6;
+void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, const u64* xa,
+                     const u64* xx, i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg,
+                     AggPlan ap, int cur_on, int exp_on, SlxRows rows, unsigned char* flags);
 void launch_slx_pass(hipStream_t s, SlRecords rec, i64 M, const u64* aop, const u64* xop, const i64* xch, const i64* xts,
                      const i64* xclk, const i64* useq, i64 n_u, i64 seq_base, i64 send_size, int cur_on, int exp_on,
                      SlxRows rows, unsigned char* flags, const i64* rsclk);

@@ -54,7 +54,7 @@ struct SlidingImpl {
     DevBuf rg, upm, useq, upm2, useq2, npend, npend2;
     int64_t x0 = 0, g0 = 0, w0 = 0, n_np = 0, np_front = 0;
     DevBuf x_sK, x_scb, x_slast, x_cK, x_cC, x_cS, x_fire, x_keep, x_idx, x_fK, x_fC, x_fS, x_blk, x_xop, x_xch,
-        x_xts, x_xclk, x_aop, x_nexp, xr_ts, xr_rep, xr_slot, xr_ch, xr_clk, xr_exp, xr_vals, xr_nulls, xr_aos;
+        x_xts, x_xclk, x_aop, x_nexp, xr_ts, xr_rep, xr_slot, xr_ch, xr_clk, xr_exp, xr_vals, xr_nulls, xr_aos, x_xa, x_xx, x_bnd;
     PinnedBuf x_h;
     // partitioned windows keyed by the partition (sh_plane.cpp): lane = 1 lengthBatch, 2 time; per slot the
     // open batch's last event, the last flushed batch's last event (expired rows), lastTimestamp, the

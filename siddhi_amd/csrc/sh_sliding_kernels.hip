@@ -2178,22 +2178,17 @@ constexpr u64 kSlxNoOp = ~0ull;
 
 template <bool HSUM, bool HMIN, bool HMAX>
 __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off, u32 nslots,
-                                                const u32* __restrict__ sorted_rank, SlRecords rec,
-                                                const u64* __restrict__ aop, const u64* __restrict__ xop,
-                                                const i64* __restrict__ xch, const i64* __restrict__ xts,
-                                                const i64* __restrict__ xclk, const i64* __restrict__ useq, i64 n_u,
-                                                i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S,
-                                                i64* __restrict__ rg, DFields fd, KOut ko, int cur_on, int exp_on,
-                                                SlxRows rows, unsigned char* __restrict__ flags,
-                                                const i64* __restrict__ rsclk) {
+                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ xa,
+                                                const u64* __restrict__ xx, i64 n_u, i64 X0, i64 G0, i64 seq_base,
+                                                i64 send_size, SlState S, i64* __restrict__ rg, DFields fd, KOut ko,
+                                                int cur_on, int exp_on, SlxRows rows,
+                                                unsigned char* __restrict__ flags) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ int di_min[HMIN ? kDqK : 1];
     __shared__ int di_max[HMAX ? kDqK : 1];
     __shared__ u64 s_aop[64], s_ax[64], s_xop[64], s_xx[64], s_val[64];
     __shared__ u64 s_pbn[HMIN ? 64 : 1], s_pbx[HMAX ? 64 : 1];
-    __shared__ u32 s_ar[64];
-    __shared__ i64 s_xu[64];
     __shared__ int s_sel[64];
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
@@ -2230,35 +2225,47 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
     int ia = 0, ie = 0;                    // adds / FIFO entries consumed
     i64 row_ch = -1, row_op = 0;           // the (chunk, key) row open at the chunk start
     for (;;) {
-        // ---- stage the next 64 adds and the next 64 FIFO entries
-        u64 a_op = kSlxNoOp, a_x = 0, x_op = kSlxNoOp, x_x = 0;
-        u32 a_r = 0;
-        i64 x_u = -1;
+        // ---- stage the next 64 adds and the next 64 FIFO entries: one 48-byte record each (xa by
+        // record, xx by window position), the row fields kept in the staging lane's registers
+        u64 a_op = kSlxNoOp, a_x = 0, a_ts = 0, a_clk = 0, a_ch = 0, a_rep = 0;
+        u64 x_op = kSlxNoOp, x_x = 0, x_ts = 0, x_clk = 0, x_ch = 0, x_rep = 0;
         if (ia + lane < A) {
-            a_r = sorted_rank[lo + (u32)(ia + lane)];
-            a_op = aop[a_r];
-            a_x = rec.vals[a_r];
+            const u32 ar = sorted_rank[lo + (u32)(ia + lane)];
+            const ulonglong2* q = (const ulonglong2*)(xa + (size_t)ar * kXaWords);
+            const ulonglong2 w0 = q[0], w1 = q[1], w2 = q[2];
+            a_op = w0.x;
+            a_x = w0.y;
+            a_ts = w1.x;
+            a_clk = w1.y;
+            a_ch = 2 * (send_size > 0 ? w2.x / (u64)send_size : 0) + 1;
+            a_rep = (u64)seq_base + w2.x;
         }
         const int p = ie + lane;
         if (p < HN) {
+            i64 x_u;
             if (p < H0) {
                 const size_t sl = kr + (size_t)((rh0 + p) & gm);
                 x_u = rg[sl] - X0;
                 x_x = S.rval[sl];
             } else {
-                const u32 r = sorted_rank[lo + (u32)(p - H0)];
-                x_u = G0 + (i64)r - X0;
-                x_x = rec.vals[r];
+                x_u = G0 + (i64)sorted_rank[lo + (u32)(p - H0)] - X0;
             }
-            if (x_u >= 0 && x_u < n_u) x_op = xop[x_u];
+            if (x_u >= 0 && x_u < n_u) {
+                const ulonglong2* q = (const ulonglong2*)(xx + (size_t)x_u * kXaWords);
+                const ulonglong2 w0 = q[0], w1 = q[1], w2 = q[2];
+                x_op = w0.x;
+                if (p >= H0) x_x = w0.y;
+                x_ts = w1.x;
+                x_clk = w1.y;
+                x_rep = w2.x;
+                x_ch = w2.y;
+            }
         }
         if (!__any(a_op != kSlxNoOp || x_op != kSlxNoOp)) break;
         s_aop[lane] = a_op;
         s_ax[lane] = a_x;
-        s_ar[lane] = a_r;
         s_xop[lane] = x_op;
         s_xx[lane] = x_x;
-        s_xu[lane] = x_u;
         __syncthreads();
         // ---- places in the merged order (both lists ascend; kNoOp pads the ends)
         int pa = 64, px = 64;
@@ -2292,8 +2299,11 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         const int si = sel & 63;
         const u64 op = in ? (is_add ? s_aop[si] : s_xop[si]) : 0;
         const u64 val = is_add ? s_ax[si] : s_xx[si];
-        const u32 r = s_ar[si];
-        const i64 u = s_xu[si];
+        // (every lane runs every shuffle)
+        const u64 sa_ts = shfl64(a_ts, si), sa_clk = shfl64(a_clk, si), sa_ch = shfl64(a_ch, si),
+                  sa_rep = shfl64(a_rep, si);
+        const u64 sx_ts = shfl64(x_ts, si), sx_clk = shfl64(x_clk, si), sx_ch = shfl64(x_ch, si),
+                  sx_rep = shfl64(x_rep, si);
         const u64 am = __ballot(is_add), xm = __ballot(in && !is_add);
         const int adds_le = __popcll(am & le), rems_le = __popcll(xm & le);
         i64 r_cnt = cnt + adds_le - rems_le;
@@ -2444,8 +2454,7 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         ia += na_c;
         ie += nx_c;
         // ---- rows: lanes segmented by their chunk among the qualifying operations
-        i64 ch = 0;
-        if (in) ch = is_add ? 2 * (send_size > 0 ? (i64)rec.raw[r] / send_size : 0) + 1 : xch[u];
+        const i64 ch = in ? (i64)(is_add ? sa_ch : sx_ch) : 0;
         const bool qual = in && (is_add ? cur_on : exp_on);
         const u64 qm = __ballot(qual);
         const u64 qb = qm & (le >> 1);  // qualifying lanes before this one
@@ -2463,16 +2472,8 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         const i64 nch = (i64)shfl64((u64)ch, nl);
         const bool end = qual && (!qa || nch != ch);
         if (end) {
-            i64 ts, rep, clk;
-            if (is_add) {
-                ts = rec.ts[r];
-                rep = seq_base + (i64)rec.raw[r];
-                clk = rsclk ? rsclk[r] : rec.clock[r];
-            } else {
-                ts = xts[u];
-                rep = useq[u];
-                clk = xclk[u];
-            }
+            const i64 ts = (i64)(is_add ? sa_ts : sx_ts), rep = (i64)(is_add ? sa_rep : sx_rep),
+                      clk = (i64)(is_add ? sa_clk : sx_clk);
             u64 w[6 + SH_MAX_AGGS];
             u64 nulls = 0;
             w[0] = (u64)ts;
@@ -2521,8 +2522,9 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
     for (int j = j0 + lane; j < HN; j += 64) {
         const size_t sl = kr + (size_t)((rh + keep + (j - j0)) & gm);
         const u32 r = sorted_rank[lo + (u32)(j - H0)];
-        S.rpm[sl] = rec.pm[r];
-        S.rval[sl] = rec.vals[r];
+        const u64* q = xa + (size_t)r * kXaWords;
+        S.rpm[sl] = (i64)q[5];
+        S.rval[sl] = q[1];
         rg[sl] = G0 + (i64)r;
     }
 #ifdef SH_XW_NOROWS
@@ -2587,10 +2589,9 @@ bool slx_keyed_ok(AggPlan ap) {
     return own_d_fields(ap, fd) && ap.n <= SH_MAX_AGGS;
 }
 
-void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, SlRecords rec,
-                     const u64* aop, const u64* xop, const i64* xch, const i64* xts, const i64* xclk, const i64* useq,
-                     i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg, AggPlan ap, int cur_on,
-                     int exp_on, SlxRows rows, unsigned char* flags, const i64* rsclk) {
+void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, i64 nslots, const u64* xa,
+                     const u64* xx, i64 n_u, i64 X0, i64 G0, i64 seq_base, i64 send_size, SlState S, i64* rg,
+                     AggPlan ap, int cur_on, int exp_on, SlxRows rows, unsigned char* flags) {
     if (nslots <= 0) return;
     DFields fd;
     own_d_fields(ap, fd);
@@ -2603,8 +2604,8 @@ void launch_slx_wkey(hipStream_t s, const u32* key_off, const u32* sorted_rank, 
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
 #define SH_SLX_K(A, B, C)                                                                                          \
     hipLaunchKernelGGL((k_slx_wkey<A, B, C>), dim3((unsigned)nslots), dim3(64), 0, s, key_off, (u32)nslots,       \
-                       sorted_rank, rec, aop, xop, xch, xts, xclk, useq, n_u, X0, G0, seq_base, send_size, S, rg, fd, \
-                       ko, cur_on, exp_on, rows, flags, rsclk)
+                       sorted_rank, xa, xx, n_u, X0, G0, seq_base, send_size, S, rg, fd, ko, cur_on, exp_on, rows,   \
+                       flags)
     if (hs && hn && hx) SH_SLX_K(true, true, true);
     else if (hs && !hn && !hx) SH_SLX_K(true, false, false);
     else if (!hs && hn && hx) SH_SLX_K(false, true, true);

@@ -264,28 +264,48 @@ void launch_slx_append(hipStream_t s, const i64* pm, const u32* raw, i64 M, i64 
 // push's records start at local index max(0, u - W0 + 1)) or a firing call f (fK[f] records before
 // it). The timer of call f precedes event point fK[f]. Operation index = u + records before the point.
 // one event's expiry point (see above); true when it has one
+// The searches are monotone in u (PM and u - W0 grow with u), so a block's answers lie between those of
+// its first and last event: [ie0, ie1] and [f0, f1] bound every thread's search (a few steps over lines
+// the block shares instead of 25 over the whole push).
+struct XBounds {
+    i64 ie0, ie1, fa0, fa1, fb0, fb1;
+};
 __device__ __forceinline__ bool slx_expiry_one(i64 u, const i64* __restrict__ upm, i64 W0, i64 M,
                                                const i64* __restrict__ rclk, const i64* __restrict__ rsclk,
                                                const u32* __restrict__ raw, i64 send_size, const i64* __restrict__ fK,
                                                const i64* __restrict__ fC, const i64* __restrict__ fS, i64 nF, i64 T,
-                                               u64* xop, i64* xch, i64* xts, i64* xclk) {
+                                               u64* xop, i64* xch, i64* xts, i64* xclk, const XBounds& B,
+                                               u64* xx, const i64* __restrict__ useq, const u64* __restrict__ rvals) {
     const i64 th = sat_add(upm[u], T);
     const i64 lo_i = max((i64)0, u - W0 + 1);
-    const i64 ie = lb_ge(rclk, lo_i, M, th);
-    const i64 f = max(lb_ge(fK, 0, nF, u - W0 + 1), lb_ge(fC, 0, nF, th));
+    const i64 ie = lb_ge(rclk, max(lo_i, B.ie0), B.ie1, th);
+    const i64 f = max(lb_ge(fK, B.fa0, B.fa1, u - W0 + 1), lb_ge(fC, B.fb0, B.fb1, th));
     u64 op = kNoOp;
+    i64 c_ch = 0, c_ts = 0, c_clk = 0;
     if (f < nF && (ie >= M || fK[f] <= ie)) {
         op = (u64)(u + fK[f]);
-        xch[u] = 2 * fS[f];
-        xts[u] = fC[f];
-        xclk[u] = fC[f];
+        c_ch = 2 * fS[f];
+        c_ts = fC[f];
+        c_clk = fC[f];
     } else if (ie < M) {
         op = (u64)(u + ie);
-        xch[u] = 2 * (send_size > 0 ? (i64)raw[ie] / send_size : 0) + 1;
-        xts[u] = rclk[ie];
-        xclk[u] = rsclk ? rsclk[ie] : rclk[ie];
+        c_ch = 2 * (send_size > 0 ? (i64)raw[ie] / send_size : 0) + 1;
+        c_ts = rclk[ie];
+        c_clk = rsclk ? rsclk[ie] : rclk[ie];
     }
-    xop[u] = op;
+    if (xx) {
+        ulonglong2* o = (ulonglong2*)(xx + (size_t)u * kXaWords);
+        o[0] = make_ulonglong2(op, u >= W0 ? rvals[u - W0] : 0ull);
+        o[1] = make_ulonglong2((u64)c_ts, (u64)c_clk);
+        o[2] = make_ulonglong2((u64)useq[u], (u64)c_ch);
+    } else {
+        if (op != kNoOp) {
+            xch[u] = c_ch;
+            xts[u] = c_ts;
+            xclk[u] = c_clk;
+        }
+        xop[u] = op;
+    }
     return op != kNoOp;
 }
 
@@ -294,37 +314,100 @@ __global__ __launch_bounds__(kBlock) void k_slx_expiry(const i64* __restrict__ u
                                                       const u32* __restrict__ raw, i64 send_size,
                                                       const i64* __restrict__ fK, const i64* __restrict__ fC,
                                                       const i64* __restrict__ fS, i64 nF, i64 T, u64* xop, i64* xch,
-                                                      i64* xts, i64* xclk, unsigned long long* n_exp) {
-    const i64 u = (i64)blockIdx.x * kBlock + threadIdx.x;
+                                                      i64* xts, i64* xclk, unsigned long long* n_exp, u64* xx,
+                                                      const i64* __restrict__ useq, const u64* __restrict__ rvals,
+                                                      const i64* __restrict__ bnd) {
+    // the block's bounds: the full searches of its first event and of the next block's (k_slx_xbounds)
+    const int bk = blockIdx.x;
+    const XBounds B{bnd[3 * bk], bnd[3 * bk + 3], bnd[3 * bk + 1], bnd[3 * bk + 4], bnd[3 * bk + 2], bnd[3 * bk + 5]};
+    const i64 u = (i64)bk * kBlock + threadIdx.x;
     const bool has = u < n_u && slx_expiry_one(u, upm, W0, M, rclk, rsclk, raw, send_size, fK, fC, fS, nF, T, xop,
-                                               xch, xts, xclk);
-    // n_exp = 1 + the last event with an expiry point: one atomic per wave, from its highest such lane
-    // (u grows with the lane) — one atomic per event on one address serialised at the L2
-    const u64 b = __ballot(has);
-    if (b && (int)(threadIdx.x & 63) == 63 - (int)__clzll(b)) atomicMax(n_exp, (unsigned long long)(u + 1));
+                                               xch, xts, xclk, B, xx, useq, rvals);
+    // The events with an expiry point form a prefix of U (PM and the first eligible point both grow with
+    // u), so n_exp is written once, by the last of them: the lane whose successor has none. (r04 took one
+    // atomicMax per wave on one address: 680k serialised L2 atomics, 5.4 of the 6 ms of c3all's kernel.)
+    __shared__ unsigned char s_has[kBlock + 1];
+    s_has[threadIdx.x] = has ? 1 : 0;
+    if (threadIdx.x == kBlock - 1) {
+        // the next block's first event: its full searches are the bounds' upper entries
+        bool hn = false;
+        if (u + 1 < n_u) {
+            const i64 f = max(B.fa1, B.fb1);
+            hn = (f < nF && (B.ie1 >= M || fK[f] <= B.ie1)) || B.ie1 < M;
+        }
+        s_has[kBlock] = hn ? 1 : 0;
+    }
+    __syncthreads();
+    if (has && !s_has[threadIdx.x + 1]) *n_exp = (unsigned long long)(u + 1);
+}
+
+// the full searches at every block start u = b * kBlock (and at n_u - 1 past the last block): entry b
+// bounds block b from below, entry b + 1 from above; one thread each, all in parallel
+__global__ __launch_bounds__(kBlock) void k_slx_xbounds(const i64* __restrict__ upm, i64 n_u, i64 W0, i64 M,
+                                                       const i64* __restrict__ rclk, const i64* __restrict__ fK,
+                                                       const i64* __restrict__ fC, i64 nF, i64 T, int nb, i64* bnd) {
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b > nb) return;
+    const i64 u = b < nb ? (i64)b * kBlock : n_u - 1;
+    const i64 th = sat_add(upm[u], T);
+    bnd[3 * b] = lb_ge(rclk, max((i64)0, u - W0 + 1), M, th);
+    bnd[3 * b + 1] = lb_ge(fK, 0, nF, u - W0 + 1);
+    bnd[3 * b + 2] = lb_ge(fC, 0, nF, th);
 }
 
 void launch_slx_expiry(hipStream_t s, const i64* upm, i64 n_u, i64 W0, i64 M, const i64* rclk, const i64* rsclk,
                        const u32* raw, i64 send_size, const i64* fK, const i64* fC, const i64* fS, i64 nF, i64 T,
-                       u64* xop, i64* xch, i64* xts, i64* xclk, unsigned long long* n_exp) {
+                       u64* xop, i64* xch, i64* xts, i64* xclk, unsigned long long* n_exp, u64* xx, const i64* useq,
+                       const u64* rvals, i64* bnd) {
     if (n_u <= 0) return;
-    hipLaunchKernelGGL(k_slx_expiry, dim3((unsigned)((n_u + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, upm, n_u, W0, M,
-                       rclk, rsclk, raw, send_size, fK, fC, fS, nF, T, xop, xch, xts, xclk, n_exp);
+    const int nb = (int)((n_u + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_slx_xbounds, dim3((unsigned)((nb + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, upm, n_u, W0,
+                       M, rclk, fK, fC, nF, T, nb, bnd);
+    hipLaunchKernelGGL(k_slx_expiry, dim3((unsigned)nb), dim3(kBlock), 0, s, upm, n_u, W0, M, rclk, rsclk, raw,
+                       send_size, fK, fC, fS, nF, T, xop, xch, xts, xclk, n_exp, xx, useq, rvals, bnd);
 }
 
 // add of record i: after the removes of every point up to and including its own
 // (X(i) - X0 = min(W0 + i, #{u : PM(u) + T <= clock_i}))
 __global__ __launch_bounds__(kBlock) void k_slx_aop(const i64* __restrict__ rclk, i64 M, const i64* __restrict__ upm,
-                                                   i64 n_u, i64 W0, i64 T, u64* aop) {
+                                                   i64 n_u, i64 W0, i64 T, u64* aop, u64* xa, SlRecords rec,
+                                                   const i64* __restrict__ rsclk, const i64* __restrict__ bnd) {
+    // (monotone in i: the full searches at this block's start and the next one's bound every thread's)
     const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= M) return;
-    aop[i] = (u64)(i + min(W0 + i, n_expirable(upm, n_u, T, rclk[i])));
+    i64 lo = bnd[blockIdx.x], hi = bnd[blockIdx.x + 1];
+    const i64 c = rclk[i];
+    while (lo < hi) {
+        const i64 m = (lo + hi) >> 1;
+        if (sat_add(upm[m], T) <= c) lo = m + 1;
+        else hi = m;
+    }
+    const u64 op = (u64)(i + min(W0 + i, lo));
+    if (xa) {
+        ulonglong2* o = (ulonglong2*)(xa + (size_t)i * kXaWords);
+        o[0] = make_ulonglong2(op, rec.vals[i]);
+        o[1] = make_ulonglong2((u64)rec.ts[i], (u64)(rsclk ? rsclk[i] : c));
+        o[2] = make_ulonglong2((u64)rec.raw[i], (u64)rec.pm[i]);
+    } else {
+        aop[i] = op;
+    }
 }
 
-void launch_slx_aop(hipStream_t s, const i64* rclk, i64 M, const i64* upm, i64 n_u, i64 W0, i64 T, u64* aop) {
+__global__ __launch_bounds__(kBlock) void k_slx_abounds(const i64* __restrict__ rclk, i64 M, const i64* __restrict__ upm,
+                                                       i64 n_u, i64 T, int nb, i64* bnd) {
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b > nb) return;
+    bnd[b] = n_expirable(upm, n_u, T, rclk[b < nb ? (i64)b * kBlock : M - 1]);
+}
+
+void launch_slx_aop(hipStream_t s, const i64* rclk, i64 M, const i64* upm, i64 n_u, i64 W0, i64 T, u64* aop, u64* xa,
+                    SlRecords rec, const i64* rsclk, i64* bnd) {
     if (M <= 0) return;
-    hipLaunchKernelGGL(k_slx_aop, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rclk, M, upm, n_u, W0,
-                       T, aop);
+    const int nb = (int)((M + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_slx_abounds, dim3((unsigned)((nb + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rclk, M, upm,
+                       n_u, T, nb, bnd);
+    hipLaunchKernelGGL(k_slx_aop, dim3((unsigned)nb), dim3(kBlock), 0, s, rclk, M, upm, n_u, W0, T, aop, xa, rec, rsclk,
+                       bnd);
 }
 
 // ---- the replay: one lane per key slot walks its adds (records sorted stably by slot) and the
