@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 10
+#define SH_ABI_VERSION 11
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -365,6 +365,10 @@ typedef struct {
                             first one picks the only partition that ever flushes); sliding
                             time(T): max ts over the slice's passing events (INT64_MIN: none,
                             the slice's PM contribution); else 0                              */
+    int64_t ts_min;      /* min / max timestamp over the slice's events (INT64_MAX / INT64_MIN:  */
+    int64_t ts_max;      /* empty): when the whole push spans less than 2^32, every record carries
+                            its timestamp as a 32-bit offset from the push's minimum (ABI 11:
+                            20-byte C2 records instead of 24)                                 */
 } sh_slice_summary;
 
 typedef struct {
@@ -378,7 +382,8 @@ typedef struct {
 typedef struct sh_shard sh_shard;
 int sh_shard_create(sh_ctx* ctx, const sh_query_desc* desc, int32_t rank, int32_t world, sh_shard** out);
 int sh_shard_destroy(sh_shard* s);
-/* Bytes per packed event record (depends on the query's value columns). */
+/* Bytes per packed event record at most (depends on the query's value columns; a push whose events
+ * span less than 2^32 in time packs 4 bytes less per record when the wire key is 32-bit). */
 int sh_shard_record_bytes(sh_shard* s, int64_t* out);
 /* Phase 1 (device slice). */
 int sh_shard_summarize(sh_shard* s, const sh_batch* slice, sh_slice_summary* out);

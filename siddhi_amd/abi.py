@@ -79,7 +79,7 @@ class Out(C.Structure):
 
 class SliceSummary(C.Structure):
     _fields_ = [("n", C.c_int64), ("n_pass", C.c_int64), ("max_tl", C.c_int64), ("first_clock", C.c_int64),
-                ("first_key", C.c_int64)]
+                ("first_key", C.c_int64), ("ts_min", C.c_int64), ("ts_max", C.c_int64)]
 
 
 class Bound(C.Structure):

@@ -331,6 +331,8 @@ struct ShardSrc {
     i64 gbase[kMaxShards];      // global stream index of each source slice's first event
     int G;
     int key32;
+    int narrow;                 // ts as a 32-bit offset from tsbase (the push's minimum timestamp)
+    i64 tsbase;
 };
 // 8-byte raw columns a shard record carries: the value columns, then the columns of time-bucket key
 // components (their raw value is needed to re-derive the bucket; only the other components travel
@@ -340,7 +342,8 @@ struct RawPlan {
     int src[SH_MAX_COLS];
 };
 void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan wkp, RawPlan rp, int G,
-                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32);
+                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32,
+                       int narrow = 0, i64 tsbase = 0);
 struct ColRoles {
     int role[SH_MAX_COLS];  // -1 unused, 0..15 raw slot, 16 + g wire-key component g
     int n;

@@ -2375,10 +2375,14 @@ void launch_sc_flushes(hipStream_t s, i64 T, const i64* osd, const u32* pre, con
 __global__ __launch_bounds__(kBlock) void k_xt_first_send(const i64* __restrict__ ts, i64 N, i64 send_size, i64 L,
                                                           unsigned long long* out) {
     const i64 n_sends = send_size > 0 ? (N + send_size - 1) / send_size : 1;
+    i64 first = INT64_MAX;  // this thread's first qualifying send (j grows along the stride)
     for (i64 j = (i64)blockIdx.x * kBlock + threadIdx.x; j < n_sends; j += (i64)gridDim.x * kBlock) {
         const i64 last = send_size > 0 ? min((j + 1) * send_size, N) - 1 : N - 1;
-        if (ts[last] >= L) atomicMin(out, (unsigned long long)j);
+        if (ts[last] >= L) { first = j; break; }
     }
+    // one atomic per block (per send, every send past the crossing queued on one address)
+    first = block_reduce(first, MinOp(), INT64_MAX);
+    if (threadIdx.x == 0 && first != INT64_MAX) atomicMin(out, (unsigned long long)first);
 }
 
 // passing events of the push in [0, hi): the open batch's events before a timeout's send

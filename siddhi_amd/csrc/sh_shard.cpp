@@ -75,16 +75,21 @@ struct sh_shard {
         std::vector<int64_t> off;
         int64_t clock, E0;
         bool clock_valid, e0_valid;
+        int narrow;      // the push's records carry ts as a 32-bit offset from tsbase
+        int64_t tsbase;
     };
     // the stream state as of the push being consumed (the ingest may already be a push ahead)
     int64_t cur_clock = 0, cur_E0 = 0;
     bool cur_clock_valid = false, cur_e0_valid = false;
+    int cur_narrow = 0;
+    int64_t cur_tsbase = 0;
     std::deque<InFlight> fl;
     PinnedBuf h_bgw;                      // pinned copies of the window starts being uploaded
     // ingest scratch
     int64_t slice_n = -1;
-    DevBuf blk_pass, blk_tl, blk_first, info, code, counts, tmp, part_off, bounds;
+    DevBuf blk_pass, blk_tl, blk_first, info, code, counts, tmp, part_off, bounds, tsmm;
     PushInfo* h_info = nullptr;
+    int64_t* h_tsmm = nullptr;  // pinned: the slice's ts min / max
     std::vector<sh_bound> my_bounds;
     // owner scratch
     DevBuf u_ts, u_wcol, u_gidx, u_cols[SH_MAX_COLS], u_bg, u_bw;
@@ -228,10 +233,11 @@ extern "C" int sh_shard_destroy(sh_shard* s) {
     if (s->owner) sh_query_destroy(s->owner);
     DevBuf* bufs[] = {&s->blk_pass, &s->blk_tl, &s->blk_first, &s->info, &s->code, &s->counts, &s->tmp,
                       &s->part_off, &s->bounds, &s->u_ts, &s->u_wcol, &s->u_gidx, &s->u_bg, &s->u_bw,
-                      &s->sl_clk, &s->sl_pmv};
+                      &s->sl_clk, &s->sl_pmv, &s->tsmm};
     for (DevBuf* b : bufs) b->release();
     for (auto& c : s->u_cols) c.release();
     if (s->h_info) (void)hipHostFree(s->h_info);
+    if (s->h_tsmm) (void)hipHostFree(s->h_tsmm);
     delete s;
     return SH_OK;
 }
@@ -249,6 +255,20 @@ static ColSet colset(const sh_shard* s, const sh_batch* b) {
     return cs;
 }
 
+// the slice's timestamp range (every event: a superset of the passing ones), read with the summary
+static int slice_ts_range(sh_shard* s, const sh_batch* b, sh_slice_summary* out) {
+    (void)out;
+    RCHK(s->tsmm.reserve(minmax_scratch_bytes(), false));
+    if (!s->h_tsmm) {
+        if (hipHostMalloc((void**)&s->h_tsmm, 16, hipHostMallocDefault) != hipSuccess)
+            return sh_fail(SH_ERR_OOM, "pinned alloc failed");
+    }
+    launch_minmax_i64(s->ctx->stream, b->ts, b->n, s->tsmm.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_tsmm, s->tsmm.p, 16, hipMemcpyDeviceToHost, s->ctx->stream));
+    return SH_OK;
+}
+
 // Phase 1: pass count, send clocks and the first passing send of the slice (k_blockagg + k_scan_blocks).
 extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summary* out) {
     SH_RANGE("sh_shard_summarize");
@@ -257,7 +277,7 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative slice size");
     if (b->n > 0 && (b->send_size < 1 || !b->ts))
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded slices need send_size >= 1 (slices cut at send boundaries)");
-    *out = sh_slice_summary{b->n, 0, INT64_MIN, INT64_MIN};
+    *out = sh_slice_summary{b->n, 0, INT64_MIN, INT64_MIN, 0, INT64_MAX, INT64_MIN};
     s->slice_n = b->n;
     if (b->n == 0) return SH_OK;
     hipStream_t st = s->ctx->stream;
@@ -273,10 +293,12 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
         wp.send_size = b->send_size;
         launch_sl_prefix(st, b->ts, colset(s, b), s->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                          s->blk_first.as<int64_t>(), nblk, s->info.as<SlInfo>());
-        HIPCHK(hipGetLastError());
+        RCHK(slice_ts_range(s, b, out));
         SlInfo si{};
         HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
+        out->ts_min = s->h_tsmm[0];
+        out->ts_max = s->h_tsmm[1];
         si = *(const SlInfo*)s->h_info;
         out->n_pass = si.total_pass;
         out->max_tl = si.max_tl;
@@ -293,9 +315,11 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
     wp.pcol1 = (s->partitioned && !s->p0_known) ? s->d.partition_col + 1 : 0;
     launch_scan_blocks(st, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), s->blk_first.as<int64_t>(), nblk, b->ts,
                        wp, s->info.as<PushInfo>(), nullptr, colset(s, b));
-    HIPCHK(hipGetLastError());
+    RCHK(slice_ts_range(s, b, out));
     HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    out->ts_min = s->h_tsmm[0];
+    out->ts_max = s->h_tsmm[1];
     out->n_pass = s->h_info->total_pass;
     out->max_tl = s->h_info->max_tl;
     out->first_clock = s->h_info->first_pass == INT64_MAX ? INT64_MIN : s->h_info->first_clk;
@@ -307,7 +331,21 @@ extern "C" int sh_shard_summarize(sh_shard* s, const sh_batch* b, sh_slice_summa
 
 static sh_shard::InFlight Shard_InFlight(const sh_shard* s) {
     return sh_shard::InFlight{s->cur_W_base, s->cur_W_end, s->cur_seq, s->cur_send_base, s->cur_send_size, s->cur_n,
-                              s->cur_off, s->clock, s->E0, s->clock_valid, s->e0_valid};
+                              s->cur_off, s->clock, s->E0, s->clock_valid, s->e0_valid, s->cur_narrow, s->cur_tsbase};
+}
+
+// The record format of a push, from the G summaries (the same on every rank): with a 32-bit wire key
+// and all of the push's timestamps within 2^32 of its minimum, ts travels as a 32-bit offset from that
+// minimum (C2: 20 bytes per record instead of 24 — the xGMI bytes of the all-to-all).
+static void push_format(sh_shard* s, const sh_slice_summary* all) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int r = 0; r < s->world; r++) {
+        if (all[r].n <= 0) continue;
+        lo = std::min(lo, all[r].ts_min);
+        hi = std::max(hi, all[r].ts_max);
+    }
+    s->cur_narrow = s->key32 && lo <= hi && (uint64_t)hi - (uint64_t)lo <= 0xFFFFFFFFull;
+    s->cur_tsbase = s->cur_narrow ? lo : 0;
 }
 
 // Phase 2 of a sliding time(T) query: every passing event gets its send's global clock and the global
@@ -318,7 +356,9 @@ static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch
                         const std::vector<int64_t>& cin, const std::vector<int64_t>& off, int64_t clock_end,
                         int64_t n_total) {
     const int G = s->world;
-    const int64_t RB = 4 * (int64_t)s->rec_words;
+    push_format(s, all);
+    const int RW = s->rec_words - s->cur_narrow;
+    const int64_t RB = 4 * (int64_t)RW;
     int64_t pm_in = s->sl_pm, pm_end = s->sl_pm, sends = 0;
     const int64_t ss = std::max<int64_t>(1, b->send_size);
     for (int r = 0; r < G; r++) {
@@ -355,7 +395,7 @@ static int pack_sliding(sh_shard* s, const sh_slice_summary* all, const sh_batch
         cs.ptr[cs.n + 1] = s->sl_pmv.p; cs.type[cs.n + 1] = SH_T_LONG;
         cs.n += 2;
         launch_shard_pack(st, cs, b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk, s->counts.as<int64_t>(),
-                          (unsigned char*)send_buf, s->rec_words, s->key32);
+                          (unsigned char*)send_buf, RW, s->key32, s->cur_narrow, s->cur_tsbase);
         launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
         HIPCHK(hipGetLastError());
         std::vector<int64_t> po(G + 1);
@@ -415,6 +455,8 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     }
     const int64_t clock_end = c, n_total = o;
     if (s->seq + (uint64_t)n_total >= (1ull << 40)) return sh_fail(SH_ERR_UNSUPPORTED, "stream longer than 2^40 events");
+    push_format(s, all);
+    const int RW = s->rec_words - s->cur_narrow;  // this push's record words
     if (s->sliding) return pack_sliding(s, all, b, send_buf, send_bytes, bounds, n_bounds, cin, off, clock_end, n_total);
     // R12: the partition of the stream's first passing event armed the shared timer and is the only
     // one that ever flushes; from here on the ingest keeps only its events (the owner needs no filter)
@@ -491,7 +533,8 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
         launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
         launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk,
-                          s->counts.as<int64_t>(), (unsigned char*)send_buf, s->rec_words, s->key32);
+                          s->counts.as<int64_t>(), (unsigned char*)send_buf, RW, s->key32, s->cur_narrow,
+                          s->cur_tsbase);
         launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
         HIPCHK(hipGetLastError());
         std::vector<int64_t> po(G + 1);
@@ -509,7 +552,7 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
             s->my_bounds.push_back(sh_bound{x.W, x.clock, (int64_t)s->seq + off[s->rank] + x.idx, 0});
         std::sort(s->my_bounds.begin(), s->my_bounds.end(),
                   [](const sh_bound& a, const sh_bound& c2) { return a.gidx < c2.gidx; });
-        for (int r = 0; r < G; r++) send_bytes[r] = (po[r + 1] - po[r]) * RB;
+        for (int r = 0; r < G; r++) send_bytes[r] = (po[r + 1] - po[r]) * 4 * (int64_t)RW;
     }
     // commit the global stream state (every rank computes the same values)
     if (clock_end != INT64_MIN) {
@@ -572,8 +615,11 @@ static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* rec
     ShardSrc src{};
     src.G = s->world;
     src.key32 = s->key32;
+    src.narrow = s->cur_narrow;
+    src.tsbase = s->cur_tsbase;
     int64_t acc = 0;
-    const int64_t RB = 4 * (int64_t)s->rec_words;
+    const int RW = s->rec_words - s->cur_narrow;
+    const int64_t RB = 4 * (int64_t)RW;
     for (int g = 0; g < s->world; g++) {
         src.start[g] = acc;
         acc += recv_bytes[g] / RB;
@@ -581,7 +627,7 @@ static int consume_sliding(sh_shard* s, const void* recv_buf, const int64_t* rec
     }
     src.start[s->world] = acc;
     if (M > 0)
-        launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->wkp, s->roles, src, nullptr,
+        launch_shard_unpack(st, (const unsigned char*)recv_buf, M, RW, s->wkp, s->roles, src, nullptr,
                             nullptr, 0, 0, s->u_ts.as<int64_t>(), cp, s->u_wcol.as<int>(), s->u_gidx.as<u64>());
     HIPCHK(hipGetLastError());
     const int nc = s->d.n_cols;
@@ -617,10 +663,13 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         s->cur_clock_valid = f.clock_valid;
         s->cur_E0 = f.E0;
         s->cur_e0_valid = f.e0_valid;
+        s->cur_narrow = f.narrow;
+        s->cur_tsbase = f.tsbase;
     }
     s->packed = !s->fl.empty();
     if (s->agg) host_out = 0;  // the root's flushes feed the roll-up levels on the device
-    const int64_t RB = 4 * (int64_t)s->rec_words;
+    const int RW = s->rec_words - s->cur_narrow;  // the consumed push's record words
+    const int64_t RB = 4 * (int64_t)RW;
     int64_t bytes = 0;
     for (int r = 0; r < s->world; r++) {
         if (recv_bytes[r] < 0 || recv_bytes[r] % RB) return sh_fail(SH_ERR_INVALID, "received block not a whole number of records");
@@ -670,6 +719,8 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     ShardSrc src{};
     src.G = s->world;
     src.key32 = s->key32;
+    src.narrow = s->cur_narrow;
+    src.tsbase = s->cur_tsbase;
     int64_t acc = 0;
     for (int g = 0; g < s->world; g++) {
         src.start[g] = acc;
@@ -677,7 +728,7 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
         src.gbase[g] = s->cur_seq + s->cur_off[g];
     }
     src.start[s->world] = acc;
-    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, s->rec_words, s->wkp, s->roles, src,
+    launch_shard_unpack(st, (const unsigned char*)recv_buf, M, RW, s->wkp, s->roles, src,
                         s->u_bg.as<int64_t>(), s->u_bw.as<int64_t>(), nb, s->cur_W_base, s->u_ts.as<int64_t>(), cp,
                         s->u_wcol.as<int>(), s->u_gidx.as<u64>());
     HIPCHK(hipGetLastError());

@@ -201,7 +201,7 @@ void launch_shard_sl_assign(hipStream_t s, const i64* ts, ColSet cols, FilterPro
 __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* __restrict__ ts,
                                                       const u32* __restrict__ code, KeyPlan kp, RawPlan rp, int G,
                                                       i64 N, int nblk, const i64* __restrict__ offsets, u32* out,
-                                                      int rec_words, int key32) {
+                                                      int rec_words, int key32, int narrow, i64 tsbase) {
     __shared__ u32 running[kMaxShards];
     __shared__ u32 wave_cnt[kBlock / 64][kMaxShards];
     const int tile = blockIdx.x;
@@ -243,9 +243,20 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
                 rec[3] = 0;
                 w8 = 4;
             }
-            u64* r8 = (u64*)(rec + w8);
-            r8[0] = (u64)ts[e];
-            for (int j = 0; j < rp.n; j++) r8[1 + j] = (u64)load_raw(cols, rp.src[j], e);
+            if (narrow) {
+                // (32-bit wire key only) ts as its offset from the push's minimum, the raw words as
+                // 4-byte-aligned pairs: 20 bytes for C2 instead of 24
+                rec[2] = (u32)((u64)ts[e] - (u64)tsbase);
+                for (int j = 0; j < rp.n; j++) {
+                    const u64 v = (u64)load_raw(cols, rp.src[j], e);
+                    rec[3 + 2 * j] = (u32)v;
+                    rec[4 + 2 * j] = (u32)(v >> 32);
+                }
+            } else {
+                u64* r8 = (u64*)(rec + w8);
+                r8[0] = (u64)ts[e];
+                for (int j = 0; j < rp.n; j++) r8[1 + j] = (u64)load_raw(cols, rp.src[j], e);
+            }
         }
         __syncthreads();
         if (threadIdx.x < G) {
@@ -258,9 +269,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(ColSet cols, const i64* _
 }
 
 void launch_shard_pack(hipStream_t s, ColSet cols, const i64* ts, const u32* code, KeyPlan wkp, RawPlan rp, int G,
-                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32) {
+                       i64 N, int nblk, const i64* offsets, unsigned char* out, int rec_words, int key32, int narrow,
+                       i64 tsbase) {
     hipLaunchKernelGGL(k_shard_pack, dim3(nblk), dim3(kBlock), 0, s, cols, ts, code, wkp, rp, G, N, nblk, offsets,
-                       (u32*)out, rec_words, key32);
+                       (u32*)out, rec_words, key32, narrow, tsbase);
 }
 
 // Received records -> the owner's SoA columns (8-byte raw form for every referenced column).
@@ -281,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(const u32* __restrict__
     if (src.key32) { key = (u64)(i64)(int)r[0]; pos = r[1]; w8 = 2; }
     else { key = *(const u64*)r; pos = r[2]; w8 = 4; }
     const u64* r8 = (const u64*)(r + w8);
-    ts[m] = (i64)r8[0];
+    ts[m] = src.narrow ? (i64)((u64)src.tsbase + (u64)r[2]) : (i64)r8[0];
     int g = 0;
     while (g + 1 < src.G && m >= src.start[g + 1]) g++;
     const i64 gi = src.gbase[g] + (i64)pos;
@@ -296,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_unpack(const u32* __restrict__
         int role = roles.role[c];
         if (role < 0) continue;
         u64 v;
-        if (role < 16) v = r8[1 + role];
+        if (role < 16) v = src.narrow ? ((u64)r[3 + 2 * role] | ((u64)r[4 + 2 * role] << 32)) : r8[1 + role];
         else if (kp.n == 1) v = key;
         else if (role == 16) v = (u64)(i64)(int)(u32)(key >> 32);
         else v = (u64)(i64)(int)(u32)key;

@@ -7,7 +7,7 @@ run of the GPU that owns its key (owner = mix64(key) % G), and aggregates what a
 The exchange itself is done here, over `torch.distributed` — RCCL over xGMI with the `nccl`
 backend on MI355X, or gloo on CPU tensors in the CPU tests:
 
-    summaries  all_gather_into_tensor   4 x int64 per rank
+    summaries  all_gather_into_tensor   7 x int64 per rank
     records    all_to_all_single        variable bytes per (source, owner), counts exchanged first
     bounds     all_gather               the window starts of every slice (few per push)
 
@@ -24,7 +24,7 @@ import numpy as np
 from . import abi
 from .runtime import Context, _check, default_context, lib
 
-SUMMARY_WORDS = 5
+SUMMARY_WORDS = 7
 BOUND_WORDS = 4
 
 
@@ -55,14 +55,15 @@ class ShardedQuery:
         self._b = _batch(n, ts_ptr, col_ptrs, send_size)
         s = abi.SliceSummary()
         _check(lib().sh_shard_summarize(self.h, C.byref(self._b), C.byref(s)))
-        return np.array([s.n, s.n_pass, s.max_tl, s.first_clock, s.first_key], dtype=np.int64)
+        return np.array([s.n, s.n_pass, s.max_tl, s.first_clock, s.first_key, s.ts_min, s.ts_max], dtype=np.int64)
 
     def pack(self, summaries: np.ndarray, send_ptr: int, send_cap: int) -> Tuple[np.ndarray, np.ndarray]:
-        """summaries: [world, 4] int64. Returns (send_bytes[world], bounds[k, 4] int64)."""
+        """summaries: [world, SUMMARY_WORDS] int64. Returns (send_bytes[world], bounds[k, 4] int64)."""
         summ = np.ascontiguousarray(summaries, dtype=np.int64).reshape(self.world, SUMMARY_WORDS)
         arr = (abi.SliceSummary * self.world)()
         for r in range(self.world):
-            arr[r].n, arr[r].n_pass, arr[r].max_tl, arr[r].first_clock, arr[r].first_key = (int(x) for x in summ[r])
+            (arr[r].n, arr[r].n_pass, arr[r].max_tl, arr[r].first_clock, arr[r].first_key, arr[r].ts_min,
+             arr[r].ts_max) = (int(x) for x in summ[r])
         sb = (C.c_int64 * self.world)()
         bp = C.POINTER(abi.Bound)()
         nb = C.c_int64()
@@ -291,6 +292,7 @@ class LocalShards:
             bounds.append(bd)
         all_bounds = np.concatenate(bounds) if bounds else np.zeros((0, BOUND_WORDS), np.int64)
         self.last_bounds = all_bounds
+        self.last_send_bytes = int(sum(int(np.sum(c)) for c in counts))  # bytes the push exchanged
         self.last_sends = (self.seq, send_size)
         self.seq += sum(int(ts.numel()) for ts, _ in slices)
         outs = []

@@ -79,6 +79,34 @@ def test_sharded_c2_matches_single_stream(world):
     assert_same(got, ref, label=f"sharded x{world}")
 
 
+def test_compact_records_and_wide_fallback():
+    """C2's records carry ts as a 32-bit offset from the push's minimum timestamp: 20 bytes per event
+    (key, slice position, ts offset, value) instead of 24; a push spanning 2^32 ms or more falls back
+    to the 64-bit ts. Both forms consume to the single-stream output."""
+    import torch
+    from siddhi_amd.shard import LocalShards
+    sp = spec(2_000)
+    ts, cols = synth.keyed_stream(0, 200_000, 0xB1, 2_000, 100)
+    ts = ts.copy()
+    ts[150_000:] += 5_000_000_000  # the second push spans more than 2^32 ms
+    pushes = [(ts[:100_000], [c[:100_000] for c in cols]), (ts[100_000:], [c[100_000:] for c in cols])]
+    adv = int(ts[-1]) + 5_000
+    got = run_sharded(sp, 3, pushes, 1, [[0.3, 0.6]], advance=adv)
+    ref = run_oracle(sp, pushes, 1, advance=adv)
+    assert_same(got, ref, label="compact / wide records")
+    dev = torch.device("cuda", 0)
+    ls = LocalShards(sp, 2)
+    per = []
+    for pts, pcols in pushes:
+        sl = [(torch.from_numpy(np.ascontiguousarray(x[a:b])).to(dev),
+               [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in pcols])
+              for a, b in ((0, 50_000), (50_000, len(pts))) for x in [pts]]
+        ls.push(sl, 1, dev)
+        per.append(ls.last_send_bytes / len(pts))
+    ls.close()
+    assert per == [20.0, 24.0], per
+
+
 def test_sharded_filter_send_chunks_start_time():
     sp = spec(5_000, filt=(">", "v", 150.0), start=137)
     pushes = stream_pushes(300_000, [100_000, 200_000], 0xC5, 5_000, 50)

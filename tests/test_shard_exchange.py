@@ -30,9 +30,9 @@ def _worker(rank, world, port, n_total, q):
         keys = rng.integers(0, 97, size=n_total)
         cut = [0, n_total // 3, n_total]  # uneven slices
         lo, hi = cut[rank], cut[rank + 1]
-        summ = np.array([hi - lo, rank, 100 + rank, -rank, 7], np.int64)
+        summ = np.array([hi - lo, rank, 100 + rank, -rank, 7, 5 - rank, 9 + rank], np.int64)
         allsumm = ex.all_gather_summaries(summ)
-        assert allsumm.shape == (world, 5) and list(allsumm[:, 2]) == [100, 101]
+        assert allsumm.shape == (world, 7) and list(allsumm[:, 2]) == [100, 101] and list(allsumm[:, 6]) == [9, 10]
         # records: (gidx, key) int64 pairs, grouped by owner = key % world in stream order
         gidx = np.arange(lo, hi)
         k = keys[lo:hi]
