@@ -224,6 +224,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     const int64_t N = b->n, ss = b->send_size, L = q->d.window_param;
     const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
     const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
+    const bool sc = q->d.stream_current != 0;  // lengthBatch(L, true), current output (k_pg_sc_*)
     if (N >= (int64_t)0x3FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 1G events");
     HIPCHK(hipEventRecord(q->ev_push0, st));
     const int64_t cap = std::max<int64_t>(N, 1);
@@ -333,6 +334,9 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                                  s->pg_err.as<int>());
             launch_pg_ext_state(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
                                 s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, s->nslots);
+        } else if (sc) {
+            launch_pg_sc_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->p_slot.as<u32>(), C, n, L, gbits,
+                                s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(), s->pg_keep.as<unsigned char>());
         } else {
             launch_pg_assign(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->p_slot.as<u32>(), s->pg_prevcnt.as<u32>(), C, n, L,
                              q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
@@ -347,8 +351,8 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                 return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch: a partition's first event is before its start time "
                                                    "(not on the GPU)");
         }
-        int64_t n_e = 0;
-        RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
+        int64_t n_e = n;  // (stream.current: one entry per event)
+        if (!sc) RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
         if (n_e > 0) {
             tb = 0;
             const int64_t ne_sort = q->d.expired_on ? ne_cap : n;  // (current only: one entry per event)
@@ -367,7 +371,9 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             launch_slx_compact(st, 1, s->pg_head.as<unsigned char>(), nullptr, nullptr, nullptr, n_e,
                                s->x_blk.as<int64_t>(), nullptr, nullptr, s->pg_seg.as<int64_t>());
             HIPCHK(hipGetLastError());
-            RCHK(read_count(q, s->x_blk.as<int64_t>() + (n_e + kTile - 1) / kTile, &n_rows));
+            int64_t n_seg = 0;
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + (n_e + kTile - 1) / kTile, &n_seg));
+            n_rows = sc ? M : n_seg;  // (stream.current: a row per event of the push, else one per segment)
             const int64_t rc = std::max<int64_t>(n_rows, 1);
             RCHK(s->xr_ts.reserve(rc * 8, false));
             RCHK(s->xr_rep.reserve(rc * 8, false));
@@ -386,19 +392,25 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                          s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
                          s->xr_nulls.as<unsigned char>(), rc};
             HIPCHK(hipEventRecord(q->ev_agg0, st));
-            launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
-                           s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
-                           ext ? s->pg_cts.as<int64_t>() : nullptr);
-            HIPCHK(hipEventRecord(q->ev_agg1, st));
-            // ---- rows in (chunk, first entry) order
-            const unsigned rbits = (unsigned)(32 + cbits);
-            tb = 0;
-            if (sort_u64_iota_bits(nullptr, &tb, s->pg_rkey.as<u64>(), nullptr, nullptr, n_rows, rbits, st))
-                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
-            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
-            if (sort_u64_iota_bits(s->sort_tmp.p, &tb, s->pg_rkey.as<u64>(), s->pg_rkey2.as<u64>(), s->pg_order.as<u32>(),
-                                   n_rows, rbits, st))
-                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            if (sc) {
+                launch_pg_sc_fold(st, s->pg_seg.as<int64_t>(), n_seg, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
+                                  s->ranks.as<u32>(), C, q->ap, gbits, n_old, rows, s->pg_rpart.as<u32>());
+                HIPCHK(hipEventRecord(q->ev_agg1, st));
+            } else {
+                launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
+                               s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
+                               ext ? s->pg_cts.as<int64_t>() : nullptr);
+                HIPCHK(hipEventRecord(q->ev_agg1, st));
+                // ---- rows in (chunk, first entry) order
+                const unsigned rbits = (unsigned)(32 + cbits);
+                tb = 0;
+                if (sort_u64_iota_bits(nullptr, &tb, s->pg_rkey.as<u64>(), nullptr, nullptr, n_rows, rbits, st))
+                    return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+                RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+                if (sort_u64_iota_bits(s->sort_tmp.p, &tb, s->pg_rkey.as<u64>(), s->pg_rkey2.as<u64>(),
+                                       s->pg_order.as<u32>(), n_rows, rbits, st))
+                    return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            }
             RCHK(s->out_ts.reserve(rc * 8, false));
             RCHK(s->out_keys.reserve((size_t)std::max(1, q->gkp.n) * rc * 8, false));
             RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * rc * 8, false));
@@ -407,7 +419,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             RCHK(s->out_clock.reserve(rc * 8, false));
             RCHK(s->out_expired.reserve(rc, false));
             RCHK(s->out_rep.reserve(rc * 8, false));
-            launch_pg_emit(st, s->pg_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, rc,
+            launch_pg_emit(st, sc ? nullptr : s->pg_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, rc,
                            s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                            s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
                            s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(),

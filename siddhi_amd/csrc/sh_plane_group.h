@@ -49,6 +49,11 @@ void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const
                       PgRecs C, i64 n, i64 L, int cur_on, int exp_on, int gbits, u64 none, u64* ekey, u32* eval,
                       unsigned char* keep, unsigned long long* n_entries);
 void launch_pg_heads(hipStream_t s, const u64* key, i64 n, unsigned char* head);
+// lengthBatch(L, true) grouped by other columns: entries by (batch, group), a row per event of the push
+void launch_pg_sc_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* p_sorted, PgRecs C, i64 n,
+                         i64 L, int gbits, u64* ekey, u32* eval, unsigned char* keep);
+void launch_pg_sc_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
+                       const u32* ranks, PgRecs C, AggPlan ap, int gbits, i64 n_old, SlxRows rows, u32* row_part);
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
                     const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,
                     const i64* chunk_ts = nullptr);

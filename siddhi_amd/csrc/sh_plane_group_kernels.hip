@@ -321,6 +321,103 @@ void launch_pg_assign(hipStream_t s, const u32* key_off, const u32* ranks, const
                        p_sorted, prev_cnt, C, n, L, cur_on, exp_on, gbits, none, ekey, eval, keep, n_entries);
 }
 
+// ---- lengthBatch(L, true) grouped by other columns (stream.current.event, current output): every event
+// is a chunk of its own (LengthBatchWindowProcessor.processStreamCurrentEvents :245-274: the event passes
+// through, a RESET before the partition's (L + 1)-th event of the batch clears the group states), so its
+// row is its group's fold over the partition's batch up to it. One entry per sorted position, keyed
+// (the batch's first combined index, group slot); the carried events of the open batches fold without
+// emitting (their rows went out with their own push). keep: the events of a run's last batch unless it
+// is complete (the next event of the partition resets).
+__global__ __launch_bounds__(kBlock) void k_pg_sc_assign(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                        const u32* __restrict__ p_sorted, PgRecs C, i64 n, i64 L,
+                                                        int gbits, u64* ekey, u32* eval, unsigned char* keep) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const u32 c = ranks[i];
+    const u32 p = p_sorted[i];
+    const i64 lo = key_off[p], run = (i64)key_off[p + 1] - lo;
+    const i64 j = i - lo, b = j / L;
+    ekey[i] = ((u64)ranks[lo + b * L] << gbits) | (u64)C.gs[c];
+    eval[i] = (u32)i;
+    keep[c] = (b == (run - 1) / L && run % L != 0) ? 2 : 0;
+}
+
+void launch_pg_sc_assign(hipStream_t s, const u32* key_off, const u32* ranks, const u32* p_sorted, PgRecs C, i64 n,
+                         i64 L, int gbits, u64* ekey, u32* eval, unsigned char* keep) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_pg_sc_assign, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
+                       p_sorted, C, n, L, gbits, ekey, eval, keep);
+}
+
+// one thread per (batch, group) segment folds its events in stream order; every event of this push
+// (combined index >= n_old) writes its row at its own place among the push's events (stream order)
+template <int NA>
+__global__ __launch_bounds__(64) void k_pg_sc_fold(const i64* __restrict__ seg_start, i64 n_seg, i64 n_e,
+                                                  const u64* __restrict__ ekey, const u32* __restrict__ eval,
+                                                  const u32* __restrict__ ranks, PgRecs C, AggPlan ap, int gbits,
+                                                  i64 n_old, SlxRows rows, u32* row_part) {
+    const i64 sidx = (i64)blockIdx.x * 64 + threadIdx.x;
+    if (sidx >= n_seg) return;
+    const i64 lo = seg_start[sidx], hi = sidx + 1 < n_seg ? seg_start[sidx + 1] : n_e;
+    const u32 g = (u32)(ekey[lo] & ((1ull << gbits) - 1));
+    u64 f[NA], mm[NA];
+    unsigned char mmh[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) { f[a] = 0; mm[a] = 0; mmh[a] = 0; }
+    i64 cnt = 0;
+    for (i64 t = lo; t < hi; t++) {
+        const u32 c = ranks[eval[t]];
+        cnt++;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            if (kind == AK_COUNT) continue;
+            const u64 x = C.vals[(size_t)ap.vcol[a] * C.cap + c];
+            if (kind == AK_SUM_L) f[a] = (u64)((i64)f[a] + (i64)x);
+            else if (kind == AK_SUM_D || kind == AK_AVG)
+                f[a] = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) + g_num(ap, a, x));
+            else {
+                const bool take = !mmh[a] || g_worse(kind, mm[a], x);
+                mm[a] = take ? x : mm[a];
+                mmh[a] = 1;
+            }
+        }
+        if ((i64)c < n_old) continue;  // carried: its row went out with its own push
+        const i64 r = (i64)c - n_old;
+        rows.ts[r] = C.ts[c];
+        rows.rep[r] = C.seq[c];
+        rows.slot[r] = g;
+        rows.ch[r] = C.seq[c];
+        rows.clk[r] = C.clk[c];
+        rows.exp[r] = 0;
+        row_part[r] = C.ps[c];
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            u64 rv = 0;
+            unsigned char rn = 0;
+            if (kind == AK_COUNT) rv = (u64)cnt;
+            else if (kind == AK_SUM_L || kind == AK_SUM_D) rv = f[a];
+            else if (kind == AK_AVG) rv = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) / (double)cnt);
+            else { rn = mmh[a] ? 0 : 1; rv = mmh[a] ? mm[a] : 0; }
+            rows.vals[(size_t)a * rows.cap + r] = rv;
+            rows.nulls[(size_t)a * rows.cap + r] = rn;
+        }
+    }
+}
+
+void launch_pg_sc_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
+                       const u32* ranks, PgRecs C, AggPlan ap, int gbits, i64 n_old, SlxRows rows, u32* row_part) {
+    if (n_seg <= 0) return;
+    const unsigned grid = (unsigned)((n_seg + 63) / 64);
+    if (ap.n <= 4) hipLaunchKernelGGL(k_pg_sc_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval,
+                                      ranks, C, ap, gbits, n_old, rows, row_part);
+    else hipLaunchKernelGGL(k_pg_sc_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks, C,
+                            ap, gbits, n_old, rows, row_part);
+}
+
 // segment heads of the sorted entries
 __global__ __launch_bounds__(kBlock) void k_pg_heads(const u64* __restrict__ key, i64 n, unsigned char* head) {
     const i64 j = (i64)blockIdx.x * kBlock + threadIdx.x;
@@ -422,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ orde
                                                    const u32* __restrict__ row_part, u32* out_part) {
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (r >= n) return;
-    const u32 j = order[r];
+    const u32 j = order ? order[r] : (u32)r;  // (null: the rows are already in output order)
     out_ts[r] = rows.ts[j];
     if (nk > 0) unpack_key(kp, slot_key(kt, rows.slot[j]), out_keys + r, out_cap);
     for (int a = 0; a < n_aggs; a++) {

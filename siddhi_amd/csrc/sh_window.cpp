@@ -232,8 +232,9 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // ... and partitioned lengthBatch grouped by other columns: (partition, group) rows by sorting (lane 3)
     // (and partitioned externalTimeBatch, any group-by: the same sorted chunks with batches by attribute time)
     const bool plane_ext = d->partition_col >= 0 && d->window == SH_WIN_EXT_TIME_BATCH && d->n_aggs >= 1;
+    // (lengthBatch(L, true) grouped by other columns: current output, a row per event — k_pg_sc_*)
     const bool plane_group = (d->partition_col >= 0 && d->window == SH_WIN_LENGTH_BATCH && !by_partition &&
-                              !d->stream_current && d->n_aggs >= 1) || plane_ext;
+                              (!d->stream_current || !d->expired_on) && d->n_aggs >= 1) || plane_ext;
     // ... and time / externalTime grouped by other columns: the time lanes' operations, replayed per
     // (partition, group) state (count / sum / avg)
     const bool plane_time_group = d->partition_col >= 0 && (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
@@ -256,7 +257,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH))))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "stream.current.event runs on aggregating lengthBatch / timeBatch windows (partitioned: "
-                       "lengthBatch with no group-by or grouped by the partition key)");
+                       "lengthBatch; grouped by other columns with current output)");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "partitioned GPU queries support timeBatch, lengthBatch, externalTimeBatch, and time with no group-by or "

@@ -163,6 +163,28 @@ def gstream(n, parts, groups, seed, runs=False, zipf=False):
     return ts, [p, g, v, x, h, ts2]
 
 
+@pytest.mark.parametrize("L,group_by,parts,runs,zipf", [(1, ["g"], 50, False, False), (4, ["g"], 30, True, False),
+                                                        (37, ["g", "h"], 12, False, False),
+                                                        (5, ["h", "p"], 80, True, False),
+                                                        (3, ["g"], 100_000, False, True)])
+def test_partitioned_lengthbatch_stream_current_group_by_other(rt, L, group_by, parts, runs, zipf):
+    """lengthBatch(L, true) grouped by other columns: every event its own chunk, its row the group's fold
+    over the partition's batch so far (the partition's (L + 1)-th event of a batch resets every group);
+    open batches carried across pushes fold without emitting again"""
+    ts, cols = gstream(200_000 if zipf else 30_000, parts, 7, 67, runs=runs, zipf=zipf)
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", L, group_by=group_by, aggs=AGGS, partition="p",
+                         filter=(">", "v", -30.0), stream_current=True, key_capacity=max(256, parts))
+    ref = both(rt, spec, split_batches(GSCHEMA, ts, cols, [1, 9_999, 17_000], 3), f"plg sc {L} {group_by}")
+    assert ref["ts"].size > 0
+
+
+def test_partitioned_stream_current_group_by_other_expired_refused(rt):
+    spec = abi.QuerySpec(GSCHEMA, "lengthBatch", 3, group_by=["g"], aggs=AGGS, partition="p", output="all",
+                         stream_current=True, key_capacity=64)
+    with pytest.raises(rt.SiddhiError, match="not on the GPU|stream.current|partitioned"):
+        rt.GpuQuery(spec)
+
+
 @pytest.mark.parametrize("output", ["current", "all", "expired"])
 @pytest.mark.parametrize("L,group_by,parts,runs", [(1, ["g"], 50, False), (4, ["g"], 30, True),
                                                    (37, ["g", "h"], 12, False), (5, ["h", "p"], 80, True),
