@@ -169,7 +169,24 @@ int empty_out(sh_query* q, const sh_out** out) {
 }
 
 static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
-                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out);
+                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out,
+                          bool presorted = false);
+
+// the push's records sorted stably by key slot (p_slot, ranks) and room for the key offsets
+static int sort_keyed(sh_query* q, const u32* slot, int64_t M) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    size_t tb = 0;
+    if (sort_slot_ranks(nullptr, &tb, slot, nullptr, nullptr, M, s->nslots, st))
+        return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+    RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+    RCHK(s->p_slot.reserve(M * 4, false));
+    RCHK(s->ranks.reserve(M * 4, false));
+    RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+    if (sort_slot_ranks(s->sort_tmp.p, &tb, slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
+        return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+    return SH_OK;
+}
 static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out);
 
 // Hashed keys of a time() window get a fresh table once more than half full: keys whose every window
@@ -264,7 +281,10 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     RCHK(s->rec_ts.reserve(N * 8, false));
     RCHK(s->rec_vals.reserve((size_t)V * N * 8, false));
     RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
-    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    // keyed replay over lane-strided records (every event passes, M = N): the records are sorted by key
+    // slot right away and the key offsets and ring need come from the sorted slots (no per-slot counts)
+    const bool pre = keyed_aos(q) && sl_records_seq_applies(q->fp, wp, q->ap);
+    if (!pre) HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), N};
     if (keyed_aos(q)) {
@@ -274,17 +294,24 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     const bool ext = q->d.window == SH_WIN_EXT_TIME;
     if (ext) RCHK(s->rec_sclk.reserve(N * 8, false));
     launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk,
-                      ext ? s->rec_sclk.as<int64_t>() : nullptr);
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
+                      pre ? nullptr : s->slot_cnt.as<u32>(), nblk, ext ? s->rec_sclk.as<int64_t>() : nullptr);
     HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
-    launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
-                   (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+    int64_t* need_dev = (int64_t*)((char*)s->info.p + offsetof(SlInfo, need));
+    if (pre) {
+        HIPCHK(hipEventRecord(q->ev_agg0, st));  // (the sort is part of the replay's time)
+        RCHK(sort_keyed(q, rec.slot, N));
+        launch_keyoff_sorted(st, s->p_slot.as<u32>(), N, s->nslots, s->key_off.as<u32>(), s->rlen.as<int64_t>(), need_dev);
+    } else {
+        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     RCHK(q->kt.check(st));
     SlInfo info = *s->h_info;
-    RCHK(sliding_finish(q, info.total_pass, N, info.need, b->send_size, s->send_base, q->seq, false, host_out, out));
+    RCHK(sliding_finish(q, info.total_pass, N, info.need, b->send_size, s->send_base, q->seq, false, host_out, out,
+                        pre));
     q->seq += N;
     // window state moves on
     q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
@@ -344,7 +371,8 @@ int sliding_push_given(sh_query* q, int64_t M, const int64_t* ts, const void* co
 // replay (launch_sliding_own), rows in rank order, one flush per send. want_order: also the global
 // stream index of every row's first event (raw_base + raw), into q->order_host / q->out_order.
 static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need, int64_t send_size,
-                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out) {
+                          int64_t send_base, int64_t raw_base, bool want_order, bool host_out, const sh_out** out,
+                          bool presorted) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
     int V = std::max(1, q->ap.n_vcols);
@@ -378,22 +406,17 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
         // the common shape (count / sum / avg / min / max of one double column, time window): records
         // sorted stably by key, one lane per key (k_sl_key); other shapes: key-partition replay
         if (keyed) {
-            HIPCHK(hipEventRecord(q->ev_agg0, st));  // the sort is part of the replay's time
-            size_t tb = 0;
-            if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
-                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
-            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
-            RCHK(s->p_slot.reserve(M * 4, false));
-            RCHK(s->ranks.reserve(M * 4, false));
-            if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
-                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
-            RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+            if (!presorted) {  // (presorted: sorted and key offsets made before the push's sync, sliding_push)
+                HIPCHK(hipEventRecord(q->ev_agg0, st));  // the sort is part of the replay's time
+                RCHK(sort_keyed(q, rec.slot, M));
+            }
             RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
             RCHK(s->p_pm.reserve(M * 8, false));
             RCHK(s->p_vals.reserve(M * 8, false));
             RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na, all_rows) * 8, false));
             if (q->tune.sl_kgather) RCHK(s->rec_aosk.reserve((size_t)M * kSlAosWords * 8, false));
-            launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
+            launch_sliding_keyed(st, presorted ? nullptr : s->slot_cnt.as<u32>(), s->key_off.as<u32>(),
+                                 s->tmp.as<int64_t>(), s->ranks.as<u32>(),
                                  rec, s->p_pm.as<int64_t>(), s->p_vals.as<u64>(), state_of(s), q->ap,
                                  q->d.window_param, send_size, send_base, s->rows_k.as<u64>(),
                                  all_rows ? nullptr : s->flags.as<unsigned char>(),
@@ -628,6 +651,7 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     int nblk = 0;
     int64_t M = 0;
     SlInfo info{};
+    bool presorted = false;
     const int64_t cap = std::max<int64_t>(N, 1);
     RCHK(s->rec_raw.reserve(cap * 4, false));
     RCHK(s->rec_slot.reserve(cap * 4, false));
@@ -655,12 +679,21 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
         launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                          s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
         if (ext) RCHK(s->rec_sclk.reserve(cap * 8, false));
+        // (lane-strided records, every event passes: sorted by key slot right away, offsets and ring need
+        // from the sorted slots instead of per-slot counts)
+        presorted = q->ap.n > 0 && sl_records_seq_applies(q->fp, wp, q->ap);
         launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk,
-                          ext ? s->rec_sclk.as<int64_t>() : nullptr);
+                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
+                          presorted ? nullptr : s->slot_cnt.as<u32>(), nblk, ext ? s->rec_sclk.as<int64_t>() : nullptr);
         HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
-        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
-                       (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+        int64_t* need_dev = (int64_t*)((char*)s->info.p + offsetof(SlInfo, need));
+        if (presorted) {
+            RCHK(sort_keyed(q, rec.slot, N));
+            launch_keyoff_sorted(st, s->p_slot.as<u32>(), N, s->nslots, s->key_off.as<u32>(), s->rlen.as<int64_t>(),
+                                 need_dev);
+        } else {
+            launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -771,19 +804,14 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
     launch_slx_aop(st, rec.clock, M, s->upm.as<int64_t>(), n_u, W0, T, s->x_aop.as<u64>(),
                    wave ? s->x_xa.as<u64>() : nullptr, rec, rsclk, s->x_bnd.as<int64_t>() + 3 * (nu1 / kBlock + 2));
     // the push's records sorted stably by key slot: each key's adds in arrival order
-    RCHK(s->ranks.reserve(cap * 4, false));
-    RCHK(s->p_slot.reserve(cap * 4, false));
-    if (M > 0 && q->ap.n > 0) {
-        size_t tb = 0;
-        if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
-            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
-        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
-        if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
-            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+    if (!presorted) {
+        RCHK(s->ranks.reserve(cap * 4, false));
+        RCHK(s->p_slot.reserve(cap * 4, false));
+        if (M > 0 && q->ap.n > 0) RCHK(sort_keyed(q, rec.slot, M));
+        RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+        RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+        launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
     }
-    RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
-    RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
-    launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
     HIPCHK(hipGetLastError());
     int64_t R = 0;
     RCHK(read_count(q, (const int64_t*)s->x_nexp.p, &R));

@@ -166,7 +166,11 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
     // the wave's 64 records staged in LDS, then stored as contiguous 16-byte pieces (each store
     // instruction covers 1 KB of whole lines instead of one piece of 64 records 48 bytes apart)
     __shared__ ulonglong2 stg[kBlock * 3];
-    for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
+    // slot_cnt null: the caller takes the per-slot counts from the sorted slots instead (k_keyoff_sorted:
+    // r05, the tile's LDS table and its global atomics were 1.2 of the kernel's 1.9 ms at C3)
+    const bool count = slot_cnt != nullptr;
+    if (count)
+        for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
     const i64 tile0 = (i64)blockIdx.x * kTile;
     const i64 r0 = blk_pass_pre[blockIdx.x];
     i64 carry_cm = blk_tl_pre[blockIdx.x];
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
                 if (send_clock) send_clock[r] = sclk;
                 rec.raw[r] = (u32)e;
                 rec.slot[r] = pos;
-                slot_tab_add(tk, tc, pos);
+                if (count) slot_tab_add(tk, tc, pos);
             }
             stg[threadIdx.x * 3 + 0] = make_ulonglong2((u64)sclk, (u64)pmx);
             stg[threadIdx.x * 3 + 1] = make_ulonglong2((u64)t, v);
@@ -216,20 +220,25 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
                 rec.ts[r] = t;
                 for (int j = 0; j < ap.n_vcols; j++) rec.vals[(size_t)j * rec.cap + r] = (u64)load_raw(cols, ap.vcol_src[j], e);
             }
-            slot_tab_add(tk, tc, pos);
+            if (count) slot_tab_add(tk, tc, pos);
         }
         carry_pm = max(carry_pm, tot);
         carry_cm = max(carry_cm, tot);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kSlotTab; i += kBlock)
-        if (tc[i]) atomicAdd(&slot_cnt[tk[i]], tc[i]);
+    if (count)
+        for (int i = threadIdx.x; i < kSlotTab; i += kBlock)
+            if (tc[i]) atomicAdd(&slot_cnt[tk[i]], tc[i]);
+}
+
+bool sl_records_seq_applies(FilterProg f, WinParams wp, AggPlan ap) {
+    return filter_kind(f) == 0 && wp.send_size == 1 && wp.kind == SH_WIN_TIME && ap.n_vcols >= 1 && wp.rec_seq;
 }
 
 void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp,
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
                        i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock) {
-    if (filter_kind(f) == 0 && wp.send_size == 1 && wp.kind == SH_WIN_TIME && ap.n_vcols >= 1 && wp.rec_seq) {
+    if (sl_records_seq_applies(f, wp, ap)) {
         hipLaunchKernelGGL(k_sl_records_seq, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap, blk_pass_pre,
                            blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
         return;
@@ -298,6 +307,40 @@ __global__ __launch_bounds__(kBlock) void k_sl_need(const u32* slot_cnt, const i
 
 void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* out) {
     hipLaunchKernelGGL(k_sl_need, dim3(256), dim3(kBlock), 0, s, slot_cnt, rlen, n, out);
+}
+
+// key_off[k] = the first sorted position whose slot is >= k (k = 0..nslots) from the slot-sorted
+// records: each run start writes the offsets of the slots from the previous run's slot up to its own
+// (the last position also those past its slot)
+__global__ __launch_bounds__(kBlock) void k_keyoff_sorted(const u32* __restrict__ ps, i64 M, i64 nslots,
+                                                         u32* __restrict__ key_off) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const i64 cur = ps[i];
+    const i64 prev = i ? (i64)ps[i - 1] : -1;
+    if (cur != prev)
+        for (i64 k = prev + 1; k <= cur; k++) key_off[k] = (u32)i;
+    if (i == M - 1)
+        for (i64 k = cur + 1; k <= nslots; k++) key_off[k] = (u32)M;
+}
+
+// max over the slots of the push of (ring length + the slot's records): the ring capacity it needs
+__global__ __launch_bounds__(kBlock) void k_sl_need_off(const u32* __restrict__ key_off, const i64* rlen, i64 n,
+                                                       i64* out) {
+    i64 m = 0;
+    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
+        const i64 c = (i64)key_off[i + 1] - (i64)key_off[i];
+        if (c) m = max(m, rlen[i] + c);
+    }
+    i64 t = block_reduce(m, MaxOp(), 0);
+    if (threadIdx.x == 0) atomicMax((unsigned long long*)out, (unsigned long long)t);
+}
+
+void launch_keyoff_sorted(hipStream_t s, const u32* ps, i64 M, i64 nslots, u32* key_off, const i64* rlen, i64* need) {
+    if (M > 0)
+        hipLaunchKernelGGL(k_keyoff_sorted, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ps, M, nslots,
+                           key_off);
+    hipLaunchKernelGGL(k_sl_need_off, dim3(256), dim3(kBlock), 0, s, key_off, rlen, nslots, need);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2133,8 +2176,10 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     }
     const i64 n = S.nslots;
     const u32 ss = send_size > 0 ? (u32)send_size : 0u;
-    hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
-    launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
+    if (slot_cnt) {  // (null: key_off already from the sorted slots, launch_keyoff_sorted)
+        hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
+        launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
+    }
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
     const int RW = sliding_keyed_row_words(ap.n, flags == nullptr);
     if (aosk && M > 0)
