@@ -314,14 +314,27 @@ void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, 
 // (the last position also those past its slot)
 __global__ __launch_bounds__(kBlock) void k_keyoff_sorted(const u32* __restrict__ ps, i64 M, i64 nslots,
                                                          u32* __restrict__ key_off) {
-    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M) return;
-    const i64 cur = ps[i];
-    const i64 prev = i ? (i64)ps[i - 1] : -1;
-    if (cur != prev)
-        for (i64 k = prev + 1; k <= cur; k++) key_off[k] = (u32)i;
-    if (i == M - 1)
-        for (i64 k = cur + 1; k <= nslots; k++) key_off[k] = (u32)M;
+    // (four positions per thread: one 16-byte load and the previous word)
+    const i64 i0 = ((i64)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (i0 >= M) return;
+    u32 v[4];
+    if (i0 + 4 <= M) {
+        const uint4 q = *(const uint4*)(ps + i0);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+        for (int t = 0; t < 4; t++) v[t] = i0 + t < M ? ps[i0 + t] : 0u;
+    }
+    i64 prev = i0 ? (i64)ps[i0 - 1] : -1;
+    for (int t = 0; t < 4; t++) {
+        const i64 i = i0 + t;
+        if (i >= M) break;
+        const i64 cur = v[t];
+        if (cur != prev)
+            for (i64 k = prev + 1; k <= cur; k++) key_off[k] = (u32)i;
+        if (i == M - 1)
+            for (i64 k = cur + 1; k <= nslots; k++) key_off[k] = (u32)M;
+        prev = cur;
+    }
 }
 
 // max over the slots of the push of (ring length + the slot's records): the ring capacity it needs
@@ -338,8 +351,8 @@ __global__ __launch_bounds__(kBlock) void k_sl_need_off(const u32* __restrict__ 
 
 void launch_keyoff_sorted(hipStream_t s, const u32* ps, i64 M, i64 nslots, u32* key_off, const i64* rlen, i64* need) {
     if (M > 0)
-        hipLaunchKernelGGL(k_keyoff_sorted, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ps, M, nslots,
-                           key_off);
+        hipLaunchKernelGGL(k_keyoff_sorted, dim3((unsigned)((M + 4 * kBlock - 1) / (4 * kBlock))), dim3(kBlock), 0, s, ps,
+                           M, nslots, key_off);
     hipLaunchKernelGGL(k_sl_need_off, dim3(256), dim3(kBlock), 0, s, key_off, rlen, nslots, need);
 }
 
@@ -1822,6 +1835,7 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                 // the quirk check: an expiring head meeting a bit-equal value of another event among the
                 // deque entries or the chunk's records
                 bool dirty = false;
+#ifndef SH_WK_NODIRTY
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
                     const int d = lane + 64 * t;
@@ -1840,6 +1854,7 @@ __global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off,
                         }
                     for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
                 }
+#endif
                 pc = !__any(dirty);
             }
             if (pc) {
