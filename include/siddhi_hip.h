@@ -121,7 +121,9 @@ typedef struct {
     int32_t current_on;     /* insert [current|all] events  (QueryParser.java:221-223)   */
     sh_agg_spec aggs[SH_MAX_AGGS];
     int32_t expired_on;     /* insert [expired|all] events                               */
-    int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`     */
+    int32_t partition_col;  /* -1: not partitioned; else `partition with (col of S)`: int / long /
+                               string id / float / double (not float / double for time windows
+                               with expired output)                                        */
     int64_t key_capacity;   /* upper bound on distinct group keys (device table sizing). Batch and
                              * time() windows rebuild their hashed table from the live keys when it
                              * is half full (a time() key is live while an event of it can still be

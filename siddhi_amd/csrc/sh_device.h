@@ -166,6 +166,15 @@ __device__ __forceinline__ bool eval_filter(const FilterProg& f, const ColSet& c
             case SH_OP_AND: sp--; sv[sp - 1] = (sv[sp - 1] && sv[sp]) ? 1 : 0; st[sp - 1] = SH_T_BOOL; break;
             case SH_OP_OR: sp--; sv[sp - 1] = (sv[sp - 1] || sv[sp]) ? 1 : 0; st[sp - 1] = SH_T_BOOL; break;
             case SH_OP_NOT: sv[sp - 1] = sv[sp - 1] ? 0 : 1; st[sp - 1] = SH_T_BOOL; break;
+            case kOpKeyEq: {
+                sp--;
+                auto canon = [](int t, i64 v) -> i64 {
+                    return (is_fp(t) && __longlong_as_double(v) != __longlong_as_double(v)) ? 0x7FF8000000000000ll : v;
+                };
+                sv[sp - 1] = canon(st[sp - 1], sv[sp - 1]) == canon(st[sp], sv[sp]) ? 1 : 0;
+                st[sp - 1] = SH_T_BOOL;
+                break;
+            }
             default: {
                 sp--;
                 bool r = java_cmp(o.op, st[sp - 1], sv[sp - 1], st[sp], sv[sp]);

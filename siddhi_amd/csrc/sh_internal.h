@@ -39,6 +39,10 @@ struct FilterProg {
 
 // Which kernel instance evaluates a filter program (eval_filter's FK): 0 none, 1 `col <cmp> const`
 // or two of those joined by AND / OR (evaluated in registers), 2 anything else (the stack machine).
+// internal filter op (never in a caller's program): the two operands' partition-key forms equal —
+// String.valueOf equality, i.e. the bits with NaN canonical for float / double (partition_filter, R12)
+constexpr int kOpKeyEq = 32;
+
 inline int filter_kind(const FilterProg& f) {
     auto leaf = [&](int i) {
         return f.ops[i].op == SH_OP_COL && f.ops[i + 1].op == SH_OP_CONST && f.ops[i + 2].op >= SH_OP_GT &&

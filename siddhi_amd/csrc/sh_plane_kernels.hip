@@ -214,7 +214,12 @@ __global__ __launch_bounds__(kBlock) void k_pl_run_start(ColSet cols, int pcol, 
     const i64 e = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (e >= N) return;
     const i64 sl = send_size > 0 ? send_size : N;
-    start[e] = (e % sl == 0) || load_raw(cols, pcol, e) != load_raw(cols, pcol, e - 1);
+    // (the partitions' String.valueOf equality: float / double keys by their bits, every NaN one key)
+    auto key = [&](i64 i) -> i64 {
+        const i64 v = load_raw(cols, pcol, i);
+        return (is_fp(cols.type[pcol]) && __longlong_as_double(v) != __longlong_as_double(v)) ? 0x7FF8000000000000ll : v;
+    };
+    start[e] = (e % sl == 0) || key(e) != key(e - 1);
 }
 
 // run number of every event: inclusive count of run starts - 1 (tile prefix from launch_scan_sum)

@@ -262,9 +262,18 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "partitioned GPU queries support timeBatch, lengthBatch, externalTimeBatch, and time with no group-by or "
                        "grouped by the partition key (lengthBatch(L, true) likewise)");
-    if (d->partition_col >= 0 && (d->partition_col >= d->n_cols || !(d->col_types[d->partition_col] == SH_T_INT ||
-                                  d->col_types[d->partition_col] == SH_T_LONG || d->col_types[d->partition_col] == SH_T_STRID)))
-        return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/string column");
+    if (d->partition_col >= 0) {
+        const int pt = d->partition_col < d->n_cols ? d->col_types[d->partition_col] : -1;
+        const bool fp_key = pt == SH_T_FLOAT || pt == SH_T_DOUBLE;
+        if (!(pt == SH_T_INT || pt == SH_T_LONG || pt == SH_T_STRID || fp_key))
+            return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/float/double/string column");
+        // float / double keys: partitions are String.valueOf(value) (bits, NaN canonical); the Scheduler's
+        // tie order among partitions due together hashes that text (Double.toString), which is not
+        // restated — it decides output only for time windows with expired output
+        if (fp_key && d->window == SH_WIN_TIME && d->expired_on)
+            return sh_fail(SH_ERR_UNSUPPORTED, "float / double partition keys of time windows with expired output "
+                                               "(the Scheduler's tie order hashes Double.toString)");
+    }
 
     sh_query* q = new sh_query();
     q->ctx = ctx;
@@ -690,8 +699,16 @@ int partition_filter(const FilterProg& base, int pcol, int ptype, int64_t key, F
     FilterProg fp = base;
     if (fp.n + 4 > kMaxFilterOps) return sh_fail(SH_ERR_UNSUPPORTED, "filter too long for a partitioned query");
     fp.ops[fp.n++] = FilterOpD{SH_OP_COL, 0, pcol, 0, 0, 0.0};
-    fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, ptype, 0, 0, key, 0.0};
-    fp.ops[fp.n++] = FilterOpD{SH_OP_EQ, 0, 0, 0, 0, 0.0};
+    if (ptype == SH_T_FLOAT || ptype == SH_T_DOUBLE) {
+        // String.valueOf equality (ValuePartitionExecutor :34-40): bits, every NaN one key, 0.0 != -0.0
+        double dv;
+        std::memcpy(&dv, &key, 8);
+        fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, SH_T_DOUBLE, 0, 0, 0, dv};
+        fp.ops[fp.n++] = FilterOpD{kOpKeyEq, 0, 0, 0, 0, 0.0};
+    } else {
+        fp.ops[fp.n++] = FilterOpD{SH_OP_CONST, ptype, 0, 0, key, 0.0};
+        fp.ops[fp.n++] = FilterOpD{SH_OP_EQ, 0, 0, 0, 0, 0.0};
+    }
     if (base.n > 0) fp.ops[fp.n++] = FilterOpD{SH_OP_AND, 0, 0, 0, 0, 0.0};
     *out = fp;
     return SH_OK;

@@ -314,3 +314,46 @@ def test_partitioned_time_group_by_other_pair_churn(rt):
     o.close()
     assert_same(_abi.concat_arrays([part1, part2]), want, label="pair churn")
     assert want["expired"].sum() > 0
+
+
+# ---- float / double partition keys (round 5): String.valueOf(value) names the partitions — the bits,
+# every NaN one partition, 0.0 and -0.0 two — except where the Scheduler's tie order (Double.toString's
+# hash) decides the output (time windows with expired output: refused)
+FSCHEMA = abi.Schema.parse("p double, g int, v double, x long, f float, ts long")
+
+
+def fstream(n, parts, seed, runs=False):
+    ts, (p, g, v, x, h, ts2) = gstream(n, parts, 7, seed, runs=runs)
+    vals = np.array([0.0, -0.0, np.nan, 1.5, -2.25, 1e300, 3.0, -7.0] + [0.5 * i for i in range(8, parts)], np.float64)
+    pd = vals[p % len(vals)]
+    pd[(np.arange(n) % 97) == 5] = np.frombuffer(np.uint64(0x7FF0000000000123).tobytes(), np.float64)[0]  # a NaN payload
+    with np.errstate(over="ignore", invalid="ignore"):  # (1e300 -> inf, the NaN payload -> a float NaN)
+        f32 = pd.astype(np.float32)
+    return ts, [pd, g, v, x, f32, ts2]
+
+
+@pytest.mark.parametrize("window,L,group_by,output,stream_current",
+                         [("lengthBatch", 3, ["p"], "all", False), ("lengthBatch", 4, ["g"], "current", False),
+                          ("lengthBatch", 2, [], "current", True), ("lengthBatch", 5, ["g"], "current", True),
+                          ("time", 40, ["p"], "current", False), ("timeBatch", 30, ["g"], "all", False),
+                          ("externalTimeBatch", 25, ["g"], "current", False)])
+@pytest.mark.parametrize("pcol", ["p", "f"])
+def test_float_partition_keys(rt, window, L, group_by, output, stream_current, pcol):
+    ts, cols = fstream(20_000, 12, 71, runs=True)
+    if pcol == "f":
+        group_by = ["f" if c == "p" else c for c in group_by]
+    kw = {"ts_attr": "ts"} if window == "externalTimeBatch" else {}
+    spec = abi.QuerySpec(FSCHEMA, window, L, group_by=group_by, aggs=[("count", None), ("sum", "v"), ("max", "x")],
+                         partition=pcol, output=output, stream_current=stream_current, key_capacity=64, **kw)
+    pushes = split_batches(FSCHEMA, ts, cols, [1, 7_000], 3)
+    if window in ("time", "timeBatch"):
+        pushes.append(("advance", int(ts[-1]) + 10 * L))
+    ref = both(rt, spec, pushes, f"fp partition {window} {group_by} {pcol}")
+    assert ref["ts"].size > 0
+
+
+def test_float_partition_keys_time_expired_refused(rt):
+    spec = abi.QuerySpec(FSCHEMA, "time", 40, group_by=["p"], aggs=[("count", None)], partition="p", output="all",
+                         key_capacity=64)
+    with pytest.raises(rt.SiddhiError, match="Double.toString"):
+        rt.GpuQuery(spec)
