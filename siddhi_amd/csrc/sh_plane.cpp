@@ -258,8 +258,12 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     wp.rec_seq = q->tune.sl_records_seq;  // (the lane-strided records where they apply, as the sliding path)
     launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                      s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+    // lane-strided records (every event passes): no per-slot counts; the partitions' offsets come from
+    // the sorted slots below (k_counts_sorted; the LDS tables and atomics were 5.2 of plb's 20 ms)
+    const bool sorted_off = sl_records_seq_applies(q->fp, wp, q->ap);
     launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
+                      sorted_off ? nullptr : s->slot_cnt.as<u32>(), nblk);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -283,7 +287,8 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             RCHK(s->pg_err.reserve(64, false));
             HIPCHK(hipMemsetAsync(s->pg_err.p, 0, 8, st));
         }
-        launch_pg_append(st, rec, M, n_old, q->seq, cs, q->gkp, q->gkt.dev(), V, C, s->slot_cnt.as<u32>(),
+        launch_pg_append(st, rec, M, n_old, q->seq, cs, q->gkp, q->gkt.dev(), V, C,
+                         sorted_off ? nullptr : s->slot_cnt.as<u32>(),
                          s->pg_prevcnt.as<u32>(), ext ? q->d.ts_col : -1,
                          ext && q->d.has_start_time == 2 ? q->d.start_col : -1, s->pg_xs.as<int64_t>(),
                          s->pg_pendcnt.as<u32>());
@@ -299,6 +304,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             return sh_fail(SH_ERR_DEVICE, "radix sort failed");
         RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
         RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+        if (sorted_off) launch_counts_sorted(st, s->p_slot.as<u32>(), n, s->slot_cnt.as<u32>());
         launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
         // ---- entries keyed (chunk, group slot)
         const int gbits = bits_for((int64_t)q->gkt.size_ + 2), cbits = bits_for(n + 1);
@@ -739,6 +745,7 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
     int nblk = 0;
     int64_t M = 0;
     SlInfo info{};
+    bool sorted_off = false;  // records sorted and partition offsets made before the push's sync
     if (b) {
         for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
         nblk = (int)((N + kTile - 1) / kTile);
@@ -753,12 +760,28 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
         wp.rec_seq = q->tune.sl_records_seq;
         launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
                          s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+        // (lanes keyed by the partition, every event passing: the partition offsets and the ring need come
+        // from the sorted slots instead of per-slot counts)
+        sorted_off = !q->group_other && sl_records_seq_applies(q->fp, wp, q->ap);
         launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
+                          sorted_off ? nullptr : s->slot_cnt.as<u32>(), nblk);
         if (sched) launch_pl_slot_key(st, cs, q->kp, q->kt.dev(), N, s->pl_key.as<int64_t>());
         HIPCHK(hipMemsetAsync((char*)s->info.p + offsetof(SlInfo, need), 0, 8, st));
-        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots,
-                       (int64_t*)((char*)s->info.p + offsetof(SlInfo, need)));
+        int64_t* need_dev = (int64_t*)((char*)s->info.p + offsetof(SlInfo, need));
+        if (sorted_off) {
+            RCHK(s->ranks.reserve(cap * 4, false));
+            RCHK(s->p_slot.reserve(cap * 4, false));
+            RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+            size_t tb = 0;
+            if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, N, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), N, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+            launch_counts_sorted(st, s->p_slot.as<u32>(), N, s->slot_cnt.as<u32>());
+        }
+        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -772,15 +795,17 @@ static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out,
         }
     }
     // each partition's records in stream order
-    RCHK(s->ranks.reserve(cap * 4, false));
-    RCHK(s->p_slot.reserve(cap * 4, false));
-    if (M > 0) {
-        size_t tb = 0;
-        if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
-            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
-        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
-        if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
-            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+    if (!sorted_off) {
+        RCHK(s->ranks.reserve(cap * 4, false));
+        RCHK(s->p_slot.reserve(cap * 4, false));
+        if (M > 0) {
+            size_t tb = 0;
+            if (sort_slot_ranks(nullptr, &tb, rec.slot, nullptr, nullptr, M, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+            RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+            if (sort_slot_ranks(s->sort_tmp.p, &tb, rec.slot, s->p_slot.as<u32>(), s->ranks.as<u32>(), M, s->nslots, st))
+                return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        }
     }
     RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
     RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));

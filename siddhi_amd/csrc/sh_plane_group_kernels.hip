@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void k_pg_count_old(PgRecs C, i64 n_old, u3
     const i64 c = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (c >= n_old) return;
     const u32 p = C.ps[c];
-    atomicAdd(&slot_cnt[p], 1u);
+    if (slot_cnt) atomicAdd(&slot_cnt[p], 1u);  // (null: the offsets come from the sorted slots)
     if (C.prev[c]) atomicAdd(&prev_cnt[p], 1u);
     else if (pend_cnt) atomicAdd(&pend_cnt[p], 1u);
 }

@@ -284,7 +284,7 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     // keyed replay over lane-strided records (every event passes, M = N): the records are sorted by key
     // slot right away and the key offsets and ring need come from the sorted slots (no per-slot counts)
     const bool pre = keyed_aos(q) && sl_records_seq_applies(q->fp, wp, q->ap);
-    if (!pre) HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
     SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), N};
     if (keyed_aos(q)) {
@@ -301,10 +301,9 @@ int sliding_push(sh_query* q, const sh_batch* b, bool host_out, const sh_out** o
     if (pre) {
         HIPCHK(hipEventRecord(q->ev_agg0, st));  // (the sort is part of the replay's time)
         RCHK(sort_keyed(q, rec.slot, N));
-        launch_keyoff_sorted(st, s->p_slot.as<u32>(), N, s->nslots, s->key_off.as<u32>(), s->rlen.as<int64_t>(), need_dev);
-    } else {
-        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
+        launch_counts_sorted(st, s->p_slot.as<u32>(), N, s->slot_cnt.as<u32>());
     }
+    launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -415,8 +414,9 @@ static int sliding_finish(sh_query* q, int64_t M, int64_t rec_cap, int64_t need,
             RCHK(s->p_vals.reserve(M * 8, false));
             RCHK(s->rows_k.reserve((size_t)M * sliding_keyed_row_words(na, all_rows) * 8, false));
             if (q->tune.sl_kgather) RCHK(s->rec_aosk.reserve((size_t)M * kSlAosWords * 8, false));
-            launch_sliding_keyed(st, presorted ? nullptr : s->slot_cnt.as<u32>(), s->key_off.as<u32>(),
-                                 s->tmp.as<int64_t>(), s->ranks.as<u32>(),
+            RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+            RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+            launch_sliding_keyed(st, s->slot_cnt.as<u32>(), s->key_off.as<u32>(), s->tmp.as<int64_t>(), s->ranks.as<u32>(),
                                  rec, s->p_pm.as<int64_t>(), s->p_vals.as<u64>(), state_of(s), q->ap,
                                  q->d.window_param, send_size, send_base, s->rows_k.as<u64>(),
                                  all_rows ? nullptr : s->flags.as<unsigned char>(),
@@ -689,11 +689,9 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
         int64_t* need_dev = (int64_t*)((char*)s->info.p + offsetof(SlInfo, need));
         if (presorted) {
             RCHK(sort_keyed(q, rec.slot, N));
-            launch_keyoff_sorted(st, s->p_slot.as<u32>(), N, s->nslots, s->key_off.as<u32>(), s->rlen.as<int64_t>(),
-                                 need_dev);
-        } else {
-            launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
+            launch_counts_sorted(st, s->p_slot.as<u32>(), N, s->slot_cnt.as<u32>());
         }
+        launch_sl_need(st, s->slot_cnt.as<u32>(), s->rlen.as<int64_t>(), s->nslots, need_dev);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -808,10 +806,10 @@ static int slx_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, c
         RCHK(s->ranks.reserve(cap * 4, false));
         RCHK(s->p_slot.reserve(cap * 4, false));
         if (M > 0 && q->ap.n > 0) RCHK(sort_keyed(q, rec.slot, M));
-        RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
-        RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
-        launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
     }
+    RCHK(s->key_off.reserve((size_t)(s->nslots + 1) * 4, false));
+    RCHK(s->tmp.reserve((size_t)((s->nslots + 1 + kTile - 1) / kTile + 16) * 8, false));
+    launch_slx_keyoff(st, s->slot_cnt.as<u32>(), s->nslots, s->key_off.as<u32>(), s->tmp.as<int64_t>());
     HIPCHK(hipGetLastError());
     int64_t R = 0;
     RCHK(read_count(q, (const int64_t*)s->x_nexp.p, &R));

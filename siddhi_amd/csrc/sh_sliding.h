@@ -60,11 +60,10 @@ void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
                        i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock = nullptr);
 void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, i64* out);
 // the lane-strided records kernel applies (no filter, per-event sends, time window): every event passes,
-// M = N, and it may skip the per-slot counts (slot_cnt null) for launch_keyoff_sorted after the sort
+// M = N, and it may skip the per-slot counts (slot_cnt null) for launch_counts_sorted after the sort
 bool sl_records_seq_applies(FilterProg f, WinParams wp, AggPlan ap);
-// key offsets (nslots + 1) from the slot-sorted records, and the ring capacity the push needs (*need,
-// zeroed by the caller)
-void launch_keyoff_sorted(hipStream_t s, const u32* ps, i64 M, i64 nslots, u32* key_off, const i64* rlen, i64* need);
+// per-slot counts (slot_cnt zeroed by the caller) from the slot-sorted records
+void launch_counts_sorted(hipStream_t s, const u32* ps, i64 M, u32* slot_cnt);
 void launch_sl_multisplit(hipStream_t s, const u32* slot, i64 n, int P, i64* counts, i64* tmp, u32* out_rank,
                           i64* part_off);
 int sliding_keys_per_partition(AggPlan ap);

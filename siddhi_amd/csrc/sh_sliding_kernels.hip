@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict
     // the wave's 64 records staged in LDS, then stored as contiguous 16-byte pieces (each store
     // instruction covers 1 KB of whole lines instead of one piece of 64 records 48 bytes apart)
     __shared__ ulonglong2 stg[kBlock * 3];
-    // slot_cnt null: the caller takes the per-slot counts from the sorted slots instead (k_keyoff_sorted:
+    // slot_cnt null: the caller takes the per-slot counts from the sorted slots instead (k_counts_sorted:
     // r05, the tile's LDS table and its global atomics were 1.2 of the kernel's 1.9 ms at C3)
     const bool count = slot_cnt != nullptr;
     if (count)
@@ -309,51 +309,23 @@ void launch_sl_need(hipStream_t s, const u32* slot_cnt, const i64* rlen, i64 n, 
     hipLaunchKernelGGL(k_sl_need, dim3(256), dim3(kBlock), 0, s, slot_cnt, rlen, n, out);
 }
 
-// key_off[k] = the first sorted position whose slot is >= k (k = 0..nslots) from the slot-sorted
-// records: each run start writes the offsets of the slots from the previous run's slot up to its own
-// (the last position also those past its slot)
-__global__ __launch_bounds__(kBlock) void k_keyoff_sorted(const u32* __restrict__ ps, i64 M, i64 nslots,
-                                                         u32* __restrict__ key_off) {
-    // (four positions per thread: one 16-byte load and the previous word)
-    const i64 i0 = ((i64)blockIdx.x * kBlock + threadIdx.x) * 4;
-    if (i0 >= M) return;
-    u32 v[4];
-    if (i0 + 4 <= M) {
-        const uint4 q = *(const uint4*)(ps + i0);
-        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else {
-        for (int t = 0; t < 4; t++) v[t] = i0 + t < M ? ps[i0 + t] : 0u;
-    }
-    i64 prev = i0 ? (i64)ps[i0 - 1] : -1;
-    for (int t = 0; t < 4; t++) {
-        const i64 i = i0 + t;
-        if (i >= M) break;
-        const i64 cur = v[t];
-        if (cur != prev)
-            for (i64 k = prev + 1; k <= cur; k++) key_off[k] = (u32)i;
-        if (i == M - 1)
-            for (i64 k = cur + 1; k <= nslots; k++) key_off[k] = (u32)M;
-        prev = cur;
-    }
+// Per-slot counts from the slot-sorted records: the first position of a slot's run subtracts its index,
+// the last adds its index + 1 (two atomics per run, each on its own slot: no contention), so
+// slot_cnt[k] = the run's length; zeroed by the caller. (Writing the key offsets directly from the run
+// starts loops over every absent slot in between: with sparse slots — 231k Zipf partitions in a 10M-slot
+// dictionary — single lanes filled gaps of thousands, plb 20 -> 103 ms per push.)
+__global__ __launch_bounds__(kBlock) void k_counts_sorted(const u32* __restrict__ ps, i64 M, u32* slot_cnt) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= M) return;
+    const u32 cur = ps[i];
+    if (i == 0 || ps[i - 1] != cur) atomicAdd(&slot_cnt[cur], (u32)(-(i64)i));
+    if (i == M - 1 || ps[i + 1] != cur) atomicAdd(&slot_cnt[cur], (u32)(i + 1));
 }
 
-// max over the slots of the push of (ring length + the slot's records): the ring capacity it needs
-__global__ __launch_bounds__(kBlock) void k_sl_need_off(const u32* __restrict__ key_off, const i64* rlen, i64 n,
-                                                       i64* out) {
-    i64 m = 0;
-    for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
-        const i64 c = (i64)key_off[i + 1] - (i64)key_off[i];
-        if (c) m = max(m, rlen[i] + c);
-    }
-    i64 t = block_reduce(m, MaxOp(), 0);
-    if (threadIdx.x == 0) atomicMax((unsigned long long*)out, (unsigned long long)t);
-}
-
-void launch_keyoff_sorted(hipStream_t s, const u32* ps, i64 M, i64 nslots, u32* key_off, const i64* rlen, i64* need) {
+void launch_counts_sorted(hipStream_t s, const u32* ps, i64 M, u32* slot_cnt) {
     if (M > 0)
-        hipLaunchKernelGGL(k_keyoff_sorted, dim3((unsigned)((M + 4 * kBlock - 1) / (4 * kBlock))), dim3(kBlock), 0, s, ps,
-                           M, nslots, key_off);
-    hipLaunchKernelGGL(k_sl_need_off, dim3(256), dim3(kBlock), 0, s, key_off, rlen, nslots, need);
+        hipLaunchKernelGGL(k_counts_sorted, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ps, M,
+                           slot_cnt);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2191,7 +2163,7 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     }
     const i64 n = S.nslots;
     const u32 ss = send_size > 0 ? (u32)send_size : 0u;
-    if (slot_cnt) {  // (null: key_off already from the sorted slots, launch_keyoff_sorted)
+    {
         hipLaunchKernelGGL(k_sl_keyoff, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, slot_cnt, n, key_off);
         launch_scan_sum_large_u32(s, key_off, n + 1, tmp);
     }
