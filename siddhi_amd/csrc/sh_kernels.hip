@@ -1846,6 +1846,9 @@ void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_
 // the group's row values at the group's first entry. A scan over those heads gives the output order.
 
 
+// The row values (sval) are one record of n_aggs words per row head ([row][agg]): the walk's rows land
+// at scattered heads, and one record is one store where [agg][row] columns were n_aggs scattered
+// partial-line stores (r05: c2cur's walk).
 // window of entry m (0 = the window open before the push; a new entry j is in window #{pcb <= j})
 // and its chunk: lengthBatch sends every event on its own (:160-182), timeBatch the whole send
 __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
@@ -1889,27 +1892,37 @@ __global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict
     for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = 0;
     u32 c = 0;
     i64 head = -1;
+    // each entry's chunk is read once and carried (the previous / next entry's chunk decide the group's
+    // first and last event): one random chunk load per entry instead of three
+    u32 m_nx = idx[i];
+    i64 ch_nx = (i64)m_nx < n_old ? -1 : chunk[m_nx], ch_prev = -2;
     for (i64 t = i; t < hi; t++) {
-        const u32 m = idx[t];
+        const u32 m = m_nx;
+        const i64 ch = ch_nx;
+        if (t + 1 < hi) {
+            m_nx = idx[t + 1];
+            ch_nx = (i64)m_nx < n_old ? -1 : chunk[m_nx];
+        }
         i64 v[SH_MAX_AGGS];
 #pragma unroll
         for (int j = 0; j < SH_MAX_AGGS; j++) v[j] = j < ap.n_vcols ? (i64)pend_vals[(size_t)j * pend_cap + m] : 0;
         fold_fields<SH_MAX_AGGS>(ap, f, c == 0, v);
         c++;
+        const i64 cp = ch_prev;
+        ch_prev = ch;
         if ((i64)m < n_old) continue;
-        const i64 ch = chunk[m];
-        if (head < 0 || chunk[idx[t - 1]] != ch) {
+        if (head < 0 || cp != ch) {
             head = m;
             ghead[m] = 1;
         }
-        if (t + 1 == hi || chunk[idx[t + 1]] != ch) {  // the group's last event: its row values
+        if (t + 1 == hi || ch_nx != ch) {  // the group's last event: its row values
 #pragma unroll
             for (int a = 0; a < SH_MAX_AGGS; a++) {
                 if (a >= ap.n) break;
                 u64 fv = f[0];
 #pragma unroll
                 for (int j = 1; j < SH_MAX_AGGS; j++) if (ap.field[a] == j) fv = f[j];
-                sval[(size_t)a * M + head] = agg_out(ap, a, c, fv);
+                sval[(size_t)head * ap.n + a] = agg_out(ap, a, c, fv);  // (one record per row: see k_sc_keys)
             }
             slast[head] = m;
         }
@@ -1934,7 +1947,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
     i64 kv[SH_MAX_GROUP] = {0, 0};
     unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
-    for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+    for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
     out_chunk[o] = chunk[m];
     out_send[o] = send[m];
 }
@@ -2097,7 +2110,7 @@ __global__ __launch_bounds__(kBlock) void k_scx_current(i64 M, i64 n_old, const 
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) {
-        out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+        out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
         out_nulls[(size_t)a * T + o] = 0;
     }
     out_exp[o] = 0;
@@ -2182,7 +2195,7 @@ __global__ __launch_bounds__(kBlock) void k_scxt_current(i64 M, i64 n_old, const
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) {
-        out_vals[(size_t)a * T + o] = sval[(size_t)a * M + m];
+        out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
         out_nulls[(size_t)a * T + o] = 0;
     }
     out_exp[o] = 0;
