@@ -81,34 +81,30 @@ __device__ __forceinline__ bool x_eq(int kind, u64 a, u64 b) {
 __global__ __launch_bounds__(kBlock) void k_slx_sends(const i64* __restrict__ ts, ColSet cols, FilterProg f,
                                                      WinParams wp, const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                      i64* sK, i64* scb, i64* slast) {
-    const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
-    bool pass[kItems];
-    i64 cnt = 0, tl = INT64_MIN;
-    filter_items(f, cols, base, wp.N, pass);
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-        const i64 e = base + i;
-        if (e < wp.N) {
-            cnt += pass[i];
-            if (is_send_last(wp, e)) tl = max(tl, ts[e]);
-        }
-    }
-    i64 r = block_excl_scan(cnt, SumOp(), 0, nullptr) + blk_pass_pre[blockIdx.x];
-    i64 cm = max(block_excl_scan(tl, MaxOp(), INT64_MIN, nullptr), blk_tl_pre[blockIdx.x]);
+    // the tile's events lane-strided (round i: tile + i * kBlock + thread), a block scan per round, so
+    // consecutive lanes write consecutive sends (per-event sends: the thread-contiguous stores were 64
+    // pieces 8 entries apart per instruction; r05: 1.2 ms of c3all's push)
+    const i64 tile = (i64)blockIdx.x * kTile;
+    i64 run = blk_pass_pre[blockIdx.x], run_cm = blk_tl_pre[blockIdx.x];
     const i64 c0 = wp.clock_valid ? wp.clock0 : INT64_MIN;
     const i64 sl = send_len(wp);
-#pragma unroll
-    for (int i = 0; i < kItems; i++) {
-        const i64 e = base + i;
-        if (e >= wp.N) break;
-        if (e % sl == 0) {
+    for (int it = 0; it < kItems; it++) {
+        const i64 e = tile + (i64)it * kBlock + threadIdx.x;
+        const bool in = e < wp.N;
+        const bool pass = in && eval_filter(f, cols, e);
+        const i64 t = in ? ts[e] : INT64_MIN;
+        const i64 tl = in && is_send_last(wp, e) ? t : INT64_MIN;
+        i64 tot, mx;
+        const i64 r = run + block_excl_scan(pass ? (i64)1 : (i64)0, SumOp(), 0, &tot);
+        const i64 cm = max(run_cm, block_excl_scan(tl, MaxOp(), INT64_MIN, &mx));
+        run += tot;
+        run_cm = max(run_cm, mx);
+        if (in && e % sl == 0) {
             const i64 s = e / sl;
             sK[s] = r;
             scb[s] = max(c0, cm);
-            slast[s] = ts[send_last_of(wp, e)];
+            slast[s] = sl == 1 ? t : ts[send_last_of(wp, e)];
         }
-        r += pass[i];
-        if (is_send_last(wp, e)) cm = max(cm, ts[e]);
     }
 }
 
