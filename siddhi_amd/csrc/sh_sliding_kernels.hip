@@ -1319,6 +1319,18 @@ static bool own_d_fields(const AggPlan& ap, DFields& fd) {
 // window is its carried ring (events of earlier pushes) followed by the run itself; only the entries
 // still in the window at the end of the push go to the ring. Rows are written in key order as one record
 // each (full-line stores) and put in stream order by the emit kernel. ------------------------------------
+// resident waves per SIMD the wave-per-key replays are compiled for: k_sl_wkey at 4 (128 VGPRs, 8 bytes
+// of spill; left alone the compiler takes 131 and 3 waves: C3 8.29 -> 7.53 ms per push, r05_wpe; 5
+// spills 412 bytes and runs 3x slower); timing experiments override it
+#ifndef SH_WK_WPE
+#define SH_WK_WPE 4
+#endif
+#define SH_WK_ATTR __attribute__((amdgpu_waves_per_eu(SH_WK_WPE)))
+#ifdef SH_XW_WPE
+#define SH_XW_ATTR __attribute__((amdgpu_waves_per_eu(SH_XW_WPE)))
+#else
+#define SH_XW_ATTR
+#endif
 constexpr int kDqK = 64;  // LDS min/max deque entries per lane (longer deques continue in global memory)
 constexpr u32 kFirstBit = 0x80000000u;
 
@@ -1679,7 +1691,7 @@ __device__ __forceinline__ void dq_commit(KDq& q, u64* dv, int* di, const DqPlan
 // (SlRecords.aos); the lanes write the key-order (PM, value) columns the window-head reads use, and
 // the first-record flags / key-order positions the emit needs.
 template <bool HSUM, bool HMIN, bool HMAX>
-__global__ __launch_bounds__(64) void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, i64* __restrict__ g_pm,
+__global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict__ key_off, u32 nslots, i64* __restrict__ g_pm,
                                                u64* __restrict__ g_v, SlState S, DFields fd, KOut ko, i64 T,
                                                u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
@@ -2209,7 +2221,7 @@ int sliding_keys_per_partition(AggPlan ap) {
 constexpr u64 kSlxNoOp = ~0ull;
 
 template <bool HSUM, bool HMIN, bool HMAX>
-__global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off, u32 nslots,
+__global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restrict__ key_off, u32 nslots,
                                                 const u32* __restrict__ sorted_rank, const u64* __restrict__ xa,
                                                 const u64* __restrict__ xx, i64 n_u, i64 X0, i64 G0, i64 seq_base,
                                                 i64 send_size, SlState S, i64* __restrict__ rg, DFields fd, KOut ko,
@@ -2256,12 +2268,23 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
     const u64 le = (2ull << lane) - 1ull;  // lanes <= this one (lane 63: all)
     int ia = 0, ie = 0;                    // adds / FIFO entries consumed
     i64 row_ch = -1, row_op = 0;           // the (chunk, key) row open at the chunk start
+    // the staged adds / FIFO entries: lane l holds add ia + l and entry ie + l; after a chunk the
+    // unconsumed ones move down (shuffles) and only the freed lanes load (each record read once)
+    u64 a_op = kSlxNoOp, a_x = 0, a_ts = 0, a_clk = 0, a_ch = 0, a_rep = 0;
+    u64 x_op = kSlxNoOp, x_x = 0, x_ts = 0, x_clk = 0, x_ch = 0, x_rep = 0;
+    int a_keep = 0, x_keep = 0;  // lanes still holding a staged operation
     for (;;) {
-        // ---- stage the next 64 adds and the next 64 FIFO entries: one 48-byte record each (xa by
-        // record, xx by window position), the row fields kept in the staging lane's registers
-        u64 a_op = kSlxNoOp, a_x = 0, a_ts = 0, a_clk = 0, a_ch = 0, a_rep = 0;
-        u64 x_op = kSlxNoOp, x_x = 0, x_ts = 0, x_clk = 0, x_ch = 0, x_rep = 0;
-        if (ia + lane < A) {
+        // ---- stage up to the next 64 adds and the next 64 FIFO entries: one 48-byte record each (xa
+        // by record, xx by window position), the row fields kept in the staging lane's registers
+        if (lane >= a_keep) {
+            a_op = kSlxNoOp;
+            a_x = a_ts = a_clk = a_ch = a_rep = 0;
+        }
+        if (lane >= x_keep) {
+            x_op = kSlxNoOp;
+            x_x = x_ts = x_clk = x_ch = x_rep = 0;
+        }
+        if (lane >= a_keep && ia + lane < A) {
             const u32 ar = sorted_rank[lo + (u32)(ia + lane)];
             const ulonglong2* q = (const ulonglong2*)(xa + (size_t)ar * kXaWords);
             const ulonglong2 w0 = q[0], w1 = q[1], w2 = q[2];
@@ -2273,7 +2296,7 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
             a_rep = (u64)seq_base + w2.x;
         }
         const int p = ie + lane;
-        if (p < HN) {
+        if (lane >= x_keep && p < HN) {
             i64 x_u;
             if (p < H0) {
                 const size_t sl = kr + (size_t)((rh0 + p) & gm);
@@ -2485,6 +2508,24 @@ __global__ __launch_bounds__(64) void k_slx_wkey(const u32* __restrict__ key_off
         cnt += na_c - nx_c;
         ia += na_c;
         ie += nx_c;
+        {
+            // the unconsumed staged operations move down to lane 0 (every lane runs every shuffle)
+            const int sa = lane + na_c < 64 ? lane + na_c : 63, sx_ = lane + nx_c < 64 ? lane + nx_c : 63;
+            a_op = shfl64(a_op, sa);
+            a_x = shfl64(a_x, sa);
+            a_ts = shfl64(a_ts, sa);
+            a_clk = shfl64(a_clk, sa);
+            a_ch = shfl64(a_ch, sa);
+            a_rep = shfl64(a_rep, sa);
+            x_op = shfl64(x_op, sx_);
+            x_x = shfl64(x_x, sx_);
+            x_ts = shfl64(x_ts, sx_);
+            x_clk = shfl64(x_clk, sx_);
+            x_ch = shfl64(x_ch, sx_);
+            x_rep = shfl64(x_rep, sx_);
+            a_keep = 64 - na_c;
+            x_keep = 64 - nx_c;
+        }
         // ---- rows: lanes segmented by their chunk among the qualifying operations
         const i64 ch = in ? (i64)(is_add ? sa_ch : sx_ch) : 0;
         const bool qual = in && (is_add ? cur_on : exp_on);
