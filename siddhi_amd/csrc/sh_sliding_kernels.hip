@@ -157,18 +157,20 @@ __global__ __launch_bounds__(kBlock) void k_sl_records(const i64* __restrict__ t
 // records (whole lines; the thread-contiguous form stored 48-byte records 8 apart per lane, and PMC saw
 // 2.3x the record bytes written). Every event passes and ends its own send, so its clock and PM are the
 // running maximum of the timestamps (a block max-scan per round, carried across rounds).
+template <bool COUNT>
 __global__ __launch_bounds__(kBlock) void k_sl_records_seq(const i64* __restrict__ ts, ColSet cols, WinParams wp,
                                                           KeyPlan kp, KeyTable kt, AggPlan ap,
                                                           const i64* blk_pass_pre, const i64* blk_tl_pre,
                                                           const i64* blk_pm_pre, i64 pm0, SlRecords rec,
                                                           u32* slot_cnt, i64* send_clock) {
-    __shared__ u32 tk[kSlotTab], tc[kSlotTab];
+    // (without the slot table the block needs 12 KB of LDS instead of 45: 8 resident waves, not 3)
+    __shared__ u32 tk[COUNT ? kSlotTab : 1], tc[COUNT ? kSlotTab : 1];
     // the wave's 64 records staged in LDS, then stored as contiguous 16-byte pieces (each store
     // instruction covers 1 KB of whole lines instead of one piece of 64 records 48 bytes apart)
     __shared__ ulonglong2 stg[kBlock * 3];
     // slot_cnt null: the caller takes the per-slot counts from the sorted slots instead (k_counts_sorted:
     // r05, the tile's LDS table and its global atomics were 1.2 of the kernel's 1.9 ms at C3)
-    const bool count = slot_cnt != nullptr;
+    constexpr bool count = COUNT;
     if (count)
         for (int i = threadIdx.x; i < kSlotTab; i += kBlock) { tk[i] = 0xFFFFFFFFu; tc[i] = 0; }
     const i64 tile0 = (i64)blockIdx.x * kTile;
@@ -239,8 +241,12 @@ void launch_sl_records(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, 
                        KeyTable kt, AggPlan ap, const i64* blk_pass_pre, const i64* blk_tl_pre, const i64* blk_pm_pre,
                        i64 pm0, SlRecords rec, u32* slot_cnt, int nblk, i64* send_clock) {
     if (sl_records_seq_applies(f, wp, ap)) {
-        hipLaunchKernelGGL(k_sl_records_seq, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap, blk_pass_pre,
-                           blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
+        if (slot_cnt)
+            hipLaunchKernelGGL(k_sl_records_seq<true>, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap,
+                               blk_pass_pre, blk_tl_pre, blk_pm_pre, pm0, rec, slot_cnt, send_clock);
+        else
+            hipLaunchKernelGGL(k_sl_records_seq<false>, dim3(nblk), dim3(kBlock), 0, s, ts, cols, wp, kp, kt, ap,
+                               blk_pass_pre, blk_tl_pre, blk_pm_pre, pm0, rec, nullptr, send_clock);
         return;
     }
     hipLaunchKernelGGL(k_sl_records, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, kp, kt, ap, blk_pass_pre,
