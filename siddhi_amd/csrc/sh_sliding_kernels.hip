@@ -1511,6 +1511,19 @@ struct KOut {
 // deque (kdq_*), and its key stays sequential for the rest of the push (the indices are not kept there).
 constexpr int kWS = 128;  // window-head entries staged per chunk (two per lane)
 
+// The quirk check compares every expiring head with each of the chunk's records; bit-equal pairs are
+// rare, so the records first go into a 32K-bit filter in LDS and a head runs the exact comparison only
+// on a hit (about 0.2% of heads on distinct values). One wave per block: its LDS accesses are in order.
+constexpr int kBfWords = 1024;
+__device__ __forceinline__ u32 bf_hash(u64 v) { return (u32)((v * 0x9E3779B97F4A7C15ull) >> 49); }
+__device__ __forceinline__ void bf_init(u32* bf, int lane) {
+    for (int i = lane; i < kBfWords; i += 64) bf[i] = 0;
+}
+__device__ __forceinline__ bool bf_hit(const u32* bf, u64 v) {
+    const u32 h = bf_hash(v);
+    return (bf[h >> 5] >> (h & 31)) & 1u;
+}
+
 // lane l's value of a 64-bit register (l wave-uniform)
 __device__ __forceinline__ u64 rl64(u64 v, int l) {
     const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, l);
@@ -1712,6 +1725,7 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
     __shared__ u64 s_op[kWS + 64];
     __shared__ int s_lo[64];
     __shared__ unsigned char s_fl[kWS + 64];
+    __shared__ u32 s_bf[kBfWords];
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= nslots) return;
@@ -1741,6 +1755,7 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
         if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
         if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
     }
+    if (HMIN || HMAX) bf_init(s_bf, lane);
     __syncthreads();
     // the parallel min / max needs the deque entries' window indices
     bool par = HMIN || HMAX;
@@ -1826,6 +1841,9 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                 // deque entries or the chunk's records
                 bool dirty = false;
 #ifndef SH_WK_NODIRTY
+                const u32 hx = bf_hash(x);
+                if (in) atomicOr(&s_bf[hx >> 5], 1u << (hx & 31));
+                __syncthreads();
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
                     const int d = lane + 64 * t;
@@ -1842,8 +1860,11 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                             const int sl = (qx.h + e) & (kDqK - 1);
                             dirty |= dq_max[sl] == v && di_max[sl] != idx;
                         }
-                    for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
+                    if (bf_hit(s_bf, v))
+                        for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
                 }
+                __syncthreads();
+                if (in) s_bf[hx >> 5] = 0;  // (after every lane's test)
 #endif
                 pc = !__any(dirty);
             }
@@ -1904,27 +1925,30 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                 if (cnt + lo2 - (d + 1) == 0) s_fl[d + lo2] = 2;
             }
             __syncthreads();
-            u64 adm[3], czm[3];
+            u64 czm[3];
 #pragma unroll
             for (int wd = 0; wd < 3; wd++) {
                 const int j = wd * 64 + lane;
                 const unsigned char fv = j < nops ? s_fl[j] : 0;
-                adm[wd] = __ballot(fv == 1);
                 czm[wd] = __ballot(fv == 2);
             }
             if (HSUM) {
+                // each lane keeps the running sum at its own add (position ap_q); the canDestroy restarts
+                // are rare, so a chunk without one runs the loop without their check
                 double sm = sum;
-                int q = 0;
-                for (int j = 0; j < nops; j++) {
-                    sm = sm + __longlong_as_double((i64)s_op[j]);
-                    const int wd = j >> 6;
-                    const u64 bit = 1ull << (j & 63);
-                    const u64 cz = wd == 0 ? czm[0] : wd == 1 ? czm[1] : czm[2];
-                    const u64 ad = wd == 0 ? adm[0] : wd == 1 ? adm[1] : adm[2];
-                    if (cz & bit) sm = sm == 0.0 ? 0.0 : sm;
-                    if (ad & bit) {
-                        r_sum = lane == q ? (u64)__double_as_longlong(sm) : r_sum;
-                        q++;
+                const int myop = in ? ap_q : -1;
+                if ((czm[0] | czm[1] | czm[2]) == 0) {
+                    for (int j = 0; j < nops; j++) {
+                        sm = sm + __longlong_as_double((i64)s_op[j]);
+                        r_sum = j == myop ? (u64)__double_as_longlong(sm) : r_sum;
+                    }
+                } else {
+                    for (int j = 0; j < nops; j++) {
+                        sm = sm + __longlong_as_double((i64)s_op[j]);
+                        const int wd = j >> 6;
+                        const u64 cz = wd == 0 ? czm[0] : wd == 1 ? czm[1] : czm[2];
+                        if ((cz >> (j & 63)) & 1ull) sm = sm == 0.0 ? 0.0 : sm;
+                        r_sum = j == myop ? (u64)__double_as_longlong(sm) : r_sum;
                     }
                 }
                 sum = sm;
@@ -2240,6 +2264,7 @@ __global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restric
     __shared__ u64 s_aop[64], s_ax[64], s_xop[64], s_xx[64], s_val[64];
     __shared__ u64 s_pbn[HMIN ? 64 : 1], s_pbx[HMAX ? 64 : 1];
     __shared__ int s_sel[64];
+    __shared__ u32 s_bf[kBfWords];
     const u32 k = blockIdx.x;
     const int lane = threadIdx.x;
     if (k >= nslots) return;
@@ -2259,6 +2284,7 @@ __global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restric
     u64* gmax = HMAX ? S.dq + ((size_t)fd.mx * S.nslots + k) * S.rc : nullptr;
     if (HMIN) kdq_load<1>(qn, S, fd.mn, k, dq_min);
     if (HMAX) kdq_load<1>(qx, S, fd.mx, k, dq_max);
+    if (HMIN || HMAX) bf_init(s_bf, lane);
     __syncthreads();
 #ifdef SH_XW_SEQ
     bool par = false;  // (timing experiment only: the sequential deque throughout)
@@ -2380,6 +2406,9 @@ __global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restric
             pc = !__any(ain && d_isnan(a_x));
             if (pc) {
                 bool dirty = false;
+                const u32 hx = bf_hash(a_x);
+                if (ain) atomicOr(&s_bf[hx >> 5], 1u << (hx & 31));
+                __syncthreads();
                 if (lane < nx_c) {
                     const int idx = ie + lane;
                     const u64 v = x_x;
@@ -2393,8 +2422,11 @@ __global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restric
                             const int sl = (qx.h + e) & (kDqK - 1);
                             dirty |= dq_max[sl] == v && di_max[sl] != idx;
                         }
-                    for (int c = 0; c < na_c; c++) dirty |= s_ax[c] == v && S0 + c != idx;
+                    if (bf_hit(s_bf, v))
+                        for (int c = 0; c < na_c; c++) dirty |= s_ax[c] == v && S0 + c != idx;
                 }
+                __syncthreads();
+                if (ain) s_bf[hx >> 5] = 0;  // (after every lane's test)
                 pc = !__any(dirty);
             }
             DqPlan pn{}, px_{};
@@ -2473,10 +2505,17 @@ __global__ __launch_bounds__(64) SH_XW_ATTR void k_slx_wkey(const u32* __restric
 #ifdef SH_XW_NOSUM
                 r_sum = s_val[lane] ^ czm;  // (timing experiment only: no sum chain)
 #else
-                for (int j = 0; j < m; j++) {
-                    sm = sm + __longlong_as_double((i64)s_val[j]);
-                    if ((czm >> j) & 1ull) sm = sm == 0.0 ? 0.0 : sm;
-                    r_sum = lane == j ? (u64)__double_as_longlong(sm) : r_sum;
+                if (czm == 0) {  // (the common chunk: no canDestroy restart to check)
+                    for (int j = 0; j < m; j++) {
+                        sm = sm + __longlong_as_double((i64)s_val[j]);
+                        r_sum = lane == j ? (u64)__double_as_longlong(sm) : r_sum;
+                    }
+                } else {
+                    for (int j = 0; j < m; j++) {
+                        sm = sm + __longlong_as_double((i64)s_val[j]);
+                        if ((czm >> j) & 1ull) sm = sm == 0.0 ? 0.0 : sm;
+                        r_sum = lane == j ? (u64)__double_as_longlong(sm) : r_sum;
+                    }
                 }
 #endif
                 sum = sm;
