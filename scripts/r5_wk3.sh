@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-5 C3: the deque entries in the quirk filter (default lib, sliding GPU tests first), and k_sl_wkey
+# timing experiments (xNOROWS: no row stores, xNOFENCE: no fence at the chunk start; timing only)
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sliding_minmax.py tests/test_gpu_scale.py tests/test_gpu_sliding_expired.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r5wk3_tests.log 2>&1 || { tail -30 gpurun_out/r5wk3_tests.log; exit 1; }
+tail -2 gpurun_out/r5wk3_tests.log
+for v in "" _xNOROWS _xNOFENCE; do
+  SH_LIB=$PWD/siddhi_amd/libsiddhi_hip$v.so timeout -k 10 300 python3 -u bench.py --workload c3 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r5wk3_c3$v.json 2>gpurun_out/r5wk3_c3$v.err || { echo "c3 $v failed"; tail -5 gpurun_out/r5wk3_c3$v.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], '%.3e' % d['value'], round(d['ms_per_step'],3))" gpurun_out/r5wk3_c3$v.json "c3$v"
+done
+echo done

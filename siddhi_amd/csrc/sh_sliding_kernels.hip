@@ -1796,7 +1796,9 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
             }
             s_x[lane] = x;
             prev_raw = __shfl(raw, m - 1, 64);
+#ifndef SH_WK_NOFENCE
             __threadfence_block();  // this chunk's own records may expire within it
+#endif
             __syncthreads();
         }
         const int hb = hj;
@@ -1841,8 +1843,13 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                 // deque entries or the chunk's records
                 bool dirty = false;
 #ifndef SH_WK_NODIRTY
+                // (the filter holds the chunk's records and the deques' entries)
                 const u32 hx = bf_hash(x);
+                const u32 hn = HMIN && lane < qn.len ? bf_hash(dq_min[(qn.h + lane) & (kDqK - 1)]) : 0u;
+                const u32 hm = HMAX && lane < qx.len ? bf_hash(dq_max[(qx.h + lane) & (kDqK - 1)]) : 0u;
                 if (in) atomicOr(&s_bf[hx >> 5], 1u << (hx & 31));
+                if (HMIN && lane < qn.len) atomicOr(&s_bf[hn >> 5], 1u << (hn & 31));
+                if (HMAX && lane < qx.len) atomicOr(&s_bf[hm >> 5], 1u << (hm & 31));
                 __syncthreads();
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
@@ -1850,6 +1857,7 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                     if (d >= ne) continue;
                     const u64 v = t ? hv1 : hv0;
                     const int idx = hb + d;
+                    if (!bf_hit(s_bf, v)) continue;
                     if (HMIN)
                         for (int e = 0; e < qn.len; e++) {
                             const int sl = (qn.h + e) & (kDqK - 1);
@@ -1860,11 +1868,13 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                             const int sl = (qx.h + e) & (kDqK - 1);
                             dirty |= dq_max[sl] == v && di_max[sl] != idx;
                         }
-                    if (bf_hit(s_bf, v))
-                        for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
+                    for (int j = 0; j < m; j++) dirty |= s_x[j] == v && Sx + j != idx;
                 }
                 __syncthreads();
-                if (in) s_bf[hx >> 5] = 0;  // (after every lane's test)
+                // (after every lane's test)
+                if (in) s_bf[hx >> 5] = 0;
+                if (HMIN && lane < qn.len) s_bf[hn >> 5] = 0;
+                if (HMAX && lane < qx.len) s_bf[hm >> 5] = 0;
 #endif
                 pc = !__any(dirty);
             }
