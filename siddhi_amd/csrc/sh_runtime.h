@@ -289,6 +289,7 @@ struct sh_query {
     int64_t n_pend = 0, pend_cap = 0;
     int64_t seq = 0;  // stream index of the next event pushed (sh_out.rep numbering)
     DevBuf pend_pos, pend_ts, pend_vals;
+    DevBuf pend_tmp;  // staging of pending_to_front's overlapping moves (kept: no allocation per push)
     // scratch
     DevBuf blk_pass, blk_tl, blk_first, blk_xm, info, bounds, segs, seg_rows, rows, counters, out_ts, out_keys, out_vals,
         out_nulls, out_expired, out_rep, blk_cnt;

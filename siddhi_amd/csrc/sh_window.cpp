@@ -1070,15 +1070,22 @@ static int sc_expire_pending(sh_query* q, int64_t now, bool host_out) {
     return SH_OK;
 }
 
-// entries [lo, lo + n) of the pending buffer moved to its front
+// entries [lo, lo + n) of the pending buffer moved to its front: one copy per column when the ranges
+// do not overlap, else through the query's staging buffer (r05: a buffer allocated per push cost a
+// hipMalloc, a stream drain and a hipFree on every stream.current push)
 static int pending_to_front(sh_query* q, int64_t lo, int64_t n) {
     if (lo == 0 || n == 0) return SH_OK;
     hipStream_t s = q->ctx->stream;
-    DevBuf t;
-    RCHK(t.reserve((size_t)n * 8, false));
+    const bool direct = lo >= n;
+    if (!direct) RCHK(q->pend_tmp.reserve((size_t)n * 8, false));
     auto move = [&](void* base, size_t elem) -> int {
-        HIPCHK(hipMemcpyAsync(t.p, (char*)base + (size_t)lo * elem, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipMemcpyAsync(base, t.p, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
+        if (direct) {
+            HIPCHK(hipMemcpyAsync(base, (char*)base + (size_t)lo * elem, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
+            return SH_OK;
+        }
+        void* t = q->pend_tmp.p;
+        HIPCHK(hipMemcpyAsync(t, (char*)base + (size_t)lo * elem, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(base, t, (size_t)n * elem, hipMemcpyDeviceToDevice, s));
         return SH_OK;
     };
     RCHK(move(q->pend_pos.p, 4));
