@@ -391,7 +391,9 @@ __global__ __launch_bounds__(kBlock) void k_pend_bucket_range(const u32* __restr
                                                               u32 ref, i64* out) {
     i64 lo = INT64_MAX, hi = INT64_MIN;
     for (i64 i = (i64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (i64)gridDim.x * kBlock) {
-        const i64 d = (i64)(int)((u32)(slot_key(kt, pos[i]) >> 32) - ref);
+        // band keys: the bucket's signed distance from the band's row 0; otherwise the whole u32 bucket
+        const u32 b = (u32)(slot_key(kt, pos[i]) >> 32);
+        const i64 d = kt.lk ? (i64)(int)(b - ref) : (i64)b;
         lo = d < lo ? d : lo;
         hi = d > hi ? d : hi;
     }

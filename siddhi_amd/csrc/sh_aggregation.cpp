@@ -779,6 +779,7 @@ static int ring_collect(sh_aggregation* a, int64_t keep) {
 static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     const sh_out* o = nullptr;
     sh_batch dev;
+    RCHK(check_batch_cols(a->root, b));
     if (host) {
         RCHK(a->root->staged.stage(a->ctx->stream, b, a->root->d.n_cols, a->root->d.col_types, &dev));
     } else {

@@ -149,7 +149,6 @@ struct PushInfo {
     int err;           // externalTimeBatch: first event before its start time
     int unsorted;      // single-pass form: a timestamp decreased (redo with the prefix passes)
     i64 first_key;     // column WinParams.pcol1 - 1 of the first passing event (partitioned queries, R12)
-    int ms_overflow;   // k_split_sweep: a partition bucket overflowed (the host redoes the split)
 };
 
 // A window boundary inside the push: first combined index of a new window.
@@ -298,11 +297,6 @@ __host__ __device__ inline int tile_of(const TileMap& m, i64 b) {
 // counts the first n_count tiles of the map (k_boundaries counted the others) and zeroes the total slot
 void launch_ms_count(hipStream_t s, TileMap m, int n_count, i64 n_pend, const u32* pend_pos, PosSrc new_pos, int P,
                      u32* counts);
-size_t split_sweep_lds(int n_vcols, int P);
-void launch_split_sweep(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals, i64 pend_cap,
-                        const i64* ts, ColSet cols, FilterProg f, WinParams wp, KeyPlan kp, KeyTable kt, AggPlan ap,
-                        int P, int logP, i64 cap_p, u32* status, u32* ticket, u32* ms_off, u32* rec_idx, u64* rec_vals,
-                        i64 rec_cap, u32* new_pos, i64* blk_pass_pre, PushInfo* info, Bound* bounds, int max_bounds);
 void launch_fix_bounds(hipStream_t s, Bound* bounds, int max_bounds, const i64* blk_pass_pre, int nblk, const i64* ts,
                        WinParams wp, PushInfo* info);
 void launch_ms_scatter(hipStream_t s, TileMap m, i64 n_pend, const u32* pend_pos, const u64* pend_vals,
@@ -456,7 +450,8 @@ void launch_sc_flush_flags(hipStream_t s, i64 T, const i64* och, u32* flag);
 void launch_sc_flushes(hipStream_t s, i64 T, const i64* osd, const u32* pre, const i64* slp, int cv0, i64 clock0,
                        const i64* bclk, i64* fo1, i64* fc);
 void launch_xt_first_send(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 L, unsigned long long* out);
-void launch_xt_count_pass(hipStream_t s, ColSet cols, FilterProg f, i64 hi, unsigned long long* out);
+void launch_xt_count_pass(hipStream_t s, ColSet cols, FilterProg f, i64 hi, unsigned long long* out, int xcol = -1,
+                          long long* xmax = nullptr);
 void launch_scx_first(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx, u32* fe,
                       u32* fpre, u32* lastidx);
 void launch_scx_count(hipStream_t s, i64 M, i64 n_old, const i64* pcb, const u64* skey, const u64* skey2,

@@ -2394,12 +2394,23 @@ __global__ __launch_bounds__(kBlock) void k_xt_first_send(const i64* __restrict_
     if (threadIdx.x == 0 && first != INT64_MAX) atomicMin(out, (unsigned long long)first);
 }
 
-// passing events of the push in [0, hi): the open batch's events before a timeout's send
-__global__ __launch_bounds__(kBlock) void k_xt_count_pass(ColSet cols, FilterProg f, i64 hi, unsigned long long* out) {
-    i64 c = 0;
-    for (i64 e = (i64)blockIdx.x * kBlock + threadIdx.x; e < hi; e += (i64)gridDim.x * kBlock) c += eval_filter(f, cols, e);
+// passing events of the push in [0, hi): the open batch's events before a timeout's send, and (xcol >=
+// 0) the largest timestamp attribute among them — lastCurrentEventTime at the timeout (the expired rows'
+// stamp, flushToOutputChunk :341-348)
+__global__ __launch_bounds__(kBlock) void k_xt_count_pass(ColSet cols, FilterProg f, i64 hi, unsigned long long* out,
+                                                          int xcol, long long* xmax) {
+    i64 c = 0, m = INT64_MIN;
+    for (i64 e = (i64)blockIdx.x * kBlock + threadIdx.x; e < hi; e += (i64)gridDim.x * kBlock)
+        if (eval_filter(f, cols, e)) {
+            c++;
+            if (xcol >= 0) m = max(m, load_raw(cols, xcol, e));
+        }
     c = block_reduce(c, [](i64 a, i64 b) { return a + b; }, 0);
     if (threadIdx.x == 0 && c) atomicAdd(out, (unsigned long long)c);
+    if (xcol >= 0) {
+        m = block_reduce(m, MaxOp(), INT64_MIN);
+        if (threadIdx.x == 0 && m != INT64_MIN) atomicMax(xmax, (long long)m);
+    }
 }
 
 void launch_xt_first_send(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 L, unsigned long long* out) {
@@ -2408,10 +2419,11 @@ void launch_xt_first_send(hipStream_t s, const i64* ts, i64 N, i64 send_size, i6
     hipLaunchKernelGGL(k_xt_first_send, dim3(std::max(1u, g)), dim3(kBlock), 0, s, ts, N, send_size, L, out);
 }
 
-void launch_xt_count_pass(hipStream_t s, ColSet cols, FilterProg f, i64 hi, unsigned long long* out) {
+void launch_xt_count_pass(hipStream_t s, ColSet cols, FilterProg f, i64 hi, unsigned long long* out, int xcol,
+                          long long* xmax) {
     if (hi <= 0) return;
     const unsigned g = (unsigned)std::min<i64>((hi + kBlock - 1) / kBlock, 2048);
-    hipLaunchKernelGGL(k_xt_count_pass, dim3(g), dim3(kBlock), 0, s, cols, f, hi, out);
+    hipLaunchKernelGGL(k_xt_count_pass, dim3(g), dim3(kBlock), 0, s, cols, f, hi, out, xcol, xmax);
 }
 
 }  // namespace shd

@@ -222,16 +222,11 @@ Tuning Tuning::from_env() {
     // measured faster on MI355X (3.12 vs 3.03 G events/s on C3, profiles/r04_c3_records_seq.txt): default,
     // SH_SL_RECORDS_SEQ=0 restores the one-pass form
     t.sl_records_seq = !getenv("SH_SL_RECORDS_SEQ") || on("SH_SL_RECORDS_SEQ");
-    t.sweep = on("SH_SWEEP");
     // sorted chunks for partitioned lengthBatch keyed by the partition: 5.5e8 vs 8.2e6 events/s over
     // C5's Zipf partitions (one sequential lane per partition serialises the hot one); SH_PL_SORT=0 walks
     t.pl_sort = !getenv("SH_PL_SORT") || on("SH_PL_SORT");
     if (getenv("SH_AGG_BAND_ROWS")) t.agg_band_rows = atoi(getenv("SH_AGG_BAND_ROWS"));
-    // the gather of the records into key order costs more than the replay saves (C3 3.01e9 vs 3.36e9
-    // events/s: k_sl_kgather 1.32 ms moving 7.1 GB, k_sl_wkey 6.4 -> 6.1 ms; profiles/r05_c3_*)
     t.slx_wave = !getenv("SH_SLX_WAVE") || on("SH_SLX_WAVE");
-    t.sl_kgather = on("SH_SL_KGATHER");
-    t.emit_gather = !getenv("SH_EMIT_GATHER") || on("SH_EMIT_GATHER");
     return t;
 }
 

@@ -225,13 +225,10 @@ struct SlidingImpl;
 // A/B switches of the measured alternatives, read from the environment once per query,
 // when it is created, so a process can run queries with different settings side by side:
 // SH_DIRECT_POS=1, SH_PART_KEYS=1024, SH_NO_ASYNC_SMALL=1, SH_SL_RECORDS_SEQ=0/1, SH_AGG_BAND_ROWS=n,
-// SH_SWEEP=1 (k_split_sweep instead of the two-pass split: measured slower), SH_SL_KGATHER=0
 struct Tuning {
-    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false, sweep = false;
+    bool direct_pos = false, part_keys_1024 = false, no_async_small = false, sl_records_seq = false;
     bool pl_sort = true;   // partitioned lengthBatch keyed by the partition on the sorted lanes (lane 3)
-    bool emit_gather = true;  // dense fold rows + one-pass emission (k_emit_gather); SH_EMIT_GATHER=0: rank scatter
     bool slx_wave = true;     // expired / all-events sliding replay with a wave per key (k_slx_wkey); SH_SLX_WAVE=0: a lane per key
-    bool sl_kgather = false;  // keyed sliding replay over key-ordered records (k_sl_kgather, SH_SL_KGATHER=1): measured slower
     int agg_band_rows = 8;
     static Tuning from_env();
 };
@@ -298,8 +295,6 @@ struct sh_query {
     const void* zeroed_nulls = nullptr;    // out_nulls / out_expired buffers already zeroed
     const void* zeroed_expired = nullptr;
     DevBuf ms_counts, ms_tmp, rec_pos, rec_idx, rec_vals, part_off;
-    DevBuf sw_status;          // k_split_sweep: look-back status words [tile][partition] + the tile ticket
-    bool sweep_off = false;    // a bucket overflowed once: this query keeps the counting split
     DevBuf new_pos, seg_off;  // key slot per event of the push (kNoPos = filtered out); segment record offsets
     PushInfo* h_info = nullptr;
     PinnedBuf h_up;    // pinned segment list of the closed windows (read by the kernels in place)
@@ -349,6 +344,9 @@ struct sh_query {
     sh_out dev_out{};
     PinnedVec<int64_t> dev_flush_offsets{0}, dev_flush_clock;
     hipEvent_t ev_push0 = nullptr, ev_push1 = nullptr, ev_agg0 = nullptr, ev_agg1 = nullptr;
+    // the presorted sliding replay's key sort, timed apart from the replay (the host sync lies between)
+    hipEvent_t ev_srt0 = nullptr, ev_srt1 = nullptr;
+    bool srt_timed = false;
     hipEvent_t ev_mid = nullptr;  // the push info and boundaries are on the host (work queued after it runs on)
     sh_stats stats{};
     int64_t agg_bytes = 0;

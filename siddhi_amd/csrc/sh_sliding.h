@@ -74,8 +74,7 @@ int sort_slot_ranks(void* temp, size_t* bytes, const u32* slot, u32* slot_out, u
                     hipStream_t s);
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
                           SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
-                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags, u64* aosk = nullptr,
-                          i64 M = 0);
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags);
 // compact: per-event sends (no flags), the row holds its values only
 int sliding_keyed_row_words(int n_aggs, bool compact = false);
 // rowsK: the keyed replay's rows at the stream rank of their first record (flags NULL: per-event sends,

@@ -36,7 +36,7 @@ struct SlidingImpl {
     DevBuf blk_pass, blk_tl, blk_pm, info, rec_raw, rec_slot, rec_clock, rec_pm, rec_ts, rec_vals, slot_cnt, counts,
         tmp, ranks, part_off, flags, rec_sclk, p_raw, p_slot, p_clock, p_pm, p_ts, p_vals, rows_ts, rows_rep, rows_slot, rows_send, rows_clock, rows_vals, rows_nulls, blk_cnt, out_ts,
         out_keys, out_vals, out_nulls, out_send, out_clock, out_expired, out_rep, flush_off, flush_clock, sort_tmp,
-        key_off, g_rank, inv, rows_k, rec_aos, rec_aosk;
+        key_off, g_rank, inv, rows_k, rec_aos;
     SlInfo* h_info = nullptr;
     PinnedBuf h_up;  // pinned staging of small host->device uploads
     sh_out dev_out{};

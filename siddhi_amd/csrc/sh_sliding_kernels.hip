@@ -1714,7 +1714,7 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
                                                u64* __restrict__ g_v, SlState S, DFields fd, KOut ko, i64 T,
                                                u32 send_size, i64 send_base, u64* __restrict__ rowsK, int RW,
                                                const u32* __restrict__ sorted_rank, const u64* __restrict__ aos,
-                                               unsigned char* __restrict__ flags, const u64* __restrict__ aosk) {
+                                               unsigned char* __restrict__ flags) {
     __shared__ u64 dq_min[HMIN ? kDqK : 1];
     __shared__ u64 dq_max[HMAX ? kDqK : 1];
     __shared__ int di_min[HMIN ? kDqK : 1];
@@ -1736,11 +1736,10 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
     const u64* rval = S.rval + (size_t)k * S.rc;
     const int rh0 = (int)(S.rhead[k] & gm), H0 = (int)S.rlen[k];
     const int n = (int)(b - a), HN = H0 + n;
-    // aosk: the records already in key order (k_sl_kgather), their PM and value read in place; otherwise
-    // they are read through the sort's rank list and the key-order PM / value columns written here
-    const bool kord = aosk != nullptr;
-    auto run_pm = [&](u32 j) -> i64 { return kord ? (i64)aosk[(size_t)j * kSlAosWords + 1] : g_pm[j]; };
-    auto run_v = [&](u32 j) -> u64 { return kord ? aosk[(size_t)j * kSlAosWords + 3] : g_v[j]; };
+    // the records are read through the sort's rank list and the key-order PM / value columns written here
+    // (a key-ordered copy of the records, k_sl_kgather in round 5, cost what it saved: r05_c3_kgather_*)
+    auto run_pm = [&](u32 j) -> i64 { return g_pm[j]; };
+    auto run_v = [&](u32 j) -> u64 { return g_v[j]; };
     auto head_pm = [&](int h) -> i64 { return h < H0 ? rpm[(rh0 + h) & gm] : run_pm(a + (u32)(h - H0)); };
     auto head_v = [&](int h) -> u64 { return h < H0 ? rval[(rh0 + h) & gm] : run_v(a + (u32)(h - H0)); };
     // the running state: the same in every lane (the sequential part runs wave-uniform)
@@ -1774,10 +1773,9 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
         u64 x;
         u32 raw, rk;
         {
-            const u32 r0 = kord ? 0u : sorted_rank[i];
-            const ulonglong2* rp = (const ulonglong2*)(kord ? aosk + (size_t)i * kSlAosWords : aos + (size_t)r0 * kSlAosWords);
+            const u32 r = sorted_rank[i];  // the record's stream rank
+            const ulonglong2* rp = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
             const ulonglong2 w0 = rp[0], w1 = rp[1], w2 = rp[2];
-            const u32 r = kord ? (u32)w2.y : r0;  // the record's stream rank
             clk = (i64)w0.x;
             ts = (i64)w1.x;
             x = w1.y;
@@ -1788,10 +1786,8 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
             const bool fst = send_size == 1 || (o0 + lane == 0) || (send_size == 0 ? false : pr / send_size != raw / send_size);
             rk = r | (fst ? kFirstBit : 0u);
             if (in) {
-                if (!kord) {
-                    g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
-                    g_v[i] = x;
-                }
+                g_pm[i] = (i64)w0.y;  // the window-head columns, in key order
+                g_v[i] = x;
                 if (flags) flags[r] = fst ? 1 : 0;  // (per-event sends: every record opens its row, no flags)
             }
             s_x[lane] = x;
@@ -2053,8 +2049,7 @@ __global__ __launch_bounds__(64) SH_WK_ATTR void k_sl_wkey(const u32* __restrict
             // the row lands at the stream rank of its first record, so the emission reads the rows in
             // stream order (whole lines) instead of gathering them from key order
             const u32 row_rank = grp == o0 + lane ? (rk & ~kFirstBit)
-                                 : kord ? (u32)aosk[(size_t)(a + (u32)grp) * kSlAosWords + 5]
-                                        : sorted_rank[a + (u32)grp];
+                                 : sorted_rank[a + (u32)grp];
             ulonglong2* dst = (ulonglong2*)(rowsK + (size_t)row_rank * RW);
             if (!flags) {
                 // per-event sends: every record's row follows its own add (count >= 1, no nulls) and the
@@ -2186,25 +2181,9 @@ bool sliding_keyed_ok(AggPlan ap) {
 
 int sliding_keyed_row_words(int n_aggs, bool compact) { return compact ? (n_aggs + 1) & ~1 : (4 + n_aggs + 1) & ~1; }
 
-// The 48-byte records in key order (sorted_rank[i] = the stream rank of key-order record i), each
-// carrying its stream rank in its last word: the replay then streams every key's run instead of
-// chasing the rank list with random reads (r04: 11.3 GB of HBM traffic per C3 push in k_sl_wkey).
-__global__ __launch_bounds__(kBlock) void k_sl_kgather(const u32* __restrict__ sorted_rank, i64 M,
-                                                      const u64* __restrict__ aos, u64* __restrict__ aosk) {
-    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M) return;
-    const u32 r = sorted_rank[i];
-    const ulonglong2* src = (const ulonglong2*)(aos + (size_t)r * kSlAosWords);
-    const ulonglong2 w0 = src[0], w1 = src[1], w2 = src[2];
-    ulonglong2* dst = (ulonglong2*)(aosk + (size_t)i * kSlAosWords);
-    dst[0] = w0;
-    dst[1] = w1;
-    dst[2] = make_ulonglong2(w2.x, (u64)r);
-}
-
 void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64* tmp, const u32* sorted_rank,
                           SlRecords rec, i64* g_pm, u64* g_v, SlState S, AggPlan ap, i64 T,
-                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags, u64* aosk, i64 M) {
+                          i64 send_size, i64 send_base, u64* rowsK, unsigned char* flags) {
     DFields fd;
     own_d_fields(ap, fd);
     KOut ko{};
@@ -2221,12 +2200,9 @@ void launch_sliding_keyed(hipStream_t s, const u32* slot_cnt, u32* key_off, i64*
     }
     const bool hs = fd.sum >= 0 || fd.avg >= 0, hn = fd.mn >= 0, hx = fd.mx >= 0;
     const int RW = sliding_keyed_row_words(ap.n, flags == nullptr);
-    if (aosk && M > 0)
-        hipLaunchKernelGGL(k_sl_kgather, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, sorted_rank, M,
-                           rec.aos, aosk);
 #define SH_SL_W(A, B, C)                                                                                            \
     hipLaunchKernelGGL((k_sl_wkey<A, B, C>), dim3((unsigned)n), dim3(64), 0, s, key_off, (u32)n, g_pm, g_v, S, fd, ko, \
-                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags, aosk)
+                       T, ss, send_base, rowsK, RW, sorted_rank, rec.aos, flags)
     if (hs && hn && hx) SH_SL_W(true, true, true);
     else if (hs && !hn && !hx) SH_SL_W(true, false, false);
     else if (!hs && hn && hx) SH_SL_W(false, true, true);

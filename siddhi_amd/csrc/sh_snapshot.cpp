@@ -263,7 +263,7 @@ int batch_restore(sh_query* q, Reader& r) {
     }
     if (q->xt_replace) {
         const uint64_t ns = r.val<uint64_t>();
-        if (!r.ok || ns > 64) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        if (!r.ok || ns > (r.n - r.o) / 16) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
         q->xr_starts.clear();
         for (uint64_t i = 0; i < ns; i++) {
             const int64_t a = r.val<int64_t>(), b = r.val<int64_t>();

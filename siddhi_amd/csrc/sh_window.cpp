@@ -329,6 +329,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         for (int i = 0; i < d->n_group_by; i++) use(d->group_by[i]);
         for (int i = 0; i < d->n_aggs; i++) if (d->aggs[i].fn != SH_AGG_COUNT) use(d->aggs[i].col);
         use(d->partition_col);
+        if (kp_override)  // (an aggregation root keys on the time bucket and its group-by column)
+            for (int i = 0; i < q->kp.n; i++) use(q->kp.col[i]);
         if (d->window == SH_WIN_EXT_TIME_BATCH || d->window == SH_WIN_EXT_TIME) use(d->ts_col);
         if (d->window == SH_WIN_EXT_TIME_BATCH && d->has_start_time == 2) use(d->start_col);
         q->cols_used = m;
@@ -371,7 +373,7 @@ static bool direct_pos_ok(const sh_query* q) {
 static bool want_direct_pos(const sh_query* q) {
     // opt-in (SH_DIRECT_POS=1) for the two-pass split: measured slower on MI355X — k_ms_scatter 290 vs
     // 236 us per C2 push reading the key column instead of the slot column k_boundaries writes
-    // (profiles/r03_c2_v3*); the one-sweep split (k_split_sweep) writes no slot column where it may
+    // (profiles/r03_c2_v3*)
     return q->tune.direct_pos && direct_pos_ok(q);
 }
 
@@ -486,8 +488,9 @@ static int run_closed(sh_query* q, const std::vector<Segment>& segs, const std::
     const u32* rec_pos = q->rec_pos.as<u32>();
     const u32* rec_idx = q->rec_idx.as<u32>();
     const u64* rec_vals = q->rec_vals.as<u64>();
-    // multisplit units leave every row at its key's slot and one pass emits them (k_emit_gather)
-    const bool gather = own && q->tune.emit_gather;
+    // multisplit units leave every row at its key's slot and one pass emits them (k_emit_gather; the
+    // round-4 rank scatter + column split remain for the other units)
+    const bool gather = own;
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_aggregate(s, dsegs, nseg, q->P, q->logP, q->NL, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(),
                      q->pend_cap, b ? q->new_pos.as<u32>() : nullptr, cs, q->ap, q->rows.as<u64>(), RW,
@@ -1244,13 +1247,17 @@ extern "C" int sh_query_set_ext_timeout(sh_query* q, int64_t ms) {
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "externalTimeBatch timeout runs on unpartitioned queries (the partitions' timeouts fire in "
                        "the Scheduler's HashMap order)");
-    if (!q->d.current_on || (q->d.expired_on && (q->d.n_group_by > 0 || q->ap.n == 0)))
-        return sh_fail(SH_ERR_UNSUPPORTED,
-                       "externalTimeBatch timeout runs with current-events output (all events: aggregating, no "
-                       "group-by)");
+    if (q->d.stream_current)
+        return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout with stream.current.event output");
     q->xt_timeout = ms;
-    // every emission ends in the batch's current events: processInBatchNoGroupBy's one row is CURRENT
-    q->xmode = false;
+    // Every emission — a timeout's flushToOutputChunk / appendToOutputChunk or a crossing's (:336-438) —
+    // is [expired copies of the previous emission's events, RESET, the open batch from its first event]:
+    // the expired chunk always holds exactly what the previous emission sent as CURRENT (a flush moves
+    // its current events there, an append adds the new ones to the re-sent ones). So the expired rows
+    // follow the batch windows' rule (sh_expired.cpp, flush j + 1 carries flush j's rows re-stamped with
+    // lastCurrentEventTime). Aggregating without group-by, all events: the chunk's one row is its last
+    // CURRENT event's (processInBatchNoGroupBy), so no expired rows are needed.
+    q->xmode = q->d.expired_on && !(q->d.current_on && q->d.n_group_by == 0 && q->ap.n > 0);
     return SH_OK;
 }
 
@@ -1258,16 +1265,17 @@ namespace {
 struct XtEmit {
     Segment seg;
     int64_t clock, window;
+    int64_t stamp;  // lastCurrentEventTime at the emission (the expired rows' timestamp)
 };
 }  // namespace
 
 // The timeout due where the push's clock reaches L: its send's first event (push index), that send's
 // clock, and the push's passing events before it.
-static int xt_probe(sh_query* q, const sh_batch* b, int64_t L, int64_t* f, int64_t* clk, int64_t* pcb) {
+static int xt_probe(sh_query* q, const sh_batch* b, int64_t L, int64_t* f, int64_t* clk, int64_t* pcb, int64_t* xmax) {
     hipStream_t s = q->ctx->stream;
     const int64_t N = b->n, ss = b->send_size;
-    RCHK(q->xt_dev.reserve(16, false));
-    RCHK(q->xt_host.reserve(16));
+    RCHK(q->xt_dev.reserve(24, false));
+    RCHK(q->xt_host.reserve(24));
     auto* d = q->xt_dev.as<unsigned long long>();
     int64_t* h = q->xt_host.as<int64_t>();
     HIPCHK(hipMemsetAsync(d, 0xFF, 8, s));
@@ -1282,20 +1290,23 @@ static int xt_probe(sh_query* q, const sh_batch* b, int64_t L, int64_t* f, int64
     ColSet cs{};
     cs.n = q->d.n_cols;
     for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->load_type[c]; cs.ptr[c] = b->cols[c]; }
+    const int64_t lo_m = INT64_MIN;
     HIPCHK(hipMemsetAsync(d + 1, 0, 8, s));
-    launch_xt_count_pass(s, cs, q->fp, *f, d + 1);
+    HIPCHK(hipMemcpyAsync(d + 2, &lo_m, 8, hipMemcpyHostToDevice, s));
+    launch_xt_count_pass(s, cs, q->fp, *f, d + 1, q->d.ts_col, (long long*)(d + 2));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(h + 1, d + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h + 1, d + 1, 16, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h, b->ts + last, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     *clk = h[0];
     *pcb = h[1];
+    *xmax = h[2];
     return SH_OK;
 }
 
 // The push's emissions in stream order: timeouts and the crossings (bounds) that have events to send.
 static int xt_plan(sh_query* q, const sh_batch* b, const PushInfo& info, const std::vector<Bound>& bounds,
-                   int64_t clock0, bool cv0, std::vector<XtEmit>& em) {
+                   int64_t clock0, bool cv0, int64_t xm0, std::vector<XtEmit>& em) {
     const int64_t T = q->xt_timeout;
     if (!q->xt_Lvalid && info.total_pass > 0) {
         // initTiming (:313-334): scheduled from the clock of the window's first event's send
@@ -1308,9 +1319,9 @@ static int xt_plan(sh_query* q, const sh_batch* b, const PushInfo& info, const s
     auto nnew_at = [&](int64_t pcb) { return (sent ? 0 : nnew0) + pcb - last_pcb; };
     auto timeouts = [&](int64_t clk) -> int {
         while (q->xt_Lvalid && clk >= q->xt_L) {
-            int64_t f, cf, pf;
-            RCHK(xt_probe(q, b, q->xt_L, &f, &cf, &pf));
-            if (nnew_at(pf) > 0) em.push_back(XtEmit{Segment{lo, q->n_pend + f}, cf, w});
+            int64_t f, cf, pf, xf;
+            RCHK(xt_probe(q, b, q->xt_L, &f, &cf, &pf, &xf));
+            if (nnew_at(pf) > 0) em.push_back(XtEmit{Segment{lo, q->n_pend + f}, cf, w, std::max(xm0, xf)});
             sent = true;
             last_pcb = pf;
             q->xt_L = cf + T;
@@ -1319,7 +1330,7 @@ static int xt_plan(sh_query* q, const sh_batch* b, const PushInfo& info, const s
     };
     for (const Bound& bd : bounds) {
         RCHK(timeouts(bd.clock));
-        if (nnew_at(bd.pcb) > 0) em.push_back(XtEmit{Segment{lo, bd.idx}, bd.clock, w});
+        if (nnew_at(bd.pcb) > 0) em.push_back(XtEmit{Segment{lo, bd.idx}, bd.clock, w, bd.pad});
         sent = true;
         last_pcb = bd.pcb;
         lo = bd.idx;
@@ -1452,6 +1463,7 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
 
 static void given_closes(sh_query* q);
 
+static int xr_trim(sh_query* q);
 static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh_out** out) {
     SH_TMARK(0);
     // expired / all-events output: the current rows stay on the device for xout_finish
@@ -1562,42 +1574,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         const bool early_split = (q->P > 1 || q->partitioned) && N >= (1 << 18) && !q->d.stream_current;
         const TileMap ms_map = make_tile_map(q->n_pend, q->n_pend + N);
         if (early_split) RCHK(reserve_ms_counts(q, ms_map));
-        // the one-sweep form (k_split_sweep, opt-in SH_SWEEP=1): window assignment and the split in one
-        // pass over the push, records in fixed-capacity partition buckets — measured slower than the two
-        // passes it replaces (730 vs 420 us per C2 push: its look-back serialises the tiles)
-        const int64_t total_ev = q->n_pend + N;
-        const int64_t cap_p = (total_ev + q->P - 1) / q->P + (total_ev + q->P - 1) / q->P / 4 + 4096;
-        const bool sweep = single_pass && early_split && b->send_size == 1 && !q->sweep_off && !q->partitioned &&
-                           q->P > 1 && q->NL <= 1024 && total_ev < (1 << 29) && (int64_t)q->P * cap_p < (1ll << 31) &&
-                           q->P <= 4096 && q->tune.sweep;
-        if (sweep) {
-            q->direct_pos = direct_pos_ok(q);
-            slot_col = q->direct_pos ? nullptr : q->new_pos.as<u32>();
-            const size_t st_bytes = (size_t)ms_map.nblk * q->P * 4;
-            RCHK(q->sw_status.reserve(st_bytes + 64, false));
-            HIPCHK(hipMemsetAsync(q->sw_status.p, 0, st_bytes + 64, s));
-            const int64_t rec_cap = (int64_t)q->P * cap_p;
-            RCHK(q->rec_idx.reserve((size_t)rec_cap * 4, false));
-            RCHK(q->rec_vals.reserve((size_t)std::max(1, q->ap.n_vcols) * rec_cap * 8, false));
-            const int nblk_new = ms_map.nblk - ms_map.np_t;
-            launch_split_sweep(s, ms_map, q->n_pend, q->pend_pos.as<u32>(), q->pend_vals.as<u64>(), q->pend_cap, b->ts,
-                               cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, q->P, q->logP, cap_p, q->sw_status.as<u32>(),
-                               (u32*)(q->sw_status.as<char>() + st_bytes), q->ms_counts.as<u32>(), q->rec_idx.as<u32>(),
-                               q->rec_vals.as<u64>(), rec_cap, slot_col, q->blk_pass.as<int64_t>(),
-                               q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds);
-            launch_fix_bounds(s, q->bounds.as<Bound>(), max_bounds, q->blk_pass.as<int64_t>(), nblk_new, b->ts, wp,
-                              q->info.as<PushInfo>());
-            q->ms_ready = true;
-            q->rec_packed = true;
-            q->ms_map = ms_map;
-            q->rec_cap = rec_cap;
-        } else {
-            launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
-                              q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
-                              slot_col, ext ? q->blk_xm.as<int64_t>() : nullptr,
-                              early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
-                              single_pass, q->blk_tl.as<int64_t>());
-        }
+        launch_boundaries(s, b->ts, cs, q->fp, wp, q->blk_pass.as<int64_t>(), q->blk_tl.as<int64_t>(),
+                          q->info.as<PushInfo>(), q->bounds.as<Bound>(), max_bounds, nblk, q->kp, q->kt.dev(),
+                          slot_col, ext ? q->blk_xm.as<int64_t>() : nullptr,
+                          early_split ? q->ms_counts.as<u32>() : nullptr, q->P, ms_map.nblk, ms_map.np_t,
+                          single_pass, q->blk_tl.as<int64_t>());
         HIPCHK(hipGetLastError());
         // the push info and the first boundaries come back in one copy; the key partitioning of the
         // push's events (independent of where the windows close) is queued behind it and runs while
@@ -1614,7 +1595,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         }
         HIPCHK(hipEventRecord(q->ev_mid, s));
         SH_TMARK(1);
-        if (early_split && !sweep) RCHK(run_multisplit(q, q->n_pend + N, b, true));
+        if (early_split) RCHK(run_multisplit(q, q->n_pend + N, b, true));
         SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
         SH_TMARK(2);
         HIPCHK(sh_wait_event(q->ev_mid));
@@ -1624,17 +1605,6 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         if (q->band_spec && q->h_spec.as<uint32_t>()[2] == 3) {
             SH_TRACE("push: a bucket outside the speculative key band, retried after a probe");
             return kRetryBand;
-        }
-        if (sweep && info.ms_overflow) {
-            // a partition bucket overflowed (skewed keys): the counting split runs in run_closed, and
-            // for this query from now on
-            SH_TRACE("push: split-sweep bucket overflow, counting split");
-            q->sweep_off = true;
-            q->ms_ready = false;
-            if (!q->direct_pos) {
-                // the slot column may have been skipped where the sweep read dictionary ids directly:
-                // it was written (slot_col) unless direct reads are valid, so nothing to redo
-            }
         }
         if (single_pass && info.unsorted) {
             // a timestamp decreased: the send clocks need the prefix passes after all (the key slots,
@@ -1654,6 +1624,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         if (ext && info.err)
             return sh_fail(SH_ERR_UNSUPPORTED,
                            "externalTimeBatch: the first event's timestamp is before its start time (not on the GPU)");
+        const int64_t xm0 = q->xm;  // (lastCurrentEventTime before the push: timeout stamps)
         if (ext) q->xm = std::max(q->xm, info.max_xm);
         std::vector<Bound> bounds(info.n_bounds);
         if (info.n_bounds) {
@@ -1665,8 +1636,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             }
             std::sort(bounds.begin(), bounds.end(), [](const Bound& a, const Bound& c) { return a.idx < c.idx; });
         }
-        if (q->xt_replace)  // (the windows start at new events: stream index = seq0 + combined index - queued)
+        if (q->xt_replace) {  // (the windows start at new events: stream index = seq0 + combined index - queued)
+            RCHK(xr_trim(q));  // (what earlier calls left, so a call failing after this point leaves few)
             for (auto& bd : bounds) q->xr_starts.emplace_back(seq0 + std::max<int64_t>(0, bd.idx - q->n_pend), bd.W);
+        }
         if (q->xmode) {
             q->x_stamps.clear();
             if (q->given) {
@@ -1696,7 +1669,11 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         const bool close_all = (q->given && q->given_W_end > W_last) || lb_full;
         if (q->xt_timeout > 0) {
             std::vector<XtEmit> em;
-            RCHK(xt_plan(q, b, info, bounds, clock0, cv0, em));
+            RCHK(xt_plan(q, b, info, bounds, clock0, cv0, xm0, em));
+            if (q->xmode) {  // (the emissions, not the crossings, are the flushes carrying expired rows)
+                q->x_stamps.clear();
+                for (const XtEmit& e : em) q->x_stamps.push_back(e.stamp);
+            }
             RCHK(xt_emit(q, em, b, host_out));
         }
         if (!bounds.empty() || close_all) {
@@ -1804,7 +1781,26 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     return query_push_staged(q, &dev, out);
 }
 
-// a push through the query's output rate limiter: device output, then the limiter (sh_rate.cpp)
+// replaceTimestampWithBatchEndTime's recorded batch starts that later rows can still name: the open
+// batch and the one before it (expired rows) — the last 4 entries — and, with an output rate limiter,
+// every batch holding a row the limiter carries into a later call (its rep is the oldest it can show)
+static int xr_trim(sh_query* q) {
+    auto& st = q->xr_starts;
+    size_t keep_from = st.size() > 4 ? st.size() - 4 : 0;
+    if (keep_from > 0 && q->rate.kind != SH_RATE_NONE && q->rate.nc > 0) {
+        std::vector<int64_t> reps((size_t)q->rate.nc);
+        HIPCHK(hipMemcpyAsync(reps.data(), q->rate.c_rep.p, reps.size() * 8, hipMemcpyDeviceToHost, q->ctx->stream));
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        const int64_t lo = *std::min_element(reps.begin(), reps.end());
+        auto it = std::upper_bound(st.begin(), st.end(), lo,
+                                   [](int64_t v, const std::pair<int64_t, int64_t>& e) { return v < e.first; });
+        const size_t cover = it == st.begin() ? 0 : (size_t)(std::prev(it) - st.begin());
+        keep_from = std::min(keep_from, cover);
+    }
+    if (keep_from > 0) st.erase(st.begin(), st.begin() + (ptrdiff_t)keep_from);
+    return SH_OK;
+}
+
 // replaceTimestampWithBatchEndTime: the timestamp attribute the window wrote into every row's
 // representative event — the end time E0 + T (W + 1) of its batch W (ExternalTimeBatchWindowProcessor
 // cloneAppend :446-456, findEndTime :440-444) — for sh_query_rep_ts_attr
@@ -1829,9 +1825,7 @@ static int rep_attr_finish(sh_query* q, const sh_out* o, bool host) {
         const int64_t W = it == st.begin() ? 0 : std::prev(it)->second;
         q->xr_vals[i] = q->E0 + T * (W + 1);
     }
-    // later rows lie in the open batch or the one before it (expired rows)
-    if (q->xr_starts.size() > 4) q->xr_starts.erase(q->xr_starts.begin(), q->xr_starts.end() - 4);
-    return SH_OK;
+    return xr_trim(q);
 }
 
 extern "C" int sh_query_set_ext_replace_ts(sh_query* q, int32_t on) {
@@ -1941,6 +1935,7 @@ static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_ou
     if (q->xt_timeout > 0 && q->xt_Lvalid && now >= q->xt_L) {
         // an externalTimeBatch timeout: the open batch, if it holds events not yet sent (:256-275)
         if (q->xt_nnew > 0 && q->n_pend > 0) {
+            if (q->xmode) q->x_stamps.assign(1, q->xm);  // (lastCurrentEventTime: the expired rows' stamp)
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{now}, windows{q->W_open};
             RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));
@@ -2023,7 +2018,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     if (q->h_info) (void)hipHostFree(q->h_info);
     if (q->small_res) (void)hipHostFree(q->small_res);
     if (q->zc_ring) (void)hipHostFree(q->zc_ring);
-    hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1, q->ev_mid};
+    hipEvent_t evs[] = {q->ev_push0, q->ev_push1, q->ev_agg0, q->ev_agg1, q->ev_mid, q->ev_srt0, q->ev_srt1};
     for (auto e : evs) if (e) (void)hipEventDestroy(e);
     delete q;
     return SH_OK;

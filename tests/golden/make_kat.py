@@ -192,6 +192,15 @@ case(name="externalTimeBatch_w17_timeout_not_replaced", source=E + ":1272-1330",
      sends=_login(*[(0, _L0 + t, 3 + i) for i, t in enumerate(_t17x)]) + [{"advance": B + 1000}],
      expect=dict(in_count=4, remove_count=0, values=[[2], [1], [2], [3]],
                  rep_cols=[["timestamp", [_L0 + 4342, _L0 + 5341, _L0 + 14345, _L0 + 24441]]]))
+# test15: externalTimeBatch(timestamp, 1 sec, timestamp, 100) — the start time from the first event's
+# `timestamp` attribute (initTiming :319-322: endTime = start + 1 sec), no group-by, all events; the sends
+# arrive within a millisecond and the 100 ms timeout fires in the final 1 s sleep (the last batch)
+case(name="externalTimeBatch_w15_start_attr_timeout", source=E + ":1162-1211", schema=LOGIN,
+     query=dict(window="externalTimeBatch", param=1000, ts_attr="timestamp", start_attr="timestamp", timeout=100,
+                aggs=[["count", None]], output="all"),
+     sends=_login(*[(0, _L0 + t, 3 + i) for i, t in enumerate(_t17x)]) + [{"advance": B + 1000}],
+     expect=dict(in_count=4, remove_count=0, values=[[2], [1], [2], [3]],
+                 rep_cols=[["timestamp", [_L0 + 4342, _L0 + 5341, _L0 + 14345, _L0 + 24441]]]))
 # test16: the same with replaceTimestampWithBatchEndTime = true (5th parameter, :210-220): cloneAppend
 # (:446-456) writes the batch's endTime into every kept event's timestamp attribute, so each row's
 # `timestamp` is its batch end (% 100 == 0): 805000, 806000 (the crossing event gets the new endTime),

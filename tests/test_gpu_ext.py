@@ -355,3 +355,15 @@ def test_ext_replace_timestamp_refusals():
     sp.replace_ts = True
     with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
         runtime.GpuQuery(sp)
+
+
+@pytest.mark.parametrize("rate", [("all", 7919), ("last", 4001), ("first", 3001)])
+def test_ext_replace_timestamp_through_rate_limiter(rate):
+    """rows an output rate limiter holds across many later batches still show their own batch's end time
+    (the recorded batch starts are kept back to the oldest row the limiter carries)"""
+    ts, cols = stream(60_000, 3_000, 0xFA, late_ms=200)
+    sp = spec(T=40, keys=3_000, output="all", aggs=RAGGS)
+    sp.replace_ts = True
+    sp.rate = rate
+    got = both(sp, split_batches(SCH, ts, cols, [1, 7_000, 7_001, 30_000, 45_000], 1), f"ext replace rate {rate}")
+    assert len(got["rep_attr"]) > 0

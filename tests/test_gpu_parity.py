@@ -362,15 +362,12 @@ def test_lengthbatch_batch_completing_on_the_push_end_flushes_in_that_push(rt):
     o.close()
 
 
-@pytest.mark.parametrize("sweep", ["1", "0"])
 @pytest.mark.parametrize("key_type,keys,filt", [("string", 100_000, None), ("int", 30_000, None),
                                                 ("string", 5_000, (">", "v", 50.0))])
-def test_c2_split_sweep_and_counting_split(rt, sweep, key_type, keys, filt, monkeypatch):
-    """timeBatch at C2 shape (per-event sends, pushes of >= 2^18 events): the one-sweep window
-    assignment + multisplit (k_split_sweep, decoupled look-back into partition buckets) and the two-pass
-    form (the default; SH_SWEEP=1 selects the sweep) both give the oracle's rows; the third push carries a
-    decreasing timestamp (the sweep's sortedness check hands over to the prefix passes)."""
-    monkeypatch.setenv("SH_SWEEP", sweep)
+def test_c2_counting_split(rt, key_type, keys, filt):
+    """timeBatch at C2 shape (per-event sends, pushes of >= 2^18 events): the early key-partition split
+    behind the window assignment gives the oracle's rows; the third push carries a decreasing timestamp
+    (the single-pass sortedness check hands over to the prefix passes)."""
     schema = abi.Schema.parse(f"k {key_type}, v double, ts long")
     ts, cols = synth.keyed_stream(0, 1_400_000, 0xC2, keys, 1000)
     ts = ts.copy()
@@ -378,13 +375,12 @@ def test_c2_split_sweep_and_counting_split(rt, sweep, key_type, keys, filt, monk
     cols[2] = ts.copy()
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"], filter=filt,
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys)
-    both(rt, spec, split_batches(schema, ts, cols, [300_000, 700_000, 1_100_000], 1), label=f"sweep {sweep}")
+    both(rt, spec, split_batches(schema, ts, cols, [300_000, 700_000, 1_100_000], 1), label=f"split {key_type} {keys}")
 
 
-def test_c2_split_sweep_bucket_overflow_falls_back(rt, monkeypatch):
-    """A hot key (a quarter of the events) overflows its partition bucket: the push redoes the split with
-    the counting passes and the query keeps them; output = oracle."""
-    monkeypatch.setenv("SH_SWEEP", "1")
+def test_c2_hot_key_split(rt):
+    """A hot key (a quarter of the events) makes one key partition far larger than the others; output =
+    oracle."""
     schema = abi.Schema.parse("k string, v double, ts long")
     ts, cols = synth.keyed_stream(0, 1_200_000, 0xC2, 50_000, 1000)
     k = cols[0].copy()
@@ -392,4 +388,4 @@ def test_c2_split_sweep_bucket_overflow_falls_back(rt, monkeypatch):
     cols[0] = k
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("sum", "v"), ("max", "v")], key_capacity=50_000)
-    both(rt, spec, split_batches(schema, ts, cols, [300_000, 700_000], 1), label="sweep overflow")
+    both(rt, spec, split_batches(schema, ts, cols, [300_000, 700_000], 1), label="hot key split")

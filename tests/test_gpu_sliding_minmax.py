@@ -62,16 +62,13 @@ def test_keyed_sliding_min_only_and_max_only(rt):
         both(rt, spec, split_batches(SCHEMA, ts, cols, [30_000], 1), f"minmax {aggs}")
 
 
-@pytest.mark.parametrize("seq,kg", [("0", "1"), ("1", "1"), ("1", "0"), ("0", "0")])
-def test_sliding_records_forms(rt, seq, kg, monkeypatch):
+@pytest.mark.parametrize("seq", ["0", "1"])
+def test_sliding_records_forms(rt, seq, monkeypatch):
     """Both forms of the sliding records pass (k_sl_records and the lane-strided k_sl_records_seq, chosen
-    per query by SH_SL_RECORDS_SEQ at creation), and the keyed replay over key-ordered records
-    (k_sl_kgather) or through the rank list (SH_SL_KGATHER=0), give the oracle's rows on a C3-shaped
-    stream."""
+    per query by SH_SL_RECORDS_SEQ at creation) give the oracle's rows on a C3-shaped stream."""
     from siddhi_amd import synth
     monkeypatch.setenv("SH_SL_RECORDS_SEQ", seq)
-    monkeypatch.setenv("SH_SL_KGATHER", kg)
     schema = abi.Schema.parse("k string, v double, ts long")
     ts, cols = synth.keyed_stream(0, 300_000, 0xC3, 2_000, 100)
     spec = abi.QuerySpec(schema, "time", 1_000, group_by=["k"], aggs=AGGS, key_capacity=2_000)
-    both(rt, spec, split_batches(schema, ts, cols, [100_000, 250_000], 1), f"records seq={seq} kgather={kg}")
+    both(rt, spec, split_batches(schema, ts, cols, [100_000, 250_000], 1), f"records seq={seq}")
