@@ -40,6 +40,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1 << 25, help="events per step (per GPU)")
     ap.add_argument("--keys", type=int, default=100_000)
+    ap.add_argument("--keys-total", type=int, default=0,
+                    help="N > 1 slice ingest (and --shard-loopback): the global key count (default N x --keys; "
+                         "north_star's 8-GPU target is the 1M-key timeBatch: --keys-total 1000000)")
+    ap.add_argument("--shard-loopback", type=int, default=0, metavar="G",
+                    help="one GPU: the sharded C2 pipeline of G owners (summarize, pack, exchange = device copy, "
+                         "consume), each owner ingesting --batch events per step; per-phase ms per owner-step")
     ap.add_argument("--events-per-ms", type=int, default=1000)
     ap.add_argument("--send-size", type=int, default=1, help="events per InputHandler.send (1 = PER_EVENT)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the oracle CPU baseline")
@@ -319,10 +325,10 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         push(i)
         if not sliced and not agg_timed:
             st = q.stats()
-            # C5's work is the scans over every event (R12 leaves one partition to aggregate); C4's the
-            # root window and every roll-up level
-            kern_ms += (st.push_ms if args.workload in ("c4", "c5", "c2all", "c2cur", "c3all", "plb", "plg")
-                        else st.main_kernel_ms)
+            # the whole device pipeline of the push (HIP events around it on the library's stream): the
+            # algorithmic bytes are the whole push's, so the fraction is the push's, not one kernel's
+            # (profiles/r06_*_kernel_stats.txt name the kernels and their shares)
+            kern_ms += st.push_ms
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -342,9 +348,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
     roof = None
     if kern_ms > 0:
         ach = bpe * B * args.steps / (kern_ms / 1e3) / 1e9
-        kname = ("whole device pipeline of the push" if args.workload in ("c5", "c2all", "c2cur", "c3all", "plb", "plg") else
-                 "whole device pipeline of the push (root window + sec..day roll-up levels)" if args.workload == "c4"
-                 else "main (aggregate / sliding)")
+        kname = ("whole device pipeline of the push (root window + sec..day roll-up levels)" if args.workload == "c4"
+                 else "whole device pipeline of the push")
         roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms_per_step": kern_ms / args.steps,
                 "bytes_per_event": bpe}
@@ -462,6 +467,100 @@ def run_host(args, dev):
         "pcie": r}), flush=True)
 
 
+def run_shard_loopback(args, dev):
+    """What one GPU of an N-GPU sliced C2 run spends per step, measured on one GPU: G owners of the
+    sharded query (ShardedQuery: sh_shard_summarize / pack / consume) in one process, each ingesting
+    --batch events of one global stream per step (G x --events-per-ms, --keys-total or G x --keys keys),
+    the all-to-all replaced by device copies of the owners' record runs. Every phase ends in a device
+    synchronisation; the per-owner figures are the phase totals / G. Not a driver line (no `value` of
+    the headline): it bounds the per-GPU rate of the multi-GPU path apart from the xGMI transfer."""
+    import numpy as np
+    import torch
+    from siddhi_amd import abi, runtime, synth
+    from siddhi_amd.shard import ShardedQuery
+    G, B = args.shard_loopback, args.batch
+    ctx = runtime.Context(dev.index)
+    keys_total = args.keys_total or args.keys * G
+    schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")
+    spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
+                         aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=keys_total)
+    shards = [ShardedQuery(spec, r, G, ctx) for r in range(G)]
+    rb = shards[0].record_bytes
+    send = [torch.empty(B * rb, dtype=torch.uint8, device=dev) for _ in range(G)]
+    recv = [torch.empty(2 * B * rb, dtype=torch.uint8, device=dev) for _ in range(G)]
+    nb = args.warmup + args.steps
+
+    def slices(i):
+        return [synth.torch_keyed_stream((i * G + r) * B, B, 0xC2, keys_total, args.events_per_ms * G, dev)
+                for r in range(G)]
+
+    ph = {"summarize": 0.0, "pack": 0.0, "exchange_device_copy": 0.0, "consume": 0.0}
+    sent_bytes, rows = 0, 0
+
+    def step(sl, timed):
+        nonlocal sent_bytes, rows
+        t0 = time.perf_counter()
+        summ = np.stack([s.summarize(B, ts.data_ptr(), [c.data_ptr() for c in cols], 1)
+                         for s, (ts, cols) in zip(shards, sl)])
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        counts, bounds = [], []
+        for s, buf in zip(shards, send):
+            sb, bd = s.pack(summ, buf.data_ptr(), int(buf.numel()))
+            counts.append(np.asarray(sb))
+            bounds.append(bd)
+        all_bounds = np.concatenate(bounds)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        rbytes = []
+        for o in range(G):
+            off, rb_o = 0, []
+            for g in range(G):
+                start, n = int(counts[g][:o].sum()), int(counts[g][o])
+                if off + n > recv[o].numel():
+                    raise SystemExit("loopback receive buffer too small")
+                recv[o][off:off + n].copy_(send[g][start:start + n])
+                off += n
+                rb_o.append(n)
+            rbytes.append(rb_o)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        for o, s in enumerate(shards):
+            out = s.consume(recv[o].data_ptr(), rbytes[o], all_bounds, host_out=False)[0]
+            if timed:
+                rows += int(out.contents.n_rows)
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        if timed:
+            for k, v in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+                ph[k] += v * 1e3
+            sent_bytes += int(sum(c.sum() for c in counts))
+
+    for i in range(nb):
+        sl = slices(i)
+        torch.cuda.synchronize()
+        step(sl, i >= args.warmup)
+        del sl
+    per_owner = {k: v / args.steps / G for k, v in ph.items()}
+    compute_ms = per_owner["summarize"] + per_owner["pack"] + per_owner["consume"]
+    off_gpu = sent_bytes / args.steps / G * (G - 1) / G  # bytes one owner sends to other GPUs per step
+    print(json.dumps({
+        "metric": "sharded C2 pipeline, one GPU's share measured on one GPU (not the headline)",
+        "shards": G, "events_per_owner_step": B, "keys_total": keys_total,
+        "event_rate": f"{args.events_per_ms * 1000 * G} events per event-time second",
+        "ms_per_owner_step": per_owner,
+        "owner_events_per_s_without_xgmi": B / (compute_ms / 1e3),
+        "exchange_bytes_per_owner_step": sent_bytes / args.steps / G,
+        "off_gpu_bytes_per_owner_step": off_gpu,
+        # all-to-all over the 7 xGMI links (≈153 GB/s each, MI355X_MICROARCH.md): one owner's share
+        "xgmi_ms_per_owner_step_at_peak": off_gpu / (7 * 153e9) * 1e3,
+        "rows_per_step": rows / args.steps,
+        "record_bytes": rb,
+    }), flush=True)
+    for s in shards:
+        s.close()
+
+
 def main():
     args = parse()
     # all-cores CPU baseline workers: started before anything touches the GPU (rank 0, N = 1 only)
@@ -496,6 +595,10 @@ def main():
 
     if args.workload != "c2":
         return run_secondary(args, dev, rank, world, dist)
+    if args.shard_loopback:
+        if world > 1:
+            raise SystemExit("--shard-loopback runs on one GPU")
+        return run_shard_loopback(args, dev)
     if args.host:
         if world > 1:
             raise SystemExit("--host runs on one GPU")
@@ -504,7 +607,7 @@ def main():
     ctx = runtime.Context(local % ndev)
     schema = abi.Schema.parse(f"k {args.key_type}, v double, ts long")
     sliced = world > 1 and args.ingest == "slice"
-    keys_total = args.keys * world if sliced else args.keys
+    keys_total = (args.keys_total or args.keys * world) if sliced else args.keys
     cap = keys_total  # whole-stream key capacity (each owner sizes its table for its share)
     spec = abi.QuerySpec(schema, "timeBatch", 1000, group_by=["k"],
                          aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], key_capacity=cap)

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 11
+#define SH_ABI_VERSION 12
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -143,7 +143,9 @@ typedef struct {
 #define SH_DUR_YEARS 5
 
 /* `define aggregation A from S[filter] select g..., agg(col)... group by g...
- *   aggregate [by ts_col] every min_dur ... max_dur;` with the default GMT aggTimeZone.
+ *   aggregate [by ts_col] every min_dur ... max_dur;` in the aggTimeZone system configuration
+ *   (IncrementalTimeConverterUtil.java:33-231: hour / day / month / year buckets start at the zone's
+ *   local boundaries), given as a fixed offset from GMT (tz_offset_ms, whole minutes; 0 = GMT).
  * Per duration the library keeps the base values AggregationParser derives
  * (avg -> sum + count, count -> sum of 1L; AggregationParser.java:693-728). */
 typedef struct {
@@ -159,6 +161,7 @@ typedef struct {
     int32_t min_duration; /* SH_DUR_*                                                    */
     int32_t max_duration;
     int64_t key_capacity;
+    int64_t tz_offset_ms; /* aggTimeZone as a fixed offset (e.g. Asia/Singapore: +8 h = 28800000) */
 } sh_aggregation_desc;
 
 /* ---- input batch: a run of InputHandler.send(Event[]) calls -----------------------------
@@ -258,10 +261,13 @@ int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
  * (ExternalTimeBatchWindowProcessor.java:196-207, `externalTimeBatch(ts, 1 sec, 0, 6 sec)`): when the
  * playback clock passes the last scheduled time (clock of the window's first event, of every batch
  * crossing and of every timeout, + ms) the open batch goes out so far (:256-275) — again whole, with
- * its new events, at a later timeout or at its crossing (appendToOutputChunk, :385-438). Replaces the
- * Java window's timeout argument. Set once, before the first push, on an unpartitioned
- * externalTimeBatch query with current-events output (all events without group-by: every emission
- * ends in current events, QuerySelector.processInBatchNoGroupBy keeps that row). ms == 0 is no timeout. */
+ * its new events, at a later timeout or at its crossing (appendToOutputChunk, :385-438); with expired
+ * output every emission carries the previous emission's events as EXPIRED. Under `partition with` every
+ * partition keeps its own last scheduled time and partitions due at the same time fire in the
+ * Scheduler's HashMap order (Scheduler.java:71-104; int / long / bool keys, or string keys with their
+ * text set through sh_query_set_strings). Replaces the Java window's timeout argument. Set once, before
+ * the first push; refused (SH_ERR_UNSUPPORTED) on sharded queries, with stream.current.event and with
+ * float / double partition keys. ms == 0 is no timeout. */
 int sh_query_set_ext_timeout(sh_query* q, int64_t ms);
 
 /* externalTimeBatch's fifth parameter, replaceTimestampWithBatchEndTime (ExternalTimeBatchWindowProcessor.java:
@@ -269,8 +275,9 @@ int sh_query_set_ext_timeout(sh_query* q, int64_t ms);
  * carries its batch's end time in the timestamp attribute (ts_col), so the output events built from the rows'
  * representative events show the batch end, not the sent value. sh_query_rep_ts_attr returns that attribute for
  * every row of the last output (host array, valid until the next call on the query); the shim writes it into
- * the row's select attributes. Set once, before the first push, on an unpartitioned externalTimeBatch query;
- * aggregators and group keys over the timestamp attribute (which would fold the replaced values) are refused
+ * the row's select attributes. Set once, before the first push, on an externalTimeBatch query (partitioned:
+ * each partition's own batch ends); aggregators and group keys over the timestamp attribute (which would fold
+ * the replaced values), sharded queries and partitioned queries with an output rate limiter are refused
  * (SH_ERR_UNSUPPORTED). Replaces the Java window's fifth argument. */
 int sh_query_set_ext_replace_ts(sh_query* q, int32_t on);
 int sh_query_rep_ts_attr(sh_query* q, const int64_t** values, int64_t* n);

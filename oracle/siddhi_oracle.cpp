@@ -531,8 +531,10 @@ struct Query {
     RateLimiter rate;
 
     // the scheduler's tie rule decides output only for partitioned time windows with expired output
+    // (and for externalTimeBatch's timeout, whose TIMER calls act on the window)
     bool tie_rule_matters() const {
-        return d.partition_col >= 0 && d.window == SH_WIN_TIME && d.expired_on;
+        return d.partition_col >= 0 &&
+               ((d.window == SH_WIN_TIME && d.expired_on) || (d.window == SH_WIN_EXT_TIME_BATCH && ext_timeout > 0));
     }
 
     // String.valueOf(partition key): Integer/Long.toString, Boolean.toString, the string itself
@@ -554,7 +556,7 @@ struct Query {
             throw std::runtime_error(schema.types[c] == SH_T_STRID
                                          ? "partition key string id " + std::to_string(key) +
                                                " has no text (sh_query_set_strings): the Scheduler's tie rule needs it"
-                                         : "float / double partition keys of time windows with expired output are not restated");
+                                         : "float / double partition keys of time windows with expired output (or an externalTimeBatch timeout) are not restated");
         return jhm::decimal(key);  // order irrelevant to the output: any stable text
     }
 
@@ -1134,6 +1136,14 @@ struct AggRuntime {
     std::vector<std::vector<OutRow>> tables, history;
     std::vector<OutBuf> views;
     int vtypes[SH_MAX_AGGS]{};
+    // aggTimeZone (IncrementalTimeConverterUtil.java:33-231 with a ZoneId): a fixed offset from GMT here,
+    // hour / day / month / year buckets starting at the zone's local boundaries
+    int64_t zst(int64_t t, int dur) const {
+        return dur >= SH_DUR_HOURS ? start_time_of(t + d.tz_offset_ms, dur) - d.tz_offset_ms : start_time_of(t, dur);
+    }
+    int64_t zne(int64_t t, int dur) const {
+        return dur >= SH_DUR_HOURS ? next_emit_of(t + d.tz_offset_ms, dur) - d.tz_offset_ms : next_emit_of(t, dur);
+    }
 
     int base_out_type(const BaseDef& b) const {
         if (b.kind == B_COUNT) return SH_T_LONG;
@@ -1148,14 +1158,14 @@ struct AggRuntime {
             // getTimestamp (:152-169)
             if (r.type == CURRENT) {
                 timestamp = r.ts;
-                if (ex.root && !ex.timer_started) { notify_queue.push_back(next_emit_of(timestamp, ex.dur)); ex.timer_started = true; }
+                if (ex.root && !ex.timer_started) { notify_queue.push_back(zne(timestamp, ex.dur)); ex.timer_started = true; }
             } else {
                 timestamp = r.ts;
-                if (ex.root) notify_queue.push_back(next_emit_of(timestamp, ex.dur));
+                if (ex.root) notify_queue.push_back(zne(timestamp, ex.dur));
             }
-            ex.start_time_of_aggs = start_time_of(timestamp, ex.dur);
+            ex.start_time_of_aggs = zst(timestamp, ex.dur);
             if (timestamp >= ex.next_emit_time) {
-                ex.next_emit_time = next_emit_of(timestamp, ex.dur);
+                ex.next_emit_time = zne(timestamp, ex.dur);
                 dispatch(ex, ex.start_time_of_aggs);
                 // sendTimerEvent (:141-150)
                 if (ex.next) {
@@ -1172,7 +1182,7 @@ struct AggRuntime {
     void process_aggregates(IncExec& ex, const InRow& r) {
         GKey key;
         int off = 0;
-        if (d.ts_col >= 0) key.k[off++] = start_time_of(r.ext, ex.dur);  // getAggregationStartTime
+        if (d.ts_col >= 0) key.k[off++] = zst(r.ext, ex.dur);  // getAggregationStartTime
         for (int g = 0; g < d.n_group_by; g++) key.k[off + g] = r.keys[g];
         auto it = ex.store.find(key);
         if (it == ex.store.end()) {
@@ -1271,7 +1281,7 @@ struct AggRuntime {
             IncExec& ex = *execs[k];
             for (const GKey& key : ex.order) {
                 const BaseRow& br = ex.store[key];
-                const int64_t b = start_time_of(d.ts_col >= 0 ? br.ext : ex.store_ts, per);
+                const int64_t b = zst(d.ts_col >= 0 ? br.ext : ex.store_ts, per);
                 GK g(b, d.n_group_by > 0 ? br.keys[0] : 0);
                 auto it = mem.find(g);
                 if (it == mem.end()) it = mem.emplace(g, new_acc()).first;

@@ -60,7 +60,8 @@ class AggregationDesc(C.Structure):
                 ("n_filter_ops", C.c_int32), ("filter", C.POINTER(FilterOp)),
                 ("n_group_by", C.c_int32), ("group_by", C.c_int32 * MAX_GROUP),
                 ("n_aggs", C.c_int32), ("aggs", AggSpec * MAX_AGGS), ("ts_col", C.c_int32),
-                ("min_duration", C.c_int32), ("max_duration", C.c_int32), ("key_capacity", C.c_int64)]
+                ("min_duration", C.c_int32), ("max_duration", C.c_int32), ("key_capacity", C.c_int64),
+                ("tz_offset_ms", C.c_int64)]
 
 
 class Batch(C.Structure):
@@ -224,6 +225,7 @@ class AggregationSpec:
     durations: tuple = ("sec", "day")
     filter: object = None
     key_capacity: int = 0
+    tz_offset_ms: int = 0  # aggTimeZone as a fixed offset from GMT (Asia/Singapore: 8 * 3600_000)
     _keep: list = field(default_factory=list, repr=False)
 
     def desc(self) -> AggregationDesc:
@@ -247,6 +249,7 @@ class AggregationSpec:
         d.min_duration = DUR_NAMES[self.durations[0]]
         d.max_duration = DUR_NAMES[self.durations[1]]
         d.key_capacity = self.key_capacity
+        d.tz_offset_ms = self.tz_offset_ms
         return d
 
     def base_names(self) -> List[str]:

@@ -24,7 +24,7 @@ struct LevelDev {
 
 void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
                         const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
-                        int* dup_dev);
+                        int* dup_dev, i64 tz);
 // rows appended to a duration table: bucket, key and every base column in one launch
 void launch_table_append(hipStream_t s, i64 n, const i64* bucket, const i64* key, const u64* vals, i64 vstride,
                          int nb, i64* t_bucket, i64* t_key, u64* t_vals, i64 t_cap);
@@ -34,7 +34,7 @@ void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket
                           int nblk, i64 cap, i64* out_bucket, i64* out_key, u64* out_vals, bool clear = true);
 // retrieval (sh_aggregation_find)
 void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i64 start, i64 end, i64* bucket_out,
-                          u32* idx);
+                          u32* idx, i64 tz);
 void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst);
 void launch_find_starts(hipStream_t s, i64 n, const u32* idx, const i64* bucket, const i64* key, u32* flag);
 void launch_find_fold(hipStream_t s, i64 n, const u32* idx, const u32* flag, const u32* pre, const i64* bucket,

@@ -38,7 +38,7 @@ __device__ __forceinline__ void civil_from_days_d(i64 z, i64& y, unsigned& m, un
 }
 
 // getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69); sec/min use `t - t % d`
-__device__ __forceinline__ i64 start_of_dev(i64 t, int dur) {
+__device__ __forceinline__ i64 start_of_gmt(i64 t, int dur) {
     switch (dur) {
         case SH_DUR_SECONDS: return t - t % 1000;
         case SH_DUR_MINUTES: return t - t % 60000;
@@ -54,6 +54,11 @@ __device__ __forceinline__ i64 start_of_dev(i64 t, int dur) {
     }
 }
 
+// in the aggregation's time zone (a fixed offset): hours and longer start at the zone's local boundaries
+__device__ __forceinline__ i64 start_of_dev(i64 t, int dur, i64 tz) {
+    return dur >= SH_DUR_HOURS ? start_of_gmt(t + tz, dur) - tz : start_of_gmt(t, dur);
+}
+
 __device__ __forceinline__ u64 level_key(int has_bucket, i64 bucket, i64 key) {
     if (!has_bucket) return (u64)key;
     return ((u64)(u32)(bucket / 1000) << 32) | (u64)(u32)key;
@@ -63,10 +68,10 @@ __device__ __forceinline__ u64 level_key(int has_bucket, i64 bucket, i64 key) {
 // dispatch so extraction can restore insertion order (the oracle's store order)
 __global__ __launch_bounds__(kBlock) void k_level_lookup(i64 n, const i64* __restrict__ bucket_in,
                                                         const i64* __restrict__ key_in, int has_bucket, int dur,
-                                                        LevelDev L, u32 epoch, u32 seq0, u32* slot_out, int* dup) {
+                                                        LevelDev L, u32 epoch, u32 seq0, u32* slot_out, int* dup, i64 tz) {
     i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    i64 cb = has_bucket ? start_of_dev(bucket_in[i], dur) : 0;
+    i64 cb = has_bucket ? start_of_dev(bucket_in[i], dur, tz) : 0;
     u32 pos = key_slot(L.kt, level_key(has_bucket, cb, key_in ? key_in[i] : 0));
     slot_out[i] = pos;
     atomicMin(&L.first_seq[pos], seq0 + (u32)i);
@@ -117,11 +122,11 @@ __global__ __launch_bounds__(kBlock) void k_level_fold(i64 n, const u32* __restr
 
 void launch_level_merge(hipStream_t s, i64 n, const i64* bucket_in, const i64* key_in, int has_bucket, int dur,
                         const u64* vin, i64 stride, LevelDev L, BasePlan bp, u32 epoch, u32 seq0, u32* slots,
-                        int* dup_dev) {
+                        int* dup_dev, i64 tz) {
     if (n == 0) return;
     unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_level_lookup, dim3(g), dim3(kBlock), 0, s, n, bucket_in, key_in, has_bucket, dur, L, epoch,
-                       seq0, slots, dup_dev);
+                       seq0, slots, dup_dev, tz);
     hipLaunchKernelGGL(k_level_fold, dim3(g), dim3(kBlock), 0, s, n, slots, vin, stride, L, bp, dup_dev, epoch);
 }
 
@@ -217,10 +222,10 @@ void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket
 // ---- retrieval (sh_aggregation_find) ---------------------------------------------------------------
 // rows re-bucketed to the `per` duration; rows outside [start, end) get bucket -1 (sorted last, dropped)
 __global__ __launch_bounds__(kBlock) void k_find_rebucket(i64 n, const i64* __restrict__ bucket_in, int per, i64 start,
-                                                         i64 end, i64* bucket_out, u32* idx) {
+                                                         i64 end, i64* bucket_out, u32* idx, i64 tz) {
     const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    const i64 b = start_of_dev(bucket_in[i], per);
+    const i64 b = start_of_dev(bucket_in[i], per, tz);
     bucket_out[i] = (b >= start && b < end) ? b : -1;
     idx[i] = (u32)i;
 }
@@ -288,10 +293,10 @@ __global__ __launch_bounds__(kBlock) void k_find_fold(i64 n, const u32* __restri
 }
 
 void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i64 start, i64 end, i64* bucket_out,
-                          u32* idx) {
+                          u32* idx, i64 tz) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_find_rebucket, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, bucket_in,
-                       per, start, end, bucket_out, idx);
+                       per, start, end, bucket_out, idx, tz);
 }
 
 void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst) {

@@ -116,6 +116,14 @@ static int64_t h_next_emit(int64_t t, int dur) {
     }
 }
 
+// ... in the aggregation's time zone, a fixed offset tz from GMT: hours and longer at local boundaries
+static int64_t h_start_of(int64_t t, int dur, int64_t tz) {
+    return dur >= SH_DUR_HOURS ? h_start_of(t + tz, dur) - tz : h_start_of(t, dur);
+}
+static int64_t h_next_emit(int64_t t, int dur, int64_t tz) {
+    return dur >= SH_DUR_HOURS ? h_next_emit(t + tz, dur) - tz : h_next_emit(t, dur);
+}
+
 // A batch of rows on the device: bucket / key / base values (stride = cap).
 struct RowBatch {
     int64_t n = 0, cap = 0;
@@ -154,6 +162,8 @@ struct sh_aggregation {
     int nb = 0;
     bool has_bucket = false;
     int64_t T_root = 0;
+    int64_t tz = 0;       // aggTimeZone as a fixed offset (ms)
+    int64_t tz_root = 0;  // the root's bucket offset: tz for hour / day roots (sec / min are zone-free)
     sh_query* root = nullptr;
     sh_shard* shard = nullptr;  // sharded: the root is this shard's owner query (owned by the shard)
     bool root_init = false;
@@ -312,9 +322,9 @@ static int level_dispatch(sh_aggregation* a, size_t li, int64_t start_of_new) {
 // IncrementalExecutor.execute for a chunk of rows that share AGG_TIMESTAMP `ts` (:110-139)
 static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t ts) {
     Level& L = a->levels[li];
-    L.start = h_start_of(ts, L.dur);
+    L.start = h_start_of(ts, L.dur, a->tz);
     if (ts >= L.next_emit) {
-        L.next_emit = h_next_emit(ts, L.dur);
+        L.next_emit = h_next_emit(ts, L.dur, a->tz);
         RCHK(level_dispatch(a, li, L.start));
         if (li + 1 < a->levels.size()) RCHK(level_timer(a, li + 1, L.start));
     }
@@ -325,7 +335,7 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
         L.epoch++;
         if (L.n_in + rb.n >= (int64_t)0xFFFFFFF0ll) return sh_fail(SH_ERR_INVALID, "too many rows in one roll-up bucket");
         launch_level_merge(s, rb.n, rb.bucket, rb.key, a->has_bucket, L.dur, rb.vals, rb.cap, level_dev(L, a->nb),
-                           a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>());
+                           a->bp, L.epoch, (u32)L.n_in, L.slots.as<u32>(), L.dup.as<int>(), a->tz);
         L.n_in += rb.n;
         HIPCHK(hipGetLastError());
         L.dirty = true;  // its key-table counters are fetched once per push (agg_after_root)
@@ -352,7 +362,7 @@ static int level_timer_run(sh_aggregation* a, size_t li, int64_t first, int64_t 
             // timers below nextEmitTime only refresh startTimeOfAggregates
             int64_t k = (L.next_emit - first + step - 1) / step;
             if (k >= count) {
-                L.start = h_start_of(first + (count - 1) * step, L.dur);
+                L.start = h_start_of(first + (count - 1) * step, L.dur, a->tz);
                 return SH_OK;
             }
             first += k * step;
@@ -427,7 +437,7 @@ static int catch_up(sh_aggregation* a) {
         a->root_bucket = q->E0 - T;
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
-    int64_t cb = h_floor_div(q->clock, T) * T;
+    int64_t cb = h_floor_div(q->clock + a->tz_root, T) * T - a->tz_root;
     if (cb > a->root_bucket && !a->levels.empty())
         RCHK(level_timer_run(a, 0, a->root_bucket + T, T, (cb - a->root_bucket) / T));
     a->root_bucket = std::max(a->root_bucket, cb);
@@ -452,6 +462,12 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     a->has_bucket = d->ts_col >= 0;
     static const int64_t unit[] = {1000, 60000, 3600000, 86400000};
     a->T_root = unit[d->min_duration];
+    if (d->tz_offset_ms % 60000 != 0 || d->tz_offset_ms <= -86400000 || d->tz_offset_ms >= 86400000) {
+        delete a;
+        return sh_fail(SH_ERR_INVALID, "aggTimeZone offset must be whole minutes within a day");
+    }
+    a->tz = d->tz_offset_ms;
+    a->tz_root = d->min_duration >= SH_DUR_HOURS ? a->tz : 0;
     // base values, de-duplicated like AggregationParser.populateFinalBaseAggregators
     struct B { int kind; int col; };
     std::vector<B> bases;
@@ -477,7 +493,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     rd.window = SH_WIN_TIME_BATCH;
     rd.window_param = a->T_root;
     rd.has_start_time = 1;
-    rd.start_time = 0;
+    rd.start_time = -a->tz_root;  // (hour / day roots close at the zone's local boundaries)
     rd.current_on = 1;
     rd.partition_col = -1;
     rd.n_aggs = (int)bases.size();
@@ -489,7 +505,9 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     rd.key_capacity = d->key_capacity > 0 ? d->key_capacity : (1 << 16);
     KeyPlan kp{};
     int g = 0;
-    if (a->has_bucket) { kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->T_root; g++; }
+    if (a->has_bucket) {
+        kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->T_root; kp.add[g] = a->tz_root; g++;
+    }
     if (d->n_group_by == 1) {
         int c = d->group_by[0];
         int t = d->col_types[c];
@@ -693,7 +711,7 @@ static int spec_push(sh_aggregation* a, const sh_batch* dev, const sh_out** o, i
         b0 = plo;
     } else {
         if (q->clock < 0) return SH_OK;
-        b0 = q->clock / a->T_root;
+        b0 = (q->clock + a->tz_root) / a->T_root;
     }
     if (b0 != q->kt.band_base) {
         RCHK(a->band_spare.init_band(a->band_lk, a->band_rows, b0, a->band_mul, a->band_add));
@@ -754,7 +772,7 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side) {
         if (side) HIPCHK(sh_wait_stream(s));
         else RCHK(agg_sync(a));
         // the key's bucket component: ts / T truncated (sh_device.h key_part)
-        const int64_t lo = a->h_minmax[0] / a->T_root, hi = a->h_minmax[1] / a->T_root;
+        const int64_t lo = (a->h_minmax[0] + a->tz_root) / a->T_root, hi = (a->h_minmax[1] + a->tz_root) / a->T_root;
         int64_t nb = hi - lo + 1;
         bound = (nb > 0 && keys <= N / nb) ? keys * nb : N;
         if (a->band_ok) return band_reserve(a, lo, hi, bound);
@@ -975,7 +993,7 @@ static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* k
     RCHK(a->g_flag.reserve((n + 1) * 4, false));
     RCHK(a->g_pre.reserve((n + 1) * 4, false));
     RCHK(a->g_tmp.reserve((size_t)((n + 1 + kTile - 1) / kTile + 16) * 8, false));
-    launch_find_rebucket(s, n, bucket, per, start, end, a->g_bucket.as<int64_t>(), a->g_idx.as<u32>());
+    launch_find_rebucket(s, n, bucket, per, start, end, a->g_bucket.as<int64_t>(), a->g_idx.as<u32>(), a->tz);
     // (bucket, key) order, input order within a group: stable LSD sorts by key, then by bucket
     size_t tb = 0;
     if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, s)) return sh_fail(SH_ERR_DEVICE, "sort sizing");

@@ -235,7 +235,7 @@ __device__ __forceinline__ i64 key_part(const KeyPlan& kp, const ColSet& cs, int
     const int t = kp.type[g];
     if (t == SH_T_FLOAT || t == SH_T_DOUBLE) return __longlong_as_double(v) != __longlong_as_double(v) ? 0x7FF8000000000000ll : v;
     // aggregation time bucket: getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69)
-    if (kp.div[g] > 0) v = v / kp.div[g];
+    if (kp.div[g] > 0) v = (v + kp.add[g]) / kp.div[g];
     return v;
 }
 
@@ -258,11 +258,11 @@ __device__ __forceinline__ u64 make_key(const KeyPlan& kp, const ColSet& cs, i64
 // a component as sh_out reports it: int64 widening; floats as the bits of the value widened to double
 __device__ __forceinline__ i64 unpack_part(const KeyPlan& kp, int g, u32 x) {
     if (kp.type[g] == SH_T_FLOAT) return __double_as_longlong((double)__uint_as_float(x));
-    return kp.div[g] > 0 ? (i64)x * kp.div[g] : (i64)(int)x;
+    return kp.div[g] > 0 ? (i64)x * kp.div[g] - kp.add[g] : (i64)(int)x;
 }
 
 __device__ __forceinline__ void unpack_key(const KeyPlan& kp, u64 key, i64* out, i64 stride) {
-    if (kp.n == 1) out[0] = kp.div[0] > 0 ? (i64)key * kp.div[0] : (i64)key;
+    if (kp.n == 1) out[0] = kp.div[0] > 0 ? (i64)key * kp.div[0] - kp.add[0] : (i64)key;
     else if (kp.n == 2) {
         out[0] = unpack_part(kp, 0, (u32)(key >> 32));
         out[stride] = unpack_part(kp, 1, (u32)key);

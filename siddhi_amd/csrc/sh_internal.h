@@ -91,7 +91,8 @@ struct KeyPlan {
     int col[SH_MAX_GROUP];
     int type[SH_MAX_GROUP];
     int dense;  // one STRID column: dictionary ids are dense in [0, key_capacity) -> slot = id
-    i64 div[SH_MAX_GROUP];  // > 0: the component is (u32)(value / div) (aggregation time buckets)
+    i64 div[SH_MAX_GROUP];  // > 0: the component is (u32)((value + add) / div) (aggregation time buckets)
+    i64 add[SH_MAX_GROUP];  // (the aggregation time zone's offset for hour / day buckets)
 };
 
 // Hash table (key -> position = group slot). positions [0, mask] plus the reserved mask+1

@@ -176,6 +176,134 @@ static int sched_register(sh_query* q, uint32_t slot, int64_t t, const std::vect
     return SH_OK;
 }
 
+// Scheduler.onTimeChange at one call (clock c) whose TIMER events act on the window at once
+// (sendTimerEvents :171-209 runs the window, which may notifyAt again, before returnAllStates): per
+// distinct due time the first state met in HashMap order fires all its due times, each TIMER handed to
+// on_timer(slot, due time) in queue order.
+template <typename F>
+static int sched_fire(SlidingImpl* s, int64_t c, F on_timer) {
+    std::vector<std::pair<int64_t, uint32_t>> win;
+    int64_t best = 0;
+    for (auto it = s->pl_armed.begin(); it != s->pl_armed.end() && it->first <= c; ++it) {
+        int64_t r = 0;
+        s->pl_states.rank(s->pl_flow[it->second], &r);
+        if (win.empty() || win.back().first != it->first) {
+            win.push_back(*it);
+            best = r;
+        } else if (r < best) {
+            win.back() = *it;
+            best = r;
+        }
+    }
+    std::vector<std::pair<int64_t, uint32_t>> gone;
+    for (auto& w : win) {
+        s->pl_armed.erase(w);
+        const uint32_t slot = w.second;
+        for (;;) {
+            auto it = s->pl_pend.find(slot);
+            if (it == s->pl_pend.end() || it->second.empty() || it->second.front() > c) break;
+            const int64_t t = it->second.front();
+            it->second.pop_front();
+            RCHK(on_timer(slot, t));
+        }
+        auto it = s->pl_pend.find(slot);
+        if (it == s->pl_pend.end() || it->second.empty()) {
+            if (it != s->pl_pend.end()) s->pl_pend.erase(it);
+            int64_t r = 0;
+            s->pl_states.rank(s->pl_flow[slot], &r);
+            gone.emplace_back(r, slot);
+        } else {
+            s->pl_armed.insert(std::make_pair(it->second.front(), slot));
+        }
+    }
+    std::sort(gone.begin(), gone.end());
+    for (auto& g : gone) s->pl_states.erase(s->pl_flow[g.second]);
+    return SH_OK;
+}
+
+// externalTimeBatch(ts, T, start, timeout) under `partition with`: ExternalTimeBatchWindowProcessor.process
+// (:238-311) per partition, walked in stream order over the push's calls (each a Scheduler.onTimeChange
+// before its send's events) and passing events (flag bit 1: initTiming :313-334, bit 0: the event crosses
+// into a new batch). Every emission — a TIMER's flushToOutputChunk / appendToOutputChunk (:256-275) or a
+// crossing's (:292-305) — sends the open batch from its first record, behind the previous emission's
+// records as EXPIRED (the expired chunk always holds what the previous emission sent as CURRENT).
+static int xt_walk(sh_query* q, const std::vector<int64_t>& calls_s, const std::vector<int64_t>& calls_c,
+                   const std::vector<uint32_t>& ev_slot, const std::vector<unsigned char>& ev_flag,
+                   const std::vector<uint32_t>& ev_raw, int64_t ss, int64_t clock0,
+                   const std::vector<int64_t>& slot_key, std::vector<PgXtEmit>& em, std::vector<uint32_t>& touched) {
+    SlidingImpl* s = q->sl;
+    const int64_t tau = q->xt_timeout;
+    const bool exp_on = q->d.expired_on != 0;
+    std::unordered_map<uint32_t, char> seen;
+    auto touch = [&](uint32_t p) { if (seen.emplace(p, 1).second) touched.push_back(p); };
+    auto emit = [&](uint32_t p, SlidingImpl::XtPart& P, int64_t hi, int64_t clock, int64_t sidx) {
+        PgXtEmit e{};
+        e.p = p;
+        e.lo = P.bs;
+        e.hi = hi;
+        e.xlo = exp_on ? P.pe_lo : 0;
+        e.xhi = exp_on ? P.pe_hi : 0;
+        e.clock = clock;
+        e.sidx = sidx;
+        em.push_back(e);
+        P.pe_lo = P.bs;
+        P.pe_hi = hi;
+    };
+    int64_t clock = clock0;
+    auto on_timer = [&](uint32_t p, int64_t t) -> int {
+        auto it = s->xt_parts.find(p);
+        if (it == s->xt_parts.end()) return sh_fail(SH_ERR_STATE, "externalTimeBatch timeout: a timer without window state");
+        SlidingImpl::XtPart& P = it->second;
+        if (P.L > t) return SH_OK;  // (rescheduled since: :258)
+        touch(p);
+        if (!P.flushed) {
+            if (P.n > P.bs) emit(p, P, P.n, clock, P.n - 1);
+            P.flushed = true;
+        } else if (P.n > P.cur0) {
+            emit(p, P, P.n, clock, P.n - 1);
+        }
+        P.cur0 = P.n;
+        P.L = clock + tau;
+        return sched_register(q, p, P.L, slot_key);
+    };
+    size_t e = 0;
+    auto events_before = [&](int64_t send_end) -> int {  // the passing events of the sends before send_end
+        for (; e < ev_slot.size(); e++) {
+            const int64_t snd = ss > 0 ? (int64_t)ev_raw[e] / ss : 0;
+            if (snd >= send_end) break;
+            const uint32_t p = ev_slot[e];
+            const unsigned char f = ev_flag[e];
+            touch(p);
+            SlidingImpl::XtPart& P = s->xt_parts[p];
+            if (f & 2) {
+                P = SlidingImpl::XtPart{};
+                P.L = clock + tau;
+                RCHK(sched_register(q, p, P.L, slot_key));
+            }
+            if (f & 1) {
+                if (P.flushed) {
+                    if (P.n > P.cur0) emit(p, P, P.n, clock, P.n);
+                    P.flushed = false;
+                } else if (P.n > P.bs) {
+                    emit(p, P, P.n, clock, P.n);
+                }
+                P.bs = P.n;
+                P.cur0 = P.n;
+                P.L = clock + tau;
+                RCHK(sched_register(q, p, P.L, slot_key));
+            }
+            P.n++;
+        }
+        return SH_OK;
+    };
+    for (size_t k = 0; k < calls_s.size(); k++) {
+        RCHK(events_before(calls_s[k]));
+        clock = calls_c[k];
+        if (!s->pl_armed.empty() && s->pl_armed.begin()->first <= clock) RCHK(sched_fire(s, clock, on_timer));
+    }
+    return events_before(INT64_MAX);
+}
+
 // bits needed for values < n
 static int bits_for(int64_t n) {
     int b = 1;
@@ -197,6 +325,8 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         RCHK(nb.vals.reserve((size_t)V * cap * 8, false));
         RCHK(nb.prev.reserve(cap, false));
         RCHK(nb.x.reserve(cap * 8, false));
+        RCHK(nb.xe.reserve(cap * 8, false));
+        RCHK(nb.xm.reserve(cap * 8, false));
         nb.cap = cap;
         to = std::move(nb);
     }
@@ -208,6 +338,8 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         HIPCHK(hipMemcpyAsync(to.clk.p, from.clk.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.prev.p, from.prev.p, keep, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.x.p, from.x.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.xe.p, from.xe.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(to.xm.p, from.xm.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpy2DAsync(to.vals.p, to.cap * 8, from.vals.p, from.cap * 8, keep * 8, V, hipMemcpyDeviceToDevice, st));
     }
     return SH_OK;
@@ -217,15 +349,24 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
 // externalTimeBatch, by sorting (sh_plane_group_kernels.hip). The records carried from earlier pushes
 // (every partition's open batch and, with expired output, its last completed batch) precede the push's
 // own in one combined array.
-static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+// b == null: a TIMER call at `now` (sh_advance_time; only the externalTimeBatch timeout acts on it)
+static int plane_run_group(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
-    const int64_t N = b->n, ss = b->send_size, L = q->d.window_param;
+    const int64_t N = b ? b->n : 0, ss = b ? b->send_size : 0, L = q->d.window_param;
     const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
     const bool ext = q->d.window == SH_WIN_EXT_TIME_BATCH;
+    const bool xt = ext && q->xt_timeout > 0;  // (the Scheduler decides when batches go out: xt_walk)
     const bool sc = q->d.stream_current != 0;  // lengthBatch(L, true), current output (k_pg_sc_*)
     if (N >= (int64_t)0x3FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 1G events");
+    if (!b && !xt) {
+        if (!q->clock_valid || now >= q->clock) {
+            q->clock = now;
+            q->clock_valid = true;
+        }
+        return empty_out(q, out);
+    }
     HIPCHK(hipEventRecord(q->ev_push0, st));
     const int64_t cap = std::max<int64_t>(N, 1);
     RCHK(s->rec_raw.reserve(cap * 4, false));
@@ -244,7 +385,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                   s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
     ColSet cs{};
     cs.n = q->d.n_cols;
-    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b ? b->cols[c] : nullptr; }
     const int nblk = (int)((N + kTile - 1) / kTile);
     RCHK(s->blk_pass.reserve(nblk * 8, false));
     RCHK(s->blk_tl.reserve(nblk * 8, false));
@@ -256,22 +397,57 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
     wp.send_size = ss;
     wp.N = N;
     wp.rec_seq = q->tune.sl_records_seq;  // (the lane-strided records where they apply, as the sliding path)
-    launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
-                     s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
-    // lane-strided records (every event passes): no per-slot counts; the partitions' offsets come from
-    // the sorted slots below (k_counts_sorted; the LDS tables and atomics were 5.2 of plb's 20 ms)
-    const bool sorted_off = sl_records_seq_applies(q->fp, wp, q->ap);
-    launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
-                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
-                      sorted_off ? nullptr : s->slot_cnt.as<u32>(), nblk);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    RCHK(q->kt.check(st));
-    const SlInfo info = *s->h_info;
+    const bool sorted_off = b && sl_records_seq_applies(q->fp, wp, q->ap);
+    SlInfo info{};
+    if (b) {
+        launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                         s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+        // lane-strided records (every event passes): no per-slot counts; the partitions' offsets come from
+        // the sorted slots below (k_counts_sorted; the LDS tables and atomics were 5.2 of plb's 20 ms)
+        launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                          s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec,
+                          sorted_off ? nullptr : s->slot_cnt.as<u32>(), nblk);
+        if (xt) launch_pl_slot_key(st, cs, q->kp, q->kt.dev(), N, s->pl_key.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        RCHK(q->kt.check(st));
+        info = *s->h_info;
+    }
     const int64_t M = info.total_pass, n_old = s->pg_n, n = n_old + M;
     int64_t n_rows = 0, n_flushes = 0;
-    if (M > 0) {
+    // the timeout: the push's calls (a send whose last event does not move the clock calls nobody,
+    // TimestampGeneratorImpl :104-122), or the advance_time call
+    std::vector<int64_t> calls_s, calls_c;
+    bool xt_fire = false;
+    if (xt) {
+        if (b) {
+            const int64_t NS = ss > 0 ? (N + ss - 1) / ss : 1;
+            const int nbS = (int)((NS + kTile - 1) / kTile);
+            RCHK(s->x_sK.reserve(NS * 8, false));
+            RCHK(s->x_scb.reserve(NS * 8, false));
+            RCHK(s->x_slast.reserve(NS * 8, false));
+            RCHK(s->x_cK.reserve(NS * 8, false));
+            RCHK(s->x_cC.reserve(NS * 8, false));
+            RCHK(s->x_cS.reserve(NS * 8, false));
+            RCHK(s->x_blk.reserve((size_t)((NS + kTile - 1) / kTile + 2) * 8, false));
+            launch_slx_sends(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), nblk,
+                             s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>());
+            launch_slx_compact(st, 0, nullptr, s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>(),
+                               NS, s->x_blk.as<int64_t>(), s->x_cK.as<int64_t>(), s->x_cC.as<int64_t>(),
+                               s->x_cS.as<int64_t>());
+            HIPCHK(hipGetLastError());
+            int64_t nC = 0;
+            RCHK(read_count(q, s->x_blk.as<int64_t>() + nbS, &nC));
+            RCHK(d2h(q, calls_s, s->x_cS.p, nC));
+            RCHK(d2h(q, calls_c, s->x_cC.p, nC));
+        } else if (!q->clock_valid || now >= q->clock) {
+            calls_s.push_back(0);
+            calls_c.push_back(now);
+        }
+        xt_fire = !s->pl_armed.empty() && !calls_c.empty() && calls_c.back() >= s->pl_armed.begin()->first;
+    }
+    if (M > 0 || (xt_fire && n_old > 0)) {
         if (n >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "partition lanes: more than 2G carried + new events");
         // ---- combined records: carried, then the push's
         if (s->pg[0].cap < n) {
@@ -333,11 +509,18 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             if (launch_pg_ext_scan(st, s->ranks.as<u32>(), s->p_slot.as<u32>(), C, n, s->pg_xv.as<int64_t>(),
                                    s->pg_ms.as<int64_t>(), s->sort_tmp.p, &tb))
                 return sh_fail(SH_ERR_DEVICE, "scan failed");
-            launch_pg_assign_ext(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
-                                 s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, n,
-                                 q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(), s->pg_eval.as<u32>(),
-                                 s->pg_keep.as<unsigned char>(), s->pg_cnt.as<unsigned long long>(), s->pg_cts.as<int64_t>(),
-                                 s->pg_err.as<int>());
+            if (xt) {
+                RCHK(s->xt_flag.reserve(n + 16, false));
+                launch_pg_xt_flags(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
+                                   s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, n,
+                                   s->xt_flag.as<unsigned char>(), s->pg_err.as<int>());
+            } else {
+                launch_pg_assign_ext(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
+                                     s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, n,
+                                     q->d.current_on, q->d.expired_on, gbits, none, s->pg_ekey.as<u64>(),
+                                     s->pg_eval.as<u32>(), s->pg_keep.as<unsigned char>(),
+                                     s->pg_cnt.as<unsigned long long>(), s->pg_cts.as<int64_t>(), s->pg_err.as<int>());
+            }
             launch_pg_ext_state(st, s->key_off.as<u32>(), s->ranks.as<u32>(), s->pg_prevcnt.as<u32>(),
                                 s->pg_pendcnt.as<u32>(), C, s->pg_xs.as<int64_t>(), s->pg_ms.as<int64_t>(), X, s->nslots);
         } else if (sc) {
@@ -358,16 +541,64 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                                                    "(not on the GPU)");
         }
         int64_t n_e = n;  // (stream.current: one entry per event)
-        if (!sc) RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
+        std::vector<PgXtEmit> em;
+        std::vector<uint32_t> touched;
+        if (xt) {
+            // ---- the Scheduler walk over the push's calls and passing events (host), then the
+            // emissions' entries (device)
+            std::vector<uint32_t> ev_slot((size_t)M), ev_raw((size_t)M);
+            std::vector<unsigned char> ev_flag((size_t)M);
+            if (M > 0) {
+                HIPCHK(hipMemcpyAsync(ev_slot.data(), C.ps + n_old, M * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(ev_raw.data(), rec.raw, M * 4, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(ev_flag.data(), s->xt_flag.as<unsigned char>() + n_old, M, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+            }
+            std::vector<int64_t> slot_key;
+            bool fresh = false;
+            for (unsigned char f : ev_flag) fresh |= (f & 2) != 0;
+            if (fresh || xt_fire) RCHK(d2h(q, slot_key, s->pl_key.p, s->nslots));
+            RCHK(xt_walk(q, calls_s, calls_c, ev_slot, ev_flag, ev_raw, ss, q->clock_valid ? q->clock : INT64_MIN,
+                         slot_key, em, touched));
+            int64_t tot = 0;
+            for (auto& e : em) {
+                e.off = tot;
+                tot += (q->d.expired_on ? e.xhi - e.xlo : 0) + (q->d.current_on ? e.hi - e.lo : 0);
+                if (!q->d.current_on) e.hi = e.lo;  // (expired rows only: no CURRENT entries)
+            }
+            n_e = tot;
+            const int ebits_x = gbits + bits_for((int64_t)em.size() + 1);
+            if (ebits_x > 64) return sh_fail(SH_ERR_UNSUPPORTED, "partition lanes: entry key wider than 64 bits");
+            if (n_e > 0) {
+                if (n_e >= (int64_t)0x7FFFFFF0ll) return sh_fail(SH_ERR_UNSUPPORTED, "partition lanes: more than 2G entries");
+                RCHK(s->pg_ekey.reserve(n_e * 8, false));
+                RCHK(s->pg_ekey2.reserve(n_e * 8, false));
+                RCHK(s->pg_eval.reserve(n_e * 4, false));
+                RCHK(s->pg_eval2.reserve(n_e * 4, false));
+                RCHK(s->xt_epos.reserve(n_e * 4, false));
+                RCHK(s->xt_up.reserve(em.size() * sizeof(PgXtEmit), false));
+                RCHK(s->xt_em.reserve(em.size() * sizeof(PgXtEmit), false));
+                HIPCHK(hipMemcpyAsync(s->xt_em.p, em.data(), em.size() * sizeof(PgXtEmit), hipMemcpyHostToDevice, st));
+                launch_pg_xt_expand(st, s->xt_em.as<PgXtEmit>(), (int64_t)em.size(), n_e, s->key_off.as<u32>(),
+                                    s->ranks.as<u32>(), C, gbits, q->d.current_on, q->d.expired_on, s->pg_ekey.as<u64>(),
+                                    s->pg_eval.as<u32>(), s->xt_epos.as<u32>());
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamSynchronize(st));  // (em is pageable)
+            }
+        } else if (!sc) {
+            RCHK(read_count(q, s->pg_cnt.as<int64_t>(), &n_e));
+        }
         if (n_e > 0) {
             tb = 0;
-            const int64_t ne_sort = q->d.expired_on ? ne_cap : n;  // (current only: one entry per event)
+            // (current only: one entry per event; the timeout's entries are exactly n_e)
+            const int64_t ne_sort = xt ? n_e : q->d.expired_on ? ne_cap : n;
+            const unsigned sbits = xt ? (unsigned)(gbits + bits_for((int64_t)em.size() + 1)) : ebits;
             if (sort_u64_pairs_bits(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_sort,
-                                    ebits, st))
+                                    sbits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
             RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
             if (sort_u64_pairs_bits(s->sort_tmp.p, &tb, s->pg_ekey.as<u64>(), s->pg_ekey2.as<u64>(), s->pg_eval.as<u32>(),
-                                    s->pg_eval2.as<u32>(), ne_sort, ebits, st))
+                                    s->pg_eval2.as<u32>(), ne_sort, sbits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort failed");
             // ---- segments = rows
             RCHK(s->pg_head.reserve(n_e + 16, false));
@@ -397,6 +628,12 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
                          s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
                          s->xr_nulls.as<unsigned char>(), rc};
+            const bool xa = ext && q->xt_replace;  // (the rows' batch ends: sh_query_rep_ts_attr)
+            if (xa) {
+                RCHK(s->xr_xa.reserve(rc * 8, false));
+                RCHK(s->out_xa.reserve(rc * 8, false));
+                rows.xa = s->xr_xa.as<int64_t>();
+            }
             HIPCHK(hipEventRecord(q->ev_agg0, st));
             if (sc) {
                 launch_pg_sc_fold(st, s->pg_seg.as<int64_t>(), n_seg, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
@@ -405,10 +642,11 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
             } else {
                 launch_pg_fold(st, s->pg_seg.as<int64_t>(), n_rows, n_e, s->pg_ekey2.as<u64>(), s->pg_eval2.as<u32>(),
                                s->ranks.as<u32>(), C, q->ap, gbits, rows, s->pg_rkey.as<u64>(), s->pg_rpart.as<u32>(),
-                               ext ? s->pg_cts.as<int64_t>() : nullptr);
+                               ext ? s->pg_cts.as<int64_t>() : nullptr, xt ? s->xt_em.as<PgXtEmit>() : nullptr,
+                               xt ? s->xt_epos.as<u32>() : nullptr, s->key_off.as<u32>());
                 HIPCHK(hipEventRecord(q->ev_agg1, st));
                 // ---- rows in (chunk, first entry) order
-                const unsigned rbits = (unsigned)(32 + cbits);
+                const unsigned rbits = (unsigned)(32 + (xt ? bits_for((int64_t)em.size() + 1) : cbits));
                 tb = 0;
                 if (sort_u64_iota_bits(nullptr, &tb, s->pg_rkey.as<u64>(), nullptr, nullptr, n_rows, rbits, st))
                     return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
@@ -429,7 +667,7 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
                            s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
                            s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(),
                            s->out_send.as<int64_t>(), s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(),
-                           s->pg_rpart.as<u32>(), s->out_part.as<u32>());
+                           s->pg_rpart.as<u32>(), s->out_part.as<u32>(), xa ? s->out_xa.as<int64_t>() : nullptr);
             HIPCHK(hipGetLastError());
             float kms = 0;
             (void)hipEventSynchronize(q->ev_agg1);
@@ -438,6 +676,40 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
         }
         // one flush per chunk (out_send = the completing event's stream index)
         RCHK(sliding_flushes(q, n_rows, &n_flushes));
+        if (xt) {
+            // ---- what each partition keeps: its open batch, and with expired output the previous
+            // emission's records (they go out again as EXPIRED); the walk's indices then start there
+            const bool exp_on = q->d.expired_on != 0;
+            std::vector<uint32_t> kslot, kval;
+            for (uint32_t p : touched) {
+                SlidingImpl::XtPart& P = s->xt_parts[p];
+                const int64_t kf = exp_on && P.pe_hi > P.pe_lo ? std::min(P.pe_lo, P.bs) : P.bs;
+                if (kf <= 0) continue;
+                kslot.push_back(p);
+                kval.push_back((uint32_t)kf);
+                P.n -= kf;
+                P.bs -= kf;
+                P.cur0 -= kf;
+                P.pe_lo = std::max<int64_t>(P.pe_lo - kf, 0);
+                P.pe_hi = std::max<int64_t>(P.pe_hi - kf, 0);
+            }
+            if (s->xt_kf.cap < (size_t)s->nslots * 4) {
+                RCHK(s->xt_kf.reserve((size_t)s->nslots * 4, false));
+                HIPCHK(hipMemsetAsync(s->xt_kf.p, 0, (size_t)s->nslots * 4, st));
+            }
+            const int64_t nk = (int64_t)kslot.size();
+            if (nk) {
+                RCHK(s->xt_up.reserve((size_t)nk * 8, false));
+                HIPCHK(hipMemcpyAsync(s->xt_up.p, kslot.data(), nk * 4, hipMemcpyHostToDevice, st));
+                HIPCHK(hipMemcpyAsync(s->xt_up.as<uint32_t>() + nk, kval.data(), nk * 4, hipMemcpyHostToDevice, st));
+                launch_pg_xt_kf(st, s->xt_up.as<uint32_t>(), s->xt_up.as<uint32_t>() + nk, nk, s->xt_kf.as<uint32_t>());
+            }
+            launch_pg_xt_keep(st, s->key_off.as<u32>(), s->ranks.as<u32>(), C, n, s->xt_kf.as<uint32_t>(),
+                              s->pg_keep.as<unsigned char>());
+            if (nk) launch_pg_xt_kf(st, s->xt_up.as<uint32_t>(), nullptr, nk, s->xt_kf.as<uint32_t>());
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(st));  // (kslot / kval are pageable)
+        }
         // ---- carry the open batches (and the last completed ones) in stream order
         RCHK(s->x_idx.reserve(n * 8, false));
         RCHK(s->x_blk.reserve((size_t)((n + kTile - 1) / kTile + 2) * 8, false));
@@ -453,8 +725,13 @@ static int plane_run_group(sh_query* q, const sh_batch* b, bool host_out, const 
         s->pg_n = n_keep;
     }
     q->seq += N;
-    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
-    q->clock_valid = true;
+    if (b) {
+        q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+        q->clock_valid = true;
+    } else if (!q->clock_valid || now >= q->clock) {
+        q->clock = now;
+        q->clock_valid = true;
+    }
     q->stats.events = N;
     HIPCHK(hipEventRecord(q->ev_push1, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -697,6 +974,9 @@ static int group_time_rows(sh_query* q, const ColSet* cs, SlRecords rec, int64_t
 }
 
 int64_t plane_slots(sh_query* q) { return q->sl->nslots; }
+// partitioned externalTimeBatch with replaceTimestampWithBatchEndTime: the output rows' batch ends
+const int64_t* plane_out_rep_attr(sh_query* q) { return q->sl->out_xa.as<int64_t>(); }
+bool plane_is_sorted_lane(const sh_query* q) { return q->sl && q->sl->lane == 3; }
 // key columns of the query's output rows (the lanes without group-by keep the partition key internal)
 int query_out_keys(sh_query* q) { return q->kind == 1 && q->sl && q->sl->nk_out >= 0 ? q->sl->nk_out : q->kp.n; }
 const u32* plane_out_part(sh_query* q) { return q->sl->out_part.as<u32>(); }
@@ -704,14 +984,7 @@ const u32* plane_out_part(sh_query* q) { return q->sl->out_part.as<u32>(); }
 // Lane pass of the push: records of M passing events sorted by slot (b == null: a TIMER call at `now`).
 static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
-    if (s->lane == 3) {
-        if (b) return plane_run_group(q, b, host_out, out);
-        if (!q->clock_valid || now >= q->clock) {
-            q->clock = now;
-            q->clock_valid = true;
-        }
-        return empty_out(q, out);
-    }
+    if (s->lane == 3) return plane_run_group(q, b, now, host_out, out);
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
     // (externalTime lanes: the window runs on the timestamp attribute, no TIMER calls reach it)
@@ -1115,6 +1388,22 @@ static int pg_save(sh_query* q, std::vector<uint8_t>& out) {
     RCHK(dev(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(dev(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
     RCHK(dev(B.x.p, n * 8));
+    RCHK(dev(B.xe.p, n * 8));
+    RCHK(dev(B.xm.p, n * 8));
+    // the timeout's per-partition window state (xt_walk), in slot order
+    std::vector<uint32_t> xs;
+    for (auto& kv : s->xt_parts) xs.push_back(kv.first);
+    std::sort(xs.begin(), xs.end());
+    const uint64_t nx = xs.size();
+    put(&nx, 8);
+    for (uint32_t sl : xs) {
+        const SlidingImpl::XtPart& P = s->xt_parts[sl];
+        const int64_t v[6] = {P.n, P.bs, P.cur0, P.pe_lo, P.pe_hi, P.L};
+        const uint8_t fl = P.flushed;
+        put(&sl, 4);
+        put(v, sizeof v);
+        put(&fl, 1);
+    }
     return SH_OK;
 }
 
@@ -1138,7 +1427,7 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     o += kb;
     get(&n, 8);
     const int V = std::max(1, q->ap.n_vcols);
-    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V + 8) > len)
+    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V + 8 + 8 + 8) > len)
         return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     // validated: now replace the state
     if (kb) HIPCHK(hipMemcpyAsync(q->gkt.keys.p, keys, kb, hipMemcpyHostToDevice, st));
@@ -1166,8 +1455,27 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     RCHK(up(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(up(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
     RCHK(up(B.x.p, n * 8));
+    RCHK(up(B.xe.p, n * 8));
+    RCHK(up(B.xm.p, n * 8));
     HIPCHK(hipStreamSynchronize(st));  // the blob may be freed after the call
     s->pg_n = n;
+    uint64_t nx = 0;
+    if (!get(&nx, 8) || nx > (len - o) / 53) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+    std::unordered_map<uint32_t, SlidingImpl::XtPart> parts;
+    for (uint64_t i = 0; i < nx; i++) {
+        uint32_t sl = 0;
+        int64_t v[6];
+        uint8_t fl = 0;
+        get(&sl, 4);
+        get(v, sizeof v);
+        get(&fl, 1);
+        if (sl >= (uint64_t)s->nslots) return sh_fail(SH_ERR_INVALID, "snapshot does not match this query");
+        SlidingImpl::XtPart P;
+        P.n = v[0]; P.bs = v[1]; P.cur0 = v[2]; P.pe_lo = v[3]; P.pe_hi = v[4]; P.L = v[5];
+        P.flushed = fl != 0;
+        parts[sl] = P;
+    }
+    s->xt_parts = std::move(parts);
     *used = o;
     return SH_OK;
 }

@@ -17,7 +17,10 @@ struct PgRecs {
     unsigned char* prev; // carried as the partition's last completed batch
     i64 cap;
     i64* x;              // externalTimeBatch: the timestamp attribute
+    i64* xe;             // externalTimeBatch: the end time of the event's batch (cloneAppend :446-456)
+    i64* xm;             // externalTimeBatch: lastCurrentEventTime once the event is in (its partition's max)
 };
+
 
 // externalTimeBatch under `partition with` (ExternalTimeBatchWindowProcessor.process :238-311 per
 // partition): per partition slot the running max of the attribute (lastCurrentEventTime), the start,
@@ -31,6 +34,30 @@ struct PgExt {
     int xcol, scol;
     i64 start_time, T;
 };
+
+// externalTimeBatch's timeout under `partition with`: one emission (a selector chunk) of partition p —
+// [its previous emission's events as EXPIRED, RESET, the open batch from its first event] — found by the
+// host's Scheduler walk (sh_plane.cpp xt_walk); ranges are relative to the partition's sorted run
+struct PgXtEmit {
+    u32 p, pad;
+    i64 lo, hi;    // CURRENT: the open batch so far [lo, hi)
+    i64 xlo, xhi;  // EXPIRED: the previous emission's CURRENT range
+    i64 off;       // first entry of the emission in the expanded entry list
+    i64 sidx;      // the record whose running max stamps the expired rows (lastCurrentEventTime)
+    i64 clock;     // flush clock
+};
+// per push position: running max, batch end, and flags for the host walk (bit 1 the partition's first
+// event — initTiming; bit 0 a crossing into a higher bucket — a new batch)
+void launch_pg_xt_flags(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                        PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 n, unsigned char* flag, int* err);
+// the emissions' entries (EXPIRED first, then CURRENT, each in stream order): key (emission, group slot),
+// value = entry index | CURRENT << 31, epos = sorted position
+void launch_pg_xt_expand(hipStream_t s, const PgXtEmit* em, i64 ne, i64 n_ent, const u32* key_off, const u32* ranks,
+                         PgRecs C, int gbits, int cur_on, int exp_on, u64* ekey, u32* eval, u32* epos);
+// keep[c] = 2 for the records at or past their partition's keep-from index kf[p] (run-relative)
+void launch_pg_xt_keep(hipStream_t s, const u32* key_off, const u32* ranks, PgRecs C, i64 n, const u32* kf,
+                       unsigned char* keep);
+void launch_pg_xt_kf(hipStream_t s, const u32* slots, const u32* vals, i64 n, u32* kf);
 
 void launch_pg_append(hipStream_t s, SlRecords rec, i64 M, i64 n_old, i64 seq_base, ColSet cols, KeyPlan gkp,
                       KeyTable gkt, int nv, PgRecs C, u32* slot_cnt, u32* prev_cnt, int xcol = -1, int scol = -1,
@@ -56,11 +83,12 @@ void launch_pg_sc_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, 
                        const u32* ranks, PgRecs C, AggPlan ap, int gbits, i64 n_old, SlxRows rows, u32* row_part);
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
                     const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,
-                    const i64* chunk_ts = nullptr);
+                    const i64* chunk_ts = nullptr, const PgXtEmit* xem = nullptr, const u32* epos = nullptr,
+                    const u32* key_off = nullptr);
 void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
                     i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
                     unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep, const u32* row_part,
-                    u32* out_part);
+                    u32* out_part, i64* out_xa = nullptr);
 void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char* keep, PgRecs C, PgRecs D, int nv);
 // stable sort of (u64 key, u32 value) pairs over key bits [0, end_bit)
 int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,

@@ -183,8 +183,11 @@ __global__ __launch_bounds__(kBlock) void k_pg_assign_ext(const u32* __restrict_
         unsigned char kp = 0;
         if (i >= R.a) {
             i64 m;
-            if (ext_bucket(R, X, ms, i, &m) < 0 || R.start < 0) atomicExch(err, 1);
+            const i64 bk = ext_bucket(R, X, ms, i, &m);
+            if (bk < 0 || R.start < 0) atomicExch(err, 1);
             chunk_ts[c] = m;  // lastCurrentEventTime once this event is in (the expired rows' stamp)
+            C.xe[c] = R.start + X.T * (bk + 1);  // endTime when the event was appended (findEndTime :440-444)
+            C.xm[c] = m;
         }
         if (i < R.lo + R.np) {
             // the last completed batch: EXPIRED into the chunk that closes the open batch, else kept
@@ -255,6 +258,103 @@ void launch_pg_ext_state(hipStream_t s, const u32* key_off, const u32* ranks, co
     if (nslots > 0)
         hipLaunchKernelGGL(k_pg_ext_state, dim3((unsigned)((nslots + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off,
                            ranks, prev_cnt, pend_cnt, C, xs, ms, X, nslots);
+}
+
+// ---- externalTimeBatch(ts, T, start, timeout) under `partition with`. Which batch every event joins is
+// still the bucket of its partition's running max, but when a batch goes out is the Scheduler's: a timeout
+// re-sends a partition's open batch whenever the playback clock passes its lastScheduledTime, and ties
+// between partitions due at the same time resolve in PartitionStateHolder's HashMap order — a sequential
+// walk the host runs (sh_plane.cpp xt_walk) over these per-event flags; the emissions it finds are then
+// expanded into (emission, group) entries and folded like the batches above.
+__global__ __launch_bounds__(kBlock) void k_pg_xt_flags(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                       const u32* __restrict__ prev_cnt, const u32* __restrict__ pend_cnt,
+                                                       PgRecs C, const i64* __restrict__ xs, const i64* __restrict__ ms,
+                                                       PgExt X, i64 n, unsigned char* flag, int* err) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const u32 c = ranks[i];
+    const ExtRun R = ext_run(key_off, ranks, prev_cnt, pend_cnt, C, xs, X, C.ps[c]);
+    if (i < R.a) return;  // (a carried record)
+    i64 m;
+    const i64 bk = ext_bucket(R, X, ms, i, &m);
+    if (bk < 0 || R.start < 0) atomicExch(err, 1);
+    C.xm[c] = m;
+    C.xe[c] = R.start + X.T * (bk + 1);
+    unsigned char f = 0;
+    if (!R.has && i == R.a) {
+        // initTiming (:313-334); with the start from an attribute the first event may already be past
+        // endTime = start + T: it "crosses" an empty batch (no output, but a reschedule)
+        f = 2 | (bk > 0 ? 1 : 0);
+    } else {
+        const i64 pb = i == R.a ? R.bopen : ext_bucket(R, X, ms, i - 1, nullptr);
+        f = bk > pb ? 1 : 0;
+    }
+    flag[c] = f;
+}
+
+void launch_pg_xt_flags(hipStream_t s, const u32* key_off, const u32* ranks, const u32* prev_cnt, const u32* pend_cnt,
+                        PgRecs C, const i64* xs, const i64* ms, PgExt X, i64 n, unsigned char* flag, int* err) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_pg_xt_flags, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
+                           prev_cnt, pend_cnt, C, xs, ms, X, n, flag, err);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_xt_expand(const PgXtEmit* __restrict__ em, i64 ne, i64 n_ent,
+                                                        const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                        PgRecs C, int gbits, int cur_on, int exp_on, u64* ekey, u32* eval,
+                                                        u32* epos) {
+    const i64 t = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= n_ent) return;
+    i64 lo = 0, hi = ne;  // the last emission whose first entry is at or before t
+    while (hi - lo > 1) {
+        const i64 mid = (lo + hi) >> 1;
+        if (em[mid].off <= t) lo = mid;
+        else hi = mid;
+    }
+    const PgXtEmit E = em[lo];
+    const i64 k = t - E.off, nx = exp_on ? E.xhi - E.xlo : 0;
+    const bool cur = k >= nx;
+    const u32 pos = key_off[E.p] + (u32)(cur ? E.lo + (k - nx) : E.xlo + k);
+    const u32 c = ranks[pos];
+    (void)cur_on;
+    ekey[t] = ((u64)lo << gbits) | (u64)C.gs[c];
+    eval[t] = (u32)t | (cur ? 0x80000000u : 0u);
+    epos[t] = pos;
+}
+
+void launch_pg_xt_expand(hipStream_t s, const PgXtEmit* em, i64 ne, i64 n_ent, const u32* key_off, const u32* ranks,
+                         PgRecs C, int gbits, int cur_on, int exp_on, u64* ekey, u32* eval, u32* epos) {
+    if (n_ent > 0)
+        hipLaunchKernelGGL(k_pg_xt_expand, dim3((unsigned)((n_ent + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, em, ne,
+                           n_ent, key_off, ranks, C, gbits, cur_on, exp_on, ekey, eval, epos);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_xt_keep(const u32* __restrict__ key_off, const u32* __restrict__ ranks,
+                                                      PgRecs C, i64 n, const u32* __restrict__ kf, unsigned char* keep) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const u32 c = ranks[i];
+    const u32 p = C.ps[c];
+    keep[c] = (u32)(i - key_off[p]) >= kf[p] ? 2 : 0;
+}
+
+void launch_pg_xt_keep(hipStream_t s, const u32* key_off, const u32* ranks, PgRecs C, i64 n, const u32* kf,
+                       unsigned char* keep) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_pg_xt_keep, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, key_off, ranks,
+                           C, n, kf, keep);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pg_xt_kf(const u32* __restrict__ slots, const u32* __restrict__ vals, i64 n,
+                                                    u32* kf) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) kf[slots[i]] = vals ? vals[i] : 0u;
+}
+
+void launch_pg_xt_kf(hipStream_t s, const u32* slots, const u32* vals, i64 n, u32* kf) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_pg_xt_kf, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, slots, vals, n,
+                           kf);
 }
 
 // ---- 2. batch of every sorted position. Partition p's run [lo, hi) of the sorted order holds its
@@ -439,7 +539,8 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
                                                const u64* __restrict__ ekey, const u32* __restrict__ eval,
                                                const u32* __restrict__ ranks, PgRecs C, AggPlan ap, int gbits,
                                                SlxRows rows, u64* row_key, u32* row_part,
-                                               const i64* __restrict__ chunk_ts) {
+                                               const i64* __restrict__ chunk_ts, const PgXtEmit* __restrict__ xem,
+                                               const u32* __restrict__ epos, const u32* __restrict__ key_off) {
     const i64 sidx = (i64)blockIdx.x * 64 + threadIdx.x;
     if (sidx >= n_seg) return;
     const i64 lo = seg_start[sidx], hi = sidx + 1 < n_seg ? seg_start[sidx + 1] : n_e;
@@ -453,7 +554,7 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
     i64 cnt = 0, last_c = -1, last_x = -1;
     for (i64 t = lo; t < hi; t++) {
         const u32 v = eval[t];
-        const u32 c = ranks[v & 0x7FFFFFFFu];
+        const u32 c = ranks[epos ? epos[v & 0x7FFFFFFFu] : v & 0x7FFFFFFFu];
         if (!(v >> 31)) { last_x = c; continue; }
         last_c = c;
         cnt++;
@@ -475,13 +576,23 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
     }
     const bool cur = last_c >= 0;
     const i64 rc = cur ? last_c : last_x;
-    rows.ts[sidx] = cur ? C.ts[rc] : chunk_ts ? chunk_ts[chunk] : C.clk[chunk];
+    if (xem) {
+        // a timeout-path emission: its own clock, partition and lastCurrentEventTime stamp
+        const PgXtEmit E = xem[chunk];
+        rows.ts[sidx] = cur ? C.ts[rc] : C.xm[ranks[key_off[E.p] + (u32)E.sidx]];
+        rows.ch[sidx] = (i64)chunk;
+        rows.clk[sidx] = E.clock;
+        row_part[sidx] = E.p;
+    } else {
+        rows.ts[sidx] = cur ? C.ts[rc] : chunk_ts ? chunk_ts[chunk] : C.clk[chunk];
+        rows.ch[sidx] = C.seq[chunk];
+        rows.clk[sidx] = C.clk[chunk];
+        row_part[sidx] = C.ps[chunk];
+    }
     rows.rep[sidx] = C.seq[rc];
+    if (rows.xa) rows.xa[sidx] = C.xe[rc];
     rows.slot[sidx] = g;
-    rows.ch[sidx] = C.seq[chunk];
-    rows.clk[sidx] = C.clk[chunk];
     rows.exp[sidx] = cur ? 0 : 1;
-    row_part[sidx] = C.ps[chunk];
 #pragma unroll
     for (int a = 0; a < NA; a++) {
         if (a >= ap.n) continue;
@@ -502,13 +613,13 @@ __global__ __launch_bounds__(64) void k_pg_fold(const i64* __restrict__ seg_star
 
 void launch_pg_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 n_e, const u64* ekey, const u32* eval,
                     const u32* ranks, PgRecs C, AggPlan ap, int gbits, SlxRows rows, u64* row_key, u32* row_part,
-                    const i64* chunk_ts) {
+                    const i64* chunk_ts, const PgXtEmit* xem, const u32* epos, const u32* key_off) {
     if (n_seg <= 0) return;
     const unsigned grid = (unsigned)((n_seg + 63) / 64);
     if (ap.n <= 4) hipLaunchKernelGGL(k_pg_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks,
-                                      C, ap, gbits, rows, row_key, row_part, chunk_ts);
+                                      C, ap, gbits, rows, row_key, row_part, chunk_ts, xem, epos, key_off);
     else hipLaunchKernelGGL(k_pg_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, n_e, ekey, eval, ranks, C, ap,
-                            gbits, rows, row_key, row_part, chunk_ts);
+                            gbits, rows, row_key, row_part, chunk_ts, xem, epos, key_off);
 }
 
 // ---- 4. the rows in (chunk, first entry) order -> the push's output columns
@@ -516,7 +627,7 @@ __global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ orde
                                                    int nk, KeyTable kt, KeyPlan kp, i64 out_cap, i64* out_ts,
                                                    i64* out_keys, u64* out_vals, unsigned char* out_nulls,
                                                    unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep,
-                                                   const u32* __restrict__ row_part, u32* out_part) {
+                                                   const u32* __restrict__ row_part, u32* out_part, i64* out_xa) {
     const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (r >= n) return;
     const u32 j = order ? order[r] : (u32)r;  // (null: the rows are already in output order)
@@ -531,16 +642,17 @@ __global__ __launch_bounds__(kBlock) void k_pg_emit(const u32* __restrict__ orde
     out_clock[r] = rows.clk[j];
     out_rep[r] = rows.rep[j];
     out_part[r] = row_part[j];
+    if (out_xa) out_xa[r] = rows.xa[j];
 }
 
 void launch_pg_emit(hipStream_t s, const u32* order, i64 n, SlxRows rows, int n_aggs, int nk, KeyTable kt, KeyPlan kp,
                     i64 out_cap, i64* out_ts, i64* out_keys, u64* out_vals, unsigned char* out_nulls,
                     unsigned char* out_exp, i64* out_ch, i64* out_clock, i64* out_rep, const u32* row_part,
-                    u32* out_part) {
+                    u32* out_part, i64* out_xa) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_pg_emit, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, order, n, rows,
                        n_aggs, nk, kt, kp, out_cap, out_ts, out_keys, out_vals, out_nulls, out_exp, out_ch, out_clock,
-                       out_rep, row_part, out_part);
+                       out_rep, row_part, out_part, out_xa);
 }
 
 // ---- carried records: the kept ones (keep != 0) of the combined order, gathered in that (stream)
@@ -557,6 +669,8 @@ __global__ __launch_bounds__(kBlock) void k_pg_gather(const i64* __restrict__ id
     D.clk[k] = C.clk[c];
     D.prev[k] = keep[c] == 1;
     if (C.x) D.x[k] = C.x[c];
+    if (C.xe) D.xe[k] = C.xe[c];
+    if (C.xm) D.xm[k] = C.xm[c];
     for (int v = 0; v < nv; v++) D.vals[(size_t)v * D.cap + k] = C.vals[(size_t)v * C.cap + c];
 }
 

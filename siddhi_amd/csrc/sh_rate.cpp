@@ -50,6 +50,9 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     // key, a partition's limiter sees one key, so the keyed First variants equal the global keyed ones
     // (their state is per key) and LastGroupBy is the positional LastPerEvent of the partition.
     const bool lanes = q->kind == 1 && q->d.partition_col >= 0;
+    if (lanes && kind != SH_RATE_NONE && q->xt_replace)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "replaceTimestampWithBatchEndTime of a partitioned query with an output rate limiter");
     bool gb = (lanes ? q->d.n_group_by > 0 : q->kp.n > 0) && kind != SH_RATE_ALL;
     bool part = false;
     if (lanes && kind != SH_RATE_NONE) {

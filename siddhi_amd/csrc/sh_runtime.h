@@ -442,6 +442,8 @@ struct sh_query {
 // the push was committed; the aggregation probes the push and pushes again)
 constexpr int kRetryBand = 17;
 // every column the query reads has a pointer in `b` (SH_ERR_INVALID otherwise)
+const int64_t* plane_out_rep_attr(sh_query* q);
+bool plane_is_sorted_lane(const sh_query* q);
 int check_batch_cols(const sh_query* q, const sh_batch* b);
 // the open window aggregated per key without closing it (sh_window.cpp; aggregation retrieval)
 int query_peek(sh_query* q, int64_t* n_rows);

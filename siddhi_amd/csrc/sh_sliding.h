@@ -124,6 +124,9 @@ struct SlxRows {
     // stores per row were 23 of the replay's 34 ms in c3all)
     u64* aos = nullptr;
     int rw = 0;
+    // partitioned externalTimeBatch with replaceTimestampWithBatchEndTime: the rows' representative
+    // events' batch end (the timestamp attribute the window wrote into them)
+    i64* xa = nullptr;
 };
 constexpr int slx_row_words(int n_aggs) { return (5 + n_aggs + 1) & ~1; }
 void launch_slx_sends(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_pass_pre,

@@ -17,11 +17,12 @@ using shd::SlInfo;
 
 // lane 3 (partitioned lengthBatch grouped by other columns): a set of carried / combined records
 struct PgBufs {
-    DevBuf ps, gs, ts, seq, clk, vals, prev, x;
+    DevBuf ps, gs, ts, seq, clk, vals, prev, x, xe, xm;
     int64_t cap = 0;
     shd::PgRecs view() const {
         return shd::PgRecs{ps.as<uint32_t>(), gs.as<uint32_t>(), ts.as<int64_t>(), seq.as<int64_t>(), clk.as<int64_t>(),
-                           vals.as<shd::u64>(), prev.as<unsigned char>(), cap, x.as<int64_t>()};
+                           vals.as<shd::u64>(), prev.as<unsigned char>(), cap, x.as<int64_t>(),
+                           xe.as<int64_t>(), xm.as<int64_t>()};
     }
 };
 
@@ -75,6 +76,20 @@ struct SlidingImpl {
     int64_t pg_n = 0;
     DevBuf out_part;  // the lanes' output rows: partition slot of each (per-partition rate limiters)
     // externalTimeBatch lanes: per partition slot the running max, start, started flag, open bucket
+    DevBuf xr_xa, out_xa;
+    // partitioned externalTimeBatch with a timeout: per partition slot the window state the Scheduler walk
+    // needs (ExternalTimeBatchWindowProcessor.WindowState :495-517), indices relative to the partition's run
+    // of carried + new records; the device's keep-from array and the push's emissions / entries
+    struct XtPart {
+        int64_t n = 0;                // records of the partition in the run so far
+        int64_t bs = 0;               // first record of the open batch
+        int64_t cur0 = 0;             // first record not yet sent (currentEventChunk)
+        int64_t pe_lo = 0, pe_hi = 0; // the previous emission's CURRENT records (expiredEventChunk)
+        int64_t L = 0;                // lastScheduledTime
+        bool flushed = false;
+    };
+    std::unordered_map<uint32_t, XtPart> xt_parts;
+    DevBuf xt_kf, xt_em, xt_epos, xt_flag, xt_up;  // partitioned externalTimeBatch, replaceTimestampWithBatchEndTime: rows' batch ends
     DevBuf pg_M, pg_start, pg_has, pg_bopen, pg_pendcnt, pg_xs, pg_xv, pg_ms, pg_cts, pg_err;
     // time lanes grouped by other columns: operation lists, their sort, the (partition, group) states
     DevBuf pg_room, op_pos, op_pg, op_kind, op_seq, op_ts, op_clk, op_vals, pg_ocnt, pg_skey, pg_sidx, pg_st_cnt, pg_st_f;

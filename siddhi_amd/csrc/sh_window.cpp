@@ -1243,10 +1243,21 @@ extern "C" int sh_query_set_ext_timeout(sh_query* q, int64_t ms) {
     if (q->seq != 0 || q->n_pend != 0 || q->clock_valid)
         return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_timeout: set it before the first push");
     if (ms == 0) { q->xt_timeout = 0; return SH_OK; }
-    if (q->kind != 0 || q->d.partition_col >= 0 || q->given || q->internal_keys)
-        return sh_fail(SH_ERR_UNSUPPORTED,
-                       "externalTimeBatch timeout runs on unpartitioned queries (the partitions' timeouts fire in "
-                       "the Scheduler's HashMap order)");
+    // partitioned: on the sorted partition lanes (lane 3), the Scheduler walked on the host (sh_plane.cpp
+    // xt_walk) with its HashMap tie order, which hashes String.valueOf of the partition key
+    const bool lanes = q->kind == 1 && q->d.partition_col >= 0 && q->sl && plane_is_sorted_lane(q);
+    if ((q->kind != 0 && !lanes) || (q->d.partition_col >= 0 && !lanes) || q->given || q->internal_keys)
+        return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout of a sharded query");
+    if (lanes) {
+        const int pt = q->d.col_types[q->d.partition_col];
+        if (pt == SH_T_FLOAT || pt == SH_T_DOUBLE)
+            return sh_fail(SH_ERR_UNSUPPORTED,
+                           "externalTimeBatch timeout with float / double partition keys (the Scheduler's tie order "
+                           "hashes Double.toString)");
+        if (q->d.stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout with stream.current.event");
+        q->xt_timeout = ms;
+        return SH_OK;
+    }
     if (q->d.stream_current)
         return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout with stream.current.event output");
     q->xt_timeout = ms;
@@ -1809,6 +1820,15 @@ static int rep_attr_finish(sh_query* q, const sh_out* o, bool host) {
     const int64_t n = o->n_rows;
     q->xr_rep.resize((size_t)n);
     q->xr_vals.resize((size_t)n);
+    if (q->kind == 1) {
+        // partition lanes: every row carries its representative event's batch end (sh_plane_group_kernels)
+        if (n) {
+            HIPCHK(hipMemcpyAsync(q->xr_vals.data(), plane_out_rep_attr(q), (size_t)n * 8, hipMemcpyDeviceToHost,
+                                  q->ctx->stream));
+            HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        }
+        return SH_OK;
+    }
     if (n) {
         if (host) {
             std::memcpy(q->xr_rep.data(), o->rep, (size_t)n * 8);
@@ -1835,9 +1855,14 @@ extern "C" int sh_query_set_ext_replace_ts(sh_query* q, int32_t on) {
     if (q->seq != 0 || q->n_pend != 0 || q->clock_valid)
         return sh_fail(SH_ERR_INVALID, "sh_query_set_ext_replace_ts: set it before the first push");
     if (!on) { q->xt_replace = false; return SH_OK; }
-    if (q->kind != 0 || q->d.partition_col >= 0 || q->given || q->internal_keys)
+    // unpartitioned, or partitioned on the sorted partition lanes (lane 3), whose rows carry the batch end
+    const bool lanes = q->kind == 1 && q->d.partition_col >= 0 && q->sl && plane_is_sorted_lane(q);
+    if ((q->kind != 0 && !lanes) || (q->d.partition_col >= 0 && !lanes) || q->given || q->internal_keys)
         return sh_fail(SH_ERR_UNSUPPORTED,
-                       "replaceTimestampWithBatchEndTime runs on unpartitioned externalTimeBatch queries");
+                       "replaceTimestampWithBatchEndTime runs on externalTimeBatch queries (not sharded)");
+    if (lanes && q->rate.kind != SH_RATE_NONE)
+        return sh_fail(SH_ERR_UNSUPPORTED,
+                       "replaceTimestampWithBatchEndTime of a partitioned query with an output rate limiter");
     for (int i = 0; i < q->d.n_group_by; i++)
         if (q->d.group_by[i] == q->d.ts_col)
             return sh_fail(SH_ERR_UNSUPPORTED, "replaceTimestampWithBatchEndTime with a group-by on the timestamp attribute");

@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 11:
+        if L.sh_abi_version() != 12:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib

@@ -438,6 +438,59 @@ case(name="retrieval18_per_years", source="ctest/aggregation/Aggregation1TestCas
                        [1483228800000, "WSO2", 65.71428571428571, 460.0], [1514764800000, "WSO2", 60.0, 60.0],
                        [1546300800000, "WSO2", 260.0, 260.0], [1577836800000, "CISCO", 260.0, 520.0]]))
 
+# ---------------------------------------------------------------- incremental aggregation (Aggregation2TestCase)
+A2 = "ctest/aggregation/Aggregation2TestCase.java"
+# tests 47 / 48 (no @app:playback: AGG_TIMESTAMP is the wall clock, the sends arrive within a few ms —
+# modelled as send clocks B + i; `timestamp` carries the event time, out of order at the 4th send)
+_t47 = [["WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["IBM", 100.0, 0.0, 200, 16, 1496289951011],
+        ["IBM", 400.0, 0.0, 200, 9, 1496289952000], ["IBM", 900.0, 0.0, 200, 60, 1496289950000],
+        ["WSO2", 500.0, 0.0, 200, 7, 1496289951011], ["IBM", 100.0, 0.0, 200, 26, 1496289953000],
+        ["WSO2", 100.0, 0.0, 200, 96, 1496289953000]]
+case(name="aggregation2_47_per_minutes", source=A2 + ":63-131", kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["sum", "price"], ["avg", "price"]], group_by=["symbol"], ts="timestamp",
+                      durations=["sec", "year"]),
+     sends=[[[B + i] + r] for i, r in enumerate(_t47)],
+     expect=dict(find=dict(per="min", start=0, end=1543664151000),
+                 rows=[[1496289900000, "WSO2", 650.0, 216.66666666666666], [1496289900000, "IBM", 1500.0, 375.0]]))
+case(name="aggregation2_48_per_seconds", source=A2 + ":133-199", kind="aggregation", schema=AGG_SCHEMA,
+     aggregation=dict(aggs=[["sum", "price"]], group_by=["symbol"], ts="timestamp", durations=["sec", "year"]),
+     sends=[[[B + i] + r] for i, r in enumerate(_t47)],
+     expect=dict(find=dict(per="sec", start=0, end=1543664151000),
+                 rows=[[1496289950000, "WSO2", 50.0], [1496289950000, "IBM", 900.0], [1496289951000, "IBM", 100.0],
+                       [1496289951000, "WSO2", 500.0], [1496289952000, "IBM", 400.0], [1496289953000, "IBM", 100.0],
+                       [1496289953000, "WSO2", 100.0]]))
+# aggTimeZone = Asia/Singapore (+08:00, no daylight saving): hour / day / month / year buckets start at
+# Singapore's local boundaries (IncrementalTimeConverterUtil with the zone). `within "2019-**-** ..."`
+# resolves in GMT (the Day5 / Year tables keep a bucket that starts at 16:00 GMT on Dec 31 of the year
+# named): 2018 = [1514764800000, 1546300800000), 2019 = [.., 1577836800000), 2020 = [.., 1609459200000)
+SGT = 8 * 3_600_000
+_y = {2018: (1514764800000, 1546300800000), 2019: (1546300800000, 1577836800000),
+      2020: (1577836800000, 1609459200000)}
+_sgt = [  # (name, lines, root, year of `within`, the three event times, expected bucket starts)
+    ("hour", "632-683", "hour", 2019, (1577721601000, 1577725199000, 1577725201000), (1577721600000, 1577725200000)),
+    ("hour2", "685-737", "hour", 2020, (1582988401000, 1582991999000, 1582992001000), (1582988400000, 1582992000000)),
+    ("day", "739-791", "day", 2020, (1580486401000, 1580572799000, 1580572801000), (1580486400000, 1580572800000)),
+    ("day2", "793-845", "day", 2020, (1582905601000, 1582991999000, 1582992001000), (1582905600000, 1582992000000)),
+    ("day3", "847-899", "day", 2019, (1551283201000, 1551369599000, 1551369601000), (1551283200000, 1551369600000)),
+    ("day4", "901-953", "day", 2019, (1548864001000, 1548950399000, 1548950401000), (1548864000000, 1548950400000)),
+    ("day5", "955-1007", "day", 2019, (1577721601000, 1577807999000, 1577808001000), (1577721600000, 1577808000000)),
+    ("month", "1008-1060", "month", 2020, (1580486401000, 1582991999000, 1582992001000), (1580486400000, 1582992000000)),
+]
+for nm, lines, root, yr, ts3, b2 in _sgt:
+    case(name=f"aggregation2_sgt_{nm}", source=f"{A2}:{lines}", kind="aggregation", schema="symbol string, price float, timestamp long",
+         aggregation=dict(aggs=[["avg", "price"]], group_by=["symbol"], ts="timestamp", durations=[root, root],
+                          tz_offset_ms=SGT),
+         sends=[[[B + i, "WSO2", p, t]] for i, (p, t) in enumerate(zip((50.0, 70.0, 80.0), ts3))],
+         expect=dict(find=dict(per=root, start=_y[yr][0], end=_y[yr][1]),
+                     rows=[[b2[0], "WSO2", 60.0], [b2[1], "WSO2", 80.0]]))
+case(name="aggregation2_sgt_year", source=A2 + ":1062-1115", kind="aggregation",
+     schema="symbol string, price float, timestamp long",
+     aggregation=dict(aggs=[["avg", "price"]], group_by=["symbol"], ts="timestamp", durations=["year", "year"],
+                      tz_offset_ms=SGT),
+     sends=[[[B + i, "WSO2", p, t]] for i, (p, t) in enumerate(zip((50.0, 70.0, 80.0),
+                                                                 (1546272001000, 1577807999000, 1577808001000)))],
+     expect=dict(find=dict(per="year", start=_y[2018][0], end=_y[2018][1]), rows=[[1546272000000, "WSO2", 60.0]]))
+
 # ---------------------------------------------------------------- filters (FilterTestCase1): expected counts
 F = "ctest/query/FilterTestCase1.java"
 FL = "symbol string, price float, volume long"

@@ -50,7 +50,7 @@ def build(case, dic):
         a = case["aggregation"]
         spec = abi.AggregationSpec(schema, aggs=[tuple(x) for x in a["aggs"]], group_by=a.get("group_by", ()),
                                    ts=a.get("ts"), durations=tuple(a["durations"]),
-                                   filter=_conv_filter(a.get("filter"), dic))
+                                   filter=_conv_filter(a.get("filter"), dic), tz_offset_ms=a.get("tz_offset_ms", 0))
         return schema, spec
     q = case["query"]
     spec = abi.QuerySpec(schema, q["window"], q.get("param", 0), group_by=q.get("group_by", ()),

@@ -59,7 +59,10 @@ def both(rt, spec, pushes, label, checkpoints=()):
     return n_rows
 
 
-AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"]
+# (month / year roots — `every month` or `every year` alone — are not on the GPU: the root runs as a
+# timeBatch of a fixed period; those transcribed tables pin the oracle only, tests/test_oracle_kat.py)
+AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"
+            and c["aggregation"]["durations"][0] not in ("month", "year")]
 
 
 @pytest.mark.parametrize("case", AGG_KATS, ids=[c["name"] for c in AGG_KATS])

@@ -271,15 +271,102 @@ def test_ext_timeout_checkpoint():
         assert_same(got, ref, label=f"ext timeout ckpt {cut}")
 
 
-@pytest.mark.parametrize("kw", [dict(output="all"), dict(output="expired")])
-def test_ext_timeout_refused_with_expired_rows(kw):
+@pytest.mark.parametrize("output,group,send_size", [("all", True, 1), ("expired", True, 7), ("all", None, 3),
+                                                     ("expired", None, 1), ("expired", False, 1)])
+def test_ext_timeout_expired_rows(output, group, send_size):
+    """timeouts with expired output (flushToOutputChunk / appendToOutputChunk :336-438): every emission
+    carries the previous emission's events as EXPIRED (stamped with lastCurrentEventTime), then RESET and
+    the open batch from its first event — group-by rows merged by key, `select *` (group None) rows one
+    per event; across advance_time calls and pushes"""
+    ts, cols = tstream(60_000, 0xF5, late_ms=300)
+    aggs = [] if group is None else None
+    pushes = with_advances(split_batches(SCH, ts, cols, [1, 15_000, 15_001, 41_000], send_size), ts)
+    got = both(tspec(output=output, group=bool(group), aggs=aggs), pushes, f"ext timeout {output} {group}")
+    # (all events: a key in both parts shows its current row at its expired position)
+    assert got["expired"].sum() > 10 or output == "all"
+
+
+def test_ext_timeout_expired_rows_checkpoint():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = tstream(50_000, 0xF8)
+    pushes = with_advances(split_batches(SCH, ts, cols, [12_000, 25_000, 37_000], 1), ts)
+    for cut in (2, 5):
+        got, ref, _ = checkpointed(tspec(output="all"), pushes, cut)
+        assert_same(got, ref, label=f"ext timeout all ckpt {cut}")
+
+
+# ---- the timeout under `partition with`: every partition's own lastScheduledTime; partitions due at
+# the same time fire in PartitionStateHolder's HashMap order, one per due time per call (Scheduler
+# .onTimeChange :71-104), the others at later calls ------------------------------------------------------
+def ptstream(n, parts, seed, late_ms=0, pause_p=1 / 2000, zero_gaps=False):
+    """arrival clock with pauses (timeouts fire) — with zero_gaps most sends share their clock, so many
+    partitions schedule the same due time (ties); event time 1 ms per 20 events, per-partition offsets"""
+    ts, cols = tstream(n, seed, pause_p=pause_p, late_ms=late_ms)
+    if zero_gaps:
+        rng = np.random.default_rng(seed + 3)
+        gaps = (rng.random(n) < 0.02) * rng.integers(1, 4, n) + (rng.random(n) < pause_p) * rng.integers(2_000, 9_000, n)
+        ts = 1_000_000 + np.cumsum(gaps).astype(np.int64)
+        cols[4] = ts.copy()
+    rng = np.random.default_rng(seed + 5)
+    p = rng.integers(0, parts, n).astype(np.int32)
+    et = cols[2] + (p.astype(np.int64) % 7) * 333
+    return ts, [p, cols[0], cols[1], et, cols[3], cols[4]]
+
+
+def ptspec(output="current", group_by=("p",), timeout=1500, T=1000, start=0, start_attr=None, aggs=None):
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", T, group_by=list(group_by), ts_attr="et", start_time=start,
+                       start_attr=start_attr, partition="p", key_capacity=4096, output=output,
+                       aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "et")] if aggs is None else aggs)
+    sp.timeout = timeout
+    return sp
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("group_by,send_size,zero_gaps", [(("p",), 1, False), (("k",), 5, True), ((), 1, True),
+                                                          (("k", "p"), 3, False)])
+def test_partitioned_ext_timeout(output, group_by, send_size, zero_gaps):
+    """ExternalTimeBatchWindowProcessor.process (:238-311) per partition with its timeout: a partition's
+    TIMER re-sends its open batch (flushToOutputChunk, then appendToOutputChunk), crossings send the batch
+    whole, expired rows are the previous emission's — ties between partitions at one due time resolved in
+    HashMap order; across pushes and advance_time calls"""
+    ts, cols = ptstream(60_000, 23, 0xD1, late_ms=300, zero_gaps=zero_gaps)
+    pushes = split_batches(PSCH, ts, cols, [1, 14_000, 14_001, 37_000], send_size)
+    got = both(ptspec(output=output, group_by=group_by), with_advances(pushes, ts), f"pext timeout {group_by} {output}")
+    assert len(got["ts"]) > 100
+
+
+def test_partitioned_ext_timeout_attribute_start_filter_replace():
+    """start from an attribute (a first event may already be past its first batch: a reschedule with
+    nothing to send), a filter, many partitions, and the replaced timestamp attribute"""
+    ts, cols = ptstream(50_000, 400, 0xD2, late_ms=500, zero_gaps=True)
+    cols[4] = cols[4] - 1_000 * (cols[0] % 3)  # (the start attribute: some partitions start 1-2 s early)
+    sp = ptspec(output="all", group_by=("k",), timeout=700, T=900, start=None, start_attr="st",
+                aggs=[("count", None), ("sum", "v"), ("max", "v")])
+    sp.filter = (">", "v", 25.0)
+    sp.replace_ts = True
+    got = both(sp, with_advances(split_batches(PSCH, ts, cols, [20_000, 35_000], 2), ts, every=1), "pext timeout attr")
+    assert len(got["rep_attr"]) == len(got["ts"])
+
+
+def test_partitioned_ext_timeout_checkpoint_and_rate():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = ptstream(40_000, 31, 0xD3, zero_gaps=True)
+    pushes = with_advances(split_batches(PSCH, ts, cols, [9_000, 21_000, 30_000], 1), ts)
+    for cut in (2, 5):
+        got, ref, _ = checkpointed(ptspec(output="all", group_by=("k",)), pushes, cut)
+        assert_same(got, ref, label=f"pext timeout ckpt {cut}")
+    sp = ptspec(output="current")
+    sp.rate = ("last", 3)
+    both(sp, pushes, "pext timeout rate")
+
+
+def test_partitioned_ext_timeout_refusals():
     from siddhi_amd import runtime
-    with pytest.raises(runtime.SiddhiError, match="timeout"):
-        runtime.GpuQuery(tspec(**kw))
-    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
+    sch = abi.Schema.parse("p double, k string, v double, et long, st long, ts long")
+    sp = abi.QuerySpec(sch, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
                        aggs=[("count", None)])
     sp.timeout = 1000
-    with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
+    with pytest.raises(runtime.SiddhiError, match="Double.toString"):
         runtime.GpuQuery(sp)
 
 
@@ -353,8 +440,36 @@ def test_ext_replace_timestamp_refusals():
     sp = abi.QuerySpec(PSCH, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
                        aggs=[("count", None)])
     sp.replace_ts = True
-    with pytest.raises(runtime.SiddhiError, match="unpartitioned"):
+    sp.rate = ("all", 5)
+    with pytest.raises(runtime.SiddhiError, match="rate limiter"):
         runtime.GpuQuery(sp)
+
+
+@pytest.mark.parametrize("output", ["current", "all", "expired"])
+@pytest.mark.parametrize("group_by,start,start_attr,late", [(["p"], None, None, 0), (["k"], 1_000, None, 800),
+                                                            ([], None, "st", 300)])
+def test_partitioned_ext_replace_timestamp(output, group_by, start, start_attr, late):
+    """`partition with` around externalTimeBatch(et, T, start, 0, true): every partition's cloneAppend
+    writes its own batch's endTime into the event (:446-456), so each row's replaced attribute is the
+    end of the batch holding its representative event — current rows their batch, expired rows the
+    previous one — carried across pushes with the partitions' open batches"""
+    ts, cols = pstream(50_000, 31, 0xEB, late_ms=late)
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 600, group_by=group_by, ts_attr="et", start_time=start,
+                       start_attr=start_attr, partition="p", key_capacity=4096, output=output,
+                       aggs=[("count", None), ("sum", "v"), ("min", "v")])
+    sp.replace_ts = True
+    got = both(sp, split_batches(PSCH, ts, cols, [1, 17_000, 17_001, 36_000], 3), f"pext replace {group_by} {output}")
+    assert len(got["rep_attr"]) == len(got["ts"]) > 0
+
+
+def test_partitioned_ext_replace_timestamp_checkpoint():
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = pstream(40_000, 19, 0xEC, late_ms=200)
+    sp = abi.QuerySpec(PSCH, "externalTimeBatch", 500, group_by=["k"], ts_attr="et", partition="p", key_capacity=4096,
+                       output="all", aggs=[("count", None), ("sum", "v")])
+    sp.replace_ts = True
+    got, ref, _ = checkpointed(sp, split_batches(PSCH, ts, cols, [15_000, 30_000], 1), 1)
+    assert_same(got, ref, label="pext replace ckpt")
 
 
 @pytest.mark.parametrize("rate", [("all", 7919), ("last", 4001), ("first", 3001)])
