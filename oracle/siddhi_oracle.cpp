@@ -346,7 +346,7 @@ int64_t key_raw(const Schema& s, const OEvent& e, int c) {
 
 // Output collection: one flush per selector output chunk.
 struct OutRow {
-    int64_t ts; uint8_t expired; int64_t keys[SH_MAX_GROUP];
+    int64_t ts; uint8_t expired; int64_t keys[SH_MAX_GROUP + 1];  // (+1: an aggregation table's bucket)
     uint64_t vals[SH_MAX_AGGS]; uint8_t nulls[SH_MAX_AGGS];
     int64_t rep;  // stream index of the event the row was built from
     int64_t rep_attr;  // externalTimeBatch: that event's timestamp attribute as the window holds it
@@ -1236,7 +1236,7 @@ struct AggRuntime {
         OutRow r{};
         r.ts = d.ts_col >= 0 ? br.ext : store_ts;
         r.keys[0] = r.ts;
-        if (d.n_group_by > 0) r.keys[1] = br.keys[0];
+        for (int g = 0; g < d.n_group_by; g++) r.keys[1 + g] = br.keys[g];
         for (size_t i = 0; i < bases.size(); i++) {
             const AggOut& o = br.val[i];
             r.nulls[i] = o.has ? 0 : 1;
@@ -1274,7 +1274,7 @@ struct AggRuntime {
         for (size_t i = 0; i < bases.size(); i++) if (vals[i].has) a.val[i] = a.st[i]->add(as_jval(i, vals[i]));
     }
     void find(int per, int64_t start, int64_t end, OutBuf& ob) {
-        typedef std::pair<int64_t, int64_t> GK;
+        typedef std::array<int64_t, 1 + SH_MAX_GROUP> GK;  // (bucket, group-by values)
         std::map<GK, Acc> mem;
         const int ip = per - d.min_duration;
         for (int k = ip; k >= 0; k--) {
@@ -1282,7 +1282,9 @@ struct AggRuntime {
             for (const GKey& key : ex.order) {
                 const BaseRow& br = ex.store[key];
                 const int64_t b = zst(d.ts_col >= 0 ? br.ext : ex.store_ts, per);
-                GK g(b, d.n_group_by > 0 ? br.keys[0] : 0);
+                GK g{};
+                g[0] = b;
+                for (int x = 0; x < d.n_group_by; x++) g[1 + x] = br.keys[x];
                 auto it = mem.find(g);
                 if (it == mem.end()) it = mem.emplace(g, new_acc()).first;
                 fold(it->second, br.val);
@@ -1291,7 +1293,9 @@ struct AggRuntime {
         std::map<GK, Acc> res;
         for (const OutRow& r : history[per]) {
             if (r.ts < start || r.ts >= end) continue;
-            GK g(r.ts, d.n_group_by > 0 ? r.keys[1] : 0);
+            GK g{};
+            g[0] = r.ts;
+            for (int x = 0; x < d.n_group_by; x++) g[1 + x] = r.keys[1 + x];
             auto it = res.find(g);
             if (it == res.end()) it = res.emplace(g, new_acc()).first;
             std::vector<AggOut> v(bases.size());
@@ -1302,7 +1306,7 @@ struct AggRuntime {
             fold(it->second, v);
         }
         for (auto& m : mem) {
-            if (m.first.first < start || m.first.first >= end) continue;
+            if (m.first[0] < start || m.first[0] >= end) continue;
             auto it = res.find(m.first);
             if (it == res.end()) it = res.emplace(m.first, new_acc()).first;
             fold(it->second, m.second.val);
@@ -1311,9 +1315,8 @@ struct AggRuntime {
         ob.with_rep = false;
         for (auto& kv : res) {
             OutRow r{};
-            r.ts = kv.first.first;
-            r.keys[0] = kv.first.first;
-            r.keys[1] = kv.first.second;
+            r.ts = kv.first[0];
+            for (int x = 0; x <= d.n_group_by; x++) r.keys[x] = kv.first[x];
             for (size_t i = 0; i < bases.size(); i++) {
                 const AggOut& o = kv.second.val[i];
                 r.nulls[i] = o.has ? 0 : 1;
@@ -1511,7 +1514,7 @@ int or_advance_time(void* h, int64_t now, const sh_out** out) {
 void* or_aggregation_create(const sh_aggregation_desc* desc) {
     if (!desc || desc->n_cols <= 0 || desc->n_cols > SH_MAX_COLS || desc->min_duration < 0 ||
         desc->max_duration > SH_DUR_YEARS || desc->min_duration > desc->max_duration ||
-        desc->n_group_by < 0 || desc->n_group_by > 1 || desc->n_aggs <= 0 || desc->n_aggs > SH_MAX_AGGS) {
+        desc->n_group_by < 0 || desc->n_group_by > SH_MAX_GROUP || desc->n_aggs <= 0 || desc->n_aggs > SH_MAX_AGGS) {
         g_err = "invalid aggregation descriptor"; return nullptr;
     }
     AggRuntime* a = new AggRuntime();

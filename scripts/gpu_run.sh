@@ -39,7 +39,7 @@ for step in "$@"; do
     kstats)
       n=${arg:-c2}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$P/kt_$n" -o run --output-format csv -- \
-          python3 bench.py $(wl_args "$arg") --steps 5 --warmup 2 --no-cpu-baseline > "$P/kt_$n.json" 2> "$P/kt_$n.err" \
+          python3 bench.py $(wl_args "$arg") --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$P/kt_$n.json" 2> "$P/kt_$n.err" \
           || fail "kstats $n" "$P/kt_$n.err"
       python3 scripts/kstats.py "$P/kt_$n" > "${O}_${n}_kernel_stats.txt" || fail "kstats summary $n"
       head -8 "${O}_${n}_kernel_stats.txt" ;;
@@ -47,7 +47,7 @@ for step in "$@"; do
       n=${arg:-c2}
       for ctr in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 150 rocprofv3 --pmc $ctr -d "$P/${n}_$ctr" -o run --output-format csv -- \
-            python3 bench.py $(wl_args "$arg") --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> "$P/${n}_$ctr.err" \
+            python3 bench.py $(wl_args "$arg") --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > /dev/null 2> "$P/${n}_$ctr.err" \
             || fail "pmc $n $ctr" "$P/${n}_$ctr.err"
       done
       F=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" "$P/${n}_FETCH_SIZE")

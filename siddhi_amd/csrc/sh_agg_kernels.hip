@@ -231,9 +231,9 @@ __global__ __launch_bounds__(kBlock) void k_find_rebucket(i64 n, const i64* __re
 }
 
 __global__ __launch_bounds__(kBlock) void k_find_gather_u64(i64 n, const u32* __restrict__ idx, const i64* __restrict__ src,
-                                                           u64* dst) {
+                                                           u64* dst, u64 flip) {
     const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) dst[i] = (u64)src[idx[i]];
+    if (i < n) dst[i] = (u64)src[idx[i]] ^ flip;
 }
 
 // group starts in (bucket, key) order; out-of-range rows (bucket -1) start no group
@@ -299,10 +299,10 @@ void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i
                        per, start, end, bucket_out, idx, tz);
 }
 
-void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst) {
+void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst, u64 flip) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_find_gather_u64, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, idx,
-                       src, dst);
+                       src, dst, flip);
 }
 
 void launch_find_starts(hipStream_t s, i64 n, const u32* idx, const i64* bucket, const i64* key, u32* flag) {
@@ -425,6 +425,40 @@ __global__ __launch_bounds__(kBlock) void k_fill_i64(i64* p, i64 n, i64 v) {
 void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_fill_i64, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, n, v);
+}
+
+}  // namespace shd
+
+namespace shd {
+
+// ---- interned group keys (two group-by columns, or a 64-bit one beside the bucket) --------------------
+// every passing event's group key -> its slot in the intern table (the root groups by (bucket, slot));
+// events the filter drops get slot 0 (the root never reads them)
+__global__ __launch_bounds__(kBlock) void k_agg_intern(ColSet cols, FilterProg f, KeyPlan ikp, KeyTable ikt, i64 n,
+                                                      u32* ids) {
+    const i64 e = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n) return;
+    ids[e] = eval_filter(f, cols, e) ? key_slot(ikt, make_key(ikp, cols, e)) : 0u;
+}
+
+void launch_agg_intern(hipStream_t s, ColSet cols, FilterProg f, KeyPlan ikp, KeyTable ikt, i64 n, u32* ids) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_agg_intern, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, f, ikp,
+                           ikt, n, ids);
+}
+
+// slots -> the group-by values as sh_out reports them ([component][n])
+__global__ __launch_bounds__(kBlock) void k_agg_unintern(const i64* __restrict__ slots, i64 n, KeyTable ikt, KeyPlan ikp,
+                                                        i64* out) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n) return;
+    unpack_key(ikp, slot_key(ikt, (u32)slots[r]), out + r, n);
+}
+
+void launch_agg_unintern(hipStream_t s, const i64* slots, i64 n, KeyTable ikt, KeyPlan ikp, i64* out) {
+    if (n > 0)
+        hipLaunchKernelGGL(k_agg_unintern, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, slots, n, ikt,
+                           ikp, out);
 }
 
 }  // namespace shd

@@ -172,7 +172,7 @@ struct sh_aggregation {
     TableBuf tables[SH_DUR_YEARS + 1];
     OutHost tout, fout;
     // retrieval scratch (sh_aggregation_find)
-    DevBuf m_bucket, m_key, m_vals, f_bucket, f_key, f_vals, g_bucket, g_idx, g_k64, g_k64s, g_idx1, g_idx2, g_flag,
+    DevBuf m_bucket, m_key, m_vals, f_bucket, f_key, f_vals, g_bucket, g_idx, g_k64, g_k64s, g_idx1, g_idx2, g_dk, g_flag,
         g_pre, g_tmp, g_sort, v_bucket, v_key, v_vals;
     DevBuf root_bucket_col, root_key_col, minmax;
     int64_t* h_minmax = nullptr;
@@ -209,6 +209,14 @@ struct sh_aggregation {
     hipEvent_t ev_pr = nullptr;
     DevBuf pr_dev;
     int64_t* h_pr = nullptr;
+    // group keys wider than the root key's 32-bit half — two group-by columns, or one long / double column
+    // beside the `aggregate by` bucket: every passing event's key is interned into a table (ikt) and its
+    // slot travels as a synthetic dictionary column (index d.n_cols of the root's batch); tables and
+    // retrievals map the slots back to the group-by values (k_agg_unintern)
+    bool intern = false;
+    KeyPlan ikp{};
+    KeyTableHost ikt;
+    DevBuf ids, dkeys;
 };
 
 // The levels' key-table overflow checks are queued with each merge and verified after the next
@@ -452,7 +460,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         return sh_fail(SH_ERR_INVALID, "invalid aggregation descriptor");
     if (d->min_duration > SH_DUR_DAYS)
         return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation roots are sec/min/hour/day");
-    if (d->n_group_by > 1) return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation supports one group-by column");
+    if (d->n_group_by > SH_MAX_GROUP) return sh_fail(SH_ERR_INVALID, "invalid aggregation descriptor");
     if (d->ts_col >= 0 && (d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG))
         return sh_fail(SH_ERR_INVALID, "`aggregate by` attribute must be a long");
     sh_aggregation* a = new sh_aggregation();
@@ -508,14 +516,27 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     if (a->has_bucket) {
         kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->T_root; kp.add[g] = a->tz_root; g++;
     }
-    if (d->n_group_by == 1) {
-        int c = d->group_by[0];
-        int t = d->col_types[c];
-        if (!(t == SH_T_INT || t == SH_T_STRID || t == SH_T_BOOL || (t == SH_T_LONG && !a->has_bucket))) {
-            delete a;
-            return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation group-by must be a 32-bit key (long only without `aggregate by`)");
+    int gtype = -1;  // the root key's group component type
+    if (d->n_group_by >= 1) {
+        const int t = d->col_types[d->group_by[0]];
+        a->intern = d->n_group_by == 2 ||
+                    !(t == SH_T_INT || t == SH_T_STRID || t == SH_T_BOOL || (t == SH_T_LONG && !a->has_bucket));
+        if (a->intern) {
+            if (shard) { delete a; return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation groups by one 32-bit column"); }
+            int rc0 = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, a->ikp);
+            if (!rc0) rc0 = a->ikt.init(rd.key_capacity);
+            if (rc0) { delete a; return rc0; }
+            if (d->n_cols + 1 > SH_MAX_COLS) { delete a; return sh_fail(SH_ERR_UNSUPPORTED, "too many columns to intern group keys"); }
+            // the interned slot: a dictionary column past the stream's own (dense in [0, slots))
+            rd.n_cols = d->n_cols + 1;
+            rd.col_types[d->n_cols] = SH_T_STRID;
+            rd.key_capacity = (int64_t)a->ikt.size_ + 1;
+            kp.col[g] = d->n_cols; kp.type[g] = SH_T_STRID; kp.div[g] = 0; g++;
+            gtype = SH_T_STRID;
+        } else {
+            kp.col[g] = d->group_by[0]; kp.type[g] = t; kp.div[g] = 0; g++;
+            gtype = t;
         }
-        kp.col[g] = c; kp.type[g] = t; kp.div[g] = 0; g++;
     }
     kp.n = g;
     rd.n_group_by = 0;
@@ -526,7 +547,7 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
         shard_attach_aggregation(a->shard, a);
         *shard = a->shard;
     }
-    if (a->has_bucket && d->n_group_by == 1 && d->col_types[d->group_by[0]] == SH_T_STRID) {
+    if (a->has_bucket && d->n_group_by >= 1 && gtype == SH_T_STRID) {
         // ids per bucket row: the GPU's share of the dictionary (sharded owners hold the ids = rank mod G)
         const int64_t cap = rd.key_capacity, per = shard ? (cap + world - 1) / world : cap;
         // (A/B switch SH_AGG_BAND_ROWS, 0 = hash keys only)
@@ -797,11 +818,29 @@ static int ring_collect(sh_aggregation* a, int64_t keep) {
 static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     const sh_out* o = nullptr;
     sh_batch dev;
-    RCHK(check_batch_cols(a->root, b));
+    if (a->intern) {  // (the stream's own columns: the interned slot column is the aggregation's)
+        if (b->n > 0)
+            for (int c = 0; c < a->d.n_cols; c++)
+                if ((a->root->cols_used >> c & 1) && !b->cols[c])
+                    return sh_fail(SH_ERR_INVALID, "batch column " + std::to_string(c) + " is NULL but the query reads it");
+    } else {
+        RCHK(check_batch_cols(a->root, b));
+    }
     if (host) {
-        RCHK(a->root->staged.stage(a->ctx->stream, b, a->root->d.n_cols, a->root->d.col_types, &dev));
+        RCHK(a->root->staged.stage(a->ctx->stream, b, a->d.n_cols, a->root->d.col_types, &dev));
     } else {
         dev = *b;
+    }
+    if (a->intern) {
+        // every passing event's group key -> its intern slot, the root's synthetic dictionary column
+        RCHK(a->ids.reserve((size_t)std::max<int64_t>(dev.n, 1) * 4, false));
+        ColSet cs{};
+        cs.n = a->d.n_cols;
+        for (int c = 0; c < a->d.n_cols; c++) { cs.type[c] = a->d.col_types[c]; cs.ptr[c] = dev.cols[c]; }
+        launch_agg_intern(a->ctx->stream, cs, a->root->fp, a->ikp, a->ikt.dev(), dev.n, a->ids.as<u32>());
+        HIPCHK(hipGetLastError());
+        RCHK(a->ikt.check(a->ctx->stream));
+        dev.cols[a->d.n_cols] = a->ids.p;
     }
     RCHK(ring_collect(a, sh_aggregation::kRing - 1));
     const int rk = (int)(a->r_next % sh_aggregation::kRing);
@@ -932,6 +971,22 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     return SH_OK;
 }
 
+// the group-by columns of n table / retrieval rows (device keys) into host memory ([column][n]); interned
+// keys are mapped back to their values on the device first
+static int agg_keys_out(sh_aggregation* a, const int64_t* keys, int64_t n, int64_t* host) {
+    hipStream_t s = a->ctx->stream;
+    if (!a->intern) {
+        HIPCHK(hipMemcpyAsync(host, keys, n * 8, hipMemcpyDeviceToHost, s));
+        return SH_OK;
+    }
+    const int ng = a->d.n_group_by;
+    RCHK(a->dkeys.reserve((size_t)ng * n * 8, false));
+    launch_agg_unintern(s, keys, n, a->ikt.dev(), a->ikp, a->dkeys.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(host, a->dkeys.p, (size_t)ng * n * 8, hipMemcpyDeviceToHost, s));
+    return SH_OK;
+}
+
 extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out** out) {
     SH_RANGE("sh_aggregation_table");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
@@ -953,7 +1008,7 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
     if (n) {
         HIPCHK(hipMemcpyAsync(o.ts.data(), t.bucket.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(o.keys.data(), t.bucket.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
-        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + n, t.key.as<int64_t>() + r0, n * 8, hipMemcpyDeviceToHost, s));
+        if (nk > 1) RCHK(agg_keys_out(a, t.key.as<int64_t>() + r0, n, o.keys.data() + n));
         for (int b = 0; b < a->nb; b++)
             HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * n, t.vals.as<u64>() + (size_t)b * t.cap + r0, n * 8,
                                   hipMemcpyDeviceToHost, s));
@@ -994,18 +1049,30 @@ static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* k
     RCHK(a->g_pre.reserve((n + 1) * 4, false));
     RCHK(a->g_tmp.reserve((size_t)((n + 1 + kTile - 1) / kTile + 16) * 8, false));
     launch_find_rebucket(s, n, bucket, per, start, end, a->g_bucket.as<int64_t>(), a->g_idx.as<u32>(), a->tz);
-    // (bucket, key) order, input order within a group: stable LSD sorts by key, then by bucket
+    // (bucket, key) order, input order within a group: stable LSD sorts by key, then by bucket. Interned
+    // keys sort by their group-by values (signed, last column first), not by their slots
     size_t tb = 0;
     if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, s)) return sh_fail(SH_ERR_DEVICE, "sort sizing");
     RCHK(a->g_sort.reserve(std::max<size_t>(tb, 16), false));
-    launch_find_gather_u64(s, n, a->g_idx.as<u32>(), key, a->g_k64.as<u64>());
-    if (sort_u64_pairs(a->g_sort.p, &tb, a->g_k64.as<u64>(), a->g_k64s.as<u64>(), a->g_idx.as<u32>(), a->g_idx1.as<u32>(),
-                       n, s))
-        return sh_fail(SH_ERR_DEVICE, "retrieval sort failed");
-    launch_find_gather_u64(s, n, a->g_idx1.as<u32>(), a->g_bucket.as<int64_t>(), a->g_k64.as<u64>());
-    if (sort_u64_pairs(a->g_sort.p, &tb, a->g_k64.as<u64>(), a->g_k64s.as<u64>(), a->g_idx1.as<u32>(),
-                       a->g_idx2.as<u32>(), n, s))
-        return sh_fail(SH_ERR_DEVICE, "retrieval sort failed");
+    u32* idx[3] = {a->g_idx.as<u32>(), a->g_idx1.as<u32>(), a->g_idx2.as<u32>()};
+    int c = 0;
+    auto pass = [&](const int64_t* src, u64 flip) -> int {
+        launch_find_gather_u64(s, n, idx[c], src, a->g_k64.as<u64>(), flip);
+        if (sort_u64_pairs(a->g_sort.p, &tb, a->g_k64.as<u64>(), a->g_k64s.as<u64>(), idx[c], idx[(c + 1) % 3], n, s))
+            return sh_fail(SH_ERR_DEVICE, "retrieval sort failed");
+        c = (c + 1) % 3;
+        return SH_OK;
+    };
+    if (a->intern) {
+        const int ng = a->d.n_group_by;
+        RCHK(a->g_dk.reserve((size_t)ng * n * 8, false));
+        launch_agg_unintern(s, key, n, a->ikt.dev(), a->ikp, a->g_dk.as<int64_t>());
+        for (int x = ng - 1; x >= 0; x--) RCHK(pass(a->g_dk.as<int64_t>() + (size_t)x * n, 1ull << 63));
+    } else {
+        RCHK(pass(key, 0));
+    }
+    RCHK(pass(a->g_bucket.as<int64_t>(), 0));
+    if (c != 2) HIPCHK(hipMemcpyAsync(idx[2], idx[c], n * 4, hipMemcpyDeviceToDevice, s));
     launch_find_starts(s, n, a->g_idx2.as<u32>(), a->g_bucket.as<int64_t>(), key, a->g_flag.as<u32>());
     HIPCHK(hipMemcpyAsync(a->g_pre.p, a->g_flag.p, (n + 1) * 4, hipMemcpyDeviceToDevice, s));
     launch_scan_sum_large_u32(s, a->g_pre.as<u32>(), n + 1, a->g_tmp.as<int64_t>());
@@ -1133,7 +1200,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
         const int64_t vcap = std::max<int64_t>(nr, 1);
         HIPCHK(hipMemcpyAsync(o.ts.data(), a->v_bucket.p, nr * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(o.keys.data(), a->v_bucket.p, nr * 8, hipMemcpyDeviceToHost, s));
-        if (nk > 1) HIPCHK(hipMemcpyAsync(o.keys.data() + nr, a->v_key.p, nr * 8, hipMemcpyDeviceToHost, s));
+        if (nk > 1) RCHK(agg_keys_out(a, a->v_key.as<int64_t>(), nr, o.keys.data() + nr));
         for (int b = 0; b < nb; b++)
             HIPCHK(hipMemcpyAsync(o.vals.data() + (size_t)b * nr, a->v_vals.as<u64>() + (size_t)b * vcap, nr * 8,
                                   hipMemcpyDeviceToHost, s));
@@ -1259,6 +1326,11 @@ static int agg_state_write(sh_aggregation* a, ABlob& w) {
         RCHK(w.dev(t.key.p, t.n * 8, s));
         for (int b = 0; b < a->nb; b++) RCHK(w.dev(t.vals.as<u64>() + (size_t)b * t.cap, t.n * 8, s));
     }
+    if (a->intern) {  // the interned group keys (their slots are the root's and the tables' keys)
+        RCHK(a->ikt.check(s));
+        w.val<int64_t>(a->ikt.n_keys);
+        RCHK(w.dev(a->ikt.keys.p, a->ikt.size_ * 8, s));
+    }
     return SH_OK;
 }
 
@@ -1340,6 +1412,17 @@ static int agg_state_read(sh_aggregation* a, AReader& r) {
         for (int b = 0; b < a->nb; b++) RCHK(r.dev(t.vals.as<u64>() + (size_t)b * t.cap, n * 8, s));
         t.n = n;
         t.drained = drained;
+    }
+    if (a->intern) {
+        const int64_t nk = r.val<int64_t>();
+        if (!r.ok || nk < 0 || nk > (int64_t)a->ikt.size_ + 1) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        RCHK(r.dev(a->ikt.keys.p, (int64_t)a->ikt.size_ * 8, s));
+        RCHK(a->ikt.h_ctrl.reserve(16));
+        uint32_t* c = a->ikt.h_ctrl.as<uint32_t>();
+        c[0] = (uint32_t)nk; c[1] = c[2] = c[3] = 0;
+        HIPCHK(hipMemcpyAsync(a->ikt.ctrl.p, c, 16, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        a->ikt.n_keys = nk;
     }
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;

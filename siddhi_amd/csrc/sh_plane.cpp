@@ -45,7 +45,7 @@ static int fill(DevBuf& b, size_t bytes, int v) {
 
 int plane_create(sh_query* q) {
     SlidingImpl* s = q->sl;
-    s->lane = q->plane_sorted ? 3 : q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
+    s->lane = q->plane_tbsc ? 4 : q->plane_sorted ? 3 : q->d.window == SH_WIN_LENGTH_BATCH ? 1 : 2;
     s->nk_out = q->d.n_group_by;
     const size_t n = (size_t)s->nslots;
     RCHK(fill(s->pl_last_ts, n * 8, 0x80));  // lastTimestamp = Long.MIN_VALUE (0x8080... < any real ts)
@@ -63,6 +63,14 @@ int plane_create(sh_query* q) {
         RCHK(fill(s->pg_dq_len, F * s->pg_st_n * 8, 0));
         RCHK(fill(s->pg_dq_pool, 64, 0));
         s->pg_dq_words = 0;
+    }
+    if (s->lane == 4) {
+        // the (partition, group) states: batch number 0, count 0, no value
+        const size_t ns = q->pgkt.size_ + 1, A = (size_t)std::max(1, q->ap.n);
+        RCHK(fill(s->tb_cnt, ns * 8, 0));
+        RCHK(fill(s->tb_bid, ns * 8, 0));
+        RCHK(fill(s->tb_f, A * ns * 8, 0));
+        RCHK(fill(s->tb_has, A * ns, 0));
     }
     if (q->d.window == SH_WIN_EXT_TIME_BATCH) {
         RCHK(fill(s->pg_M, n * 8, 0));
@@ -742,6 +750,281 @@ static int plane_run_group(sh_query* q, const sh_batch* b, int64_t now, bool hos
     return sliding_output(q, n_rows, n_flushes, false, host_out, out);
 }
 
+// ---- lane 4: `partition with (p of S) begin from S#window.timeBatch(T[, start], true) select g…, aggs
+// group by g… insert [current] events into O; end` (TimeBatchWindowProcessor.process :262-340 per partition
+// state, nextEmitTime a processor field shared by the partitions, :128). Every partition chunk goes out at
+// once with its groups' running values; a partition's state is RESET by its own chunk or TIMER that finds
+// the playback clock at or past nextEmitTime — that chunk advances nextEmitTime and schedules the next
+// TIMER under its own partition (so the TIMERs stay with the first partition while events keep coming, and
+// pass to whichever partition meets a lagging nextEmitTime after an idle stretch). The host walks those
+// calls (the Scheduler as in the other lanes); the device folds every (partition, group) state.
+static int tb_register(sh_query* q, uint32_t p, int64_t t, std::vector<int64_t>& slot_key) {
+    SlidingImpl* s = q->sl;
+    if (s->pl_flow.find(p) == s->pl_flow.end() && slot_key.empty()) {
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        RCHK(d2h(q, slot_key, s->pl_key.p, s->nslots));
+    }
+    return sched_register(q, p, t, slot_key);
+}
+
+// the window's send check at `clock` for partition p (:266-281): true when p's state is RESET
+static int tb_check(sh_query* q, uint32_t p, int64_t clock, std::vector<int64_t>& slot_key, bool* reset) {
+    SlidingImpl* s = q->sl;
+    const int64_t T = q->d.window_param;
+    *reset = false;
+    if (s->tb_next_emit == -1) {
+        s->tb_next_emit = q->d.has_start_time ? clock + (T - (clock - q->d.start_time) % T) : clock + T;
+        RCHK(tb_register(q, p, s->tb_next_emit, slot_key));
+    }
+    if (clock >= s->tb_next_emit) {
+        s->tb_next_emit += T;
+        RCHK(tb_register(q, p, s->tb_next_emit, slot_key));
+        *reset = true;
+    }
+    return SH_OK;
+}
+
+static int plane_run_tbsc(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
+    SlidingImpl* s = q->sl;
+    hipStream_t st = q->ctx->stream;
+    q->stats = sh_stats{};
+    std::vector<int64_t> slot_key;
+    if (!b) {
+        // a TIMER call: the due partition's window RESETs (no row: its current events went out already)
+        if (q->clock_valid && now < q->clock) return empty_out(q, out);
+        q->clock = now;
+        q->clock_valid = true;
+        if (!s->pl_armed.empty() && s->pl_armed.begin()->first <= now)
+            RCHK(sched_fire(s, now, [&](uint32_t p, int64_t) -> int {
+                bool r;
+                RCHK(tb_check(q, p, now, slot_key, &r));
+                if (r) s->tb_bids[p]++;
+                return SH_OK;
+            }));
+        return empty_out(q, out);
+    }
+    const int64_t N = b->n, ss = b->send_size;
+    const int V = std::max(1, q->ap.n_vcols), na = q->ap.n;
+    if (N >= (int64_t)0x3FFFFFF0ll) return sh_fail(SH_ERR_INVALID, "push larger than 1G events");
+    HIPCHK(hipEventRecord(q->ev_push0, st));
+    const int64_t cap = std::max<int64_t>(N, 1);
+    RCHK(s->rec_raw.reserve(cap * 4, false));
+    RCHK(s->rec_slot.reserve(cap * 4, false));
+    RCHK(s->rec_clock.reserve(cap * 8, false));
+    RCHK(s->rec_pm.reserve(cap * 8, false));
+    RCHK(s->rec_ts.reserve(cap * 8, false));
+    RCHK(s->rec_vals.reserve((size_t)V * cap * 8, false));
+    RCHK(s->slot_cnt.reserve(s->nslots * 4, false));
+    HIPCHK(hipMemsetAsync(s->slot_cnt.p, 0, s->nslots * 4, st));
+    SlRecords rec{s->rec_raw.as<u32>(), s->rec_slot.as<u32>(), s->rec_clock.as<int64_t>(), s->rec_pm.as<int64_t>(),
+                  s->rec_ts.as<int64_t>(), s->rec_vals.as<u64>(), cap};
+    ColSet cs{};
+    cs.n = q->d.n_cols;
+    for (int c = 0; c < q->d.n_cols; c++) { cs.type[c] = q->d.col_types[c]; cs.ptr[c] = b->cols[c]; }
+    const int nblk = (int)((N + kTile - 1) / kTile);
+    RCHK(s->blk_pass.reserve(nblk * 8, false));
+    RCHK(s->blk_tl.reserve(nblk * 8, false));
+    RCHK(s->blk_pm.reserve(nblk * 8, false));
+    WinParams wp{};
+    wp.kind = SH_WIN_TIME;  // the clock / pass-count prefix of the sliding path
+    wp.clock_valid = q->clock_valid;
+    wp.clock0 = q->clock;
+    wp.send_size = ss;
+    wp.N = N;
+    wp.rec_seq = q->tune.sl_records_seq;
+    launch_sl_prefix(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(),
+                     s->blk_pm.as<int64_t>(), nblk, s->info.as<SlInfo>());
+    launch_sl_records(st, b->ts, cs, q->fp, wp, q->kp, q->kt.dev(), q->ap, s->blk_pass.as<int64_t>(),
+                      s->blk_tl.as<int64_t>(), s->blk_pm.as<int64_t>(), s->pm, rec, s->slot_cnt.as<u32>(), nblk);
+    launch_pl_slot_key(st, cs, q->kp, q->kt.dev(), N, s->pl_key.as<int64_t>());
+    // partition runs over every event (the receiver cuts a send at key changes, before the filter)
+    RCHK(s->tb_start.reserve(cap + 16, false));
+    RCHK(s->tb_run.reserve(cap * 8, false));
+    RCHK(s->tb_blk.reserve((size_t)(nblk + 16) * 8, false));
+    launch_pl_runs(st, cs, q->d.partition_col, N, ss, s->tb_start.as<unsigned char>(), s->tb_blk.as<int64_t>(),
+                   s->tb_run.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(s->h_info, s->info.p, sizeof(SlInfo), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    RCHK(q->kt.check(st));
+    const SlInfo info = *s->h_info;
+    const int64_t M = info.total_pass;
+    // the push's calls (a send whose last event does not move the clock calls nobody)
+    std::vector<int64_t> calls_s, calls_c;
+    {
+        const int64_t NS = ss > 0 ? (N + ss - 1) / ss : 1;
+        const int nbS = (int)((NS + kTile - 1) / kTile);
+        RCHK(s->x_sK.reserve(NS * 8, false));
+        RCHK(s->x_scb.reserve(NS * 8, false));
+        RCHK(s->x_slast.reserve(NS * 8, false));
+        RCHK(s->x_cK.reserve(NS * 8, false));
+        RCHK(s->x_cC.reserve(NS * 8, false));
+        RCHK(s->x_cS.reserve(NS * 8, false));
+        RCHK(s->x_blk.reserve((size_t)((std::max(NS, M) + kTile - 1) / kTile + 2) * 8, false));
+        launch_slx_sends(st, b->ts, cs, q->fp, wp, s->blk_pass.as<int64_t>(), s->blk_tl.as<int64_t>(), nblk,
+                         s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>());
+        launch_slx_compact(st, 0, nullptr, s->x_sK.as<int64_t>(), s->x_scb.as<int64_t>(), s->x_slast.as<int64_t>(), NS,
+                           s->x_blk.as<int64_t>(), s->x_cK.as<int64_t>(), s->x_cC.as<int64_t>(), s->x_cS.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        int64_t nC = 0;
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + nbS, &nC));
+        RCHK(d2h(q, calls_s, s->x_cS.p, nC));
+        RCHK(d2h(q, calls_c, s->x_cC.p, nC));
+    }
+    // the chunks (partition runs with passing events) and their partition, send and clock
+    int64_t nch = 0;
+    std::vector<int64_t> ch_send, ch_clk, ch_bid;
+    std::vector<uint32_t> ch_slot;
+    if (M > 0) {
+        RCHK(s->tb_flag.reserve(M + 16, false));
+        RCHK(s->tb_first.reserve(M * 8, false));
+        launch_tb_chunk_flags(st, rec, M, s->tb_run.as<int64_t>(), s->tb_flag.as<unsigned char>());
+        launch_slx_compact(st, 1, s->tb_flag.as<unsigned char>(), nullptr, nullptr, nullptr, M, s->x_blk.as<int64_t>(),
+                           nullptr, nullptr, s->tb_first.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (M + kTile - 1) / kTile, &nch));
+        RCHK(s->tb_cslot.reserve(nch * 4 + 16, false));
+        RCHK(s->tb_csend.reserve(nch * 8 + 16, false));
+        RCHK(s->tb_cclk.reserve(nch * 8 + 16, false));
+        launch_tb_chunk_info(st, rec, s->tb_first.as<int64_t>(), nch, ss, s->tb_cslot.as<u32>(), s->tb_csend.as<int64_t>(),
+                             s->tb_cclk.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        ch_slot.resize((size_t)nch);
+        HIPCHK(hipMemcpyAsync(ch_slot.data(), s->tb_cslot.p, nch * 4, hipMemcpyDeviceToHost, st));
+        RCHK(d2h(q, ch_send, s->tb_csend.p, nch));
+    }
+    // ---- the walk: each call's TIMERs, then the chunks of the sends before the next call
+    ch_bid.resize((size_t)nch);
+    int64_t clock = q->clock_valid ? q->clock : INT64_MIN;
+    size_t k = 0;
+    auto chunks_before = [&](int64_t send_end) -> int {
+        for (; k < (size_t)nch && ch_send[k] < send_end; k++) {
+            const uint32_t p = ch_slot[k];
+            bool r;
+            RCHK(tb_check(q, p, clock, slot_key, &r));
+            int64_t& bid = s->tb_bids[p];
+            ch_bid[k] = bid;
+            if (r) bid++;  // (the RESET follows the chunk's events: they went out with the old state)
+        }
+        return SH_OK;
+    };
+    for (size_t c = 0; c < calls_s.size(); c++) {
+        RCHK(chunks_before(calls_s[c]));
+        clock = calls_c[c];
+        if (!s->pl_armed.empty() && s->pl_armed.begin()->first <= clock)
+            RCHK(sched_fire(s, clock, [&](uint32_t p, int64_t) -> int {
+                bool r;
+                RCHK(tb_check(q, p, clock, slot_key, &r));
+                if (r) s->tb_bids[p]++;
+                return SH_OK;
+            }));
+    }
+    RCHK(chunks_before(INT64_MAX));
+    int64_t n_rows = 0, n_flushes = 0;
+    if (M > 0) {
+        RCHK(s->tb_chbid.reserve(nch * 8 + 16, false));
+        HIPCHK(hipMemcpyAsync(s->tb_chbid.p, ch_bid.data(), nch * 8, hipMemcpyHostToDevice, st));
+        RCHK(s->tb_chunk_of.reserve(M * 8, false));
+        launch_tb_chunk_of(st, s->tb_first.as<int64_t>(), nch, M, s->tb_chunk_of.as<int64_t>());
+        RCHK(s->tb_pair.reserve(M * 4, false));
+        RCHK(s->tb_gslot.reserve(M * 4, false));
+        launch_tb_pairs(st, rec, M, cs, q->gkp, q->gkt.dev(), q->pgkt.dev(), s->tb_pair.as<u32>(), s->tb_gslot.as<u32>());
+        HIPCHK(hipGetLastError());
+        RCHK(q->gkt.check(st));
+        RCHK(q->pgkt.check(st));
+        // ---- the records by (partition, group) state, stably
+        const int64_t nst = (int64_t)q->pgkt.size_ + 1;
+        RCHK(s->tb_skey.reserve(M * 4, false));
+        RCHK(s->tb_sidx.reserve(M * 4, false));
+        size_t tb = 0;
+        if (sort_slot_ranks(nullptr, &tb, s->tb_pair.as<u32>(), nullptr, nullptr, M, nst, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_slot_ranks(s->sort_tmp.p, &tb, s->tb_pair.as<u32>(), s->tb_skey.as<u32>(), s->tb_sidx.as<u32>(), M, nst,
+                            st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        RCHK(s->tb_head.reserve(M + 16, false));
+        RCHK(s->tb_seg.reserve(M * 8, false));
+        launch_pg_heads32(st, s->tb_skey.as<u32>(), M, s->tb_head.as<unsigned char>());
+        launch_slx_compact(st, 1, s->tb_head.as<unsigned char>(), nullptr, nullptr, nullptr, M, s->x_blk.as<int64_t>(),
+                           nullptr, nullptr, s->tb_seg.as<int64_t>());
+        HIPCHK(hipGetLastError());
+        int64_t n_seg = 0;
+        RCHK(read_count(q, s->x_blk.as<int64_t>() + (M + kTile - 1) / kTile, &n_seg));
+        // ---- a row per (chunk, group): the states fold their records from the carried values
+        const int64_t rc = M;
+        RCHK(s->xr_ts.reserve(rc * 8, false));
+        RCHK(s->xr_rep.reserve(rc * 8, false));
+        RCHK(s->xr_slot.reserve(rc * 4, false));
+        RCHK(s->xr_ch.reserve(rc * 8, false));
+        RCHK(s->xr_clk.reserve(rc * 8, false));
+        RCHK(s->xr_exp.reserve(rc, false));
+        RCHK(s->xr_vals.reserve((size_t)std::max(na, 1) * rc * 8, false));
+        RCHK(s->xr_nulls.reserve((size_t)std::max(na, 1) * rc, false));
+        RCHK(s->tb_rkey.reserve(rc * 8, false));
+        RCHK(s->tb_rkey2.reserve(rc * 8, false));
+        RCHK(s->tb_order.reserve(rc * 4, false));
+        RCHK(s->pg_rpart.reserve(rc * 4, false));
+        RCHK(s->out_part.reserve(rc * 4, false));
+        RCHK(s->tb_nrows.reserve(16, false));
+        HIPCHK(hipMemsetAsync(s->tb_nrows.p, 0, 8, st));
+        SlxRows rows{s->xr_ts.as<int64_t>(), s->xr_rep.as<int64_t>(), s->xr_slot.as<u32>(), s->xr_ch.as<int64_t>(),
+                     s->xr_clk.as<int64_t>(), s->xr_exp.as<unsigned char>(), s->xr_vals.as<u64>(),
+                     s->xr_nulls.as<unsigned char>(), rc};
+        TbState S{s->tb_cnt.as<int64_t>(), s->tb_bid.as<int64_t>(), s->tb_f.as<u64>(), s->tb_has.as<unsigned char>(), nst};
+        HIPCHK(hipEventRecord(q->ev_agg0, st));
+        launch_tb_fold(st, s->tb_seg.as<int64_t>(), n_seg, M, s->tb_skey.as<u32>(), s->tb_sidx.as<u32>(), rec,
+                       s->tb_chunk_of.as<int64_t>(), s->tb_chbid.as<int64_t>(), s->tb_gslot.as<u32>(), q->ap, S,
+                       s->tb_chunk_base, rows, s->tb_rkey.as<u64>(), s->pg_rpart.as<u32>(),
+                       s->tb_nrows.as<unsigned int>(), q->seq);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(q->ev_agg1, st));
+        RCHK(read_count(q, s->tb_nrows.as<int64_t>(), &n_rows));
+        n_rows &= 0xFFFFFFFFll;
+        // ---- rows in (chunk, first record) order -> the output columns
+        const unsigned rbits = (unsigned)(32 + bits_for(nch + 1));
+        tb = 0;
+        if (sort_u64_iota_bits(nullptr, &tb, s->tb_rkey.as<u64>(), nullptr, nullptr, n_rows, rbits, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
+        RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
+        if (sort_u64_iota_bits(s->sort_tmp.p, &tb, s->tb_rkey.as<u64>(), s->tb_rkey2.as<u64>(), s->tb_order.as<u32>(),
+                               n_rows, rbits, st))
+            return sh_fail(SH_ERR_DEVICE, "radix sort failed");
+        const int64_t oc = std::max<int64_t>(n_rows, 1);
+        RCHK(s->out_ts.reserve(oc * 8, false));
+        RCHK(s->out_keys.reserve((size_t)std::max(1, q->gkp.n) * oc * 8, false));
+        RCHK(s->out_vals.reserve((size_t)std::max(na, 1) * oc * 8, false));
+        RCHK(s->out_nulls.reserve((size_t)std::max(na, 1) * oc, false));
+        RCHK(s->out_send.reserve(oc * 8, false));
+        RCHK(s->out_clock.reserve(oc * 8, false));
+        RCHK(s->out_expired.reserve(oc, false));
+        RCHK(s->out_rep.reserve(oc * 8, false));
+        launch_pg_emit(st, s->tb_order.as<u32>(), n_rows, rows, na, s->nk_out, q->gkt.dev(), q->gkp, n_rows,
+                       s->out_ts.as<int64_t>(), s->out_keys.as<int64_t>(), s->out_vals.as<u64>(),
+                       s->out_nulls.as<unsigned char>(), s->out_expired.as<unsigned char>(), s->out_send.as<int64_t>(),
+                       s->out_clock.as<int64_t>(), s->out_rep.as<int64_t>(), s->pg_rpart.as<u32>(),
+                       s->out_part.as<u32>());
+        HIPCHK(hipGetLastError());
+        float kms = 0;
+        (void)hipEventSynchronize(q->ev_agg1);
+        (void)hipEventElapsedTime(&kms, q->ev_agg0, q->ev_agg1);
+        q->stats.main_kernel_ms = kms;
+        RCHK(sliding_flushes(q, n_rows, &n_flushes));
+        s->tb_chunk_base += nch;
+    }
+    q->seq += N;
+    q->clock = q->clock_valid ? std::max(q->clock, info.max_tl) : info.max_tl;
+    q->clock_valid = true;
+    q->stats.events = N;
+    HIPCHK(hipEventRecord(q->ev_push1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, q->ev_push0, q->ev_push1);
+    q->stats.push_ms = ms;
+    q->stats.main_kernel_bytes = M * (int64_t)(16 + 8 * V) + n_rows * (int64_t)(8 + 8 * na);
+    return sliding_output(q, n_rows, n_flushes, false, host_out, out);
+}
+
 // Time / externalTime lanes grouped by other columns (sh_plane_group_kernels.hip, k_pg_walk_ops /
 // k_pg_replay): the partitions' walks write their add / remove operations, the operations sorted stably
 // by (partition, group) state are replayed one thread per state, rows sorted by (chunk, first operation).
@@ -985,6 +1268,7 @@ const u32* plane_out_part(sh_query* q) { return q->sl->out_part.as<u32>(); }
 static int plane_run(sh_query* q, const sh_batch* b, int64_t now, bool host_out, const sh_out** out) {
     SlidingImpl* s = q->sl;
     if (s->lane == 3) return plane_run_group(q, b, now, host_out, out);
+    if (s->lane == 4) return plane_run_tbsc(q, b, now, host_out, out);
     hipStream_t st = q->ctx->stream;
     q->stats = sh_stats{};
     // (externalTime lanes: the window runs on the timestamp attribute, no TIMER calls reach it)
@@ -1514,6 +1798,32 @@ int plane_host_save(sh_query* q, std::vector<uint8_t>& out) {
             HIPCHK(hipStreamSynchronize(q->ctx->stream));
         }
     }
+    if (s->lane == 4) {
+        // partitioned timeBatch(T, true): the group and (partition, group) tables, the shared nextEmitTime,
+        // every partition's RESET count and the states
+        RCHK(table_save(q, q->gkt, out));
+        RCHK(table_save(q, q->pgkt, out));
+        std::vector<uint32_t> sl;
+        for (auto& kv : s->tb_bids) sl.push_back(kv.first);
+        std::sort(sl.begin(), sl.end());
+        const uint64_t nb = sl.size();
+        put(&s->tb_next_emit, 8);
+        put(&s->tb_chunk_base, 8);
+        put(&nb, 8);
+        for (uint32_t x : sl) {
+            put(&x, 4);
+            put(&s->tb_bids[x], 8);
+        }
+        const size_t ns = q->pgkt.size_ + 1, A = (size_t)std::max(1, q->ap.n);
+        const std::pair<const DevBuf*, size_t> bufs[] = {{&s->tb_cnt, ns * 8}, {&s->tb_bid, ns * 8},
+                                                         {&s->tb_f, A * ns * 8}, {&s->tb_has, A * ns}};
+        for (auto& b : bufs) {
+            const size_t o = out.size();
+            out.resize(o + b.second);
+            HIPCHK(hipMemcpyAsync(out.data() + o, b.first->p, b.second, hipMemcpyDeviceToHost, q->ctx->stream));
+        }
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+    }
     return s->lane == 3 ? pg_save(q, out) : SH_OK;
 }
 
@@ -1569,6 +1879,37 @@ int plane_host_load(sh_query* q, const uint8_t* p, size_t n, size_t* used) {
         HIPCHK(hipStreamSynchronize(q->ctx->stream));
         s->pg_dq_words = (int64_t)w;
         o += w * 8;
+    }
+    if (s->lane == 4) {
+        size_t u = 0;
+        RCHK(table_load(q, q->gkt, p + o, n - o, &u));
+        o += u;
+        RCHK(table_load(q, q->pgkt, p + o, n - o, &u));
+        o += u;
+        int64_t ne = 0, cb = 0;
+        uint64_t nb = 0;
+        if (!get(&ne, 8) || !get(&cb, 8) || !get(&nb, 8) || nb > (n - o) / 12)
+            return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        std::unordered_map<uint32_t, int64_t> bids;
+        for (uint64_t i = 0; i < nb; i++) {
+            uint32_t x = 0;
+            int64_t v = 0;
+            get(&x, 4);
+            get(&v, 8);
+            bids[x] = v;
+        }
+        const size_t ns = q->pgkt.size_ + 1, A = (size_t)std::max(1, q->ap.n);
+        const std::pair<DevBuf*, size_t> bufs[] = {{&s->tb_cnt, ns * 8}, {&s->tb_bid, ns * 8}, {&s->tb_f, A * ns * 8},
+                                                   {&s->tb_has, A * ns}};
+        for (auto& b : bufs) {
+            if (o + b.second > n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+            HIPCHK(hipMemcpyAsync(b.first->p, p + o, b.second, hipMemcpyHostToDevice, q->ctx->stream));
+            o += b.second;
+        }
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+        s->tb_next_emit = ne;
+        s->tb_chunk_base = cb;
+        s->tb_bids = std::move(bids);
     }
     size_t pg_used = 0;
     if (s->lane == 3) {

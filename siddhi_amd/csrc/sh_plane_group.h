@@ -141,5 +141,23 @@ void launch_pg_heads32(hipStream_t s, const u32* key, i64 n, unsigned char* head
 void launch_pg_sum_u32(hipStream_t s, const u32* a, i64 n, unsigned long long* out);
 int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,
                        unsigned end_bit, hipStream_t s);
+// partitioned timeBatch(T, true) (lane 4): per (partition, group) state — batch number, count and per
+// aggregator its running value and has-flag ([a][n] layouts)
+struct TbState {
+    i64* cnt;
+    i64* bid;
+    u64* f;
+    unsigned char* has;
+    i64 n;
+};
+void launch_tb_chunk_flags(hipStream_t s, SlRecords rec, i64 M, const i64* run, unsigned char* flag);
+void launch_tb_chunk_info(hipStream_t s, SlRecords rec, const i64* first, i64 nch, i64 send_size, u32* slot, i64* send,
+                          i64* clock);
+void launch_tb_chunk_of(hipStream_t s, const i64* first, i64 nch, i64 M, i64* chunk_of);
+void launch_tb_pairs(hipStream_t s, SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt, KeyTable pgkt,
+                     u32* pair, u32* gslot);
+void launch_tb_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 M, const u32* skey, const u32* sidx,
+                    SlRecords rec, const i64* chunk_of, const i64* chunk_bid, const u32* gslot, AggPlan ap, TbState S,
+                    i64 chunk_base, SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows, i64 seq_base);
 
 }  // namespace shd

@@ -1143,3 +1143,187 @@ void launch_pg_rehash(hipStream_t s, KeyTable okt, i64 on, const i64* cnt, const
 }
 
 }  // namespace shd
+
+namespace shd {
+
+// ==== partitioned timeBatch(T, true) — stream.current.event, current output (lane 4) ==================
+// TimeBatchWindowProcessor.process (:262-340) per partition: every partition chunk (its run of events
+// in a send, PartitionStreamReceiver.receive :176-272) goes out at once with the running aggregates of
+// its groups; a partition's state is RESET only when its own chunk or TIMER finds the playback clock
+// past the shared nextEmitTime (a processor field, :128) — the host walks those calls (sh_plane.cpp
+// tbsc_walk) and gives every chunk its partition's batch number. Here: per record its chunk, its
+// (partition, group) state slot; one thread per state folds its records in stream order from the
+// carried state (a new batch number starts fresh) and writes a row per (chunk, group) after the group's
+// last record of the chunk.
+
+// a chunk starts at the first passing record of a partition run (runs: k_pl_run_start over all events)
+__global__ __launch_bounds__(kBlock) void k_tb_chunk_flags(SlRecords rec, i64 M, const i64* __restrict__ run,
+                                                          unsigned char* flag) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= M) return;
+    flag[r] = r == 0 || run[rec.raw[r]] != run[rec.raw[r - 1]];
+}
+
+void launch_tb_chunk_flags(hipStream_t s, SlRecords rec, i64 M, const i64* run, unsigned char* flag) {
+    if (M > 0)
+        hipLaunchKernelGGL(k_tb_chunk_flags, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M,
+                           run, flag);
+}
+
+// per chunk (its first record r): partition slot, send number, clock
+__global__ __launch_bounds__(kBlock) void k_tb_chunk_info(SlRecords rec, const i64* __restrict__ first, i64 nch,
+                                                         i64 send_size, u32* slot, i64* send, i64* clock) {
+    const i64 k = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nch) return;
+    const i64 r = first[k];
+    slot[k] = rec.slot[r];
+    send[k] = send_size > 0 ? (i64)rec.raw[r] / send_size : 0;
+    clock[k] = rec.clock[r];
+}
+
+void launch_tb_chunk_info(hipStream_t s, SlRecords rec, const i64* first, i64 nch, i64 send_size, u32* slot, i64* send,
+                          i64* clock) {
+    if (nch > 0)
+        hipLaunchKernelGGL(k_tb_chunk_info, dim3((unsigned)((nch + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec,
+                           first, nch, send_size, slot, send, clock);
+}
+
+// per record its chunk: the last chunk whose first record is at or before it
+__global__ __launch_bounds__(kBlock) void k_tb_chunk_of(const i64* __restrict__ first, i64 nch, i64 M, i64* chunk_of) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= M) return;
+    i64 lo = 0, hi = nch;
+    while (hi - lo > 1) {
+        const i64 mid = (lo + hi) >> 1;
+        if (first[mid] <= r) lo = mid;
+        else hi = mid;
+    }
+    chunk_of[r] = lo;
+}
+
+void launch_tb_chunk_of(hipStream_t s, const i64* first, i64 nch, i64 M, i64* chunk_of) {
+    if (M > 0)
+        hipLaunchKernelGGL(k_tb_chunk_of, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, first, nch, M,
+                           chunk_of);
+}
+
+// per record: its chunk (inclusive count of chunk starts - 1, from the flags' scan), its group slot and
+// its (partition, group) state slot
+__global__ __launch_bounds__(kBlock) void k_tb_pairs(SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt,
+                                                    KeyTable pgkt, u32* pair, u32* gslot) {
+    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= M) return;
+    const u32 g = gkp.n ? key_slot(gkt, make_key(gkp, cols, rec.raw[r])) : 0u;
+    gslot[r] = g;
+    pair[r] = key_slot(pgkt, ((u64)rec.slot[r] << 32) | g);
+}
+
+void launch_tb_pairs(hipStream_t s, SlRecords rec, i64 M, ColSet cols, KeyPlan gkp, KeyTable gkt, KeyTable pgkt,
+                     u32* pair, u32* gslot) {
+    if (M > 0)
+        hipLaunchKernelGGL(k_tb_pairs, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, rec, M, cols, gkp,
+                           gkt, pgkt, pair, gslot);
+}
+
+// one thread per state segment of the records sorted stably by state slot (sidx: record indices)
+template <int NA>
+__global__ __launch_bounds__(64) void k_tb_fold(const i64* __restrict__ seg_start, i64 n_seg, i64 M,
+                                               const u32* __restrict__ skey, const u32* __restrict__ sidx, SlRecords rec,
+                                               const i64* __restrict__ chunk_of, const i64* __restrict__ chunk_bid,
+                                               const u32* __restrict__ gslot, AggPlan ap, TbState S, i64 chunk_base,
+                                               SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows,
+                                               i64 seq_base) {
+    const i64 t = (i64)blockIdx.x * 64 + threadIdx.x;
+    if (t >= n_seg) return;
+    const i64 lo = seg_start[t], hi = t + 1 < n_seg ? seg_start[t + 1] : M;
+    const u32 st = skey[lo];
+    i64 cnt = S.cnt[st], bid = S.bid[st];
+    u64 f[NA];
+    unsigned char h[NA];
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        f[a] = a < ap.n ? S.f[(size_t)a * S.n + st] : 0;
+        h[a] = a < ap.n ? S.has[(size_t)a * S.n + st] : 0;
+    }
+    i64 first_r = -1;
+    for (i64 i = lo; i < hi; i++) {
+        const u32 r = sidx[i];
+        const i64 ch = chunk_of[r];
+        const i64 b = chunk_bid[ch];
+        if (b != bid) {  // a RESET of the partition since the state's last event: fresh state
+            bid = b;
+            cnt = 0;
+#pragma unroll
+            for (int a = 0; a < NA; a++) { f[a] = 0; h[a] = 0; }
+        }
+        if (first_r < 0) first_r = r;
+        cnt++;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            if (kind == AK_COUNT) continue;
+            const u64 x = rec.vals[(size_t)ap.vcol[a] * rec.cap + r];
+            if (kind == AK_SUM_L) {
+                f[a] = (u64)((i64)f[a] + (i64)x);
+                h[a] = 1;
+            } else if (kind == AK_SUM_D || kind == AK_AVG) {
+                f[a] = (u64)__double_as_longlong((h[a] ? __longlong_as_double((i64)f[a]) : 0.0) + g_num(ap, a, x));
+                h[a] = 1;
+            } else {
+                const bool take = !h[a] || g_worse(kind, f[a], x);
+                f[a] = take ? x : f[a];
+                h[a] = 1;
+            }
+        }
+        const bool last = i + 1 == hi || chunk_of[sidx[i + 1]] != ch;
+        if (!last) continue;
+        // the group's row of this chunk: its last event carrying the running values (QuerySelector
+        // .processInBatchGroupBy :315-374: LinkedHashMap.put keeps the group's first position)
+        const u32 o = atomicAdd(n_rows, 1u);
+        rows.ts[o] = rec.ts[r];
+        rows.rep[o] = seq_base + (i64)rec.raw[r];
+        rows.slot[o] = gslot[r];
+        rows.ch[o] = chunk_base + ch;
+        rows.clk[o] = rec.clock[r];
+        rows.exp[o] = 0;
+        row_part[o] = rec.slot[r];
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            if (a >= ap.n) continue;
+            const int kind = ap.kind[a];
+            u64 rv = 0;
+            unsigned char rn = 0;
+            if (kind == AK_COUNT) rv = (u64)cnt;
+            else if (kind == AK_AVG) rv = (u64)__double_as_longlong(__longlong_as_double((i64)f[a]) / (double)cnt);
+            else { rv = f[a]; rn = h[a] ? 0 : 1; }
+            rows.vals[(size_t)a * rows.cap + o] = rv;
+            rows.nulls[(size_t)a * rows.cap + o] = rn;
+        }
+        row_key[o] = ((u64)ch << 32) | (u64)(u32)first_r;
+        first_r = -1;
+    }
+    S.cnt[st] = cnt;
+    S.bid[st] = bid;
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+        if (a >= ap.n) continue;
+        S.f[(size_t)a * S.n + st] = f[a];
+        S.has[(size_t)a * S.n + st] = h[a];
+    }
+}
+
+void launch_tb_fold(hipStream_t s, const i64* seg_start, i64 n_seg, i64 M, const u32* skey, const u32* sidx,
+                    SlRecords rec, const i64* chunk_of, const i64* chunk_bid, const u32* gslot, AggPlan ap, TbState S,
+                    i64 chunk_base, SlxRows rows, u64* row_key, u32* row_part, unsigned int* n_rows, i64 seq_base) {
+    if (n_seg <= 0) return;
+    const unsigned grid = (unsigned)((n_seg + 63) / 64);
+    if (ap.n <= 4)
+        hipLaunchKernelGGL(k_tb_fold<4>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, M, skey, sidx, rec, chunk_of,
+                           chunk_bid, gslot, ap, S, chunk_base, rows, row_key, row_part, n_rows, seq_base);
+    else
+        hipLaunchKernelGGL(k_tb_fold<8>, dim3(grid), dim3(64), 0, s, seg_start, n_seg, M, skey, sidx, rec, chunk_of,
+                           chunk_bid, gslot, ap, S, chunk_base, rows, row_key, row_part, n_rows, seq_base);
+}
+
+}  // namespace shd

@@ -259,6 +259,7 @@ struct sh_query {
     KeyTableHost pgkt;          // time lanes grouped by other columns: (partition slot, group slot) -> state
     size_t pg_min_size = 0;     // its size at creation (a rebuild never shrinks below it)
     bool group_other = false;   // ... grouped by columns other than the partition key
+    bool plane_tbsc = false;    // lane 4: partitioned timeBatch(T, true), current output
     int P = 1, logP = 0, NL = 0;
     // playback clock + window state
     bool clock_valid = false;

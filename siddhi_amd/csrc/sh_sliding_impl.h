@@ -89,6 +89,12 @@ struct SlidingImpl {
         bool flushed = false;
     };
     std::unordered_map<uint32_t, XtPart> xt_parts;
+    // partitioned timeBatch(T, true) (lane 4): the shared nextEmitTime, every partition's RESET count
+    // (its batch number), the (partition, group) states and the push's scratch
+    int64_t tb_next_emit = -1, tb_chunk_base = 0;
+    std::unordered_map<uint32_t, int64_t> tb_bids;
+    DevBuf tb_cnt, tb_bid, tb_f, tb_has, tb_run, tb_start, tb_blk, tb_flag, tb_first, tb_cslot, tb_csend, tb_cclk,
+        tb_chunk_of, tb_chbid, tb_pair, tb_gslot, tb_skey, tb_sidx, tb_seg, tb_head, tb_rkey, tb_rkey2, tb_order, tb_nrows;
     DevBuf xt_kf, xt_em, xt_epos, xt_flag, xt_up;  // partitioned externalTimeBatch, replaceTimestampWithBatchEndTime: rows' batch ends
     DevBuf pg_M, pg_start, pg_has, pg_bopen, pg_pendcnt, pg_xs, pg_xv, pg_ms, pg_cts, pg_err;
     // time lanes grouped by other columns: operation lists, their sort, the (partition, group) states

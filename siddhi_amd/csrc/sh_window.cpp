@@ -239,9 +239,14 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // (partition, group) state (count / sum / avg)
     const bool plane_time_group = d->partition_col >= 0 && (d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
                                   !by_partition && d->n_aggs >= 1;
+    // ... and timeBatch(T, true) (stream.current.event), current output: every partition's chunks go out
+    // with its groups' running values, a partition RESET only where its own chunk or TIMER meets the shared
+    // nextEmitTime (lane 4)
+    const bool plane_tbsc = d->partition_col >= 0 && d->window == SH_WIN_TIME_BATCH && d->stream_current &&
+                            d->n_aggs >= 1 && d->current_on && !d->expired_on;
     const bool plane = (d->partition_col >= 0 &&
                         (d->window == SH_WIN_LENGTH_BATCH || d->window == SH_WIN_TIME || d->window == SH_WIN_EXT_TIME) &&
-                        by_partition) || plane_group || plane_time_group;
+                        by_partition) || plane_group || plane_time_group || plane_tbsc;
     // partitioned timeBatch (R12): only the partition that armed the shared nextEmitTime ever flushes, with
     // its own expired queue (TimeBatchWindowProcessor.process :262-340 per partition state), so its expired
     // / all-events output is the unpartitioned form over that partition's events
@@ -254,10 +259,10 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
                        "externalTime windows (partitioned: timeBatch, lengthBatch, and time grouped by the partition key)");
     // (partitioned: lengthBatch lanes, every event its own chunk of one key)
     if (d->stream_current &&
-        !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH))))
+        !(batch_win && d->n_aggs >= 1 && (d->partition_col < 0 || (plane && d->window == SH_WIN_LENGTH_BATCH) || plane_tbsc)))
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "stream.current.event runs on aggregating lengthBatch / timeBatch windows (partitioned: "
-                       "lengthBatch; grouped by other columns with current output)");
+                       "lengthBatch; grouped by other columns with current output; timeBatch with current output)");
     if (d->partition_col >= 0 && d->window != SH_WIN_TIME_BATCH && !plane)
         return sh_fail(SH_ERR_UNSUPPORTED,
                        "partitioned GPU queries support timeBatch, lengthBatch, externalTimeBatch, and time with no group-by or "
@@ -292,7 +297,8 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     // lane 3: grouped by other columns, or (opt-in, SH_PL_SORT=1) lengthBatch keyed by the partition —
     // the sorted chunks have no per-partition sequential walk, so a hot partition does not serialise
     q->group_other = (plane_group && !by_partition) || plane_time_group;
-    if (plane_time_group) {
+    q->plane_tbsc = plane_tbsc;
+    if (plane_time_group || plane_tbsc) {
         if ((rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, q->gkp))) {
             delete q;
             return rc;
@@ -312,13 +318,13 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (d->n_group_by == 1 && d->group_by[0] == d->partition_col) cap = 1;
     }
     if ((rc = q->kp.dense ? q->kt.init_dense(cap, 1, 0) : q->kt.init(cap))) { delete q; return rc; }
-    if ((q->plane_sorted || plane_time_group) &&
+    if ((q->plane_sorted || plane_time_group || plane_tbsc) &&
         (rc = q->gkp.dense ? q->gkt.init_dense(cap, 1, 0) : q->gkt.init(q->gkp.n ? cap : 1))) {
         delete q;
         return rc;
     }
     // (partition, group) pairs: room for four per group key, at least 64k
-    if (plane_time_group && (rc = q->pgkt.init(std::max<int64_t>(4 * cap, 1 << 16)))) { delete q; return rc; }
+    if ((plane_time_group || plane_tbsc) && (rc = q->pgkt.init(std::max<int64_t>(4 * cap, 1 << 16)))) { delete q; return rc; }
     q->pg_min_size = q->pgkt.size_;
     q->fp_orig = q->fp;
     for (int c = 0; c < d->n_cols; c++) q->load_type[c] = d->col_types[c];

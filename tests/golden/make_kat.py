@@ -491,6 +491,27 @@ case(name="aggregation2_sgt_year", source=A2 + ":1062-1115", kind="aggregation",
                                                                  (1546272001000, 1577807999000, 1577808001000)))],
      expect=dict(find=dict(per="year", start=_y[2018][0], end=_y[2018][1]), rows=[[1546272000000, "WSO2", 60.0]]))
 
+# SelectOptimisationAggregationTestCase.aggregationFunctionTestcase5: `group by symbol, name`, every sec, min;
+# the reference joins the retrieval `within 1496200000000L, 1596434876000L per "seconds"` and sums count per
+# symbol (WSO2 4, IBM 6, CISCO 1). The join is outside this path: the per-second rows below are hand-traced
+# from the sends (two events per second bucket except the last three) and sum to those totals.
+SO = "ctest/aggregation/SelectOptimisationAggregationTestCase.java"
+_so5 = [["WSO2", "WSO2", 50.0, 60.0, 90, 6, 1496289950000], ["WSO2", "WSO2", 70.0, 0.0, 40, 10, 1496289950000],
+        ["WSO2", "WSO2", 60.0, 44.0, 200, 56, 1496289952000], ["WSO2", "WSO2", 100.0, 0.0, 200, 16, 1496289952000],
+        ["IBM", "IBM", 100.0, 0.0, 200, 26, 1496289954000], ["IBM", "IBM", 100.0, 0.0, 200, 96, 1496289954000],
+        ["IBM", "IBM", 900.0, 0.0, 200, 60, 1496289956000], ["IBM", "IBM", 500.0, 0.0, 200, 7, 1496289956000],
+        ["IBM", "IBM", 400.0, 0.0, 200, 9, 1496290016000], ["IBM", "IBM", 600.0, 0.0, 200, 6, 1496290076000],
+        ["CISCO", "CISCO", 700.0, 0.0, 200, 20, 1496293676000]]
+case(name="select_optimisation5_two_group_by", source=SO + ":436-525", kind="aggregation",
+     schema="symbol string, name string, price float, lastClosingPrice float, volume long, quantity int, timestamp long",
+     aggregation=dict(aggs=[["count", None]], group_by=["symbol", "name"], ts="timestamp", durations=["sec", "min"]),
+     sends=[[[B + i] + r] for i, r in enumerate(_so5)],
+     expect=dict(find=dict(per="sec", start=1496200000000, end=1596434876000),
+                 rows=[[1496289950000, "WSO2", "WSO2", 2], [1496289952000, "WSO2", "WSO2", 2],
+                       [1496289954000, "IBM", "IBM", 2], [1496289956000, "IBM", "IBM", 2],
+                       [1496290016000, "IBM", "IBM", 1], [1496290076000, "IBM", "IBM", 1],
+                       [1496293676000, "CISCO", "CISCO", 1]]))
+
 # ---------------------------------------------------------------- filters (FilterTestCase1): expected counts
 F = "ctest/query/FilterTestCase1.java"
 FL = "symbol string, price float, volume long"

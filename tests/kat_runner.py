@@ -186,7 +186,7 @@ def check_aggregation_table(case, spec, dic, table_rows):
     got = []
     for ts, _, keys, vals in table_rows:
         base = dict(zip(names, vals))
-        row = [keys[0], dic.name(keys[1])] if spec.group_by else [keys[0]]
+        row = [keys[0]] + [dic.name(keys[1 + g]) for g in range(len(spec.group_by))]
         for fn, col in spec.aggs:
             if fn == "avg":
                 row.append(base[f"sum_{col}"] / base["count"])
@@ -198,7 +198,7 @@ def check_aggregation_table(case, spec, dic, table_rows):
                 row.append(base[f"{fn}_{col}"])
         got.append(row)
     exp = [list(r) for r in e["rows"]]
-    key = lambda r: (r[0], r[1]) if spec.group_by else (r[0],)
+    key = lambda r: tuple(r[:1 + len(spec.group_by)])
     assert sorted(got, key=key) == sorted(exp, key=key), (sorted(got, key=key), sorted(exp, key=key))
 
 

@@ -343,3 +343,75 @@ def test_device_pushes_speculative_band(rt):
     assert_tables_equal(tables(g, spec), tables(o, spec), "spec band end")
     g.close()
     o.close()
+
+
+# ---- group keys the root cannot key directly: two group-by columns, 64-bit keys (interned) ------------
+@pytest.mark.parametrize("schema_text,group_by", [
+    ("k int, s string, v double, ts long", ["k", "s"]),
+    ("k long, s string, v double, ts long", ["k"]),
+    ("k int, s string, v double, ts long", ["s", "k"]),
+])
+def test_interned_group_keys_rollups_retrieval_checkpoint(rt, schema_text, group_by):
+    """`group by a, b` and `group by <long>` under `aggregate by`: the group key is interned to a dense
+    id on the device (sh_aggregation.cpp intern) and decoded back on every table row and retrieval.
+    Late events, a mid-stream checkpoint restored into a fresh aggregation, retrievals and every
+    duration's table equal the oracle's."""
+    rng = np.random.default_rng(71)
+    n = 40_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 30, n)).astype(np.int64)
+    ext = clock - rng.integers(0, 50_000, n).astype(np.int64)
+    schema = abi.Schema.parse(schema_text)
+    k = rng.integers(0, 40, n)
+    k = (k * 3_000_000_007 - 60_000_000_000).astype(np.int64) if schema_text.startswith("k long") else k.astype(np.int32)
+    s = rng.integers(0, 7, n).astype(np.int32)
+    v = np.round(rng.normal(50, 20, n), 3)
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("count", None), ("min", "v"), ("max", "v")],
+                               group_by=group_by, ts="ts", durations=("sec", "day"), key_capacity=512)
+    bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], s[a_:b_], v[a_:b_], ext[a_:b_]], 7)
+    g, o = rt.GpuAggregation(spec), OracleAggregation(spec)
+    cut = 17_001
+    for x in (g, o):
+        x.push(bat(0, cut))
+    spans = [(abi.DUR_NAMES[d], 0, 1 << 62) for d in ("sec", "min", "day")]
+    assert _finds(g, spans) == _finds(o, spans)
+    blob = g.snapshot()
+    fresh = rt.GpuAggregation(spec)
+    fresh.restore(blob)
+    rest = [bat(cut, 30_000), bat(30_000, n), ("advance", int(clock[-1]) + 2 * 86_400_000)]
+    for x in (g, fresh, o):
+        drive(x, rest[:2])
+    assert _finds(fresh, spans) == _finds(o, spans) == _finds(g, spans)
+    for x in (g, fresh, o):
+        drive(x, rest[2:])
+    ot = tables(o, spec)
+    assert sum(len(t["ts"]) for t in ot.values()) > 0
+    assert_tables_equal(tables(g, spec), ot, "interned")
+    # tables drain on read: the restored copy is compared against a re-run oracle
+    o2 = OracleAggregation(spec)
+    for p in [bat(0, cut)] + rest:
+        drive(o2, [p])
+    assert_tables_equal(tables(fresh, spec), tables(o2, spec), "interned restored")
+    for x in (g, fresh, o, o2):
+        x.close()
+
+
+@pytest.mark.parametrize("tz_hours", [8, -5])
+def test_agg_time_zone_offset_buckets(rt, tz_hours):
+    """`@store(aggTimeZone)` as a fixed offset: hour and day buckets start at local boundaries
+    (IncrementalTimeConverterUtil with a zone); sec/min are offset-invariant."""
+    ts, cols = synth.keyed_stream(1_700_000_000_000 - 15_000, 120_000, 0xA7, 300, 1)
+    cols[2] = ts - (np.arange(len(ts)) % 97) * 1_000  # late events crossing hour boundaries
+    pushes = split_batches(C4_SCHEMA, ts, cols, [40_000, 80_000], 300)
+    pushes.append(("advance", int(ts[-1]) + 3 * 86_400_000))
+    spec = abi.AggregationSpec(C4_SCHEMA, [("sum", "v"), ("count", None), ("max", "v")], group_by=["k"], ts="ts",
+                               durations=("min", "day"), key_capacity=300, tz_offset_ms=tz_hours * 3_600_000)
+    assert both(rt, spec, pushes, f"tz{tz_hours}", checkpoints=(0, 1)) > 0
+
+
+def test_two_group_by_columns_wider_than_64_bits_refused(rt):
+    """Two group-by columns intern as one 64-bit key: a long beside another column is refused."""
+    schema = abi.Schema.parse("k long, s string, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v")], group_by=["s", "k"], ts="ts", durations=("sec", "min"),
+                               key_capacity=64)
+    with pytest.raises(Exception, match="32-bit"):
+        rt.GpuAggregation(spec)

@@ -357,3 +357,60 @@ def test_float_partition_keys_time_expired_refused(rt):
                          key_capacity=64)
     with pytest.raises(rt.SiddhiError, match="Double.toString"):
         rt.GpuQuery(spec)
+
+
+# ---- partitioned timeBatch(T, true) — stream.current.event, current output (lane 4): every partition
+# chunk goes out with its groups' running values; TimeBatchWindowProcessor's nextEmitTime is one field
+# for all partitions (:128), so a partition's state is RESET only when its own chunk or TIMER finds the
+# playback clock at or past it — the first partition's TIMERs while events keep coming, whichever
+# partition meets a lagging nextEmitTime after an idle stretch (it then schedules the next TIMER) ---------
+def gap_stream(n, parts, seed, zipf=False, gaps=True, runs=False):
+    ts, cols = stream(n, parts, seed, step=3, runs=runs, zipf=zipf)
+    if gaps:  # idle stretches of several periods: nextEmitTime lags and other partitions reset
+        rng = np.random.default_rng(seed + 1)
+        jump = (rng.random(n) < 1 / 3000) * rng.integers(2_000, 9_000, n)
+        ts = ts + np.cumsum(jump).astype(np.int64)
+        cols[3] = ts.copy()
+    return ts, cols
+
+
+TB_SCHEMA = abi.Schema.parse("p int, g int, v double, x long, ts long")
+
+
+@pytest.mark.parametrize("group_by,send_size,runs", [(["p"], 1, False), ([], 5, True), (["g"], 1, False),
+                                                      (["g", "p"], 3, True)])
+def test_partitioned_timebatch_stream_current(rt, group_by, send_size, runs):
+    ts, cols = gap_stream(40_000, 97, 61, runs=runs)
+    g = ((cols[0].astype(np.int64) * 7 + np.arange(len(ts))) % 5).astype(np.int32)
+    tcols = [cols[0], g, cols[1], cols[2], cols[3]]
+    spec = abi.QuerySpec(TB_SCHEMA, "timeBatch", 700, group_by=group_by, aggs=AGGS, partition="p",
+                         stream_current=True, filter=(">", "v", -40.0), key_capacity=256)
+    pushes = split_batches(TB_SCHEMA, ts, tcols, [1, 9_000, 9_001, 25_000], send_size)
+    out = []
+    for i, p in enumerate(pushes):  # advance_time between some pushes (TIMER calls without events)
+        out.append(p)
+        if i % 2 == 1:
+            out.append(("advance", int(p.ts[-1]) + (3_000 if i % 4 == 1 else 1)))
+    ref = both(rt, spec, out, f"ptbsc {group_by} {send_size}")
+    assert ref["ts"].size > 1000
+
+
+def test_partitioned_timebatch_stream_current_zipf_100k_partitions(rt):
+    ts, cols = gap_stream(2_000_000, 1_000_000, 62, zipf=True)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 1000, group_by=["p"], aggs=[("count", None), ("sum", "v"), ("max", "x")],
+                         partition="p", stream_current=True, key_capacity=1_000_000)
+    ref = both(rt, spec, split_batches(SCHEMA, ts, cols, [700_000, 1_400_000], 1), "ptbsc zipf")
+    assert len(np.unique(cols[0])) > 100_000 and ref["ts"].size > 100_000
+
+
+def test_partitioned_timebatch_stream_current_checkpoint_and_rate(rt):
+    from tests.parity import assert_same
+    from tests.test_gpu_snapshot import checkpointed
+    ts, cols = gap_stream(30_000, 41, 63)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 500, group_by=["p"], aggs=[("count", None), ("sum", "v"), ("min", "v")],
+                         partition="p", stream_current=True, key_capacity=64)
+    pushes = split_batches(SCHEMA, ts, cols, [8_000, 19_000], 1)
+    got, ref, _ = checkpointed(spec, pushes, 1)
+    assert_same(got, ref, label="ptbsc ckpt")
+    spec.rate = ("first", 4)
+    both(rt, spec, pushes, "ptbsc rate")
