@@ -293,6 +293,8 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
     else:
         q = runtime.GpuAggregation(agg, ctx) if agg else runtime.GpuQuery(spec, ctx)
+        if args.workload == "c2cur":
+            q.set_compact_flushes()  # a row per event: flush i = row i at its ts (no 16 B/row flush arrays)
     batches = [mk(gen(i)) for i in range(nb)]
     torch.cuda.synchronize()
     phases, timing = {}, False

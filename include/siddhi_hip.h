@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 12
+#define SH_ABI_VERSION 13
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -281,6 +281,14 @@ int sh_query_set_ext_timeout(sh_query* q, int64_t ms);
  * (SH_ERR_UNSUPPORTED). Replaces the Java window's fifth argument. */
 int sh_query_set_ext_replace_ts(sh_query* q, int32_t on);
 int sh_query_rep_ts_attr(sh_query* q, const int64_t** values, int64_t* n);
+
+/* Compact flushes: when on, an output in which every flush holds exactly one row and every flush's clock
+ * equals that row's timestamp (stream.current.event output, `timeBatch(T, true)` / `lengthBatch(L, true)`,
+ * sends of one event) comes back with flush_offsets = flush_clock = NULL and n_flushes = n_rows: flush i
+ * is row i, emitted at clock ts[i]. Any other output keeps the full arrays, so a caller that sets this
+ * checks flush_offsets for NULL. Saves the 16 B per row the flush arrays would cost (host memory even for
+ * sh_push_device). Off by default; queries with an output rate limiter always get the full form. */
+int sh_query_set_compact_flushes(sh_query* q, int32_t on);
 
 /* The text of dictionary ids [first_id, first_id + n) of string column `col`, as UTF-16 code units (what a
  * java.lang.String holds): id first_id + i is units[offsets[i] .. offsets[i + 1]) (offsets has n + 1

@@ -296,14 +296,26 @@ class Flush:
     reps: List[int] = field(default_factory=list)  # stream index of each row's representative event
 
 
+def flush_arrays(o, ts=None):
+    """(flush_offsets, flush_clock) of an sh_out; a compact output (sh_query_set_compact_flushes: NULL arrays)
+    is one flush per row at the row's timestamp (`ts`: the host copy of the rows' timestamps)."""
+    if not o.n_flushes:
+        return np.zeros(1, np.int64), np.zeros(0, np.int64)
+    if not o.flush_offsets:
+        if ts is None:
+            ts = np.ctypeslib.as_array(o.ts, shape=(o.n_rows,))
+        return np.arange(o.n_flushes + 1, dtype=np.int64), np.asarray(ts, np.int64)[:o.n_flushes].copy()
+    return (np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy(),
+            np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy())
+
+
 def decode_out(out_ptr) -> List[Flush]:
     o = out_ptr.contents
     n = o.n_rows
     flushes: List[Flush] = []
     if o.n_flushes == 0:
         return flushes
-    offs = np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
-    clocks = np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
+    offs, clocks = flush_arrays(o)
     if n:
         ts = np.ctypeslib.as_array(o.ts, shape=(n,)).copy()
         exp = np.ctypeslib.as_array(o.expired, shape=(n,)).copy()
@@ -336,11 +348,9 @@ def out_arrays(out_ptr) -> Dict[str, np.ndarray]:
     """Vectorised view of an sh_out (copies), for large parity comparisons."""
     o = out_ptr.contents
     n = o.n_rows
+    fo, fc = flush_arrays(o)
     res: Dict[str, np.ndarray] = {
-        "flush_offsets": np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
-        if o.n_flushes else np.zeros(1, np.int64),
-        "flush_clock": np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
-        if o.n_flushes else np.zeros(0, np.int64),
+        "flush_offsets": fo, "flush_clock": fc,
         "val_types": np.array([o.val_types[i] for i in range(o.n_vals)], np.int32),
     }
     if n:
@@ -400,6 +410,7 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
     lib.sh_query_set_ext_timeout.argtypes = [C.c_void_p, C.c_int64]
     lib.sh_query_set_ext_replace_ts.argtypes = [C.c_void_p, C.c_int32]
+    lib.sh_query_set_compact_flushes.argtypes = [C.c_void_p, C.c_int32]
     lib.sh_query_rep_ts_attr.argtypes = [C.c_void_p, P(P(C.c_int64)), P(C.c_int64)]
     lib.sh_aggregation_timing.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
     lib.sh_shard_flush_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -446,7 +457,7 @@ ABI_SYMBOLS = [
     "sh_shard_create", "sh_shard_destroy", "sh_shard_record_bytes", "sh_shard_summarize", "sh_shard_pack",
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
-    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate", "sh_query_set_ext_timeout", "sh_query_set_ext_replace_ts", "sh_query_rep_ts_attr", "sh_aggregation_timing", "sh_shard_flush_windows",
+    "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate", "sh_query_set_ext_timeout", "sh_query_set_ext_replace_ts", "sh_query_set_compact_flushes", "sh_query_rep_ts_attr", "sh_aggregation_timing", "sh_shard_flush_windows",
     "sh_shard_snapshot", "sh_shard_restore", "sh_query_set_strings",
 ]
 

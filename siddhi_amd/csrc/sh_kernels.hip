@@ -2378,6 +2378,21 @@ void launch_sc_flushes(hipStream_t s, i64 T, const i64* osd, const u32* pre, con
                        cv0, clock0, bclk, fo1, fc);
 }
 
+// compact flushes (sh_query_set_compact_flushes): ok[0] stays 1 iff every flush's clock equals its one
+// row's timestamp (the caller has checked one row per flush); plain stores of one value, no atomics
+__global__ __launch_bounds__(kBlock) void k_flush_clock_is_ts(i64 n, const i64* __restrict__ fc,
+                                                             const i64* __restrict__ ts, u32* ok) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && fc[i] != ts[i]) ok[0] = 0u;
+}
+
+void launch_flush_clock_is_ts(hipStream_t s, i64 n, const i64* fc, const i64* ts, u32* ok) {
+    (void)hipMemsetD32Async((hipDeviceptr_t)ok, 1, 1, s);
+    if (n > 0)
+        hipLaunchKernelGGL(k_flush_clock_is_ts, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, fc,
+                           ts, ok);
+}
+
 // ---- externalTimeBatch timeout: where the push's clock passes lastScheduledTime --------------------
 // First send whose last event's timestamp reaches L (InputHandler.send sets the clock from it, and
 // every earlier send's clock stays below L): out[0] = its index (u64 max: none).

@@ -275,6 +275,9 @@ struct sh_query {
     // of the last windows, with their number (a row's representative event lies in the last window that
     // starts at or before it), and the batch end times of the last output's rows
     bool xt_replace = false;
+    // sh_query_set_compact_flushes: an output of one row per flush whose clocks equal the rows' ts leaves
+    // flush_offsets / flush_clock NULL (compact_now: this call's output is in that form)
+    bool compact_flushes = false, compact_now = false;
     std::vector<std::pair<int64_t, int64_t>> xr_starts;
     std::vector<int64_t> xr_rep, xr_vals;
     bool xt_Lvalid = false;

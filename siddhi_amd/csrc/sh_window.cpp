@@ -645,16 +645,24 @@ static int closed_finish(sh_query* q, bool host_out) {
 }
 
 static void finish_out(sh_query* q, bool host_out, const sh_out** out) {
+    const bool compact = q->compact_now;
+    q->compact_now = false;
     if (host_out) {
-        *out = q->out.view(q->kp.n, q->ap.n, q->vtypes);
+        q->out.view(q->kp.n, q->ap.n, q->vtypes);
+        if (compact) {
+            q->out.out.n_flushes = q->out.out.n_rows;
+            q->out.out.flush_offsets = nullptr;
+            q->out.out.flush_clock = nullptr;
+        }
+        *out = &q->out.out;
     } else {
         sh_out& o = q->dev_out;
-        o.n_flushes = (int64_t)q->dev_flush_clock.size();
+        o.n_flushes = compact ? o.n_rows : (int64_t)q->dev_flush_clock.size();
         o.n_keys = q->kp.n;
         o.n_vals = q->ap.n;
         for (int i = 0; i < q->ap.n; i++) o.val_types[i] = q->vtypes[i];
-        o.flush_offsets = q->dev_flush_offsets.data();
-        o.flush_clock = q->dev_flush_clock.data();
+        o.flush_offsets = compact ? nullptr : q->dev_flush_offsets.data();
+        o.flush_clock = compact ? nullptr : q->dev_flush_clock.data();
         o.ts = q->out_ts.as<int64_t>();
         o.expired = q->out_expired.as<uint8_t>();
         o.keys = q->out_keys.as<int64_t>();
@@ -937,11 +945,20 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), q->sc_fflag.as<u32>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0,
                           clock0, q->sc_bclk.as<int64_t>(), q->sc_fo.as<int64_t>(), q->sc_fc.as<int64_t>());
         HIPCHK(hipGetLastError());
-        fo.resize((size_t)nf + 1);
-        fc.resize((size_t)nf);
-        if (nf) {
-            HIPCHK(hipMemcpyAsync(fo.data() + 1, q->sc_fo.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipMemcpyAsync(fc.data(), q->sc_fc.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
+        if (q->compact_flushes && q->rate.kind == SH_RATE_NONE && !q->xmode && nf > 0 && nf == T) {
+            // one row per flush: offsets implicit; clocks implicit too when each equals its row's ts
+            launch_flush_clock_is_ts(s, nf, q->sc_fc.as<int64_t>(), q->out_ts.as<int64_t>(), q->h_small_sc.as<uint32_t>() + 1);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(s));
+            q->compact_now = q->h_small_sc.as<uint32_t>()[1] == 1u;
+        }
+        if (!q->compact_now) {
+            fo.resize((size_t)nf + 1);
+            fc.resize((size_t)nf);
+            if (nf) {
+                HIPCHK(hipMemcpyAsync(fo.data() + 1, q->sc_fo.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(fc.data(), q->sc_fc.p, (size_t)nf * 8, hipMemcpyDeviceToHost, s));
+            }
         }
         HIPCHK(hipStreamSynchronize(s));
     }
@@ -1852,6 +1869,12 @@ static int rep_attr_finish(sh_query* q, const sh_out* o, bool host) {
         q->xr_vals[i] = q->E0 + T * (W + 1);
     }
     return xr_trim(q);
+}
+
+extern "C" int sh_query_set_compact_flushes(sh_query* q, int32_t on) {
+    if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_compact_flushes: NULL query");
+    q->compact_flushes = on != 0;
+    return SH_OK;
 }
 
 extern "C" int sh_query_set_ext_replace_ts(sh_query* q, int32_t on) {

@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 12:
+        if L.sh_abi_version() != 13:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -53,11 +53,9 @@ def device_out_arrays(out_ptr):
             if rc != 0:
                 raise SiddhiError(abi.SH_ERR_DEVICE, f"hipMemcpy of output column {name} failed ({rc})")
         host[name] = a[:cnt]
+    fo, fc = abi.flush_arrays(o, host["ts"])
     return {
-        "flush_offsets": np.ctypeslib.as_array(o.flush_offsets, shape=(o.n_flushes + 1,)).copy()
-        if o.n_flushes else np.zeros(1, np.int64),
-        "flush_clock": np.ctypeslib.as_array(o.flush_clock, shape=(o.n_flushes,)).copy()
-        if o.n_flushes else np.zeros(0, np.int64),
+        "flush_offsets": fo, "flush_clock": fc,
         "val_types": np.array([o.val_types[i] for i in range(na)], np.int32),
         "ts": host["ts"], "expired": host["expired"], "rep": host["rep"],
         "keys": host["keys"].reshape(nk, n), "vals": host["vals"].reshape(na, n), "nulls": host["nulls"].reshape(na, n),
@@ -120,6 +118,10 @@ class GpuQuery:
         except Exception:
             self.close()
             raise
+
+    def set_compact_flushes(self, on: bool = True):
+        """sh_query_set_compact_flushes: one-row flushes at their rows' timestamps leave the flush arrays NULL."""
+        _check(lib().sh_query_set_compact_flushes(self.h, 1 if on else 0))
 
     def set_strings(self, col: str, names, first_id: int = 0):
         """The text of string column `col`'s dictionary ids first_id.. (sh_query_set_strings)."""

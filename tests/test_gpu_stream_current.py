@@ -95,3 +95,36 @@ def test_timebatch_stream_current_expired(rt, output, send_size, group_by):
     pushes.append(("advance", int(ts[-1]) + 5_000))
     out = both(rt, spec, pushes, label=f"timeBatch stream current {output} send {send_size}")
     assert out["expired"].sum() > 0
+
+
+@pytest.mark.parametrize("window,param", [("timeBatch", 700), ("lengthBatch", 50)])
+def test_compact_flushes(rt, window, param):
+    """sh_query_set_compact_flushes: per-event sends give one row per flush at its row's timestamp, so the
+    flush arrays come back NULL (n_flushes = n_rows) and are rebuilt from the rows; sends of several events
+    keep the full arrays. Host and device outputs equal the oracle's either way."""
+    import torch
+    from oracle.oracle import OracleQuery
+    from tests.parity import assert_same
+    ts, cols = stream(20_000, 300, 17)
+    spec = abi.QuerySpec(SCHEMA, window, param, group_by=["k"], aggs=AGGS, filter=(">", "v", -150.0),
+                         stream_current=True, key_capacity=512)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    g.set_compact_flushes()
+    compact = []
+    for a, b, send in ((0, 6_000, 1), (6_000, 9_000, 13), (9_000, 14_000, 1)):
+        hb = abi.HostBatch(SCHEMA, ts[a:b], [c[a:b] for c in cols], send)
+        raw = g.push_raw(hb)
+        compact.append(not raw.contents.flush_offsets)
+        assert_same(abi.out_arrays(raw), abi.out_arrays(o.push_raw(hb)), label=f"compact host {a}")
+    assert compact == [True, False, True]
+    dev = torch.device("cuda", 0)
+    t = torch.from_numpy(ts[14_000:]).to(dev)
+    dc = [torch.from_numpy(np.ascontiguousarray(c[14_000:])).to(dev) for c in cols]
+    torch.cuda.synchronize()
+    raw = g.push_device(len(t), t.data_ptr(), [c.data_ptr() for c in dc], 1)
+    assert not raw.contents.flush_offsets and raw.contents.n_flushes == raw.contents.n_rows > 0
+    got = rt.device_out_arrays(raw)
+    ref = abi.out_arrays(o.push_raw(abi.HostBatch(SCHEMA, ts[14_000:], [c[14_000:] for c in cols], 1)))
+    assert_same(got, ref, label="compact device")
+    g.close()
+    o.close()
