@@ -8,6 +8,8 @@
 #   kstats=WL           rocprofv3 --kernel-trace --stats of bench.py --workload WL -> TAG_WL_kernel_stats.txt
 #   pmc=WL              FETCH_SIZE and WRITE_SIZE passes (separate runs) -> TAG_WL_pmc.json
 #   shard=WL            bench.py --workload WL --shard-loopback G=8 (one-GPU sharded pipeline phases)
+#   timeline=WL         kernel trace of 5 steps -> per-step kernel timeline (TL_FIRST = the step's first kernel)
+#   htiming=WL          SH_TIMING=1 host-side times between the push's numbered points
 # Extra bench arguments: BENCH_ARGS env (e.g. BENCH_ARGS="--steps 10 --warmup 3").
 set -o pipefail
 TAG=$1; shift
@@ -54,6 +56,19 @@ for step in "$@"; do
       W=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" "$P/${n}_WRITE_SIZE")
       python3 scripts/pmc_summary.py "$F" "$W" --pushes 3 > "${O}_${n}_pmc.json" || fail "pmc summary $n"
       python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'GB per push %.3f' % (d['per_push_bytes']/1e9))" "${O}_${n}_pmc.json" "$n" ;;
+    timeline)
+      n=${arg:-c2}
+      first=${TL_FIRST:-k_boundaries}
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$P/tl_$n" -o run --output-format csv -- \
+          python3 bench.py $(wl_args "$arg") --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > "$P/tl_$n.json" 2> "$P/tl_$n.err" \
+          || fail "timeline $n" "$P/tl_$n.err"
+      python3 scripts/timeline.py "$P/tl_$n" "$first" > "${O}_${n}_timeline.txt" || fail "timeline summary $n"
+      tail -1 "${O}_${n}_timeline.txt" ;;
+    htiming)
+      n=${arg:-c2}
+      SH_TIMING=1 timeout -k 10 300 python -u bench.py $(wl_args "$arg") --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} \
+          > "${O}_${n}_htiming.json" 2> "${O}_${n}_htiming.txt" || fail "htiming $n" "${O}_${n}_htiming.txt"
+      grep "sh timing" "${O}_${n}_htiming.txt" | head -12 ;;
     shard)
       n=${arg:-c2}
       timeout -k 10 400 python -u bench.py $(wl_args "$arg") --shard-loopback 8 --steps 5 --warmup 2 --no-cpu-baseline \

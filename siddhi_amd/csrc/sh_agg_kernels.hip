@@ -10,32 +10,7 @@
 
 namespace shd {
 
-// ---- GMT calendar (IncrementalTimeConverterUtil with ZoneId "GMT") ------------------------------
-__device__ __forceinline__ i64 floor_div_d(i64 a, i64 b) {
-    i64 q = a / b;
-    if ((a % b != 0) && ((a < 0) != (b < 0))) q--;
-    return q;
-}
-__device__ __forceinline__ i64 days_from_civil_d(i64 y, unsigned m, unsigned d) {
-    y -= m <= 2;
-    const i64 era = (y >= 0 ? y : y - 399) / 400;
-    const unsigned yoe = (unsigned)(y - era * 400);
-    const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-    const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-    return era * 146097 + (i64)doe - 719468;
-}
-__device__ __forceinline__ void civil_from_days_d(i64 z, i64& y, unsigned& m, unsigned& d) {
-    z += 719468;
-    const i64 era = (z >= 0 ? z : z - 146096) / 146097;
-    const unsigned doe = (unsigned)(z - era * 146097);
-    const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-    y = (i64)yoe + era * 400;
-    const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
-    const unsigned mp = (5 * doy + 2) / 153;
-    d = doy - (153 * mp + 2) / 5 + 1;
-    m = mp + (mp < 10 ? 3 : -9);
-    y += (m <= 2);
-}
+// (the GMT calendar helpers floor_div_d / days_from_civil_d / civil_from_days_d are in sh_device.h)
 
 // getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69); sec/min use `t - t % d`
 __device__ __forceinline__ i64 start_of_gmt(i64 t, int dur) {

@@ -124,6 +124,19 @@ static int64_t h_next_emit(int64_t t, int dur, int64_t tz) {
     return dur >= SH_DUR_HOURS ? h_next_emit(t + tz, dur) - tz : h_next_emit(t, dur);
 }
 
+// calendar buckets of a month (cal 1) / year (cal 2) root in the zone offset tz (sh_device.h cal_idx_d)
+int64_t cal_idx_h(int64_t t, int cal, int64_t tz) {
+    const HCivil c = h_civil(t + tz);
+    return cal == 1 ? c.y * 12 + (int64_t)(c.m - 1) : c.y;
+}
+int64_t cal_start_h(int64_t i, int cal, int64_t tz) {
+    if (cal == 1) {
+        const int64_t y = h_floor_div(i, 12);
+        return h_epoch(y, i - y * 12 + 1, 1, 0) - tz;
+    }
+    return h_epoch(i, 1, 1, 0) - tz;
+}
+
 // A batch of rows on the device: bucket / key / base values (stride = cap).
 struct RowBatch {
     int64_t n = 0, cap = 0;
@@ -164,6 +177,7 @@ struct sh_aggregation {
     int64_t T_root = 0;
     int64_t tz = 0;       // aggTimeZone as a fixed offset (ms)
     int64_t tz_root = 0;  // the root's bucket offset: tz for hour / day roots (sec / min are zone-free)
+    int cal = 0;          // a month (1) / year (2) root: calendar buckets and windows, T_root unused
     sh_query* root = nullptr;
     sh_shard* shard = nullptr;  // sharded: the root is this shard's owner query (owned by the shard)
     bool root_init = false;
@@ -380,14 +394,37 @@ static int level_timer_run(sh_aggregation* a, size_t li, int64_t first, int64_t 
     return SH_OK;
 }
 
+// the root's buckets: fixed periods T_root from the zone's offset, or calendar months / years
+static int64_t root_floor(const sh_aggregation* a, int64_t t) {
+    if (a->cal) return cal_start_h(cal_idx_h(t, a->cal, a->tz_root), a->cal, a->tz_root);
+    return h_floor_div(t + a->tz_root, a->T_root) * a->T_root - a->tz_root;
+}
+static int64_t root_shift(const sh_aggregation* a, int64_t start, int64_t k) {  // the bucket k after start's
+    if (a->cal) return cal_start_h(cal_idx_h(start, a->cal, a->tz_root) + k, a->cal, a->tz_root);
+    return start + k * a->T_root;
+}
+static int64_t root_count(const sh_aggregation* a, int64_t from, int64_t to) {  // buckets from -> to
+    if (a->cal) return cal_idx_h(to, a->cal, a->tz_root) - cal_idx_h(from, a->cal, a->tz_root);
+    return (to - from) / a->T_root;
+}
+// start of the root's window W (window 1 starts at E0, the first nextEmitTime)
+static int64_t root_window_start(const sh_aggregation* a, int64_t W) { return root_shift(a, a->root->E0, W - 1); }
+
+// TIMERs of the root buckets after `last` up to `cb` (one per bucket the clock passed)
+static int root_timers(sh_aggregation* a, int64_t last, int64_t cb) {
+    if (cb <= last || a->levels.empty()) return SH_OK;
+    if (!a->cal) return level_timer_run(a, 0, last + a->T_root, a->T_root, (cb - last) / a->T_root);
+    const int64_t n = root_count(a, last, cb);
+    for (int64_t k = 1; k <= n; k++) RCHK(level_timer(a, 0, root_shift(a, last, k)));
+    return SH_OK;
+}
+
 static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
     sh_query* q = a->root;
-    int64_t T = a->T_root;
-    int64_t E0 = q->E0;
     int nk = o->n_keys;
     for (int64_t f = 0; f < o->n_flushes; f++) {
         int64_t W = q->flush_window[f];
-        int64_t s_f = E0 + (W - 1) * T;  // processing bucket of the closed root store
+        int64_t s_f = root_window_start(a, W);  // processing bucket of the closed root store
         int64_t lo = o->flush_offsets[f], hi = o->flush_offsets[f + 1];
         RowBatch rb;
         rb.n = hi - lo;
@@ -402,8 +439,7 @@ static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
         }
         rb.vals = (const u64*)o->vals + lo;
         // timers of the empty root buckets before s_f
-        if (s_f > a->root_bucket && !a->levels.empty())
-            RCHK(level_timer_run(a, 0, a->root_bucket + T, T, (s_f - a->root_bucket) / T));
+        RCHK(root_timers(a, a->root_bucket, s_f));
         a->root_bucket = std::max(a->root_bucket, s_f);
         // the root table gets the rows; without `aggregate by` AGG_TIMESTAMP is the store timestamp
         if (!a->has_bucket) {
@@ -427,9 +463,9 @@ static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
                 HIPCHK(hipStreamWaitEvent(a->lstream, a->ev_tab, 0));
             }
             RCHK(level_rows(a, 0, rb.n > 0 ? tb : rb, s_f));
-            RCHK(level_timer(a, 0, s_f + T));
+            RCHK(level_timer(a, 0, root_shift(a, s_f, 1)));
         }
-        a->root_bucket = s_f + T;
+        a->root_bucket = root_shift(a, s_f, 1);
     }
     return SH_OK;
 }
@@ -438,16 +474,14 @@ static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
 static int catch_up(sh_aggregation* a) {
     sh_query* q = a->root;
     if (!q->e0_valid) return SH_OK;
-    int64_t T = a->T_root;
     if (!a->root_init) {
         // first event: root store opens at the bucket of the first clock and TIMERs its child (:141-150)
         a->root_init = true;
-        a->root_bucket = q->E0 - T;
+        a->root_bucket = root_shift(a, q->E0, -1);
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
-    int64_t cb = h_floor_div(q->clock + a->tz_root, T) * T - a->tz_root;
-    if (cb > a->root_bucket && !a->levels.empty())
-        RCHK(level_timer_run(a, 0, a->root_bucket + T, T, (cb - a->root_bucket) / T));
+    int64_t cb = root_floor(a, q->clock);
+    RCHK(root_timers(a, a->root_bucket, cb));
     a->root_bucket = std::max(a->root_bucket, cb);
     return SH_OK;
 }
@@ -458,8 +492,6 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS || d->n_aggs <= 0 || d->n_aggs > SH_MAX_AGGS ||
         d->min_duration < 0 || d->max_duration > SH_DUR_YEARS || d->min_duration > d->max_duration)
         return sh_fail(SH_ERR_INVALID, "invalid aggregation descriptor");
-    if (d->min_duration > SH_DUR_DAYS)
-        return sh_fail(SH_ERR_UNSUPPORTED, "GPU aggregation roots are sec/min/hour/day");
     if (d->n_group_by > SH_MAX_GROUP) return sh_fail(SH_ERR_INVALID, "invalid aggregation descriptor");
     if (d->ts_col >= 0 && (d->ts_col >= d->n_cols || d->col_types[d->ts_col] != SH_T_LONG))
         return sh_fail(SH_ERR_INVALID, "`aggregate by` attribute must be a long");
@@ -468,8 +500,10 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     a->d = *d;
     a->d.filter = nullptr;
     a->has_bucket = d->ts_col >= 0;
-    static const int64_t unit[] = {1000, 60000, 3600000, 86400000};
+    // (month / year roots: calendar windows and buckets; T_root is only a nominal positive period)
+    static const int64_t unit[] = {1000, 60000, 3600000, 86400000, 31 * 86400000ll, 366 * 86400000ll};
     a->T_root = unit[d->min_duration];
+    a->cal = d->min_duration == SH_DUR_MONTHS ? 1 : d->min_duration == SH_DUR_YEARS ? 2 : 0;
     if (d->tz_offset_ms % 60000 != 0 || d->tz_offset_ms <= -86400000 || d->tz_offset_ms >= 86400000) {
         delete a;
         return sh_fail(SH_ERR_INVALID, "aggTimeZone offset must be whole minutes within a day");
@@ -514,7 +548,8 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     KeyPlan kp{};
     int g = 0;
     if (a->has_bucket) {
-        kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->T_root; kp.add[g] = a->tz_root; g++;
+        kp.col[g] = d->ts_col; kp.type[g] = SH_T_LONG; kp.div[g] = a->cal ? -a->cal : a->T_root; kp.add[g] = a->tz_root;
+        g++;
     }
     int gtype = -1;  // the root key's group component type
     if (d->n_group_by >= 1) {
@@ -543,11 +578,13 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     int rc = shard ? shard_create_root(ctx, &rd, kp, rank, world, &a->shard, &a->root)
                    : sh_query_create_internal(ctx, &rd, kp, &a->root);
     if (rc) { delete a; return rc; }
+    a->root->cal = a->cal;
+    a->root->cal_tz = a->tz_root;
     if (shard) {
         shard_attach_aggregation(a->shard, a);
         *shard = a->shard;
     }
-    if (a->has_bucket && d->n_group_by >= 1 && gtype == SH_T_STRID) {
+    if (a->has_bucket && d->n_group_by >= 1 && gtype == SH_T_STRID && !a->cal) {
         // ids per bucket row: the GPU's share of the dictionary (sharded owners hold the ids = rank mod G)
         const int64_t cap = rd.key_capacity, per = shard ? (cap + world - 1) / world : cap;
         // (A/B switch SH_AGG_BAND_ROWS, 0 = hash keys only)
@@ -621,6 +658,8 @@ extern "C" int sh_aggregation_shard_create(sh_ctx* ctx, const sh_aggregation_des
     StreamScope _ss(ctx ? ctx->stream : nullptr);
     if (!shard) return sh_fail(SH_ERR_INVALID, "sh_aggregation_shard_create: NULL argument");
     if (d && d->n_group_by != 1) return sh_fail(SH_ERR_UNSUPPORTED, "sharded aggregations need one group-by key");
+    if (d && d->min_duration > SH_DUR_DAYS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded aggregations have sec / min / hour / day roots");
     return agg_create(ctx, d, rank, world, shard, out);
 }
 
@@ -793,7 +832,8 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side) {
         if (side) HIPCHK(sh_wait_stream(s));
         else RCHK(agg_sync(a));
         // the key's bucket component: ts / T truncated (sh_device.h key_part)
-        const int64_t lo = (a->h_minmax[0] + a->tz_root) / a->T_root, hi = (a->h_minmax[1] + a->tz_root) / a->T_root;
+        const int64_t lo = a->cal ? cal_idx_h(a->h_minmax[0], a->cal, a->tz_root) : (a->h_minmax[0] + a->tz_root) / a->T_root;
+        const int64_t hi = a->cal ? cal_idx_h(a->h_minmax[1], a->cal, a->tz_root) : (a->h_minmax[1] + a->tz_root) / a->T_root;
         int64_t nb = hi - lo + 1;
         bound = (nb > 0 && keys <= N / nb) ? keys * nb : N;
         if (a->band_ok) return band_reserve(a, lo, hi, bound);
@@ -916,7 +956,7 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
         return sh_fail(SH_ERR_UNSUPPORTED, "too many rows in one flush for a constant key column");
     if (!a->root_init && a->root->e0_valid) {
         a->root_init = true;
-        a->root_bucket = a->root->E0 - a->T_root;
+        a->root_bucket = root_shift(a, a->root->E0, -1);
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
     RCHK(pass_root_flushes(a, o));
@@ -1150,7 +1190,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
             else HIPCHK(hipMemsetAsync(a->m_key.as<int64_t>() + m, 0, R * 8, s));
         } else {
             // processing time: AGG_TIMESTAMP of the root store = the open window's start
-            launch_fill_i64(s, a->m_bucket.as<int64_t>() + m, R, q->E0 + (q->W_open - 1) * a->T_root);
+            launch_fill_i64(s, a->m_bucket.as<int64_t>() + m, R, root_window_start(a, q->W_open));
             if (nk > 0) HIPCHK(hipMemcpyAsync(a->m_key.as<int64_t>() + m, keys, R * 8, hipMemcpyDeviceToDevice, s));
             else HIPCHK(hipMemsetAsync(a->m_key.as<int64_t>() + m, 0, R * 8, s));
         }

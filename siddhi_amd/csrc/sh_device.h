@@ -230,12 +230,56 @@ __device__ __forceinline__ void filter_items(const FilterProg& f, const ColSet& 
 // except NaN, whose payloads all print "NaN" — so the key is the value's bits with NaN made canonical.
 // A float alone is keyed by its value widened to double (an injective map); as one of two 32-bit
 // components by its own (canonical) bits.
+// ---- GMT calendar (IncrementalTimeConverterUtil with ZoneId "GMT") ------------------------------
+__device__ __forceinline__ i64 floor_div_d(i64 a, i64 b) {
+    i64 q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q--;
+    return q;
+}
+__device__ __forceinline__ i64 days_from_civil_d(i64 y, unsigned m, unsigned d) {
+    y -= m <= 2;
+    const i64 era = (y >= 0 ? y : y - 399) / 400;
+    const unsigned yoe = (unsigned)(y - era * 400);
+    const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + (i64)doe - 719468;
+}
+__device__ __forceinline__ void civil_from_days_d(i64 z, i64& y, unsigned& m, unsigned& d) {
+    z += 719468;
+    const i64 era = (z >= 0 ? z : z - 146096) / 146097;
+    const unsigned doe = (unsigned)(z - era * 146097);
+    const unsigned yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    y = (i64)yoe + era * 400;
+    const unsigned doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const unsigned mp = (5 * doy + 2) / 153;
+    d = doy - (153 * mp + 2) / 5 + 1;
+    m = mp + (mp < 10 ? 3 : -9);
+    y += (m <= 2);
+}
+
+// Calendar buckets (aggregation roots `every month` / `every year`, IncrementalTimeConverterUtil with
+// a fixed-offset zone tz): cal 1 = months, 2 = years; the bucket index of t and the start of index i
+__device__ __forceinline__ i64 cal_idx_d(i64 t, int cal, i64 tz) {
+    i64 y; unsigned m, d;
+    civil_from_days_d(floor_div_d(t + tz, 86400000), y, m, d);
+    return cal == 1 ? y * 12 + (i64)(m - 1) : y;
+}
+__device__ __forceinline__ i64 cal_start_d(i64 i, int cal, i64 tz) {
+    if (cal == 1) {
+        const i64 y = floor_div_d(i, 12);
+        return days_from_civil_d(y, (unsigned)(i - y * 12 + 1), 1) * 86400000 - tz;
+    }
+    return days_from_civil_d(i, 1, 1) * 86400000 - tz;
+}
+
 __device__ __forceinline__ i64 key_part(const KeyPlan& kp, const ColSet& cs, int g, i64 e) {
     i64 v = load_raw(cs, kp.col[g], e);
     const int t = kp.type[g];
     if (t == SH_T_FLOAT || t == SH_T_DOUBLE) return __longlong_as_double(v) != __longlong_as_double(v) ? 0x7FF8000000000000ll : v;
-    // aggregation time bucket: getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69)
+    // aggregation time bucket: getStartTimeOfAggregates (IncrementalTimeConverterUtil.java:52-69);
+    // div < 0: a calendar bucket (-1 months, -2 years) in the zone offset `add`
     if (kp.div[g] > 0) v = (v + kp.add[g]) / kp.div[g];
+    else if (kp.div[g] < 0) v = cal_idx_d(v, (int)-kp.div[g], kp.add[g]);
     return v;
 }
 
@@ -258,11 +302,13 @@ __device__ __forceinline__ u64 make_key(const KeyPlan& kp, const ColSet& cs, i64
 // a component as sh_out reports it: int64 widening; floats as the bits of the value widened to double
 __device__ __forceinline__ i64 unpack_part(const KeyPlan& kp, int g, u32 x) {
     if (kp.type[g] == SH_T_FLOAT) return __double_as_longlong((double)__uint_as_float(x));
+    if (kp.div[g] < 0) return cal_start_d((i64)x, (int)-kp.div[g], kp.add[g]);
     return kp.div[g] > 0 ? (i64)x * kp.div[g] - kp.add[g] : (i64)(int)x;
 }
 
 __device__ __forceinline__ void unpack_key(const KeyPlan& kp, u64 key, i64* out, i64 stride) {
-    if (kp.n == 1) out[0] = kp.div[0] > 0 ? (i64)key * kp.div[0] - kp.add[0] : (i64)key;
+    if (kp.n == 1) out[0] = kp.div[0] > 0 ? (i64)key * kp.div[0] - kp.add[0]
+                            : kp.div[0] < 0 ? cal_start_d((i64)key, (int)-kp.div[0], kp.add[0]) : (i64)key;
     else if (kp.n == 2) {
         out[0] = unpack_part(kp, 0, (u32)(key >> 32));
         out[stride] = unpack_part(kp, 1, (u32)key);
@@ -456,6 +502,7 @@ __device__ __forceinline__ i64 wfun(const WinParams& wp, i64 E0, int e0_valid, i
     if (wp.kind == SH_WIN_LENGTH_BATCH) return (wp.n_pend + pcb) / wp.L;
     if (!e0_valid) return wp.W_open;
     if (wp.kind == SH_WIN_EXT_TIME_BATCH) return clock < E0 ? 0 : (clock - E0) / wp.T;
+    if (wp.cal) return clock < E0 ? 0 : cal_idx_d(clock, wp.cal, wp.cal_tz) - cal_idx_d(E0, wp.cal, wp.cal_tz) + 1;
     return clock < E0 ? 0 : (clock - E0) / wp.T + 1;
 }
 
@@ -468,6 +515,7 @@ struct WinCursor {
         if (wp.kind == SH_WIN_LENGTH_BATCH) lim = (W + 1) * wp.L - wp.n_pend;
         else if (!e0v) lim = INT64_MAX;
         else if (wp.kind == SH_WIN_EXT_TIME_BATCH) lim = E0 + (W + 1) * wp.T;
+        else if (wp.cal) lim = cal_start_d(cal_idx_d(E0, wp.cal, wp.cal_tz) + W, wp.cal, wp.cal_tz);
         else lim = E0 + W * wp.T;
     }
     __device__ __forceinline__ i64 at(const WinParams& wp, i64 E0, int e0v, i64 pcb, i64 clk) {

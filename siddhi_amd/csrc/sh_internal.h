@@ -135,6 +135,8 @@ struct WinParams {
     int ts_col, start_col;
     i64 xm0;
     int rec_seq;  // sliding records: the lane-strided form (k_sl_records_seq) where it applies
+    int cal;      // timeBatch of calendar months (1) / years (2) in the zone offset cal_tz (aggregation roots)
+    i64 cal_tz;
 };
 
 // Result of the block-aggregate scan (written by k_scan_blocks, read back by the host).

@@ -199,7 +199,9 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(i64* blk_pass, i64* blk_tl
             if (init_e0) {
                 if (wp.clock_valid) cl = max(cl, wp.clock0);
                 i64 E0;
-                if (wp.has_start) {
+                if (wp.cal) {
+                    E0 = cal_start_d(cal_idx_d(cl, wp.cal, wp.cal_tz) + 1, wp.cal, wp.cal_tz);
+                } else if (wp.has_start) {
                     i64 elapsed = (cl - wp.start_time) % wp.T;  // Java % truncates like C++
                     E0 = cl + (wp.T - elapsed);
                 } else {

@@ -266,6 +266,10 @@ struct sh_query {
     int64_t clock = 0;
     bool e0_valid = false;
     int64_t E0 = 0;
+    // timeBatch windows of calendar months (1) / years (2) in the zone offset cal_tz: the root of an
+    // aggregation `every month` / `every year` (set by the aggregation before its first push)
+    int cal = 0;
+    int64_t cal_tz = 0;
     int64_t W_open = 0;
     int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
     // externalTimeBatch timeout (sh_query_set_ext_timeout): lastScheduledTime, and the open batch's

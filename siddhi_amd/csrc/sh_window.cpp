@@ -78,8 +78,10 @@ int StagedBatch::stage(hipStream_t s, const sh_batch* b, int n_cols, const int32
     return SH_OK;
 }
 
+int64_t cal_idx_h(int64_t t, int cal, int64_t tz);
 static int64_t wfun_host(const sh_query* q, int64_t clock) {
     if (!q->e0_valid) return q->W_open;
+    if (q->cal) return clock < q->E0 ? 0 : cal_idx_h(clock, q->cal, q->cal_tz) - cal_idx_h(q->E0, q->cal, q->cal_tz) + 1;
     return clock < q->E0 ? 0 : (clock - q->E0) / q->d.window_param + 1;
 }
 
@@ -1228,6 +1230,8 @@ static int small_async(sh_query* q, bool* done) {
     wp.e0_valid = q->e0_valid;
     wp.clock_valid = q->clock_valid;
     wp.L = wp.T = q->d.window_param;
+    wp.cal = q->cal;
+    wp.cal_tz = q->cal_tz;
     wp.E0 = q->E0;
     wp.clock0 = q->clock;
     wp.W_open = q->W_open;
@@ -1459,6 +1463,8 @@ static int try_small_push(sh_query* q, const sh_batch* b, bool* done) {
     wp.e0_valid = q->e0_valid;
     wp.clock_valid = q->clock_valid;
     wp.L = wp.T = q->d.window_param;
+    wp.cal = q->cal;
+    wp.cal_tz = q->cal_tz;
     wp.E0 = q->E0;
     wp.clock0 = q->clock;
     wp.W_open = q->W_open;
@@ -1560,6 +1566,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         wp.has_start = q->d.has_start_time;
         wp.L = q->d.window_param;
         wp.T = q->d.window_param;
+        wp.cal = q->cal;
+        wp.cal_tz = q->cal_tz;
         wp.E0 = q->E0;
         wp.start_time = q->d.start_time;
         wp.clock0 = q->clock;

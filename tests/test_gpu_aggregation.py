@@ -59,10 +59,8 @@ def both(rt, spec, pushes, label, checkpoints=()):
     return n_rows
 
 
-# (month / year roots — `every month` or `every year` alone — are not on the GPU: the root runs as a
-# timeBatch of a fixed period; those transcribed tables pin the oracle only, tests/test_oracle_kat.py)
-AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"
-            and c["aggregation"]["durations"][0] not in ("month", "year")]
+# (month / year roots included: the root runs as a timeBatch of calendar months / years)
+AGG_KATS = [c for c in kat_runner.load_cases() if c.get("kind") == "aggregation"]
 
 
 @pytest.mark.parametrize("case", AGG_KATS, ids=[c["name"] for c in AGG_KATS])
@@ -415,3 +413,53 @@ def test_two_group_by_columns_wider_than_64_bits_refused(rt):
                                key_capacity=64)
     with pytest.raises(Exception, match="32-bit"):
         rt.GpuAggregation(spec)
+
+
+@pytest.mark.parametrize("root,tz_hours,proc_time", [("month", 0, False), ("month", 8, False), ("year", -5, False),
+                                                     ("month", 0, True)])
+def test_calendar_roots(rt, root, tz_hours, proc_time):
+    """`every month ...` / `every year` roots: the root window closes at calendar boundaries of the clock
+    (getNextEmitTime MONTHS / YEARS) and its buckets are the events' calendar months / years in the zone
+    offset; late events, idle gaps of several months, retrievals and a checkpoint = oracle."""
+    rng = np.random.default_rng(91)
+    n = 30_000
+    day = 86_400_000
+    step = 40 * day // n if root == "month" else 900 * day // n  # ~40 days or ~2.5 years of clock
+    clock = 1_700_000_000_000 + np.cumsum(rng.integers(0, 2 * step, n)).astype(np.int64)
+    clock[n // 2:] += (95 if root == "month" else 800) * day  # an idle gap
+    ext = clock - rng.integers(0, 20 * day, n).astype(np.int64)
+    k = rng.integers(0, 25, n).astype(np.int32)
+    v = np.round(rng.normal(50, 20, n), 3)
+    schema = abi.Schema.parse("k int, v double, ts long")
+    durs = (root, "year")
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("count", None), ("min", "v"), ("max", "v")], group_by=["k"],
+                               ts=None if proc_time else "ts", durations=durs, key_capacity=32,
+                               tz_offset_ms=tz_hours * 3_600_000)
+    bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], v[a_:b_], ext[a_:b_]], 11)
+    cuts = [0, 5_000, 14_999, 15_000, 22_000, n]
+    g, o = rt.GpuAggregation(spec), OracleAggregation(spec)
+    spans = [(abi.DUR_NAMES[d], 0, 1 << 62) for d in dict.fromkeys(durs)]
+    blob = None
+    for a_, b_ in zip(cuts[:-1], cuts[1:]):
+        for x in (g, o):
+            x.push(bat(a_, b_))
+        assert _finds(g, spans) == _finds(o, spans), f"retrieval after {b_}"
+        if b_ == 14_999:
+            blob = g.snapshot()
+    for x in (g, o):
+        x.advance_time(int(clock[-1]) + 800 * day)
+    ot = tables(o, spec)
+    assert sum(len(t["ts"]) for t in ot.values()) > 0
+    assert_tables_equal(tables(g, spec), ot, f"{root} root")
+    fresh, o2 = rt.GpuAggregation(spec), OracleAggregation(spec)
+    fresh.restore(blob)
+    o2.push(bat(0, 5_000))
+    o2.push(bat(5_000, 14_999))
+    for a_, b_ in zip(cuts[2:-1], cuts[3:]):
+        for x in (fresh, o2):
+            x.push(bat(a_, b_))
+    for x in (fresh, o2):
+        x.advance_time(int(clock[-1]) + 800 * day)
+    assert_tables_equal(tables(fresh, spec), tables(o2, spec), f"{root} root restored")
+    for x in (g, o, fresh, o2):
+        x.close()
