@@ -184,6 +184,14 @@ struct sh_aggregation {
     int64_t root_bucket = 0;
     std::vector<Level> levels;            // durations above the root
     TableBuf tables[SH_DUR_YEARS + 1];
+    // a grown table's old blocks, freed at the next call that synchronises anyway (a hipFree drains the
+    // device: in a push it would stall the queued root and level work)
+    std::vector<DevBuf> retired;
+    // the last push's root flushes, handed to the levels during the next call (agg_settle)
+    bool dfr_on = false;
+    sh_out dfr_out{};
+    std::vector<int64_t> dfr_offs, dfr_windows;
+    int64_t dfr_clock = 0;
     OutHost tout, fout;
     // retrieval scratch (sh_aggregation_find)
     DevBuf m_bucket, m_key, m_vals, f_bucket, f_key, f_vals, g_bucket, g_idx, g_k64, g_k64s, g_idx1, g_idx2, g_dk, g_flag,
@@ -247,6 +255,7 @@ static int agg_verify(sh_aggregation* a) {
 static int agg_sync(sh_aggregation* a) {
     HIPCHK(sh_wait_stream(a->ctx->stream));
     if (a->lstream) HIPCHK(sh_wait_stream(a->lstream));
+    a->retired.clear();  // (both streams are idle: nothing reads the grown tables' old blocks)
     return agg_verify(a);
 }
 
@@ -272,8 +281,9 @@ static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
     hipStream_t s = dur == a->d.min_duration ? a->ctx->stream : lvl(a);
     int64_t need = t.n + rb.n;
     if (need > t.cap) {
-        // (both streams drained: level merges may still read the root table's old block)
-        RCHK(agg_sync(a));
+        // the rows so far copied on the stream that appends to this table (after its earlier appends);
+        // the old block stays allocated until a synchronising call (level merges queued on the other
+        // stream may still read the root table's old block) — no wait inside the push
         int64_t ncap = std::max<int64_t>(need, std::max<int64_t>(1024, t.cap * 2));
         DevBuf b2, k2, v2;
         RCHK(b2.reserve(ncap * 8, false));
@@ -286,8 +296,9 @@ static int table_append(sh_aggregation* a, int dur, const RowBatch& rb) {
                 HIPCHK(hipMemcpyAsync((char*)v2.p + (size_t)b * ncap * 8, (char*)t.vals.p + (size_t)b * t.cap * 8,
                                       t.n * 8, hipMemcpyDeviceToDevice, s));
         }
-        HIPCHK(hipStreamSynchronize(s));
-        StreamScope _sc(s);
+        a->retired.push_back(std::move(t.bucket));
+        a->retired.push_back(std::move(t.key));
+        a->retired.push_back(std::move(t.vals));
         t.bucket = std::move(b2); t.key = std::move(k2); t.vals = std::move(v2);
         t.cap = ncap;
     }
@@ -419,11 +430,10 @@ static int root_timers(sh_aggregation* a, int64_t last, int64_t cb) {
     return SH_OK;
 }
 
-static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
-    sh_query* q = a->root;
+static int pass_root_flushes(sh_aggregation* a, const sh_out* o, const int64_t* windows) {
     int nk = o->n_keys;
     for (int64_t f = 0; f < o->n_flushes; f++) {
-        int64_t W = q->flush_window[f];
+        int64_t W = windows[f];
         int64_t s_f = root_window_start(a, W);  // processing bucket of the closed root store
         int64_t lo = o->flush_offsets[f], hi = o->flush_offsets[f + 1];
         RowBatch rb;
@@ -471,7 +481,7 @@ static int pass_root_flushes(sh_aggregation* a, const sh_out* o) {
 }
 
 // after a push / advance: timers of the root buckets up to the clock
-static int catch_up(sh_aggregation* a) {
+static int catch_up(sh_aggregation* a, int64_t clock) {
     sh_query* q = a->root;
     if (!q->e0_valid) return SH_OK;
     if (!a->root_init) {
@@ -480,12 +490,13 @@ static int catch_up(sh_aggregation* a) {
         a->root_bucket = root_shift(a, q->E0, -1);
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
-    int64_t cb = root_floor(a, q->clock);
+    int64_t cb = root_floor(a, clock);
     RCHK(root_timers(a, a->root_bucket, cb));
     a->root_bucket = std::max(a->root_bucket, cb);
     return SH_OK;
 }
 
+static int agg_mid_hook(void* p);
 static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, int32_t world, sh_shard** shard,
                       sh_aggregation** out) {
     if (!ctx || !d || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_create: NULL argument");
@@ -580,6 +591,10 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     if (rc) { delete a; return rc; }
     a->root->cal = a->cal;
     a->root->cal_tz = a->tz_root;
+    if (!shard) {
+        a->root->mid_hook = agg_mid_hook;
+        a->root->mid_arg = a;
+    }
     if (shard) {
         shard_attach_aggregation(a->shard, a);
         *shard = a->shard;
@@ -778,6 +793,7 @@ static int spec_push(sh_aggregation* a, const sh_batch* dev, const sh_out** o, i
         RCHK(query_swap_keys(q, a->band_spare));
     }
     q->band_spec = true;
+    SH_TMARK(10);
     const int rc = sh_push_device(q, dev, o);
     q->band_spec = false;
     if (rc == kRetryBand) {
@@ -855,7 +871,13 @@ static int ring_collect(sh_aggregation* a, int64_t keep) {
     return SH_OK;
 }
 
+static int agg_settle(sh_aggregation* a);
+static void agg_defer(sh_aggregation* a, const sh_out* o);
+static int agg_mid_hook(void* p);
+
 static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
+    SH_TMARK(11);  // (since the previous push's last point: the caller's time between pushes)
+    SH_TMARK(0);
     const sh_out* o = nullptr;
     sh_batch dev;
     if (a->intern) {  // (the stream's own columns: the interned slot column is the aggregation's)
@@ -890,7 +912,7 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     }
     HIPCHK(hipEventRecord(a->ev0, a->ctx->stream));
     HIPCHK(hipEventRecord(a->r0[rk], a->ctx->stream));
-    SH_TMARK(0);
+    SH_TMARK(9);
     int taken = 0;
     if (!host) RCHK(spec_push(a, &dev, &o, &taken));
     if (!taken) {
@@ -899,9 +921,10 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
         SH_TMARK(7);  // (the root's push marks 0..6 follow)
         RCHK(sh_push_device(a->root, &dev, &o));
     }
+    RCHK(agg_settle(a));  // (pushes that did not reach the root's mid point: no events, small pushes)
     RCHK(agg_verify(a));  // (the root's push synchronised the stream: the last push's level checks are in)
     RCHK(pend_range_queue(a));
-    RCHK(agg_after_root(a, o));
+    agg_defer(a, o);
     SH_TMARK(8);
     // the push's end: its root work (compute stream) and its level work (level stream)
     if (a->lstream) {
@@ -921,6 +944,25 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
 extern "C" int sh_aggregation_timing(sh_aggregation* a, double* total_ms, int64_t* pushes, int32_t reset) {
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !total_ms || !pushes) return sh_fail(SH_ERR_INVALID, "sh_aggregation_timing: NULL argument");
+    if (a->dfr_on) {
+        // the last push's deferred level work belongs to it: timed as part of the sum
+        RCHK(ring_collect(a, sh_aggregation::kRing - 1));
+        const int rk = (int)(a->r_next % sh_aggregation::kRing);
+        if (!a->r0[rk]) {
+            HIPCHK(hipEventCreate(&a->r0[rk]));
+            HIPCHK(hipEventCreate(&a->r1[rk]));
+        }
+        HIPCHK(hipEventRecord(a->r0[rk], a->ctx->stream));
+        RCHK(agg_settle(a));
+        if (a->lstream) {
+            HIPCHK(hipEventRecord(a->ev_tab, a->ctx->stream));
+            HIPCHK(hipStreamWaitEvent(a->lstream, a->ev_tab, 0));
+        }
+        HIPCHK(hipEventRecord(a->r1[rk], lvl(a)));
+        a->r_next++;
+        RCHK(ring_collect(a, 0));
+        a->r_pushes--;  // (the same push: its time, not another push)
+    }
     RCHK(ring_collect(a, 0));
     *total_ms = a->r_ms;
     *pushes = a->r_pushes;
@@ -951,7 +993,7 @@ extern "C" int sh_aggregation_stats(sh_aggregation* a, sh_stats* out) {
     return SH_OK;
 }
 
-int agg_after_root(sh_aggregation* a, const sh_out* o) {
+static int after_root_core(sh_aggregation* a, const sh_out* o, const int64_t* windows, int64_t clock) {
     if (o->n_rows > (8 << 20) / 8 && a->d.n_group_by == 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "too many rows in one flush for a constant key column");
     if (!a->root_init && a->root->e0_valid) {
@@ -959,8 +1001,8 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
         a->root_bucket = root_shift(a, a->root->E0, -1);
         if (!a->levels.empty()) RCHK(level_timer(a, 0, a->root_bucket));
     }
-    RCHK(pass_root_flushes(a, o));
-    RCHK(catch_up(a));
+    RCHK(pass_root_flushes(a, o, windows));
+    RCHK(catch_up(a, clock));
     // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
     for (auto& L : a->levels) {
         if (!L.dirty) continue;
@@ -970,6 +1012,31 @@ int agg_after_root(sh_aggregation* a, const sh_out* o) {
     }
     if (a->chk_pending) HIPCHK(hipEventRecord(a->ev_lchk, lvl(a)));
     return SH_OK;
+}
+
+int agg_after_root(sh_aggregation* a, const sh_out* o) {
+    return after_root_core(a, o, a->root->flush_window.data(), a->root->clock);
+}
+
+// A push's root flushes are handed to the roll-up levels (host logic + the table / level launches, a few
+// hundred microseconds of host time) while the NEXT push's first kernels run: the root query calls
+// back here just before it waits for its boundaries (sh_query.mid_hook). The flushes' rows stay in the
+// root's output buffers until then: the next push writes them only after this work is queued ahead on
+// the same stream. Every other entry point runs the deferred work first (agg_settle).
+static int agg_settle(sh_aggregation* a) {
+    if (!a->dfr_on) return SH_OK;
+    a->dfr_on = false;
+    return after_root_core(a, &a->dfr_out, a->dfr_windows.data(), a->dfr_clock);
+}
+static int agg_mid_hook(void* p) { return agg_settle((sh_aggregation*)p); }
+static void agg_defer(sh_aggregation* a, const sh_out* o) {
+    a->dfr_out = *o;
+    a->dfr_offs.assign(o->flush_offsets, o->flush_offsets + o->n_flushes + 1);
+    a->dfr_out.flush_offsets = a->dfr_offs.data();
+    a->dfr_out.flush_clock = nullptr;
+    a->dfr_windows.assign(a->root->flush_window.begin(), a->root->flush_window.end());
+    a->dfr_clock = a->root->clock;
+    a->dfr_on = true;
 }
 
 extern "C" int sh_aggregation_push(sh_aggregation* a, const sh_batch* b) {
@@ -996,10 +1063,11 @@ extern "C" int sh_aggregation_advance_time(sh_aggregation* a, int64_t now) {
     if (!a) return sh_fail(SH_ERR_INVALID, "sh_aggregation_advance_time: NULL argument");
     if (a->shard) return sh_fail(SH_ERR_STATE, "a sharded aggregation advances through sh_shard_advance_time");
     const sh_out* o = nullptr;
+    RCHK(agg_settle(a));
     a->pr_valid = false;  // (the TIMER may flush the queued events)
     RCHK(sh_advance_time_device(a->root, now, &o));
-    RCHK(pass_root_flushes(a, o));
-    RCHK(catch_up(a));
+    RCHK(pass_root_flushes(a, o, a->root->flush_window.data()));
+    RCHK(catch_up(a, a->root->clock));
     // the merged levels' key-table counters, verified after the next synchronisation (agg_verify)
     for (auto& L : a->levels) {
         if (!L.dirty) continue;
@@ -1031,6 +1099,7 @@ extern "C" int sh_aggregation_table(sh_aggregation* a, int32_t dur, const sh_out
     SH_RANGE("sh_aggregation_table");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_table: NULL argument");
+    RCHK(agg_settle(a));
     if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (dur < a->d.min_duration || dur > a->d.max_duration) return sh_fail(SH_ERR_INVALID, "duration not aggregated");
     TableBuf& t = a->tables[dur];
@@ -1135,6 +1204,7 @@ extern "C" int sh_aggregation_find(sh_aggregation* a, int32_t per, int64_t start
     SH_RANGE("sh_aggregation_find");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !out) return sh_fail(SH_ERR_INVALID, "sh_aggregation_find: NULL argument");
+    RCHK(agg_settle(a));
     if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (per < a->d.min_duration || per > a->d.max_duration)
         return sh_fail(SH_ERR_INVALID, "the aggregation does not contain the `per` duration");
@@ -1378,6 +1448,7 @@ extern "C" int sh_aggregation_snapshot(sh_aggregation* a, void* buf, int64_t cap
     SH_RANGE("sh_aggregation_snapshot");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !len) return sh_fail(SH_ERR_INVALID, "sh_aggregation_snapshot: NULL argument");
+    RCHK(agg_settle(a));
     if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is checkpointed by sh_shard_snapshot");
     ABlob w;
@@ -1494,6 +1565,7 @@ extern "C" int sh_aggregation_restore(sh_aggregation* a, const void* buf, int64_
     SH_RANGE("sh_aggregation_restore");
     StreamScope _ss(a && a->ctx ? a->ctx->stream : nullptr);
     if (!a || !buf || len < 20) return sh_fail(SH_ERR_INVALID, "sh_aggregation_restore: bad arguments");
+    RCHK(agg_settle(a));
     if (a->lstream) HIPCHK(hipStreamSynchronize(a->lstream));  // (the level stream's tables / states)
     if (a->shard) return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation is restored by sh_shard_restore");
     ABlob backup;

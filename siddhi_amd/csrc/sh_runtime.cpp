@@ -28,7 +28,7 @@ int sh_fail(int code, const std::string& msg) {
 
 namespace {
 struct HostTiming {
-    static constexpr int kPts = 12;
+    static constexpr int kPts = 16;
     std::vector<double> d[kPts];
     std::chrono::steady_clock::time_point last;
     int last_pt = -1;

@@ -270,6 +270,10 @@ struct sh_query {
     // aggregation `every month` / `every year` (set by the aggregation before its first push)
     int cal = 0;
     int64_t cal_tz = 0;
+    // called by push_core while the push's first kernels run, before it waits for their results (an
+    // aggregation hands its previous push's root flushes to the roll-up levels there)
+    int (*mid_hook)(void*) = nullptr;
+    void* mid_arg = nullptr;
     int64_t W_open = 0;
     int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
     // externalTimeBatch timeout (sh_query_set_ext_timeout): lastScheduledTime, and the open batch's

@@ -1640,6 +1640,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         if (early_split) RCHK(run_multisplit(q, q->n_pend + N, b, true));
         SH_TRACE("push N=%lld n_pend=%lld: boundaries queued", (long long)N, (long long)q->n_pend);
         SH_TMARK(2);
+        if (q->mid_hook) {
+            RCHK(q->mid_hook(q->mid_arg));
+            SH_TMARK(12);
+        }
         HIPCHK(sh_wait_event(q->ev_mid));
         SH_TMARK(3);
         PushInfo info = *q->h_info;
