@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 13
+#define SH_ABI_VERSION 14
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -97,7 +97,10 @@ typedef struct {
 
 #define SH_MAX_COLS 8
 #define SH_MAX_AGGS 8
-#define SH_MAX_GROUP 2
+/* group-by columns: any number up to SH_MAX_GROUP; one column of any type or two 32-bit ones (int, string
+ * id, bool, float) key the window directly, any other combination is interned on the device into one
+ * 32-bit id per distinct key (needs a spare column slot: n_cols < SH_MAX_COLS; not partitioned or sharded) */
+#define SH_MAX_GROUP 8
 
 /* Compiled form of
  *   [partition with (pcol of S) begin]

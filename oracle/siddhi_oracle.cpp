@@ -323,7 +323,7 @@ int agg_out_type(int fn, int in_type) {
 // 63-73) concatenates toString()+":-:"; for the integral columns used as keys, string equality is
 // value equality, so the key is the tuple of raw values.
 struct GKey {
-    int64_t k[SH_MAX_GROUP + 1] = {0, 0, 0};
+    int64_t k[SH_MAX_GROUP + 1] = {};
     bool operator==(const GKey& o) const { return k[0] == o.k[0] && k[1] == o.k[1] && k[2] == o.k[2]; }
 };
 struct GKeyHash {
@@ -1094,7 +1094,7 @@ struct BaseDef { int kind; int col; int type; };  // type: LONG or DOUBLE for su
 // base executor is sum()/min()/max() in BATCH mode over the per-key rows.
 struct BaseRow {
     int64_t ext = 0;  // AGG_EXTERNAL_TIMESTAMP bucket at this duration (or 0)
-    int64_t keys[SH_MAX_GROUP] = {0, 0};
+    int64_t keys[SH_MAX_GROUP] = {};
     std::vector<std::unique_ptr<AggState>> st;  // per base value
     std::vector<AggOut> val;                    // last value returned by each executor
 };

@@ -33,7 +33,7 @@ AGG_NAMES = {"sum": AGG_SUM, "avg": AGG_AVG, "count": AGG_COUNT, "min": AGG_MIN,
 DUR_SECONDS, DUR_MINUTES, DUR_HOURS, DUR_DAYS, DUR_MONTHS, DUR_YEARS = range(6)
 DUR_NAMES = {"sec": 0, "min": 1, "hour": 2, "day": 3, "month": 4, "year": 5}
 
-MAX_COLS, MAX_AGGS, MAX_GROUP = 8, 8, 2
+MAX_COLS, MAX_AGGS, MAX_GROUP = 8, 8, 8
 
 
 class FilterOp(C.Structure):

@@ -18,6 +18,7 @@
 
 #include "sh_agg.h"
 #include "sh_runtime.h"
+#include "sh_wide.h"
 
 using namespace shd;
 
@@ -236,9 +237,8 @@ struct sh_aggregation {
     // slot travels as a synthetic dictionary column (index d.n_cols of the root's batch); tables and
     // retrievals map the slots back to the group-by values (k_agg_unintern)
     bool intern = false;
-    KeyPlan ikp{};
-    KeyTableHost ikt;
-    DevBuf ids, dkeys;
+    WideKeys wk;  // (sh_wide.h: any number of group-by columns, 64-bit ones included)
+    DevBuf dkeys;
 };
 
 // The levels' key-table overflow checks are queued with each merge and verified after the next
@@ -565,18 +565,17 @@ static int agg_create(sh_ctx* ctx, const sh_aggregation_desc* d, int32_t rank, i
     int gtype = -1;  // the root key's group component type
     if (d->n_group_by >= 1) {
         const int t = d->col_types[d->group_by[0]];
-        a->intern = d->n_group_by == 2 ||
+        a->intern = d->n_group_by >= 2 ||
                     !(t == SH_T_INT || t == SH_T_STRID || t == SH_T_BOOL || (t == SH_T_LONG && !a->has_bucket));
         if (a->intern) {
             if (shard) { delete a; return sh_fail(SH_ERR_UNSUPPORTED, "a sharded aggregation groups by one 32-bit column"); }
-            int rc0 = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, a->ikp);
-            if (!rc0) rc0 = a->ikt.init(rd.key_capacity);
-            if (rc0) { delete a; return rc0; }
             if (d->n_cols + 1 > SH_MAX_COLS) { delete a; return sh_fail(SH_ERR_UNSUPPORTED, "too many columns to intern group keys"); }
-            // the interned slot: a dictionary column past the stream's own (dense in [0, slots))
+            int rc0 = a->wk.init(d->n_group_by, d->group_by, d->n_cols, d->col_types, rd.key_capacity);
+            if (rc0) { delete a; return rc0; }
+            // the interned id: a dictionary column past the stream's own (dense in [0, id space))
             rd.n_cols = d->n_cols + 1;
             rd.col_types[d->n_cols] = SH_T_STRID;
-            rd.key_capacity = (int64_t)a->ikt.size_ + 1;
+            rd.key_capacity = a->wk.id_space();
             kp.col[g] = d->n_cols; kp.type[g] = SH_T_STRID; kp.div[g] = 0; g++;
             gtype = SH_T_STRID;
         } else {
@@ -894,15 +893,13 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
         dev = *b;
     }
     if (a->intern) {
-        // every passing event's group key -> its intern slot, the root's synthetic dictionary column
-        RCHK(a->ids.reserve((size_t)std::max<int64_t>(dev.n, 1) * 4, false));
+        // every passing event's group key -> its interned id, the root's synthetic dictionary column
         ColSet cs{};
         cs.n = a->d.n_cols;
         for (int c = 0; c < a->d.n_cols; c++) { cs.type[c] = a->d.col_types[c]; cs.ptr[c] = dev.cols[c]; }
-        launch_agg_intern(a->ctx->stream, cs, a->root->fp, a->ikp, a->ikt.dev(), dev.n, a->ids.as<u32>());
-        HIPCHK(hipGetLastError());
-        RCHK(a->ikt.check(a->ctx->stream));
-        dev.cols[a->d.n_cols] = a->ids.p;
+        const uint32_t* ids = nullptr;
+        RCHK(a->wk.intern(a->ctx->stream, cs, a->root->fp, dev.n, &ids));
+        dev.cols[a->d.n_cols] = ids;
     }
     RCHK(ring_collect(a, sh_aggregation::kRing - 1));
     const int rk = (int)(a->r_next % sh_aggregation::kRing);
@@ -1089,7 +1086,7 @@ static int agg_keys_out(sh_aggregation* a, const int64_t* keys, int64_t n, int64
     }
     const int ng = a->d.n_group_by;
     RCHK(a->dkeys.reserve((size_t)ng * n * 8, false));
-    launch_agg_unintern(s, keys, n, a->ikt.dev(), a->ikp, a->dkeys.as<int64_t>());
+    RCHK(a->wk.decode(s, keys, n, a->dkeys.as<int64_t>()));
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(host, a->dkeys.p, (size_t)ng * n * 8, hipMemcpyDeviceToHost, s));
     return SH_OK;
@@ -1175,7 +1172,7 @@ static int group_fold(sh_aggregation* a, const int64_t* bucket, const int64_t* k
     if (a->intern) {
         const int ng = a->d.n_group_by;
         RCHK(a->g_dk.reserve((size_t)ng * n * 8, false));
-        launch_agg_unintern(s, key, n, a->ikt.dev(), a->ikp, a->g_dk.as<int64_t>());
+        RCHK(a->wk.decode(s, key, n, a->g_dk.as<int64_t>()));
         for (int x = ng - 1; x >= 0; x--) RCHK(pass(a->g_dk.as<int64_t>() + (size_t)x * n, 1ull << 63));
     } else {
         RCHK(pass(key, 0));
@@ -1436,10 +1433,11 @@ static int agg_state_write(sh_aggregation* a, ABlob& w) {
         RCHK(w.dev(t.key.p, t.n * 8, s));
         for (int b = 0; b < a->nb; b++) RCHK(w.dev(t.vals.as<u64>() + (size_t)b * t.cap, t.n * 8, s));
     }
-    if (a->intern) {  // the interned group keys (their slots are the root's and the tables' keys)
-        RCHK(a->ikt.check(s));
-        w.val<int64_t>(a->ikt.n_keys);
-        RCHK(w.dev(a->ikt.keys.p, a->ikt.size_ * 8, s));
+    if (a->intern) {  // the interned group keys (their ids are the root's and the tables' keys)
+        std::vector<uint8_t> kb;
+        RCHK(a->wk.save(kb, s));
+        w.val<uint64_t>(kb.size());
+        w.b.insert(w.b.end(), kb.begin(), kb.end());
     }
     return SH_OK;
 }
@@ -1525,15 +1523,11 @@ static int agg_state_read(sh_aggregation* a, AReader& r) {
         t.drained = drained;
     }
     if (a->intern) {
-        const int64_t nk = r.val<int64_t>();
-        if (!r.ok || nk < 0 || nk > (int64_t)a->ikt.size_ + 1) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
-        RCHK(r.dev(a->ikt.keys.p, (int64_t)a->ikt.size_ * 8, s));
-        RCHK(a->ikt.h_ctrl.reserve(16));
-        uint32_t* c = a->ikt.h_ctrl.as<uint32_t>();
-        c[0] = (uint32_t)nk; c[1] = c[2] = c[3] = 0;
-        HIPCHK(hipMemcpyAsync(a->ikt.ctrl.p, c, 16, hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));
-        a->ikt.n_keys = nk;
+        const uint64_t kn = r.val<uint64_t>();
+        if (!r.ok || r.o + kn > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        size_t off = 0;
+        RCHK(a->wk.load(r.p + r.o, (size_t)kn, off, s));
+        r.o += kn;
     }
     if (!r.ok) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     return SH_OK;

@@ -52,6 +52,7 @@ extern "C" int sh_stage(sh_query* q, const sh_batch* b, int32_t* ticket) {
     if (b->n < 0) return sh_fail(SH_ERR_INVALID, "negative batch size");
     if (b->n > 0 && !b->ts) return sh_fail(SH_ERR_INVALID, "batch without timestamps");
     RCHK(check_batch_cols(q, b));
+    if (q->wide) return sh_fail(SH_ERR_UNSUPPORTED, "queries with wide group keys take sh_push / sh_push_device");
     auto& g = q->ing;
     if (g.outstanding >= 2) return sh_fail(SH_ERR_INVALID, "sh_stage: two staged batches are waiting for sh_push_staged");
     RCHK(ingest_init(q));

@@ -86,13 +86,16 @@ struct AggPlan {
 enum FieldOp { FOP_ADD_I = 0, FOP_ADD_D, FOP_ADD_DI, FOP_MIN_I, FOP_MAX_I, FOP_MIN_D, FOP_MAX_D, FOP_MIN_F, FOP_MAX_F };
 
 // Group key plan: 0, 1 or 2 integral columns packed into a u64.
+// a window's key: one column of any type or two 32-bit columns packed into one u64 (wider group keys are
+// interned first, sh_wide.h, and key the window by their 32-bit id)
+constexpr int kKeyParts = 2;
 struct KeyPlan {
     int n;
-    int col[SH_MAX_GROUP];
-    int type[SH_MAX_GROUP];
+    int col[kKeyParts];
+    int type[kKeyParts];
     int dense;  // one STRID column: dictionary ids are dense in [0, key_capacity) -> slot = id
-    i64 div[SH_MAX_GROUP];  // > 0: the component is (u32)((value + add) / div) (aggregation time buckets)
-    i64 add[SH_MAX_GROUP];  // (the aggregation time zone's offset for hour / day buckets)
+    i64 div[kKeyParts];  // > 0: the component is (u32)((value + add) / div) (aggregation time buckets)
+    i64 add[kKeyParts];  // (the aggregation time zone's offset for hour / day buckets)
 };
 
 // Hash table (key -> position = group slot). positions [0, mask] plus the reserved mask+1

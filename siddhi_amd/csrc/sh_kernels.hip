@@ -1081,7 +1081,7 @@ __host__ __device__ constexpr int stage_words(int nk, int na, int order) { retur
 // slot. The records of a wave are then stored cooperatively through LDS: consecutive lanes write
 // consecutive 16-byte pieces of one record, so each store instruction covers whole 64-byte records
 // instead of one piece of 64 scattered ones.
-constexpr int kStageMax = 2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1;
+constexpr int kStageMax = 2 + kKeyParts + 1 + SH_MAX_AGGS + 1;
 __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ rows, int RW,
                                                      const u32* __restrict__ unit_rows, i64 n_units,
                                                      int unit_stride,
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_rank(const u64* __restrict__ ro
         u64 w[kStageMax + 1];
         const ulonglong2 tr = *(const ulonglong2*)(row + 2);  // the last event's timestamp and stream index
         w[0] = tr.x;
-        i64 kv[SH_MAX_GROUP] = {0, 0};
+        i64 kv[kKeyParts] = {0, 0};
         unpack_key(kp, slot_key(kt, pos), kv, 1);
         w[1] = tr.y;
         w[2] = (u64)kv[0];
@@ -1155,9 +1155,9 @@ __global__ __launch_bounds__(kBlock) void k_emit_soa(const u64* __restrict__ sta
     (void)out_cap;
     const int SW = stage_words(nk, n_aggs, want_order);
     const u64* src = stage + (size_t)o * SW;
-    u64 w[2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1];
+    u64 w[2 + kKeyParts + 1 + SH_MAX_AGGS + 1];
 #pragma unroll
-    for (int i = 0; i < (2 + SH_MAX_GROUP + 1 + SH_MAX_AGGS + 1) / 2; i++) {
+    for (int i = 0; i < (2 + kKeyParts + 1 + SH_MAX_AGGS + 1) / 2; i++) {
         if (2 * i >= SW) break;
         const ulonglong2 v = ((const ulonglong2*)src)[i];
         w[2 * i] = v.x;
@@ -1266,7 +1266,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_gather(const u64* __restrict__ 
         const i64 o = o0 + j;
         out_ts[o] = (i64)h0.x;
         out_rep[o] = (i64)h0.y;
-        i64 kv[SH_MAX_GROUP] = {0, 0};
+        i64 kv[kKeyParts] = {0, 0};
         unpack_key(kp, slot_key(kt, slot), kv, 1);
         for (int k = 0; k < nk; k++) out_keys[(size_t)k * n + o] = kv[k];
         if (out_order)
@@ -1942,7 +1942,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
     const u32 l = slast[m];
     out_ts[o] = pend_ts[l];
     out_rep[o] = (i64)pend_gidx[l];
-    i64 kv[SH_MAX_GROUP] = {0, 0};
+    i64 kv[kKeyParts] = {0, 0};
     unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
@@ -2069,7 +2069,7 @@ __global__ __launch_bounds__(kBlock) void k_scx_expired(i64 M, i64 n_old, const 
     const i64 o = base[jb] + rank;
     out_ts[o] = tb ? bclk[w] : send_clock[send[mb]];  // (timeBatch: mb may be past the push's entries)
     out_rep[o] = (i64)pend_gidx[lastidx[m]];
-    i64 kv[SH_MAX_GROUP] = {0, 0};
+    i64 kv[kKeyParts] = {0, 0};
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < ap.n; a++) {
@@ -2104,7 +2104,7 @@ __global__ __launch_bounds__(kBlock) void k_scx_current(i64 M, i64 n_old, const 
     }
     out_ts[o] = pend_ts[m];
     out_rep[o] = (i64)pend_gidx[m];
-    i64 kv[SH_MAX_GROUP] = {0, 0};
+    i64 kv[kKeyParts] = {0, 0};
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) {
@@ -2189,7 +2189,7 @@ __global__ __launch_bounds__(kBlock) void k_scxt_current(i64 M, i64 n_old, const
     const u32 l = slast[m];
     out_ts[o] = pend_ts[l];
     out_rep[o] = (i64)pend_gidx[l];
-    i64 kv[SH_MAX_GROUP] = {0, 0};
+    i64 kv[kKeyParts] = {0, 0};
     unpack_key(kp, slot_key(kt, (u32)key), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) {
@@ -2214,7 +2214,7 @@ __global__ __launch_bounds__(kBlock) void k_scx_pending_rows(i64 M, const u32* _
     const i64 o = fpre[m];
     out_ts[o] = now;
     out_rep[o] = (i64)pend_gidx[lastidx[m]];
-    i64 kv[SH_MAX_GROUP] = {0, 0};
+    i64 kv[kKeyParts] = {0, 0};
     unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < ap.n; a++) {

@@ -351,6 +351,8 @@ int compile_keys(int n_group, const int32_t* group, int n_cols, const int32_t* t
     kp = KeyPlan{};
     kp.n = n_group;
     if (n_group < 0 || n_group > SH_MAX_GROUP) return sh_fail(SH_ERR_INVALID, "bad group-by count");
+    if (n_group > kKeyParts)
+        return sh_fail(SH_ERR_UNSUPPORTED, "more than two group-by columns key this window only interned (sh_wide.h)");
     for (int g = 0; g < n_group; g++) {
         int c = group[g];
         if (c < 0 || c >= n_cols) return sh_fail(SH_ERR_INVALID, "group-by column out of range");

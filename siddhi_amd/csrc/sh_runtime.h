@@ -233,6 +233,7 @@ struct Tuning {
     static Tuning from_env();
 };
 
+struct WideKeys;
 struct sh_query {
     int kind = 0;
     Tuning tune = Tuning::from_env();            // 0 = batch window (lengthBatch/timeBatch), 1 = sliding time window
@@ -274,6 +275,14 @@ struct sh_query {
     // aggregation hands its previous push's root flushes to the roll-up levels there)
     int (*mid_hook)(void*) = nullptr;
     void* mid_arg = nullptr;
+    // wide group keys (sh_wide.h): the window is keyed by an interned id in a synthetic column past the
+    // stream's own (d.n_cols = wide_n_cols + 1); rows get their group-by values back at the end of a call
+    WideKeys* wide = nullptr;
+    int wide_n_cols = 0;
+    uint64_t wide_cols_used = 0;  // the stream columns a batch must carry
+    DevBuf wide_keys;
+    sh_out wide_out{};
+    OutHost wide_host;
     int64_t W_open = 0;
     int64_t xm = 0;  // externalTimeBatch: lastCurrentEventTime (running max of the timestamp attribute)
     // externalTimeBatch timeout (sh_query_set_ext_timeout): lastScheduledTime, and the open batch's

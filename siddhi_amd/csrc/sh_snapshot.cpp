@@ -19,6 +19,7 @@
 
 #include "sh_internal.h"
 #include "sh_runtime.h"
+#include "sh_wide.h"
 
 using namespace shd;
 
@@ -358,7 +359,14 @@ static int query_snapshot_blob(sh_query* q, Writer& w) {
     w.val<uint64_t>(fingerprint(q));
     w.val<uint32_t>((uint32_t)q->kind);
     RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
-    return rate_snapshot(q, w);
+    RCHK(rate_snapshot(q, w));
+    if (q->wide) {  // the interned group keys (the window's key ids)
+        std::vector<uint8_t> kb;
+        RCHK(q->wide->save(kb, q->ctx->stream));
+        w.val<uint64_t>(kb.size());
+        w.put(kb.data(), kb.size());
+    }
+    return SH_OK;
 }
 
 extern "C" int sh_query_snapshot(sh_query* q, void* buf, int64_t cap, int64_t* len) {
@@ -386,7 +394,15 @@ static int query_restore_blob(sh_query* q, const void* buf, int64_t len) {
     RCHK(query_drain_async(q));  // a queued report must not land on the restored counters
     (void)hipStreamSynchronize(q->ctx->stream);
     RCHK(q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r));
-    return rate_restore(q, r);
+    RCHK(rate_restore(q, r));
+    if (q->wide) {
+        const uint64_t kn = r.val<uint64_t>();
+        if (!r.ok || r.o + kn > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        size_t off = 0;
+        RCHK(q->wide->load(r.p + r.o, (size_t)kn, off, q->ctx->stream));
+        r.o += kn;
+    }
+    return SH_OK;
 }
 
 // A restore either applies the whole blob or leaves the query as it was: the current state is

@@ -17,6 +17,7 @@
 #include "sh_agg.h"
 #include "sh_internal.h"
 #include "sh_runtime.h"
+#include "sh_wide.h"
 
 using namespace shd;
 
@@ -189,8 +190,46 @@ int query_reserve_keys(sh_query* q, int64_t extra) {
     return compacted && want == q->kt.size_ ? SH_OK : rekey(q, want);
 }
 
+// Group keys the window cannot key directly (three or more columns, a long / double beside another
+// column; GroupByKeyGenerator.java:63-73): the query is built over the stream plus one synthetic
+// dictionary column holding every event's interned key id (sh_wide.h), grouped by that column alone.
+static int wide_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
+    if (d->partition_col >= 0)
+        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned queries group by one column or two 32-bit ones");
+    if (d->n_cols <= 0 || d->n_cols >= SH_MAX_COLS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "wide group keys need a spare column slot (fewer than 8 columns)");
+    for (int i = 0; i < d->n_group_by; i++)
+        if (d->group_by[i] < 0 || d->group_by[i] >= d->n_cols) return sh_fail(SH_ERR_INVALID, "group-by column out of range");
+    for (int c = 0; c < d->n_cols; c++)
+        if (d->col_types[c] < SH_T_INT || d->col_types[c] > SH_T_BOOL) return sh_fail(SH_ERR_INVALID, "bad column type");
+    WideKeys* w = new WideKeys();
+    int rc = w->init(d->n_group_by, d->group_by, d->n_cols, d->col_types,
+                     d->key_capacity > 0 ? d->key_capacity : (1 << 16));
+    if (rc) { delete w; return rc; }
+    sh_query_desc in = *d;
+    in.n_cols = d->n_cols + 1;
+    in.col_types[d->n_cols] = SH_T_STRID;
+    in.n_group_by = 1;
+    in.group_by[0] = d->n_cols;
+    in.key_capacity = w->id_space();
+    sh_query* q = nullptr;
+    if ((rc = query_create(ctx, &in, nullptr, &q))) { delete w; return rc; }
+    q->wide = w;
+    q->wide_n_cols = d->n_cols;
+    uint32_t m = q->cols_used & ~(1u << d->n_cols);
+    for (int i = 0; i < d->n_group_by; i++) m |= 1u << d->group_by[i];
+    q->wide_cols_used = m;
+    *out = q;
+    return SH_OK;
+}
+
 extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
     StreamScope _ss(ctx ? ctx->stream : nullptr);
+    if (d && out && d->n_group_by > 0 && d->n_group_by <= SH_MAX_GROUP && d->n_cols > 0 && d->n_cols <= SH_MAX_COLS) {
+        bool in_range = true;
+        for (int i = 0; i < d->n_group_by; i++) in_range &= d->group_by[i] >= 0 && d->group_by[i] < d->n_cols;
+        if (in_range && WideKeys::needed(d->n_group_by, d->group_by, d->col_types)) return wide_create(ctx, d, out);
+    }
     return query_create(ctx, d, nullptr, out);
 }
 
@@ -1811,8 +1850,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
 // calls run_closed at most once.
 int check_batch_cols(const sh_query* q, const sh_batch* b) {
     if (b->n <= 0) return SH_OK;
-    for (int c = 0; c < q->d.n_cols; c++)
-        if ((q->cols_used >> c & 1) && !b->cols[c])
+    const int nc = q->wide ? q->wide_n_cols : q->d.n_cols;
+    const uint64_t used = q->wide ? q->wide_cols_used : q->cols_used;
+    for (int c = 0; c < nc; c++)
+        if ((used >> c & 1) && !b->cols[c])
             return sh_fail(SH_ERR_INVALID, "batch column " + std::to_string(c) + " is NULL but the query reads it");
     return SH_OK;
 }
@@ -1823,7 +1864,7 @@ extern "C" int sh_push(sh_query* q, const sh_batch* b, const sh_out** out) {
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push: NULL argument");
     RCHK(check_batch_cols(q, b));
     sh_batch dev;
-    RCHK(q->staged.stage(q->ctx->stream, b, q->d.n_cols, q->d.col_types, &dev));
+    RCHK(q->staged.stage(q->ctx->stream, b, q->wide ? q->wide_n_cols : q->d.n_cols, q->d.col_types, &dev));
     return query_push_staged(q, &dev, out);
 }
 
@@ -1907,6 +1948,9 @@ extern "C" int sh_query_set_ext_replace_ts(sh_query* q, int32_t on) {
     for (int i = 0; i < q->d.n_group_by; i++)
         if (q->d.group_by[i] == q->d.ts_col)
             return sh_fail(SH_ERR_UNSUPPORTED, "replaceTimestampWithBatchEndTime with a group-by on the timestamp attribute");
+    for (int i = 0; q->wide && i < q->wide->n; i++)
+        if (q->wide->col[i] == q->d.ts_col)
+            return sh_fail(SH_ERR_UNSUPPORTED, "replaceTimestampWithBatchEndTime with a group-by on the timestamp attribute");
     for (int i = 0; i < q->d.n_aggs; i++)
         if (q->d.aggs[i].fn != SH_AGG_COUNT && q->d.aggs[i].col == q->d.ts_col)
             return sh_fail(SH_ERR_UNSUPPORTED,
@@ -1966,7 +2010,9 @@ int query_peek(sh_query* q, int64_t* n_rows) {
 }
 
 // a push whose batch is already on the device, with host output (sh_push_staged)
+static int wide_push(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out);
 int query_push_staged(sh_query* q, const sh_batch* dev, const sh_out** out) {
+    if (q->wide) return wide_push(q, dev, true, out);
     return push_any(q, dev, true, out);
 }
 
@@ -1975,7 +2021,74 @@ extern "C" int sh_push_device(sh_query* q, const sh_batch* b, const sh_out** out
     StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
     if (!q || !b || !out) return sh_fail(SH_ERR_INVALID, "sh_push_device: NULL argument");
     RCHK(check_batch_cols(q, b));
+    if (q->wide) return wide_push(q, b, false, out);
     return push_any(q, b, false, out);
+}
+
+// ---- wide group keys: intern before the window, decode after it -----------------------------------
+// the call's device output with its rows' group-by values decoded; host output copies every column
+static int wide_finish(sh_query* q, bool host_out, const sh_out** out) {
+    hipStream_t s = q->ctx->stream;
+    const sh_out& o = **out;
+    const int64_t n = o.n_rows;
+    const int N = q->wide->n;
+    RCHK(q->wide_keys.reserve((size_t)std::max<int64_t>(n, 1) * N * 8, false));
+    RCHK(q->wide->decode(s, o.keys, n, q->wide_keys.as<int64_t>()));
+    sh_out v = o;
+    v.n_keys = N;
+    v.keys = q->wide_keys.as<int64_t>();
+    if (!host_out) {
+        q->wide_out = v;
+        *out = &q->wide_out;
+        return SH_OK;
+    }
+    OutHost& h = q->wide_host;
+    h.reset();
+    h.ts.resize(n);
+    h.expired.resize(n);
+    h.rep.resize(n);
+    h.keys.resize((size_t)N * n);
+    h.vals.resize((size_t)v.n_vals * n);
+    h.nulls.resize((size_t)v.n_vals * n);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(h.ts.data(), v.ts, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h.expired.data(), v.expired, n, hipMemcpyDeviceToHost, s));
+        if (v.rep) HIPCHK(hipMemcpyAsync(h.rep.data(), v.rep, n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h.keys.data(), v.keys, (size_t)N * n * 8, hipMemcpyDeviceToHost, s));
+        if (v.n_vals) {
+            HIPCHK(hipMemcpyAsync(h.vals.data(), v.vals, (size_t)v.n_vals * n * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(h.nulls.data(), v.nulls, (size_t)v.n_vals * n, hipMemcpyDeviceToHost, s));
+        }
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (v.flush_offsets) {
+        h.flush_offsets.assign(v.flush_offsets, v.flush_offsets + v.n_flushes + 1);
+        h.flush_clock.assign(v.flush_clock, v.flush_clock + v.n_flushes);
+    }
+    if (!v.rep) h.rep.assign(n, -1);
+    h.view(N, v.n_vals, v.val_types);
+    if (!v.flush_offsets) {  // (compact flushes: one row each at its timestamp)
+        h.out.n_flushes = v.n_flushes;
+        h.out.flush_offsets = nullptr;
+        h.out.flush_clock = nullptr;
+    }
+    *out = &h.out;
+    return SH_OK;
+}
+
+static int wide_push(sh_query* q, const sh_batch* dev, bool host_out, const sh_out** out) {
+    hipStream_t s = q->ctx->stream;
+    sh_batch b = *dev;
+    const uint32_t* ids = nullptr;
+    if (b.n > 0) {
+        ColSet full{};
+        full.n = q->wide_n_cols;
+        for (int c = 0; c < q->wide_n_cols; c++) { full.type[c] = q->d.col_types[c]; full.ptr[c] = b.cols[c]; }
+        RCHK(q->wide->intern(s, full, q->fp, b.n, &ids));
+    }
+    b.cols[q->wide_n_cols] = ids;
+    RCHK(push_any(q, &b, false, out));
+    return wide_finish(q, host_out, out);
 }
 
 static int advance_core(sh_query* q, int64_t now, bool host_out_req, const sh_out** out) {
@@ -2044,6 +2157,16 @@ extern "C" int sh_advance_time(sh_query* q, int64_t now, const sh_out** out) {
 }
 
 static int advance_any(sh_query* q, int64_t now, const sh_out** out) {
+    if (q->wide) {  // (device output, then the group-by values decoded and copied to the host)
+        if (q->kind == 1) {
+            RCHK(sliding_advance(q, now, out, false));
+            if (q->rate.kind != SH_RATE_NONE) RCHK(rate_apply(q, *out, true, false, out));
+        } else {
+            RCHK(advance_core(q, now, false, out));
+            if (q->rate.kind != SH_RATE_NONE) RCHK(rate_apply(q, *out, false, false, out));
+        }
+        return wide_finish(q, true, out);
+    }
     if (q->kind == 1) {
         if (q->rate.kind == SH_RATE_NONE) return sliding_advance(q, now, out, true);
         RCHK(sliding_advance(q, now, out, false));  // the TIMER chunks' rows reach the limiter too
@@ -2081,6 +2204,7 @@ extern "C" int sh_query_destroy(sh_query* q) {
     q->kt.release();
     q->gkt.release();
     q->pgkt.release();
+    delete q->wide;
     if (q->h_info) (void)hipHostFree(q->h_info);
     if (q->small_res) (void)hipHostFree(q->small_res);
     if (q->zc_ring) (void)hipHostFree(q->zc_ring);

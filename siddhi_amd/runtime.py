@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 13:
+        if L.sh_abi_version() != 14:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib

@@ -348,6 +348,7 @@ def test_device_pushes_speculative_band(rt):
     ("k int, s string, v double, ts long", ["k", "s"]),
     ("k long, s string, v double, ts long", ["k"]),
     ("k int, s string, v double, ts long", ["s", "k"]),
+    ("k long, s string, v double, ts long", ["s", "k"]),
 ])
 def test_interned_group_keys_rollups_retrieval_checkpoint(rt, schema_text, group_by):
     """`group by a, b` and `group by <long>` under `aggregate by`: the group key is interned to a dense
@@ -406,15 +407,6 @@ def test_agg_time_zone_offset_buckets(rt, tz_hours):
     assert both(rt, spec, pushes, f"tz{tz_hours}", checkpoints=(0, 1)) > 0
 
 
-def test_two_group_by_columns_wider_than_64_bits_refused(rt):
-    """Two group-by columns intern as one 64-bit key: a long beside another column is refused."""
-    schema = abi.Schema.parse("k long, s string, v double, ts long")
-    spec = abi.AggregationSpec(schema, [("sum", "v")], group_by=["s", "k"], ts="ts", durations=("sec", "min"),
-                               key_capacity=64)
-    with pytest.raises(Exception, match="32-bit"):
-        rt.GpuAggregation(spec)
-
-
 @pytest.mark.parametrize("root,tz_hours,proc_time", [("month", 0, False), ("month", 8, False), ("year", -5, False),
                                                      ("month", 0, True)])
 def test_calendar_roots(rt, root, tz_hours, proc_time):
@@ -462,4 +454,40 @@ def test_calendar_roots(rt, root, tz_hours, proc_time):
         x.advance_time(int(clock[-1]) + 800 * day)
     assert_tables_equal(tables(fresh, spec), tables(o2, spec), f"{root} root restored")
     for x in (g, o, fresh, o2):
+        x.close()
+
+
+def test_three_group_by_columns_rollups_and_retrieval(rt):
+    """`group by k, s, l` (int, string, long) under `aggregate by`: interned by the chain of sh_wide.h;
+    tables, retrievals and a checkpoint = oracle."""
+    rng = np.random.default_rng(73)
+    n = 30_000
+    clock = 1_706_745_000_000 + np.cumsum(rng.integers(0, 30, n)).astype(np.int64)
+    ext = clock - rng.integers(0, 40_000, n).astype(np.int64)
+    schema = abi.Schema.parse("k int, s string, l long, v double, ts long")
+    k = rng.integers(-4, 5, n).astype(np.int32)
+    s = rng.integers(0, 4, n).astype(np.int32)
+    l = (rng.integers(0, 5, n) * 7_000_000_001).astype(np.int64)
+    v = np.round(rng.normal(50, 20, n), 3)
+    spec = abi.AggregationSpec(schema, [("sum", "v"), ("count", None), ("max", "v")], group_by=["s", "k", "l"],
+                               ts="ts", durations=("sec", "hour"), key_capacity=512)
+    bat = lambda a_, b_: abi.HostBatch(schema, clock[a_:b_], [k[a_:b_], s[a_:b_], l[a_:b_], v[a_:b_], ext[a_:b_]], 5)
+    g, o = rt.GpuAggregation(spec), OracleAggregation(spec)
+    spans = [(abi.DUR_NAMES[d], 0, 1 << 62) for d in ("sec", "min", "hour")]
+    for a_, b_ in ((0, 9_000), (9_000, 21_000)):
+        for x in (g, o):
+            x.push(bat(a_, b_))
+        assert _finds(g, spans) == _finds(o, spans)
+    blob = g.snapshot()
+    fresh = rt.GpuAggregation(spec)
+    fresh.restore(blob)
+    for x in (g, fresh, o):
+        x.push(bat(21_000, n))
+    assert _finds(fresh, spans) == _finds(o, spans) == _finds(g, spans)
+    for x in (g, o):
+        x.advance_time(int(clock[-1]) + 7_200_000)
+    ot = tables(o, spec)
+    assert all(t["keys"].shape[0] == 4 for t in ot.values())
+    assert_tables_equal(tables(g, spec), ot, "three group-by columns")
+    for x in (g, fresh, o):
         x.close()
