@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -877,6 +878,8 @@ static int agg_mid_hook(void* p);
 static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     SH_TMARK(11);  // (since the previous push's last point: the caller's time between pushes)
     SH_TMARK(0);
+    static const bool atrace = getenv("SH_ALLOC_TRACE") != nullptr;
+    if (atrace) fprintf(stderr, "[sh alloc] --- push %lld\n", (long long)a->r_next);
     const sh_out* o = nullptr;
     sh_batch dev;
     if (a->intern) {  // (the stream's own columns: the interned slot column is the aggregation's)

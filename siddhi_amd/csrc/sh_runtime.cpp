@@ -109,6 +109,9 @@ int DevBuf::reserve(size_t n, bool keep) {
     if (n <= cap) return SH_OK;
     size_t ncap = std::max(n, cap + cap / 2);
     void* np = nullptr;
+    static const bool trace = getenv("SH_ALLOC_TRACE") != nullptr;  // (diagnostics: growth in a push)
+    if (trace && ncap >= (1u << 20))
+        fprintf(stderr, "[sh alloc] %zu -> %zu bytes (keep %d)\n", cap, ncap, (int)keep);
     hipError_t e = hipMalloc(&np, ncap);
     if (e != hipSuccess) return sh_fail(SH_ERR_OOM, "device allocation failed: " + std::string(hipGetErrorString(e)));
     if (p) {
