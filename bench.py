@@ -293,8 +293,10 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         send_buf = torch.empty(B * q.record_bytes, dtype=torch.uint8, device=dev)
     else:
         q = runtime.GpuAggregation(agg, ctx) if agg else runtime.GpuQuery(spec, ctx)
-        if args.workload == "c2cur":
+        if args.workload in ("c2cur", "c3"):
             q.set_compact_flushes()  # a row per event: flush i = row i at its ts (no 16 B/row flush arrays)
+        if args.workload in ("c3all", "plb", "plg"):
+            q.set_device_flushes()  # the per-send flush layout stays in HBM with the rows (nothing crosses PCIe)
     batches = [mk(gen(i)) for i in range(nb)]
     torch.cuda.synchronize()
     phases, timing = {}, False
@@ -355,7 +357,11 @@ def run_secondary(args, dev, rank=0, world=1, dist=None):
         roof = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms_per_step": kern_ms / args.steps,
                 "bytes_per_event": bpe}
-    config = {"workload": desc, "events_per_step_per_gpu": B, "send_size": send}
+    config = {"workload": desc, "events_per_step_per_gpu": B, "send_size": send,
+              # sh_out's flush layout for sh_push_device: host arrays (the ABI default), compact (NULL: a row per
+              # flush at its timestamp) or left in device memory (sh_query_set_device_flushes)
+              "flush_layout": ("compact" if args.workload in ("c2cur", "c3") else
+                               "device" if args.workload in ("c3all", "plb", "plg") else "host") if not sliced else "host"}
     if sliced:
         config.update(parallelism=f"slice ingest x{world}, key re-shard over "
                                   f"{'RCCL' if args.backend == 'nccl' else 'gloo (host)'} all-to-all",

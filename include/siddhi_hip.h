@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 14
+#define SH_ABI_VERSION 15
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -240,7 +240,8 @@ int sh_query_destroy(sh_query* q);
  * OutputRateLimiter for every send in the batch. Host-memory batch (H2D included).          */
 int sh_push(sh_query* q, const sh_batch* batch, const sh_out** out);
 /* Same with device-resident columns (the HBM-resident hot path). flush_offsets/flush_clock of
- * *out are host memory; ts/expired/keys/vals/nulls are device pointers (results stay in HBM). */
+ * *out are host memory (NULL in the compact form, sh_query_set_compact_flushes), for every window
+ * kind; ts/expired/keys/vals/nulls/rep are device pointers (results stay in HBM). */
 int sh_push_device(sh_query* q, const sh_batch* batch, const sh_out** out);
 /* TIMER path: advance the playback clock to `now` without events (Scheduler.onTimeChange). */
 int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
@@ -292,6 +293,10 @@ int sh_query_rep_ts_attr(sh_query* q, const int64_t** values, int64_t* n);
  * checks flush_offsets for NULL. Saves the 16 B per row the flush arrays would cost (host memory even for
  * sh_push_device). Off by default; queries with an output rate limiter always get the full form. */
 int sh_query_set_compact_flushes(sh_query* q, int32_t on);
+/* Device flush layout: when on, sh_push_device leaves flush_offsets / flush_clock in device memory too
+ * (a consumer on the GPU: nothing of the output crosses PCIe). The compact form, when it applies, still
+ * comes first (NULL arrays). Queries with an output rate limiter keep the host layout. Off by default. */
+int sh_query_set_device_flushes(sh_query* q, int32_t on);
 
 /* The text of dictionary ids [first_id, first_id + n) of string column `col`, as UTF-16 code units (what a
  * java.lang.String holds): id first_id + i is units[offsets[i] .. offsets[i + 1]) (offsets has n + 1

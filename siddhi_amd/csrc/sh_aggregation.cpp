@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -316,6 +317,8 @@ static int level_rows(sh_aggregation* a, size_t li, const RowBatch& rb, int64_t 
 // dispatchEvent (:201-258) + cleanBaseIncrementalValueStore (:260-266)
 static int level_dispatch(sh_aggregation* a, size_t li, int64_t start_of_new) {
     Level& L = a->levels[li];
+    static const bool atrace = getenv("SH_ALLOC_TRACE") != nullptr;
+    if (atrace && L.processed) fprintf(stderr, "[sh alloc] dispatch level %zu (%lld rows in)\n", li, (long long)L.n_in);
     hipStream_t s = lvl(a);
     StreamScope _sc(s);
     if (L.processed) {
@@ -879,7 +882,13 @@ static int agg_push(sh_aggregation* a, const sh_batch* b, bool host) {
     SH_TMARK(11);  // (since the previous push's last point: the caller's time between pushes)
     SH_TMARK(0);
     static const bool atrace = getenv("SH_ALLOC_TRACE") != nullptr;
-    if (atrace) fprintf(stderr, "[sh alloc] --- push %lld\n", (long long)a->r_next);
+    if (atrace) {
+        static auto prev = std::chrono::steady_clock::now();
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[sh alloc] --- push %lld (%.1f us since the previous push began)\n", (long long)a->r_next,
+                std::chrono::duration<double, std::micro>(now - prev).count());
+        prev = now;
+    }
     const sh_out* o = nullptr;
     sh_batch dev;
     if (a->intern) {  // (the stream's own columns: the interned slot column is the aggregation's)

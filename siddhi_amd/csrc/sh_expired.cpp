@@ -304,6 +304,7 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         o.vals = q->x_vals.as<uint64_t>();
         o.nulls = q->x_nulls.as<uint8_t>();
         o.rep = q->x_rep.as<int64_t>();
+        RCHK(flush_layout_to_device(q, o));
         *out = &o;
     }
     q->x_closes.clear();

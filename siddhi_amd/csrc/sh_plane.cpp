@@ -333,8 +333,10 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         RCHK(nb.vals.reserve((size_t)V * cap * 8, false));
         RCHK(nb.prev.reserve(cap, false));
         RCHK(nb.x.reserve(cap * 8, false));
-        RCHK(nb.xe.reserve(cap * 8, false));
-        RCHK(nb.xm.reserve(cap * 8, false));
+        if (q->d.window == SH_WIN_EXT_TIME_BATCH) {  // (batch ends / attribute maxima: externalTimeBatch only)
+            RCHK(nb.xe.reserve(cap * 8, false));
+            RCHK(nb.xm.reserve(cap * 8, false));
+        }
         nb.cap = cap;
         to = std::move(nb);
     }
@@ -346,8 +348,10 @@ static int pg_grow(sh_query* q, PgBufs& to, const PgBufs& from, int64_t n, int64
         HIPCHK(hipMemcpyAsync(to.clk.p, from.clk.p, keep * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.prev.p, from.prev.p, keep, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(to.x.p, from.x.p, keep * 8, hipMemcpyDeviceToDevice, st));
-        HIPCHK(hipMemcpyAsync(to.xe.p, from.xe.p, keep * 8, hipMemcpyDeviceToDevice, st));
-        HIPCHK(hipMemcpyAsync(to.xm.p, from.xm.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        if (to.xe.p && from.xe.p) {
+            HIPCHK(hipMemcpyAsync(to.xe.p, from.xe.p, keep * 8, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(to.xm.p, from.xm.p, keep * 8, hipMemcpyDeviceToDevice, st));
+        }
         HIPCHK(hipMemcpy2DAsync(to.vals.p, to.cap * 8, from.vals.p, from.cap * 8, keep * 8, V, hipMemcpyDeviceToDevice, st));
     }
     return SH_OK;
@@ -1672,8 +1676,10 @@ static int pg_save(sh_query* q, std::vector<uint8_t>& out) {
     RCHK(dev(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(dev(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
     RCHK(dev(B.x.p, n * 8));
-    RCHK(dev(B.xe.p, n * 8));
-    RCHK(dev(B.xm.p, n * 8));
+    if (B.xe.p) {
+        RCHK(dev(B.xe.p, n * 8));
+        RCHK(dev(B.xm.p, n * 8));
+    }
     // the timeout's per-partition window state (xt_walk), in slot order
     std::vector<uint32_t> xs;
     for (auto& kv : s->xt_parts) xs.push_back(kv.first);
@@ -1739,8 +1745,10 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     RCHK(up(B.prev.p, n));
     for (int v = 0; v < V; v++) RCHK(up(B.vals.as<u64>() + (size_t)v * B.cap, n * 8));
     RCHK(up(B.x.p, n * 8));
-    RCHK(up(B.xe.p, n * 8));
-    RCHK(up(B.xm.p, n * 8));
+    if (B.xe.p) {
+        RCHK(up(B.xe.p, n * 8));
+        RCHK(up(B.xm.p, n * 8));
+    }
     HIPCHK(hipStreamSynchronize(st));  // the blob may be freed after the call
     s->pg_n = n;
     uint64_t nx = 0;

@@ -295,6 +295,9 @@ struct sh_query {
     // sh_query_set_compact_flushes: an output of one row per flush whose clocks equal the rows' ts leaves
     // flush_offsets / flush_clock NULL (compact_now: this call's output is in that form)
     bool compact_flushes = false, compact_now = false;
+    // sh_query_set_device_flushes: sh_push_device's flush layout stays in device memory (fl_dev)
+    bool device_flushes = false;
+    DevBuf fl_dev;
     std::vector<std::pair<int64_t, int64_t>> xr_starts;
     std::vector<int64_t> xr_rep, xr_vals;
     bool xt_Lvalid = false;
@@ -506,6 +509,7 @@ int shard_create_root(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan& kp, in
                       sh_shard** out, sh_query** owner);
 void shard_attach_aggregation(sh_shard* s, sh_aggregation* a);
 // (sh_aggregation.cpp)
+int flush_layout_to_device(sh_query* q, sh_out& o);  // (sh_query_set_device_flushes)
 int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side = false);  // key room before the root's push
 int agg_after_root(sh_aggregation* a, const sh_out* root_out);  // root flushes -> roll-up levels
 void agg_release_sharded(sh_aggregation* a);                     // called by sh_shard_destroy

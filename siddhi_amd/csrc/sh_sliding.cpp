@@ -607,8 +607,35 @@ int sliding_output(sh_query* q, int64_t n_rows, int64_t n_flushes, bool want_ord
         o.n_keys = nk;
         o.n_vals = na;
         for (int i = 0; i < na; i++) o.val_types[i] = q->vtypes[i];
-        o.flush_offsets = const_cast<int64_t*>(s->fo);
-        o.flush_clock = const_cast<int64_t*>(s->fc);
+        // the flush layout in host memory (the ABI's sh_push_device contract), or compact: one row per
+        // flush at its row's timestamp (sh_query_set_compact_flushes) leaves both arrays NULL
+        bool compact = false;
+        if (q->compact_flushes && q->rate.kind == SH_RATE_NONE && n_flushes > 0 && n_flushes == n_rows) {
+            RCHK(q->h_small_sc.reserve(64));
+            launch_flush_clock_is_ts(st, n_flushes, s->fc, s->out_ts.as<int64_t>(), q->h_small_sc.as<uint32_t>() + 1);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(st));
+            compact = q->h_small_sc.as<uint32_t>()[1] == 1u;
+        }
+        if (compact) {
+            o.flush_offsets = nullptr;
+            o.flush_clock = nullptr;
+        } else if (q->device_flushes && q->rate.kind == SH_RATE_NONE && !q->wide) {
+            o.flush_offsets = const_cast<int64_t*>(s->fo);  // (sh_query_set_device_flushes)
+            o.flush_clock = const_cast<int64_t*>(s->fc);
+        } else {
+            q->dev_flush_offsets.resize((size_t)n_flushes + 1);
+            q->dev_flush_clock.resize((size_t)n_flushes);
+            if (n_flushes > 0) {
+                HIPCHK(hipMemcpyAsync(q->dev_flush_offsets.data(), s->fo, (n_flushes + 1) * 8, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpyAsync(q->dev_flush_clock.data(), s->fc, n_flushes * 8, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipStreamSynchronize(st));
+            } else {
+                q->dev_flush_offsets[0] = 0;
+            }
+            o.flush_offsets = q->dev_flush_offsets.data();
+            o.flush_clock = q->dev_flush_clock.data();
+        }
         o.ts = s->out_ts.as<int64_t>();
         o.expired = s->out_expired.as<uint8_t>();
         o.keys = s->out_keys.as<int64_t>();

@@ -685,6 +685,21 @@ static int closed_finish(sh_query* q, bool host_out) {
     return SH_OK;
 }
 
+// sh_query_set_device_flushes: a batch window's flush layout (built on the host: a few entries per
+// push) goes up to the device, so sh_push_device's whole output is in device memory
+int flush_layout_to_device(sh_query* q, sh_out& o) {
+    if (!q->device_flushes || q->rate.kind != SH_RATE_NONE || q->wide || !o.flush_offsets) return SH_OK;
+    const size_t nf = (size_t)o.n_flushes;
+    hipStream_t s = q->ctx->stream;
+    RCHK(q->fl_dev.reserve((2 * nf + 1) * 8, false));
+    HIPCHK(hipMemcpyAsync(q->fl_dev.p, o.flush_offsets, (nf + 1) * 8, hipMemcpyHostToDevice, s));
+    if (nf) HIPCHK(hipMemcpyAsync(q->fl_dev.as<int64_t>() + nf + 1, o.flush_clock, nf * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    o.flush_offsets = q->fl_dev.as<int64_t>();
+    o.flush_clock = q->fl_dev.as<int64_t>() + nf + 1;
+    return SH_OK;
+}
+
 static void finish_out(sh_query* q, bool host_out, const sh_out** out) {
     const bool compact = q->compact_now;
     q->compact_now = false;
@@ -704,6 +719,7 @@ static void finish_out(sh_query* q, bool host_out, const sh_out** out) {
         for (int i = 0; i < q->ap.n; i++) o.val_types[i] = q->vtypes[i];
         o.flush_offsets = compact ? nullptr : q->dev_flush_offsets.data();
         o.flush_clock = compact ? nullptr : q->dev_flush_clock.data();
+        if (!compact) (void)flush_layout_to_device(q, o);
         o.ts = q->out_ts.as<int64_t>();
         o.expired = q->out_expired.as<uint8_t>();
         o.keys = q->out_keys.as<int64_t>();
@@ -1924,6 +1940,12 @@ static int rep_attr_finish(sh_query* q, const sh_out* o, bool host) {
     return xr_trim(q);
 }
 
+extern "C" int sh_query_set_device_flushes(sh_query* q, int32_t on) {
+    if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_device_flushes: NULL query");
+    q->device_flushes = on != 0;
+    return SH_OK;
+}
+
 extern "C" int sh_query_set_compact_flushes(sh_query* q, int32_t on) {
     if (!q) return sh_fail(SH_ERR_INVALID, "sh_query_set_compact_flushes: NULL query");
     q->compact_flushes = on != 0;
@@ -1977,7 +1999,7 @@ static int push_any_core(sh_query* q, const sh_batch* dev, bool host_out, const 
     if (q->rate.kind != SH_RATE_NONE) {
         const bool sl = q->kind == 1;
         RCHK(sl ? sliding_push(q, dev, false, out) : push_core(q, dev, false, out));
-        return rate_apply(q, *out, sl, host_out, out);
+        return rate_apply(q, *out, false, host_out, out);  // (flush layout in host memory, sliding_output)
     }
     if (q->kind == 1) return sliding_push(q, dev, host_out, out);
     return push_core(q, dev, host_out, out);
@@ -2160,7 +2182,7 @@ static int advance_any(sh_query* q, int64_t now, const sh_out** out) {
     if (q->wide) {  // (device output, then the group-by values decoded and copied to the host)
         if (q->kind == 1) {
             RCHK(sliding_advance(q, now, out, false));
-            if (q->rate.kind != SH_RATE_NONE) RCHK(rate_apply(q, *out, true, false, out));
+            if (q->rate.kind != SH_RATE_NONE) RCHK(rate_apply(q, *out, false, false, out));
         } else {
             RCHK(advance_core(q, now, false, out));
             if (q->rate.kind != SH_RATE_NONE) RCHK(rate_apply(q, *out, false, false, out));
@@ -2170,7 +2192,7 @@ static int advance_any(sh_query* q, int64_t now, const sh_out** out) {
     if (q->kind == 1) {
         if (q->rate.kind == SH_RATE_NONE) return sliding_advance(q, now, out, true);
         RCHK(sliding_advance(q, now, out, false));  // the TIMER chunks' rows reach the limiter too
-        return rate_apply(q, *out, true, true, out);
+        return rate_apply(q, *out, false, true, out);
     }
     if (q->rate.kind != SH_RATE_NONE) {
         RCHK(advance_core(q, now, false, out));

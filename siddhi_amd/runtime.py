@@ -31,19 +31,28 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 14:
+        if L.sh_abi_version() != 15:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
 
 
-def device_out_arrays(out_ptr):
+def device_out_arrays(out_ptr, device_flushes: bool = False):
     """abi.out_arrays for an sh_push_device result: its row arrays are copied out of HBM (hipMemcpy, a
-    synchronising copy) into host arrays; flush offsets / clocks are already on the host."""
+    synchronising copy) into host arrays; flush offsets / clocks are on the host unless the query set the
+    device flush layout (sh_query_set_device_flushes)."""
     o = out_ptr.contents
     n, nk, na = o.n_rows, o.n_keys, o.n_vals
     hip = C.CDLL("libamdhip64.so")
     host = {}
+    if device_flushes and o.flush_offsets and o.n_flushes:
+        fo = np.zeros(o.n_flushes + 1, np.int64)
+        fc = np.zeros(o.n_flushes, np.int64)
+        for a, p in ((fo, o.flush_offsets), (fc, o.flush_clock)):
+            rc = hip.hipMemcpy(C.c_void_p(a.ctypes.data), C.cast(p, C.c_void_p), C.c_size_t(a.nbytes), 2)
+            if rc != 0:
+                raise SiddhiError(abi.SH_ERR_DEVICE, f"hipMemcpy of the flush layout failed ({rc})")
+        host["flush"] = (fo, fc)
     for name, cnt, dt in (("ts", n, np.int64), ("expired", n, np.uint8), ("keys", nk * n, np.int64),
                           ("vals", na * n, np.uint64), ("nulls", na * n, np.uint8), ("rep", n, np.int64)):
         a = np.zeros(max(cnt, 1), dt)
@@ -53,7 +62,7 @@ def device_out_arrays(out_ptr):
             if rc != 0:
                 raise SiddhiError(abi.SH_ERR_DEVICE, f"hipMemcpy of output column {name} failed ({rc})")
         host[name] = a[:cnt]
-    fo, fc = abi.flush_arrays(o, host["ts"])
+    fo, fc = host["flush"] if "flush" in host else abi.flush_arrays(o, host["ts"])
     return {
         "flush_offsets": fo, "flush_clock": fc,
         "val_types": np.array([o.val_types[i] for i in range(na)], np.int32),
@@ -118,6 +127,10 @@ class GpuQuery:
         except Exception:
             self.close()
             raise
+
+    def set_device_flushes(self, on: bool = True):
+        """sh_query_set_device_flushes: sh_push_device leaves the flush layout in device memory too."""
+        _check(lib().sh_query_set_device_flushes(self.h, 1 if on else 0))
 
     def set_compact_flushes(self, on: bool = True):
         """sh_query_set_compact_flushes: one-row flushes at their rows' timestamps leave the flush arrays NULL."""

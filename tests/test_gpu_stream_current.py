@@ -128,3 +128,57 @@ def test_compact_flushes(rt, window, param):
     assert_same(got, ref, label="compact device")
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("window", ["time", "externalTime"])
+def test_sliding_device_output_flush_layout(rt, window):
+    """sh_push_device of a sliding window: the flush layout is host memory (the ABI contract) — read here
+    as host arrays — or, with compact flushes and one row per event at its clock, NULL."""
+    import torch
+    from oracle.oracle import OracleQuery
+    from tests.parity import assert_same
+    ts, cols = stream(12_000, 200, 23)
+    spec = abi.QuerySpec(SCHEMA, window, 2_000, group_by=["k"], aggs=AGGS, key_capacity=256,
+                         ts_attr="ts" if window == "externalTime" else None)
+    dev = torch.device("cuda", 0)
+    for compact, send, devf in ((False, 1, False), (True, 1, False), (True, 7, False), (False, 3, True),
+                                (True, 5, True)):
+        g, o = rt.GpuQuery(spec), OracleQuery(spec)
+        if compact:
+            g.set_compact_flushes()
+        if devf:
+            g.set_device_flushes()
+        t = torch.from_numpy(ts).to(dev)
+        dc = [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols]
+        torch.cuda.synchronize()
+        raw = g.push_device(len(ts), t.data_ptr(), [c.data_ptr() for c in dc], send)
+        assert bool(raw.contents.flush_offsets) == (not compact or send > 1)
+        got = rt.device_out_arrays(raw, device_flushes=devf)
+        ref = abi.out_arrays(o.push_raw(abi.HostBatch(SCHEMA, ts, cols, send)))
+        assert_same(got, ref, label=f"{window} device compact={compact} send={send} device flushes={devf}")
+        g.close()
+        o.close()
+
+
+
+@pytest.mark.parametrize("output", ["current", "all"])
+def test_batch_window_device_flush_layout(rt, output):
+    """sh_query_set_device_flushes on a timeBatch query: the flush layout of sh_push_device comes back in
+    device memory (current output: the windows' flushes; all events: the expired rows' path)."""
+    import torch
+    from oracle.oracle import OracleQuery
+    from tests.parity import assert_same
+    ts, cols = stream(15_000, 100, 29)
+    spec = abi.QuerySpec(SCHEMA, "timeBatch", 700, group_by=["k"], aggs=AGGS, output=output, key_capacity=128)
+    g, o = rt.GpuQuery(spec), OracleQuery(spec)
+    g.set_device_flushes()
+    dev = torch.device("cuda", 0)
+    t = torch.from_numpy(ts).to(dev)
+    dc = [torch.from_numpy(np.ascontiguousarray(c)).to(dev) for c in cols]
+    torch.cuda.synchronize()
+    got = rt.device_out_arrays(g.push_device(len(ts), t.data_ptr(), [c.data_ptr() for c in dc], 2), device_flushes=True)
+    ref = abi.out_arrays(o.push_raw(abi.HostBatch(SCHEMA, ts, cols, 2)))
+    assert ref["flush_clock"].size > 5
+    assert_same(got, ref, label=f"timeBatch device flushes {output}")
+    g.close()
+    o.close()
