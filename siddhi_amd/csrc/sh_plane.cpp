@@ -1717,7 +1717,8 @@ static int pg_load(sh_query* q, const uint8_t* p, size_t len, size_t* used) {
     o += kb;
     get(&n, 8);
     const int V = std::max(1, q->ap.n_vcols);
-    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V + 8 + 8 + 8) > len)
+    const size_t xb = q->d.window == SH_WIN_EXT_TIME_BATCH ? 16 : 0;  // (batch ends, attribute maxima)
+    if (n < 0 || n > (int64_t)(len / 8) || o + (size_t)n * (4 + 4 + 8 + 8 + 8 + 1 + 8 * (size_t)V + 8 + xb) > len)
         return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
     // validated: now replace the state
     if (kb) HIPCHK(hipMemcpyAsync(q->gkt.keys.p, keys, kb, hipMemcpyHostToDevice, st));
