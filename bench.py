@@ -133,8 +133,8 @@ def cpu_baseline_all_cores(args, pool, P):
 
 
 # The PMC summary the roofline's `traffic` is read from: collected on exactly the default C2
-# configuration with the current kernels (scripts/r5_final_c.sh + scripts/pmc_summary.py).
-TRAFFIC_SUMMARY = "profiles/r05_final_c2_pmc.json"
+# configuration with the current kernels (scripts/gpu_run.sh r6final pmc=c2 + scripts/pmc_summary.py).
+TRAFFIC_SUMMARY = "profiles/r06_final_c2_pmc.json"
 TRAFFIC_KERNEL = "shd::k_aggregate_own"
 
 

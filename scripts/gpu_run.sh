@@ -54,7 +54,7 @@ for step in "$@"; do
       done
       F=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" "$P/${n}_FETCH_SIZE")
       W=$(python3 -c "import glob,sys;print(glob.glob(sys.argv[1]+'/**/run_counter_collection.csv',recursive=True)[0])" "$P/${n}_WRITE_SIZE")
-      python3 scripts/pmc_summary.py "$F" "$W" --pushes 3 > "${O}_${n}_pmc.json" || fail "pmc summary $n"
+      python3 scripts/pmc_summary.py "$F" "$W" > "${O}_${n}_pmc.json" || fail "pmc summary $n"
       python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'GB per push %.3f' % (d['per_push_bytes']/1e9))" "${O}_${n}_pmc.json" "$n" ;;
     timeline)
       n=${arg:-c2}

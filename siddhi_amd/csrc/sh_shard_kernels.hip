@@ -40,6 +40,14 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
     SendCursor sc(wp, base);
     load_items_i64(ts, base, wp.N, t, INT64_MIN);
     filter_items(f, cols, base, wp.N, pass);
+    // one 32-bit key column (the usual wire key): the thread's keys in vector loads, codes stored as two
+    // 16-byte words below (a lane's 8 scalar stores at a 32-byte stride otherwise)
+    const bool vkey = kp.n == 1 && kp.div[0] == 0 && (kp.type[0] == SH_T_INT || kp.type[0] == SH_T_STRID);
+    i64 kv[kItems];
+    if (vkey) load_items_raw(cols, kp.col[0], base, wp.N, kv);
+    u32 cd[kItems];
+#pragma unroll
+    for (int i = 0; i < kItems; i++) cd[i] = kNoPos;
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         i64 e = base + i;
@@ -73,12 +81,12 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
                         bounds[k] = b;
                     }
                 }
-                u32 o = owner_of(kp, make_key(kp, cols, e), G);
+                u32 o = owner_of(kp, vkey ? (u64)kv[i] : make_key(kp, cols, e), G);
                 c = ((u32)Wr << kOwnerBits) | o;
                 atomicAdd(&hist[o], 1u);
                 pcb++;
             }
-            code[e] = c;
+            cd[i] = c;
             if (sc2.last(wp, e)) pm = max(pm, t[i]);
             sc2.next();
         }
@@ -116,16 +124,26 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
             }
             u32 c = kNoPos;
             if (pass[i]) {
-                u32 o = owner_of(kp, make_key(kp, cols, e), G);
+                u32 o = owner_of(kp, vkey ? (u64)kv[i] : make_key(kp, cols, e), G);
                 c = ((u32)(W - wp.W_base) << kOwnerBits) | o;
                 atomicAdd(&hist[o], 1u);
             }
-            code[e] = c;
+            cd[i] = c;
             Wprev = W;
             clock_prev = clk;
             if (sc2.last(wp, e)) pm = max(pm, t[i]);
             sc2.next();
         }
+    }
+    static_assert(kItems == 8, "two 16-byte code stores per thread");
+    if (base + kItems <= wp.N) {
+        uint4* q = (uint4*)(code + base);
+        q[0] = make_uint4(cd[0], cd[1], cd[2], cd[3]);
+        q[1] = make_uint4(cd[4], cd[5], cd[6], cd[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; i++)
+            if (base + i < wp.N) code[base + i] = cd[i];
     }
     __syncthreads();
     if (threadIdx.x < G) counts[(i64)threadIdx.x * nblk + blockIdx.x] = hist[threadIdx.x];
