@@ -174,6 +174,12 @@ __global__ __launch_bounds__(kBlock) void k_shard_sl_assign(const i64* __restric
     bool pass[kItems];
     i64 tl = INT64_MIN, pm = INT64_MIN;
     filter_items(f, cols, base, wp.N, pass);
+    const bool vkey = kp.n == 1 && kp.div[0] == 0 && (kp.type[0] == SH_T_INT || kp.type[0] == SH_T_STRID);
+    i64 kv[kItems];
+    if (vkey) load_items_raw(cols, kp.col[0], base, wp.N, kv);
+    u32 cd[kItems];
+#pragma unroll
+    for (int i = 0; i < kItems; i++) cd[i] = kNoPos;
 #pragma unroll
     for (int i = 0; i < kItems; i++) {
         const i64 e = base + i;
@@ -196,11 +202,20 @@ __global__ __launch_bounds__(kBlock) void k_shard_sl_assign(const i64* __restric
             pmx = max(pmx, t);
             clk_out[e] = max(c0, max(cm, ts[send_last_of(wp, e)]));
             pm_out[e] = pmx;
-            c = owner_of(kp, make_key(kp, cols, e), G);
+            c = owner_of(kp, vkey ? (u64)kv[i] : make_key(kp, cols, e), G);
             atomicAdd(&hist[c], 1u);
         }
-        code[e] = c;
+        cd[i] = c;
         if (is_send_last(wp, e)) cm = max(cm, t);
+    }
+    if (base + kItems <= wp.N) {
+        uint4* q = (uint4*)(code + base);
+        q[0] = make_uint4(cd[0], cd[1], cd[2], cd[3]);
+        q[1] = make_uint4(cd[4], cd[5], cd[6], cd[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kItems; i++)
+            if (base + i < wp.N) code[base + i] = cd[i];
     }
     __syncthreads();
     if (threadIdx.x < G) counts[(i64)threadIdx.x * nblk + blockIdx.x] = hist[threadIdx.x];
