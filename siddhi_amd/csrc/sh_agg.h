@@ -35,8 +35,6 @@ void launch_level_extract(hipStream_t s, LevelDev L, BasePlan bp, int has_bucket
 // retrieval (sh_aggregation_find)
 void launch_find_rebucket(hipStream_t s, i64 n, const i64* bucket_in, int per, i64 start, i64 end, i64* bucket_out,
                           u32* idx, i64 tz);
-void launch_agg_intern(hipStream_t s, ColSet cols, FilterProg f, KeyPlan ikp, KeyTable ikt, i64 n, u32* ids);
-void launch_agg_unintern(hipStream_t s, const i64* slots, i64 n, KeyTable ikt, KeyPlan ikp, i64* out);
 // dst[i] = src[idx[i]] ^ flip (flip = the sign bit: signed order as unsigned)
 void launch_find_gather_u64(hipStream_t s, i64 n, const u32* idx, const i64* src, u64* dst, u64 flip = 0);
 void launch_find_starts(hipStream_t s, i64 n, const u32* idx, const i64* bucket, const i64* key, u32* flag);

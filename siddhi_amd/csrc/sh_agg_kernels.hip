@@ -406,34 +406,4 @@ void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v) {
 
 namespace shd {
 
-// ---- interned group keys (two group-by columns, or a 64-bit one beside the bucket) --------------------
-// every passing event's group key -> its slot in the intern table (the root groups by (bucket, slot));
-// events the filter drops get slot 0 (the root never reads them)
-__global__ __launch_bounds__(kBlock) void k_agg_intern(ColSet cols, FilterProg f, KeyPlan ikp, KeyTable ikt, i64 n,
-                                                      u32* ids) {
-    const i64 e = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (e >= n) return;
-    ids[e] = eval_filter(f, cols, e) ? key_slot(ikt, make_key(ikp, cols, e)) : 0u;
-}
-
-void launch_agg_intern(hipStream_t s, ColSet cols, FilterProg f, KeyPlan ikp, KeyTable ikt, i64 n, u32* ids) {
-    if (n > 0)
-        hipLaunchKernelGGL(k_agg_intern, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, cols, f, ikp,
-                           ikt, n, ids);
-}
-
-// slots -> the group-by values as sh_out reports them ([component][n])
-__global__ __launch_bounds__(kBlock) void k_agg_unintern(const i64* __restrict__ slots, i64 n, KeyTable ikt, KeyPlan ikp,
-                                                        i64* out) {
-    const i64 r = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= n) return;
-    unpack_key(ikp, slot_key(ikt, (u32)slots[r]), out + r, n);
-}
-
-void launch_agg_unintern(hipStream_t s, const i64* slots, i64 n, KeyTable ikt, KeyPlan ikp, i64* out) {
-    if (n > 0)
-        hipLaunchKernelGGL(k_agg_unintern, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, slots, n, ikt,
-                           ikp, out);
-}
-
 }  // namespace shd
