@@ -99,7 +99,7 @@ typedef struct {
 #define SH_MAX_AGGS 8
 /* group-by columns: any number up to SH_MAX_GROUP; one column of any type or two 32-bit ones (int, string
  * id, bool, float) key the window directly, any other combination is interned on the device into one
- * 32-bit id per distinct key (needs a spare column slot: n_cols < SH_MAX_COLS; not partitioned or sharded) */
+ * 32-bit id per distinct key (needs a spare column slot: n_cols < SH_MAX_COLS; not sharded) */
 #define SH_MAX_GROUP 8
 
 /* Compiled form of

@@ -194,8 +194,6 @@ int query_reserve_keys(sh_query* q, int64_t extra) {
 // column; GroupByKeyGenerator.java:63-73): the query is built over the stream plus one synthetic
 // dictionary column holding every event's interned key id (sh_wide.h), grouped by that column alone.
 static int wide_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** out) {
-    if (d->partition_col >= 0)
-        return sh_fail(SH_ERR_UNSUPPORTED, "partitioned queries group by one column or two 32-bit ones");
     if (d->n_cols <= 0 || d->n_cols >= SH_MAX_COLS)
         return sh_fail(SH_ERR_UNSUPPORTED, "wide group keys need a spare column slot (fewer than 8 columns)");
     for (int i = 0; i < d->n_group_by; i++)

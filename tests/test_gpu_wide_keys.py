@@ -3,7 +3,7 @@ core/query/selector/GroupByKeyGenerator.java:63-73 joins every group-by attribut
 more columns, or a long / double beside another column. The GPU interns such keys into one 32-bit id per
 distinct key (sh_wide.h: a chain of two-component levels) and keys the window by it; rows get the
 group-by values back. GPU = oracle for batch and sliding windows, every output mode, stream.current,
-a rate limiter, checkpoints and device output. No reference KAT groups by more than two attributes:
+a rate limiter, partition lanes, checkpoints and device output. No reference KAT groups by more than two attributes:
 these cases are GPU = oracle only (the oracle keys by the attributes' values, as the reference does)."""
 import numpy as np
 import pytest
@@ -96,9 +96,29 @@ def test_wide_keys_device_output(rt):
     o.close()
 
 
+@pytest.mark.parametrize("window,param,output,group", [
+    ("lengthBatch", 20, "current", ["a", "s", "l"]), ("lengthBatch", 7, "all", ["s", "d", "a"]),
+    ("time", 300, "all", ["a", "s", "l"]), ("timeBatch", 250, "all", ["s", "l", "d"]),
+    ("externalTimeBatch", 400, "current", ["a", "l", "s"])])
+def test_wide_keys_partitioned(rt, window, param, output, group):
+    """`partition with (a of S)` around a query grouped by a wide key: the key is interned before the
+    partition lanes (which then group by its id) and decoded after them."""
+    ts, cols = stream(20_000, 13)
+    spec = abi.QuerySpec(SCH, window, param, group_by=group, aggs=AGGS, output=output, partition="a", key_capacity=2048,
+                         ts_attr="ts" if window.startswith("external") else None)
+    out = both(rt, spec, split_batches(SCH, ts, cols, [5_000, 12_000], 3), label=f"wide partitioned {window} {output}")
+    assert out["ts"].size > 0
+
+
+@pytest.mark.parametrize("kind", ["first", "last"])
+def test_wide_keys_partitioned_keyed_rate(rt, kind):
+    ts, cols = stream(12_000, 17)
+    spec = abi.QuerySpec(SCH, "lengthBatch", 9, group_by=["s", "l", "d"], aggs=AGGS, partition="a", key_capacity=1024,
+                         rate=(kind, 4))
+    both(rt, spec, split_batches(SCH, ts, cols, [4_000], 2), label=f"wide partitioned rate {kind}")
+
+
 def test_wide_keys_refusals(rt):
-    with pytest.raises(rt.SiddhiError, match="partitioned"):
-        rt.GpuQuery(abi.QuerySpec(SCH, "lengthBatch", 10, group_by=["a", "s", "l"], aggs=AGGS, partition="a"))
     full = abi.Schema.parse("a int, b int, c int, d int, e int, f int, v double, ts long")
     with pytest.raises(rt.SiddhiError, match="spare column"):
         rt.GpuQuery(abi.QuerySpec(full, "lengthBatch", 10, group_by=["a", "b", "c"], aggs=[("sum", "v")]))
