@@ -39,9 +39,9 @@ __global__ __launch_bounds__(kBlock) void k_wide_decode(WideDev w, const i64* __
         const WideLevel& L = w.lv[lvl_stack[sp]];
         const u64 key = slot_key(L.t, id_stack[sp]);
         if (L.kp.n == 1) {
-            const i64 v = L.kp.type[0] == SH_T_LONG || L.kp.type[0] == SH_T_DOUBLE ? (i64)key
-                                                                                    : unpack_part(L.kp, 0, (u32)key);
-            if (L.out[0] >= 0) out[(i64)L.out[0] * n + r] = v;
+            // a one-column key is the value's 8-byte raw form already (ints sign-extended, floats widened
+            // to double bits with NaN canonical): as sh_out reports it
+            if (L.out[0] >= 0) out[(i64)L.out[0] * n + r] = (i64)key;
             continue;
         }
 #pragma unroll

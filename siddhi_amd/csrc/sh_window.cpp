@@ -226,7 +226,17 @@ extern "C" int sh_query_create(sh_ctx* ctx, const sh_query_desc* d, sh_query** o
     if (d && out && d->n_group_by > 0 && d->n_group_by <= SH_MAX_GROUP && d->n_cols > 0 && d->n_cols <= SH_MAX_COLS) {
         bool in_range = true;
         for (int i = 0; i < d->n_group_by; i++) in_range &= d->group_by[i] >= 0 && d->group_by[i] < d->n_cols;
-        if (in_range && WideKeys::needed(d->n_group_by, d->group_by, d->col_types)) return wide_create(ctx, d, out);
+        // partitioned: the lanes key their (partition, group) pairs by one 32-bit group id, so a group key of
+        // two columns or of one 64-bit / floating column other than the partition key is interned too (its
+        // keyed output rate limiters then run on the id)
+        bool lanes_wide = false;
+        if (in_range && d->partition_col >= 0 && d->n_cols < SH_MAX_COLS) {
+            const int t0 = d->col_types[d->group_by[0]];
+            lanes_wide = d->n_group_by >= 2 ||
+                         (d->group_by[0] != d->partition_col && (t0 == SH_T_LONG || t0 == SH_T_DOUBLE || t0 == SH_T_FLOAT));
+        }
+        if (in_range && (lanes_wide || WideKeys::needed(d->n_group_by, d->group_by, d->col_types)))
+            return wide_create(ctx, d, out);
     }
     return query_create(ctx, d, nullptr, out);
 }

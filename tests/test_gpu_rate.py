@@ -198,8 +198,14 @@ def test_partition_lanes_rate(rt, kind, n, window, param, group_by, output):
     assert out["ts"].size > 0
 
 
-def test_partition_lanes_keyed_rate_refused_for_long_group_keys(rt):
-    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 5, group_by=["x"], aggs=[("count", None)], partition="p",
-                         key_capacity=64, rate=("last", 3))
-    with pytest.raises(rt.SiddhiError, match="long / floating / two-column"):
-        rt.GpuQuery(spec)
+@pytest.mark.parametrize("kind,n", [("first", 2), ("last", 3), ("first_time", 90)])
+@pytest.mark.parametrize("group_by", [["x"], ["g", "x"], ["p", "g"]])
+def test_partition_lanes_keyed_rate_interned_group_keys(rt, kind, n, group_by):
+    """keyed limiters of lanes grouped by a long or two-column key: the key is interned to one 32-bit id
+    (sh_wide.h), which the lanes and the limiter key on"""
+    ts, cols = pstream(12_000, 23, 11)
+    cols[3] = (cols[3] % 7) * 1_000_000_007  # (few distinct long values: keys repeat within a partition)
+    spec = abi.QuerySpec(PSCHEMA, "lengthBatch", 5, group_by=group_by, aggs=[("count", None), ("sum", "v")],
+                         partition="p", output="all", key_capacity=256, rate=(kind, n))
+    out = both(rt, spec, split_batches(PSCHEMA, ts, cols, [1, 4_000], 1), label=f"lanes interned {group_by} {kind} {n}")
+    assert out["ts"].size > 0
