@@ -850,6 +850,10 @@ int agg_reserve_root(sh_aggregation* a, const sh_batch* dev, bool side) {
         HIPCHK(hipMemcpyAsync(a->h_minmax, a->minmax.p, 16, hipMemcpyDeviceToHost, s));
         if (side) HIPCHK(sh_wait_stream(s));
         else RCHK(agg_sync(a));
+        // (bucket indices are unsigned and the reference floors hours / days but truncates seconds /
+        // minutes: events before 1970 are not restated)
+        if (a->h_minmax[0] < 0)
+            return sh_fail(SH_ERR_UNSUPPORTED, "aggregate-by timestamps before 1970 (negative) are not on the GPU");
         // the key's bucket component: ts / T truncated (sh_device.h key_part)
         const int64_t lo = a->cal ? cal_idx_h(a->h_minmax[0], a->cal, a->tz_root) : (a->h_minmax[0] + a->tz_root) / a->T_root;
         const int64_t hi = a->cal ? cal_idx_h(a->h_minmax[1], a->cal, a->tz_root) : (a->h_minmax[1] + a->tz_root) / a->T_root;

@@ -491,3 +491,20 @@ def test_three_group_by_columns_rollups_and_retrieval(rt):
     assert_tables_equal(tables(g, spec), ot, "three group-by columns")
     for x in (g, fresh, o):
         x.close()
+
+
+def test_negative_aggregate_by_timestamps_refused(rt):
+    """Events before 1970 (negative `aggregate by` values) fail loudly instead of landing in wrong buckets."""
+    schema = abi.Schema.parse("k int, v double, ts long")
+    spec = abi.AggregationSpec(schema, [("sum", "v")], group_by=["k"], ts="ts", durations=("sec", "hour"), key_capacity=16)
+    g = rt.GpuAggregation(spec)
+    n = 70_000
+    clock = 1_700_000_000_000 + np.arange(n, dtype=np.int64)
+    k = (np.arange(n) % 7).astype(np.int32)
+    v = np.ones(n)
+    g.push(abi.HostBatch(schema, clock, [k, v, clock.copy()], 1))
+    bad = clock.copy()
+    bad[n // 2] = -5_000
+    with pytest.raises(rt.SiddhiError, match="before 1970"):
+        g.push(abi.HostBatch(schema, clock + n, [k, v, bad], 1))
+    g.close()
