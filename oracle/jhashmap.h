@@ -17,7 +17,12 @@
 //    iteration order: a node is linked after its tree parent, the root is moved to the bin's front
 //    (putTreeVal, treeify, moveRootToFront, balanceInsertion / balanceDeletion, removeTreeNode).
 #pragma once
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -473,6 +478,58 @@ class HashMap {
 inline std::u16string decimal(int64_t v) {
     std::string s = std::to_string(v);
     return std::u16string(s.begin(), s.end());
+}
+
+// String.valueOf(x) of a double / float key: Double.toString / Float.toString as the JDK 8 javadoc specifies
+// them — the fewest significant digits (at least one after the point) that tell the value apart from its
+// neighbours of the type, searched here by printing with 1, 2, ... 17 digits until the text reads back as
+// the value (printf rounds to nearest, so the text found is also the nearest of its length); when one digit
+// suffices a two-digit text that reads back and lies nearer wins (Double.MIN_VALUE prints "4.9E-324").
+// Plain notation for 1e-3 <= |x| < 1e7, else "d.dddE<exponent>". (JDK 8's FloatingDecimal prints more digits
+// for a few values, JDK-4511638; those are not restated.)
+inline std::u16string fp_decimal(double x, bool is_float) {
+    if (std::isnan(x)) return u"NaN";
+    if (std::isinf(x)) return x < 0 ? u"-Infinity" : u"Infinity";
+    if (x == 0.0) return std::signbit(x) ? u"-0.0" : u"0.0";
+    auto reads_back = [&](const char* t) {
+        return is_float ? (std::strtof(t, nullptr) == (float)x) : (std::strtod(t, nullptr) == x);
+    };
+    char t[64];
+    int p = 0;
+    for (; p < 17; p++) {
+        std::snprintf(t, sizeof t, "%.*e", p, x);
+        if (reads_back(t)) break;
+    }
+    if (p == 0) {
+        char u[64];
+        std::snprintf(u, sizeof u, "%.1e", x);
+        // (distances in long double: both texts read back as x itself)
+        const long double lx = x;
+        if (reads_back(u) && std::fabs(std::strtold(u, nullptr) - lx) < std::fabs(std::strtold(t, nullptr) - lx))
+            std::memcpy(t, u, sizeof t);
+    }
+    // mantissa digits (trailing zeros dropped) and the decimal exponent
+    std::string m;
+    const char* e = std::strchr(t, 'e');
+    for (const char* c = t; c < e; c++)
+        if (*c >= '0' && *c <= '9') m += *c;
+    while (m.size() > 1 && m.back() == '0') m.pop_back();
+    const int ex = std::atoi(e + 1);
+    std::string r = x < 0 ? "-" : "";
+    const double ax = std::fabs(x);
+    if (ax >= 1e-3 && ax < 1e7) {
+        if (ex < 0) {
+            r += "0." + std::string((size_t)(-ex - 1), '0') + m;
+        } else {
+            std::string ip = m.substr(0, std::min(m.size(), (size_t)ex + 1));
+            ip.resize((size_t)ex + 1, '0');
+            const std::string fp = m.size() > (size_t)ex + 1 ? m.substr((size_t)ex + 1) : "0";
+            r += ip + "." + fp;
+        }
+    } else {
+        r += m.substr(0, 1) + "." + (m.size() > 1 ? m.substr(1) : "0") + "E" + std::to_string(ex);
+    }
+    return std::u16string(r.begin(), r.end());
 }
 
 }  // namespace jhm

@@ -46,8 +46,17 @@ def lib():
         L.or_aggregation_advance_time.argtypes = [C.c_void_p, C.c_int64]
         L.or_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(abi.Out))]
         L.or_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(abi.Out))]
+        L.or_fp_text.argtypes = [C.c_double, C.c_int32, C.c_char_p, C.c_int32]
         _lib = L
     return _lib
+
+
+def fp_text(v: float, is_float: bool = False) -> str:
+    """Double.toString / Float.toString of v as the restatement computes it (a partition flow id)."""
+    buf = C.create_string_buffer(64)
+    if lib().or_fp_text(float(v), int(is_float), buf, 64):
+        raise ValueError("or_fp_text")
+    return buf.value.decode()
 
 
 class OracleQuery:

@@ -537,12 +537,16 @@ struct Query {
                ((d.window == SH_WIN_TIME && d.expired_on) || (d.window == SH_WIN_EXT_TIME_BATCH && ext_timeout > 0));
     }
 
-    // String.valueOf(partition key): Integer/Long.toString, Boolean.toString, the string itself
+    // String.valueOf(partition key): Integer/Long/Float/Double.toString, Boolean.toString, the string itself
     std::u16string flow_id_of(int64_t key) const {
         const int c = d.partition_col;
         if (c < 0) return std::u16string();
         switch (schema.types[c]) {
             case SH_T_INT: case SH_T_LONG: return jhm::decimal(key);
+            case SH_T_FLOAT: case SH_T_DOUBLE: {  // the key is the value's bits widened to double
+                double v; std::memcpy(&v, &key, 8);
+                return jhm::fp_decimal(v, schema.types[c] == SH_T_FLOAT);
+            }
             case SH_T_BOOL: return key ? u"true" : u"false";
             case SH_T_STRID: {
                 auto it = strings.find(c);
@@ -556,7 +560,7 @@ struct Query {
             throw std::runtime_error(schema.types[c] == SH_T_STRID
                                          ? "partition key string id " + std::to_string(key) +
                                                " has no text (sh_query_set_strings): the Scheduler's tie rule needs it"
-                                         : "float / double partition keys of time windows with expired output (or an externalTimeBatch timeout) are not restated");
+                                         : "partition key type without a String.valueOf restatement");
         return jhm::decimal(key);  // order irrelevant to the output: any stable text
     }
 
@@ -1585,6 +1589,15 @@ int or_aggregation_find(void* h, int32_t per, int64_t start, int64_t end, const 
     OutBuf& ob = a->views[SH_DUR_YEARS + 1];
     a->find(per, start, end, ob);
     *out = ob.view(1 + a->d.n_group_by, (int)a->bases.size(), a->vtypes);
+    return SH_OK;
+}
+
+// String.valueOf of a double / float (the partition flow id of such keys) as ASCII, for the tests
+int or_fp_text(double v, int32_t is_float, char* out, int32_t cap) {
+    const std::u16string t = jhm::fp_decimal(v, is_float != 0);
+    if (!out || cap <= (int32_t)t.size()) return SH_ERR_INVALID;
+    for (size_t i = 0; i < t.size(); i++) out[i] = (char)t[i];
+    out[t.size()] = 0;
     return SH_OK;
 }
 

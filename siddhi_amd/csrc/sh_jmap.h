@@ -18,7 +18,10 @@
 //     rebalances, turning a tree whose root lacks a child or left grandchild back into a list (JDK 8).
 // Nodes are slots of a pool addressed by int32 (-1 = null); a node's payload is the partition's slot.
 #pragma once
+#include <charconv>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -30,6 +33,68 @@ inline int32_t java_string_hash(const std::u16string& s) {
     uint32_t h = 0;
     for (char16_t c : s) h = h * 31u + c;
     return (int32_t)h;
+}
+
+// Double.toString / Float.toString (String.valueOf of a double / float partition key) per the published
+// specification (java.lang.Double#toString(double), JDK 8 javadoc): the fewest significant digits that still
+// single the value out among its type's values — at least two when one would do and a two-digit decimal
+// rounding to the value is nearer to it (Double.MIN_VALUE is "4.9E-324") —, plain notation for
+// 10^-3 <= |v| < 10^7 ("100.0", "0.001"), otherwise "d.dddE<n>". JDK 8's FloatingDecimal prints a few values
+// with more digits than this (JDK-4511638, fixed in JDK 19); partition keys hitting those are not restated.
+inline std::u16string java_fp_text(double v, bool f32) {
+    if (v != v) return u"NaN";
+    if (v == 0) return std::signbit(v) ? u"-0.0" : u"0.0";
+    if (std::isinf(v)) return v > 0 ? u"Infinity" : u"-Infinity";
+    char buf[64];
+    auto sci = [&](int prec) -> std::string {  // shortest (prec < 0) or prec + 1 significant digits
+        std::to_chars_result r = prec < 0 ? (f32 ? std::to_chars(buf, buf + 63, (float)v, std::chars_format::scientific)
+                                                 : std::to_chars(buf, buf + 63, v, std::chars_format::scientific))
+                                          : std::to_chars(buf, buf + 63, v, std::chars_format::scientific, prec);
+        return std::string(buf, r.ptr);
+    };
+    auto rounds_to_v = [&](const std::string& s) {
+        return f32 ? std::strtof(s.c_str(), nullptr) == (float)v : std::strtod(s.c_str(), nullptr) == v;
+    };
+    std::string s = sci(-1);
+    std::string two = sci(1);
+    // digits and decimal exponent of "-d.ddde±x"
+    auto split = [](const std::string& t, std::string& dig, int& ex) {
+        const size_t e = t.find('e');
+        dig.clear();
+        for (size_t i = 0; i < e; i++)
+            if (t[i] >= '0' && t[i] <= '9') dig.push_back(t[i]);
+        ex = std::atoi(t.c_str() + e + 1);
+        while (dig.size() > 1 && dig.back() == '0') dig.pop_back();
+    };
+    std::string dig;
+    int ex = 0;
+    split(s, dig, ex);
+    if (dig.size() == 1 && rounds_to_v(two)) {
+        // (both texts read back as v: their distances to it are compared in long double)
+        const long double lv = v;
+        const long double a = std::fabs(std::strtold(s.c_str(), nullptr) - lv),
+                          b = std::fabs(std::strtold(two.c_str(), nullptr) - lv);
+        if (b < a) split(two, dig, ex);
+    }
+    std::string o = v < 0 ? "-" : "";
+    const double m = std::fabs(v);
+    if (m >= 1e-3 && m < 1e7) {
+        if (ex >= 0) {
+            for (int i = 0; i <= ex; i++) o.push_back(i < (int)dig.size() ? dig[i] : '0');
+            o.push_back('.');
+            o += (int)dig.size() > ex + 1 ? dig.substr(ex + 1) : "0";
+        } else {
+            o += "0.";
+            o.append(-ex - 1, '0');
+            o += dig;
+        }
+    } else {
+        o.push_back(dig[0]);
+        o.push_back('.');
+        o += dig.size() > 1 ? dig.substr(1) : "0";
+        o += "E" + std::to_string(ex);
+    }
+    return std::u16string(o.begin(), o.end());
 }
 
 class JavaStringMap {

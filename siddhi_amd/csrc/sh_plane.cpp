@@ -103,8 +103,8 @@ struct Firing {
     uint32_t slot;
 };
 
-// String.valueOf(partition key) (ValuePartitionExecutor.execute :34-40): Integer / Long.toString,
-// Boolean.toString, or the string itself (its UTF-16 text from sh_query_set_strings)
+// String.valueOf(partition key) (ValuePartitionExecutor.execute :34-40): Integer / Long / Float /
+// Double.toString, Boolean.toString, or the string itself (its UTF-16 text from sh_query_set_strings)
 static int flow_id(sh_query* q, int64_t key, std::u16string* out) {
     const int c = q->d.partition_col;
     switch (q->d.col_types[c]) {
@@ -125,7 +125,14 @@ static int flow_id(sh_query* q, int64_t key, std::u16string* out) {
                                                " has no text: the Scheduler's tie rule orders partitions by "
                                                "String.hashCode (call sh_query_set_strings)");
         }
-        default: return sh_fail(SH_ERR_UNSUPPORTED, "float / double partition keys of time windows with expired output");
+        case SH_T_FLOAT:
+        case SH_T_DOUBLE: {  // Float / Double.toString of the value (the key is its bits widened to double)
+            double v;
+            std::memcpy(&v, &key, 8);
+            *out = shj::java_fp_text(v, q->d.col_types[c] == SH_T_FLOAT);
+            return SH_OK;
+        }
+        default: return sh_fail(SH_ERR_UNSUPPORTED, "partition key type without a String.valueOf restatement");
     }
 }
 

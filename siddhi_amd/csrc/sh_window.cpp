@@ -322,11 +322,7 @@ static int query_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         if (!(pt == SH_T_INT || pt == SH_T_LONG || pt == SH_T_STRID || fp_key))
             return sh_fail(SH_ERR_UNSUPPORTED, "partition key must be an int/long/float/double/string column");
         // float / double keys: partitions are String.valueOf(value) (bits, NaN canonical); the Scheduler's
-        // tie order among partitions due together hashes that text (Double.toString), which is not
-        // restated — it decides output only for time windows with expired output
-        if (fp_key && d->window == SH_WIN_TIME && d->expired_on)
-            return sh_fail(SH_ERR_UNSUPPORTED, "float / double partition keys of time windows with expired output "
-                                               "(the Scheduler's tie order hashes Double.toString)");
+        // tie order among partitions due together hashes that text (Double / Float.toString, sh_jmap.h)
     }
 
     sh_query* q = new sh_query();
@@ -1339,11 +1335,6 @@ extern "C" int sh_query_set_ext_timeout(sh_query* q, int64_t ms) {
     if ((q->kind != 0 && !lanes) || (q->d.partition_col >= 0 && !lanes) || q->given || q->internal_keys)
         return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout of a sharded query");
     if (lanes) {
-        const int pt = q->d.col_types[q->d.partition_col];
-        if (pt == SH_T_FLOAT || pt == SH_T_DOUBLE)
-            return sh_fail(SH_ERR_UNSUPPORTED,
-                           "externalTimeBatch timeout with float / double partition keys (the Scheduler's tie order "
-                           "hashes Double.toString)");
         if (q->d.stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "externalTimeBatch timeout with stream.current.event");
         q->xt_timeout = ms;
         return SH_OK;

@@ -360,14 +360,22 @@ def test_partitioned_ext_timeout_checkpoint_and_rate():
     both(sp, pushes, "pext timeout rate")
 
 
-def test_partitioned_ext_timeout_refusals():
-    from siddhi_amd import runtime
-    sch = abi.Schema.parse("p double, k string, v double, et long, st long, ts long")
-    sp = abi.QuerySpec(sch, "externalTimeBatch", 700, ts_attr="et", partition="p", key_capacity=64,
-                       aggs=[("count", None)])
-    sp.timeout = 1000
-    with pytest.raises(runtime.SiddhiError, match="Double.toString"):
-        runtime.GpuQuery(sp)
+@pytest.mark.parametrize("ptype", ["double", "float"])
+def test_partitioned_ext_timeout_float_keys(ptype):
+    """float / double partition keys: the timeout ties between partitions go in the HashMap order of
+    Double.toString / Float.toString of the keys"""
+    sch = abi.Schema.parse(f"p {ptype}, k string, v double, et long, st long, ts long")
+    ts, cols = ptstream(40_000, 19, 0xD4, zero_gaps=True)
+    vals = np.array([0.0, -0.0, np.nan, 1.5, -2.25, 1e300, 5e-324, 1e-5, 12345678.9, 0.1, 1 / 3, 100.0, 1e7, -7.0,
+                     2.5e-3, 6.02e23, 9999999.0, 0.3, 42.0], np.float64)
+    with np.errstate(over="ignore"):
+        p = vals[cols[0]].astype(np.float32 if ptype == "float" else np.float64)
+    cols[0] = p
+    sp = abi.QuerySpec(sch, "externalTimeBatch", 1000, group_by=["p"], ts_attr="et", start_time=0, partition="p",
+                       key_capacity=256, output="all", aggs=[("count", None), ("sum", "v"), ("max", "et")])
+    sp.timeout = 1500
+    got = both(sp, with_advances(split_batches(sch, ts, cols, [9_000, 21_000], 1), ts), f"pext timeout {ptype} keys")
+    assert len(got["ts"]) > 100
 
 
 @pytest.mark.parametrize("rate", [("all", 3), ("last", 2)])

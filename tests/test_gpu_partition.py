@@ -317,8 +317,8 @@ def test_partitioned_time_group_by_other_pair_churn(rt):
 
 
 # ---- float / double partition keys (round 5): String.valueOf(value) names the partitions — the bits,
-# every NaN one partition, 0.0 and -0.0 two — except where the Scheduler's tie order (Double.toString's
-# hash) decides the output (time windows with expired output: refused)
+# every NaN one partition, 0.0 and -0.0 two; where the Scheduler's tie order decides the output (time windows
+# with expired output) it hashes that text, Double.toString / Float.toString
 FSCHEMA = abi.Schema.parse("p double, g int, v double, x long, f float, ts long")
 
 
@@ -352,11 +352,28 @@ def test_float_partition_keys(rt, window, L, group_by, output, stream_current, p
     assert ref["ts"].size > 0
 
 
-def test_float_partition_keys_time_expired_refused(rt):
-    spec = abi.QuerySpec(FSCHEMA, "time", 40, group_by=["p"], aggs=[("count", None)], partition="p", output="all",
-                         key_capacity=64)
-    with pytest.raises(rt.SiddhiError, match="Double.toString"):
-        rt.GpuQuery(spec)
+@pytest.mark.parametrize("pcol,group_by,output", [("p", ["p"], "all"), ("p", [], "expired"), ("f", ["f"], "all"),
+                                                  ("f", [], "all")])
+def test_float_partition_keys_time_expired(rt, pcol, group_by, output):
+    """time windows with expired output: partitions due at one clock fire in the HashMap order of their
+    String.valueOf texts — Double.toString / Float.toString ("-0.0", "NaN", "1.0E300", "Infinity", "4.9E-324")
+    (sh_jmap.h java_fp_text; oracle jhashmap.h fp_decimal)"""
+    ts, cols = fstream(20_000, 40, 73)
+    rng = np.random.default_rng(74)
+    ts = (10_000 + np.cumsum(rng.random(ts.size) < 0.15)).astype(np.int64)  # ~7 events per ms: ties
+    cols[5] = ts.copy()
+    cols[0][::53] = 5e-324
+    cols[0][7::61] = 1e-5
+    cols[0][9::67] = 12345678.9
+    if pcol == "f":
+        with np.errstate(over="ignore", invalid="ignore"):
+            cols[4] = cols[0].astype(np.float32)
+    spec = abi.QuerySpec(FSCHEMA, "time", 40, group_by=group_by, aggs=[("count", None), ("sum", "v")], partition=pcol,
+                         output=output, key_capacity=128)
+    pushes = split_batches(FSCHEMA, ts, cols, [3_000, 11_000], 2)
+    pushes.append(("advance", int(ts[-1]) + 400))
+    ref = both(rt, spec, pushes, f"fp partition time expired {pcol} {group_by} {output}")
+    assert ref["expired"].sum() > 0
 
 
 # ---- partitioned timeBatch(T, true) — stream.current.event, current output (lane 4): every partition
