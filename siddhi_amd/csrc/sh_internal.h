@@ -323,7 +323,7 @@ void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_
 constexpr int kMaxShards = 16;
 void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
                          const i64* blk_pass_pre, const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code,
-                         i64* counts, Bound* bounds, int max_bounds, int* n_bounds);
+                         i64* counts, Bound* bounds, int max_bounds, int* n_bounds, i64* clk_out = nullptr);
 void launch_shard_sl_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp,
                             const i64* blk_tl_pre, const i64* blk_pm_pre, i64 pm0, KeyPlan kp, int G, int nblk,
                             u32* code, i64* counts, i64* clk_out, i64* pm_out);
@@ -442,14 +442,15 @@ void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey,
 
 // ---- stream.current.event batch windows (sh_kernels.hip, driven by sh_window.cpp) ----
 void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
-                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send);
+                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send,
+                    int by_entry = 0);
 void launch_sc_walk(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx,
                     const i64* chunk, const u64* pend_vals, i64 pend_cap, AggPlan ap, i64 n_old, u32* ghead, u64* sval,
                     u32* slast);
 void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32* pre, const u32* slast, const u64* sval,
                     const u32* pend_pos, const i64* pend_ts, const u64* pend_gidx, const i64* chunk, const i64* send,
                     KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys, u64* out_vals, i64* out_rep,
-                    i64* out_chunk, i64* out_send);
+                    i64* out_chunk, i64* out_send, i64* out_order = nullptr);
 void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out);
 int scan_max_i64(void* temp, size_t* bytes, const i64* in, i64* out, i64 n, hipStream_t s);
 void launch_sc_flush_flags(hipStream_t s, i64 T, const i64* och, u32* flag);

@@ -1852,7 +1852,7 @@ void launch_rekey(hipStream_t s, i64 n, u32* pos, KeyTable old_kt, KeyTable new_
 __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64* __restrict__ pcb, int nb,
                                                    const u32* __restrict__ pend_pos, const u64* __restrict__ pend_gidx,
                                                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx,
-                                                   i64* chunk, i64* send) {
+                                                   i64* chunk, i64* send, int by_entry) {
     const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
     if (m >= M) return;
     u32 w = 0;
@@ -1867,7 +1867,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64*
         const i64 e = (i64)pend_gidx[m] - seq0;  // the event's index in the push
         const i64 sd = send_size > 0 ? e / send_size : 0;
         chunk[m] = per_event ? j : sd;
-        send[m] = sd;
+        // (a sharded owner: the chunk is the global send, the clock is looked up per record — by_entry)
+        send[m] = by_entry ? j : sd;
     } else {
         chunk[m] = -1;
         send[m] = -1;
@@ -1935,7 +1936,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
                                                    const i64* __restrict__ pend_ts, const u64* __restrict__ pend_gidx,
                                                    const i64* __restrict__ chunk, const i64* __restrict__ send,
                                                    KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys,
-                                                   u64* out_vals, i64* out_rep, i64* out_chunk, i64* out_send) {
+                                                   u64* out_vals, i64* out_rep, i64* out_chunk, i64* out_send,
+                                                   i64* out_order) {
     const i64 m = n_old + (i64)blockIdx.x * kBlock + threadIdx.x;
     if (m >= M || !ghead[m]) return;
     const i64 o = pre[m - n_old];
@@ -1948,6 +1950,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
     for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
     out_chunk[o] = chunk[m];
     out_send[o] = send[m];
+    if (out_order) out_order[o] = (i64)pend_gidx[m];  // (the group's first event in the chunk: merge order)
 }
 
 // the last timestamp of every send of the push (the send's playback clock before the prefix max)
@@ -1962,10 +1965,11 @@ __global__ __launch_bounds__(kBlock) void k_sc_send_last(const i64* __restrict__
 static inline unsigned sc_grid(i64 n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
-                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send) {
+                    int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send,
+                    int by_entry) {
     if (M <= 0) return;
     hipLaunchKernelGGL(k_sc_keys, dim3(sc_grid(M)), dim3(kBlock), 0, s, M, n_old, pcb, nb, pend_pos, pend_gidx, per_event,
-                       send_size, seq0, skey, idx, chunk, send);
+                       send_size, seq0, skey, idx, chunk, send, by_entry);
 }
 
 void launch_sc_walk(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u32* starts, const u32* idx,
@@ -1979,11 +1983,11 @@ void launch_sc_walk(hipStream_t s, i64 M, const u32* hd, const u32* pos, const u
 void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32* pre, const u32* slast, const u64* sval,
                     const u32* pend_pos, const i64* pend_ts, const u64* pend_gidx, const i64* chunk, const i64* send,
                     KeyTable kt, KeyPlan kp, int na, i64 T, i64* out_ts, i64* out_keys, u64* out_vals, i64* out_rep,
-                    i64* out_chunk, i64* out_send) {
+                    i64* out_chunk, i64* out_send, i64* out_order) {
     if (M <= n_old || T <= 0) return;
     hipLaunchKernelGGL(k_sc_emit, dim3(sc_grid(M - n_old)), dim3(kBlock), 0, s, M, n_old, ghead, pre, slast, sval,
                        pend_pos, pend_ts, pend_gidx, chunk, send, kt, kp, na, T, out_ts, out_keys, out_vals, out_rep,
-                       out_chunk, out_send);
+                       out_chunk, out_send, out_order);
 }
 
 void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out) {

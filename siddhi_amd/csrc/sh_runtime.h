@@ -388,6 +388,8 @@ struct sh_query {
     bool given = false;
     const int* given_wcol = nullptr;
     const shd::u64* given_gidx = nullptr;
+    const int64_t* given_clk = nullptr;  // stream.current.event owners: each record's global send clock,
+    int64_t given_seq0 = 0, given_ss = 1;  // the push's first global index and send size (rows per send)
     int64_t given_W_base = 0, given_W_end = 0;
     std::vector<sh_bound> gbounds;  // this push's global window starts, sorted by gidx
     DevBuf pend_gidx, out_order;  // pend_gidx: stream index of every queued event (all modes)

@@ -60,6 +60,7 @@ struct sh_shard {
     uint64_t seq = 0;     // events of the stream so far (global index of the next event)
     // sliding time(T): PM (max ts over the stream's passing events so far) and sends so far
     bool sliding = false;
+    bool sc = false;      // stream.current.event (batch windows): records carry their send's global clock
     int64_t sl_pm = INT64_MIN;
     int64_t send_base = 0, cur_send_base = 0, cur_send_size = 1, cur_n = 0;
     DevBuf sl_clk, sl_pmv;
@@ -114,7 +115,13 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows carry 2 extra columns: at most 6 stream columns");
     if (d->window == SH_WIN_LENGTH_BATCH && d->partition_col >= 0)
         return sh_fail(SH_ERR_UNSUPPORTED, "partitioned lengthBatch is not on the GPU");
-    if (d->stream_current) return sh_fail(SH_ERR_UNSUPPORTED, "sharded stream.current.event windows are not on the GPU");
+    // stream.current.event: a row per passing event with its key's running values since the batch reset;
+    // the owner needs each record's global send clock (its flush clock), carried as one extra raw column
+    if (d->stream_current && (d->partition_col >= 0 || d->expired_on || d->window == SH_WIN_TIME))
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded stream.current.event windows: unpartitioned batch windows "
+                                           "with current output only");
+    if (d->stream_current && d->n_cols + 1 > SH_MAX_COLS)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded stream.current.event carries 1 extra column: at most 7 stream columns");
     if (d->n_aggs < 1) return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries run aggregations");
     if (d->window == SH_WIN_TIME && (d->expired_on || !d->current_on))
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows emit current events (`insert into`)");
@@ -155,10 +162,14 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         }
     }
     // sliding: the send's global clock and the global PM travel as two extra raw columns
+    // (stream.current.event batch windows: the send's global clock)
     s->sliding = d->window == SH_WIN_TIME;
+    s->sc = d->stream_current != 0;
     if (s->sliding) {
         s->rp.src[s->rp.n++] = d->n_cols;
         s->rp.src[s->rp.n++] = d->n_cols + 1;
+    } else if (s->sc) {
+        s->rp.src[s->rp.n++] = d->n_cols;
     }
     // round-robin owners for one dictionary-id component (dense ids stay dense per owner)
     s->wkp.dense = (s->wkp.n == 1 && s->wkp.type[0] == SH_T_STRID) ? 1 : 0;
@@ -191,7 +202,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
         q->kt.dmul = (uint32_t)world;
         q->kt.dadd = (uint32_t)rank;
     }
-    s->roles.n = d->n_cols + (s->sliding ? 2 : 0);
+    s->roles.n = d->n_cols + (s->sliding ? 2 : s->sc ? 1 : 0);
     for (int c = 0; c < s->roles.n; c++) {
         int t = c < d->n_cols ? d->col_types[c] : SH_T_LONG;
         if (c < d->n_cols) q->load_type[c] = (t == SH_T_FLOAT || t == SH_T_DOUBLE) ? SH_T_DOUBLE : SH_T_LONG;
@@ -497,6 +508,8 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
     s->cur_W_end = W_end;
     s->cur_seq = (int64_t)s->seq;
     s->cur_off = off;
+    s->cur_send_size = std::max<int64_t>(1, b->send_size);  // (stream.current.event rows are per send)
+    s->cur_n = n_total;
     s->my_bounds.clear();
     for (int r = 0; r < G; r++) send_bytes[r] = 0;
     const int64_t N = b->n;
@@ -526,13 +539,20 @@ extern "C" int sh_shard_pack(sh_shard* s, const sh_slice_summary* all, const sh_
         wp.N = N;
         wp.send_size = b->send_size;
         PushInfo* info = s->info.as<PushInfo>();
+        if (s->sc) RCHK(s->sl_clk.reserve(N * 8, false));
         launch_shard_assign(st, b->ts, colset(s, b), s->fp, wp, s->blk_tl.as<int64_t>(), s->blk_pass.as<int64_t>(),
                             info, s->wkp, G, nblk,
                             s->code.as<u32>(), s->counts.as<int64_t>(), s->bounds.as<Bound>(), max_bounds,
-                            &info->n_bounds);
+                            &info->n_bounds, s->sc ? s->sl_clk.as<int64_t>() : nullptr);
         HIPCHK(hipMemsetAsync(s->counts.as<int64_t>() + ncnt, 0, 8, st));
         launch_scan_sum_large(st, s->counts.as<int64_t>(), ncnt + 1, s->tmp.as<int64_t>());
-        launch_shard_pack(st, colset(s, b), b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk,
+        ColSet pcs = colset(s, b);
+        if (s->sc) {
+            pcs.ptr[pcs.n] = s->sl_clk.p;
+            pcs.type[pcs.n] = SH_T_LONG;
+            pcs.n += 1;
+        }
+        launch_shard_pack(st, pcs, b->ts, s->code.as<u32>(), s->wkp, s->rp, G, N, nblk,
                           s->counts.as<int64_t>(), (unsigned char*)send_buf, RW, s->key32, s->cur_narrow,
                           s->cur_tsbase);
         launch_part_off(st, s->counts.as<int64_t>(), nblk, G, s->part_off.as<int64_t>());
@@ -698,11 +718,11 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     sh_batch b{};
     b.n = M;
     b.send_size = 1;
-    for (int c = 0; c < s->d.n_cols; c++) {
+    for (int c = 0; c < s->roles.n; c++) {
         if (s->roles.role[c] < 0) continue;
         RCHK(s->u_cols[c].reserve(M * 8, false));
         cp.p[c] = s->u_cols[c].as<u64>();
-        b.cols[c] = cp.p[c];
+        if (c < s->d.n_cols) b.cols[c] = cp.p[c];
     }
     // the global window starts, sorted by stream index, for the per-record window lookup
     const int nb = (int)q->gbounds.size();
@@ -735,10 +755,14 @@ extern "C" int sh_shard_consume(sh_shard* s, const void* recv_buf, const int64_t
     b.ts = s->u_ts.as<int64_t>();
     q->given_wcol = s->u_wcol.as<int>();
     q->given_gidx = s->u_gidx.as<u64>();
+    q->given_clk = s->sc ? s->u_cols[s->d.n_cols].as<int64_t>() : nullptr;
+    q->given_seq0 = s->cur_seq;
+    q->given_ss = s->cur_send_size;
     int rc = s->agg ? agg_reserve_root(s->agg, &b) : SH_OK;
     if (!rc) rc = query_push_given(q, &b, host_out != 0, out);
     q->given_wcol = nullptr;
     q->given_gidx = nullptr;
+    q->given_clk = nullptr;
     if (rc) return rc;
     sync_owner(s);
     if (s->agg) RCHK(agg_after_root(s->agg, *out));

@@ -4,7 +4,8 @@
 // owns its group key. The all-to-all itself is done by the caller over RCCL/xGMI.
 //
 //   k_shard_assign  window of every event (clock carried in from the slices before), owner =
-//                   mix64(key) % G, per-(owner, tile) histogram, window starts of the slice
+//                   mix64(key) % G, per-(owner, tile) histogram, window starts of the slice (and, for
+//                   stream.current.event, every passing event's send clock: its row's flush clock)
 //   k_shard_pack    stable multisplit of the passing events into per-owner runs of AoS records
 //                   {key, slice position, ts, values...} (event order kept inside every run)
 //   k_shard_unpack  received records -> SoA columns of the owner's pipeline (given-window mode)
@@ -30,7 +31,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
                                                         WinParams wp, const i64* __restrict__ blk_tl_pre,
                                                         const i64* __restrict__ blk_pass_pre, KeyPlan kp,
                                                         int G, int nblk, u32* code, i64* counts, Bound* bounds,
-                                                        int max_bounds, int* n_bounds) {
+                                                        int max_bounds, int* n_bounds, i64* clk_out) {
     __shared__ u32 hist[kMaxShards];
     if (threadIdx.x < kMaxShards) hist[threadIdx.x] = 0;
     const i64 base = (i64)blockIdx.x * kTile + (i64)threadIdx.x * kItems;
@@ -69,6 +70,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
             i64 e = base + i;
             if (e >= wp.N) break;
             u32 c = kNoPos;
+            if (pass[i] && clk_out) {  // (stream.current.event: the send's global clock, the row's flush clock)
+                const i64 tsl = sc2.s == 1 ? t[i] : ts[sc2.last_of(wp, e)];
+                clk_out[e] = max(c0, max(pm, tsl));
+            }
             if (pass[i]) {
                 const i64 Wr = pcb / wp.L;
                 if ((pcb + 1) % wp.L == 0) {
@@ -113,6 +118,7 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
             if (e >= wp.N) break;
             i64 tsl = sc2.s == 1 ? t[i] : ts[sc2.last_of(wp, e)];
             i64 clk = max(c0, max(pm, tsl));
+            if (clk_out && pass[i]) clk_out[e] = clk;
             i64 W = max(wp.W_open, wc.at(wp, E0, e0v, 0, clk));
             if (W > Wprev) {
                 int k = atomicAdd(n_bounds, 1);
@@ -151,10 +157,10 @@ __global__ __launch_bounds__(kBlock) void k_shard_assign(const i64* __restrict__
 
 void launch_shard_assign(hipStream_t s, const i64* ts, ColSet cols, FilterProg f, WinParams wp, const i64* blk_tl_pre,
                          const i64* blk_pass_pre, const PushInfo* info, KeyPlan kp, int G, int nblk, u32* code,
-                         i64* counts, Bound* bounds, int max_bounds, int* n_bounds) {
+                         i64* counts, Bound* bounds, int max_bounds, int* n_bounds, i64* clk_out) {
     (void)info;
     hipLaunchKernelGGL(k_shard_assign, dim3(nblk), dim3(kBlock), 0, s, ts, cols, f, wp, blk_tl_pre, blk_pass_pre, kp,
-                       G, nblk, code, counts, bounds, max_bounds, n_bounds);
+                       G, nblk, code, counts, bounds, max_bounds, n_bounds, clk_out);
 }
 
 // Sliding time(T) (TimeWindowProcessor :132-169): the owner needs, per passing event, the global

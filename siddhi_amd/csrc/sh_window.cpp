@@ -848,9 +848,11 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     RCHK(q->sc_sval.reserve((size_t)std::max(na, 1) * M * 8, false));
     RCHK(q->sc_tmp.reserve((size_t)((M + 1 + kTile - 1) / kTile + 16) * 8, false));
     RCHK(q->sc_sl.reserve((size_t)n_sends * 8, false));
+    // (a sharded owner: records are one send each for their clocks, chunks are the global sends)
+    const bool gv = q->given_clk != nullptr;
     launch_sc_keys(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(),
-                   per_event ? 1 : 0, ss, seq0, q->sc_skey.as<u64>(), q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(),
-                   q->sc_send.as<int64_t>());
+                   per_event ? 1 : 0, gv ? q->given_ss : ss, gv ? q->given_seq0 : seq0, q->sc_skey.as<u64>(),
+                   q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), gv ? 1 : 0);
     size_t tb = 0;
     if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, M, s))
         return sh_fail(SH_ERR_DEVICE, "stream.current: sort sizing");
@@ -867,8 +869,15 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                    q->sc_sval.as<u64>(), q->sc_slast.as<u32>());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     const int64_t nn = M - n_old;
-    // the sends' playback clocks: TimestampGeneratorImpl only moves forward (prefix max of send-last ts)
-    launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
+    // the sends' playback clocks: TimestampGeneratorImpl only moves forward (prefix max of send-last ts);
+    // a sharded owner's records (one send each) carry their global send's clock instead
+    if (q->given_clk) {
+        if (ss != 1) return sh_fail(SH_ERR_INVALID, "sharded stream.current: records are one send each");
+        cv0 = false;  // (the records' clocks are whole; the owner's clock is already the push's end clock)
+        HIPCHK(hipMemcpyAsync(q->sc_sl.p, q->given_clk, (size_t)N * 8, hipMemcpyDeviceToDevice, s));
+    } else {
+        launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
+    }
     HIPCHK(hipGetLastError());
     const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
     const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
@@ -954,6 +963,7 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     RCHK(q->out_rep.reserve(TC * 8, false));
     RCHK(q->sc_ochunk.reserve(TC * 8, false));
     RCHK(q->sc_osend.reserve(TC * 8, false));
+    if (q->given) RCHK(q->out_order.reserve(TC * 8, false));
     HIPCHK(hipMemsetAsync(q->out_nulls.p, 0, q->out_nulls.cap, s));
     HIPCHK(hipMemsetAsync(q->out_expired.p, 0, q->out_expired.cap, s));
     q->zeroed_nulls = q->out_nulls.p;
@@ -980,7 +990,8 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                        q->sc_sval.as<u64>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(),
                        q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T,
                        q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
-                       q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>());
+                       q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>(),
+                       q->given ? q->out_order.as<int64_t>() : nullptr);
     }
     HIPCHK(hipGetLastError());
     PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
@@ -1063,6 +1074,12 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
             HIPCHK(hipMemcpyAsync(o.rep.data(), q->out_rep.p, T * 8, hipMemcpyDeviceToHost, s));
             if (nk) HIPCHK(hipMemcpyAsync(o.keys.data(), q->out_keys.p, (size_t)nk * T * 8, hipMemcpyDeviceToHost, s));
             if (na) HIPCHK(hipMemcpyAsync(o.vals.data(), q->out_vals.p, (size_t)na * T * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        // sharded owner: a row's merge order is the global stream index of its group's first event in the chunk
+        if (q->given) {
+            q->order_host.resize(T);
+            if (T) HIPCHK(hipMemcpyAsync(q->order_host.data(), q->out_order.p, T * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
         }
     } else {
@@ -1821,7 +1838,8 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
             RCHK(grow_pending(q, M, n_old));
             launch_compact_pending(s, b->ts, cs, pos_src(q, b), q->ap, 0, N, 0, n_old,
                                    q->blk_pass.as<int64_t>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(),
-                                   q->pend_vals.as<u64>(), q->pend_cap, nullptr, q->pend_gidx.as<u64>(), q->seq);
+                                   q->pend_vals.as<u64>(), q->pend_cap, q->given ? q->given_gidx : nullptr,
+                                   q->pend_gidx.as<u64>(), q->seq);
             HIPCHK(hipGetLastError());
             // (a window may close with no passing event in the push: its expired rows still go out)
             if (M > n_old || (q->d.expired_on && !bounds.empty() && n_old > 0))
@@ -2314,7 +2332,9 @@ int query_close_given(sh_query* q, bool host_out_req, const sh_out** out) {
     q->ms_ready = false;
     q->tail.active = false;
     if (q->given_W_end > q->W_open) {
-        if (q->n_pend > 0) {
+        if (q->n_pend > 0 && q->d.stream_current) {
+            q->n_pend = 0;  // (RESET: the events went out as they arrived; current output only)
+        } else if (q->n_pend > 0) {
             std::vector<Segment> segs{Segment{0, q->n_pend}};
             std::vector<int64_t> clocks{given_flush_clock(q, q->W_open)}, windows{q->W_open};
             RCHK(run_closed(q, segs, clocks, windows, nullptr, host_out));

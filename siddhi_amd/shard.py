@@ -246,6 +246,17 @@ def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None,
     return res
 
 
+def merge_sends(spec, last_sends: Tuple[int, int]) -> Optional[Tuple[int, int]]:
+    """The `sends` argument of merge_owner_outputs for a query: sliding windows and timeBatch(T, true) flush
+    once per send (the send's chunk), lengthBatch(L, true) once per passing event (LengthBatchWindowProcessor
+    sends each event's chunk on its own, :160-182); other batch windows merge by window (None)."""
+    if spec.window == "time" or (spec.stream_current and spec.window == "timeBatch"):
+        return last_sends
+    if spec.stream_current and spec.window == "lengthBatch":
+        return (last_sends[0], 1)
+    return None
+
+
 def _merge_by_send(parts: List[dict], sends: Tuple[int, int]) -> dict:
     """One flush per send: the global row order is the order of the rows' first events (rows of an
     earlier send come first), and a flush ends where the send number changes."""

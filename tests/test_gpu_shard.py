@@ -26,7 +26,7 @@ def spec(keys, filt=None, start=None, aggs=None, group_by=("k",), schema=SCHEMA)
 def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
     """pushes: list of (ts, cols) numpy global pushes; each is cut into `world` send-aligned slices."""
     import torch
-    from siddhi_amd.shard import LocalShards, merge_owner_outputs
+    from siddhi_amd.shard import LocalShards, merge_owner_outputs, merge_sends
     dev = torch.device("cuda", 0)
     ls = LocalShards(sp, world)
     parts = []
@@ -41,7 +41,7 @@ def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
             slices.append((torch.from_numpy(np.ascontiguousarray(ts[a:b])).to(dev),
                            [torch.from_numpy(np.ascontiguousarray(c[a:b])).to(dev) for c in cols]))
         outs = ls.push(slices, send_size, dev)
-        parts.append(merge_owner_outputs(outs, ls.last_bounds, ls.last_sends if sp.window == "time" else None))
+        parts.append(merge_owner_outputs(outs, ls.last_bounds, merge_sends(sp, ls.last_sends)))
     if advance is not None:
         parts.append(merge_owner_outputs(ls.advance_time(advance)))
     ls.close()
@@ -276,3 +276,39 @@ def test_sharded_lengthbatch_expired_and_all_events(output):
     ref = run_oracle(sp, pushes, 10)
     assert ref["expired"].sum() > 100
     assert_same(got, ref, label=f"sharded lengthBatch {output}")
+
+
+# ---- stream.current.event over G GPUs: a row per passing event with its key's running values since the
+# batch reset (TimeBatchWindowProcessor :262-340 RESET mode, LengthBatchWindowProcessor
+# .processStreamCurrentEvents :245-274); the owner folds its keys' records in global order and stamps each
+# row with its send's global clock (carried in the record), rows merge by global stream index ----------
+@pytest.mark.parametrize("window,param,world,send_size", [("timeBatch", 1000, 2, 1), ("timeBatch", 700, 3, 50),
+                                                          ("lengthBatch", 97, 4, 1), ("lengthBatch", 500, 3, 20),
+                                                          ("timeBatch", 300, 8, 1)])
+def test_sharded_stream_current(window, param, world, send_size):
+    sp = abi.QuerySpec(SCHEMA, window, param, group_by=["k"], stream_current=True, key_capacity=3_000,
+                       aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")], filter=(">", "v", 20.0))
+    pushes = stream_pushes(150_000, [60_000, 1, 89_999], 0xC7, 3_000, 40)
+    # an idle stretch of several periods: batches reset with no event
+    pushes[2] = (pushes[2][0] + (np.arange(len(pushes[2][0])) >= 40_000) * 3_500, pushes[2][1])
+    pushes[2][1][2] = pushes[2][0].copy()
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.07 * (g + 1) for g in range(world - 1)]]
+    adv = int(pushes[-1][0][-1]) + 5_000
+    got = run_sharded(sp, world, pushes, send_size, fr, advance=adv)
+    ref = run_oracle(sp, pushes, send_size, advance=adv)
+    assert ref["ts"].size > 100_000
+    assert_same(got, ref, label=f"sharded stream.current {window} x{world} send {send_size}")
+
+
+def test_sharded_stream_current_two_keys():
+    sch = abi.Schema.parse("a int, b int, x long, v double, ts long")
+    ts, cols = synth.keyed_stream(0, 80_000, 0xA9, 5, 20)
+    rng = np.random.default_rng(9)
+    full = [cols[0], rng.integers(0, 3, len(ts)).astype(np.int32), rng.integers(-1000, 1000, len(ts)).astype(np.int64),
+            cols[1], cols[2]]
+    sp = abi.QuerySpec(sch, "timeBatch", 500, group_by=["a", "b"], stream_current=True, key_capacity=64,
+                       aggs=[("sum", "x"), ("max", "x"), ("sum", "v"), ("count", None)])
+    pushes = [(ts[:30_000], [c[:30_000] for c in full]), (ts[30_000:], [c[30_000:] for c in full])]
+    got = run_sharded(sp, 5, pushes, 3, [[0.2, 0.4, 0.6, 0.8]], advance=int(ts[-1]) + 3000)
+    ref = run_oracle(sp, pushes, 3, advance=int(ts[-1]) + 3000)
+    assert_same(got, ref, label="sharded stream.current two keys")

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 def run_sharded_restored(sp, world, pushes, send_size, cut_at, advance=None):
     import torch
-    from siddhi_amd.shard import LocalShards, merge_owner_outputs
+    from siddhi_amd.shard import LocalShards, merge_owner_outputs, merge_sends
     dev = torch.device("cuda", 0)
     ls = LocalShards(sp, world)
     parts = []
@@ -30,7 +30,7 @@ def run_sharded_restored(sp, world, pushes, send_size, cut_at, advance=None):
                    [torch.from_numpy(np.ascontiguousarray(c[edges[g]:edges[g + 1]])).to(dev) for c in cols])
                   for g in range(world)]
         outs = ls.push(slices, send_size, dev)
-        parts.append(merge_owner_outputs(outs, ls.last_bounds, ls.last_sends if sp.window == "time" else None))
+        parts.append(merge_owner_outputs(outs, ls.last_bounds, merge_sends(sp, ls.last_sends)))
     if advance is not None:
         parts.append(merge_owner_outputs(ls.advance_time(advance)))
     ls.close()
@@ -53,6 +53,17 @@ def test_sharded_lengthbatch_checkpoint():
     pushes = stream_pushes(120_000, [50_000, 3_333, 66_667], 7, 2_000, 50)
     got = run_sharded_restored(sp, 2, pushes, 3, 1)
     assert_same(got, run_oracle(sp, pushes, 3), label="lengthBatch x2")
+
+
+@pytest.mark.parametrize("window,param,send_size", [("timeBatch", 600, 4), ("lengthBatch", 333, 1)])
+def test_sharded_stream_current_checkpoint(window, param, send_size):
+    """stream.current.event owners keep their open batch's entries (the running values) across the cut"""
+    sp = abi.QuerySpec(SCHEMA, window, param, group_by=["k"], aggs=[("sum", "v"), ("count", None), ("min", "v")],
+                       stream_current=True, key_capacity=2_000)
+    pushes = stream_pushes(90_000, [30_001, 29_999, 30_000], 13, 2_000, 40)
+    adv = int(pushes[-1][0][-1]) + 3_000
+    got = run_sharded_restored(sp, 3, pushes, send_size, 1, advance=adv)
+    assert_same(got, run_oracle(sp, pushes, send_size, advance=adv), label=f"stream.current {window} x3")
 
 
 def test_sharded_sliding_checkpoint():

@@ -50,3 +50,17 @@ def test_sliding_owner_outputs_merge_per_send():
     assert m["vals"][0].tolist() == [4, 1, 2, 5, 6, 3, 7]
     e = merge_owner_outputs([owner_out([], [], [0], []), owner_out([], [], [0], [])], sends=(0, 1))
     assert e["flush_offsets"].tolist() == [0] and e["keys"].shape == (1, 0)
+
+
+def test_merge_sends_per_query_kind():
+    """how owners' flushes merge: by window for batch windows; by send for sliding windows and
+    timeBatch(T, true); by passing event for lengthBatch(L, true)"""
+    from siddhi_amd import abi
+    from siddhi_amd.shard import merge_sends
+    sch = abi.Schema.parse("k int, v double, ts long")
+    q = lambda w, sc=False: abi.QuerySpec(sch, w, 100, group_by=["k"], aggs=[("count", None)], stream_current=sc)
+    assert merge_sends(q("timeBatch"), (7, 4)) is None
+    assert merge_sends(q("lengthBatch"), (7, 4)) is None
+    assert merge_sends(q("time"), (7, 4)) == (7, 4)
+    assert merge_sends(q("timeBatch", True), (7, 4)) == (7, 4)
+    assert merge_sends(q("lengthBatch", True), (7, 4)) == (7, 1)
