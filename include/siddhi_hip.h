@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SH_ABI_VERSION 15
+#define SH_ABI_VERSION 16
 
 /* ---- return codes ---------------------------------------------------------------------- */
 #define SH_OK 0
@@ -260,6 +260,12 @@ int sh_advance_time(sh_query* q, int64_t now, const sh_out** out);
 #define SH_RATE_LAST 3
 #define SH_RATE_FIRST_TIME 4
 int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n);
+/* The limiter of a sharded query (ABI 16; OutputRateLimiter.process sits after the selector, so it sees
+ * the merged single-stream output): `q` is a query created from the same descriptor with its rate set
+ * and never pushed; the merging rank passes every merged call output (host arrays, flush by flush, in
+ * stream order — pushes and advance_time calls alike) and gets the limited output back (host arrays).
+ * The limiter's kernels run on q's device. */
+int sh_rate_apply_merged(sh_query* q, const sh_out* merged, const sh_out** out);
 
 /* externalTimeBatch's fourth parameter, the scheduler timeout in milliseconds
  * (ExternalTimeBatchWindowProcessor.java:196-207, `externalTimeBatch(ts, 1 sec, 0, 6 sec)`): when the

@@ -408,6 +408,7 @@ def setup_lib_prototypes(lib, prefix: str):
     lib.sh_aggregation_table.argtypes = [C.c_void_p, C.c_int32, P(P(Out))]
     lib.sh_aggregation_find.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, P(P(Out))]
     lib.sh_query_set_output_rate.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+    lib.sh_rate_apply_merged.argtypes = [C.c_void_p, P(Out), P(P(Out))]
     lib.sh_query_set_ext_timeout.argtypes = [C.c_void_p, C.c_int64]
     lib.sh_query_set_ext_replace_ts.argtypes = [C.c_void_p, C.c_int32]
     lib.sh_query_set_compact_flushes.argtypes = [C.c_void_p, C.c_int32]
@@ -459,7 +460,7 @@ ABI_SYMBOLS = [
     "sh_shard_consume", "sh_shard_advance_time", "sh_shard_stats", "sh_query_snapshot", "sh_query_restore",
     "sh_aggregation_shard_create", "sh_aggregation_stats", "sh_stage", "sh_push_staged", "sh_ingest_stats",
     "sh_aggregation_find", "sh_aggregation_snapshot", "sh_aggregation_restore", "sh_query_set_output_rate", "sh_query_set_ext_timeout", "sh_query_set_ext_replace_ts", "sh_query_set_compact_flushes", "sh_query_set_device_flushes", "sh_query_rep_ts_attr", "sh_aggregation_timing", "sh_shard_flush_windows",
-    "sh_shard_snapshot", "sh_shard_restore", "sh_query_set_strings",
+    "sh_shard_snapshot", "sh_shard_restore", "sh_query_set_strings", "sh_rate_apply_merged",
 ]
 
 

@@ -44,7 +44,8 @@ extern "C" int sh_query_set_output_rate(sh_query* q, int32_t kind, int64_t n) {
     if (q->seq > 0 || q->clock_valid) return sh_fail(SH_ERR_INVALID, "output rate must be set before the first push");
     // a partitioned query holds one limiter per partition instance (PartitionRuntime clones the query);
     // the GPU's partitioned timeBatch flushes only partition p0 (R12), so its one limiter is p0's
-    if (kind != SH_RATE_NONE && q->given) return sh_fail(SH_ERR_UNSUPPORTED, "output rate limiting of a sharded query");
+    if (kind != SH_RATE_NONE && q->given)
+        return sh_fail(SH_ERR_UNSUPPORTED, "a sharded query's limiter runs over the merged output (sh_rate_apply_merged)");
     if (kind != SH_RATE_NONE && q->kp.n > 2) return sh_fail(SH_ERR_UNSUPPORTED, "output rate with more than 2 group-by keys");
     // the partition lanes (sh_plane.cpp): one limiter per partition instance. Grouped by the partition
     // key, a partition's limiter sees one key, so the keyed First variants equal the global keyed ones
@@ -617,4 +618,48 @@ static int rate_part(sh_query* q, const sh_out* in, const i64* foff, int nf, boo
     }
     r.seq += n;
     return rate_finish(q, o, T, nk, na, host_out, out);
+}
+
+// A sharded query's limiter (OutputRateLimiter.process after the selector: it sees the merged
+// single-stream output). The merged rows come from the host; they go to the device once and run through
+// the same limiter kernels as an unsharded query's output.
+extern "C" int sh_rate_apply_merged(sh_query* q, const sh_out* in, const sh_out** out) {
+    StreamScope _ss(q && q->ctx ? q->ctx->stream : nullptr);
+    if (!q || !in || !out) return sh_fail(SH_ERR_INVALID, "sh_rate_apply_merged: NULL argument");
+    if (q->rate.kind == SH_RATE_NONE) return sh_fail(SH_ERR_INVALID, "sh_rate_apply_merged: the query has no output rate");
+    if (q->seq > 0 || q->clock_valid)
+        return sh_fail(SH_ERR_INVALID, "sh_rate_apply_merged: the limiter's query must never be pushed");
+    if (q->wide || q->kind == 1 && q->d.partition_col >= 0)
+        return sh_fail(SH_ERR_UNSUPPORTED, "sh_rate_apply_merged: a query the sharded ingest does not run");
+    if (in->n_keys != q->kp.n || in->n_vals != q->ap.n || in->n_rows < 0 || in->n_flushes < 0 ||
+        (in->n_rows > 0 && (!in->ts || !in->expired || (in->n_keys && !in->keys) || (in->n_vals && (!in->vals || !in->nulls)))))
+        return sh_fail(SH_ERR_INVALID, "sh_rate_apply_merged: rows do not match the query's keys / aggregators");
+    if (in->n_rows > 0 && (!in->flush_offsets || in->flush_offsets[in->n_flushes] != in->n_rows))
+        return sh_fail(SH_ERR_INVALID, "sh_rate_apply_merged: the merged output needs its flush offsets");
+    auto& r = q->rate;
+    hipStream_t s = q->ctx->stream;
+    const int nk = (int)in->n_keys, na = (int)in->n_vals;
+    const int64_t n = in->n_rows;
+    RateRows d{};
+    RCHK(reserve_set(r.m_ts, r.m_exp, r.m_rep, r.m_keys, r.m_vals, r.m_nulls, n, nk, na, &d));
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(d.ts, in->ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(d.expired, in->expired, (size_t)n, hipMemcpyHostToDevice, s));
+        if (in->rep) HIPCHK(hipMemcpyAsync(d.rep, in->rep, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        else HIPCHK(hipMemsetAsync(d.rep, 0xFF, (size_t)n * 8, s));
+        if (nk) HIPCHK(hipMemcpyAsync(d.keys, in->keys, (size_t)nk * n * 8, hipMemcpyHostToDevice, s));
+        if (na) {
+            HIPCHK(hipMemcpyAsync(d.vals, in->vals, (size_t)na * n * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(d.nulls, in->nulls, (size_t)na * n, hipMemcpyHostToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));  // (the caller's host arrays may go once this returns)
+    }
+    sh_out dv = *in;
+    dv.ts = d.ts;
+    dv.expired = d.expired;
+    dv.rep = d.rep;
+    dv.keys = d.keys;
+    dv.vals = (const uint64_t*)d.vals;
+    dv.nulls = d.nulls;
+    return rate_apply(q, &dv, false, true, out);
 }

@@ -424,6 +424,7 @@ struct sh_query {
         DevBuf c_ts, c_exp, c_rep, c_keys, c_vals, c_nulls;          // carried rows (stride nc)
         DevBuf s_ts, s_exp, s_rep, s_keys, s_vals, s_nulls;          // source rows of a call
         DevBuf o_ts, o_exp, o_rep, o_keys, o_vals, o_nulls, o_flush;  // kept rows
+        DevBuf m_ts, m_exp, m_rep, m_keys, m_vals, m_nulls;          // merged sharded rows (sh_rate_apply_merged)
         DevBuf foff, flag, pre, src, eflush, tmp, skey, skey2, idx, idx2, hd, pos, starts, seg_c0, seg_new, sort_tmp;
         DevBuf tk, tc, tk2, tc2, n_keys;  // FirstGroupBy key -> count table
         int64_t t_cap = 0, t_keys = 0;

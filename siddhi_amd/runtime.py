@@ -31,7 +31,7 @@ def lib():
                               "(the GPU path has no CPU fallback)")
         L = C.CDLL(LIB_PATH)
         abi.setup_lib_prototypes(L, "sh")
-        if L.sh_abi_version() != 15:
+        if L.sh_abi_version() != 16:
             raise ImportError("libsiddhi_hip ABI version mismatch")
         _lib = L
     return _lib
@@ -135,6 +135,33 @@ class GpuQuery:
     def set_compact_flushes(self, on: bool = True):
         """sh_query_set_compact_flushes: one-row flushes at their rows' timestamps leave the flush arrays NULL."""
         _check(lib().sh_query_set_compact_flushes(self.h, 1 if on else 0))
+
+    def rate_apply_merged(self, merged: dict) -> dict:
+        """sh_rate_apply_merged: this query (rate set, never pushed) as the output rate limiter of a sharded
+        query; `merged` is one call's merged owner output (out_arrays layout), the result the limited rows."""
+        n = int(merged["ts"].size)
+        dt = {"flush_offsets": np.int64, "flush_clock": np.int64, "ts": np.int64, "expired": np.uint8,
+              "keys": np.int64, "vals": np.uint64, "nulls": np.uint8, "rep": np.int64}
+        keep = {k: np.ascontiguousarray(merged[k], dtype=t) for k, t in dt.items()}
+        o = abi.Out()
+        o.n_flushes = int(keep["flush_clock"].size)
+        o.n_rows = n
+        o.n_keys = int(keep["keys"].shape[0])
+        o.n_vals = int(keep["vals"].shape[0])
+        for i, t in enumerate(merged["val_types"]):
+            o.val_types[i] = int(t)
+        P = C.POINTER
+        o.flush_offsets = keep["flush_offsets"].ctypes.data_as(P(C.c_int64))
+        o.flush_clock = keep["flush_clock"].ctypes.data_as(P(C.c_int64))
+        o.ts = keep["ts"].ctypes.data_as(P(C.c_int64))
+        o.expired = keep["expired"].ctypes.data_as(P(C.c_uint8))
+        o.keys = keep["keys"].ctypes.data_as(P(C.c_int64))
+        o.vals = keep["vals"].ctypes.data_as(P(C.c_uint64))
+        o.nulls = keep["nulls"].ctypes.data_as(P(C.c_uint8))
+        o.rep = keep["rep"].ctypes.data_as(P(C.c_int64))
+        out = C.POINTER(abi.Out)()
+        _check(lib().sh_rate_apply_merged(self.h, C.byref(o), C.byref(out)))
+        return abi.out_arrays(out)
 
     def set_strings(self, col: str, names, first_id: int = 0):
         """The text of string column `col`'s dictionary ids first_id.. (sh_query_set_strings)."""

@@ -246,6 +246,22 @@ def merge_owner_outputs(parts: List[dict], bounds: Optional[np.ndarray] = None,
     return res
 
 
+class MergedRateLimiter:
+    """`output … every …` of a sharded query: OutputRateLimiter.process sits after the selector, so it sees
+    the merged single-stream output. The merging rank holds one never-pushed query of the same spec (its
+    rate set) and passes every merged call output through it on its GPU (sh_rate_apply_merged)."""
+
+    def __init__(self, spec, ctx: Optional[Context] = None):
+        from siddhi_amd import runtime
+        self.q = runtime.GpuQuery(spec, ctx)
+
+    def apply(self, merged: dict) -> dict:
+        return self.q.rate_apply_merged(merged)
+
+    def close(self):
+        self.q.close()
+
+
 def merge_sends(spec, last_sends: Tuple[int, int]) -> Optional[Tuple[int, int]]:
     """The `sends` argument of merge_owner_outputs for a query: sliding windows and timeBatch(T, true) flush
     once per send (the send's chunk), lengthBatch(L, true) once per passing event (LengthBatchWindowProcessor

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     L = C.CDLL(LIB)
     L.sh_abi_version.restype = C.c_int32
-    assert L.sh_abi_version() == 15
+    assert L.sh_abi_version() == 16
 
 
 def test_struct_layout_matches_c(tmp_path):

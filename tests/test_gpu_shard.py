@@ -24,11 +24,13 @@ def spec(keys, filt=None, start=None, aggs=None, group_by=("k",), schema=SCHEMA)
 
 
 def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
-    """pushes: list of (ts, cols) numpy global pushes; each is cut into `world` send-aligned slices."""
+    """pushes: list of (ts, cols) numpy global pushes; each is cut into `world` send-aligned slices. A spec
+    with an output rate runs its limiter over the merged output (MergedRateLimiter)."""
     import torch
-    from siddhi_amd.shard import LocalShards, merge_owner_outputs, merge_sends
+    from siddhi_amd.shard import LocalShards, MergedRateLimiter, merge_owner_outputs, merge_sends
     dev = torch.device("cuda", 0)
     ls = LocalShards(sp, world)
+    rl = MergedRateLimiter(sp) if sp.rate else None
     parts = []
     for pi, (ts, cols) in enumerate(pushes):
         n = len(ts)
@@ -45,6 +47,9 @@ def run_sharded(sp, world, pushes, send_size, cut_fracs, advance=None):
     if advance is not None:
         parts.append(merge_owner_outputs(ls.advance_time(advance)))
     ls.close()
+    if rl is not None:
+        parts = [rl.apply(p) for p in parts]
+        rl.close()
     return abi.concat_arrays(parts)
 
 
@@ -312,3 +317,22 @@ def test_sharded_stream_current_two_keys():
     got = run_sharded(sp, 5, pushes, 3, [[0.2, 0.4, 0.6, 0.8]], advance=int(ts[-1]) + 3000)
     ref = run_oracle(sp, pushes, 3, advance=int(ts[-1]) + 3000)
     assert_same(got, ref, label="sharded stream.current two keys")
+
+
+# ---- output rate limiting of a sharded query: the limiter sits after the selector
+# (OutputRateLimiter.process), so it runs over the merged single-stream output, call by call ----------
+@pytest.mark.parametrize("rate,window,param,send_size,grouped", [
+    (("first", 7), "timeBatch", 25, 1, False), (("last", 5), "timeBatch", 35, 3, False),
+    (("all", 4), "lengthBatch", 40, 1, False), (("first", 3), "timeBatch", 600, 1, True),
+    (("last", 4), "lengthBatch", 300, 2, True), (("first_time", 70), "timeBatch", 20, 1, False),
+    (("first_time", 900), "timeBatch", 500, 1, True), (("last", 6), "time", 400, 1, True)])
+def test_sharded_output_rate(rate, window, param, send_size, grouped):
+    sp = abi.QuerySpec(SCHEMA, window, param, group_by=["k"] if grouped else [], key_capacity=2_000, rate=rate,
+                       aggs=[("count", None), ("min", "v"), ("max", "v"), ("avg", "v")])
+    pushes = stream_pushes(90_000, [30_000, 1, 59_999], 0xB7, 2_000, 30)
+    fr = [[0.3, 0.6], [0.0, 0.0], [0.2, 0.9]]
+    adv = int(pushes[-1][0][-1]) + 4_000
+    got = run_sharded(sp, 3, pushes, send_size, fr, advance=adv)
+    ref = run_oracle(sp, pushes, send_size, advance=adv)
+    assert ref["ts"].size > 10
+    assert_same(got, ref, label=f"sharded rate {rate} {window} grouped={grouped}")
