@@ -285,7 +285,9 @@ __device__ __forceinline__ i64 key_part(const KeyPlan& kp, const ColSet& cs, int
 
 __device__ __forceinline__ u32 key_part32(const KeyPlan& kp, const ColSet& cs, int g, i64 e) {
     if (kp.type[g] == SH_T_FLOAT) {
-        const float f = ((const float*)cs.ptr[kp.col[g]])[e];
+        // (a column loaded in its raw 8-byte form holds the value widened to double)
+        const float f = cs.type[kp.col[g]] == SH_T_FLOAT ? ((const float*)cs.ptr[kp.col[g]])[e]
+                                                         : (float)__longlong_as_double(load_raw(cs, kp.col[g], e));
         return f != f ? 0x7FC00000u : __float_as_uint(f);
     }
     return (u32)key_part(kp, cs, g, e);

@@ -21,6 +21,7 @@
 #include "sh_internal.h"
 #include "sh_runtime.h"
 #include "sh_sliding.h"
+#include "sh_wide.h"
 
 using namespace shd;
 
@@ -126,6 +127,14 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     if (d->window == SH_WIN_TIME && (d->expired_on || !d->current_on))
         return sh_fail(SH_ERR_UNSUPPORTED, "sharded sliding windows emit current events (`insert into`)");
     if (d->n_cols <= 0 || d->n_cols > SH_MAX_COLS) return sh_fail(SH_ERR_INVALID, "bad column count");
+    // group keys the owner interns (more than two columns, or a 64-bit / floating one beside another): owners by
+    // a prefix of the key (one 64-bit column or two 32-bit ones — all of a key's events share it), the other
+    // group-by columns travel raw; batch windows with current output (or stream.current.event)
+    const bool wide = !kp_override && d->n_group_by > 0 && d->n_group_by <= SH_MAX_GROUP &&
+                      WideKeys::needed(d->n_group_by, d->group_by, d->col_types);
+    if (wide && (d->window == SH_WIN_TIME || d->partition_col >= 0 || d->expired_on || d->n_cols + 1 >= SH_MAX_COLS))
+        return sh_fail(SH_ERR_UNSUPPORTED, "sharded queries with wide group keys: unpartitioned batch windows, current "
+                                           "output, at most 6 stream columns");
     sh_shard* s = new sh_shard();
     s->ctx = ctx;
     s->d = *d;
@@ -134,9 +143,15 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     s->world = world;
     int32_t vt[SH_MAX_AGGS];
     int rc;
+    int32_t kg[2] = {d->n_group_by > 0 ? d->group_by[0] : 0, d->n_group_by > 1 ? d->group_by[1] : 0};
+    int nkg = d->n_group_by;
+    if (wide) {
+        const auto w64 = [&](int c) { const int t = d->col_types[c]; return t == SH_T_LONG || t == SH_T_DOUBLE || t == SH_T_FLOAT; };
+        nkg = (w64(kg[0]) || w64(kg[1])) ? 1 : 2;
+    }
     if ((rc = compile_filter(d->n_filter_ops, d->filter, d->n_cols, d->col_types, s->fp)) ||
         (rc = compile_aggs(d->n_aggs, d->aggs, d->n_cols, d->col_types, s->ap, vt)) ||
-        (!kp_override && (rc = compile_keys(d->n_group_by, d->group_by, d->n_cols, d->col_types, s->kp)))) {
+        (!kp_override && (rc = compile_keys(nkg, wide ? kg : d->group_by, d->n_cols, d->col_types, s->kp)))) {
         delete s;
         return rc;
     }
@@ -159,6 +174,15 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
             s->wkp.type[s->wkp.n] = s->kp.type[g];
             s->wkp.div[s->wkp.n] = 0;
             s->wkp.n++;
+        }
+    }
+    if (wide) {  // (the group-by columns beyond the owner prefix travel raw)
+        for (int g = 0; g < d->n_group_by; g++) {
+            const int c = d->group_by[g];
+            bool have = false;
+            for (int j = 0; j < s->wkp.n; j++) have |= s->wkp.col[j] == c;
+            for (int j = 0; j < s->rp.n; j++) have |= s->rp.src[j] == c;
+            if (!have) s->rp.src[s->rp.n++] = c;
         }
     }
     // sliding: the send's global clock and the global PM travel as two extra raw columns
@@ -190,7 +214,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     od.n_filter_ops = 0;
     od.filter = nullptr;
     int64_t cap = d->key_capacity > 0 ? d->key_capacity : (1 << 16);
-    od.key_capacity = s->kp.dense ? (cap + world - 1) / world : cap / world + cap / (4 * world) + 64;
+    od.key_capacity = wide ? cap : s->kp.dense ? (cap + world - 1) / world : cap / world + cap / (4 * world) + 64;
     if ((rc = kp_override ? sh_query_create_internal(ctx, &od, *kp_override, &s->owner)
                           : sh_query_create(ctx, &od, &s->owner))) {
         delete s;
@@ -198,7 +222,7 @@ static int shard_create(sh_ctx* ctx, const sh_query_desc* d, const KeyPlan* kp_o
     }
     sh_query* q = s->owner;
     q->given = true;
-    if (q->kp.dense) {
+    if (q->kp.dense && !q->wide) {  // (a wide owner's ids are its own interned ones)
         q->kt.dmul = (uint32_t)world;
         q->kt.dadd = (uint32_t)rank;
     }

@@ -527,6 +527,12 @@ static int shard_snapshot_blob(sh_shard* sd, sh_query* q, Writer& w) {
     w.val<uint32_t>((uint32_t)q->kind);
     for (int i = 0; i < 14; i++) w.val<int64_t>(sc[i]);
     RCHK(q->kind == 1 ? sliding_snapshot(q, w) : batch_snapshot(q, w));
+    if (q->wide) {  // an owner's interned group keys (its window's key ids)
+        std::vector<uint8_t> kb;
+        RCHK(q->wide->save(kb, q->ctx->stream));
+        w.val<uint64_t>(kb.size());
+        w.put(kb.data(), kb.size());
+    }
     sh_aggregation* a = shard_aggregation(sd);
     w.val<uint8_t>(a ? 1 : 0);
     if (a) {
@@ -573,6 +579,13 @@ static int shard_restore_blob(sh_shard* sd, sh_query* q, const void* buf, int64_
     const int rc = q->kind == 1 ? sliding_restore(q, r) : batch_restore(q, r);
     q->fp = keep;
     RCHK(rc);
+    if (q->wide) {
+        const uint64_t kn = r.val<uint64_t>();
+        if (!r.ok || r.o + kn > r.n) return sh_fail(SH_ERR_INVALID, "snapshot blob truncated");
+        size_t off = 0;
+        RCHK(q->wide->load(r.p + r.o, (size_t)kn, off, q->ctx->stream));
+        r.o += kn;
+    }
     sh_aggregation* a = shard_aggregation(sd);
     const bool has_agg = r.val<uint8_t>() != 0;
     if (!r.ok || has_agg != (a != nullptr)) return sh_fail(SH_ERR_INVALID, "snapshot does not match this shard");

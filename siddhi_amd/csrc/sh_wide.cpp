@@ -99,6 +99,7 @@ int WideKeys::intern(hipStream_t s, const ColSet& full, const FilterProg& f, int
             const int src = w.lv[l].src[j];
             cs2.type[j] = w.lv[l].kp.type[j];
             if (src >= 0) {
+                cs2.type[j] = full.type[src];  // (the column as loaded: a sharded owner's are 8-byte raw)
                 cs2.ptr[j] = full.ptr[src];
             } else {
                 cs2.ptr[j] = ids[-src - 1].p;

@@ -2122,7 +2122,8 @@ static int wide_push(sh_query* q, const sh_batch* dev, bool host_out, const sh_o
     if (b.n > 0) {
         ColSet full{};
         full.n = q->wide_n_cols;
-        for (int c = 0; c < q->wide_n_cols; c++) { full.type[c] = q->d.col_types[c]; full.ptr[c] = b.cols[c]; }
+        // (at the query's load widths: a sharded owner's columns are in their 8-byte raw form)
+        for (int c = 0; c < q->wide_n_cols; c++) { full.type[c] = q->load_type[c]; full.ptr[c] = b.cols[c]; }
         RCHK(q->wide->intern(s, full, q->fp, b.n, &ids));
     }
     b.cols[q->wide_n_cols] = ids;
@@ -2314,13 +2315,30 @@ int64_t given_flush_clock(const sh_query* q, int64_t W) {
     return q->clock;
 }
 
+// a sharded owner grouped by a wide key runs the window on the interned ids (device output); its rows get
+// their group-by values back (wide_finish) and the merge order comes back from the device
+static int given_order_host(sh_query* q, bool host_out, const sh_out* o) {
+    if (!q->given || !host_out) return SH_OK;
+    const int64_t n = o->n_rows;
+    q->order_host.resize(n);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(q->order_host.data(), q->out_order.p, n * 8, hipMemcpyDeviceToHost, q->ctx->stream));
+        HIPCHK(hipStreamSynchronize(q->ctx->stream));
+    }
+    return SH_OK;
+}
+
 int query_push_given(sh_query* q, const sh_batch* b, bool host_out, const sh_out** out) {
+    if (q->wide) {
+        RCHK(wide_push(q, b, host_out, out));
+        return given_order_host(q, host_out, *out);
+    }
     return push_core(q, b, host_out, out);
 }
 
 // No events reached this owner in the push: close its open window if the global clock moved past it.
 int query_close_given(sh_query* q, bool host_out_req, const sh_out** out) {
-    const bool host_out = host_out_req && !q->xmode;
+    const bool host_out = host_out_req && !q->xmode && !q->wide;
     if (q->xmode) given_closes(q);
     q->out.reset();
     q->order_host.clear();
@@ -2346,9 +2364,18 @@ int query_close_given(sh_query* q, bool host_out_req, const sh_out** out) {
     }
     if (q->xmode) return xout_finish(q, host_out_req, out);
     finish_out(q, host_out, out);
+    if (q->wide) {
+        RCHK(wide_finish(q, host_out_req, out));
+        return given_order_host(q, host_out_req, *out);
+    }
     return SH_OK;
 }
 
 int query_advance(sh_query* q, int64_t now, bool host_out, const sh_out** out) {
+    if (q->wide) {
+        RCHK(advance_core(q, now, false, out));
+        RCHK(wide_finish(q, host_out, out));
+        return given_order_host(q, host_out, *out);
+    }
     return advance_core(q, now, host_out, out);
 }

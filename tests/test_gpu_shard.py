@@ -336,3 +336,69 @@ def test_sharded_output_rate(rate, window, param, send_size, grouped):
     ref = run_oracle(sp, pushes, send_size, advance=adv)
     assert ref["ts"].size > 10
     assert_same(got, ref, label=f"sharded rate {rate} {window} grouped={grouped}")
+
+
+# ---- group keys the owners intern (three columns, a long beside another): owners by a prefix of the key
+# (all of a key's events share it), the other group-by columns travel raw, each owner interns its keys
+WSCH = abi.Schema.parse("a int, s string, l long, v double, ts long")
+
+
+def wide_pushes(n, sizes, seed):
+    rng = np.random.default_rng(seed)
+    ts = (synth.T0 + np.arange(n, dtype=np.int64) // 30).astype(np.int64)
+    a = rng.integers(-4, 5, n).astype(np.int32)
+    s = rng.integers(0, 40, n).astype(np.int32)
+    l = (rng.integers(0, 7, n) * 10_000_000_019 - 30_000_000_000).astype(np.int64)
+    v = rng.integers(-500, 500, n).astype(np.float64) / 4
+    cols = [a, s, l, v, ts.copy()]
+    out, o = [], 0
+    for z in sizes:
+        out.append((ts[o:o + z], [c[o:o + z] for c in cols]))
+        o += z
+    return out
+
+
+@pytest.mark.parametrize("window,param,group,world,send_size,sc", [
+    ("timeBatch", 700, ["a", "s", "l"], 3, 1, False), ("timeBatch", 400, ["l", "a"], 2, 5, False),
+    ("lengthBatch", 900, ["s", "l", "a"], 4, 1, False), ("lengthBatch", 333, ["a", "l"], 3, 2, False),
+    ("timeBatch", 500, ["s", "a", "l"], 3, 1, True)])
+def test_sharded_wide_group_keys(window, param, group, world, send_size, sc):
+    sp = abi.QuerySpec(WSCH, window, param, group_by=group, stream_current=sc, key_capacity=4_096,
+                       aggs=[("count", None), ("sum", "v"), ("min", "v"), ("max", "l")], filter=(">", "v", -100.0))
+    pushes = wide_pushes(60_000, [20_000, 1, 39_999], 0xA1)
+    fr = [[(g + 1) / world for g in range(world - 1)], [0.0] * (world - 1), [0.1 * (g + 1) for g in range(world - 1)]]
+    adv = int(pushes[-1][0][-1]) + 3_000
+    got = run_sharded(sp, world, pushes, send_size, fr, advance=adv)
+    ref = run_oracle(sp, pushes, send_size, advance=adv)
+    assert ref["keys"].shape[0] == len(group) and ref["ts"].size > 100
+    assert_same(got, ref, label=f"sharded wide {window} {group} x{world} sc={sc}")
+
+
+def test_sharded_wide_group_keys_refusals():
+    from siddhi_amd.runtime import SiddhiError
+    from siddhi_amd.shard import ShardedQuery
+    for sp in (abi.QuerySpec(WSCH, "time", 100, group_by=["a", "s", "l"], aggs=[("count", None)]),
+               abi.QuerySpec(WSCH, "timeBatch", 100, group_by=["a", "s", "l"], aggs=[("count", None)], output="all")):
+        with pytest.raises(SiddhiError, match="wide group keys"):
+            ShardedQuery(sp, 0, 2)
+
+
+def test_sharded_wide_group_keys_float_and_checkpoint():
+    """a float key column in the owner prefix (its 64-bit wire form) and a 2-part level over a float, then a
+    checkpoint of the owners' interned keys between pushes"""
+    from tests.test_gpu_shard_snapshot import run_sharded_restored
+    sch = abi.Schema.parse("f float, a int, l long, v double, ts long")
+    rng = np.random.default_rng(5)
+    n = 40_000
+    ts = (synth.T0 + np.arange(n, dtype=np.int64) // 20).astype(np.int64)
+    f = np.array([0.5, -1.25, np.nan, 3.0, -0.0, 0.0], np.float32)[rng.integers(0, 6, n)]
+    cols = [f, rng.integers(-3, 4, n).astype(np.int32), (rng.integers(0, 5, n) * 7_000_000_001).astype(np.int64),
+            rng.integers(-99, 99, n).astype(np.float64) / 8, ts.copy()]
+    pushes = [(ts[a:b], [c[a:b] for c in cols]) for a, b in ((0, 15_000), (15_000, 27_000), (27_000, n))]
+    for group in (["f", "a", "l"], ["a", "f", "l"]):
+        sp = abi.QuerySpec(sch, "timeBatch", 300, group_by=group, key_capacity=1_024,
+                           aggs=[("count", None), ("sum", "v"), ("max", "l")])
+        adv = int(ts[-1]) + 2_000
+        ref = run_oracle(sp, pushes, 1, advance=adv)
+        assert_same(run_sharded(sp, 3, pushes, 1, [[0.4, 0.7]], advance=adv), ref, label=f"sharded wide float {group}")
+        assert_same(run_sharded_restored(sp, 2, pushes, 1, 2, advance=adv), ref, label=f"sharded wide ckpt {group}")
