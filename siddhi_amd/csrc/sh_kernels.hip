@@ -1877,15 +1877,18 @@ __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64*
     idx[m] = (u32)m;
 }
 
-// one thread per (window, key) run of the sorted entries
+// one thread per (window, key) run of the sorted entries, the runs packed onto the first threads (pos[M]
+// runs: a thread per entry that returned unless it was a head left ~9 of 10 lanes idle, C2's runs being
+// ~10 entries long)
 __global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict__ hd, const u32* __restrict__ pos,
                                                    const u32* __restrict__ starts, const u32* __restrict__ idx,
                                                    const i64* __restrict__ chunk, const u64* __restrict__ pend_vals,
                                                    i64 pend_cap, AggPlan ap, i64 n_old, u32* ghead, u64* sval,
                                                    u32* slast) {
-    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= M || !hd[i]) return;
-    const i64 hi = starts[pos[i] + 1];
+    (void)hd;
+    const i64 sg = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (sg >= (i64)pos[M]) return;
+    const i64 i = starts[sg], hi = starts[sg + 1];
     u64 f[SH_MAX_AGGS];
 #pragma unroll
     for (int j = 0; j < SH_MAX_AGGS; j++) f[j] = 0;
