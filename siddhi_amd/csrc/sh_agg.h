@@ -43,6 +43,8 @@ void launch_find_fold(hipStream_t s, i64 n, const u32* idx, const u32* flag, con
                       i64* out_key, u64* out_vals);
 int sort_u64_pairs(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out, i64 n,
                    hipStream_t s);
+int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
+                        i64 n, unsigned end_bit, hipStream_t s);
 void launch_fill_i64(hipStream_t s, i64* p, i64 n, i64 v);
 void launch_minmax_i64(hipStream_t s, const i64* x, i64 n, i64* out);  // out: minmax_scratch_bytes()
 size_t minmax_scratch_bytes();

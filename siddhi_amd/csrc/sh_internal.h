@@ -441,6 +441,8 @@ void launch_ratep_gather(hipStream_t s, i64 T, const u32* list, const u64* okey,
                          const u32* in_part, RateRows out, int nk, int na, int* out_flush, u32* out_part);
 
 // ---- stream.current.event batch windows (sh_kernels.hip, driven by sh_window.cpp) ----
+// (w << 32 | slot) -> (w << kb | slot): the sort then reads kb + the window bits only
+void launch_sc_pack_keys(hipStream_t s, i64 M, unsigned kb, u64* skey);
 void launch_sc_keys(hipStream_t s, i64 M, i64 n_old, const i64* pcb, int nb, const u32* pend_pos, const u64* pend_gidx,
                     int per_event, i64 send_size, i64 seq0, u64* skey, u32* idx, i64* chunk, i64* send,
                     int by_entry = 0);

@@ -1877,6 +1877,18 @@ __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64*
     idx[m] = (u32)m;
 }
 
+__global__ __launch_bounds__(kBlock) void k_sc_pack_keys(i64 M, unsigned kb, u64* skey) {
+    const i64 m = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= M) return;
+    const u64 k = skey[m];
+    skey[m] = ((k >> 32) << kb) | (k & 0xFFFFFFFFull);
+}
+
+void launch_sc_pack_keys(hipStream_t s, i64 M, unsigned kb, u64* skey) {
+    if (M <= 0) return;
+    hipLaunchKernelGGL(k_sc_pack_keys, dim3((unsigned)((M + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, M, kb, skey);
+}
+
 // one thread per (window, key) run of the sorted entries, the runs packed onto the first threads (pos[M]
 // runs: a thread per entry that returned unless it was a head left ~9 of 10 lanes idle, C2's runs being
 // ~10 entries long)

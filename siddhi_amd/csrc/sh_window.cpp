@@ -853,12 +853,26 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     launch_sc_keys(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(),
                    per_event ? 1 : 0, gv ? q->given_ss : ss, gv ? q->given_seq0 : seq0, q->sc_skey.as<u64>(),
                    q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), gv ? 1 : 0);
+    const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
+    const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
+    // current rows only: the sorted keys are compared for equality alone, so the window index goes right
+    // above the slot bits and the radix sort reads those bits only (C2: 24 of 64)
+    unsigned end_bit = 64;
+    if (!(xs || xt)) {
+        unsigned kb = 1, wb = 1;
+        while (kb < 32 && ((uint64_t)1 << kb) < (uint64_t)q->kt.size_) kb++;
+        while (wb < 31 && ((int64_t)1 << wb) <= (int64_t)nb) wb++;
+        if (kb + wb <= 48) {
+            launch_sc_pack_keys(s, M, kb, q->sc_skey.as<u64>());
+            end_bit = kb + wb;
+        }
+    }
     size_t tb = 0;
-    if (sort_u64_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, M, s))
+    if (sort_u64_pairs_bits(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, M, end_bit, s))
         return sh_fail(SH_ERR_DEVICE, "stream.current: sort sizing");
     RCHK(q->sc_sort.reserve(std::max<size_t>(tb, 16), false));
-    if (sort_u64_pairs(q->sc_sort.p, &tb, q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(), q->sc_idx.as<u32>(),
-                       q->sc_idx2.as<u32>(), M, s))
+    if (sort_u64_pairs_bits(q->sc_sort.p, &tb, q->sc_skey.as<u64>(), q->sc_skey2.as<u64>(), q->sc_idx.as<u32>(),
+                            q->sc_idx2.as<u32>(), M, end_bit, s))
         return sh_fail(SH_ERR_DEVICE, "stream.current: sort failed");
     launch_rate_segments(s, M, q->sc_skey2.as<u64>(), q->sc_idx2.as<u32>(), 1, 0, q->sc_hd.as<u32>(),
                          q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_tmp.as<int64_t>());
@@ -879,8 +893,6 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         launch_sc_send_last(s, b->ts, N, ss, n_sends, q->sc_sl.as<int64_t>());
     }
     HIPCHK(hipGetLastError());
-    const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
-    const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
     // (host scratch kept by the query: a fresh 8-byte-per-send vector per push faulted in its pages —
     // hundreds of MB per C2-sized push)
     std::vector<int64_t>& sl = q->sc_sl_host;
