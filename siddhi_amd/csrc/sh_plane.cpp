@@ -612,12 +612,16 @@ static int plane_run_group(sh_query* q, const sh_batch* b, int64_t now, bool hos
             // (current only: one entry per event; the timeout's entries are exactly n_e)
             const int64_t ne_sort = xt ? n_e : q->d.expired_on ? ne_cap : n;
             const unsigned sbits = xt ? (unsigned)(gbits + bits_for((int64_t)em.size() + 1)) : ebits;
-            if (sort_u64_pairs_bits(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_sort,
-                                    sbits, st))
+            // grouped by the partition key (or not at all) a chunk — one partition's batch — has one group, so
+            // the (chunk, group) order is the chunk order: the radix sort skips the group bits (stable: a
+            // chunk's entries keep their order either way; the `none` key's chunk bits are all ones)
+            const unsigned sbeg = (!xt && !q->group_other) ? (unsigned)gbits : 0u;
+            if (sort_u64_pairs_range(nullptr, &tb, s->pg_ekey.as<u64>(), nullptr, s->pg_eval.as<u32>(), nullptr, ne_sort,
+                                     sbeg, sbits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort sizing failed");
             RCHK(s->sort_tmp.reserve(std::max<size_t>(tb, 16), false));
-            if (sort_u64_pairs_bits(s->sort_tmp.p, &tb, s->pg_ekey.as<u64>(), s->pg_ekey2.as<u64>(), s->pg_eval.as<u32>(),
-                                    s->pg_eval2.as<u32>(), ne_sort, sbits, st))
+            if (sort_u64_pairs_range(s->sort_tmp.p, &tb, s->pg_ekey.as<u64>(), s->pg_ekey2.as<u64>(), s->pg_eval.as<u32>(),
+                                     s->pg_eval2.as<u32>(), ne_sort, sbeg, sbits, st))
                 return sh_fail(SH_ERR_DEVICE, "radix sort failed");
             // ---- segments = rows
             RCHK(s->pg_head.reserve(n_e + 16, false));

@@ -93,6 +93,8 @@ void launch_pg_gather(hipStream_t s, const i64* idx, i64 n, const unsigned char*
 // stable sort of (u64 key, u32 value) pairs over key bits [0, end_bit)
 int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
                         i64 n, unsigned end_bit, hipStream_t s);
+int sort_u64_pairs_range(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
+                         i64 n, unsigned begin_bit, unsigned end_bit, hipStream_t s);
 // time / externalTime windows grouped by other columns: the partitions' operations in order
 struct PgOps {
     i64* pos;            // chunk position (the lanes' output position of the point)

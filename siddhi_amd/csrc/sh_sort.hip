@@ -44,6 +44,13 @@ int sort_u64_pairs_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_ou
     return e == hipSuccess ? 0 : -1;
 }
 
+// the same over key bits [begin_bit, end_bit) (keys whose low bits follow from the high ones)
+int sort_u64_pairs_range(void* temp, size_t* bytes, const u64* keys, u64* keys_out, const u32* vals, u32* vals_out,
+                         i64 n, unsigned begin_bit, unsigned end_bit, hipStream_t s) {
+    hipError_t e = rocprim::radix_sort_pairs(temp, *bytes, keys, keys_out, vals, vals_out, (unsigned)n, begin_bit, end_bit, s);
+    return e == hipSuccess ? 0 : -1;
+}
+
 // stable sort of u64 keys over bits [0, end_bit), values = the keys' input positions
 int sort_u64_iota_bits(void* temp, size_t* bytes, const u64* keys, u64* keys_out, u32* vals_out, i64 n,
                        unsigned end_bit, hipStream_t s) {
