@@ -1927,7 +1927,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict
         if ((i64)m < n_old) continue;
         if (head < 0 || cp != ch) {
             head = m;
-            ghead[m] = 1;
+            if (ghead) ghead[m] = 1;  // (null: every new entry is its own chunk, so its own row)
         }
         if (t + 1 == hi || ch_nx != ch) {  // the group's last event: its row values
 #pragma unroll
@@ -1938,7 +1938,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict
                 for (int j = 1; j < SH_MAX_AGGS; j++) if (ap.field[a] == j) fv = f[j];
                 sval[(size_t)head * ap.n + a] = agg_out(ap, a, c, fv);  // (one record per row: see k_sc_keys)
             }
-            slast[head] = m;
+            if (ghead) slast[head] = m;
         }
     }
 }
@@ -1954,9 +1954,10 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
                                                    u64* out_vals, i64* out_rep, i64* out_chunk, i64* out_send,
                                                    i64* out_order) {
     const i64 m = n_old + (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= M || !ghead[m]) return;
-    const i64 o = pre[m - n_old];
-    const u32 l = slast[m];
+    if (m >= M || (ghead && !ghead[m])) return;
+    // (ghead null: every new entry is its own chunk — per-event sends — so row o is entry m itself)
+    const i64 o = ghead ? (i64)pre[m - n_old] : m - n_old;
+    const u32 l = ghead ? slast[m] : (u32)m;
     out_ts[o] = pend_ts[l];
     out_rep[o] = (i64)pend_gidx[l];
     i64 kv[kKeyParts] = {0, 0};

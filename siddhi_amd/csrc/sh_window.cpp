@@ -876,10 +876,14 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         return sh_fail(SH_ERR_DEVICE, "stream.current: sort failed");
     launch_rate_segments(s, M, q->sc_skey2.as<u64>(), q->sc_idx2.as<u32>(), 1, 0, q->sc_hd.as<u32>(),
                          q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_tmp.as<int64_t>());
-    HIPCHK(hipMemsetAsync(q->sc_ghead.p, 0, (size_t)(M + 1) * 4, s));
+    // every new entry its own chunk (per-event sends, lengthBatch(L, true)): each is its own row, no head
+    // flags, no scan of them and no read-back of the row count (current rows only)
+    const bool all_heads = !(xs || xt) && (per_event || (gv ? q->given_ss : ss) == 1);
+    if (!all_heads) HIPCHK(hipMemsetAsync(q->sc_ghead.p, 0, (size_t)(M + 1) * 4, s));
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_sc_walk(s, M, q->sc_hd.as<u32>(), q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_idx2.as<u32>(),
-                   q->sc_chunk.as<int64_t>(), q->pend_vals.as<u64>(), q->pend_cap, q->ap, n_old, q->sc_ghead.as<u32>(),
+                   q->sc_chunk.as<int64_t>(), q->pend_vals.as<u64>(), q->pend_cap, q->ap, n_old,
+                   all_heads ? nullptr : q->sc_ghead.as<u32>(),
                    q->sc_sval.as<u64>(), q->sc_slast.as<u32>());
     HIPCHK(hipEventRecord(q->ev_agg1, s));
     const int64_t nn = M - n_old;
@@ -956,6 +960,8 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->scx_rows.as<uint32_t>() + nr - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         T = *q->h_small_sc.as<uint32_t>();
+    } else if (all_heads) {
+        T = nn;
     } else {
         HIPCHK(hipMemcpyAsync(q->sc_pre.p, q->sc_ghead.as<uint32_t>() + n_old, (size_t)(nn + 1) * 4,
                               hipMemcpyDeviceToDevice, s));
@@ -998,7 +1004,7 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                          q->out_expired.as<unsigned char>(), q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(),
                          q->sc_osend.as<int64_t>());
     } else {
-        launch_sc_emit(s, M, n_old, q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(),
+        launch_sc_emit(s, M, n_old, all_heads ? nullptr : q->sc_ghead.as<u32>(), q->sc_pre.as<u32>(), q->sc_slast.as<u32>(),
                        q->sc_sval.as<u64>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(),
                        q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T,
                        q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
