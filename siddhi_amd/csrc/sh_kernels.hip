@@ -1908,14 +1908,16 @@ __global__ __launch_bounds__(kBlock) void k_sc_walk(i64 M, const u32* __restrict
     i64 head = -1;
     // each entry's chunk is read once and carried (the previous / next entry's chunk decide the group's
     // first and last event): one random chunk load per entry instead of three
+    // (every new entry its own chunk — ghead null —: the entry's own index names its chunk, no load)
+    const bool ah = ghead == nullptr;
     u32 m_nx = idx[i];
-    i64 ch_nx = (i64)m_nx < n_old ? -1 : chunk[m_nx], ch_prev = -2;
+    i64 ch_nx = (i64)m_nx < n_old ? -1 : ah ? (i64)m_nx : chunk[m_nx], ch_prev = -2;
     for (i64 t = i; t < hi; t++) {
         const u32 m = m_nx;
         const i64 ch = ch_nx;
         if (t + 1 < hi) {
             m_nx = idx[t + 1];
-            ch_nx = (i64)m_nx < n_old ? -1 : chunk[m_nx];
+            ch_nx = (i64)m_nx < n_old ? -1 : ah ? (i64)m_nx : chunk[m_nx];
         }
         i64 v[SH_MAX_AGGS];
 #pragma unroll
