@@ -2384,8 +2384,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_flushes(i64 T, const i64* __restr
                                                       const i64* __restrict__ slp, int cv0, i64 clock0,
                                                       const i64* __restrict__ bclk, i64* fo1, i64* fc) {
     const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= T || pre[i + 1] == pre[i]) return;
-    const u32 k = pre[i];
+    if (i >= T || (pre && pre[i + 1] == pre[i])) return;
+    const u32 k = pre ? pre[i] : (u32)i;  // (pre null: every row ends its own flush)
     const i64 sd = osd[i];
     fo1[k] = i + 1;
     fc[k] = sd >= 0 ? (cv0 ? max(clock0, slp[sd]) : slp[sd]) : bclk[-sd - 1];

@@ -1022,17 +1022,20 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         RCHK(q->sc_h.reserve((size_t)std::max(nb, 1) * 8 + 64));
         for (int i = 0; i < nb; i++) q->sc_h.as<int64_t>()[i] = bounds[i].clock;
         if (nb) HIPCHK(hipMemcpyAsync(q->sc_bclk.p, q->sc_h.p, (size_t)nb * 8, hipMemcpyHostToDevice, s));
-        RCHK(q->sc_fflag.reserve((size_t)(T + 1) * 4, false));
-        RCHK(q->sc_tmp.reserve((size_t)((T + 1 + kTile - 1) / kTile + 16) * 8, false));
-        launch_sc_flush_flags(s, T, q->sc_ochunk.as<int64_t>(), q->sc_fflag.as<u32>());
-        launch_scan_sum_large_u32(s, q->sc_fflag.as<u32>(), T + 1, q->sc_tmp.as<int64_t>());
         RCHK(q->h_small_sc.reserve(64));
-        HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->sc_fflag.as<uint32_t>() + T, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const int64_t nf = *q->h_small_sc.as<uint32_t>();
+        int64_t nf = T;  // (every row its own chunk: a flush per row, no flags to scan)
+        if (!all_heads) {
+            RCHK(q->sc_fflag.reserve((size_t)(T + 1) * 4, false));
+            RCHK(q->sc_tmp.reserve((size_t)((T + 1 + kTile - 1) / kTile + 16) * 8, false));
+            launch_sc_flush_flags(s, T, q->sc_ochunk.as<int64_t>(), q->sc_fflag.as<u32>());
+            launch_scan_sum_large_u32(s, q->sc_fflag.as<u32>(), T + 1, q->sc_tmp.as<int64_t>());
+            HIPCHK(hipMemcpyAsync(q->h_small_sc.p, q->sc_fflag.as<uint32_t>() + T, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            nf = *q->h_small_sc.as<uint32_t>();
+        }
         RCHK(q->sc_fo.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
         RCHK(q->sc_fc.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
-        launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), q->sc_fflag.as<u32>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0,
+        launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), all_heads ? nullptr : q->sc_fflag.as<u32>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0,
                           clock0, q->sc_bclk.as<int64_t>(), q->sc_fo.as<int64_t>(), q->sc_fc.as<int64_t>());
         HIPCHK(hipGetLastError());
         if (q->compact_flushes && q->rate.kind == SH_RATE_NONE && !q->xmode && nf > 0 && nf == T) {
