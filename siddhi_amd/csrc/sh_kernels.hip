@@ -1866,11 +1866,11 @@ __global__ __launch_bounds__(kBlock) void k_sc_keys(i64 M, i64 n_old, const i64*
         w = (u32)lo;
         const i64 e = (i64)pend_gidx[m] - seq0;  // the event's index in the push
         const i64 sd = send_size > 0 ? e / send_size : 0;
-        chunk[m] = per_event ? j : sd;
+        if (chunk) chunk[m] = per_event ? j : sd;  // (null: every entry its own chunk)
         // (a sharded owner: the chunk is the global send, the clock is looked up per record — by_entry)
         send[m] = by_entry ? j : sd;
     } else {
-        chunk[m] = -1;
+        if (chunk) chunk[m] = -1;
         send[m] = -1;
     }
     skey[m] = ((u64)w << 32) | (u64)pend_pos[m];
@@ -1966,7 +1966,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_emit(i64 M, i64 n_old, const u32*
     unpack_key(kp, slot_key(kt, pend_pos[m]), kv, 1);
     for (int k = 0; k < kp.n; k++) out_keys[(size_t)k * T + o] = kv[k];
     for (int a = 0; a < na; a++) out_vals[(size_t)a * T + o] = sval[(size_t)m * na + a];
-    out_chunk[o] = chunk[m];
+    if (out_chunk) out_chunk[o] = chunk[m];  // (null: every row its own chunk and flush)
     out_send[o] = send[m];
     if (out_order) out_order[o] = (i64)pend_gidx[m];  // (the group's first event in the chunk: merge order)
 }

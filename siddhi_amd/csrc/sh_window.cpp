@@ -850,11 +850,15 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
     RCHK(q->sc_sl.reserve((size_t)n_sends * 8, false));
     // (a sharded owner: records are one send each for their clocks, chunks are the global sends)
     const bool gv = q->given_clk != nullptr;
-    launch_sc_keys(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(),
-                   per_event ? 1 : 0, gv ? q->given_ss : ss, gv ? q->given_seq0 : seq0, q->sc_skey.as<u64>(),
-                   q->sc_idx.as<u32>(), q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), gv ? 1 : 0);
     const bool xs = q->d.expired_on && per_event;   // lengthBatch(L, true) with expired / all events
     const bool xt = q->d.expired_on && !per_event;  // timeBatch(T, true) with expired / all events
+    // every new entry its own chunk (per-event sends, lengthBatch(L, true)): each is its own row, no head
+    // flags, no scan of them, no chunk column and no read-back of the row count (current rows only)
+    const bool all_heads = !(xs || xt) && (per_event || (gv ? q->given_ss : ss) == 1);
+    launch_sc_keys(s, M, n_old, q->sc_pcb.as<int64_t>(), nb, q->pend_pos.as<u32>(), q->pend_gidx.as<u64>(),
+                   per_event ? 1 : 0, gv ? q->given_ss : ss, gv ? q->given_seq0 : seq0, q->sc_skey.as<u64>(),
+                   q->sc_idx.as<u32>(), all_heads ? nullptr : q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(),
+                   gv ? 1 : 0);
     // current rows only: the sorted keys are compared for equality alone, so the window index goes right
     // above the slot bits and the radix sort reads those bits only (C2: 24 of 64)
     unsigned end_bit = 64;
@@ -876,9 +880,6 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
         return sh_fail(SH_ERR_DEVICE, "stream.current: sort failed");
     launch_rate_segments(s, M, q->sc_skey2.as<u64>(), q->sc_idx2.as<u32>(), 1, 0, q->sc_hd.as<u32>(),
                          q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_tmp.as<int64_t>());
-    // every new entry its own chunk (per-event sends, lengthBatch(L, true)): each is its own row, no head
-    // flags, no scan of them and no read-back of the row count (current rows only)
-    const bool all_heads = !(xs || xt) && (per_event || (gv ? q->given_ss : ss) == 1);
     if (!all_heads) HIPCHK(hipMemsetAsync(q->sc_ghead.p, 0, (size_t)(M + 1) * 4, s));
     HIPCHK(hipEventRecord(q->ev_agg0, s));
     launch_sc_walk(s, M, q->sc_hd.as<u32>(), q->sc_pos.as<u32>(), q->sc_starts.as<u32>(), q->sc_idx2.as<u32>(),
@@ -1008,8 +1009,8 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
                        q->sc_sval.as<u64>(), q->pend_pos.as<u32>(), q->pend_ts.as<int64_t>(), q->pend_gidx.as<u64>(),
                        q->sc_chunk.as<int64_t>(), q->sc_send.as<int64_t>(), q->kt.dev(), q->kp, na, T,
                        q->out_ts.as<int64_t>(), q->out_keys.as<int64_t>(), q->out_vals.as<u64>(),
-                       q->out_rep.as<int64_t>(), q->sc_ochunk.as<int64_t>(), q->sc_osend.as<int64_t>(),
-                       q->given ? q->out_order.as<int64_t>() : nullptr);
+                       q->out_rep.as<int64_t>(), all_heads ? nullptr : q->sc_ochunk.as<int64_t>(),
+                       q->sc_osend.as<int64_t>(), q->given ? q->out_order.as<int64_t>() : nullptr);
     }
     HIPCHK(hipGetLastError());
     PinnedVec<int64_t>& fo = host_out ? q->out.flush_offsets : q->dev_flush_offsets;
