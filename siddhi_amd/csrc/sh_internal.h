@@ -456,6 +456,8 @@ void launch_sc_emit(hipStream_t s, i64 M, i64 n_old, const u32* ghead, const u32
 void launch_sc_send_last(hipStream_t s, const i64* ts, i64 N, i64 send_size, i64 n_sends, i64* out);
 int scan_max_i64(void* temp, size_t* bytes, const i64* in, i64* out, i64 n, hipStream_t s);
 void launch_sc_flush_flags(hipStream_t s, i64 T, const i64* och, u32* flag);
+void launch_sc_clock_is_ts(hipStream_t s, i64 n, const i64* osd, const i64* slp, int cv0, i64 clock0, const i64* ts,
+                           u32* ok);
 void launch_flush_clock_is_ts(hipStream_t s, i64 n, const i64* fc, const i64* ts, u32* ok);
 void launch_sc_flushes(hipStream_t s, i64 T, const i64* osd, const u32* pre, const i64* slp, int cv0, i64 clock0,
                        const i64* bclk, i64* fo1, i64* fc);

@@ -2410,6 +2410,23 @@ __global__ __launch_bounds__(kBlock) void k_flush_clock_is_ts(i64 n, const i64* 
     if (i < n && fc[i] != ts[i]) ok[0] = 0u;
 }
 
+// the same for stream.current rows that are their own flushes, the clocks taken from the sends' clocks
+__global__ __launch_bounds__(kBlock) void k_sc_clock_is_ts(i64 n, const i64* __restrict__ osd, const i64* __restrict__ slp,
+                                                          int cv0, i64 clock0, const i64* __restrict__ ts, u32* ok) {
+    const i64 i = (i64)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const i64 c = cv0 ? max(clock0, slp[osd[i]]) : slp[osd[i]];
+    if (c != ts[i]) ok[0] = 0u;
+}
+
+void launch_sc_clock_is_ts(hipStream_t s, i64 n, const i64* osd, const i64* slp, int cv0, i64 clock0, const i64* ts,
+                           u32* ok) {
+    (void)hipMemsetD32Async((hipDeviceptr_t)ok, 1, 1, s);
+    if (n > 0)
+        hipLaunchKernelGGL(k_sc_clock_is_ts, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, osd, slp,
+                           cv0, clock0, ts, ok);
+}
+
 void launch_flush_clock_is_ts(hipStream_t s, i64 n, const i64* fc, const i64* ts, u32* ok) {
     (void)hipMemsetD32Async((hipDeviceptr_t)ok, 1, 1, s);
     if (n > 0)

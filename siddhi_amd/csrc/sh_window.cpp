@@ -1034,12 +1034,25 @@ static int sc_rows(sh_query* q, const sh_batch* b, const std::vector<Bound>& bou
             HIPCHK(hipStreamSynchronize(s));
             nf = *q->h_small_sc.as<uint32_t>();
         }
-        RCHK(q->sc_fo.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
-        RCHK(q->sc_fc.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
-        launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), all_heads ? nullptr : q->sc_fflag.as<u32>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0,
-                          clock0, q->sc_bclk.as<int64_t>(), q->sc_fo.as<int64_t>(), q->sc_fc.as<int64_t>());
-        HIPCHK(hipGetLastError());
-        if (q->compact_flushes && q->rate.kind == SH_RATE_NONE && !q->xmode && nf > 0 && nf == T) {
+        q->compact_now = false;
+        const bool want_compact = q->compact_flushes && q->rate.kind == SH_RATE_NONE && !q->xmode && nf > 0 && nf == T;
+        if (all_heads && want_compact) {
+            // (a flush per row: check the rows' clocks against their timestamps before writing any flush)
+            launch_sc_clock_is_ts(s, T, q->sc_osend.as<int64_t>(), q->sc_slp.as<int64_t>(), cv0 ? 1 : 0, clock0,
+                                  q->out_ts.as<int64_t>(), q->h_small_sc.as<uint32_t>() + 1);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(s));
+            q->compact_now = q->h_small_sc.as<uint32_t>()[1] == 1u;
+        }
+        if (!q->compact_now) {
+            RCHK(q->sc_fo.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
+            RCHK(q->sc_fc.reserve((size_t)std::max<int64_t>(nf, 1) * 8, false));
+            launch_sc_flushes(s, T, q->sc_osend.as<int64_t>(), all_heads ? nullptr : q->sc_fflag.as<u32>(),
+                              q->sc_slp.as<int64_t>(), cv0 ? 1 : 0, clock0, q->sc_bclk.as<int64_t>(),
+                              q->sc_fo.as<int64_t>(), q->sc_fc.as<int64_t>());
+            HIPCHK(hipGetLastError());
+        }
+        if (!all_heads && want_compact) {
             // one row per flush: offsets implicit; clocks implicit too when each equals its row's ts
             launch_flush_clock_is_ts(s, nf, q->sc_fc.as<int64_t>(), q->out_ts.as<int64_t>(), q->h_small_sc.as<uint32_t>() + 1);
             HIPCHK(hipGetLastError());
