@@ -97,6 +97,10 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         }
     }
     const bool merge_ok = !(nk == 0 && na == 0);  // pass-through rows are never merged
+    // one dictionary-id key (dense, ids below the table's capacity): a flush's table is indexed by the id
+    // itself when it is at most 4x the hashed table's size (no hashing, no key column, no probing)
+    const int64_t dense_cap = (nk == 1 && q->kp.n == 1 && q->kt.dense && q->kt.dmul == 1 && q->kt.dadd == 0 && !q->wide)
+                                  ? (int64_t)q->kt.size_ : 0;
     std::vector<XItem> items;
     std::vector<int64_t> item_w;
     int64_t tab_total = 0;
@@ -111,6 +115,10 @@ int xout_finish(sh_query* q, bool host_out, const sh_out** out) {
         if (x.p_n > 0 && x.c_n > 0 && merge_ok) {
             int64_t ts = 2;
             while (ts < 2 * x.c_n) ts <<= 1;
+            if (dense_cap > 0 && dense_cap <= 4 * ts) {
+                ts = std::max<int64_t>(ts, dense_cap);
+                x.pad = 1;  // (direct: slot = the id)
+            }
             x.tab_off = tab_total;
             x.tab_size = ts;
             tab_total += ts;

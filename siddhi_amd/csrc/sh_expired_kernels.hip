@@ -48,6 +48,10 @@ __global__ __launch_bounds__(kBlock) void k_x_insert(const XItem* items, const i
     const XItem it = items[i];
     const i64 r = it.c_lo + (g - cum[i]);
     const u64 key = x_packed_key(s_keys, S, nk, r);
+    if (it.pad) {  // (a dense id below the table size: its own slot, distinct within the flush)
+        if (key < (u64)it.tab_size) trow[it.tab_off + (i64)key] = (u32)r;
+        return;
+    }
     const u32 mask = (u32)it.tab_size - 1;
     u32 h = (u32)mix64(key) & mask;
     for (;;) {
@@ -73,14 +77,19 @@ __global__ __launch_bounds__(kBlock) void k_x_probe(const XItem* items, const i6
         const XItem it = items[i];
         const i64 r = it.p_lo + (g - cum[i]);
         const u64 key = x_packed_key(s_keys, S, nk, r);
-        const u32 mask = (u32)it.tab_size - 1;
-        u32 h = (u32)mix64(key) & mask;
         int m = -1;
-        for (;;) {
-            const u32 t = trow[it.tab_off + h];
-            if (t == kXEmpty) break;
-            if (tkey[it.tab_off + h] == key) { m = (int)t; break; }
-            h = (h + 1) & mask;
+        if (it.pad) {  // (direct table: the id is the slot)
+            const u32 t = key < (u64)it.tab_size ? trow[it.tab_off + (i64)key] : kXEmpty;
+            m = t == kXEmpty ? -1 : (int)t;
+        } else {
+            const u32 mask = (u32)it.tab_size - 1;
+            u32 h = (u32)mix64(key) & mask;
+            for (;;) {
+                const u32 t = trow[it.tab_off + h];
+                if (t == kXEmpty) break;
+                if (tkey[it.tab_off + h] == key) { m = (int)t; break; }
+                h = (h + 1) & mask;
+            }
         }
         match[r] = m;
         if (m >= 0) {
