@@ -97,15 +97,35 @@ __global__ __launch_bounds__(kBlock) void k_x_probe(const XItem* items, const i6
             mt = true;
         }
     }
-    // the matched count per flush: one atomic per wave when the wave's rows belong to one flush (the
-    // usual case: a flush has ~100k rows) — a per-row atomic on a few counters serialised at the L2
+    // the matched count per flush: one atomic per block when the block's rows belong to one flush (the
+    // usual case: a flush has ~100k rows) — per-row, even per-wave atomics on a few counters serialise at
+    // the L2 (C2 `insert all events`: ~1600 waves per flush counter)
+    __shared__ int s_item[kBlock / 64];
+    __shared__ u32 s_cnt[kBlock / 64];
+    const int w = threadIdx.x >> 6;
     const int i0 = __shfl(i, 0, 64);  // lane 0 holds the wave's smallest g: valid if any lane is
     const u64 same = __ballot(!valid || i == i0);
+    const u64 b = __ballot(mt);
     if (same == ~0ull) {
-        const u64 b = __ballot(mt);
-        if ((threadIdx.x & 63) == 0 && b) atomicAdd(&item_matched[i0], (u32)__popcll(b));
-    } else if (mt) {
-        atomicAdd(&item_matched[i], 1u);
+        if ((threadIdx.x & 63) == 0) { s_item[w] = b ? i0 : -1; s_cnt[w] = (u32)__popcll(b); }
+    } else {
+        if ((threadIdx.x & 63) == 0) { s_item[w] = -1; s_cnt[w] = 0; }
+        if (mt) atomicAdd(&item_matched[i], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int cur = -1;
+        u32 acc = 0;
+        for (int x = 0; x < kBlock / 64; x++) {
+            if (s_item[x] < 0) continue;
+            if (s_item[x] != cur) {
+                if (cur >= 0 && acc) atomicAdd(&item_matched[cur], acc);
+                cur = s_item[x];
+                acc = 0;
+            }
+            acc += s_cnt[x];
+        }
+        if (cur >= 0 && acc) atomicAdd(&item_matched[cur], acc);
     }
 }
 
