@@ -27,6 +27,18 @@
 
 namespace shd {
 
+// a row slot from one counter for every active lane of the wave: one atomic per wave (the rows' order is
+// set by a later sort; per-row atomics on one counter serialise at the L2)
+__device__ __forceinline__ u32 wave_row_slot(u32* ctr) {
+    const u64 act = __ballot(1);
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)act) - 1;
+    u32 base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (u32)__popcll(act));
+    base = __shfl(base, leader, 64);
+    return base + (u32)__popcll(act & ((1ull << lane) - 1ull));
+}
+
 namespace {
 
 __device__ __forceinline__ bool g_worse(int kind, u64 cur, u64 v) {
@@ -911,7 +923,7 @@ __global__ __launch_bounds__(64) void k_pg_replay(const i64* __restrict__ seg_st
     for (int a = 0; a < NA; a++) { rv[a] = 0; rn[a] = 0; }
     auto flush_row = [&]() {
         if (first < 0) return;
-        const u32 slot = atomicAdd(n_rows, 1u);
+        const u32 slot = wave_row_slot(n_rows);
         rows.ts[slot] = q_ts;
         rows.rep[slot] = q_seq;
         rows.slot[slot] = (u32)pk;
@@ -1280,7 +1292,7 @@ __global__ __launch_bounds__(64) void k_tb_fold(const i64* __restrict__ seg_star
         if (!last) continue;
         // the group's row of this chunk: its last event carrying the running values (QuerySelector
         // .processInBatchGroupBy :315-374: LinkedHashMap.put keeps the group's first position)
-        const u32 o = atomicAdd(n_rows, 1u);
+        const u32 o = wave_row_slot(n_rows);
         rows.ts[o] = rec.ts[r];
         rows.rep[o] = seq_base + (i64)rec.raw[r];
         rows.slot[o] = gslot[r];
