@@ -308,6 +308,7 @@ struct sh_query {
     DevBuf xt_dev;
     PinnedBuf xt_host;
     int64_t n_pend = 0, pend_cap = 0;
+    int64_t last_nb = 0;  // window starts the last push found (sizes the first read-back of the next)
     int64_t seq = 0;  // stream index of the next event pushed (sh_out.rep numbering)
     DevBuf pend_pos, pend_ts, pend_vals;
     DevBuf pend_tmp;  // staging of pending_to_front's overlapping moves (kept: no allocation per push)

@@ -1731,8 +1731,10 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         // the push info and the first boundaries come back in one copy; the key partitioning of the
         // push's events (independent of where the windows close) is queued behind it and runs while
         // the host reads them
+        // (as many as the last push found, with room: a push closing thousands of windows — C1 — would
+        // otherwise read the rest after the split queued behind this copy, the host waiting for it)
         constexpr int kFirstBounds = 256;
-        const int nb0 = std::min(kFirstBounds, max_bounds);
+        const int nb0 = (int)std::min<int64_t>(max_bounds, std::max<int64_t>(kFirstBounds, q->last_nb + q->last_nb / 4 + 64));
         RCHK(q->h_bounds.reserve((size_t)nb0 * sizeof(Bound)));
         HIPCHK(hipMemcpyAsync(q->h_info, q->info.p, sizeof(PushInfo), hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(q->h_bounds.p, q->bounds.p, (size_t)nb0 * sizeof(Bound), hipMemcpyDeviceToHost, s));
@@ -1779,6 +1781,7 @@ static int push_core(sh_query* q, const sh_batch* b, bool host_out_req, const sh
         const int64_t xm0 = q->xm;  // (lastCurrentEventTime before the push: timeout stamps)
         if (ext) q->xm = std::max(q->xm, info.max_xm);
         std::vector<Bound> bounds(info.n_bounds);
+        q->last_nb = std::min<int64_t>(info.n_bounds, 1 << 16);
         if (info.n_bounds) {
             if (info.n_bounds <= nb0) {
                 std::memcpy(bounds.data(), q->h_bounds.p, info.n_bounds * sizeof(Bound));
